@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Headline benchmark: PQL queries/sec on a 1M-row x 1B-column set field.
+
+Config (BASELINE.json config 2/3): index ``i`` with one set field ``f``;
+1,000,000 rows x 1,000,000,000 columns (954 shards of 2^20 columns); every
+column holds 8 bits whose rows follow the reference's Zipf(s=1.6, v=50) row
+generator (fragment_internal_test.go:2377-2460) -> ~8e9 set bits, random-init
+synthetic data generated deterministically per shard (no dataset download).
+
+A *step* is one batch of B concurrent PQL queries
+``Count(Intersect(Row(f=a), Row(f=b)))`` with a, b drawn from the same Zipf
+law (hot rows are queried most, as in production).  The step includes PQL
+parsing + planning on the host, program upload, the batched HIP kernel over
+all local shards, the cross-GPU RCCL all-reduce of the counts and the D2H of
+the results.  With N GPUs each rank owns a contiguous 1/N of the shards
+(strong scaling: the index size is fixed).  ``value`` = total queries/sec.
+
+Run: python bench.py [--gpus N --steps K --warmup W --batch B]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+TOTAL_COLS = 1_000_000_000
+NROWS = 1_000_000
+SHARD_WIDTH = 1 << 20
+
+
+def zipf_rows(rng, n, nrows=NROWS, s=1.6, v=50.0):
+    # inverse-CDF sampling of P(k) ~ (v+k)^-s, k in [0, nrows)
+    k = np.arange(nrows, dtype=np.float64)
+    w = (v + k) ** (-s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return np.searchsorted(cdf, rng.random(n)).astype(np.int64)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="queries per step")
+    ap.add_argument("--cols", type=int, default=TOTAL_COLS)
+    ap.add_argument("--rows", type=int, default=NROWS)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--topn", action="store_true", help="also time TopN(n=100) batches")
+    ap.add_argument("--cpu-baseline-shards", type=int, default=0,
+                    help="also time the host C++ roaring executor on this many shards (extrapolated)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.ops.device import DeviceView, GpuEngine
+    from pilosa_amd.pql import parse_string
+    from pilosa_amd.ops.planner import BenchPlanner
+
+    nshards = math.ceil(args.cols / SHARD_WIDTH)
+    lo = nshards * rank // world
+    hi = nshards * (rank + 1) // world
+    t0 = time.time()
+    rows, rowptr, sb, meta, payload = _roaring.gen_zipf_arena(lo, hi, args.cols, args.rows, 8.0, 1.6, 50.0, 1,
+                                                              args.threads)
+    tgen = time.time() - t0
+    view = DeviceView(rows, rowptr, sb, meta, payload, dev, shards=list(range(lo, hi)))
+    del rows, rowptr, sb, meta, payload
+    torch.cuda.synchronize(dev)
+    tload = time.time() - t0 - tgen
+    eng = GpuEngine(dev)
+    planner = BenchPlanner({"f": view})
+
+    rng = np.random.default_rng(1234)
+    nq = args.batch * (args.steps + args.warmup)
+    ra = zipf_rows(rng, nq, args.rows)
+    rb = zipf_rows(rng, nq, args.rows)
+    queries = [f"Count(Intersect(Row(f={a}), Row(f={b})))" for a, b in zip(ra, rb)]
+
+    def step(i):
+        qs = queries[i * args.batch:(i + 1) * args.batch]
+        exprs = [planner.plan(parse_string(q).calls[0]) for q in qs]
+        out = eng.count_async(exprs)
+        if world > 1:
+            dist.all_reduce(out)
+        return out.cpu()
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    last = None
+    for i in range(args.warmup, args.warmup + args.steps):
+        last = step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms = elapsed / args.steps * 1000.0
+    qps = args.batch * args.steps / elapsed
+
+    extra = {"gen_s": round(tgen, 2), "h2d_s": round(tload, 2), "hbm_bytes_per_gpu": view.nbytes(),
+             "containers_per_gpu": view.container_count, "shards": nshards,
+             "mean_count": float(last.double().mean()) if last is not None else None}
+
+    if rank == 0:
+        rec = {"metric": "PQL queries/sec (Count(Intersect(Row,Row))) on 1M-row x 1B-col set field",
+               "value": round(qps, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "bitmap(u64 words)",
+               "data": "synthetic (zipf s=1.6 v=50 rows, 8 bits/column, deterministic per shard)",
+               "config": {"model": "set field f, 1M rows x 1B cols (954 shards)", "global_batch": args.batch,
+                          "seq_len": args.cols, "parallelism": f"shard-range x{world} + RCCL all-reduce"},
+               "extra": extra}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,96 @@
+// torch extension binding for the gfx950 bitmap kernels (module
+// pilosa_amd._hipkernels).  Every entry point launches on torch's current HIP
+// stream of the tensors' device, so the executor can overlap queries on
+// separate streams and capture launch sequences in HIP graphs.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include "kernels.h"
+
+namespace {
+
+void check_dev(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+hipStream_t cur_stream(const torch::Tensor& t) {
+  return at::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor out,
+                c10::optional<torch::Tensor> per_key, bool fast) {
+  check_dev(progs, "progs");
+  check_dev(views, "views");
+  TORCH_CHECK(progs.numel() % sizeof(pk::QueryProg) == 0, "progs size");
+  TORCH_CHECK(views.numel() % sizeof(pk::ViewDev) == 0, "views size");
+  const int Q = int(progs.numel() / sizeof(pk::QueryProg));
+  unsigned long long* o = nullptr;
+  if (out.numel()) {
+    check_dev(out, "out");
+    TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() >= Q, "out must be int64[Q]");
+    o = reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>());
+  }
+  int32_t* pk_ = nullptr;
+  if (per_key.has_value() && per_key->numel()) {
+    check_dev(*per_key, "per_key");
+    TORCH_CHECK(per_key->scalar_type() == torch::kInt32 && per_key->numel() >= int64_t(Q) * S * 16,
+                "per_key must be int32[Q*S*16]");
+    pk_ = per_key->data_ptr<int32_t>();
+  }
+  pk::launch_expr_count(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
+                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), o, pk_, fast,
+                        cur_stream(progs));
+}
+
+void expr_materialize(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor counts,
+                      torch::Tensor offs, torch::Tensor outp) {
+  check_dev(progs, "progs");
+  check_dev(views, "views");
+  check_dev(counts, "counts");
+  check_dev(offs, "offs");
+  check_dev(outp, "outp");
+  const int Q = int(progs.numel() / sizeof(pk::QueryProg));
+  TORCH_CHECK(counts.numel() >= int64_t(Q) * S * 16 && offs.numel() >= int64_t(Q) * S * 16, "counts/offs size");
+  pk::launch_expr_materialize(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
+                              reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
+                              counts.data_ptr<int32_t>(), offs.data_ptr<int64_t>(),
+                              reinterpret_cast<uint16_t*>(outp.data_ptr<int16_t>()), cur_stream(progs));
+}
+
+void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out_sum,
+             torch::Tensor out_cnt) {
+  check_dev(progs, "progs");
+  check_dev(views, "views");
+  check_dev(out_sum, "out_sum");
+  check_dev(out_cnt, "out_cnt");
+  TORCH_CHECK(!bsi_args.is_cuda() && bsi_args.scalar_type() == torch::kInt64 && bsi_args.numel() == 67,
+              "bsi_args must be a cpu int64[67]: view, depth, exists, sign, bit_row[63]");
+  auto a = bsi_args.data_ptr<int64_t>();
+  pk::BsiArgs b{};
+  b.view = int32_t(a[0]);
+  b.depth = int32_t(a[1]);
+  TORCH_CHECK(b.depth >= 0 && b.depth <= 63, "bsi depth");
+  b.row_exists = a[2];
+  b.row_sign = a[3];
+  for (int i = 0; i < 64; i++) b.bit_row[i] = i < 63 ? a[4 + i] : -1;
+  const int Q = int(progs.numel() / sizeof(pk::QueryProg));
+  pk::launch_bsi_sum(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
+                     reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), b,
+                     reinterpret_cast<unsigned long long*>(out_sum.data_ptr<int64_t>()),
+                     reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>()), cur_stream(progs));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels for the bitmap index";
+  m.attr("QUERYPROG_BYTES") = int(sizeof(pk::QueryProg));
+  m.attr("VIEWDEV_BYTES") = int(sizeof(pk::ViewDev));
+  m.attr("MAXLEAF") = pk::MAXLEAF;
+  m.attr("MAXPROG") = pk::MAXPROG;
+  m.def("expr_count", &expr_count, "batched boolean-expression count over all local shards",
+        py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("fast") = false);
+  m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
+  m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
+}

@@ -1,0 +1,512 @@
+// CDNA4 (gfx950) kernels for the bitmap index hot path.
+//
+// Reference hot loops replaced here:
+//   K1/K2 popcountAndSlice / intersectionCount  roaring/roaring.go:3078-3215,5061-5072
+//   K3-K6 intersect/union/difference/xor        roaring/roaring.go:3217-4344
+//   K8    count/countRange                      roaring/roaring.go:2000-2110
+//   K10   OffsetRange row extraction             roaring/roaring.go:535-558
+//   K13   BSI sum                                fragment.go:1109-1141
+//   K17/K21 TopN / GroupBy intersection counts  fragment.go:1568-1700, executor.go:3060-3230
+//
+// Execution model (ours): a whole batch of queries is evaluated over ALL local
+// shards in one launch.  One 64-lane wave owns one (query, shard) work item
+// and walks the <=16 container keys of the row in that shard.  A container is
+// held as a register "tile": 1024 u64 words spread over the wave, lane l owns
+// words {128*i + 2*l + h | i<8, h<2} so every tile load is eight fully
+// coalesced 1 KiB global_load_dwordx4 wave-instructions.  Array and run
+// containers are expanded into a wave-private 8 KiB LDS bitmap (ds_or_b64
+// scatter) and read back in the same layout.  Boolean query trees are compiled
+// on the host to a tiny postfix program (<=16 ops, <=8 leaves) that the wave
+// interprets with a 4-deep register stack (static register moves, no scratch).
+// Fast paths: Count(Row) sums container cardinalities from the metadata only;
+// Count(Intersect(a,b)) dispatches on the container type pair
+// (bitmap&bitmap popcount, array->bitmap probe, array->LDS-bitmap probe).
+//
+// Workgroups are remapped XCD-aware: consecutive logical blocks (same shard,
+// different queries -> the same hot containers) are kept on one XCD so they
+// share its L2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace pk {
+
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
+  // bijective remap: blocks b, b+8, b+16 ... (same XCD) get consecutive ids
+  const uint32_t nx = 8;
+  uint32_t xcd = bid % nx, loc = bid / nx;
+  uint32_t q = nblk / nx, r = nblk % nx;
+  uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + loc;
+}
+
+struct Tile {
+  ulong2 w[8];
+};
+
+__device__ __forceinline__ void tile_zero(Tile& t) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) t.w[i] = make_ulong2(0, 0);
+}
+
+__device__ __forceinline__ int tile_popc(const Tile& t) {
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) c += __popcll(t.w[i].x) + __popcll(t.w[i].y);
+  return c;
+}
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Expand an array / run container into the wave-private LDS bitmap `lb`
+// (1024 u64).  Caller reads it back.
+__device__ __forceinline__ void lds_expand(uint64_t* lb, const uint16_t* payload, int64_t m) {
+  const int lane = wave_lane();
+  ulong2* l2 = reinterpret_cast<ulong2*>(lb);
+#pragma unroll
+  for (int i = 0; i < 8; i++) l2[i * 64 + lane] = make_ulong2(0, 0);
+  lds_fence();
+  const int type = meta_type(m);
+  const uint16_t* p = payload + meta_off16(m) * 8;
+  if (type == CT_ARRAY) {
+    const int n = meta_n(m);
+    for (int e = lane; e < n; e += 64) {
+      uint32_t v = p[e];
+      atomicOr(reinterpret_cast<unsigned long long*>(&lb[v >> 6]), 1ull << (v & 63));
+    }
+  } else {  // run
+    const int nr = p[0];
+    for (int r = lane; r < nr; r += 64) {
+      uint32_t s = p[8 + 2 * r], e = uint32_t(p[9 + 2 * r]) + 1;  // [s,e)
+      uint32_t ws = s >> 6, we = (e - 1) >> 6;
+      if (ws == we) {
+        uint64_t mk = (e - s == 64) ? ~0ull : (((1ull << (e - s)) - 1) << (s & 63));
+        atomicOr(reinterpret_cast<unsigned long long*>(&lb[ws]), mk);
+      } else {
+        atomicOr(reinterpret_cast<unsigned long long*>(&lb[ws]), ~0ull << (s & 63));
+        for (uint32_t w = ws + 1; w < we; w++) lb[w] = ~0ull;
+        uint32_t hb = e & 63;
+        atomicOr(reinterpret_cast<unsigned long long*>(&lb[we]), hb ? ((1ull << hb) - 1) : ~0ull);
+      }
+    }
+  }
+  lds_fence();
+}
+
+__device__ __forceinline__ void tile_load(Tile& t, const uint16_t* payload, int64_t m, uint64_t* lb) {
+  const int lane = wave_lane();
+  if (meta_type(m) == CT_BITMAP) {
+    const ulong2* p = reinterpret_cast<const ulong2*>(payload + meta_off16(m) * 8);
+#pragma unroll
+    for (int i = 0; i < 8; i++) t.w[i] = p[i * 64 + lane];
+  } else {
+    lds_expand(lb, payload, m);
+    const ulong2* l2 = reinterpret_cast<const ulong2*>(lb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) t.w[i] = l2[i * 64 + lane];
+    lds_fence();
+  }
+}
+
+template <int OP>
+__device__ __forceinline__ void tile_op(Tile& a, const Tile& b) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (OP == OP_AND) { a.w[i].x &= b.w[i].x; a.w[i].y &= b.w[i].y; }
+    if (OP == OP_OR) { a.w[i].x |= b.w[i].x; a.w[i].y |= b.w[i].y; }
+    if (OP == OP_XOR) { a.w[i].x ^= b.w[i].x; a.w[i].y ^= b.w[i].y; }
+    if (OP == OP_ANDNOT) { a.w[i].x &= ~b.w[i].x; a.w[i].y &= ~b.w[i].y; }
+  }
+}
+
+// Per-wave scratch in LDS.
+struct WaveScratch {
+  uint64_t lb[1024];          // 8 KiB expansion bitmap
+  int32_t slot[MAXLEAF][16];  // container index per (leaf, j), -1 absent
+};
+
+// Build the slot table for every leaf of query `qp` in shard `s`; returns the
+// presence mask of each leaf in `mask[]` (wave-uniform).
+__device__ __forceinline__ void build_slots(const QueryProg& qp, const ViewDev* views, int s, WaveScratch& ws,
+                                            uint32_t* mask) {
+  const int lane = wave_lane();
+  for (int t = lane; t < MAXLEAF * 16; t += 64) (&ws.slot[0][0])[t] = -1;
+  lds_fence();
+  for (int k = 0; k < qp.nleaf; k++) {
+    const int64_t d = qp.leaf_row[k];
+    if (d < 0) continue;
+    const ViewDev& v = views[qp.leaf_view[k]];
+    const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+    const int64_t base = v.shard_base[s];
+    const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+    if (lane < hi - lo) {
+      const int64_t ci = lo + lane;
+      ws.slot[k][meta_j(v.meta[ci])] = int32_t(ci - base);
+    }
+  }
+  lds_fence();
+  for (int k0 = 0; k0 < MAXLEAF; k0 += 4) {
+    const int k = k0 + (lane >> 4);
+    const bool has = ws.slot[k][lane & 15] >= 0;
+    const uint64_t b = __ballot(has);
+#pragma unroll
+    for (int i = 0; i < 4; i++) mask[k0 + i] = uint32_t((b >> (16 * i)) & 0xffff);
+  }
+}
+
+// Candidate keys: evaluate the program over presence masks.
+__device__ __forceinline__ uint32_t candidate_mask(const QueryProg& qp, const uint32_t* mask) {
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // s0 = top
+  for (int pc = 0; pc < qp.nprog; pc++) {
+    const int op = qp.prog[pc];
+    if (op < OP_AND) {
+      s3 = s2; s2 = s1; s1 = s0; s0 = mask[op];
+    } else {
+      uint32_t r;
+      if (op == OP_AND) r = s1 & s0;
+      else if (op == OP_ANDNOT) r = s1;
+      else r = s1 | s0;  // OR, XOR
+      s0 = r; s1 = s2; s2 = s3; s3 = 0;
+    }
+  }
+  return s0;
+}
+
+// Evaluate the program for key j into `acc`.
+__device__ __forceinline__ void eval_tile(const QueryProg& qp, const ViewDev* views, int s, int j, WaveScratch& ws,
+                                          Tile& acc) {
+  Tile t1, t2, t3;
+  tile_zero(acc);
+  tile_zero(t1);
+  tile_zero(t2);
+  tile_zero(t3);
+  for (int pc = 0; pc < qp.nprog; pc++) {
+    const int op = qp.prog[pc];
+    if (op < OP_AND) {
+      t3 = t2; t2 = t1; t1 = acc;
+      const int32_t c = ws.slot[op][j];
+      if (c < 0) {
+        tile_zero(acc);
+      } else {
+        const ViewDev& v = views[qp.leaf_view[op]];
+        tile_load(acc, v.payload, v.meta[v.shard_base[s] + c], ws.lb);
+      }
+    } else {
+      // acc = t1 OP acc
+      if (op == OP_AND) { tile_op<OP_AND>(t1, acc); }
+      else if (op == OP_OR) { tile_op<OP_OR>(t1, acc); }
+      else if (op == OP_XOR) { tile_op<OP_XOR>(t1, acc); }
+      else { tile_op<OP_ANDNOT>(t1, acc); }
+      acc = t1; t1 = t2; t2 = t3; tile_zero(t3);
+    }
+  }
+}
+
+// |A ∩ B| for two containers with a type-pair dispatch (no full tiles for arrays).
+__device__ __forceinline__ int and2_count(const ViewDev& va, int64_t ma, const ViewDev& vb, int64_t mb,
+                                          uint64_t* lb) {
+  const int lane = wave_lane();
+  const int ta = meta_type(ma), tb = meta_type(mb);
+  int c = 0;
+  if (ta == CT_BITMAP && tb == CT_BITMAP) {
+    const ulong2* pa = reinterpret_cast<const ulong2*>(va.payload + meta_off16(ma) * 8);
+    const ulong2* pb = reinterpret_cast<const ulong2*>(vb.payload + meta_off16(mb) * 8);
+    ulong2 x[8], y[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = pa[i * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 8; i++) y[i] = pb[i * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 8; i++) c += __popcll(x[i].x & y[i].x) + __popcll(x[i].y & y[i].y);
+    return c;
+  }
+  if (ta == CT_RUN || tb == CT_RUN) {
+    Tile a, b;
+    tile_load(a, va.payload, ma, lb);
+    tile_load(b, vb.payload, mb, lb);
+    tile_op<OP_AND>(a, b);
+    return tile_popc(a);
+  }
+  if (ta == CT_BITMAP || tb == CT_BITMAP) {
+    // probe the bitmap with the array values
+    const bool abit = ta == CT_BITMAP;
+    const uint64_t* bw = reinterpret_cast<const uint64_t*>((abit ? va.payload : vb.payload) +
+                                                           meta_off16(abit ? ma : mb) * 8);
+    const int64_t am = abit ? mb : ma;
+    const uint16_t* arr = (abit ? vb.payload : va.payload) + meta_off16(am) * 8;
+    const int n = meta_n(am);
+    for (int e = lane; e < n; e += 64) {
+      const uint32_t v = arr[e];
+      c += (bw[v >> 6] >> (v & 63)) & 1;
+    }
+    return c;
+  }
+  // array & array: scatter the larger into LDS, probe with the smaller
+  const bool abig = meta_n(ma) >= meta_n(mb);
+  const int64_t mbig = abig ? ma : mb, msmall = abig ? mb : ma;
+  const ViewDev& vbig = abig ? va : vb;
+  const ViewDev& vsmall = abig ? vb : va;
+  lds_expand(lb, vbig.payload, mbig);
+  const uint16_t* arr = vsmall.payload + meta_off16(msmall) * 8;
+  const int n = meta_n(msmall);
+  for (int e = lane; e < n; e += 64) {
+    const uint32_t v = arr[e];
+    c += (lb[v >> 6] >> (v & 63)) & 1;
+  }
+  lds_fence();
+  return c;
+}
+
+constexpr int WAVES_PER_BLOCK = 4;
+
+// Count kernel: out[q] += |program(q)| over all local shards.
+// FAST=true handles only Count(Row) and Count(Intersect(a,b)) programs (no
+// register tile stack -> far fewer VGPRs, higher occupancy); the host routes
+// every other program shape to FAST=false.
+template <bool FAST>
+__global__ __launch_bounds__(256) void expr_count_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                         const ViewDev* __restrict__ views, int S,
+                                                         unsigned long long* __restrict__ out,
+                                                         int32_t* __restrict__ per_key) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S) return;
+  const int q = int(item % Q);
+  const int s = int(item / Q);
+  const QueryProg& qp = progs[q];
+  WaveScratch& ws = scratch[wave];
+  uint32_t mask[MAXLEAF];
+  build_slots(qp, views, s, ws, mask);
+  const uint32_t cand = candidate_mask(qp, mask);
+  int64_t total = 0;
+  if (cand) {
+    if (qp.nprog == 1) {
+      // Count(Row): metadata only
+      const ViewDev& v = views[qp.leaf_view[0]];
+      if (lane < 16 && ((cand >> lane) & 1)) {
+        const int c = ws.slot[0][lane];
+        const int n = meta_n(v.meta[v.shard_base[s] + c]);
+        total = n;
+        if (per_key) per_key[(int64_t(q) * S + s) * 16 + lane] = n;
+      }
+    } else if (FAST) {
+      // Count(Intersect(leaf0, leaf1)) with a container type-pair dispatch
+      const ViewDev& va = views[qp.leaf_view[0]];
+      const ViewDev& vb = views[qp.leaf_view[1]];
+      for (uint32_t cm = cand; cm; cm &= cm - 1) {
+        const int j = __builtin_ctz(cm);
+        const int64_t ma = va.meta[va.shard_base[s] + ws.slot[0][j]];
+        const int64_t mb = vb.meta[vb.shard_base[s] + ws.slot[1][j]];
+        total += and2_count(va, ma, vb, mb, ws.lb);
+      }
+    } else {
+      for (uint32_t cm = cand; cm; cm &= cm - 1) {
+        const int j = __builtin_ctz(cm);
+        Tile acc;
+        eval_tile(qp, views, s, j, ws, acc);
+        int c = tile_popc(acc);
+        if (per_key) {
+          const int64_t cj = wave_sum_i64(c);
+          if (lane == 0) per_key[(int64_t(q) * S + s) * 16 + j] = int32_t(cj);
+        }
+        total += c;
+      }
+    }
+  }
+  total = wave_sum_i64(total);
+  if (lane == 0 && total && out) atomicAdd(out + q, (unsigned long long)total);
+}
+
+// Materialize kernel: writes result containers for every (q, s, j) with
+// counts[q,s,j] > 0 at u16 offset offs[q,s,j]; array if n <= 4096 else bitmap.
+__global__ __launch_bounds__(256) void expr_materialize_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                               const ViewDev* __restrict__ views, int S,
+                                                               const int32_t* __restrict__ counts,
+                                                               const int64_t* __restrict__ offs,
+                                                               uint16_t* __restrict__ outp) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S) return;
+  const int q = int(item % Q);
+  const int s = int(item / Q);
+  const QueryProg& qp = progs[q];
+  WaveScratch& ws = scratch[wave];
+  uint32_t mask[MAXLEAF];
+  build_slots(qp, views, s, ws, mask);
+  const uint32_t cand = candidate_mask(qp, mask);
+  for (uint32_t cm = cand; cm; cm &= cm - 1) {
+    const int j = __builtin_ctz(cm);
+    const int64_t key = (int64_t(q) * S + s) * 16 + j;
+    const int n = counts[key];
+    if (n <= 0) continue;
+    Tile acc;
+    eval_tile(qp, views, s, j, ws, acc);
+    uint16_t* dst = outp + offs[key];
+    if (n > ARRAY_MAX) {
+      ulong2* d2 = reinterpret_cast<ulong2*>(dst);
+#pragma unroll
+      for (int i = 0; i < 8; i++) d2[i * 64 + lane] = acc.w[i];
+    } else {
+      // ordered compaction: chunk i covers words [128i, 128i+128), lane l owns
+      // words 128i+2l, 128i+2l+1 -> exclusive wave scan of per-lane popcounts.
+      int base = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint64_t x = acc.w[i].x, y = acc.w[i].y;
+        const int c = __popcll(x) + __popcll(y);
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int t = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += t;
+        }
+        int pos = base + incl - c;
+        const int wbase = 128 * i + 2 * lane;
+        for (uint64_t b = x; b; b &= b - 1) dst[pos++] = uint16_t(wbase * 64 + __builtin_ctzll(b));
+        for (uint64_t b = y; b; b &= b - 1) dst[pos++] = uint16_t((wbase + 1) * 64 + __builtin_ctzll(b));
+        base += __shfl(incl, 63, 64);
+      }
+    }
+  }
+}
+
+// BSI sum over bit-sliced rows (fragment.go:1109-1141):
+//   consider = exists & filter ; count = |consider|
+//   sum = Σ_i 2^i (|B_i & consider & ~sign| - |B_i & consider & sign|)
+// The host resolves the BSI view's rows 0 (exists), 1 (sign) and 2+i (bit i)
+// to dense row indices (bsi.row_exists / row_sign / bit_row[i], -1 = absent).
+__global__ __launch_bounds__(256) void bsi_sum_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                      const ViewDev* __restrict__ views, int S, BsiArgs bsi,
+                                                      unsigned long long* __restrict__ out_sum,
+                                                      unsigned long long* __restrict__ out_cnt) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S) return;
+  const int q = int(item % Q);
+  const int s = int(item / Q);
+  const QueryProg& qp = progs[q];  // filter program (nprog == 0: no filter)
+  WaveScratch& ws = scratch[wave];
+  const ViewDev& bv = views[bsi.view];
+  uint32_t mask[MAXLEAF];
+  build_slots(qp, views, s, ws, mask);
+  uint32_t cand = qp.nprog ? candidate_mask(qp, mask) : 0xffffu;
+  // exists row presence
+  const uint32_t* rp = bv.rowptr + int64_t(s) * (bv.D + 1);
+  const int64_t base = bv.shard_base[s];
+  auto row_range = [&](int64_t d, int64_t& lo, int64_t& hi) {
+    if (d < 0) { lo = hi = 0; return; }
+    lo = rp[d]; hi = rp[d + 1];
+  };
+  auto find_j = [&](int64_t d, int j) -> int64_t {
+    // container of dense row d at key j in this shard (or -1); wave-uniform
+    int64_t lo, hi;
+    row_range(d, lo, hi);
+    int64_t found = -1;
+    if (lane < hi - lo) {
+      if (meta_j(bv.meta[base + lo + lane]) == j) found = base + lo + lane;
+    }
+    const uint64_t b = __ballot(found >= 0);
+    if (!b) return -1;
+    return __shfl(found, __builtin_ctzll(b), 64);
+  };
+  int64_t lo_e, hi_e;
+  row_range(bsi.row_exists, lo_e, hi_e);
+  uint32_t emask = 0;
+  {
+    int64_t j = -1;
+    if (lane < hi_e - lo_e) j = meta_j(bv.meta[base + lo_e + lane]);
+    for (int t = 0; t < 16; t++) emask |= (__ballot(j == t) ? 1u : 0u) << t;
+  }
+  cand &= emask;
+  int64_t acc_sum = 0, acc_cnt = 0;
+  for (uint32_t cm = cand; cm; cm &= cm - 1) {
+    const int j = __builtin_ctz(cm);
+    Tile consider, sign, bits;
+    tile_load(consider, bv.payload, bv.meta[find_j(bsi.row_exists, j)], ws.lb);
+    if (qp.nprog) {
+      Tile f;
+      eval_tile(qp, views, s, j, ws, f);
+      tile_op<OP_AND>(consider, f);
+    }
+    acc_cnt += tile_popc(consider);
+    const int64_t cs = find_j(bsi.row_sign, j);
+    if (cs >= 0) tile_load(sign, bv.payload, bv.meta[cs], ws.lb);
+    else tile_zero(sign);
+    for (int i = 0; i < bsi.depth; i++) {
+      const int64_t cb = find_j(bsi.bit_row[i], j);
+      if (cb < 0) continue;
+      tile_load(bits, bv.payload, bv.meta[cb], ws.lb);
+      int pc = 0, nc = 0;
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        const uint64_t bx = bits.w[w].x & consider.w[w].x, by = bits.w[w].y & consider.w[w].y;
+        pc += __popcll(bx & ~sign.w[w].x) + __popcll(by & ~sign.w[w].y);
+        nc += __popcll(bx & sign.w[w].x) + __popcll(by & sign.w[w].y);
+      }
+      acc_sum += int64_t(uint64_t(int64_t(pc - nc)) << i);
+    }
+  }
+  acc_sum = wave_sum_i64(acc_sum);
+  acc_cnt = wave_sum_i64(acc_cnt);
+  if (lane == 0) {
+    if (acc_sum) atomicAdd(out_sum + q, (unsigned long long)acc_sum);
+    if (acc_cnt) atomicAdd(out_cnt + q, (unsigned long long)acc_cnt);
+  }
+}
+
+}  // namespace pk
+
+// ------------------------------------------------------------ launchers
+namespace pk {
+
+static inline unsigned grid_for(int64_t items) {
+  return unsigned((items + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+}
+
+void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int S, unsigned long long* out,
+                       int32_t* per_key, bool fast, hipStream_t st) {
+  const int64_t items = int64_t(Q) * S;
+  if (items == 0) return;
+  if (fast && per_key == nullptr)
+    hipLaunchKernelGGL(expr_count_kernel<true>, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
+                       Q, views, S, out, per_key);
+  else
+    hipLaunchKernelGGL(expr_count_kernel<false>, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
+                       Q, views, S, out, per_key);
+}
+
+void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views, int S, const int32_t* counts,
+                             const int64_t* offs, uint16_t* outp, hipStream_t st) {
+  const int64_t items = int64_t(Q) * S;
+  if (items == 0) return;
+  hipLaunchKernelGGL(expr_materialize_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
+                     Q, views, S, counts, offs, outp);
+}
+
+void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
+                    unsigned long long* out_sum, unsigned long long* out_cnt, hipStream_t st) {
+  const int64_t items = int64_t(Q) * S;
+  if (items == 0) return;
+  hipLaunchKernelGGL(bsi_sum_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs, Q, views,
+                     S, bsi, out_sum, out_cnt);
+}
+
+}  // namespace pk

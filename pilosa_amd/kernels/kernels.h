@@ -1,0 +1,58 @@
+// Shared host/device declarations for the gfx950 bitmap kernels.
+// The byte layouts of QueryProg / ViewDev / BsiArgs are mirrored by numpy
+// structured dtypes in pilosa_amd/ops/device.py (static_asserts below pin them).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pk {
+
+constexpr int MAXLEAF = 8;
+constexpr int MAXPROG = 16;
+constexpr int ARRAY_MAX = 4096;
+constexpr int CT_ARRAY = 1, CT_BITMAP = 2, CT_RUN = 3;
+// opcodes: 0..MAXLEAF-1 push leaf k; then binary ops
+constexpr int OP_AND = 16, OP_OR = 17, OP_XOR = 18, OP_ANDNOT = 19;
+
+// container metadata word (see pilosa_amd/native/pyroaring.cpp)
+__host__ __device__ __forceinline__ int meta_j(int64_t m) { return int(m & 15); }
+__host__ __device__ __forceinline__ int meta_type(int64_t m) { return int((m >> 4) & 3); }
+__host__ __device__ __forceinline__ int meta_n(int64_t m) { return int((m >> 6) & 0x1ffff); }
+__host__ __device__ __forceinline__ int64_t meta_off16(int64_t m) { return int64_t(uint64_t(m) >> 23); }
+
+struct QueryProg {
+  int32_t nleaf;
+  int32_t nprog;
+  int32_t leaf_view[MAXLEAF];
+  int64_t leaf_row[MAXLEAF];  // dense row index in the view, -1 = empty row
+  uint8_t prog[MAXPROG];
+  int64_t pad;
+};
+static_assert(sizeof(QueryProg) == 128, "QueryProg layout");
+
+struct ViewDev {
+  const uint32_t* rowptr;      // [S][D+1]
+  const int64_t* shard_base;   // [S+1]
+  const int64_t* meta;         // [C]
+  const uint16_t* payload;     // [P]
+  int64_t D;
+  int64_t pad[3];
+};
+static_assert(sizeof(ViewDev) == 64, "ViewDev layout");
+
+struct BsiArgs {
+  int32_t view;
+  int32_t depth;
+  int64_t row_exists;
+  int64_t row_sign;
+  int64_t bit_row[64];
+};
+
+void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int S, unsigned long long* out,
+                       int32_t* per_key, bool fast, hipStream_t st);
+void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views, int S, const int32_t* counts,
+                             const int64_t* offs, uint16_t* outp, hipStream_t st);
+void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
+                    unsigned long long* out_sum, unsigned long long* out_cnt, hipStream_t st);
+
+}  // namespace pk

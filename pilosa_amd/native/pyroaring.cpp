@@ -1,0 +1,544 @@
+// pybind11 bindings for the host roaring core (module pilosa_amd._roaring).
+//
+// Besides the Bitmap API used by the fragment layer, this module builds the
+// per-device container arena (build_arena) that the HIP kernels consume and
+// converts device result containers back into host bitmaps
+// (bitmap_from_containers).  Arena layout (one per field-view per GPU):
+//
+//   rows      u64[D]        sorted distinct row ids present in any local shard
+//   rowptr    u32[S*(D+1)]  per shard, CSR offsets (relative to shard_base[s])
+//                           of the first container of each row
+//   shard_base i64[S+1]     first container index of each shard
+//   meta      i64[C]        packed container descriptor:
+//                             bits 0-3   j    = key % 16 (container within row)
+//                             bits 4-5   type (1 array, 2 bitmap, 3 run)
+//                             bits 6-22  n    = cardinality (1..65536)
+//                             bits 23-63 payload offset in 16-byte units
+//   payload   u16[P]        array: n values (padded to 8); bitmap: 4096 u16
+//                           (1024 little-endian u64 words); run: 8-u16 header
+//                           (nruns at [0]) then (start,last) pairs, padded.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <thread>
+
+#include "roaring.hpp"
+
+namespace py = pybind11;
+using pr::Bitmap;
+using pr::Container;
+
+using u64arr = py::array_t<uint64_t, py::array::c_style | py::array::forcecast>;
+
+static u64arr to_np(const std::vector<uint64_t>& v) {
+  u64arr out(v.size());
+  if (!v.empty()) memcpy(out.mutable_data(), v.data(), v.size() * 8);
+  return out;
+}
+
+static size_t payload_u16(const Container& c) {
+  switch (c.type) {
+    case pr::CT_ARRAY: return (c.a.size() + 7) & ~size_t(7);
+    case pr::CT_BITMAP: return 4096;
+    case pr::CT_RUN: return 8 + ((c.r.size() * 2 + 7) & ~size_t(7));
+  }
+  return 0;
+}
+
+static void write_payload(const Container& c, uint16_t* dst) {
+  switch (c.type) {
+    case pr::CT_ARRAY:
+      memcpy(dst, c.a.data(), c.a.size() * 2);
+      break;
+    case pr::CT_BITMAP:
+      memcpy(dst, c.b.data(), 8192);
+      break;
+    case pr::CT_RUN:
+      dst[0] = uint16_t(c.r.size());
+      for (size_t i = 0; i < c.r.size(); i++) {
+        dst[8 + 2 * i] = c.r[i].start;
+        dst[9 + 2 * i] = c.r[i].last;
+      }
+      break;
+  }
+}
+
+static py::tuple build_arena(std::vector<py::object> shards, uint64_t cpr, int nthreads) {
+  if (cpr != 16) throw std::invalid_argument("build_arena: only 16 containers per row (ShardWidth 2^20) supported");
+  size_t S = shards.size();
+  std::vector<const Bitmap*> bms(S, nullptr);
+  for (size_t s = 0; s < S; s++)
+    if (!shards[s].is_none()) bms[s] = shards[s].cast<const Bitmap*>();
+
+  // distinct rows
+  std::vector<uint64_t> rows;
+  for (size_t s = 0; s < S; s++) {
+    if (!bms[s]) continue;
+    uint64_t last = ~0ull;
+    for (auto& kv : bms[s]->cs) {
+      if (!kv.second.n) continue;
+      uint64_t r = kv.first / cpr;
+      if (r != last) rows.push_back(r), last = r;
+    }
+  }
+  std::sort(rows.begin(), rows.end());
+  rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+  size_t D = rows.size();
+
+  // container counts per shard + payload sizes
+  std::vector<int64_t> shard_base(S + 1, 0), pay_base(S + 1, 0);
+  for (size_t s = 0; s < S; s++) {
+    int64_t nc = 0, np = 0;
+    if (bms[s])
+      for (auto& kv : bms[s]->cs)
+        if (kv.second.n) nc++, np += int64_t(payload_u16(kv.second));
+    shard_base[s + 1] = shard_base[s] + nc;
+    pay_base[s + 1] = pay_base[s] + np;
+  }
+  int64_t C = shard_base[S], P = pay_base[S];
+  py::array_t<uint64_t> rows_np(D);
+  if (D) memcpy(rows_np.mutable_data(), rows.data(), D * 8);
+  py::array_t<uint32_t> rowptr({(py::ssize_t)S, (py::ssize_t)(D + 1)});
+  py::array_t<int64_t> sb(S + 1);
+  memcpy(sb.mutable_data(), shard_base.data(), (S + 1) * 8);
+  py::array_t<int64_t> meta(std::max<int64_t>(C, 1));
+  py::array_t<uint16_t> payload(std::max<int64_t>(P, 8));
+  uint32_t* rp = rowptr.mutable_data();
+  int64_t* mp = meta.mutable_data();
+  uint16_t* pp = payload.mutable_data();
+  memset(pp, 0, size_t(std::max<int64_t>(P, 8)) * 2);
+  if (C == 0) mp[0] = 0;
+
+  auto work = [&](size_t s0, size_t s1) {
+    for (size_t s = s0; s < s1; s++) {
+      uint32_t* rps = rp + s * (D + 1);
+      int64_t ci = 0, pi = pay_base[s];
+      size_t d = 0;
+      if (bms[s]) {
+        for (auto& kv : bms[s]->cs) {
+          const Container& c = kv.second;
+          if (!c.n) continue;
+          uint64_t r = kv.first / cpr;
+          while (d < D && rows[d] < r) rps[d++] = uint32_t(ci);
+          if (d < D && rows[d] == r) rps[d++] = uint32_t(ci);  // first container of row r
+          // (subsequent containers of the same row do not advance d)
+          uint64_t j = kv.first % cpr;
+          uint64_t m = j | (uint64_t(c.type) << 4) | (uint64_t(c.n) << 6) | (uint64_t(pi / 8) << 23);
+          mp[shard_base[s] + ci] = int64_t(m);
+          write_payload(c, pp + pi);
+          pi += int64_t(payload_u16(c));
+          ci++;
+        }
+      }
+      while (d <= D) rps[d++] = uint32_t(ci);
+    }
+  };
+  {
+    py::gil_scoped_release nogil;
+    int nt = std::max(1, std::min<int>(nthreads, int(S)));
+    std::vector<std::thread> th;
+    size_t per = (S + nt - 1) / std::max(nt, 1);
+    for (int t = 0; t < nt; t++) {
+      size_t a = t * per, b = std::min(S, a + per);
+      if (a < b) th.emplace_back(work, a, b);
+    }
+    for (auto& t : th) t.join();
+  }
+  return py::make_tuple(rows_np, rowptr, sb, meta, payload);
+}
+
+// Device results → host bitmap.  keys u64[K], types u8[K], ns i32[K],
+// offs i64[K] (u16 units into payload), payload u16[].
+static Bitmap bitmap_from_containers(py::array_t<uint64_t> keys, py::array_t<uint8_t> types,
+                                     py::array_t<int32_t> ns, py::array_t<int64_t> offs,
+                                     py::array_t<uint16_t> payload) {
+  Bitmap out;
+  auto K = keys.size();
+  const uint64_t* kp = keys.data();
+  const uint8_t* tp = types.data();
+  const int32_t* np_ = ns.data();
+  const int64_t* op = offs.data();
+  const uint16_t* pp = payload.data();
+  for (py::ssize_t i = 0; i < K; i++) {
+    if (np_[i] <= 0) continue;
+    Container c;
+    c.type = tp[i];
+    c.n = np_[i];
+    const uint16_t* src = pp + op[i];
+    if (c.type == pr::CT_ARRAY) {
+      c.a.assign(src, src + c.n);
+    } else if (c.type == pr::CT_BITMAP) {
+      c.b.resize(pr::BITMAP_N);
+      memcpy(c.b.data(), src, 8192);
+      c.recount();
+      if (c.n == 0) continue;
+    } else {
+      throw std::invalid_argument("bitmap_from_containers: unsupported type");
+    }
+    out.cs[kp[i]] = std::move(c);
+  }
+  return out;
+}
+
+
+// ------------------------------------------------------------------ synthetic data
+// Deterministic synthetic set-field generator writing the device arena layout
+// directly (no host Bitmaps), used by bench.py for the 1M-row x 1B-column
+// config.  Row r has column density d_r = min(1, bits_per_col * (v+r)^-s / Z),
+// Z = sum_k (v+k)^-s, i.e. the reference's Zipf(s=1.6, v=50) row generator
+// (fragment_internal_test.go:2377-2460) drawn bits_per_col times per column.
+// Sparse row-shards draw Poisson(d_r * cols) uniform positions; dense ones draw
+// a per-container count and place it stratified (distinct, sorted).
+namespace {
+struct Rng {
+  uint64_t s;
+  explicit Rng(uint64_t seed) : s(seed) {}
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  double uni() { return double(next() >> 11) * (1.0 / 9007199254740992.0); }
+  int64_t poisson(double lam) {
+    if (lam <= 0) return 0;
+    if (lam < 30) {
+      double L = std::exp(-lam), p = 1.0;
+      int64_t k = 0;
+      do { k++; p *= uni(); } while (p > L);
+      return k - 1;
+    }
+    double u1 = std::max(uni(), 1e-300), u2 = uni();
+    double z = std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    int64_t k = int64_t(std::llround(lam + std::sqrt(lam) * z));
+    return k < 0 ? 0 : k;
+  }
+};
+inline uint64_t mix3(uint64_t a, uint64_t b, uint64_t c) {
+  Rng r(a * 0x100000001B3ull ^ (b << 21) ^ (c * 0xD6E8FEB86659FD93ull));
+  r.next();
+  return r.next();
+}
+}  // namespace
+
+static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t total_cols, int64_t nrows,
+                                double bits_per_col, double zs, double zv, uint64_t seed, int nthreads) {
+  const int64_t S = shard_hi - shard_lo;
+  const int64_t R = nrows;
+  std::vector<double> dens(R);
+  {
+    double Z = 0;
+    for (int64_t r = 0; r < R; r++) Z += std::pow(zv + double(r), -zs);
+    for (int64_t r = 0; r < R; r++) dens[r] = std::min(1.0, bits_per_col * std::pow(zv + double(r), -zs) / Z);
+  }
+  struct ShardOut {
+    std::vector<uint32_t> rowptr;
+    std::vector<int64_t> meta;   // offsets relative to shard payload start
+    std::vector<uint16_t> payload;
+  };
+  std::vector<ShardOut> outs(S);
+  auto work = [&](int64_t s0, int64_t s1) {
+    std::vector<uint64_t> pos;
+    std::vector<uint64_t> words(1024);
+    for (int64_t si = s0; si < s1; si++) {
+      const int64_t shard = shard_lo + si;
+      const int64_t cols = std::max<int64_t>(0, std::min<int64_t>(1 << 20, total_cols - shard * (1 << 20)));
+      ShardOut& o = outs[si];
+      o.rowptr.assign(R + 1, 0);
+      auto emit = [&](int j, const uint16_t* vals, int n, const uint64_t* w) {
+        // n values sorted distinct (vals) or bitmap words (w) when n > 4096
+        const int64_t off = int64_t(o.payload.size());
+        int type;
+        if (n <= pr::ARRAY_MAX) {
+          type = pr::CT_ARRAY;
+          o.payload.insert(o.payload.end(), vals, vals + n);
+          o.payload.resize((o.payload.size() + 7) & ~size_t(7), 0);
+        } else {
+          type = pr::CT_BITMAP;
+          const uint16_t* p = reinterpret_cast<const uint16_t*>(w);
+          o.payload.insert(o.payload.end(), p, p + 4096);
+        }
+        o.meta.push_back(int64_t(uint64_t(j) | (uint64_t(type) << 4) | (uint64_t(n) << 6) | (uint64_t(off / 8) << 23)));
+      };
+      std::vector<uint16_t> vals;
+      for (int64_t r = 0; r < R; r++) {
+        o.rowptr[r] = uint32_t(o.meta.size());
+        if (cols == 0) continue;
+        Rng rng(mix3(seed, uint64_t(shard), uint64_t(r)));
+        const double lam_row = dens[r] * double(cols);
+        if (lam_row < 2048.0) {
+          int64_t N = rng.poisson(lam_row);
+          if (N == 0) continue;
+          pos.resize(N);
+          for (int64_t k = 0; k < N; k++) pos[k] = rng.next() % uint64_t(cols);
+          std::sort(pos.begin(), pos.end());
+          pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+          size_t i = 0;
+          while (i < pos.size()) {
+            int j = int(pos[i] >> 16);
+            vals.clear();
+            while (i < pos.size() && int(pos[i] >> 16) == j) vals.push_back(uint16_t(pos[i] & 0xffff)), i++;
+            emit(j, vals.data(), int(vals.size()), nullptr);
+          }
+        } else {
+          for (int j = 0; j < 16; j++) {
+            const int64_t lim = std::min<int64_t>(65536, cols - int64_t(j) * 65536);
+            if (lim <= 0) break;
+            int64_t n = dens[r] >= 1.0 ? lim : rng.poisson(dens[r] * double(lim));
+            n = std::min<int64_t>(n, lim);
+            if (n == 0) continue;
+            // stratified distinct positions
+            vals.resize(n);
+            for (int64_t k = 0; k < n; k++) {
+              int64_t a = k * lim / n, b = (k + 1) * lim / n;
+              vals[k] = uint16_t(a + int64_t(rng.next() % uint64_t(std::max<int64_t>(1, b - a))));
+            }
+            if (n > pr::ARRAY_MAX) {
+              std::fill(words.begin(), words.end(), 0);
+              for (int64_t k = 0; k < n; k++) words[vals[k] >> 6] |= 1ull << (vals[k] & 63);
+              emit(j, nullptr, int(n), words.data());
+            } else {
+              emit(j, vals.data(), int(n), nullptr);
+            }
+          }
+        }
+      }
+      o.rowptr[R] = uint32_t(o.meta.size());
+    }
+  };
+  {
+    py::gil_scoped_release nogil;
+    int nt = std::max<int>(1, std::min<int64_t>(nthreads, S));
+    std::vector<std::thread> th;
+    std::atomic<int64_t> next{0};
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&]() {
+        for (;;) {
+          int64_t s = next.fetch_add(1);
+          if (s >= S) break;
+          work(s, s + 1);
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  // concatenate
+  std::vector<int64_t> sb(S + 1, 0), pb(S + 1, 0);
+  for (int64_t s = 0; s < S; s++) {
+    sb[s + 1] = sb[s] + int64_t(outs[s].meta.size());
+    pb[s + 1] = pb[s] + int64_t(outs[s].payload.size());
+  }
+  py::array_t<uint64_t> rows_np(R);
+  for (int64_t r = 0; r < R; r++) rows_np.mutable_data()[r] = uint64_t(r);
+  py::array_t<uint32_t> rowptr({(py::ssize_t)S, (py::ssize_t)(R + 1)});
+  py::array_t<int64_t> sbn(S + 1);
+  memcpy(sbn.mutable_data(), sb.data(), (S + 1) * 8);
+  py::array_t<int64_t> meta(std::max<int64_t>(sb[S], 1));
+  py::array_t<uint16_t> payload(std::max<int64_t>(pb[S], 8));
+  {
+    py::gil_scoped_release nogil;
+    uint32_t* rp = rowptr.mutable_data();
+    int64_t* mp = meta.mutable_data();
+    uint16_t* pp = payload.mutable_data();
+    if (sb[S] == 0) mp[0] = 0;
+    if (pb[S] == 0) memset(pp, 0, 16);
+    std::vector<std::thread> th;
+    std::atomic<int64_t> next{0};
+    int nt = std::max<int>(1, std::min<int64_t>(nthreads, S));
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&]() {
+        for (;;) {
+          int64_t s = next.fetch_add(1);
+          if (s >= S) break;
+          ShardOut& o = outs[s];
+          memcpy(rp + s * (R + 1), o.rowptr.data(), (R + 1) * 4);
+          const int64_t poff16 = pb[s] / 8;
+          for (size_t i = 0; i < o.meta.size(); i++) {
+            uint64_t m = uint64_t(o.meta[i]);
+            uint64_t off = (m >> 23) + uint64_t(poff16);
+            mp[sb[s] + int64_t(i)] = int64_t((m & ((1ull << 23) - 1)) | (off << 23));
+          }
+          if (!o.payload.empty()) memcpy(pp + pb[s], o.payload.data(), o.payload.size() * 2);
+          ShardOut().rowptr.swap(o.rowptr);
+          std::vector<int64_t>().swap(o.meta);
+          std::vector<uint16_t>().swap(o.payload);
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  return py::make_tuple(rows_np, rowptr, sbn, meta, payload);
+}
+
+// Rebuild a host Bitmap for one local shard of an arena (CPU oracle / baseline).
+static Bitmap arena_shard_bitmap(py::array_t<uint64_t> rows, py::array_t<uint32_t> rowptr,
+                                 py::array_t<int64_t> shard_base, py::array_t<int64_t> meta,
+                                 py::array_t<uint16_t> payload, int64_t s) {
+  Bitmap out;
+  const int64_t D = rows.size();
+  const uint32_t* rp = rowptr.data() + s * (D + 1);
+  const int64_t base = shard_base.data()[s];
+  const int64_t* mp = meta.data();
+  const uint16_t* pp = payload.data();
+  for (int64_t d = 0; d < D; d++) {
+    for (uint32_t c = rp[d]; c < rp[d + 1]; c++) {
+      uint64_t m = uint64_t(mp[base + c]);
+      int j = int(m & 15), type = int((m >> 4) & 3), n = int((m >> 6) & 0x1ffff);
+      const uint16_t* src = pp + (m >> 23) * 8;
+      Container ct;
+      ct.type = uint8_t(type);
+      ct.n = n;
+      if (type == pr::CT_ARRAY) ct.a.assign(src, src + n);
+      else if (type == pr::CT_BITMAP) { ct.b.resize(1024); memcpy(ct.b.data(), src, 8192); }
+      else {
+        int nr = src[0];
+        ct.r.resize(nr);
+        for (int i = 0; i < nr; i++) ct.r[i] = {src[8 + 2 * i], src[9 + 2 * i]};
+      }
+      out.cs.emplace_hint(out.cs.end(), rows.data()[d] * 16 + uint64_t(j), std::move(ct));
+    }
+  }
+  return out;
+}
+
+PYBIND11_MODULE(_roaring, m) {
+  m.doc() = "Host roaring core (containers, pilosa file format, op log, device arena builder)";
+  m.attr("ARRAY_MAX") = pr::ARRAY_MAX;
+  m.attr("RUN_MAX") = pr::RUN_MAX;
+  m.attr("MAGIC") = pr::MAGIC;
+
+  py::class_<Bitmap>(m, "Bitmap")
+      .def(py::init<>())
+      .def(py::init([](u64arr vals) {
+        Bitmap b;
+        std::vector<uint64_t> v(vals.data(), vals.data() + vals.size());
+        std::sort(v.begin(), v.end());
+        b.add_many(v.data(), v.size());
+        return b;
+      }))
+      .def("add", &Bitmap::add)
+      .def("remove", &Bitmap::remove)
+      .def("contains", &Bitmap::contains)
+      .def("__contains__", &Bitmap::contains)
+      .def("add_many", [](Bitmap& b, u64arr vals, bool sorted) {
+        std::vector<uint64_t> v(vals.data(), vals.data() + vals.size());
+        if (!sorted) std::sort(v.begin(), v.end());
+        py::gil_scoped_release nogil;
+        return b.add_many(v.data(), v.size());
+      }, py::arg("values"), py::arg("sorted") = false)
+      .def("remove_many", [](Bitmap& b, u64arr vals) {
+        return b.remove_many(vals.data(), size_t(vals.size()));
+      })
+      .def("count", &Bitmap::count)
+      .def("__len__", &Bitmap::count)
+      .def("count_range", &Bitmap::count_range)
+      .def("any", &Bitmap::any)
+      .def("max", &Bitmap::max)
+      .def("min", &Bitmap::min)
+      .def("slice", [](const Bitmap& b) { return to_np(b.slice()); })
+      .def("slice_range", [](const Bitmap& b, uint64_t s, uint64_t e) { return to_np(b.slice_range(s, e)); })
+      .def("offset_range", &Bitmap::offset_range)
+      .def("intersect", &Bitmap::intersect, py::call_guard<py::gil_scoped_release>())
+      .def("union", &Bitmap::unite, py::call_guard<py::gil_scoped_release>())
+      .def("difference", &Bitmap::difference, py::call_guard<py::gil_scoped_release>())
+      .def("xor", &Bitmap::xor_, py::call_guard<py::gil_scoped_release>())
+      .def("intersection_count", &Bitmap::intersection_count, py::call_guard<py::gil_scoped_release>())
+      .def("union_in_place", [](Bitmap& b, std::vector<const Bitmap*> others) {
+        py::gil_scoped_release nogil;
+        b.union_in_place(others);
+      })
+      .def("shift", &Bitmap::shift)
+      .def("flip", &Bitmap::flip)
+      .def("optimize", &Bitmap::optimize)
+      .def("clone", [](const Bitmap& b) { return Bitmap(b); })
+      .def("equals", &Bitmap::equals)
+      .def("__eq__", &Bitmap::equals)
+      .def("check", &Bitmap::check)
+      .def_readwrite("flags", &Bitmap::flags)
+      .def_readwrite("ops", &Bitmap::ops)
+      .def_readwrite("opn", &Bitmap::opn)
+      .def("container_count", [](const Bitmap& b) { return b.cs.size(); })
+      .def("keys", [](const Bitmap& b) {
+        std::vector<uint64_t> k;
+        for (auto& kv : b.cs)
+          if (kv.second.n) k.push_back(kv.first);
+        return to_np(k);
+      })
+      .def("container_info", [](const Bitmap& b) {
+        py::list out;
+        for (auto& kv : b.cs) {
+          static const char* names[] = {"nil", "array", "bitmap", "run"};
+          out.append(py::make_tuple(kv.first, names[kv.second.type & 3], kv.second.n));
+        }
+        return out;
+      })
+      .def("to_bytes", [](Bitmap& b) {
+        std::string s = b.to_bytes();
+        return py::bytes(s);
+      })
+      .def_static("from_bytes", [](py::bytes data) {
+        std::string s = data;
+        Bitmap b;
+        b.from_bytes(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+        return b;
+      })
+      .def("load_bytes", [](Bitmap& b, py::buffer data) {
+        py::buffer_info info = data.request();
+        b.from_bytes(reinterpret_cast<const uint8_t*>(info.ptr), size_t(info.size * info.itemsize));
+      })
+      .def("import_roaring", [](Bitmap& b, py::bytes data, bool clear, uint64_t cpr) {
+        std::string s = data;
+        std::map<uint64_t, int64_t> rd;
+        int64_t ch = b.import_roaring(reinterpret_cast<const uint8_t*>(s.data()), s.size(), clear, cpr, &rd);
+        py::dict d;
+        for (auto& kv : rd) d[py::int_(kv.first)] = kv.second;
+        return py::make_tuple(ch, d);
+      }, py::arg("data"), py::arg("clear") = false, py::arg("containers_per_row") = 16)
+      .def("row_counts", [](const Bitmap& b, uint64_t cpr) {
+        // count per row (row = key / cpr), used by rank-cache rebuilds
+        py::dict d;
+        uint64_t cur = ~0ull;
+        int64_t acc = 0;
+        for (auto& kv : b.cs) {
+          if (!kv.second.n) continue;
+          uint64_t r = kv.first / cpr;
+          if (r != cur) {
+            if (cur != ~0ull) d[py::int_(cur)] = acc;
+            cur = r;
+            acc = 0;
+          }
+          acc += kv.second.n;
+        }
+        if (cur != ~0ull) d[py::int_(cur)] = acc;
+        return d;
+      }, py::arg("containers_per_row") = 16)
+      .def("row_ids", [](const Bitmap& b, uint64_t cpr) {
+        std::vector<uint64_t> rows;
+        uint64_t cur = ~0ull;
+        for (auto& kv : b.cs) {
+          if (!kv.second.n) continue;
+          uint64_t r = kv.first / cpr;
+          if (r != cur) rows.push_back(r), cur = r;
+        }
+        return to_np(rows);
+      }, py::arg("containers_per_row") = 16);
+
+  m.def("encode_op", [](uint8_t typ, uint64_t value, u64arr values, py::bytes roaring, uint32_t opn) {
+    std::string r = roaring;
+    return py::bytes(pr::encode_op(typ, value, values.data(), size_t(values.size()), r, opn));
+  }, py::arg("typ"), py::arg("value") = 0, py::arg("values") = u64arr(0), py::arg("roaring") = py::bytes(""),
+     py::arg("opn") = 0);
+  m.def("fnv32a", [](py::bytes data) {
+    std::string s = data;
+    return pr::fnv32a(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  m.def("build_arena", &build_arena, py::arg("shards"), py::arg("containers_per_row") = 16,
+        py::arg("nthreads") = 8);
+  m.def("bitmap_from_containers", &bitmap_from_containers);
+  m.def("gen_zipf_arena", &gen_zipf_arena, py::arg("shard_lo"), py::arg("shard_hi"), py::arg("total_cols"),
+        py::arg("nrows"), py::arg("bits_per_col") = 8.0, py::arg("zipf_s") = 1.6, py::arg("zipf_v") = 50.0,
+        py::arg("seed") = 1, py::arg("nthreads") = 8);
+  m.def("arena_shard_bitmap", &arena_shard_bitmap);
+}

@@ -1,0 +1,140 @@
+// Host roaring core for the MI355X bitmap index.
+//
+// 64-bit roaring bitmap: key = value >> 16 selects a container holding the low
+// 16 bits.  Three container encodings (array / bitmap / run) as in the
+// reference (roaring/roaring.go:46-51, ArrayMaxSize=4096 :1984, runMaxSize=2048
+// :1987).  This is the authoritative host copy of every fragment and the CPU
+// oracle the HIP kernels are tested against.  It also owns the bit-exact
+// Pilosa file format (roaring.go:1052-1122 writer, :1562-1653 reader), the
+// official-roaring reader (:5081-5139) and the op-log WAL codec
+// (:4416-4559, fnv32a checksums).
+//
+// Design notes (ours, not the reference's):
+//  * containers live in a std::map keyed by the 48-bit high key; payloads are
+//    plain vectors (no mmap aliasing / frozen copy-on-write: the GPU arena is
+//    the read-mostly replica, the host copy is mutable);
+//  * pairwise ops have merge fast paths for array/array and word-parallel
+//    paths for everything else; results are canonicalised (array if n<=4096,
+//    else bitmap); runs only appear through optimize() or file loads;
+//  * export_containers()/build_arena() flatten a set of shard bitmaps into the
+//    device arena layout consumed by pilosa_amd/kernels/bitmap_kernels.hip.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+#include <utility>
+#include <stdexcept>
+
+namespace pr {
+
+constexpr int ARRAY_MAX = 4096;
+constexpr int RUN_MAX = 2048;
+constexpr int BITMAP_N = 1024;
+constexpr uint32_t MAGIC = 12348;
+constexpr uint32_t STORAGE_VERSION = 0;
+constexpr int HEADER_BASE = 8;
+constexpr uint32_t OFFICIAL_NORUN = 12346;
+constexpr uint32_t OFFICIAL_RUN = 12347;
+
+enum : uint8_t { CT_NIL = 0, CT_ARRAY = 1, CT_BITMAP = 2, CT_RUN = 3 };
+
+struct Iv {
+  uint16_t start, last;
+};
+
+struct Container {
+  uint8_t type = CT_ARRAY;
+  int32_t n = 0;
+  std::vector<uint16_t> a;   // sorted values (array)
+  std::vector<uint64_t> b;   // 1024 words (bitmap)
+  std::vector<Iv> r;         // sorted disjoint runs (run)
+
+  bool empty() const { return n == 0; }
+  bool contains(uint16_t v) const;
+  bool add(uint16_t v);
+  bool remove(uint16_t v);
+  void to_words(uint64_t* w) const;          // OR-materialise into w (w must be zeroed)
+  void set_words(const uint64_t* w);         // canonical array/bitmap from words
+  int count_runs() const;
+  int32_t count_range(int start, int end) const;  // [start,end) in 0..65536
+  int max() const;
+  int min() const;
+  void optimize();
+  void to_bitmap();
+  void to_array();
+  void to_run();
+  size_t encoded_size() const;               // bytes in pilosa file
+  std::string check() const;
+  void recount();
+};
+
+Container c_intersect(const Container& x, const Container& y);
+Container c_union(const Container& x, const Container& y);
+Container c_difference(const Container& x, const Container& y);
+Container c_xor(const Container& x, const Container& y);
+int64_t c_intersection_count(const Container& x, const Container& y);
+
+// op log
+enum OpType : uint8_t {
+  OP_ADD = 0, OP_REMOVE = 1, OP_ADD_BATCH = 2, OP_REMOVE_BATCH = 3,
+  OP_ADD_ROARING = 4, OP_REMOVE_ROARING = 5
+};
+
+uint32_t fnv32a(const uint8_t* p, size_t n, uint32_t h = 2166136261u);
+std::string encode_op(uint8_t typ, uint64_t value, const uint64_t* values, size_t nvalues,
+                      const std::string& roaring, uint32_t opn);
+
+class Bitmap {
+ public:
+  std::map<uint64_t, Container> cs;
+  uint8_t flags = 0;
+  int64_t ops = 0;   // number of ops replayed/logged
+  int64_t opn = 0;   // number of bits touched by ops
+
+  Bitmap() = default;
+
+  bool add(uint64_t v);
+  bool remove(uint64_t v);
+  bool contains(uint64_t v) const;
+  int64_t add_many(const uint64_t* v, size_t n);
+  int64_t remove_many(const uint64_t* v, size_t n);
+  int64_t count() const;
+  int64_t count_range(uint64_t start, uint64_t end) const;
+  bool any() const;
+  uint64_t max() const;
+  uint64_t min() const;
+  std::vector<uint64_t> slice() const;
+  std::vector<uint64_t> slice_range(uint64_t start, uint64_t end) const;
+  Bitmap offset_range(uint64_t offset, uint64_t start, uint64_t end) const;
+  Bitmap intersect(const Bitmap& o) const;
+  Bitmap unite(const Bitmap& o) const;
+  Bitmap difference(const Bitmap& o) const;
+  Bitmap xor_(const Bitmap& o) const;
+  int64_t intersection_count(const Bitmap& o) const;
+  void union_in_place(const std::vector<const Bitmap*>& others);
+  Bitmap shift(int n) const;
+  Bitmap flip(uint64_t start, uint64_t end) const;
+  void optimize();
+  void remove_empty();
+  bool equals(const Bitmap& o) const;
+  std::string check() const;
+
+  // serialization
+  std::string to_bytes();                           // pilosa format (optimizes)
+  void from_bytes(const uint8_t* data, size_t n);   // pilosa or official; replays op log
+  // merge a serialized roaring blob without keeping it; returns changed bits and
+  // per-row deltas (row = key / containers_per_row)
+  int64_t import_roaring(const uint8_t* data, size_t n, bool clear, uint64_t containers_per_row,
+                         std::map<uint64_t, int64_t>* rowdelta);
+
+ private:
+  void parse_pilosa(const uint8_t* data, size_t n, size_t* ops_offset);
+  void parse_official(const uint8_t* data, size_t n);
+  void replay_ops(const uint8_t* data, size_t n);
+};
+
+Container& get_or_create(Bitmap& b, uint64_t key);
+
+}  // namespace pr
