@@ -78,10 +78,19 @@ __device__ __forceinline__ void lds_expand(uint64_t* lb, const uint16_t* payload
   const int type = meta_type(m);
   const uint16_t* p = payload + meta_off16(m) * 8;
   if (type == CT_ARRAY) {
+    // 16-byte loads: 8 values per lane per instruction (payload is 16B aligned,
+    // padded to a multiple of 8 values; the tail is masked by index).
     const int n = meta_n(m);
-    for (int e = lane; e < n; e += 64) {
-      uint32_t v = p[e];
-      atomicOr(reinterpret_cast<unsigned long long*>(&lb[v >> 6]), 1ull << (v & 63));
+    const uint4* p4 = reinterpret_cast<const uint4*>(p);
+    const int n8 = (n + 7) >> 3;
+    for (int e8 = lane; e8 < n8; e8 += 64) {
+      const uint4 v4 = p4[e8];
+      const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
+        if (e8 * 8 + k < n) atomicOr(reinterpret_cast<unsigned long long*>(&lb[v >> 6]), 1ull << (v & 63));
+      }
     }
   } else {  // run
     const int nr = p[0];
@@ -211,6 +220,26 @@ __device__ __forceinline__ void eval_tile(const QueryProg& qp, const ViewDev* vi
   }
 }
 
+// Count array values whose bit is set in the 1024-word bitmap `bm` (global or
+// LDS); 16-byte loads of 8 values per lane.
+__device__ __forceinline__ int probe_array(const uint64_t* bm, const uint16_t* arr, int n) {
+  const int lane = wave_lane();
+  const uint4* p4 = reinterpret_cast<const uint4*>(arr);
+  const int n8 = (n + 7) >> 3;
+  int c = 0;
+  for (int e8 = lane; e8 < n8; e8 += 64) {
+    const uint4 v4 = p4[e8];
+    const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
+      const int hit = int((bm[v >> 6] >> (v & 63)) & 1);
+      c += (e8 * 8 + k < n) ? hit : 0;
+    }
+  }
+  return c;
+}
+
 // |A ∩ B| for two containers with a type-pair dispatch (no full tiles for arrays).
 __device__ __forceinline__ int and2_count(const ViewDev& va, int64_t ma, const ViewDev& vb, int64_t mb,
                                           uint64_t* lb) {
@@ -237,17 +266,29 @@ __device__ __forceinline__ int and2_count(const ViewDev& va, int64_t ma, const V
     return tile_popc(a);
   }
   if (ta == CT_BITMAP || tb == CT_BITMAP) {
-    // probe the bitmap with the array values
+    // probe the bitmap with the array values; large arrays first stage the
+    // 8 KiB bitmap into LDS with coalesced 16 B loads (random 8 B global
+    // probes would touch every line anyway).
     const bool abit = ta == CT_BITMAP;
     const uint64_t* bw = reinterpret_cast<const uint64_t*>((abit ? va.payload : vb.payload) +
                                                            meta_off16(abit ? ma : mb) * 8);
     const int64_t am = abit ? mb : ma;
     const uint16_t* arr = (abit ? vb.payload : va.payload) + meta_off16(am) * 8;
     const int n = meta_n(am);
-    for (int e = lane; e < n; e += 64) {
-      const uint32_t v = arr[e];
-      c += (bw[v >> 6] >> (v & 63)) & 1;
+    const uint64_t* probe = bw;
+    if (n >= 256) {
+      const ulong2* src = reinterpret_cast<const ulong2*>(bw);
+      ulong2* l2 = reinterpret_cast<ulong2*>(lb);
+      ulong2 t[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) t[i] = src[i * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 8; i++) l2[i * 64 + lane] = t[i];
+      lds_fence();
+      probe = lb;
     }
+    c = probe_array(probe, arr, n);
+    if (n >= 256) lds_fence();
     return c;
   }
   // array & array: scatter the larger into LDS, probe with the smaller
@@ -256,12 +297,7 @@ __device__ __forceinline__ int and2_count(const ViewDev& va, int64_t ma, const V
   const ViewDev& vbig = abig ? va : vb;
   const ViewDev& vsmall = abig ? vb : va;
   lds_expand(lb, vbig.payload, mbig);
-  const uint16_t* arr = vsmall.payload + meta_off16(msmall) * 8;
-  const int n = meta_n(msmall);
-  for (int e = lane; e < n; e += 64) {
-    const uint32_t v = arr[e];
-    c += (lb[v >> 6] >> (v & 63)) & 1;
-  }
+  c = probe_array(lb, vsmall.payload + meta_off16(msmall) * 8, meta_n(msmall));
   lds_fence();
   return c;
 }

@@ -65,57 +65,78 @@ class CompileError(Exception):
     pass
 
 
-def compile_expr(expr, view_index: Dict[int, int]) -> Tuple[np.void, List[object]]:
-    """Compile an Expr tree to one QueryProg record.
+def compile_expr(expr, view_index: Dict[int, int]):
+    """Compile an Expr tree to (leaf_views, leaf_rows, prog).
 
     ``view_index`` maps id(DeviceView) -> slot in the batch view table (it is
     extended as new views are seen).  Raises CompileError when the tree does
     not fit the kernel's limits (8 leaves, 16 ops, stack depth 4).
     """
-    leaves: List[Tuple[int, int]] = []
+    leaf_views: List[int] = []
+    leaf_rows: List[int] = []
     leaf_ids: Dict[Tuple[int, int], int] = {}
     prog: List[int] = []
     depth = [0, 0]  # current, max
 
-    def push():
-        depth[0] += 1
-        depth[1] = max(depth[1], depth[0])
-
     def emit(node):
-        if isinstance(node, Leaf):
+        if type(node) is Leaf:
             v = node.view
-            vi = view_index.setdefault(id(v), len(view_index))
+            vi = view_index.get(id(v))
+            if vi is None:
+                vi = view_index[id(v)] = len(view_index)
             d = v.dense(node.row)
             key = (vi, d)
-            if key not in leaf_ids:
-                if len(leaves) >= MAXLEAF:
+            k = leaf_ids.get(key)
+            if k is None:
+                if len(leaf_views) >= MAXLEAF:
                     raise CompileError("too many leaves")
-                leaf_ids[key] = len(leaves)
-                leaves.append(key)
-            prog.append(leaf_ids[key])
-            push()
+                k = leaf_ids[key] = len(leaf_views)
+                leaf_views.append(vi)
+                leaf_rows.append(d)
+            prog.append(k)
+            depth[0] += 1
+            if depth[0] > depth[1]:
+                depth[1] = depth[0]
             return
-        if not isinstance(node, Op) or node.op not in _OPS:
+        if type(node) is not Op or node.op not in _OPS:
             raise CompileError(f"bad node {node!r}")
         args = node.args
         if len(args) == 0:
             raise CompileError("empty op")
         emit(args[0])
+        code = _OPS[node.op]
         for a in args[1:]:
             emit(a)
-            prog.append(_OPS[node.op])
+            prog.append(code)
             depth[0] -= 1
     emit(expr)
     if len(prog) > MAXPROG or depth[1] > 4:
         raise CompileError("program too large")
-    rec = np.zeros((), dtype=QPROG_DTYPE)
-    rec["nleaf"] = len(leaves)
-    rec["nprog"] = len(prog)
-    for i, (vi, d) in enumerate(leaves):
-        rec["leaf_view"][i] = vi
-        rec["leaf_row"][i] = d
-    rec["prog"][: len(prog)] = prog
-    return rec, leaves
+    return leaf_views, leaf_rows, prog
+
+
+def pack_programs(compiled) -> np.ndarray:
+    """List of (leaf_views, leaf_rows, prog) -> QPROG_DTYPE array."""
+    Q = len(compiled)
+    progs = np.zeros(Q, dtype=QPROG_DTYPE)
+    lv = np.zeros((Q, MAXLEAF), np.int32)
+    lr = np.zeros((Q, MAXLEAF), np.int64)
+    pg = np.zeros((Q, MAXPROG), np.uint8)
+    nl = np.zeros(Q, np.int32)
+    npg = np.zeros(Q, np.int32)
+    for i, (v, r, p) in enumerate(compiled):
+        n = len(v)
+        nl[i] = n
+        lv[i, :n] = v
+        lr[i, :n] = r
+        npg[i] = len(p)
+        pg[i, :len(p)] = p
+    progs["nleaf"] = nl
+    progs["nprog"] = npg
+    progs["leaf_view"] = lv
+    progs["leaf_row"] = lr
+    progs["prog"] = pg
+    return progs
 
 
 # ---------------------------------------------------------------- arena
@@ -199,23 +220,23 @@ class GpuEngine:
     def compile_batch(self, exprs: Sequence[object]):
         view_index: Dict[int, int] = {}
         views: Dict[int, DeviceView] = {}
-        progs = np.zeros(len(exprs), dtype=QPROG_DTYPE)
-        S = None
 
         def collect(node):
-            if isinstance(node, Leaf):
+            if type(node) is Leaf:
                 views[id(node.view)] = node.view
-            elif isinstance(node, Op):
+            elif type(node) is Op:
                 for a in node.args:
                     collect(a)
 
-        for i, e in enumerate(exprs):
+        compiled = []
+        for e in exprs:
             collect(e)
-            rec, _ = compile_expr(e, view_index)
-            progs[i] = rec
+            compiled.append(compile_expr(e, view_index))
+        progs = pack_programs(compiled)
         ordered = [None] * len(view_index)
         for vid, slot in view_index.items():
             ordered[slot] = views[vid]
+        S = None
         for v in ordered:
             if S is None:
                 S = v.S
@@ -234,31 +255,52 @@ class GpuEngine:
         p = rec["prog"]
         return n == 1 or (n == 3 and p[0] == 0 and p[1] == 1 and p[2] == OP_AND)
 
-    def count_async(self, exprs: Sequence[object]):
-        """Launch counts for a batch; returns the device int64[Q] result tensor.
+    def prepare_count(self, exprs: Sequence[object], sort: bool = True):
+        """Host half of a count batch: compile, order, split by kernel flavour
+        and upload the programs.  Returns a handle for :meth:`launch_count`.
 
-        The batch is split by program shape: Count(Row) / Count(Intersect(a,b))
-        go to the low-register fast kernel, everything else to the generic
-        tile interpreter; both write into the same output vector."""
+        Queries are reordered by their leaf rows so that consecutive work items
+        (same shard, neighbouring queries) touch the same hot containers and
+        hit in the XCD's L2; results are scattered back to submission order."""
         torch = self.torch
         progs, views, S = self.compile_batch(exprs)
         Q = len(exprs)
-        out = torch.zeros(Q, dtype=torch.int64, device=self.device)
         if not S or not Q:
-            return out
-        fast = np.fromiter((self._is_fast(progs[i]) for i in range(Q)), dtype=bool, count=Q)
+            return (Q, S, None, [])
+        np_ = progs["nprog"]
+        pg = progs["prog"]
+        lr = progs["leaf_row"]
+        fast = (np_ == 1) | ((np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND))
         tv = self._views_tensor(views)
-        if fast.all() or not fast.any():
-            tp = torch.from_numpy(progs.view(np.uint8)).to(self.device, non_blocking=True)
-            self.ext.expr_count(tp, tv, S, out, None, bool(fast.all()))
-            return out
+        parts = []
         for sel, is_fast in ((np.nonzero(fast)[0], True), (np.nonzero(~fast)[0], False)):
+            if len(sel) == 0:
+                continue
+            if sort and len(sel) > 1:
+                sel = sel[np.lexsort((lr[sel, 1], lr[sel, 0]))]
             sub = np.ascontiguousarray(progs[sel])
             tp = torch.from_numpy(sub.view(np.uint8)).to(self.device, non_blocking=True)
-            o = torch.zeros(len(sel), dtype=torch.int64, device=self.device)
+            ti = torch.from_numpy(sel.astype(np.int64)).to(self.device, non_blocking=True)
+            parts.append((tp, ti, is_fast, len(sel)))
+        return (Q, S, tv, parts)
+
+    def launch_count(self, handle):
+        """Device half: launch the kernels; returns the device int64[Q] result."""
+        torch = self.torch
+        Q, S, tv, parts = handle
+        out = torch.zeros(Q, dtype=torch.int64, device=self.device)
+        for tp, ti, is_fast, n in parts:
+            o = torch.zeros(n, dtype=torch.int64, device=self.device)
             self.ext.expr_count(tp, tv, S, o, None, is_fast)
-            out.index_copy_(0, torch.from_numpy(sel).to(self.device), o)
+            out.index_copy_(0, ti, o)
         return out
+
+    def count_async(self, exprs: Sequence[object]):
+        """Launch counts for a batch; returns the device int64[Q] result tensor.
+
+        Count(Row) / Count(Intersect(a,b)) programs go to the low-register fast
+        kernel, everything else to the generic tile interpreter."""
+        return self.launch_count(self.prepare_count(exprs))
 
     def count(self, exprs: Sequence[object]) -> np.ndarray:
         return self.count_async(exprs).cpu().numpy()
@@ -304,7 +346,6 @@ class GpuEngine:
         exprs = [f for f in filters if f is not None]
         view_index: Dict[int, int] = {id(bsi_view): 0}
         views = {id(bsi_view): bsi_view}
-        progs = np.zeros(len(filters), dtype=QPROG_DTYPE)
 
         def collect(node):
             if isinstance(node, Leaf):
@@ -313,12 +354,14 @@ class GpuEngine:
                 for a in node.args:
                     collect(a)
 
-        for i, f in enumerate(filters):
+        compiled = []
+        for f in filters:
             if f is None:
+                compiled.append(([], [], []))
                 continue
             collect(f)
-            rec, _ = compile_expr(f, view_index)
-            progs[i] = rec
+            compiled.append(compile_expr(f, view_index))
+        progs = pack_programs(compiled)
         ordered = [None] * len(view_index)
         for vid, slot in view_index.items():
             ordered[slot] = views[vid]

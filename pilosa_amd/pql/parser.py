@@ -31,6 +31,7 @@ _BARE = re.compile(r"[A-Za-z0-9\-_:]+")
 _UINT = re.compile(r"[1-9][0-9]*|0")
 _CONDINT = re.compile(r"-?[1-9][0-9]*|0")
 _SP = re.compile(r"[ \t\n]*")
+_CALL_AHEAD = re.compile(r"[A-Za-z][A-Za-z0-9]*\(")
 _INT64_MIN, _INT64_MAX = -(1 << 63), (1 << 63) - 1
 
 
@@ -59,7 +60,10 @@ class Parser:
 
     # ------------------------------------------------------------ lexing helpers
     def sp(self, i: int) -> int:
-        return _SP.match(self.s, i).end()
+        s = self.s
+        if i < self.n and s[i] not in " \t\n":
+            return i
+        return _SP.match(s, i).end()
 
     def lit(self, i: int, t: str) -> int:
         if self.s.startswith(t, i):
@@ -227,6 +231,15 @@ class Parser:
     # ------------------------------------------------------------ args
     def _allargs(self, i, a: _Args, children: List[Call]):
         # Call (comma Call)* (comma args)? / args / sp
+        if not _CALL_AHEAD.match(self.s, i):
+            try:
+                sub = _Args()
+                k = self._args(i, sub)
+                for kk, vv in sub.d.items():
+                    a.put(kk, vv)
+                return k
+            except _Fail:
+                return self.sp(i)
         try:
             k, c = self.call(i)
             kids = [c]
@@ -280,6 +293,14 @@ class Parser:
         return self.rx(i, _FIELD)
 
     def _arg(self, i, a: _Args):
+        # fast path: field '=' value
+        m = _FIELD.match(self.s, i)
+        if m and not self.s.startswith("_", i):
+            k = self.sp(m.end())
+            if self.s.startswith("=", k) and not self.s.startswith("==", k):
+                k, v = self._value(self.sp(k + 1))
+                a.put(m.group(0), v)
+                return k
         # field sp '=' sp value
         try:
             k, f = self._field(i)
@@ -428,10 +449,12 @@ class Parser:
         for word, val in (("null", None), ("true", True), ("false", False)):
             if self.s.startswith(word, i) and self._peek_end(i + len(word)):
                 return i + len(word), val
-        try:
-            return self._timestampfmt(i)
-        except _Fail:
-            pass
+        c0 = self.s[i:i + 1]
+        if c0 in ('"', "'") or c0.isdigit():
+            try:
+                return self._timestampfmt(i)
+            except _Fail:
+                pass
         m = _NUM1.match(self.s, i) or _NUM2.match(self.s, i)
         if m:
             return m.end(), self._num(m.group(0))
