@@ -51,6 +51,23 @@ def build_roaring(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_pql(force: bool = False, verbose: bool = False) -> str:
+    import pybind11
+
+    out = os.path.join(PKG, "_pql" + _ext_suffix())
+    src = os.path.join(HERE, "pql_parser.cpp")
+    if not force and not _newer(out, [src]):
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-std=c++17", "-O2", "-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
+           "-I", sysconfig.get_paths()["include"], src, "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def hip_sources():
     return [os.path.join(KDIR, f) for f in sorted(os.listdir(KDIR))
             if f.endswith((".hip", ".cpp", ".h", ".hpp"))]
@@ -107,6 +124,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
 
 def build_all(force: bool = False, verbose: bool = False):
     r = build_roaring(force, verbose)
+    build_pql(force, verbose)
     h = build_hip(force, verbose) if os.path.exists(os.path.join(KDIR, "binding.cpp")) else None
     return r, h
 

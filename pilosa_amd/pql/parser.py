@@ -512,6 +512,19 @@ def _unquote(raw: str) -> str:
     return "".join(out)
 
 
+def parse_string_py(s: str) -> Query:
+    """Pure-Python parser (executable specification of the native one)."""
+    return Parser(s).parse()
+
+
+try:  # native parser (pilosa_amd/native/pql_parser.cpp)
+    from pilosa_amd import _pql as _native
+except ImportError:  # pragma: no cover - build() not run yet
+    _native = None
+
+
 def parse_string(s: str) -> Query:
     """Parse a PQL string (pql/parser.go:49 ParseString)."""
+    if _native is not None:
+        return Query(_native.parse_calls(s))
     return Parser(s).parse()
