@@ -1,0 +1,199 @@
+"""TopN count caches (reference: cache.go).
+
+* ``RankCache`` – id -> count map with a sorted ``rankings`` list; new entries
+  below the threshold (count of the first trimmed item) are ignored, rankings
+  are recomputed at most every 10 s on ``invalidate`` (cache.go:235-243), and
+  entries are trimmed once they exceed 1.1 x max (cache.go:245-281).
+* ``LRUCache`` – bounded LRU of counts (cache.go:58-133).
+* ``NopCache``.
+* ``Pair``/``Pairs`` helpers incl. ``pairs_add`` (cache.go:356-375).
+
+Ordering is (count desc, id asc) so results are deterministic (Go's sort.Sort
+is unstable; the reference leaves tie order unspecified).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+import time
+from typing import Dict, Iterable, List, Tuple
+
+THRESHOLD_FACTOR = 1.1
+CACHE_TYPE_RANKED = "ranked"
+CACHE_TYPE_LRU = "lru"
+CACHE_TYPE_NONE = "none"
+DEFAULT_CACHE_SIZE = 50000
+INVALIDATE_INTERVAL_S = 10.0
+
+
+class Pair:
+    __slots__ = ("id", "key", "count")
+
+    def __init__(self, id: int, count: int, key: str = ""):
+        self.id = int(id)
+        self.count = int(count)
+        self.key = key
+
+    def to_json(self):
+        d = {"id": self.id, "count": self.count}
+        if self.key:
+            d["key"] = self.key
+        return d
+
+    def __eq__(self, other):
+        return isinstance(other, Pair) and (self.id, self.count, self.key) == (other.id, other.count, other.key)
+
+    def __repr__(self):
+        return f"Pair({self.id}, {self.count}{', ' + repr(self.key) if self.key else ''})"
+
+
+def sort_pairs(pairs: List[Pair]) -> List[Pair]:
+    return sorted(pairs, key=lambda p: (-p.count, p.id))
+
+
+def pairs_add(a: Iterable[Pair], b: Iterable[Pair]) -> List[Pair]:
+    m: Dict[int, int] = collections.OrderedDict()
+    for p in a:
+        m[p.id] = p.count
+    for p in b:
+        m[p.id] = m.get(p.id, 0) + p.count
+    return [Pair(k, v) for k, v in m.items()]
+
+
+class NopCache:
+    def add(self, id, n):
+        pass
+
+    def bulk_add(self, id, n):
+        pass
+
+    def get(self, id):
+        return 0
+
+    def __len__(self):
+        return 0
+
+    def ids(self):
+        return []
+
+    def invalidate(self):
+        pass
+
+    def recalculate(self):
+        pass
+
+    def top(self) -> List[Tuple[int, int]]:
+        return []
+
+
+class LRUCache:
+    def __init__(self, max_entries: int):
+        self.max_entries = int(max_entries)
+        self._d: "collections.OrderedDict[int, int]" = collections.OrderedDict()
+        self._lock = threading.Lock()
+
+    def add(self, id, n):
+        with self._lock:
+            self._d[id] = n
+            self._d.move_to_end(id)
+            while self.max_entries > 0 and len(self._d) > self.max_entries:
+                self._d.popitem(last=False)
+
+    bulk_add = add
+
+    def get(self, id):
+        with self._lock:
+            n = self._d.get(id)
+            if n is None:
+                return 0
+            self._d.move_to_end(id)
+            return n
+
+    def __len__(self):
+        return len(self._d)
+
+    def ids(self):
+        return sorted(self._d)
+
+    def invalidate(self):
+        pass
+
+    def recalculate(self):
+        pass
+
+    def top(self):
+        return sorted(self._d.items(), key=lambda kv: (-kv[1], kv[0]))
+
+
+class RankCache:
+    def __init__(self, max_entries: int):
+        self.max_entries = int(max_entries)
+        self.threshold_buffer = int(THRESHOLD_FACTOR * self.max_entries)
+        self.entries: Dict[int, int] = {}
+        self.rankings: List[Tuple[int, int]] = []
+        self.threshold_value = 0
+        self.update_time = 0.0
+        self._lock = threading.Lock()
+
+    def add(self, id, n):
+        with self._lock:
+            if n < self.threshold_value and n > 0:
+                return
+            self.entries[id] = n
+            self._invalidate()
+
+    def bulk_add(self, id, n):
+        with self._lock:
+            if n < self.threshold_value:
+                return
+            self.entries[id] = n
+
+    def get(self, id):
+        with self._lock:
+            return self.entries.get(id, 0)
+
+    def __len__(self):
+        return len(self.entries)
+
+    def ids(self):
+        with self._lock:
+            return sorted(self.entries)
+
+    def invalidate(self):
+        with self._lock:
+            self._invalidate()
+
+    def recalculate(self):
+        with self._lock:
+            self._recalculate()
+
+    def _invalidate(self):
+        if time.monotonic() - self.update_time < INVALIDATE_INTERVAL_S:
+            return
+        self._recalculate()
+
+    def _recalculate(self):
+        rankings = sorted(self.entries.items(), key=lambda kv: (-kv[1], kv[0]))
+        remove = []
+        if len(rankings) > self.max_entries:
+            self.threshold_value = rankings[self.max_entries][1]
+            remove = rankings[self.max_entries:]
+            rankings = rankings[: self.max_entries]
+        else:
+            self.threshold_value = 1
+        self.rankings = rankings
+        self.update_time = time.monotonic()
+        if len(self.entries) > self.threshold_buffer:
+            for id, _ in remove:
+                self.entries.pop(id, None)
+
+    def top(self):
+        return self.rankings
+
+
+def new_cache(cache_type: str, size: int):
+    if cache_type == CACHE_TYPE_RANKED:
+        return RankCache(size)
+    if cache_type == CACHE_TYPE_LRU:
+        return LRUCache(size)
+    return NopCache()

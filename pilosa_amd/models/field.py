@@ -1,0 +1,538 @@
+"""Field: a typed column family of views (reference: field.go).
+
+Types: ``set`` (ranked/LRU TopN cache), ``int`` (bit-sliced integer, view
+``bsig_<name>``, sign-magnitude with base offset and on-demand bit depth
+growth), ``time`` (standard + one view per time quantum unit), ``mutex`` (at
+most one row per column) and ``bool`` (rows 0/1, mutex semantics).
+Options persist in ``.meta`` (protobuf FieldOptions, reference-compatible);
+``.available.shards`` is a roaring bitmap of shards with data anywhere in the
+cluster (local fragments + remote shards learned from peers).
+"""
+from __future__ import annotations
+
+import datetime as dt
+import os
+import shutil
+import threading
+from dataclasses import dataclass, field as dc_field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from pilosa_amd import _roaring
+from pilosa_amd.errors import (ErrBSIGroupNotFound, ErrBSIGroupValueTooHigh, ErrBSIGroupValueTooLow,
+                               ErrInvalidCacheType, ErrInvalidTimeQuantum, ErrInvalidView, PilosaError,
+                               validate_name)
+from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
+from pilosa_amd.models.cache import CACHE_TYPE_LRU, CACHE_TYPE_NONE, CACHE_TYPE_RANKED, DEFAULT_CACHE_SIZE
+from pilosa_amd.models.fragment import SHARD_WIDTH
+from pilosa_amd.models.row import Row
+from pilosa_amd.models.timeq import valid_quantum, views_by_time
+from pilosa_amd.models.view import VIEW_BSI_PREFIX, VIEW_STANDARD, View
+
+FIELD_TYPE_SET, FIELD_TYPE_INT, FIELD_TYPE_TIME, FIELD_TYPE_MUTEX, FIELD_TYPE_BOOL = \
+    "set", "int", "time", "mutex", "bool"
+FIELD_TYPES = (FIELD_TYPE_SET, FIELD_TYPE_INT, FIELD_TYPE_TIME, FIELD_TYPE_MUTEX, FIELD_TYPE_BOOL)
+MAX_INT = (1 << 63) - 1
+
+
+def bit_depth(v: int) -> int:
+    for i in range(63):
+        if v < (1 << i):
+            return i
+    return 63
+
+
+def bit_depth_int64(v: int) -> int:
+    return bit_depth(abs(v))
+
+
+@dataclass
+class FieldOptions:
+    type: str = ""
+    cache_type: str = ""
+    cache_size: int = 0
+    time_quantum: str = ""
+    min: int = 0
+    max: int = 0
+    keys: bool = False
+    no_standard_view: bool = False
+    base: int = 0
+    bit_depth: int = 0
+
+    @classmethod
+    def default(cls) -> "FieldOptions":
+        return cls(type=FIELD_TYPE_SET, cache_type=CACHE_TYPE_RANKED, cache_size=DEFAULT_CACHE_SIZE)
+
+    def to_json(self) -> dict:
+        """Type-dependent JSON (field.go:1430-1496)."""
+        t = self.type
+        if t in (FIELD_TYPE_SET, FIELD_TYPE_MUTEX):
+            return {"type": t, "cacheType": self.cache_type, "cacheSize": self.cache_size, "keys": self.keys}
+        if t == FIELD_TYPE_INT:
+            return {"type": t, "base": self.base, "bitDepth": self.bit_depth, "min": self.min, "max": self.max,
+                    "keys": self.keys}
+        if t == FIELD_TYPE_TIME:
+            return {"type": t, "timeQuantum": self.time_quantum, "keys": self.keys,
+                    "noStandardView": self.no_standard_view}
+        if t == FIELD_TYPE_BOOL:
+            return {"type": t}
+        raise PilosaError("invalid field type")
+
+    def to_pb(self):
+        from pilosa_amd.wire import pb
+        return pb.FieldOptions(Type=self.type, CacheType=self.cache_type, CacheSize=self.cache_size,
+                               TimeQuantum=self.time_quantum, Min=self.min, Max=self.max, Keys=self.keys,
+                               NoStandardView=self.no_standard_view, Base=self.base, BitDepth=self.bit_depth)
+
+    @classmethod
+    def from_pb(cls, m) -> "FieldOptions":
+        return cls(type=m.Type, cache_type=m.CacheType, cache_size=m.CacheSize, time_quantum=m.TimeQuantum,
+                   min=m.Min, max=m.Max, keys=m.Keys, no_standard_view=m.NoStandardView, base=m.Base,
+                   bit_depth=m.BitDepth)
+
+    @classmethod
+    def from_json(cls, d: dict) -> "FieldOptions":
+        """HTTP create-field options with per-type validation
+        (http/handler.go:811-901)."""
+        t = d.get("type", "") or ""
+        o = cls(type=t)
+        allowed = {
+            "": {"cacheType", "cacheSize", "keys", "type"},
+            FIELD_TYPE_SET: {"cacheType", "cacheSize", "keys", "type"},
+            FIELD_TYPE_MUTEX: {"cacheType", "cacheSize", "keys", "type"},
+            FIELD_TYPE_INT: {"min", "max", "keys", "type"},
+            FIELD_TYPE_TIME: {"timeQuantum", "keys", "noStandardView", "type"},
+            FIELD_TYPE_BOOL: {"type"},
+        }
+        if t not in allowed:
+            raise PilosaError(f"invalid field type: {t}")
+        for k in d:
+            if k not in allowed[t]:
+                raise PilosaError(f"{k} does not apply to field type {t or 'set'}")
+        if t in ("", FIELD_TYPE_SET, FIELD_TYPE_MUTEX):
+            o.type = t or FIELD_TYPE_SET
+            o.cache_type = d.get("cacheType", CACHE_TYPE_RANKED)
+            if o.cache_type not in (CACHE_TYPE_RANKED, CACHE_TYPE_LRU, CACHE_TYPE_NONE):
+                raise ErrInvalidCacheType
+            o.cache_size = int(d.get("cacheSize", DEFAULT_CACHE_SIZE))
+            o.keys = bool(d.get("keys", False))
+        elif t == FIELD_TYPE_INT:
+            if "min" not in d:
+                raise PilosaError("min is required for field type int")
+            if "max" not in d:
+                raise PilosaError("max is required for field type int")
+            o.min, o.max = int(d["min"]), int(d["max"])
+            if o.min > o.max:
+                raise PilosaError("int field min cannot be greater than max")
+            o.keys = bool(d.get("keys", False))
+        elif t == FIELD_TYPE_TIME:
+            if "timeQuantum" not in d:
+                raise PilosaError("timeQuantum is required for field type time")
+            o.time_quantum = d["timeQuantum"]
+            if not valid_quantum(o.time_quantum):
+                raise ErrInvalidTimeQuantum
+            o.keys = bool(d.get("keys", False))
+            o.no_standard_view = bool(d.get("noStandardView", False))
+        return o
+
+
+@dataclass
+class BSIGroup:
+    name: str
+    type: str = "int"
+    min: int = 0
+    max: int = 0
+    base: int = 0
+    bit_depth: int = 0
+
+    def bit_depth_min(self) -> int:
+        return self.base - (1 << self.bit_depth) + 1
+
+    def bit_depth_max(self) -> int:
+        return self.base + (1 << self.bit_depth) - 1
+
+    def base_value(self, op: str, value: int) -> Tuple[int, bool]:
+        """field.go:1526-1553 (out-of-range detection and clamping)."""
+        mn, mx = self.bit_depth_min(), self.bit_depth_max()
+        bv = 0
+        if op in (">", ">="):
+            if value > mx:
+                return bv, True
+            if value > mn:
+                bv = value - self.base
+        elif op in ("<", "<="):
+            if value < mn:
+                return bv, True
+            bv = (mx - self.base) if value > mx else (value - self.base)
+        elif op in ("==", "!="):
+            if value < mn or value > mx:
+                return bv, True
+            bv = value - self.base
+        return bv, False
+
+    def base_value_between(self, lo: int, hi: int) -> Tuple[int, int, bool]:
+        mn, mx = self.bit_depth_min(), self.bit_depth_max()
+        if hi < mn or lo > mx:
+            return 0, 0, True
+        lo, hi = max(lo, mn), min(hi, mx)
+        return lo - self.base, hi - self.base, False
+
+
+class Field:
+    def __init__(self, path: str, index: str, name: str, options: Optional[FieldOptions] = None,
+                 max_opn: int = 10000, stats=None, persistent_attrs: bool = True):
+        validate_name(name) if not name.startswith("_") else None
+        self.path = path
+        self.index = index
+        self.name = name
+        self.options = options or FieldOptions.default()
+        self.views: Dict[str, View] = {}
+        self.bsi: Optional[BSIGroup] = None
+        self.remote_available_shards = set()
+        self.local_shards = set()
+        self.max_opn = max_opn
+        self.stats = stats
+        self.mu = threading.RLock()
+        self.row_attr_store = SQLiteAttrStore(os.path.join(path, ".data")) if persistent_attrs else MemAttrStore()
+        self.on_create_shard = None  # holder/cluster broadcast hook (view.go:223-264)
+        self._apply_options(self.options)
+
+    # ------------------------------------------------------------ options
+    def _apply_options(self, o: FieldOptions):
+        t = o.type or FIELD_TYPE_SET
+        if t in (FIELD_TYPE_SET, FIELD_TYPE_MUTEX):
+            o.type = t
+            o.cache_type = o.cache_type or CACHE_TYPE_RANKED
+            if o.cache_type == CACHE_TYPE_NONE:
+                o.cache_size = 0
+            elif not o.cache_size:
+                o.cache_size = DEFAULT_CACHE_SIZE
+            o.min = o.max = o.base = o.bit_depth = 0
+            o.time_quantum = ""
+        elif t == FIELD_TYPE_INT:
+            o.cache_type, o.cache_size = CACHE_TYPE_NONE, 0
+            o.time_quantum = ""
+            if o.base == 0 and not (o.min <= 0 <= o.max):
+                # reference keeps base 0; values outside [min,max] are rejected
+                pass
+            self.bsi = BSIGroup(self.name, "int", o.min, o.max, o.base, o.bit_depth)
+        elif t == FIELD_TYPE_TIME:
+            o.cache_type, o.cache_size = CACHE_TYPE_NONE, 0
+            o.min = o.max = o.base = o.bit_depth = 0
+            if not valid_quantum(o.time_quantum):
+                raise ErrInvalidTimeQuantum
+        elif t == FIELD_TYPE_BOOL:
+            o.cache_type, o.cache_size = CACHE_TYPE_NONE, 0
+            o.min = o.max = o.base = o.bit_depth = 0
+            o.time_quantum = ""
+            o.keys = False
+        else:
+            raise PilosaError("invalid field type")
+        self.options = o
+
+    @property
+    def type(self) -> str:
+        return self.options.type
+
+    def keys(self) -> bool:
+        return self.options.keys
+
+    def time_quantum(self) -> str:
+        return self.options.time_quantum
+
+    def meta_path(self) -> str:
+        return os.path.join(self.path, ".meta")
+
+    def save_meta(self):
+        os.makedirs(self.path, exist_ok=True)
+        tmp = self.meta_path() + ".tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(self.options.to_pb().SerializeToString())
+        os.replace(tmp, self.meta_path())
+
+    def load_meta(self):
+        from pilosa_amd.wire import pb
+        if not os.path.exists(self.meta_path()):
+            return
+        m = pb.FieldOptions()
+        with open(self.meta_path(), "rb") as fh:
+            m.ParseFromString(fh.read())
+        self._apply_options(FieldOptions.from_pb(m))
+
+    def available_shards_path(self) -> str:
+        return os.path.join(self.path, ".available.shards")
+
+    def _save_available_shards(self):
+        bm = _roaring.Bitmap(np.array(sorted(self.remote_available_shards | self.local_shards), dtype=np.uint64))
+        tmp = self.available_shards_path() + ".tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(bm.to_bytes())
+        os.replace(tmp, self.available_shards_path())
+
+    def _load_available_shards(self):
+        p = self.available_shards_path()
+        if os.path.exists(p):
+            with open(p, "rb") as fh:
+                data = fh.read()
+            if data:
+                self.remote_available_shards |= {int(x) for x in _roaring.Bitmap.from_bytes(data).slice()}
+
+    # ------------------------------------------------------------ lifecycle
+    def open(self):
+        with self.mu:
+            os.makedirs(self.path, exist_ok=True)
+            self.load_meta()
+            self._load_available_shards()
+            self.row_attr_store.open()
+            vdir = os.path.join(self.path, "views")
+            os.makedirs(vdir, exist_ok=True)
+            for name in sorted(os.listdir(vdir)):
+                if os.path.isdir(os.path.join(vdir, name)):
+                    v = self._new_view(name).open()
+                    self.views[name] = v
+                    self.local_shards |= set(v.fragments)
+        return self
+
+    def close(self):
+        with self.mu:
+            for v in self.views.values():
+                v.close()
+            self.views.clear()
+            self.row_attr_store.close()
+
+    def delete(self):
+        self.close()
+        shutil.rmtree(self.path, ignore_errors=True)
+
+    def _new_view(self, name: str) -> View:
+        v = View(os.path.join(self.path, "views", name), self.index, self.name, name, field_obj=self)
+        return v
+
+    def view(self, name: str) -> Optional[View]:
+        return self.views.get(name)
+
+    def create_view_if_not_exists(self, name: str) -> View:
+        with self.mu:
+            v = self.views.get(name)
+            if v is None:
+                v = self._new_view(name).open()
+                self.views[name] = v
+            return v
+
+    def delete_view(self, name: str):
+        with self.mu:
+            v = self.views.pop(name, None)
+            if v is None:
+                raise ErrInvalidView
+            v.delete()
+
+    def _note_shard(self, shard: int):
+        if shard not in self.local_shards:
+            self.local_shards.add(shard)
+            try:
+                self._save_available_shards()
+            except OSError:
+                pass
+            if self.on_create_shard is not None:
+                self.on_create_shard(self, shard)
+
+    def available_shards(self) -> List[int]:
+        with self.mu:
+            local = set()
+            for v in self.views.values():
+                local |= set(v.fragments)
+            return sorted(local | self.remote_available_shards)
+
+    def add_remote_available_shards(self, shards: Iterable[int]):
+        with self.mu:
+            self.remote_available_shards |= {int(s) for s in shards}
+            self._save_available_shards()
+
+    def remove_available_shard(self, shard: int):
+        with self.mu:
+            self.remote_available_shards.discard(int(shard))
+            self._save_available_shards()
+
+    def bsi_group(self, name: Optional[str] = None) -> Optional[BSIGroup]:
+        if self.bsi is not None and (name is None or name == self.bsi.name):
+            return self.bsi
+        return None
+
+    def info(self) -> dict:
+        return {"name": self.name, "options": self.options.to_json(),
+                "views": [{"name": v} for v in sorted(self.views)]}
+
+    # ------------------------------------------------------------ rows / bits
+    def row(self, row_id: int, view: str = VIEW_STANDARD) -> Row:
+        v = self.views.get(view)
+        if v is None:
+            raise ErrInvalidView
+        return v.row(row_id)
+
+    def set_bit(self, row_id: int, col: int, t: Optional[dt.datetime] = None) -> bool:
+        changed = False
+        if not self.options.no_standard_view:
+            changed = self.create_view_if_not_exists(VIEW_STANDARD).set_bit(row_id, col) or changed
+        if t is None:
+            return changed
+        for name in views_by_time(VIEW_STANDARD, t, self.time_quantum()):
+            changed = self.create_view_if_not_exists(name).set_bit(row_id, col) or changed
+        return changed
+
+    def clear_bit(self, row_id: int, col: int) -> bool:
+        v = self.views.get(VIEW_STANDARD)
+        changed = False
+        if v is not None:
+            changed = v.clear_bit(row_id, col)
+        for name, tv in list(self.views.items()):
+            if name.startswith(VIEW_STANDARD + "_"):
+                changed = tv.clear_bit(row_id, col) or changed
+        return changed
+
+    # ------------------------------------------------------------ BSI
+    def bsi_view_name(self) -> str:
+        return VIEW_BSI_PREFIX + self.name
+
+    def value(self, col: int) -> Tuple[int, bool]:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        v = self.views.get(self.bsi_view_name())
+        if v is None:
+            return 0, False
+        val, ok = v.value(col, b.bit_depth)
+        if not ok:
+            return 0, False
+        return val + b.base, True
+
+    def _grow_bit_depth(self, base_value: int):
+        b = self.bsi
+        need = bit_depth_int64(base_value)
+        if need > b.bit_depth:
+            with self.mu:
+                b.bit_depth = need
+                self.options.bit_depth = need
+                self.save_meta()
+
+    def set_value(self, col: int, value: int) -> bool:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        if value < b.min:
+            raise ErrBSIGroupValueTooLow
+        if value > b.max:
+            raise ErrBSIGroupValueTooHigh
+        bv = value - b.base
+        self._grow_bit_depth(bv)
+        return self.create_view_if_not_exists(self.bsi_view_name()).set_value(col, b.bit_depth, bv)
+
+    def clear_value(self, col: int) -> bool:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        v = self.views.get(self.bsi_view_name())
+        if v is None:
+            return False
+        val, ok = v.value(col, b.bit_depth)
+        if not ok:
+            return False
+        return v.clear_value(col, b.bit_depth, val)
+
+    def sum(self, filt: Optional[Row]) -> Tuple[int, int]:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        v = self.views.get(self.bsi_view_name())
+        if v is None:
+            return 0, 0
+        s, c = v.sum(filt, b.bit_depth)
+        return s + c * b.base, c
+
+    def min(self, filt: Optional[Row]) -> Tuple[int, int]:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        v = self.views.get(self.bsi_view_name())
+        if v is None:
+            return 0, 0
+        m, c = v.min(filt, b.bit_depth)
+        return m + b.base, c
+
+    def max(self, filt: Optional[Row]) -> Tuple[int, int]:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        v = self.views.get(self.bsi_view_name())
+        if v is None:
+            return 0, 0
+        m, c = v.max(filt, b.bit_depth)
+        return m + b.base, c
+
+    # ------------------------------------------------------------ imports
+    def import_bits(self, row_ids: Sequence[int], col_ids: Sequence[int],
+                    timestamps: Optional[Sequence[Optional[dt.datetime]]] = None, clear: bool = False) -> int:
+        """field.go:1163-1241: split by (view, shard) and bulk import."""
+        rows = np.asarray(row_ids, dtype=np.uint64)
+        cols = np.asarray(col_ids, dtype=np.uint64)
+        if len(rows) != len(cols):
+            raise PilosaError("row/column length mismatch")
+        groups: Dict[Tuple[str, int], List[int]] = {}
+        shards = (cols >> np.uint64(20)).astype(np.int64)
+        q = self.time_quantum()
+        std_ok = not self.options.no_standard_view
+        if timestamps is None or all(t is None for t in timestamps):
+            if std_ok:
+                for s in np.unique(shards):
+                    groups[(VIEW_STANDARD, int(s))] = np.nonzero(shards == s)[0]
+        else:
+            tmp: Dict[Tuple[str, int], List[int]] = {}
+            for i, t in enumerate(timestamps):
+                s = int(shards[i])
+                if std_ok:
+                    tmp.setdefault((VIEW_STANDARD, s), []).append(i)
+                if t is not None:
+                    if not q:
+                        raise PilosaError("time quantum not set in field")
+                    for name in views_by_time(VIEW_STANDARD, t, q):
+                        tmp.setdefault((name, s), []).append(i)
+            groups = {k: np.array(v, dtype=np.int64) for k, v in tmp.items()}
+        changed = 0
+        for (vname, shard), idx in sorted(groups.items()):
+            frag = self.create_view_if_not_exists(vname).create_fragment_if_not_exists(shard)
+            changed += frag.bulk_import(rows[idx], cols[idx], clear=clear)
+        return changed
+
+    def import_values(self, col_ids: Sequence[int], values: Sequence[int], clear: bool = False) -> int:
+        b = self.bsi_group()
+        if b is None:
+            raise ErrBSIGroupNotFound
+        cols = np.asarray(col_ids, dtype=np.uint64)
+        vals = np.asarray(values, dtype=np.int64)
+        if len(vals):
+            if vals.min() < b.min:
+                raise PilosaError(f"{ErrBSIGroupValueTooLow}: {int(vals.min())} < {b.min}")
+            if vals.max() > b.max:
+                raise PilosaError(f"{ErrBSIGroupValueTooHigh}: {int(vals.max())} > {b.max}")
+            base_vals = vals - np.int64(b.base)
+            self._grow_bit_depth(int(max(abs(int(base_vals.min())), abs(int(base_vals.max())))))
+        else:
+            base_vals = vals
+        view = self.create_view_if_not_exists(self.bsi_view_name())
+        shards = (cols >> np.uint64(20)).astype(np.int64)
+        changed = 0
+        for s in np.unique(shards):
+            idx = shards == s
+            frag = view.create_fragment_if_not_exists(int(s))
+            changed += frag.import_value(cols[idx], base_vals[idx], b.bit_depth, clear=clear)
+        return changed
+
+    def import_roaring(self, shard: int, views: Dict[str, bytes], clear: bool = False) -> int:
+        changed = 0
+        for vname, data in views.items():
+            name = vname or VIEW_STANDARD
+            if self.type == FIELD_TYPE_INT:
+                name = self.bsi_view_name()
+            frag = self.create_view_if_not_exists(name).create_fragment_if_not_exists(int(shard))
+            changed += frag.import_roaring(data, clear)
+        return changed

@@ -1,0 +1,895 @@
+"""Fragment: one (index, field, view, shard) bitmap (reference: fragment.go).
+
+Storage is a host roaring ``Bitmap`` (C++ core) whose bit ``row*ShardWidth +
+col%ShardWidth`` is set for every (row, column) pair.  Durability follows the
+reference exactly: the file holds a Pilosa-format snapshot followed by an
+append-only op log (13-byte ops with fnv32a checksums); opening replays the
+log, a snapshot (write ``.snapshotting`` -> fsync -> rename) runs once more
+than ``max_opn`` bits were logged (fragment.go:2284-2381).  A ``.cache`` file
+(protobuf ``Cache{IDs}``) persists the TopN rank-cache membership.
+
+Every mutation bumps ``version`` so the GPU arena (pilosa_amd/ops/) knows when
+its HBM replica of this fragment is stale.
+"""
+from __future__ import annotations
+
+import fcntl
+import heapq
+import io
+import math
+import os
+import tarfile
+import threading
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import xxhash
+
+from pilosa_amd import _roaring
+from pilosa_amd.errors import PilosaError
+from pilosa_amd.models.cache import (CACHE_TYPE_NONE, CACHE_TYPE_RANKED, DEFAULT_CACHE_SIZE, Pair, new_cache,
+                                     sort_pairs)
+from pilosa_amd.models.row import Row
+
+Bitmap = _roaring.Bitmap
+
+SHARD_WIDTH_EXP = 20
+SHARD_WIDTH = 1 << SHARD_WIDTH_EXP
+CONTAINERS_PER_ROW = SHARD_WIDTH >> 16
+HASH_BLOCK_SIZE = 100
+DEFAULT_MAX_OPN = 10000
+FALSE_ROW_ID, TRUE_ROW_ID = 0, 1
+BSI_EXISTS_BIT, BSI_SIGN_BIT, BSI_OFFSET_BIT = 0, 1, 2
+ROARING_FLAG_BSI_V2 = 0x01
+
+OP_ADD, OP_REMOVE, OP_ADD_BATCH, OP_REMOVE_BATCH, OP_ADD_ROARING, OP_REMOVE_ROARING = range(6)
+
+
+def pos(row: int, col: int) -> int:
+    return row * SHARD_WIDTH + (col % SHARD_WIDTH)
+
+
+class TopOptions:
+    __slots__ = ("n", "src", "row_ids", "min_threshold", "filter_name", "filter_values", "tanimoto_threshold",
+                 "attr_store")
+
+    def __init__(self, n=0, src: Optional[Row] = None, row_ids: Optional[Sequence[int]] = None, min_threshold=0,
+                 filter_name="", filter_values=None, tanimoto_threshold=0, attr_store=None):
+        self.n = n
+        self.src = src
+        self.row_ids = list(row_ids or [])
+        self.min_threshold = min_threshold
+        self.filter_name = filter_name
+        self.filter_values = filter_values or []
+        self.tanimoto_threshold = tanimoto_threshold
+        self.attr_store = attr_store
+
+
+class Fragment:
+    def __init__(self, path: str, index: str, field: str, view: str, shard: int,
+                 cache_type: str = CACHE_TYPE_RANKED, cache_size: int = DEFAULT_CACHE_SIZE,
+                 max_opn: int = DEFAULT_MAX_OPN, mutex: bool = False, bool_field: bool = False, stats=None):
+        self.path = path
+        self.index, self.field, self.view, self.shard = index, field, view, int(shard)
+        self.cache_type = cache_type
+        self.cache_size = cache_size
+        self.max_opn = max_opn
+        self.mutex = mutex
+        self.bool_field = bool_field
+        self.storage = Bitmap()
+        self.cache = new_cache(cache_type, cache_size)
+        self.checksums: Dict[int, bytes] = {}
+        self.opn = 0
+        self.ops = 0
+        self.max_row_id = 0
+        self.version = 0
+        self.mu = threading.RLock()
+        self._fh = None
+        self._lockfd = None
+        self.stats = stats
+        self.row_attr_store = None
+
+    # ------------------------------------------------------------ lifecycle
+    def open(self):
+        with self.mu:
+            self._open_storage()
+            self._open_cache()
+        return self
+
+    def _open_storage(self):
+        os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+        if os.path.exists(self.path) and os.path.getsize(self.path) > 0:
+            with open(self.path, "rb") as fh:
+                data = fh.read()
+            try:
+                self.storage = Bitmap.from_bytes(data)
+            except Exception as e:  # noqa: BLE001
+                raise PilosaError(f"unmarshal storage: file={self.path}, err={e}")
+            self.opn = int(self.storage.opn)
+            self.ops = int(self.storage.ops)
+        else:
+            self.storage = Bitmap()
+            # new fragments start with a valid empty snapshot (BSI v2 flag)
+            self.storage.flags = ROARING_FLAG_BSI_V2
+            with open(self.path, "wb") as fh:
+                fh.write(self.storage.to_bytes())
+        self._fh = open(self.path, "ab", buffering=0)
+        try:
+            fcntl.flock(self._fh.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
+        except OSError as e:
+            raise PilosaError(f"flock: {e}")
+        self.max_row_id = int(self.storage.max()) // SHARD_WIDTH if self.storage.any() else 0
+        self.version += 1
+
+    def cache_path(self) -> str:
+        return self.path + ".cache"
+
+    def _open_cache(self):
+        if self.cache_type == CACHE_TYPE_NONE:
+            return
+        p = self.cache_path()
+        if not os.path.exists(p):
+            return
+        from pilosa_amd.wire import pb
+        m = pb.Cache()
+        try:
+            with open(p, "rb") as fh:
+                m.ParseFromString(fh.read())
+        except Exception:  # noqa: BLE001 - a corrupt cache is rebuilt
+            return
+        for rid in m.IDs:
+            n = self.storage.count_range(rid * SHARD_WIDTH, (rid + 1) * SHARD_WIDTH)
+            self.cache.bulk_add(rid, n)
+        self.cache.invalidate()
+
+    def flush_cache(self):
+        if self.cache_type == CACHE_TYPE_NONE:
+            return
+        from pilosa_amd.wire import pb
+        with self.mu:
+            ids = self.cache.ids()
+        data = pb.Cache(IDs=ids).SerializeToString()
+        tmp = self.cache_path() + ".tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(data)
+        os.replace(tmp, self.cache_path())
+
+    def close(self):
+        with self.mu:
+            try:
+                self.flush_cache()
+            except OSError:
+                pass
+            if self._fh is not None:
+                try:
+                    fcntl.flock(self._fh.fileno(), fcntl.LOCK_UN)
+                except OSError:
+                    pass
+                self._fh.close()
+                self._fh = None
+
+    # ------------------------------------------------------------ op log
+    def _log(self, typ: int, value: int = 0, values: Optional[np.ndarray] = None, roaring: bytes = b"",
+             opn: int = 0):
+        if self._fh is None:
+            return
+        vals = values if values is not None else np.zeros(0, dtype=np.uint64)
+        self._fh.write(_roaring.encode_op(typ, value, vals, roaring, opn))
+
+    def _increment_opn(self, changed: int):
+        if changed <= 0:
+            return
+        self.opn += changed
+        self.ops += 1
+        self.version += 1
+        if self.opn > self.max_opn:
+            self.snapshot()
+
+    def snapshot(self):
+        """Write storage + truncate the op log (write -> fsync -> rename)."""
+        with self.mu:
+            tmp = self.path + ".snapshotting"
+            data = self.storage.to_bytes()
+            with open(tmp, "wb") as fh:
+                fh.write(data)
+                fh.flush()
+                os.fsync(fh.fileno())
+            if self._fh is not None:
+                try:
+                    fcntl.flock(self._fh.fileno(), fcntl.LOCK_UN)
+                except OSError:
+                    pass
+                self._fh.close()
+            os.replace(tmp, self.path)
+            self._fh = open(self.path, "ab", buffering=0)
+            fcntl.flock(self._fh.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
+            self.opn = 0
+            self.ops = 0
+            if self.stats:
+                self.stats.count("snapshot", 1)
+
+    # ------------------------------------------------------------ rows
+    def row(self, row_id: int) -> Row:
+        with self.mu:
+            bm = self.storage.offset_range(self.shard * SHARD_WIDTH, row_id * SHARD_WIDTH,
+                                           (row_id + 1) * SHARD_WIDTH)
+        return Row.from_segment(self.shard, bm)
+
+    def row_bitmap(self, row_id: int) -> Bitmap:
+        with self.mu:
+            return self.storage.offset_range(self.shard * SHARD_WIDTH, row_id * SHARD_WIDTH,
+                                             (row_id + 1) * SHARD_WIDTH)
+
+    def row_count(self, row_id: int) -> int:
+        with self.mu:
+            return self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
+
+    def _pos(self, row_id: int, col: int) -> int:
+        lo = self.shard * SHARD_WIDTH
+        if col < lo or col >= lo + SHARD_WIDTH:
+            raise PilosaError(f"column:{col} out of bounds")
+        return pos(row_id, col)
+
+    def bit(self, row_id: int, col: int) -> bool:
+        return self.storage.contains(self._pos(row_id, col))
+
+    def _after_row_change(self, row_id: int, bulk: bool = False):
+        self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
+        if self.cache_type != CACHE_TYPE_NONE:
+            n = self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
+            if bulk:
+                self.cache.bulk_add(row_id, n)
+            else:
+                self.cache.add(row_id, n)
+        if row_id > self.max_row_id:
+            self.max_row_id = row_id
+
+    def _unprotected_set_bit(self, row_id: int, col: int) -> bool:
+        p = self._pos(row_id, col)
+        changed = self.storage.add(p)
+        if not changed:
+            return False
+        self._log(OP_ADD, p)
+        self._after_row_change(row_id)
+        self._increment_opn(1)
+        if self.stats:
+            self.stats.count("setBit", 1)
+        return True
+
+    def _unprotected_clear_bit(self, row_id: int, col: int) -> bool:
+        p = self._pos(row_id, col)
+        changed = self.storage.remove(p)
+        if not changed:
+            return False
+        self._log(OP_REMOVE, p)
+        self._after_row_change(row_id)
+        self._increment_opn(1)
+        if self.stats:
+            self.stats.count("clearBit", 1)
+        return True
+
+    def set_bit(self, row_id: int, col: int) -> bool:
+        with self.mu:
+            changed = False
+            if self.mutex or self.bool_field:
+                existing = self._vector_get(col)
+                if existing is not None and existing != row_id:
+                    self._unprotected_clear_bit(existing, col)
+                    changed = True
+            return self._unprotected_set_bit(row_id, col) or changed
+
+    def clear_bit(self, row_id: int, col: int) -> bool:
+        with self.mu:
+            return self._unprotected_clear_bit(row_id, col)
+
+    def _vector_get(self, col: int) -> Optional[int]:
+        rows = self.storage.rows_with_column(col % SHARD_WIDTH, CONTAINERS_PER_ROW)
+        if len(rows) > 1:
+            raise PilosaError("found multiple row values for column")
+        if len(rows) == 1:
+            r = int(rows[0])
+            if self.bool_field and r not in (FALSE_ROW_ID, TRUE_ROW_ID):
+                raise PilosaError("found non-boolean value")
+            return r
+        return None
+
+    def set_row(self, row: Row, row_id: int) -> bool:
+        """Replace ``row_id`` with the segment of ``row`` for this shard."""
+        with self.mu:
+            seg = row.segment(self.shard)
+            src = seg if seg is not None else Bitmap()
+            self.storage.set_row_from(row_id, src, self.shard * CONTAINERS_PER_ROW, CONTAINERS_PER_ROW)
+            self._after_row_change(row_id, bulk=True)
+            if self.cache_type != CACHE_TYPE_NONE:
+                self.cache.invalidate()
+            self.version += 1
+            self.snapshot()
+            return True
+
+    def clear_row(self, row_id: int) -> bool:
+        with self.mu:
+            changed = self.storage.clear_row(row_id, CONTAINERS_PER_ROW)
+            self.cache.add(row_id, 0)
+            self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
+            self.version += 1
+            self.snapshot()
+            return changed
+
+    # ------------------------------------------------------------ BSI
+    def value(self, col: int, bit_depth: int) -> Tuple[int, bool]:
+        with self.mu:
+            if not self.bit(BSI_EXISTS_BIT, col):
+                return 0, False
+            v = 0
+            for i in range(bit_depth):
+                if self.bit(BSI_OFFSET_BIT + i, col):
+                    v |= 1 << i
+            if self.bit(BSI_SIGN_BIT, col):
+                v = -v
+            return v, True
+
+    def _positions_for_values(self, cols: np.ndarray, values: np.ndarray, bit_depth: int, clear: bool):
+        cols = np.asarray(cols, dtype=np.uint64) % np.uint64(SHARD_WIDTH)
+        values = np.asarray(values, dtype=np.int64)
+        uval = np.abs(values).astype(np.uint64)
+        sets, clears = [], []
+        ex = np.uint64(BSI_EXISTS_BIT * SHARD_WIDTH) + cols
+        (clears if clear else sets).append(ex)
+        sg = np.uint64(BSI_SIGN_BIT * SHARD_WIDTH) + cols
+        neg = (values < 0) & (not clear)
+        sets.append(sg[neg])
+        clears.append(sg[~neg])
+        for i in range(bit_depth):
+            p = np.uint64((BSI_OFFSET_BIT + i) * SHARD_WIDTH) + cols
+            on = ((uval >> np.uint64(i)) & np.uint64(1)).astype(bool)
+            sets.append(p[on])
+            clears.append(p[~on])
+        s = np.concatenate(sets) if sets else np.zeros(0, np.uint64)
+        c = np.concatenate(clears) if clears else np.zeros(0, np.uint64)
+        return s, c
+
+    def set_value(self, col: int, bit_depth: int, value: int, clear: bool = False) -> bool:
+        with self.mu:
+            self._pos(0, col)
+            s, c = self._positions_for_values(np.array([col], np.uint64), np.array([value], np.int64), bit_depth,
+                                              clear)
+            return self._import_positions(s, c, range(bit_depth + 2)) > 0
+
+    def clear_value(self, col: int, bit_depth: int, value: int) -> bool:
+        return self.set_value(col, bit_depth, value, clear=True)
+
+    def sum(self, filt: Optional[Row], bit_depth: int) -> Tuple[int, int]:
+        """fragment.go:1109.  NB: negatives are filtered too (the reference
+        counts all negatives regardless of the filter; we apply it)."""
+        consider = self.row(BSI_EXISTS_BIT)
+        if filt is not None:
+            consider = consider.intersect(filt)
+        count = consider.count()
+        nrow = self.row(BSI_SIGN_BIT).intersect(consider)
+        prow = consider.difference(nrow)
+        total = 0
+        for i in range(bit_depth):
+            r = self.row(BSI_OFFSET_BIT + i)
+            total += (1 << i) * (r.intersection_count(prow) - r.intersection_count(nrow))
+        return _wrap_i64(total), count
+
+    def min(self, filt: Optional[Row], bit_depth: int) -> Tuple[int, int]:
+        consider = self.row(BSI_EXISTS_BIT)
+        if filt is not None:
+            consider = consider.intersect(filt)
+        if consider.count() == 0:
+            return 0, 0
+        neg = self.row(BSI_SIGN_BIT).intersect(consider)
+        if neg.any():
+            v, c = self._max_unsigned(neg, bit_depth)
+            return -v, c
+        return self._min_unsigned(consider, bit_depth)
+
+    def max(self, filt: Optional[Row], bit_depth: int) -> Tuple[int, int]:
+        consider = self.row(BSI_EXISTS_BIT)
+        if filt is not None:
+            consider = consider.intersect(filt)
+        if not consider.any():
+            return 0, 0
+        pos_ = consider.difference(self.row(BSI_SIGN_BIT))
+        if not pos_.any():
+            v, c = self._min_unsigned(consider, bit_depth)
+            return -v, c
+        return self._max_unsigned(pos_, bit_depth)
+
+    def _min_unsigned(self, filt: Row, bit_depth: int) -> Tuple[int, int]:
+        mn, count = 0, 0
+        for i in range(bit_depth - 1, -1, -1):
+            row = filt.difference(self.row(BSI_OFFSET_BIT + i))
+            count = row.count()
+            if count > 0:
+                filt = row
+            else:
+                mn += 1 << i
+                if i == 0:
+                    count = filt.count()
+        return mn, count
+
+    def _max_unsigned(self, filt: Row, bit_depth: int) -> Tuple[int, int]:
+        mx, count = 0, 0
+        for i in range(bit_depth - 1, -1, -1):
+            row = self.row(BSI_OFFSET_BIT + i).intersect(filt)
+            count = row.count()
+            if count > 0:
+                mx += 1 << i
+                filt = row
+            elif i == 0:
+                count = filt.count()
+        return mx, count
+
+    def range_op(self, op: str, bit_depth: int, predicate: int) -> Row:
+        if op == "==":
+            return self._range_eq(bit_depth, predicate)
+        if op == "!=":
+            return self.row(BSI_EXISTS_BIT).difference(self._range_eq(bit_depth, predicate))
+        if op in ("<", "<="):
+            return self._range_lt(bit_depth, predicate, op == "<=")
+        if op in (">", ">="):
+            return self._range_gt(bit_depth, predicate, op == ">=")
+        from pilosa_amd.errors import ErrInvalidRangeOperation
+        raise ErrInvalidRangeOperation
+
+    def not_null(self) -> Row:
+        return self.row(BSI_EXISTS_BIT)
+
+    def _range_eq(self, bit_depth, predicate):
+        b = self.row(BSI_EXISTS_BIT)
+        up = abs(predicate)
+        if predicate < 0:
+            b = b.intersect(self.row(BSI_SIGN_BIT))
+        else:
+            b = b.difference(self.row(BSI_SIGN_BIT))
+        for i in range(bit_depth - 1, -1, -1):
+            row = self.row(BSI_OFFSET_BIT + i)
+            b = b.intersect(row) if (up >> i) & 1 else b.difference(row)
+        return b
+
+    def _range_lt(self, bit_depth, predicate, allow_eq):
+        b = self.row(BSI_EXISTS_BIT)
+        up = abs(predicate)
+        if (predicate >= 0 and allow_eq) or (predicate >= -1 and not allow_eq):
+            pos_ = self._range_lt_unsigned(b.difference(self.row(BSI_SIGN_BIT)), bit_depth, up, allow_eq)
+            return self.row(BSI_SIGN_BIT).union(pos_)
+        return self._range_gt_unsigned(b.intersect(self.row(BSI_SIGN_BIT)), bit_depth, up, allow_eq)
+
+    def _range_lt_unsigned(self, filt: Row, bit_depth, predicate, allow_eq):
+        keep = Row()
+        leading_zeros = True
+        for i in range(bit_depth - 1, -1, -1):
+            row = self.row(BSI_OFFSET_BIT + i)
+            bit = (predicate >> i) & 1
+            if leading_zeros:
+                if bit == 0:
+                    filt = filt.difference(row)
+                    continue
+                leading_zeros = False
+            if i == 0 and not allow_eq:
+                if bit == 0:
+                    return keep
+                return filt.difference(row.difference(keep))
+            if bit == 0:
+                filt = filt.difference(row.difference(keep))
+                continue
+            if i > 0:
+                keep = keep.union(filt.difference(row))
+        return filt
+
+    def _range_gt(self, bit_depth, predicate, allow_eq):
+        b = self.row(BSI_EXISTS_BIT)
+        up = abs(predicate)
+        if (predicate >= 0 and allow_eq) or (predicate >= -1 and not allow_eq):
+            return self._range_gt_unsigned(b.difference(self.row(BSI_SIGN_BIT)), bit_depth, up, allow_eq)
+        neg = self._range_lt_unsigned(b.intersect(self.row(BSI_SIGN_BIT)), bit_depth, up, allow_eq)
+        return b.difference(self.row(BSI_SIGN_BIT)).union(neg)
+
+    def _range_gt_unsigned(self, filt: Row, bit_depth, predicate, allow_eq):
+        keep = Row()
+        for i in range(bit_depth - 1, -1, -1):
+            row = self.row(BSI_OFFSET_BIT + i)
+            bit = (predicate >> i) & 1
+            if i == 0 and not allow_eq:
+                if bit == 1:
+                    return keep
+                return filt.difference(filt.difference(row).difference(keep))
+            if bit == 1:
+                filt = filt.difference(filt.difference(row).difference(keep))
+                continue
+            if i > 0:
+                keep = keep.union(filt.intersect(row))
+        return filt
+
+    def range_between(self, bit_depth, pmin, pmax) -> Row:
+        b = self.row(BSI_EXISTS_BIT)
+        umin, umax = abs(pmin), abs(pmax)
+        if pmin >= 0:
+            return self._range_between_unsigned(b.difference(self.row(BSI_SIGN_BIT)), bit_depth, umin, umax)
+        if pmax < 0:
+            return self._range_between_unsigned(b.intersect(self.row(BSI_SIGN_BIT)), bit_depth, umax, umin)
+        pos_ = self._range_lt_unsigned(b.difference(self.row(BSI_SIGN_BIT)), bit_depth, umax, True)
+        neg = self._range_lt_unsigned(b.intersect(self.row(BSI_SIGN_BIT)), bit_depth, umin, True)
+        return pos_.union(neg)
+
+    def _range_between_unsigned(self, filt: Row, bit_depth, pmin, pmax):
+        keep1, keep2 = Row(), Row()
+        for i in range(bit_depth - 1, -1, -1):
+            row = self.row(BSI_OFFSET_BIT + i)
+            b1, b2 = (pmin >> i) & 1, (pmax >> i) & 1
+            if b1 == 1:
+                filt = filt.difference(filt.difference(row).difference(keep1))
+            elif i > 0:
+                keep1 = keep1.union(filt.intersect(row))
+            if b2 == 0:
+                filt = filt.difference(row.difference(keep2))
+            elif i > 0:
+                keep2 = keep2.union(filt.difference(row))
+        return filt
+
+    # ------------------------------------------------------------ min/max row
+    def min_row_id(self) -> Tuple[int, bool]:
+        if not self.storage.any():
+            return 0, False
+        return int(self.storage.min()) // SHARD_WIDTH, True
+
+    def min_row(self, filt: Optional[Row]) -> Tuple[int, int]:
+        mn, ok = self.min_row_id()
+        if not ok:
+            return 0, 0
+        if filt is None:
+            return mn, 1
+        for r in self.rows(mn):
+            c = self.row(r).intersection_count(filt)
+            if c > 0:
+                return r, c
+        return 0, 0
+
+    def max_row(self, filt: Optional[Row]) -> Tuple[int, int]:
+        mn, ok = self.min_row_id()
+        if not ok:
+            return 0, 0
+        mx = int(self.storage.max()) // SHARD_WIDTH
+        if filt is None:
+            return mx, 1
+        for r in reversed(self.rows(mn)):
+            c = self.row(r).intersection_count(filt)
+            if c > 0:
+                return r, c
+        return 0, 0
+
+    # ------------------------------------------------------------ rows listing
+    def rows(self, start: int = 0, column: Optional[int] = None, limit: Optional[int] = None,
+             row_filter: Optional[Sequence[int]] = None) -> List[int]:
+        """Non-empty row ids >= start (fragment.go:2675-2712 with the
+        column / rows / limit filters of :2601-2667)."""
+        with self.mu:
+            if column is not None:
+                ids = self.storage.rows_with_column(column % SHARD_WIDTH, CONTAINERS_PER_ROW)
+            else:
+                ids = self.storage.row_ids(CONTAINERS_PER_ROW)
+        ids = ids[ids >= np.uint64(start)] if len(ids) else ids
+        if row_filter is not None:
+            ids = ids[np.isin(ids, np.asarray(row_filter, dtype=np.uint64))]
+        out = [int(x) for x in ids]
+        if limit is not None:
+            out = out[:limit]
+        return out
+
+    # ------------------------------------------------------------ TopN
+    def top(self, opt: TopOptions) -> List[Pair]:
+        pairs = self._top_bitmap_pairs(opt.row_ids)
+        n = 0 if opt.row_ids else opt.n
+        filters = None
+        if opt.filter_name and opt.filter_values:
+            filters = set(_hashable(v) for v in opt.filter_values)
+        tan = 0
+        min_t = max_t = 0.0
+        src_count = 0
+        if opt.tanimoto_threshold > 0 and opt.src is not None:
+            tan = opt.tanimoto_threshold
+            src_count = opt.src.count()
+            min_t = float(src_count * tan) / 100
+            max_t = float(src_count * 100) / float(tan)
+        heap: List[Tuple[int, int]] = []  # (count, -id) min-heap
+        results: List[Pair] = []
+        for row_id, cnt in pairs:
+            if cnt == 0:
+                continue
+            if tan > 0:
+                if cnt <= min_t or cnt >= max_t:
+                    continue
+            elif cnt < opt.min_threshold:
+                continue
+            if filters is not None:
+                attrs = opt.attr_store.attrs(row_id) if opt.attr_store is not None else None
+                if not attrs or attrs.get(opt.filter_name) is None or \
+                        _hashable(attrs.get(opt.filter_name)) not in filters:
+                    continue
+            if n == 0 or len(heap) < n:
+                count = cnt
+                if opt.src is not None:
+                    count = opt.src.intersection_count(self.row(row_id))
+                if count == 0:
+                    continue
+                if tan > 0:
+                    t = math.ceil(float(count * 100) / float(cnt + src_count - count))
+                    if t <= tan:
+                        continue
+                elif count < opt.min_threshold:
+                    continue
+                heapq.heappush(heap, (count, -row_id))
+                if n > 0 and len(heap) == n and opt.src is None:
+                    break
+                continue
+            threshold = heap[0][0]
+            if threshold < opt.min_threshold or cnt < threshold:
+                break
+            count = opt.src.intersection_count(self.row(row_id))
+            if count < threshold:
+                continue
+            heapq.heappush(heap, (count, -row_id))
+        results = [Pair(-nid, c) for c, nid in heap]
+        return sort_pairs(results)
+
+    def _top_bitmap_pairs(self, row_ids: Sequence[int]) -> List[Tuple[int, int]]:
+        if self.cache_type == CACHE_TYPE_NONE and not row_ids:
+            return list(self.cache.top())
+        if not row_ids:
+            with self.mu:
+                self.cache.invalidate()
+                return list(self.cache.top())
+        out = []
+        for rid in row_ids:
+            n = self.cache.get(rid)
+            if n > 0:
+                out.append((rid, n))
+                continue
+            c = self.row_count(rid)
+            if c > 0:
+                out.append((rid, c))
+        out.sort(key=lambda kv: (-kv[1], kv[0]))
+        return out
+
+    def recalculate_cache(self):
+        with self.mu:
+            self.cache.recalculate()
+
+    def rebuild_cache(self):
+        """Recount every row into the cache (used after bulk device imports)."""
+        with self.mu:
+            if self.cache_type == CACHE_TYPE_NONE:
+                return
+            for rid, n in self.storage.row_counts(CONTAINERS_PER_ROW).items():
+                self.cache.bulk_add(int(rid), int(n))
+            self.cache.recalculate()
+
+    # ------------------------------------------------------------ imports
+    def _import_positions(self, set_pos: np.ndarray, clear_pos: np.ndarray, row_set: Iterable[int]) -> int:
+        changed = 0
+        if len(set_pos):
+            set_pos = np.unique(np.asarray(set_pos, dtype=np.uint64))
+            n = self.storage.add_many(set_pos, True)
+            if n:
+                self._log(OP_ADD_BATCH, values=set_pos)
+            changed += n
+        if len(clear_pos):
+            clear_pos = np.unique(np.asarray(clear_pos, dtype=np.uint64))
+            n = self.storage.remove_many(clear_pos)
+            if n:
+                self._log(OP_REMOVE_BATCH, values=clear_pos)
+            changed += n
+        for rid in row_set:
+            self._after_row_change(int(rid), bulk=True)
+        if self.cache_type != CACHE_TYPE_NONE:
+            self.cache.recalculate()
+        self._increment_opn(changed)
+        if self.stats:
+            self.stats.count("ImportedN", changed)
+        self.version += 1
+        return changed
+
+    def bulk_import(self, row_ids: Sequence[int], col_ids: Sequence[int], clear: bool = False) -> int:
+        rows = np.asarray(row_ids, dtype=np.uint64)
+        cols = np.asarray(col_ids, dtype=np.uint64)
+        if len(rows) != len(cols):
+            raise PilosaError(f"mismatch of row/column len: {len(rows)} != {len(cols)}")
+        lo = np.uint64(self.shard * SHARD_WIDTH)
+        if len(cols) and (np.any(cols < lo) or np.any(cols >= lo + np.uint64(SHARD_WIDTH))):
+            bad = int(cols[(cols < lo) | (cols >= lo + np.uint64(SHARD_WIDTH))][0])
+            raise PilosaError(f"column:{bad} out of bounds")
+        with self.mu:
+            if (self.mutex or self.bool_field) and not clear:
+                return self._bulk_import_mutex(rows, cols)
+            positions = rows * np.uint64(SHARD_WIDTH) + (cols % np.uint64(SHARD_WIDTH))
+            row_set = np.unique(rows)
+            if clear:
+                return self._import_positions(np.zeros(0, np.uint64), positions, row_set)
+            return self._import_positions(positions, np.zeros(0, np.uint64), row_set)
+
+    def _bulk_import_mutex(self, rows: np.ndarray, cols: np.ndarray) -> int:
+        to_set: Dict[int, int] = {}
+        to_clear: List[int] = []
+        row_set = set()
+        for r, c in zip(rows.tolist(), cols.tolist()):
+            existing = self._vector_get(c)
+            if existing is not None and existing != r:
+                to_clear.append(pos(existing, c))
+                row_set.add(existing)
+            elif existing is not None and existing == r:
+                continue
+            if c in to_set:  # a later bit for the same column wins
+                prev_row = to_set[c] // SHARD_WIDTH
+                row_set.add(prev_row)
+            to_set[c] = pos(r, c)
+            row_set.add(r)
+        return self._import_positions(np.array(list(to_set.values()), np.uint64),
+                                      np.array(to_clear, np.uint64), row_set)
+
+    def import_value(self, col_ids: Sequence[int], values: Sequence[int], bit_depth: int, clear: bool = False):
+        cols = np.asarray(col_ids, dtype=np.uint64)
+        vals = np.asarray(values, dtype=np.int64)
+        if len(cols) != len(vals):
+            raise PilosaError(f"mismatch of column/value len: {len(cols)} != {len(vals)}")
+        # last write per column wins (fragment.go importValueSmallWrite iterates backwards)
+        if len(cols):
+            _, idx = np.unique(cols[::-1], return_index=True)
+            keep = len(cols) - 1 - idx
+            cols, vals = cols[keep], vals[keep]
+        with self.mu:
+            s, c = self._positions_for_values(cols, vals, bit_depth, clear)
+            c = np.setdiff1d(c, s)
+            return self._import_positions(s, c, range(bit_depth + 2))
+
+    def import_roaring(self, data: bytes, clear: bool = False) -> int:
+        with self.mu:
+            changed, rowdelta = self.storage.import_roaring(data, clear, CONTAINERS_PER_ROW)
+            if changed:
+                self._log(OP_REMOVE_ROARING if clear else OP_ADD_ROARING, roaring=data, opn=changed)
+            any_changed = False
+            for rid, d in rowdelta.items():
+                if d == 0:
+                    continue
+                self.checksums.pop(int(rid) // HASH_BLOCK_SIZE, None)
+                if int(rid) > self.max_row_id:
+                    self.max_row_id = int(rid)
+                if self.cache_type != CACHE_TYPE_NONE:
+                    any_changed = True
+                    self.cache.bulk_add(int(rid), max(0, self.cache.get(int(rid)) + int(d)))
+            if any_changed:
+                self.cache.recalculate()
+            self._increment_opn(changed)
+            self.version += 1
+            return changed
+
+    # ------------------------------------------------------------ anti-entropy
+    def blocks(self) -> List[Tuple[int, bytes]]:
+        """(block id, xxhash64 checksum) of every 100-row block with data
+        (fragment.go:1776-1854; values hashed big-endian)."""
+        with self.mu:
+            vals = self.storage.slice()
+        if len(vals) == 0:
+            return []
+        bids = vals // np.uint64(HASH_BLOCK_SIZE * SHARD_WIDTH)
+        out = []
+        bounds = np.flatnonzero(np.diff(bids)) + 1
+        starts = np.concatenate([[0], bounds])
+        ends = np.concatenate([bounds, [len(vals)]])
+        for s, e in zip(starts, ends):
+            bid = int(bids[s])
+            cached = self.checksums.get(bid)
+            if cached is None:
+                cached = xxhash.xxh64(vals[s:e].astype(">u8").tobytes()).digest()
+                self.checksums[bid] = cached
+            out.append((bid, cached))
+        return out
+
+    def checksum(self) -> bytes:
+        h = xxhash.xxh64()
+        for _, c in self.blocks():
+            h.update(c)
+        return h.digest()
+
+    def block_data(self, block_id: int) -> Tuple[np.ndarray, np.ndarray]:
+        lo = block_id * HASH_BLOCK_SIZE * SHARD_WIDTH
+        hi = (block_id + 1) * HASH_BLOCK_SIZE * SHARD_WIDTH
+        with self.mu:
+            v = self.storage.slice_range(lo, hi)
+        return v // np.uint64(SHARD_WIDTH), v % np.uint64(SHARD_WIDTH)
+
+    def merge_block(self, block_id: int, data: List[Tuple[Sequence[int], Sequence[int]]]):
+        """Majority-vote merge of replica block data (fragment.go:1873-1991).
+        Returns (sets, clears) diffs per remote replica."""
+        lr, lc = self.block_data(block_id)
+        sets_all = [set(zip(lr.tolist(), lc.tolist()))]
+        max_row = (block_id + 1) * HASH_BLOCK_SIZE
+        for rows, cols in data:
+            if len(rows) != len(cols):
+                raise PilosaError(f"pair set mismatch: {len(rows)} != {len(cols)}")
+            sets_all.append({(int(r), int(c)) for r, c in zip(rows, cols)
+                             if block_id * HASH_BLOCK_SIZE <= int(r) < max_row and int(c) < SHARD_WIDTH})
+        majority = (len(sets_all) + 1) // 2
+        universe = sorted(set().union(*sets_all))
+        sets = [([], []) for _ in sets_all]
+        clears = [([], []) for _ in sets_all]
+        for pr in universe:
+            have = [pr in s for s in sets_all]
+            new = sum(have) >= majority
+            for i, h in enumerate(have):
+                if h == new:
+                    continue
+                tgt = sets[i] if new else clears[i]
+                tgt[0].append(pr[0])
+                tgt[1].append(pr[1])
+        with self.mu:
+            for r, c in zip(*sets[0]):
+                self._unprotected_set_bit(r, self.shard * SHARD_WIDTH + c)
+            for r, c in zip(*clears[0]):
+                self._unprotected_clear_bit(r, self.shard * SHARD_WIDTH + c)
+        return sets[1:], clears[1:]
+
+    # ------------------------------------------------------------ backup
+    def write_to(self, fileobj) -> None:
+        """Tar archive with ``data`` (snapshot) and ``cache`` entries
+        (fragment.go:2424-2500)."""
+        from pilosa_amd.wire import pb
+        with self.mu:
+            data = self.storage.to_bytes()
+            ids = self.cache.ids()
+        cache = pb.Cache(IDs=ids).SerializeToString()
+        with tarfile.open(fileobj=fileobj, mode="w|") as tw:
+            for name, payload in (("data", data), ("cache", cache)):
+                ti = tarfile.TarInfo(name)
+                ti.size = len(payload)
+                ti.mode = 0o600
+                tw.addfile(ti, io.BytesIO(payload))
+
+    def read_from(self, fileobj) -> None:
+        from pilosa_amd.wire import pb
+        with tarfile.open(fileobj=fileobj, mode="r|") as tr:
+            for ti in tr:
+                payload = tr.extractfile(ti).read() if ti.isfile() else b""
+                if ti.name == "data":
+                    with self.mu:
+                        self.storage = Bitmap.from_bytes(payload)
+                        tmp = self.path + ".snapshotting"
+                        with open(tmp, "wb") as fh:
+                            fh.write(payload)
+                        if self._fh is not None:
+                            self._fh.close()
+                        os.replace(tmp, self.path)
+                        self._fh = open(self.path, "ab", buffering=0)
+                        self.opn = 0
+                        self.version += 1
+                elif ti.name == "cache":
+                    m = pb.Cache()
+                    m.ParseFromString(payload)
+                    with self.mu:
+                        self.cache = new_cache(self.cache_type, self.cache_size)
+                        for rid in m.IDs:
+                            self.cache.bulk_add(rid, self.row_count(rid))
+                        self.cache.recalculate()
+
+    # ------------------------------------------------------------ misc
+    def for_each_bit(self):
+        with self.mu:
+            v = self.storage.slice()
+        base = self.shard * SHARD_WIDTH
+        for x in v.tolist():
+            yield x // SHARD_WIDTH, base + (x % SHARD_WIDTH)
+
+    def check(self) -> str:
+        return self.storage.check()
+
+
+def _wrap_i64(v: int) -> int:
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _hashable(v):
+    if isinstance(v, list):
+        return tuple(v)
+    return v

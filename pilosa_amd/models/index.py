@@ -1,0 +1,149 @@
+"""Index: a set of fields sharing one column space (reference: index.go).
+
+``track_existence`` maintains the ``_exists`` field (row 0 set for every
+column ever written) that ``Not()`` and column-existence queries use.
+Options persist in ``.meta`` (protobuf IndexMeta); column attributes live in
+the index's ``.data`` store.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import threading
+from typing import Dict, List, Optional
+
+from pilosa_amd.errors import ErrFieldExists, ErrFieldNotFound, ErrName, validate_name
+from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
+from pilosa_amd.models.cache import CACHE_TYPE_NONE
+from pilosa_amd.models.field import Field, FieldOptions
+
+EXISTENCE_FIELD_NAME = "_exists"
+
+
+class Index:
+    def __init__(self, path: str, name: str, keys: bool = False, track_existence: bool = True,
+                 max_opn: int = 10000, stats=None, persistent_attrs: bool = True):
+        validate_name(name)
+        self.path = path
+        self.name = name
+        self.keys = keys
+        self.track_existence = track_existence
+        self.fields: Dict[str, Field] = {}
+        self.max_opn = max_opn
+        self.stats = stats
+        self.persistent_attrs = persistent_attrs
+        self.column_attr_store = SQLiteAttrStore(os.path.join(path, ".data")) if persistent_attrs \
+            else MemAttrStore()
+        self.mu = threading.RLock()
+        self.on_create_shard = None
+
+    def meta_path(self) -> str:
+        return os.path.join(self.path, ".meta")
+
+    def save_meta(self):
+        from pilosa_amd.wire import pb
+        os.makedirs(self.path, exist_ok=True)
+        with open(self.meta_path(), "wb") as fh:
+            fh.write(pb.IndexMeta(Keys=self.keys, TrackExistence=self.track_existence).SerializeToString())
+
+    def load_meta(self):
+        from pilosa_amd.wire import pb
+        if os.path.exists(self.meta_path()):
+            m = pb.IndexMeta()
+            with open(self.meta_path(), "rb") as fh:
+                m.ParseFromString(fh.read())
+            self.keys, self.track_existence = m.Keys, m.TrackExistence
+
+    def open(self):
+        with self.mu:
+            os.makedirs(self.path, exist_ok=True)
+            self.load_meta()
+            self.column_attr_store.open()
+            for name in sorted(os.listdir(self.path)):
+                p = os.path.join(self.path, name)
+                if name.startswith(".") or not os.path.isdir(p):
+                    continue
+                f = self._new_field(name, None)
+                f.open()
+                self.fields[name] = f
+            if self.track_existence:
+                self._open_existence_field()
+        return self
+
+    def _open_existence_field(self):
+        if EXISTENCE_FIELD_NAME not in self.fields:
+            self._create_field(EXISTENCE_FIELD_NAME, FieldOptions(type="set", cache_type=CACHE_TYPE_NONE))
+
+    def close(self):
+        with self.mu:
+            for f in self.fields.values():
+                f.close()
+            self.fields.clear()
+            self.column_attr_store.close()
+
+    def delete(self):
+        self.close()
+        shutil.rmtree(self.path, ignore_errors=True)
+
+    def _new_field(self, name: str, opts: Optional[FieldOptions]) -> Field:
+        f = Field(os.path.join(self.path, name), self.name, name, opts, max_opn=self.max_opn, stats=self.stats,
+                  persistent_attrs=self.persistent_attrs)
+        f.on_create_shard = self._field_created_shard
+        return f
+
+    def _field_created_shard(self, field: Field, shard: int):
+        if self.on_create_shard is not None:
+            self.on_create_shard(self, field, shard)
+
+    def _create_field(self, name: str, opts: FieldOptions) -> Field:
+        f = self._new_field(name, opts)
+        f.save_meta()
+        f.open()
+        self.fields[name] = f
+        return f
+
+    def create_field(self, name: str, opts: Optional[FieldOptions] = None) -> Field:
+        with self.mu:
+            if name == EXISTENCE_FIELD_NAME:
+                raise ErrName
+            validate_name(name)
+            if name in self.fields:
+                raise ErrFieldExists
+            return self._create_field(name, opts or FieldOptions.default())
+
+    def create_field_if_not_exists(self, name: str, opts: Optional[FieldOptions] = None) -> Field:
+        with self.mu:
+            f = self.fields.get(name)
+            if f is not None:
+                return f
+            validate_name(name)
+            return self._create_field(name, opts or FieldOptions.default())
+
+    def field(self, name: str) -> Optional[Field]:
+        return self.fields.get(name)
+
+    def existence_field(self) -> Optional[Field]:
+        return self.fields.get(EXISTENCE_FIELD_NAME) if self.track_existence else None
+
+    def public_fields(self) -> List[Field]:
+        return [self.fields[n] for n in sorted(self.fields) if n != EXISTENCE_FIELD_NAME]
+
+    def delete_field(self, name: str):
+        with self.mu:
+            f = self.fields.pop(name, None)
+            if f is None:
+                raise ErrFieldNotFound
+            f.delete()
+
+    def available_shards(self) -> List[int]:
+        s = set()
+        for f in list(self.fields.values()):
+            s |= set(f.available_shards())
+        return sorted(s)
+
+    def options_json(self) -> dict:
+        return {"keys": self.keys, "trackExistence": self.track_existence}
+
+    def info(self) -> dict:
+        return {"name": self.name, "options": self.options_json(),
+                "fields": [f.info() for f in self.public_fields()], "shardWidth": 1 << 20}

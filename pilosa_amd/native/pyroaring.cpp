@@ -514,6 +514,29 @@ PYBIND11_MODULE(_roaring, m) {
         if (cur != ~0ull) d[py::int_(cur)] = acc;
         return d;
       }, py::arg("containers_per_row") = 16)
+      .def("rows_with_column", [](const Bitmap& b, uint64_t col, uint64_t cpr) {
+        // rows whose container at key (row*cpr + col>>16) holds col (mutex/bool vectors)
+        std::vector<uint64_t> rows;
+        const uint64_t j = (col >> 16) % cpr;
+        const uint16_t lo = uint16_t(col & 0xffff);
+        for (auto& kv : b.cs)
+          if (kv.first % cpr == j && kv.second.n && kv.second.contains(lo)) rows.push_back(kv.first / cpr);
+        return to_np(rows);
+      }, py::arg("col"), py::arg("containers_per_row") = 16)
+      .def("clear_row", [](Bitmap& b, uint64_t row, uint64_t cpr) {
+        bool changed = false;
+        for (uint64_t k = row * cpr; k < (row + 1) * cpr; k++) {
+          auto it = b.cs.find(k);
+          if (it != b.cs.end()) { changed = changed || it->second.n > 0; b.cs.erase(it); }
+        }
+        return changed;
+      }, py::arg("row"), py::arg("containers_per_row") = 16)
+      .def("set_row_from", [](Bitmap& b, uint64_t row, const Bitmap& src, uint64_t src_key0, uint64_t cpr) {
+        // replace row with the containers of src keys [src_key0, src_key0+cpr)
+        for (uint64_t k = row * cpr; k < (row + 1) * cpr; k++) b.cs.erase(k);
+        for (auto it = src.cs.lower_bound(src_key0); it != src.cs.end() && it->first < src_key0 + cpr; ++it)
+          if (it->second.n) b.cs[row * cpr + (it->first - src_key0)] = it->second;
+      }, py::arg("row"), py::arg("src"), py::arg("src_key0"), py::arg("containers_per_row") = 16)
       .def("row_ids", [](const Bitmap& b, uint64_t cpr) {
         std::vector<uint64_t> rows;
         uint64_t cur = ~0ull;
