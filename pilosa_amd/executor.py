@@ -608,6 +608,11 @@ class Executor:
                             lambda p, v: (p or 0) + (v or 0), local)
         return int(r or 0)
 
+    def count_host(self, index: str, child: Call, shards) -> int:
+        """Count on the host roaring path only (GPU-ineligible trees)."""
+        return int(self._map_local(list(shards), lambda s: self.bitmap_call_shard(index, child, s).count(),
+                                   lambda p, v: (p or 0) + (v or 0), None) or 0)
+
     def _bsi_filter_shard(self, index, c: Call, shard):
         if len(c.children) == 1:
             return self.bitmap_call_shard(index, c.children[0], shard)

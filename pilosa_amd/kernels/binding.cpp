@@ -19,7 +19,7 @@ hipStream_t cur_stream(const torch::Tensor& t) {
 }
 
 void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor out,
-                c10::optional<torch::Tensor> per_key, bool fast) {
+                c10::optional<torch::Tensor> per_key, bool fast, c10::optional<torch::Tensor> per_shard) {
   check_dev(progs, "progs");
   check_dev(views, "views");
   TORCH_CHECK(progs.numel() % sizeof(pk::QueryProg) == 0, "progs size");
@@ -38,8 +38,15 @@ void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
                 "per_key must be int32[Q*S*16]");
     pk_ = per_key->data_ptr<int32_t>();
   }
+  int64_t* ps = nullptr;
+  if (per_shard.has_value() && per_shard->numel()) {
+    check_dev(*per_shard, "per_shard");
+    TORCH_CHECK(per_shard->scalar_type() == torch::kInt64 && per_shard->numel() >= int64_t(Q) * S,
+                "per_shard must be int64[Q*S]");
+    ps = per_shard->data_ptr<int64_t>();
+  }
   pk::launch_expr_count(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
-                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), o, pk_, fast,
+                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), o, pk_, ps, fast,
                         cur_stream(progs));
 }
 
@@ -90,7 +97,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("MAXLEAF") = pk::MAXLEAF;
   m.attr("MAXPROG") = pk::MAXPROG;
   m.def("expr_count", &expr_count, "batched boolean-expression count over all local shards",
-        py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("fast") = false);
+        py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("fast") = false,
+        py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
 }

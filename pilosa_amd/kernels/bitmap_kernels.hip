@@ -16,7 +16,7 @@
 // coalesced 1 KiB global_load_dwordx4 wave-instructions.  Array and run
 // containers are expanded into a wave-private 8 KiB LDS bitmap (ds_or_b64
 // scatter) and read back in the same layout.  Boolean query trees are compiled
-// on the host to a tiny postfix program (<=16 ops, <=8 leaves) that the wave
+// on the host to a tiny postfix program (<=32 ops, <=16 leaves) that the wave
 // interprets with a 4-deep register stack (static register moves, no scratch).
 // Fast paths: Count(Row) sums container cardinalities from the metadata only;
 // Count(Intersect(a,b)) dispatches on the container type pair
@@ -312,7 +312,8 @@ template <bool FAST>
 __global__ __launch_bounds__(256) void expr_count_kernel(const QueryProg* __restrict__ progs, int Q,
                                                          const ViewDev* __restrict__ views, int S,
                                                          unsigned long long* __restrict__ out,
-                                                         int32_t* __restrict__ per_key) {
+                                                         int32_t* __restrict__ per_key,
+                                                         int64_t* __restrict__ per_shard) {
   __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
   const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x >> 6;
@@ -363,6 +364,7 @@ __global__ __launch_bounds__(256) void expr_count_kernel(const QueryProg* __rest
   }
   total = wave_sum_i64(total);
   if (lane == 0 && total && out) atomicAdd(out + q, (unsigned long long)total);
+  if (lane == 0 && per_shard) per_shard[int64_t(q) * S + s] = total;
 }
 
 // Materialize kernel: writes result containers for every (q, s, j) with
@@ -518,15 +520,15 @@ static inline unsigned grid_for(int64_t items) {
 }
 
 void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int S, unsigned long long* out,
-                       int32_t* per_key, bool fast, hipStream_t st) {
+                       int32_t* per_key, int64_t* per_shard, bool fast, hipStream_t st) {
   const int64_t items = int64_t(Q) * S;
   if (items == 0) return;
   if (fast && per_key == nullptr)
     hipLaunchKernelGGL(expr_count_kernel<true>, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
-                       Q, views, S, out, per_key);
+                       Q, views, S, out, per_key, per_shard);
   else
     hipLaunchKernelGGL(expr_count_kernel<false>, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
-                       Q, views, S, out, per_key);
+                       Q, views, S, out, per_key, per_shard);
 }
 
 void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views, int S, const int32_t* counts,

@@ -7,12 +7,12 @@
 
 namespace pk {
 
-constexpr int MAXLEAF = 8;
-constexpr int MAXPROG = 16;
+constexpr int MAXLEAF = 16;
+constexpr int MAXPROG = 32;
 constexpr int ARRAY_MAX = 4096;
 constexpr int CT_ARRAY = 1, CT_BITMAP = 2, CT_RUN = 3;
 // opcodes: 0..MAXLEAF-1 push leaf k; then binary ops
-constexpr int OP_AND = 16, OP_OR = 17, OP_XOR = 18, OP_ANDNOT = 19;
+constexpr int OP_AND = 32, OP_OR = 33, OP_XOR = 34, OP_ANDNOT = 35;
 
 // container metadata word (see pilosa_amd/native/pyroaring.cpp)
 __host__ __device__ __forceinline__ int meta_j(int64_t m) { return int(m & 15); }
@@ -26,9 +26,9 @@ struct QueryProg {
   int32_t leaf_view[MAXLEAF];
   int64_t leaf_row[MAXLEAF];  // dense row index in the view, -1 = empty row
   uint8_t prog[MAXPROG];
-  int64_t pad;
+  int64_t pad[3];
 };
-static_assert(sizeof(QueryProg) == 128, "QueryProg layout");
+static_assert(sizeof(QueryProg) == 256, "QueryProg layout");
 
 struct ViewDev {
   const uint32_t* rowptr;      // [S][D+1]
@@ -49,7 +49,7 @@ struct BsiArgs {
 };
 
 void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int S, unsigned long long* out,
-                       int32_t* per_key, bool fast, hipStream_t st);
+                       int32_t* per_key, int64_t* per_shard, bool fast, hipStream_t st);
 void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views, int S, const int32_t* counts,
                              const int64_t* offs, uint16_t* outp, hipStream_t st);
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,

@@ -7,7 +7,7 @@ The HIP kernels in pilosa_amd/kernels/bitmap_kernels.hip evaluate a whole
 batch of boolean query programs over all local shards of the arena in one
 launch (reference per-shard worker loop: executor.go:2564-2611 — replaced).
 
-Query programs are tiny postfix byte codes over <=8 leaves (a leaf = one row
+Query programs are tiny postfix byte codes over <=16 leaves (a leaf = one row
 of one view).  ``Expr`` trees are compiled here.
 """
 from __future__ import annotations
@@ -18,16 +18,16 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-MAXLEAF = 8
-MAXPROG = 16
-OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 16, 17, 18, 19
+MAXLEAF = 16
+MAXPROG = 32
+OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 32, 33, 34, 35
 _OPS = {"and": OP_AND, "or": OP_OR, "xor": OP_XOR, "andnot": OP_ANDNOT}
 
 QPROG_DTYPE = np.dtype([("nleaf", "<i4"), ("nprog", "<i4"), ("leaf_view", "<i4", (MAXLEAF,)),
-                        ("leaf_row", "<i8", (MAXLEAF,)), ("prog", "u1", (MAXPROG,)), ("pad", "<i8")])
+                        ("leaf_row", "<i8", (MAXLEAF,)), ("prog", "u1", (MAXPROG,)), ("pad", "<i8", (3,))])
 VIEWDEV_DTYPE = np.dtype([("rowptr", "<u8"), ("shard_base", "<u8"), ("meta", "<u8"), ("payload", "<u8"),
                           ("D", "<i8"), ("pad", "<i8", (3,))])
-assert QPROG_DTYPE.itemsize == 128 and VIEWDEV_DTYPE.itemsize == 64
+assert QPROG_DTYPE.itemsize == 256 and VIEWDEV_DTYPE.itemsize == 64
 
 _ext = None
 _ext_lock = threading.Lock()
@@ -70,7 +70,7 @@ def compile_expr(expr, view_index: Dict[int, int]):
 
     ``view_index`` maps id(DeviceView) -> slot in the batch view table (it is
     extended as new views are seen).  Raises CompileError when the tree does
-    not fit the kernel's limits (8 leaves, 16 ops, stack depth 4).
+    not fit the kernel's limits (16 leaves, 32 ops, stack depth 4).
     """
     leaf_views: List[int] = []
     leaf_rows: List[int] = []
@@ -294,6 +294,20 @@ class GpuEngine:
             self.ext.expr_count(tp, tv, S, o, None, is_fast)
             out.index_copy_(0, ti, o)
         return out
+
+    def count_per_shard(self, exprs: Sequence[object]) -> np.ndarray:
+        """Counts per (query, local shard) -> int64[Q, S] (TopN per-shard semantics)."""
+        torch = self.torch
+        progs, views, S = self.compile_batch(exprs)
+        Q = len(exprs)
+        if not S or not Q:
+            return np.zeros((Q, S), dtype=np.int64)
+        tv = self._views_tensor(views)
+        tp = torch.from_numpy(progs.view(np.uint8)).to(self.device, non_blocking=True)
+        ps = torch.zeros(Q * S, dtype=torch.int64, device=self.device)
+        empty = torch.empty(0, dtype=torch.int64, device=self.device)
+        self.ext.expr_count(tp, tv, S, empty, None, False, ps)
+        return ps.cpu().numpy().reshape(Q, S)
 
     def count_async(self, exprs: Sequence[object]):
         """Launch counts for a batch; returns the device int64[Q] result tensor.

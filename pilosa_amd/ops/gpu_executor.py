@@ -1,0 +1,384 @@
+"""GPU execution of PQL calls over all local shards at once.
+
+The host executor (pilosa_amd/executor.py) hands the *local* part of every
+map/reduce to this class; instead of the reference's per-shard worker loop
+(executor.go:2564-2611) each call becomes ONE batched kernel launch over the
+device arenas of the involved field-views:
+
+* ``count``     Count(<bitmap tree>)                 -> expr_count
+* ``bitmap``    Row/Intersect/Union/Difference/Xor/Not/time ranges -> materialize
+* ``bsi_sum``   Sum(<filter>, field=f)                -> bsi_sum kernel
+* ``topn``      TopN phase-1/phase-2 with src          -> per-shard counts +
+                reference heap semantics replayed on host (fragment.top)
+* ``group_by``  GroupBy(Rows..., filter)               -> batched k-way counts
+
+Arenas are (re)built lazily from the host fragments and cached per
+(index, field, view, shard list); every fragment carries a ``version`` that is
+bumped on mutation, so stale arenas are rebuilt before use.  Anything not
+expressible on the device raises ``NotImplementedError`` -> host fallback.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from pilosa_amd.models.cache import Pair, sort_pairs
+from pilosa_amd.models.fragment import SHARD_WIDTH
+from pilosa_amd.models.index import EXISTENCE_FIELD_NAME
+from pilosa_amd.models.row import Row
+from pilosa_amd.models.view import VIEW_BSI_PREFIX, VIEW_STANDARD
+from pilosa_amd.pql import Call
+
+from .device import CompileError, DeviceView, GpuEngine, Leaf, Op
+
+MAX_GROUPS_PER_LAUNCH = 1 << 16
+
+
+class _Empty:
+    """Placeholder for a leaf whose field/view does not exist (empty row)."""
+
+
+EMPTY = _Empty()
+
+
+class GpuExecutor:
+    def __init__(self, holder, device="cuda:0", executor=None):
+        self.holder = holder
+        self.engine = GpuEngine(device)
+        self.device = self.engine.device
+        self.executor = executor
+        self._arenas: Dict[Tuple, Tuple[Tuple, DeviceView]] = {}
+        self.mu = threading.RLock()
+        self.launches = 0
+
+    # ------------------------------------------------------------ arenas
+    def view_arena(self, index: str, field: str, view: str, shards: Sequence[int]) -> Optional[DeviceView]:
+        v = self.holder.view(index, field, view)
+        if v is None:
+            return None
+        shards = tuple(int(s) for s in shards)
+        frags = [v.fragment(s) for s in shards]
+        sig = tuple((id(f), f.version) if f is not None else None for f in frags)
+        key = (index, field, view, shards)
+        with self.mu:
+            hit = self._arenas.get(key)
+            if hit is not None and hit[0] == sig:
+                return hit[1]
+            bms = []
+            for f in frags:
+                if f is None:
+                    bms.append(None)
+                else:
+                    with f.mu:
+                        bms.append(f.storage)
+            dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards))
+            self._arenas[key] = (sig, dv)
+            return dv
+
+    def invalidate(self):
+        with self.mu:
+            self._arenas.clear()
+
+    def hbm_bytes(self) -> int:
+        with self.mu:
+            return sum(dv.nbytes() for _, dv in self._arenas.values())
+
+    # ------------------------------------------------------------ planning
+    def _ex(self):
+        if self.executor is None:
+            raise NotImplementedError
+        return self.executor
+
+    def plan(self, index: str, c: Call, shards: Sequence[int]):
+        """PQL bitmap call -> Leaf/Op tree (or EMPTY)."""
+        n = c.name
+        if n in ("Row", "Range", "Bitmap"):
+            if c.has_condition_arg():
+                raise NotImplementedError("BSI predicate leaf")
+            try:
+                fname = c.field_arg()
+            except ValueError:
+                raise NotImplementedError
+            f = self.holder.field(index, fname)
+            if f is None:
+                raise NotImplementedError  # host path raises the proper error
+            rid, ok = c.uint_arg(fname)
+            if not ok:
+                raise NotImplementedError
+            views = self._ex().time_views(f, c)
+            if views is None:
+                views = [VIEW_STANDARD]
+            leaves = []
+            for vname in views:
+                dv = self.view_arena(index, fname, vname, shards)
+                if dv is not None:
+                    leaves.append(Leaf(dv, rid))
+            if not leaves:
+                return EMPTY
+            return leaves[0] if len(leaves) == 1 else Op("or", tuple(leaves))
+        if n in ("Intersect", "Union", "Difference", "Xor"):
+            if not c.children:
+                if n == "Union":
+                    return EMPTY
+                raise NotImplementedError
+            kids = [self.plan(index, k, shards) for k in c.children]
+            if n == "Intersect":
+                if any(k is EMPTY for k in kids):
+                    return EMPTY
+                return kids[0] if len(kids) == 1 else Op("and", tuple(kids))
+            if n == "Union":
+                kids = [k for k in kids if k is not EMPTY]
+                if not kids:
+                    return EMPTY
+                return kids[0] if len(kids) == 1 else Op("or", tuple(kids))
+            if n == "Difference":
+                if kids[0] is EMPTY:
+                    return EMPTY
+                rest = [k for k in kids[1:] if k is not EMPTY]
+                return kids[0] if not rest else Op("andnot", (kids[0], *rest))
+            kids = [k for k in kids if k is not EMPTY]  # Xor
+            if not kids:
+                return EMPTY
+            return kids[0] if len(kids) == 1 else Op("xor", tuple(kids))
+        if n == "Not":
+            idx = self.holder.index(index)
+            if idx is None or idx.existence_field() is None or len(c.children) != 1:
+                raise NotImplementedError
+            ex = self.view_arena(index, EXISTENCE_FIELD_NAME, VIEW_STANDARD, shards)
+            child = self.plan(index, c.children[0], shards)
+            if ex is None:
+                return EMPTY
+            if child is EMPTY:
+                return Leaf(ex, 0)
+            return Op("andnot", (Leaf(ex, 0), child))
+        raise NotImplementedError(n)
+
+    # ------------------------------------------------------------ calls
+    def count(self, index: str, child: Call, shards: List[int]) -> int:
+        e = self.plan(index, child, shards)
+        if e is EMPTY:
+            return 0
+        try:
+            self.launches += 1
+            return int(self.engine.count([e])[0])
+        except CompileError:
+            raise NotImplementedError
+
+    def try_count_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
+        """Many Count() calls of one request -> one launch; calls whose tree
+        does not fit the kernel limits are counted on the host."""
+        from .device import compile_expr
+        try:
+            exprs = []
+            for c in calls:
+                if len(c.children) != 1:
+                    return None
+                exprs.append(self.plan(index, c.children[0], shards))
+        except NotImplementedError:
+            return None
+        out = [0] * len(exprs)
+        live = []
+        for i, e in enumerate(exprs):
+            if e is EMPTY:
+                continue
+            try:
+                compile_expr(e, {})
+                live.append(i)
+            except CompileError:
+                out[i] = self._ex().count_host(index, calls[i].children[0], shards)
+        if live:
+            self.launches += 1
+            got = self.engine.count([exprs[i] for i in live])
+            for i, v in zip(live, got):
+                out[i] = int(v)
+        return out
+
+    def bitmap(self, index: str, c: Call, shards: List[int]) -> Row:
+        if c.name == "Shift":
+            raise NotImplementedError
+        e = self.plan(index, c, shards)
+        if e is EMPTY:
+            return Row()
+        try:
+            self.launches += 1
+            bms, shard_list = self.engine.materialize(e)
+        except CompileError:
+            raise NotImplementedError
+        row = Row()
+        for s, bm in zip(shard_list, bms):
+            if bm is not None and bm.any():
+                row.segments[int(s)] = bm
+        return row
+
+    def bsi_sum(self, index: str, c: Call, shards: List[int]):
+        from pilosa_amd.executor import ValCount, _wrap
+        fname = c.args.get("field")
+        f = self.holder.field(index, fname) if isinstance(fname, str) else None
+        if f is None or f.bsi_group(fname) is None:
+            raise NotImplementedError
+        b = f.bsi_group(fname)
+        bv = self.view_arena(index, fname, VIEW_BSI_PREFIX + fname, shards)
+        if bv is None:
+            return ValCount()
+        filt = None
+        if len(c.children) == 1:
+            filt = self.plan(index, c.children[0], shards)
+            if filt is EMPTY:
+                return ValCount()
+        try:
+            self.launches += 1
+            s, n = self.engine.bsi_sum_async([filt], bv, b.bit_depth)
+        except CompileError:
+            raise NotImplementedError
+        s, n = int(s.cpu()[0]), int(n.cpu()[0])
+        return ValCount(_wrap(s + n * b.base), n)
+
+    # ------------------------------------------------------------ TopN
+    def topn(self, index: str, c: Call, shards: List[int]) -> List[Pair]:
+        from pilosa_amd.models.fragment import TopOptions
+        ex = self._ex()
+        fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
+        if len(c.children) != 1 or tanimoto or (attr_name and attr_values):
+            raise NotImplementedError  # cache-only TopN is cheap on the host; exotic options stay there
+        src = self.plan(index, c.children[0], shards)
+        frags = [self.holder.fragment(index, fname, VIEW_STANDARD, s) for s in shards]
+        for f in frags:
+            if f is not None and f.cache_type == "none":
+                from pilosa_amd.errors import PilosaError
+                raise PilosaError(f"cannot compute TopN(), field has no cache: {fname!r}")
+        # candidate (row, cached count) lists per shard, as fragment.top() would see them
+        per_shard_pairs = [f._top_bitmap_pairs(ids) if f is not None else [] for f in frags]
+        cand = sorted({rid for pairs in per_shard_pairs for rid, _ in pairs})
+        if not cand:
+            return []
+        if src is EMPTY:
+            return []
+        rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+        exprs = [Op("and", (src, Leaf(rv, r))) for r in cand]
+        try:
+            mats = []
+            for i in range(0, len(exprs), MAX_GROUPS_PER_LAUNCH):
+                self.launches += 1
+                mats.append(self.engine.count_per_shard(exprs[i:i + MAX_GROUPS_PER_LAUNCH]))
+            counts = np.concatenate(mats, axis=0)  # [C, S]
+        except CompileError:
+            raise NotImplementedError
+        col = {r: i for i, r in enumerate(cand)}
+        total: Dict[int, int] = {}
+        for si, pairs in enumerate(per_shard_pairs):
+            if not pairs:
+                continue
+            got = _replay_top(pairs, lambda rid: int(counts[col[rid], si]), 0 if ids else n, threshold)
+            for p in got:
+                total[p.id] = total.get(p.id, 0) + p.count
+        return sort_pairs([Pair(k, v) for k, v in total.items()])
+
+    # ------------------------------------------------------------ GroupBy
+    def group_by(self, index: str, c: Call, filt: Optional[Call], shards: List[int], child_rows, limit: int):
+        from pilosa_amd.executor import FieldRow, GroupCount
+        ex = self._ex()
+        k = len(c.children)
+        if k == 0 or k + (1 if filt is not None else 0) > 16:
+            raise NotImplementedError
+        fields = []
+        arenas = []
+        cand: List[List[int]] = []
+        for i, ch in enumerate(c.children):
+            fname = ch.args.get("_field")
+            if not isinstance(fname, str) or self.holder.field(index, fname) is None:
+                raise NotImplementedError
+            dv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+            if dv is None:
+                return []
+            rows = [int(r) for r in dv.rows] if dv.D else []
+            if child_rows[i] is not None:
+                keep = set(child_rows[i])
+                rows = [r for r in rows if r in keep]
+            if not rows:
+                return []
+            fields.append(fname)
+            arenas.append(dv)
+            cand.append(rows)
+        fexpr = None
+        if filt is not None:
+            fexpr = self.plan(index, filt, shards)
+            if fexpr is EMPTY:
+                return []
+        prev = ex.group_by_previous(c)
+        results: List[GroupCount] = []
+        # enumerate combos lexicographically in chunks; stop at `limit`
+        batch_keys: List[Tuple[int, ...]] = []
+
+        def flush():
+            if not batch_keys:
+                return False
+            exprs = []
+            for key in batch_keys:
+                leaves = [Leaf(arenas[i], key[i]) for i in range(k)]
+                if fexpr is not None:
+                    leaves = [fexpr] + leaves
+                exprs.append(leaves[0] if len(leaves) == 1 else Op("and", tuple(leaves)))
+            self.launches += 1
+            got = self.engine.count(exprs)
+            for key, v in zip(batch_keys, got):
+                if v > 0:
+                    results.append(GroupCount([FieldRow(fields[i], key[i]) for i in range(k)], int(v)))
+                    if len(results) >= limit:
+                        batch_keys.clear()
+                        return True
+            batch_keys.clear()
+            return False
+
+        try:
+            for key in _lex_product(cand, prev):
+                batch_keys.append(key)
+                if len(batch_keys) >= MAX_GROUPS_PER_LAUNCH:
+                    if flush():
+                        return results
+            flush()
+        except CompileError:
+            raise NotImplementedError
+        return results[:limit]
+
+
+def _lex_product(cand: List[List[int]], prev: Optional[Tuple[int, ...]]):
+    k = len(cand)
+
+    def rec(level, prefix):
+        for r in cand[level]:
+            key = prefix + (r,)
+            if prev is not None and key < prev[:len(key)]:
+                continue
+            if level == k - 1:
+                if prev is not None and key <= prev:
+                    continue
+                yield key
+            else:
+                yield from rec(level + 1, key)
+
+    yield from rec(0, ())
+
+
+def _replay_top(pairs: List[Tuple[int, int]], count_of, n: int, min_threshold: int) -> List[Pair]:
+    """fragment.top() heap logic with precomputed src∩row counts."""
+    import heapq
+    heap: List[Tuple[int, int]] = []
+    for rid, cnt in pairs:
+        if cnt == 0 or cnt < min_threshold:
+            continue
+        if n == 0 or len(heap) < n:
+            count = count_of(rid)
+            if count == 0 or count < min_threshold:
+                continue
+            heapq.heappush(heap, (count, -rid))
+            continue
+        threshold = heap[0][0]
+        if threshold < min_threshold or cnt < threshold:
+            break
+        count = count_of(rid)
+        if count < threshold:
+            continue
+        heapq.heappush(heap, (count, -rid))
+    return sort_pairs([Pair(-nid, cc) for cc, nid in heap])

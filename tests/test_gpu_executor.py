@@ -1,0 +1,121 @@
+"""GPU executor vs host executor on the same holder (differential test)."""
+import numpy as np
+import pytest
+
+from tests.helpers import SW, Env, cols
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def envs():
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    cpu = Env()
+    rng = np.random.default_rng(3)
+    for e in (cpu,):
+        e.create_index("i")
+        e.field("i", "f")
+        e.field("i", "g")
+        e.field("i", "t", type="time", time_quantum="YMD")
+        e.field("i", "n", type="int", min=-1000, max=100000)
+    idx = cpu.holder.index("i")
+    f, g, t, n = (idx.field(x) for x in "fgtn")
+    nshard = 4
+    for r in range(12):
+        density = [0.5, 0.05, 0.002, 0.0001][r % 4]
+        k = int(density * nshard * SW)
+        c = rng.choice(nshard * SW, size=k, replace=False).astype(np.uint64)
+        f.import_bits(np.full(k, r, np.uint64), c)
+        c2 = rng.choice(nshard * SW, size=k // 2 + 1, replace=False).astype(np.uint64)
+        g.import_bits(np.full(len(c2), r % 5, np.uint64), c2)
+    # runs
+    f.import_bits(np.full(200000, 20, np.uint64), np.arange(100000, 300000, dtype=np.uint64))
+    import datetime as dt
+    cc = rng.choice(nshard * SW, size=5000, replace=False)
+    ts = [dt.datetime(2020, 1 + int(x % 12), 1 + int(x % 27)) for x in cc]
+    t.import_bits(np.full(len(cc), 1, np.uint64), cc.astype(np.uint64), timestamps=ts)
+    vc = rng.choice(nshard * SW, size=20000, replace=False).astype(np.uint64)
+    n.import_values(vc, rng.integers(-1000, 100000, size=len(vc)))
+    idx.existence_field().import_bits(np.zeros(nshard * SW // 2, np.uint64),
+                                      np.arange(nshard * SW // 2, dtype=np.uint64))
+    for frag in cpu.holder.all_fragments():
+        frag.rebuild_cache()
+    gpu = GpuExecutor(cpu.holder, "cuda:0", executor=cpu.executor)
+    yield cpu, gpu
+    cpu.close()
+
+
+QUERIES = [
+    "Count(Row(f=0))", "Count(Row(f=3))", "Count(Intersect(Row(f=0), Row(f=1)))",
+    "Count(Intersect(Row(f=1), Row(f=2)))", "Count(Intersect(Row(f=2), Row(f=3)))",
+    "Count(Intersect(Row(f=0), Row(f=20)))", "Count(Union(Row(f=1), Row(f=2), Row(f=20)))",
+    "Count(Difference(Row(f=0), Row(g=1)))", "Count(Xor(Row(f=4), Row(g=0)))",
+    "Count(Not(Row(f=1)))", "Count(Intersect(Union(Row(f=0), Row(g=2)), Not(Row(f=5))))",
+    "Count(Row(t=1, from=2020-03-01T00:00, to=2020-07-15T00:00))", "Count(Row(f=999))",
+    "Count(Intersect(Row(f=0), Row(f=999)))",
+]
+
+
+@pytest.mark.parametrize("q", QUERIES)
+def test_counts_match_host(envs, q):
+    cpu, gpu = envs
+    want = cpu.q1("i", q)
+    cpu.executor.gpu = gpu
+    try:
+        got = cpu.q1("i", q)
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
+
+
+def test_count_batch(envs):
+    cpu, gpu = envs
+    want = cpu.q("i", " ".join(QUERIES))
+    cpu.executor.gpu = gpu
+    try:
+        n0 = gpu.launches
+        got = cpu.q("i", " ".join(QUERIES))
+        assert gpu.launches == n0 + 1
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
+
+
+@pytest.mark.parametrize("q", ["Row(f=2)", "Intersect(Row(f=0), Row(f=1))", "Union(Row(f=3), Row(f=20))",
+                               "Difference(Row(f=20), Row(f=0))", "Not(Row(f=0))"])
+def test_rows_match_host(envs, q):
+    cpu, gpu = envs
+    want = cols(cpu.q1("i", q))
+    cpu.executor.gpu = gpu
+    try:
+        got = cols(cpu.q1("i", q))
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
+
+
+@pytest.mark.parametrize("q", ["Sum(field=n)", "Sum(Row(f=0), field=n)", "TopN(f, Row(g=1), n=5)",
+                               "TopN(f, Row(g=0))", "GroupBy(Rows(g), Rows(f), limit=20)",
+                               "GroupBy(Rows(g), Rows(f), filter=Row(f=1), limit=7)"])
+def test_aggregates_match_host(envs, q):
+    cpu, gpu = envs
+    want = cpu.q1("i", q)
+    cpu.executor.gpu = gpu
+    try:
+        got = cpu.q1("i", q)
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
+
+
+def test_arena_invalidation_on_write(envs):
+    cpu, gpu = envs
+    cpu.executor.gpu = gpu
+    try:
+        before = cpu.q1("i", "Count(Row(f=7))")
+        cpu.q("i", f"Set({3 * SW + 12345}, f=7)")
+        after = cpu.q1("i", "Count(Row(f=7))")
+    finally:
+        cpu.executor.gpu = None
+    assert after == cpu.q1("i", "Count(Row(f=7))")
+    assert after in (before, before + 1)
