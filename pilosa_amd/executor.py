@@ -360,7 +360,9 @@ class Executor:
         out: Dict[Any, List[int]] = {}
         for s in shards:
             owners = self.cluster.shard_nodes(index, s)
-            node = owners[0] if owners else None
+            live = [n for n in owners if n.state != "DOWN"] or owners
+            # prefer the local replica, then the first live owner
+            node = next((n for n in live if n.id == self.cluster.node.id), live[0] if live else None)
             out.setdefault(node, []).append(s)
         return out
 

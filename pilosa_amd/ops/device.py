@@ -210,12 +210,13 @@ class GpuEngine:
         self.torch = torch
         self.device = torch.device(device)
         self.ext = kernels()
+        self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
 
     def _views_tensor(self, views: List["DeviceView"]):
         arr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
         for i, v in enumerate(views):
             arr[i] = v.viewdev()
-        return self.torch.from_numpy(arr.view(np.uint8)).to(self.device, non_blocking=True)
+        return self._h2d(arr.view(np.uint8))
 
     def compile_batch(self, exprs: Sequence[object]):
         view_index: Dict[int, int] = {}
@@ -244,8 +245,25 @@ class GpuEngine:
                 raise CompileError("views in one batch must share the local shard list")
         return progs, ordered, S or 0
 
+    def _h2d(self, arr: np.ndarray):
+        """Host->device upload on the engine's copy stream, so a batch can be
+        staged while the compute stream is still busy with the previous one
+        (a pageable copy on the compute stream would wait for its kernels)."""
+        torch = self.torch
+        t = torch.from_numpy(arr)
+        if self.copy_stream is None:
+            return t.to(self.device, non_blocking=True)
+        with torch.cuda.stream(self.copy_stream):
+            d = t.to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(self.copy_stream)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(ev)
+        d.record_stream(cur)
+        return d
+
     def upload_batch(self, progs: np.ndarray, views: List[DeviceView]):
-        tp = self.torch.from_numpy(progs.view(np.uint8)).to(self.device, non_blocking=True)
+        tp = self._h2d(progs.view(np.uint8))
         tv = self._views_tensor(views)
         return tp, tv
 
@@ -279,8 +297,8 @@ class GpuEngine:
             if sort and len(sel) > 1:
                 sel = sel[np.lexsort((lr[sel, 1], lr[sel, 0]))]
             sub = np.ascontiguousarray(progs[sel])
-            tp = torch.from_numpy(sub.view(np.uint8)).to(self.device, non_blocking=True)
-            ti = torch.from_numpy(sel.astype(np.int64)).to(self.device, non_blocking=True)
+            tp = self._h2d(sub.view(np.uint8))
+            ti = self._h2d(sel.astype(np.int64))
             parts.append((tp, ti, is_fast, len(sel)))
         return (Q, S, tv, parts)
 
@@ -303,7 +321,7 @@ class GpuEngine:
         if not S or not Q:
             return np.zeros((Q, S), dtype=np.int64)
         tv = self._views_tensor(views)
-        tp = torch.from_numpy(progs.view(np.uint8)).to(self.device, non_blocking=True)
+        tp = self._h2d(progs.view(np.uint8))
         ps = torch.zeros(Q * S, dtype=torch.int64, device=self.device)
         empty = torch.empty(0, dtype=torch.int64, device=self.device)
         self.ext.expr_count(tp, tv, S, empty, None, False, ps)

@@ -35,12 +35,19 @@ class GpuPlanner:
     def bitmap(self, c: Call):
         n = c.name
         if n == "Row" or n == "Bitmap":
+            args = c.args
+            if len(args) == 1:
+                # fast path: Row(field=<int>)
+                for f, row in args.items():
+                    t = type(row)
+                    if t is int and not f.startswith("_") and f not in ("from", "to"):
+                        return Leaf(self.resolve(f, "standard"), row)
             if c.has_condition_arg():
                 raise Unsupported("BSI row")
-            if any(k in c.args for k in ("from", "to", "_start", "_end")):
+            if any(k in args for k in ("from", "to", "_start", "_end")):
                 raise Unsupported("time range")
             f = c.field_arg()
-            row = c.args[f]
+            row = args[f]
             if isinstance(row, bool):
                 row = 1 if row else 0
             if not isinstance(row, int):
@@ -49,8 +56,8 @@ class GpuPlanner:
         if n in ("Intersect", "Union", "Difference", "Xor"):
             if not c.children:
                 raise Unsupported("empty set op")
-            op = {"Intersect": "and", "Union": "or", "Difference": "andnot", "Xor": "xor"}[n]
-            kids = tuple(self.bitmap(k) for k in c.children)
+            op = _SETOPS[n]
+            kids = tuple([self.bitmap(k) for k in c.children])
             if len(kids) == 1:
                 return kids[0]
             return Op(op, kids)
@@ -59,6 +66,9 @@ class GpuPlanner:
                 raise Unsupported("Not without existence tracking")
             return Op("andnot", (Leaf(self.exists_view(), 0), self.bitmap(c.children[0])))
         raise Unsupported(n)
+
+
+_SETOPS = {"Intersect": "and", "Union": "or", "Difference": "andnot", "Xor": "xor"}
 
 
 class BenchPlanner(GpuPlanner):

@@ -1,0 +1,511 @@
+"""Node runtime (reference: server.go, server/server.go, cluster.go resize,
+holder.go syncer/cleaner, gossip/).
+
+Wires holder + cluster + executor (+ GPU executor) + API + HTTP handler and
+runs the background loops:
+
+* membership: the coordinator probes every node's ``/version``
+  (probe interval, N misses -> DOWN, like confirmNodeDown cluster.go:1699)
+  and pushes the cluster status; joining nodes announce themselves to the
+  coordinator (replaces memberlist gossip, which is not available here);
+* resize: node join/leave with data -> coordinator computes per-node fragment
+  sources (cluster.frag_sources), nodes stream fragments over HTTP, report
+  completion, coordinator commits the topology, nodes drop fragments they no
+  longer own (holderCleaner);
+* anti-entropy (ReplicaN > 1): block checksum compare, majority-vote merge,
+  attribute diffs (holder.go:683-839, fragment.go:2849-3014);
+* cache flush (holder.go:506) and runtime/GPU gauges.
+"""
+from __future__ import annotations
+
+import io
+import os
+import threading
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from pilosa_amd.executor import Executor
+from pilosa_amd.models.field import FieldOptions
+from pilosa_amd.models.holder import Holder
+from pilosa_amd.parallel.cluster import (NODE_DOWN, NODE_READY, STATE_NORMAL, STATE_RESIZING, STATE_STARTING,
+                                         Cluster, JumpHasher, ModHasher, Node, URI)
+from pilosa_amd.server.api import API
+from pilosa_amd.server.client import InternalClient
+from pilosa_amd.server.http_handler import Handler, make_http_server
+from pilosa_amd.utils.logger import NopLogger, StandardLogger
+from pilosa_amd.utils.stats import NopStatsClient, new_stats_client
+
+
+class Server:
+    def __init__(self, data_dir: str, bind: str = "127.0.0.1:10101", node_id: Optional[str] = None,
+                 replica_n: int = 1, hosts: Optional[List[str]] = None, coordinator: bool = True,
+                 coordinator_uri: Optional[str] = None, gpu: str = "auto", workers: int = 8,
+                 max_writes: int = 5000, anti_entropy_interval: float = 600.0, probe_interval: float = 1.0,
+                 long_query_time: float = 60.0, stats: str = "expvar", logger=None, hasher: str = "jump",
+                 max_opn: int = 10000, cluster_disabled: bool = False):
+        self.data_dir = data_dir
+        self.bind = bind
+        self.logger = logger or StandardLogger()
+        self.stats = new_stats_client(stats) if isinstance(stats, str) else (stats or NopStatsClient())
+        self.holder = Holder(data_dir, max_opn=max_opn, stats=self.stats)
+        self.client = InternalClient()
+        self.long_query_time = long_query_time
+        self.anti_entropy_interval = anti_entropy_interval
+        self.probe_interval = probe_interval
+        self.hosts = [URI.parse(h) for h in (hosts or [])]
+        self.coordinator_uri = URI.parse(coordinator_uri) if coordinator_uri else None
+        self.is_coordinator_cfg = coordinator
+        self.cluster_disabled = cluster_disabled
+        self._node_id = node_id
+        self.replica_n = replica_n
+        self.hasher = ModHasher() if hasher == "mod" else JumpHasher()
+        self.gpu = None
+        self.gpu_mode = gpu
+        self.workers = workers
+        self.max_writes = max_writes
+        self.cluster: Optional[Cluster] = None
+        self.executor: Optional[Executor] = None
+        self.api = API(self)
+        self.handler = None
+        self.httpd = None
+        self._closing = threading.Event()
+        self._threads: List[threading.Thread] = []
+        self._misses: Dict[str, int] = {}
+        self._resize: Optional[dict] = None
+        self.mu = threading.RLock()
+
+    # ------------------------------------------------------------ lifecycle
+    def open(self):
+        self.holder.open(background=True)
+        nid = self._node_id or self.holder.load_node_id()
+        host, _, port = self.bind.rpartition(":")
+        self.httpd = make_http_server(Handler(self.api, self, self.logger, self.stats), self.bind)
+        port = self.httpd.server_address[1]
+        adv = host if host not in ("", "0.0.0.0") else "127.0.0.1"
+        self.node = Node(nid, URI("http", adv, port), state=NODE_READY)
+        self.cluster = Cluster(self.node, replica_n=self.replica_n, hasher=self.hasher, path=self.data_dir)
+        self.cluster.on_state_change = lambda s: self.logger.debugf("cluster state -> %s", s)
+        self._init_gpu()
+        self.executor = Executor(self.holder, cluster=self.cluster, client=self.client, gpu=self.gpu,
+                                 workers=self.workers, max_writes=self.max_writes, stats=self.stats)
+        if self.gpu is not None:
+            self.gpu.executor = self.executor
+        self.holder.on_create_shard = self._on_create_shard
+        self.holder.on_schema_change = lambda: self.gpu.invalidate() if self.gpu is not None else None
+        t = threading.Thread(target=self.httpd.serve_forever, name="http", daemon=True)
+        t.start()
+        self._threads.append(t)
+        if self.cluster_disabled or (not self.hosts and self.coordinator_uri is None):
+            self.cluster.set_state(STATE_NORMAL)
+        elif self.is_coordinator_cfg:
+            self.cluster.set_coordinator(self.node.id)
+            self._start_loop(self._membership_loop, "membership")
+            self.cluster.set_state(self.cluster.determine_state())
+        else:
+            self._join()
+        if self.replica_n > 1 and self.anti_entropy_interval > 0:
+            self._start_loop(self._anti_entropy_loop, "anti-entropy")
+        self._start_loop(self._runtime_loop, "runtime")
+        return self
+
+    def _init_gpu(self):
+        mode = (self.gpu_mode or "auto").lower()
+        if mode in ("off", "none", "cpu"):
+            return
+        try:
+            import torch
+            if not torch.cuda.is_available():
+                if mode == "on":
+                    raise RuntimeError("gpu=on but no GPU is visible")
+                return
+            from pilosa_amd.ops.gpu_executor import GpuExecutor
+            self.gpu = GpuExecutor(self.holder, "cuda:0")
+        except ImportError:
+            if mode == "on":
+                raise
+
+    def gpu_info(self) -> dict:
+        if self.gpu is None:
+            return {"enabled": False}
+        import torch
+        p = torch.cuda.get_device_properties(self.gpu.device)
+        return {"enabled": True, "name": p.name, "arch": getattr(p, "gcnArchName", ""),
+                "hbmBytes": p.total_memory, "arenaBytes": self.gpu.hbm_bytes(), "launches": self.gpu.launches}
+
+    def close(self):
+        self._closing.set()
+        if self.httpd is not None:
+            self.httpd.shutdown()
+            self.httpd.server_close()
+        if self.executor is not None:
+            self.executor.close()
+        self.holder.close()
+
+    @property
+    def uri(self) -> URI:
+        return self.node.uri
+
+    def _start_loop(self, fn, name):
+        t = threading.Thread(target=fn, name=name, daemon=True)
+        t.start()
+        self._threads.append(t)
+
+    # ------------------------------------------------------------ broadcast
+    def broadcast(self, msg: dict):
+        """SendSync to every other node (server.go:646-667)."""
+        if self.cluster is None:
+            return
+        errs = []
+        for n in list(self.cluster.nodes):
+            if n.id == self.node.id or n.state == NODE_DOWN:
+                continue
+            try:
+                self.client.send_message(n, msg)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        if errs:
+            self.logger.printf("broadcast %s: %d errors, first: %s", msg.get("type"), len(errs), errs[0])
+
+    def _on_create_shard(self, index, field, shard):
+        self.broadcast({"type": "CreateShard", "index": index, "field": field, "shard": shard})
+
+    def receive_message(self, msg: dict):
+        """Dispatch of internal cluster messages (server.go:549-643)."""
+        t = msg.get("type")
+        h = self.holder
+        if t == "CreateIndex":
+            o = msg.get("options", {})
+            h.create_index_if_not_exists(msg["index"], keys=o.get("keys", False),
+                                         track_existence=o.get("trackExistence", True))
+        elif t == "DeleteIndex":
+            if h.index(msg["index"]) is not None:
+                h.delete_index(msg["index"])
+        elif t == "CreateField":
+            idx = h.index(msg["index"])
+            if idx is not None and idx.field(msg["field"]) is None:
+                o = msg.get("options", {})
+                idx.create_field(msg["field"], _field_options(o))
+        elif t == "DeleteField":
+            idx = h.index(msg["index"])
+            if idx is not None and idx.field(msg["field"]) is not None:
+                idx.delete_field(msg["field"])
+        elif t == "DeleteAvailableShard":
+            f = h.field(msg["index"], msg["field"])
+            if f is not None:
+                f.remove_available_shard(msg["shard"])
+        elif t == "DeleteView":
+            f = h.field(msg["index"], msg["field"])
+            if f is not None and f.view(msg["view"]) is not None:
+                f.delete_view(msg["view"])
+        elif t == "CreateShard":
+            f = h.field(msg["index"], msg["field"])
+            if f is not None:
+                f.add_remote_available_shards([msg["shard"]])
+        elif t == "ApplySchema":
+            h.apply_schema(msg["schema"])
+        elif t == "RecalculateCaches":
+            h.recalculate_caches()
+        elif t in ("SetCoordinator", "UpdateCoordinator"):
+            self.cluster.set_coordinator(msg["node"]["id"])
+        elif t == "ClusterStatus":
+            self._merge_cluster_status(msg["status"])
+        elif t == "NodeJoin":
+            self._node_join(Node.from_json(msg["node"]))
+        elif t == "NodeLeave":
+            self._node_down(msg["node"]["id"])
+        elif t == "NodeStatus":
+            self._merge_node_status(msg)
+        elif t == "ResizeInstruction":
+            threading.Thread(target=self._follow_resize, args=(msg,), daemon=True).start()
+        elif t == "ResizeInstructionComplete":
+            self._resize_complete(msg)
+        elif t == "ResizeAbort":
+            self.cluster.set_state(self.cluster.determine_state() if self.cluster.state != STATE_RESIZING
+                                   else STATE_NORMAL)
+        else:
+            raise ValueError(f"unknown message type: {t}")
+
+    # ------------------------------------------------------------ membership
+    def _join(self):
+        target = self.coordinator_uri or (self.hosts[0] if self.hosts else None)
+        if target is None:
+            self.cluster.set_state(STATE_NORMAL)
+            return
+        deadline = time.time() + 30
+        while not self._closing.is_set():
+            try:
+                tmp = Node("?", target)
+                self.client.send_message(tmp, {"type": "NodeJoin", "node": self.node.to_json(),
+                                               "status": self._node_status()})
+                return
+            except Exception as e:  # noqa: BLE001
+                if time.time() > deadline:
+                    self.logger.printf("join %s failed: %s", target, e)
+                    return
+                time.sleep(0.2)
+
+    def _node_status(self) -> dict:
+        return {"node": self.node.to_json(), "schema": self.holder.schema(),
+                "shards": {n: {f.name: f.available_shards() for f in idx.fields.values()}
+                           for n, idx in self.holder.indexes.items()}}
+
+    def _merge_node_status(self, msg: dict):
+        st = msg.get("status") or msg
+        if st.get("schema"):
+            self.holder.apply_schema(st["schema"])
+        for index, fields in (st.get("shards") or {}).items():
+            for fname, shards in fields.items():
+                f = self.holder.field(index, fname)
+                if f is not None and shards:
+                    f.add_remote_available_shards(shards)
+
+    def _node_join(self, n: Node):
+        if not self.cluster.is_coordinator():
+            c = self.cluster.coordinator()
+            if c is not None and c.id != self.node.id:
+                self.client.send_message(c, {"type": "NodeJoin", "node": n.to_json()})
+            return
+        with self.mu:
+            known = self.cluster.node_by_id(n.id)
+            if known is not None:
+                known.uri = n.uri
+                self.cluster.set_node_state(n.id, NODE_READY)
+                self._publish_status()
+                return
+            has_data = any(idx.available_shards() for idx in self.holder.indexes.values())
+            n.state = NODE_READY
+            if has_data and n.id not in self.cluster.topology.node_ids:
+                self._start_resize(self.cluster.nodes + [n], joining=n)
+                return
+            self.cluster.add_node(n)
+            self._publish_status()
+
+    def _node_down(self, nid: str):
+        if self.cluster.set_node_state(nid, NODE_DOWN):
+            self.cluster.set_state(self.cluster.determine_state())
+            if self.cluster.is_coordinator():
+                self._publish_status()
+
+    def _publish_status(self):
+        self.cluster.set_state(self.cluster.determine_state())
+        st = self.cluster.status()
+        st["coordinator"] = self.cluster.coordinator_id
+        msg = {"type": "ClusterStatus", "status": st, "schema": self.holder.schema()}
+        self.broadcast(msg)
+
+    def _merge_cluster_status(self, st: dict):
+        nodes = [Node.from_json(d) for d in st.get("nodes", [])]
+        coord = st.get("coordinator") or next((d["id"] for d in st.get("nodes", []) if d.get("isCoordinator")),
+                                               None)
+        self.cluster.topology.cluster_id = st.get("clusterID", self.cluster.topology.cluster_id)
+        self.cluster.set_nodes(nodes, coord)
+        me = self.cluster.node_by_id(self.node.id)
+        if me is not None:
+            me.state = NODE_READY
+        self.cluster.set_state(st.get("state", STATE_NORMAL))
+
+    def _membership_loop(self):
+        while not self._closing.wait(self.probe_interval):
+            if not self.cluster.is_coordinator():
+                continue
+            changed = False
+            for n in list(self.cluster.nodes):
+                if n.id == self.node.id:
+                    continue
+                try:
+                    self.client.version(n.uri)
+                    self._misses[n.id] = 0
+                    if n.state != NODE_READY:
+                        changed |= self.cluster.set_node_state(n.id, NODE_READY)
+                except Exception:  # noqa: BLE001
+                    self._misses[n.id] = self._misses.get(n.id, 0) + 1
+                    if self._misses[n.id] >= 3 and n.state != NODE_DOWN:
+                        changed |= self.cluster.set_node_state(n.id, NODE_DOWN)
+            new_state = self.cluster.determine_state()
+            if changed or new_state != self.cluster.state:
+                self._publish_status()
+
+    # ------------------------------------------------------------ resize
+    def _holder_layout(self) -> Dict[str, Dict[str, List[str]]]:
+        return {n: {f.name: sorted(f.views) for f in idx.fields.values()} for n, idx in self.holder.indexes.items()}
+
+    def _start_resize(self, new_nodes: List[Node], joining: Optional[Node] = None, leaving: Optional[Node] = None):
+        layout = self._holder_layout()
+        avail = {n: idx.available_shards() for n, idx in self.holder.indexes.items()}
+        sources = self.cluster.frag_sources(new_nodes, layout, avail)
+        job_id = int(time.time() * 1000)
+        self._resize = {"id": job_id, "pending": {n.id for n in new_nodes}, "nodes": new_nodes,
+                        "leaving": leaving.id if leaving else None, "errors": []}
+        self.cluster.set_state(STATE_RESIZING)
+        status = self.cluster.status()
+        for n in new_nodes:
+            msg = {"type": "ResizeInstruction", "jobID": job_id, "node": n.to_json(),
+                   "coordinator": self.node.to_json(), "sources": sources.get(n.id, []),
+                   "schema": self.holder.schema(), "status": status}
+            try:
+                if n.id == self.node.id:
+                    threading.Thread(target=self._follow_resize, args=(msg,), daemon=True).start()
+                else:
+                    self.client.send_message(n, msg)
+            except Exception as e:  # noqa: BLE001
+                self._resize["errors"].append(str(e))
+                self._resize["pending"].discard(n.id)
+
+    def _follow_resize(self, msg: dict):
+        err = ""
+        try:
+            self.cluster.set_state(STATE_RESIZING)
+            self.holder.apply_schema(msg.get("schema", []))
+            for src in msg.get("sources", []):
+                sn = Node.from_json(src["node"])
+                data = self.client.fragment_data(sn.uri, src["index"], src["field"], src["view"], src["shard"])
+                f = self.holder.field(src["index"], src["field"])
+                frag = f.create_view_if_not_exists(src["view"]).create_fragment_if_not_exists(src["shard"])
+                frag.read_from(io.BytesIO(data))
+        except Exception as e:  # noqa: BLE001
+            err = str(e)
+        done = {"type": "ResizeInstructionComplete", "jobID": msg["jobID"], "node": self.node.to_json(),
+                "error": err}
+        coord = Node.from_json(msg["coordinator"])
+        if coord.id == self.node.id:
+            self._resize_complete(done)
+        else:
+            self.client.send_message(coord, done)
+
+    def _resize_complete(self, msg: dict):
+        with self.mu:
+            job = self._resize
+            if job is None or msg.get("jobID") != job["id"]:
+                return
+            if msg.get("error"):
+                job["errors"].append(msg["error"])
+            job["pending"].discard(msg["node"]["id"])
+            if job["pending"]:
+                return
+            self._resize = None
+            if job["errors"]:
+                self.logger.printf("resize job %s failed: %s", job["id"], job["errors"][0])
+            else:
+                self.cluster.set_nodes(job["nodes"], self.cluster.coordinator_id)
+                if job.get("leaving"):
+                    self.cluster.remove_node(job["leaving"])
+            self.cluster.state = STATE_NORMAL
+            self._publish_status()
+            self.clean_holder()
+            self.broadcast({"type": "RecalculateCaches"})
+
+    def resize_remove_node(self, n: Node):
+        remaining = [x for x in self.cluster.nodes if x.id != n.id]
+        has_data = any(idx.available_shards() for idx in self.holder.indexes.values())
+        if has_data:
+            self._start_resize(remaining, leaving=n)
+        else:
+            self.cluster.remove_node(n.id)
+            self._publish_status()
+
+    def abort_resize(self) -> bool:
+        with self.mu:
+            if self._resize is None:
+                return False
+            self._resize = None
+            self.cluster.state = STATE_NORMAL
+            self._publish_status()
+            self.broadcast({"type": "ResizeAbort"})
+            return True
+
+    def clean_holder(self):
+        """Delete local fragments this node no longer owns (holderCleaner)."""
+        for idx in list(self.holder.indexes.values()):
+            for f in list(idx.fields.values()):
+                for v in list(f.views.values()):
+                    for shard in list(v.fragments):
+                        if not self.cluster.owns_shard(self.node.id, idx.name, shard):
+                            v.delete_fragment(shard)
+        if self.gpu is not None:
+            self.gpu.invalidate()
+
+    # ------------------------------------------------------------ anti-entropy
+    def _anti_entropy_loop(self):
+        while not self._closing.wait(self.anti_entropy_interval):
+            if self.cluster.state != STATE_NORMAL:
+                continue
+            try:
+                self.sync_holder()
+            except Exception as e:  # noqa: BLE001
+                self.logger.printf("anti-entropy: %s", e)
+
+    def sync_holder(self):
+        """One anti-entropy pass over every local fragment and attr store."""
+        for idx in list(self.holder.indexes.values()):
+            self._sync_attrs(idx.name, None, idx.column_attr_store)
+            for f in list(idx.fields.values()):
+                self._sync_attrs(idx.name, f.name, f.row_attr_store)
+                for v in list(f.views.values()):
+                    for shard, frag in list(v.fragments.items()):
+                        self._sync_fragment(idx.name, f.name, v.name, shard, frag)
+
+    def _sync_attrs(self, index, field, store):
+        blocks = [{"id": b, "checksum": c.hex()} for b, c in store.blocks()]
+        for n in self.cluster.nodes:
+            if n.id == self.node.id or n.state != NODE_READY:
+                continue
+            try:
+                diff = self.client.attr_diff(n.uri, index, field, blocks)
+            except Exception:  # noqa: BLE001
+                continue
+            if diff:
+                store.set_bulk_attrs(diff)
+
+    def _sync_fragment(self, index, field, view, shard, frag):
+        owners = [n for n in self.cluster.shard_nodes(index, shard) if n.id != self.node.id]
+        if not owners:
+            return
+        local = dict(frag.blocks())
+        remote_blocks = {}
+        for n in owners:
+            try:
+                remote_blocks[n.id] = {b["id"]: bytes.fromhex(b["checksum"])
+                                       for b in self.client.fragment_blocks(n.uri, index, field, view, shard)}
+            except Exception:  # noqa: BLE001
+                remote_blocks[n.id] = None
+        live = [n for n in owners if remote_blocks.get(n.id) is not None]
+        ids = set(local)
+        for n in live:
+            ids |= set(remote_blocks[n.id])
+        for bid in sorted(ids):
+            if all(remote_blocks[n.id].get(bid) == local.get(bid) for n in live):
+                continue
+            data = [self.client.block_data(n.uri, index, field, view, shard, bid) for n in live]
+            sets, clears = frag.merge_block(bid, data)
+            base = shard << 20
+            for n, (sr, sc), (cr, cc) in zip(live, sets, clears):
+                if sr:
+                    self.client.import_bits(n, index, field, shard, sr, [base + c for c in sc],
+                                            ignore_key_check=True)
+                if cr:
+                    self.client.import_bits(n, index, field, shard, cr, [base + c for c in cc], clear=True,
+                                            ignore_key_check=True)
+
+    # ------------------------------------------------------------ runtime gauges
+    def _runtime_loop(self):
+        while not self._closing.wait(10.0):
+            try:
+                import resource
+                ru = resource.getrusage(resource.RUSAGE_SELF)
+                self.stats.gauge("maxrss_kb", ru.ru_maxrss)
+                self.stats.gauge("open_files", len(os.listdir("/proc/self/fd")))
+                self.stats.gauge("threads", threading.active_count())
+                if self.gpu is not None:
+                    self.stats.gauge("gpu.arena_bytes", self.gpu.hbm_bytes())
+                    self.stats.gauge("gpu.launches", self.gpu.launches)
+            except Exception:  # noqa: BLE001
+                pass
+
+
+def _field_options(o: dict) -> FieldOptions:
+    return FieldOptions(type=o.get("type", "set"), cache_type=o.get("cacheType", ""), cache_size=o.get("cacheSize", 0),
+                        time_quantum=o.get("timeQuantum", ""), min=o.get("min", 0), max=o.get("max", 0),
+                        keys=o.get("keys", False), no_standard_view=o.get("noStandardView", False),
+                        base=o.get("base", 0), bit_depth=o.get("bitDepth", 0))
