@@ -107,20 +107,31 @@ def main():
             dist.all_reduce(out)
         return out
 
+    tm = {"prep": 0.0, "launch": 0.0, "wait": 0.0}
+
     def run(first, n):
         # software pipeline: the host prepares batch i+1 while the GPU runs i
         h = prep(first)
         pending = launch(h)
         res = None
         for i in range(first + 1, first + n):
+            t0 = time.perf_counter()
             h = prep(i)
+            t1 = time.perf_counter()
             nxt = launch(h)
+            t2 = time.perf_counter()
             res = pending.cpu()
+            t3 = time.perf_counter()
+            tm["prep"] += t1 - t0
+            tm["launch"] += t2 - t1
+            tm["wait"] += t3 - t2
             pending = nxt
         res = pending.cpu()
         return res
 
     run(0, args.warmup)
+    for k in tm:
+        tm[k] = 0.0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -139,7 +150,8 @@ def main():
 
     extra = {"gen_s": round(tgen, 2), "h2d_s": round(tload, 2), "hbm_bytes_per_gpu": view.nbytes(),
              "containers_per_gpu": view.container_count, "shards": nshards,
-             "mean_count": float(last.double().mean()) if last is not None else None}
+             "mean_count": float(last.double().mean()) if last is not None else None,
+             "host_ms_per_step": {k: round(v / max(1, args.steps - 1) * 1000, 3) for k, v in tm.items()}}
 
     if rank == 0:
         rec = {"metric": "PQL queries/sec (Count(Intersect(Row,Row))) on 1M-row x 1B-col set field",

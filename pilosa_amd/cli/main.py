@@ -1,0 +1,343 @@
+"""Command line (reference: cmd/root.go, cmd/*.go, ctl/*.go).
+
+    python -m pilosa_amd.cli server  [--data-dir D --bind H:P --cluster.hosts ... --gpu.mode auto]
+    python -m pilosa_amd.cli import  -i INDEX -f FIELD [--host H] [--create-schema] [--clear] FILE...
+    python -m pilosa_amd.cli export  -i INDEX -f FIELD [--host H] [-o OUT]
+    python -m pilosa_amd.cli check   FRAGMENT_FILE...
+    python -m pilosa_amd.cli inspect FRAGMENT_FILE
+    python -m pilosa_amd.cli config  [--config FILE]        (resolved configuration as TOML)
+    python -m pilosa_amd.cli generate-config                 (defaults as TOML)
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import datetime as dt
+import io
+import json
+import os
+import signal
+import sys
+import threading
+from typing import Dict, List, Optional
+
+SHARD_WIDTH = 1 << 20
+
+
+# ------------------------------------------------------------------ config plumbing
+def _add_config_flags(p: argparse.ArgumentParser):
+    from pilosa_amd.server.config import DEFAULTS
+
+    def walk(d, prefix=""):
+        for k, v in d.items():
+            key = f"{prefix}{k}"
+            if isinstance(v, dict):
+                walk(v, key + ".")
+            else:
+                p.add_argument(f"--{key}", dest=f"cfg__{key}", default=None,
+                               help=f"(default {v!r})")
+    walk(DEFAULTS)
+
+
+def resolve_config(args) -> "object":
+    from pilosa_amd.server.config import Config
+    cfg = Config()
+    path = getattr(args, "config", None)
+    if path:
+        cfg.load_toml(path)
+    cfg.load_env()
+    for k, v in vars(args).items():
+        if k.startswith("cfg__") and v is not None:
+            cfg.set(k[5:], v)
+    return cfg
+
+
+# ------------------------------------------------------------------ server
+def cmd_server(args, stdout, stderr) -> int:
+    from pilosa_amd.server.config import parse_duration
+    from pilosa_amd.server.server import Server
+    from pilosa_amd.utils import tracing
+    from pilosa_amd.utils.logger import StandardLogger
+
+    cfg = resolve_config(args)
+    log_stream = stderr
+    if cfg.get("log-path"):
+        log_stream = open(os.path.expanduser(cfg.get("log-path")), "a")
+    logger = StandardLogger(log_stream, verbose=cfg.get("verbose"))
+    if cfg.get("tracing.sampler-type") not in ("", "off", "none"):
+        tracing.set_global_tracer(tracing.RecordingTracer())
+    bind = cfg.get("bind")
+    if bind.startswith(":"):
+        bind = "0.0.0.0" + bind
+    hosts = cfg.get("cluster.hosts")
+    srv = Server(cfg.data_dir(), bind=bind, replica_n=cfg.get("cluster.replicas"), hosts=hosts,
+                 coordinator=cfg.get("cluster.coordinator") or not hosts,
+                 coordinator_uri=cfg.get("cluster.coordinator-uri") or (hosts[0] if hosts and
+                                                                         not cfg.get("cluster.coordinator")
+                                                                         else None),
+                 gpu=cfg.get("gpu.mode"), workers=cfg.get("worker-pool-size"),
+                 max_writes=cfg.get("max-writes-per-request"),
+                 anti_entropy_interval=cfg.duration("anti-entropy.interval"),
+                 probe_interval=cfg.duration("gossip.probe-interval"),
+                 long_query_time=cfg.duration("cluster.long-query-time"), stats=cfg.get("metric.service")
+                 if cfg.get("metric.service") != "none" else "expvar", logger=logger,
+                 cluster_disabled=cfg.get("cluster.disabled"))
+    srv.open()
+    logger.printf("listening as %s (node %s, gpu=%s)", srv.uri.normalize(), srv.node.id,
+                  "on" if srv.gpu is not None else "off")
+    stop = threading.Event()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            signal.signal(sig, lambda *a: stop.set())
+        except ValueError:
+            pass
+    if getattr(args, "_run_seconds", None):
+        stop.wait(args._run_seconds)
+    else:
+        stop.wait()
+    srv.close()
+    return 0
+
+
+# ------------------------------------------------------------------ import
+def _client_uri(host: str):
+    from pilosa_amd.parallel.cluster import URI
+    return URI.parse(host)
+
+
+def cmd_import(args, stdout, stderr) -> int:
+    from pilosa_amd.parallel.cluster import Node
+    from pilosa_amd.server.client import InternalClient
+
+    if not args.index:
+        print("index required", file=stderr)
+        return 1
+    if not args.field:
+        print("field required", file=stderr)
+        return 1
+    if not args.paths:
+        print("path required", file=stderr)
+        return 1
+    uri = _client_uri(args.host)
+    c = InternalClient()
+    if args.create_schema:
+        c.create_index(uri, args.index, keys=args.index_keys)
+        ftype = args.field_type or ("time" if args.field_time_quantum else "int" if (args.field_min or args.field_max)
+                                    else "set")
+        opts: Dict[str, object] = {"type": ftype}
+        if ftype in ("set", "mutex"):
+            opts["keys"] = args.field_keys
+        elif ftype == "int":
+            opts.update({"min": args.field_min, "max": args.field_max})
+        elif ftype == "time":
+            opts.update({"timeQuantum": args.field_time_quantum, "keys": args.field_keys})
+        c.create_field(uri, args.index, args.field, opts)
+    schema = c.schema(uri)
+    idx = next((i for i in schema if i["name"] == args.index), None)
+    if idx is None:
+        print("index not found", file=stderr)
+        return 1
+    fld = next((f for f in idx.get("fields", []) if f["name"] == args.field), None)
+    if fld is None:
+        print("field not found", file=stderr)
+        return 1
+    is_int = fld["options"].get("type") == "int"
+    use_col_keys = idx["options"].get("keys", False)
+    use_row_keys = fld["options"].get("keys", False)
+    node = Node("cli", uri)
+    total = 0
+    for path in args.paths:
+        fh = sys.stdin if path == "-" else open(path, newline="")
+        buf: List[list] = []
+        for rnum, rec in enumerate(csv.reader(fh), 1):
+            if not rec or rec[0] == "":
+                continue
+            if len(rec) < 2:
+                print(f"bad column count on row {rnum}: col={len(rec)}", file=stderr)
+                return 1
+            buf.append(rec)
+            if len(buf) >= args.buffer_size:
+                total += _flush(c, node, args, buf, is_int, use_col_keys, use_row_keys)
+                buf = []
+        total += _flush(c, node, args, buf, is_int, use_col_keys, use_row_keys)
+        if fh is not sys.stdin:
+            fh.close()
+    print(f"imported {total} records", file=stderr)
+    return 0
+
+
+def _flush(c, node, args, buf, is_int, col_keys, row_keys) -> int:
+    if not buf:
+        return 0
+    if is_int:
+        if col_keys:
+            c.import_values(node, args.index, args.field, 0, [], [int(r[1]) for r in buf],
+                            col_keys=[r[0] for r in buf], clear=args.clear)
+            return len(buf)
+        by: Dict[int, list] = {}
+        for r in buf:
+            col = int(r[0])
+            by.setdefault(col // SHARD_WIDTH, []).append((col, int(r[1])))
+        for shard, pairs in sorted(by.items()):
+            if args.sort:
+                pairs.sort()
+            c.import_values(node, args.index, args.field, shard, [p[0] for p in pairs], [p[1] for p in pairs],
+                            clear=args.clear)
+        return len(buf)
+    ts = []
+    for r in buf:
+        if len(r) > 2 and r[2]:
+            t = dt.datetime.strptime(r[2], "%Y-%m-%dT%H:%M")
+            ts.append(int((t - dt.datetime(1970, 1, 1)).total_seconds() * 1e9))
+        else:
+            ts.append(0)
+    if col_keys or row_keys:
+        c.import_bits(node, args.index, args.field, 0, [] if row_keys else [int(r[0]) for r in buf],
+                      [] if col_keys else [int(r[1]) for r in buf], ts if any(ts) else [], clear=args.clear,
+                      row_keys=[r[0] for r in buf] if row_keys else [],
+                      col_keys=[r[1] for r in buf] if col_keys else [])
+        return len(buf)
+    by2: Dict[int, list] = {}
+    for r, t in zip(buf, ts):
+        col = int(r[1])
+        by2.setdefault(col // SHARD_WIDTH, []).append((int(r[0]), col, t))
+    for shard, bits in sorted(by2.items()):
+        if args.sort:
+            bits.sort(key=lambda b: (b[0], b[1]))
+        tt = [b[2] for b in bits]
+        c.import_bits(node, args.index, args.field, shard, [b[0] for b in bits], [b[1] for b in bits],
+                      tt if any(tt) else [], clear=args.clear)
+    return len(buf)
+
+
+# ------------------------------------------------------------------ export
+def cmd_export(args, stdout, stderr) -> int:
+    from pilosa_amd.server.client import InternalClient
+    if not args.index or not args.field:
+        print("index and field required", file=stderr)
+        return 1
+    uri = _client_uri(args.host)
+    c = InternalClient()
+    maxs = c.max_shards(uri).get(args.index, 0)
+    out = open(args.output, "w") if args.output else stdout
+    for shard in range(maxs + 1):
+        nodes = c.fragment_nodes(uri, args.index, shard)
+        from pilosa_amd.parallel.cluster import URI
+        target = URI.from_json(nodes[0]["uri"]) if nodes else uri
+        out.write(c.export_csv(target, args.index, args.field, shard))
+    if args.output:
+        out.close()
+    return 0
+
+
+# ------------------------------------------------------------------ check / inspect
+def cmd_check(args, stdout, stderr) -> int:
+    from pilosa_amd import _roaring
+    rc = 0
+    for p in args.paths:
+        if p.endswith(".cache") or p.endswith(".snapshotting"):
+            print(f"{p}: ignoring", file=stdout)
+            continue
+        try:
+            with open(p, "rb") as fh:
+                bm = _roaring.Bitmap.from_bytes(fh.read())
+            errs = bm.check()
+        except Exception as e:  # noqa: BLE001
+            errs = str(e)
+        if errs:
+            rc = 1
+            print(f"{p}: {errs.strip()}", file=stdout)
+        else:
+            print(f"{p}: ok", file=stdout)
+    return rc
+
+
+def cmd_inspect(args, stdout, stderr) -> int:
+    from collections import Counter
+
+    from pilosa_amd import _roaring
+    with open(args.path, "rb") as fh:
+        data = fh.read()
+    bm = _roaring.Bitmap.from_bytes(data)
+    info = bm.container_info()
+    types = Counter(t for _, t, _ in info)
+    print("== Bitmap Info ==", file=stdout)
+    print(f"Containers: {len(info)}", file=stdout)
+    print(f"Operations: {bm.ops}", file=stdout)
+    print(f"Bits: {bm.count()}", file=stdout)
+    print(f"Types: {dict(types)}", file=stdout)
+    print("", file=stdout)
+    print("== Containers ==", file=stdout)
+    print(f"{'KEY':>12} {'TYPE':>8} {'N':>8}", file=stdout)
+    for k, t, n in info[: args.limit]:
+        print(f"{k:>12} {t:>8} {n:>8}", file=stdout)
+    return 0
+
+
+def cmd_config(args, stdout, stderr) -> int:
+    stdout.write(resolve_config(args).to_toml())
+    return 0
+
+
+def cmd_generate_config(args, stdout, stderr) -> int:
+    from pilosa_amd.server.config import Config
+    stdout.write(Config().to_toml())
+    return 0
+
+
+# ------------------------------------------------------------------ main
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="pilosa", description="MI355X-native distributed bitmap index")
+    sub = p.add_subparsers(dest="cmd")
+    s = sub.add_parser("server", help="run a node")
+    s.add_argument("-c", "--config", default=None)
+    _add_config_flags(s)
+    i = sub.add_parser("import", help="bulk load CSV data")
+    i.add_argument("--host", default="localhost:10101")
+    i.add_argument("-i", "--index", default="")
+    i.add_argument("-f", "--field", default="")
+    i.add_argument("--create-schema", action="store_true")
+    i.add_argument("--clear", action="store_true")
+    i.add_argument("--index-keys", action="store_true")
+    i.add_argument("--field-keys", action="store_true")
+    i.add_argument("--field-type", default="")
+    i.add_argument("--field-min", type=int, default=0)
+    i.add_argument("--field-max", type=int, default=0)
+    i.add_argument("--field-time-quantum", default="")
+    i.add_argument("-b", "--buffer-size", type=int, default=10000000)
+    i.add_argument("--sort", action="store_true")
+    i.add_argument("paths", nargs="*")
+    e = sub.add_parser("export", help="export a field as CSV")
+    e.add_argument("--host", default="localhost:10101")
+    e.add_argument("-i", "--index", default="")
+    e.add_argument("-f", "--field", default="")
+    e.add_argument("-o", "--output", default="")
+    ck = sub.add_parser("check", help="consistency check of fragment files")
+    ck.add_argument("paths", nargs="+")
+    ins = sub.add_parser("inspect", help="inspect a fragment file")
+    ins.add_argument("path")
+    ins.add_argument("--limit", type=int, default=100)
+    cf = sub.add_parser("config", help="print the resolved configuration")
+    cf.add_argument("-c", "--config", default=None)
+    _add_config_flags(cf)
+    sub.add_parser("generate-config", help="print the default configuration")
+    return p
+
+
+COMMANDS = {"server": cmd_server, "import": cmd_import, "export": cmd_export, "check": cmd_check,
+            "inspect": cmd_inspect, "config": cmd_config, "generate-config": cmd_generate_config}
+
+
+def main(argv=None, stdout=None, stderr=None) -> int:
+    stdout = stdout or sys.stdout
+    stderr = stderr or sys.stderr
+    p = build_parser()
+    args = p.parse_args(argv)
+    if not args.cmd:
+        p.print_help(stdout)
+        return 0
+    return COMMANDS[args.cmd](args, stdout, stderr)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

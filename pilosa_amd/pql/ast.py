@@ -156,7 +156,9 @@ def format_value(v: Any) -> str:
     if isinstance(v, bool):
         return "true" if v else "false"
     if v is None:
-        return "<nil>"
+        # the reference prints Go's "<nil>", which its own grammar cannot
+        # re-parse when a call is forwarded to a remote node; emit PQL null.
+        return "null"
     if isinstance(v, list):
         return "[" + ",".join(_go_quote(x) if isinstance(x, str) else format_value(x) for x in v) + "]"
     if isinstance(v, _dt.datetime):
