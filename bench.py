@@ -72,8 +72,7 @@ def main():
 
     from pilosa_amd import _roaring
     from pilosa_amd.ops.device import DeviceView, GpuEngine
-    from pilosa_amd.pql import parse_string
-    from pilosa_amd.ops.planner import BenchPlanner
+    from pilosa_amd.ops.planner import NativeCountCompiler
 
     nshards = math.ceil(args.cols / SHARD_WIDTH)
     lo = nshards * rank // world
@@ -87,7 +86,7 @@ def main():
     torch.cuda.synchronize(dev)
     tload = time.time() - t0 - tgen
     eng = GpuEngine(dev)
-    planner = BenchPlanner({"f": view})
+    compiler = NativeCountCompiler({"f": view})
 
     rng = np.random.default_rng(1234)
     nq = args.batch * (args.steps + args.warmup)
@@ -96,10 +95,10 @@ def main():
     queries = [f"Count(Intersect(Row(f={a}), Row(f={b})))" for a, b in zip(ra, rb)]
 
     def prep(i):
-        # host half: PQL parse + plan + compile + program upload
+        # host half: PQL text -> device programs (native scanner, general
+        # parser for anything else) + batch ordering + program upload
         qs = queries[i * args.batch:(i + 1) * args.batch]
-        exprs = [planner.plan(parse_string(q).calls[0]) for q in qs]
-        return eng.prepare_count(exprs)
+        return eng.prepare_progs(*compiler.compile(qs))
 
     def launch(h):
         out = eng.launch_count(h)
@@ -151,6 +150,7 @@ def main():
     extra = {"gen_s": round(tgen, 2), "h2d_s": round(tload, 2), "hbm_bytes_per_gpu": view.nbytes(),
              "containers_per_gpu": view.container_count, "shards": nshards,
              "mean_count": float(last.double().mean()) if last is not None else None,
+             "native_compiled": compiler.native_hits, "fallback_compiled": compiler.fallbacks,
              "host_ms_per_step": {k: round(v / max(1, args.steps - 1) * 1000, 3) for k, v in tm.items()}}
 
     if rank == 0:

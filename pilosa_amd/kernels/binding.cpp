@@ -88,6 +88,22 @@ void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor 
                      reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>()), cur_stream(progs));
 }
 
+void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor pairs, torch::Tensor partial,
+                int64_t cq) {
+  check_dev(progs, "progs");
+  check_dev(views, "views");
+  check_dev(pairs, "pairs");
+  check_dev(partial, "partial");
+  const int Q = int(progs.numel() / sizeof(pk::QueryProg));
+  const int64_t n = int64_t(Q) * S * 16;
+  TORCH_CHECK(pairs.numel() * pairs.element_size() >= n * 8, "pairs scratch must hold S*16*Q uint2");
+  TORCH_CHECK(partial.scalar_type() == torch::kInt32 && partial.numel() >= n, "partial must be int32[S*16*Q]");
+  pk::launch_and2_pairs(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
+                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
+                        reinterpret_cast<uint2*>(pairs.data_ptr()), partial.data_ptr<int32_t>(), int(cq),
+                        cur_stream(progs));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -100,5 +116,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("fast") = false,
         py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
+  m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),
+        py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 8);
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
 }

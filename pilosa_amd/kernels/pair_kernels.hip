@@ -1,0 +1,333 @@
+// Count(Intersect(Row(a), Row(b))) for a batch of queries, organised around
+// container keys instead of (query, shard) work items.
+//
+// Why a separate path: in the headline workload ~70 % of container pairs are
+// array&array (~1.1k values each), 26 % array&bitmap.  The generic kernel
+// walks the <=16 keys of one (query, shard) sequentially, so every container
+// costs two dependent global round trips (meta -> payload) and a wave never
+// has more than one container in flight; it also streams each row once per
+// query, although in a Zipf batch every hot row is read by many queries.
+//
+// Here the work is split in two launches:
+//   K1 pair_build   one thread per (shard, query): resolves both rows' CSR
+//                   ranges, derives the key-presence masks (no meta loads for
+//                   full rows) and writes the matching container index pair
+//                   for every key j to pairs[(s*16 + j) * Q + q].
+//   K2 and2_pairs   one wave per (shard, key, chunk of CQ queries).  The
+//                   batch is sorted on the host by (hot row, other row), so
+//                   consecutive queries in a chunk usually share row a: the
+//                   wave stages a's container ONCE into its 8 KiB LDS bitmap
+//                   and only streams b's container per query.  Waves of one
+//                   (shard, key) unit are consecutive and XCD-remapped onto
+//                   one XCD, so the unit's containers (~1.3 MB) live in that
+//                   XCD's 4 MB L2 while all its chunks run.
+// Per-(unit, query) counts go to an int32 partial buffer that torch reduces
+// (deterministic, no contended atomics).
+//
+// Reference hot loops replaced: roaring/roaring.go:3078-3215 intersectionCount*
+// and executor.go:1230-1290 (executeCount over executeIntersect).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace pk {
+namespace {
+
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int PAIR_WAVES = 4;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t xcd_remap_blocks(uint32_t bid, uint32_t nblk) {
+  const uint32_t nx = 8;
+  const uint32_t xcd = bid % nx, loc = bid / nx;
+  const uint32_t q = nblk / nx, r = nblk % nx;
+  const uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + loc;
+}
+
+// Payload/meta pointers live in ViewDev as generic pointers; casting them to
+// the global address space gives global_load (vmcnt only) instead of
+// flat_load, which also counts against lgkmcnt and so serialises with LDS.
+// (The host compilation pass parses these bodies too, without address spaces.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PK_GLOBAL __attribute__((address_space(1)))
+#else
+#define PK_GLOBAL
+#endif
+template <class T>
+__device__ __forceinline__ const PK_GLOBAL T* gp(const T* p) {
+  return (const PK_GLOBAL T*)(p);
+}
+
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Key-presence mask and absolute first-container index of dense row d in shard s.
+__device__ __forceinline__ uint32_t row_keys(const ViewDev& v, int s, int64_t d, int64_t& lo) {
+  lo = 0;
+  if (d < 0) return 0;
+  const auto rp = gp(v.rowptr + int64_t(s) * (v.D + 1));
+  const uint32_t r0 = rp[d], r1 = rp[d + 1];
+  lo = gp(v.shard_base)[s] + r0;
+  const int n = int(r1 - r0);
+  if (n == 16) return 0xffffu;
+  uint32_t pres = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if (k < n) pres |= 1u << meta_j(gp(v.meta)[lo + k]);
+  return pres;
+}
+
+__global__ __launch_bounds__(256) void pair_build_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                         const ViewDev* __restrict__ views, int S,
+                                                         uint2* __restrict__ pairs) {
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= int64_t(Q) * S) return;
+  const int s = int(t / Q), q = int(t % Q);
+  const QueryProg& qp = progs[q];
+  int64_t loa, lob;
+  const uint32_t pa = row_keys(views[qp.leaf_view[0]], s, qp.leaf_row[0], loa);
+  const uint32_t pb = row_keys(views[qp.leaf_view[1]], s, qp.leaf_row[1], lob);
+  const uint32_t both = pa & pb;
+  uint2* dst = pairs + int64_t(s) * 16 * Q + q;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    uint2 e = make_uint2(NONE, NONE);
+    if ((both >> j) & 1) {
+      const uint32_t below = (1u << j) - 1;
+      e.x = uint32_t(loa + __popc(pa & below));
+      e.y = uint32_t(lob + __popc(pb & below));
+    }
+    dst[int64_t(j) * Q] = e;
+  }
+}
+
+// ---- container primitives (wave-cooperative, lb = wave-private 1024-word LDS bitmap)
+
+__device__ __forceinline__ const uint16_t* payload_of(const ViewDev& v, int64_t m) {
+  return v.payload + meta_off16(m) * 8;
+}
+
+__device__ __forceinline__ void lds_clear(uint64_t* lb) {
+  ulong2* l2 = reinterpret_cast<ulong2*>(lb);
+  const int lane = lane_id();
+#pragma unroll
+  for (int i = 0; i < 8; i++) l2[i * 64 + lane] = make_ulong2(0, 0);
+}
+
+// Stage a container of any type into lb as a bitmap.
+__device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m) {
+  const int lane = lane_id();
+  const int type = meta_type(m);
+  ulong2* l2 = reinterpret_cast<ulong2*>(lb);
+  if (type == CT_BITMAP) {
+    const auto g = gp(reinterpret_cast<const ulong2*>(p));
+    const ulong2 t0 = g[lane], t1 = g[64 + lane], t2 = g[128 + lane], t3 = g[192 + lane];
+    const ulong2 t4 = g[256 + lane], t5 = g[320 + lane], t6 = g[384 + lane], t7 = g[448 + lane];
+    l2[lane] = t0; l2[64 + lane] = t1; l2[128 + lane] = t2; l2[192 + lane] = t3;
+    l2[256 + lane] = t4; l2[320 + lane] = t5; l2[384 + lane] = t6; l2[448 + lane] = t7;
+    lds_wait();
+    return;
+  }
+  lds_clear(lb);
+  lds_wait();
+  if (type == CT_ARRAY) {
+    const int n = meta_n(m);
+    const auto p4 = gp(reinterpret_cast<const uint4*>(p));
+    const int n8 = (n + 7) >> 3;
+    for (int e8 = lane; e8 < n8; e8 += 64) {
+      const uint4 v4 = p4[e8];
+      const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
+        if (e8 * 8 + k < n) atomicOr(reinterpret_cast<unsigned long long*>(&lb[v >> 6]), 1ull << (v & 63));
+      }
+    }
+  } else {
+    const auto pr = gp(p);
+    const int nr = pr[0];
+    for (int r = lane; r < nr; r += 64) {
+      const uint32_t s = pr[8 + 2 * r], e = uint32_t(pr[9 + 2 * r]) + 1;
+      const uint32_t ws = s >> 6, we = (e - 1) >> 6;
+      if (ws == we) {
+        const uint64_t mk = (e - s == 64) ? ~0ull : (((1ull << (e - s)) - 1) << (s & 63));
+        atomicOr(reinterpret_cast<unsigned long long*>(&lb[ws]), mk);
+      } else {
+        atomicOr(reinterpret_cast<unsigned long long*>(&lb[ws]), ~0ull << (s & 63));
+        for (uint32_t w = ws + 1; w < we; w++) lb[w] = ~0ull;
+        const uint32_t hb = e & 63;
+        atomicOr(reinterpret_cast<unsigned long long*>(&lb[we]), hb ? ((1ull << hb) - 1) : ~0ull);
+      }
+    }
+  }
+  lds_wait();
+}
+
+// Count array values present in a 1024-word bitmap (LDS or global).
+template <class BM>
+__device__ __forceinline__ int probe(BM bm, const uint16_t* arr, int n) {
+  const int lane = lane_id();
+  const auto p4 = gp(reinterpret_cast<const uint4*>(arr));
+  const int n8 = (n + 7) >> 3;
+  int c = 0;
+  for (int e8 = lane; e8 < n8; e8 += 64) {
+    const uint4 v4 = p4[e8];
+    const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
+      c += (e8 * 8 + k < n) ? int((bm[v >> 6] >> (v & 63)) & 1) : 0;
+    }
+  }
+  return c;
+}
+
+template <class PX>
+__device__ __forceinline__ int and_bitmaps(PX a, const uint64_t* y) {
+  const int lane = lane_id();
+  const auto b = gp(reinterpret_cast<const ulong2*>(y));
+  ulong2 u[8], v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) u[i] = a[i * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = b[i * 64 + lane];
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) c += __popcll(u[i].x & v[i].x) + __popcll(u[i].y & v[i].y);
+  return c;
+}
+
+// Count bits of a run container inside the LDS bitmap.
+__device__ __forceinline__ int runs_in_lds(const uint64_t* lb, const uint16_t* p) {
+  const int lane = lane_id();
+  const auto pr = gp(p);
+  const int nr = pr[0];
+  int c = 0;
+  for (int r = lane; r < nr; r += 64) {
+    const uint32_t s = pr[8 + 2 * r], e = uint32_t(pr[9 + 2 * r]) + 1;
+    const uint32_t ws = s >> 6, we = (e - 1) >> 6;
+    for (uint32_t w = ws; w <= we; w++) {
+      uint64_t mk = ~0ull;
+      if (w == ws) mk &= ~0ull << (s & 63);
+      if (w == we && (e & 63)) mk &= (1ull << (e & 63)) - 1;
+      c += __popcll(lb[w] & mk);
+    }
+  }
+  return c;
+}
+
+// |B ∩ staged| where staged lives in lb.
+__device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* p, int64_t m) {
+  const int type = meta_type(m);
+  if (type == CT_BITMAP) return and_bitmaps(reinterpret_cast<const ulong2*>(lb), reinterpret_cast<const uint64_t*>(p));
+  if (type == CT_ARRAY) return probe(lb, p, meta_n(m));
+  return runs_in_lds(lb, p);
+}
+
+template <int CQ>
+__global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                                    const ViewDev* __restrict__ views, int S,
+                                                                    const uint2* __restrict__ pairs,
+                                                                    int32_t* __restrict__ partial) {
+  __shared__ uint64_t lbs[PAIR_WAVES][1024];
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int64_t gw = int64_t(xcd_remap_blocks(blockIdx.x, gridDim.x)) * PAIR_WAVES + wave;
+  const int nch = (Q + CQ - 1) / CQ;
+  const int64_t u = gw / nch;
+  if (u >= int64_t(S) * 16) return;
+  const int q0 = int(gw % nch) * CQ;
+  uint64_t* lb = lbs[wave];
+
+  // lane i < CQ prefetches query q0+i's pair, views and both metas
+  uint32_t ea = NONE, eb = NONE;
+  int vai = 0, vbi = 0;
+  int64_t ma = 0, mb = 0;
+  if (lane < CQ && q0 + lane < Q) {
+    const uint2 e = pairs[u * Q + q0 + lane];
+    ea = e.x;
+    eb = e.y;
+    if (ea != NONE) {
+      vai = progs[q0 + lane].leaf_view[0];
+      vbi = progs[q0 + lane].leaf_view[1];
+      ma = gp(views[vai].meta)[ea];
+      mb = gp(views[vbi].meta)[eb];
+    }
+  }
+  int mine = 0;
+  uint32_t cached = NONE;
+  int cached_v = -1;
+  const int nq = min(CQ, Q - q0);
+  for (int i = 0; i < nq; i++) {
+    const uint32_t a = __builtin_amdgcn_readlane(ea, i);
+    if (a == NONE) continue;
+    const int va = __builtin_amdgcn_readlane(vai, i);
+    const int vb = __builtin_amdgcn_readlane(vbi, i);
+    const int64_t mA = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(ma >> 32), i))) << 32) |
+                               uint32_t(__builtin_amdgcn_readlane(int(ma), i)));
+    const int64_t mB = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(mb >> 32), i))) << 32) |
+                               uint32_t(__builtin_amdgcn_readlane(int(mb), i)));
+    const uint16_t* pA = payload_of(views[va], mA);
+    const uint16_t* pB = payload_of(views[vb], mB);
+    const int tA = meta_type(mA), tB = meta_type(mB);
+    int c;
+    if (a == cached && va == cached_v) {
+      c = count_vs_lds(lb, pB, mB);
+    } else {
+      const bool next_same = i + 1 < nq && __builtin_amdgcn_readlane(ea, i + 1) == a &&
+                             __builtin_amdgcn_readlane(vai, i + 1) == va;
+      if (!next_same && tA != CT_RUN && tB != CT_RUN && (tA == CT_BITMAP || tB == CT_BITMAP)) {
+        // one-off pair with a bitmap side: no staging, work straight from L2
+        if (tA == CT_BITMAP && tB == CT_BITMAP)
+          c = and_bitmaps(gp(reinterpret_cast<const ulong2*>(pA)), reinterpret_cast<const uint64_t*>(pB));
+        else if (tA == CT_BITMAP)
+          c = probe(gp(reinterpret_cast<const uint64_t*>(pA)), pB, meta_n(mB));
+        else
+          c = probe(gp(reinterpret_cast<const uint64_t*>(pB)), pA, meta_n(mA));
+      } else {
+        lds_wait();  // previous readers of lb are done before it is rewritten
+        stage(lb, pA, mA);
+        cached = a;
+        cached_v = va;
+        c = count_vs_lds(lb, pB, mB);
+      }
+    }
+    c = wave_sum(c);
+    if (lane == i) mine = c;
+  }
+  if (lane < nq) partial[u * Q + q0 + lane] = mine;
+}
+
+}  // namespace
+
+void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
+                       int cq, hipStream_t st) {
+  const int64_t items = int64_t(Q) * S;
+  if (items == 0) return;
+  hipLaunchKernelGGL(pair_build_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, progs, Q, views, S,
+                     pairs);
+  const int64_t units = int64_t(S) * 16;
+#define PK_LAUNCH(CQV)                                                                                        \
+  {                                                                                                           \
+    const int64_t waves = units * ((Q + CQV - 1) / CQV);                                                      \
+    hipLaunchKernelGGL(and2_pairs_kernel<CQV>, dim3(unsigned((waves + PAIR_WAVES - 1) / PAIR_WAVES)),         \
+                       dim3(64 * PAIR_WAVES), 0, st, progs, Q, views, S, pairs, partial);                     \
+  }
+  switch (cq) {
+    case 4: PK_LAUNCH(4) break;
+    case 16: PK_LAUNCH(16) break;
+    case 32: PK_LAUNCH(32) break;
+    default: PK_LAUNCH(8) break;
+  }
+#undef PK_LAUNCH
+}
+
+}  // namespace pk

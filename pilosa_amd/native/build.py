@@ -55,12 +55,12 @@ def build_pql(force: bool = False, verbose: bool = False) -> str:
     import pybind11
 
     out = os.path.join(PKG, "_pql" + _ext_suffix())
-    src = os.path.join(HERE, "pql_parser.cpp")
-    if not force and not _newer(out, [src]):
+    srcs = [os.path.join(HERE, "pql_parser.cpp"), os.path.join(HERE, "pql_compile.cpp")]
+    if not force and not _newer(out, srcs):
         return out
     cxx = os.environ.get("CXX", "g++")
     cmd = [cxx, "-std=c++17", "-O2", "-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
-           "-I", sysconfig.get_paths()["include"], src, "-o", out + ".tmp"]
+           "-I", sysconfig.get_paths()["include"], *srcs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
@@ -86,7 +86,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     tinc = cpp_extension.include_paths()
     tlib = cpp_extension.library_paths()
     arch = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-    srcs = [os.path.join(KDIR, "bitmap_kernels.hip"), os.path.join(KDIR, "binding.cpp")]
+    srcs = sorted(os.path.join(KDIR, f) for f in os.listdir(KDIR) if f.endswith((".hip", ".cpp")))
     objs = []
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",

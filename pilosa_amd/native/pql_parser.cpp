@@ -629,8 +629,11 @@ class Parser {
 
 }  // namespace
 
+void register_compile(py::module_& m);  // pql_compile.cpp
+
 PYBIND11_MODULE(_pql, m) {
   m.doc() = "Native PQL parser (grammar: reference pql/pql.peg)";
   m.def("parse_calls", [](const std::string& s) { return Parser(s).parse(); },
         "Parse PQL text into a list of pilosa_amd.pql.ast.Call objects");
+  register_compile(m);
 }

@@ -12,6 +12,7 @@ of one view).  ``Expr`` trees are compiled here.
 """
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -21,6 +22,8 @@ import numpy as np
 MAXLEAF = 16
 MAXPROG = 32
 OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 32, 33, 34, 35
+# count-batch kernel routes
+KIND_AND2, KIND_ROW, KIND_GENERIC = 0, 1, 2
 _OPS = {"and": OP_AND, "or": OP_OR, "xor": OP_XOR, "andnot": OP_ANDNOT}
 
 QPROG_DTYPE = np.dtype([("nleaf", "<i4"), ("nprog", "<i4"), ("leaf_view", "<i4", (MAXLEAF,)),
@@ -113,6 +116,22 @@ def compile_expr(expr, view_index: Dict[int, int]):
     if len(prog) > MAXPROG or depth[1] > 4:
         raise CompileError("program too large")
     return leaf_views, leaf_rows, prog
+
+
+def _canonical_and2(progs: np.ndarray) -> np.ndarray:
+    """Intersect(Row(a), Row(a)) compiles to one leaf with prog [0, 0, AND];
+    give it a second (identical) leaf so it takes the pair-kernel route."""
+    pg = progs["prog"]
+    m = (progs["nprog"] == 3) & (progs["nleaf"] == 1) & (pg[:, 0] == 0) & (pg[:, 1] == 0) & (pg[:, 2] == OP_AND)
+    if not m.any():
+        return progs
+    progs = progs.copy()
+    idx = np.nonzero(m)[0]
+    progs["nleaf"][idx] = 2
+    progs["leaf_row"][idx, 1] = progs["leaf_row"][idx, 0]
+    progs["leaf_view"][idx, 1] = progs["leaf_view"][idx, 0]
+    progs["prog"][idx, 1] = 1
+    return progs
 
 
 def pack_programs(compiled) -> np.ndarray:
@@ -211,6 +230,9 @@ class GpuEngine:
         self.device = torch.device(device)
         self.ext = kernels()
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        # Count(Intersect(a,b)) route: key-major pair kernels (pair_kernels.hip)
+        self.use_and2 = os.environ.get("PILOSA_AND2", "1") != "0"
+        self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "8"))
 
     def _views_tensor(self, views: List["DeviceView"]):
         arr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
@@ -246,21 +268,40 @@ class GpuEngine:
         return progs, ordered, S or 0
 
     def _h2d(self, arr: np.ndarray):
-        """Host->device upload on the engine's copy stream, so a batch can be
-        staged while the compute stream is still busy with the previous one
-        (a pageable copy on the compute stream would wait for its kernels)."""
+        return self._h2d_many([arr])[0]
+
+    def _h2d_many(self, arrs: Sequence[np.ndarray]):
+        """Upload several host arrays with ONE copy from pinned memory on the
+        engine's copy stream; returns uint8 device views (256B-aligned).
+
+        Pinned staging matters: a pageable hipMemcpyAsync is serviced only
+        after the device drains, which serialised batch i+1's upload behind
+        batch i's kernel.  The caching host allocator keeps the staging block
+        alive until the copy-stream event fires."""
         torch = self.torch
-        t = torch.from_numpy(arr)
+        offs, total = [], 0
+        for a in arrs:
+            offs.append(total)
+            total += (a.nbytes + 255) & ~255
+        total = max(total, 256)
         if self.copy_stream is None:
-            return t.to(self.device, non_blocking=True)
-        with torch.cuda.stream(self.copy_stream):
-            d = t.to(self.device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(self.copy_stream)
-        cur = torch.cuda.current_stream(self.device)
-        cur.wait_event(ev)
-        d.record_stream(cur)
-        return d
+            host = np.zeros(total, np.uint8)
+            for a, o in zip(arrs, offs):
+                host[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+            d = torch.from_numpy(host).to(self.device)
+        else:
+            pt = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+            host = pt.numpy()
+            for a, o in zip(arrs, offs):
+                host[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+            with torch.cuda.stream(self.copy_stream):
+                d = pt.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            d.record_stream(cur)
+        return [d[o:o + a.nbytes] for a, o in zip(arrs, offs)]
 
     def upload_batch(self, progs: np.ndarray, views: List[DeviceView]):
         tp = self._h2d(progs.view(np.uint8))
@@ -280,36 +321,85 @@ class GpuEngine:
         Queries are reordered by their leaf rows so that consecutive work items
         (same shard, neighbouring queries) touch the same hot containers and
         hit in the XCD's L2; results are scattered back to submission order."""
-        torch = self.torch
         progs, views, S = self.compile_batch(exprs)
-        Q = len(exprs)
+        return self.prepare_progs(progs, views, S, sort)
+
+    def prepare_progs(self, progs: np.ndarray, views: List["DeviceView"], S: int, sort: bool = True):
+        """:meth:`prepare_count` for already compiled QPROG_DTYPE records
+        (e.g. from the native PQL compiler, pilosa_amd/native/pql_compile.cpp)."""
+        torch = self.torch
+        Q = len(progs)
         if not S or not Q:
             return (Q, S, None, [])
+        progs = _canonical_and2(progs)
         np_ = progs["nprog"]
         pg = progs["prog"]
         lr = progs["leaf_row"]
-        fast = (np_ == 1) | ((np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND))
-        tv = self._views_tensor(views)
-        parts = []
-        for sel, is_fast in ((np.nonzero(fast)[0], True), (np.nonzero(~fast)[0], False)):
+        is_row = np_ == 1
+        is_and2 = (np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND)
+        if not self.use_and2 or max(v.container_count for v in views) >= 0xFFFFFFFF:
+            is_row = is_row | is_and2
+            is_and2 = np.zeros_like(is_and2)
+        kind = np.where(is_and2, KIND_AND2, np.where(is_row, KIND_ROW, KIND_GENERIC))
+        if is_and2.any():
+            progs = self._hot_leaf_first(progs, is_and2)
+            lr = progs["leaf_row"]
+        varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
+        for i, v in enumerate(views):
+            varr[i] = v.viewdev()
+        host = [varr.view(np.uint8)]
+        meta = []
+        for k in (KIND_AND2, KIND_ROW, KIND_GENERIC):
+            sel = np.nonzero(kind == k)[0]
             if len(sel) == 0:
                 continue
             if sort and len(sel) > 1:
                 sel = sel[np.lexsort((lr[sel, 1], lr[sel, 0]))]
-            sub = np.ascontiguousarray(progs[sel])
-            tp = self._h2d(sub.view(np.uint8))
-            ti = self._h2d(sel.astype(np.int64))
-            parts.append((tp, ti, is_fast, len(sel)))
+            host.append(np.ascontiguousarray(progs[sel]).view(np.uint8))
+            host.append(sel.astype(np.int64))
+            meta.append((k, len(sel)))
+        dev = self._h2d_many(host)
+        tv = dev[0]
+        parts = [(dev[1 + 2 * i], dev[2 + 2 * i].view(torch.int64), k, n) for i, (k, n) in enumerate(meta)]
         return (Q, S, tv, parts)
+
+    @staticmethod
+    def _hot_leaf_first(progs: np.ndarray, sel: np.ndarray) -> np.ndarray:
+        """For Count(Intersect(a, b)) put the row used most often in the batch
+        in leaf 0: the pair kernel stages leaf 0 once per run of equal rows."""
+        lr = progs["leaf_row"]
+        lv = progs["leaf_view"]
+        idx = np.nonzero(sel)[0]
+        keys = np.concatenate([lv[idx, 0].astype(np.int64) << 40 | lr[idx, 0], lv[idx, 1].astype(np.int64) << 40 | lr[idx, 1]])
+        uniq, inv, cnt = np.unique(keys, return_inverse=True, return_counts=True)
+        ca, cb = cnt[inv[:len(idx)]], cnt[inv[len(idx):]]
+        swap = idx[(cb > ca) | ((cb == ca) & (keys[len(idx):] < keys[:len(idx)]))]
+        if len(swap):
+            progs = progs.copy()
+            for f in ("leaf_row", "leaf_view"):
+                col = progs[f]
+                col[swap, 0], col[swap, 1] = col[swap, 1].copy(), col[swap, 0].copy()
+        return progs
+
+    def _and2_partial(self, tp, tv, S: int, n: int):
+        """Per-(shard, key, query) Count(Intersect) partials -> int32[S, 16, n]."""
+        torch = self.torch
+        pairs = torch.empty(S * 16 * n * 2, dtype=torch.int32, device=self.device)
+        partial = torch.empty(S * 16 * n, dtype=torch.int32, device=self.device)
+        self.ext.and2_count(tp, tv, S, pairs, partial, self.and2_cq)
+        return partial.view(S, 16, n)
 
     def launch_count(self, handle):
         """Device half: launch the kernels; returns the device int64[Q] result."""
         torch = self.torch
         Q, S, tv, parts = handle
         out = torch.zeros(Q, dtype=torch.int64, device=self.device)
-        for tp, ti, is_fast, n in parts:
-            o = torch.zeros(n, dtype=torch.int64, device=self.device)
-            self.ext.expr_count(tp, tv, S, o, None, is_fast)
+        for tp, ti, kind, n in parts:
+            if kind == KIND_AND2:
+                o = self._and2_partial(tp, tv, S, n).sum(dim=(0, 1), dtype=torch.int64)
+            else:
+                o = torch.zeros(n, dtype=torch.int64, device=self.device)
+                self.ext.expr_count(tp, tv, S, o, None, kind == KIND_ROW)
             out.index_copy_(0, ti, o)
         return out
 
@@ -320,6 +410,14 @@ class GpuEngine:
         Q = len(exprs)
         if not S or not Q:
             return np.zeros((Q, S), dtype=np.int64)
+        np_, pg = progs["nprog"], progs["prog"]
+        if self.use_and2 and bool(np.all((np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND))):
+            varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
+            for i, v in enumerate(views):
+                varr[i] = v.viewdev()
+            tv, tp = self._h2d_many([varr.view(np.uint8), progs.view(np.uint8)])
+            part = self._and2_partial(tp, tv, S, Q).sum(dim=1, dtype=torch.int64)
+            return part.t().contiguous().cpu().numpy()
         tv = self._views_tensor(views)
         tp = self._h2d(progs.view(np.uint8))
         ps = torch.zeros(Q * S, dtype=torch.int64, device=self.device)

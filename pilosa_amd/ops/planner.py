@@ -74,3 +74,58 @@ _SETOPS = {"Intersect": "and", "Union": "or", "Difference": "andnot", "Xor": "xo
 class BenchPlanner(GpuPlanner):
     def __init__(self, views: Dict[str, object]):
         super().__init__(lambda f, v: views[f])
+
+
+class NativeCountCompiler:
+    """Batch compiler for ``Count(<bitmap tree>)`` PQL text over a fixed
+    ``{field: DeviceView}`` map.
+
+    The common shapes (Row(field=id) leaves under Intersect/Union/Difference/
+    Xor) are compiled by the native scanner in pilosa_amd/native/pql_compile.cpp
+    straight to QueryProg records (~0.3 us/query); anything else goes through
+    the general parser + :class:`GpuPlanner` + ``compile_expr`` with the same
+    view slots, so results never depend on which path compiled a query.
+    """
+
+    def __init__(self, views: Dict[str, object], exists_view=None):
+        from pilosa_amd import _pql
+
+        self._pql = _pql
+        self.fields = {f: i for i, f in enumerate(views)}
+        self.views = list(views.values())
+        self.dirs = [v.rows for v in self.views]
+        self.planner = GpuPlanner(lambda f, v: views[f], exists_view)
+        self.native_hits = 0
+        self.fallbacks = 0
+
+    def compile(self, queries):
+        """-> (progs QPROG_DTYPE[Q], views, S)."""
+        import numpy as np
+
+        from pilosa_amd.pql import parse_string
+
+        from .device import QPROG_DTYPE, CompileError, compile_expr, pack_programs
+
+        raw, ok = self._pql.compile_counts(list(queries), self.fields, self.dirs)
+        progs = raw.view(QPROG_DTYPE)
+        views = list(self.views)
+        bad = np.nonzero(~ok)[0]
+        self.native_hits += len(queries) - len(bad)
+        if len(bad):
+            self.fallbacks += len(bad)
+            view_index = {id(v): i for i, v in enumerate(views)}
+            comp = []
+            for i in bad:
+                calls = parse_string(queries[i]).calls
+                if len(calls) != 1 or calls[0].name != "Count":
+                    raise Unsupported("not a single Count query")
+                try:
+                    comp.append(compile_expr(self.planner.plan(calls[0]), view_index))
+                except CompileError as e:
+                    raise Unsupported(str(e)) from e
+            progs[bad] = pack_programs(comp)
+            if len(view_index) > len(views):
+                extra = sorted((slot, vid) for vid, slot in view_index.items() if slot >= len(views))
+                raise Unsupported(f"query referenced {len(extra)} view(s) outside the compiler's map")
+        S = views[0].S if views else 0
+        return progs, views, S
