@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="queries per step")
+    ap.add_argument("--batch", type=int, default=4096, help="queries per step (concurrent queries per batch)")
     ap.add_argument("--cols", type=int, default=TOTAL_COLS)
     ap.add_argument("--rows", type=int, default=NROWS)
     ap.add_argument("--threads", type=int, default=16)

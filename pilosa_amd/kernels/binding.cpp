@@ -89,7 +89,7 @@ void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor 
 }
 
 void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor pairs, torch::Tensor partial,
-                int64_t cq) {
+                int64_t cq, int64_t variant) {
   check_dev(progs, "progs");
   check_dev(views, "views");
   check_dev(pairs, "pairs");
@@ -101,7 +101,7 @@ void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   pk::launch_and2_pairs(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
                         reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
                         reinterpret_cast<uint2*>(pairs.data_ptr()), partial.data_ptr<int32_t>(), int(cq),
-                        cur_stream(progs));
+                        int(variant), cur_stream(progs));
 }
 
 }  // namespace
@@ -117,6 +117,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
   m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),
-        py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 8);
+        py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 0,
+        py::arg("variant") = 1);
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
 }

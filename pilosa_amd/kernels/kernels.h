@@ -55,7 +55,7 @@ void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views
 // Count(Intersect(a, b)) via key-major pair kernels (pair_kernels.hip):
 // pairs = uint2[S*16*Q] scratch, partial = int32[S*16*Q] per-(shard,key,query) counts.
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
-                       int cq, hipStream_t st);
+                       int cq, int variant, hipStream_t st);
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
                     unsigned long long* out_sum, unsigned long long* out_cnt, hipStream_t st);
 

@@ -145,10 +145,11 @@ __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m
     for (int e8 = lane; e8 < n8; e8 += 64) {
       const uint4 v4 = p4[e8];
       const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+      const int rem = n - e8 * 8;
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
-        if (e8 * 8 + k < n) atomicOr(reinterpret_cast<unsigned long long*>(&lb[v >> 6]), 1ull << (v & 63));
+        atomicOr(reinterpret_cast<uint32_t*>(lb) + (v >> 5), k < rem ? (1u << (v & 31)) : 0u);
       }
     }
   } else {
@@ -181,10 +182,11 @@ __device__ __forceinline__ int probe(BM bm, const uint16_t* arr, int n) {
   for (int e8 = lane; e8 < n8; e8 += 64) {
     const uint4 v4 = p4[e8];
     const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+    const int rem = n - e8 * 8;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
-      c += (e8 * 8 + k < n) ? int((bm[v >> 6] >> (v & 63)) & 1) : 0;
+      c += k < rem ? int((bm[v >> 5] >> (v & 31)) & 1) : 0;
     }
   }
   return c;
@@ -228,7 +230,7 @@ __device__ __forceinline__ int runs_in_lds(const uint64_t* lb, const uint16_t* p
 __device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* p, int64_t m) {
   const int type = meta_type(m);
   if (type == CT_BITMAP) return and_bitmaps(reinterpret_cast<const ulong2*>(lb), reinterpret_cast<const uint64_t*>(p));
-  if (type == CT_ARRAY) return probe(lb, p, meta_n(m));
+  if (type == CT_ARRAY) return probe(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
   return runs_in_lds(lb, p);
 }
 
@@ -289,9 +291,9 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
         if (tA == CT_BITMAP && tB == CT_BITMAP)
           c = and_bitmaps(gp(reinterpret_cast<const ulong2*>(pA)), reinterpret_cast<const uint64_t*>(pB));
         else if (tA == CT_BITMAP)
-          c = probe(gp(reinterpret_cast<const uint64_t*>(pA)), pB, meta_n(mB));
+          c = probe(gp(reinterpret_cast<const uint32_t*>(pA)), pB, meta_n(mB));
         else
-          c = probe(gp(reinterpret_cast<const uint64_t*>(pB)), pA, meta_n(mA));
+          c = probe(gp(reinterpret_cast<const uint32_t*>(pB)), pA, meta_n(mA));
       } else {
         lds_wait();  // previous readers of lb are done before it is rewritten
         stage(lb, pA, mA);
@@ -306,26 +308,241 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
   if (lane < nq) partial[u * Q + q0 + lane] = mine;
 }
 
+
+// ---- v2: register-resident operands, software-pipelined over the chunk.
+//
+// v1 is latency-bound (PMC: SQ_WAIT_ANY ~63 % of wave cycles, ~1 VMEM load in
+// flight per wave): every pair waited for A's payload, then for B's.  v2
+// loads any container payload as exactly 8 lane-strided 16 B chunks (bitmap:
+// the whole 8 KiB; array: n <= 4096 values = <= 512 chunks, index clamped so
+// nothing is read past the container), issues query i+1's B while query i is
+// staged and counted, and issues A before B so one vmcnt wait covers A while
+// B(i+1) stays in flight.  Bitmap&bitmap pairs never touch LDS.
+
+struct R8 {
+  uint4 r[8];
+};
+
+__device__ __forceinline__ int chunks_of(int64_t m) {
+  const int t = meta_type(m);
+  return t == CT_BITMAP ? 512 : (t == CT_ARRAY ? (meta_n(m) + 7) >> 3 : 1);
+}
+
+__device__ __forceinline__ void issue8(const uint16_t* p, int64_t m, R8& x) {
+  const int lane = lane_id();
+  const auto g = gp(reinterpret_cast<const uint4*>(p));
+  const int nc = chunks_of(m);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (k * 64 < nc) x.r[k] = g[min(k * 64 + lane, nc - 1)];  // wave-uniform skip of absent chunks
+}
+
+// scatter an array held in registers into the (cleared) LDS bitmap.
+// Per-element bounds use rem = n - 8*chunk (one VGPR per chunk) rather than
+// 64 distinct "8*chunk+e < n" compares, which LICM hoisted into 64 live VGPRs;
+// masked elements OR in 0 instead of branching around the atomic.
+__device__ __forceinline__ void scatter_regs(uint64_t* lb, int n, const R8& x) {
+  const int lane = lane_id();
+  uint32_t* l32 = reinterpret_cast<uint32_t*>(lb);
+  const int n8 = (n + 7) >> 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k * 64 >= n8) break;  // wave-uniform
+    const int rem = n - (k * 64 + lane) * 8;
+    const uint32_t w[4] = {x.r[k].x, x.r[k].y, x.r[k].z, x.r[k].w};
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t v = (w[e >> 1] >> ((e & 1) * 16)) & 0xffff;
+      atomicOr(l32 + (v >> 5), e < rem ? (1u << (v & 31)) : 0u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void copy_regs(uint64_t* lb, const R8& x) {
+  const int lane = lane_id();
+  uint4* l4 = reinterpret_cast<uint4*>(lb);
+#pragma unroll
+  for (int k = 0; k < 8; k++) l4[k * 64 + lane] = x.r[k];
+}
+
+__device__ __forceinline__ int probe_regs(const uint64_t* lb, int n, const R8& x) {
+  const int lane = lane_id();
+  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lb);
+  const int n8 = (n + 7) >> 3;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k * 64 >= n8) break;  // wave-uniform
+    const int rem = n - (k * 64 + lane) * 8;
+    const uint32_t w[4] = {x.r[k].x, x.r[k].y, x.r[k].z, x.r[k].w};
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t v = (w[e >> 1] >> ((e & 1) * 16)) & 0xffff;
+      c += e < rem ? int((l32[v >> 5] >> (v & 31)) & 1) : 0;
+    }
+    // keep at most one chunk of LDS reads in flight (VGPR pressure)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return c;
+}
+
+__device__ __forceinline__ int and_regs_lds(const uint64_t* lb, const R8& x) {
+  const int lane = lane_id();
+  const uint4* l4 = reinterpret_cast<const uint4*>(lb);
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint4 y = l4[k * 64 + lane];
+    c += __popc(y.x & x.r[k].x) + __popc(y.y & x.r[k].y) + __popc(y.z & x.r[k].z) + __popc(y.w & x.r[k].w);
+  }
+  return c;
+}
+
+__device__ __forceinline__ int and_regs(const R8& a, const R8& b) {
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    c += __popc(a.r[k].x & b.r[k].x) + __popc(a.r[k].y & b.r[k].y) + __popc(a.r[k].z & b.r[k].z) +
+         __popc(a.r[k].w & b.r[k].w);
+  return c;
+}
+
+// |B ∩ staged-in-LDS| with B in registers (runs read from memory)
+__device__ __forceinline__ int count_b(const uint64_t* lb, const uint16_t* pB, int64_t mB, const R8& b) {
+  const int t = meta_type(mB);
+  if (t == CT_BITMAP) return and_regs_lds(lb, b);
+  if (t == CT_ARRAY) return probe_regs(lb, meta_n(mB), b);
+  return runs_in_lds(lb, pB);
+}
+
+__device__ __forceinline__ int64_t rl64(int64_t v, int i) {
+  return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(v >> 32), i))) << 32) |
+                 uint32_t(__builtin_amdgcn_readlane(int(v), i)));
+}
+
+template <int CQ>
+__global__ __launch_bounds__(64 * PAIR_WAVES, 3) void and2_pairs_v2_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                                       const ViewDev* __restrict__ views, int S,
+                                                                       const uint2* __restrict__ pairs,
+                                                                       int32_t* __restrict__ partial) {
+  __shared__ uint64_t lbs[PAIR_WAVES][1024];
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int64_t gw = int64_t(xcd_remap_blocks(blockIdx.x, gridDim.x)) * PAIR_WAVES + wave;
+  const int nch = (Q + CQ - 1) / CQ;
+  const int64_t u = gw / nch;
+  if (u >= int64_t(S) * 16) return;
+  const int q0 = int(gw % nch) * CQ;
+  uint64_t* lb = lbs[wave];
+
+  uint32_t ea = NONE;
+  int vai = 0, vbi = 0;
+  int64_t ma = 0, mb = 0;
+  if (lane < CQ && q0 + lane < Q) {
+    const uint2 e = pairs[u * Q + q0 + lane];
+    if (e.x != NONE) {
+      ea = e.x;
+      vai = progs[q0 + lane].leaf_view[0];
+      vbi = progs[q0 + lane].leaf_view[1];
+      ma = gp(views[vai].meta)[e.x];
+      mb = gp(views[vbi].meta)[e.y];
+    }
+  }
+  const int nq = min(CQ, Q - q0);
+  int mine = 0;
+  uint32_t cached = NONE;
+  int cached_v = -1;
+  R8 ra, rb, rn;
+  // prologue: B of the first valid query
+  int i = 0;
+  while (i < nq && __builtin_amdgcn_readlane(ea, i) == NONE) i++;
+  if (i < nq) {
+    const int64_t m = rl64(mb, i);
+    issue8(payload_of(views[__builtin_amdgcn_readlane(vbi, i)], m), m, rb);
+  }
+  while (i < nq) {
+    const uint32_t a = __builtin_amdgcn_readlane(ea, i);
+    const int va = __builtin_amdgcn_readlane(vai, i);
+    const int64_t mA = rl64(ma, i), mB = rl64(mb, i);
+    const uint16_t* pA = payload_of(views[va], mA);
+    const uint16_t* pB = payload_of(views[__builtin_amdgcn_readlane(vbi, i)], mB);
+    const int tA = meta_type(mA), tB = meta_type(mB);
+    // next valid query
+    int j = i + 1;
+    while (j < nq && __builtin_amdgcn_readlane(ea, j) == NONE) j++;
+    const bool hit = a == cached && va == cached_v;
+    if (!hit) issue8(pA, mA, ra);  // A first: its wait leaves B(j) in flight
+    if (j < nq) {
+      const int64_t m = rl64(mb, j);
+      issue8(payload_of(views[__builtin_amdgcn_readlane(vbi, j)], m), m, rn);
+    }
+    const bool next_same = j < nq && __builtin_amdgcn_readlane(ea, j) == a && __builtin_amdgcn_readlane(vai, j) == va;
+    // one code site per primitive (inlining each per branch tripled VGPRs)
+    const bool bb = tA == CT_BITMAP && tB == CT_BITMAP;
+    if (!hit) {
+      if (tA == CT_RUN || tB == CT_RUN) {
+        lds_wait();
+        stage(lb, pA, mA);
+      } else if (tA == CT_BITMAP) {
+        if (!bb || next_same) copy_regs(lb, ra);
+      } else {
+        lds_clear(lb);
+        scatter_regs(lb, meta_n(mA), ra);
+      }
+      if (!bb || next_same) {
+        cached = a;
+        cached_v = va;
+      }
+    }
+    int c;
+    if (!hit && bb) c = and_regs(ra, rb);
+    else c = count_b(lb, pB, mB, rb);
+    c = wave_sum(c);
+    if (lane == i) mine = c;
+    rb = rn;
+    i = j;
+  }
+  if (lane < nq) partial[u * Q + q0 + lane] = mine;
+}
+
 }  // namespace
 
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
-                       int cq, hipStream_t st) {
+                       int cq, int variant, hipStream_t st) {
   const int64_t items = int64_t(Q) * S;
   if (items == 0) return;
   hipLaunchKernelGGL(pair_build_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, progs, Q, views, S,
                      pairs);
   const int64_t units = int64_t(S) * 16;
-#define PK_LAUNCH(CQV)                                                                                        \
+#define PK_LAUNCH(KERNEL, CQV)                                                                                \
   {                                                                                                           \
     const int64_t waves = units * ((Q + CQV - 1) / CQV);                                                      \
-    hipLaunchKernelGGL(and2_pairs_kernel<CQV>, dim3(unsigned((waves + PAIR_WAVES - 1) / PAIR_WAVES)),         \
+    hipLaunchKernelGGL(KERNEL<CQV>, dim3(unsigned((waves + PAIR_WAVES - 1) / PAIR_WAVES)),                    \
                        dim3(64 * PAIR_WAVES), 0, st, progs, Q, views, S, pairs, partial);                     \
   }
-  switch (cq) {
-    case 4: PK_LAUNCH(4) break;
-    case 16: PK_LAUNCH(16) break;
-    case 32: PK_LAUNCH(32) break;
-    default: PK_LAUNCH(8) break;
+  // variant 1 (default): stage-on-demand kernel; variant 2: register-pipelined
+  // kernel (fewer waits, but 168 VGPRs -> 3 waves/SIMD; slower on the Zipf
+  // benchmark, kept for batches of dense rows).  cq <= 0 picks by batch size:
+  // bigger chunks amortise more leaf-0 stagings (measured: 32 for Q <= 2048,
+  // 64 above).
+  if (cq <= 0) cq = Q <= 2048 ? 32 : 64;
+  if (variant == 2) {
+    switch (cq) {
+      case 4: PK_LAUNCH(and2_pairs_v2_kernel, 4) break;
+      case 8: PK_LAUNCH(and2_pairs_v2_kernel, 8) break;
+      case 16: PK_LAUNCH(and2_pairs_v2_kernel, 16) break;
+      case 32: PK_LAUNCH(and2_pairs_v2_kernel, 32) break;
+      default: PK_LAUNCH(and2_pairs_v2_kernel, 64) break;
+    }
+  } else {
+    switch (cq) {
+      case 4: PK_LAUNCH(and2_pairs_kernel, 4) break;
+      case 8: PK_LAUNCH(and2_pairs_kernel, 8) break;
+      case 16: PK_LAUNCH(and2_pairs_kernel, 16) break;
+      case 32: PK_LAUNCH(and2_pairs_kernel, 32) break;
+      default: PK_LAUNCH(and2_pairs_kernel, 64) break;
+    }
   }
 #undef PK_LAUNCH
 }

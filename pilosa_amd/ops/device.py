@@ -232,7 +232,8 @@ class GpuEngine:
         self.copy_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         # Count(Intersect(a,b)) route: key-major pair kernels (pair_kernels.hip)
         self.use_and2 = os.environ.get("PILOSA_AND2", "1") != "0"
-        self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "8"))
+        self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "0"))  # 0 = by batch size
+        self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "1"))
 
     def _views_tensor(self, views: List["DeviceView"]):
         arr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
@@ -386,7 +387,7 @@ class GpuEngine:
         torch = self.torch
         pairs = torch.empty(S * 16 * n * 2, dtype=torch.int32, device=self.device)
         partial = torch.empty(S * 16 * n, dtype=torch.int32, device=self.device)
-        self.ext.and2_count(tp, tv, S, pairs, partial, self.and2_cq)
+        self.ext.and2_count(tp, tv, S, pairs, partial, self.and2_cq, self.and2_variant)
         return partial.view(S, 16, n)
 
     def launch_count(self, handle):

@@ -126,9 +126,10 @@ def test_and2_pair_kernels_match_tile_kernel(setup):
         exprs.append(Op("and", (Leaf(va, min(a, 5) if va is view2 else a), Leaf(view, b))))
         ra = min(a, 5) if va is view2 else a
         want.append(sum(_row(x, ra).intersection_count(_row(f, b)) for x, f in zip(fa, frags)))
-    for cq in (4, 8, 16, 32):
+    for cq, variant in [(c, v) for v in (1, 2) for c in (0, 4, 8, 16, 32, 64)]:
         e2 = GpuEngine(view.device)
         e2.and2_cq = cq
+        e2.and2_variant = variant
         np.testing.assert_array_equal(e2.count(exprs), np.array(want))
     old = GpuEngine(view.device)
     old.use_and2 = False
