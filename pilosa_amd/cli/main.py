@@ -66,6 +66,13 @@ def cmd_server(args, stdout, stderr) -> int:
     logger = StandardLogger(log_stream, verbose=cfg.get("verbose"))
     if cfg.get("tracing.sampler-type") not in ("", "off", "none"):
         tracing.set_global_tracer(tracing.RecordingTracer())
+    from pilosa_amd.parallel import mesh as M
+    rank, world, _ = M.dist_env()
+    if world > 1 and rank != 0:
+        # one process per GPU (torch.distributed.run): non-front-end ranks own
+        # shard subsets and execute what rank 0 broadcasts (parallel/mesh.py)
+        return M.run_worker(cfg.data_dir(), gpu_mode=cfg.get("gpu.mode"), block=cfg.get("gpu.shard-block"),
+                            logger=logger)
     bind = cfg.get("bind")
     if bind.startswith(":"):
         bind = "0.0.0.0" + bind
@@ -81,7 +88,7 @@ def cmd_server(args, stdout, stderr) -> int:
                  probe_interval=cfg.duration("gossip.probe-interval"),
                  long_query_time=cfg.duration("cluster.long-query-time"), stats=cfg.get("metric.service")
                  if cfg.get("metric.service") != "none" else "expvar", logger=logger,
-                 cluster_disabled=cfg.get("cluster.disabled"))
+                 cluster_disabled=cfg.get("cluster.disabled"), mesh_block=cfg.get("gpu.shard-block"))
     srv.open()
     logger.printf("listening as %s (node %s, gpu=%s)", srv.uri.normalize(), srv.node.id,
                   "on" if srv.gpu is not None else "off")

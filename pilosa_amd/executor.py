@@ -38,16 +38,19 @@ MAX_INT = (1 << 63) - 1
 
 
 class ExecOptions:
-    __slots__ = ("remote", "exclude_row_attrs", "exclude_columns", "column_attrs")
+    __slots__ = ("remote", "exclude_row_attrs", "exclude_columns", "column_attrs", "mesh_local")
 
     def __init__(self, remote=False, exclude_row_attrs=False, exclude_columns=False, column_attrs=False):
         self.remote = remote
         self.exclude_row_attrs = exclude_row_attrs
         self.exclude_columns = exclude_columns
         self.column_attrs = column_attrs
+        self.mesh_local = False  # set on a rank's own share of a multi-GPU call
 
     def copy(self):
-        return ExecOptions(self.remote, self.exclude_row_attrs, self.exclude_columns, self.column_attrs)
+        o = ExecOptions(self.remote, self.exclude_row_attrs, self.exclude_columns, self.column_attrs)
+        o.mesh_local = self.mesh_local
+        return o
 
 
 class ValCount:
@@ -192,6 +195,7 @@ class Executor:
         self.cluster = cluster
         self.client = client
         self.gpu = gpu            # GpuExecutor or None
+        self.mesh = None          # parallel.mesh.ShardMesh on a multi-GPU node (rank 0 front end)
         self.max_writes = max_writes
         self.stats = stats
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, workers), thread_name_prefix="shard")
@@ -245,6 +249,9 @@ class Executor:
         if q.calls and all(c.name == "SetRowAttrs" for c in q.calls):
             return self._bulk_set_row_attrs(index, q.calls, opt)
         # Batch fast path: many Count() calls in one request go to the GPU together.
+        if self._use_mesh(opt) and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
+                not self._has_remote(index, shards, opt):
+            return self.mesh.count_batch(index, q.calls, shards)
         if self.gpu is not None and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
                 not self._has_remote(index, shards, opt):
             res = self.gpu.try_count_batch(index, q.calls, shards)
@@ -346,6 +353,9 @@ class Executor:
         remote_jobs = []
         for node, nshards in by_node.items():
             if node is None or (self.cluster is not None and node.id == self.cluster.node.id):
+                if self._use_mesh(opt):
+                    result = reduce_fn(result, self.mesh.map_local(index, c, nshards, opt, reduce_fn))
+                    continue
                 result = reduce_fn(result, self._map_local(nshards, map_fn, reduce_fn, local_fn))
             elif not opt.remote:
                 remote_jobs.append((node, nshards))
@@ -353,6 +363,9 @@ class Executor:
             result = reduce_fn(result, self._remote_with_failover(index, c, node, nshards, opt, map_fn, reduce_fn,
                                                                   local_fn, {node.id}))
         return result
+
+    def _use_mesh(self, opt) -> bool:
+        return self.mesh is not None and self.mesh.world > 1 and not getattr(opt, "mesh_local", False)
 
     def _shards_by_node(self, index, shards, opt) -> Dict[Any, List[int]]:
         if self.cluster is None or opt.remote:
@@ -919,7 +932,10 @@ class Executor:
         ret = False
         for node in self._shard_owned_locally(index, shard):
             if node is None or node.id == self.cluster.node.id:
-                if local_fn():
+                if self._use_mesh(opt) and self.mesh.owner(shard) != self.mesh.rank:
+                    if self.mesh.forward_write(index, c, shard, opt):
+                        ret = True
+                elif local_fn():
                     ret = True
                 continue
             if opt.remote:

@@ -97,6 +97,7 @@ class API:
             if e is ErrIndexExists:
                 raise ConflictError(e)
             raise BadRequestError(e)
+        self._mesh_schema()
         if not remote:
             self.server.broadcast({"type": "CreateIndex", "index": name,
                                    "options": {"keys": keys, "trackExistence": track_existence}})
@@ -117,6 +118,8 @@ class API:
             raise NotFoundError(e)
         if self.server.gpu is not None:
             self.server.gpu.invalidate()
+        if getattr(self.server, "mesh", None) is not None:
+            self.server.mesh.delete_index(name)
         if not remote:
             self.server.broadcast({"type": "DeleteIndex", "index": name})
 
@@ -131,6 +134,7 @@ class API:
             if e is ErrFieldExists:
                 raise ConflictError(e)
             raise BadRequestError(e)
+        self._mesh_schema()
         if not remote:
             self.server.broadcast({"type": "CreateField", "index": index, "field": name,
                                    "options": f.options.to_json()})
@@ -157,6 +161,8 @@ class API:
             raise NotFoundError(e)
         if self.server.gpu is not None:
             self.server.gpu.invalidate()
+        if getattr(self.server, "mesh", None) is not None:
+            self.server.mesh.delete_field(index, name)
         if not remote:
             self.server.broadcast({"type": "DeleteField", "index": index, "field": name})
 
@@ -192,6 +198,20 @@ class API:
             self.server.broadcast({"type": "ApplySchema", "schema": schema})
 
     # ------------------------------------------------------------ imports
+    def _mesh_schema(self):
+        mesh = getattr(self.server, "mesh", None)
+        if mesh is not None:
+            mesh.apply_schema()
+
+    def _mesh_route(self, index: str, field: str, kind: str, shard: int, payload: dict) -> bool:
+        """Multi-GPU node: hand an import for a shard owned by another rank to
+        that rank (parallel/mesh.py).  Returns True when it was routed."""
+        mesh = getattr(self.server, "mesh", None)
+        if mesh is None or mesh.world <= 1 or mesh.owner(shard) == mesh.rank:
+            return False
+        mesh.forward_import(kind, index, field, shard, payload)
+        return True
+
     def _owns(self, index: str, shard: int):
         if not self.cluster.owns_shard(self.cluster.node.id, index, shard):
             raise ErrClusterDoesNotOwnShard
@@ -236,6 +256,10 @@ class API:
 
     def _local_import(self, idx, f, rows, cols, timestamps, clear):
         import datetime as dt
+        if len(cols) and self._mesh_route(idx.name, f.name, "bits", int(cols[0]) // SHARD_WIDTH,
+                                          {"rows": list(rows), "cols": list(cols), "clear": clear,
+                                           "timestamps": _ts_list(timestamps)}):
+            return
         tss = None
         if timestamps and any(timestamps):
             tss = [dt.datetime.utcfromtimestamp(t / 1e9) if t else None for t in timestamps]
@@ -272,6 +296,9 @@ class API:
         self._local_import_values(idx, f, col_ids, values, clear)
 
     def _local_import_values(self, idx, f, cols, vals, clear):
+        if len(cols) and self._mesh_route(idx.name, f.name, "values", int(cols[0]) // SHARD_WIDTH,
+                                          {"cols": list(cols), "values": list(vals), "clear": clear}):
+            return
         if not clear and idx.existence_field() is not None and len(cols):
             idx.existence_field().import_bits(np.zeros(len(cols), np.uint64), np.asarray(cols, np.uint64))
         f.import_values(cols, vals, clear=clear)
@@ -282,7 +309,8 @@ class API:
         f = self.field(index, field)
         for node in self.cluster.shard_nodes(index, shard):
             if node.id == self.cluster.node.id:
-                f.import_roaring(shard, views, clear)
+                if not self._mesh_route(index, field, "roaring", shard, {"views": dict(views), "clear": clear}):
+                    f.import_roaring(shard, views, clear)
             elif not remote:
                 self.server.client.import_roaring(node, index, field, shard, views, clear=clear, remote=True)
 
@@ -404,3 +432,11 @@ class API:
         self.validate("ResizeAbort")
         if not self.server.abort_resize():
             raise ErrResizeNotRunning
+
+
+def _ts_list(timestamps):
+    """Import timestamps (ns since epoch) -> datetimes, as Field.import_bits takes."""
+    import datetime as dt
+    if not timestamps or not any(timestamps):
+        return None
+    return [dt.datetime.utcfromtimestamp(t / 1e9) if t else None for t in timestamps]

@@ -44,7 +44,7 @@ class Server:
                  coordinator_uri: Optional[str] = None, gpu: str = "auto", workers: int = 8,
                  max_writes: int = 5000, anti_entropy_interval: float = 600.0, probe_interval: float = 1.0,
                  long_query_time: float = 60.0, stats: str = "expvar", logger=None, hasher: str = "jump",
-                 max_opn: int = 10000, cluster_disabled: bool = False):
+                 max_opn: int = 10000, cluster_disabled: bool = False, mesh_block: int = 1):
         self.data_dir = data_dir
         self.bind = bind
         self.logger = logger or StandardLogger()
@@ -63,6 +63,8 @@ class Server:
         self.hasher = ModHasher() if hasher == "mod" else JumpHasher()
         self.gpu = None
         self.gpu_mode = gpu
+        self.mesh = None          # multi-GPU node: parallel.mesh.ShardMesh (this process is rank 0)
+        self.mesh_block = mesh_block
         self.workers = workers
         self.max_writes = max_writes
         self.cluster: Optional[Cluster] = None
@@ -92,6 +94,7 @@ class Server:
                                  workers=self.workers, max_writes=self.max_writes, stats=self.stats)
         if self.gpu is not None:
             self.gpu.executor = self.executor
+        self._init_mesh()
         self.holder.on_create_shard = self._on_create_shard
         self.holder.on_schema_change = lambda: self.gpu.invalidate() if self.gpu is not None else None
         t = threading.Thread(target=self.httpd.serve_forever, name="http", daemon=True)
@@ -110,6 +113,21 @@ class Server:
         self._start_loop(self._runtime_loop, "runtime")
         return self
 
+    def _init_mesh(self):
+        """Under torch.distributed.run with WORLD_SIZE > 1 this process is the
+        front end (rank 0) of a one-process-per-GPU node; the other ranks run
+        parallel.mesh.run_worker."""
+        from pilosa_amd.parallel import mesh as M
+        rank, world, local = M.dist_env()
+        if world <= 1:
+            return
+        if rank != 0:
+            raise RuntimeError("Server must run on rank 0; other ranks run parallel.mesh.run_worker")
+        M.init_process_group(local)
+        self.mesh = M.ShardMesh(self.executor, block=self.mesh_block)
+        self.executor.mesh = self.mesh
+        self.mesh.apply_schema()
+
     def _init_gpu(self):
         mode = (self.gpu_mode or "auto").lower()
         if mode in ("off", "none", "cpu"):
@@ -121,7 +139,8 @@ class Server:
                     raise RuntimeError("gpu=on but no GPU is visible")
                 return
             from pilosa_amd.ops.gpu_executor import GpuExecutor
-            self.gpu = GpuExecutor(self.holder, "cuda:0")
+            from pilosa_amd.parallel.mesh import dist_env
+            self.gpu = GpuExecutor(self.holder, f"cuda:{dist_env()[2]}")
         except ImportError:
             if mode == "on":
                 raise
@@ -136,6 +155,8 @@ class Server:
 
     def close(self):
         self._closing.set()
+        if self.mesh is not None:
+            self.mesh.stop()
         if self.httpd is not None:
             self.httpd.shutdown()
             self.httpd.server_close()

@@ -1,0 +1,159 @@
+"""Multi-rank shard mesh (pilosa_amd/parallel/mesh.py) over gloo on the CPU.
+
+Every rank owns a block-cyclic subset of shards in its own holder; rank 0 is
+the front end.  Results of a query workload must equal a single-process
+executor holding all shards (the reference's multi-node tests assert the same
+for HTTP fan-out: executor_test.go TestExecutor_Execute_Remote*)."""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+SW = 1 << 20
+
+QUERIES = [
+    "Count(Row(f=1))",
+    "Count(Intersect(Row(f=1), Row(f=2)))",
+    "Count(Union(Row(f=1), Row(g=3)))",
+    "Row(f=2)",
+    "Difference(Row(f=1), Row(f=2))",
+    "Not(Row(f=3))",
+    "TopN(f, n=3)",
+    "TopN(f, Row(g=3), n=2)",
+    "Sum(field=v)",
+    "Sum(Row(f=1), field=v)",
+    "Min(field=v)",
+    "Max(Row(f=2), field=v)",
+    "MinRow(field=f)",
+    "MaxRow(field=f)",
+    "Rows(f)",
+    "Rows(f, limit=2)",
+    "GroupBy(Rows(f), Rows(g))",
+    "GroupBy(Rows(f), limit=3)",
+    "Row(v > 10)",
+    "Count(Row(v >< [5, 50]))",
+    "Count(Row(f=1))Count(Row(f=2))Count(Intersect(Row(f=1), Row(g=3)))",
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _data():
+    rng = np.random.default_rng(5)
+    bits = []
+    for _ in range(3000):
+        col = int(rng.integers(0, 6 * SW))
+        bits.append(("f", int(rng.integers(0, 5)), col))
+        if rng.random() < 0.5:
+            bits.append(("g", int(rng.integers(0, 4)), col))
+    vals = [(int(rng.integers(0, 6 * SW)), int(rng.integers(-20, 100))) for _ in range(500)]
+    return bits, vals
+
+
+def _setup_schema(holder):
+    from pilosa_amd.models.field import FieldOptions
+    idx = holder.create_index("i")
+    idx.create_field("f", FieldOptions(cache_type="ranked", cache_size=1000))
+    idx.create_field("g")
+    idx.create_field("v", FieldOptions(type="int", min=-100, max=1000))
+
+
+def _load(ex, bits, vals, mesh=None):
+    """Writes: single Set() calls through the executor plus bulk imports
+    (routed to owner ranks when a mesh is present)."""
+    for fld, row, col in bits[:200]:
+        ex.execute("i", f"Set({col}, {fld}={row})")
+    rest = bits[200:]
+    for fld in ("f", "g"):
+        by_shard = {}
+        for ff, row, col in rest:
+            if ff == fld:
+                by_shard.setdefault(col // SW, []).append((row, col))
+        for shard, rc in sorted(by_shard.items()):
+            rows = [r for r, _ in rc]
+            cols = [c for _, c in rc]
+            if mesh is not None and mesh.owner(shard) != 0:
+                mesh.forward_import("bits", "i", fld, shard, {"rows": rows, "cols": cols})
+            else:
+                idx = ex.holder.index("i")
+                idx.existence_field().import_bits(np.zeros(len(cols), np.uint64), np.asarray(cols, np.uint64))
+                idx.field(fld).import_bits(rows, cols)
+    for col, v in vals:
+        ex.execute("i", f"Set({col}, v={v})")
+
+
+def _canon(results):
+    from pilosa_amd.server.encoding import result_to_json
+    return json.dumps([result_to_json(r) for r in results], sort_keys=True, default=str)
+
+
+def _worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = tempfile.mkdtemp(prefix=f"mesh{rank}_")
+    holder = Holder(d).open()
+    ex = Executor(holder)
+    mesh = ShardMesh(ex, block=1)
+    ex.mesh = mesh
+    try:
+        if rank != 0:
+            mesh.serve()
+            return
+        _setup_schema(holder)
+        mesh.apply_schema()
+        bits, vals = _data()
+        _load(ex, bits, vals, mesh)
+        got = [_canon(ex.execute("i", q).results) for q in QUERIES]
+        per_rank = mesh.shard_counts()
+        with open(os.path.join(outdir, "mesh.json"), "w") as fh:
+            json.dump({"got": got, "ops": mesh.ops, "per_rank": {str(k): v for k, v in per_rank.items()}}, fh)
+        mesh.stop()
+    finally:
+        ex.close()
+        holder.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mesh_matches_single_process(world, tmp_path):
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    res = json.load(open(tmp_path / "mesh.json"))
+
+    d = tempfile.mkdtemp(prefix="mesh_ref_")
+    holder = Holder(d).open()
+    ex = Executor(holder)
+    _setup_schema(holder)
+    bits, vals = _data()
+    _load(ex, bits, vals)
+    want = [_canon(ex.execute("i", q).results) for q in QUERIES]
+    ex.close()
+    holder.close()
+    for q, g, w in zip(QUERIES, res["got"], want):
+        assert g == w, q
+    # every rank held a share of the 6 shards; rank 0 stored only its own
+    per_rank = res["per_rank"]
+    owned = [set(per_rank[str(r)]["i"]) for r in range(world)]
+    assert set().union(*owned) == set(range(6))
+    for r in range(world):
+        assert all(s % world == r for s in owned[r]), (r, owned[r])
