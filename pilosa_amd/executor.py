@@ -681,7 +681,13 @@ class Executor:
             red = lambda p, v: (p or ValCount()).smaller(v or ValCount())  # noqa: E731
         else:
             red = lambda p, v: (p or ValCount()).larger(v or ValCount())  # noqa: E731
-        r = self.map_reduce(index, shards, c, opt, map_fn, red) or ValCount()
+
+        def local(ss):
+            r = None
+            for vc in self.gpu.bsi_minmax(index, c, ss, which):
+                r = red(r, vc)
+            return r
+        r = self.map_reduce(index, shards, c, opt, map_fn, red, local if self.gpu is not None else None) or ValCount()
         return r if r.count else ValCount()
 
     def _minmax_row(self, index: str, c: Call, shards, opt, is_min: bool) -> Pair:

@@ -65,6 +65,44 @@ void expr_materialize(torch::Tensor progs, torch::Tensor views, int64_t S, torch
                               reinterpret_cast<uint16_t*>(outp.data_ptr<int16_t>()), cur_stream(progs));
 }
 
+pk::BsiArgs bsi_args_from(const torch::Tensor& bsi_args) {
+  TORCH_CHECK(!bsi_args.is_cuda() && bsi_args.scalar_type() == torch::kInt64 && bsi_args.numel() == 67,
+              "bsi_args must be a cpu int64[67]: view, depth, exists, sign, bit_row[63]");
+  auto a = bsi_args.data_ptr<int64_t>();
+  pk::BsiArgs b{};
+  b.view = int32_t(a[0]);
+  b.depth = int32_t(a[1]);
+  TORCH_CHECK(b.depth >= 0 && b.depth <= 63, "bsi depth");
+  b.row_exists = a[2];
+  b.row_sign = a[3];
+  for (int i = 0; i < 64; i++) b.bit_row[i] = i < 63 ? a[4 + i] : -1;
+  return b;
+}
+
+void bsi_range(torch::Tensor views, int64_t S, torch::Tensor bsi_args, int64_t op, int64_t p1, int64_t p2,
+               torch::Tensor out_payload, torch::Tensor out_meta) {
+  check_dev(views, "views");
+  check_dev(out_payload, "out_payload");
+  check_dev(out_meta, "out_meta");
+  TORCH_CHECK(op >= 0 && op <= 7, "bsi op");
+  TORCH_CHECK(out_payload.numel() >= S * 16 * 4096 && out_meta.numel() >= S * 16, "bsi_range outputs too small");
+  TORCH_CHECK(out_meta.scalar_type() == torch::kInt64, "out_meta must be int64");
+  pk::launch_bsi_range(reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), bsi_args_from(bsi_args),
+                       int(op), p1, p2, reinterpret_cast<uint16_t*>(out_payload.data_ptr<int16_t>()),
+                       out_meta.data_ptr<int64_t>(), cur_stream(views));
+}
+
+void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out) {
+  check_dev(progs, "progs");
+  check_dev(views, "views");
+  check_dev(out, "out");
+  TORCH_CHECK(progs.numel() >= int64_t(sizeof(pk::QueryProg)), "one filter program required");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() >= S * 16 * 10, "out must be int64[S*16*10]");
+  pk::launch_bsi_minmax(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()),
+                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
+                        bsi_args_from(bsi_args), out.data_ptr<int64_t>(), cur_stream(views));
+}
+
 void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out_sum,
              torch::Tensor out_cnt) {
   check_dev(progs, "progs");
@@ -119,5 +157,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 0,
         py::arg("variant") = 1);
+  m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
+  m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
 }

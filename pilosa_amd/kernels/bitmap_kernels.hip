@@ -510,6 +510,328 @@ __global__ __launch_bounds__(256) void bsi_sum_kernel(const QueryProg* __restric
   }
 }
 
+// ---------------------------------------------------------------- BSI range
+// Bit-sliced comparators (O'Neil), reference fragment.go:1271-1534, with the
+// exact control flow of pilosa_amd/models/fragment.py (_range_eq/_lt/_gt/
+// _between).  One wave per (shard, key): the predicate result of that
+// container is built in registers from the exists/sign/bit-slice tiles and
+// written as a bitmap container of a temporary device view, which ordinary
+// expression programs then consume as a leaf (Count(Intersect(Row(f=1),
+// Row(v > 10))) = one range launch + one count launch).
+
+struct BsiCtx {
+  const BsiArgs& bsi;
+  const ViewDev& bv;
+  int s;
+  int j;
+  int64_t base;
+  const uint32_t* rp;
+  uint64_t* lb;
+};
+
+// container index of dense row d at key j in shard s (wave-uniform, -1 absent)
+__device__ __forceinline__ int64_t bsi_find(const BsiCtx& c, int64_t d) {
+  if (d < 0) return -1;
+  const int lane = wave_lane();
+  const int64_t lo = c.rp[d], hi = c.rp[d + 1];
+  int64_t found = -1;
+  if (lane < hi - lo && meta_j(c.bv.meta[c.base + lo + lane]) == c.j) found = c.base + lo + lane;
+  const uint64_t b = __ballot(found >= 0);
+  if (!b) return -1;
+  return __shfl(found, __builtin_ctzll(b), 64);
+}
+
+__device__ __forceinline__ void bsi_row(const BsiCtx& c, int64_t d, Tile& t) {
+  const int64_t ci = bsi_find(c, d);
+  if (ci < 0) tile_zero(t);
+  else tile_load(t, c.bv.payload, c.bv.meta[ci], c.lb);
+}
+
+__device__ __forceinline__ void bsi_bit(const BsiCtx& c, int i, Tile& t) {
+  bsi_row(c, i < 64 ? c.bsi.bit_row[i] : -1, t);
+}
+
+// filt = filt & ~(filt & ~r & ~keep)   (reference: filt.Difference(filt.Difference(row).Difference(keep)))
+__device__ __forceinline__ void keep_set_bits(Tile& f, const Tile& r, const Tile& k) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    f.w[i].x &= ~(f.w[i].x & ~r.w[i].x & ~k.w[i].x);
+    f.w[i].y &= ~(f.w[i].y & ~r.w[i].y & ~k.w[i].y);
+  }
+}
+
+// filt = filt & ~(r & ~keep)
+__device__ __forceinline__ void drop_set_bits(Tile& f, const Tile& r, const Tile& k) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    f.w[i].x &= ~(r.w[i].x & ~k.w[i].x);
+    f.w[i].y &= ~(r.w[i].y & ~k.w[i].y);
+  }
+}
+
+__device__ void bsi_lt_unsigned(const BsiCtx& c, Tile& filt, int depth, uint64_t pred, bool allow_eq) {
+  Tile keep, r;
+  tile_zero(keep);
+  bool leading = true;
+  for (int i = depth - 1; i >= 0; i--) {
+    bsi_bit(c, i, r);
+    const int bit = int((pred >> i) & 1);
+    if (leading) {
+      if (bit == 0) {
+        tile_op<OP_ANDNOT>(filt, r);
+        continue;
+      }
+      leading = false;
+    }
+    if (i == 0 && !allow_eq) {
+      if (bit == 0) {
+        filt = keep;
+        return;
+      }
+      drop_set_bits(filt, r, keep);
+      return;
+    }
+    if (bit == 0) {
+      drop_set_bits(filt, r, keep);
+      continue;
+    }
+    if (i > 0) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        keep.w[w].x |= filt.w[w].x & ~r.w[w].x;
+        keep.w[w].y |= filt.w[w].y & ~r.w[w].y;
+      }
+    }
+  }
+}
+
+__device__ void bsi_gt_unsigned(const BsiCtx& c, Tile& filt, int depth, uint64_t pred, bool allow_eq) {
+  Tile keep, r;
+  tile_zero(keep);
+  for (int i = depth - 1; i >= 0; i--) {
+    bsi_bit(c, i, r);
+    const int bit = int((pred >> i) & 1);
+    if (i == 0 && !allow_eq) {
+      if (bit == 1) {
+        filt = keep;
+        return;
+      }
+      keep_set_bits(filt, r, keep);
+      return;
+    }
+    if (bit == 1) {
+      keep_set_bits(filt, r, keep);
+      continue;
+    }
+    if (i > 0) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        keep.w[w].x |= filt.w[w].x & r.w[w].x;
+        keep.w[w].y |= filt.w[w].y & r.w[w].y;
+      }
+    }
+  }
+}
+
+__device__ void bsi_between_unsigned(const BsiCtx& c, Tile& filt, int depth, uint64_t pmin, uint64_t pmax) {
+  Tile keep1, keep2, r;
+  tile_zero(keep1);
+  tile_zero(keep2);
+  for (int i = depth - 1; i >= 0; i--) {
+    bsi_bit(c, i, r);
+    const int b1 = int((pmin >> i) & 1), b2 = int((pmax >> i) & 1);
+    if (b1 == 1) {
+      keep_set_bits(filt, r, keep1);
+    } else if (i > 0) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        keep1.w[w].x |= filt.w[w].x & r.w[w].x;
+        keep1.w[w].y |= filt.w[w].y & r.w[w].y;
+      }
+    }
+    if (b2 == 0) {
+      drop_set_bits(filt, r, keep2);
+    } else if (i > 0) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        keep2.w[w].x |= filt.w[w].x & ~r.w[w].x;
+        keep2.w[w].y |= filt.w[w].y & ~r.w[w].y;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void tile_or(Tile& a, const Tile& b) { tile_op<OP_OR>(a, b); }
+
+// op: 0 EQ, 1 NEQ, 2 LT, 3 LTE, 4 GT, 5 GTE, 6 BETWEEN(p1..p2), 7 NOT NULL
+__global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restrict__ views, int S, BsiArgs bsi,
+                                                        int op, int64_t p1, int64_t p2,
+                                                        uint16_t* __restrict__ out_payload,
+                                                        int64_t* __restrict__ out_meta) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(S) * 16) return;
+  const int s = int(item >> 4), j = int(item & 15);
+  const ViewDev& bv = views[bsi.view];
+  BsiCtx c{bsi, bv, s, j, bv.shard_base[s], bv.rowptr + int64_t(s) * (bv.D + 1), scratch[wave].lb};
+  const int depth = bsi.depth;
+  Tile b, sign, res;
+  bsi_row(c, bsi.row_exists, b);
+  bsi_row(c, bsi.row_sign, sign);
+  if (op == 7) {
+    res = b;
+  } else if (op == 0 || op == 1) {
+    Tile eq = b, r;
+    const uint64_t up = uint64_t(p1 < 0 ? -p1 : p1);
+    if (p1 < 0) tile_op<OP_AND>(eq, sign);
+    else tile_op<OP_ANDNOT>(eq, sign);
+    for (int i = depth - 1; i >= 0; i--) {
+      bsi_bit(c, i, r);
+      if ((up >> i) & 1) tile_op<OP_AND>(eq, r);
+      else tile_op<OP_ANDNOT>(eq, r);
+    }
+    res = b;
+    if (op == 1) tile_op<OP_ANDNOT>(res, eq);
+    else res = eq;
+  } else if (op == 2 || op == 3) {
+    const bool allow = op == 3;
+    const uint64_t up = uint64_t(p1 < 0 ? -p1 : p1);
+    if ((p1 >= 0 && allow) || (p1 >= -1 && !allow)) {
+      Tile pos = b;
+      tile_op<OP_ANDNOT>(pos, sign);
+      bsi_lt_unsigned(c, pos, depth, up, allow);
+      res = sign;
+      tile_or(res, pos);
+    } else {
+      res = b;
+      tile_op<OP_AND>(res, sign);
+      bsi_gt_unsigned(c, res, depth, up, allow);
+    }
+  } else if (op == 4 || op == 5) {
+    const bool allow = op == 5;
+    const uint64_t up = uint64_t(p1 < 0 ? -p1 : p1);
+    if ((p1 >= 0 && allow) || (p1 >= -1 && !allow)) {
+      res = b;
+      tile_op<OP_ANDNOT>(res, sign);
+      bsi_gt_unsigned(c, res, depth, up, allow);
+    } else {
+      Tile neg = b;
+      tile_op<OP_AND>(neg, sign);
+      bsi_lt_unsigned(c, neg, depth, up, allow);
+      res = b;
+      tile_op<OP_ANDNOT>(res, sign);
+      tile_or(res, neg);
+    }
+  } else {  // between
+    const uint64_t umin = uint64_t(p1 < 0 ? -p1 : p1), umax = uint64_t(p2 < 0 ? -p2 : p2);
+    if (p1 >= 0) {
+      res = b;
+      tile_op<OP_ANDNOT>(res, sign);
+      bsi_between_unsigned(c, res, depth, umin, umax);
+    } else if (p2 < 0) {
+      res = b;
+      tile_op<OP_AND>(res, sign);
+      bsi_between_unsigned(c, res, depth, umax, umin);
+    } else {
+      Tile pos = b, neg = b;
+      tile_op<OP_ANDNOT>(pos, sign);
+      tile_op<OP_AND>(neg, sign);
+      bsi_lt_unsigned(c, pos, depth, umax, true);
+      bsi_lt_unsigned(c, neg, depth, umin, true);
+      res = pos;
+      tile_or(res, neg);
+    }
+  }
+  const int64_t n = wave_sum_i64(tile_popc(res));
+  ulong2* dst = reinterpret_cast<ulong2*>(out_payload + item * 4096);
+#pragma unroll
+  for (int i = 0; i < 8; i++) dst[i * 64 + lane] = res.w[i];
+  if (lane == 0) out_meta[item] = int64_t(j) | (int64_t(CT_BITMAP) << 4) | (n << 6) | ((item * 512) << 23);
+}
+
+// ---------------------------------------------------------------- BSI min/max
+// Per (shard, key) MSB-first descents (reference fragment.go:1145-1225):
+// consider = exists & filter; for Min the max-magnitude negative and the
+// unsigned minimum of the positives, for Max the unsigned maximum of the
+// positives and the minimum magnitude of the negatives.  out[item] = 4 x
+// (value, count); the host folds keys into shard results exactly as one
+// shard-wide descent would (the key sets partition the shard).
+__global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __restrict__ progs,
+                                                         const ViewDev* __restrict__ views, int S, BsiArgs bsi,
+                                                         int64_t* __restrict__ out) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(S) * 16) return;
+  const int s = int(item >> 4), j = int(item & 15);
+  const ViewDev& bv = views[bsi.view];
+  WaveScratch& ws = scratch[wave];
+  BsiCtx c{bsi, bv, s, j, bv.shard_base[s], bv.rowptr + int64_t(s) * (bv.D + 1), ws.lb};
+  const int depth = bsi.depth;
+  const QueryProg& qp = progs[0];
+  Tile pos, neg;
+  bsi_row(c, bsi.row_exists, pos);
+  if (qp.nprog) {
+    uint32_t mask[MAXLEAF];
+    build_slots(qp, views, s, ws, mask);
+    Tile f;
+    if ((candidate_mask(qp, mask) >> j) & 1) eval_tile(qp, views, s, j, ws, f);
+    else tile_zero(f);
+    tile_op<OP_AND>(pos, f);
+  }
+  {
+    Tile sign;
+    bsi_row(c, bsi.row_sign, sign);
+    neg = pos;
+    tile_op<OP_AND>(neg, sign);
+    tile_op<OP_ANDNOT>(pos, sign);
+  }
+  // four descents share each bit-slice load: maxU(neg), minU(pos), maxU(pos), minU(neg)
+  Tile fmaxn = neg, fminp = pos, fmaxp = pos, fminn = neg, r;
+  int64_t vmaxn = 0, vminp = 0, vmaxp = 0, vminn = 0;
+  int64_t cmaxn = 0, cminp = 0, cmaxp = 0, cminn = 0;
+  for (int i = depth - 1; i >= 0; i--) {
+    bsi_bit(c, i, r);
+    Tile t;
+    // maxU(neg)
+    t = fmaxn;
+    tile_op<OP_AND>(t, r);
+    int64_t k = wave_sum_i64(tile_popc(t));
+    if (k > 0) { vmaxn |= int64_t(1) << i; fmaxn = t; cmaxn = k; }
+    else if (i == 0) cmaxn = wave_sum_i64(tile_popc(fmaxn));
+    // maxU(pos)
+    t = fmaxp;
+    tile_op<OP_AND>(t, r);
+    k = wave_sum_i64(tile_popc(t));
+    if (k > 0) { vmaxp |= int64_t(1) << i; fmaxp = t; cmaxp = k; }
+    else if (i == 0) cmaxp = wave_sum_i64(tile_popc(fmaxp));
+    // minU(pos)
+    t = fminp;
+    tile_op<OP_ANDNOT>(t, r);
+    k = wave_sum_i64(tile_popc(t));
+    if (k > 0) { fminp = t; cminp = k; }
+    else { vminp += int64_t(1) << i; if (i == 0) cminp = wave_sum_i64(tile_popc(fminp)); }
+    // minU(neg)
+    t = fminn;
+    tile_op<OP_ANDNOT>(t, r);
+    k = wave_sum_i64(tile_popc(t));
+    if (k > 0) { fminn = t; cminn = k; }
+    else { vminn += int64_t(1) << i; if (i == 0) cminn = wave_sum_i64(tile_popc(fminn)); }
+  }
+  const int64_t npos = wave_sum_i64(tile_popc(pos)), nneg = wave_sum_i64(tile_popc(neg));
+  if (lane == 0) {
+    int64_t* o = out + item * 10;
+    o[0] = vmaxn; o[1] = cmaxn; o[2] = vminp; o[3] = cminp;
+    o[4] = vmaxp; o[5] = cmaxp; o[6] = vminn; o[7] = cminn;
+    o[8] = npos; o[9] = nneg;
+  }
+}
+
 }  // namespace pk
 
 // ------------------------------------------------------------ launchers
@@ -537,6 +859,22 @@ void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views
   if (items == 0) return;
   hipLaunchKernelGGL(expr_materialize_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
                      Q, views, S, counts, offs, outp);
+}
+
+void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t p1, int64_t p2, uint16_t* out_payload,
+                      int64_t* out_meta, hipStream_t st) {
+  const int64_t items = int64_t(S) * 16;
+  if (items == 0) return;
+  hipLaunchKernelGGL(bsi_range_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, views, S, bsi, op,
+                     p1, p2, out_payload, out_meta);
+}
+
+void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
+                       hipStream_t st) {
+  const int64_t items = int64_t(S) * 16;
+  if (items == 0) return;
+  hipLaunchKernelGGL(bsi_minmax_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs, views, S,
+                     bsi, out);
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,

@@ -181,6 +181,23 @@ class DeviceView:
         self._row_index = None
 
     @classmethod
+    def from_device(cls, rows: np.ndarray, t_rowptr, t_shard_base, t_meta, t_payload, device, shards,
+                    container_count: int) -> "DeviceView":
+        """Wrap device tensors produced on the GPU (e.g. BSI predicate results)."""
+        import torch
+
+        self = cls.__new__(cls)
+        self.device = torch.device(device)
+        self.rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        self.S = int(t_shard_base.numel()) - 1
+        self.D = int(self.rows.shape[0])
+        self.shards = list(shards)
+        self.t_rowptr, self.t_shard_base, self.t_meta, self.t_payload = t_rowptr, t_shard_base, t_meta, t_payload
+        self.container_count = int(container_count)
+        self._row_index = None
+        return self
+
+    @classmethod
     def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=()):
         from pilosa_amd import _roaring
 
@@ -471,6 +488,68 @@ class GpuEngine:
                                                           o[s * 16 + nz].astype(np.int64), pay))
         return result, shards
 
+    @staticmethod
+    def bsi_args(bsi_view: "DeviceView", depth: int, slot: int = 0) -> np.ndarray:
+        """cpu int64[67]: view slot, depth, dense rows of exists / sign / bit i."""
+        args = np.full(67, -1, dtype=np.int64)
+        args[0] = slot
+        args[1] = depth
+        args[2] = bsi_view.dense(0)
+        args[3] = bsi_view.dense(1)
+        for i in range(min(depth, 63)):
+            args[4 + i] = bsi_view.dense(2 + i)
+        return args
+
+    BSI_OPS = {"==": 0, "!=": 1, "<": 2, "<=": 3, ">": 4, ">=": 5, "between": 6, "notnull": 7}
+
+    def bsi_range_view(self, bsi_view: "DeviceView", depth: int, op: str, p1: int = 0, p2: int = 0) -> "DeviceView":
+        """Evaluate a BSI predicate (base-relative values) over every local
+        shard into a temporary one-row device view: row 0 = matching columns,
+        one bitmap container per (shard, key)."""
+        torch = self.torch
+        S = bsi_view.S
+        payload = torch.empty(S * 16 * 4096, dtype=torch.int16, device=self.device)
+        meta = torch.empty(S * 16, dtype=torch.int64, device=self.device)
+        args = self.bsi_args(bsi_view, depth)
+        if S and args[2] >= 0:
+            tv = self._views_tensor([bsi_view])
+            self.ext.bsi_range(tv, S, torch.from_numpy(args), self.BSI_OPS[op], int(p1), int(p2), payload, meta)
+        else:
+            payload.zero_()
+            meta.copy_(torch.arange(S * 16, dtype=torch.int64, device=self.device) % 16 | (2 << 4)
+                       | ((torch.arange(S * 16, dtype=torch.int64, device=self.device) * 512) << 23))
+        rowptr = torch.tensor([0, 16], dtype=torch.int32, device=self.device).repeat(max(S, 0))
+        sb = torch.arange(S + 1, dtype=torch.int64, device=self.device) * 16
+        return DeviceView.from_device(np.zeros(1, np.uint64), rowptr, sb, meta, payload, self.device,
+                                      bsi_view.shards, S * 16)
+
+    def bsi_minmax(self, filt: Optional[object], bsi_view: "DeviceView", depth: int) -> np.ndarray:
+        """Per (shard, key) descents -> int64[S, 16, 10] (see bsi_minmax_kernel)."""
+        torch = self.torch
+        S = bsi_view.S
+        view_index: Dict[int, int] = {id(bsi_view): 0}
+        views = {id(bsi_view): bsi_view}
+        if filt is not None:
+            def collect(node):
+                if isinstance(node, Leaf):
+                    views[id(node.view)] = node.view
+                elif isinstance(node, Op):
+                    for a in node.args:
+                        collect(a)
+            collect(filt)
+            progs = pack_programs([compile_expr(filt, view_index)])
+        else:
+            progs = pack_programs([([], [], [])])
+        ordered = [None] * len(view_index)
+        for vid, slot in view_index.items():
+            ordered[slot] = views[vid]
+        out = torch.zeros(S * 16 * 10, dtype=torch.int64, device=self.device)
+        args = self.bsi_args(bsi_view, depth)
+        if S and args[2] >= 0:
+            tp, tv = self.upload_batch(progs, ordered)
+            self.ext.bsi_minmax(tp, tv, S, torch.from_numpy(args), out)
+        return out.cpu().numpy().reshape(S, 16, 10)
+
     def bsi_sum_async(self, filters: Sequence[Optional[object]], bsi_view: "DeviceView", depth: int):
         """Sum/count of a BSI field for a batch of filters (None = no filter)."""
         torch = self.torch
@@ -496,13 +575,7 @@ class GpuEngine:
         ordered = [None] * len(view_index)
         for vid, slot in view_index.items():
             ordered[slot] = views[vid]
-        args = np.full(67, -1, dtype=np.int64)
-        args[0] = 0
-        args[1] = depth
-        args[2] = bsi_view.dense(0)
-        args[3] = bsi_view.dense(1)
-        for i in range(min(depth, 63)):
-            args[4 + i] = bsi_view.dense(2 + i)
+        args = self.bsi_args(bsi_view, depth)
         out_sum = torch.zeros(len(filters), dtype=torch.int64, device=self.device)
         out_cnt = torch.zeros(len(filters), dtype=torch.int64, device=self.device)
         if bsi_view.S and args[2] >= 0:

@@ -50,6 +50,7 @@ class GpuExecutor:
         self.device = self.engine.device
         self.executor = executor
         self._arenas: Dict[Tuple, Tuple[Tuple, DeviceView]] = {}
+        self._bsi_views: Dict[Tuple, DeviceView] = {}  # predicate results (small LRU)
         self.mu = threading.RLock()
         self.launches = 0
 
@@ -80,6 +81,88 @@ class GpuExecutor:
     def invalidate(self):
         with self.mu:
             self._arenas.clear()
+            self._bsi_views.clear()
+
+    BSI_CACHE = 8
+
+    def bsi_leaf(self, index: str, c: Call, shards: Sequence[int]):
+        """Row(v <op> x) -> Leaf over a device-evaluated predicate view
+        (bsi_range_kernel); NOT NULL uses the exists row directly."""
+        f, b, kind, args = self._ex().bsi_predicate(index, c)
+        if kind == "empty":
+            return EMPTY
+        bv = self.view_arena(index, f.name, VIEW_BSI_PREFIX + f.name, shards)
+        if bv is None:
+            return EMPTY
+        if kind == "notnull":
+            return Leaf(bv, 0)
+        if kind == "between":
+            op, p1, p2 = "between", int(args[0]), int(args[1])
+        else:
+            op, p1, p2 = args[0], int(args[1]), 0
+        key = (id(bv), op, p1, p2, b.bit_depth)
+        with self.mu:
+            rv = self._bsi_views.get(key)
+            if rv is None:
+                self.launches += 1
+                rv = self.engine.bsi_range_view(bv, b.bit_depth, op, p1, p2)
+                rv._src = bv  # keep the source arena alive while cached (id() key)
+                if len(self._bsi_views) >= self.BSI_CACHE:
+                    self._bsi_views.pop(next(iter(self._bsi_views)))
+                self._bsi_views[key] = rv
+        return Leaf(rv, 0)
+
+    def bsi_minmax(self, index: str, c: Call, shards: List[int], which: str):
+        """Min/Max -> per-shard ValCounts in shard order (the executor folds
+        them with ValCount.smaller/larger, like its per-shard map)."""
+        from pilosa_amd.executor import ValCount
+        fname = c.args.get("field")
+        f = self.holder.field(index, fname) if isinstance(fname, str) else None
+        if f is None or f.bsi_group(fname) is None or len(c.children) > 1:
+            raise NotImplementedError
+        b = f.bsi_group(fname)
+        bv = self.view_arena(index, fname, VIEW_BSI_PREFIX + fname, shards)
+        if bv is None:
+            return [ValCount() for _ in shards]
+        filt = None
+        if len(c.children) == 1:
+            filt = self.plan(index, c.children[0], shards)
+            if filt is EMPTY:
+                return [ValCount() for _ in shards]
+        try:
+            self.launches += 1
+            o = self.engine.bsi_minmax(filt, bv, b.bit_depth)
+        except CompileError:
+            raise NotImplementedError
+        out = []
+        for si in range(len(shards)):
+            k = o[si]
+            npos, nneg = int(k[:, 8].sum()), int(k[:, 9].sum())
+            if npos + nneg == 0:
+                out.append(ValCount())
+                continue
+            if which == "min":
+                if nneg:  # -(max magnitude among negatives)
+                    sel = k[k[:, 9] > 0]
+                    v = int(sel[:, 0].max())
+                    cnt = int(sel[sel[:, 0] == v][:, 1].sum())
+                    v = -v
+                else:
+                    sel = k[k[:, 8] > 0]
+                    v = int(sel[:, 2].min())
+                    cnt = int(sel[sel[:, 2] == v][:, 3].sum())
+            else:
+                if npos:
+                    sel = k[k[:, 8] > 0]
+                    v = int(sel[:, 4].max())
+                    cnt = int(sel[sel[:, 4] == v][:, 5].sum())
+                else:  # all negative: -(min magnitude), fragment.max quirk
+                    sel = k[k[:, 9] > 0]
+                    v = int(sel[:, 6].min())
+                    cnt = int(sel[sel[:, 6] == v][:, 7].sum())
+                    v = -v
+            out.append(ValCount(v + b.base, cnt))
+        return out
 
     def hbm_bytes(self) -> int:
         with self.mu:
@@ -96,7 +179,7 @@ class GpuExecutor:
         n = c.name
         if n in ("Row", "Range", "Bitmap"):
             if c.has_condition_arg():
-                raise NotImplementedError("BSI predicate leaf")
+                return self.bsi_leaf(index, c, shards)
             try:
                 fname = c.field_arg()
             except ValueError:

@@ -18,6 +18,7 @@ def envs():
         e.field("i", "g")
         e.field("i", "t", type="time", time_quantum="YMD")
         e.field("i", "n", type="int", min=-1000, max=100000)
+        e.field("i", "m", type="int", min=-5000, max=-10)
     idx = cpu.holder.index("i")
     f, g, t, n = (idx.field(x) for x in "fgtn")
     nshard = 4
@@ -36,6 +37,8 @@ def envs():
     t.import_bits(np.full(len(cc), 1, np.uint64), cc.astype(np.uint64), timestamps=ts)
     vc = rng.choice(nshard * SW, size=20000, replace=False).astype(np.uint64)
     n.import_values(vc, rng.integers(-1000, 100000, size=len(vc)))
+    mc = rng.choice(nshard * SW, size=3000, replace=False).astype(np.uint64)
+    idx.field("m").import_values(mc, rng.integers(-5000, -10, size=len(mc)))
     idx.existence_field().import_bits(np.zeros(nshard * SW // 2, np.uint64),
                                       np.arange(nshard * SW // 2, dtype=np.uint64))
     for frag in cpu.holder.all_fragments():
@@ -119,3 +122,43 @@ def test_arena_invalidation_on_write(envs):
         cpu.executor.gpu = None
     assert after == cpu.q1("i", "Count(Row(f=7))")
     assert after in (before, before + 1)
+
+
+BSI_QUERIES = [
+    "Count(Row(n < 0))", "Count(Row(n <= -1))", "Count(Row(n > 500))", "Count(Row(n >= 0))",
+    "Count(Row(n < -1))", "Count(Row(n > -1))", "Count(Row(n >= -7))", "Count(Row(n < 77777))",
+    "Count(Row(n == 1234))", "Count(Row(n != 5))", "Count(Row(n >< [-100, 100]))",
+    "Count(Row(n >< [10, 5000]))", "Count(Row(n >< [-900, -10]))", "Count(Row(n != null))",
+    "Count(Intersect(Row(f=0), Row(n > 50000)))", "Count(Union(Row(n < -500), Row(m > -100)))",
+    "Count(Row(m == -20))", "Count(Row(m < -4000))", "Count(Row(n > 200000))",
+    "Min(field=n)", "Max(field=n)", "Min(Row(f=1), field=n)", "Max(Row(f=2), field=n)",
+    "Min(field=m)", "Max(field=m)", "Max(Row(f=0), field=m)", "Min(Row(n > 90000), field=n)",
+    "Sum(Row(n < 0), field=n)",
+]
+
+
+@pytest.mark.parametrize("q", BSI_QUERIES)
+def test_bsi_on_device_matches_host(envs, q):
+    cpu, gpu = envs
+    want = cpu.q1("i", q)
+    cpu.executor.gpu = gpu
+    try:
+        n0 = gpu.launches
+        got = cpu.q1("i", q)
+        if "200000" not in q:  # out-of-range predicate: answered without a launch
+            assert gpu.launches > n0, "device path not taken"
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
+
+
+def test_bsi_rows_match_host(envs):
+    cpu, gpu = envs
+    for q in ("Row(n > 99000)", "Row(n >< [-3, 3])", "Row(m < -4990)"):
+        want = cols(cpu.q1("i", q))
+        cpu.executor.gpu = gpu
+        try:
+            got = cols(cpu.q1("i", q))
+        finally:
+            cpu.executor.gpu = None
+        assert got == want, q
