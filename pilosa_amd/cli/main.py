@@ -88,7 +88,11 @@ def cmd_server(args, stdout, stderr) -> int:
                  probe_interval=cfg.duration("gossip.probe-interval"),
                  long_query_time=cfg.duration("cluster.long-query-time"), stats=cfg.get("metric.service")
                  if cfg.get("metric.service") != "none" else "expvar", logger=logger,
-                 cluster_disabled=cfg.get("cluster.disabled"), mesh_block=cfg.get("gpu.shard-block"))
+                 cluster_disabled=cfg.get("cluster.disabled"), mesh_block=cfg.get("gpu.shard-block"),
+                 translation_primary_url=cfg.get("translation.primary-url"),
+                 tls_certificate=cfg.get("tls.certificate"), tls_key=cfg.get("tls.key"),
+                 tls_skip_verify=cfg.get("tls.skip-verify"),
+                 diagnostics_host=cfg.get("metric.diagnostics-host") if cfg.get("metric.diagnostics") else "")
     srv.open()
     logger.printf("listening as %s (node %s, gpu=%s)", srv.uri.normalize(), srv.node.id,
                   "on" if srv.gpu is not None else "off")

@@ -183,11 +183,17 @@ class Fragment:
         self.ops += 1
         self.version += 1
         if self.opn > self.max_opn:
-            self.snapshot()
+            q = getattr(self, "snapshot_queue", None)
+            if q is not None:
+                q.enqueue(self)
+            else:
+                self.snapshot()
 
     def snapshot(self):
         """Write storage + truncate the op log (write -> fsync -> rename)."""
         with self.mu:
+            if self._fh is None and not os.path.exists(self.path):
+                return  # closed/deleted while queued
             tmp = self.path + ".snapshotting"
             data = self.storage.to_bytes()
             with open(tmp, "wb") as fh:

@@ -36,11 +36,15 @@ class Holder:
         self._flusher: Optional[threading.Thread] = None
         self.on_create_shard = None   # (index, field, shard) -> None, set by the server (broadcast)
         self.on_schema_change = None  # () -> None, e.g. GPU arena invalidation
+        self.snapshot_queue = None    # background snapshots, created by open() (holder.go:160)
 
     # ------------------------------------------------------------ lifecycle
     def open(self, background: bool = False):
+        from pilosa_amd.models.snapshot import SnapshotQueue
         with self.mu:
             os.makedirs(self.path, exist_ok=True)
+            if self.snapshot_queue is None:
+                self.snapshot_queue = SnapshotQueue(100, 2)
             self._set_file_limit()
             self.translate.open()
             for name in sorted(os.listdir(self.path)):
@@ -61,6 +65,9 @@ class Holder:
 
     def close(self):
         self._closing.set()
+        if self.snapshot_queue is not None:
+            self.snapshot_queue.close()
+            self.snapshot_queue = None
         with self.mu:
             for idx in self.indexes.values():
                 idx.close()
@@ -110,6 +117,7 @@ class Holder:
         idx = Index(os.path.join(self.path, name), name, keys=keys, track_existence=track_existence,
                     max_opn=self.max_opn, stats=self.stats, persistent_attrs=self.persistent_attrs)
         idx.on_create_shard = self._index_created_shard
+        idx.snapshot_queue = self.snapshot_queue
         return idx
 
     def _index_created_shard(self, idx, field, shard):

@@ -89,6 +89,7 @@ class Index:
         f = Field(os.path.join(self.path, name), self.name, name, opts, max_opn=self.max_opn, stats=self.stats,
                   persistent_attrs=self.persistent_attrs)
         f.on_create_shard = self._field_created_shard
+        f.snapshot_queue = getattr(self, "snapshot_queue", None)
         return f
 
     def _field_created_shard(self, field: Field, shard: int):

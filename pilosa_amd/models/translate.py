@@ -66,6 +66,10 @@ class TranslateFile:
         self._log: List[bytes] = []  # in-memory copy when no path
         self._fh = None
         self.size = 0
+        self._next: Dict[Tuple[str, str], int] = {}  # (index, field or "") -> next id
+        # read-only replicas: (index, field or None, keys) -> ids resolved by
+        # the primary (http translate proxy, reference http/translator.go)
+        self.forward = None
 
     def open(self):
         with self.mu:
@@ -92,9 +96,13 @@ class TranslateFile:
         if t == T_COLUMN:
             self._cols.setdefault(index, {})[key] = id
             self._col_ids.setdefault(index, {})[id] = key
+            nk = (index, "")
         else:
             self._rows.setdefault((index, field), {})[key] = id
             self._row_ids.setdefault((index, field), {})[id] = key
+            nk = (index, field)
+        if id >= self._next.get(nk, 1):
+            self._next[nk] = id + 1
 
     def _append(self, rec: bytes):
         if self._fh is not None:
@@ -129,21 +137,36 @@ class TranslateFile:
                     return fh.read()
             return b"".join(self._log)[offset:]
 
-    def _next_id(self, m: Dict[int, str]) -> int:
-        return (max(m) + 1) if m else 1
+    def _next_id(self, index: str, field: str = "") -> int:
+        return self._next.get((index, field), 1)
+
+    def _forward(self, index: str, field: Optional[str], keys: List[str]) -> List[int]:
+        if self.forward is None:
+            raise ErrTranslateStoreReadOnly
+        ids = self.forward(index, field, keys)
+        with self.mu:
+            for k, i in zip(keys, ids):  # visible now; the replicated log entry follows
+                self._apply(T_ROW if field else T_COLUMN, index, field or "", int(i), k)
+        return [int(i) for i in ids]
 
     # ------------------------------------------------------------ columns
     def translate_columns_to_uint64(self, index: str, keys: Sequence[str]) -> List[int]:
         out = []
+        keys = list(keys)
+        if self.read_only:
+            with self.mu:
+                cm = self._cols.get(index, {})
+                missing = [k for k in keys if k not in cm]
+            if missing:
+                self._forward(index, None, sorted(set(missing)))
         with self.mu:
             cm = self._cols.setdefault(index, {})
-            im = self._col_ids.setdefault(index, {})
             for k in keys:
                 id = cm.get(k)
                 if id is None:
                     if self.read_only:
                         raise ErrTranslateStoreReadOnly
-                    id = self._next_id(im)
+                    id = self._next_id(index)
                     self._apply(T_COLUMN, index, "", id, k)
                     self._append(_encode(T_COLUMN, index, "", id, k))
                 out.append(id)
@@ -163,15 +186,21 @@ class TranslateFile:
     # ------------------------------------------------------------ rows
     def translate_rows_to_uint64(self, index: str, field: str, keys: Sequence[str]) -> List[int]:
         out = []
+        keys = list(keys)
+        if self.read_only:
+            with self.mu:
+                rm = self._rows.get((index, field), {})
+                missing = [k for k in keys if k not in rm]
+            if missing:
+                self._forward(index, field, sorted(set(missing)))
         with self.mu:
             rm = self._rows.setdefault((index, field), {})
-            im = self._row_ids.setdefault((index, field), {})
             for k in keys:
                 id = rm.get(k)
                 if id is None:
                     if self.read_only:
                         raise ErrTranslateStoreReadOnly
-                    id = self._next_id(im)
+                    id = self._next_id(index, field)
                     self._apply(T_ROW, index, field, id, k)
                     self._append(_encode(T_ROW, index, field, id, k))
                 out.append(id)

@@ -47,6 +47,7 @@ class View:
                         bool_field=opts is not None and opts.type == "bool",
                         stats=f.stats if f is not None else None)
         frag.row_attr_store = f.row_attr_store if f is not None else None
+        frag.snapshot_queue = getattr(f, "snapshot_queue", None)
         return frag
 
     def open(self):

@@ -339,24 +339,46 @@ class GpuExecutor:
         if src is EMPTY:
             return []
         rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
-        exprs = [Op("and", (src, Leaf(rv, r))) for r in cand]
-        try:
-            mats = []
-            for i in range(0, len(exprs), MAX_GROUPS_PER_LAUNCH):
-                self.launches += 1
-                mats.append(self.engine.count_per_shard(exprs[i:i + MAX_GROUPS_PER_LAUNCH]))
-            counts = np.concatenate(mats, axis=0)  # [C, S]
-        except CompileError:
-            raise NotImplementedError
-        col = {r: i for i, r in enumerate(cand)}
+        # Each shard's fragment.top() walks its cache in order and stops once a
+        # row's cached count falls below the heap threshold, so usually only a
+        # short prefix of the (up to cache-size) candidates is ever counted.
+        # Count growing prefixes on the device (one launch per round for all
+        # shards), replay the exact heap logic on the host, and only extend
+        # the shards whose replay ran past what was counted.
+        counted: Dict[int, np.ndarray] = {}
+        depth = [0] * len(shards)
+        k = max(256, 2 * n) if not ids else max(len(p) for p in per_shard_pairs)
+        pending = list(range(len(shards)))
         total: Dict[int, int] = {}
-        for si, pairs in enumerate(per_shard_pairs):
-            if not pairs:
-                continue
-            got = _replay_top(pairs, lambda rid: int(counts[col[rid], si]), 0 if ids else n, threshold)
-            for p in got:
-                total[p.id] = total.get(p.id, 0) + p.count
-        return sort_pairs([Pair(k, v) for k, v in total.items()])
+        while pending:
+            want = set()
+            for si in pending:
+                depth[si] = min(len(per_shard_pairs[si]), max(depth[si] * 4, k))
+                want.update(rid for rid, _ in per_shard_pairs[si][:depth[si]] if rid not in counted)
+            if want:
+                rows = sorted(want)
+                exprs = [Op("and", (src, Leaf(rv, r))) for r in rows]
+                try:
+                    for i in range(0, len(exprs), MAX_GROUPS_PER_LAUNCH):
+                        self.launches += 1
+                        m = self.engine.count_per_shard(exprs[i:i + MAX_GROUPS_PER_LAUNCH])  # [R, S]
+                        for r, row_counts in zip(rows[i:i + MAX_GROUPS_PER_LAUNCH], m):
+                            counted[r] = row_counts
+                except CompileError:
+                    raise NotImplementedError
+            nxt = []
+            for si in pending:
+                pairs = per_shard_pairs[si]
+                try:
+                    got = _replay_top(pairs, lambda rid, si=si: _counted(counted, rid, si), 0 if ids else n,
+                                      threshold)
+                except _NeedMore:
+                    nxt.append(si)
+                    continue
+                for p in got:
+                    total[p.id] = total.get(p.id, 0) + p.count
+            pending = nxt
+        return sort_pairs([Pair(k2, v) for k2, v in total.items()])
 
     # ------------------------------------------------------------ GroupBy
     def group_by(self, index: str, c: Call, filt: Optional[Call], shards: List[int], child_rows, limit: int):
@@ -442,6 +464,17 @@ def _lex_product(cand: List[List[int]], prev: Optional[Tuple[int, ...]]):
                 yield from rec(level + 1, key)
 
     yield from rec(0, ())
+
+
+class _NeedMore(Exception):
+    """A replay reached a candidate whose count was not computed yet."""
+
+
+def _counted(counted: Dict[int, np.ndarray], rid: int, si: int) -> int:
+    row = counted.get(rid)
+    if row is None:
+        raise _NeedMore
+    return int(row[si])
 
 
 def _replay_top(pairs: List[Tuple[int, int]], count_of, n: int, min_threshold: int) -> List[Pair]:

@@ -400,10 +400,11 @@ class API:
                 "localID": self.cluster.node.id}
 
     def info(self) -> dict:
-        import os
+        from pilosa_amd.utils.sysinfo import SystemInfo
+        si = SystemInfo()
         gpu = self.server.gpu_info()
-        return {"shardWidth": SHARD_WIDTH, "cpuPhysicalCores": os.cpu_count(), "cpuLogicalCores": os.cpu_count(),
-                "version": __version__, "gpus": gpu}
+        return {"shardWidth": SHARD_WIDTH, "cpuPhysicalCores": si.cpu_cores(), "cpuLogicalCores": si.cpu_threads(),
+                "cpuType": si.cpu_model(), "memory": si.mem_total(), "version": __version__, "gpus": gpu}
 
     def version(self) -> str:
         return __version__

@@ -29,8 +29,9 @@ class ClientError(PilosaError):
 
 
 class InternalClient:
-    def __init__(self, timeout: float = 30.0):
+    def __init__(self, timeout: float = 30.0, skip_verify: bool = False):
         self.timeout = timeout
+        self.skip_verify = skip_verify
         self._local = threading.local()
 
     def _conn(self, uri) -> http.client.HTTPConnection:
@@ -40,7 +41,15 @@ class InternalClient:
         key = (uri.host, uri.port)
         c = pool.get(key)
         if c is None:
-            c = http.client.HTTPConnection(uri.host, uri.port, timeout=self.timeout)
+            if getattr(uri, "scheme", "http") == "https":
+                import ssl
+                ctx = ssl.create_default_context()
+                if self.skip_verify:
+                    ctx.check_hostname = False
+                    ctx.verify_mode = ssl.CERT_NONE
+                c = http.client.HTTPSConnection(uri.host, uri.port, timeout=self.timeout, context=ctx)
+            else:
+                c = http.client.HTTPConnection(uri.host, uri.port, timeout=self.timeout)
             pool[key] = c
         return c
 

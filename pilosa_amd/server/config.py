@@ -77,7 +77,7 @@ DEFAULTS: Dict[str, Any] = {
                "interval": "200ms", "nodes": 3, "to-the-dead-time": "30s"},
     "translation": {"map-size": 10737418240, "primary-url": ""},
     "anti-entropy": {"interval": "10m0s"},
-    "metric": {"service": "none", "host": "", "poll-interval": "0s", "diagnostics": True},
+    "metric": {"service": "none", "host": "", "poll-interval": "0s", "diagnostics": True, "diagnostics-host": ""},
     "tracing": {"sampler-type": "remote", "sampler-param": 0.001, "agent-host-port": ""},
     "profile": {"block-rate": 10000000, "mutex-fraction": 100},
     "gpu": {"mode": "auto", "devices": [], "hbm-budget": 0, "shard-block": 1},

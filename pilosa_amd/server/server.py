@@ -44,7 +44,9 @@ class Server:
                  coordinator_uri: Optional[str] = None, gpu: str = "auto", workers: int = 8,
                  max_writes: int = 5000, anti_entropy_interval: float = 600.0, probe_interval: float = 1.0,
                  long_query_time: float = 60.0, stats: str = "expvar", logger=None, hasher: str = "jump",
-                 max_opn: int = 10000, cluster_disabled: bool = False, mesh_block: int = 1):
+                 max_opn: int = 10000, cluster_disabled: bool = False, mesh_block: int = 1,
+                 translation_primary_url: str = "", tls_certificate: str = "", tls_key: str = "",
+                 tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0):
         self.data_dir = data_dir
         self.bind = bind
         self.logger = logger or StandardLogger()
@@ -65,6 +67,12 @@ class Server:
         self.gpu_mode = gpu
         self.mesh = None          # multi-GPU node: parallel.mesh.ShardMesh (this process is rank 0)
         self.mesh_block = mesh_block
+        self.translation_primary = URI.parse(translation_primary_url) if translation_primary_url else None
+        self.tls_certificate, self.tls_key = tls_certificate, tls_key
+        self.client.skip_verify = tls_skip_verify
+        self.diagnostics = None
+        self.diagnostics_host, self.diagnostics_interval = diagnostics_host, diagnostics_interval
+        self.gc_notifier = None
         self.workers = workers
         self.max_writes = max_writes
         self.cluster: Optional[Cluster] = None
@@ -84,9 +92,16 @@ class Server:
         nid = self._node_id or self.holder.load_node_id()
         host, _, port = self.bind.rpartition(":")
         self.httpd = make_http_server(Handler(self.api, self, self.logger, self.stats), self.bind)
+        scheme = "http"
+        if self.tls_certificate and self.tls_key:
+            import ssl
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(self.tls_certificate, self.tls_key)
+            self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True)
+            scheme = "https"
         port = self.httpd.server_address[1]
         adv = host if host not in ("", "0.0.0.0") else "127.0.0.1"
-        self.node = Node(nid, URI("http", adv, port), state=NODE_READY)
+        self.node = Node(nid, URI(scheme, adv, port), state=NODE_READY)
         self.cluster = Cluster(self.node, replica_n=self.replica_n, hasher=self.hasher, path=self.data_dir)
         self.cluster.on_state_change = lambda s: self.logger.debugf("cluster state -> %s", s)
         self._init_gpu()
@@ -111,7 +126,50 @@ class Server:
         if self.replica_n > 1 and self.anti_entropy_interval > 0:
             self._start_loop(self._anti_entropy_loop, "anti-entropy")
         self._start_loop(self._runtime_loop, "runtime")
+        if self.translation_primary is not None:
+            self._start_translate_replica()
+        from pilosa_amd.utils.gcnotify import GCNotifier
+        self.gc_notifier = GCNotifier(self.stats).start()
+        from pilosa_amd.utils.diagnostics import DiagnosticsCollector
+        self.diagnostics = DiagnosticsCollector(self.diagnostics_host, self.diagnostics_interval, self.logger)
+        if self.diagnostics_host:
+            self.diagnostics.start(self._refresh_diagnostics)
         return self
+
+    # ------------------------------------------------------------ translate replica
+    def _start_translate_replica(self):
+        """Non-primary translate store: read-only, tails the primary's log from
+        its byte offset over /internal/translate/data and forwards unknown keys
+        to the primary (reference translate.go:423-474, http/translator.go)."""
+        ts = self.holder.translate
+        ts.read_only = True
+        primary = self.translation_primary
+        ts.forward = lambda index, field, keys: self.client.translate_keys(primary, index, field, keys)
+
+        def loop():
+            while not self._closing.is_set():
+                try:
+                    data = self.client.translate_data(primary, ts.size)
+                    if data:
+                        ts.apply_log(data)
+                        continue
+                except Exception as e:  # noqa: BLE001 - primary briefly unavailable
+                    self.logger.debugf("translate replication: %s", e)
+                self._closing.wait(0.5)
+        self._start_loop(loop, "translate-replica")
+
+    def _refresh_diagnostics(self):
+        d = self.diagnostics
+        d.set("Host", self.uri.host)
+        d.set("Cluster", ",".join(n.id for n in self.cluster.nodes))
+        d.set("NumNodes", len(self.cluster.nodes))
+        d.set("NodeID", self.node.id)
+        d.set("ClusterID", getattr(self.cluster, "id", ""))
+        d.set("GPUs", len(self.diagnostics.sysinfo.gpus()) if self.gpu is not None else 0)
+        d.enrich_with_cpu()
+        d.enrich_with_os()
+        d.enrich_with_memory()
+        d.enrich_with_schema(self.holder)
 
     def _init_mesh(self):
         """Under torch.distributed.run with WORLD_SIZE > 1 this process is the
@@ -155,6 +213,10 @@ class Server:
 
     def close(self):
         self._closing.set()
+        if self.diagnostics is not None:
+            self.diagnostics.stop()
+        if self.gc_notifier is not None:
+            self.gc_notifier.stop()
         if self.mesh is not None:
             self.mesh.stop()
         if self.httpd is not None:

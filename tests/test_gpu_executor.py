@@ -19,6 +19,7 @@ def envs():
         e.field("i", "t", type="time", time_quantum="YMD")
         e.field("i", "n", type="int", min=-1000, max=100000)
         e.field("i", "m", type="int", min=-5000, max=-10)
+        e.field("i", "h", cache_type="ranked", cache_size=5000)
     idx = cpu.holder.index("i")
     f, g, t, n = (idx.field(x) for x in "fgtn")
     nshard = 4
@@ -37,6 +38,10 @@ def envs():
     t.import_bits(np.full(len(cc), 1, np.uint64), cc.astype(np.uint64), timestamps=ts)
     vc = rng.choice(nshard * SW, size=20000, replace=False).astype(np.uint64)
     n.import_values(vc, rng.integers(-1000, 100000, size=len(vc)))
+    # many rows with Zipf-like sizes: TopN replays need several counted prefixes
+    hr = (rng.zipf(1.3, size=400000) % 3000).astype(np.uint64)
+    hc = rng.integers(0, nshard * SW, size=len(hr)).astype(np.uint64)
+    idx.field("h").import_bits(hr, hc)
     mc = rng.choice(nshard * SW, size=3000, replace=False).astype(np.uint64)
     idx.field("m").import_values(mc, rng.integers(-5000, -10, size=len(mc)))
     idx.existence_field().import_bits(np.zeros(nshard * SW // 2, np.uint64),
@@ -162,3 +167,17 @@ def test_bsi_rows_match_host(envs):
         finally:
             cpu.executor.gpu = None
         assert got == want, q
+
+
+@pytest.mark.parametrize("q", ["TopN(h, Row(f=2), n=5)", "TopN(h, Row(f=3), n=300)", "TopN(h, Row(f=0), n=50)",
+                               "TopN(h, Row(g=1), n=1000)", "TopN(h, Row(f=1), ids=[1, 5, 7, 2999])",
+                               "TopN(h, Row(f=0), n=20, threshold=50)"])
+def test_topn_prefix_rounds_match_host(envs, q):
+    cpu, gpu = envs
+    want = cpu.q1("i", q)
+    cpu.executor.gpu = gpu
+    try:
+        got = cpu.q1("i", q)
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
