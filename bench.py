@@ -45,6 +45,96 @@ def zipf_rows(rng, n, nrows=NROWS, s=1.6, v=50.0):
     return np.searchsorted(cdf, rng.random(n)).astype(np.int64)
 
 
+def bench_topn(args, view, eng, rng, world, rank, dev):
+    """TopN batches on the device rank caches (pilosa_amd/ops/topn.py):
+      cache:  TopN(f, n=100)            -- ranked-cache TopN (BASELINE config 3)
+      src:    TopN(f, Row(f=a), n=100)  -- src-filtered, a from the 1000 hottest rows
+    Multi-GPU: phase-1 pairs are all-gathered and summed by id, the ids=
+    re-count is all-reduced (RCCL), as the reference coordinator does over HTTP."""
+    import torch
+    import torch.distributed as dist
+
+    from pilosa_amd.ops.planner import BenchPlanner
+    from pilosa_amd.ops.topn import (DeviceRankCache, finish_topn, topn_cache_phase1, topn_cache_phase2_counts,
+                                     topn_phase1, topn_phase2_counts)
+    from pilosa_amd.pql import parse_string
+
+    n = 100
+    t0 = time.perf_counter()
+    cache = DeviceRankCache.from_view(view, k=args.topn_cache, keep_row_counts=True)
+    torch.cuda.synchronize(dev)
+    t_cache = time.perf_counter() - t0
+    planner = BenchPlanner({"f": view})
+
+    def merge(totals):
+        if world == 1:
+            return totals
+        gathered = [None] * world
+        dist.all_gather_object(gathered, totals)
+        out = []
+        for q in range(len(totals)):
+            t = {}
+            for part in gathered:
+                for i, c in part[q].items():
+                    t[i] = t.get(i, 0) + c
+            out.append(t)
+        return out
+
+    def allreduce(exact, ids):
+        if world == 1:
+            return exact
+        flat = torch.from_numpy(np.concatenate(exact) if exact else np.zeros(0, np.int64)).to(dev)
+        dist.all_reduce(flat)
+        flat = flat.cpu().numpy()
+        o, out = 0, []
+        for q in range(len(ids)):
+            out.append(flat[o:o + len(ids[q])])
+            o += len(ids[q])
+        return out
+
+    def run_cache(qs):
+        calls = [parse_string(q).calls[0] for q in qs]
+        totals = merge([topn_cache_phase1(cache, c.uint_arg("n")[0]) for c in calls])
+        ids = [sorted(t) for t in totals]
+        exact = allreduce([topn_cache_phase2_counts(cache, view, i) for i in ids], ids)
+        return [finish_topn(ids[q], exact[q], n) for q in range(len(qs))]
+
+    def run_src(qs):
+        calls = [parse_string(q).calls[0] for q in qs]
+        srcs = [planner.plan(c.children[0]) for c in calls]
+        totals = merge(topn_phase1(eng, view, cache, srcs, n=n))
+        ids = [sorted(t) for t in totals]
+        exact = allreduce(topn_phase2_counts(eng, view, srcs, ids), ids)
+        return [finish_topn(ids[q], exact[q], n) for q in range(len(qs))]
+
+    def timed(fn, queries, B, batches):
+        fn(queries[:B])  # warmup
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        res = None
+        for b in range(1, batches + 1):
+            res = fn(queries[b * B:(b + 1) * B])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        elt = torch.tensor([el], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        el = float(elt.item())
+        return {"qps": round(B * batches / el, 2), "ms_per_batch": round(el / batches * 1000, 2), "batch": B,
+                "sample_top3": [(p.id, p.count) for p in res[0][:3]] if res and res[0] else []}
+
+    B, nb = args.topn_batch, args.topn_batches
+    out = {"n": n, "cache_k": args.topn_cache, "cache_build_s": round(t_cache, 2)}
+    out["cache"] = timed(run_cache, [f"TopN(f, n={n})"] * (B * (nb + 1)), B, nb)
+    hot = zipf_rows(rng, B * (nb + 1), 1000)
+    out["src"] = timed(run_src, [f"TopN(f, Row(f={a}), n={n})" for a in hot], B, nb)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,7 +144,10 @@ def main():
     ap.add_argument("--cols", type=int, default=TOTAL_COLS)
     ap.add_argument("--rows", type=int, default=NROWS)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--topn", action="store_true", help="also time TopN(n=100) batches")
+    ap.add_argument("--topn-batches", type=int, default=3,
+                    help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
+    ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
+    ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
     ap.add_argument("--cpu-baseline-shards", type=int, default=0,
                     help="also time the host C++ roaring executor on this many shards (extrapolated)")
     args = ap.parse_args()
@@ -152,6 +245,9 @@ def main():
              "mean_count": float(last.double().mean()) if last is not None else None,
              "native_compiled": compiler.native_hits, "fallback_compiled": compiler.fallbacks,
              "host_ms_per_step": {k: round(v / max(1, args.steps - 1) * 1000, 3) for k, v in tm.items()}}
+
+    if args.topn_batches > 0:
+        extra["topn"] = bench_topn(args, view, eng, rng, world, rank, dev)
 
     if rank == 0:
         rec = {"metric": "PQL queries/sec (Count(Intersect(Row,Row))) on 1M-row x 1B-col set field",

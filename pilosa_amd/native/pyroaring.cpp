@@ -22,6 +22,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <queue>
 #include <atomic>
 #include <cmath>
 #include <thread>
@@ -403,6 +404,81 @@ static Bitmap arena_shard_bitmap(py::array_t<uint64_t> rows, py::array_t<uint32_
   return out;
 }
 
+
+// TopN per-shard heap replay (reference fragment.go:1568-1700 top(); same
+// control flow as pilosa_amd/models/fragment.py Fragment.top with a src row):
+// cache candidates in rank order, the first n counted unconditionally, then
+// stop at the first candidate whose cached count is below the heap minimum.
+// Intersection counts come from the device (counted[R, S] for the sorted row
+// ids in counted_rows); a shard whose walk reaches an uncounted row is
+// reported in need_more and contributes nothing yet.
+static py::tuple topn_replay(py::array_t<int64_t, py::array::c_style | py::array::forcecast> cand_rows,
+                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> cand_cnts,
+                             py::array_t<int32_t, py::array::c_style | py::array::forcecast> shards, int64_t n,
+                             int64_t min_threshold,
+                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> counted_rows,
+                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> counted) {
+  if (cand_rows.ndim() != 2 || cand_cnts.ndim() != 2 || counted.ndim() != 2)
+    throw std::invalid_argument("topn_replay: 2-d candidate / count arrays expected");
+  const int64_t S = cand_rows.shape(0), K = cand_rows.shape(1);
+  const int64_t R = counted_rows.shape(0);
+  if (counted.shape(0) != R || counted.shape(1) != S || cand_cnts.shape(0) != S || cand_cnts.shape(1) != K)
+    throw std::invalid_argument("topn_replay: shape mismatch");
+  const int64_t* cr = cand_rows.data();
+  const int64_t* cc = cand_cnts.data();
+  const int64_t* rows = counted_rows.data();
+  const int64_t* cnt = counted.data();
+  const int32_t* sh = shards.data();
+  const int64_t M = shards.shape(0);
+  py::array_t<bool> need(M);
+  bool* needp = need.mutable_data();
+  std::vector<int64_t> out_ids, out_cnt;
+  {
+    py::gil_scoped_release nogil;
+    using E = std::pair<int64_t, int64_t>;  // (count, -id): min-heap top = smallest count, then largest id
+    for (int64_t m = 0; m < M; m++) {
+      const int64_t s = sh[m];
+      if (s < 0 || s >= S) throw std::out_of_range("topn_replay: shard index");
+      std::priority_queue<E, std::vector<E>, std::greater<E>> heap;
+      bool more = false;
+      auto count_of = [&](int64_t rid, int64_t& v) -> bool {
+        const int64_t* it = std::lower_bound(rows, rows + R, rid);
+        if (it == rows + R || *it != rid) return false;
+        v = cnt[(it - rows) * S + s];
+        return true;
+      };
+      for (int64_t k = 0; k < K; k++) {
+        const int64_t rid = cr[s * K + k], c = cc[s * K + k];
+        if (c == 0 || c < min_threshold) continue;
+        if (n == 0 || int64_t(heap.size()) < n) {
+          int64_t v;
+          if (!count_of(rid, v)) { more = true; break; }
+          if (v == 0 || v < min_threshold) continue;
+          heap.emplace(v, -rid);
+          continue;
+        }
+        const int64_t thr = heap.top().first;
+        if (thr < min_threshold || c < thr) break;
+        int64_t v;
+        if (!count_of(rid, v)) { more = true; break; }
+        if (v < thr) continue;
+        heap.emplace(v, -rid);
+      }
+      needp[m] = more;
+      if (more) continue;
+      while (!heap.empty()) {
+        out_ids.push_back(-heap.top().second);
+        out_cnt.push_back(heap.top().first);
+        heap.pop();
+      }
+    }
+  }
+  py::array_t<int64_t> ids(out_ids.size()), cnts(out_cnt.size());
+  std::copy(out_ids.begin(), out_ids.end(), ids.mutable_data());
+  std::copy(out_cnt.begin(), out_cnt.end(), cnts.mutable_data());
+  return py::make_tuple(need, ids, cnts);
+}
+
 PYBIND11_MODULE(_roaring, m) {
   m.doc() = "Host roaring core (containers, pilosa file format, op log, device arena builder)";
   m.attr("ARRAY_MAX") = pr::ARRAY_MAX;
@@ -560,6 +636,9 @@ PYBIND11_MODULE(_roaring, m) {
   m.def("build_arena", &build_arena, py::arg("shards"), py::arg("containers_per_row") = 16,
         py::arg("nthreads") = 8);
   m.def("bitmap_from_containers", &bitmap_from_containers);
+  m.def("topn_replay", &topn_replay, py::arg("cand_rows"), py::arg("cand_cnts"), py::arg("shards"), py::arg("n"),
+        py::arg("min_threshold"), py::arg("counted_rows"), py::arg("counted"),
+        "Per-shard TopN heap replay over device-counted candidates -> (need_more, ids, counts)");
   m.def("gen_zipf_arena", &gen_zipf_arena, py::arg("shard_lo"), py::arg("shard_hi"), py::arg("total_cols"),
         py::arg("nrows"), py::arg("bits_per_col") = 8.0, py::arg("zipf_s") = 1.6, py::arg("zipf_v") = 50.0,
         py::arg("seed") = 1, py::arg("nthreads") = 8);

@@ -423,25 +423,60 @@ class GpuEngine:
 
     def count_per_shard(self, exprs: Sequence[object]) -> np.ndarray:
         """Counts per (query, local shard) -> int64[Q, S] (TopN per-shard semantics)."""
-        torch = self.torch
         progs, views, S = self.compile_batch(exprs)
-        Q = len(exprs)
+        return self.count_per_shard_progs(progs, views, S)
+
+    @staticmethod
+    def pair_programs(slot_a: int, dense_a: np.ndarray, slot_b: int, dense_b: np.ndarray) -> np.ndarray:
+        """Count(Intersect(Row a, Row b)) QueryProg records built directly
+        (vectorised; no expression objects) for dense row indices."""
+        dense_a = np.broadcast_to(np.asarray(dense_a, np.int64), np.shape(dense_b)) if np.ndim(dense_a) == 0 \
+            else np.asarray(dense_a, np.int64)
+        dense_b = np.asarray(dense_b, np.int64)
+        Q = len(dense_b)
+        p = np.zeros(Q, dtype=QPROG_DTYPE)
+        p["nleaf"] = 2
+        p["nprog"] = 3
+        p["leaf_view"][:, 0] = slot_a
+        p["leaf_view"][:, 1] = slot_b
+        p["leaf_row"][:, 0] = dense_a
+        p["leaf_row"][:, 1] = dense_b
+        p["prog"][:, 0] = 0
+        p["prog"][:, 1] = 1
+        p["prog"][:, 2] = OP_AND
+        return p
+
+    def count_per_shard_progs(self, progs: np.ndarray, views: List["DeviceView"], S: int,
+                              as_tensor: bool = False):
+        """:meth:`count_per_shard` for compiled records.  Count(Intersect)
+        batches take the pair kernels, ordered by leaf rows for reuse."""
+        torch = self.torch
+        Q = len(progs)
         if not S or not Q:
-            return np.zeros((Q, S), dtype=np.int64)
+            z = np.zeros((Q, S), dtype=np.int64)
+            return torch.from_numpy(z) if as_tensor else z
+        progs = _canonical_and2(progs)
         np_, pg = progs["nprog"], progs["prog"]
-        if self.use_and2 and bool(np.all((np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND))):
-            varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
-            for i, v in enumerate(views):
-                varr[i] = v.viewdev()
-            tv, tp = self._h2d_many([varr.view(np.uint8), progs.view(np.uint8)])
-            part = self._and2_partial(tp, tv, S, Q).sum(dim=1, dtype=torch.int64)
-            return part.t().contiguous().cpu().numpy()
-        tv = self._views_tensor(views)
-        tp = self._h2d(progs.view(np.uint8))
+        varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
+        for i, v in enumerate(views):
+            varr[i] = v.viewdev()
+        if self.use_and2 and max(v.container_count for v in views) < 0xFFFFFFFF and \
+                bool(np.all((np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND))):
+            progs = self._hot_leaf_first(progs, np.ones(Q, bool))
+            lr = progs["leaf_row"]
+            order = np.lexsort((lr[:, 1], lr[:, 0]))
+            tv, tp, to = self._h2d_many([varr.view(np.uint8), np.ascontiguousarray(progs[order]).view(np.uint8),
+                                         order.astype(np.int64)])
+            part = self._and2_partial(tp, tv, S, Q).sum(dim=1, dtype=torch.int64)  # [S, Q] in sorted order
+            out = torch.empty((Q, S), dtype=torch.int64, device=self.device)
+            out.index_copy_(0, to.view(torch.int64), part.t())
+            return out if as_tensor else out.cpu().numpy()
+        tv, tp = self._h2d_many([varr.view(np.uint8), progs.view(np.uint8)])
         ps = torch.zeros(Q * S, dtype=torch.int64, device=self.device)
         empty = torch.empty(0, dtype=torch.int64, device=self.device)
         self.ext.expr_count(tp, tv, S, empty, None, False, ps)
-        return ps.cpu().numpy().reshape(Q, S)
+        ps = ps.view(Q, S)
+        return ps if as_tensor else ps.cpu().numpy()
 
     def count_async(self, exprs: Sequence[object]):
         """Launch counts for a batch; returns the device int64[Q] result tensor.

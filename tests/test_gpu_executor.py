@@ -181,3 +181,40 @@ def test_topn_prefix_rounds_match_host(envs, q):
     finally:
         cpu.executor.gpu = None
     assert got == want
+
+
+def test_device_rank_cache_topn_batch_matches_host(envs):
+    """HBM rank caches + batched two-phase TopN (ops/topn.py) == host TopN."""
+    from pilosa_amd.ops.topn import DeviceRankCache, topn_batch
+    from pilosa_amd.pql import parse_string
+    cpu, gpu = envs
+    shards = cpu.holder.index("i").available_shards()
+    hv = gpu.view_arena("i", "h", "standard", shards)
+    cache = DeviceRankCache.from_view(hv, k=5000)
+    # the device cache order equals the fragments' rank caches (all rows fit)
+    for si, s in enumerate(shards):
+        frag = cpu.holder.fragment("i", "h", "standard", s)
+        host = [(p[0], p[1]) for p in frag._top_bitmap_pairs([])]
+        dev = [(int(r), int(c)) for r, c in zip(cache.rows[si], cache.counts[si]) if c > 0]
+        assert dev == host
+    cases = [("Row(f=2)", 5), ("Row(f=3)", 300), ("Row(g=1)", 1000), ("Row(f=0)", 50)]
+    srcs = [gpu.plan("i", parse_string(q).calls[0], shards) for q, _ in cases]
+    for n in sorted({n for _, n in cases}):
+        got = topn_batch(gpu.engine, hv, cache, srcs, n=n)
+        for (q, _), g in zip(cases, got):
+            want = cpu.q1("i", f"TopN(h, {q}, n={n})")
+            assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in want], (q, n)
+
+
+def test_cache_only_topn_matches_host(envs):
+    from pilosa_amd.ops.topn import DeviceRankCache, finish_topn, topn_cache_phase1, topn_cache_phase2_counts
+    cpu, gpu = envs
+    shards = cpu.holder.index("i").available_shards()
+    hv = gpu.view_arena("i", "h", "standard", shards)
+    cache = DeviceRankCache.from_view(hv, k=5000, keep_row_counts=True)
+    for n in (1, 10, 100):
+        t = topn_cache_phase1(cache, n)
+        ids = sorted(t)
+        got = finish_topn(ids, topn_cache_phase2_counts(cache, hv, ids), n)
+        want = cpu.q1("i", f"TopN(h, n={n})")
+        assert [(p.id, p.count) for p in got] == [(p.id, p.count) for p in want], n
