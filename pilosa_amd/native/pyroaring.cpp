@@ -226,6 +226,93 @@ inline uint64_t mix3(uint64_t a, uint64_t b, uint64_t c) {
 }
 }  // namespace
 
+// One shard of a synthetic arena (rowptr relative, meta payload offsets relative to the shard).
+struct ShardOut {
+  std::vector<uint32_t> rowptr;
+  std::vector<int64_t> meta;
+  std::vector<uint16_t> payload;
+  // n values sorted distinct (vals) or bitmap words (w) when n > 4096
+  void emit(int j, const uint16_t* vals, int n, const uint64_t* w) {
+    const int64_t off = int64_t(payload.size());
+    int type;
+    if (n <= pr::ARRAY_MAX) {
+      type = pr::CT_ARRAY;
+      payload.insert(payload.end(), vals, vals + n);
+      payload.resize((payload.size() + 7) & ~size_t(7), 0);
+    } else {
+      type = pr::CT_BITMAP;
+      const uint16_t* p = reinterpret_cast<const uint16_t*>(w);
+      payload.insert(payload.end(), p, p + 4096);
+    }
+    meta.push_back(int64_t(uint64_t(j) | (uint64_t(type) << 4) | (uint64_t(n) << 6) | (uint64_t(off / 8) << 23)));
+  }
+  // emit a container from bitmap words (array when sparse)
+  void emit_words(int j, const uint64_t* w, std::vector<uint16_t>& tmp) {
+    int n = 0;
+    for (int i = 0; i < 1024; i++) n += __builtin_popcountll(w[i]);
+    if (n == 0) return;
+    if (n > pr::ARRAY_MAX) {
+      emit(j, nullptr, n, w);
+      return;
+    }
+    tmp.clear();
+    for (int i = 0; i < 1024; i++)
+      for (uint64_t b = w[i]; b; b &= b - 1) tmp.push_back(uint16_t(i * 64 + __builtin_ctzll(b)));
+    emit(j, tmp.data(), n, nullptr);
+  }
+};
+
+// Concatenate per-shard outputs into (rows, rowptr[S][R+1], shard_base, meta, payload).
+static py::tuple concat_arena(std::vector<ShardOut>& outs, const std::vector<uint64_t>& rows, int nthreads) {
+  const int64_t S = int64_t(outs.size());
+  const int64_t R = int64_t(rows.size());
+  // concatenate
+  std::vector<int64_t> sb(S + 1, 0), pb(S + 1, 0);
+  for (int64_t s = 0; s < S; s++) {
+    sb[s + 1] = sb[s] + int64_t(outs[s].meta.size());
+    pb[s + 1] = pb[s] + int64_t(outs[s].payload.size());
+  }
+  py::array_t<uint64_t> rows_np(R);
+  for (int64_t r = 0; r < R; r++) rows_np.mutable_data()[r] = rows[r];
+  py::array_t<uint32_t> rowptr({(py::ssize_t)S, (py::ssize_t)(R + 1)});
+  py::array_t<int64_t> sbn(S + 1);
+  memcpy(sbn.mutable_data(), sb.data(), (S + 1) * 8);
+  py::array_t<int64_t> meta(std::max<int64_t>(sb[S], 1));
+  py::array_t<uint16_t> payload(std::max<int64_t>(pb[S], 8));
+  {
+    py::gil_scoped_release nogil;
+    uint32_t* rp = rowptr.mutable_data();
+    int64_t* mp = meta.mutable_data();
+    uint16_t* pp = payload.mutable_data();
+    if (sb[S] == 0) mp[0] = 0;
+    if (pb[S] == 0) memset(pp, 0, 16);
+    std::vector<std::thread> th;
+    std::atomic<int64_t> next{0};
+    int nt = std::max<int>(1, std::min<int64_t>(nthreads, S));
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&]() {
+        for (;;) {
+          int64_t s = next.fetch_add(1);
+          if (s >= S) break;
+          ShardOut& o = outs[s];
+          memcpy(rp + s * (R + 1), o.rowptr.data(), (R + 1) * 4);
+          const int64_t poff16 = pb[s] / 8;
+          for (size_t i = 0; i < o.meta.size(); i++) {
+            uint64_t m = uint64_t(o.meta[i]);
+            uint64_t off = (m >> 23) + uint64_t(poff16);
+            mp[sb[s] + int64_t(i)] = int64_t((m & ((1ull << 23) - 1)) | (off << 23));
+          }
+          if (!o.payload.empty()) memcpy(pp + pb[s], o.payload.data(), o.payload.size() * 2);
+          ShardOut().rowptr.swap(o.rowptr);
+          std::vector<int64_t>().swap(o.meta);
+          std::vector<uint16_t>().swap(o.payload);
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  return py::make_tuple(rows_np, rowptr, sbn, meta, payload);
+}
+
 static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t total_cols, int64_t nrows,
                                 double bits_per_col, double zs, double zv, uint64_t seed, int nthreads) {
   const int64_t S = shard_hi - shard_lo;
@@ -236,11 +323,6 @@ static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t tota
     for (int64_t r = 0; r < R; r++) Z += std::pow(zv + double(r), -zs);
     for (int64_t r = 0; r < R; r++) dens[r] = std::min(1.0, bits_per_col * std::pow(zv + double(r), -zs) / Z);
   }
-  struct ShardOut {
-    std::vector<uint32_t> rowptr;
-    std::vector<int64_t> meta;   // offsets relative to shard payload start
-    std::vector<uint16_t> payload;
-  };
   std::vector<ShardOut> outs(S);
   auto work = [&](int64_t s0, int64_t s1) {
     std::vector<uint64_t> pos;
@@ -250,21 +332,7 @@ static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t tota
       const int64_t cols = std::max<int64_t>(0, std::min<int64_t>(1 << 20, total_cols - shard * (1 << 20)));
       ShardOut& o = outs[si];
       o.rowptr.assign(R + 1, 0);
-      auto emit = [&](int j, const uint16_t* vals, int n, const uint64_t* w) {
-        // n values sorted distinct (vals) or bitmap words (w) when n > 4096
-        const int64_t off = int64_t(o.payload.size());
-        int type;
-        if (n <= pr::ARRAY_MAX) {
-          type = pr::CT_ARRAY;
-          o.payload.insert(o.payload.end(), vals, vals + n);
-          o.payload.resize((o.payload.size() + 7) & ~size_t(7), 0);
-        } else {
-          type = pr::CT_BITMAP;
-          const uint16_t* p = reinterpret_cast<const uint16_t*>(w);
-          o.payload.insert(o.payload.end(), p, p + 4096);
-        }
-        o.meta.push_back(int64_t(uint64_t(j) | (uint64_t(type) << 4) | (uint64_t(n) << 6) | (uint64_t(off / 8) << 23)));
-      };
+      auto emit = [&](int j, const uint16_t* vals, int n, const uint64_t* w) { o.emit(j, vals, n, w); };
       std::vector<uint16_t> vals;
       for (int64_t r = 0; r < R; r++) {
         o.rowptr[r] = uint32_t(o.meta.size());
@@ -326,51 +394,65 @@ static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t tota
       });
     for (auto& t : th) t.join();
   }
-  // concatenate
-  std::vector<int64_t> sb(S + 1, 0), pb(S + 1, 0);
-  for (int64_t s = 0; s < S; s++) {
-    sb[s + 1] = sb[s] + int64_t(outs[s].meta.size());
-    pb[s + 1] = pb[s] + int64_t(outs[s].payload.size());
-  }
-  py::array_t<uint64_t> rows_np(R);
-  for (int64_t r = 0; r < R; r++) rows_np.mutable_data()[r] = uint64_t(r);
-  py::array_t<uint32_t> rowptr({(py::ssize_t)S, (py::ssize_t)(R + 1)});
-  py::array_t<int64_t> sbn(S + 1);
-  memcpy(sbn.mutable_data(), sb.data(), (S + 1) * 8);
-  py::array_t<int64_t> meta(std::max<int64_t>(sb[S], 1));
-  py::array_t<uint16_t> payload(std::max<int64_t>(pb[S], 8));
+  std::vector<uint64_t> rows(R);
+  for (int64_t r = 0; r < R; r++) rows[r] = uint64_t(r);
+  return concat_arena(outs, rows, nthreads);
+}
+
+// Synthetic BSI arena (BASELINE config 4): a fraction `fill` of the columns
+// hold a value uniform in [vmin, vmax]; rows 0 = exists, 1 = sign, 2+i = bit i
+// of |value| (reference bsiExistsBit / bsiSignBit / bsiOffsetBit layout).
+static py::tuple gen_bsi_arena(int64_t shard_lo, int64_t shard_hi, int64_t total_cols, int depth, double fill,
+                               int64_t vmin, int64_t vmax, uint64_t seed, int nthreads) {
+  if (depth < 1 || depth > 62) throw std::invalid_argument("depth must be in 1..62");
+  const int64_t S = shard_hi - shard_lo;
+  const int64_t R = depth + 2;
+  std::vector<ShardOut> outs(S);
+  auto work = [&](int64_t si) {
+    const int64_t shard = shard_lo + si;
+    const int64_t cols = std::max<int64_t>(0, std::min<int64_t>(1 << 20, total_cols - shard * (1 << 20)));
+    ShardOut& o = outs[si];
+    o.rowptr.assign(R + 1, 0);
+    // planes[r][j][1024]
+    std::vector<uint64_t> planes(size_t(R) * 16 * 1024, 0);
+    Rng rng(mix3(seed, uint64_t(shard), 0xB51));
+    const uint64_t span = uint64_t(vmax - vmin) + 1;
+    for (int64_t c = 0; c < cols; c++) {
+      if (double(rng.next() >> 11) * (1.0 / 9007199254740992.0) >= fill) continue;
+      const int64_t v = vmin + int64_t(rng.next() % span);
+      const uint64_t u = uint64_t(v < 0 ? -v : v);
+      const int j = int(c >> 16), w = int((c & 0xffff) >> 6);
+      const uint64_t bit = 1ull << (c & 63);
+      planes[(size_t(0) * 16 + j) * 1024 + w] |= bit;
+      if (v < 0) planes[(size_t(1) * 16 + j) * 1024 + w] |= bit;
+      for (int i = 0; i < depth; i++)
+        if ((u >> i) & 1) planes[(size_t(2 + i) * 16 + j) * 1024 + w] |= bit;
+    }
+    std::vector<uint16_t> tmp;
+    for (int64_t r = 0; r < R; r++) {
+      o.rowptr[r] = uint32_t(o.meta.size());
+      for (int j = 0; j < 16; j++) o.emit_words(j, &planes[(size_t(r) * 16 + j) * 1024], tmp);
+    }
+    o.rowptr[R] = uint32_t(o.meta.size());
+  };
   {
     py::gil_scoped_release nogil;
-    uint32_t* rp = rowptr.mutable_data();
-    int64_t* mp = meta.mutable_data();
-    uint16_t* pp = payload.mutable_data();
-    if (sb[S] == 0) mp[0] = 0;
-    if (pb[S] == 0) memset(pp, 0, 16);
+    int nt = std::max<int>(1, std::min<int64_t>(nthreads, S));
     std::vector<std::thread> th;
     std::atomic<int64_t> next{0};
-    int nt = std::max<int>(1, std::min<int64_t>(nthreads, S));
     for (int t = 0; t < nt; t++)
       th.emplace_back([&]() {
         for (;;) {
           int64_t s = next.fetch_add(1);
           if (s >= S) break;
-          ShardOut& o = outs[s];
-          memcpy(rp + s * (R + 1), o.rowptr.data(), (R + 1) * 4);
-          const int64_t poff16 = pb[s] / 8;
-          for (size_t i = 0; i < o.meta.size(); i++) {
-            uint64_t m = uint64_t(o.meta[i]);
-            uint64_t off = (m >> 23) + uint64_t(poff16);
-            mp[sb[s] + int64_t(i)] = int64_t((m & ((1ull << 23) - 1)) | (off << 23));
-          }
-          if (!o.payload.empty()) memcpy(pp + pb[s], o.payload.data(), o.payload.size() * 2);
-          ShardOut().rowptr.swap(o.rowptr);
-          std::vector<int64_t>().swap(o.meta);
-          std::vector<uint16_t>().swap(o.payload);
+          work(s);
         }
       });
     for (auto& t : th) t.join();
   }
-  return py::make_tuple(rows_np, rowptr, sbn, meta, payload);
+  std::vector<uint64_t> rows(R);
+  for (int64_t r = 0; r < R; r++) rows[r] = uint64_t(r);
+  return concat_arena(outs, rows, nthreads);
 }
 
 // Rebuild a host Bitmap for one local shard of an arena (CPU oracle / baseline).
@@ -639,6 +721,9 @@ PYBIND11_MODULE(_roaring, m) {
   m.def("topn_replay", &topn_replay, py::arg("cand_rows"), py::arg("cand_cnts"), py::arg("shards"), py::arg("n"),
         py::arg("min_threshold"), py::arg("counted_rows"), py::arg("counted"),
         "Per-shard TopN heap replay over device-counted candidates -> (need_more, ids, counts)");
+  m.def("gen_bsi_arena", &gen_bsi_arena, py::arg("shard_lo"), py::arg("shard_hi"), py::arg("total_cols"),
+        py::arg("depth"), py::arg("fill"), py::arg("vmin"), py::arg("vmax"), py::arg("seed") = 1,
+        py::arg("nthreads") = 8, "synthetic BSI field arena (exists, sign, bit planes)");
   m.def("gen_zipf_arena", &gen_zipf_arena, py::arg("shard_lo"), py::arg("shard_hi"), py::arg("total_cols"),
         py::arg("nrows"), py::arg("bits_per_col") = 8.0, py::arg("zipf_s") = 1.6, py::arg("zipf_v") = 50.0,
         py::arg("seed") = 1, py::arg("nthreads") = 8);
