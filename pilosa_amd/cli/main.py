@@ -63,6 +63,12 @@ def cmd_server(args, stdout, stderr) -> int:
     log_stream = stderr
     if cfg.get("log-path"):
         log_stream = open(os.path.expanduser(cfg.get("log-path")), "a")
+        # like server/setup_logger.go: send the process's stderr (native
+        # library and interpreter messages too) to the log file
+        try:
+            os.dup2(log_stream.fileno(), 2)
+        except OSError:
+            pass
     logger = StandardLogger(log_stream, verbose=cfg.get("verbose"))
     if cfg.get("tracing.sampler-type") not in ("", "off", "none"):
         tracing.set_global_tracer(tracing.RecordingTracer())

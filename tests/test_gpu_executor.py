@@ -218,3 +218,26 @@ def test_cache_only_topn_matches_host(envs):
         got = finish_topn(ids, topn_cache_phase2_counts(cache, hv, ids), n)
         want = cpu.q1("i", f"TopN(h, n={n})")
         assert [(p.id, p.count) for p in got] == [(p.id, p.count) for p in want], n
+
+
+def test_generated_queries_gpu_vs_host(envs):
+    """Random PQL (pilosa_amd/testing/querygen.py) through the executor with
+    and without the GPU: identical results."""
+    from pilosa_amd.testing.querygen import QueryGenerator
+    cpu, gpu = envs
+    g = QueryGenerator(seed=21, set_fields=["f", "g"], int_fields=["n"], time_fields=["t"], max_row=14,
+                       int_range=(-1000, 100000))
+    qs = g.queries(120, depth=3)
+    want = [cpu.q("i", q) for q in qs]
+    cpu.executor.gpu = gpu
+    try:
+        n0 = gpu.launches
+        got = [cpu.q("i", q) for q in qs]
+        assert gpu.launches > n0 + 50
+    finally:
+        cpu.executor.gpu = None
+    for q, w, r in zip(qs, want, got):
+        if hasattr(w[0], "columns"):
+            assert cols(r[0]) == cols(w[0]), q
+        else:
+            assert r == w, q
