@@ -53,6 +53,9 @@ class Server:
         self.stats = new_stats_client(stats) if isinstance(stats, str) else (stats or NopStatsClient())
         self.holder = Holder(data_dir, max_opn=max_opn, stats=self.stats)
         self.client = InternalClient()
+        # liveness probes use a short timeout so a hung peer is noticed quickly
+        # (reference confirmNodeDown: 2 s per /version attempt, cluster.go:1699-1726)
+        self.probe_client = InternalClient(timeout=2.0)
         self.long_query_time = long_query_time
         self.anti_entropy_interval = anti_entropy_interval
         self.probe_interval = probe_interval
@@ -69,7 +72,7 @@ class Server:
         self.mesh_block = mesh_block
         self.translation_primary = URI.parse(translation_primary_url) if translation_primary_url else None
         self.tls_certificate, self.tls_key = tls_certificate, tls_key
-        self.client.skip_verify = tls_skip_verify
+        self.client.skip_verify = self.probe_client.skip_verify = tls_skip_verify
         self.diagnostics = None
         self.diagnostics_host, self.diagnostics_interval = diagnostics_host, diagnostics_interval
         self.gc_notifier = None
@@ -398,7 +401,7 @@ class Server:
                 if n.id == self.node.id:
                     continue
                 try:
-                    self.client.version(n.uri)
+                    self.probe_client.version(n.uri)
                     self._misses[n.id] = 0
                     if n.state != NODE_READY:
                         changed |= self.cluster.set_node_state(n.id, NODE_READY)
