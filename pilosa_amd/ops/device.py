@@ -179,6 +179,85 @@ class DeviceView:
         self.t_payload = nb(payload.view(np.int16)).to(self.device)
         self.container_count = int(shard_base[-1])
         self._row_index = None
+        self.generation = 0          # bumped by in-place shard updates
+        self._sb_host = np.asarray(shard_base, dtype=np.int64).copy()
+        self._cap = None             # per-shard meta capacity (patchable arenas)
+        self.payload_used = int(payload.shape[0])
+        self.garbage_u16 = 0
+
+    # ------------------------------------------------------------ patchable layout
+    @classmethod
+    def patchable(cls, rows, rowptr, shard_base, meta, payload, device, shards=(), slack: float = 0.125,
+                  payload_slack: float = 0.25) -> "DeviceView":
+        """Like the constructor, but every shard's metadata segment and the
+        payload get spare capacity so a changed shard can be rewritten in
+        place (:meth:`update_shard`) instead of re-uploading the whole view."""
+        shard_base = np.asarray(shard_base, dtype=np.int64)
+        n = np.diff(shard_base)
+        cap = n + np.maximum(16, (n * slack).astype(np.int64))
+        nsb = np.zeros(len(shard_base), np.int64)
+        nsb[1:] = np.cumsum(cap)
+        nmeta = np.zeros(max(int(nsb[-1]), 1), np.int64)
+        if len(meta) and int(shard_base[-1]):
+            src = np.repeat(nsb[:-1] - shard_base[:-1], n) + np.arange(int(shard_base[-1]))
+            nmeta[src] = meta[:int(shard_base[-1])]
+        used = int(payload.shape[0])
+        pcap = used + max(4096 * 16, int(used * payload_slack))
+        npay = np.zeros(pcap, np.uint16)
+        npay[:used] = payload
+        self = cls(rows, rowptr, nsb, nmeta, npay, device, shards)
+        self.container_count = int(nsb[-1])
+        self._cap = cap
+        self.payload_used = used
+        return self
+
+    def update_shard(self, si: int, bitmap) -> bool:
+        """Rewrite local shard ``si`` from a host bitmap in place (metadata
+        segment, rowptr row, payload appended at the tail).  False when the
+        view must be rebuilt instead: not patchable, a row id outside the
+        directory, segment or payload capacity exceeded, or too much garbage."""
+        import torch
+
+        from pilosa_amd import _roaring
+
+        if self._cap is None:
+            return False
+        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], 16, 1)
+        n_new = int(sb_s[-1])
+        if n_new > int(self._cap[si]):
+            return False
+        dense = self.dense_many(rows_s) if len(rows_s) else np.zeros(0, np.int64)
+        if len(dense) and (dense < 0).any():
+            return False
+        npay = int(pay_s.shape[0]) if n_new else 0
+        if self.payload_used + npay > int(self.t_payload.numel()):
+            return False
+        # rowptr over the view's full row directory
+        counts = np.zeros(self.D, np.int64)
+        if len(dense):
+            counts[dense] = np.diff(rp_s[0].astype(np.int64))
+        rowptr = np.zeros(self.D + 1, np.int64)
+        rowptr[1:] = np.cumsum(counts)
+        m = np.zeros(int(self._cap[si]), np.int64)
+        if n_new:
+            mm = meta_s[:n_new].astype(np.int64)
+            off = (mm.view(np.uint64) >> np.uint64(23)) + np.uint64(self.payload_used // 8)
+            m[:n_new] = ((mm.view(np.uint64) & np.uint64((1 << 23) - 1)) | (off << np.uint64(23))).view(np.int64)
+        base = int(self._sb_host[si])
+        dev = self.device
+        self.t_meta[base:base + len(m)].copy_(torch.from_numpy(m).to(dev))
+        self.t_rowptr.view(self.S, self.D + 1)[si].copy_(torch.from_numpy(rowptr.astype(np.int32)).to(dev))
+        if npay:
+            self.t_payload[self.payload_used:self.payload_used + npay].copy_(
+                torch.from_numpy(pay_s[:npay].view(np.int16)).to(dev))
+        self.payload_used += npay
+        self.garbage_u16 += npay  # approximate: the shard's previous payload is now unreachable
+        self.generation += 1
+        return True
+
+    def needs_compaction(self) -> bool:
+        """Dead payload from in-place updates exceeds half the buffer."""
+        return self._cap is not None and self.garbage_u16 > int(self.t_payload.numel()) // 2
 
     @classmethod
     def from_device(cls, rows: np.ndarray, t_rowptr, t_shard_base, t_meta, t_payload, device, shards,
@@ -195,13 +274,19 @@ class DeviceView:
         self.t_rowptr, self.t_shard_base, self.t_meta, self.t_payload = t_rowptr, t_shard_base, t_meta, t_payload
         self.container_count = int(container_count)
         self._row_index = None
+        self.generation = 0
+        self._cap = None
+        self.payload_used = int(t_payload.numel())
+        self.garbage_u16 = 0
         return self
 
     @classmethod
-    def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=()):
+    def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=(), patchable: bool = False):
         from pilosa_amd import _roaring
 
         rows, rowptr, sb, meta, payload = _roaring.build_arena(list(bitmaps), 16, 8)
+        if patchable:
+            return cls.patchable(rows, rowptr, sb, meta, payload, device, shards)
         return cls(rows, rowptr, sb, meta, payload, device, shards)
 
     def nbytes(self) -> int:

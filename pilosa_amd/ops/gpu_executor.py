@@ -53,6 +53,8 @@ class GpuExecutor:
         self._bsi_views: Dict[Tuple, DeviceView] = {}  # predicate results (small LRU)
         self.mu = threading.RLock()
         self.launches = 0
+        self.rebuilds = 0        # full view uploads
+        self.shard_updates = 0   # in-place shard segment rewrites
 
     # ------------------------------------------------------------ arenas
     def view_arena(self, index: str, field: str, view: str, shards: Sequence[int]) -> Optional[DeviceView]:
@@ -67,6 +69,24 @@ class GpuExecutor:
             hit = self._arenas.get(key)
             if hit is not None and hit[0] == sig:
                 return hit[1]
+            if hit is not None and len(hit[0]) == len(sig) and not hit[1].needs_compaction():
+                # only some shards changed: rewrite their segments in place
+                dv = hit[1]
+                ok = True
+                for si, (old, new, f) in enumerate(zip(hit[0], sig, frags)):
+                    if old == new:
+                        continue
+                    if f is None:
+                        ok = False
+                        break
+                    with f.mu:
+                        ok = dv.update_shard(si, f.storage)
+                    if not ok:
+                        break
+                    self.shard_updates += 1
+                if ok:
+                    self._arenas[key] = (sig, dv)
+                    return dv
             bms = []
             for f in frags:
                 if f is None:
@@ -74,7 +94,8 @@ class GpuExecutor:
                 else:
                     with f.mu:
                         bms.append(f.storage)
-            dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards))
+            dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards), patchable=True)
+            self.rebuilds += 1
             self._arenas[key] = (sig, dv)
             return dv
 
@@ -100,7 +121,7 @@ class GpuExecutor:
             op, p1, p2 = "between", int(args[0]), int(args[1])
         else:
             op, p1, p2 = args[0], int(args[1]), 0
-        key = (id(bv), op, p1, p2, b.bit_depth)
+        key = (id(bv), bv.generation, op, p1, p2, b.bit_depth)
         with self.mu:
             rv = self._bsi_views.get(key)
             if rv is None:

@@ -241,3 +241,28 @@ def test_generated_queries_gpu_vs_host(envs):
             assert cols(r[0]) == cols(w[0]), q
         else:
             assert r == w, q
+
+
+def test_incremental_shard_updates(envs):
+    """Writes to a few shards patch the device arena in place (no full
+    re-upload); a new row id outside the directory forces a rebuild."""
+    cpu, gpu = envs
+    cpu.executor.gpu = gpu
+    try:
+        q = "Count(Intersect(Row(g=1), Row(f=0)))"
+        cpu.q1("i", q)
+        r0, u0 = gpu.rebuilds, gpu.shard_updates
+        for k in range(20):
+            cpu.q("i", f"Set({(k % 4) * SW + 777 + k}, g=1) Set({(k % 4) * SW + 777 + k}, f=0)")
+            got = cpu.q1("i", q)
+            cpu.executor.gpu = None
+            want = cpu.q1("i", q)
+            cpu.executor.gpu = gpu
+            assert got == want
+        assert gpu.rebuilds == r0, "writes to existing rows must not re-upload the view"
+        assert gpu.shard_updates > u0
+        cpu.q("i", f"Set({2 * SW + 5}, g=4321)")  # new row id -> rebuild of g's view
+        got = cpu.q1("i", "Count(Row(g=4321))")
+        assert got == 1 and gpu.rebuilds > r0
+    finally:
+        cpu.executor.gpu = None
