@@ -19,7 +19,7 @@ hipStream_t cur_stream(const torch::Tensor& t) {
 }
 
 void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor out,
-                c10::optional<torch::Tensor> per_key, bool fast, c10::optional<torch::Tensor> per_shard) {
+                c10::optional<torch::Tensor> per_key, int64_t mode, c10::optional<torch::Tensor> per_shard) {
   check_dev(progs, "progs");
   check_dev(views, "views");
   TORCH_CHECK(progs.numel() % sizeof(pk::QueryProg) == 0, "progs size");
@@ -46,7 +46,7 @@ void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
     ps = per_shard->data_ptr<int64_t>();
   }
   pk::launch_expr_count(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
-                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), o, pk_, ps, fast,
+                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), o, pk_, ps, int(mode),
                         cur_stream(progs));
 }
 
@@ -151,7 +151,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("MAXLEAF") = pk::MAXLEAF;
   m.attr("MAXPROG") = pk::MAXPROG;
   m.def("expr_count", &expr_count, "batched boolean-expression count over all local shards",
-        py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("fast") = false,
+        py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("mode") = 0,
         py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
   m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),

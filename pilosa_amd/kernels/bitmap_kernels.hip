@@ -305,11 +305,40 @@ __device__ __forceinline__ int and2_count(const ViewDev& va, int64_t ma, const V
 constexpr int WAVES_PER_BLOCK = 4;
 
 // Count kernel: out[q] += |program(q)| over all local shards.
-// FAST=true handles only Count(Row) and Count(Intersect(a,b)) programs (no
-// register tile stack -> far fewer VGPRs, higher occupancy); the host routes
-// every other program shape to FAST=false.
-template <bool FAST>
-__global__ __launch_bounds__(256) void expr_count_kernel(const QueryProg* __restrict__ progs, int Q,
+// MODE 1 (fast) handles only Count(Row) and Count(Intersect(a,b)) programs
+// (no register tile stack -> far fewer VGPRs, higher occupancy); MODE 2
+// (flat) handles left folds "l0 l1 op l2 op ..." (Union/Intersect/Difference/
+// Xor of leaves, time-range view unions, Not) with one accumulator tile and
+// one load tile; MODE 0 interprets any program with the 4-deep tile stack.
+
+// Flat fold: acc = l0; acc = acc op_i l_i.
+__device__ __forceinline__ void load_leaf(const QueryProg& qp, const ViewDev* views, int s, int j, WaveScratch& ws,
+                                          int k, Tile& t) {
+  const int32_t c = ws.slot[k][j];
+  if (c < 0) {
+    tile_zero(t);
+  } else {
+    const ViewDev& v = views[qp.leaf_view[k]];
+    tile_load(t, v.payload, v.meta[v.shard_base[s] + c], ws.lb);
+  }
+}
+
+__device__ __forceinline__ void eval_flat(const QueryProg& qp, const ViewDev* views, int s, int j, WaveScratch& ws,
+                                          Tile& acc) {
+  load_leaf(qp, views, s, j, ws, qp.prog[0], acc);
+  for (int pc = 1; pc + 1 < qp.nprog; pc += 2) {
+    Tile t;
+    load_leaf(qp, views, s, j, ws, qp.prog[pc], t);
+    const int op = qp.prog[pc + 1];
+    if (op == OP_AND) tile_op<OP_AND>(acc, t);
+    else if (op == OP_OR) tile_op<OP_OR>(acc, t);
+    else if (op == OP_XOR) tile_op<OP_XOR>(acc, t);
+    else tile_op<OP_ANDNOT>(acc, t);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, MODE == 0 ? 1 : 4) void expr_count_kernel(const QueryProg* __restrict__ progs, int Q,
                                                          const ViewDev* __restrict__ views, int S,
                                                          unsigned long long* __restrict__ out,
                                                          int32_t* __restrict__ per_key,
@@ -338,7 +367,7 @@ __global__ __launch_bounds__(256) void expr_count_kernel(const QueryProg* __rest
         total = n;
         if (per_key) per_key[(int64_t(q) * S + s) * 16 + lane] = n;
       }
-    } else if (FAST) {
+    } else if (MODE == 1) {
       // Count(Intersect(leaf0, leaf1)) with a container type-pair dispatch
       const ViewDev& va = views[qp.leaf_view[0]];
       const ViewDev& vb = views[qp.leaf_view[1]];
@@ -352,7 +381,8 @@ __global__ __launch_bounds__(256) void expr_count_kernel(const QueryProg* __rest
       for (uint32_t cm = cand; cm; cm &= cm - 1) {
         const int j = __builtin_ctz(cm);
         Tile acc;
-        eval_tile(qp, views, s, j, ws, acc);
+        if (MODE == 2) eval_flat(qp, views, s, j, ws, acc);
+        else eval_tile(qp, views, s, j, ws, acc);
         int c = tile_popc(acc);
         if (per_key) {
           const int64_t cj = wave_sum_i64(c);
@@ -842,15 +872,16 @@ static inline unsigned grid_for(int64_t items) {
 }
 
 void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int S, unsigned long long* out,
-                       int32_t* per_key, int64_t* per_shard, bool fast, hipStream_t st) {
+                       int32_t* per_key, int64_t* per_shard, int mode, hipStream_t st) {
   const int64_t items = int64_t(Q) * S;
   if (items == 0) return;
-  if (fast && per_key == nullptr)
-    hipLaunchKernelGGL(expr_count_kernel<true>, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
-                       Q, views, S, out, per_key, per_shard);
+  const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
+  if (mode == 1 && per_key == nullptr)
+    hipLaunchKernelGGL(expr_count_kernel<1>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
+  else if (mode == 2)
+    hipLaunchKernelGGL(expr_count_kernel<2>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
   else
-    hipLaunchKernelGGL(expr_count_kernel<false>, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
-                       Q, views, S, out, per_key, per_shard);
+    hipLaunchKernelGGL(expr_count_kernel<0>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
 }
 
 void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views, int S, const int32_t* counts,

@@ -49,7 +49,7 @@ struct BsiArgs {
 };
 
 void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int S, unsigned long long* out,
-                       int32_t* per_key, int64_t* per_shard, bool fast, hipStream_t st);
+                       int32_t* per_key, int64_t* per_shard, int mode, hipStream_t st);
 void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views, int S, const int32_t* counts,
                              const int64_t* offs, uint16_t* outp, hipStream_t st);
 // Count(Intersect(a, b)) via key-major pair kernels (pair_kernels.hip):

@@ -83,6 +83,9 @@ class Fragment:
         self.ops = 0
         self.max_row_id = 0
         self.version = 0
+        # per-consumer dirty-row sets (device arenas patch only changed rows);
+        # None = unknown / too many -> the consumer refreshes the whole shard
+        self._dirty_subs: Dict[object, Optional[set]] = {}
         self.mu = threading.RLock()
         self._fh = None
         self._lockfd = None
@@ -239,7 +242,50 @@ class Fragment:
     def bit(self, row_id: int, col: int) -> bool:
         return self.storage.contains(self._pos(row_id, col))
 
-    def _after_row_change(self, row_id: int, bulk: bool = False):
+    DIRTY_LIMIT = 4096
+
+    def _note_rows(self, rows):
+        for k, d in self._dirty_subs.items():
+            if d is not None:
+                d[0].update(rows)
+                if len(d[0]) + len(d[1]) > self.DIRTY_LIMIT:
+                    self._dirty_subs[k] = None
+
+    def _note_container(self, pos: int):
+        """A single-bit change: only container (row, key) of ``pos`` changed."""
+        key = int(pos) >> 16
+        for k, d in self._dirty_subs.items():
+            if d is not None:
+                d[1].add(key)
+                if len(d[0]) + len(d[1]) > self.DIRTY_LIMIT:
+                    self._dirty_subs[k] = None
+
+    def _note_unknown(self):
+        for k in self._dirty_subs:
+            self._dirty_subs[k] = None
+
+    def take_dirty(self, token):
+        """(rows, container keys) changed since ``token`` last asked; container
+        keys are row*16 + local key.  None = unknown -> refresh everything;
+        the first call registers the token and returns None."""
+        with self.mu:
+            if token not in self._dirty_subs:
+                self._dirty_subs[token] = (set(), set())
+                return None
+            d = self._dirty_subs[token]
+            self._dirty_subs[token] = (set(), set())
+            return d
+
+    def drop_dirty(self, token):
+        with self.mu:
+            self._dirty_subs.pop(token, None)
+
+    def _after_row_change(self, row_id: int, bulk: bool = False, pos: Optional[int] = None):
+        if self._dirty_subs:
+            if pos is None:
+                self._note_rows((row_id,))
+            else:
+                self._note_container(pos)
         self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
         if self.cache_type != CACHE_TYPE_NONE:
             n = self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
@@ -256,7 +302,7 @@ class Fragment:
         if not changed:
             return False
         self._log(OP_ADD, p)
-        self._after_row_change(row_id)
+        self._after_row_change(row_id, pos=p)
         self._increment_opn(1)
         if self.stats:
             self.stats.count("setBit", 1)
@@ -268,7 +314,7 @@ class Fragment:
         if not changed:
             return False
         self._log(OP_REMOVE, p)
-        self._after_row_change(row_id)
+        self._after_row_change(row_id, pos=p)
         self._increment_opn(1)
         if self.stats:
             self.stats.count("clearBit", 1)
@@ -315,6 +361,7 @@ class Fragment:
     def clear_row(self, row_id: int) -> bool:
         with self.mu:
             changed = self.storage.clear_row(row_id, CONTAINERS_PER_ROW)
+            self._note_rows((row_id,))
             self.cache.add(row_id, 0)
             self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
             self.version += 1
@@ -752,6 +799,7 @@ class Fragment:
     def import_roaring(self, data: bytes, clear: bool = False) -> int:
         with self.mu:
             changed, rowdelta = self.storage.import_roaring(data, clear, CONTAINERS_PER_ROW)
+            self._note_rows(int(r) for r, d in rowdelta.items() if d)
             if changed:
                 self._log(OP_REMOVE_ROARING if clear else OP_ADD_ROARING, roaring=data, opn=changed)
             any_changed = False
@@ -860,6 +908,7 @@ class Fragment:
                 if ti.name == "data":
                     with self.mu:
                         self.storage = Bitmap.from_bytes(payload)
+                        self._note_unknown()
                         tmp = self.path + ".snapshotting"
                         with open(tmp, "wb") as fh:
                             fh.write(payload)

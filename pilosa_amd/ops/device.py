@@ -23,7 +23,19 @@ MAXLEAF = 16
 MAXPROG = 32
 OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 32, 33, 34, 35
 # count-batch kernel routes
-KIND_AND2, KIND_ROW, KIND_GENERIC = 0, 1, 2
+KIND_AND2, KIND_ROW, KIND_GENERIC, KIND_FLAT = 0, 1, 2, 3
+_KERNEL_MODE = {KIND_ROW: 1, KIND_GENERIC: 0, KIND_FLAT: 2}  # expr_count_kernel<MODE>
+
+
+def flat_mask(progs: np.ndarray) -> np.ndarray:
+    """Programs that are left folds "l0 l1 op l2 op ..." (flat kernel mode)."""
+    pg = progs["prog"].astype(np.int32)
+    n = progs["nprog"].astype(np.int64)
+    pos = np.arange(pg.shape[1])
+    want_leaf = (pos == 0) | (pos % 2 == 1)
+    valid = pos[None, :] < n[:, None]
+    ok = np.where(valid, (pg < OP_AND) == want_leaf[None, :], True).all(axis=1)
+    return ok & (n >= 3) & (n % 2 == 1)
 _OPS = {"and": OP_AND, "or": OP_OR, "xor": OP_XOR, "andnot": OP_ANDNOT}
 
 QPROG_DTYPE = np.dtype([("nleaf", "<i4"), ("nprog", "<i4"), ("leaf_view", "<i4", (MAXLEAF,)),
@@ -202,14 +214,97 @@ class DeviceView:
             src = np.repeat(nsb[:-1] - shard_base[:-1], n) + np.arange(int(shard_base[-1]))
             nmeta[src] = meta[:int(shard_base[-1])]
         used = int(payload.shape[0])
-        pcap = used + max(4096 * 16, int(used * payload_slack))
+        pcap = used + max(8 << 20, int(used * payload_slack))  # >= 16 MB of room for patches
         npay = np.zeros(pcap, np.uint16)
         npay[:used] = payload
         self = cls(rows, rowptr, nsb, nmeta, npay, device, shards)
         self.container_count = int(nsb[-1])
         self._cap = cap
         self.payload_used = used
+        # host mirrors of the metadata for row-level patches
+        self._meta_host = nmeta
+        self._rowptr_host = np.asarray(rowptr, dtype=np.int64).reshape(self.S, self.D + 1).copy()
         return self
+
+    def update_rows(self, si: int, rows, storage, keys=()) -> bool:
+        """Patch local shard ``si`` in place: every container of ``rows`` (row
+        ids) and the single containers ``keys`` (row*16 + local key) are
+        rebuilt from the fragment storage and spliced into the shard's
+        metadata segment; the payload grows by just those containers."""
+        import torch
+
+        from pilosa_amd import _roaring
+
+        if self._cap is None:
+            return False
+        rows = set(int(r) for r in rows)
+        keys = sorted(int(k) for k in keys if (int(k) >> 4) not in rows)
+        if not rows and not keys:
+            return True
+        touched = sorted(rows | {k >> 4 for k in keys})
+        dense_of = dict(zip(touched, self.dense_many(np.array(touched, np.uint64)).tolist()))
+        if any(d < 0 for d in dense_of.values()):
+            return False
+        sw, cw = 1 << 20, 1 << 16
+        parts = [storage.offset_range(r * sw, r * sw, (r + 1) * sw) for r in sorted(rows)]
+        parts += [storage.offset_range(k * cw, k * cw, (k + 1) * cw) for k in keys]
+        part = _roaring.Bitmap()
+        part.union_in_place(parts)
+        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([part], 16, 1)
+        n_part = int(sb_s[-1])
+        npay = int(pay_s.shape[0]) if n_part else 0
+        if self.payload_used + npay > int(self.t_payload.numel()):
+            return False
+        new_meta = np.zeros(n_part, np.int64)
+        if n_part:
+            mm = meta_s[:n_part].astype(np.int64).view(np.uint64)
+            off = (mm >> np.uint64(23)) + np.uint64(self.payload_used // 8)
+            new_meta = ((mm & np.uint64((1 << 23) - 1)) | (off << np.uint64(23))).view(np.int64)
+        fresh = {}  # row id -> new metas of that row (only the rebuilt keys)
+        rps = rp_s[0].astype(np.int64) if len(rows_s) else None
+        for k, r in enumerate(rows_s.tolist()):
+            fresh[int(r)] = new_meta[rps[k]:rps[k + 1]]
+        keys_of: Dict[int, set] = {}
+        for k in keys:
+            keys_of.setdefault(k >> 4, set()).add(k & 15)
+        base = int(self._sb_host[si])
+        rp_old = self._rowptr_host[si]
+        seg_old = self._meta_host[base:base + int(rp_old[-1])]
+        counts = np.diff(rp_old)
+        pieces, cur = [], 0
+        for r in touched:
+            d = dense_of[r]
+            pieces.append(seg_old[rp_old[cur]:rp_old[d]])
+            nm = fresh.get(r, np.zeros(0, np.int64))
+            if r not in rows:  # splice single keys into the row's old containers
+                old = seg_old[rp_old[d]:rp_old[d + 1]]
+                ks = keys_of[r]
+                keep = old[~np.isin(old & 15, list(ks))]
+                nm = np.concatenate([keep, nm])
+                nm = nm[np.argsort(nm & 15, kind="stable")]
+            pieces.append(nm)
+            counts[d] = len(nm)
+            cur = d + 1
+        pieces.append(seg_old[rp_old[cur]:rp_old[-1]])
+        seg = np.concatenate(pieces)
+        if len(seg) > int(self._cap[si]):
+            return False
+        rp_new = np.zeros(self.D + 1, np.int64)
+        rp_new[1:] = np.cumsum(counts)
+        full = np.zeros(int(self._cap[si]), np.int64)
+        full[:len(seg)] = seg
+        dev = self.device
+        if npay:
+            self.t_payload[self.payload_used:self.payload_used + npay].copy_(
+                torch.from_numpy(pay_s[:npay].view(np.int16)).to(dev))
+        self.t_meta[base:base + len(full)].copy_(torch.from_numpy(full).to(dev))
+        self.t_rowptr.view(self.S, self.D + 1)[si].copy_(torch.from_numpy(rp_new.astype(np.int32)).to(dev))
+        self._meta_host[base:base + len(full)] = full
+        self._rowptr_host[si] = rp_new
+        self.payload_used += npay
+        self.garbage_u16 += npay
+        self.generation += 1
+        return True
 
     def update_shard(self, si: int, bitmap) -> bool:
         """Rewrite local shard ``si`` from a host bitmap in place (metadata
@@ -247,6 +342,8 @@ class DeviceView:
         dev = self.device
         self.t_meta[base:base + len(m)].copy_(torch.from_numpy(m).to(dev))
         self.t_rowptr.view(self.S, self.D + 1)[si].copy_(torch.from_numpy(rowptr.astype(np.int32)).to(dev))
+        self._meta_host[base:base + len(m)] = m
+        self._rowptr_host[si] = rowptr
         if npay:
             self.t_payload[self.payload_used:self.payload_used + npay].copy_(
                 torch.from_numpy(pay_s[:npay].view(np.int16)).to(dev))
@@ -443,7 +540,8 @@ class GpuEngine:
         if not self.use_and2 or max(v.container_count for v in views) >= 0xFFFFFFFF:
             is_row = is_row | is_and2
             is_and2 = np.zeros_like(is_and2)
-        kind = np.where(is_and2, KIND_AND2, np.where(is_row, KIND_ROW, KIND_GENERIC))
+        kind = np.where(is_and2, KIND_AND2, np.where(is_row, KIND_ROW,
+                                                      np.where(flat_mask(progs), KIND_FLAT, KIND_GENERIC)))
         if is_and2.any():
             progs = self._hot_leaf_first(progs, is_and2)
             lr = progs["leaf_row"]
@@ -452,7 +550,7 @@ class GpuEngine:
             varr[i] = v.viewdev()
         host = [varr.view(np.uint8)]
         meta = []
-        for k in (KIND_AND2, KIND_ROW, KIND_GENERIC):
+        for k in (KIND_AND2, KIND_ROW, KIND_FLAT, KIND_GENERIC):
             sel = np.nonzero(kind == k)[0]
             if len(sel) == 0:
                 continue
@@ -502,7 +600,7 @@ class GpuEngine:
                 o = self._and2_partial(tp, tv, S, n).sum(dim=(0, 1), dtype=torch.int64)
             else:
                 o = torch.zeros(n, dtype=torch.int64, device=self.device)
-                self.ext.expr_count(tp, tv, S, o, None, kind == KIND_ROW)
+                self.ext.expr_count(tp, tv, S, o, None, _KERNEL_MODE[kind])
             out.index_copy_(0, ti, o)
         return out
 
@@ -559,7 +657,7 @@ class GpuEngine:
         tv, tp = self._h2d_many([varr.view(np.uint8), progs.view(np.uint8)])
         ps = torch.zeros(Q * S, dtype=torch.int64, device=self.device)
         empty = torch.empty(0, dtype=torch.int64, device=self.device)
-        self.ext.expr_count(tp, tv, S, empty, None, False, ps)
+        self.ext.expr_count(tp, tv, S, empty, None, 2 if bool(flat_mask(progs).all()) else 0, ps)
         ps = ps.view(Q, S)
         return ps if as_tensor else ps.cpu().numpy()
 
@@ -583,7 +681,8 @@ class GpuEngine:
             return [], []
         tp, tv = self.upload_batch(progs, views)
         counts = torch.zeros(S * 16, dtype=torch.int32, device=self.device)
-        self.ext.expr_count(tp, tv, S, torch.empty(0, dtype=torch.int64, device=self.device), counts, False)
+        self.ext.expr_count(tp, tv, S, torch.empty(0, dtype=torch.int64, device=self.device), counts,
+                            2 if bool(flat_mask(progs).all()) else 0)
         sizes = torch.where(counts > 4096, torch.full_like(counts, 4096), (counts + 7) // 8 * 8).to(torch.int64)
         sizes = torch.where(counts > 0, sizes, torch.zeros_like(sizes))
         offs = torch.cumsum(sizes, 0) - sizes

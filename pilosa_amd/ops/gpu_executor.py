@@ -55,6 +55,7 @@ class GpuExecutor:
         self.launches = 0
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
+        self.row_updates = 0     # ... of which only the changed rows were re-sent
 
     # ------------------------------------------------------------ arenas
     def view_arena(self, index: str, field: str, view: str, shards: Sequence[int]) -> Optional[DeviceView]:
@@ -80,21 +81,36 @@ class GpuExecutor:
                         ok = False
                         break
                     with f.mu:
-                        ok = dv.update_shard(si, f.storage)
+                        dirty = f.take_dirty(dv.token) if old is not None and old[0] == id(f) else None
+                        if dirty is not None:
+                            ok = dv.update_rows(si, dirty[0], f.storage, keys=dirty[1])
+                            self.row_updates += ok
+                        else:
+                            ok = False
+                        if not ok:
+                            f.take_dirty(dv.token)
+                            ok = dv.update_shard(si, f.storage)
                     if not ok:
                         break
                     self.shard_updates += 1
                 if ok:
                     self._arenas[key] = (sig, dv)
                     return dv
+            if hit is not None:
+                for f in frags:
+                    if f is not None:
+                        f.drop_dirty(hit[1].token)
+            token = object()  # dirty-row subscription of the new arena
             bms = []
             for f in frags:
                 if f is None:
                     bms.append(None)
                 else:
                     with f.mu:
+                        f.take_dirty(token)  # register before the contents are read
                         bms.append(f.storage)
             dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards), patchable=True)
+            dv.token = token
             self.rebuilds += 1
             self._arenas[key] = (sig, dv)
             return dv
