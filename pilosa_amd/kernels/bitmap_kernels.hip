@@ -34,10 +34,15 @@ namespace pk {
 
 __device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Wave-wide sum through DPP row ops (ockl) instead of six dependent
+// ds_bpermute round trips (__shfl_xor).
+extern "C" __device__ long __ockl_wfred_add_i64(long);
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) { return int64_t(__ockl_wfred_add_i64(long(v))); }
+
+// broadcast lane `src` (wave-uniform) with scalar readlanes, no LDS pipe
+__device__ __forceinline__ int64_t rl_i64(int64_t v, int src) {
+  return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint64_t(v) >> 32), src))) << 32) |
+                 uint32_t(__builtin_amdgcn_readlane(int(v), src)));
 }
 
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
@@ -493,7 +498,7 @@ __global__ __launch_bounds__(256) void bsi_sum_kernel(const QueryProg* __restric
     }
     const uint64_t b = __ballot(found >= 0);
     if (!b) return -1;
-    return __shfl(found, __builtin_ctzll(b), 64);
+    return rl_i64(found, int(__builtin_ctzll(b)));
   };
   int64_t lo_e, hi_e;
   row_range(bsi.row_exists, lo_e, hi_e);
@@ -568,7 +573,7 @@ __device__ __forceinline__ int64_t bsi_find(const BsiCtx& c, int64_t d) {
   if (lane < hi - lo && meta_j(c.bv.meta[c.base + lo + lane]) == c.j) found = c.base + lo + lane;
   const uint64_t b = __ballot(found >= 0);
   if (!b) return -1;
-  return __shfl(found, __builtin_ctzll(b), 64);
+  return rl_i64(found, int(__builtin_ctzll(b)));
 }
 
 __device__ __forceinline__ void bsi_row(const BsiCtx& c, int64_t d, Tile& t) {

@@ -39,11 +39,10 @@ constexpr int PAIR_WAVES = 4;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// Wave-wide sum through DPP row ops (ockl), not __shfl_xor: the latter is six
+// dependent ds_bpermute round trips through the LDS pipe per call.
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+__device__ __forceinline__ int wave_sum(int v) { return __ockl_wfred_add_i32(v); }
 
 __device__ __forceinline__ uint32_t xcd_remap_blocks(uint32_t bid, uint32_t nblk) {
   const uint32_t nx = 8;
