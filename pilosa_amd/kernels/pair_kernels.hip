@@ -233,7 +233,9 @@ __device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* 
   return runs_in_lds(lb, p);
 }
 
-template <int CQ>
+// DBG (profiling builds only): bit 0 = never stage (probe the stale LDS
+// bitmap), bit 1 = skip counting; results are wrong, timings isolate costs.
+template <int CQ, int DBG = 0>
 __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const QueryProg* __restrict__ progs, int Q,
                                                                     const ViewDev* __restrict__ views, int S,
                                                                     const uint2* __restrict__ pairs,
@@ -280,19 +282,32 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
     const uint16_t* pB = payload_of(views[vb], mB);
     const int tA = meta_type(mA), tB = meta_type(mB);
     int c;
-    if (a == cached && va == cached_v) {
+    if (DBG) {
+      c = 0;
+      if (!(DBG & 1) && !(a == cached && va == cached_v)) {
+        lds_wait();
+        stage(lb, pA, mA);
+        cached = a;
+        cached_v = va;
+      }
+      if (!(DBG & 2)) c = count_vs_lds(lb, pB, mB);
+    } else if (a == cached && va == cached_v) {
       c = count_vs_lds(lb, pB, mB);
     } else {
       const bool next_same = i + 1 < nq && __builtin_amdgcn_readlane(ea, i + 1) == a &&
                              __builtin_amdgcn_readlane(vai, i + 1) == va;
-      if (!next_same && tA != CT_RUN && tB != CT_RUN && (tA == CT_BITMAP || tB == CT_BITMAP)) {
-        // one-off pair with a bitmap side: no staging, work straight from L2
-        if (tA == CT_BITMAP && tB == CT_BITMAP)
-          c = and_bitmaps(gp(reinterpret_cast<const ulong2*>(pA)), reinterpret_cast<const uint64_t*>(pB));
-        else if (tA == CT_BITMAP)
-          c = probe(gp(reinterpret_cast<const uint32_t*>(pA)), pB, meta_n(mB));
-        else
-          c = probe(gp(reinterpret_cast<const uint32_t*>(pB)), pA, meta_n(mA));
+      if (!next_same && tA == CT_BITMAP && tB == CT_BITMAP) {
+        // one-off bitmap pair: two coalesced 8 KiB streams, no LDS
+        c = and_bitmaps(gp(reinterpret_cast<const ulong2*>(pA)), reinterpret_cast<const uint64_t*>(pB));
+      } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
+        // one-off array & bitmap: copy the bitmap into LDS (64 coalesced lines)
+        // and probe the array there; probing the bitmap in global memory
+        // instead costs one cache-line request per value (measured 3x slower)
+        lds_wait();
+        stage(lb, pB, mB);
+        cached = NONE;
+        cached_v = -1;
+        c = count_vs_lds(lb, pA, mA);
       } else {
         lds_wait();  // previous readers of lb are done before it is rewritten
         stage(lb, pA, mA);
@@ -526,6 +541,14 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   // bigger chunks amortise more leaf-0 stagings (measured: 32 for Q <= 2048,
   // 64 above).
   if (cq <= 0) cq = Q <= 2048 ? 32 : 64;
+  if (variant >= 11 && variant <= 13) {  // cost-isolation builds (scripts/kbench.py --cq2 / variant)
+    const int64_t waves = units * ((Q + 31) / 32);
+    const dim3 g(unsigned((waves + PAIR_WAVES - 1) / PAIR_WAVES)), b(64 * PAIR_WAVES);
+    if (variant == 11) hipLaunchKernelGGL((and2_pairs_kernel<32, 1>), g, b, 0, st, progs, Q, views, S, pairs, partial);
+    else if (variant == 12) hipLaunchKernelGGL((and2_pairs_kernel<32, 2>), g, b, 0, st, progs, Q, views, S, pairs, partial);
+    else hipLaunchKernelGGL((and2_pairs_kernel<32, 3>), g, b, 0, st, progs, Q, views, S, pairs, partial);
+    return;
+  }
   if (variant == 2) {
     switch (cq) {
       case 4: PK_LAUNCH(and2_pairs_v2_kernel, 4) break;

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--shards", type=int, default=0, help="0 = full 954")
     ap.add_argument("--cq", default="0,32,64", help="chunk sizes for variant 1")
     ap.add_argument("--cq2", default="", help="chunk sizes for variant 2")
+    ap.add_argument("--dbg", action="store_true", help="also time the cost-isolation variants 11-13")
     args = ap.parse_args()
     import torch
 
@@ -44,6 +45,9 @@ def main():
     ref = None
     configs = [("tile", {"use_and2": False})] + [(f"and2_cq{c}", {"and2_cq": int(c)}) for c in args.cq.split(",") if c]
     configs += [(f"and2v2_cq{c}", {"and2_cq": int(c), "and2_variant": 2}) for c in args.cq2.split(",") if c]
+    if args.dbg:
+        configs += [("dbg_nostage", {"and2_variant": 11}), ("dbg_nocount", {"and2_variant": 12}),
+                    ("dbg_neither", {"and2_variant": 13})]
     for name, cfg in configs:
         eng = GpuEngine(dev)
         for k, v in cfg.items():
@@ -54,7 +58,7 @@ def main():
         got = out.cpu().numpy()
         if ref is None:
             ref = got
-        ok = bool(np.array_equal(got, ref))
+        ok = bool(np.array_equal(got, ref)) or name.startswith("dbg")
         ts = []
         for _ in range(args.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
