@@ -494,46 +494,75 @@ static Bitmap arena_shard_bitmap(py::array_t<uint64_t> rows, py::array_t<uint32_
 // Intersection counts come from the device (counted[R, S] for the sorted row
 // ids in counted_rows); a shard whose walk reaches an uncounted row is
 // reported in need_more and contributes nothing yet.
-static py::tuple topn_replay(py::array_t<int64_t, py::array::c_style | py::array::forcecast> cand_rows,
-                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> cand_cnts,
+using I64Arr = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+
+static py::tuple topn_replay(I64Arr cand_rows, I64Arr cand_cnts,
                              py::array_t<int32_t, py::array::c_style | py::array::forcecast> shards, int64_t n,
                              int64_t min_threshold,
-                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> counted_rows,
-                             py::array_t<int64_t, py::array::c_style | py::array::forcecast> counted) {
-  if (cand_rows.ndim() != 2 || cand_cnts.ndim() != 2 || counted.ndim() != 2)
-    throw std::invalid_argument("topn_replay: 2-d candidate / count arrays expected");
+                             std::vector<std::pair<I64Arr, py::array_t<int32_t, py::array::c_style | py::array::forcecast>>> blocks,
+                             int nthreads) {
+  if (cand_rows.ndim() != 2 || cand_cnts.ndim() != 2)
+    throw std::invalid_argument("topn_replay: 2-d candidate arrays expected");
   const int64_t S = cand_rows.shape(0), K = cand_rows.shape(1);
-  const int64_t R = counted_rows.shape(0);
-  if (counted.shape(0) != R || counted.shape(1) != S || cand_cnts.shape(0) != S || cand_cnts.shape(1) != K)
-    throw std::invalid_argument("topn_replay: shape mismatch");
+  if (cand_cnts.shape(0) != S || cand_cnts.shape(1) != K) throw std::invalid_argument("topn_replay: shape mismatch");
+  // counted blocks: rows[r_b] with shard-major counts[S, r_b]
+  struct Blk { const int64_t* rows; const int32_t* cnt; int64_t r; };
+  std::vector<Blk> bl;
+  int64_t maxid = -1, R = 0;
+  for (auto& b : blocks) {
+    if (b.second.ndim() != 2 || b.second.shape(0) != S || b.second.shape(1) != b.first.shape(0))
+      throw std::invalid_argument("topn_replay: block must be (rows[r], counts[S, r])");
+    Blk x{b.first.data(), b.second.data(), b.first.shape(0)};
+    for (int64_t i = 0; i < x.r; i++) maxid = std::max(maxid, x.rows[i]);
+    R += x.r;
+    bl.push_back(x);
+  }
   const int64_t* cr = cand_rows.data();
   const int64_t* cc = cand_cnts.data();
-  const int64_t* rows = counted_rows.data();
-  const int64_t* cnt = counted.data();
   const int32_t* sh = shards.data();
   const int64_t M = shards.shape(0);
+  for (int64_t m = 0; m < M; m++)
+    if (sh[m] < 0 || sh[m] >= S) throw std::out_of_range("topn_replay: shard index");
   py::array_t<bool> need(M);
   bool* needp = need.mutable_data();
-  std::vector<int64_t> out_ids, out_cnt;
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> res(M);
   {
     py::gil_scoped_release nogil;
+    // row id -> (block, column): dense table for small ids, sorted index otherwise
+    std::vector<int64_t> dense;                       // (block << 32) | col, -1 = absent
+    std::vector<std::pair<int64_t, int64_t>> sorted;  // (row id, (block << 32) | col)
+    if (maxid >= 0 && maxid < (int64_t(1) << 26)) {
+      dense.assign(size_t(maxid + 1), -1);
+      for (size_t b = 0; b < bl.size(); b++)
+        for (int64_t i = 0; i < bl[b].r; i++)
+          if (bl[b].rows[i] >= 0) dense[size_t(bl[b].rows[i])] = (int64_t(b) << 32) | i;
+    } else {
+      for (size_t b = 0; b < bl.size(); b++)
+        for (int64_t i = 0; i < bl[b].r; i++) sorted.emplace_back(bl[b].rows[i], (int64_t(b) << 32) | i);
+      std::sort(sorted.begin(), sorted.end());
+    }
+    auto loc = [&](int64_t rid) -> int64_t {
+      if (!dense.empty() || sorted.empty()) return (rid >= 0 && rid <= maxid && !dense.empty()) ? dense[size_t(rid)] : -1;
+      auto it = std::lower_bound(sorted.begin(), sorted.end(), std::make_pair(rid, int64_t(-1)));
+      return (it == sorted.end() || it->first != rid) ? -1 : it->second;
+    };
     using E = std::pair<int64_t, int64_t>;  // (count, -id): min-heap top = smallest count, then largest id
-    for (int64_t m = 0; m < M; m++) {
+    auto walk = [&](int64_t m) {
       const int64_t s = sh[m];
-      if (s < 0 || s >= S) throw std::out_of_range("topn_replay: shard index");
-      std::priority_queue<E, std::vector<E>, std::greater<E>> heap;
-      bool more = false;
       auto count_of = [&](int64_t rid, int64_t& v) -> bool {
-        const int64_t* it = std::lower_bound(rows, rows + R, rid);
-        if (it == rows + R || *it != rid) return false;
-        v = cnt[(it - rows) * S + s];
+        const int64_t l = loc(rid);
+        if (l < 0) return false;
+        const Blk& b = bl[size_t(l >> 32)];
+        v = b.cnt[s * b.r + (l & 0xffffffff)];
         return true;
       };
+      std::priority_queue<E, std::vector<E>, std::greater<E>> heap;
+      bool more = false;
       for (int64_t k = 0; k < K; k++) {
         const int64_t rid = cr[s * K + k], c = cc[s * K + k];
         if (c == 0 || c < min_threshold) continue;
+        int64_t v;
         if (n == 0 || int64_t(heap.size()) < n) {
-          int64_t v;
           if (!count_of(rid, v)) { more = true; break; }
           if (v == 0 || v < min_threshold) continue;
           heap.emplace(v, -rid);
@@ -541,23 +570,40 @@ static py::tuple topn_replay(py::array_t<int64_t, py::array::c_style | py::array
         }
         const int64_t thr = heap.top().first;
         if (thr < min_threshold || c < thr) break;
-        int64_t v;
         if (!count_of(rid, v)) { more = true; break; }
         if (v < thr) continue;
         heap.emplace(v, -rid);
       }
       needp[m] = more;
-      if (more) continue;
+      if (more) return;
+      auto& out = res[m];
+      out.reserve(heap.size());
       while (!heap.empty()) {
-        out_ids.push_back(-heap.top().second);
-        out_cnt.push_back(heap.top().first);
+        out.emplace_back(-heap.top().second, heap.top().first);
         heap.pop();
       }
-    }
+    };
+    const int nt = std::max<int>(1, std::min<int64_t>(nthreads, M));
+    std::vector<std::thread> th;
+    std::atomic<int64_t> next{0};
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&]() {
+        for (;;) {
+          const int64_t m = next.fetch_add(1);
+          if (m >= M) break;
+          walk(m);
+        }
+      });
+    for (auto& t : th) t.join();
+    (void)R;
   }
-  py::array_t<int64_t> ids(out_ids.size()), cnts(out_cnt.size());
-  std::copy(out_ids.begin(), out_ids.end(), ids.mutable_data());
-  std::copy(out_cnt.begin(), out_cnt.end(), cnts.mutable_data());
+  size_t tot = 0;
+  for (auto& r : res) tot += r.size();
+  py::array_t<int64_t> ids(tot), cnts(tot);
+  int64_t* ip = ids.mutable_data();
+  int64_t* cp = cnts.mutable_data();
+  for (auto& r : res)
+    for (auto& e : r) *ip++ = e.first, *cp++ = e.second;
   return py::make_tuple(need, ids, cnts);
 }
 
@@ -719,7 +765,7 @@ PYBIND11_MODULE(_roaring, m) {
         py::arg("nthreads") = 8);
   m.def("bitmap_from_containers", &bitmap_from_containers);
   m.def("topn_replay", &topn_replay, py::arg("cand_rows"), py::arg("cand_cnts"), py::arg("shards"), py::arg("n"),
-        py::arg("min_threshold"), py::arg("counted_rows"), py::arg("counted"),
+        py::arg("min_threshold"), py::arg("blocks"), py::arg("nthreads") = 8,
         "Per-shard TopN heap replay over device-counted candidates -> (need_more, ids, counts)");
   m.def("gen_bsi_arena", &gen_bsi_arena, py::arg("shard_lo"), py::arg("shard_hi"), py::arg("total_cols"),
         py::arg("depth"), py::arg("fill"), py::arg("vmin"), py::arg("vmax"), py::arg("seed") = 1,

@@ -77,41 +77,90 @@ class DeviceRankCache:
         return cls(rows_out, cnt_out, all_counts)
 
 
+def _union_ids(a: np.ndarray) -> np.ndarray:
+    """Sorted distinct ids; O(n) through a presence mask for small ids."""
+    if not len(a):
+        return a.astype(np.int64)
+    mx = int(a.max())
+    if 0 <= int(a.min()) and mx < (1 << 26):
+        m = np.zeros(mx + 1, bool)
+        m[a] = True
+        return np.flatnonzero(m).astype(np.int64)
+    return np.unique(a)
+
+
 def topn_phase1(engine: GpuEngine, rv: DeviceView, cache: DeviceRankCache, srcs: Sequence[object], n: int = 10,
-                threshold: int = 1, first_depth: int = 256) -> List[Dict[int, int]]:
+                threshold: int = 1, first_depth: int = 256, nthreads: int = 16) -> List[Dict[int, int]]:
     """Per query: {row id: summed per-shard heap count} over the local shards."""
     from pilosa_amd import _roaring
 
     Q, S, K = len(srcs), cache.S, cache.rows.shape[1]
-    counted: List[Dict[int, np.ndarray]] = [dict() for _ in range(Q)]
+    seen: List[np.ndarray] = [np.zeros(0, np.int64) for _ in range(Q)]
+    blocks: List[list] = [[] for _ in range(Q)]  # per query: (rows[r], counts[S, r]) per round
     depth = np.zeros(Q, np.int64)
     pending: Dict[int, np.ndarray] = {q: np.arange(S, dtype=np.int32) for q in range(Q)}
-    totals: List[Dict[int, int]] = [dict() for _ in range(Q)]
+    got_ids: List[list] = [[] for _ in range(Q)]
+    got_cnt: List[list] = [[] for _ in range(Q)]
     while pending:
-        owners = []
+        qs, news = [], []
         for q, shards in pending.items():
             depth[q] = min(K, max(first_depth, max(n * 2, 1), int(depth[q]) * 4))
-            cand = np.unique(cache.rows[shards, :depth[q]][cache.counts[shards, :depth[q]] > 0])
-            for r in cand.tolist():
-                if r not in counted[q]:
-                    owners.append((q, int(r)))
-        if owners:
-            mat = _count_src_rows(engine, rv, srcs, owners)  # [P, S]
-            for (q, r), row in zip(owners, mat):
-                counted[q][r] = row
+            c = cache.rows[shards, :depth[q]][cache.counts[shards, :depth[q]] > 0]
+            cand = _union_ids(c)
+            new = cand[~np.isin(cand, seen[q], assume_unique=True)] if len(seen[q]) else cand
+            seen[q] = np.union1d(seen[q], new)
+            qs.append(q)
+            news.append(new)
+        if sum(len(x) for x in news):
+            mat = _count_src_rows_vec(engine, rv, srcs, qs, news)  # [S, P]
+            o = 0
+            for q, new in zip(qs, news):
+                if len(new):
+                    blocks[q].append((new, np.ascontiguousarray(mat[:, o:o + len(new)])))
+                o += len(new)
         nxt: Dict[int, np.ndarray] = {}
         for q, shards in pending.items():
-            keys = np.array(sorted(counted[q]), dtype=np.int64)
-            m = np.stack([counted[q][int(r)] for r in keys]) if len(keys) else np.zeros((0, S), np.int64)
-            need, ids, cnts = _roaring.topn_replay(cache.rows, cache.counts, shards, n, threshold, keys,
-                                                   np.ascontiguousarray(m, dtype=np.int64))
-            t = totals[q]
-            for i, c in zip(ids.tolist(), cnts.tolist()):
-                t[i] = t.get(i, 0) + c
+            need, ids, cnts = _roaring.topn_replay(cache.rows, cache.counts, shards, n, threshold, blocks[q], nthreads)
+            got_ids[q].append(ids)
+            got_cnt[q].append(cnts)
             if need.any():
                 nxt[q] = shards[need]
         pending = nxt
+    totals = []
+    for q in range(Q):
+        ids = np.concatenate(got_ids[q]) if got_ids[q] else np.zeros(0, np.int64)
+        cnts = np.concatenate(got_cnt[q]) if got_cnt[q] else np.zeros(0, np.int64)
+        u, inv = np.unique(ids, return_inverse=True)
+        sums = np.zeros(len(u), np.int64)
+        np.add.at(sums, inv, cnts)
+        totals.append(dict(zip(u.tolist(), sums.tolist())))
     return totals
+
+
+def _count_src_rows_vec(engine: GpuEngine, rv: DeviceView, srcs: Sequence[object], qs: List[int],
+                        rows: List[np.ndarray]) -> np.ndarray:
+    """Shard-major [S, P] counts of |src_q ∩ row| for every (q, rows[q]) block."""
+    if all(type(srcs[q]) is Leaf for q in qs):
+        views: List[DeviceView] = [rv]
+        slot = {id(rv): 0}
+        a_slot, a_dense = [], []
+        for q, r in zip(qs, rows):
+            src = srcs[q]
+            sl = slot.get(id(src.view))
+            if sl is None:
+                sl = slot[id(src.view)] = len(views)
+                views.append(src.view)
+            a_slot.append(np.full(len(r), sl, np.int32))
+            a_dense.append(np.full(len(r), src.view.dense(src.row), np.int64))
+        allrows = np.concatenate(rows)
+        progs = engine.pair_programs(0, np.concatenate(a_dense), 0, rv.dense_many(allrows.astype(np.uint64)))
+        progs["leaf_view"][:, 0] = np.concatenate(a_slot)
+        t = engine.count_per_shard_progs(progs, views, rv.S, as_tensor=True)
+        # per-shard counts fit int32 (<= 2^20): halve the device->host bytes
+        import torch
+        return t.t().to(torch.int32).contiguous().cpu().numpy()
+    owners = [(q, int(r)) for q, rr in zip(qs, rows) for r in rr.tolist()]
+    return _count_src_rows(engine, rv, srcs, owners, shard_major=True).astype(np.int32)
 
 
 def topn_phase2_counts(engine: GpuEngine, rv: DeviceView, srcs: Sequence[object], ids: Sequence[Sequence[int]],
@@ -131,8 +180,10 @@ def topn_phase2_counts(engine: GpuEngine, rv: DeviceView, srcs: Sequence[object]
     return out
 
 
-def _count_src_rows(engine: GpuEngine, rv: DeviceView, srcs: Sequence[object], owners) -> np.ndarray:
-    """|src_q ∩ row r| per local shard for (q, r) pairs -> int64[P, S].
+def _count_src_rows(engine: GpuEngine, rv: DeviceView, srcs: Sequence[object], owners,
+                    shard_major: bool = False) -> np.ndarray:
+    """|src_q ∩ row r| per local shard for (q, r) pairs -> int64[P, S]
+    (or [S, P] with ``shard_major``, transposed on the device).
     Single-row sources (the common TopN(f, Row(...)) shape) are encoded as
     pair programs directly; other trees go through the expression compiler."""
     if all(type(srcs[q]) is Leaf for q, _ in owners):
@@ -151,8 +202,13 @@ def _count_src_rows(engine: GpuEngine, rv: DeviceView, srcs: Sequence[object], o
         b_dense = rv.dense_many(np.array([r for _, r in owners], np.uint64))
         progs = engine.pair_programs(0, a_dense, 0, b_dense)
         progs["leaf_view"][:, 0] = a_slot
-        return engine.count_per_shard_progs(progs, views, rv.S)
-    return engine.count_per_shard([Op("and", (srcs[q], Leaf(rv, int(r)))) for q, r in owners])
+        t = engine.count_per_shard_progs(progs, views, rv.S, as_tensor=True)
+    else:
+        p, v, S = engine.compile_batch([Op("and", (srcs[q], Leaf(rv, int(r)))) for q, r in owners])
+        t = engine.count_per_shard_progs(p, v, S, as_tensor=True)
+    if shard_major:
+        t = t.t()
+    return t.contiguous().cpu().numpy()
 
 
 def finish_topn(ids: Sequence[int], counts: np.ndarray, n: int) -> List[Pair]:
