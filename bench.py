@@ -36,6 +36,22 @@ NROWS = 1_000_000
 SHARD_WIDTH = 1 << 20
 
 
+_REHEARSE = False
+
+
+def all_reduce(t, op=None):
+    """dist.all_reduce (RCCL); the gloo rehearsal mode reduces a host copy."""
+    import torch.distributed as dist
+    op = dist.ReduceOp.SUM if op is None else op
+    if _REHEARSE:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
 def zipf_rows(rng, n, nrows=NROWS, s=1.6, v=50.0):
     # inverse-CDF sampling of P(k) ~ (v+k)^-s, k in [0, nrows)
     k = np.arange(nrows, dtype=np.float64)
@@ -84,7 +100,7 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         if world == 1:
             return exact
         flat = torch.from_numpy(np.concatenate(exact) if exact else np.zeros(0, np.int64)).to(dev)
-        dist.all_reduce(flat)
+        all_reduce(flat)
         flat = flat.cpu().numpy()
         o, out = 0, []
         for q in range(len(ids)):
@@ -122,7 +138,7 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         el = time.perf_counter() - t0
         elt = torch.tensor([el], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+            all_reduce(elt, op=dist.ReduceOp.MAX)
         el = float(elt.item())
         return {"qps": round(B * batches / el, 2), "ms_per_batch": round(el / batches * 1000, 2), "batch": B,
                 "sample_top3": [(p.id, p.count) for p in res[0][:3]] if res and res[0] else []}
@@ -158,9 +174,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-GPU path on a 1-GPU box: every rank on cuda:0, gloo
+    # collectives through host copies (PILOSA_BENCH_REHEARSE=1); never used
+    # for reported numbers
+    rehearse = os.environ.get("PILOSA_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    global _REHEARSE
+    _REHEARSE = rehearse
     dev = torch.device("cuda", local_rank)
 
     from pilosa_amd import _roaring
@@ -196,7 +223,7 @@ def main():
     def launch(h):
         out = eng.launch_count(h)
         if world > 1:
-            dist.all_reduce(out)
+            all_reduce(out)
         return out
 
     tm = {"prep": 0.0, "launch": 0.0, "wait": 0.0}
@@ -235,7 +262,7 @@ def main():
     elapsed = time.perf_counter() - t
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms = elapsed / args.steps * 1000.0
     qps = args.batch * args.steps / elapsed
