@@ -98,7 +98,9 @@ def cmd_server(args, stdout, stderr) -> int:
                  translation_primary_url=cfg.get("translation.primary-url"),
                  tls_certificate=cfg.get("tls.certificate"), tls_key=cfg.get("tls.key"),
                  tls_skip_verify=cfg.get("tls.skip-verify"),
-                 diagnostics_host=cfg.get("metric.diagnostics-host") if cfg.get("metric.diagnostics") else "")
+                 diagnostics_host=cfg.get("metric.diagnostics-host") if cfg.get("metric.diagnostics") else "",
+                 gpu_device=int(cfg.get("gpu.devices")[0]) if cfg.get("gpu.devices") else None,
+                 hbm_budget=int(cfg.get("gpu.hbm-budget")))
     srv.open()
     logger.printf("listening as %s (node %s, gpu=%s)", srv.uri.normalize(), srv.node.id,
                   "on" if srv.gpu is not None else "off")

@@ -18,6 +18,13 @@ hipStream_t cur_stream(const torch::Tensor& t) {
   return at::hip::getCurrentHIPStream(t.device().index()).stream();
 }
 
+// Launch-time errors (bad grid, missing code object, ...) surface here
+// instead of as a later, unrelated failure.
+void check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, what, ": kernel launch failed: ", hipGetErrorString(e));
+}
+
 void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor out,
                 c10::optional<torch::Tensor> per_key, int64_t mode, c10::optional<torch::Tensor> per_shard) {
   check_dev(progs, "progs");
@@ -48,6 +55,7 @@ void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   pk::launch_expr_count(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
                         reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), o, pk_, ps, int(mode),
                         cur_stream(progs));
+  check_launch("expr_count");
 }
 
 void expr_materialize(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor counts,
@@ -63,6 +71,7 @@ void expr_materialize(torch::Tensor progs, torch::Tensor views, int64_t S, torch
                               reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
                               counts.data_ptr<int32_t>(), offs.data_ptr<int64_t>(),
                               reinterpret_cast<uint16_t*>(outp.data_ptr<int16_t>()), cur_stream(progs));
+  check_launch("expr_materialize");
 }
 
 pk::BsiArgs bsi_args_from(const torch::Tensor& bsi_args) {
@@ -90,6 +99,7 @@ void bsi_range(torch::Tensor views, int64_t S, torch::Tensor bsi_args, int64_t o
   pk::launch_bsi_range(reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), bsi_args_from(bsi_args),
                        int(op), p1, p2, reinterpret_cast<uint16_t*>(out_payload.data_ptr<int16_t>()),
                        out_meta.data_ptr<int64_t>(), cur_stream(views));
+  check_launch("bsi_range");
 }
 
 void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out) {
@@ -101,6 +111,7 @@ void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   pk::launch_bsi_minmax(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()),
                         reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
                         bsi_args_from(bsi_args), out.data_ptr<int64_t>(), cur_stream(views));
+  check_launch("bsi_minmax");
 }
 
 void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out_sum,
@@ -124,6 +135,7 @@ void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor 
                      reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), b,
                      reinterpret_cast<unsigned long long*>(out_sum.data_ptr<int64_t>()),
                      reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>()), cur_stream(progs));
+  check_launch("bsi_sum");
 }
 
 void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor pairs, torch::Tensor partial,
@@ -140,6 +152,7 @@ void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
                         reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
                         reinterpret_cast<uint2*>(pairs.data_ptr()), partial.data_ptr<int32_t>(), int(cq),
                         int(variant), cur_stream(progs));
+  check_launch("and2_pairs");
 }
 
 }  // namespace

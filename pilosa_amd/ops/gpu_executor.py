@@ -20,6 +20,7 @@ expressible on the device raises ``NotImplementedError`` -> host fallback.
 from __future__ import annotations
 
 import threading
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -44,12 +45,16 @@ EMPTY = _Empty()
 
 
 class GpuExecutor:
-    def __init__(self, holder, device="cuda:0", executor=None):
+    def __init__(self, holder, device="cuda:0", executor=None, hbm_budget: int = 0):
         self.holder = holder
         self.engine = GpuEngine(device)
         self.device = self.engine.device
         self.executor = executor
-        self._arenas: Dict[Tuple, Tuple[Tuple, DeviceView]] = {}
+        # arena cache in LRU order; hbm_budget > 0 caps the resident bytes
+        # (least recently used views are dropped and rebuilt on demand)
+        self.hbm_budget = int(hbm_budget)
+        self.evictions = 0
+        self._arenas: "OrderedDict[Tuple, Tuple[Tuple, DeviceView]]" = OrderedDict()
         self._bsi_views: Dict[Tuple, DeviceView] = {}  # predicate results (small LRU)
         self.mu = threading.RLock()
         self.launches = 0
@@ -68,6 +73,8 @@ class GpuExecutor:
         key = (index, field, view, shards)
         with self.mu:
             hit = self._arenas.get(key)
+            if hit is not None:
+                self._arenas.move_to_end(key)
             if hit is not None and hit[0] == sig:
                 return hit[1]
             if hit is not None and len(hit[0]) == len(sig) and not hit[1].needs_compaction():
@@ -109,11 +116,48 @@ class GpuExecutor:
                     with f.mu:
                         f.take_dirty(token)  # register before the contents are read
                         bms.append(f.storage)
+            self._evict_for(key)
             dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards), patchable=True)
             dv.token = token
             self.rebuilds += 1
             self._arenas[key] = (sig, dv)
+            self._arenas.move_to_end(key)
+            self._evict_for(key)
             return dv
+
+    def _evict_for(self, keep):
+        """Drop least recently used arenas while over the HBM budget."""
+        if self.hbm_budget <= 0:
+            return
+        while len(self._arenas) > 1 and self.hbm_bytes() > self.hbm_budget:
+            k = next(iter(self._arenas))
+            if k == keep:
+                break
+            _, dv = self._arenas.pop(k)
+            self._drop_subscriptions(k, dv)
+            self.evictions += 1
+
+    def _drop_subscriptions(self, key, dv):
+        v = self.holder.view(key[0], key[1], key[2])
+        if v is None or getattr(dv, "token", None) is None:
+            return
+        for s in key[3]:
+            f = v.fragment(s)
+            if f is not None:
+                f.drop_dirty(dv.token)
+
+    def stats(self) -> dict:
+        """Device gauges: resident bytes, containers by type."""
+        with self.mu:
+            views = [dv for _, dv in self._arenas.values()]
+        types = {"array": 0, "bitmap": 0, "run": 0}
+        for dv in views:
+            t = ((dv.t_meta >> 4) & 3)
+            for name, code in (("array", 1), ("bitmap", 2), ("run", 3)):
+                types[name] += int((t == code).sum())
+        return {"arenas": len(views), "arenaBytes": self.hbm_bytes(), "containers": types,
+                "launches": self.launches, "rebuilds": self.rebuilds, "shardUpdates": self.shard_updates,
+                "rowUpdates": self.row_updates, "evictions": self.evictions, "hbmBudget": self.hbm_budget}
 
     def invalidate(self):
         with self.mu:

@@ -46,7 +46,8 @@ class Server:
                  long_query_time: float = 60.0, stats: str = "expvar", logger=None, hasher: str = "jump",
                  max_opn: int = 10000, cluster_disabled: bool = False, mesh_block: int = 1,
                  translation_primary_url: str = "", tls_certificate: str = "", tls_key: str = "",
-                 tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0):
+                 tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
+                 gpu_device: Optional[int] = None, hbm_budget: int = 0):
         self.data_dir = data_dir
         self.bind = bind
         self.logger = logger or StandardLogger()
@@ -68,6 +69,8 @@ class Server:
         self.hasher = ModHasher() if hasher == "mod" else JumpHasher()
         self.gpu = None
         self.gpu_mode = gpu
+        self.gpu_device = gpu_device
+        self.hbm_budget = hbm_budget
         self.mesh = None          # multi-GPU node: parallel.mesh.ShardMesh (this process is rank 0)
         self.mesh_block = mesh_block
         self.translation_primary = URI.parse(translation_primary_url) if translation_primary_url else None
@@ -201,7 +204,8 @@ class Server:
                 return
             from pilosa_amd.ops.gpu_executor import GpuExecutor
             from pilosa_amd.parallel.mesh import dist_env
-            self.gpu = GpuExecutor(self.holder, f"cuda:{dist_env()[2]}")
+            dev = self.gpu_device if self.gpu_device is not None else dist_env()[2]
+            self.gpu = GpuExecutor(self.holder, f"cuda:{dev}", hbm_budget=self.hbm_budget)
         except ImportError:
             if mode == "on":
                 raise
@@ -211,8 +215,9 @@ class Server:
             return {"enabled": False}
         import torch
         p = torch.cuda.get_device_properties(self.gpu.device)
-        return {"enabled": True, "name": p.name, "arch": getattr(p, "gcnArchName", ""),
-                "hbmBytes": p.total_memory, "arenaBytes": self.gpu.hbm_bytes(), "launches": self.gpu.launches}
+        out = {"enabled": True, "name": p.name, "arch": getattr(p, "gcnArchName", ""), "hbmBytes": p.total_memory}
+        out.update(self.gpu.stats())
+        return out
 
     def close(self):
         self._closing.set()
@@ -584,8 +589,13 @@ class Server:
                 self.stats.gauge("open_files", len(os.listdir("/proc/self/fd")))
                 self.stats.gauge("threads", threading.active_count())
                 if self.gpu is not None:
-                    self.stats.gauge("gpu.arena_bytes", self.gpu.hbm_bytes())
-                    self.stats.gauge("gpu.launches", self.gpu.launches)
+                    st = self.gpu.stats()
+                    self.stats.gauge("gpu.arena_bytes", st["arenaBytes"])
+                    self.stats.gauge("gpu.launches", st["launches"])
+                    self.stats.gauge("gpu.arena_rebuilds", st["rebuilds"])
+                    self.stats.gauge("gpu.arena_row_updates", st["rowUpdates"])
+                    for t, n in st["containers"].items():
+                        self.stats.gauge(f"gpu.containers.{t}", n)
             except Exception:  # noqa: BLE001
                 pass
 

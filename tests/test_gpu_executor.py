@@ -266,3 +266,22 @@ def test_incremental_shard_updates(envs):
         assert got == 1 and gpu.rebuilds > r0
     finally:
         cpu.executor.gpu = None
+
+
+def test_hbm_budget_lru_eviction(envs):
+    """gpu.hbm-budget: least recently used view arenas are dropped and
+    rebuilt on demand; results stay exact."""
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    cpu, gpu = envs
+    small = GpuExecutor(cpu.holder, "cuda:0", executor=cpu.executor, hbm_budget=1)
+    qs = ["Count(Row(f=1))", "Count(Row(g=1))", "Count(Row(h=3))", "Count(Row(f=2))", "Count(Row(g=2))"]
+    want = [cpu.q1("i", q) for q in qs]
+    cpu.executor.gpu = small
+    try:
+        got = [cpu.q1("i", q) for q in qs]
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
+    st = small.stats()
+    assert st["evictions"] >= 3 and st["arenas"] == 1
+    assert sum(st["containers"].values()) > 0
