@@ -508,7 +508,6 @@ class GpuEngine:
         tv = self._views_tensor(views)
         return tp, tv
 
-    @staticmethod
     def _is_fast(rec) -> bool:
         n = int(rec["nprog"])
         p = rec["prog"]
