@@ -508,11 +508,6 @@ class GpuEngine:
         tv = self._views_tensor(views)
         return tp, tv
 
-    def _is_fast(rec) -> bool:
-        n = int(rec["nprog"])
-        p = rec["prog"]
-        return n == 1 or (n == 3 and p[0] == 0 and p[1] == 1 and p[2] == OP_AND)
-
     def prepare_count(self, exprs: Sequence[object], sort: bool = True):
         """Host half of a count batch: compile, order, split by kernel flavour
         and upload the programs.  Returns a handle for :meth:`launch_count`.
