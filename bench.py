@@ -75,12 +75,24 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
                                      topn_phase1, topn_phase2_counts)
     from pilosa_amd.pql import parse_string
 
+    from pilosa_amd.ops.topn_index import DeviceTopNIndex
+
     n = 100
     t0 = time.perf_counter()
     cache = DeviceRankCache.from_view(view, k=args.topn_cache, keep_row_counts=True)
     torch.cuda.synchronize(dev)
     t_cache = time.perf_counter() - t0
     planner = BenchPlanner({"f": view})
+    # node-wide row-id space of the TopN accumulators (identical on every rank)
+    space = np.asarray(view.rows, dtype=np.uint64)
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, space)
+        space = np.unique(np.concatenate(parts))
+    t0 = time.perf_counter()
+    tindex = DeviceTopNIndex(view, cache, space=space)
+    torch.cuda.synchronize(dev)
+    t_index = time.perf_counter() - t0
 
     def merge(totals):
         if world == 1:
@@ -109,6 +121,12 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         return out
 
     def run_cache(qs):
+        # device phase 1 (scatter-add of cache prefixes) + device ids= re-count
+        calls = [parse_string(q).calls[0] for q in qs]
+        return tindex.topn_nosrc(cache.row_counts, [c.uint_arg("n")[0] for c in calls], [1] * len(calls),
+                                 reduce=all_reduce if world > 1 else None)
+
+    def run_cache_host(qs):
         calls = [parse_string(q).calls[0] for q in qs]
         totals = merge([topn_cache_phase1(cache, c.uint_arg("n")[0]) for c in calls])
         ids = [sorted(t) for t in totals]
@@ -116,6 +134,14 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         return [finish_topn(ids[q], exact[q], n) for q in range(len(qs))]
 
     def run_src(qs):
+        # slot-index path: LDS histogram + in-kernel heap walk (ops/topn_index.py)
+        calls = [parse_string(q).calls[0] for q in qs]
+        srcs = [planner.plan(c.children[0]) for c in calls]
+        ns = [c.uint_arg("n")[0] for c in calls]
+        return tindex.topn(eng, srcs, ns, [1] * len(srcs), reduce=all_reduce if world > 1 else None)
+
+    def run_src_pairs(qs):
+        # pair-count path with the native heap replay (ops/topn.py), for comparison
         calls = [parse_string(q).calls[0] for q in qs]
         srcs = [planner.plan(c.children[0]) for c in calls]
         totals = merge(topn_phase1(eng, view, cache, srcs, n=n))
@@ -144,10 +170,22 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
                 "sample_top3": [(p.id, p.count) for p in res[0][:3]] if res and res[0] else []}
 
     B, nb = args.topn_batch, args.topn_batches
-    out = {"n": n, "cache_k": args.topn_cache, "cache_build_s": round(t_cache, 2)}
-    out["cache"] = timed(run_cache, [f"TopN(f, n={n})"] * (B * (nb + 1)), B, nb)
+    out = {"n": n, "cache_k": args.topn_cache, "cache_build_s": round(t_cache, 2),
+           "slot_index_build_s": round(t_index, 2), "slot_index_bytes": tindex.nbytes()}
+    cq = [f"TopN(f, n={n})"] * (B * (nb + 1))
+    out["cache"] = timed(run_cache, cq, B, nb)
+    out["cache_paths_agree"] = [[(p.id, p.count) for p in r] for r in run_cache(cq[:B])] == \
+        [[(p.id, p.count) for p in r] for r in run_cache_host(cq[:B])]
     hot = zipf_rows(rng, B * (nb + 1), 1000)
-    out["src"] = timed(run_src, [f"TopN(f, Row(f={a}), n={n})" for a in hot], B, nb)
+    src_q = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
+    out["src"] = timed(run_src, src_q, B, nb)
+    if args.topn_pairs_batches > 0:
+        nbp = min(nb, args.topn_pairs_batches)
+        res_idx = run_src(src_q[B:2 * B])
+        res_pairs = run_src_pairs(src_q[B:2 * B])
+        out["src_pairs"] = timed(run_src_pairs, src_q, B, nbp)
+        out["src_paths_agree"] = [[(p.id, p.count) for p in r] for r in res_idx] == \
+            [[(p.id, p.count) for p in r] for r in res_pairs]
     return out
 
 
@@ -164,6 +202,8 @@ def main():
                     help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
+    ap.add_argument("--topn-pairs-batches", type=int, default=1,
+                    help="also time the pair-count src TopN path on this many batches (0 = skip)")
     ap.add_argument("--cpu-baseline-shards", type=int, default=0,
                     help="also time the host C++ roaring executor on this many shards (extrapolated)")
     args = ap.parse_args()

@@ -155,6 +155,106 @@ void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   check_launch("and2_pairs");
 }
 
+pk::ViewDev viewdev_from(const torch::Tensor& vd) {
+  TORCH_CHECK(!vd.is_cuda() && vd.numel() * vd.element_size() == int64_t(sizeof(pk::ViewDev)),
+              "view must be a cpu tensor holding one ViewDev (64 bytes)");
+  pk::ViewDev v;
+  memcpy(&v, vd.data_ptr(), sizeof(v));
+  return v;
+}
+
+void topn_index(torch::Tensor view, int64_t S, int64_t K, torch::Tensor cache_dense, torch::Tensor colcnt,
+                torch::Tensor colptr, torch::Tensor entbase, torch::Tensor slots, bool fill) {
+  check_dev(cache_dense, "cache_dense");
+  check_dev(colcnt, "colcnt");
+  TORCH_CHECK(cache_dense.scalar_type() == torch::kInt32 && cache_dense.numel() == S * K, "cache_dense int32[S*K]");
+  TORCH_CHECK(colcnt.scalar_type() == torch::kInt32 && colcnt.numel() == S * (int64_t(1) << 20),
+              "colcnt int32[S*2^20]");
+  TORCH_CHECK(K > 0 && K <= 65535, "slot index needs 0 < K <= 65535");
+  const uint32_t* cp = nullptr;
+  const int64_t* eb = nullptr;
+  uint16_t* sl = nullptr;
+  if (fill) {
+    check_dev(colptr, "colptr");
+    check_dev(entbase, "entbase");
+    check_dev(slots, "slots");
+    TORCH_CHECK(colptr.scalar_type() == torch::kInt32 && colptr.numel() == S * ((int64_t(1) << 20) + 1),
+                "colptr int32[S*(2^20+1)]");
+    TORCH_CHECK(entbase.scalar_type() == torch::kInt64 && entbase.numel() >= S, "entbase int64[S]");
+    TORCH_CHECK(slots.scalar_type() == torch::kInt16, "slots int16");
+    cp = reinterpret_cast<const uint32_t*>(colptr.data_ptr<int32_t>());
+    eb = entbase.data_ptr<int64_t>();
+    sl = reinterpret_cast<uint16_t*>(slots.data_ptr<int16_t>());
+  }
+  pk::launch_topn_index(viewdev_from(view), int(S), int(K), cache_dense.data_ptr<int32_t>(),
+                        reinterpret_cast<uint32_t*>(colcnt.data_ptr<int32_t>()), cp, eb, sl, fill,
+                        cur_stream(cache_dense));
+  check_launch("topn_index");
+}
+
+void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, int64_t A, torch::Tensor src_counts,
+              torch::Tensor src_offs, torch::Tensor src_vals, torch::Tensor colptr, torch::Tensor entbase,
+              torch::Tensor slots, torch::Tensor cache_cnt, torch::Tensor cache_acc, torch::Tensor slotmap,
+              torch::Tensor a2dense, torch::Tensor ns, torch::Tensor min_threshold, int64_t mode, torch::Tensor acc,
+              torch::Tensor pair_off, torch::Tensor pair_idx, torch::Tensor out) {
+  for (auto* t : {&src_counts, &src_offs, &src_vals, &colptr, &entbase, &slots, &cache_cnt, &cache_acc, &slotmap,
+                  &a2dense, &ns, &min_threshold})
+    check_dev(*t, "topn_src input");
+  TORCH_CHECK(mode == 1 || mode == 2, "topn_src mode");
+  TORCH_CHECK(K > 0 && K <= 65535 && H >= 0 && H <= K, "topn_src K/H");
+  TORCH_CHECK(pk::topn_lds_bytes(int(K), int(H)) <= 160 * 1024 - 1024, "slot histogram exceeds LDS");
+  TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * S * 16,
+              "src_counts int32[Q*S*16]");
+  TORCH_CHECK(src_offs.scalar_type() == torch::kInt64 && src_offs.numel() == Q * S * 16, "src_offs int64[Q*S*16]");
+  TORCH_CHECK(src_vals.scalar_type() == torch::kInt16, "src_vals int16");
+  TORCH_CHECK(colptr.scalar_type() == torch::kInt32 && colptr.numel() == S * ((int64_t(1) << 20) + 1),
+              "colptr int32[S*(2^20+1)]");
+  TORCH_CHECK(entbase.scalar_type() == torch::kInt64 && entbase.numel() >= S, "entbase int64[S]");
+  TORCH_CHECK(slots.scalar_type() == torch::kInt16, "slots int16");
+  TORCH_CHECK(cache_cnt.scalar_type() == torch::kInt32 && cache_cnt.numel() == S * K, "cache_cnt int32[S*K]");
+  TORCH_CHECK(cache_acc.scalar_type() == torch::kInt32 && cache_acc.numel() == S * K, "cache_acc int32[S*K]");
+  TORCH_CHECK(slotmap.scalar_type() == torch::kInt32 && slotmap.numel() == S * A, "slotmap int32[S*A]");
+  TORCH_CHECK(a2dense.scalar_type() == torch::kInt32 && a2dense.numel() == A, "a2dense int32[A]");
+  TORCH_CHECK(ns.scalar_type() == torch::kInt32 && ns.numel() == Q, "ns int32[Q]");
+  TORCH_CHECK(min_threshold.scalar_type() == torch::kInt32 && min_threshold.numel() == Q, "min_threshold int32[Q]");
+  pk::TopNLaunch a{};
+  a.v = viewdev_from(view);
+  a.Q = int(Q);
+  a.S = int(S);
+  a.K = int(K);
+  a.H = int(H);
+  a.A = A;
+  a.src_counts = src_counts.data_ptr<int32_t>();
+  a.src_offs = src_offs.data_ptr<int64_t>();
+  a.src_vals = reinterpret_cast<const uint16_t*>(src_vals.data_ptr<int16_t>());
+  a.colptr = reinterpret_cast<const uint32_t*>(colptr.data_ptr<int32_t>());
+  a.entbase = entbase.data_ptr<int64_t>();
+  a.slots = reinterpret_cast<const uint16_t*>(slots.data_ptr<int16_t>());
+  a.cache_cnt = cache_cnt.data_ptr<int32_t>();
+  a.cache_acc = cache_acc.data_ptr<int32_t>();
+  a.slotmap = slotmap.data_ptr<int32_t>();
+  a.a2dense = a2dense.data_ptr<int32_t>();
+  a.ns = ns.data_ptr<int32_t>();
+  a.min_threshold = min_threshold.data_ptr<int32_t>();
+  if (mode == 1) {
+    check_dev(acc, "acc");
+    TORCH_CHECK(acc.scalar_type() == torch::kInt32 && acc.numel() == Q * A, "acc int32[Q*A]");
+    a.acc = acc.data_ptr<int32_t>();
+  } else {
+    check_dev(pair_off, "pair_off");
+    check_dev(pair_idx, "pair_idx");
+    check_dev(out, "out");
+    TORCH_CHECK(pair_off.scalar_type() == torch::kInt64 && pair_off.numel() == Q + 1, "pair_off int64[Q+1]");
+    TORCH_CHECK(pair_idx.scalar_type() == torch::kInt32, "pair_idx int32");
+    TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() == pair_idx.numel(), "out int64[P]");
+    a.pair_off = pair_off.data_ptr<int64_t>();
+    a.pair_idx = pair_idx.data_ptr<int32_t>();
+    a.out = reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>());
+  }
+  pk::launch_topn_src(a, int(mode), cur_stream(cache_cnt));
+  check_launch("topn_src");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -172,5 +272,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("variant") = 1);
   m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
+  m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
+  m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2 ids= re-count");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
 }

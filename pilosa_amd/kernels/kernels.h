@@ -66,4 +66,37 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
                     unsigned long long* out_sum, unsigned long long* out_cnt, hipStream_t st);
 
+// Device TopN slot index (topn_kernels.hip): pass 1 counts cached-row bits per
+// column into colcnt[S*2^20]; pass 2 (fill) scatters cache slots behind the
+// per-shard exclusive scan colptr[S][2^20+1] (colcnt reused as cursors).
+void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dense, uint32_t* colcnt,
+                       const uint32_t* colptr, const int64_t* entbase, uint16_t* slots, bool fill, hipStream_t st);
+// Arguments of the src-TopN kernel.  Rows are addressed in an "acc space" of
+// A sorted row ids (identical on every rank of a node).
+struct TopNLaunch {
+  ViewDev v;                      // the TopN field's view (fallback probes)
+  int Q, S, K, H;                 // queries, shards, cache slots, u32 slots
+  int64_t A;                      // acc-space size
+  const int32_t* src_counts;      // [Q*S*16] materialised src containers
+  const int64_t* src_offs;        // [Q*S*16] u16 offsets into src_vals
+  const uint16_t* src_vals;       // array (n <= 4096) or bitmap (4096 u16)
+  const uint32_t* colptr;         // [S][2^20+1] per-shard entry offsets
+  const int64_t* entbase;         // [S] first slot entry of each shard
+  const uint16_t* slots;          // cache slot per (column, cached row)
+  const int32_t* cache_cnt;       // [S][K] cached counts (desc), 0 = empty
+  const int32_t* cache_acc;       // [S][K] acc index of each slot's row
+  const int32_t* slotmap;         // [S][A] cache slot of each acc row, -1
+  const int32_t* a2dense;         // [A] dense row in v, -1 = absent here
+  const int32_t* ns;              // [Q] n (0 = unlimited)
+  const int32_t* min_threshold;   // [Q]
+  int32_t* acc;                   // mode 1: [Q][A] summed pushed counts
+  const int64_t* pair_off;        // mode 2: [Q+1]
+  const int32_t* pair_idx;        // mode 2: [P] acc index of each id
+  unsigned long long* out;        // mode 2: [P] summed counts >= threshold
+};
+// LDS bytes of the (query, shard) slot histogram: H u32 slots + packed u16 rest.
+int topn_lds_bytes(int K, int H);
+// mode 1: phase-1 heap walk -> acc[Q][A]; mode 2: ids= re-count -> out[P].
+void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
+
 }  // namespace pk

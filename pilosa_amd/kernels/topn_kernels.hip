@@ -1,0 +1,343 @@
+// Device TopN with a src filter: TopN(f, <src>, n) without counting
+// src ∩ row for every cached row one pair at a time.
+//
+// Reference semantics (fragment.go:1568-1700 `top`, executor.go:863-930):
+// per shard the ranked cache (rows by count desc, id asc) is walked; the
+// first n rows with count = |src ∩ row| >= max(1, threshold) fill a heap,
+// T = the heap minimum; later rows are pushed while their cached count is
+// >= T and their src count is >= T, and the walk stops at the first cached
+// count < T.  Phase 1 sums the pushed (row, count) pairs over shards, phase 2
+// (ids=) re-counts exactly those ids on every shard.
+//
+// MI355X design.  The pair-per-candidate formulation costs |cache| row
+// intersections per (query, shard) (~10k in the Zipf headline index).  We
+// invert it: a column-major *slot index* of the cached rows is kept in HBM
+// next to the arena (per shard: colptr[2^20+1] + u16 cache slots, 2 B per
+// set bit of a cached row), so the src counts of ALL cached rows of a shard
+// are one histogram over src's columns: |src_s| x (bits per column) LDS
+// increments.  One 1024-thread workgroup owns one (query, shard):
+//   1. zero an LDS histogram over the K cache slots (u32 for the hot slots
+//      whose counts can reach 2^16, packed u16 for the rest: K = 50,000 fits
+//      in ~100 KB of the 160 KB LDS);
+//   2. stream src's materialised columns and, per column, its slot list;
+//   3. mode 1: run the reference heap walk with block scans over the slots
+//      (fill = first n qualifying slots, T = their min, then the sorted cache
+//      counts bound the tail) and add pushed counts into acc[q][row];
+//      mode 2: gather the counts of the phase-1 ids (slot map, with an exact
+//      probe for ids outside this shard's cache).
+// Rows are addressed in an "acc space" (sorted row ids shared by every rank of
+// a multi-GPU node) so acc / out reduce with one all-reduce.
+// The index is built on the device by two passes over the cached rows'
+// containers (count per column, then scatter slots behind an exclusive scan).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace pk {
+namespace {
+
+constexpr int TN_THREADS = 1024;
+constexpr int TN_WAVES = TN_THREADS / 64;
+constexpr int64_t SW = int64_t(1) << 20;  // columns per shard
+constexpr int64_t CP_STRIDE = SW + 1;      // colptr entries per shard
+
+__device__ __forceinline__ uint32_t tn_xcd_remap(uint32_t bid, uint32_t nblk) {
+  // consecutive units (same shard, different queries) land on one XCD so the
+  // shard's colptr / slot lists are shared through that XCD's L2
+  const uint32_t nx = 8;
+  const uint32_t xcd = bid % nx, loc = bid / nx;
+  const uint32_t q = nblk / nx, r = nblk % nx;
+  const uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + loc;
+}
+
+// f(x) for every value x of the container described by meta word m; the
+// threads tid, tid + nthr, ... of a group split the work.
+template <class F>
+__device__ __forceinline__ void container_values(const uint16_t* payload, int64_t m, int tid, int nthr, F&& f) {
+  const uint16_t* p = payload + meta_off16(m) * 8;
+  const int t = meta_type(m);
+  if (t == CT_ARRAY) {
+    const int n = meta_n(m);
+    for (int i = tid; i < n; i += nthr) f(int(p[i]));
+  } else if (t == CT_BITMAP) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
+    for (int i = tid; i < 1024; i += nthr)
+      for (uint64_t b = w[i]; b; b &= b - 1) f(i * 64 + __builtin_ctzll(b));
+  } else {
+    const int nr = p[0];
+    const uint16_t* r = p + 8;
+    for (int k = 0; k < nr; k++) {
+      const int a = r[2 * k], b = r[2 * k + 1];
+      for (int x = a + tid; x <= b; x += nthr) f(x);
+    }
+  }
+}
+
+// Pass 1 (FILL=false): colcnt[s][col] = number of cached rows of shard s with
+// a bit at col.  Pass 2 (FILL=true): scatter the cache slot k of each such
+// (row, col) to slots[entbase[s] + colptr[s][col] + cursor].  One wave per
+// cache entry (s, k); grid-stride.
+template <bool FILL>
+__global__ __launch_bounds__(256) void topn_index_kernel(ViewDev v, int S, int K,
+                                                         const int32_t* __restrict__ cache_dense,
+                                                         uint32_t* __restrict__ colcnt,
+                                                         const uint32_t* __restrict__ colptr,
+                                                         const int64_t* __restrict__ entbase,
+                                                         uint16_t* __restrict__ slots) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = int64_t(gridDim.x) * 4;
+  const int64_t total = int64_t(S) * K;
+  for (int64_t e = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); e < total; e += nw) {
+    const int d = cache_dense[e];
+    if (d < 0) continue;
+    const int s = int(e / K);
+    const uint16_t k = uint16_t(e - int64_t(s) * K);
+    const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+    const int64_t sb = v.shard_base[s];
+    const int64_t c0 = sb + rp[d], c1 = sb + rp[d + 1];
+    for (int64_t c = c0; c < c1; c++) {
+      const int64_t m = v.meta[c];
+      const int64_t colbase = int64_t(meta_j(m)) << 16;
+      uint32_t* cc = colcnt + int64_t(s) * SW + colbase;
+      if constexpr (!FILL) {
+        container_values(v.payload, m, lane, 64, [&](int x) { atomicAdd(cc + x, 1u); });
+      } else {
+        const uint32_t* cp = colptr + int64_t(s) * CP_STRIDE + colbase;
+        uint16_t* sl = slots + entbase[s];
+        container_values(v.payload, m, lane, 64, [&](int x) {
+          const uint32_t pos = atomicAdd(cc + x, 1u);
+          sl[cp[x] + pos] = k;
+        });
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- src TopN
+
+__device__ __forceinline__ void hist_inc(uint32_t* h, int H, int k) {
+  if (k < H) {
+    atomicAdd(h + k, 1u);
+  } else {
+    const int r = k - H;
+    atomicAdd(h + H + (r >> 1), 1u << ((r & 1) * 16));
+  }
+}
+
+__device__ __forceinline__ uint32_t hist_get(const uint32_t* h, int H, int k) {
+  if (k < H) return h[k];
+  const int r = k - H;
+  return (h[H + (r >> 1)] >> ((r & 1) * 16)) & 0xffffu;
+}
+
+struct BlockScratch {
+  int wsum[TN_WAVES];
+  uint32_t wmin[TN_WAVES];
+  int wmax[TN_WAVES];
+};
+
+// Exclusive rank of `flag` among the block's threads (thread order) and the
+// block total.  Contains two barriers.
+__device__ __forceinline__ int block_rank(bool flag, BlockScratch& bs, int& total) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t m = __ballot(flag);
+  const int below = __popcll(m & ((uint64_t(1) << lane) - 1));
+  if (lane == 0) bs.wsum[wave] = __popcll(m);
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < TN_WAVES; w++) {
+    const int c = bs.wsum[w];
+    pre += w < wave ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return pre + below;
+}
+
+__device__ __forceinline__ void block_minmax(uint32_t vmin, int vmax, BlockScratch& bs, uint32_t& omin, int& omax) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    vmin = min(vmin, uint32_t(__shfl_xor(int(vmin), o, 64)));
+    vmax = max(vmax, __shfl_xor(vmax, o, 64));
+  }
+  if (lane == 0) {
+    bs.wmin[wave] = vmin;
+    bs.wmax[wave] = vmax;
+  }
+  __syncthreads();
+  uint32_t a = 0xffffffffu;
+  int b = -1;
+#pragma unroll
+  for (int w = 0; w < TN_WAVES; w++) {
+    a = min(a, bs.wmin[w]);
+    b = max(b, bs.wmax[w]);
+  }
+  __syncthreads();
+  omin = a;
+  omax = b;
+}
+
+// |src(q, s) ∩ row d of shard s| by probing the (sorted) materialised src
+// containers with the row's values: ids outside this shard's cache (rare, cold).
+__device__ uint32_t src_row_count(const ViewDev& v, int s, int d, const int32_t* scnt, const int64_t* soff,
+                                  const uint16_t* svals) {
+  const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+  const int64_t sb = v.shard_base[s];
+  uint32_t total = 0;
+  for (int64_t c = sb + rp[d]; c < sb + rp[d + 1]; c++) {
+    const int64_t m = v.meta[c];
+    const int j = meta_j(m);
+    const int n = scnt[j];
+    if (n <= 0) continue;
+    const uint16_t* a = svals + soff[j];
+    if (n > ARRAY_MAX) {
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(a);
+      container_values(v.payload, m, 0, 1, [&](int x) { total += uint32_t(w[x >> 6] >> (x & 63)) & 1u; });
+    } else {
+      container_values(v.payload, m, 0, 1, [&](int x) {
+        int lo = 0, hi = n;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (int(a[mid]) < x) lo = mid + 1; else hi = mid;
+        }
+        total += (lo < n && int(a[lo]) == x) ? 1u : 0u;
+      });
+    }
+  }
+  return total;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
+  extern __shared__ uint32_t hist[];
+  __shared__ BlockScratch bs;
+  const uint32_t unit = tn_xcd_remap(blockIdx.x, gridDim.x);
+  const int q = int(unit % p.Q), s = int(unit / p.Q);
+  const int tid = threadIdx.x;
+  const int K = p.K, H = p.H;
+  const int words = H + ((K - H + 1) >> 1);
+  for (int i = tid; i < words; i += TN_THREADS) hist[i] = 0;
+  __syncthreads();
+
+  // histogram of cache slots over src's columns
+  const int64_t kb = (int64_t(q) * p.S + s) * 16;
+  const uint16_t* sl = p.slots + p.entbase[s];
+  for (int j = 0; j < 16; j++) {
+    const int n = p.src_counts[kb + j];
+    if (n <= 0) continue;
+    const uint16_t* vals = p.src_vals + p.src_offs[kb + j];
+    const uint32_t* cp = p.colptr + int64_t(s) * CP_STRIDE + (int64_t(j) << 16);
+    auto emit = [&](int x) {
+      const uint32_t e1 = cp[x + 1];
+      for (uint32_t e = cp[x]; e < e1; e++) hist_inc(hist, H, sl[e]);
+    };
+    if (n <= ARRAY_MAX) {
+      for (int i = tid; i < n; i += TN_THREADS) emit(vals[i]);
+    } else {
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(vals);
+      for (int i = tid; i < 1024; i += TN_THREADS)
+        for (uint64_t b = w[i]; b; b &= b - 1) emit(i * 64 + __builtin_ctzll(b));
+    }
+  }
+  __syncthreads();
+
+  const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
+  if constexpr (MODE == 1) {
+    const int32_t* cc = p.cache_cnt + int64_t(s) * K;
+    const int32_t* ca = p.cache_acc + int64_t(s) * K;
+    int32_t* acc = p.acc + int64_t(q) * p.A;
+    const int nmax = p.ns[q];
+    int found = 0, P = -1;
+    uint32_t T = 0xffffffffu;
+    bool filled = false;
+    // fill phase: the first nmax slots with cached count and src count >= mt
+    for (int base = 0; base < K; base += TN_THREADS) {
+      const int k = base + tid;
+      const uint32_t cnt = k < K ? uint32_t(cc[k]) : 0u;
+      const uint32_t cv = k < K ? hist_get(hist, H, k) : 0u;
+      const bool ok = cnt >= mt && cv >= mt;
+      int tot;
+      const int rank = block_rank(ok, bs, tot);
+      const bool take = ok && (nmax == 0 || found + rank < nmax);
+      if (take) atomicAdd(acc + ca[k], int32_t(cv));
+      uint32_t tmin;
+      int pmax;
+      block_minmax(take ? cv : 0xffffffffu, take ? k : -1, bs, tmin, pmax);
+      T = min(T, tmin);
+      P = max(P, pmax);
+      found += tot;
+      if (nmax > 0 && found >= nmax) {
+        filled = true;
+        break;
+      }
+      // cached counts are sorted desc: nothing after a chunk ending below mt qualifies
+      if (uint32_t(cc[min(base + TN_THREADS, K) - 1]) < mt) break;
+    }
+    if (filled) {
+      // tail: rows whose cached count can still reach the heap minimum T
+      for (int base = P + 1; base < K; base += TN_THREADS) {
+        const int k = base + tid;
+        if (k < K && uint32_t(cc[k]) >= T) {
+          const uint32_t cv = hist_get(hist, H, k);
+          if (cv >= T) atomicAdd(acc + ca[k], int32_t(cv));
+        }
+        if (uint32_t(cc[min(base + TN_THREADS, K) - 1]) < T) break;
+      }
+    }
+  } else {
+    const int32_t* sm = p.slotmap + int64_t(s) * p.A;
+    const int64_t p0 = p.pair_off[q], p1 = p.pair_off[q + 1];
+    for (int64_t i = p0 + tid; i < p1; i += TN_THREADS) {
+      const int a = p.pair_idx[i];
+      const int k = sm[a];
+      uint32_t c = 0;
+      if (k >= 0) {
+        c = hist_get(hist, H, k);
+      } else {
+        const int d = p.a2dense[a];
+        if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
+      }
+      if (c >= mt) atomicAdd(p.out + i, (unsigned long long)c);
+    }
+  }
+}
+
+}  // namespace
+
+void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dense, uint32_t* colcnt,
+                       const uint32_t* colptr, const int64_t* entbase, uint16_t* slots, bool fill, hipStream_t st) {
+  const int64_t waves = int64_t(S) * K;
+  const int64_t want = (waves + 3) / 4;
+  const int blocks = int(want < 256 * 64 ? want : 256 * 64);
+  if (blocks <= 0) return;
+  if (fill)
+    hipLaunchKernelGGL(topn_index_kernel<true>, dim3(blocks), dim3(256), 0, st, v, S, K, cache_dense, colcnt, colptr,
+                       entbase, slots);
+  else
+    hipLaunchKernelGGL(topn_index_kernel<false>, dim3(blocks), dim3(256), 0, st, v, S, K, cache_dense, colcnt, colptr,
+                       entbase, slots);
+}
+
+int topn_lds_bytes(int K, int H) { return (H + ((K - H + 1) >> 1)) * 4; }
+
+void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st) {
+  const int lds = topn_lds_bytes(a.K, a.H);
+  const int64_t units = int64_t(a.Q) * a.S;
+  if (units <= 0) return;
+  if (mode == 1) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_src_kernel<1>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(topn_src_kernel<1>, dim3(unsigned(units)), dim3(TN_THREADS), lds, st, a);
+  } else {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_src_kernel<2>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(topn_src_kernel<2>, dim3(unsigned(units)), dim3(TN_THREADS), lds, st, a);
+  }
+}
+
+}  // namespace pk

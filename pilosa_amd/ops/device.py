@@ -665,16 +665,11 @@ class GpuEngine:
     def count(self, exprs: Sequence[object]) -> np.ndarray:
         return self.count_async(exprs).cpu().numpy()
 
-    def materialize(self, expr) -> Tuple[List[object], List[int]]:
-        """Evaluate one expression to per-shard host Bitmaps (row results)."""
-        from pilosa_amd import _roaring
-
+    def _materialize(self, progs: np.ndarray, views: List["DeviceView"], S: int):
         torch = self.torch
-        progs, views, S = self.compile_batch([expr])
-        if not S:
-            return [], []
+        Q = len(progs)
         tp, tv = self.upload_batch(progs, views)
-        counts = torch.zeros(S * 16, dtype=torch.int32, device=self.device)
+        counts = torch.zeros(Q * S * 16, dtype=torch.int32, device=self.device)
         self.ext.expr_count(tp, tv, S, torch.empty(0, dtype=torch.int64, device=self.device), counts,
                             2 if bool(flat_mask(progs).all()) else 0)
         sizes = torch.where(counts > 4096, torch.full_like(counts, 4096), (counts + 7) // 8 * 8).to(torch.int64)
@@ -684,6 +679,26 @@ class GpuEngine:
         outp = torch.zeros(max(total, 8), dtype=torch.int16, device=self.device)
         if total:
             self.ext.expr_materialize(tp, tv, S, counts, offs, outp)
+        return counts, offs, outp
+
+    def materialize_batch(self, exprs: Sequence[object], S: int):
+        """Device result containers of a batch of expressions over S local
+        shards: (counts int32[Q*S*16], u16 offsets int64[Q*S*16], payload
+        int16[]); container (q, s, j) is an array when 0 < n <= 4096, else a
+        bitmap of 4096 u16."""
+        progs, views, S2 = self.compile_batch(exprs)
+        if S2 != S:
+            raise CompileError(f"expressions span {S2} shards, expected {S}")
+        return self._materialize(progs, views, S)
+
+    def materialize(self, expr) -> Tuple[List[object], List[int]]:
+        """Evaluate one expression to per-shard host Bitmaps (row results)."""
+        from pilosa_amd import _roaring
+
+        progs, views, S = self.compile_batch([expr])
+        if not S:
+            return [], []
+        counts, offs, outp = self._materialize(progs, views, S)
         c = counts.cpu().numpy()
         o = offs.cpu().numpy()
         pay = outp.cpu().numpy().view(np.uint16)

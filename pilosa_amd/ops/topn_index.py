@@ -1,0 +1,239 @@
+"""Src-filtered TopN over an HBM-resident column-major slot index.
+
+Reference: fragment.go:1568-1700 (``top``: rank-cache walk with a src row,
+heap threshold, ids= re-count) and executor.go:863-930 (two phases, Pairs.Add
+over shards, trim to n).
+
+The pair-per-candidate formulation (ops/topn.py ``topn_phase1``) counts
+|src ∩ row| for every cached row the walk may reach: ~10k row intersections
+per (query, shard) on the Zipf headline index.  :class:`DeviceTopNIndex`
+keeps, next to a view's arena, the cache slot of every set bit of every
+cached row grouped by column (per shard: ``colptr[2^20+1]`` + u16 slots).
+The src counts of all cached rows of a shard are then one LDS histogram over
+src's columns, and the reference heap walk runs on that histogram inside the
+same workgroup (pilosa_amd/kernels/topn_kernels.hip).  Phase 1 leaves one
+dense accumulator per query over the node-wide "acc space" of row ids, so
+multi-GPU merging is a single all-reduce; phase 2 (the ids= re-count) reuses
+the kernel with a gather instead of the walk.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from pilosa_amd.models.cache import Pair
+
+from .device import DeviceView, GpuEngine, kernels
+
+SHARD_WIDTH = 1 << 20
+LDS_LIMIT = 160 * 1024 - 1024
+MAX_SLOTS = 65535
+
+
+def lds_bytes(K: int, H: int) -> int:
+    return (H + (K - H + 1) // 2) * 4
+
+
+class DeviceTopNIndex:
+    """Slot index of a view's rank caches (``cache``: a DeviceRankCache whose
+    rows are ordered count desc, id asc per shard).
+
+    ``space`` is the sorted row-id space of the phase-1/phase-2 accumulators;
+    pass the union of every rank's rows on a multi-GPU node (default: this
+    view's rows)."""
+
+    def __init__(self, view: DeviceView, cache, space: Optional[np.ndarray] = None):
+        import torch
+
+        ext = kernels()
+        S, K = cache.rows.shape
+        if K > MAX_SLOTS:
+            raise ValueError(f"rank cache of {K} slots exceeds the u16 slot index ({MAX_SLOTS})")
+        if S != view.S:
+            raise ValueError("rank cache and view disagree on the shard count")
+        dev = view.device
+        self.view, self.S, self.K = view, S, K
+        self.generation = view.generation
+        space = np.asarray(view.rows if space is None else space, dtype=np.uint64)
+        self.space = space
+        self.A = A = int(len(space))
+        counts = np.asarray(cache.counts, dtype=np.int64)
+        valid = counts > 0
+        rows = np.asarray(cache.rows, dtype=np.uint64).reshape(-1)
+        dense = view.dense_many(rows).reshape(S, K)
+        dense = np.where(valid, dense, -1)
+        acc_i = np.searchsorted(space, rows).reshape(S, K)
+        acc_i = np.minimum(acc_i, max(A - 1, 0))
+        if valid.any() and not np.array_equal(space[acc_i[valid]], rows.reshape(S, K)[valid]):
+            raise ValueError("acc space misses cached rows")
+        acc_i = np.where(valid, acc_i, 0)
+
+        def t32(a):
+            return torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(dev)
+
+        self.cache_dense = t32(dense)
+        self.cache_acc = t32(acc_i)
+        self.cache_cnt = t32(np.where(valid, np.minimum(counts, 2 ** 31 - 1), 0))
+        self.a2dense = t32(view.dense_many(space) if A else np.zeros(0))
+        hot = int((counts >= 65536).sum(axis=1).max()) if S else 0
+        self.H = min(K, (hot + 63) // 64 * 64)
+        self.lds = lds_bytes(K, self.H)
+        self.ok = self.lds <= LDS_LIMIT
+        self._vd = torch.from_numpy(np.frombuffer(view.viewdev().tobytes(), dtype=np.uint8).copy())
+
+        def empty(dt):
+            return torch.empty(0, dtype=dt, device=dev)
+
+        colcnt = torch.zeros(S * SHARD_WIDTH, dtype=torch.int32, device=dev)
+        if S:
+            ext.topn_index(self._vd, S, K, self.cache_dense, colcnt, empty(torch.int32), empty(torch.int64),
+                           empty(torch.int16), False)
+        self.colptr = torch.zeros((S, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
+        if S:
+            self.colptr[:, 1:] = torch.cumsum(colcnt.view(S, SHARD_WIDTH), dim=1, dtype=torch.int32)
+        tot = self.colptr[:, SHARD_WIDTH].to(torch.int64)
+        self.entbase = torch.zeros(max(S, 1), dtype=torch.int64, device=dev)
+        if S > 1:
+            self.entbase[1:S] = torch.cumsum(tot, 0)[:-1]
+        self.entries = int(tot.sum().item()) if S else 0
+        self.slots = torch.empty(max(self.entries, 1), dtype=torch.int16, device=dev)
+        if S:
+            colcnt.zero_()
+            ext.topn_index(self._vd, S, K, self.cache_dense, colcnt, self.colptr, self.entbase, self.slots, True)
+        del colcnt
+        self.slotmap = torch.full((S, max(A, 1)), -1, dtype=torch.int32, device=dev)
+        si, ki = torch.nonzero(self.cache_dense >= 0, as_tuple=True)
+        self.slotmap[si, self.cache_acc[si, ki].long()] = ki.to(torch.int32)
+        if A == 0:
+            self.slotmap = self.slotmap[:, :0].contiguous()
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.cache_dense, self.cache_acc, self.cache_cnt,
+                                                          self.a2dense, self.colptr, self.entbase, self.slots,
+                                                          self.slotmap))
+
+    @property
+    def stale(self) -> bool:
+        return self.view.generation != self.generation
+
+    # ------------------------------------------------------------ queries
+    def _launch(self, mode: int, Q: int, src, ns_t, th_t, acc=None, pair_off=None, pair_idx=None, out=None):
+        import torch
+
+        dev = self.view.device
+        counts, offs, vals = src
+        e32 = torch.empty(0, dtype=torch.int32, device=dev)
+        e64 = torch.empty(0, dtype=torch.int64, device=dev)
+        kernels().topn_src(self._vd, Q, self.S, self.K, self.H, self.A, counts, offs, vals, self.colptr,
+                           self.entbase, self.slots, self.cache_cnt, self.cache_acc, self.slotmap, self.a2dense,
+                           ns_t, th_t, mode, acc if acc is not None else e32,
+                           pair_off if pair_off is not None else e64, pair_idx if pair_idx is not None else e32,
+                           out if out is not None else e64)
+
+    def phase1(self, src, Q: int, ns: Sequence[int], thresholds: Sequence[int]):
+        """acc int32[Q, A]: per query the per-shard heap results summed by row."""
+        import torch
+
+        dev = self.view.device
+        ns_t = torch.tensor(list(ns), dtype=torch.int32).to(dev)
+        th_t = torch.tensor(list(thresholds), dtype=torch.int32).to(dev)
+        acc = torch.zeros((Q, self.A), dtype=torch.int32, device=dev)
+        if Q and self.S and self.A:
+            self._launch(1, Q, src, ns_t, th_t, acc=acc)
+        return acc, ns_t, th_t
+
+    def phase2(self, src, Q: int, ns_t, th_t, pair_q, pair_idx):
+        """Exact per-shard re-count of (query, acc index) pairs, summed over
+        the local shards where it reaches the threshold (ids= semantics)."""
+        import torch
+
+        dev = self.view.device
+        P = int(pair_idx.numel())
+        out = torch.zeros(P, dtype=torch.int64, device=dev)
+        if P and self.S:
+            off = torch.zeros(Q + 1, dtype=torch.int64, device=dev)
+            off[1:] = torch.cumsum(torch.bincount(pair_q, minlength=Q), 0)
+            self._launch(2, Q, src, ns_t, th_t, pair_off=off, pair_idx=pair_idx.to(torch.int32).contiguous(),
+                         out=out)
+        return out
+
+    def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
+             reduce: Optional[Callable[[object], object]] = None) -> List[List[Pair]]:
+        """TopN(field, src_q, n=ns[q], threshold=thresholds[q]) for a batch.
+        ``reduce`` sums a device tensor across the ranks of a node in place
+        (dist.all_reduce); every rank must call with the same batch."""
+        import torch
+
+        Q = len(srcs)
+        if Q == 0:
+            return []
+        src = engine.materialize_batch(srcs, self.S)
+        acc, ns_t, th_t = self.phase1(src, Q, ns, thresholds)
+        if reduce is not None:
+            reduce(acc)
+        nz = torch.nonzero(acc > 0)
+        pair_q = nz[:, 0].contiguous()
+        pair_idx = nz[:, 1].contiguous()
+        out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx)
+        if reduce is not None:
+            reduce(out)
+        return finish_batch(self.space, Q, pair_q.cpu().numpy(), pair_idx.cpu().numpy(), out.cpu().numpy(), ns)
+
+    def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int],
+                   reduce: Optional[Callable[[object], object]] = None) -> List[List[Pair]]:
+        """TopN(field, n) without a src row for a batch, all on the device.
+        Phase 1: per shard the first n cache entries at or above the
+        threshold (fragment.top stops once its heap holds n rows), summed by
+        row with one scatter-add; phase 2 (ids=): every shard's row count of
+        each phase-1 id where it reaches the threshold (``row_counts``: the
+        int32[S, D] per-shard row counts of the view)."""
+        import torch
+
+        Q = len(ns)
+        if Q == 0:
+            return []
+        dev = self.view.device
+        nmax = self.K if any(int(n) == 0 for n in ns) else min(self.K, max(int(n) for n in ns))
+        lim = torch.tensor([int(n) if int(n) else self.K for n in ns], dtype=torch.int64).to(dev)
+        mt = torch.tensor([max(1, int(t)) for t in thresholds], dtype=torch.int32).to(dev)
+        acc = torch.zeros((Q, max(self.A, 1)), dtype=torch.int32, device=dev)
+        if self.S and self.A and nmax:
+            cnt = self.cache_cnt[:, :nmax]                                       # [S, n]
+            k = torch.arange(nmax, device=dev)
+            take = (k[None, None, :] < lim[:, None, None]) & (cnt[None] >= mt[:, None, None])
+            vals = torch.where(take, cnt[None], torch.zeros((), dtype=torch.int32, device=dev))
+            idx = self.cache_acc[:, :nmax].reshape(1, -1).expand(Q, -1).to(torch.int64)
+            acc.scatter_add_(1, idx, vals.reshape(Q, -1))
+        if reduce is not None:
+            reduce(acc)
+        nz = torch.nonzero(acc > 0)
+        pq, pa = nz[:, 0], nz[:, 1]
+        out = torch.zeros(pa.numel(), dtype=torch.int64, device=dev)
+        if pa.numel() and self.S:
+            d = self.a2dense[pa].to(torch.int64)
+            c = row_counts.index_select(1, d.clamp(min=0))                       # [S, P]
+            c = torch.where((c >= mt[pq][None, :]) & (d[None, :] >= 0), c, torch.zeros_like(c))
+            out = c.sum(dim=0, dtype=torch.int64)
+        if reduce is not None:
+            reduce(out)
+        return finish_batch(self.space, Q, pq.cpu().numpy(), pa.cpu().numpy(), out.cpu().numpy(), ns)
+
+
+def finish_batch(space: np.ndarray, Q: int, pq: np.ndarray, pa: np.ndarray, cnt: np.ndarray,
+                 ns: Sequence[int]) -> List[List[Pair]]:
+    """Per query: pairs with a positive total, count desc then id asc, trimmed to n."""
+    keep = cnt > 0
+    pq, pa, cnt = pq[keep], pa[keep], cnt[keep]
+    ids = space[pa] if len(pa) else np.zeros(0, np.uint64)
+    order = np.lexsort((ids, -cnt, pq))
+    pq, ids, cnt = pq[order], ids[order], cnt[order]
+    bounds = np.searchsorted(pq, np.arange(Q + 1))
+    out = []
+    for q in range(Q):
+        lo, hi = int(bounds[q]), int(bounds[q + 1])
+        n = int(ns[q])
+        if n:
+            hi = min(hi, lo + n)
+        out.append([Pair(int(i), int(c)) for i, c in zip(ids[lo:hi].tolist(), cnt[lo:hi].tolist())])
+    return out

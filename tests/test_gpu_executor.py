@@ -285,3 +285,31 @@ def test_hbm_budget_lru_eviction(envs):
     st = small.stats()
     assert st["evictions"] >= 3 and st["arenas"] == 1
     assert sum(st["containers"].values()) > 0
+
+
+@pytest.mark.parametrize("k", [5000, 100, 7])
+def test_slot_index_topn_matches_replay(envs, k):
+    """Column-major slot index + LDS-histogram heap walk (ops/topn_index.py)
+    == the exact host replay over the same device rank cache; small caches
+    exercise the ids outside a shard's cache (in-kernel exact probe)."""
+    from pilosa_amd.ops.topn import DeviceRankCache, topn_batch
+    from pilosa_amd.ops.topn_index import DeviceTopNIndex
+    from pilosa_amd.pql import parse_string
+    cpu, gpu = envs
+    shards = cpu.holder.index("i").available_shards()
+    hv = gpu.view_arena("i", "h", "standard", shards)
+    cache = DeviceRankCache.from_view(hv, k=k)
+    idx = DeviceTopNIndex(hv, cache)
+    assert idx.ok and idx.entries > 0
+    cases = ["Row(f=2)", "Row(f=3)", "Row(g=1)", "Row(f=0)", "Row(h=0)", "Intersect(Row(f=0), Row(g=2))",
+             "Union(Row(f=20), Row(f=1))"]
+    srcs = [gpu.plan("i", parse_string(q).calls[0], shards) for q in cases]
+    for n, th in ((5, 1), (50, 1), (1000, 1), (20, 40), (0, 1)):
+        got = idx.topn(gpu.engine, srcs, [n] * len(srcs), [th] * len(srcs))
+        want = topn_batch(gpu.engine, hv, cache, srcs, n=n, threshold=th)
+        for q, g, w in zip(cases, got, want):
+            assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in w], (q, n, th, k)
+        if k == 5000 and th == 1 and n:
+            for q, g in zip(cases, got):
+                want = cpu.q1("i", f"TopN(h, {q}, n={n})")
+                assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in want], (q, n)
