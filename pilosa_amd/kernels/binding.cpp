@@ -196,11 +196,11 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, in
               torch::Tensor src_offs, torch::Tensor src_vals, torch::Tensor colptr, torch::Tensor entbase,
               torch::Tensor slots, torch::Tensor cache_cnt, torch::Tensor cache_acc, torch::Tensor slotmap,
               torch::Tensor a2dense, torch::Tensor ns, torch::Tensor min_threshold, int64_t mode, torch::Tensor acc,
-              torch::Tensor pair_off, torch::Tensor pair_idx, torch::Tensor out) {
+              torch::Tensor pair_off, torch::Tensor pair_idx, torch::Tensor out, torch::Tensor hist) {
   for (auto* t : {&src_counts, &src_offs, &src_vals, &colptr, &entbase, &slots, &cache_cnt, &cache_acc, &slotmap,
                   &a2dense, &ns, &min_threshold})
     check_dev(*t, "topn_src input");
-  TORCH_CHECK(mode == 1 || mode == 2, "topn_src mode");
+  TORCH_CHECK(mode >= 1 && mode <= 3, "topn_src mode");
   TORCH_CHECK(K > 0 && K <= 65535 && H >= 0 && H <= K, "topn_src K/H");
   TORCH_CHECK(pk::topn_lds_bytes(int(K), int(H)) <= 160 * 1024 - 1024, "slot histogram exceeds LDS");
   TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * S * 16,
@@ -236,6 +236,13 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, in
   a.a2dense = a2dense.data_ptr<int32_t>();
   a.ns = ns.data_ptr<int32_t>();
   a.min_threshold = min_threshold.data_ptr<int32_t>();
+  const int64_t hist_words = int64_t(pk::topn_lds_bytes(int(K), int(H)) / 4) * Q * S;
+  if (hist.numel() || mode == 3) {
+    check_dev(hist, "hist");
+    TORCH_CHECK(hist.scalar_type() == torch::kInt32 && hist.numel() == hist_words, "hist int32[Q*S*words]");
+    if (mode == 1) a.hist_out = reinterpret_cast<uint32_t*>(hist.data_ptr<int32_t>());
+    if (mode == 3) a.hist_in = reinterpret_cast<const uint32_t*>(hist.data_ptr<int32_t>());
+  }
   if (mode == 1) {
     check_dev(acc, "acc");
     TORCH_CHECK(acc.scalar_type() == torch::kInt32 && acc.numel() == Q * A, "acc int32[Q*A]");
@@ -273,6 +280,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
-  m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2 ids= re-count");
+  m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
 }

@@ -92,11 +92,14 @@ struct TopNLaunch {
   int32_t* acc;                   // mode 1: [Q][A] summed pushed counts
   const int64_t* pair_off;        // mode 2: [Q+1]
   const int32_t* pair_idx;        // mode 2: [P] acc index of each id
-  unsigned long long* out;        // mode 2: [P] summed counts >= threshold
+  unsigned long long* out;        // mode 2/3: [P] summed counts >= threshold
+  uint32_t* hist_out;             // mode 1 (optional): [Q*S][words] kept histograms
+  const uint32_t* hist_in;        // mode 3: histograms kept by mode 1
 };
 // LDS bytes of the (query, shard) slot histogram: H u32 slots + packed u16 rest.
 int topn_lds_bytes(int K, int H);
-// mode 1: phase-1 heap walk -> acc[Q][A]; mode 2: ids= re-count -> out[P].
+// mode 1: phase-1 heap walk -> acc[Q][A] (+ hist_out); mode 2: ids= re-count
+// -> out[P] (rebuilds the histograms); mode 3: ids= re-count from hist_in.
 void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
 
 }  // namespace pk

@@ -52,6 +52,16 @@ __device__ __forceinline__ uint32_t tn_xcd_remap(uint32_t bid, uint32_t nblk) {
   return base + loc;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TN_GLOBAL __attribute__((address_space(1)))
+#else
+#define TN_GLOBAL
+#endif
+template <class T>
+__device__ __forceinline__ const TN_GLOBAL T* gp(const T* ptr) {
+  return (const TN_GLOBAL T*)(ptr);
+}
+
 // f(x) for every value x of the container described by meta word m; the
 // threads tid, tid + nthr, ... of a group split the work.
 template <class F>
@@ -212,6 +222,10 @@ __device__ uint32_t src_row_count(const ViewDev& v, int s, int d, const int32_t*
   return total;
 }
 
+__device__ __forceinline__ int64_t unit_hist_base(const TopNLaunch& p, int q, int s, int words) {
+  return (int64_t(q) * p.S + s) * int64_t(words);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
   extern __shared__ uint32_t hist[];
@@ -224,27 +238,64 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
   for (int i = tid; i < words; i += TN_THREADS) hist[i] = 0;
   __syncthreads();
 
-  // histogram of cache slots over src's columns
+  // histogram of cache slots over src's columns, 4 columns per thread in
+  // flight: the colptr pairs and slot runs of a batch are independent global
+  // loads (global address space, so they are not ordered behind the LDS atomics)
   const int64_t kb = (int64_t(q) * p.S + s) * 16;
-  const uint16_t* sl = p.slots + p.entbase[s];
+  const auto sl = gp(p.slots + p.entbase[s]);
   for (int j = 0; j < 16; j++) {
     const int n = p.src_counts[kb + j];
     if (n <= 0) continue;
-    const uint16_t* vals = p.src_vals + p.src_offs[kb + j];
-    const uint32_t* cp = p.colptr + int64_t(s) * CP_STRIDE + (int64_t(j) << 16);
-    auto emit = [&](int x) {
-      const uint32_t e1 = cp[x + 1];
-      for (uint32_t e = cp[x]; e < e1; e++) hist_inc(hist, H, sl[e]);
+    const auto vals = gp(p.src_vals + p.src_offs[kb + j]);
+    const auto cp = gp(p.colptr + int64_t(s) * CP_STRIDE + (int64_t(j) << 16));
+    auto run4 = [&](const int (&x)[4]) {
+      uint32_t e0[4], e1[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        e0[r] = x[r] >= 0 ? cp[x[r]] : 0u;
+        e1[r] = x[r] >= 0 ? cp[x[r] + 1] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        for (uint32_t e = e0[r]; e < e1[r]; e += 4) {
+          uint16_t k4[4];
+#pragma unroll
+          for (int t = 0; t < 4; t++) k4[t] = e + t < e1[r] ? sl[e + t] : uint16_t(0);
+#pragma unroll
+          for (int t = 0; t < 4; t++)
+            if (e + t < e1[r]) hist_inc(hist, H, k4[t]);
+        }
+      }
     };
     if (n <= ARRAY_MAX) {
-      for (int i = tid; i < n; i += TN_THREADS) emit(vals[i]);
+      for (int i = tid; i < n; i += 4 * TN_THREADS) {
+        int x[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) x[r] = i + r * TN_THREADS < n ? int(vals[i + r * TN_THREADS]) : -1;
+        run4(x);
+      }
     } else {
-      const uint64_t* w = reinterpret_cast<const uint64_t*>(vals);
-      for (int i = tid; i < 1024; i += TN_THREADS)
-        for (uint64_t b = w[i]; b; b &= b - 1) emit(i * 64 + __builtin_ctzll(b));
+      const auto w = gp(reinterpret_cast<const uint64_t*>(p.src_vals + p.src_offs[kb + j]));
+      for (int i = tid; i < 1024; i += TN_THREADS) {
+        uint64_t b = w[i];
+        while (b) {
+          int x[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            x[r] = b ? i * 64 + __builtin_ctzll(b) : -1;
+            b &= b ? b - 1 : 0;
+          }
+          run4(x);
+        }
+      }
     }
   }
   __syncthreads();
+  if (MODE == 1 && p.hist_out) {
+    // keep the histogram for the ids= re-count (topn_gather_kernel)
+    uint32_t* ho = p.hist_out + unit_hist_base(p, q, s, words);
+    for (int i = tid; i < words; i += TN_THREADS) ho[i] = hist[i];
+  }
 
   const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
   if constexpr (MODE == 1) {
@@ -307,6 +358,32 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
   }
 }
 
+// ids= re-count from the histograms phase 1 kept (hist_in): one 256-thread
+// block per (query, shard) gathers the slot counts of that query's ids.
+__global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
+  const uint32_t unit = tn_xcd_remap(blockIdx.x, gridDim.x);
+  const int q = int(unit % p.Q), s = int(unit / p.Q);
+  const int K = p.K, H = p.H;
+  const int words = H + ((K - H + 1) >> 1);
+  const auto h = gp(p.hist_in + unit_hist_base(p, q, s, words));
+  const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
+  const int32_t* sm = p.slotmap + int64_t(s) * p.A;
+  const int64_t kb = (int64_t(q) * p.S + s) * 16;
+  const int64_t p0 = p.pair_off[q], p1 = p.pair_off[q + 1];
+  for (int64_t i = p0 + threadIdx.x; i < p1; i += blockDim.x) {
+    const int a = p.pair_idx[i];
+    const int k = sm[a];
+    uint32_t c = 0;
+    if (k >= 0) {
+      c = k < H ? h[k] : (h[H + ((k - H) >> 1)] >> (((k - H) & 1) * 16)) & 0xffffu;
+    } else {
+      const int d = p.a2dense[a];
+      if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
+    }
+    if (c >= mt) atomicAdd(p.out + i, (unsigned long long)c);
+  }
+}
+
 }  // namespace
 
 void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dense, uint32_t* colcnt,
@@ -329,7 +406,9 @@ void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st) {
   const int lds = topn_lds_bytes(a.K, a.H);
   const int64_t units = int64_t(a.Q) * a.S;
   if (units <= 0) return;
-  if (mode == 1) {
+  if (mode == 3) {
+    hipLaunchKernelGGL(topn_gather_kernel, dim3(unsigned(units)), dim3(256), 0, st, a);
+  } else if (mode == 1) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_src_kernel<1>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(topn_src_kernel<1>, dim3(unsigned(units)), dim3(TN_THREADS), lds, st, a);

@@ -61,6 +61,8 @@ def pairs_add(a: Iterable[Pair], b: Iterable[Pair]) -> List[Pair]:
 
 
 class NopCache:
+    version = 0
+
     def add(self, id, n):
         pass
 
@@ -91,9 +93,11 @@ class LRUCache:
         self.max_entries = int(max_entries)
         self._d: "collections.OrderedDict[int, int]" = collections.OrderedDict()
         self._lock = threading.Lock()
+        self.version = 0
 
     def add(self, id, n):
         with self._lock:
+            self.version += 1
             self._d[id] = n
             self._d.move_to_end(id)
             while self.max_entries > 0 and len(self._d) > self.max_entries:
@@ -131,6 +135,7 @@ class RankCache:
         self.threshold_buffer = int(THRESHOLD_FACTOR * self.max_entries)
         self.entries: Dict[int, int] = {}
         self.rankings: List[Tuple[int, int]] = []
+        self.version = 0  # bumped whenever top() can change (device TopN index validity)
         self.threshold_value = 0
         self.update_time = 0.0
         self._lock = threading.Lock()
@@ -182,6 +187,7 @@ class RankCache:
         else:
             self.threshold_value = 1
         self.rankings = rankings
+        self.version += 1
         self.update_time = time.monotonic()
         if len(self.entries) > self.threshold_buffer:
             for id, _ in remove:

@@ -8,8 +8,10 @@ device arenas of the involved field-views:
 * ``count``     Count(<bitmap tree>)                 -> expr_count
 * ``bitmap``    Row/Intersect/Union/Difference/Xor/Not/time ranges -> materialize
 * ``bsi_sum``   Sum(<filter>, field=f)                -> bsi_sum kernel
-* ``topn``      TopN phase-1/phase-2 with src          -> per-shard counts +
-                reference heap semantics replayed on host (fragment.top)
+* ``topn``      TopN phase-1/phase-2 with src          -> slot-index LDS
+                histogram + in-kernel heap walk (ops/topn_index.py); while
+                that index is stale: per-shard pair counts + the reference
+                heap semantics replayed on host (fragment.top)
 * ``group_by``  GroupBy(Rows..., filter)               -> batched k-way counts
 
 Arenas are (re)built lazily from the host fragments and cached per
@@ -19,7 +21,9 @@ expressible on the device raises ``NotImplementedError`` -> host fallback.
 """
 from __future__ import annotations
 
+import os
 import threading
+import time
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -35,6 +39,9 @@ from pilosa_amd.pql import Call
 from .device import CompileError, DeviceView, GpuEngine, Leaf, Op
 
 MAX_GROUPS_PER_LAUNCH = 1 << 16
+# minimum spacing of device TopN index rebuilds per view (the reference
+# re-ranks its caches at most every 10 s too, cache.go:235-243)
+TOPN_INDEX_REBUILD_S = float(os.environ.get("PILOSA_TOPN_INDEX_REBUILD_S", "10"))
 
 
 class _Empty:
@@ -61,6 +68,8 @@ class GpuExecutor:
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
+        self.topn_index_enabled = os.environ.get("PILOSA_TOPN_INDEX", "1") != "0"
+        self._topn_indexes: Dict[Tuple, Tuple] = {}  # (index, field, shards) -> (versions, index, built_at)
 
     # ------------------------------------------------------------ arenas
     def view_arena(self, index: str, field: str, view: str, shards: Sequence[int]) -> Optional[DeviceView]:
@@ -163,6 +172,7 @@ class GpuExecutor:
         with self.mu:
             self._arenas.clear()
             self._bsi_views.clear()
+            self._topn_indexes.clear()
 
     BSI_CACHE = 8
 
@@ -420,6 +430,11 @@ class GpuExecutor:
         if src is EMPTY:
             return []
         rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+        if not ids or threshold <= 1:
+            tix = self._topn_index(index, fname, shards, frags, rv)
+            if tix is not None:
+                self.launches += 1
+                return sort_pairs(tix.shard_pairs(self.engine, src, 0 if ids else n, threshold, ids or None))
         # Each shard's fragment.top() walks its cache in order and stops once a
         # row's cached count falls below the heap threshold, so usually only a
         # short prefix of the (up to cache-size) candidates is ever counted.
@@ -460,6 +475,42 @@ class GpuExecutor:
                     total[p.id] = total.get(p.id, 0) + p.count
             pending = nxt
         return sort_pairs([Pair(k2, v) for k2, v in total.items()])
+
+    def _topn_index(self, index: str, fname: str, shards: List[int], frags, rv):
+        """Device slot index (ops/topn_index.py) of the fragments' rank caches,
+        rebuilt when a cache re-ranks or the arena changes, at most once per
+        TOPN_INDEX_REBUILD_S per view (stale in between: pair-count path)."""
+        if rv is None or not self.topn_index_enabled:
+            return None
+        from pilosa_amd.ops.topn import DeviceRankCache
+        from pilosa_amd.ops.topn_index import MAX_SLOTS, DeviceTopNIndex
+        key = (index, fname, tuple(shards))
+        ver = tuple(getattr(f.cache, "version", -1) if f is not None else -2 for f in frags)
+        ent = self._topn_indexes.get(key)
+        if ent is not None and ent[0] == ver and ent[1].view is rv and not ent[1].stale:
+            return ent[1]
+        now = time.monotonic()
+        if ent is not None and now - ent[2] < TOPN_INDEX_REBUILD_S:
+            return None
+        lists = [list(f.cache.top()) if f is not None else [] for f in frags]
+        K = max((len(x) for x in lists), default=0)
+        if K == 0 or K > MAX_SLOTS:
+            return None
+        rows = np.zeros((len(frags), K), np.int64)
+        counts = np.zeros((len(frags), K), np.int64)
+        for si, pairs in enumerate(lists):
+            if pairs:
+                a = np.asarray(pairs, dtype=np.int64)
+                rows[si, :len(a)] = a[:, 0]
+                counts[si, :len(a)] = a[:, 1]
+        try:
+            tix = DeviceTopNIndex(rv, DeviceRankCache(rows, counts))
+        except ValueError:
+            return None
+        if not tix.ok:
+            return None
+        self._topn_indexes[key] = (ver, tix, now)
+        return tix
 
     # ------------------------------------------------------------ GroupBy
     def group_by(self, index: str, c: Call, filt: Optional[Call], shards: List[int], child_rows, limit: int):

@@ -29,6 +29,8 @@ from .device import DeviceView, GpuEngine, kernels
 SHARD_WIDTH = 1 << 20
 LDS_LIMIT = 160 * 1024 - 1024
 MAX_SLOTS = 65535
+# phase-1 histograms are kept for the ids= gather up to this many bytes per batch
+HIST_KEEP_BYTES = 8 << 30
 
 
 def lds_bytes(K: int, H: int) -> int:
@@ -118,7 +120,8 @@ class DeviceTopNIndex:
         return self.view.generation != self.generation
 
     # ------------------------------------------------------------ queries
-    def _launch(self, mode: int, Q: int, src, ns_t, th_t, acc=None, pair_off=None, pair_idx=None, out=None):
+    def _launch(self, mode: int, Q: int, src, ns_t, th_t, acc=None, pair_off=None, pair_idx=None, out=None,
+                hist=None):
         import torch
 
         dev = self.view.device
@@ -129,23 +132,30 @@ class DeviceTopNIndex:
                            self.entbase, self.slots, self.cache_cnt, self.cache_acc, self.slotmap, self.a2dense,
                            ns_t, th_t, mode, acc if acc is not None else e32,
                            pair_off if pair_off is not None else e64, pair_idx if pair_idx is not None else e32,
-                           out if out is not None else e64)
+                           out if out is not None else e64, hist if hist is not None else e32)
 
-    def phase1(self, src, Q: int, ns: Sequence[int], thresholds: Sequence[int]):
-        """acc int32[Q, A]: per query the per-shard heap results summed by row."""
+    def hist_bytes(self, Q: int) -> int:
+        return self.lds * Q * self.S
+
+    def phase1(self, src, Q: int, ns: Sequence[int], thresholds: Sequence[int], keep_hist: bool = False):
+        """acc int32[Q, A]: per query the per-shard heap results summed by row.
+        ``keep_hist`` also returns the (query, shard) slot histograms so the
+        ids= re-count is a gather (else None)."""
         import torch
 
         dev = self.view.device
         ns_t = torch.tensor(list(ns), dtype=torch.int32).to(dev)
         th_t = torch.tensor(list(thresholds), dtype=torch.int32).to(dev)
         acc = torch.zeros((Q, self.A), dtype=torch.int32, device=dev)
+        hist = torch.empty(self.hist_bytes(Q) // 4, dtype=torch.int32, device=dev) if keep_hist else None
         if Q and self.S and self.A:
-            self._launch(1, Q, src, ns_t, th_t, acc=acc)
-        return acc, ns_t, th_t
+            self._launch(1, Q, src, ns_t, th_t, acc=acc, hist=hist)
+        return acc, ns_t, th_t, hist
 
-    def phase2(self, src, Q: int, ns_t, th_t, pair_q, pair_idx):
+    def phase2(self, src, Q: int, ns_t, th_t, pair_q, pair_idx, hist=None):
         """Exact per-shard re-count of (query, acc index) pairs, summed over
-        the local shards where it reaches the threshold (ids= semantics)."""
+        the local shards where it reaches the threshold (ids= semantics);
+        from phase 1's kept histograms when given, else rebuilt."""
         import torch
 
         dev = self.view.device
@@ -154,8 +164,8 @@ class DeviceTopNIndex:
         if P and self.S:
             off = torch.zeros(Q + 1, dtype=torch.int64, device=dev)
             off[1:] = torch.cumsum(torch.bincount(pair_q, minlength=Q), 0)
-            self._launch(2, Q, src, ns_t, th_t, pair_off=off, pair_idx=pair_idx.to(torch.int32).contiguous(),
-                         out=out)
+            self._launch(3 if hist is not None else 2, Q, src, ns_t, th_t, pair_off=off,
+                         pair_idx=pair_idx.to(torch.int32).contiguous(), out=out, hist=hist)
         return out
 
     def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
@@ -169,16 +179,46 @@ class DeviceTopNIndex:
         if Q == 0:
             return []
         src = engine.materialize_batch(srcs, self.S)
-        acc, ns_t, th_t = self.phase1(src, Q, ns, thresholds)
+        keep = self.hist_bytes(Q) <= HIST_KEEP_BYTES
+        acc, ns_t, th_t, hist = self.phase1(src, Q, ns, thresholds, keep_hist=keep)
         if reduce is not None:
             reduce(acc)
         nz = torch.nonzero(acc > 0)
         pair_q = nz[:, 0].contiguous()
         pair_idx = nz[:, 1].contiguous()
-        out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx)
+        out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx, hist=hist)
         if reduce is not None:
             reduce(out)
         return finish_batch(self.space, Q, pair_q.cpu().numpy(), pair_idx.cpu().numpy(), out.cpu().numpy(), ns)
+
+    def shard_pairs(self, engine: GpuEngine, src, n: int, threshold: int,
+                    ids: Optional[Sequence[int]] = None) -> List[Pair]:
+        """One TopN call over the local shards as the executor's map step
+        sees it (executor.go:905-930): without ``ids`` the per-shard heap
+        results summed by row (phase 1, untrimmed); with ``ids`` the exact
+        re-count of those rows (phase 2, summed where >= threshold)."""
+        import torch
+
+        dev = self.view.device
+        src_t = engine.materialize_batch([src], self.S)
+        if ids is None:
+            acc, _, _, _ = self.phase1(src_t, 1, [n], [threshold])
+            nz = torch.nonzero(acc[0] > 0).reshape(-1)
+            a = nz.cpu().numpy()
+            c = acc[0].index_select(0, nz).cpu().numpy()
+        else:
+            want = np.unique(np.asarray(list(ids), dtype=np.uint64))
+            pos = np.searchsorted(self.space, want)
+            pos = np.minimum(pos, max(self.A - 1, 0))
+            a = pos[(self.A > 0) & (self.space[pos] == want)] if self.A else np.zeros(0, np.int64)
+            ns_t = torch.zeros(1, dtype=torch.int32, device=dev)
+            th_t = torch.tensor([threshold], dtype=torch.int32).to(dev)
+            pa = torch.from_numpy(a.astype(np.int64)).to(dev)
+            out = self.phase2(src_t, 1, ns_t, th_t, torch.zeros_like(pa), pa)
+            c = out.cpu().numpy()
+        keep = c > 0
+        ids_out = self.space[a[keep]] if len(a) else np.zeros(0, np.uint64)
+        return [Pair(int(i), int(v)) for i, v in zip(ids_out.tolist(), c[keep].tolist())]
 
     def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int],
                    reduce: Optional[Callable[[object], object]] = None) -> List[List[Pair]]:
