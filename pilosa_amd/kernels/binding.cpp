@@ -192,7 +192,7 @@ void topn_index(torch::Tensor view, int64_t S, int64_t K, torch::Tensor cache_de
   check_launch("topn_index");
 }
 
-void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, int64_t A, torch::Tensor src_counts,
+void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, int64_t H16, int64_t A, torch::Tensor src_counts,
               torch::Tensor src_offs, torch::Tensor src_vals, torch::Tensor colptr, torch::Tensor entbase,
               torch::Tensor slots, torch::Tensor cache_cnt, torch::Tensor cache_acc, torch::Tensor slotmap,
               torch::Tensor a2dense, torch::Tensor ns, torch::Tensor min_threshold, int64_t mode, torch::Tensor acc,
@@ -201,8 +201,8 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, in
                   &a2dense, &ns, &min_threshold})
     check_dev(*t, "topn_src input");
   TORCH_CHECK(mode >= 1 && mode <= 3, "topn_src mode");
-  TORCH_CHECK(K > 0 && K <= 65535 && H >= 0 && H <= K, "topn_src K/H");
-  TORCH_CHECK(pk::topn_lds_bytes(int(K), int(H)) <= 160 * 1024 - 1024, "slot histogram exceeds LDS");
+  TORCH_CHECK(K > 0 && K <= 65535 && H32 >= 0 && H32 <= H16 && H16 <= K, "topn_src K/H32/H16");
+  TORCH_CHECK(pk::topn_lds_bytes(int(K), int(H32), int(H16)) <= 160 * 1024 - 1024, "slot histogram exceeds LDS");
   TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * S * 16,
               "src_counts int32[Q*S*16]");
   TORCH_CHECK(src_offs.scalar_type() == torch::kInt64 && src_offs.numel() == Q * S * 16, "src_offs int64[Q*S*16]");
@@ -222,7 +222,8 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, in
   a.Q = int(Q);
   a.S = int(S);
   a.K = int(K);
-  a.H = int(H);
+  a.H32 = int(H32);
+  a.H16 = int(H16);
   a.A = A;
   a.src_counts = src_counts.data_ptr<int32_t>();
   a.src_offs = src_offs.data_ptr<int64_t>();
@@ -236,7 +237,7 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H, in
   a.a2dense = a2dense.data_ptr<int32_t>();
   a.ns = ns.data_ptr<int32_t>();
   a.min_threshold = min_threshold.data_ptr<int32_t>();
-  const int64_t hist_words = int64_t(pk::topn_lds_bytes(int(K), int(H)) / 4) * Q * S;
+  const int64_t hist_words = int64_t(pk::topn_lds_bytes(int(K), int(H32), int(H16)) / 4) * Q * S;
   if (hist.numel() || mode == 3) {
     check_dev(hist, "hist");
     TORCH_CHECK(hist.scalar_type() == torch::kInt32 && hist.numel() == hist_words, "hist int32[Q*S*words]");

@@ -75,7 +75,8 @@ void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dens
 // A sorted row ids (identical on every rank of a node).
 struct TopNLaunch {
   ViewDev v;                      // the TopN field's view (fallback probes)
-  int Q, S, K, H;                 // queries, shards, cache slots, u32 slots
+  int Q, S, K;                     // queries, shards, cache slots
+  int H32, H16;                   // counter tiers: u32 < H32 <= u16 < H16 <= u8
   int64_t A;                      // acc-space size
   const int32_t* src_counts;      // [Q*S*16] materialised src containers
   const int64_t* src_offs;        // [Q*S*16] u16 offsets into src_vals
@@ -95,9 +96,10 @@ struct TopNLaunch {
   unsigned long long* out;        // mode 2/3: [P] summed counts >= threshold
   uint32_t* hist_out;             // mode 1 (optional): [Q*S][words] kept histograms
   const uint32_t* hist_in;        // mode 3: histograms kept by mode 1
+  int dbg;                        // profiling builds: bit 0 skip histogram, bit 1 skip walk
 };
-// LDS bytes of the (query, shard) slot histogram: H u32 slots + packed u16 rest.
-int topn_lds_bytes(int K, int H);
+// LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).
+int topn_lds_bytes(int K, int H32, int H16);
 // mode 1: phase-1 heap walk -> acc[Q][A] (+ hist_out); mode 2: ids= re-count
 // -> out[P] (rebuilds the histograms); mode 3: ids= re-count from hist_in.
 void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);

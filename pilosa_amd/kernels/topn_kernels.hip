@@ -16,9 +16,9 @@
 // set bit of a cached row), so the src counts of ALL cached rows of a shard
 // are one histogram over src's columns: |src_s| x (bits per column) LDS
 // increments.  One 1024-thread workgroup owns one (query, shard):
-//   1. zero an LDS histogram over the K cache slots (u32 for the hot slots
-//      whose counts can reach 2^16, packed u16 for the rest: K = 50,000 fits
-//      in ~100 KB of the 160 KB LDS);
+//   1. zero an LDS histogram over the K cache slots (u32 / u16 / u8 counters
+//      by the slot's cached-count bound: K = 50,000 Zipf slots fit in ~52 KB,
+//      two 1024-thread workgroups per CU);
 //   2. stream src's materialised columns and, per column, its slot list;
 //   3. mode 1: run the reference heap walk with block scans over the slots
 //      (fill = first n qualifying slots, T = their min, then the sorted cache
@@ -31,6 +31,7 @@
 // containers (count per column, then scatter slots behind an exclusive scan).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.h"
 
@@ -127,19 +128,42 @@ __global__ __launch_bounds__(256) void topn_index_kernel(ViewDev v, int S, int K
 
 // ---------------------------------------------------------------- src TopN
 
-__device__ __forceinline__ void hist_inc(uint32_t* h, int H, int k) {
-  if (k < H) {
+// Slot histogram layout, three counter widths chosen from the cached counts
+// (a slot's src count never exceeds its row's count in the shard):
+//   [0, H32)   u32   slots whose cached count can reach 2^16
+//   [H32, H16) u16   two per word (cached counts < 2^16 in every shard)
+//   [H16, K)   u8    four per word (cached counts < 2^8)
+// Packed fields are bumped with a shifted 32-bit LDS atomic add; they never
+// carry into their neighbour because the count bound holds.
+struct HistLayout {
+  int H32, H16, W16, words;
+  __device__ __forceinline__ HistLayout(int K, int h32, int h16) : H32(h32), H16(h16) {
+    W16 = H32 + ((H16 - H32 + 1) >> 1);
+    words = W16 + ((K - H16 + 3) >> 2);
+  }
+};
+
+__device__ __forceinline__ void hist_inc(uint32_t* h, const HistLayout& L, int k) {
+  if (k < L.H32) {
     atomicAdd(h + k, 1u);
+  } else if (k < L.H16) {
+    const int r = k - L.H32;
+    atomicAdd(h + L.H32 + (r >> 1), 1u << ((r & 1) * 16));
   } else {
-    const int r = k - H;
-    atomicAdd(h + H + (r >> 1), 1u << ((r & 1) * 16));
+    const int r = k - L.H16;
+    atomicAdd(h + L.W16 + (r >> 2), 1u << ((r & 3) * 8));
   }
 }
 
-__device__ __forceinline__ uint32_t hist_get(const uint32_t* h, int H, int k) {
-  if (k < H) return h[k];
-  const int r = k - H;
-  return (h[H + (r >> 1)] >> ((r & 1) * 16)) & 0xffffu;
+template <class P>
+__device__ __forceinline__ uint32_t hist_get(P h, const HistLayout& L, int k) {
+  if (k < L.H32) return h[k];
+  if (k < L.H16) {
+    const int r = k - L.H32;
+    return (h[L.H32 + (r >> 1)] >> ((r & 1) * 16)) & 0xffffu;
+  }
+  const int r = k - L.H16;
+  return (h[L.W16 + (r >> 2)] >> ((r & 3) * 8)) & 0xffu;
 }
 
 struct BlockScratch {
@@ -227,14 +251,15 @@ __device__ __forceinline__ int64_t unit_hist_base(const TopNLaunch& p, int q, in
 }
 
 template <int MODE>
-__global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
+__global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
   extern __shared__ uint32_t hist[];
   __shared__ BlockScratch bs;
   const uint32_t unit = tn_xcd_remap(blockIdx.x, gridDim.x);
   const int q = int(unit % p.Q), s = int(unit / p.Q);
   const int tid = threadIdx.x;
-  const int K = p.K, H = p.H;
-  const int words = H + ((K - H + 1) >> 1);
+  const int K = p.K;
+  const HistLayout L(K, p.H32, p.H16);
+  const int words = L.words;
   for (int i = tid; i < words; i += TN_THREADS) hist[i] = 0;
   __syncthreads();
 
@@ -243,7 +268,7 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
   // loads (global address space, so they are not ordered behind the LDS atomics)
   const int64_t kb = (int64_t(q) * p.S + s) * 16;
   const auto sl = gp(p.slots + p.entbase[s]);
-  for (int j = 0; j < 16; j++) {
+  for (int j = 0; j < ((p.dbg & 1) ? 0 : 16); j++) {
     const int n = p.src_counts[kb + j];
     if (n <= 0) continue;
     const auto vals = gp(p.src_vals + p.src_offs[kb + j]);
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
           for (int t = 0; t < 4; t++) k4[t] = e + t < e1[r] ? sl[e + t] : uint16_t(0);
 #pragma unroll
           for (int t = 0; t < 4; t++)
-            if (e + t < e1[r]) hist_inc(hist, H, k4[t]);
+            if (e + t < e1[r]) hist_inc(hist, L, k4[t]);
         }
       }
     };
@@ -298,6 +323,7 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
   }
 
   const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
+  if (MODE == 1 && (p.dbg & 2)) return;
   if constexpr (MODE == 1) {
     const int32_t* cc = p.cache_cnt + int64_t(s) * K;
     const int32_t* ca = p.cache_acc + int64_t(s) * K;
@@ -310,7 +336,7 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
     for (int base = 0; base < K; base += TN_THREADS) {
       const int k = base + tid;
       const uint32_t cnt = k < K ? uint32_t(cc[k]) : 0u;
-      const uint32_t cv = k < K ? hist_get(hist, H, k) : 0u;
+      const uint32_t cv = k < K ? hist_get(hist, L, k) : 0u;
       const bool ok = cnt >= mt && cv >= mt;
       int tot;
       const int rank = block_rank(ok, bs, tot);
@@ -319,9 +345,10 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
       uint32_t tmin;
       int pmax;
       block_minmax(take ? cv : 0xffffffffu, take ? k : -1, bs, tmin, pmax);
-      T = min(T, tmin);
-      P = max(P, pmax);
-      found += tot;
+      // block-uniform: keep them in SGPRs
+      T = min(T, uint32_t(__builtin_amdgcn_readfirstlane(int(tmin))));
+      P = max(P, __builtin_amdgcn_readfirstlane(pmax));
+      found += __builtin_amdgcn_readfirstlane(tot);
       if (nmax > 0 && found >= nmax) {
         filled = true;
         break;
@@ -334,7 +361,7 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
       for (int base = P + 1; base < K; base += TN_THREADS) {
         const int k = base + tid;
         if (k < K && uint32_t(cc[k]) >= T) {
-          const uint32_t cv = hist_get(hist, H, k);
+          const uint32_t cv = hist_get(hist, L, k);
           if (cv >= T) atomicAdd(acc + ca[k], int32_t(cv));
         }
         if (uint32_t(cc[min(base + TN_THREADS, K) - 1]) < T) break;
@@ -348,7 +375,7 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
       const int k = sm[a];
       uint32_t c = 0;
       if (k >= 0) {
-        c = hist_get(hist, H, k);
+        c = hist_get(hist, L, k);
       } else {
         const int d = p.a2dense[a];
         if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
@@ -363,9 +390,8 @@ __global__ __launch_bounds__(TN_THREADS) void topn_src_kernel(TopNLaunch p) {
 __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
   const uint32_t unit = tn_xcd_remap(blockIdx.x, gridDim.x);
   const int q = int(unit % p.Q), s = int(unit / p.Q);
-  const int K = p.K, H = p.H;
-  const int words = H + ((K - H + 1) >> 1);
-  const auto h = gp(p.hist_in + unit_hist_base(p, q, s, words));
+  const HistLayout L(p.K, p.H32, p.H16);
+  const auto h = gp(p.hist_in + unit_hist_base(p, q, s, L.words));
   const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
   const int32_t* sm = p.slotmap + int64_t(s) * p.A;
   const int64_t kb = (int64_t(q) * p.S + s) * 16;
@@ -375,7 +401,7 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
     const int k = sm[a];
     uint32_t c = 0;
     if (k >= 0) {
-      c = k < H ? h[k] : (h[H + ((k - H) >> 1)] >> (((k - H) & 1) * 16)) & 0xffffu;
+      c = hist_get(h, L, k);
     } else {
       const int d = p.a2dense[a];
       if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
@@ -400,10 +426,18 @@ void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dens
                        entbase, slots);
 }
 
-int topn_lds_bytes(int K, int H) { return (H + ((K - H + 1) >> 1)) * 4; }
+int topn_lds_bytes(int K, int H32, int H16) {
+  return (H32 + ((H16 - H32 + 1) >> 1) + ((K - H16 + 3) >> 2)) * 4;
+}
 
-void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st) {
-  const int lds = topn_lds_bytes(a.K, a.H);
+void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
+  TopNLaunch a = a0;
+  static const int dbg = [] {
+    const char* e = getenv("PILOSA_TOPN_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
+  const int lds = topn_lds_bytes(a.K, a.H32, a.H16);
   const int64_t units = int64_t(a.Q) * a.S;
   if (units <= 0) return;
   if (mode == 3) {

@@ -33,8 +33,10 @@ MAX_SLOTS = 65535
 HIST_KEEP_BYTES = 8 << 30
 
 
-def lds_bytes(K: int, H: int) -> int:
-    return (H + (K - H + 1) // 2) * 4
+def lds_bytes(K: int, H32: int, H16: int) -> int:
+    """Slot histogram bytes: u32 counters below H32, u16 below H16, u8 above
+    (topn_kernels.hip HistLayout)."""
+    return (H32 + (H16 - H32 + 1) // 2 + (K - H16 + 3) // 4) * 4
 
 
 class DeviceTopNIndex:
@@ -78,9 +80,12 @@ class DeviceTopNIndex:
         self.cache_acc = t32(acc_i)
         self.cache_cnt = t32(np.where(valid, np.minimum(counts, 2 ** 31 - 1), 0))
         self.a2dense = t32(view.dense_many(space) if A else np.zeros(0))
-        hot = int((counts >= 65536).sum(axis=1).max()) if S else 0
-        self.H = min(K, (hot + 63) // 64 * 64)
-        self.lds = lds_bytes(K, self.H)
+        # counter tiers from the cached counts (a src count never exceeds them)
+        n32 = int((counts >= 65536).sum(axis=1).max()) if S else 0
+        n16 = int((counts >= 256).sum(axis=1).max()) if S else 0
+        self.H32 = min(K, (n32 + 63) // 64 * 64)
+        self.H16 = max(self.H32, min(K, (n16 + 63) // 64 * 64))
+        self.lds = lds_bytes(K, self.H32, self.H16)
         self.ok = self.lds <= LDS_LIMIT
         self._vd = torch.from_numpy(np.frombuffer(view.viewdev().tobytes(), dtype=np.uint8).copy())
 
@@ -128,7 +133,7 @@ class DeviceTopNIndex:
         counts, offs, vals = src
         e32 = torch.empty(0, dtype=torch.int32, device=dev)
         e64 = torch.empty(0, dtype=torch.int64, device=dev)
-        kernels().topn_src(self._vd, Q, self.S, self.K, self.H, self.A, counts, offs, vals, self.colptr,
+        kernels().topn_src(self._vd, Q, self.S, self.K, self.H32, self.H16, self.A, counts, offs, vals, self.colptr,
                            self.entbase, self.slots, self.cache_cnt, self.cache_acc, self.slotmap, self.a2dense,
                            ns_t, th_t, mode, acc if acc is not None else e32,
                            pair_off if pair_off is not None else e64, pair_idx if pair_idx is not None else e32,

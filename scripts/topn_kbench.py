@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Kernel-level timing of the slot-index TopN (ops/topn_index.py) on the
+headline arena: phase-1 kernel per src class (hot / warm / cold src rows),
+optionally with PILOSA_TOPN_DBG cost isolation (bit 0 skip histogram, bit 1
+skip walk; results are then wrong, timings isolate the parts)."""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cols", type=int, default=1_000_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from bench import NROWS, SHARD_WIDTH
+    from pilosa_amd import _roaring
+    from pilosa_amd.ops.device import DeviceView, GpuEngine, Leaf
+    from pilosa_amd.ops.topn import DeviceRankCache
+    from pilosa_amd.ops.topn_index import DeviceTopNIndex
+
+    dev = torch.device("cuda", 0)
+    S = math.ceil(args.cols / SHARD_WIDTH)
+    arena = _roaring.gen_zipf_arena(0, S, args.cols, NROWS, 8.0, 1.6, 50.0, 1, 16)
+    view = DeviceView(*arena, dev, shards=list(range(S)))
+    del arena
+    eng = GpuEngine(dev)
+    cache = DeviceRankCache.from_view(view, k=50000)
+    t0 = time.perf_counter()
+    idx = DeviceTopNIndex(view, cache)
+    torch.cuda.synchronize()
+    out = {"shards": S, "index_build_s": round(time.perf_counter() - t0, 2), "H32": idx.H32, "H16": idx.H16,
+           "lds_bytes": idx.lds, "classes": {}}
+    B = args.batch
+    for name, rows in (("hot 0-15", range(0, 16)), ("warm 100-115", range(100, 116)),
+                       ("cold 900-915", range(900, 900 + B))):
+        srcs = [Leaf(view, r) for r in list(rows)[:B]]
+        src = eng.materialize_batch(srcs, idx.S)
+        acc, ns_t, th_t, hist = idx.phase1(src, B, [100] * B, [1] * B, keep_hist=True)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            idx._launch(1, B, src, ns_t, th_t, acc=acc, hist=hist)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.reps
+        nsrc = int(src[0].sum().item())
+        out["classes"][name] = {"phase1_ms": round(ms, 3), "src_bits": nsrc,
+                                "dbg": int(os.environ.get("PILOSA_TOPN_DBG", "0"))}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
