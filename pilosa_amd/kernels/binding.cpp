@@ -115,7 +115,7 @@ void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
 }
 
 void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out_sum,
-             torch::Tensor out_cnt) {
+             torch::Tensor out_cnt, int64_t fmode) {
   check_dev(progs, "progs");
   check_dev(views, "views");
   check_dev(out_sum, "out_sum");
@@ -134,7 +134,8 @@ void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor 
   pk::launch_bsi_sum(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
                      reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), b,
                      reinterpret_cast<unsigned long long*>(out_sum.data_ptr<int64_t>()),
-                     reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>()), cur_stream(progs));
+                     reinterpret_cast<unsigned long long*>(out_cnt.data_ptr<int64_t>()), int(fmode),
+                     cur_stream(progs));
   check_launch("bsi_sum");
 }
 
@@ -282,5 +283,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
-  m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program");
+  m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program", py::arg("progs"),
+        py::arg("views"), py::arg("S"), py::arg("bsi_args"), py::arg("out_sum"), py::arg("out_cnt"),
+        py::arg("fmode") = 2);
 }

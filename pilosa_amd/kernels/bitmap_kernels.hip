@@ -27,6 +27,7 @@
 // share its L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.h"
 
@@ -545,6 +546,83 @@ __global__ __launch_bounds__(256) void bsi_sum_kernel(const QueryProg* __restric
   }
 }
 
+// BSI sum, key-parallel (default): one wave per (shard, key, query), the
+// queries of one (shard, key) on consecutive waves of one XCD so the bit
+// planes they all read are shared through its L2.  Lanes first resolve the
+// container of every bit plane at this key in parallel (lane i: plane i), so
+// the plane loop issues its tile loads without a dependent metadata walk.
+// FMODE: 0 no filter, 1 flat-fold filter (two tiles), 2 any program (tile stack).
+template <int FMODE>
+__global__ __launch_bounds__(256) void bsi_sum_keys_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                           const ViewDev* __restrict__ views, int S, BsiArgs bsi,
+                                                           unsigned long long* __restrict__ out_sum,
+                                                           unsigned long long* __restrict__ out_cnt) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S * 16) return;
+  const int q = int(item % Q);
+  const int j = int((item / Q) & 15);
+  const int s = int(item / (int64_t(Q) * 16));
+  const QueryProg& qp = progs[q];
+  WaveScratch& ws = scratch[wave];
+  const ViewDev& bv = views[bsi.view];
+  const uint32_t* rp = bv.rowptr + int64_t(s) * (bv.D + 1);
+  const int64_t base = bv.shard_base[s];
+  // container index of dense row d at key j (or -1), evaluated per lane
+  auto lane_find = [&](int64_t d) -> int64_t {
+    if (d < 0) return -1;
+    const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+    for (int64_t c = lo; c < hi; c++)
+      if (meta_j(bv.meta[c]) == j) return c;
+    return -1;
+  };
+  // lane 0..depth-1: bit planes, lane 62: sign, lane 63: exists
+  int64_t mine = -1;
+  if (lane < bsi.depth) mine = lane_find(bsi.bit_row[lane]);
+  else if (lane == 62) mine = lane_find(bsi.row_sign);
+  else if (lane == 63) mine = lane_find(bsi.row_exists);
+  const int64_t ce = rl_i64(mine, 63);
+  if (ce < 0) return;
+  Tile consider, sign, bits;
+  tile_load(consider, bv.payload, bv.meta[ce], ws.lb);
+  if (FMODE != 0 && qp.nprog) {
+    uint32_t mask[MAXLEAF];
+    build_slots(qp, views, s, ws, mask);
+    if (!((candidate_mask(qp, mask) >> j) & 1)) return;
+    Tile f;
+    if (FMODE == 1) eval_flat(qp, views, s, j, ws, f);
+    else eval_tile(qp, views, s, j, ws, f);
+    tile_op<OP_AND>(consider, f);
+  }
+  const int64_t acc_cnt = tile_popc(consider);
+  const int64_t cs = rl_i64(mine, 62);
+  if (cs >= 0) tile_load(sign, bv.payload, bv.meta[cs], ws.lb);
+  else tile_zero(sign);
+  int64_t acc_sum = 0;
+  for (int i = 0; i < bsi.depth; i++) {
+    const int64_t cb = rl_i64(mine, i);
+    if (cb < 0) continue;
+    tile_load(bits, bv.payload, bv.meta[cb], ws.lb);
+    int pc = 0, nc = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+      const uint64_t bx = bits.w[w].x & consider.w[w].x, by = bits.w[w].y & consider.w[w].y;
+      pc += __popcll(bx & ~sign.w[w].x) + __popcll(by & ~sign.w[w].y);
+      nc += __popcll(bx & sign.w[w].x) + __popcll(by & sign.w[w].y);
+    }
+    acc_sum += int64_t(uint64_t(int64_t(pc - nc)) << i);
+  }
+  const int64_t tsum = wave_sum_i64(acc_sum);
+  const int64_t tcnt = wave_sum_i64(acc_cnt);
+  if (lane == 0) {
+    if (tsum) atomicAdd(out_sum + q, (unsigned long long)tsum);
+    if (tcnt) atomicAdd(out_cnt + q, (unsigned long long)tcnt);
+  }
+}
+
 // ---------------------------------------------------------------- BSI range
 // Bit-sliced comparators (O'Neil), reference fragment.go:1271-1534, with the
 // exact control flow of pilosa_amd/models/fragment.py (_range_eq/_lt/_gt/
@@ -914,11 +992,27 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
-                    unsigned long long* out_sum, unsigned long long* out_cnt, hipStream_t st) {
-  const int64_t items = int64_t(Q) * S;
+                    unsigned long long* out_sum, unsigned long long* out_cnt, int fmode, hipStream_t st) {
+  static const int variant = [] {
+    const char* e = getenv("PILOSA_BSI_SUM_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  if (variant == 0) {  // one wave per (query, shard), keys walked in sequence
+    const int64_t items = int64_t(Q) * S;
+    if (items == 0) return;
+    hipLaunchKernelGGL(bsi_sum_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs, Q, views,
+                       S, bsi, out_sum, out_cnt);
+    return;
+  }
+  const int64_t items = int64_t(Q) * S * 16;
   if (items == 0) return;
-  hipLaunchKernelGGL(bsi_sum_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs, Q, views,
-                     S, bsi, out_sum, out_cnt);
+  const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
+  if (fmode == 0)
+    hipLaunchKernelGGL(bsi_sum_keys_kernel<0>, grid, block, 0, st, progs, Q, views, S, bsi, out_sum, out_cnt);
+  else if (fmode == 1)
+    hipLaunchKernelGGL(bsi_sum_keys_kernel<1>, grid, block, 0, st, progs, Q, views, S, bsi, out_sum, out_cnt);
+  else
+    hipLaunchKernelGGL(bsi_sum_keys_kernel<2>, grid, block, 0, st, progs, Q, views, S, bsi, out_sum, out_cnt);
 }
 
 }  // namespace pk

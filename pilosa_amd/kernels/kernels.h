@@ -63,8 +63,9 @@ void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t 
 // BSI min/max descents per (shard, key): out int64[S*16*10] (see bitmap_kernels.hip).
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
                        hipStream_t st);
+// fmode: 0 no filters, 1 flat-fold filter programs, 2 any program.
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
-                    unsigned long long* out_sum, unsigned long long* out_cnt, hipStream_t st);
+                    unsigned long long* out_sum, unsigned long long* out_cnt, int fmode, hipStream_t st);
 
 // Device TopN slot index (topn_kernels.hip): pass 1 counts cached-row bits per
 // column into colcnt[S*2^20]; pass 2 (fill) scatters cache slots behind the

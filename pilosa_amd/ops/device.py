@@ -808,5 +808,13 @@ class GpuEngine:
         out_cnt = torch.zeros(len(filters), dtype=torch.int64, device=self.device)
         if bsi_view.S and args[2] >= 0:
             tp, tv = self.upload_batch(progs, ordered)
-            self.ext.bsi_sum(tp, tv, bsi_view.S, torch.from_numpy(args), out_sum, out_cnt)
+            # filter flavour: none / flat folds (2 tiles) / any program (tile stack)
+            nprog = progs["nprog"]
+            if not (nprog > 0).any():
+                fmode = 0
+            elif bool(((nprog <= 1) | flat_mask(progs)).all()):
+                fmode = 1
+            else:
+                fmode = 2
+            self.ext.bsi_sum(tp, tv, bsi_view.S, torch.from_numpy(args), out_sum, out_cnt, fmode)
         return out_sum, out_cnt

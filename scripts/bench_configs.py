@@ -70,10 +70,25 @@ def config4(args, dev):
     def q_min():
         return int(eng.bsi_minmax(None, bv, depth)[..., 0].max())
 
+    # filter rows for batched Sum(Row(f=r), field=v): a Zipf set field, 1 bit/column
+    farena = _roaring.gen_zipf_arena(0, S, args.cols, 1000, 1.0, 1.6, 50.0, 11, 16)
+    fv = DeviceView(*farena, dev, shards=list(range(S)))
+    del farena
+    FB = 32
+
+    def q_sum_filtered_batch():
+        rows = rng.integers(0, 200, size=FB)
+        s, n = eng.bsi_sum_async([Leaf(fv, int(r)) for r in rows], bv, depth)
+        return int(s.cpu()[0]), int(n.cpu()[0])
+
     for name, fn in (("Sum(field=v)", q_sum), ("Count(Row(v > x))", q_gt), ("Count(Row(v >< [a,b]))", q_between),
                      ("Min/Max(field=v)", q_min)):
         dt, out = timed(fn, args.reps)
         res["queries"][name] = {"ms": round(dt * 1000, 3), "qps": round(1 / dt, 1), "sample": out}
+    dt, out = timed(q_sum_filtered_batch, args.reps)
+    res["queries"][f"Sum(Row(f=r), field=v) x{FB} filters per launch"] = {
+        "ms_per_batch": round(dt * 1000, 3), "qps": round(FB / dt, 1), "sample": out}
+    del fv
     s, n = q_sum()
     res["check"] = {"count": n, "mean": s / max(n, 1),
                     "expected_count": args.cols * 0.5, "expected_mean": (1_000_000 - 1000) / 2}
