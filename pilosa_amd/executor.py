@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import datetime as dt
+import os
 import threading
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -196,6 +197,9 @@ class Executor:
         self.client = client
         self.gpu = gpu            # GpuExecutor or None
         self.mesh = None          # parallel.mesh.ShardMesh on a multi-GPU node (rank 0 front end)
+        # concurrent single-Count requests share GPU launches (ops/coalescer.py)
+        self.coalesce = os.environ.get("PILOSA_COALESCE", "1") != "0"
+        self._coalescer = None
         self.max_writes = max_writes
         self.stats = stats
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, workers), thread_name_prefix="shard")
@@ -248,6 +252,12 @@ class Executor:
             shards = idx.available_shards() or [0]
         if q.calls and all(c.name == "SetRowAttrs" for c in q.calls):
             return self._bulk_set_row_attrs(index, q.calls, opt)
+        # Concurrent requests of one Count() each are batched across requests.
+        if len(q.calls) == 1 and q.calls[0].name == "Count" and self.coalesce and \
+                (self.gpu is not None or self._use_mesh(opt)) and not self._has_remote(index, shards, opt):
+            c = q.calls[0]
+            key = (index, tuple(shards), self._use_mesh(opt))
+            return [self.coalescer.submit(key, c, lambda: self.execute_call(index, c, shards, opt))]
         # Batch fast path: many Count() calls in one request go to the GPU together.
         if self._use_mesh(opt) and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
                 not self._has_remote(index, shards, opt):
@@ -258,6 +268,21 @@ class Executor:
             if res is not None:
                 return res
         return [self.execute_call(index, c, shards, opt) for c in q.calls]
+
+    @property
+    def coalescer(self):
+        if self._coalescer is None:
+            from pilosa_amd.ops.coalescer import CountCoalescer
+            self._coalescer = CountCoalescer(self._run_count_batch)
+        return self._coalescer
+
+    def _run_count_batch(self, key, calls):
+        index, shards, mesh = key
+        if mesh:
+            return self.mesh.count_batch(index, list(calls), list(shards))
+        if self.gpu is None:
+            return None
+        return self.gpu.try_count_batch(index, list(calls), list(shards))
 
     def _has_remote(self, index, shards, opt) -> bool:
         if self.cluster is None or opt.remote:

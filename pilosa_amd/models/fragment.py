@@ -65,6 +65,21 @@ class TopOptions:
         self.attr_store = attr_store
 
 
+
+# Process-wide mutation epoch: bumped with every fragment version (and when a
+# fragment is created), so device-side caches keyed on many fragments can
+# skip re-reading each fragment's version while nothing changed.
+_EPOCH = [0]
+
+
+def _bump_epoch():
+    _EPOCH[0] += 1
+
+
+def mutation_epoch() -> int:
+    return _EPOCH[0]
+
+
 class Fragment:
     def __init__(self, path: str, index: str, field: str, view: str, shard: int,
                  cache_type: str = CACHE_TYPE_RANKED, cache_size: int = DEFAULT_CACHE_SIZE,
@@ -83,6 +98,7 @@ class Fragment:
         self.ops = 0
         self.max_row_id = 0
         self.version = 0
+        _bump_epoch()
         # per-consumer dirty-row sets (device arenas patch only changed rows);
         # None = unknown / too many -> the consumer refreshes the whole shard
         self._dirty_subs: Dict[object, Optional[set]] = {}
@@ -122,7 +138,11 @@ class Fragment:
         except OSError as e:
             raise PilosaError(f"flock: {e}")
         self.max_row_id = int(self.storage.max()) // SHARD_WIDTH if self.storage.any() else 0
+        self._bump()
+
+    def _bump(self):
         self.version += 1
+        _EPOCH[0] += 1
 
     def cache_path(self) -> str:
         return self.path + ".cache"
@@ -184,7 +204,7 @@ class Fragment:
             return
         self.opn += changed
         self.ops += 1
-        self.version += 1
+        self._bump()
         if self.opn > self.max_opn:
             q = getattr(self, "snapshot_queue", None)
             if q is not None:
@@ -354,7 +374,7 @@ class Fragment:
             self._after_row_change(row_id, bulk=True)
             if self.cache_type != CACHE_TYPE_NONE:
                 self.cache.invalidate()
-            self.version += 1
+            self._bump()
             self.snapshot()
             return True
 
@@ -364,7 +384,7 @@ class Fragment:
             self._note_rows((row_id,))
             self.cache.add(row_id, 0)
             self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
-            self.version += 1
+            self._bump()
             self.snapshot()
             return changed
 
@@ -741,7 +761,7 @@ class Fragment:
         self._increment_opn(changed)
         if self.stats:
             self.stats.count("ImportedN", changed)
-        self.version += 1
+        self._bump()
         return changed
 
     def bulk_import(self, row_ids: Sequence[int], col_ids: Sequence[int], clear: bool = False) -> int:
@@ -815,7 +835,7 @@ class Fragment:
             if any_changed:
                 self.cache.recalculate()
             self._increment_opn(changed)
-            self.version += 1
+            self._bump()
             return changed
 
     # ------------------------------------------------------------ anti-entropy
@@ -917,7 +937,7 @@ class Fragment:
                         os.replace(tmp, self.path)
                         self._fh = open(self.path, "ab", buffering=0)
                         self.opn = 0
-                        self.version += 1
+                        self._bump()
                 elif ti.name == "cache":
                     m = pb.Cache()
                     m.ParseFromString(payload)

@@ -30,7 +30,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from pilosa_amd.models.cache import Pair, sort_pairs
-from pilosa_amd.models.fragment import SHARD_WIDTH
+from pilosa_amd.models.fragment import SHARD_WIDTH, mutation_epoch
 from pilosa_amd.models.index import EXISTENCE_FIELD_NAME
 from pilosa_amd.models.row import Row
 from pilosa_amd.models.view import VIEW_BSI_PREFIX, VIEW_STANDARD
@@ -62,6 +62,7 @@ class GpuExecutor:
         self.hbm_budget = int(hbm_budget)
         self.evictions = 0
         self._arenas: "OrderedDict[Tuple, Tuple[Tuple, DeviceView]]" = OrderedDict()
+        self._arena_epoch: Dict[Tuple, int] = {}  # mutation epoch at the last validation of each arena
         self._bsi_views: Dict[Tuple, DeviceView] = {}  # predicate results (small LRU)
         self.mu = threading.RLock()
         self.launches = 0
@@ -73,14 +74,24 @@ class GpuExecutor:
 
     # ------------------------------------------------------------ arenas
     def view_arena(self, index: str, field: str, view: str, shards: Sequence[int]) -> Optional[DeviceView]:
+        shards = tuple(int(s) for s in shards)
+        key = (index, field, view, shards)
+        epoch = mutation_epoch()
+        with self.mu:
+            # nothing mutated since this arena was last validated: skip the
+            # per-shard version signature (the serving hot path)
+            if self._arena_epoch.get(key) == epoch:
+                hit = self._arenas.get(key)
+                if hit is not None:
+                    self._arenas.move_to_end(key)
+                    return hit[1]
         v = self.holder.view(index, field, view)
         if v is None:
             return None
-        shards = tuple(int(s) for s in shards)
         frags = [v.fragment(s) for s in shards]
         sig = tuple((id(f), f.version) if f is not None else None for f in frags)
-        key = (index, field, view, shards)
         with self.mu:
+            self._arena_epoch[key] = epoch
             hit = self._arenas.get(key)
             if hit is not None:
                 self._arenas.move_to_end(key)
@@ -171,6 +182,7 @@ class GpuExecutor:
     def invalidate(self):
         with self.mu:
             self._arenas.clear()
+            self._arena_epoch.clear()
             self._bsi_views.clear()
             self._topn_indexes.clear()
 

@@ -593,6 +593,10 @@ def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
 
     class _H(BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
+        # headers and body go out as separate writes; without TCP_NODELAY the
+        # body waits for the peer's delayed ACK of the headers (~40 ms per
+        # keep-alive request)
+        disable_nagle_algorithm = True
 
         def log_message(self, fmt, *args):  # quiet
             pass

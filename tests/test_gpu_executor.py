@@ -313,3 +313,31 @@ def test_slot_index_topn_matches_replay(envs, k):
             for q, g in zip(cases, got):
                 want = cpu.q1("i", f"TopN(h, {q}, n={n})")
                 assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in want], (q, n)
+
+
+def test_concurrent_counts_coalesce_on_gpu(envs):
+    """Independent concurrent Count() requests share GPU launches
+    (ops/coalescer.py) and each gets exactly its host result."""
+    import threading
+    cpu, gpu = envs
+    qs = [QUERIES[i % len(QUERIES)] for i in range(96)]
+    want = [cpu.q1("i", q) for q in qs]
+    got = [None] * len(qs)
+    cpu.executor.gpu = gpu
+    try:
+        co = cpu.executor.coalescer
+        b0, n0 = co.batches, co.batched + co.fallbacks
+
+        def work(i):
+            got[i] = cpu.q1("i", qs[i])
+
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(len(qs))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+        assert co.batched + co.fallbacks - n0 == len(qs)
+        assert co.batches - b0 <= len(qs)
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
