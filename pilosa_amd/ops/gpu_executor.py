@@ -352,10 +352,48 @@ class GpuExecutor:
         except CompileError:
             raise NotImplementedError
 
+    NATIVE_BATCH_MIN = 4
+
+    def _native_fields(self, index: str) -> List[str]:
+        """Fields whose ``Row(f=id)`` reads exactly the standard view (set,
+        mutex, bool and time fields; BSI fields are excluded)."""
+        from pilosa_amd.models.field import FIELD_TYPE_INT
+        idx = self.holder.index(index)
+        if idx is None:
+            return []
+        return [f.name for f in idx.fields.values() if f.type != FIELD_TYPE_INT and f.name != EXISTENCE_FIELD_NAME]
+
+    def _count_batch_native(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
+        """Serving fast path: the calls' canonical PQL goes through the native
+        program compiler (pilosa_amd/native/pql_compile.cpp, ~0.3 us/query)
+        instead of Python planning; any call outside its subset is compiled by
+        the planner against the same views, anything else returns None."""
+        from .planner import NativeCountCompiler, Unsupported
+        views: Dict[str, DeviceView] = {}
+        for f in self._native_fields(index):
+            dv = self.view_arena(index, f, VIEW_STANDARD, shards)
+            if dv is not None:
+                views[f] = dv
+        if not views:
+            return None
+        comp = NativeCountCompiler(views)
+        try:
+            progs, vlist, S = comp.compile([str(c) for c in calls])
+        except (Unsupported, KeyError, ValueError):
+            return None
+        if comp.fallbacks:
+            return None  # rows missing from every arena (EMPTY) etc.: planner path
+        self.launches += 1
+        return [int(v) for v in self.engine.launch_count(self.engine.prepare_progs(progs, vlist, S)).cpu().tolist()]
+
     def try_count_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
         """Many Count() calls of one request -> one launch; calls whose tree
         does not fit the kernel limits are counted on the host."""
         from .device import compile_expr
+        if len(calls) >= self.NATIVE_BATCH_MIN:
+            got = self._count_batch_native(index, calls, shards)
+            if got is not None:
+                return got
         try:
             exprs = []
             for c in calls:

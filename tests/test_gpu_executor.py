@@ -341,3 +341,18 @@ def test_concurrent_counts_coalesce_on_gpu(envs):
     finally:
         cpu.executor.gpu = None
     assert got == want
+
+
+def test_native_count_batch_path(envs):
+    """Batches of plain Row/set-op counts take the native-compiler fast path
+    (GpuExecutor._count_batch_native) and match the host."""
+    cpu, gpu = envs
+    qs = ["Count(Row(f=0))", "Count(Intersect(Row(f=0), Row(f=1)))", "Count(Union(Row(f=1), Row(g=2), Row(f=20)))",
+          "Count(Difference(Row(f=20), Row(f=0)))", "Count(Xor(Row(f=4), Row(g=0)))", "Count(Row(f=999))",
+          "Count(Intersect(Row(f=0), Row(f=999)))", "Count(Row(h=3))"]
+    want = cpu.q("i", " ".join(qs))
+    from pilosa_amd.pql import parse_string
+    calls = [parse_string(q).calls[0] for q in qs]
+    shards = cpu.holder.index("i").available_shards()
+    got = gpu._count_batch_native("i", calls, shards)
+    assert got == want
