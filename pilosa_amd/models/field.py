@@ -10,6 +10,7 @@ cluster (local fragments + remote shards learned from peers).
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
 import datetime as dt
 import os
 import shutil
@@ -34,6 +35,9 @@ FIELD_TYPE_SET, FIELD_TYPE_INT, FIELD_TYPE_TIME, FIELD_TYPE_MUTEX, FIELD_TYPE_BO
     "set", "int", "time", "mutex", "bool"
 FIELD_TYPES = (FIELD_TYPE_SET, FIELD_TYPE_INT, FIELD_TYPE_TIME, FIELD_TYPE_MUTEX, FIELD_TYPE_BOOL)
 MAX_INT = (1 << 63) - 1
+# bulk imports larger than this split their per-fragment work over threads
+PARALLEL_IMPORT_MIN = 1 << 16
+IMPORT_WORKERS = max(1, min(16, os.cpu_count() or 1))
 
 
 def bit_depth(v: int) -> int:
@@ -482,9 +486,15 @@ class Field:
         q = self.time_quantum()
         std_ok = not self.options.no_standard_view
         if timestamps is None or all(t is None for t in timestamps):
-            if std_ok:
-                for s in np.unique(shards):
-                    groups[(VIEW_STANDARD, int(s))] = np.nonzero(shards == s)[0]
+            if std_ok and len(shards):
+                # one stable sort by shard instead of a mask per shard (radix
+                # sort on 16-bit keys)
+                key = shards.astype(np.uint16) if int(shards.max()) < 65536 else shards
+                order = np.argsort(key, kind="stable")
+                ss = shards[order]
+                cut = np.flatnonzero(np.diff(ss)) + 1
+                for part in np.split(order, cut):
+                    groups[(VIEW_STANDARD, int(shards[part[0]]))] = part
         else:
             tmp: Dict[Tuple[str, int], List[int]] = {}
             for i, t in enumerate(timestamps):
@@ -497,11 +507,16 @@ class Field:
                     for name in views_by_time(VIEW_STANDARD, t, q):
                         tmp.setdefault((name, s), []).append(i)
             groups = {k: np.array(v, dtype=np.int64) for k, v in tmp.items()}
-        changed = 0
-        for (vname, shard), idx in sorted(groups.items()):
-            frag = self.create_view_if_not_exists(vname).create_fragment_if_not_exists(shard)
-            changed += frag.bulk_import(rows[idx], cols[idx], clear=clear)
-        return changed
+        items = sorted(groups.items())
+        frags = [self.create_view_if_not_exists(v).create_fragment_if_not_exists(s) for (v, s), _ in items]
+        jobs = [(frag, idx) for frag, (_, idx) in zip(frags, items)]
+        if len(jobs) > 1 and len(rows) >= PARALLEL_IMPORT_MIN:
+            # fragments import independently (own locks; the native inserts,
+            # sorts and op encoding release the GIL), like the reference's
+            # per-fragment import workers (api.go:86-93)
+            with cf.ThreadPoolExecutor(max_workers=min(len(jobs), IMPORT_WORKERS)) as pool:
+                return sum(pool.map(lambda j: j[0].bulk_import(rows[j[1]], cols[j[1]], clear=clear), jobs))
+        return sum(frag.bulk_import(rows[idx], cols[idx], clear=clear) for frag, idx in jobs)
 
     def import_values(self, col_ids: Sequence[int], values: Sequence[int], clear: bool = False) -> int:
         b = self.bsi_group()

@@ -633,7 +633,10 @@ PYBIND11_MODULE(_roaring, m) {
         return b.add_many(v.data(), v.size());
       }, py::arg("values"), py::arg("sorted") = false)
       .def("remove_many", [](Bitmap& b, u64arr vals) {
-        return b.remove_many(vals.data(), size_t(vals.size()));
+        const uint64_t* p = vals.data();
+        const size_t n = size_t(vals.size());
+        py::gil_scoped_release nogil;
+        return b.remove_many(p, n);
       })
       .def("count", &Bitmap::count)
       .def("__len__", &Bitmap::count)
@@ -718,6 +721,24 @@ PYBIND11_MODULE(_roaring, m) {
         if (cur != ~0ull) d[py::int_(cur)] = acc;
         return d;
       }, py::arg("containers_per_row") = 16)
+      .def("count_rows", [](const Bitmap& b, u64arr rows, uint64_t cpr) {
+        // cardinality of each given row (rows*cpr .. +cpr container keys), one
+        // map lookup per row: bulk imports refresh caches without per-row calls
+        const uint64_t* r = rows.data();
+        const py::ssize_t n = rows.size();
+        py::array_t<int64_t> out(n);
+        int64_t* o = out.mutable_data();
+        {
+          py::gil_scoped_release nogil;
+          for (py::ssize_t i = 0; i < n; i++) {
+            int64_t acc = 0;
+            const uint64_t k0 = r[i] * cpr;
+            for (auto it = b.cs.lower_bound(k0); it != b.cs.end() && it->first < k0 + cpr; ++it) acc += it->second.n;
+            o[i] = acc;
+          }
+        }
+        return out;
+      }, py::arg("rows"), py::arg("containers_per_row") = 16)
       .def("rows_with_column", [](const Bitmap& b, uint64_t col, uint64_t cpr) {
         // rows whose container at key (row*cpr + col>>16) holds col (mutex/bool vectors)
         std::vector<uint64_t> rows;
@@ -754,7 +775,14 @@ PYBIND11_MODULE(_roaring, m) {
 
   m.def("encode_op", [](uint8_t typ, uint64_t value, u64arr values, py::bytes roaring, uint32_t opn) {
     std::string r = roaring;
-    return py::bytes(pr::encode_op(typ, value, values.data(), size_t(values.size()), r, opn));
+    const uint64_t* p = values.data();
+    const size_t n = size_t(values.size());
+    std::string enc;
+    {
+      py::gil_scoped_release nogil;
+      enc = pr::encode_op(typ, value, p, n, r, opn);
+    }
+    return py::bytes(enc);
   }, py::arg("typ"), py::arg("value") = 0, py::arg("values") = u64arr(0), py::arg("roaring") = py::bytes(""),
      py::arg("opn") = 0);
   m.def("fnv32a", [](py::bytes data) {
