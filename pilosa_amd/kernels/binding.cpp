@@ -264,6 +264,34 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
   check_launch("topn_src");
 }
 
+void bitgemm(torch::Tensor A, torch::Tensor B, int64_t M, int64_t N, int64_t KW, int64_t splits, int64_t mode,
+             torch::Tensor C) {
+  check_dev(A, "A");
+  check_dev(B, "B");
+  check_dev(C, "C");
+  TORCH_CHECK(A.scalar_type() == torch::kInt64 && A.numel() == M * KW, "A int64[M*KW]");
+  TORCH_CHECK(B.scalar_type() == torch::kInt64 && B.numel() == N * KW, "B int64[N*KW]");
+  TORCH_CHECK(C.scalar_type() == torch::kInt32 && C.numel() == M * N, "C int32[M*N]");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "bitgemm mode");
+  pk::launch_bitgemm(reinterpret_cast<const uint64_t*>(A.data_ptr<int64_t>()),
+                     reinterpret_cast<const uint64_t*>(B.data_ptr<int64_t>()), int(M), int(N), KW, int(splits),
+                     int(mode), C.data_ptr<int32_t>(), cur_stream(A));
+  check_launch("bitgemm");
+}
+
+void densify(torch::Tensor view, torch::Tensor rows, int64_t s0, int64_t s1, torch::Tensor out) {
+  check_dev(rows, "rows");
+  check_dev(out, "out");
+  const pk::ViewDev v = viewdev_from(view);
+  TORCH_CHECK(rows.scalar_type() == torch::kInt64, "rows int64 (dense indices, -1 = empty)");
+  TORCH_CHECK(s0 >= 0 && s1 >= s0, "shard range");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() == rows.numel() * (s1 - s0) * 16384,
+              "out int64[R*(s1-s0)*16384]");
+  pk::launch_densify(v, rows.data_ptr<int64_t>(), int(rows.numel()), int(s0), int(s1),
+                     reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()), cur_stream(rows));
+  check_launch("densify");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -283,6 +311,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
+  m.def("bitgemm", &bitgemm, "row-pair intersection count matrix of dense bit rows (mode 1 MFMA i8, 0 VALU)");
+  m.def("densify", &densify, "dense bit rows of an arena over a shard range");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("bsi_args"), py::arg("out_sum"), py::arg("out_cnt"),
         py::arg("fmode") = 2);

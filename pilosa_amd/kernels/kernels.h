@@ -105,4 +105,12 @@ int topn_lds_bytes(int K, int H32, int H16);
 // -> out[P] (rebuilds the histograms); mode 3: ids= re-count from hist_in.
 void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
 
+// Row-pair intersection count matrix C[M][N] (int32, atomically accumulated)
+// of dense bit rows A[M][KW] and B[N][KW] (u64 words), bitgemm.hip.
+// mode 1: i8 MFMA (v_mfma_i32_32x32x32_i8), mode 0: VALU popcount.
+void launch_bitgemm(const uint64_t* A, const uint64_t* B, int M, int N, int64_t KW, int splits, int mode,
+                    int32_t* C, hipStream_t st);
+// Dense bit rows of an arena: out[R][(s1-s0) * 16384] u64 for dense rows `rows`.
+void launch_densify(const ViewDev& v, const int64_t* rows, int R, int s0, int s1, uint64_t* out, hipStream_t st);
+
 }  // namespace pk

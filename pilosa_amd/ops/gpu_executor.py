@@ -39,6 +39,8 @@ from pilosa_amd.pql import Call
 from .device import CompileError, DeviceView, GpuEngine, Leaf, Op
 
 MAX_GROUPS_PER_LAUNCH = 1 << 16
+# two-field GroupBy with at least this many row pairs runs as one count matrix
+GROUPBY_MATRIX_MIN = int(os.environ.get("PILOSA_GROUPBY_MATRIX_MIN", "1024"))
 # minimum spacing of device TopN index rebuilds per view (the reference
 # re-ranks its caches at most every 10 s too, cache.go:235-243)
 TOPN_INDEX_REBUILD_S = float(os.environ.get("PILOSA_TOPN_INDEX_REBUILD_S", "10"))
@@ -594,6 +596,16 @@ class GpuExecutor:
             if fexpr is EMPTY:
                 return []
         prev = ex.group_by_previous(c)
+        if k == 2 and len(cand[0]) * len(cand[1]) >= GROUPBY_MATRIX_MIN and \
+                (fexpr is None or type(fexpr) is Leaf):
+            # two fields: the whole count matrix in one bit-GEMM (MFMA), then
+            # the lexicographic walk on the host (ops/groupby.py)
+            from .groupby import emit_groups, pair_count_matrix
+            self.launches += 1
+            mat = pair_count_matrix(arenas[0], cand[0], arenas[1], cand[1],
+                                    filt=(fexpr.view, fexpr.row) if fexpr is not None else None)
+            return [GroupCount([FieldRow(fields[0], ra), FieldRow(fields[1], rb)], n)
+                    for ra, rb, n in emit_groups(cand[0], cand[1], mat, prev, limit)]
         results: List[GroupCount] = []
         # enumerate combos lexicographically in chunks; stop at `limit`
         batch_keys: List[Tuple[int, ...]] = []

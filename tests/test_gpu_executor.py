@@ -356,3 +356,24 @@ def test_native_count_batch_path(envs):
     shards = cpu.holder.index("i").available_shards()
     got = gpu._count_batch_native("i", calls, shards)
     assert got == want
+
+
+@pytest.mark.parametrize("q", ["GroupBy(Rows(g), Rows(f))", "GroupBy(Rows(f), Rows(g), limit=7)",
+                               "GroupBy(Rows(f), Rows(h), limit=50)",
+                               "GroupBy(Rows(f, previous=3), Rows(g, previous=1), limit=10)",
+                               "GroupBy(Rows(g), Rows(f), filter=Row(f=0))",
+                               "GroupBy(Rows(f), Rows(g), previous=[2, 2], limit=5)"])
+def test_groupby_count_matrix_matches_host(envs, monkeypatch, q):
+    """Two-field GroupBy through the bit-GEMM count matrix (ops/groupby.py)."""
+    import pilosa_amd.ops.gpu_executor as ge
+    cpu, gpu = envs
+    monkeypatch.setattr(ge, "GROUPBY_MATRIX_MIN", 1)
+    want = cpu.q1("i", q)
+    cpu.executor.gpu = gpu
+    try:
+        n0 = gpu.launches
+        got = cpu.q1("i", q)
+        assert gpu.launches > n0
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
