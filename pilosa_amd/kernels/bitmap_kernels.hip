@@ -579,12 +579,11 @@ __global__ __launch_bounds__(256) void bsi_sum_keys_kernel(const QueryProg* __re
       if (meta_j(bv.meta[c]) == j) return c;
     return -1;
   };
-  // lane 0..depth-1: bit planes, lane 62: sign, lane 63: exists
-  int64_t mine = -1;
-  if (lane < bsi.depth) mine = lane_find(bsi.bit_row[lane]);
-  else if (lane == 62) mine = lane_find(bsi.row_sign);
-  else if (lane == 63) mine = lane_find(bsi.row_exists);
-  const int64_t ce = rl_i64(mine, 63);
+  // lane i < depth (<= 63): bit plane i; lanes 0 / 1 then resolve exists /
+  // sign in a second parallel lookup
+  const int64_t mine = lane < bsi.depth ? lane_find(bsi.bit_row[lane]) : -1;
+  const int64_t extra = lane == 0 ? lane_find(bsi.row_exists) : (lane == 1 ? lane_find(bsi.row_sign) : -1);
+  const int64_t ce = rl_i64(extra, 0);
   if (ce < 0) return;
   Tile consider, sign, bits;
   tile_load(consider, bv.payload, bv.meta[ce], ws.lb);
@@ -598,7 +597,7 @@ __global__ __launch_bounds__(256) void bsi_sum_keys_kernel(const QueryProg* __re
     tile_op<OP_AND>(consider, f);
   }
   const int64_t acc_cnt = tile_popc(consider);
-  const int64_t cs = rl_i64(mine, 62);
+  const int64_t cs = rl_i64(extra, 1);
   if (cs >= 0) tile_load(sign, bv.payload, bv.meta[cs], ws.lb);
   else tile_zero(sign);
   int64_t acc_sum = 0;
@@ -640,7 +639,27 @@ struct BsiCtx {
   int64_t base;
   const uint32_t* rp;
   uint64_t* lb;
+  // lane i < depth (<= 63): container of bit plane i at key j (-1 = absent),
+  // resolved once, in parallel, by plane_index().
+  int64_t planes = -1;
 };
+
+// Every lane resolves one BSI row's container at (s, j): the plane loops then
+// broadcast it with readlanes instead of a dependent ballot walk per plane.
+__device__ __forceinline__ void plane_index(BsiCtx& c) {
+  const int lane = wave_lane();
+  const int64_t d = lane < c.bsi.depth ? c.bsi.bit_row[lane] : -1;
+  int64_t found = -1;
+  if (d >= 0) {
+    const int64_t lo = c.base + c.rp[d], hi = c.base + c.rp[d + 1];
+    for (int64_t ci = lo; ci < hi; ci++)
+      if (meta_j(c.bv.meta[ci]) == c.j) {
+        found = ci;
+        break;
+      }
+  }
+  c.planes = found;
+}
 
 // container index of dense row d at key j in shard s (wave-uniform, -1 absent)
 __device__ __forceinline__ int64_t bsi_find(const BsiCtx& c, int64_t d) {
@@ -660,8 +679,15 @@ __device__ __forceinline__ void bsi_row(const BsiCtx& c, int64_t d, Tile& t) {
   else tile_load(t, c.bv.payload, c.bv.meta[ci], c.lb);
 }
 
+__device__ __forceinline__ void bsi_plane(const BsiCtx& c, int lane_slot, Tile& t) {
+  const int64_t ci = rl_i64(c.planes, lane_slot);
+  if (ci < 0) tile_zero(t);
+  else tile_load(t, c.bv.payload, c.bv.meta[ci], c.lb);
+}
+
 __device__ __forceinline__ void bsi_bit(const BsiCtx& c, int i, Tile& t) {
-  bsi_row(c, i < 64 ? c.bsi.bit_row[i] : -1, t);
+  if (i < 0 || i >= c.bsi.depth) tile_zero(t);
+  else bsi_plane(c, i, t);
 }
 
 // filt = filt & ~(filt & ~r & ~keep)   (reference: filt.Difference(filt.Difference(row).Difference(keep)))
@@ -790,6 +816,7 @@ __global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restric
   const int s = int(item >> 4), j = int(item & 15);
   const ViewDev& bv = views[bsi.view];
   BsiCtx c{bsi, bv, s, j, bv.shard_base[s], bv.rowptr + int64_t(s) * (bv.D + 1), scratch[wave].lb};
+  plane_index(c);
   const int depth = bsi.depth;
   Tile b, sign, res;
   bsi_row(c, bsi.row_exists, b);
@@ -885,6 +912,7 @@ __global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __rest
   const ViewDev& bv = views[bsi.view];
   WaveScratch& ws = scratch[wave];
   BsiCtx c{bsi, bv, s, j, bv.shard_base[s], bv.rowptr + int64_t(s) * (bv.D + 1), ws.lb};
+  plane_index(c);
   const int depth = bsi.depth;
   const QueryProg& qp = progs[0];
   Tile pos, neg;
