@@ -98,8 +98,20 @@ void bsi_range(torch::Tensor views, int64_t S, torch::Tensor bsi_args, int64_t o
   TORCH_CHECK(out_meta.scalar_type() == torch::kInt64, "out_meta must be int64");
   pk::launch_bsi_range(reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), bsi_args_from(bsi_args),
                        int(op), p1, p2, reinterpret_cast<uint16_t*>(out_payload.data_ptr<int16_t>()),
-                       out_meta.data_ptr<int64_t>(), cur_stream(views));
+                       out_meta.data_ptr<int64_t>(), nullptr, cur_stream(views));
   check_launch("bsi_range");
+}
+
+void bsi_range_count(torch::Tensor views, int64_t S, torch::Tensor bsi_args, int64_t op, int64_t p1, int64_t p2,
+                     torch::Tensor out_count) {
+  check_dev(views, "views");
+  check_dev(out_count, "out_count");
+  TORCH_CHECK(op >= 0 && op <= 7, "bsi op");
+  TORCH_CHECK(out_count.scalar_type() == torch::kInt64 && out_count.numel() >= 1, "out_count int64[1]");
+  pk::launch_bsi_range(reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S), bsi_args_from(bsi_args),
+                       int(op), p1, p2, nullptr, nullptr,
+                       reinterpret_cast<unsigned long long*>(out_count.data_ptr<int64_t>()), cur_stream(views));
+  check_launch("bsi_range_count");
 }
 
 void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out) {
@@ -308,6 +320,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 0,
         py::arg("variant") = 1);
   m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
+  m.def("bsi_range_count", &bsi_range_count, "Count(Row(v <op> x)): fused BSI predicate + count");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");

@@ -806,7 +806,8 @@ __device__ __forceinline__ void tile_or(Tile& a, const Tile& b) { tile_op<OP_OR>
 __global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restrict__ views, int S, BsiArgs bsi,
                                                         int op, int64_t p1, int64_t p2,
                                                         uint16_t* __restrict__ out_payload,
-                                                        int64_t* __restrict__ out_meta) {
+                                                        int64_t* __restrict__ out_meta,
+                                                        unsigned long long* __restrict__ out_count) {
   __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
   const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x >> 6;
@@ -886,6 +887,10 @@ __global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restric
     }
   }
   const int64_t n = wave_sum_i64(tile_popc(res));
+  if (out_count) {  // Count(Row(v <op> x)): no predicate view is written
+    if (lane == 0 && n) atomicAdd(out_count, (unsigned long long)n);
+    return;
+  }
   ulong2* dst = reinterpret_cast<ulong2*>(out_payload + item * 4096);
 #pragma unroll
   for (int i = 0; i < 8; i++) dst[i * 64 + lane] = res.w[i];
@@ -1004,11 +1009,11 @@ void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views
 }
 
 void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t p1, int64_t p2, uint16_t* out_payload,
-                      int64_t* out_meta, hipStream_t st) {
+                      int64_t* out_meta, unsigned long long* out_count, hipStream_t st) {
   const int64_t items = int64_t(S) * 16;
   if (items == 0) return;
   hipLaunchKernelGGL(bsi_range_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, views, S, bsi, op,
-                     p1, p2, out_payload, out_meta);
+                     p1, p2, out_payload, out_meta, out_count);
 }
 
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,

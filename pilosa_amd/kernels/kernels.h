@@ -58,8 +58,9 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                        int cq, int variant, hipStream_t st);
 // BSI predicate -> one bitmap container per (shard, key): payload u16[S*16*4096], meta int64[S*16].
 // op: 0 EQ, 1 NEQ, 2 LT, 3 LTE, 4 GT, 5 GTE, 6 BETWEEN, 7 NOT NULL (values are base-relative).
+// out_count != nullptr: only add the matching column count (no view is written).
 void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t p1, int64_t p2, uint16_t* out_payload,
-                      int64_t* out_meta, hipStream_t st);
+                      int64_t* out_meta, unsigned long long* out_count, hipStream_t st);
 // BSI min/max descents per (shard, key): out int64[S*16*10] (see bitmap_kernels.hip).
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
                        hipStream_t st);

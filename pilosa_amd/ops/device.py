@@ -751,6 +751,17 @@ class GpuEngine:
         return DeviceView.from_device(np.zeros(1, np.uint64), rowptr, sb, meta, payload, self.device,
                                       bsi_view.shards, S * 16)
 
+    def bsi_range_count_async(self, bsi_view: "DeviceView", depth: int, op: str, p1: int = 0, p2: int = 0):
+        """Count(Row(v <op> x)) without materialising the predicate view:
+        device int64[1]."""
+        torch = self.torch
+        out = torch.zeros(1, dtype=torch.int64, device=self.device)
+        args = self.bsi_args(bsi_view, depth)
+        if bsi_view.S and args[2] >= 0:
+            self.ext.bsi_range_count(self._views_tensor([bsi_view]), bsi_view.S, torch.from_numpy(args),
+                                     self.BSI_OPS[op], int(p1), int(p2), out)
+        return out
+
     def bsi_minmax(self, filt: Optional[object], bsi_view: "DeviceView", depth: int) -> np.ndarray:
         """Per (shard, key) descents -> int64[S, 16, 10] (see bsi_minmax_kernel)."""
         torch = self.torch

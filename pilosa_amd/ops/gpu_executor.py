@@ -190,6 +190,23 @@ class GpuExecutor:
 
     BSI_CACHE = 8
 
+    def _bsi_count(self, index: str, c: Call, shards: Sequence[int]) -> Optional[int]:
+        """Count(Row(v <op> x)) in one fused predicate+count launch."""
+        f, b, kind, args = self._ex().bsi_predicate(index, c)
+        if kind == "empty":
+            return 0
+        if kind == "notnull":
+            return None  # the exists row: plain Count(Row) path
+        bv = self.view_arena(index, f.name, VIEW_BSI_PREFIX + f.name, shards)
+        if bv is None:
+            return 0
+        if kind == "between":
+            op, p1, p2 = "between", int(args[0]), int(args[1])
+        else:
+            op, p1, p2 = args[0], int(args[1]), 0
+        self.launches += 1
+        return int(self.engine.bsi_range_count_async(bv, b.bit_depth, op, p1, p2).item())
+
     def bsi_leaf(self, index: str, c: Call, shards: Sequence[int]):
         """Row(v <op> x) -> Leaf over a device-evaluated predicate view
         (bsi_range_kernel); NOT NULL uses the exists row directly."""
@@ -345,6 +362,10 @@ class GpuExecutor:
 
     # ------------------------------------------------------------ calls
     def count(self, index: str, child: Call, shards: List[int]) -> int:
+        if child.name in ("Row", "Range") and child.has_condition_arg():
+            n = self._bsi_count(index, child, shards)
+            if n is not None:
+                return n
         e = self.plan(index, child, shards)
         if e is EMPTY:
             return 0

@@ -62,6 +62,10 @@ def config4(args, dev):
         rv = eng.bsi_range_view(bv, depth, ">", x)
         return int(eng.count([Leaf(rv, 0)])[0])
 
+    def q_gt_fused():
+        x = int(rng.integers(0, 1_000_000))
+        return int(eng.bsi_range_count_async(bv, depth, ">", x).item())
+
     def q_between():
         a = int(rng.integers(0, 900_000))
         rv = eng.bsi_range_view(bv, depth, "between", a, a + 50_000)
@@ -81,7 +85,8 @@ def config4(args, dev):
         s, n = eng.bsi_sum_async([Leaf(fv, int(r)) for r in rows], bv, depth)
         return int(s.cpu()[0]), int(n.cpu()[0])
 
-    for name, fn in (("Sum(field=v)", q_sum), ("Count(Row(v > x))", q_gt), ("Count(Row(v >< [a,b]))", q_between),
+    for name, fn in (("Sum(field=v)", q_sum), ("Count(Row(v > x))", q_gt),
+                     ("Count(Row(v > x)) fused predicate+count", q_gt_fused), ("Count(Row(v >< [a,b]))", q_between),
                      ("Min/Max(field=v)", q_min)):
         dt, out = timed(fn, args.reps)
         res["queries"][name] = {"ms": round(dt * 1000, 3), "qps": round(1 / dt, 1), "sample": out}
