@@ -403,6 +403,90 @@ __global__ __launch_bounds__(256, MODE == 0 ? 1 : 4) void expr_count_kernel(cons
   if (lane == 0 && per_shard) per_shard[int64_t(q) * S + s] = total;
 }
 
+// Union count (MODE 3 of launch_expr_count): Count(Union(l0, l1, ...)) of
+// plain leaves, e.g. the covering time views of Row(t=r, from, to)
+// (reference executeRowShard unions the views, executor.go:1444-1533).  Per
+// key the wave clears one LDS bitmap and ORs every leaf container into it
+// with returning LDS atomics; a bit counts when its OR flips it
+// (popcount(mask & ~old)), so no tile is expanded, combined or read back --
+// for the small arrays of time views that is most of the work.
+__global__ __launch_bounds__(256) void union_count_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                          const ViewDev* __restrict__ views, int S,
+                                                          unsigned long long* __restrict__ out) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S) return;
+  const int q = int(item % Q);
+  const int s = int(item / Q);
+  const QueryProg& qp = progs[q];
+  WaveScratch& ws = scratch[wave];
+  uint32_t mask[MAXLEAF];
+  build_slots(qp, views, s, ws, mask);
+  uint32_t cand = 0;
+  for (int k = 0; k < qp.nleaf; k++) cand |= mask[k];
+  unsigned long long* lb64 = reinterpret_cast<unsigned long long*>(ws.lb);
+  uint32_t* lb32 = reinterpret_cast<uint32_t*>(ws.lb);
+  int64_t total = 0;
+  for (uint32_t cm = cand; cm; cm &= cm - 1) {
+    const int j = __builtin_ctz(cm);
+    ulong2* l2 = reinterpret_cast<ulong2*>(ws.lb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) l2[i * 64 + lane] = make_ulong2(0, 0);
+    lds_fence();
+    for (int k = 0; k < qp.nleaf; k++) {
+      const int32_t c = ws.slot[k][j];
+      if (c < 0) continue;
+      const ViewDev& v = views[qp.leaf_view[k]];
+      const int64_t m = v.meta[v.shard_base[s] + c];
+      const uint16_t* p = v.payload + meta_off16(m) * 8;
+      const int type = meta_type(m);
+      if (type == CT_BITMAP) {
+        const ulong2* g = reinterpret_cast<const ulong2*>(p);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const ulong2 w = g[i * 64 + lane];
+          const int wi = 2 * (i * 64 + lane);
+          const unsigned long long ox = atomicOr(lb64 + wi, (unsigned long long)w.x);
+          const unsigned long long oy = atomicOr(lb64 + wi + 1, (unsigned long long)w.y);
+          total += __popcll(w.x & ~ox) + __popcll(w.y & ~oy);
+        }
+      } else if (type == CT_ARRAY) {
+        const int n = meta_n(m);
+        const uint4* p4 = reinterpret_cast<const uint4*>(p);
+        for (int e8 = lane; e8 < ((n + 7) >> 3); e8 += 64) {
+          const uint4 v4 = p4[e8];
+          const uint32_t w4[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (int t = 0; t < 8; t++) {
+            if (e8 * 8 + t < n) {
+              const uint32_t x = (w4[t >> 1] >> ((t & 1) * 16)) & 0xffff;
+              const uint32_t bit = 1u << (x & 31);
+              total += (atomicOr(lb32 + (x >> 5), bit) & bit) ? 0 : 1;
+            }
+          }
+        }
+      } else {
+        const int nr = p[0];
+        for (int r = lane; r < nr; r += 64) {
+          const uint32_t st = p[8 + 2 * r], e = uint32_t(p[9 + 2 * r]) + 1;
+          for (uint32_t w = st >> 6; w <= (e - 1) >> 6; w++) {
+            uint64_t mk = ~0ull;
+            if (w == (st >> 6)) mk &= ~0ull << (st & 63);
+            if (w == ((e - 1) >> 6) && (e & 63)) mk &= (1ull << (e & 63)) - 1;
+            total += __popcll(mk & ~atomicOr(lb64 + w, (unsigned long long)mk));
+          }
+        }
+      }
+    }
+    lds_fence();
+  }
+  total = wave_sum_i64(total);
+  if (lane == 0 && total) atomicAdd(out + q, (unsigned long long)total);
+}
+
 // Materialize kernel: writes result containers for every (q, s, j) with
 // counts[q,s,j] > 0 at u16 offset offs[q,s,j]; array if n <= 4096 else bitmap.
 __global__ __launch_bounds__(256) void expr_materialize_kernel(const QueryProg* __restrict__ progs, int Q,
@@ -992,9 +1076,11 @@ void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int 
   const int64_t items = int64_t(Q) * S;
   if (items == 0) return;
   const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
-  if (mode == 1 && per_key == nullptr)
+  if (mode == 3 && per_key == nullptr && per_shard == nullptr)
+    hipLaunchKernelGGL(union_count_kernel, grid, block, 0, st, progs, Q, views, S, out);
+  else if (mode == 1 && per_key == nullptr)
     hipLaunchKernelGGL(expr_count_kernel<1>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
-  else if (mode == 2)
+  else if (mode == 2 || mode == 3)
     hipLaunchKernelGGL(expr_count_kernel<2>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
   else
     hipLaunchKernelGGL(expr_count_kernel<0>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);

@@ -23,8 +23,9 @@ MAXLEAF = 16
 MAXPROG = 32
 OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 32, 33, 34, 35
 # count-batch kernel routes
-KIND_AND2, KIND_ROW, KIND_GENERIC, KIND_FLAT = 0, 1, 2, 3
-_KERNEL_MODE = {KIND_ROW: 1, KIND_GENERIC: 0, KIND_FLAT: 2}  # expr_count_kernel<MODE>
+KIND_AND2, KIND_ROW, KIND_GENERIC, KIND_FLAT, KIND_UNION = 0, 1, 2, 3, 4
+# launch_expr_count modes: expr_count_kernel<0/1/2>, 3 = union_count_kernel
+_KERNEL_MODE = {KIND_ROW: 1, KIND_GENERIC: 0, KIND_FLAT: 2, KIND_UNION: 3}
 
 
 def flat_mask(progs: np.ndarray) -> np.ndarray:
@@ -433,6 +434,8 @@ class GpuEngine:
         self.use_and2 = os.environ.get("PILOSA_AND2", "1") != "0"
         self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "0"))  # 0 = by batch size
         self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "1"))
+        # Count(Union(leaves)) route: union_count_kernel (bitmap_kernels.hip)
+        self.use_union = os.environ.get("PILOSA_UNION_KERNEL", "1") != "0"
 
     def _views_tensor(self, views: List["DeviceView"]):
         arr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
@@ -534,8 +537,15 @@ class GpuEngine:
         if not self.use_and2 or max(v.container_count for v in views) >= 0xFFFFFFFF:
             is_row = is_row | is_and2
             is_and2 = np.zeros_like(is_and2)
+        flat = flat_mask(progs)
         kind = np.where(is_and2, KIND_AND2, np.where(is_row, KIND_ROW,
-                                                      np.where(flat_mask(progs), KIND_FLAT, KIND_GENERIC)))
+                                                      np.where(flat, KIND_FLAT, KIND_GENERIC)))
+        # flat folds whose every operator is OR: union count kernel
+        pos = np.arange(pg.shape[1])
+        is_op = (pos[None, :] % 2 == 0) & (pos[None, :] > 0) & (pos[None, :] < np_[:, None])
+        all_or = np.where(is_op, pg == OP_OR, True).all(axis=1)
+        if self.use_union:
+            kind = np.where((kind == KIND_FLAT) & all_or, KIND_UNION, kind)
         if is_and2.any():
             progs = self._hot_leaf_first(progs, is_and2)
             lr = progs["leaf_row"]
@@ -544,7 +554,7 @@ class GpuEngine:
             varr[i] = v.viewdev()
         host = [varr.view(np.uint8)]
         meta = []
-        for k in (KIND_AND2, KIND_ROW, KIND_FLAT, KIND_GENERIC):
+        for k in (KIND_AND2, KIND_ROW, KIND_FLAT, KIND_UNION, KIND_GENERIC):
             sel = np.nonzero(kind == k)[0]
             if len(sel) == 0:
                 continue
