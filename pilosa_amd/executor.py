@@ -189,6 +189,20 @@ def merge_group_counts(a: List[GroupCount], b: List[GroupCount], limit: int) -> 
     return out
 
 
+GPU_FAULT_LIMIT = int(os.environ.get("PILOSA_GPU_FAULT_LIMIT", "3"))
+
+
+def _results_equal(a, b) -> bool:
+    """Device vs host result equality for the paranoia check (rows compare
+    by columns, pairs/group counts by value)."""
+    if isinstance(a, Row) and isinstance(b, Row):
+        return list(a.columns()) == list(b.columns())
+    if isinstance(a, Row) or isinstance(b, Row):
+        a = a if not isinstance(a, Row) else list(a.columns())
+        b = b if not isinstance(b, Row) else list(b.columns())
+    return a == b or (not a and not b)
+
+
 class Executor:
     def __init__(self, holder, cluster=None, client=None, gpu=None, workers: int = 8, max_writes: int = 5000,
                  stats=None):
@@ -199,6 +213,11 @@ class Executor:
         self.mesh = None          # parallel.mesh.ShardMesh on a multi-GPU node (rank 0 front end)
         # concurrent single-Count requests share GPU launches (ops/coalescer.py)
         self.coalesce = os.environ.get("PILOSA_COALESCE", "1") != "0"
+        # PILOSA_PARANOIA=1: every device result is re-derived on the host and
+        # compared (the reference's roaringparanoia build tag, for the GPU path)
+        self.paranoia = os.environ.get("PILOSA_PARANOIA", "0") == "1"
+        self.gpu_faults = 0
+        self.logger = None
         self._coalescer = None
         self.max_writes = max_writes
         self.stats = stats
@@ -264,7 +283,13 @@ class Executor:
             return self.mesh.count_batch(index, q.calls, shards)
         if self.gpu is not None and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
                 not self._has_remote(index, shards, opt):
-            res = self.gpu.try_count_batch(index, q.calls, shards)
+            try:
+                res = self.gpu.try_count_batch(index, q.calls, shards)
+            except PilosaError:
+                raise
+            except Exception as err:  # noqa: BLE001 - device fault: host path below
+                self._gpu_fault(err)
+                res = None
             if res is not None:
                 return res
         return [self.execute_call(index, c, shards, opt) for c in q.calls]
@@ -430,8 +455,20 @@ class Executor:
                 r = local_fn(shards)
             except NotImplementedError:
                 r = NotImplemented
+            except PilosaError:
+                raise
+            except Exception as err:  # noqa: BLE001 - device fault: the host fragments answer
+                self._gpu_fault(err)
+                r = NotImplemented
             if r is not NotImplemented:
+                if self.paranoia:
+                    want = self._map_host(shards, map_fn, reduce_fn)
+                    if not _results_equal(r, want):
+                        raise AssertionError(f"paranoia: device result {r!r} != host result {want!r}")
                 return r
+        return self._map_host(shards, map_fn, reduce_fn)
+
+    def _map_host(self, shards: List[int], map_fn, reduce_fn):
         result = None
         if len(shards) <= 1:
             for s in shards:
@@ -441,6 +478,22 @@ class Executor:
         for f in futs:
             result = reduce_fn(result, f.result())
         return result
+
+    def _gpu_fault(self, err: BaseException):
+        """A device call failed (HIP error, lost device, out of memory): the
+        query falls back to the host fragments, which are the source of truth
+        (SURVEY §5.3); after GPU_FAULT_LIMIT faults the device is detached and
+        the node keeps serving from the host path."""
+        self.gpu_faults += 1
+        if self.stats is not None:
+            self.stats.count("gpuFault", 1)
+        if self.logger is not None:
+            self.logger.printf("gpu fault %d (%s: %s), answering from host fragments", self.gpu_faults,
+                               type(err).__name__, err)
+        if self.gpu_faults >= GPU_FAULT_LIMIT and self.gpu is not None:
+            if self.logger is not None:
+                self.logger.printf("gpu detached after %d faults", self.gpu_faults)
+            self.gpu = None
 
     # ================================================================ bitmap calls
     def _bitmap_call(self, index: str, c: Call, shards, opt: ExecOptions) -> Row:

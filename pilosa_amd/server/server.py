@@ -113,6 +113,7 @@ class Server:
         self._init_gpu()
         self.executor = Executor(self.holder, cluster=self.cluster, client=self.client, gpu=self.gpu,
                                  workers=self.workers, max_writes=self.max_writes, stats=self.stats)
+        self.executor.logger = self.logger
         if self.gpu is not None:
             self.gpu.executor = self.executor
         self._init_mesh()

@@ -377,3 +377,19 @@ def test_groupby_count_matrix_matches_host(envs, monkeypatch, q):
     finally:
         cpu.executor.gpu = None
     assert got == want
+
+
+def test_paranoia_cross_check_on_device(envs):
+    """PILOSA_PARANOIA: every device result is re-derived on the host; the
+    whole query mix must pass the cross-check."""
+    cpu, gpu = envs
+    cpu.executor.gpu = gpu
+    cpu.executor.paranoia = True
+    cpu.executor.coalesce = False
+    try:
+        for q in QUERIES + ["Row(f=2)", "Not(Row(f=0))", "TopN(h, Row(f=2), n=5)", "Sum(Row(f=0), field=n)"]:
+            cpu.q1("i", q)
+    finally:
+        cpu.executor.paranoia = False
+        cpu.executor.coalesce = True
+        cpu.executor.gpu = None
