@@ -172,21 +172,64 @@ __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m
 }
 
 // Count array values present in a 1024-word bitmap (LDS or global).
-template <class BM>
+// DBG (cost isolation, scripts/kbench.py variants 14/15; results wrong):
+// bit 2 = synthetic array values instead of loading B, bit 3 = load B but
+// skip the LDS probes.
+template <int DBG = 0, class BM>
 __device__ __forceinline__ int probe(BM bm, const uint16_t* arr, int n) {
   const int lane = lane_id();
   const auto p4 = gp(reinterpret_cast<const uint4*>(arr));
   const int n8 = (n + 7) >> 3;
   int c = 0;
   for (int e8 = lane; e8 < n8; e8 += 64) {
-    const uint4 v4 = p4[e8];
+    uint4 v4;
+    if (DBG & 4) {
+      const uint32_t h = uint32_t(e8) * 2654435761u;
+      v4 = make_uint4(h, h * 7u + 1u, h * 13u + 5u, h * 31u + 9u);
+    } else {
+      v4 = p4[e8];
+    }
     const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+    const int rem = n - e8 * 8;
+    if (DBG & 8) {
+      c += int((w[0] ^ w[1] ^ w[2] ^ w[3]) & 1) + (rem > 0);
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
+      c += k < rem ? int((bm[v >> 5] >> (v & 31)) & 1) : 0;
+    }
+  }
+  return c;
+}
+
+// probe() with the next chunk's load issued before the current chunk's LDS
+// probes (2-deep register pipeline inside one array; the later load is issued
+// after the one being waited for, so the in-order vmcnt wait does not cover it).
+template <class BM>
+__device__ __forceinline__ int probe_pipe(BM bm, const uint16_t* arr, int n) {
+  const int lane = lane_id();
+  const auto p4 = gp(reinterpret_cast<const uint4*>(arr));
+  const int n8 = (n + 7) >> 3;
+  const int iters = (n8 + 63) >> 6;
+  int c = 0;
+  int e8 = lane;
+  uint4 cur = make_uint4(0, 0, 0, 0);
+  if (e8 < n8) cur = p4[e8];
+  for (int it = 0; it < iters; it++) {
+    const int ne8 = e8 + 64;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (it + 1 < iters && ne8 < n8) nxt = p4[ne8];
+    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
     const int rem = n - e8 * 8;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
       c += k < rem ? int((bm[v >> 5] >> (v & 31)) & 1) : 0;
     }
+    cur = nxt;
+    e8 = ne8;
   }
   return c;
 }
@@ -225,11 +268,17 @@ __device__ __forceinline__ int runs_in_lds(const uint64_t* lb, const uint16_t* p
   return c;
 }
 
-// |B ∩ staged| where staged lives in lb.
+// |B ∩ staged| where staged lives in lb.  Arrays use the pipelined probe
+// (34.7 -> 33.2 ms per 4096-query batch, profiles/r01_and2/kbench_b4096_pipe.log);
+// the cost-isolation builds (DBG 4 / 8) use the plain loop they modify.
+template <int DBG = 0>
 __device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* p, int64_t m) {
   const int type = meta_type(m);
   if (type == CT_BITMAP) return and_bitmaps(reinterpret_cast<const ulong2*>(lb), reinterpret_cast<const uint64_t*>(p));
-  if (type == CT_ARRAY) return probe(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
+  if (type == CT_ARRAY) {
+    if (DBG & 12) return probe<DBG>(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
+    return probe_pipe(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
+  }
   return runs_in_lds(lb, p);
 }
 
@@ -282,7 +331,7 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
     const uint16_t* pB = payload_of(views[vb], mB);
     const int tA = meta_type(mA), tB = meta_type(mB);
     int c;
-    if (DBG) {
+    if (DBG & 3) {
       c = 0;
       if (!(DBG & 1) && !(a == cached && va == cached_v)) {
         lds_wait();
@@ -292,7 +341,7 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
       }
       if (!(DBG & 2)) c = count_vs_lds(lb, pB, mB);
     } else if (a == cached && va == cached_v) {
-      c = count_vs_lds(lb, pB, mB);
+      c = count_vs_lds<DBG>(lb, pB, mB);
     } else {
       const bool next_same = i + 1 < nq && __builtin_amdgcn_readlane(ea, i + 1) == a &&
                              __builtin_amdgcn_readlane(vai, i + 1) == va;
@@ -313,7 +362,7 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
         stage(lb, pA, mA);
         cached = a;
         cached_v = va;
-        c = count_vs_lds(lb, pB, mB);
+        c = count_vs_lds<DBG>(lb, pB, mB);
       }
     }
     c = wave_sum(c);
@@ -541,6 +590,13 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   // bigger chunks amortise more leaf-0 stagings (measured: 32 for Q <= 2048,
   // 64 above).
   if (cq <= 0) cq = Q <= 2048 ? 32 : 64;
+  if (variant == 14 || variant == 15) {  // cost isolation: no B loads (14) / no LDS probes (15)
+    const int64_t waves = units * ((Q + 63) / 64);
+    const dim3 g(unsigned((waves + PAIR_WAVES - 1) / PAIR_WAVES)), b(64 * PAIR_WAVES);
+    if (variant == 14) hipLaunchKernelGGL((and2_pairs_kernel<64, 4>), g, b, 0, st, progs, Q, views, S, pairs, partial);
+    else hipLaunchKernelGGL((and2_pairs_kernel<64, 8>), g, b, 0, st, progs, Q, views, S, pairs, partial);
+    return;
+  }
   if (variant >= 11 && variant <= 13) {  // cost-isolation builds (scripts/kbench.py --cq2 / variant)
     const int64_t waves = units * ((Q + 31) / 32);
     const dim3 g(unsigned((waves + PAIR_WAVES - 1) / PAIR_WAVES)), b(64 * PAIR_WAVES);

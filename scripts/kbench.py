@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--shards", type=int, default=0, help="0 = full 954")
     ap.add_argument("--cq", default="0,32,64", help="chunk sizes for variant 1")
     ap.add_argument("--cq2", default="", help="chunk sizes for variant 2")
-    ap.add_argument("--dbg", action="store_true", help="also time the cost-isolation variants 11-13")
+    ap.add_argument("--dbg", action="store_true", help="also time the cost-isolation variants 11-15")
     args = ap.parse_args()
     import torch
 
@@ -47,7 +47,8 @@ def main():
     configs += [(f"and2v2_cq{c}", {"and2_cq": int(c), "and2_variant": 2}) for c in args.cq2.split(",") if c]
     if args.dbg:
         configs += [("dbg_nostage", {"and2_variant": 11}), ("dbg_nocount", {"and2_variant": 12}),
-                    ("dbg_neither", {"and2_variant": 13})]
+                    ("dbg_neither", {"and2_variant": 13}), ("dbg_no_b_loads", {"and2_variant": 14}),
+                    ("dbg_no_probes", {"and2_variant": 15})]
     for name, cfg in configs:
         eng = GpuEngine(dev)
         for k, v in cfg.items():
