@@ -217,6 +217,7 @@ __device__ __forceinline__ int probe_pipe(BM bm, const uint16_t* arr, int n) {
   int e8 = lane;
   uint4 cur = make_uint4(0, 0, 0, 0);
   if (e8 < n8) cur = p4[e8];
+#pragma unroll 2
   for (int it = 0; it < iters; it++) {
     const int ne8 = e8 + 64;
     uint4 nxt = make_uint4(0, 0, 0, 0);
