@@ -859,8 +859,9 @@ class Executor:
             shards = [col // SHARD_WIDTH]
         lim, has_lim = c.uint_arg("limit")
         limit = lim if has_lim else MAX_INT
+        local = (lambda ss: self.gpu.rows(index, fname, c, ss)) if self.gpu is not None else None
         r = self.map_reduce(index, shards, c, opt, lambda s: self._rows_shard(index, fname, c, s),
-                            lambda p, v: merge_row_ids(p or [], v or [], limit))
+                            lambda p, v: merge_row_ids(p or [], v or [], limit), local)
         return r or []
 
     def _rows_shard(self, index: str, fname: str, c: Call, shard: int) -> List[int]:
@@ -869,23 +870,7 @@ class Executor:
         f = self.holder.field(index, fname)
         if f is None:
             raise ErrFieldNotFound
-        views = [VIEW_STANDARD]
-        if f.type == FIELD_TYPE_TIME:
-            from_t = parse_time(c.args["from"]) if "from" in c.args else None
-            to_t = parse_time(c.args["to"]) if "to" in c.args else None
-            if from_t is not None or to_t is not None or f.options.no_standard_view:
-                q = f.time_quantum()
-                if not q:
-                    return []
-                mn, mx = min_max_views(list(f.views), q)
-                if not mn or not mx:
-                    return []
-                min_t, max_t = time_of_view(mn, False), time_of_view(mx, True)
-                if from_t is None or from_t < min_t:
-                    from_t = min_t
-                if to_t is None or to_t > max_t:
-                    to_t = max_t
-                views = views_by_time_range(VIEW_STANDARD, from_t, to_t, q)
+        views = self.rows_views(f, c)
         start = 0
         prev, has_prev = c.uint_arg("previous")
         if has_prev:
@@ -903,6 +888,29 @@ class Executor:
             rows = frag.rows(start, column=col if has_col else None, limit=limit if has_lim else None)
             out = merge_row_ids(out, rows, limit)
         return out
+
+    def rows_views(self, f, c: Call) -> List[str]:
+        """Views a Rows() call lists: standard, or the covering time views of
+        its from/to range clamped to the field's existing views
+        (executor.go:1071-1155)."""
+        views = [VIEW_STANDARD]
+        if f.type == FIELD_TYPE_TIME:
+            from_t = parse_time(c.args["from"]) if "from" in c.args else None
+            to_t = parse_time(c.args["to"]) if "to" in c.args else None
+            if from_t is not None or to_t is not None or f.options.no_standard_view:
+                q = f.time_quantum()
+                if not q:
+                    return []
+                mn, mx = min_max_views(list(f.views), q)
+                if not mn or not mx:
+                    return []
+                min_t, max_t = time_of_view(mn, False), time_of_view(mx, True)
+                if from_t is None or from_t < min_t:
+                    from_t = min_t
+                if to_t is None or to_t > max_t:
+                    to_t = max_t
+                views = views_by_time_range(VIEW_STANDARD, from_t, to_t, q)
+        return views
 
     def _group_by(self, index: str, c: Call, shards, opt) -> List[GroupCount]:
         if not c.children:

@@ -304,6 +304,50 @@ void densify(torch::Tensor view, torch::Tensor rows, int64_t s0, int64_t s1, tor
   check_launch("densify");
 }
 
+void expr_dense(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor outp, torch::Tensor out_meta) {
+  check_dev(progs, "progs");
+  check_dev(views, "views");
+  check_dev(outp, "outp");
+  check_dev(out_meta, "out_meta");
+  TORCH_CHECK(progs.numel() % sizeof(pk::QueryProg) == 0, "progs size");
+  const int Q = int(progs.numel() / sizeof(pk::QueryProg));
+  TORCH_CHECK(outp.scalar_type() == torch::kInt16 && outp.numel() >= int64_t(Q) * S * 16 * 4096,
+              "outp int16[Q*S*16*4096]");
+  TORCH_CHECK(out_meta.scalar_type() == torch::kInt64 && out_meta.numel() >= int64_t(Q) * S * 16,
+              "out_meta int64[Q*S*16]");
+  pk::launch_expr_dense(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()), Q,
+                        reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
+                        reinterpret_cast<uint16_t*>(outp.data_ptr<int16_t>()), out_meta.data_ptr<int64_t>(),
+                        cur_stream(progs));
+  check_launch("expr_dense");
+}
+
+void shift_dense(torch::Tensor src, int64_t S, int64_t n, torch::Tensor main_out, torch::Tensor main_meta,
+                 torch::Tensor spill_out, torch::Tensor spill_meta) {
+  for (auto* t : {&src, &main_out, &spill_out}) {
+    check_dev(*t, "shift payload");
+    TORCH_CHECK(t->scalar_type() == torch::kInt16 && t->numel() == S * 16 * 4096, "shift payload int16[S*16*4096]");
+  }
+  for (auto* t : {&main_meta, &spill_meta}) {
+    check_dev(*t, "shift meta");
+    TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == S * 16, "shift meta int64[S*16]");
+  }
+  TORCH_CHECK(n > 0 && n < (int64_t(1) << 20), "shift needs 0 < n < 2^20");
+  auto u64 = [](torch::Tensor& t) { return reinterpret_cast<uint64_t*>(t.data_ptr<int16_t>()); };
+  pk::launch_shift_dense(u64(src), int(S), n, u64(main_out), main_meta.data_ptr<int64_t>(), u64(spill_out),
+                         spill_meta.data_ptr<int64_t>(), cur_stream(src));
+  check_launch("shift_dense");
+}
+
+void rows_list(torch::Tensor view, int64_t s0, int64_t ns, int64_t j, int64_t col16, torch::Tensor flags) {
+  check_dev(flags, "flags");
+  const pk::ViewDev v = viewdev_from(view);
+  TORCH_CHECK(flags.scalar_type() == torch::kUInt8 && flags.numel() >= v.D, "flags uint8[D]");
+  TORCH_CHECK(s0 >= 0 && ns >= 0 && j < 16 && col16 >= 0 && col16 < 65536, "rows_list arguments");
+  pk::launch_rows(v, int(s0), int(ns), int(j), uint32_t(col16), flags.data_ptr<uint8_t>(), cur_stream(flags));
+  check_launch("rows_list");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -325,6 +369,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
   m.def("bitgemm", &bitgemm, "row-pair intersection count matrix of dense bit rows (mode 1 MFMA i8, 0 VALU)");
+  m.def("expr_dense", &expr_dense, "evaluate expressions into dense one-row views (bitmap per shard/key)");
+  m.def("shift_dense", &shift_dense, "Shift a dense view by n columns per shard (main + next-shard spill)");
+  m.def("rows_list", &rows_list, "flag dense rows with non-empty containers (optionally holding one column)");
   m.def("densify", &densify, "dense bit rows of an arena over a shard range");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("bsi_args"), py::arg("out_sum"), py::arg("out_cnt"),

@@ -543,6 +543,40 @@ __global__ __launch_bounds__(256) void expr_materialize_kernel(const QueryProg* 
   }
 }
 
+// Dense evaluation: every (q, s, j) result tile is written as a bitmap
+// container at the fixed u16 offset ((q*S + s)*16 + j) * 4096 of `outp`, with
+// its metadata word (key j, bitmap, n, offset) in out_meta.  The result is a
+// one-row device view per query whose shard layout matches the inputs; Shift
+// (row_kernels.hip) reads it back word-addressed.
+__global__ __launch_bounds__(256) void expr_dense_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                         const ViewDev* __restrict__ views, int S,
+                                                         uint16_t* __restrict__ outp, int64_t* __restrict__ out_meta) {
+  __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S) return;
+  const int q = int(item % Q);
+  const int s = int(item / Q);
+  const QueryProg& qp = progs[q];
+  WaveScratch& ws = scratch[wave];
+  uint32_t mask[MAXLEAF];
+  build_slots(qp, views, s, ws, mask);
+  const uint32_t cand = candidate_mask(qp, mask);
+  for (int j = 0; j < 16; j++) {
+    const int64_t key = (int64_t(q) * S + s) * 16 + j;
+    Tile acc;
+    if ((cand >> j) & 1) eval_tile(qp, views, s, j, ws, acc);
+    else tile_zero(acc);
+    ulong2* d2 = reinterpret_cast<ulong2*>(outp + key * 4096);
+#pragma unroll
+    for (int i = 0; i < 8; i++) d2[i * 64 + lane] = acc.w[i];
+    const int64_t n = wave_sum_i64(tile_popc(acc));
+    if (lane == 0) out_meta[key] = int64_t(j) | (int64_t(CT_BITMAP) << 4) | (n << 6) | ((key * 512) << 23);
+  }
+}
+
 // BSI sum over bit-sliced rows (fragment.go:1109-1141):
 //   consider = exists & filter ; count = |consider|
 //   sum = Σ_i 2^i (|B_i & consider & ~sign| - |B_i & consider & sign|)
@@ -1092,6 +1126,14 @@ void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views
   if (items == 0) return;
   hipLaunchKernelGGL(expr_materialize_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs,
                      Q, views, S, counts, offs, outp);
+}
+
+void launch_expr_dense(const QueryProg* progs, int Q, const ViewDev* views, int S, uint16_t* outp, int64_t* out_meta,
+                       hipStream_t st) {
+  const int64_t items = int64_t(Q) * S;
+  if (items == 0) return;
+  hipLaunchKernelGGL(expr_dense_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs, Q, views, S,
+                     outp, out_meta);
 }
 
 void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t p1, int64_t p2, uint16_t* out_payload,

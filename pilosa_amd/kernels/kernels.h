@@ -114,4 +114,17 @@ void launch_bitgemm(const uint64_t* A, const uint64_t* B, int M, int N, int64_t 
 // Dense bit rows of an arena: out[R][(s1-s0) * 16384] u64 for dense rows `rows`.
 void launch_densify(const ViewDev& v, const int64_t* rows, int R, int s0, int s1, uint64_t* out, hipStream_t st);
 
+// Dense one-row result views: container (q, s, j) is a bitmap at u16 offset
+// ((q*S + s)*16 + j) * 4096 of outp; out_meta[(q*S + s)*16 + j] its metadata.
+void launch_expr_dense(const QueryProg* progs, int Q, const ViewDev* views, int S, uint16_t* outp, int64_t* out_meta,
+                       hipStream_t st);
+// Shift a dense view (u64[S][16384]) up by n (0 < n < 2^20) columns per shard:
+// main_out = bits that stay in the shard, spill_out = bits carried into the
+// next shard (both dense, with metadata like launch_expr_dense).
+void launch_shift_dense(const uint64_t* src, int S, int64_t n, uint64_t* main_out, int64_t* main_meta,
+                        uint64_t* spill_out, int64_t* spill_meta, hipStream_t st);
+// Rows listing: flags[d] = 1 for dense rows with a non-empty container in
+// shards [s0, s0 + ns) (j >= 0: only rows whose key-j container holds col16).
+void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_t* flags, hipStream_t st);
+
 }  // namespace pk

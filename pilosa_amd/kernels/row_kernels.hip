@@ -1,0 +1,132 @@
+// Row-level device kernels (gfx950): Shift and the Rows listing.
+//
+//   K7  Shift(row, n)   roaring/roaring.go:944-977 (Bitmap.Shift), row.go:217-239
+//   K20 Rows listing    fragment.go:2601-2712 (rows / rowsForColumn)
+//
+// Shift.  The reference shifts a row segment by one bit n times, container by
+// container with a carry.  Here the child expression is first evaluated into
+// a dense one-row view (expr_dense_kernel: one 8 KiB bitmap per (shard, key),
+// i.e. 16384 words per shard), then one pass moves every word: target word T
+// takes source words T - n/64 and T - n/64 - 1, funnel-shifted by n % 64.
+// Targets past the shard's last column form the "spill" view: the bits a
+// per-shard evaluation carries into the next shard's segment (row.go keeps
+// them in the shard's segment; Row.Merge folds them into shard s + 1).  One
+// wave per (shard, half, key), 16 words per lane, fully coalesced.
+//
+// Rows.  One thread per (shard, dense row): the row is listed when one of its
+// containers is non-empty (and, with column=, holds that column's bit:
+// bitmap word test, binary search over array values or run starts).  Flags are
+// a byte per dense row; benign same-value races between shards.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+extern "C" __device__ long __ockl_wfred_add_i64(long);
+
+namespace pk {
+
+namespace {
+
+constexpr int SHARD_WORDS = 16 * 1024;
+
+__global__ __launch_bounds__(256) void shift_dense_kernel(const uint64_t* __restrict__ src, int S, int64_t n,
+                                                          uint64_t* __restrict__ main_out,
+                                                          int64_t* __restrict__ main_meta,
+                                                          uint64_t* __restrict__ spill_out,
+                                                          int64_t* __restrict__ spill_meta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t item = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (item >= int64_t(S) * 32) return;
+  const int s = int(item >> 5);
+  const int half = int(item >> 4) & 1;
+  const int k = int(item & 15);
+  const int64_t nw = n >> 6;
+  const int sh = int(n & 63);
+  const uint64_t* sp = src + int64_t(s) * SHARD_WORDS;
+  uint64_t* dst = (half ? spill_out : main_out) + int64_t(s) * SHARD_WORDS + k * 1024;
+  int c = 0;
+#pragma unroll 4
+  for (int i = 0; i < 16; i++) {
+    const int w = i * 64 + lane;
+    const int64_t a = int64_t(half) * SHARD_WORDS + k * 1024 + w - nw;
+    const uint64_t x = (a >= 0 && a < SHARD_WORDS) ? sp[a] : 0ull;
+    uint64_t r = x;
+    if (sh) {
+      const uint64_t y = (a - 1 >= 0 && a - 1 < SHARD_WORDS) ? sp[a - 1] : 0ull;
+      r = (x << sh) | (y >> (64 - sh));
+    }
+    dst[w] = r;
+    c += __popcll(r);
+  }
+  const int64_t tot = int64_t(__ockl_wfred_add_i64(long(c)));
+  if (lane == 0) {
+    const int64_t key = int64_t(s) * 16 + k;
+    (half ? spill_meta : main_meta)[key] =
+        int64_t(k) | (int64_t(CT_BITMAP) << 4) | (tot << 6) | ((key * 512) << 23);
+  }
+}
+
+__device__ __forceinline__ bool container_has(const uint16_t* payload, int64_t m, uint32_t v) {
+  const int type = meta_type(m);
+  const uint16_t* p = payload + meta_off16(m) * 8;
+  if (type == CT_BITMAP) return (reinterpret_cast<const uint64_t*>(p)[v >> 6] >> (v & 63)) & 1;
+  if (type == CT_ARRAY) {
+    int lo = 0, hi = meta_n(m);  // first index with p[i] >= v
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (p[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo < meta_n(m) && p[lo] == v;
+  }
+  const int nr = p[0];  // runs [start, last] at p[8 + 2r], p[9 + 2r]
+  int lo = 0, hi = nr;  // last run with start <= v
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (p[8 + 2 * mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo > 0 && v <= p[9 + 2 * (lo - 1)];
+}
+
+__global__ __launch_bounds__(256) void rows_kernel(ViewDev v, int s0, int ns, int j, uint32_t col16,
+                                                   uint8_t* __restrict__ flags) {
+  const int64_t item = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (item >= int64_t(ns) * v.D) return;
+  const int s = s0 + int(item / v.D);
+  const int64_t d = item % v.D;
+  const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+  const int64_t base = v.shard_base[s];
+  const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+  for (int64_t ci = lo; ci < hi; ci++) {
+    const int64_t m = v.meta[ci];
+    if (meta_n(m) == 0) continue;
+    if (j < 0) {
+      flags[d] = 1;
+      return;
+    }
+    if (meta_j(m) == j) {
+      if (container_has(v.payload, m, col16)) flags[d] = 1;
+      return;
+    }
+  }
+}
+
+}  // namespace
+
+void launch_shift_dense(const uint64_t* src, int S, int64_t n, uint64_t* main_out, int64_t* main_meta,
+                        uint64_t* spill_out, int64_t* spill_meta, hipStream_t st) {
+  const int64_t waves = int64_t(S) * 32;
+  if (waves == 0) return;
+  hipLaunchKernelGGL(shift_dense_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, src, S, n, main_out,
+                     main_meta, spill_out, spill_meta);
+}
+
+void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_t* flags, hipStream_t st) {
+  const int64_t items = int64_t(ns) * v.D;
+  if (items == 0) return;
+  hipLaunchKernelGGL(rows_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, v, s0, ns, j, col16, flags);
+}
+
+}  // namespace pk

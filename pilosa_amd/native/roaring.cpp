@@ -2,6 +2,7 @@
 // Reference behaviour: roaring/roaring.go (container kernels :2000-4963,
 // file format :1052-1653, op log :4416-4559, official format :5081-5139).
 #include "roaring.hpp"
+#include <map>
 
 #include <algorithm>
 #include <cstdio>
@@ -800,9 +801,49 @@ static Bitmap shift1(const Bitmap& in) {
 }
 
 Bitmap Bitmap::shift(int n) const {
+  // Equivalent to n rounds of shift1 (the reference's Shift(1) loop,
+  // row.go:217-239): every value moves up by n, bits past the largest
+  // container key are dropped.  One pass: container k lands in keys k + n/2^16
+  // and the next one, funnel-shifted by n % 2^16.
   if (n < 0) throw std::invalid_argument("shift: negative shift");
-  Bitmap out = *this;
-  for (int i = 0; i < n; i++) out = shift1(out);
+  if (n == 0) return *this;
+  if (n == 1) return shift1(*this);
+  constexpr uint64_t MAXKEY = (1ull << 48) - 1;
+  const uint64_t nk = uint64_t(n) >> 16;
+  const int rw = (n & 0xffff) >> 6, rb = n & 63;
+  std::map<uint64_t, std::vector<uint64_t>> acc;
+  std::vector<uint64_t> w(BITMAP_N);
+  for (auto& kv : cs) {
+    if (!kv.second.n) continue;
+    std::fill(w.begin(), w.end(), 0);
+    kv.second.to_words(w.data());
+    const uint64_t k0 = kv.first + nk;
+    if (k0 < kv.first || k0 > MAXKEY) continue;  // moved past the last key
+    auto& lo = acc[k0];
+    lo.resize(BITMAP_N, 0);
+    std::vector<uint64_t>* hi = nullptr;
+    if (k0 < MAXKEY) {
+      hi = &acc[k0 + 1];
+      hi->resize(BITMAP_N, 0);
+    }
+    for (int j = 0; j < BITMAP_N; j++) {
+      if (!w[j]) continue;
+      const int t = j + rw;
+      const uint64_t a = w[j] << rb, b = rb ? (w[j] >> (64 - rb)) : 0;
+      if (t < BITMAP_N) lo[t] |= a;
+      else if (hi) (*hi)[t - BITMAP_N] |= a;
+      if (b) {
+        if (t + 1 < BITMAP_N) lo[t + 1] |= b;
+        else if (hi) (*hi)[t + 1 - BITMAP_N] |= b;
+      }
+    }
+  }
+  Bitmap out;
+  for (auto& kv : acc) {
+    Container c;
+    c.set_words(kv.second.data());
+    if (c.n) out.cs.emplace_hint(out.cs.end(), kv.first, std::move(c));
+  }
   return out;
 }
 

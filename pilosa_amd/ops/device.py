@@ -761,6 +761,60 @@ class GpuEngine:
         return DeviceView.from_device(np.zeros(1, np.uint64), rowptr, sb, meta, payload, self.device,
                                       bsi_view.shards, S * 16)
 
+    def _one_row_view(self, payload, meta, shards) -> "DeviceView":
+        """Wrap dense device results (one bitmap per (shard, key)) as a
+        one-row view (row id 0) usable as an expression leaf."""
+        torch = self.torch
+        S = len(shards)
+        rowptr = torch.tensor([0, 16], dtype=torch.int32, device=self.device).repeat(max(S, 0))
+        sb = torch.arange(S + 1, dtype=torch.int64, device=self.device) * 16
+        return DeviceView.from_device(np.zeros(1, np.uint64), rowptr, sb, meta, payload, self.device, shards, S * 16)
+
+    def dense_view(self, expr) -> "DeviceView":
+        """Evaluate one expression over every local shard into a dense one-row
+        view (expr_dense_kernel)."""
+        torch = self.torch
+        progs, views, S = self.compile_batch([expr])
+        payload = torch.empty(S * 16 * 4096, dtype=torch.int16, device=self.device)
+        meta = torch.empty(S * 16, dtype=torch.int64, device=self.device)
+        if S:
+            tp, tv = self.upload_batch(progs, views)
+            self.ext.expr_dense(tp, tv, S, payload, meta)
+        return self._one_row_view(payload, meta, views[0].shards if views else [])
+
+    def shift_views(self, expr, n: int) -> Tuple["DeviceView", "DeviceView"]:
+        """Shift(expr, n) for 0 < n < ShardWidth (row_kernels.hip): the part
+        that stays in each shard, and the spill each shard carries into the
+        next shard's segment (row.go:217-239, roaring.go:944-977)."""
+        torch = self.torch
+        src = self.dense_view(expr)
+        S = src.S
+        outs = [torch.empty(S * 16 * 4096, dtype=torch.int16, device=self.device) for _ in range(2)]
+        metas = [torch.empty(S * 16, dtype=torch.int64, device=self.device) for _ in range(2)]
+        if S:
+            self.ext.shift_dense(src.t_payload, S, int(n), outs[0], metas[0], outs[1], metas[1])
+        return (self._one_row_view(outs[0], metas[0], src.shards),
+                self._one_row_view(outs[1], metas[1], src.shards))
+
+    def row_ids(self, view: "DeviceView", column: Optional[int] = None) -> np.ndarray:
+        """Sorted row ids with a non-empty container on this GPU (with
+        ``column``: rows holding that column's bit), rows_kernel."""
+        torch = self.torch
+        if view.D == 0 or view.S == 0:
+            return np.zeros(0, np.uint64)
+        flags = torch.zeros(view.D, dtype=torch.uint8, device=self.device)
+        vd = torch.from_numpy(np.frombuffer(view.viewdev().tobytes(), dtype=np.uint8).copy())
+        if column is None:
+            self.ext.rows_list(vd, 0, view.S, -1, 0, flags)
+        else:
+            shard, off = divmod(int(column), 1 << 20)
+            if shard not in view.shards:
+                return np.zeros(0, np.uint64)
+            si = view.shards.index(shard)
+            self.ext.rows_list(vd, si, 1, off >> 16, off & 0xffff, flags)
+        idx = torch.nonzero(flags).reshape(-1).cpu().numpy()
+        return np.sort(view.rows[idx])
+
     def bsi_range_count_async(self, bsi_view: "DeviceView", depth: int, op: str, p1: int = 0, p2: int = 0):
         """Count(Row(v <op> x)) without materialising the predicate view:
         device int64[1]."""

@@ -347,6 +347,22 @@ class GpuExecutor:
             if not kids:
                 return EMPTY
             return kids[0] if len(kids) == 1 else Op("xor", tuple(kids))
+        if n == "Shift":
+            k, _ = c.int_arg("n")
+            if len(c.children) != 1 or k < 0:
+                raise NotImplementedError  # the host path raises the proper error
+            child = self.plan(index, c.children[0], shards)
+            if k == 0 or child is EMPTY:
+                return child
+            if k >= SHARD_WIDTH or _has_shift(child):
+                raise NotImplementedError  # multi-shard carries: host path
+            try:
+                self.launches += 2
+                main, spill = self.engine.shift_views(child, k)
+            except CompileError:
+                raise NotImplementedError
+            main._spill = spill
+            return Leaf(main, 0)
         if n == "Not":
             idx = self.holder.index(index)
             if idx is None or idx.existence_field() is None or len(c.children) != 1:
@@ -369,9 +385,14 @@ class GpuExecutor:
         e = self.plan(index, child, shards)
         if e is EMPTY:
             return 0
+        exprs = [e]
+        if _has_shift(e):
+            se = spill_expr(e)
+            if se is not EMPTY:
+                exprs.append(se)
         try:
             self.launches += 1
-            return int(self.engine.count([e])[0])
+            return int(self.engine.count(exprs).sum())
         except CompileError:
             raise NotImplementedError
 
@@ -437,27 +458,68 @@ class GpuExecutor:
                 out[i] = self._ex().count_host(index, calls[i].children[0], shards)
         if live:
             self.launches += 1
-            got = self.engine.count([exprs[i] for i in live])
-            for i, v in zip(live, got):
+            extra = [(i, spill_expr(exprs[i])) for i in live if _has_shift(exprs[i])]
+            extra = [(i, se) for i, se in extra if se is not EMPTY]
+            got = self.engine.count([exprs[i] for i in live] + [se for _, se in extra])
+            for i, v in zip(live, got[:len(live)]):
                 out[i] = int(v)
+            for (i, _), v in zip(extra, got[len(live):]):
+                out[i] += int(v)
         return out
 
     def bitmap(self, index: str, c: Call, shards: List[int]) -> Row:
-        if c.name == "Shift":
-            raise NotImplementedError
         e = self.plan(index, c, shards)
         if e is EMPTY:
             return Row()
         try:
             self.launches += 1
             bms, shard_list = self.engine.materialize(e)
+            spill = ([], [])
+            if _has_shift(e):
+                se = spill_expr(e)
+                if se is not EMPTY:
+                    self.launches += 1
+                    spill = self.engine.materialize(se)
         except CompileError:
             raise NotImplementedError
         row = Row()
         for s, bm in zip(shard_list, bms):
             if bm is not None and bm.any():
                 row.segments[int(s)] = bm
+        # bits a shard's Shift carried past its last column belong to the
+        # next shard's segment (Row.Merge in the reference's reduce)
+        for s, bm in zip(spill[1], spill[0]):
+            if bm is not None and bm.any():
+                part = _rebase_spill(bm)
+                t = int(s) + 1
+                row.segments[t] = row.segments[t].union(part) if t in row.segments else part
         return row
+
+    def rows(self, index: str, fname: str, c: Call, shards: List[int]) -> List[int]:
+        """Rows(field, previous=, column=, limit=, from=, to=) over the local
+        shards in one rows_kernel launch per view (fragment.go:2601-2712)."""
+        from pilosa_amd.executor import MAX_INT
+        if self.holder.index(index) is None:
+            raise NotImplementedError
+        f = self.holder.field(index, fname)
+        if f is None:
+            raise NotImplementedError  # host path raises the proper error
+        prev, has_prev = c.uint_arg("previous")
+        start = prev + 1 if has_prev else 0
+        col, has_col = c.uint_arg("column")
+        lim, has_lim = c.uint_arg("limit")
+        limit = lim if has_lim else MAX_INT
+        if has_col and col // SHARD_WIDTH not in shards:
+            return []
+        ids = np.zeros(0, np.uint64)
+        for vname in self._ex().rows_views(f, c):
+            dv = self.view_arena(index, fname, vname, shards)
+            if dv is None:
+                continue
+            self.launches += 1
+            ids = np.union1d(ids, self.engine.row_ids(dv, col if has_col else None))
+        ids = ids[ids >= np.uint64(start)]
+        return [int(x) for x in ids[:limit]]
 
     def bsi_sum(self, index: str, c: Call, shards: List[int]):
         from pilosa_amd.executor import ValCount, _wrap
@@ -661,6 +723,49 @@ class GpuExecutor:
         except CompileError:
             raise NotImplementedError
         return results[:limit]
+
+
+def _has_shift(e) -> bool:
+    if type(e) is Leaf:
+        return getattr(e.view, "_spill", None) is not None
+    if type(e) is Op:
+        return any(_has_shift(a) for a in e.args)
+    return False
+
+
+def spill_expr(e):
+    """The expression evaluated over the next-shard spill of every Shift leaf:
+    plain leaves hold no bits past their shard (EMPTY), so an Intersect with
+    one drops the spill while Union/Xor/Difference-left keep it -- exactly the
+    per-shard Row algebra of the reference (row.go Intersect/Union/...)."""
+    if type(e) is Leaf:
+        sp = getattr(e.view, "_spill", None)
+        return Leaf(sp, 0) if sp is not None else EMPTY
+    if type(e) is not Op:
+        return EMPTY
+    kids = [spill_expr(a) for a in e.args]
+    if e.op == "and":
+        return EMPTY if any(k is EMPTY for k in kids) else Op("and", tuple(kids))
+    if e.op == "andnot":
+        if kids[0] is EMPTY:
+            return EMPTY
+        rest = [k for k in kids[1:] if k is not EMPTY]
+        return kids[0] if not rest else Op("andnot", (kids[0], *rest))
+    kids = [k for k in kids if k is not EMPTY]  # or / xor
+    if not kids:
+        return EMPTY
+    return kids[0] if len(kids) == 1 else Op(e.op, tuple(kids))
+
+
+def _rebase_spill(bm):
+    """Spill bitmap of `shard` (positions in shard's column range) -> the same
+    bits at shard + 1's columns."""
+    from pilosa_amd import _roaring
+
+    cols = np.asarray(bm.slice(), dtype=np.uint64) + np.uint64(SHARD_WIDTH)
+    out = _roaring.Bitmap()
+    out.add_many(cols)
+    return out
 
 
 def _lex_product(cand: List[List[int]], prev: Optional[Tuple[int, ...]]):

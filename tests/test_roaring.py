@@ -181,3 +181,24 @@ def test_arena_builder_layout():
     assert j.tolist() == [0, 1, 0] and n.tolist() == [1, 1, 1]
     back = R.arena_shard_bitmap(rows, rowptr, sb, meta, payload, 0)
     assert back.slice().tolist() == [5, 70000, (1 << 20) * 3 + 2]
+
+
+def test_shift_n_one_pass_matches_repeated_shift1():
+    """Bitmap.shift(n) moves every value up by n in one pass; it must equal n
+    rounds of the reference's Shift(1) (row.go:217-239)."""
+    rng = np.random.default_rng(7)
+    vals = np.unique(np.concatenate([
+        rng.integers(0, 1 << 20, 3000),                      # sparse arrays
+        np.arange(65536 - 40, 65536 + 40),                   # container boundary
+        np.arange(3 * 65536, 3 * 65536 + 20000),             # a run
+        rng.integers(5 << 16, 6 << 16, 30000),               # a bitmap container
+    ]).astype(np.uint64))
+    b = R.Bitmap()
+    b.add_many(vals)
+    for n in (1, 2, 63, 64, 65, 1000, 65535, 65536, 65537, 200003):
+        want = b
+        if n <= 70:
+            for _ in range(n):
+                want = want.shift(1)
+            assert want.slice().tolist() == b.shift(n).slice().tolist(), n
+        assert b.shift(n).slice().tolist() == (vals + np.uint64(n)).tolist(), n
