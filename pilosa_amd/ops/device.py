@@ -227,6 +227,36 @@ class DeviceView:
         self._rowptr_host = np.asarray(rowptr, dtype=np.int64).reshape(self.S, self.D + 1).copy()
         return self
 
+    def add_rows(self, new_rows) -> bool:
+        """Insert row ids into the dense directory in place: every shard gets an
+        empty container range for them (device rowptr re-gathered column-wise,
+        host mirror likewise), so a write that creates a row patches the arena
+        instead of rebuilding it.  Dense indices shift: generation is bumped,
+        which invalidates everything keyed on them (TopN index, BSI views)."""
+        import torch
+
+        if self._cap is None:
+            return False
+        new = np.setdiff1d(np.asarray(new_rows, dtype=np.uint64), self.rows)
+        if not len(new):
+            return True
+        merged = np.union1d(self.rows, new).astype(np.uint64)
+        if len(merged) >= (1 << 31):
+            return False
+        # new column c starts where the first old row >= merged[c] starts
+        src = np.searchsorted(self.rows, merged).astype(np.int64)
+        src = np.concatenate([src, [self.D]])
+        D2 = len(merged)
+        rp = self.t_rowptr.view(self.S, self.D + 1)
+        idx = torch.from_numpy(src).to(self.device)
+        self.t_rowptr = torch.index_select(rp, 1, idx).contiguous().view(-1)
+        self._rowptr_host = np.take(self._rowptr_host, src, axis=1)
+        self.rows = merged
+        self.D = D2
+        self._row_index = None
+        self.generation += 1
+        return True
+
     def update_rows(self, si: int, rows, storage, keys=()) -> bool:
         """Patch local shard ``si`` in place: every container of ``rows`` (row
         ids) and the single containers ``keys`` (row*16 + local key) are
@@ -245,7 +275,9 @@ class DeviceView:
         touched = sorted(rows | {k >> 4 for k in keys})
         dense_of = dict(zip(touched, self.dense_many(np.array(touched, np.uint64)).tolist()))
         if any(d < 0 for d in dense_of.values()):
-            return False
+            if not self.add_rows([r for r, d in dense_of.items() if d < 0]):
+                return False
+            dense_of = dict(zip(touched, self.dense_many(np.array(touched, np.uint64)).tolist()))
         sw, cw = 1 << 20, 1 << 16
         parts = [storage.offset_range(r * sw, r * sw, (r + 1) * sw) for r in sorted(rows)]
         parts += [storage.offset_range(k * cw, k * cw, (k + 1) * cw) for k in keys]
@@ -324,7 +356,9 @@ class DeviceView:
             return False
         dense = self.dense_many(rows_s) if len(rows_s) else np.zeros(0, np.int64)
         if len(dense) and (dense < 0).any():
-            return False
+            if not self.add_rows(rows_s[dense < 0]):
+                return False
+            dense = self.dense_many(rows_s)
         npay = int(pay_s.shape[0]) if n_new else 0
         if self.payload_used + npay > int(self.t_payload.numel()):
             return False

@@ -245,7 +245,7 @@ def test_generated_queries_gpu_vs_host(envs):
 
 def test_incremental_shard_updates(envs):
     """Writes to a few shards patch the device arena in place (no full
-    re-upload); a new row id outside the directory forces a rebuild."""
+    re-upload), including writes that create new row ids."""
     cpu, gpu = envs
     cpu.executor.gpu = gpu
     try:
@@ -261,9 +261,23 @@ def test_incremental_shard_updates(envs):
             assert got == want
         assert gpu.rebuilds == r0, "writes to existing rows must not re-upload the view"
         assert gpu.shard_updates > u0
-        cpu.q("i", f"Set({2 * SW + 5}, g=4321)")  # new row id -> rebuild of g's view
-        got = cpu.q1("i", "Count(Row(g=4321))")
-        assert got == 1 and gpu.rebuilds > r0
+        # new row ids are inserted into the dense directory in place (no rebuild),
+        # in the middle (g=3 < 4321 < ...) and past the end of the directory
+        for rid, col in ((4321, 2 * SW + 5), (3, 3 * SW + 99), (2, 17), (99999, SW + 1)):
+            cpu.q("i", f"Set({col}, g={rid})")
+            for qq in (f"Count(Row(g={rid}))", "Count(Intersect(Row(g=1), Row(f=0)))", "Count(Row(g=2))",
+                       "Count(Union(Row(g=3), Row(g=4321)))"):
+                got = cpu.q1("i", qq)
+                cpu.executor.gpu = None
+                want = cpu.q1("i", qq)
+                cpu.executor.gpu = gpu
+                assert got == want, qq
+        got = cpu.q1("i", "Rows(g)")
+        cpu.executor.gpu = None
+        want = cpu.q1("i", "Rows(g)")
+        cpu.executor.gpu = gpu
+        assert got == want
+        assert gpu.rebuilds == r0, "a new row id must patch the directory, not re-upload the view"
     finally:
         cpu.executor.gpu = None
 
