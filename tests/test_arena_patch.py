@@ -62,9 +62,16 @@ def test_patched_arena_matches_fragments():
         for si, s in enumerate(SHARDS):
             frag = env.holder.fragment("i", "g", "standard", s)
             assert _decode(dv, si) == frag.storage.slice().astype(np.int64).tolist()
-        # a brand-new row id is outside the directory: full rebuild
-        env.q("i", f"Set({SW + 3}, g=999)")
-        dv = g.view_arena("i", "g", "standard", SHARDS)
-        assert g.rebuilds == 2 and 999 in dv.rows.tolist()
+        # brand-new row ids go into the directory in place (past the end and
+        # in the middle); every shard still decodes to its fragment
+        for col, rid in ((SW + 3, 999), (3 * SW + 70000, 7), (5, 999), (2 * SW + 1, 6)):
+            env.q("i", f"Set({col}, g={rid})")
+            dv = g.view_arena("i", "g", "standard", SHARDS)
+        assert g.rebuilds == 1 and {6, 7, 999} <= set(dv.rows.tolist())
+        assert dv.rows.tolist() == sorted(dv.rows.tolist())
+        for si, s in enumerate(SHARDS):
+            frag = env.holder.fragment("i", "g", "standard", s)
+            assert _decode(dv, si) == frag.storage.slice().astype(np.int64).tolist()
+            assert (dv.t_rowptr.view(dv.S, dv.D + 1)[si].numpy() == dv._rowptr_host[si]).all()
     finally:
         env.close()
