@@ -795,7 +795,8 @@ class Executor:
                 return p if p.id > v.id else v
             return p if p.count > 0 else v
 
-        return self.map_reduce(index, shards, c, opt, map_fn, red) or Pair(0, 0)
+        local = (lambda ss: self.gpu.minmax_row(index, c, ss, is_min)) if self.gpu is not None else None
+        return self.map_reduce(index, shards, c, opt, map_fn, red, local) or Pair(0, 0)
 
     # ================================================================ TopN
     def _topn(self, index: str, c: Call, shards, opt) -> List[Pair]:

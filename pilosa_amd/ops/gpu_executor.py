@@ -521,6 +521,88 @@ class GpuExecutor:
         ids = ids[ids >= np.uint64(start)]
         return [int(x) for x in ids[:limit]]
 
+    MINMAX_ROW_CHUNK = 256
+
+    def minmax_row(self, index: str, c: Call, shards: List[int], is_min: bool) -> Pair:
+        """MinRow/MaxRow(field, [filter]) over the local shards (K16,
+        fragment.go:1230-1268).  Unfiltered: each shard's first/last non-empty
+        row from the arena's per-row cardinalities.  Filtered: rows are
+        counted against the filter in growing chunks (ascending for MinRow,
+        descending for MaxRow) with the pair kernels, all shards per launch,
+        until every shard found its first row with a non-zero intersection.
+        Per-shard pairs are folded in shard order with the reference's reduce
+        (executor.go:517-548)."""
+        import torch
+        fname = c.args.get("field")
+        if not isinstance(fname, str) or self.holder.field(index, fname) is None:
+            raise NotImplementedError
+        rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+        if rv is None or rv.D == 0 or rv.S == 0:
+            return Pair(0, 0)
+        S, D = rv.S, rv.D
+        rid = np.zeros(S, np.int64)
+        cnt = np.zeros(S, np.int64)
+        if len(c.children) != 1:
+            self.launches += 1
+            n = ((rv.t_meta >> 6) & 0x1FFFF).to(torch.int64)
+            cs = torch.zeros(n.numel() + 1, dtype=torch.int64, device=rv.device)
+            torch.cumsum(n, 0, out=cs[1:])
+            rp = rv.t_rowptr.view(S, D + 1).to(torch.int64)
+            sb = rv.t_shard_base.to(torch.int64)
+            for s0 in range(0, S, 32):
+                s1 = min(S, s0 + 32)
+                idx = sb[s0:s1, None] + rp[s0:s1]
+                nz = (cs[idx[:, 1:]] - cs[idx[:, :-1]]) > 0          # [c, D] row non-empty
+                has = nz.any(dim=1)
+                pos = nz.to(torch.int8).argmax(dim=1) if is_min else \
+                    D - 1 - nz.flip(1).to(torch.int8).argmax(dim=1)
+                h, p = has.cpu().numpy(), pos.cpu().numpy()
+                rid[s0:s1] = np.where(h, rv.rows[p].astype(np.int64), 0)
+                cnt[s0:s1] = h.astype(np.int64)
+        else:
+            filt = self.plan(index, c.children[0], shards)
+            if filt is EMPTY:
+                return Pair(0, 0)
+            if type(filt) is Leaf and filt.view.S == S:
+                fview, fdense = filt.view, filt.view.dense(filt.row)
+                if fdense < 0:
+                    return Pair(0, 0)
+            else:
+                try:
+                    self.launches += 1
+                    fview, fdense = self.engine.dense_view(filt), 0
+                except CompileError:
+                    raise NotImplementedError
+            open_ = np.ones(S, bool)
+            lo, chunk = 0, self.MINMAX_ROW_CHUNK
+            while open_.any() and lo < D:
+                hi = min(D, lo + chunk)
+                dense = np.arange(lo, hi, dtype=np.int64) if is_min else np.arange(D - 1 - lo, D - 1 - hi, -1,
+                                                                                   dtype=np.int64)
+                progs = self.engine.pair_programs(0, fdense, 1, dense)
+                self.launches += 1
+                m = self.engine.count_per_shard_progs(progs, [fview, rv], S)   # [rows, S]
+                hit = m > 0
+                first = hit.argmax(axis=0)
+                found = hit.any(axis=0) & open_
+                rid[found] = rv.rows[dense[first[found]]].astype(np.int64)
+                cnt[found] = m[first[found], np.nonzero(found)[0]]
+                open_ &= ~found
+                lo, chunk = hi, chunk * 4
+        out = None
+        for r, n_ in zip(rid.tolist(), cnt.tolist()):
+            v = Pair(r, n_)
+            if out is None:
+                out = v
+            elif out.count > 0 and v.count > 0:
+                if is_min:
+                    out = out if out.id < v.id else v
+                else:
+                    out = out if out.id > v.id else v
+            elif out.count <= 0:
+                out = v
+        return out or Pair(0, 0)
+
     def bsi_sum(self, index: str, c: Call, shards: List[int]):
         from pilosa_amd.executor import ValCount, _wrap
         fname = c.args.get("field")

@@ -452,3 +452,20 @@ def test_rows_listing_on_device_matches_host(envs, q):
     finally:
         cpu.executor.gpu = None
     assert got == want
+
+
+@pytest.mark.parametrize("q", ["MinRow(field=f)", "MaxRow(field=f)", "MinRow(Row(g=1), field=f)",
+                               "MaxRow(Row(g=2), field=f)", "MinRow(Intersect(Row(f=20), Row(g=1)), field=h)",
+                               "MaxRow(Row(f=999), field=f)", "MaxRow(field=h)", "MinRow(Row(f=11), field=h)",
+                               "MaxRow(Union(Row(f=3), Row(g=4)), field=h)", "MinRow(Shift(Row(f=2), n=9), field=f)"])
+def test_minmax_row_on_device_matches_host(envs, q):
+    cpu, gpu = envs
+    want = cpu.q1("i", q)
+    cpu.executor.gpu = gpu
+    try:
+        n0 = gpu.launches
+        got = cpu.q1("i", q)
+        assert "999" in q or gpu.launches > n0  # no silent host fallback
+    finally:
+        cpu.executor.gpu = None
+    assert got == want
