@@ -13,10 +13,10 @@
 // them in the shard's segment; Row.Merge folds them into shard s + 1).  One
 // wave per (shard, half, key), 16 words per lane, fully coalesced.
 //
-// Rows.  One thread per (shard, dense row): the row is listed when one of its
-// containers is non-empty (and, with column=, holds that column's bit:
-// bitmap word test, binary search over array values or run starts).  Flags are
-// a byte per dense row; benign same-value races between shards.
+// Rows.  One thread per dense row walks the shards: the row is listed at its
+// first non-empty container (with column=: the first key-j container holding
+// that column's bit -- bitmap word test, binary search over array values or
+// run starts).  Flags are a byte per dense row.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -92,23 +92,28 @@ __device__ __forceinline__ bool container_has(const uint16_t* payload, int64_t m
 
 __global__ __launch_bounds__(256) void rows_kernel(ViewDev v, int s0, int ns, int j, uint32_t col16,
                                                    uint8_t* __restrict__ flags) {
-  const int64_t item = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (item >= int64_t(ns) * v.D) return;
-  const int s = s0 + int(item / v.D);
-  const int64_t d = item % v.D;
-  const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
-  const int64_t base = v.shard_base[s];
-  const int64_t lo = base + rp[d], hi = base + rp[d + 1];
-  for (int64_t ci = lo; ci < hi; ci++) {
-    const int64_t m = v.meta[ci];
-    if (meta_n(m) == 0) continue;
-    if (j < 0) {
-      flags[d] = 1;
-      return;
-    }
-    if (meta_j(m) == j) {
-      if (container_has(v.payload, m, col16)) flags[d] = 1;
-      return;
+  // one thread per dense row, walking the shards until the row shows up
+  // (hot rows stop at the first shard; rowptr reads are coalesced across d)
+  const int64_t d = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (d >= v.D) return;
+  for (int s = s0; s < s0 + ns; s++) {
+    const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+    const int64_t base = v.shard_base[s];
+    const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+    for (int64_t ci = lo; ci < hi; ci++) {
+      const int64_t m = v.meta[ci];
+      if (meta_n(m) == 0) continue;
+      if (j < 0) {
+        flags[d] = 1;
+        return;
+      }
+      if (meta_j(m) == j) {
+        if (container_has(v.payload, m, col16)) {
+          flags[d] = 1;
+          return;
+        }
+        break;
+      }
     }
   }
 }
@@ -124,9 +129,8 @@ void launch_shift_dense(const uint64_t* src, int S, int64_t n, uint64_t* main_ou
 }
 
 void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_t* flags, hipStream_t st) {
-  const int64_t items = int64_t(ns) * v.D;
-  if (items == 0) return;
-  hipLaunchKernelGGL(rows_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, v, s0, ns, j, col16, flags);
+  if (ns == 0 || v.D == 0) return;
+  hipLaunchKernelGGL(rows_kernel, dim3(unsigned((v.D + 255) / 256)), dim3(256), 0, st, v, s0, ns, j, col16, flags);
 }
 
 }  // namespace pk

@@ -847,7 +847,7 @@ class GpuEngine:
             si = view.shards.index(shard)
             self.ext.rows_list(vd, si, 1, off >> 16, off & 0xffff, flags)
         idx = torch.nonzero(flags).reshape(-1).cpu().numpy()
-        return np.sort(view.rows[idx])
+        return view.rows[idx]  # the directory is sorted
 
     def bsi_range_count_async(self, bsi_view: "DeviceView", depth: int, op: str, p1: int = 0, p2: int = 0):
         """Count(Row(v <op> x)) without materialising the predicate view:

@@ -136,6 +136,50 @@ def config5(args, dev):
     return res
 
 
+def config_rowops(args, dev):
+    """Row-level calls on the config-2 index (1M rows x 1B cols, 8 bits per
+    column): Rows listing (rows_kernel), Rows(column=), Shift (expr_dense +
+    shift_dense + spill count), Count(Intersect(Shift(a), b))."""
+    import torch
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.ops.device import DeviceView, GpuEngine, Leaf, Op
+
+    S = math.ceil(args.cols / SHARD_WIDTH)
+    nrows = 1_000_000
+    t0 = time.time()
+    arena = _roaring.gen_zipf_arena(0, S, args.cols, nrows, 8.0, 1.6, 50.0, 1, 16)
+    gen_s = time.time() - t0
+    view = DeviceView(*arena, dev, shards=list(range(S)))
+    del arena
+    eng = GpuEngine(dev)
+    rng = np.random.default_rng(3)
+    q = {}
+
+    def rec(name, fn):
+        dt, out = timed(fn, args.reps)
+        q[name] = {"ms": round(dt * 1000, 3), "result": out}
+
+    rec("Rows(f)", lambda: len(eng.row_ids(view)))
+    rec("Rows(f, column=c)", lambda: len(eng.row_ids(view, int(rng.integers(0, args.cols)))))
+
+    def shift_count(a, n, b=None):
+        main, spill = eng.shift_views(Leaf(view, a), n)
+        if b is None:
+            return int(eng.count([Leaf(main, 0), Leaf(spill, 0)]).sum())
+        return int(eng.count([Op("and", (Leaf(main, 0), Leaf(view, b)))])[0])
+
+    rec("Count(Shift(Row(f=0), n=1))", lambda: shift_count(0, 1))
+    rec("Count(Shift(Row(f=500), n=1000))", lambda: shift_count(500, 1000))
+    rec("Count(Intersect(Shift(Row(f=0), n=1), Row(f=1)))", lambda: shift_count(0, 1, 1))
+    rec("Count(Row(f=0))", lambda: int(eng.count([Leaf(view, 0)])[0]))
+    res = {"config": "row ops on the config-2 index (1M rows x 1B cols)", "gen_s": round(gen_s, 1),
+           "hbm_bytes": view.nbytes(), "queries": q}
+    del view
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cols", type=int, default=TOTAL_COLS)
@@ -149,6 +193,8 @@ def main():
         print(json.dumps(config4(args, dev)), flush=True)
     if "5" in args.only:
         print(json.dumps(config5(args, dev)), flush=True)
+    if "r" in args.only:
+        print(json.dumps(config_rowops(args, dev)), flush=True)
 
 
 if __name__ == "__main__":
