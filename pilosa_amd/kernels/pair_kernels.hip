@@ -235,6 +235,49 @@ __device__ __forceinline__ int probe_pipe(BM bm, const uint16_t* arr, int n) {
   return c;
 }
 
+// probe_pipe() that also carries the first chunk across pairs: `pre` holds
+// this array's first chunk when have_pre (loaded during the previous pair's
+// last iteration), and the last iteration here loads the next pair's first
+// chunk (next != nullptr) into `pre` -- issued after every load of this
+// array, so the in-order vmcnt waits of this pair never cover it.
+template <class BM>
+__device__ __forceinline__ int probe_pipe_x(BM bm, const uint16_t* arr, int n, uint4& pre, bool have_pre,
+                                            const uint16_t* next, int next_n) {
+  const int lane = lane_id();
+  const auto p4 = gp(reinterpret_cast<const uint4*>(arr));
+  const int n8 = (n + 7) >> 3;
+  const int iters = (n8 + 63) >> 6;
+  const int nn8 = (next_n + 7) >> 3;
+  int c = 0;
+  int e8 = lane;
+  uint4 cur = pre;
+  if (!have_pre) {
+    cur = make_uint4(0, 0, 0, 0);
+    if (e8 < n8) cur = p4[e8];
+  }
+#pragma unroll 2
+  for (int it = 0; it < iters; it++) {
+    const int ne8 = e8 + 64;
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    if (it + 1 < iters) {
+      if (ne8 < n8) nxt = p4[ne8];
+    } else if (next != nullptr && lane < nn8) {
+      nxt = gp(reinterpret_cast<const uint4*>(next))[lane];
+    }
+    const uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w};
+    const int rem = n - e8 * 8;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
+      c += k < rem ? int((bm[v >> 5] >> (v & 31)) & 1) : 0;
+    }
+    cur = nxt;
+    e8 = ne8;
+  }
+  pre = cur;
+  return c;
+}
+
 template <class PX>
 __device__ __forceinline__ int and_bitmaps(PX a, const uint64_t* y) {
   const int lane = lane_id();
@@ -283,6 +326,42 @@ __device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* 
   return runs_in_lds(lb, p);
 }
 
+// Cross-pair prefetch of the next B array's first chunk: measured slower
+// (37.0 vs 32.0 ms per 4096-query batch, profiles/r01_and2/kbench_b4096_xpf*.log),
+// kept selectable.
+constexpr bool PAIR_XPF = false;
+
+// B payload of pair i + 1 when it is an array (the only case probed by
+// probe_pipe_x); wave-uniform.
+__device__ __forceinline__ uint64_t rl_u64(uint64_t v, int i) {
+  return (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(v >> 32), i))) << 32) |
+         uint32_t(__builtin_amdgcn_readlane(int(v), i));
+}
+
+__device__ __forceinline__ void next_b_array(int i, int nq, uint32_t ea, int64_t mb, uint64_t pbl,
+                                             const uint16_t*& nB, int& nBn) {
+  if (i + 1 >= nq || __builtin_amdgcn_readlane(ea, i + 1) == NONE) return;
+  const int64_t m1 = int64_t(rl_u64(uint64_t(mb), i + 1));
+  if (meta_type(m1) != CT_ARRAY) return;
+  nB = reinterpret_cast<const uint16_t*>(rl_u64(pbl, i + 1));
+  nBn = meta_n(m1);
+}
+
+// count_vs_lds() for DBG == 0 with the cross-pair first-chunk prefetch;
+// have_pre is updated to whether `pre` now holds the next array's chunk.
+__device__ __forceinline__ int count_vs_lds_x(const uint64_t* lb, const uint16_t* p, int64_t m, uint4& pre,
+                                              bool& have_pre, const uint16_t* next, int next_n) {
+  const int type = meta_type(m);
+  if (type == CT_ARRAY) {
+    const int c = probe_pipe_x(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m), pre, have_pre, next, next_n);
+    have_pre = next != nullptr;
+    return c;
+  }
+  have_pre = false;
+  if (type == CT_BITMAP) return and_bitmaps(reinterpret_cast<const ulong2*>(lb), reinterpret_cast<const uint64_t*>(p));
+  return runs_in_lds(lb, p);
+}
+
 // DBG (profiling builds only): bit 0 = never stage (probe the stale LDS
 // bitmap), bit 1 = skip counting; results are wrong, timings isolate costs.
 template <int CQ, int DBG = 0>
@@ -304,6 +383,7 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
   uint32_t ea = NONE, eb = NONE;
   int vai = 0, vbi = 0;
   int64_t ma = 0, mb = 0;
+  uint64_t pal = 0, pbl = 0;  // per-lane payload addresses: no scalar loads in the pair loop
   if (lane < CQ && q0 + lane < Q) {
     const uint2 e = pairs[u * Q + q0 + lane];
     ea = e.x;
@@ -313,23 +393,30 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
       vbi = progs[q0 + lane].leaf_view[1];
       ma = gp(views[vai].meta)[ea];
       mb = gp(views[vbi].meta)[eb];
+      pal = reinterpret_cast<uint64_t>(payload_of(views[vai], ma));
+      pbl = reinterpret_cast<uint64_t>(payload_of(views[vbi], mb));
     }
   }
   int mine = 0;
   uint32_t cached = NONE;
   int cached_v = -1;
   const int nq = min(CQ, Q - q0);
+  uint4 pre = make_uint4(0, 0, 0, 0);  // first chunk of this pair's B array (cross-pair prefetch)
+  bool have_pre = false;
   for (int i = 0; i < nq; i++) {
     const uint32_t a = __builtin_amdgcn_readlane(ea, i);
-    if (a == NONE) continue;
+    if (a == NONE) {
+      have_pre = false;
+      continue;
+    }
     const int va = __builtin_amdgcn_readlane(vai, i);
     const int vb = __builtin_amdgcn_readlane(vbi, i);
     const int64_t mA = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(ma >> 32), i))) << 32) |
                                uint32_t(__builtin_amdgcn_readlane(int(ma), i)));
     const int64_t mB = int64_t((uint64_t(uint32_t(__builtin_amdgcn_readlane(int(mb >> 32), i))) << 32) |
                                uint32_t(__builtin_amdgcn_readlane(int(mb), i)));
-    const uint16_t* pA = payload_of(views[va], mA);
-    const uint16_t* pB = payload_of(views[vb], mB);
+    const uint16_t* pA = reinterpret_cast<const uint16_t*>(rl_u64(pal, i));
+    const uint16_t* pB = reinterpret_cast<const uint16_t*>(rl_u64(pbl, i));
     const int tA = meta_type(mA), tB = meta_type(mB);
     int c;
     if (DBG & 3) {
@@ -342,13 +429,21 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
       }
       if (!(DBG & 2)) c = count_vs_lds(lb, pB, mB);
     } else if (a == cached && va == cached_v) {
-      c = count_vs_lds<DBG>(lb, pB, mB);
+      if (DBG || !PAIR_XPF) {
+        c = count_vs_lds<DBG>(lb, pB, mB);
+      } else {
+        const uint16_t* nB = nullptr;
+        int nBn = 0;
+        next_b_array(i, nq, ea, mb, pbl, nB, nBn);
+        c = count_vs_lds_x(lb, pB, mB, pre, have_pre, nB, nBn);
+      }
     } else {
       const bool next_same = i + 1 < nq && __builtin_amdgcn_readlane(ea, i + 1) == a &&
                              __builtin_amdgcn_readlane(vai, i + 1) == va;
       if (!next_same && tA == CT_BITMAP && tB == CT_BITMAP) {
         // one-off bitmap pair: two coalesced 8 KiB streams, no LDS
         c = and_bitmaps(gp(reinterpret_cast<const ulong2*>(pA)), reinterpret_cast<const uint64_t*>(pB));
+        have_pre = false;
       } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
         // one-off array & bitmap: copy the bitmap into LDS (64 coalesced lines)
         // and probe the array there; probing the bitmap in global memory
@@ -358,12 +453,20 @@ __global__ __launch_bounds__(64 * PAIR_WAVES) void and2_pairs_kernel(const Query
         cached = NONE;
         cached_v = -1;
         c = count_vs_lds(lb, pA, mA);
+        have_pre = false;
       } else {
         lds_wait();  // previous readers of lb are done before it is rewritten
         stage(lb, pA, mA);
         cached = a;
         cached_v = va;
-        c = count_vs_lds<DBG>(lb, pB, mB);
+        if (DBG || !PAIR_XPF) {
+          c = count_vs_lds<DBG>(lb, pB, mB);
+        } else {
+          const uint16_t* nB = nullptr;
+          int nBn = 0;
+          next_b_array(i, nq, ea, mb, pbl, nB, nBn);
+          c = count_vs_lds_x(lb, pB, mB, pre, have_pre, nB, nBn);
+        }
       }
     }
     c = wave_sum(c);
