@@ -613,6 +613,22 @@ PYBIND11_MODULE(_roaring, m) {
   m.attr("RUN_MAX") = pr::RUN_MAX;
   m.attr("MAGIC") = pr::MAGIC;
 
+  // value iterator with Seek (reference roaring.go:1767-1982); next() returns
+  // (value, eof) like the reference, and the object is a Python iterator too
+  py::class_<pr::Iterator>(m, "Iterator")
+      .def("seek", &pr::Iterator::seek)
+      .def("next", [](pr::Iterator& it) {
+        uint64_t v = 0;
+        bool ok = it.next(&v);
+        return py::make_tuple(v, !ok);
+      })
+      .def("__iter__", [](pr::Iterator& it) -> pr::Iterator& { return it; })
+      .def("__next__", [](pr::Iterator& it) {
+        uint64_t v = 0;
+        if (!it.next(&v)) throw py::stop_iteration();
+        return v;
+      });
+
   py::class_<Bitmap>(m, "Bitmap")
       .def(py::init<>())
       .def(py::init([](u64arr vals) {
@@ -644,6 +660,7 @@ PYBIND11_MODULE(_roaring, m) {
       .def("any", &Bitmap::any)
       .def("max", &Bitmap::max)
       .def("min", &Bitmap::min)
+      .def("iterator", [](const Bitmap& b) { return pr::Iterator(&b); }, py::keep_alive<0, 1>())
       .def("slice", [](const Bitmap& b) { return to_np(b.slice()); })
       .def("slice_range", [](const Bitmap& b, uint64_t s, uint64_t e) { return to_np(b.slice_range(s, e)); })
       .def("offset_range", &Bitmap::offset_range)

@@ -331,6 +331,51 @@ int Container::min() const {
   return -1;
 }
 
+int Container::next_from(int v) const {
+  if (v > 65535) return -1;
+  switch (type) {
+    case CT_ARRAY: {
+      auto p = std::lower_bound(a.begin(), a.end(), uint16_t(v));
+      return p == a.end() ? -1 : int(*p);
+    }
+    case CT_BITMAP: {
+      int i = v >> 6;
+      uint64_t w = b[i] & (~0ull << (v & 63));
+      while (true) {
+        if (w) return i * 64 + __builtin_ctzll(w);
+        if (++i >= BITMAP_N) return -1;
+        w = b[i];
+      }
+    }
+    case CT_RUN:
+      for (const Iv& iv : r) {  // runs are few (<= 2048); linear is fine
+        if (iv.last < v) continue;
+        return iv.start > v ? int(iv.start) : v;
+      }
+      return -1;
+  }
+  return -1;
+}
+
+void Iterator::seek(uint64_t v) {
+  it_ = bm_->cs.lower_bound(v >> 16);
+  low_ = (it_ != bm_->cs.end() && it_->first == (v >> 16)) ? int(v & 0xffff) : 0;
+}
+
+bool Iterator::next(uint64_t* v) {
+  while (it_ != bm_->cs.end()) {
+    int x = it_->second.n ? it_->second.next_from(low_) : -1;
+    if (x >= 0) {
+      *v = (it_->first << 16) | uint64_t(x);
+      low_ = x + 1;
+      return true;
+    }
+    ++it_;
+    low_ = 0;
+  }
+  return false;
+}
+
 size_t Container::encoded_size() const {
   switch (type) {
     case CT_ARRAY: return a.size() * 2;

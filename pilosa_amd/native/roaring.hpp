@@ -61,6 +61,7 @@ struct Container {
   int32_t count_range(int start, int end) const;  // [start,end) in 0..65536
   int max() const;
   int min() const;
+  int next_from(int v) const;               // smallest value >= v, or -1
   void optimize();
   void to_bitmap();
   void to_array();
@@ -136,5 +137,21 @@ class Bitmap {
 };
 
 Container& get_or_create(Bitmap& b, uint64_t key);
+
+// Value iterator with Seek (reference roaring.go:1767-1982 Iterator).  Holds
+// the container map position between calls, so a forward walk costs one map
+// step per container; Seek re-positions with one lower_bound.  The bitmap must
+// not be mutated while an iterator is live (same contract as the reference).
+class Iterator {
+ public:
+  explicit Iterator(const Bitmap* b) : bm_(b) { seek(0); }
+  void seek(uint64_t v);
+  // next value, or eof=true when exhausted
+  bool next(uint64_t* v);
+ private:
+  const Bitmap* bm_;
+  std::map<uint64_t, Container>::const_iterator it_;
+  int low_ = 0;  // next low-16 candidate inside *it_ (65536 = past the end)
+};
 
 }  // namespace pr

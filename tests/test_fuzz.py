@@ -81,3 +81,35 @@ def test_generated_queries_execute_consistently():
             env.q("i", q)
     finally:
         env.close()
+
+
+def test_iterator_seek_matches_naive():
+    """Bitmap.iterator() with seek (reference roaring.go:1767-1982)."""
+    from pilosa_amd.testing.naive import NaiveBitmap
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([rng.integers(0, 1 << 30, 3000, dtype=np.uint64),
+                           np.arange(70000, 140000, dtype=np.uint64),        # bitmap containers
+                           np.arange(1 << 33, (1 << 33) + 9000, dtype=np.uint64)])
+    b = R.Bitmap(vals)
+    b.optimize()  # the long ranges become run containers
+    nb = NaiveBitmap(vals.tolist())
+    assert list(b.iterator()) == nb.slice()
+    for x in rng.integers(0, (1 << 33) + 10000, 300).tolist() + [0, 70000, 139999, 140000, (1 << 40)]:
+        it = b.iterator()
+        it.seek(x)
+        v, eof = it.next()
+        assert (None if eof else v) == nb.seek_next(x)
+    it = R.Bitmap().iterator()
+    assert it.next() == (0, True)
+
+
+def test_fuzz_roaring_ops_vs_naive():
+    """FuzzRoaringOps analog: one op stream on native and naive bitmaps."""
+    from pilosa_amd.testing.naive import fuzz_ops
+    assert sum(fuzz_ops(seed, 120) for seed in range(8)) == 960
+
+
+def test_fuzz_unmarshal_never_crashes():
+    """FuzzBitmapUnmarshalBinary analog: mutated files load or raise."""
+    from pilosa_amd.testing.naive import fuzz_unmarshal
+    assert sum(fuzz_unmarshal(seed, 60) for seed in range(6)) > 0
