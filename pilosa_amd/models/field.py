@@ -262,6 +262,10 @@ class Field:
         m = pb.FieldOptions()
         with open(self.meta_path(), "rb") as fh:
             m.ParseFromString(fh.read())
+        # v1 BSI meta has no bit depth: base starts at min (field.go:500-507)
+        if m.BitDepth == 0 and m.Type == "int":
+            m.Base = m.Min
+            m.BitDepth = bit_depth_int64(m.Max - m.Min) or 1
         self._apply_options(FieldOptions.from_pb(m))
 
     def available_shards_path(self) -> str:
@@ -294,6 +298,10 @@ class Field:
             for name in sorted(os.listdir(vdir)):
                 if os.path.isdir(os.path.join(vdir, name)):
                     v = self._new_view(name).open()
+                    if name.startswith("bsig_") and self.bsi is not None:
+                        # upgrade v1 BSI fragments in place (field.go:461-473)
+                        for frag in v.all_fragments():
+                            frag.upgrade_bsi_v2(self.bsi.bit_depth)
                     self.views[name] = v
                     self.local_shards |= set(v.fragments)
         return self

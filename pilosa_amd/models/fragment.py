@@ -237,6 +237,27 @@ class Fragment:
             if self.stats:
                 self.stats.count("snapshot", 1)
 
+    def upgrade_bsi_v2(self, bit_depth: int) -> bool:
+        """Rewrite a v1 BSI fragment in the v2 layout (reference
+        fragment.go:2717-2757 ``upgradeRoaringBSIv2``, view.go:436-454).  v1
+        kept the bit planes at rows ``0..bitDepth-1`` and the not-null row at
+        ``bitDepth``; v2 has exists=0, sign=1 and the planes from row 2.
+        Returns True when the fragment was rewritten."""
+        with self.mu:
+            if self.storage.flags & ROARING_FLAG_BSI_V2:
+                return False
+            vals = self.storage.slice()
+            w = np.uint64(SHARD_WIDTH_EXP)
+            rows = vals >> w
+            low = vals & np.uint64(SHARD_WIDTH - 1)
+            new_rows = np.where(rows == np.uint64(bit_depth), np.uint64(BSI_EXISTS_BIT),
+                                rows + np.uint64(BSI_OFFSET_BIT))
+            other = Bitmap(np.sort((new_rows << w) | low))
+            other.flags = ROARING_FLAG_BSI_V2
+            self.storage = other
+        self.snapshot()  # write -> fsync -> rename, as the reference's tmp file + rename
+        return True
+
     # ------------------------------------------------------------ rows
     def row(self, row_id: int) -> Row:
         with self.mu:

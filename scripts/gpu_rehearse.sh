@@ -1,12 +1,13 @@
 #!/bin/bash
-# 2-rank rehearsal of the N-GPU bench path on a 1-GPU box (gloo collectives
+# NP-rank (default 2) rehearsal of the N-GPU bench path on a 1-GPU box (gloo collectives
 # through host copies), then a kernel-trace profile of the TopN paths.
 set -o pipefail
 mkdir -p gpurun_out/prof
-PILOSA_BENCH_REHEARSE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --cols 100000000 \
-  --batch 1024 > gpurun_out/rehearse2.log 2>&1 || { tail -c 2000 gpurun_out/rehearse2.log; exit 1; }
-tail -c 1500 gpurun_out/rehearse2.log
+NP=${NP:-2}
+PILOSA_BENCH_REHEARSE=1 timeout -k 10 ${RTIMEOUT:-300} python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP \
+  --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus $NP --steps 3 --warmup 1 --cols ${COLS:-100000000} \
+  --batch ${BATCH:-1024} > gpurun_out/rehearse$NP.log 2>&1 || { tail -c 2000 gpurun_out/rehearse$NP.log; exit 1; }
+tail -c 1500 gpurun_out/rehearse$NP.log
 [ -n "$PROFILE" ] || exit 0
 R=$PWD
 cd /tmp && export TMPDIR=/tmp

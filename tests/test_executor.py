@@ -283,3 +283,56 @@ def test_persistence_reopen(env):
     assert cols(env.q1("i", "Row(f=1)")) == [1, SW + 7]
     assert env.q1("i", "Sum(field=n)") == ValCount(-25, 2)
     assert env.holder.field("i", "n").bsi.bit_depth == 6
+
+
+def test_bsi_v1_fragment_upgrade():
+    """v1 BSI files (planes at rows 0.., not-null at row bitDepth, values
+    offset by min, no bitDepth in the meta) are rewritten as v2 on open
+    (reference fragment.go:2717 upgradeRoaringBSIv2, field.go:500-507)."""
+    import os
+    import numpy as np
+    from pilosa_amd import _roaring as R
+    from pilosa_amd.models.field import bit_depth_int64
+    from pilosa_amd.wire import pb
+    env = Env()
+    try:
+        env.create_index("i")
+        f = env.field("i", "v", type="int", min=10, max=1000)
+        vals = {1: 10, 5: 17, SW + 3: 999, SW + 9: 500}
+        for c, x in vals.items():
+            env.q("i", f"Set({c}, v={x})")
+        meta_path = f.meta_path()
+        env.holder.close()
+        bd = bit_depth_int64(1000 - 10)
+        for shard in (0, 1):
+            pos = []
+            for c, x in vals.items():
+                if c // SW != shard:
+                    continue
+                lo = c % SW
+                pos.append(bd * SW + lo)  # v1 not-null row
+                for i in range(bd):
+                    if (x - 10) >> i & 1:
+                        pos.append(i * SW + lo)
+            b = R.Bitmap(np.array(sorted(pos), dtype=np.uint64))
+            b.flags = 0
+            path = os.path.join(env.dir, "i", "v", "views", "bsig_v", "fragments", str(shard))
+            with open(path, "wb") as fh:
+                fh.write(b.to_bytes())
+        m = pb.FieldOptions()
+        with open(meta_path, "rb") as fh:
+            m.ParseFromString(fh.read())
+        m.BitDepth, m.Base = 0, 0
+        with open(meta_path, "wb") as fh:
+            fh.write(m.SerializeToString())
+        env.reopen()
+        assert env.q1("i", "Sum(field=v)") == ValCount(sum(vals.values()), len(vals))
+        assert env.q1("i", "Min(field=v)") == ValCount(10, 1)
+        assert env.q1("i", "Max(field=v)") == ValCount(999, 1)
+        assert cols(env.q1("i", "Row(v > 100)")) == [SW + 3, SW + 9]
+        frag = env.holder.index("i").field("v").views["bsig_v"].fragment(0)
+        assert frag.storage.flags & 1
+        env.reopen()  # upgraded file is v2 on disk: a second open keeps it
+        assert env.q1("i", "Sum(field=v)") == ValCount(sum(vals.values()), len(vals))
+    finally:
+        env.close()
