@@ -262,11 +262,17 @@ class Field:
         m = pb.FieldOptions()
         with open(self.meta_path(), "rb") as fh:
             m.ParseFromString(fh.read())
-        # v1 BSI meta has no bit depth: base starts at min (field.go:500-507)
-        if m.BitDepth == 0 and m.Type == "int":
+        # v1 BSI meta has no bit depth: base starts at min (field.go:500-507).
+        # Only a field that already holds BSI data can be v1; a freshly
+        # created int field also has bit depth 0 until its first write.
+        if m.BitDepth == 0 and m.Type == "int" and self._has_bsi_data(m):
             m.Base = m.Min
             m.BitDepth = bit_depth_int64(m.Max - m.Min) or 1
         self._apply_options(FieldOptions.from_pb(m))
+
+    def _has_bsi_data(self, m) -> bool:
+        vdir = os.path.join(self.path, "views", VIEW_BSI_PREFIX + self.name, "fragments")
+        return os.path.isdir(vdir) and any(not n.endswith((".cache", ".tmp")) for n in os.listdir(vdir))
 
     def available_shards_path(self) -> str:
         return os.path.join(self.path, ".available.shards")
@@ -420,7 +426,7 @@ class Field:
 
     def _grow_bit_depth(self, base_value: int):
         b = self.bsi
-        need = bit_depth_int64(base_value)
+        need = max(1, bit_depth_int64(base_value))  # 0 on disk would read back as v1
         if need > b.bit_depth:
             with self.mu:
                 b.bit_depth = need
