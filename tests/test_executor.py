@@ -336,3 +336,23 @@ def test_bsi_v1_fragment_upgrade():
         assert env.q1("i", "Sum(field=v)") == ValCount(sum(vals.values()), len(vals))
     finally:
         env.close()
+
+
+def test_fresh_int_field_reopen_keeps_v2_meta():
+    """A v2 int field with no writes yet has bit depth 0 on disk; reopening it
+    must not take the v1 upgrade path (base := min), which would shift every
+    later value by min and overflow at min = -2^63."""
+    env = Env()
+    try:
+        env.create_index("i")
+        env.field("i", "x", type="int", min=-(1 << 63), max=(1 << 63) - 1)
+        env.field("i", "y", type="int", min=10, max=1000)
+        env.reopen()
+        env.q("i", "Set(3, x=2000) Set(4, y=10) Set(5, y=17)")
+        assert env.q1("i", "Sum(field=x)") == ValCount(2000, 1)
+        assert env.q1("i", "Sum(field=y)") == ValCount(27, 2)
+        env.reopen()
+        assert env.q1("i", "Sum(field=x)") == ValCount(2000, 1)
+        assert env.q1("i", "Min(field=y)") == ValCount(10, 1)
+    finally:
+        env.close()
