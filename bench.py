@@ -189,6 +189,39 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
     return out
 
 
+def bench_cpu_host(args, ra, rb, nshards, nq=256):
+    """CPU stand-in for the reference (no published numbers).
+
+    Runs the same Count(Intersect(Row, Row)) queries through the host C++
+    roaring core the way the reference's executor does per shard (row
+    extraction from the fragment, then container-pair intersectionCount;
+    reference executor.go executeCount -> fragment.row ->
+    roaring IntersectionCount) on the first ``args.cpu_baseline_shards``
+    shards, single-threaded, and extrapolates to all shards.  The reference
+    runs one goroutine per shard, so ``qps_per_core`` times the host core
+    count is its ideal-scaling ceiling on that host."""
+    from pilosa_amd import _roaring
+    k = min(args.cpu_baseline_shards, nshards)
+    arena = _roaring.gen_zipf_arena(0, k, args.cols, args.rows, 8.0, 1.6, 50.0, 1, args.threads)
+    frags = [_roaring.arena_shard_bitmap(*arena, s) for s in range(k)]
+    del arena
+    w = SHARD_WIDTH
+    n = min(nq, len(ra))
+    t0 = time.perf_counter()
+    total = 0
+    for a, b in zip(ra[:n], rb[:n]):
+        a, b = int(a), int(b)
+        for f in frags:
+            r1 = f.offset_range(0, a * w, (a + 1) * w)
+            r2 = f.offset_range(0, b * w, (b + 1) * w)
+            total += r1.intersection_count(r2)
+    dt = time.perf_counter() - t0
+    per_q_all_shards = dt / n * (nshards / k)
+    return {"shards_timed": k, "queries": n, "threads": 1, "checksum": total,
+            "ms_per_query_all_shards_1core": round(per_q_all_shards * 1000, 3),
+            "qps_per_core": round(1.0 / per_q_all_shards, 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -312,6 +345,9 @@ def main():
              "mean_count": float(last.double().mean()) if last is not None else None,
              "native_compiled": compiler.native_hits, "fallback_compiled": compiler.fallbacks,
              "host_ms_per_step": {k: round(v / max(1, args.steps - 1) * 1000, 3) for k, v in tm.items()}}
+
+    if args.cpu_baseline_shards > 0 and rank == 0:
+        extra["cpu_host"] = bench_cpu_host(args, ra, rb, nshards)
 
     if args.topn_batches > 0:
         extra["topn"] = bench_topn(args, view, eng, rng, world, rank, dev)
