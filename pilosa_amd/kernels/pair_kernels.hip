@@ -36,6 +36,9 @@ namespace {
 
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr int PAIR_WAVES = 4;
+#ifndef PAIR_SMALL
+#define PAIR_SMALL 1
+#endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
@@ -315,12 +318,30 @@ __device__ __forceinline__ int runs_in_lds(const uint64_t* lb, const uint16_t* p
 // |B ∩ staged| where staged lives in lb.  Arrays use the pipelined probe
 // (34.7 -> 33.2 ms per 4096-query batch, profiles/r01_and2/kbench_b4096_pipe.log);
 // the cost-isolation builds (DBG 4 / 8) use the plain loop they modify.
+// Small arrays (n <= 2 * 64, the Zipf tail rows): one value per lane and
+// iteration.  probe_pipe() gives each lane 8 values of one 16-byte chunk, so a
+// 20-value array would run 8 LDS probe instructions on 3 lanes; here it is one
+// 2-byte load and one probe per lane (both loads issued before either probe).
+constexpr int SMALL_ARRAY_N = 128;
+template <class BM>
+__device__ __forceinline__ int probe_small(BM bm, const uint16_t* arr, int n) {
+  const int lane = lane_id();
+  const auto p = gp(arr);
+  const uint32_t v0 = lane < n ? p[lane] : 0u;
+  const uint32_t v1 = lane + 64 < n ? p[lane + 64] : 0u;
+  int c = lane < n ? int((bm[v0 >> 5] >> (v0 & 31)) & 1) : 0;
+  c += lane + 64 < n ? int((bm[v1 >> 5] >> (v1 & 31)) & 1) : 0;
+  return c;
+}
+
 template <int DBG = 0>
 __device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* p, int64_t m) {
   const int type = meta_type(m);
   if (type == CT_BITMAP) return and_bitmaps(reinterpret_cast<const ulong2*>(lb), reinterpret_cast<const uint64_t*>(p));
   if (type == CT_ARRAY) {
     if (DBG & 12) return probe<DBG>(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
+    if (PAIR_SMALL && meta_n(m) <= SMALL_ARRAY_N)
+      return probe_small(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
     return probe_pipe(reinterpret_cast<const uint32_t*>(lb), p, meta_n(m));
   }
   return runs_in_lds(lb, p);
