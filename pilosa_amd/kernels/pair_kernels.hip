@@ -318,19 +318,26 @@ __device__ __forceinline__ int runs_in_lds(const uint64_t* lb, const uint16_t* p
 // |B ∩ staged| where staged lives in lb.  Arrays use the pipelined probe
 // (34.7 -> 33.2 ms per 4096-query batch, profiles/r01_and2/kbench_b4096_pipe.log);
 // the cost-isolation builds (DBG 4 / 8) use the plain loop they modify.
-// Small arrays (n <= 2 * 64, the Zipf tail rows): one value per lane and
-// iteration.  probe_pipe() gives each lane 8 values of one 16-byte chunk, so a
-// 20-value array would run 8 LDS probe instructions on 3 lanes; here it is one
-// 2-byte load and one probe per lane (both loads issued before either probe).
-constexpr int SMALL_ARRAY_N = 128;
+// Small arrays (n <= SMALL_ARRAY_N, the Zipf tail rows): one value per lane
+// and iteration.  probe_pipe() gives each lane 8 values of one 16-byte chunk,
+// so a 20-value array would run 8 LDS probe instructions on 3 lanes; here it
+// is one 2-byte load and one probe per lane, all loads issued before the
+// probes.  Per 4096-query batch: 31.7 ms without, 29.8 (n <= 128),
+// 29.5 (256), 30.6 (512) (profiles/r01_small_probe/kbench_*.log).
+#ifndef SMALL_ARRAY_N
+#define SMALL_ARRAY_N 256
+#endif
+constexpr int SMALL_ITERS = SMALL_ARRAY_N / 64;
 template <class BM>
 __device__ __forceinline__ int probe_small(BM bm, const uint16_t* arr, int n) {
   const int lane = lane_id();
   const auto p = gp(arr);
-  const uint32_t v0 = lane < n ? p[lane] : 0u;
-  const uint32_t v1 = lane + 64 < n ? p[lane + 64] : 0u;
-  int c = lane < n ? int((bm[v0 >> 5] >> (v0 & 31)) & 1) : 0;
-  c += lane + 64 < n ? int((bm[v1 >> 5] >> (v1 & 31)) & 1) : 0;
+  uint32_t v[SMALL_ITERS];
+#pragma unroll
+  for (int k = 0; k < SMALL_ITERS; k++) v[k] = lane + 64 * k < n ? p[lane + 64 * k] : 0u;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < SMALL_ITERS; k++) c += lane + 64 * k < n ? int((bm[v[k] >> 5] >> (v[k] & 31)) & 1) : 0;
   return c;
 }
 
