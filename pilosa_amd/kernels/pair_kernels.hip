@@ -323,7 +323,8 @@ __device__ __forceinline__ int runs_in_lds(const uint64_t* lb, const uint16_t* p
 // so a 20-value array would run 8 LDS probe instructions on 3 lanes; here it
 // is one 2-byte load and one probe per lane, all loads issued before the
 // probes.  Per 4096-query batch: 31.7 ms without, 29.8 (n <= 128),
-// 29.5 (256), 30.6 (512) (profiles/r01_small_probe/kbench_*.log).
+// 29.5 (256), 29.55 (192, with the one-off gather; 256: 29.40), 30.6 (512)
+// (profiles/r01_small_probe/kbench_*.log).
 #ifndef SMALL_ARRAY_N
 #define SMALL_ARRAY_N 256
 #endif
