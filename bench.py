@@ -9,13 +9,26 @@ synthetic data generated deterministically per shard (no dataset download).
 
 A *step* is one batch of B concurrent PQL queries
 ``Count(Intersect(Row(f=a), Row(f=b)))`` with a, b drawn from the same Zipf
-law (hot rows are queried most, as in production).  The step includes PQL
-parsing + planning on the host, program upload, the batched HIP kernel over
-all local shards, the cross-GPU RCCL all-reduce of the counts and the D2H of
-the results.  With N GPUs each rank owns a contiguous 1/N of the shards
-(strong scaling: the index size is fixed).  ``value`` = total queries/sec.
+law (hot rows are queried most, as in production).  Two modes:
 
-Run: python bench.py [--gpus N --steps K --warmup W --batch B]
+* ``--mode disk`` (default): the product path.  The index is written as 954
+  Pilosa-format fragment files (one per shard) into a data dir, opened by a
+  ``Holder`` (lazy fragments), and its view is loaded from the files straight
+  into HBM (native/arena_io.cpp, ops/loader.py).  Every step is one request
+  ``Executor.execute("i", "<B Count calls>")`` through the same entry point the
+  HTTP handler uses (PQL text -> native compile -> batched HIP kernel ->
+  results); ``--clients`` request threads keep the GPU busy while the next
+  request is prepared.
+* ``--mode synthetic``: the kernel harness.  The arena is generated in memory
+  and batches go to the engine directly (no holder, no executor).
+
+Both modes re-derive a sample of the counts (64 queries x 8 shards) on the host
+roaring core and report ``verified`` in ``extra``.  With N GPUs each rank owns a
+contiguous 1/N of the shards (strong scaling: the index size is fixed) and the
+per-batch counts are summed with an RCCL all-reduce.  ``value`` = total
+queries/sec.
+
+Run: python bench.py [--gpus N --steps K --warmup W --batch B --mode disk|synthetic]
 """
 from __future__ import annotations
 
@@ -222,28 +235,44 @@ def bench_cpu_host(args, ra, rb, nshards, nq=256):
             "qps_per_core": round(1.0 / per_q_all_shards, 3)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="queries per step (concurrent queries per batch)")
-    ap.add_argument("--cols", type=int, default=TOTAL_COLS)
-    ap.add_argument("--rows", type=int, default=NROWS)
-    ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--topn-batches", type=int, default=3,
-                    help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
-    ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
-    ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
-    ap.add_argument("--topn-pairs-batches", type=int, default=1,
-                    help="also time the pair-count src TopN path on this many batches (0 = skip)")
-    ap.add_argument("--cpu-baseline-shards", type=int, default=0,
-                    help="also time the host C++ roaring executor on this many shards (extrapolated)")
-    args = ap.parse_args()
+def host_pair_counts(bitmaps, pairs):
+    """Host roaring oracle: counts[q, k] = |Row(a_q) & Row(b_q)| in shard k."""
+    w = SHARD_WIDTH
+    out = np.zeros((len(pairs), len(bitmaps)), np.int64)
+    for k, bm in enumerate(bitmaps):
+        for q, (a, b) in enumerate(pairs):
+            r1 = bm.offset_range(0, a * w, (a + 1) * w)
+            r2 = bm.offset_range(0, b * w, (b + 1) * w)
+            out[q, k] = r1.intersection_count(r2)
+    return out
 
+
+def verify_sample(eng, view, host_bitmap, pairs, answered, world, dev, nshards_check=8):
+    """Re-derive a sample of the timed batch's counts on the host: GPU
+    per-shard counts of ``pairs`` over the whole local arena vs the host
+    roaring core on ``nshards_check`` local shards, and the per-shard sums
+    (all-reduced over ranks) vs the answers the timed path returned."""
+    import torch
+    from pilosa_amd.ops.device import GpuEngine
+    S = view.S
+    pairs = [(int(a), int(b)) for a, b in pairs]
+    progs = GpuEngine.pair_programs(0, view.dense_many(np.array([a for a, _ in pairs], np.uint64)), 0,
+                                    view.dense_many(np.array([b for _, b in pairs], np.uint64)))
+    per_shard = eng.count_per_shard_progs(progs, [view], S)          # [Q, S]
+    sel = sorted(set(np.linspace(0, max(S - 1, 0), min(nshards_check, S)).astype(int).tolist())) if S else []
+    host = host_pair_counts([host_bitmap(si) for si in sel], pairs)
+    bad_shard = int((per_shard[:, sel] != host).sum()) if sel else 0
+    tot = torch.from_numpy(per_shard.sum(axis=1)).to(dev)
+    if world > 1:
+        all_reduce(tot)
+    bad_total = int((tot.cpu().numpy() != np.asarray(answered, np.int64)).sum())
+    return {"queries": len(pairs), "shards_checked": len(sel), "mismatch_shard_counts": bad_shard,
+            "mismatch_totals": bad_total, "verified": bad_shard == 0 and bad_total == 0}
+
+
+def setup_dist():
     import torch
     import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -261,7 +290,13 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     global _REHEARSE
     _REHEARSE = rehearse
-    dev = torch.device("cuda", local_rank)
+    return world, rank, torch.device("cuda", local_rank)
+
+
+def run_synthetic(args, world, rank, dev, queries, ra, rb):
+    """Kernel harness: in-memory arena, batches straight to the engine."""
+    import torch
+    import torch.distributed as dist
 
     from pilosa_amd import _roaring
     from pilosa_amd.ops.device import DeviceView, GpuEngine
@@ -280,12 +315,6 @@ def main():
     tload = time.time() - t0 - tgen
     eng = GpuEngine(dev)
     compiler = NativeCountCompiler({"f": view})
-
-    rng = np.random.default_rng(1234)
-    nq = args.batch * (args.steps + args.warmup)
-    ra = zipf_rows(rng, nq, args.rows)
-    rb = zipf_rows(rng, nq, args.rows)
-    queries = [f"Count(Intersect(Row(f={a}), Row(f={b})))" for a, b in zip(ra, rb)]
 
     def prep(i):
         # host half: PQL text -> device programs (native scanner, general
@@ -333,34 +362,241 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t
+
+    extra = {"path": "kernel harness (in-memory arena, engine direct)", "gen_s": round(tgen, 2),
+             "h2d_s": round(tload, 2), "hbm_bytes_per_gpu": view.nbytes(), "containers_per_gpu": view.container_count,
+             "shards": nshards, "mean_count": float(last.double().mean()) if last is not None else None,
+             "native_compiled": compiler.native_hits, "fallback_compiled": compiler.fallbacks,
+             "host_ms_per_step": {k: round(v / max(1, args.steps - 1) * 1000, 3) for k, v in tm.items()}}
+    if args.verify > 0:
+        b0 = (args.warmup + args.steps - 1) * args.batch
+        n = min(args.verify, args.batch)
+        pairs = list(zip(ra[b0:b0 + n], rb[b0:b0 + n]))
+
+        def host_bitmap(si):
+            return _roaring.arena_shard_bitmap(*_roaring.gen_zipf_arena(lo + si, lo + si + 1, args.cols, args.rows,
+                                                                        8.0, 1.6, 50.0, 1, args.threads), 0)
+        extra["verify"] = verify_sample(eng, view, host_bitmap, pairs, last.numpy()[:n], world, dev)
+    if args.cpu_baseline_shards > 0 and rank == 0:
+        extra["cpu_host"] = bench_cpu_host(args, ra, rb, nshards)
+    if args.topn_batches > 0:
+        extra["topn"] = bench_topn(args, view, eng, np.random.default_rng(99), world, rank, dev)
+    return elapsed, extra
+
+
+def _dir_bytes(path):
+    tot = 0
+    for root, _, files in os.walk(path):
+        for f in files:
+            try:
+                tot += os.path.getsize(os.path.join(root, f))
+            except OSError:
+                pass
+    return tot
+
+
+def run_disk(args, world, rank, dev, queries, ra, rb):
+    """Product path: Pilosa-format fragment files on disk -> Holder (lazy) ->
+    HBM via the native file loader -> Executor.execute(PQL text)."""
+    import resource
+    import shutil
+    import tempfile
+    import threading
+
+    import torch
+    import torch.distributed as dist
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.field import FieldOptions
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+
+    nshards = math.ceil(args.cols / SHARD_WIDTH)
+    lo = nshards * rank // world
+    hi = nshards * (rank + 1) // world
+    shards = list(range(lo, hi))
+    own = args.data_dir is None
+    base = tempfile.mkdtemp(prefix=f"pilosa_bench_r{rank}_", dir=os.environ.get("TMPDIR") or "/tmp") if own \
+        else os.path.join(args.data_dir, f"rank{rank}of{world}")
+    extra = {"path": "Holder(lazy) + file loader -> HBM, Executor.execute(PQL text) per request", "data_dir": base}
+    try:
+        tag = f"{args.cols}:{args.rows}:{lo}:{hi}:zipf1.6/50:8:seed1"
+        marker = os.path.join(base, ".bench_data")
+        fdir = os.path.join(base, "i", "f", "views", "standard", "fragments")
+        t0 = time.perf_counter()
+        if not (os.path.exists(marker) and open(marker).read() == tag):
+            shutil.rmtree(base, ignore_errors=True)
+            os.makedirs(base, exist_ok=True)
+            need = int(36e9 * (hi - lo) / 954 * (args.rows / NROWS))
+            free = shutil.disk_usage(base).free
+            if free < need:
+                raise SystemExit(f"bench --mode disk: {free / 1e9:.1f} GB free in {base}, need ~{need / 1e9:.1f} GB "
+                                 "(set --data-dir or use --mode synthetic)")
+            h = Holder(base).open()
+            h.create_index("i", keys=False, track_existence=True)
+            h.index("i").create_field("f", FieldOptions())
+            h.close()
+            os.makedirs(fdir, exist_ok=True)
+            w = _roaring.write_zipf_fragments(fdir, lo, hi, args.cols, args.rows, 8.0, 1.6, 50.0, 1, args.threads)
+            with open(marker, "w") as fh:
+                fh.write(tag)
+            extra["write"] = {"files": int(w["shards"]), "bytes": int(w["bytes"]), "containers": int(w["containers"]),
+                              "s": round(time.perf_counter() - t0, 2)}
+        else:
+            extra["write"] = {"reused": True, "bytes": _dir_bytes(fdir)}
+        t1 = time.perf_counter()
+        holder = Holder(base, lazy_fragments=True).open()
+        t2 = time.perf_counter()
+        gpu = GpuExecutor(holder, dev)
+        ex = Executor(holder, gpu=gpu)
+        ex.strict_gpu = True  # a device fault fails the bench instead of timing the host path
+        view = gpu.view_arena("i", "f", "standard", shards)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        extra.update({"holder_open_s": round(t2 - t1, 2), "load_s": round(t3 - t2, 2), "load": gpu.last_load,
+                      "hbm_bytes_per_gpu": view.nbytes(), "containers_per_gpu": int(view.container_count),
+                      "cold_loads": gpu.cold_loads, "shards": nshards,
+                      "fragments_cold_after_load": sum(f.is_cold() for f in holder.view("i", "f", "standard")
+                                                       .all_fragments())})
+        assert holder.index("i").available_shards() == shards, "holder must serve exactly this rank's shards"
+
+        texts = [" ".join(queries[i * args.batch:(i + 1) * args.batch]) for i in range(args.warmup + args.steps)]
+        results = [None] * len(texts)
+        lock = threading.Lock()
+        nxt = [0]
+        err = []
+
+        def client(end):
+            while True:
+                with lock:
+                    i = nxt[0]
+                    if i >= end or err:
+                        return
+                    nxt[0] += 1
+                try:
+                    results[i] = ex.execute("i", texts[i], shards=shards).results
+                except BaseException as e:  # noqa: BLE001
+                    err.append(e)
+                    return
+
+        def run(first, n):
+            nxt[0] = first
+            ts = [threading.Thread(target=client, args=(first + n,)) for _ in range(max(1, args.clients))]
+            for t in ts:
+                t.start()
+            # ranks all-reduce each request's counts in request order (one
+            # collective per batch, issued from this thread only)
+            for i in range(first, first + n):
+                if world > 1:
+                    while results[i] is None and not err:
+                        time.sleep(0.0002)
+                    if err:
+                        break
+                    tt = torch.tensor(results[i], dtype=torch.int64, device=dev)
+                    all_reduce(tt)
+                    results[i] = tt.cpu().tolist()
+            for t in ts:
+                t.join()
+            if err:
+                raise err[0]
+
+        n0 = gpu.launches
+        run(0, args.warmup)
+        assert gpu.launches > n0, "requests did not reach the device"
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        run(args.warmup, args.steps)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t
+        last = results[args.warmup + args.steps - 1]
+        extra.update({"clients": args.clients, "mean_count": float(np.mean(last)), "launches": gpu.launches - n0,
+                      "gpu_faults": ex.gpu_faults, "peak_host_rss_gb":
+                      round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)})
+        if args.verify > 0:
+            b0 = (args.warmup + args.steps - 1) * args.batch
+            n = min(args.verify, args.batch)
+            pairs = list(zip(ra[b0:b0 + n], rb[b0:b0 + n]))
+
+            def host_bitmap(si):
+                with open(os.path.join(fdir, str(shards[si])), "rb") as fh:
+                    return _roaring.Bitmap.from_bytes(fh.read())
+            extra["verify"] = verify_sample(gpu.engine, view, host_bitmap, pairs, last[:n], world, dev)
+        if args.topn_batches > 0:
+            extra["topn"] = bench_topn(args, view, gpu.engine, np.random.default_rng(99), world, rank, dev)
+        holder.close()
+        return elapsed, extra
+    finally:
+        if own and not args.keep_data:
+            shutil.rmtree(base, ignore_errors=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="queries per step (concurrent queries per batch)")
+    ap.add_argument("--mode", choices=("disk", "synthetic"), default=os.environ.get("PILOSA_BENCH_MODE", "disk"))
+    ap.add_argument("--cols", type=int, default=TOTAL_COLS)
+    ap.add_argument("--rows", type=int, default=NROWS)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--clients", type=int, default=2, help="disk mode: concurrent request threads")
+    ap.add_argument("--data-dir", default=None, help="disk mode: reuse/keep fragment files under this dir")
+    ap.add_argument("--keep-data", action="store_true")
+    ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")
+    ap.add_argument("--topn-batches", type=int, default=3,
+                    help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
+    ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
+    ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
+    ap.add_argument("--topn-pairs-batches", type=int, default=1,
+                    help="also time the pair-count src TopN path on this many batches (0 = skip)")
+    ap.add_argument("--cpu-baseline-shards", type=int, default=0,
+                    help="also time the host C++ roaring executor on this many shards (extrapolated)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world, rank, dev = setup_dist()
+    rng = np.random.default_rng(1234)
+    nq = args.batch * (args.steps + args.warmup)
+    ra = zipf_rows(rng, nq, args.rows)
+    rb = zipf_rows(rng, nq, args.rows)
+    queries = [f"Count(Intersect(Row(f={a}), Row(f={b})))" for a, b in zip(ra, rb)]
+
+    run = run_disk if args.mode == "disk" else run_synthetic
+    elapsed, extra = run(args, world, rank, dev, queries, ra, rb)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms = elapsed / args.steps * 1000.0
     qps = args.batch * args.steps / elapsed
-
-    extra = {"gen_s": round(tgen, 2), "h2d_s": round(tload, 2), "hbm_bytes_per_gpu": view.nbytes(),
-             "containers_per_gpu": view.container_count, "shards": nshards,
-             "mean_count": float(last.double().mean()) if last is not None else None,
-             "native_compiled": compiler.native_hits, "fallback_compiled": compiler.fallbacks,
-             "host_ms_per_step": {k: round(v / max(1, args.steps - 1) * 1000, 3) for k, v in tm.items()}}
-
-    if args.cpu_baseline_shards > 0 and rank == 0:
-        extra["cpu_host"] = bench_cpu_host(args, ra, rb, nshards)
-
-    if args.topn_batches > 0:
-        extra["topn"] = bench_topn(args, view, eng, rng, world, rank, dev)
+    if "verify" in extra:
+        ok = torch.tensor([0 if extra["verify"]["verified"] else 1], dtype=torch.int64, device=dev)
+        if world > 1:
+            all_reduce(ok)
+        extra["verify"]["verified_all_ranks"] = int(ok.item()) == 0
 
     if rank == 0:
-        rec = {"metric": "PQL queries/sec (Count(Intersect(Row,Row))) on 1M-row x 1B-col set field",
+        nshards = math.ceil(args.cols / SHARD_WIDTH)
+        size = f"{args.rows / 1e6:g}M-row x {args.cols / 1e9:g}B-col"
+        rec = {"metric": f"PQL queries/sec (Count(Intersect(Row,Row))) on {size} set field",
                "value": round(qps, 2), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "bitmap(u64 words)",
-               "data": "synthetic (zipf s=1.6 v=50 rows, 8 bits/column, deterministic per shard)",
-               "config": {"model": "set field f, 1M rows x 1B cols (954 shards)", "global_batch": args.batch,
-                          "seq_len": args.cols, "parallelism": f"shard-range x{world} + RCCL all-reduce"},
-               "extra": extra}
+               "data": "synthetic (zipf s=1.6 v=50 rows, 8 bits/column, deterministic per shard)"
+                       + ("; written as Pilosa fragment files and loaded from disk" if args.mode == "disk" else ""),
+               "config": {"model": f"set field f, {size} ({nshards} shards)", "global_batch": args.batch,
+                          "seq_len": args.cols,
+                          "parallelism": f"shard-range x{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+               "verified": extra.get("verify", {}).get("verified_all_ranks"),
+               "mode": args.mode, "extra": extra}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

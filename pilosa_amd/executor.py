@@ -190,6 +190,9 @@ def merge_group_counts(a: List[GroupCount], b: List[GroupCount], limit: int) -> 
 
 
 GPU_FAULT_LIMIT = int(os.environ.get("PILOSA_GPU_FAULT_LIMIT", "3"))
+# process-wide count of device faults answered from the host (tests assert
+# that a device-routed query never took this path)
+DEVICE_FAULTS = [0]
 
 
 def _results_equal(a, b) -> bool:
@@ -220,6 +223,9 @@ class Executor:
         # compared (the reference's roaringparanoia build tag, for the GPU path)
         self.paranoia = os.environ.get("PILOSA_PARANOIA", "0") == "1"
         self.gpu_faults = 0
+        # strict: a device fault raises instead of falling back to the host
+        # fragments (also PILOSA_GPU_STRICT=1; tests: the device must answer)
+        self.strict_gpu = False
         self.logger = None
         self._coalescer = None
         self.max_writes = max_writes
@@ -234,6 +240,9 @@ class Executor:
                 opt: Optional[ExecOptions] = None) -> QueryResponse:
         with tracing.span("Executor.Execute"):
             if isinstance(q, str):
+                fast = self._count_text_fast(index, q, shards, opt)
+                if fast is not None:
+                    return QueryResponse(fast)
                 q = parse_string(q)
             if not index:
                 raise ErrIndexRequired
@@ -266,6 +275,43 @@ class Executor:
             if not opt.remote:
                 resp.results = [self._translate_result(index, idx, c, r) for c, r in zip(q.calls, results)]
             return resp
+
+    # requests of at least this many Count() calls try the native text path
+    COUNT_TEXT_MIN = int(os.environ.get("PILOSA_COUNT_TEXT_MIN", "2"))
+
+    def _count_text_fast(self, index: str, text: str, shards, opt: Optional[ExecOptions]) -> Optional[List[int]]:
+        """Serving fast path for a request that is only Count(<Row/set-op
+        tree>) calls over local shards: the PQL text is compiled natively
+        straight to device programs (no Python AST; native/pql_compile.cpp)
+        and answered in one launch.  None = use the general path (which also
+        produces every error the reference would)."""
+        gpu = self.gpu
+        if gpu is None or (opt is not None and (opt.remote or opt.column_attrs)):
+            return None
+        head = text.lstrip()[:6]
+        if head != "Count(" and head != "Count ":
+            return None
+        if text.count("Count") < self.COUNT_TEXT_MIN:
+            return None
+        idx = self.holder.index(index)
+        if idx is None:
+            return None
+        shards = list(shards) if shards else (idx.available_shards() or [0])
+        if self._has_remote(index, shards, opt or ExecOptions()):
+            return None
+        fn = getattr(gpu, "try_count_text", None)
+        if fn is None:
+            return None
+        try:
+            res = fn(index, text, shards)
+        except PilosaError:
+            raise
+        except Exception as err:  # noqa: BLE001 - device fault: general path
+            self._gpu_fault(err)
+            return None
+        if res is not None and self.stats is not None:
+            self.stats.count_with_tags("Count", len(res), [f"index:{index}"])
+        return res
 
     def _execute(self, index: str, q: Query, shards: List[int], opt: ExecOptions) -> List[Any]:
         needs = any(c.name not in ("Clear", "Set", "SetRowAttrs", "SetColumnAttrs") for c in q.calls)
@@ -310,7 +356,13 @@ class Executor:
             return self.mesh.count_batch(index, list(calls), list(shards))
         if self.gpu is None:
             return None
-        return self.gpu.try_count_batch(index, list(calls), list(shards))
+        try:
+            return self.gpu.try_count_batch(index, list(calls), list(shards))
+        except PilosaError:
+            raise
+        except Exception as err:  # noqa: BLE001 - counted; each call then runs alone
+            self._gpu_fault(err)
+            return None
 
     def _has_remote(self, index, shards, opt) -> bool:
         if self.cluster is None or opt.remote:
@@ -490,6 +542,9 @@ class Executor:
         self.gpu_faults += 1
         if self.stats is not None:
             self.stats.count("gpuFault", 1)
+        DEVICE_FAULTS[0] += 1
+        if self.strict_gpu or os.environ.get("PILOSA_GPU_STRICT", "0") == "1":
+            raise err
         if self.logger is not None:
             self.logger.printf("gpu fault %d (%s: %s), answering from host fragments", self.gpu_faults,
                                type(err).__name__, err)

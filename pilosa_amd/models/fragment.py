@@ -91,12 +91,19 @@ class Fragment:
         self.max_opn = max_opn
         self.mutex = mutex
         self.bool_field = bool_field
-        self.storage = Bitmap()
-        self.cache = new_cache(cache_type, cache_size)
+        self._storage = Bitmap()
+        self._cache = new_cache(cache_type, cache_size)
         self.checksums: Dict[int, bytes] = {}
         self.opn = 0
         self.ops = 0
-        self.max_row_id = 0
+        self._max_row_id = 0
+        # lazy open: the file is only validated by its header; the storage (and
+        # the rank cache that needs its counts) is read on first host access.
+        # A GPU node reads cold fragments straight into HBM instead
+        # (native/arena_io.cpp), so the host never holds their containers.
+        self.lazy = False
+        self._flags_hint = 0
+        self._cache_pending = False
         self.version = 0
         _bump_epoch()
         # per-consumer dirty-row sets (device arenas patch only changed rows);
@@ -112,20 +119,86 @@ class Fragment:
     def open(self):
         with self.mu:
             self._open_storage()
-            self._open_cache()
+            if self._storage is None:
+                self._cache_pending = self.cache_type != CACHE_TYPE_NONE
+            else:
+                self._open_cache()
         return self
+
+    # ------------------------------------------------------------ lazy storage
+    @property
+    def storage(self):
+        s = self._storage
+        if s is None:
+            s = self._load_cold()
+        return s
+
+    @storage.setter
+    def storage(self, bm):
+        self._storage = bm
+        self._cache_pending = False
+
+    @property
+    def cache(self):
+        if self._cache_pending:
+            self._load_cold()
+        return self._cache
+
+    @cache.setter
+    def cache(self, c):
+        self._cache = c
+
+    @property
+    def max_row_id(self) -> int:
+        if self._storage is None:
+            self._load_cold()
+        return self._max_row_id
+
+    @max_row_id.setter
+    def max_row_id(self, v: int):
+        self._max_row_id = v
+
+    def is_cold(self) -> bool:
+        """True while the storage has not been read from the file (the file
+        is exactly the fragment's state: any write loads it first)."""
+        return self._storage is None
+
+    def _read_storage(self) -> Bitmap:
+        with open(self.path, "rb") as fh:
+            data = fh.read()
+        try:
+            return Bitmap.from_bytes(data)
+        except Exception as e:  # noqa: BLE001
+            raise PilosaError(f"unmarshal storage: file={self.path}, err={e}")
+
+    def _load_cold(self) -> Bitmap:
+        with self.mu:
+            if self._storage is None:
+                bm = self._read_storage()
+                self.opn = int(bm.opn)
+                self.ops = int(bm.ops)
+                self._storage = bm
+                self._max_row_id = int(bm.max()) // SHARD_WIDTH if bm.any() else 0
+            if self._cache_pending:
+                self._cache_pending = False
+                self._open_cache()
+            return self._storage
 
     def _open_storage(self):
         os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
         if os.path.exists(self.path) and os.path.getsize(self.path) > 0:
-            with open(self.path, "rb") as fh:
-                data = fh.read()
-            try:
-                self.storage = Bitmap.from_bytes(data)
-            except Exception as e:  # noqa: BLE001
-                raise PilosaError(f"unmarshal storage: file={self.path}, err={e}")
-            self.opn = int(self.storage.opn)
-            self.ops = int(self.storage.ops)
+            if self.lazy:
+                with open(self.path, "rb") as fh:
+                    head = fh.read(8)
+                if len(head) < 8:
+                    raise PilosaError(f"unmarshal storage: file={self.path}, err=data too small")
+                self._flags_hint = head[3] if int.from_bytes(head[:2], "little") == _roaring.MAGIC else 0
+                self._storage = None
+            else:
+                bm = self._read_storage()
+                self._storage = bm
+                self.opn = int(bm.opn)
+                self.ops = int(bm.ops)
         else:
             self.storage = Bitmap()
             # new fragments start with a valid empty snapshot (BSI v2 flag)
@@ -137,7 +210,8 @@ class Fragment:
             fcntl.flock(self._fh.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
         except OSError as e:
             raise PilosaError(f"flock: {e}")
-        self.max_row_id = int(self.storage.max()) // SHARD_WIDTH if self.storage.any() else 0
+        if self._storage is not None:
+            self._max_row_id = int(self._storage.max()) // SHARD_WIDTH if self._storage.any() else 0
         self._bump()
 
     def _bump(self):
@@ -150,6 +224,7 @@ class Fragment:
     def _open_cache(self):
         if self.cache_type == CACHE_TYPE_NONE:
             return
+        self._cache_pending = False
         p = self.cache_path()
         if not os.path.exists(p):
             return
@@ -160,14 +235,15 @@ class Fragment:
                 m.ParseFromString(fh.read())
         except Exception:  # noqa: BLE001 - a corrupt cache is rebuilt
             return
+        st = self.storage
         for rid in m.IDs:
-            n = self.storage.count_range(rid * SHARD_WIDTH, (rid + 1) * SHARD_WIDTH)
-            self.cache.bulk_add(rid, n)
-        self.cache.invalidate()
+            n = st.count_range(rid * SHARD_WIDTH, (rid + 1) * SHARD_WIDTH)
+            self._cache.bulk_add(rid, n)
+        self._cache.invalidate()
 
     def flush_cache(self):
-        if self.cache_type == CACHE_TYPE_NONE:
-            return
+        if self.cache_type == CACHE_TYPE_NONE or self._storage is None or self._cache_pending:
+            return  # cold fragment: the cache file on disk is current
         from pilosa_amd.wire import pb
         with self.mu:
             ids = self.cache.ids()
@@ -244,6 +320,8 @@ class Fragment:
         ``bitDepth``; v2 has exists=0, sign=1 and the planes from row 2.
         Returns True when the fragment was rewritten."""
         with self.mu:
+            if self._storage is None and self._flags_hint & ROARING_FLAG_BSI_V2:
+                return False
             if self.storage.flags & ROARING_FLAG_BSI_V2:
                 return False
             vals = self.storage.slice()

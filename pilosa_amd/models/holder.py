@@ -24,8 +24,12 @@ CACHE_FLUSH_INTERVAL_S = 60.0
 
 
 class Holder:
-    def __init__(self, path: str, max_opn: int = 10000, stats=None, persistent_attrs: bool = True):
+    def __init__(self, path: str, max_opn: int = 10000, stats=None, persistent_attrs: bool = True,
+                 lazy_fragments: bool = False):
         self.path = path
+        # open fragments by header only; storage is read on first host use
+        # (a GPU node loads cold fragments straight into HBM, ops/loader.py)
+        self.lazy_fragments = lazy_fragments
         self.indexes: Dict[str, Index] = {}
         self.max_opn = max_opn
         self.stats = stats
@@ -118,6 +122,7 @@ class Holder:
                     max_opn=self.max_opn, stats=self.stats, persistent_attrs=self.persistent_attrs)
         idx.on_create_shard = self._index_created_shard
         idx.snapshot_queue = self.snapshot_queue
+        idx.lazy_fragments = self.lazy_fragments
         return idx
 
     def _index_created_shard(self, idx, field, shard):

@@ -90,6 +90,7 @@ class Index:
                   persistent_attrs=self.persistent_attrs)
         f.on_create_shard = self._field_created_shard
         f.snapshot_queue = getattr(self, "snapshot_queue", None)
+        f.lazy_fragments = getattr(self, "lazy_fragments", False)
         return f
 
     def _field_created_shard(self, field: Field, shard: int):

@@ -48,6 +48,7 @@ class View:
                         stats=f.stats if f is not None else None)
         frag.row_attr_store = f.row_attr_store if f is not None else None
         frag.snapshot_queue = getattr(f, "snapshot_queue", None)
+        frag.lazy = bool(getattr(f, "lazy_fragments", False))
         return frag
 
     def open(self):

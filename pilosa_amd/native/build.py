@@ -35,8 +35,8 @@ def build_roaring(force: bool = False, verbose: bool = False) -> str:
     import pybind11
 
     out = os.path.join(PKG, "_roaring" + _ext_suffix())
-    srcs = [os.path.join(HERE, "roaring.cpp"), os.path.join(HERE, "pyroaring.cpp")]
-    deps = srcs + [os.path.join(HERE, "roaring.hpp")]
+    srcs = [os.path.join(HERE, f) for f in ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp")]
+    deps = srcs + [os.path.join(HERE, f) for f in ("roaring.hpp", "synth.hpp")]
     if not force and not _newer(out, deps):
         return out
     cxx = os.environ.get("CXX", "g++")

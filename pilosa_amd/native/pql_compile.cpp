@@ -20,6 +20,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cctype>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -68,10 +69,18 @@ class Compiler {
  public:
   Compiler(std::string_view s, const std::unordered_map<std::string, int>& fields, const std::vector<View>& views,
            QueryProg& out)
-      : s_(s), fields_(fields), views_(views), out_(out) {}
+      : s_(s), fields_(fields), views_(views), outp_(&out) {}
 
   bool run() {
-    std::memset(&out_, 0, sizeof(out_));
+    if (!call()) return false;
+    ws();
+    return i_ == s_.size();
+  }
+
+  // One `Count(<expr>)` call starting at pos(); leaves the cursor after it.
+  bool call() {
+    std::memset(outp_, 0, sizeof(QueryProg));
+    nleaf_ = nprog_ = depth_ = 0;
     ws();
     if (!word("Count")) return false;
     ws();
@@ -80,11 +89,17 @@ class Compiler {
     if (!expr()) return false;
     ws();
     if (!ch(')')) return false;
-    ws();
-    if (i_ != s_.size()) return false;
-    out_.nleaf = nleaf_;
-    out_.nprog = nprog_;
+    outp_->nleaf = nleaf_;
+    outp_->nprog = nprog_;
     return true;
+  }
+
+  size_t pos() const { return i_; }
+  void seek(size_t i) { i_ = i; }
+  void retarget(QueryProg* out) { outp_ = out; }
+  bool at_end() {
+    ws();
+    return i_ >= s_.size();
   }
 
  private:
@@ -92,7 +107,7 @@ class Compiler {
   size_t i_ = 0;
   const std::unordered_map<std::string, int>& fields_;
   const std::vector<View>& views_;
-  QueryProg& out_;
+  QueryProg* outp_;
   int nleaf_ = 0, nprog_ = 0, depth_ = 0;
 
   void ws() {
@@ -115,7 +130,7 @@ class Compiler {
   }
   bool emit(uint8_t code) {
     if (nprog_ >= MAXPROG) return false;
-    out_.prog[nprog_++] = code;
+    outp_->prog[nprog_++] = code;
     return true;
   }
 
@@ -147,12 +162,12 @@ class Compiler {
     const int64_t d = views_[slot].dense(row);
     int k = -1;
     for (int x = 0; x < nleaf_; x++)
-      if (out_.leaf_view[x] == slot && out_.leaf_row[x] == d) k = x;
+      if (outp_->leaf_view[x] == slot && outp_->leaf_row[x] == d) k = x;
     if (k < 0) {
       if (nleaf_ >= MAXLEAF) return false;
       k = nleaf_++;
-      out_.leaf_view[k] = slot;
-      out_.leaf_row[k] = d;
+      outp_->leaf_view[k] = slot;
+      outp_->leaf_row[k] = d;
     }
     if (++depth_ > MAXDEPTH) return false;
     return emit(uint8_t(k));
@@ -212,9 +227,78 @@ py::tuple compile_counts(const std::vector<std::string>& queries, const std::uno
   return py::make_tuple(progs, ok);
 }
 
+// compile_count_text(text, fields, dirs) -> (progs uint8[Q*256], Q) or None.
+// `text` is a whole request of top-level Count() calls ("Count(..) Count(..)");
+// None when any call is outside the subset (the caller parses generally).
+py::object compile_count_text(const std::string& text, const std::unordered_map<std::string, int>& fields,
+                              const std::vector<py::array_t<uint64_t, py::array::c_style | py::array::forcecast>>& dirs) {
+  std::vector<View> views;
+  views.reserve(dirs.size());
+  for (const auto& d : dirs) {
+    View v;
+    v.rows = d.data();
+    v.D = d.size();
+    v.identity = v.D > 0 && v.rows[v.D - 1] == uint64_t(v.D - 1);
+    views.push_back(v);
+  }
+  for (const auto& kv : fields)
+    if (kv.second < 0 || kv.second >= int(views.size())) throw std::out_of_range("field slot out of range");
+  std::vector<QueryProg> out;
+  bool ok = true;
+  {
+    py::gil_scoped_release nogil;
+    out.reserve(text.size() / 40 + 1);
+    QueryProg tmp;
+    Compiler c(text, fields, views, tmp);
+    while (!c.at_end()) {
+      out.emplace_back();
+      c.retarget(&out.back());
+      if (!c.call()) {
+        ok = false;
+        break;
+      }
+    }
+    ok = ok && !out.empty();
+  }
+  if (!ok) return py::none();
+  const size_t Q = out.size();
+  py::array_t<uint8_t> progs(Q * sizeof(QueryProg));
+  std::memcpy(progs.mutable_data(), out.data(), Q * sizeof(QueryProg));
+  return py::make_tuple(progs, Q);
+}
+
+// Field names of the Row(field=...) leaves of a request (distinct, first-seen
+// order); views for them are resolved before compile_count_text.
+std::vector<std::string> count_text_fields(const std::string& text) {
+  std::vector<std::string> out;
+  const size_t n = text.size();
+  for (size_t i = 0; i + 4 < n; i++) {
+    if (text[i] != 'R' || text.compare(i, 3, "Row") != 0) continue;
+    if (i > 0 && (std::isalnum(static_cast<unsigned char>(text[i - 1])) || text[i - 1] == '_')) continue;
+    size_t j = i + 3;
+    while (j < n && (text[j] == ' ' || text[j] == '\t' || text[j] == '\n' || text[j] == '\r')) j++;
+    if (j >= n || text[j] != '(') continue;
+    j++;
+    while (j < n && (text[j] == ' ' || text[j] == '\t' || text[j] == '\n' || text[j] == '\r')) j++;
+    const size_t f0 = j;
+    while (j < n && (std::isalnum(static_cast<unsigned char>(text[j])) || text[j] == '_' || text[j] == '-')) j++;
+    if (j == f0) continue;
+    std::string f = text.substr(f0, j - f0);
+    bool seen = false;
+    for (const auto& x : out) seen = seen || x == f;
+    if (!seen) out.push_back(std::move(f));
+    i = j;
+  }
+  return out;
+}
+
 }  // namespace
 
 void register_compile(py::module_& m) {
+  m.def("compile_count_text", &compile_count_text, py::arg("text"), py::arg("fields"), py::arg("dirs"),
+        "Compile a request of top-level Count(<Row/Intersect/Union/Difference/Xor tree>) calls straight to "
+        "QueryProg records; (progs uint8[Q*256], Q), or None when a call needs the general path");
+  m.def("count_text_fields", &count_text_fields, py::arg("text"));
   m.def("compile_counts", &compile_counts, py::arg("queries"), py::arg("fields"), py::arg("dirs"),
         "Compile Count(<Row/Intersect/Union/Difference/Xor tree>) PQL strings straight to QueryProg records; "
         "returns (progs uint8[Q*256], ok bool[Q]) -- rows with ok=False need the general path");

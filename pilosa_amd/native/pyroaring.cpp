@@ -28,6 +28,7 @@
 #include <thread>
 
 #include "roaring.hpp"
+#include "synth.hpp"
 
 namespace py = pybind11;
 using pr::Bitmap;
@@ -187,80 +188,10 @@ static Bitmap bitmap_from_containers(py::array_t<uint64_t> keys, py::array_t<uin
 
 
 // ------------------------------------------------------------------ synthetic data
-// Deterministic synthetic set-field generator writing the device arena layout
-// directly (no host Bitmaps), used by bench.py for the 1M-row x 1B-column
-// config.  Row r has column density d_r = min(1, bits_per_col * (v+r)^-s / Z),
-// Z = sum_k (v+k)^-s, i.e. the reference's Zipf(s=1.6, v=50) row generator
-// (fragment_internal_test.go:2377-2460) drawn bits_per_col times per column.
-// Sparse row-shards draw Poisson(d_r * cols) uniform positions; dense ones draw
-// a per-container count and place it stratified (distinct, sorted).
-namespace {
-struct Rng {
-  uint64_t s;
-  explicit Rng(uint64_t seed) : s(seed) {}
-  uint64_t next() {
-    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-  }
-  double uni() { return double(next() >> 11) * (1.0 / 9007199254740992.0); }
-  int64_t poisson(double lam) {
-    if (lam <= 0) return 0;
-    if (lam < 30) {
-      double L = std::exp(-lam), p = 1.0;
-      int64_t k = 0;
-      do { k++; p *= uni(); } while (p > L);
-      return k - 1;
-    }
-    double u1 = std::max(uni(), 1e-300), u2 = uni();
-    double z = std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
-    int64_t k = int64_t(std::llround(lam + std::sqrt(lam) * z));
-    return k < 0 ? 0 : k;
-  }
-};
-inline uint64_t mix3(uint64_t a, uint64_t b, uint64_t c) {
-  Rng r(a * 0x100000001B3ull ^ (b << 21) ^ (c * 0xD6E8FEB86659FD93ull));
-  r.next();
-  return r.next();
-}
-}  // namespace
-
-// One shard of a synthetic arena (rowptr relative, meta payload offsets relative to the shard).
-struct ShardOut {
-  std::vector<uint32_t> rowptr;
-  std::vector<int64_t> meta;
-  std::vector<uint16_t> payload;
-  // n values sorted distinct (vals) or bitmap words (w) when n > 4096
-  void emit(int j, const uint16_t* vals, int n, const uint64_t* w) {
-    const int64_t off = int64_t(payload.size());
-    int type;
-    if (n <= pr::ARRAY_MAX) {
-      type = pr::CT_ARRAY;
-      payload.insert(payload.end(), vals, vals + n);
-      payload.resize((payload.size() + 7) & ~size_t(7), 0);
-    } else {
-      type = pr::CT_BITMAP;
-      const uint16_t* p = reinterpret_cast<const uint16_t*>(w);
-      payload.insert(payload.end(), p, p + 4096);
-    }
-    meta.push_back(int64_t(uint64_t(j) | (uint64_t(type) << 4) | (uint64_t(n) << 6) | (uint64_t(off / 8) << 23)));
-  }
-  // emit a container from bitmap words (array when sparse)
-  void emit_words(int j, const uint64_t* w, std::vector<uint16_t>& tmp) {
-    int n = 0;
-    for (int i = 0; i < 1024; i++) n += __builtin_popcountll(w[i]);
-    if (n == 0) return;
-    if (n > pr::ARRAY_MAX) {
-      emit(j, nullptr, n, w);
-      return;
-    }
-    tmp.clear();
-    for (int i = 0; i < 1024; i++)
-      for (uint64_t b = w[i]; b; b &= b - 1) tmp.push_back(uint16_t(i * 64 + __builtin_ctzll(b)));
-    emit(j, tmp.data(), n, nullptr);
-  }
-};
+// Generator and per-shard arena builder: synth.hpp.
+using synth::Rng;
+using synth::ShardOut;
+using synth::mix3;
 
 // Concatenate per-shard outputs into (rows, rowptr[S][R+1], shard_base, meta, payload).
 static py::tuple concat_arena(std::vector<ShardOut>& outs, const std::vector<uint64_t>& rows, int nthreads) {
@@ -317,68 +248,8 @@ static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t tota
                                 double bits_per_col, double zs, double zv, uint64_t seed, int nthreads) {
   const int64_t S = shard_hi - shard_lo;
   const int64_t R = nrows;
-  std::vector<double> dens(R);
-  {
-    double Z = 0;
-    for (int64_t r = 0; r < R; r++) Z += std::pow(zv + double(r), -zs);
-    for (int64_t r = 0; r < R; r++) dens[r] = std::min(1.0, bits_per_col * std::pow(zv + double(r), -zs) / Z);
-  }
+  const std::vector<double> dens = synth::zipf_densities(R, bits_per_col, zs, zv);
   std::vector<ShardOut> outs(S);
-  auto work = [&](int64_t s0, int64_t s1) {
-    std::vector<uint64_t> pos;
-    std::vector<uint64_t> words(1024);
-    for (int64_t si = s0; si < s1; si++) {
-      const int64_t shard = shard_lo + si;
-      const int64_t cols = std::max<int64_t>(0, std::min<int64_t>(1 << 20, total_cols - shard * (1 << 20)));
-      ShardOut& o = outs[si];
-      o.rowptr.assign(R + 1, 0);
-      auto emit = [&](int j, const uint16_t* vals, int n, const uint64_t* w) { o.emit(j, vals, n, w); };
-      std::vector<uint16_t> vals;
-      for (int64_t r = 0; r < R; r++) {
-        o.rowptr[r] = uint32_t(o.meta.size());
-        if (cols == 0) continue;
-        Rng rng(mix3(seed, uint64_t(shard), uint64_t(r)));
-        const double lam_row = dens[r] * double(cols);
-        if (lam_row < 2048.0) {
-          int64_t N = rng.poisson(lam_row);
-          if (N == 0) continue;
-          pos.resize(N);
-          for (int64_t k = 0; k < N; k++) pos[k] = rng.next() % uint64_t(cols);
-          std::sort(pos.begin(), pos.end());
-          pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
-          size_t i = 0;
-          while (i < pos.size()) {
-            int j = int(pos[i] >> 16);
-            vals.clear();
-            while (i < pos.size() && int(pos[i] >> 16) == j) vals.push_back(uint16_t(pos[i] & 0xffff)), i++;
-            emit(j, vals.data(), int(vals.size()), nullptr);
-          }
-        } else {
-          for (int j = 0; j < 16; j++) {
-            const int64_t lim = std::min<int64_t>(65536, cols - int64_t(j) * 65536);
-            if (lim <= 0) break;
-            int64_t n = dens[r] >= 1.0 ? lim : rng.poisson(dens[r] * double(lim));
-            n = std::min<int64_t>(n, lim);
-            if (n == 0) continue;
-            // stratified distinct positions
-            vals.resize(n);
-            for (int64_t k = 0; k < n; k++) {
-              int64_t a = k * lim / n, b = (k + 1) * lim / n;
-              vals[k] = uint16_t(a + int64_t(rng.next() % uint64_t(std::max<int64_t>(1, b - a))));
-            }
-            if (n > pr::ARRAY_MAX) {
-              std::fill(words.begin(), words.end(), 0);
-              for (int64_t k = 0; k < n; k++) words[vals[k] >> 6] |= 1ull << (vals[k] & 63);
-              emit(j, nullptr, int(n), words.data());
-            } else {
-              emit(j, vals.data(), int(n), nullptr);
-            }
-          }
-        }
-      }
-      o.rowptr[R] = uint32_t(o.meta.size());
-    }
-  };
   {
     py::gil_scoped_release nogil;
     int nt = std::max<int>(1, std::min<int64_t>(nthreads, S));
@@ -389,7 +260,7 @@ static py::tuple gen_zipf_arena(int64_t shard_lo, int64_t shard_hi, int64_t tota
         for (;;) {
           int64_t s = next.fetch_add(1);
           if (s >= S) break;
-          work(s, s + 1);
+          synth::gen_zipf_shard(outs[s], shard_lo + s, total_cols, dens, seed);
         }
       });
     for (auto& t : th) t.join();
@@ -607,6 +478,8 @@ static py::tuple topn_replay(I64Arr cand_rows, I64Arr cand_cnts,
   return py::make_tuple(need, ids, cnts);
 }
 
+void register_arena_io(py::module_& m);  // arena_io.cpp
+
 PYBIND11_MODULE(_roaring, m) {
   m.doc() = "Host roaring core (containers, pilosa file format, op log, device arena builder)";
   m.attr("ARRAY_MAX") = pr::ARRAY_MAX;
@@ -819,4 +692,5 @@ PYBIND11_MODULE(_roaring, m) {
         py::arg("nrows"), py::arg("bits_per_col") = 8.0, py::arg("zipf_s") = 1.6, py::arg("zipf_v") = 50.0,
         py::arg("seed") = 1, py::arg("nthreads") = 8);
   m.def("arena_shard_bitmap", &arena_shard_bitmap);
+  register_arena_io(m);
 }

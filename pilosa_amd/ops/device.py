@@ -413,6 +413,38 @@ class DeviceView:
         return self
 
     @classmethod
+    def from_host_index(cls, rows, rowptr, shard_base, meta, t_payload, payload_used: int, device, shards,
+                        cap=None) -> "DeviceView":
+        """Wrap an arena index built on the host (ops/loader.py) around an
+        already uploaded payload; ``cap`` (per-shard metadata capacity) makes
+        the view patchable, the host index arrays then stay as its mirrors."""
+        import torch
+
+        self = cls.__new__(cls)
+        self.device = torch.device(device)
+        self.rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        self.S = int(rowptr.shape[0])
+        self.D = int(self.rows.shape[0])
+        self.shards = list(shards) if shards else list(range(self.S))
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.uint32).reshape(self.S, self.D + 1)
+        self.t_rowptr = torch.from_numpy(rowptr.view(np.int32).reshape(-1)).to(self.device)
+        self.t_shard_base = torch.from_numpy(np.ascontiguousarray(shard_base, dtype=np.int64)).to(self.device)
+        self.t_meta = torch.from_numpy(np.ascontiguousarray(meta, dtype=np.int64)).to(self.device)
+        self.t_payload = t_payload
+        self.container_count = int(shard_base[-1])
+        self._row_index = None
+        self.generation = 0
+        self._sb_host = np.asarray(shard_base, dtype=np.int64).copy()
+        self.payload_used = int(payload_used)
+        self.garbage_u16 = 0
+        self._cap = None
+        if cap is not None:
+            self._cap = np.asarray(cap, dtype=np.int64)
+            self._meta_host = meta
+            self._rowptr_host = rowptr
+        return self
+
+    @classmethod
     def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=(), patchable: bool = False):
         from pilosa_amd import _roaring
 

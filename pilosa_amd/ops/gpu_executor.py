@@ -71,6 +71,10 @@ class GpuExecutor:
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
+        # cold views load from their fragment files (no host bitmaps)
+        self.file_loader = os.environ.get("PILOSA_FILE_LOADER", "1") != "0"
+        self.cold_loads = 0
+        self.last_load: Dict = {}
         self.topn_index_enabled = os.environ.get("PILOSA_TOPN_INDEX", "1") != "0"
         self._topn_indexes: Dict[Tuple, Tuple] = {}  # (index, field, shards) -> (versions, index, built_at)
 
@@ -130,22 +134,50 @@ class GpuExecutor:
                     if f is not None:
                         f.drop_dirty(hit[1].token)
             token = object()  # dirty-row subscription of the new arena
-            bms = []
-            for f in frags:
-                if f is None:
-                    bms.append(None)
-                else:
-                    with f.mu:
-                        f.take_dirty(token)  # register before the contents are read
-                        bms.append(f.storage)
             self._evict_for(key)
-            dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards), patchable=True)
+            dv = self._load_cold(frags, shards, token, key) if self.file_loader else None
+            if dv is None:
+                bms = []
+                for f in frags:
+                    if f is None:
+                        bms.append(None)
+                    else:
+                        with f.mu:
+                            f.take_dirty(token)  # register before the contents are read
+                            bms.append(f.storage)
+                dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards), patchable=True)
             dv.token = token
             self.rebuilds += 1
             self._arenas[key] = (sig, dv)
             self._arenas.move_to_end(key)
             self._evict_for(key)
             return dv
+
+    def _load_cold(self, frags, shards, token, key) -> Optional[DeviceView]:
+        """Arena straight from the fragment files when every fragment of the
+        view is still cold (never read on the host since open): the files are
+        then exactly the fragments' state (ops/loader.py).  Writers are held
+        off while the files are read; the dirty-row subscription is registered
+        first, so writes after the load patch the arena as usual."""
+        import contextlib
+
+        from .loader import load_view
+        live = [f for f in frags if f is not None]
+        if not live or not all(f.is_cold() for f in live):
+            return None
+        with contextlib.ExitStack() as st:
+            for f in live:
+                st.enter_context(f.mu)
+            if not all(f.is_cold() for f in live):
+                return None
+            for f in live:
+                f.take_dirty(token)
+            info: Dict = {}
+            dv = load_view([f.path if f is not None else "" for f in frags], shards, self.device, patchable=True,
+                           stats=info)
+        self.cold_loads += 1
+        self.last_load = dict(info, view=list(key[:3]))
+        return dv
 
     def _evict_for(self, keep):
         """Drop least recently used arenas while over the HBM budget."""
@@ -429,6 +461,38 @@ class GpuExecutor:
             return None  # rows missing from every arena (EMPTY) etc.: planner path
         self.launches += 1
         return [int(v) for v in self.engine.launch_count(self.engine.prepare_progs(progs, vlist, S)).cpu().tolist()]
+
+    def try_count_text(self, index: str, text: str, shards: List[int]) -> Optional[List[int]]:
+        """A whole request of ``Count(<Row/set-op tree>)`` calls, compiled from
+        the PQL text natively (no Python AST) into one launch.  None when any
+        call, field or view needs the general executor path (keys, BSI and
+        time-range leaves, unknown fields, ...)."""
+        from pilosa_amd import _pql
+        from pilosa_amd.models.field import FIELD_TYPE_INT
+        idx = self.holder.index(index)
+        if idx is None or idx.keys:
+            return None
+        names = _pql.count_text_fields(text)
+        views: Dict[str, DeviceView] = {}
+        for name in names:
+            f = idx.field(name)
+            if f is None or f.type == FIELD_TYPE_INT or f.options.keys or name == EXISTENCE_FIELD_NAME:
+                return None
+            dv = self.view_arena(index, name, VIEW_STANDARD, shards)
+            if dv is None:
+                return None
+            views[name] = dv
+        if not views:
+            return None
+        vlist = list(views.values())
+        got = _pql.compile_count_text(text, {n: i for i, n in enumerate(views)}, [v.rows for v in vlist])
+        if got is None:
+            return None
+        raw, Q = got
+        from .device import QPROG_DTYPE
+        progs = raw.view(QPROG_DTYPE)  # rows absent from a view compile to dense -1 (empty leaf)
+        self.launches += 1
+        return self.engine.launch_count(self.engine.prepare_progs(progs, vlist, vlist[0].S)).cpu().tolist()
 
     def try_count_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
         """Many Count() calls of one request -> one launch; calls whose tree

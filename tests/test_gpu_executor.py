@@ -53,6 +53,19 @@ def envs():
     cpu.close()
 
 
+def _dev(cpu, gpu, fn):
+    """Run ``fn`` with the GPU attached; the device must really answer (a
+    launch happened; faults raise in strict mode, tests/conftest.py)."""
+    cpu.executor.gpu = gpu
+    try:
+        n0 = gpu.launches
+        got = fn()
+        assert gpu.launches > n0, "device path not taken"
+    finally:
+        cpu.executor.gpu = None
+    return got
+
+
 QUERIES = [
     "Count(Row(f=0))", "Count(Row(f=3))", "Count(Intersect(Row(f=0), Row(f=1)))",
     "Count(Intersect(Row(f=1), Row(f=2)))", "Count(Intersect(Row(f=2), Row(f=3)))",
@@ -68,11 +81,7 @@ QUERIES = [
 def test_counts_match_host(envs, q):
     cpu, gpu = envs
     want = cpu.q1("i", q)
-    cpu.executor.gpu = gpu
-    try:
-        got = cpu.q1("i", q)
-    finally:
-        cpu.executor.gpu = None
+    got = _dev(cpu, gpu, lambda: cpu.q1("i", q))
     assert got == want
 
 
@@ -94,11 +103,7 @@ def test_count_batch(envs):
 def test_rows_match_host(envs, q):
     cpu, gpu = envs
     want = cols(cpu.q1("i", q))
-    cpu.executor.gpu = gpu
-    try:
-        got = cols(cpu.q1("i", q))
-    finally:
-        cpu.executor.gpu = None
+    got = cols(_dev(cpu, gpu, lambda: cpu.q1("i", q)))
     assert got == want
 
 
@@ -108,11 +113,7 @@ def test_rows_match_host(envs, q):
 def test_aggregates_match_host(envs, q):
     cpu, gpu = envs
     want = cpu.q1("i", q)
-    cpu.executor.gpu = gpu
-    try:
-        got = cpu.q1("i", q)
-    finally:
-        cpu.executor.gpu = None
+    got = _dev(cpu, gpu, lambda: cpu.q1("i", q))
     assert got == want
 
 
@@ -161,11 +162,7 @@ def test_bsi_rows_match_host(envs):
     cpu, gpu = envs
     for q in ("Row(n > 99000)", "Row(n >< [-3, 3])", "Row(m < -4990)"):
         want = cols(cpu.q1("i", q))
-        cpu.executor.gpu = gpu
-        try:
-            got = cols(cpu.q1("i", q))
-        finally:
-            cpu.executor.gpu = None
+        got = cols(_dev(cpu, gpu, lambda: cpu.q1("i", q)))
         assert got == want, q
 
 
@@ -175,11 +172,7 @@ def test_bsi_rows_match_host(envs):
 def test_topn_prefix_rounds_match_host(envs, q):
     cpu, gpu = envs
     want = cpu.q1("i", q)
-    cpu.executor.gpu = gpu
-    try:
-        got = cpu.q1("i", q)
-    finally:
-        cpu.executor.gpu = None
+    got = _dev(cpu, gpu, lambda: cpu.q1("i", q))
     assert got == want
 
 
@@ -469,3 +462,22 @@ def test_minmax_row_on_device_matches_host(envs, q):
     finally:
         cpu.executor.gpu = None
     assert got == want
+
+
+def test_count_text_fast_path_matches_host(envs):
+    """A request of many Count() calls is compiled from its PQL text natively
+    (Executor._count_text_fast -> GpuExecutor.try_count_text) in one launch."""
+    cpu, gpu = envs
+    qs = ["Count(Row(f=0))", "Count(Intersect(Row(f=0), Row(f=1)))", "Count(Union(Row(f=1), Row(g=2), Row(f=20)))",
+          "Count(Difference(Row(f=20), Row(f=0)))", "Count(Xor(Row(f=4), Row(g=0)))", "Count(Row(f=999))",
+          "Count(Intersect(Row(f=0), Row(f=999)))", "Count( Intersect( Row(f=2) ,Row(g=1) ) )"]
+    text = "\n".join(qs)
+    want = cpu.q("i", text)
+    got = _dev(cpu, gpu, lambda: cpu.q("i", text))
+    assert got == want
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    shards = cpu.holder.index("i").available_shards()
+    assert gpu.try_count_text("i", text, shards) == want
+    # outside the native subset: None (the general path answers)
+    assert gpu.try_count_text("i", "Count(Row(f=1)) Count(Row(n > 5))", shards) is None
+    assert gpu.try_count_text("i", "Count(Row(f=1)) TopN(f)", shards) is None

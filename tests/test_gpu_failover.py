@@ -69,3 +69,13 @@ def test_paranoia_catches_wrong_device_results(env):
         env.q1("i", "Count(Row(f=1))")
     env.executor.paranoia = False
     assert env.q1("i", "Count(Row(f=1))") == 12345
+
+
+def test_strict_mode_raises_device_faults(env):
+    env.executor.gpu = _FaultyGpu()
+    env.executor.coalesce = False
+    env.executor.strict_gpu = True
+    with pytest.raises(RuntimeError, match="hipErrorLaunchFailure"):
+        env.q1("i", "Count(Row(f=1))")
+    with pytest.raises(RuntimeError, match="hipErrorLaunchFailure"):
+        env.q("i", "Count(Row(f=1)) Count(Row(f=2))")

@@ -83,3 +83,24 @@ def test_limits(views):
     deep = "Count(" + "Intersect(Row(f=1), " * 5 + "Row(f=2)" + ")" * 5 + ")"
     _, ok = _pql.compile_counts([wide, deep], {"f": 0}, [views["f"].rows])
     assert not ok.any()
+
+
+def test_count_text_equals_per_query(views):
+    """compile_count_text over a whole request == compile_counts per call."""
+    from pilosa_amd import _pql
+    rng = np.random.default_rng(11)
+    qs = [f"Count({_gen(rng)})" for _ in range(300)]
+    fields = {"f": 0, "g": 1}
+    dirs = [views["f"].rows, views["g"].rows]
+    raw, ok = _pql.compile_counts(qs, fields, dirs)
+    assert ok.all()
+    for sep in (" ", "\n", "  \t"):
+        got = _pql.compile_count_text(sep.join(qs), fields, dirs)
+        assert got is not None and got[1] == len(qs)
+        assert (got[0] == raw).all()
+    assert _pql.count_text_fields(" ".join(qs)) == sorted(set(_pql.count_text_fields(" ".join(qs))),
+                                                          key=_pql.count_text_fields(" ".join(qs)).index)
+    assert set(_pql.count_text_fields("Count(Row(f=1)) Count(Intersect(Row(g=2),Row( f =3)))")) == {"f", "g"}
+    for bad in ("Count(Row(f=1)) TopN(f)", "Count(Row(f=1)) Count(Row(n > 3))", "", "Count(Row(f=1)) x",
+                "Count(Row(f=1)) Count(Row(zz=1))", "Count(Row(f=1)) Count(Row(f=\"a\"))"):
+        assert _pql.compile_count_text(bad, fields, dirs) is None, bad
