@@ -499,7 +499,7 @@ class GpuEngine:
         # Count(Intersect(a,b)) route: key-major pair kernels (pair_kernels.hip)
         self.use_and2 = os.environ.get("PILOSA_AND2", "1") != "0"
         self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "0"))  # 0 = by batch size
-        self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "1"))
+        self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "6"))
         # Count(Union(leaves)) route: union_count_kernel (bitmap_kernels.hip)
         self.use_union = os.environ.get("PILOSA_UNION_KERNEL", "1") != "0"
 

@@ -126,7 +126,7 @@ def test_and2_pair_kernels_match_tile_kernel(setup):
         exprs.append(Op("and", (Leaf(va, min(a, 5) if va is view2 else a), Leaf(view, b))))
         ra = min(a, 5) if va is view2 else a
         want.append(sum(_row(x, ra).intersection_count(_row(f, b)) for x, f in zip(fa, frags)))
-    for cq, variant in [(c, v) for v in (1, 2) for c in (0, 4, 8, 16, 32, 64)]:
+    for cq, variant in [(c, v) for v in (1, 2, 3, 4, 5, 6) for c in (0, 4, 8, 16, 32, 64)]:
         e2 = GpuEngine(view.device)
         e2.and2_cq = cq
         e2.and2_variant = variant
@@ -184,3 +184,49 @@ def test_bitgemm_count_matrix_matches_host(mode):
             for k, b in enumerate(rb):
                 want[i, k] += rows[a].intersection_count(rows[b])
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6])
+@pytest.mark.parametrize("cq", [4, 64])
+def test_pair_kernel_array_size_boundaries(cq, variant):
+    """Array containers of 1, 63, 64, 65, 255, 256, 257 (the small-probe
+    boundary), 511, 512, 513 and 4096 values against bitmap, array and run
+    rows, each paired once (one-off: the gather / LDS-staged-bitmap branches)
+    and many times in a row (the staged, reused-row branch), including value 0
+    (the pad-correction path) -> host intersection_count."""
+    import torch
+
+    from pilosa_amd.ops.device import DeviceView, GpuEngine, Leaf, Op
+    rng = np.random.default_rng(cq)
+    sizes = [1, 63, 64, 65, 255, 256, 257, 511, 512, 513, 4096]
+    rows = []
+    for k, n in enumerate(sizes):  # array rows 0..10: key 0 (with value 0 when k is even) and key 3
+        c0 = np.sort(rng.choice(65536, n, replace=False))
+        if k % 2 == 0:
+            c0[0] = 0
+        c3 = 3 * 65536 + np.sort(rng.choice(65536, n, replace=False))
+        rows.append(np.concatenate([c0, c3]))
+    dense = np.concatenate([rng.choice(65536, 30000, replace=False), 3 * 65536 + rng.choice(65536, 9000, replace=False)])
+    rows.append(np.concatenate([[0], dense]))                                   # 11: bitmaps, holds value 0
+    rows.append(np.concatenate([np.arange(0, 40000), 3 * 65536 + np.arange(100, 30000)]))  # 12: runs
+    rows.append(rng.choice(65536, 5000, replace=False) + 65536 * 3)            # 13: one bitmap container
+    vals = np.concatenate([np.uint64(r) * np.uint64(1 << 20) + np.unique(c).astype(np.uint64) for r, c in enumerate(rows)])
+    frag = R.Bitmap(vals)
+    frag.optimize()
+    dev = torch.device("cuda:0")
+    view = DeviceView.from_bitmaps([frag], dev)
+    eng = GpuEngine(dev)
+    eng.and2_cq = cq
+    eng.and2_variant = variant
+    pairs = []
+    for a in range(len(rows)):
+        for b in range(len(rows)):
+            pairs.append((a, b))              # one-off pairs
+    for a in (11, 12, 3, 10):
+        pairs += [(a, b) for b in range(len(rows))] * 3  # runs of the same staged row
+    exprs = [Op("and", (Leaf(view, a), Leaf(view, b))) for a, b in pairs]
+    want = [_row(frag, a).intersection_count(_row(frag, b)) for a, b in pairs]
+    got = eng.count(exprs)
+    np.testing.assert_array_equal(got, np.array(want))
+    per = eng.count_per_shard(exprs)
+    np.testing.assert_array_equal(per[:, 0], np.array(want))
