@@ -49,20 +49,13 @@ NROWS = 1_000_000
 SHARD_WIDTH = 1 << 20
 
 
-_REHEARSE = False
+_COMM = None  # parallel/collectives.Comm when WORLD_SIZE > 1
 
 
 def all_reduce(t, op=None):
-    """dist.all_reduce (RCCL); the gloo rehearsal mode reduces a host copy."""
-    import torch.distributed as dist
-    op = dist.ReduceOp.SUM if op is None else op
-    if _REHEARSE:
-        h = t.cpu()
-        dist.all_reduce(h, op=op)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=op)
-    return t
+    """Sum (or ``op``) a device tensor over the ranks (RCCL; the gloo rehearsal
+    mode goes through host copies)."""
+    return _COMM.all_reduce(t, op)
 
 
 def zipf_rows(rng, n, nrows=NROWS, s=1.6, v=50.0):
@@ -99,26 +92,27 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
     # node-wide row-id space of the TopN accumulators (identical on every rank)
     space = np.asarray(view.rows, dtype=np.uint64)
     if world > 1:
-        parts = [None] * world
-        dist.all_gather_object(parts, space)
-        space = np.unique(np.concatenate(parts))
+        import torch as _t
+        parts = _COMM.all_gather_var(_t.from_numpy(space.view(np.int64).copy()).to(dev))
+        space = np.unique(np.concatenate([p.cpu().numpy().view(np.uint64) for p in parts]))
     t0 = time.perf_counter()
     tindex = DeviceTopNIndex(view, cache, space=space)
     torch.cuda.synchronize(dev)
     t_index = time.perf_counter() - t0
 
     def merge(totals):
+        # phase-1 pairs summed by (query, id) over ranks: (q, id, count)
+        # triples all-gathered as int64 tensors
         if world == 1:
             return totals
-        gathered = [None] * world
-        dist.all_gather_object(gathered, totals)
-        out = []
-        for q in range(len(totals)):
-            t = {}
-            for part in gathered:
-                for i, c in part[q].items():
-                    t[i] = t.get(i, 0) + c
-            out.append(t)
+        from pilosa_amd.parallel.collectives import pairs_to_arrays
+        q, ids, cnt = pairs_to_arrays(totals)
+        flat = torch.from_numpy(np.stack([q, ids, cnt], axis=1).reshape(-1)).to(dev)
+        parts = [p.cpu().numpy().reshape(-1, 3) for p in _COMM.all_gather_var(flat)]
+        allp = np.concatenate(parts) if parts else np.zeros((0, 3), np.int64)
+        out = [dict() for _ in totals]
+        for qq, i, c in allp.tolist():
+            out[qq][i] = out[qq].get(i, 0) + c
         return out
 
     def allreduce(exact, ids):
@@ -137,7 +131,7 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         # device phase 1 (scatter-add of cache prefixes) + device ids= re-count
         calls = [parse_string(q).calls[0] for q in qs]
         return tindex.topn_nosrc(cache.row_counts, [c.uint_arg("n")[0] for c in calls], [1] * len(calls),
-                                 reduce=all_reduce if world > 1 else None)
+                                 comm=_COMM if world > 1 else None)
 
     def run_cache_host(qs):
         calls = [parse_string(q).calls[0] for q in qs]
@@ -151,7 +145,7 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         calls = [parse_string(q).calls[0] for q in qs]
         srcs = [planner.plan(c.children[0]) for c in calls]
         ns = [c.uint_arg("n")[0] for c in calls]
-        return tindex.topn(eng, srcs, ns, [1] * len(srcs), reduce=all_reduce if world > 1 else None)
+        return tindex.topn(eng, srcs, ns, [1] * len(srcs), comm=_COMM if world > 1 else None)
 
     def run_src_pairs(qs):
         # pair-count path with the native heap replay (ops/topn.py), for comparison
@@ -282,15 +276,14 @@ def setup_dist():
     rehearse = os.environ.get("PILOSA_BENCH_REHEARSE") == "1"
     if rehearse:
         local_rank = 0
+    dev = torch.device("cuda", local_rank)
     if world > 1:
+        from pilosa_amd.parallel.collectives import Comm, init
         torch.cuda.set_device(local_rank)
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    global _REHEARSE
-    _REHEARSE = rehearse
-    return world, rank, torch.device("cuda", local_rank)
+        init("gloo" if rehearse else "nccl", local_rank, timeout_s=600)
+        global _COMM
+        _COMM = Comm(device=dev, host_copies=rehearse)
+    return world, rank, dev
 
 
 def run_synthetic(args, world, rank, dev, queries, ra, rb):
@@ -480,22 +473,26 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
                     err.append(e)
                     return
 
+        comm_stream = torch.cuda.Stream(dev) if world > 1 else None
+
         def run(first, n):
             nxt[0] = first
             ts = [threading.Thread(target=client, args=(first + n,)) for _ in range(max(1, args.clients))]
             for t in ts:
                 t.start()
             # ranks all-reduce each request's counts in request order (one
-            # collective per batch, issued from this thread only)
+            # collective per batch, issued from this thread only) on a stream
+            # of its own, so it never queues behind the next batch's kernels
             for i in range(first, first + n):
                 if world > 1:
                     while results[i] is None and not err:
                         time.sleep(0.0002)
                     if err:
                         break
-                    tt = torch.tensor(results[i], dtype=torch.int64, device=dev)
-                    all_reduce(tt)
-                    results[i] = tt.cpu().tolist()
+                    with torch.cuda.stream(comm_stream):
+                        tt = torch.tensor(results[i], dtype=torch.int64, device=dev)
+                        all_reduce(tt)
+                        results[i] = tt.cpu().tolist()
             for t in ts:
                 t.join()
             if err:

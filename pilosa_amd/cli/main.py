@@ -78,6 +78,7 @@ def cmd_server(args, stdout, stderr) -> int:
         # one process per GPU (torch.distributed.run): non-front-end ranks own
         # shard subsets and execute what rank 0 broadcasts (parallel/mesh.py)
         return M.run_worker(cfg.data_dir(), gpu_mode=cfg.get("gpu.mode"), block=cfg.get("gpu.shard-block"),
+                            timeout_s=cfg.duration("gpu.rccl-timeout"),
                             logger=logger)
     bind = cfg.get("bind")
     if bind.startswith(":"):
@@ -100,7 +101,8 @@ def cmd_server(args, stdout, stderr) -> int:
                  tls_skip_verify=cfg.get("tls.skip-verify"),
                  diagnostics_host=cfg.get("metric.diagnostics-host") if cfg.get("metric.diagnostics") else "",
                  gpu_device=int(cfg.get("gpu.devices")[0]) if cfg.get("gpu.devices") else None,
-                 hbm_budget=int(cfg.get("gpu.hbm-budget")))
+                 hbm_budget=int(cfg.get("gpu.hbm-budget")), mesh_timeout_s=cfg.duration("gpu.rccl-timeout"),
+                 lazy_fragments=bool(cfg.get("gpu.lazy-fragments")))
     srv.open()
     logger.printf("listening as %s (node %s, gpu=%s)", srv.uri.normalize(), srv.node.id,
                   "on" if srv.gpu is not None else "off")

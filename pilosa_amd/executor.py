@@ -31,6 +31,7 @@ from pilosa_amd.models.row import Row
 from pilosa_amd.models.timeq import (TIME_FORMAT, min_max_views, parse_time, time_of_view, views_by_time_range)
 from pilosa_amd.models.view import VIEW_BSI_PREFIX, VIEW_STANDARD
 from pilosa_amd.pql import BETWEEN, EQ, GT, GTE, LT, LTE, NEQ, Call, Condition, Query, parse_string
+from pilosa_amd.parallel.mesh import MeshError
 from pilosa_amd.utils import tracing
 
 DEFAULT_FIELD = "general"
@@ -329,7 +330,13 @@ class Executor:
         # Batch fast path: many Count() calls in one request go to the GPU together.
         if self._use_mesh(opt) and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
                 not self._has_remote(index, shards, opt):
-            return self.mesh.count_batch(index, q.calls, shards)
+            mesh = self.mesh
+            try:
+                return mesh.count_batch(index, q.calls, shards)
+            except MeshError:
+                if not mesh.failed_over:
+                    raise  # a rank reported an error: the query's error
+                # a rank is gone: this process adopted its shards, answer locally
         if self.gpu is not None and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
                 not self._has_remote(index, shards, opt):
             try:
@@ -353,7 +360,13 @@ class Executor:
     def _run_count_batch(self, key, calls):
         index, shards, mesh = key
         if mesh:
-            return self.mesh.count_batch(index, list(calls), list(shards))
+            m = self.mesh
+            if m is None:
+                return None
+            try:
+                return m.count_batch(index, list(calls), list(shards))
+            except MeshError:
+                return None  # each call then runs alone (and reports its own error)
         if self.gpu is None:
             return None
         try:
@@ -459,8 +472,14 @@ class Executor:
         for node, nshards in by_node.items():
             if node is None or (self.cluster is not None and node.id == self.cluster.node.id):
                 if self._use_mesh(opt):
-                    result = reduce_fn(result, self.mesh.map_local(index, c, nshards, opt, reduce_fn))
-                    continue
+                    mesh = self.mesh
+                    try:
+                        result = reduce_fn(result, mesh.map_local(index, c, nshards, opt, reduce_fn))
+                        continue
+                    except MeshError:
+                        if not mesh.failed_over:
+                            raise
+                        # failed over: this process now holds every local shard
                 result = reduce_fn(result, self._map_local(nshards, map_fn, reduce_fn, local_fn))
             elif not opt.remote:
                 remote_jobs.append((node, nshards))

@@ -12,13 +12,14 @@ cached row grouped by column (per shard: ``colptr[2^20+1]`` + u16 slots).
 The src counts of all cached rows of a shard are then one LDS histogram over
 src's columns, and the reference heap walk runs on that histogram inside the
 same workgroup (pilosa_amd/kernels/topn_kernels.hip).  Phase 1 leaves one
-dense accumulator per query over the node-wide "acc space" of row ids, so
-multi-GPU merging is a single all-reduce; phase 2 (the ids= re-count) reuses
-the kernel with a gather instead of the walk.
+accumulator per query over the node-wide "acc space" of row ids; across the
+GPUs of a node only its non-zero entries (the candidate set) are all-gathered
+and unioned, and phase 2 (the ids= re-count, the kernel with a gather instead
+of the walk) sums one int64 per candidate with an all-reduce.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 
@@ -173,27 +174,37 @@ class DeviceTopNIndex:
                          pair_idx=pair_idx.to(torch.int32).contiguous(), out=out, hist=hist)
         return out
 
-    def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
-             reduce: Optional[Callable[[object], object]] = None) -> List[List[Pair]]:
-        """TopN(field, src_q, n=ns[q], threshold=thresholds[q]) for a batch.
-        ``reduce`` sums a device tensor across the ranks of a node in place
-        (dist.all_reduce); every rank must call with the same batch."""
+    def _candidates(self, acc, comm):
+        """(query, acc index) of every phase-1 candidate.  Across the ranks of
+        a node only the candidate SET matters (phase 2 re-counts exactly), so
+        the ranks all-gather their fixed-k candidate keys and take the union
+        (parallel/collectives.py) instead of all-reducing the dense
+        [Q x row-space] accumulator."""
         import torch
 
+        nz = torch.nonzero(acc > 0)
+        if comm is None:
+            return nz[:, 0].contiguous(), nz[:, 1].contiguous()
+        A = max(self.A, 1)
+        keys = comm.union(nz[:, 0].to(torch.int64) * A + nz[:, 1].to(torch.int64))
+        return (keys // A).contiguous(), (keys % A).contiguous()
+
+    def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
+             comm=None) -> List[List[Pair]]:
+        """TopN(field, src_q, n=ns[q], threshold=thresholds[q]) for a batch.
+        ``comm`` (parallel/collectives.Comm) spans the ranks of a node: the
+        candidate union and the phase-2 sums go through it; every rank must
+        call with the same batch."""
         Q = len(srcs)
         if Q == 0:
             return []
         src = engine.materialize_batch(srcs, self.S)
         keep = self.hist_bytes(Q) <= HIST_KEEP_BYTES
         acc, ns_t, th_t, hist = self.phase1(src, Q, ns, thresholds, keep_hist=keep)
-        if reduce is not None:
-            reduce(acc)
-        nz = torch.nonzero(acc > 0)
-        pair_q = nz[:, 0].contiguous()
-        pair_idx = nz[:, 1].contiguous()
+        pair_q, pair_idx = self._candidates(acc, comm)
         out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx, hist=hist)
-        if reduce is not None:
-            reduce(out)
+        if comm is not None:
+            comm.all_reduce(out)
         return finish_batch(self.space, Q, pair_q.cpu().numpy(), pair_idx.cpu().numpy(), out.cpu().numpy(), ns)
 
     def shard_pairs(self, engine: GpuEngine, src, n: int, threshold: int,
@@ -225,8 +236,7 @@ class DeviceTopNIndex:
         ids_out = self.space[a[keep]] if len(a) else np.zeros(0, np.uint64)
         return [Pair(int(i), int(v)) for i, v in zip(ids_out.tolist(), c[keep].tolist())]
 
-    def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int],
-                   reduce: Optional[Callable[[object], object]] = None) -> List[List[Pair]]:
+    def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None) -> List[List[Pair]]:
         """TopN(field, n) without a src row for a batch, all on the device.
         Phase 1: per shard the first n cache entries at or above the
         threshold (fragment.top stops once its heap holds n rows), summed by
@@ -250,18 +260,15 @@ class DeviceTopNIndex:
             vals = torch.where(take, cnt[None], torch.zeros((), dtype=torch.int32, device=dev))
             idx = self.cache_acc[:, :nmax].reshape(1, -1).expand(Q, -1).to(torch.int64)
             acc.scatter_add_(1, idx, vals.reshape(Q, -1))
-        if reduce is not None:
-            reduce(acc)
-        nz = torch.nonzero(acc > 0)
-        pq, pa = nz[:, 0], nz[:, 1]
+        pq, pa = self._candidates(acc, comm)
         out = torch.zeros(pa.numel(), dtype=torch.int64, device=dev)
         if pa.numel() and self.S:
             d = self.a2dense[pa].to(torch.int64)
             c = row_counts.index_select(1, d.clamp(min=0))                       # [S, P]
             c = torch.where((c >= mt[pq][None, :]) & (d[None, :] >= 0), c, torch.zeros_like(c))
             out = c.sum(dim=0, dtype=torch.int64)
-        if reduce is not None:
-            reduce(out)
+        if comm is not None:
+            comm.all_reduce(out)
         return finish_batch(self.space, Q, pq.cpu().numpy(), pa.cpu().numpy(), out.cpu().numpy(), ns)
 
 

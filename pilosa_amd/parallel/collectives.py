@@ -1,0 +1,252 @@
+"""Tensor-only collectives for the intra-node mesh (RCCL over xGMI on the GPU
+box, gloo for CPU tests) and a compact binary codec for partial results.
+
+Reference analog: the coordinator fan-out/reduce of executor.go:2458-2555 and
+the QueryResponse protobuf a remote node returns (internal/public.proto).  Here
+the ranks of one node exchange only tensors:
+
+* ``bcast_bytes``  command broadcast: an int64 header (op, length) then the
+  payload as a uint8 tensor (2 collectives, no pickling);
+* ``all_reduce``   counts / sums (int64) with an error flag folded into the
+  same tensor, so a healthy Count batch costs one collective;
+* ``all_gather_var`` variable-length 1-D tensors (sizes first, then one padded
+  all_gather): TopN candidate ids, encoded partial results;
+* ``union``        sorted distinct values over ranks (TopN phase-1 candidate
+  sets: only membership matters because phase 2 re-counts exactly, so fixed-k
+  candidate lists are gathered instead of a dense [Q x rows] all-reduce).
+
+Every collective runs under the process group's timeout (``init(timeout=)``;
+RCCL aborts the communicator when it expires), and a failure marks the Comm
+broken so callers can fail over instead of hanging.
+
+Partial results are encoded with msgpack (a schema-less binary format; no
+code is executed on decode) with extension types for the executor's result
+objects.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+
+class CommError(RuntimeError):
+    """A collective failed or timed out; the mesh must fail over."""
+
+
+class Comm:
+    def __init__(self, group=None, device=None, host_copies: bool = False):
+        import torch
+        import torch.distributed as dist
+
+        self.torch = torch
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        backend = dist.get_backend(group)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        self.device = torch.device(device)
+        # gloo rehearsal of a GPU run: collectives on host copies
+        self.host_copies = host_copies or (backend == "gloo" and self.device.type == "cuda")
+        self.broken: Optional[BaseException] = None
+        self.calls = 0
+
+    # ------------------------------------------------------------ guard
+    def _guard(self, fn, *a, **kw):
+        if self.broken is not None:
+            raise CommError(f"communicator broken: {self.broken}")
+        self.calls += 1
+        try:
+            return fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001 - timeouts / peer loss surface here
+            self.broken = e
+            raise CommError(f"collective failed: {type(e).__name__}: {e}") from e
+
+    def _on(self, t):
+        return t.cpu() if self.host_copies and t.device.type != "cpu" else t
+
+    # ------------------------------------------------------------ primitives
+    def all_reduce(self, t, op=None):
+        """In-place sum (or ``op``) of ``t`` over the ranks."""
+        op = self.dist.ReduceOp.SUM if op is None else op
+        h = self._on(t)
+        self._guard(self.dist.all_reduce, h, op=op, group=self.group)
+        if h is not t:
+            t.copy_(h)
+        return t
+
+    def broadcast(self, t, src: int = 0):
+        h = self._on(t)
+        self._guard(self.dist.broadcast, h, src=src, group=self.group)
+        if h is not t:
+            t.copy_(h)
+        return t
+
+    def bcast_bytes(self, op: int = 0, payload: bytes = b"", src: int = 0):
+        """Rank ``src`` sends (op, payload); every rank returns them."""
+        torch = self.torch
+        hdr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        if self.rank == src:
+            hdr[0], hdr[1] = int(op), len(payload)
+        self.broadcast(hdr, src)
+        op_, n = (int(x) for x in hdr.cpu().tolist())
+        if n == 0:
+            return op_, b""
+        buf = torch.empty(n, dtype=torch.uint8, device=self.device)
+        if self.rank == src:
+            buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+        self.broadcast(buf, src)
+        return op_, buf.cpu().numpy().tobytes()
+
+    def all_gather_var(self, t) -> List:
+        """1-D tensors of any length per rank -> list of per-rank tensors."""
+        torch = self.torch
+        t = t.reshape(-1)
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        hs = [self._on(x) for x in sizes]
+        self._guard(self.dist.all_gather, hs, self._on(n), group=self.group)
+        lens = [int(x.item()) for x in hs]
+        m = max(lens) if lens else 0
+        if m == 0:
+            return [t[:0] for _ in range(self.world)]
+        pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+        pad[:t.numel()] = t
+        outs = [torch.empty(m, dtype=t.dtype, device=t.device) for _ in range(self.world)]
+        ho = [self._on(x) for x in outs]
+        self._guard(self.dist.all_gather, ho, self._on(pad), group=self.group)
+        return [x[:k].to(t.device) for x, k in zip(ho, lens)]
+
+    def union(self, t):
+        """Sorted distinct values of ``t`` over all ranks (same on every rank)."""
+        parts = self.all_gather_var(t)
+        return self.torch.unique(self.torch.cat(parts)) if parts else t
+
+    def gather_bytes(self, payload: bytes) -> List[bytes]:
+        """Every rank's bytes, on every rank (small control-plane payloads)."""
+        torch = self.torch
+        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if payload else torch.zeros(0, dtype=torch.uint8)
+        parts = self.all_gather_var(t.to(self.device))
+        return [p.cpu().numpy().tobytes() for p in parts]
+
+    def barrier(self):
+        self.all_reduce(self.torch.zeros(1, dtype=self.torch.int64, device=self.device))
+
+
+def init(backend: Optional[str] = None, local_rank: int = 0, timeout_s: float = 120.0):
+    """One process per GPU: RCCL ("nccl") when GPUs are visible, else gloo;
+    collectives time out after ``timeout_s`` (RCCL: the communicator aborts
+    and the waiting call raises)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return dist.get_backend()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    to = _dt.timedelta(seconds=float(timeout_s))
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=to)
+    else:
+        dist.init_process_group(backend, timeout=to)
+    return backend
+
+
+# ---------------------------------------------------------------- result codec
+_EXT_ROW, _EXT_PAIR, _EXT_VALCOUNT, _EXT_GROUPCOUNT, _EXT_ROWIDS, _EXT_FIELDROW, _EXT_ERR, _EXT_U64 = range(1, 9)
+
+
+def _default(o):
+    import msgpack
+
+    from pilosa_amd.executor import FieldRow, GroupCount, RowIdentifiers, ValCount
+    from pilosa_amd.models.cache import Pair
+    from pilosa_amd.models.row import Row
+
+    if isinstance(o, Row):
+        segs = {int(s): bm.to_bytes() for s, bm in o.segments.items()}
+        return msgpack.ExtType(_EXT_ROW, msgpack.packb([segs, o.attrs, o.keys], default=_default))
+    if isinstance(o, Pair):
+        return msgpack.ExtType(_EXT_PAIR, msgpack.packb([int(o.id), int(o.count), getattr(o, "key", "") or ""]))
+    if isinstance(o, ValCount):
+        return msgpack.ExtType(_EXT_VALCOUNT, msgpack.packb([int(o.val), int(o.count)]))
+    if isinstance(o, GroupCount):
+        return msgpack.ExtType(_EXT_GROUPCOUNT, msgpack.packb([[_default(g) for g in o.group], int(o.count)],
+                                                              default=_default))
+    if isinstance(o, RowIdentifiers):
+        return msgpack.ExtType(_EXT_ROWIDS, msgpack.packb([list(o.rows), o.keys]))
+    if isinstance(o, FieldRow):
+        return msgpack.ExtType(_EXT_FIELDROW, msgpack.packb([o.field, int(o.row_id), o.row_key]))
+    if isinstance(o, BaseException):
+        return msgpack.ExtType(_EXT_ERR, msgpack.packb(f"{type(o).__name__}: {o}"))
+    if isinstance(o, (np.integer,)):
+        return int(o)
+    if isinstance(o, np.ndarray):
+        return o.tolist()
+    raise TypeError(f"cannot encode {type(o).__name__}")
+
+
+def _ext_hook(code, data):
+    import msgpack
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.executor import FieldRow, GroupCount, RowIdentifiers, ValCount
+    from pilosa_amd.models.cache import Pair
+    from pilosa_amd.models.row import Row
+
+    v = msgpack.unpackb(data, ext_hook=_ext_hook, strict_map_key=False)
+    if code == _EXT_ROW:
+        segs, attrs, keys = v
+        r = Row(segments={int(s): _roaring.Bitmap.from_bytes(b) for s, b in segs.items()})
+        r.attrs, r.keys = attrs, keys
+        return r
+    if code == _EXT_PAIR:
+        p = Pair(v[0], v[1])
+        if v[2]:
+            p.key = v[2]
+        return p
+    if code == _EXT_VALCOUNT:
+        return ValCount(v[0], v[1])
+    if code == _EXT_GROUPCOUNT:
+        return GroupCount(list(v[0]), v[1])
+    if code == _EXT_ROWIDS:
+        return RowIdentifiers(v[0], v[1])
+    if code == _EXT_FIELDROW:
+        return FieldRow(v[0], v[1], v[2])
+    if code == _EXT_ERR:
+        return RemoteError(v)
+    return msgpack.ExtType(code, data)
+
+
+class RemoteError(Exception):
+    """An error raised on another rank, carried back in a partial result."""
+
+
+def encode(obj) -> bytes:
+    import msgpack
+    return msgpack.packb(obj, default=_default, strict_types=False, use_bin_type=True)
+
+
+def decode(data: bytes):
+    import msgpack
+    if not data:
+        return None
+    return msgpack.unpackb(data, ext_hook=_ext_hook, strict_map_key=False, raw=False)
+
+
+def pairs_to_arrays(totals: Sequence[dict]):
+    """[{id: count}] per query -> (q, id, count) int64 arrays."""
+    q, ids, cnt = [], [], []
+    for k, t in enumerate(totals):
+        for i, c in t.items():
+            q.append(k)
+            ids.append(int(i))
+            cnt.append(int(c))
+    return np.array(q, np.int64), np.array(ids, np.int64), np.array(cnt, np.int64)

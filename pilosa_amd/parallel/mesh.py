@@ -15,18 +15,25 @@ hop with a process group (backend ``nccl`` = RCCL over xGMI on the GPU box,
   reference's remote QueryRequest), each rank runs it over the shards it owns
   with ``remote`` semantics (TopN phase-1 pairs, unmerged row segments), and
   the partial results are reduced with collectives: ``all_reduce(SUM)`` of
-  int64 tensors for Count / batched Counts / Sum, an object gather folded
-  with the executor's own reduce function for everything else (TopN pairs,
-  Rows, GroupBy, MinRow/MaxRow, Min/Max, Row segments).
+  int64 tensors for Count / batched Counts (an error flag rides in the same
+  tensor), a variable-length byte all-gather of msgpack-encoded partials
+  folded with the executor's own reduce function for everything else (TopN
+  pairs, Rows, GroupBy, MinRow/MaxRow, Min/Max, Row segments).
 * writes and imports are routed to the owning rank only.
 
-Collectives are issued strictly in the same order on every rank, so the front
-end serialises mesh operations with a lock.
+Transport is tensors only (parallel/collectives.py): a command is an int64
+header plus a uint8 payload tensor, no pickled objects.  Collectives are
+issued strictly in the same order on every rank, so the front end serialises
+mesh operations with a lock.  Every collective has the process group's
+timeout; when one fails (a rank died or hung) the front end fails over: it
+adopts the other ranks' fragment files from their data dirs into its own
+holder (lazily opened, loaded into its HBM on first use) and keeps serving
+single-GPU (a dead GPU's shard range is reloaded onto the
+survivors).
 """
 from __future__ import annotations
 
 import threading
-import traceback
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 SHARD_WIDTH = 1 << 20
@@ -37,48 +44,38 @@ class MeshError(RuntimeError):
 
 
 # ---------------------------------------------------------------- transport
-def encode_result(r):
-    """Make a partial result picklable (Row segments hold native bitmaps)."""
-    from pilosa_amd.models.row import Row
-
-    if isinstance(r, Row):
-        return ("__row__", {int(s): bm.to_bytes() for s, bm in r.segments.items()})
-    if isinstance(r, BaseException):
-        return ("__err__", f"{type(r).__name__}: {r}", traceback.format_exception(type(r), r, r.__traceback__))
-    return r
+OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS = range(9)
 
 
-def decode_result(r):
-    from pilosa_amd import _roaring
-    from pilosa_amd.models.row import Row
+def _raise_remote(parts):
+    from .collectives import RemoteError
 
-    if isinstance(r, tuple) and r and r[0] == "__row__":
-        return Row(segments={s: _roaring.Bitmap.from_bytes(b) for s, b in r[1].items()})
-    if isinstance(r, tuple) and r and r[0] == "__err__":
-        raise MeshError(r[1])
-    return r
+    for p in parts:
+        if isinstance(p, RemoteError):
+            raise MeshError(str(p))
 
 
 class ShardMesh:
     """Shard-owner routing and collective reductions for one node's GPUs."""
 
-    def __init__(self, executor, group=None, block: int = 1, device=None):
-        import torch
-        import torch.distributed as dist
+    def __init__(self, executor, group=None, block: int = 1, device=None, peer_dirs: Optional[Dict[int, str]] = None):
+        from .collectives import Comm
 
-        self.torch = torch
-        self.dist = dist
+        self.comm = Comm(group, device=device)
+        self.torch = self.comm.torch
+        self.dist = self.comm.dist
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        self.rank = self.comm.rank
+        self.world = self.comm.world
         self.block = max(1, int(block))
         self.executor = executor
-        backend = dist.get_backend(group)
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-        self.device = torch.device(device)
+        self.device = self.comm.device
         self.lock = threading.RLock()
         self.ops = 0
+        # rank -> data dir of that rank's holder (failover adopts its fragments)
+        self.peer_dirs: Dict[int, str] = dict(peer_dirs or {})
+        self.failed_over = False
+        self.failover_error: Optional[str] = None
 
     # ------------------------------------------------------------ ownership
     def owner(self, shard: int) -> int:
@@ -93,79 +90,77 @@ class ShardMesh:
         return self.rank == 0
 
     # ------------------------------------------------------------ plumbing
-    def _bcast(self, cmd):
-        box = [cmd]
-        self.dist.broadcast_object_list(box, src=0, group=self.group, device=self._obj_device())
-        return box[0]
+    def _gather(self, obj) -> list:
+        """Every rank's partial result (msgpack over a byte all-gather)."""
+        from .collectives import decode, encode
 
-    def _obj_device(self):
-        return self.device if self.device.type == "cuda" else None
+        return [decode(b) for b in self.comm.gather_bytes(encode(obj))]
 
-    def _gather(self, obj) -> Optional[list]:
-        out = [None] * self.world if self.rank == 0 else None
-        self.dist.gather_object(encode_result(obj), out, dst=0, group=self.group)
-        return out
+    def _run(self, op: int, *args):
+        """Front end: broadcast the command and take part in it like any rank.
+        A failed collective turns into failover (MeshError for this call)."""
+        from .collectives import CommError, encode
 
-    def _sum_i64(self, values: Sequence[int]) -> List[int]:
-        t = self.torch.tensor(list(values), dtype=self.torch.int64, device=self.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
-        return [int(x) for x in t.cpu().tolist()]
-
-    def _run(self, cmd):
-        """Front end: broadcast ``cmd`` and take part in it like any rank."""
         if not self.is_frontend:
             raise MeshError("only rank 0 issues mesh commands")
         with self.lock:
+            if self.failed_over:
+                raise MeshError(f"mesh failed over: {self.failover_error}")
             self.ops += 1
-            self._bcast(cmd)
-            return self._dispatch(cmd)
+            try:
+                self.comm.bcast_bytes(op, encode(list(args)))
+                return self._dispatch(op, list(args))
+            except CommError as e:
+                self.failover(e)
+                raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
 
     # ------------------------------------------------------------ front-end API
     def map_local(self, index: str, c, shards: Sequence[int], opt, reduce_fn: Callable[[Any, Any], Any]):
         """Execute call ``c`` over ``shards`` on their owner ranks and fold the
         partial results with ``reduce_fn`` (the executor's reduce step)."""
         if c.name == "Count":
-            return self._run(("count", index, [str(c)], list(shards)))[0]
-        parts = self._run(("call", index, str(c), list(shards), _opt_dict(opt)))
+            return self._run(OP_COUNT, index, [str(c)], list(shards))[0]
+        parts = self._run(OP_CALL, index, str(c), list(shards), _opt_dict(opt))
         result = None
         for p in parts:
-            result = reduce_fn(result, decode_result(p))
+            result = reduce_fn(result, p)
         return result
 
     def count_batch(self, index: str, calls, shards: Sequence[int]) -> List[int]:
-        return self._run(("count", index, [str(c) for c in calls], list(shards)))
+        return self._run(OP_COUNT, index, [str(c) for c in calls], list(shards))
 
     def forward_write(self, index: str, c, shard: int, opt) -> Any:
-        parts = self._run(("write", index, str(c), int(shard), _opt_dict(opt)))
-        out = decode_result(parts[self.owner(shard)])
+        parts = self._run(OP_WRITE, index, str(c), int(shard), _opt_dict(opt))
         self._note_shard(index, shard)
-        return out
+        return parts[self.owner(shard)]
 
     def forward_import(self, kind: str, index: str, field: str, shard: int, payload: dict):
-        parts = self._run(("import", kind, index, field, int(shard), payload))
-        decode_result(parts[self.owner(shard)])
+        self._run(OP_IMPORT, kind, index, field, int(shard), _plain(payload))
         self._note_shard(index, shard)
 
     def apply_schema(self):
         """Push the front end's schema to every rank (after schema changes)."""
         schema = self.executor.holder.schema()
-        self._run(("schema", schema))
+        self._run(OP_SCHEMA, schema)
 
     def delete_index(self, name: str):
-        self._run(("delete_index", name))
+        self._run(OP_DEL_INDEX, name)
 
     def delete_field(self, index: str, name: str):
-        self._run(("delete_field", index, name))
+        self._run(OP_DEL_FIELD, index, name)
 
     def shard_counts(self) -> Dict[int, Dict[str, List[int]]]:
         """Available shards per rank (status/debug)."""
-        parts = self._run(("shards",))
-        return {r: decode_result(p) for r, p in enumerate(parts)}
+        parts = self._run(OP_SHARDS)
+        return {r: p for r, p in enumerate(parts)}
 
     def stop(self):
-        if self.is_frontend:
+        if self.is_frontend and not self.failed_over:
             with self.lock:
-                self._bcast(("stop",))
+                try:
+                    self.comm.bcast_bytes(OP_STOP, b"")
+                except Exception:  # noqa: BLE001 - peers already gone
+                    pass
 
     def _note_shard(self, index: str, shard: int):
         idx = self.executor.holder.index(index)
@@ -175,79 +170,103 @@ class ShardMesh:
             if int(shard) not in f.remote_available_shards:
                 f.add_remote_available_shards([int(shard)])
 
+    # ------------------------------------------------------------ failover
+    def failover(self, err: BaseException):
+        """A collective failed: stop using the mesh and adopt every other
+        rank's fragment files (their data dirs) into the front end's holder,
+        so all shards are served by this process's GPU (or host)."""
+        if self.failed_over:
+            return
+        self.failed_over = True
+        self.failover_error = f"{type(err).__name__}: {err}"
+        ex = self.executor
+        if getattr(ex, "mesh", None) is self:
+            ex.mesh = None
+        adopted = 0
+        for r, d in sorted(self.peer_dirs.items()):
+            if r == self.rank:
+                continue
+            try:
+                adopted += adopt_holder_dir(ex.holder, d)
+            except Exception as e:  # noqa: BLE001 - keep serving what we have
+                if getattr(ex, "logger", None) is not None:
+                    ex.logger.printf("mesh failover: cannot adopt rank %d (%s): %s", r, d, e)
+        if ex.gpu is not None:
+            ex.gpu.invalidate()
+        if getattr(ex, "logger", None) is not None:
+            ex.logger.printf("mesh failover after %s: adopted %d fragments", self.failover_error, adopted)
+        return adopted
+
     # ------------------------------------------------------------ worker loop
     def serve(self):
         """Ranks > 0: execute broadcast commands until ``stop``."""
+        from .collectives import decode
+
         while True:
-            cmd = self._bcast(None)
-            if cmd[0] == "stop":
+            op, payload = self.comm.bcast_bytes()
+            if op == OP_STOP:
                 return
-            self._dispatch(cmd)
+            self._dispatch(op, decode(payload) or [])
 
     # ------------------------------------------------------------ all ranks
-    def _dispatch(self, cmd):
-        kind = cmd[0]
+    def _dispatch(self, op: int, args: list):
         ex = self.executor
-        if kind == "count":
-            _, index, pqls, shards = cmd
-            local = [0] * len(pqls)
+        if op == OP_COUNT:
+            index, pqls, shards = args
+            torch = self.torch
             err = None
+            local = [0] * len(pqls)
             try:
                 local = self._local_counts(index, pqls, self.owned(shards))
-            except Exception as e:  # noqa: BLE001 - reported through the gather below
+            except Exception as e:  # noqa: BLE001 - flagged in the reduced tensor below
                 err = e
-            out = self._sum_i64(local)
-            errs = self._gather(err)
-            if self.is_frontend:
-                for e in errs:
-                    decode_result(e)
-            return out
-        if kind == "call":
-            _, index, pql, shards, optd = cmd
-            try:
+            t = torch.tensor(list(local) + [1 if err is not None else 0], dtype=torch.int64, device=self.device)
+            self.comm.all_reduce(t)
+            out = [int(x) for x in t.cpu().tolist()]
+            if out[-1]:
+                parts = self._gather(err)
+                if self.is_frontend:
+                    _raise_remote(parts)
+            return out[:-1]
+        mine = None
+        try:
+            if op == OP_CALL:
+                index, pql, shards, optd = args
                 mine = self._local_call(index, pql, self.owned(shards), optd)
-            except Exception as e:  # noqa: BLE001
-                mine = e
-            return self._gather(mine)
-        if kind == "write":
-            _, index, pql, shard, optd = cmd
-            mine = None
-            if self.owner(shard) == self.rank:
-                try:
+            elif op == OP_WRITE:
+                index, pql, shard, optd = args
+                if self.owner(shard) == self.rank:
                     mine = self._local_call(index, pql, [shard], optd)
-                except Exception as e:  # noqa: BLE001
-                    mine = e
-            return self._gather(mine)
-        if kind == "import":
-            _, what, index, field, shard, payload = cmd
-            mine = None
-            if self.owner(shard) == self.rank:
-                try:
+            elif op == OP_IMPORT:
+                what, index, field, shard, payload = args
+                if self.owner(shard) == self.rank:
                     self._local_import(what, index, field, shard, payload)
-                except Exception as e:  # noqa: BLE001
-                    mine = e
-            return self._gather(mine)
-        if kind == "schema":
-            if not self.is_frontend:
-                ex.holder.apply_schema(cmd[1])
-            return self._gather(None)
-        if kind == "delete_index":
-            if not self.is_frontend and ex.holder.index(cmd[1]) is not None:
-                ex.holder.delete_index(cmd[1])
-            return self._gather(None)
-        if kind == "delete_field":
-            if not self.is_frontend:
-                idx = ex.holder.index(cmd[1])
-                if idx is not None and idx.field(cmd[2]) is not None:
-                    idx.delete_field(cmd[2])
-            return self._gather(None)
-        if kind == "shards":
-            mine = {name: idx.available_shards() for name, idx in ex.holder.indexes.items()}
-            if self.is_frontend:
-                mine = {name: sorted({s for f in idx.fields.values() for s in f.local_shards})
-                        for name, idx in ex.holder.indexes.items()}
-            return self._gather(mine)
-        raise MeshError(f"unknown mesh command {kind!r}")
+            elif op == OP_SCHEMA:
+                if not self.is_frontend:
+                    ex.holder.apply_schema(args[0])
+            elif op == OP_DEL_INDEX:
+                if not self.is_frontend and ex.holder.index(args[0]) is not None:
+                    ex.holder.delete_index(args[0])
+            elif op == OP_DEL_FIELD:
+                if not self.is_frontend:
+                    idx = ex.holder.index(args[0])
+                    if idx is not None and idx.field(args[1]) is not None:
+                        idx.delete_field(args[1])
+            elif op == OP_SHARDS:
+                mine = {name: idx.available_shards() for name, idx in ex.holder.indexes.items()}
+                if self.is_frontend:
+                    mine = {name: sorted({s for f in idx.fields.values() for s in f.local_shards})
+                            for name, idx in ex.holder.indexes.items()}
+            else:
+                raise MeshError(f"unknown mesh command {op!r}")
+        except Exception as e:  # noqa: BLE001 - reported through the gather below
+            if isinstance(e, MeshError) and "unknown mesh command" in str(e):
+                raise
+            mine = e
+        parts = self._gather(mine)
+        if self.is_frontend:
+            _raise_remote(parts)
+        return parts
 
     def _local_opt(self, optd: dict):
         from pilosa_amd.executor import ExecOptions
@@ -274,6 +293,10 @@ class ShardMesh:
         ex = self.executor
         if not shards:
             return [0] * len(pqls)
+        if ex.gpu is not None and len(pqls) > 1 and hasattr(ex.gpu, "try_count_text"):
+            res = ex.gpu.try_count_text(index, " ".join(pqls), shards)
+            if res is not None:
+                return [int(x) for x in res]
         calls = [parse_string(p).calls[0] for p in pqls]
         if ex.gpu is not None and len(calls) > 1:
             res = ex.gpu.try_count_batch(index, calls, shards)
@@ -309,6 +332,49 @@ class ShardMesh:
             raise MeshError(f"unknown import kind {what!r}")
 
 
+def _plain(v):
+    """numpy arrays -> lists for the msgpack codec."""
+    import numpy as np
+
+    if isinstance(v, dict):
+        return {k: _plain(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, np.integer):
+        return int(v)
+    return v
+
+
+def adopt_holder_dir(holder, data_dir: str) -> int:
+    """Move every fragment of the holder at ``data_dir`` (another rank's, whose
+    process is gone) into ``holder``'s views, lazily opened from their files.
+    Returns the number of fragments adopted."""
+    from pilosa_amd.models.holder import Holder
+
+    peer = Holder(data_dir, lazy_fragments=True).open()
+    n = 0
+    for iname, pidx in peer.indexes.items():
+        idx = holder.index(iname)
+        if idx is None:
+            continue
+        for fname, pf in pidx.fields.items():
+            f = idx.field(fname)
+            if f is None:
+                continue
+            for vname, pv in pf.views.items():
+                v = f.create_view_if_not_exists(vname)
+                for shard, frag in list(pv.fragments.items()):
+                    if shard in v.fragments:
+                        continue
+                    v.fragments[shard] = frag
+                    pv.fragments.pop(shard)
+                    f.local_shards.add(int(shard))
+                    n += 1
+    return n
+
+
 def _opt_dict(opt) -> dict:
     if opt is None:
         return {}
@@ -327,21 +393,12 @@ def dist_env():
     return rank, world, local
 
 
-def init_process_group(local_rank: int, backend: Optional[str] = None):
-    """One process per GPU: RCCL ("nccl") when GPUs are visible, else gloo."""
-    import torch
-    import torch.distributed as dist
+def init_process_group(local_rank: int, backend: Optional[str] = None, timeout_s: float = 120.0):
+    """One process per GPU: RCCL ("nccl") when GPUs are visible, else gloo,
+    with a collective timeout (parallel/collectives.py init)."""
+    from .collectives import init
 
-    if dist.is_initialized():
-        return dist.get_backend()
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        dist.init_process_group(backend)
-    return backend
+    return init(backend, local_rank, timeout_s)
 
 
 def rank_data_dir(data_dir: str, rank: int) -> str:
@@ -352,7 +409,7 @@ def rank_data_dir(data_dir: str, rank: int) -> str:
     return data_dir if rank == 0 else os.path.join(data_dir, f".rank{rank}")
 
 
-def run_worker(data_dir: str, gpu_mode: str = "auto", block: int = 1, logger=None) -> int:
+def run_worker(data_dir: str, gpu_mode: str = "auto", block: int = 1, logger=None, timeout_s: float = 120.0) -> int:
     """Entry point of ranks > 0 of a multi-GPU server (``pilosa_amd server``
     under ``torch.distributed.run``): own holder + GPU engine, serve the mesh."""
     import torch
@@ -362,8 +419,9 @@ def run_worker(data_dir: str, gpu_mode: str = "auto", block: int = 1, logger=Non
     from pilosa_amd.models.holder import Holder
 
     rank, world, local = dist_env()
-    init_process_group(local)
-    holder = Holder(rank_data_dir(data_dir, rank)).open()
+    init_process_group(local, timeout_s=timeout_s)
+    use_gpu = (gpu_mode or "auto").lower() not in ("off", "none", "cpu") and torch.cuda.is_available()
+    holder = Holder(rank_data_dir(data_dir, rank), lazy_fragments=use_gpu).open()
     gpu = None
     if (gpu_mode or "auto").lower() not in ("off", "none", "cpu") and torch.cuda.is_available():
         from pilosa_amd.ops.gpu_executor import GpuExecutor

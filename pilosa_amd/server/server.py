@@ -38,6 +38,14 @@ from pilosa_amd.utils.logger import NopLogger, StandardLogger
 from pilosa_amd.utils.stats import NopStatsClient, new_stats_client
 
 
+def _gpu_present() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        return False
+
+
 class Server:
     def __init__(self, data_dir: str, bind: str = "127.0.0.1:10101", node_id: Optional[str] = None,
                  replica_n: int = 1, hosts: Optional[List[str]] = None, coordinator: bool = True,
@@ -47,12 +55,18 @@ class Server:
                  max_opn: int = 10000, cluster_disabled: bool = False, mesh_block: int = 1,
                  translation_primary_url: str = "", tls_certificate: str = "", tls_key: str = "",
                  tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
-                 gpu_device: Optional[int] = None, hbm_budget: int = 0):
+                 gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
+                 lazy_fragments: Optional[bool] = None):
         self.data_dir = data_dir
+        self.mesh_timeout_s = mesh_timeout_s
         self.bind = bind
         self.logger = logger or StandardLogger()
         self.stats = new_stats_client(stats) if isinstance(stats, str) else (stats or NopStatsClient())
-        self.holder = Holder(data_dir, max_opn=max_opn, stats=self.stats)
+        # a GPU node reads cold fragments straight into HBM (ops/loader.py); the
+        # host copy of a fragment is only materialised when a host path needs it
+        if lazy_fragments is None or lazy_fragments:
+            lazy_fragments = (gpu or "auto").lower() not in ("off", "none", "cpu") and _gpu_present()
+        self.holder = Holder(data_dir, max_opn=max_opn, stats=self.stats, lazy_fragments=lazy_fragments)
         self.client = InternalClient()
         # liveness probes use a short timeout so a hung peer is noticed quickly
         # (reference confirmNodeDown: 2 s per /version attempt, cluster.go:1699-1726)
@@ -188,8 +202,9 @@ class Server:
             return
         if rank != 0:
             raise RuntimeError("Server must run on rank 0; other ranks run parallel.mesh.run_worker")
-        M.init_process_group(local)
-        self.mesh = M.ShardMesh(self.executor, block=self.mesh_block)
+        M.init_process_group(local, timeout_s=self.mesh_timeout_s)
+        self.mesh = M.ShardMesh(self.executor, block=self.mesh_block,
+                                peer_dirs={r: M.rank_data_dir(self.data_dir, r) for r in range(world)})
         self.executor.mesh = self.mesh
         self.mesh.apply_schema()
 

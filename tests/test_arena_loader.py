@@ -124,11 +124,10 @@ def test_lazy_fragment_close_keeps_files_and_cache():
     env = Env()
     try:
         _populate(env)
-        env.holder.flush_caches()
         frags = _frags(env)
+        env.holder.close()  # drains the snapshot queue, flushes caches
         sizes = [os.path.getsize(fr.path) for fr in frags]
         caches = [open(fr.cache_path(), "rb").read() for fr in frags]
-        env.holder.close()
         env.holder = Holder(env.dir, lazy_fragments=True).open()
         env.holder.flush_caches()
         env.holder.close()

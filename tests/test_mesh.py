@@ -131,7 +131,7 @@ def _worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_mesh_matches_single_process(world, tmp_path):
     from pilosa_amd.executor import Executor
     from pilosa_amd.models.holder import Holder
@@ -157,3 +157,71 @@ def test_mesh_matches_single_process(world, tmp_path):
     assert set().union(*owned) == set(range(6))
     for r in range(world):
         assert all(s % world == r for s in owned[r]), (r, owned[r])
+
+
+def _failover_worker(rank, world, port, outdir):
+    """Rank 1 serves the load phase, then dies without a clean shutdown; rank 0
+    must notice on its next collective (timeout / peer loss), adopt rank 1's
+    fragment files from its data dir and keep answering every query."""
+    import datetime as dt
+
+    import torch.distributed as dist
+
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=dt.timedelta(seconds=15))
+    dirs = {r: os.path.join(outdir, f"rank{r}") for r in range(world)}
+    holder = Holder(dirs[rank]).open()
+    ex = Executor(holder)
+    mesh = ShardMesh(ex, block=1, peer_dirs=dirs)
+    ex.mesh = mesh
+    if rank != 0:
+        mesh.serve()            # until the front end's stop below
+        ex.close()
+        holder.close()          # releases the fragment flocks, like a dead process
+        os._exit(0)             # no destroy_process_group: the peer just vanishes
+    _setup_schema(holder)
+    mesh.apply_schema()
+    bits, vals = _data()
+    _load(ex, bits, vals, mesh)
+    before = [_canon(ex.execute("i", q).results) for q in QUERIES]
+    mesh.stop()
+    import time
+    time.sleep(1.0)
+    after = [_canon(ex.execute("i", q).results) for q in QUERIES]
+    with open(os.path.join(outdir, "failover.json"), "w") as fh:
+        json.dump({"before": before, "after": after, "failed_over": mesh.failed_over,
+                   "error": mesh.failover_error, "mesh_detached": ex.mesh is None}, fh)
+    ex.close()
+    holder.close()
+    os._exit(0)
+
+
+def test_mesh_failover_adopts_dead_rank_shards(tmp_path):
+    mp.start_processes(_failover_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    res = json.load(open(tmp_path / "failover.json"))
+    assert res["failed_over"] and res["mesh_detached"], res["error"]
+    assert res["after"] == res["before"]
+
+
+def test_result_codec_round_trip():
+    from pilosa_amd.executor import FieldRow, GroupCount, RowIdentifiers, ValCount
+    from pilosa_amd.models.cache import Pair
+    from pilosa_amd.models.row import Row
+    from pilosa_amd.parallel.collectives import RemoteError, decode, encode
+    r = Row(np.array([1, 5, 3 << 20], np.uint64))
+    r.attrs = {"x": 1}
+    objs = [3, None, True, [Pair(1, 2), Pair(3, 4, "k")], ValCount(-5, 6),
+            [GroupCount([FieldRow("f", 1), FieldRow("g", 2, "x")], 7)], RowIdentifiers([1, 2], ["a", "b"]),
+            {"i": [1, 2]}]
+    for o in objs:
+        assert decode(encode(o)) == o
+    got = decode(encode(r))
+    assert [int(c) for c in got.columns()] == [1, 5, 3 << 20] and got.attrs == {"x": 1}
+    e = decode(encode(ValueError("boom")))
+    assert isinstance(e, RemoteError) and "boom" in str(e)
