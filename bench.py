@@ -542,7 +542,7 @@ def main():
     ap.add_argument("--cols", type=int, default=TOTAL_COLS)
     ap.add_argument("--rows", type=int, default=NROWS)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--clients", type=int, default=2, help="disk mode: concurrent request threads")
+    ap.add_argument("--clients", type=int, default=3, help="disk mode: concurrent request threads")
     ap.add_argument("--data-dir", default=None, help="disk mode: reuse/keep fragment files under this dir")
     ap.add_argument("--keep-data", action="store_true")
     ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")

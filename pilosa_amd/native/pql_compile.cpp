@@ -20,7 +20,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cctype>
+#include <thread>
+#include <tuple>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -267,6 +270,216 @@ py::object compile_count_text(const std::string& text, const std::unordered_map<
   return py::make_tuple(progs, Q);
 }
 
+// ---------------------------------------------------------------- batch planner
+// plan_count_text(text, fields, dirs, use_and2, use_union, nthreads): the host
+// half of a count batch in one native call (the numpy version is
+// ops/device.py GpuEngine.prepare_progs): compile every Count() call of the
+// request, canonicalise Intersect(a, a), classify each program by kernel
+// route, put the batch's more frequent row first in Count(Intersect(a, b))
+// (the pair kernel stages leaf 0 once per run of equal rows), sort each
+// route's programs by (leaf row 0, leaf row 1) and lay them out with their
+// submission indices in one buffer ready for a single H2D copy.
+// -> (Q, [(kind, n, progs_off, order_off)], buf uint8[]) or None.
+enum Kind { K_AND2 = 0, K_ROW = 1, K_GENERIC = 2, K_FLAT = 3, K_UNION = 4 };
+
+static bool is_flat(const QueryProg& p) {
+  const int n = p.nprog;
+  if (n < 3 || (n % 2) == 0) return false;
+  for (int i = 0; i < n; i++) {
+    const bool want_leaf = i == 0 || (i % 2 == 1);
+    if ((p.prog[i] < OP_AND) != want_leaf) return false;
+  }
+  return true;
+}
+
+py::object plan_count_text(const std::string& text, const std::unordered_map<std::string, int>& fields,
+                           const std::vector<py::array_t<uint64_t, py::array::c_style | py::array::forcecast>>& dirs,
+                           bool use_and2, bool use_union, int nthreads) {
+  std::vector<View> views;
+  views.reserve(dirs.size());
+  for (const auto& d : dirs) {
+    View v;
+    v.rows = d.data();
+    v.D = d.size();
+    v.identity = v.D > 0 && v.rows[v.D - 1] == uint64_t(v.D - 1);
+    views.push_back(v);
+  }
+  for (const auto& kv : fields)
+    if (kv.second < 0 || kv.second >= int(views.size())) throw std::out_of_range("field slot out of range");
+  std::vector<QueryProg> progs;
+  std::vector<int> kind;
+  bool ok = true;
+  std::vector<uint8_t> buf;
+  std::vector<std::tuple<int, size_t, size_t, size_t>> segs;
+  {
+    py::gil_scoped_release nogil;
+    // 1. call boundaries (top-level parentheses), then compile in parallel
+    std::vector<std::pair<size_t, size_t>> calls;
+    {
+      size_t i = 0, n = text.size();
+      while (i < n) {
+        while (i < n && (text[i] == ' ' || text[i] == '\t' || text[i] == '\n' || text[i] == '\r')) i++;
+        if (i >= n) break;
+        const size_t b = i;
+        int depth = 0;
+        bool seen = false;
+        for (; i < n; i++) {
+          const char c = text[i];
+          if (c == '"' || c == '\'') {  // quoted strings: never in the native subset
+            ok = false;
+            break;
+          }
+          if (c == '(') depth++, seen = true;
+          else if (c == ')' && --depth == 0) {
+            i++;
+            break;
+          }
+          if (depth < 0) {
+            ok = false;
+            break;
+          }
+        }
+        if (!ok || !seen || depth != 0) {
+          ok = false;
+          break;
+        }
+        calls.emplace_back(b, i);
+      }
+    }
+    const size_t Q = calls.size();
+    ok = ok && Q > 0;
+    if (ok) {
+      progs.resize(Q);
+      std::vector<char> good(Q, 0);
+      auto work = [&](size_t lo, size_t hi) {
+        for (size_t q = lo; q < hi; q++) {
+          Compiler c(std::string_view(text).substr(calls[q].first, calls[q].second - calls[q].first), fields, views,
+                     progs[q]);
+          good[q] = c.run() ? 1 : 0;
+        }
+      };
+      const int nt = Q >= 1024 ? std::max(1, std::min(nthreads, 8)) : 1;
+      if (nt == 1) {
+        work(0, Q);
+      } else {
+        std::vector<std::thread> th;
+        const size_t per = (Q + nt - 1) / nt;
+        for (int t = 0; t < nt; t++) {
+          const size_t lo = std::min(Q, t * per), hi = std::min(Q, lo + per);
+          if (lo < hi) th.emplace_back(work, lo, hi);
+        }
+        for (auto& t : th) t.join();
+      }
+      for (size_t q = 0; q < Q && ok; q++) ok = good[q] != 0;
+    }
+    if (ok) {
+      // 2. canonicalise + classify
+      kind.resize(Q);
+      for (size_t q = 0; q < Q; q++) {
+        QueryProg& p = progs[q];
+        if (p.nprog == 3 && p.nleaf == 1 && p.prog[0] == 0 && p.prog[1] == 0 && p.prog[2] == OP_AND) {
+          p.nleaf = 2;
+          p.leaf_row[1] = p.leaf_row[0];
+          p.leaf_view[1] = p.leaf_view[0];
+          p.prog[1] = 1;
+        }
+        const bool and2 = p.nprog == 3 && p.prog[0] == 0 && p.prog[1] == 1 && p.prog[2] == OP_AND;
+        int k;
+        if (p.nprog == 1 || (and2 && !use_and2)) {
+          k = K_ROW;
+        } else if (and2) {
+          k = K_AND2;
+        } else if (is_flat(p)) {
+          bool all_or = true;
+          for (int i = 2; i < p.nprog; i += 2) all_or = all_or && p.prog[i] == OP_OR;
+          k = (all_or && use_union) ? K_UNION : K_FLAT;
+        } else {
+          k = K_GENERIC;
+        }
+        kind[q] = k;
+      }
+      // 3. hot leaf first for Count(Intersect(a, b)): frequency of every
+      // (view, row) leaf over the pair programs (open-addressing hash count)
+      size_t cap = 16;
+      while (cap < Q * 4) cap <<= 1;
+      std::vector<uint64_t> hk(cap, ~0ull);
+      std::vector<uint32_t> hc(cap, 0);
+      auto slot = [&](uint64_t k) {
+        size_t h = size_t((k * 0x9E3779B97F4A7C15ull) >> 20) & (cap - 1);
+        while (hk[h] != ~0ull && hk[h] != k) h = (h + 1) & (cap - 1);
+        return h;
+      };
+      auto key_of = [](const QueryProg& p, int l) {
+        return ((uint64_t(uint32_t(p.leaf_view[l])) << 40) ^ uint64_t(p.leaf_row[l])) & ~(1ull << 63);
+      };
+      for (size_t q = 0; q < Q; q++)
+        if (kind[q] == K_AND2)
+          for (int l = 0; l < 2; l++) {
+            const uint64_t k = key_of(progs[q], l);
+            const size_t h = slot(k);
+            hk[h] = k;
+            hc[h]++;
+          }
+      std::vector<uint32_t> cnt(Q * 2, 0);
+      for (size_t q = 0; q < Q; q++)
+        if (kind[q] == K_AND2)
+          for (int l = 0; l < 2; l++) cnt[q * 2 + size_t(l)] = hc[slot(key_of(progs[q], l))];
+      for (size_t q = 0; q < Q; q++) {
+        if (kind[q] != K_AND2) continue;
+        QueryProg& p = progs[q];
+        const uint64_t ka = (uint64_t(uint32_t(p.leaf_view[0])) << 40) ^ uint64_t(p.leaf_row[0]);
+        const uint64_t kb = (uint64_t(uint32_t(p.leaf_view[1])) << 40) ^ uint64_t(p.leaf_row[1]);
+        const uint32_t ca = cnt[q * 2], cb = cnt[q * 2 + 1];
+        if (cb > ca || (cb == ca && kb < ka)) {
+          std::swap(p.leaf_row[0], p.leaf_row[1]);
+          std::swap(p.leaf_view[0], p.leaf_view[1]);
+        }
+      }
+      // 4. per route: sort by (leaf row 0, leaf row 1, submission), lay out
+      const int route_order[5] = {K_AND2, K_ROW, K_FLAT, K_UNION, K_GENERIC};
+      struct SortKey {
+        int64_t r0, r1;
+        int64_t q;
+        bool operator<(const SortKey& o) const {
+          return r0 != o.r0 ? r0 < o.r0 : (r1 != o.r1 ? r1 < o.r1 : q < o.q);
+        }
+      };
+      std::vector<std::vector<SortKey>> sel(5);
+      for (size_t q = 0; q < Q; q++)
+        sel[size_t(kind[q])].push_back({progs[q].leaf_row[0], progs[q].leaf_row[1], int64_t(q)});
+      size_t total = 0;
+      auto align = [](size_t x) { return (x + 255) & ~size_t(255); };
+      for (int r : route_order) {
+        auto& v = sel[size_t(r)];
+        if (v.empty()) continue;
+        std::sort(v.begin(), v.end());
+        const size_t po = total;
+        total = align(total + v.size() * sizeof(QueryProg));
+        const size_t oo = total;
+        total = align(total + v.size() * 8);
+        segs.emplace_back(r, v.size(), po, oo);
+      }
+      buf.resize(std::max<size_t>(total, 256));
+      for (auto& sg : segs) {
+        const auto& v = sel[size_t(std::get<0>(sg))];
+        QueryProg* dst = reinterpret_cast<QueryProg*>(buf.data() + std::get<2>(sg));
+        int64_t* ord = reinterpret_cast<int64_t*>(buf.data() + std::get<3>(sg));
+        for (size_t i = 0; i < v.size(); i++) {
+          dst[i] = progs[size_t(v[i].q)];
+          ord[i] = v[i].q;
+        }
+      }
+    }
+  }
+  if (!ok) return py::none();
+  py::array_t<uint8_t> out(buf.size());
+  std::memcpy(out.mutable_data(), buf.data(), buf.size());
+  py::list sl;
+  for (auto& sg : segs)
+    sl.append(py::make_tuple(std::get<0>(sg), std::get<1>(sg), std::get<2>(sg), std::get<3>(sg)));
+  return py::make_tuple(progs.size(), sl, out);
+}
+
 // Field names of the Row(field=...) leaves of a request (distinct, first-seen
 // order); views for them are resolved before compile_count_text.
 std::vector<std::string> count_text_fields(const std::string& text) {
@@ -299,6 +512,10 @@ void register_compile(py::module_& m) {
         "Compile a request of top-level Count(<Row/Intersect/Union/Difference/Xor tree>) calls straight to "
         "QueryProg records; (progs uint8[Q*256], Q), or None when a call needs the general path");
   m.def("count_text_fields", &count_text_fields, py::arg("text"));
+  m.def("plan_count_text", &plan_count_text, py::arg("text"), py::arg("fields"), py::arg("dirs"),
+        py::arg("use_and2") = true, py::arg("use_union") = true, py::arg("nthreads") = 4,
+        "Compile + classify + order a request of Count() calls into one H2D-ready buffer; "
+        "(Q, [(kind, n, progs_off, order_off)], buf) or None");
   m.def("compile_counts", &compile_counts, py::arg("queries"), py::arg("fields"), py::arg("dirs"),
         "Compile Count(<Row/Intersect/Union/Difference/Xor tree>) PQL strings straight to QueryProg records; "
         "returns (progs uint8[Q*256], ok bool[Q]) -- rows with ok=False need the general path");

@@ -634,6 +634,23 @@ class GpuEngine:
         parts = [(dev[1 + 2 * i], dev[2 + 2 * i].view(torch.int64), k, n) for i, (k, n) in enumerate(meta)]
         return (Q, S, tv, parts)
 
+    def prepare_planned(self, Q: int, segs, buf: np.ndarray, views: List["DeviceView"], S: int):
+        """:meth:`prepare_progs` for a batch planned natively
+        (native/pql_compile.cpp plan_count_text): one pinned H2D copy of the
+        view table and the planner's buffer (routes' programs + submission
+        indices), no host-side numpy work."""
+        torch = self.torch
+        if not S or not Q:
+            return (Q, S, None, [])
+        varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
+        for i, v in enumerate(views):
+            varr[i] = v.viewdev()
+        tv, tb = self._h2d_many([varr.view(np.uint8), buf])
+        parts = []
+        for kind, n, po, oo in segs:
+            parts.append((tb[po:po + n * QPROG_DTYPE.itemsize], tb[oo:oo + n * 8].view(torch.int64), int(kind), int(n)))
+        return (Q, S, tv, parts)
+
     @staticmethod
     def _hot_leaf_first(progs: np.ndarray, sel: np.ndarray) -> np.ndarray:
         """For Count(Intersect(a, b)) put the row used most often in the batch

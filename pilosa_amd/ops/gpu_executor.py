@@ -75,6 +75,7 @@ class GpuExecutor:
         self.file_loader = os.environ.get("PILOSA_FILE_LOADER", "1") != "0"
         self.cold_loads = 0
         self.last_load: Dict = {}
+        self.plan_threads = int(os.environ.get("PILOSA_PLAN_THREADS", "4"))
         self.topn_index_enabled = os.environ.get("PILOSA_TOPN_INDEX", "1") != "0"
         self._topn_indexes: Dict[Tuple, Tuple] = {}  # (index, field, shards) -> (versions, index, built_at)
 
@@ -485,14 +486,16 @@ class GpuExecutor:
         if not views:
             return None
         vlist = list(views.values())
-        got = _pql.compile_count_text(text, {n: i for i, n in enumerate(views)}, [v.rows for v in vlist])
+        eng = self.engine
+        use_and2 = eng.use_and2 and max(v.container_count for v in vlist) < 0xFFFFFFFF
+        # rows absent from a view compile to dense -1 (empty leaf)
+        got = _pql.plan_count_text(text, {n: i for i, n in enumerate(views)}, [v.rows for v in vlist],
+                                   use_and2, eng.use_union, self.plan_threads)
         if got is None:
             return None
-        raw, Q = got
-        from .device import QPROG_DTYPE
-        progs = raw.view(QPROG_DTYPE)  # rows absent from a view compile to dense -1 (empty leaf)
+        Q, segs, buf = got
         self.launches += 1
-        return self.engine.launch_count(self.engine.prepare_progs(progs, vlist, vlist[0].S)).cpu().tolist()
+        return eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S)).cpu().tolist()
 
     def try_count_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
         """Many Count() calls of one request -> one launch; calls whose tree

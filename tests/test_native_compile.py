@@ -104,3 +104,49 @@ def test_count_text_equals_per_query(views):
     for bad in ("Count(Row(f=1)) TopN(f)", "Count(Row(f=1)) Count(Row(n > 3))", "", "Count(Row(f=1)) x",
                 "Count(Row(f=1)) Count(Row(zz=1))", "Count(Row(f=1)) Count(Row(f=\"a\"))"):
         assert _pql.compile_count_text(bad, fields, dirs) is None, bad
+
+
+def test_plan_count_text_matches_numpy_planner(views):
+    """plan_count_text (native planner) == compile_counts + the numpy route
+    classification / ordering of GpuEngine.prepare_progs, up to the
+    orientation of Count(Intersect(a, b)) (a count is symmetric)."""
+    from pilosa_amd import _pql
+    from pilosa_amd.ops.device import OP_AND, flat_mask
+    rng = np.random.default_rng(5)
+    qs = [f"Count({_gen(rng)})" for _ in range(2500)]
+    qs += ["Count(Intersect(Row(f=3), Row(f=3)))", "Count(Row(f=7))", "Count(Union(Row(f=1), Row(g=9), Row(f=2)))"]
+    fields = {"f": 0, "g": 1}
+    dirs = [views["f"].rows, views["g"].rows]
+    Q, segs, buf = _pql.plan_count_text("\n".join(qs), fields, dirs, True, True, 4)
+    assert Q == len(qs)
+    raw, ok = _pql.compile_counts(qs, fields, dirs)
+    want = raw.view(QPROG_DTYPE)
+    seen = np.zeros(Q, bool)
+    for kind, n, po, oo in segs:
+        progs = buf[po:po + n * 256].view(QPROG_DTYPE)
+        order = buf[oo:oo + n * 8].view(np.int64)
+        assert not seen[order].any()
+        seen[order] = True
+        lr = progs["leaf_row"]
+        key = [(int(a), int(b)) for a, b in zip(lr[:, 0], lr[:, 1])]
+        assert key == sorted(key)
+        for p, q in zip(progs, order):
+            w = want[q]
+            pg, n_ = p["prog"], int(p["nprog"])
+            is_and2 = n_ == 3 and pg[0] == 0 and pg[1] == 1 and pg[2] == OP_AND
+            if kind == 0:
+                assert is_and2
+                a = sorted([(int(p["leaf_view"][i]), int(p["leaf_row"][i])) for i in range(2)])
+                wl = [(int(w["leaf_view"][i]), int(w["leaf_row"][i])) for i in range(int(w["nleaf"]))]
+                assert a == sorted(wl * (2 if len(wl) == 1 else 1))
+            elif kind == 1:
+                assert n_ == 1 and p.tobytes() == w.tobytes()
+            else:
+                assert p.tobytes() == w.tobytes()
+                fm = bool(flat_mask(w.reshape(1))[0])
+                assert (kind in (3, 4)) == fm
+                if kind == 4:
+                    assert all(pg[i] == 33 for i in range(2, n_, 2))
+    assert seen.all()
+    assert _pql.plan_count_text("Count(Row(f=1)) TopN(f)", fields, dirs, True, True, 4) is None
+    assert _pql.plan_count_text("Count(Row(f=\"a\"))", fields, dirs, True, True, 4) is None
