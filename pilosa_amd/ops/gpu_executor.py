@@ -829,49 +829,134 @@ class GpuExecutor:
                 return []
         prev = ex.group_by_previous(c)
         if k == 2 and len(cand[0]) * len(cand[1]) >= GROUPBY_MATRIX_MIN and \
-                (fexpr is None or type(fexpr) is Leaf):
+                (fexpr is None or type(fexpr) is Leaf) and self._matrix_fits(len(cand[0]), len(cand[1])):
             # two fields: the whole count matrix in one bit-GEMM (MFMA), then
             # the lexicographic walk on the host (ops/groupby.py)
             from .groupby import emit_groups, pair_count_matrix
             self.launches += 1
             mat = pair_count_matrix(arenas[0], cand[0], arenas[1], cand[1],
-                                    filt=(fexpr.view, fexpr.row) if fexpr is not None else None)
+                                    filt=(fexpr.view, fexpr.row) if fexpr is not None else None,
+                                    chunk_bytes=self._groupby_budget() - len(cand[0]) * len(cand[1]) * 12)
             return [GroupCount([FieldRow(fields[0], ra), FieldRow(fields[1], rb)], n)
                     for ra, rb, n in emit_groups(cand[0], cand[1], mat, prev, limit)]
-        results: List[GroupCount] = []
-        # enumerate combos lexicographically in chunks; stop at `limit`
-        batch_keys: List[Tuple[int, ...]] = []
-
-        def flush():
-            if not batch_keys:
-                return False
-            exprs = []
-            for key in batch_keys:
-                leaves = [Leaf(arenas[i], key[i]) for i in range(k)]
-                if fexpr is not None:
-                    leaves = [fexpr] + leaves
-                exprs.append(leaves[0] if len(leaves) == 1 else Op("and", tuple(leaves)))
-            self.launches += 1
-            got = self.engine.count(exprs)
-            for key, v in zip(batch_keys, got):
-                if v > 0:
-                    results.append(GroupCount([FieldRow(fields[i], key[i]) for i in range(k)], int(v)))
-                    if len(results) >= limit:
-                        batch_keys.clear()
-                        return True
-            batch_keys.clear()
-            return False
-
         try:
-            for key in _lex_product(cand, prev):
-                batch_keys.append(key)
-                if len(batch_keys) >= MAX_GROUPS_PER_LAUNCH:
-                    if flush():
-                        return results
-            flush()
+            groups = self._pruned_groups(arenas, cand, fexpr, prev, limit)
         except CompileError:
             raise NotImplementedError
-        return results[:limit]
+        return [GroupCount([FieldRow(fields[i], key[i]) for i in range(k)], n) for key, n in groups]
+
+    # HBM the two-field count matrix may use (densified rows + the matrix)
+    GROUPBY_HBM = int(os.environ.get("PILOSA_GROUPBY_HBM", str(8 << 30)))
+
+    def _groupby_budget(self) -> int:
+        budget = self.GROUPBY_HBM
+        if self.device.type == "cuda":
+            import torch
+            free, _ = torch.cuda.mem_get_info(self.device)
+            budget = min(budget, int(free * 0.5))
+        return budget
+
+    def _matrix_fits(self, ra: int, rb: int) -> bool:
+        """The count matrix densifies (ra + rb) rows x 128 KiB for at least one
+        shard and keeps an ra x rb int64+int32 matrix; two 1M-row fields would
+        need terabytes -> the pruned enumeration instead."""
+        from .groupby import WORDS_PER_SHARD
+        need = (ra + rb) * WORDS_PER_SHARD * 8 + ra * rb * 12
+        return need <= self._groupby_budget()
+
+    def _pruned_groups(self, arenas, cand, fexpr, prev, limit: int):
+        """GroupBy combinations in lexicographic order with cumulative-
+        intersection pruning (reference groupByIterator, executor.go:3060-3230):
+        a prefix whose intersection (with the filter) is empty is never
+        extended.  The work list holds (prefix, next row index) items in
+        lexicographic order; each launch counts the next children of the
+        front items (1024 per launch at first, doubling up to
+        MAX_GROUPS_PER_LAUNCH), so the output order is lexicographic and the
+        walk stops as soon as ``limit`` groups exist -- two 1M-row fields with
+        limit=100 cost a couple of launches, not a 10^12-cell matrix."""
+        k = len(cand)
+        out: List[Tuple[Tuple[int, ...], int]] = []
+        todo: List[Tuple[Tuple[int, ...], int]] = [((), 0)]
+        budget = 1024
+        while todo and len(out) < limit:
+            lvl = len(todo[0][0])
+            keys: List[Tuple[int, ...]] = []
+            rest: List[Tuple[Tuple[int, ...], int]] = []
+            i = 0
+            while i < len(todo) and len(todo[i][0]) == lvl and len(keys) < budget:
+                pre, j = todo[i]
+                rows = self._next_rows(cand[lvl], pre, prev)
+                take = rows[j:j + budget - len(keys)]
+                keys.extend(pre + (r,) for r in take)
+                if j + len(take) < len(rows):
+                    rest.append((pre, j + len(take)))  # unfinished: its remaining children come next
+                    i += 1
+                    break
+                i += 1
+            todo = rest + todo[i:]
+            budget = min(budget * 2, MAX_GROUPS_PER_LAUNCH)
+            if not keys:
+                continue
+            self.launches += 1
+            got = self._count_keys(arenas, keys, fexpr)
+            live = [(key, int(v)) for key, v in zip(keys, got) if v > 0]
+            if lvl + 1 == k:
+                for key, v in live:
+                    if prev is not None and key <= prev:
+                        continue
+                    out.append((key, v))
+                    if len(out) >= limit:
+                        break
+            else:
+                # children go before everything after their parents; an
+                # unfinished parent's remaining children come after them
+                todo = [(key, 0) for key, _ in live] + todo
+        return out[:limit]
+
+    def _count_keys(self, arenas, keys: List[Tuple[int, ...]], fexpr) -> np.ndarray:
+        """|filter & row_0 & ... & row_l| for every key of one level: programs
+        built column-wise with numpy (a left AND-fold over the leaves) instead
+        of one expression object per key; a non-leaf filter goes through the
+        expression compiler."""
+        from .device import OP_AND, QPROG_DTYPE
+        if fexpr is not None and type(fexpr) is not Leaf:
+            exprs = [Op("and", (fexpr, *[Leaf(arenas[x], key[x]) for x in range(len(key))])) for key in keys]
+            return self.engine.count(exprs)
+        L0 = 1 if fexpr is not None else 0
+        lvl = len(keys[0])
+        L = L0 + lvl
+        views: List[DeviceView] = []
+        slot_of: Dict[int, int] = {}
+
+        def slot(v):
+            if id(v) not in slot_of:
+                slot_of[id(v)] = len(views)
+                views.append(v)
+            return slot_of[id(v)]
+        Q = len(keys)
+        progs = np.zeros(Q, dtype=QPROG_DTYPE)
+        progs["nleaf"] = L
+        progs["nprog"] = 2 * L - 1
+        kk = np.asarray(keys, dtype=np.uint64).reshape(Q, lvl)
+        if fexpr is not None:
+            progs["leaf_view"][:, 0] = slot(fexpr.view)
+            progs["leaf_row"][:, 0] = fexpr.view.dense(fexpr.row)
+        for x in range(lvl):
+            progs["leaf_view"][:, L0 + x] = slot(arenas[x])
+            progs["leaf_row"][:, L0 + x] = arenas[x].dense_many(kk[:, x])
+        pg = [0] + [v for i in range(1, L) for v in (i, OP_AND)]
+        progs["prog"][:, :len(pg)] = np.asarray(pg, np.uint8)
+        eng = self.engine
+        return eng.launch_count(eng.prepare_progs(progs, views, views[0].S)).cpu().numpy()
+
+    @staticmethod
+    def _next_rows(rows: List[int], prefix: Tuple[int, ...], prev: Optional[Tuple[int, ...]]) -> List[int]:
+        """Rows of the next field for ``prefix``: while the prefix equals
+        ``prev``'s, only rows from prev's row on (paging)."""
+        if prev is None or tuple(prev[:len(prefix)]) != prefix:
+            return rows
+        lo = prev[len(prefix)]
+        return [r for r in rows if r >= lo]
 
 
 def _has_shift(e) -> bool:
@@ -915,24 +1000,6 @@ def _rebase_spill(bm):
     out = _roaring.Bitmap()
     out.add_many(cols)
     return out
-
-
-def _lex_product(cand: List[List[int]], prev: Optional[Tuple[int, ...]]):
-    k = len(cand)
-
-    def rec(level, prefix):
-        for r in cand[level]:
-            key = prefix + (r,)
-            if prev is not None and key < prev[:len(key)]:
-                continue
-            if level == k - 1:
-                if prev is not None and key <= prev:
-                    continue
-                yield key
-            else:
-                yield from rec(level + 1, key)
-
-    yield from rec(0, ())
 
 
 class _NeedMore(Exception):

@@ -1,14 +1,31 @@
 """Host half of the two-field GroupBy count-matrix path (ops/groupby.py
 emit_groups): lexicographic order, previous/limit paging and zero skipping
-must equal the reference walk (executor.go:1241-1442) that
-gpu_executor._lex_product implements."""
+must equal the reference walk (executor.go:1241-1442), written out below as
+a plain lexicographic product."""
 import itertools
 
 import numpy as np
 import pytest
 
 from pilosa_amd.ops.groupby import emit_groups
-from pilosa_amd.ops.gpu_executor import _lex_product
+
+
+def _lex_product(cand, prev):
+    k = len(cand)
+
+    def rec(level, prefix):
+        for r in cand[level]:
+            key = prefix + (r,)
+            if prev is not None and key < prev[:len(key)]:
+                continue
+            if level == k - 1:
+                if prev is not None and key <= prev:
+                    continue
+                yield key
+            else:
+                yield from rec(level + 1, key)
+
+    yield from rec(0, ())
 
 
 def _walk(cand_a, cand_b, counts, prev, limit):
