@@ -229,6 +229,157 @@ def bench_cpu_host(args, ra, rb, nshards, nq=256):
             "qps_per_core": round(1.0 / per_q_all_shards, 3)}
 
 
+def _timed(fn, reps, world, dev):
+    """(seconds per call, max over ranks, last result) with a device sync."""
+    import torch
+    import torch.distributed as dist
+    fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize(dev)
+    el = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+    if world > 1:
+        all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item()), out
+
+
+def bench_bsi(args, world, rank, dev):
+    """BASELINE config 4: a BSI int field over the same 1B columns (half of
+    them hold a value uniform in [-1000, 1e6], bit depth 20): Sum, range
+    counts, Min/Max, and Sum for a batch of 32 filters on the per-filter
+    VALU kernel vs the bit-plane matrix product on the matrix cores
+    (ops/bsi.py).  Every rank evaluates its shard range; sums/counts are
+    all-reduced."""
+    import torch
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.ops.bsi import bsi_sum_matrix
+    from pilosa_amd.ops.device import DeviceView, GpuEngine, Leaf
+
+    nshards = math.ceil(args.cols / SHARD_WIDTH)
+    lo, hi = nshards * rank // world, nshards * (rank + 1) // world
+    depth, vmin, vmax = 20, -1000, 1_000_000
+    t0 = time.time()
+    arena = _roaring.gen_bsi_arena(lo, hi, args.cols, depth, 0.5, vmin, vmax, 7, args.threads)
+    bv = DeviceView(*arena, dev, shards=list(range(lo, hi)))
+    farena = _roaring.gen_zipf_arena(lo, hi, args.cols, 1000, 1.0, 1.6, 50.0, 11, args.threads)
+    fv = DeviceView(*farena, dev, shards=list(range(lo, hi)))
+    del arena, farena
+    gen_s = time.time() - t0
+    eng = GpuEngine(dev)
+    rng = np.random.default_rng(5)
+    reps = args.config_reps
+    res = {"config": "BSI int field v, 1B cols, depth 20, fill 0.5, values [-1000, 1e6]", "gen_s": round(gen_s, 1),
+           "hbm_bytes_per_gpu": bv.nbytes(), "queries": {}}
+
+    def red(*ts):
+        t = torch.stack([x.reshape(-1)[0].to(torch.int64) for x in ts])
+        if world > 1:
+            all_reduce(t)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def q_sum():
+        s, n = eng.bsi_sum_async([None], bv, depth)
+        return red(s, n)
+
+    def q_gt():
+        return red(eng.bsi_range_count_async(bv, depth, ">", int(rng.integers(0, vmax))))[0]
+
+    def q_between():
+        a = int(rng.integers(0, 900_000))
+        return red(eng.bsi_range_count_async(bv, depth, "between", a, a + 50_000))[0]
+
+    def q_minmax():
+        k = eng.bsi_minmax(None, bv, depth)
+        return int(k[..., 4].max())
+
+    FB = 32
+    frows = [int(r) for r in rng.integers(0, 200, size=FB)]
+    filters = [Leaf(fv, r) for r in frows]
+
+    def q_batch_valu():
+        s, n = eng.bsi_sum_async(filters, bv, depth, matrix=False)
+        t = torch.cat([s, n])
+        if world > 1:
+            all_reduce(t)
+        return t.cpu().numpy()
+
+    def q_batch_matrix(mode):
+        def fn():
+            s, n = bsi_sum_matrix(eng, filters, bv, depth, mode=mode)
+            t = torch.cat([s, n])
+            if world > 1:
+                all_reduce(t)
+            return t.cpu().numpy()
+        return fn
+
+    for name, fn in (("Sum(field=v)", q_sum), ("Count(Row(v > x))", q_gt), ("Count(Row(v >< [a,b]))", q_between),
+                     ("Max(field=v)", q_minmax)):
+        dt, out = _timed(fn, reps, world, dev)
+        res["queries"][name] = {"ms": round(dt * 1000, 3), "qps": round(1 / dt, 1), "sample": out}
+    dt_v, out_v = _timed(q_batch_valu, reps, world, dev)
+    res["queries"][f"Sum(Row(f=r), field=v) x{FB} per-filter kernel"] = {
+        "ms_per_batch": round(dt_v * 1000, 3), "qps": round(FB / dt_v, 1)}
+    agree = True
+    for mode, label in ((4, "MFMA 32x64 K-sliced tiles"), (3, "MFMA 64x64 tiles"), (2, "MFMA 128x128 tiles"),
+                        (0, "VALU popcount tiles")):
+        dt_m, out_m = _timed(q_batch_matrix(mode), reps, world, dev)
+        res["queries"][f"Sum(Row(f=r), field=v) x{FB} bit-plane matrix, {label}"] = {
+            "ms_per_batch": round(dt_m * 1000, 3), "qps": round(FB / dt_m, 1)}
+        agree = agree and bool(np.array_equal(out_v, out_m))
+    res["batched_sum_paths_agree"] = agree
+    s, n = q_sum()
+    res["check"] = {"count": n, "mean": s / max(n, 1), "expected_count": args.cols * 0.5,
+                    "expected_mean": (vmax + vmin) / 2}
+    del bv, fv
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_time_union(args, world, rank, dev):
+    """BASELINE config 5: a time field's range query over YMDH views =
+    Count(Union) of the covering views (here 2 day views + 5 hour views of a
+    1M-row Zipf field over 1B columns, the day views holding 4x the bits),
+    batches of 1024 queries on the union count kernel."""
+    import torch
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.ops.device import DeviceView, GpuEngine, Leaf, Op
+
+    nshards = math.ceil(args.cols / SHARD_WIDTH)
+    lo, hi = nshards * rank // world, nshards * (rank + 1) // world
+    t0 = time.time()
+    views = []
+    for k, bpc in enumerate([1.0, 1.0, 0.25, 0.25, 0.25, 0.25, 0.25]):
+        arena = _roaring.gen_zipf_arena(lo, hi, args.cols, args.rows, bpc, 1.6, 50.0, 100 + k, args.threads)
+        views.append(DeviceView(*arena, dev, shards=list(range(lo, hi))))
+        del arena
+    gen_s = time.time() - t0
+    eng = GpuEngine(dev)
+    rng = np.random.default_rng(9)
+    B = 1024
+
+    def q_union():
+        rows = zipf_rows(rng, B, args.rows)
+        t = eng.count_async([Op("or", tuple(Leaf(v, int(r)) for v in views)) for r in rows])
+        if world > 1:
+            all_reduce(t)
+        return int(t.sum().item())
+
+    dt, out = _timed(q_union, args.config_reps, world, dev)
+    res = {"config": "time field, Count(Row(t=r, from, to)) = Count(Union of 2 D + 5 H views), 1M rows x 1B cols",
+           "gen_s": round(gen_s, 1), "hbm_bytes_per_gpu": sum(v.nbytes() for v in views), "batch": B,
+           "ms_per_batch": round(dt * 1000, 2), "qps": round(B / dt, 1), "sample_sum": out}
+    del views
+    torch.cuda.empty_cache()
+    return res
+
+
 def host_pair_counts(bitmaps, pairs):
     """Host roaring oracle: counts[q, k] = |Row(a_q) & Row(b_q)| in shard k."""
     w = SHARD_WIDTH
@@ -552,6 +703,9 @@ def main():
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
     ap.add_argument("--topn-pairs-batches", type=int, default=1,
                     help="also time the pair-count src TopN path on this many batches (0 = skip)")
+    ap.add_argument("--configs", default=os.environ.get("PILOSA_BENCH_CONFIGS", "4,5"),
+                    help="also run BASELINE configs 4 (BSI) and 5 (time union) into extra (empty = skip)")
+    ap.add_argument("--config-reps", type=int, default=5)
     ap.add_argument("--cpu-baseline-shards", type=int, default=0,
                     help="also time the host C++ roaring executor on this many shards (extrapolated)")
     args = ap.parse_args()
@@ -568,6 +722,11 @@ def main():
 
     run = run_disk if args.mode == "disk" else run_synthetic
     elapsed, extra = run(args, world, rank, dev, queries, ra, rb)
+    torch.cuda.empty_cache()
+    if "4" in args.configs.split(","):
+        extra["config4_bsi"] = bench_bsi(args, world, rank, dev)
+    if "5" in args.configs.split(","):
+        extra["config5_time_union"] = bench_time_union(args, world, rank, dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         all_reduce(el, op=dist.ReduceOp.MAX)

@@ -284,7 +284,7 @@ void bitgemm(torch::Tensor A, torch::Tensor B, int64_t M, int64_t N, int64_t KW,
   TORCH_CHECK(A.scalar_type() == torch::kInt64 && A.numel() == M * KW, "A int64[M*KW]");
   TORCH_CHECK(B.scalar_type() == torch::kInt64 && B.numel() == N * KW, "B int64[N*KW]");
   TORCH_CHECK(C.scalar_type() == torch::kInt32 && C.numel() == M * N, "C int32[M*N]");
-  TORCH_CHECK(mode >= 0 && mode <= 2, "bitgemm mode");
+  TORCH_CHECK(mode >= 0 && mode <= 4, "bitgemm mode");
   pk::launch_bitgemm(reinterpret_cast<const uint64_t*>(A.data_ptr<int64_t>()),
                      reinterpret_cast<const uint64_t*>(B.data_ptr<int64_t>()), int(M), int(N), KW, int(splits),
                      int(mode), C.data_ptr<int32_t>(), cur_stream(A));

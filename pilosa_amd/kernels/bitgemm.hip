@@ -32,6 +32,16 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int BT = 64;            // output tile (rows of A and of B) per workgroup
+
+// 16 k-bits -> 16 bytes of 0/1: per nibble one 24-bit multiply spreads
+// bits 0..3 to bits 0, 8, 16, 24 (x * 0x204081, no carries) and a mask keeps
+// them: 3 full-rate VALU ops per 4 bits, no LDS traffic.
+__device__ __forceinline__ v4i unpack16(uint32_t x) {
+  v4i r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = int(__umul24((x >> (4 * i)) & 0xfu, 0x204081u) & 0x01010101u);
+  return r;
+}
 constexpr int KC_WORDS = 8;       // 512 bits per row per LDS chunk
 constexpr int KC_BYTES = KC_WORDS * 8;
 
@@ -81,7 +91,23 @@ __global__ __launch_bounds__(256) void bitgemm_kernel(const uint64_t* __restrict
       sb[srow][sw + 1] = vb.y;
     }
     __syncthreads();
-    if (MODE == 1) {
+    if (MODE == 3) {
+      // 64x64 workgroup tile, one 32x32 accumulator per wave, operands
+      // unpacked with 24-bit multiplies (unpack16); a wave whose rows or
+      // columns lie past M / N skips its MFMAs (skinny shapes, e.g. the
+      // Q filters x (2 depth + 1) planes of a batched BSI Sum)
+      if (m0 + wm < M && n0 + wn < N) {
+        const int r = lane & 31, h = lane >> 5;
+        const uint64_t* ar = &sa[wm + r][0];
+        const uint64_t* br = &sb[wn + r][0];
+#pragma unroll 4
+        for (int ks = 0; ks < KC_WORDS * 2; ks++) {
+          const uint32_t xa = uint32_t(ar[ks >> 1] >> (32 * (ks & 1))) >> (16 * h);
+          const uint32_t xb = uint32_t(br[ks >> 1] >> (32 * (ks & 1))) >> (16 * h);
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(unpack16(xa), unpack16(xb), acc, 0, 0, 0);
+        }
+      }
+    } else if (MODE == 1) {
       const int r = lane & 31, h = lane >> 5;
       const uint8_t* ar = reinterpret_cast<const uint8_t*>(&sa[wm + r][0]);
       const uint8_t* br = reinterpret_cast<const uint8_t*>(&sb[wn + r][0]);
@@ -112,19 +138,9 @@ __global__ __launch_bounds__(256) void bitgemm_kernel(const uint64_t* __restrict
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     const int m = m0 + wm + (i & 3) + 8 * (i >> 2) + 4 * h, n = n0 + wn + c;
-    const int v = MODE == 1 ? acc[i] : cnt[i];
+    const int v = MODE >= 1 ? acc[i] : cnt[i];
     if (m < M && n < N && v) atomicAdd(C + int64_t(m) * N + n, v);
   }
-}
-
-// 16 k-bits -> 16 bytes of 0/1: per nibble one 24-bit multiply spreads
-// bits 0..3 to bits 0, 8, 16, 24 (x * 0x204081, no carries) and a mask keeps
-// them: 3 full-rate VALU ops per 4 bits, no LDS traffic.
-__device__ __forceinline__ v4i unpack16(uint32_t x) {
-  v4i r;
-#pragma unroll
-  for (int i = 0; i < 4; i++) r[i] = int(__umul24((x >> (4 * i)) & 0xfu, 0x204081u) & 0x01010101u);
-  return r;
 }
 
 // MODE 2 (MFMA, default): each wave owns a 64x64 output tile (2x2 MFMA
@@ -195,6 +211,77 @@ __global__ __launch_bounds__(256) void bitgemm_mfma64_kernel(const uint64_t* __r
       }
 }
 
+// MODE 4 (MFMA, K-sliced skinny): workgroup tile 32 x 64 (rows of A x rows
+// of B, e.g. the Q <= 32 filters x 2*depth+1 planes of a batched BSI Sum).
+// The 4 waves do not split the tile but the k-steps of each staged chunk
+// (wave w takes steps w, w+4, ...), so no wave idles on a skinny shape and
+// every unpacked A operand feeds two MFMAs (both 32-column halves of B).
+// The waves' accumulators are summed in LDS before one set of atomics per
+// workgroup.
+constexpr int K4_WORDS = 32;  // 2048 bits per row per staged chunk
+
+__global__ __launch_bounds__(256) void bitgemm_kslice_kernel(const uint64_t* __restrict__ A,
+                                                             const uint64_t* __restrict__ B, int M, int N,
+                                                             int64_t KW, int64_t kw_per_split,
+                                                             int32_t* __restrict__ C) {
+  __shared__ uint64_t sa[32][K4_WORDS + 1];
+  __shared__ uint64_t sb[64][K4_WORDS + 1];
+  __shared__ int red[2][16][64];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tiles_n = (N + 63) / 64;
+  const int m0 = (blockIdx.x / tiles_n) * 32, n0 = (blockIdx.x % tiles_n) * 64;
+  const int64_t k0 = int64_t(blockIdx.y) * kw_per_split;
+  const int64_t k1 = k0 + kw_per_split < KW ? k0 + kw_per_split : KW;
+  v16i acc[2];
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[b][i] = 0;
+  for (int e = tid; e < 2 * 16 * 64; e += 256) (&red[0][0][0])[e] = 0;
+  const int r = lane & 31, h = lane >> 5;
+  for (int64_t kc = k0; kc < k1; kc += K4_WORDS) {
+    __syncthreads();
+    // 96 rows x 32 words: thread t stages 12 words
+#pragma unroll
+    for (int e = 0; e < 12; e++) {
+      const int idx = e * 256 + tid;  // 0 .. 3071
+      const int row = idx >> 5, w = idx & 31;
+      const int64_t kw = kc + w;
+      if (row < 32) {
+        sa[row][w] = (m0 + row < M && kw < k1) ? A[int64_t(m0 + row) * KW + kw] : 0ull;
+      } else {
+        const int rb = row - 32;
+        sb[rb][w] = (n0 + rb < N && kw < k1) ? B[int64_t(n0 + rb) * KW + kw] : 0ull;
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int ks = wave; ks < K4_WORDS * 2; ks += 4) {
+      const int sh = 32 * (ks & 1) + 16 * h;
+      const v4i av = unpack16(uint32_t(sa[r][ks >> 1] >> sh));
+      const v4i b0 = unpack16(uint32_t(sb[r][ks >> 1] >> sh));
+      const v4i b1 = unpack16(uint32_t(sb[32 + r][ks >> 1] >> sh));
+      acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, b1, acc[1], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 2; b++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) atomicAdd(&red[b][i][lane], acc[b][i]);
+  __syncthreads();
+  // 2 x 16 x 64 = 2048 outputs, 8 per thread
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const int o = e * 256 + tid;
+    const int b = o >> 10, i = (o >> 6) & 15, l = o & 63;
+    const int v = red[b][i][l];
+    const int m = m0 + (i & 3) + 8 * (i >> 2) + 4 * (l >> 5), n = n0 + 32 * b + (l & 31);
+    if (m < M && n < N && v) atomicAdd(C + int64_t(m) * N + n, v);
+  }
+}
+
 // Dense bit rows from an arena: out[r][(s - s0) * 16384 + j * 1024 + w] for
 // dense row rows[r] of view v, shards [s0, s1); absent containers are zero.
 // One wave per (row, shard, key).
@@ -260,14 +347,19 @@ void launch_bitgemm(const uint64_t* A, const uint64_t* B, int M, int N, int64_t 
                     int32_t* C, hipStream_t st) {
   if (M <= 0 || N <= 0 || KW <= 0) return;
   const int bt = mode == 2 ? BT2 : BT;
-  const int tiles = ((M + bt - 1) / bt) * ((N + bt - 1) / bt);
+  const int tiles = mode == 4 ? ((M + 31) / 32) * ((N + 63) / 64) : ((M + bt - 1) / bt) * ((N + bt - 1) / bt);
   if (splits < 1) splits = 1;
   int64_t per = (KW + splits - 1) / splits;
-  per = (per + KC_WORDS - 1) / KC_WORDS * KC_WORDS;
+  const int chunk = mode == 4 ? K4_WORDS : KC_WORDS;
+  per = (per + chunk - 1) / chunk * chunk;
   const int ns = int((KW + per - 1) / per);
   const dim3 grid(tiles, ns);
   if (mode == 2)
     hipLaunchKernelGGL(bitgemm_mfma64_kernel, grid, dim3(256), 0, st, A, B, M, N, KW, per, C);
+  else if (mode == 3)
+    hipLaunchKernelGGL(bitgemm_kernel<3>, grid, dim3(256), 0, st, A, B, M, N, KW, per, C);
+  else if (mode == 4)
+    hipLaunchKernelGGL(bitgemm_kslice_kernel, grid, dim3(256), 0, st, A, B, M, N, KW, per, C);
   else if (mode == 1)
     hipLaunchKernelGGL(bitgemm_kernel<1>, grid, dim3(256), 0, st, A, B, M, N, KW, per, C);
   else

@@ -936,9 +936,21 @@ class GpuEngine:
             self.ext.bsi_minmax(tp, tv, S, torch.from_numpy(args), out)
         return out.cpu().numpy().reshape(S, 16, 10)
 
-    def bsi_sum_async(self, filters: Sequence[Optional[object]], bsi_view: "DeviceView", depth: int):
-        """Sum/count of a BSI field for a batch of filters (None = no filter)."""
+    def bsi_sum_async(self, filters: Sequence[Optional[object]], bsi_view: "DeviceView", depth: int,
+                      matrix: Optional[bool] = None):
+        """Sum/count of a BSI field for a batch of filters (None = no filter).
+        Batches of BSI_MATRIX_MIN+ filters run as one bit-plane count matrix
+        on the matrix cores (ops/bsi.py); ``matrix`` forces either path."""
         torch = self.torch
+        if matrix is None:
+            from .bsi import BSI_MATRIX_MIN
+            matrix = len(filters) >= BSI_MATRIX_MIN
+        if matrix:
+            from .bsi import bsi_sum_matrix
+            try:
+                return bsi_sum_matrix(self, filters, bsi_view, depth)
+            except CompileError:
+                pass  # a filter the dense evaluator cannot take: per-filter kernel
         exprs = [f for f in filters if f is not None]
         view_index: Dict[int, int] = {id(bsi_view): 0}
         views = {id(bsi_view): bsi_view}

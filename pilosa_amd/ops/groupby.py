@@ -22,7 +22,7 @@ import numpy as np
 from .device import DeviceView, kernels
 
 WORDS_PER_SHARD = 1 << 14        # 2^20 bits
-MODE_VALU, MODE_MFMA_TABLE, MODE_MFMA = 0, 1, 2
+MODE_VALU, MODE_MFMA_TABLE, MODE_MFMA, MODE_MFMA_SKINNY, MODE_MFMA_KSLICE = 0, 1, 2, 3, 4
 # below this many rows on either side the 128x128 MFMA tiles run mostly empty
 # and the VALU kernel is faster (profiles/r01_groupby/bitgemm_bench.log)
 MFMA_MIN_ROWS = 96

@@ -521,3 +521,25 @@ def test_groupby_two_million_row_fields_limit():
     finally:
         env.executor.gpu = None
         env.close()
+
+
+@pytest.mark.parametrize("mode", [0, 2, 3, 4])
+def test_bsi_sum_matrix_matches_per_filter_kernel(envs, mode):
+    """Batched Sum as the bit-plane count matrix (ops/bsi.py, bitgemm VALU
+    and MFMA modes) == the per-filter bsi_sum kernel == the host executor."""
+    from pilosa_amd.ops.bsi import bsi_sum_matrix
+    from pilosa_amd.pql import parse_string
+    cpu, gpu = envs
+    shards = cpu.holder.index("i").available_shards()
+    bv = gpu.view_arena("i", "n", "bsig_n", shards)
+    depth = cpu.holder.index("i").field("n").bsi_group("n").bit_depth
+    qs = ["Row(f=0)", "Row(f=1)", "Row(g=2)", "Intersect(Row(f=0), Row(g=1))", None, "Row(f=999)",
+          "Union(Row(f=2), Row(f=20))", "Not(Row(f=3))"] * 3
+    filters = [None if q is None else gpu.plan("i", parse_string(q).calls[0], shards) for q in qs]
+    s0, n0 = gpu.engine.bsi_sum_async(filters, bv, depth, matrix=False)
+    s1, n1 = bsi_sum_matrix(gpu.engine, filters, bv, depth, mode=mode)
+    assert s0.cpu().tolist() == s1.cpu().tolist() and n0.cpu().tolist() == n1.cpu().tolist()
+    base = cpu.holder.index("i").field("n").bsi_group("n").base
+    for q, s, n in list(zip(qs, s1.cpu().tolist(), n1.cpu().tolist()))[:8]:
+        want = cpu.q1("i", f"Sum({q}, field=n)" if q else "Sum(field=n)")
+        assert (want.val, want.count) == (s + n * base, n), q
