@@ -224,6 +224,8 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
               "colptr int32[S*(2^20+1)]");
   TORCH_CHECK(entbase.scalar_type() == torch::kInt64 && entbase.numel() >= S, "entbase int64[S]");
   TORCH_CHECK(slots.scalar_type() == torch::kInt16, "slots int16");
+  TORCH_CHECK(slots.numel() >= 16 && slots.numel() % 8 == 0 && (reinterpret_cast<uintptr_t>(slots.data_ptr()) & 15) == 0,
+              "slots: 16-byte aligned, padded by 16 entries, multiple of 8");
   TORCH_CHECK(cache_cnt.scalar_type() == torch::kInt32 && cache_cnt.numel() == S * K, "cache_cnt int32[S*K]");
   TORCH_CHECK(cache_acc.scalar_type() == torch::kInt32 && cache_acc.numel() == S * K, "cache_acc int32[S*K]");
   TORCH_CHECK(slotmap.scalar_type() == torch::kInt32 && slotmap.numel() == S * A, "slotmap int32[S*A]");
@@ -244,6 +246,7 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
   a.colptr = reinterpret_cast<const uint32_t*>(colptr.data_ptr<int32_t>());
   a.entbase = entbase.data_ptr<int64_t>();
   a.slots = reinterpret_cast<const uint16_t*>(slots.data_ptr<int16_t>());
+  a.slots_n = slots.numel();
   a.cache_cnt = cache_cnt.data_ptr<int32_t>();
   a.cache_acc = cache_acc.data_ptr<int32_t>();
   a.slotmap = slotmap.data_ptr<int32_t>();

@@ -86,6 +86,7 @@ struct TopNLaunch {
   const uint32_t* colptr;         // [S][2^20+1] per-shard entry offsets
   const int64_t* entbase;         // [S] first slot entry of each shard
   const uint16_t* slots;          // cache slot per (column, cached row)
+  int64_t slots_n;                // entries allocated (>= used + 16, multiple of 8)
   const int32_t* cache_cnt;       // [S][K] cached counts (desc), 0 = empty
   const int32_t* cache_acc;       // [S][K] acc index of each slot's row
   const int32_t* slotmap;         // [S][A] cache slot of each acc row, -1

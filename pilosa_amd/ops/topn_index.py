@@ -105,7 +105,8 @@ class DeviceTopNIndex:
         if S > 1:
             self.entbase[1:S] = torch.cumsum(tot, 0)[:-1]
         self.entries = int(tot.sum().item()) if S else 0
-        self.slots = torch.empty(max(self.entries, 1), dtype=torch.int16, device=dev)
+        # +16 entries: the histogram reads each slot run as aligned 16-byte words
+        self.slots = torch.zeros((self.entries + 16 + 7) // 8 * 8, dtype=torch.int16, device=dev)
         if S:
             colcnt.zero_()
             ext.topn_index(self._vd, S, K, self.cache_dense, colcnt, self.colptr, self.entbase, self.slots, True)
@@ -205,7 +206,7 @@ class DeviceTopNIndex:
         out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx, hist=hist)
         if comm is not None:
             comm.all_reduce(out)
-        return finish_batch(self.space, Q, pair_q.cpu().numpy(), pair_idx.cpu().numpy(), out.cpu().numpy(), ns)
+        return finish_batch_dev(self.space, Q, pair_q, pair_idx, out, ns)
 
     def shard_pairs(self, engine: GpuEngine, src, n: int, threshold: int,
                     ids: Optional[Sequence[int]] = None) -> List[Pair]:
@@ -269,7 +270,39 @@ class DeviceTopNIndex:
             out = c.sum(dim=0, dtype=torch.int64)
         if comm is not None:
             comm.all_reduce(out)
-        return finish_batch(self.space, Q, pq.cpu().numpy(), pa.cpu().numpy(), out.cpu().numpy(), ns)
+        return finish_batch_dev(self.space, Q, pq, pa, out, ns)
+
+
+def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) -> List[List[Pair]]:
+    """finish_batch on the device: (query, count desc, id asc) order by three
+    stable sorts (acc indexes are in id order), per-query trim to n, and only
+    the kept Q x n pairs cross to the host."""
+    import torch
+
+    keep = cnt > 0
+    pq, pa, cnt = pq[keep], pa[keep], cnt[keep]
+    if pq.numel() == 0:
+        return [[] for _ in range(Q)]
+    pa = pa.to(torch.int64)
+    o = torch.sort(pa, stable=True)[1]
+    pq, pa, cnt = pq[o], pa[o], cnt[o]
+    o = torch.sort(cnt, descending=True, stable=True)[1]
+    pq, pa, cnt = pq[o], pa[o], cnt[o]
+    o = torch.sort(pq, stable=True)[1]
+    pq, pa, cnt = pq[o], pa[o], cnt[o]
+    dev = pq.device
+    bounds = torch.searchsorted(pq, torch.arange(Q + 1, device=dev, dtype=pq.dtype))
+    lim = torch.tensor([int(n) if int(n) else (1 << 62) for n in ns], dtype=torch.int64).to(dev)
+    rank = torch.arange(pq.numel(), device=dev) - bounds[pq]
+    sel = rank < lim[pq]
+    q_h = pq[sel].cpu().numpy()
+    a_h = pa[sel].cpu().numpy()
+    c_h = cnt[sel].cpu().numpy()
+    ids = space[a_h]
+    out: List[List[Pair]] = [[] for _ in range(Q)]
+    for qq, i, c in zip(q_h.tolist(), ids.tolist(), c_h.tolist()):
+        out[qq].append(Pair(int(i), int(c)))
+    return out
 
 
 def finish_batch(space: np.ndarray, Q: int, pq: np.ndarray, pa: np.ndarray, cnt: np.ndarray,

@@ -58,6 +58,41 @@ def main():
         nsrc = int(src[0].sum().item())
         out["classes"][name] = {"phase1_ms": round(ms, 3), "src_bits": nsrc,
                                 "dbg": int(os.environ.get("PILOSA_TOPN_DBG", "0"))}
+    if not int(os.environ.get("PILOSA_TOPN_DBG", "0")):
+        # the bench mix (src rows Zipf over the 1000 hottest): end to end and
+        # a synchronised breakdown of one batch
+        from bench import zipf_rows
+        from pilosa_amd.ops.topn_index import finish_batch_dev
+        rng = np.random.default_rng(99)
+        batches = [[Leaf(view, int(r)) for r in zipf_rows(rng, B, 1000)] for _ in range(args.reps + 1)]
+        idx.topn(eng, batches[0], [100] * B, [1] * B)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in batches[1:]:
+            idx.topn(eng, b, [100] * B, [1] * B)
+        torch.cuda.synchronize()
+        e2e = (time.perf_counter() - t0) / args.reps * 1000
+        parts = {}
+
+        def mark(name, t):
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            parts[name] = round((now - t) * 1000, 3)
+            return now
+        srcs = batches[1]
+        t = time.perf_counter()
+        src = eng.materialize_batch(srcs, idx.S)
+        t = mark("materialize", t)
+        acc, ns_t, th_t, hist = idx.phase1(src, B, [100] * B, [1] * B, keep_hist=True)
+        t = mark("phase1", t)
+        pq, pa = idx._candidates(acc, None)
+        t = mark("candidates", t)
+        cnt = idx.phase2(src, B, ns_t, th_t, pq, pa, hist=hist)
+        t = mark("phase2", t)
+        finish_batch_dev(idx.space, B, pq, pa, cnt, [100] * B)
+        mark("finish", t)
+        out["mix"] = {"e2e_ms_per_batch": round(e2e, 3), "qps": round(B / e2e * 1000, 1), "parts_ms": parts,
+                      "candidates": int(pa.numel()), "src_bits": int(src[0].sum().item())}
     print(json.dumps(out), flush=True)
 
 
