@@ -102,7 +102,8 @@ def cmd_server(args, stdout, stderr) -> int:
                  diagnostics_host=cfg.get("metric.diagnostics-host") if cfg.get("metric.diagnostics") else "",
                  gpu_device=int(cfg.get("gpu.devices")[0]) if cfg.get("gpu.devices") else None,
                  hbm_budget=int(cfg.get("gpu.hbm-budget")), mesh_timeout_s=cfg.duration("gpu.rccl-timeout"),
-                 lazy_fragments=bool(cfg.get("gpu.lazy-fragments")))
+                 lazy_fragments=bool(cfg.get("gpu.lazy-fragments")),
+                 native_http=bool(cfg.get("gpu.native-http")))
     srv.open()
     logger.printf("listening as %s (node %s, gpu=%s)", srv.uri.normalize(), srv.node.id,
                   "on" if srv.gpu is not None else "off")

@@ -280,7 +280,8 @@ class Executor:
     # requests of at least this many Count() calls try the native text path
     COUNT_TEXT_MIN = int(os.environ.get("PILOSA_COUNT_TEXT_MIN", "2"))
 
-    def _count_text_fast(self, index: str, text: str, shards, opt: Optional[ExecOptions]) -> Optional[List[int]]:
+    def _count_text_fast(self, index: str, text: str, shards, opt: Optional[ExecOptions],
+                         min_calls: Optional[int] = None) -> Optional[List[int]]:
         """Serving fast path for a request that is only Count(<Row/set-op
         tree>) calls over local shards: the PQL text is compiled natively
         straight to device programs (no Python AST; native/pql_compile.cpp)
@@ -292,7 +293,7 @@ class Executor:
         head = text.lstrip()[:6]
         if head != "Count(" and head != "Count ":
             return None
-        if text.count("Count") < self.COUNT_TEXT_MIN:
+        if text.count("Count") < (self.COUNT_TEXT_MIN if min_calls is None else min_calls):
             return None
         idx = self.holder.index(index)
         if idx is None:
@@ -380,7 +381,21 @@ class Executor:
     def _has_remote(self, index, shards, opt) -> bool:
         if self.cluster is None or opt.remote:
             return False
-        return any(n.id != self.cluster.node.id for n in self._nodes_for(index, shards, opt))
+        nodes = self.cluster.nodes
+        me = self.cluster.node.id
+        if len(nodes) == 1 and nodes[0].id == me:
+            return False  # single node: every shard is local
+        # placement depends only on (index, shards, membership, replicas):
+        # memoised so the serving path does not re-hash every shard per request
+        key = (index, tuple(shards), tuple(n.id for n in nodes), self.cluster.replica_n)
+        memo = self.__dict__.setdefault("_remote_memo", {})
+        hit = memo.get(key)
+        if hit is None:
+            hit = any(n.id != me for n in self._nodes_for(index, shards, opt))
+            if len(memo) > 256:
+                memo.clear()
+            memo[key] = hit
+        return hit
 
     def _nodes_for(self, index, shards, opt):
         nodes = set()

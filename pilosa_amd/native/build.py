@@ -68,6 +68,24 @@ def build_pql(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_httpd(force: bool = False, verbose: bool = False) -> str:
+    """Native HTTP/1.1 front end (httpd.cpp), pybind11 module ``_httpd``."""
+    import pybind11
+
+    out = os.path.join(PKG, "_httpd" + _ext_suffix())
+    srcs = [os.path.join(HERE, "httpd.cpp")]
+    if not force and not _newer(out, srcs):
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-std=c++17", "-O2", "-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
+           "-I", sysconfig.get_paths()["include"], *srcs, "-o", out + ".tmp", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def hip_sources():
     return [os.path.join(KDIR, f) for f in sorted(os.listdir(KDIR))
             if f.endswith((".hip", ".cpp", ".h", ".hpp"))]
@@ -125,6 +143,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
 def build_all(force: bool = False, verbose: bool = False):
     r = build_roaring(force, verbose)
     build_pql(force, verbose)
+    build_httpd(force, verbose)
     h = build_hip(force, verbose) if os.path.exists(os.path.join(KDIR, "binding.cpp")) else None
     return r, h
 

@@ -81,7 +81,7 @@ DEFAULTS: Dict[str, Any] = {
     "tracing": {"sampler-type": "remote", "sampler-param": 0.001, "agent-host-port": ""},
     "profile": {"block-rate": 10000000, "mutex-fraction": 100},
     "gpu": {"mode": "auto", "devices": [], "hbm-budget": 0, "shard-block": 1, "rccl-timeout": "2m",
-            "lazy-fragments": True},
+            "lazy-fragments": True, "native-http": True},
 }
 
 

@@ -636,6 +636,11 @@ def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
             self.send_header("Content-Length", "0")
             self.end_headers()
 
-    srv = ThreadingHTTPServer((host, int(port)), _H)
+    class _Srv(ThreadingHTTPServer):
+        # listen backlog (socketserver's default of 5 drops SYNs under
+        # 100+ concurrent clients)
+        request_queue_size = 1024
+
+    srv = _Srv((host, int(port)), _H)
     srv.daemon_threads = True
     return srv

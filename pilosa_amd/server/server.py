@@ -56,8 +56,12 @@ class Server:
                  translation_primary_url: str = "", tls_certificate: str = "", tls_key: str = "",
                  tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
                  gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
-                 lazy_fragments: Optional[bool] = None):
+                 lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None):
         self.data_dir = data_dir
+        # native epoll front end (native/httpd.cpp) unless TLS is configured
+        if native_http is None:
+            native_http = os.environ.get("PILOSA_NATIVE_HTTP", "1") != "0"
+        self.native_http = bool(native_http) and not (tls_certificate and tls_key)
         self.mesh_timeout_s = mesh_timeout_s
         self.bind = bind
         self.logger = logger or StandardLogger()
@@ -111,7 +115,14 @@ class Server:
         self.holder.open(background=True)
         nid = self._node_id or self.holder.load_node_id()
         host, _, port = self.bind.rpartition(":")
-        self.httpd = make_http_server(Handler(self.api, self, self.logger, self.stats), self.bind)
+        handler = Handler(self.api, self, self.logger, self.stats)
+        self.httpd = None
+        if self.native_http:
+            from pilosa_amd.server import native_http
+            if native_http.available():
+                self.httpd = native_http.make_native_http_server(handler, self.bind)
+        if self.httpd is None:
+            self.httpd = make_http_server(handler, self.bind)
         scheme = "http"
         if self.tls_certificate and self.tls_key:
             import ssl

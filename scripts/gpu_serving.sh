@@ -1,13 +1,14 @@
 #!/bin/bash
-# GPU executor tests, then end-to-end HTTP serving throughput with and
-# without cross-request coalescing (scripts/bench_server.py).
+# End-to-end HTTP serving on the config-2 index (1B cols x 1M rows as
+# Pilosa-format fragment files, scripts/bench_server.py): native front end
+# (native/httpd.cpp + Count group commit) vs the stdlib ThreadingHTTPServer,
+# 128 keep-alive connections from the native load client.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_executor.py -x -q --timeout 120 --timeout-method thread \
-  > gpurun_out/pytest_gpu_exec.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_exec.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu_exec.log
-for c in 1 0; do
-  PILOSA_COALESCE=$c timeout -k 10 300 python -u scripts/bench_server.py --shards ${SHARDS:-64} --seconds 10 \
-    > gpurun_out/serving_c$c.log 2>&1 || { tail -20 gpurun_out/serving_c$c.log; exit 1; }
-  tail -1 gpurun_out/serving_c$c.log
+D=${TMPDIR:-/tmp}/pilosa_serve_data
+for srvmode in 1 0; do
+  PILOSA_NATIVE_HTTP=$srvmode timeout -k 10 400 python -u scripts/bench_server.py --data-dir $D --cols ${COLS:-1000000000} \
+    --conns ${CONNS:-128} --seconds ${SECS:-10} > gpurun_out/serving_native$srvmode.log 2>&1 \
+    || { tail -20 gpurun_out/serving_native$srvmode.log; exit 1; }
+  tail -1 gpurun_out/serving_native$srvmode.log
 done

@@ -1,0 +1,213 @@
+"""Native HTTP front end (native/httpd.cpp, server/native_http.py): same
+answers as the stdlib server on the reference's routes (http/handler.go
+:276-314, query responses :977-1052), HTTP/1.1 details (keep-alive,
+pipelining, chunked bodies, Connection: close, Expect: 100-continue,
+OPTIONS), and the Count group commit -- concurrent Count-only requests
+answered as one batch, with a fallback to the general path that keeps every
+answer and error identical."""
+import json
+import socket
+import tempfile
+import threading
+
+import pytest
+
+from pilosa_amd.server import native_http
+
+pytestmark = [pytest.mark.skipif(not native_http.available(), reason="_httpd not built"), pytest.mark.timeout(90)]
+
+
+def _server(native: bool):
+    from pilosa_amd.server.server import Server
+    from pilosa_amd.utils.logger import CaptureLogger
+    return Server(tempfile.mkdtemp(), bind="127.0.0.1:0", gpu="off", logger=CaptureLogger(),
+                  native_http=native).open()
+
+
+def _raw(port, data: bytes) -> bytes:
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(data)
+    out = b""
+    while True:
+        x = s.recv(65536)
+        if not x:
+            break
+        out += x
+    s.close()
+    return out
+
+
+def _responses(raw: bytes):
+    """[(status, body)] of a stream of HTTP/1.1 responses."""
+    out = []
+    while raw:
+        he = raw.index(b"\r\n\r\n")
+        head = raw[:he].decode()
+        status = int(head.split(" ", 2)[1])
+        n = 0
+        for line in head.split("\r\n")[1:]:
+            k, _, v = line.partition(":")
+            if k.lower() == "content-length":
+                n = int(v)
+        if status == 100:
+            raw = raw[he + 4:]
+            continue
+        out.append((status, raw[he + 4:he + 4 + n]))
+        raw = raw[he + 4 + n:]
+    return out
+
+
+def _req(method, path, body=b"", headers=(), close=False):
+    h = [f"{method} {path} HTTP/1.1", "Host: x", f"Content-Length: {len(body)}", *headers]
+    if close:
+        h.append("Connection: close")
+    return ("\r\n".join(h) + "\r\n\r\n").encode() + body
+
+
+SCRIPT = [
+    ("POST", "/index/i", b""),
+    ("POST", "/index/i/field/f", b""),
+    ("POST", "/index/i/field/g", b'{"options": {"type": "int", "min": 0, "max": 1000}}'),
+    ("POST", "/index/i/query", b"Set(1, f=2) Set(5, f=2) Set(3, f=7) Set(2, g=40)"),
+    ("POST", "/index/i/query", b"Count(Row(f=2))"),
+    ("POST", "/index/i/query", b"Count(Row(f=2)) Count(Union(Row(f=2), Row(f=7)))"),
+    ("POST", "/index/i/query", b"Row(f=2)"),
+    ("POST", "/index/i/query", b"Sum(field=g)"),
+    ("POST", "/index/i/query", b"Count(Row(nope=2))"),
+    ("POST", "/index/missing/query", b"Count(Row(f=2))"),
+    ("POST", "/index/i/query", b"Count(Row(f=2)"),
+    ("POST", "/index/i/query?shards=0", b"Count(Row(f=2))"),
+    ("POST", "/index/i/query?bogus=1", b"Count(Row(f=2))"),
+    ("GET", "/index/i", b""),
+    ("GET", "/schema", b""),
+    ("GET", "/nope", b""),
+    ("DELETE", "/index/i/query", b""),
+    ("GET", "/version", b""),
+]
+
+
+def test_native_matches_stdlib_server():
+    got = {}
+    for native in (True, False):
+        srv = _server(native)
+        try:
+            assert type(srv.httpd).__name__ == ("NativeHTTPServer" if native else "_Srv")
+            port = srv.httpd.server_address[1]
+            got[native] = [_responses(_raw(port, _req(m, p, b, close=True)))[0] for m, p, b in SCRIPT]
+        finally:
+            srv.close()
+    for (m, p, b), a, c in zip(SCRIPT, got[True], got[False]):
+        assert a == c, (m, p, b, a, c)
+    statuses = [s for s, _ in got[True]]
+    assert statuses[4] == 200 and json.loads(got[True][4][1]) == {"results": [2]}
+    assert 404 in statuses and 400 in statuses and 405 in statuses
+
+
+def test_pipelining_chunked_close_options_continue():
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        _raw(port, _req("POST", "/index/i", close=True))
+        _raw(port, _req("POST", "/index/i/field/f", close=True))
+        _raw(port, _req("POST", "/index/i/query", b"Set(10, f=1) Set(11, f=1)", close=True))
+        chunked = (b"POST /index/i/query HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+                   b"6\r\nCount(\r\n9\r\nRow(f=1))\r\n0\r\nX-Trailer: 1\r\n\r\n")
+        stream = (_req("POST", "/index/i/query", b"Count(Row(f=1))") + chunked
+                  + _req("OPTIONS", "/index/i/query") + _req("GET", "/version")
+                  + _req("POST", "/index/i/query", b"Count(Row(f=9))", close=True)
+                  + _req("GET", "/version"))  # after Connection: close: never answered
+        rs = _responses(_raw(port, stream))
+        assert [s for s, _ in rs] == [200, 200, 200, 200, 200]
+        assert json.loads(rs[0][1]) == {"results": [2]} and json.loads(rs[1][1]) == {"results": [2]}
+        assert rs[2][1] == b"" and b"version" in rs[3][1]
+        assert json.loads(rs[4][1]) == {"results": [0]}
+        # Expect: 100-continue: the interim response arrives before the body is sent
+        s = socket.create_connection(("127.0.0.1", port), timeout=10)
+        body = b"Count(Row(f=1))"
+        s.sendall(f"POST /index/i/query HTTP/1.1\r\nHost: x\r\nExpect: 100-continue\r\n"
+                  f"Content-Length: {len(body)}\r\nConnection: close\r\n\r\n".encode())
+        assert s.recv(100).startswith(b"HTTP/1.1 100 Continue")
+        s.sendall(body)
+        out = b""
+        while True:
+            x = s.recv(65536)
+            if not x:
+                break
+            out += x
+        assert _responses(out) == [(200, b'{"results": [2]}\n')]
+        # malformed request line
+        assert _responses(_raw(port, b"BROKEN\r\n\r\n"))[0][0] == 400
+    finally:
+        srv.close()
+
+
+def _host_fast(ex, calls):
+    """A stand-in device fast path: the concatenated group text answered by
+    the host executor (records each call)."""
+    from pilosa_amd.pql import parse_string
+
+    def fast(index, text, shards, opt, min_calls=None):
+        calls.append(text)
+        q = parse_string(text)
+        gpu = ex.gpu
+        return [int(r) for r in ex.execute(index, q).results] if gpu is None else None
+    return fast
+
+
+def test_count_group_commit_and_fallback():
+    from pilosa_amd import _httpd
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        for m, p, b in SCRIPT[:4]:
+            _raw(port, _req(m, p, b, close=True))
+        ex = srv.executor
+        calls = []
+        ex._count_text_fast = _host_fast(ex, calls)
+        srv.httpd.srv.set_count_batching(True)
+        bodies = [b"Count(Row(f=2))", b"Count(Row(f=7)) Count(Row(f=2))", b"Count(Intersect(Row(f=2), Row(f=7)))",
+                  b"Count(Row(f=99))"]
+        want = [[2], [1, 2], [0], [0]]
+        res = _httpd.load("127.0.0.1", port, "/index/i/query", bodies, 32, 4, 1.0, 400)
+        assert res["errors"] == 0 and res["requests"] > 50
+        assert len(res["samples"]) == 400
+        for k, body in res["samples"]:
+            assert json.loads(body)["results"] == want[k]
+        st = srv.httpd.stats()
+        assert st["count_requests"] >= res["requests"] and st["batched_requests"] > 0
+        assert any(t.count("Count(") > 2 for t in calls), "no multi-request group was formed"
+        # a group the fast path declines (unknown field) goes to the general
+        # path: same error as the stdlib server, other groups unaffected
+        rs = _responses(_raw(port, _req("POST", "/index/i/query", b"Count(Row(nope=1))", close=True)))
+        assert rs[0] == (400, b"{\"error\": \"field not found\"}\n")
+        assert srv.httpd.stats()["requeued"] >= 1
+    finally:
+        srv.close()
+
+
+def test_concurrent_generic_requests():
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        _raw(port, _req("POST", "/index/i", close=True))
+        _raw(port, _req("POST", "/index/i/field/f", close=True))
+        errs = []
+
+        def writer(k):
+            try:
+                for j in range(20):
+                    rs = _responses(_raw(port, _req("POST", "/index/i/query", f"Set({k * 100 + j}, f=3)".encode(),
+                                                    close=True)))
+                    assert rs[0][0] == 200
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=writer, args=(k,)) for k in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs
+        rs = _responses(_raw(port, _req("POST", "/index/i/query", b"Count(Row(f=3))", close=True)))
+        assert json.loads(rs[0][1]) == {"results": [160]}
+    finally:
+        srv.close()
