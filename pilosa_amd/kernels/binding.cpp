@@ -176,7 +176,7 @@ pk::ViewDev viewdev_from(const torch::Tensor& vd) {
   return v;
 }
 
-void topn_index(torch::Tensor view, int64_t S, int64_t K, torch::Tensor cache_dense, torch::Tensor colcnt,
+void topn_index(torch::Tensor view, int64_t S, int64_t K, int64_t k0, torch::Tensor cache_dense, torch::Tensor colcnt,
                 torch::Tensor colptr, torch::Tensor entbase, torch::Tensor slots, bool fill) {
   check_dev(cache_dense, "cache_dense");
   check_dev(colcnt, "colcnt");
@@ -184,6 +184,7 @@ void topn_index(torch::Tensor view, int64_t S, int64_t K, torch::Tensor cache_de
   TORCH_CHECK(colcnt.scalar_type() == torch::kInt32 && colcnt.numel() == S * (int64_t(1) << 20),
               "colcnt int32[S*2^20]");
   TORCH_CHECK(K > 0 && K <= 65535, "slot index needs 0 < K <= 65535");
+  TORCH_CHECK(k0 >= 0 && k0 <= K, "slot index tail start 0 <= k0 <= K");
   const uint32_t* cp = nullptr;
   const int64_t* eb = nullptr;
   uint16_t* sl = nullptr;
@@ -199,23 +200,49 @@ void topn_index(torch::Tensor view, int64_t S, int64_t K, torch::Tensor cache_de
     eb = entbase.data_ptr<int64_t>();
     sl = reinterpret_cast<uint16_t*>(slots.data_ptr<int16_t>());
   }
-  pk::launch_topn_index(viewdev_from(view), int(S), int(K), cache_dense.data_ptr<int32_t>(),
+  pk::launch_topn_index(viewdev_from(view), int(S), int(K), int(k0), cache_dense.data_ptr<int32_t>(),
                         reinterpret_cast<uint32_t*>(colcnt.data_ptr<int32_t>()), cp, eb, sl, fill,
                         cur_stream(cache_dense));
   check_launch("topn_index");
+}
+
+void topn_hot_meta(torch::Tensor view, int64_t S, int64_t K, int64_t R, torch::Tensor cache_dense,
+                   torch::Tensor hot_meta, torch::Tensor hot_split) {
+  check_dev(cache_dense, "cache_dense");
+  check_dev(hot_meta, "hot_meta");
+  TORCH_CHECK(cache_dense.scalar_type() == torch::kInt32 && cache_dense.numel() == S * K, "cache_dense int32[S*K]");
+  TORCH_CHECK(R >= 0 && R <= K, "hot ranks 0 <= R <= K");
+  TORCH_CHECK(hot_meta.scalar_type() == torch::kInt32 && hot_meta.numel() == S * 16 * R, "hot_meta int32[S*16*R]");
+  check_dev(hot_split, "hot_split");
+  TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == S * 16, "hot_split int32[S*16]");
+  pk::launch_topn_hot_meta(viewdev_from(view), int(S), int(K), int(R), cache_dense.data_ptr<int32_t>(),
+                           hot_meta.data_ptr<int32_t>(), hot_split.data_ptr<int32_t>(), cur_stream(cache_dense));
+  check_launch("topn_hot_meta");
 }
 
 void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, int64_t H16, int64_t A, torch::Tensor src_counts,
               torch::Tensor src_offs, torch::Tensor src_vals, torch::Tensor colptr, torch::Tensor entbase,
               torch::Tensor slots, torch::Tensor cache_cnt, torch::Tensor cache_acc, torch::Tensor slotmap,
               torch::Tensor a2dense, torch::Tensor ns, torch::Tensor min_threshold, int64_t mode, torch::Tensor acc,
-              torch::Tensor pair_off, torch::Tensor pair_idx, torch::Tensor out, torch::Tensor hist) {
+              torch::Tensor pair_off, torch::Tensor pair_idx, torch::Tensor out, torch::Tensor hist, int64_t R,
+              torch::Tensor hot_meta, torch::Tensor hot_cnt, torch::Tensor tail_built, torch::Tensor cache_dense,
+              torch::Tensor hot_split) {
   for (auto* t : {&src_counts, &src_offs, &src_vals, &colptr, &entbase, &slots, &cache_cnt, &cache_acc, &slotmap,
                   &a2dense, &ns, &min_threshold})
     check_dev(*t, "topn_src input");
-  TORCH_CHECK(mode >= 1 && mode <= 3, "topn_src mode");
-  TORCH_CHECK(K > 0 && K <= 65535 && H32 >= 0 && H32 <= H16 && H16 <= K, "topn_src K/H32/H16");
-  TORCH_CHECK(pk::topn_lds_bytes(int(K), int(H32), int(H16)) <= 160 * 1024 - 1024, "slot histogram exceeds LDS");
+  TORCH_CHECK(mode >= 1 && mode <= 4, "topn_src mode");
+  TORCH_CHECK(R >= 0 && R <= K, "topn_src hot ranks 0 <= R <= K");
+  TORCH_CHECK(K > 0 && K <= 65535 && H32 >= 0 && H32 <= H16 && H16 <= K - R, "topn_src K/H32/H16");
+  TORCH_CHECK(pk::topn_lds_bytes(int(K - R), int(H32), int(H16)) <= 160 * 1024 - 1024, "slot histogram exceeds LDS");
+  if (R > 0) {
+    check_dev(hot_meta, "hot_meta");
+    check_dev(hot_cnt, "hot_cnt");
+    TORCH_CHECK(Q <= 16, "hot-rank counting takes at most 16 queries per launch");
+    TORCH_CHECK(hot_meta.scalar_type() == torch::kInt32 && hot_meta.numel() == S * 16 * R, "hot_meta int32[S*16*R]");
+    TORCH_CHECK(hot_cnt.scalar_type() == torch::kInt32 && hot_cnt.numel() == S * Q * R, "hot_cnt int32[S*Q*R]");
+    check_dev(hot_split, "hot_split");
+    TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == S * 16, "hot_split int32[S*16]");
+  }
   TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * S * 16,
               "src_counts int32[Q*S*16]");
   TORCH_CHECK(src_offs.scalar_type() == torch::kInt64 && src_offs.numel() == Q * S * 16, "src_offs int64[Q*S*16]");
@@ -253,14 +280,30 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
   a.a2dense = a2dense.data_ptr<int32_t>();
   a.ns = ns.data_ptr<int32_t>();
   a.min_threshold = min_threshold.data_ptr<int32_t>();
-  const int64_t hist_words = int64_t(pk::topn_lds_bytes(int(K), int(H32), int(H16)) / 4) * Q * S;
+  a.R = int(R);
+  if (tail_built.numel()) {
+    check_dev(tail_built, "tail_built");
+    TORCH_CHECK(tail_built.scalar_type() == torch::kInt32 && tail_built.numel() == Q * S, "tail_built int32[Q*S]");
+    a.tail_built = tail_built.data_ptr<int32_t>();
+  }
+  check_dev(cache_dense, "cache_dense");
+  TORCH_CHECK(cache_dense.scalar_type() == torch::kInt32 && cache_dense.numel() == S * K, "cache_dense int32[S*K]");
+  a.cache_dense = cache_dense.data_ptr<int32_t>();
+  if (R > 0) {
+    a.hot_meta = hot_meta.data_ptr<int32_t>();
+    a.hot_cnt = reinterpret_cast<uint32_t*>(hot_cnt.data_ptr<int32_t>());
+    a.hot_split = hot_split.data_ptr<int32_t>();
+  }
+  const int64_t hist_words = int64_t(pk::topn_lds_bytes(int(K - R), int(H32), int(H16)) / 4) * Q * S;
   if (hist.numel() || mode == 3) {
     check_dev(hist, "hist");
     TORCH_CHECK(hist.scalar_type() == torch::kInt32 && hist.numel() == hist_words, "hist int32[Q*S*words]");
     if (mode == 1) a.hist_out = reinterpret_cast<uint32_t*>(hist.data_ptr<int32_t>());
     if (mode == 3) a.hist_in = reinterpret_cast<const uint32_t*>(hist.data_ptr<int32_t>());
   }
-  if (mode == 1) {
+  if (mode == 4) {
+    TORCH_CHECK(R > 0, "mode 4 needs hot ranks");
+  } else if (mode == 1) {
     check_dev(acc, "acc");
     TORCH_CHECK(acc.scalar_type() == torch::kInt32 && acc.numel() == Q * A, "acc int32[Q*A]");
     a.acc = acc.data_ptr<int32_t>();
@@ -369,6 +412,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
   m.def("bsi_range_count", &bsi_range_count, "Count(Row(v <op> x)): fused BSI predicate + count");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
+  m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
   m.def("bitgemm", &bitgemm, "row-pair intersection count matrix of dense bit rows (mode 1 MFMA i8, 0 VALU)");

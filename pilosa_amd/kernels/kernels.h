@@ -71,7 +71,7 @@ void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, 
 // Device TopN slot index (topn_kernels.hip): pass 1 counts cached-row bits per
 // column into colcnt[S*2^20]; pass 2 (fill) scatters cache slots behind the
 // per-shard exclusive scan colptr[S][2^20+1] (colcnt reused as cursors).
-void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dense, uint32_t* colcnt,
+void launch_topn_index(const ViewDev& v, int S, int K, int k0, const int32_t* cache_dense, uint32_t* colcnt,
                        const uint32_t* colptr, const int64_t* entbase, uint16_t* slots, bool fill, hipStream_t st);
 // Arguments of the src-TopN kernel.  Rows are addressed in an "acc space" of
 // A sorted row ids (identical on every rank of a node).
@@ -99,13 +99,22 @@ struct TopNLaunch {
   unsigned long long* out;        // mode 2/3: [P] summed counts >= threshold
   uint32_t* hist_out;             // mode 1 (optional): [Q*S][words] kept histograms
   const uint32_t* hist_in;        // mode 3: histograms kept by mode 1
+  int R;                          // hot ranks [0, R) counted by mode 4; slot index / histogram cover [R, K)
+  const int32_t* hot_meta;        // [S][16][R] key-j container of each hot row (meta index in shard), -1
+  const int32_t* hot_split;       // [S][16] ranks before it hold the big (cooperative) containers
+  uint32_t* hot_cnt;              // [S][Q][R] src counts of the hot ranks (mode 4 writes, 1-3 read)
+  int32_t* tail_built;            // [Q*S] mode 1: 1 = unit's tail histogram built (kept), 0 = skipped
+  const int32_t* cache_dense;     // [S][K] dense row of each cache slot (mode 3 exact probes)
   int dbg;                        // profiling builds: bit 0 skip histogram, bit 1 skip walk
 };
 // LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).
 int topn_lds_bytes(int K, int H32, int H16);
 // mode 1: phase-1 heap walk -> acc[Q][A] (+ hist_out); mode 2: ids= re-count
 // -> out[P] (rebuilds the histograms); mode 3: ids= re-count from hist_in.
+// mode 4: hot-rank count matrix hot_cnt (row-major over the batch).
 void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
+void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
+                          int32_t* hot_split, hipStream_t st);
 
 // Row-pair intersection count matrix C[M][N] (int32, atomically accumulated)
 // of dense bit rows A[M][KW] and B[N][KW] (u64 words), bitgemm.hip.

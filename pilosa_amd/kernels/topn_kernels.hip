@@ -86,12 +86,13 @@ __device__ __forceinline__ void container_values(const uint16_t* payload, int64_
   }
 }
 
-// Pass 1 (FILL=false): colcnt[s][col] = number of cached rows of shard s with
-// a bit at col.  Pass 2 (FILL=true): scatter the cache slot k of each such
-// (row, col) to slots[entbase[s] + colptr[s][col] + cursor].  One wave per
-// cache entry (s, k); grid-stride.
+// Pass 1 (FILL=false): colcnt[s][col] = number of cached rows of shard s
+// ranked k >= k0 (the tail; ranks below k0 are counted by topn_hot_kernel)
+// with a bit at col.  Pass 2 (FILL=true): scatter the tail slot k - k0 of
+// each such (row, col) to slots[entbase[s] + colptr[s][col] + cursor].  One
+// wave per cache entry (s, k); grid-stride.
 template <bool FILL>
-__global__ __launch_bounds__(256) void topn_index_kernel(ViewDev v, int S, int K,
+__global__ __launch_bounds__(256) void topn_index_kernel(ViewDev v, int S, int K, int k0,
                                                          const int32_t* __restrict__ cache_dense,
                                                          uint32_t* __restrict__ colcnt,
                                                          const uint32_t* __restrict__ colptr,
@@ -99,12 +100,14 @@ __global__ __launch_bounds__(256) void topn_index_kernel(ViewDev v, int S, int K
                                                          uint16_t* __restrict__ slots) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = int64_t(gridDim.x) * 4;
-  const int64_t total = int64_t(S) * K;
+  const int Kt = K - k0;
+  const int64_t total = int64_t(S) * Kt;
   for (int64_t e = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); e < total; e += nw) {
-    const int d = cache_dense[e];
+    const int s = int(e / Kt);
+    const int kt = int(e - int64_t(s) * Kt);
+    const int d = cache_dense[int64_t(s) * K + k0 + kt];
     if (d < 0) continue;
-    const int s = int(e / K);
-    const uint16_t k = uint16_t(e - int64_t(s) * K);
+    const uint16_t k = uint16_t(kt);
     const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
     const int64_t sb = v.shard_base[s];
     const int64_t c0 = sb + rp[d], c1 = sb + rp[d + 1];
@@ -162,6 +165,14 @@ __device__ __forceinline__ uint32_t hist_get(P h, const HistLayout& L, int k) {
   }
   const int r = k - L.H16;
   return (h[L.W16 + (r >> 2)] >> ((r & 3) * 8)) & 0xffu;
+}
+
+// src count of cache slot k of unit (q, s): the hot-rank count matrix below
+// R, the tail histogram (tail-relative slot) above.
+template <class P>
+__device__ __forceinline__ uint32_t slot_count(const TopNLaunch& p, P h, const HistLayout& L, int q, int s, int k) {
+  if (k < p.R) return p.hot_cnt[(int64_t(s) * p.Q + q) * p.R + k];
+  return hist_get(h, L, k - p.R);
 }
 
 struct BlockScratch {
@@ -244,6 +255,8 @@ __device__ uint32_t src_row_count(const ViewDev& v, int s, int d, const int32_t*
   return total;
 }
 
+__device__ __forceinline__ int64_t unit_index(const TopNLaunch& p, int q, int s) { return int64_t(q) * p.S + s; }
+
 __device__ __forceinline__ int64_t unit_hist_base(const TopNLaunch& p, int q, int s, int words) {
   return (int64_t(q) * p.S + s) * int64_t(words);
 }
@@ -256,9 +269,48 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
   const int q = int(unit % p.Q), s = int(unit / p.Q);
   const int tid = threadIdx.x;
   const int K = p.K;
-  const HistLayout L(K, p.H32, p.H16);
+  const HistLayout L(K - p.R, p.H32, p.H16);
   const int words = L.words;
-  for (int i = tid; i < words; i += TN_THREADS) hist[i] = 0;
+  const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
+  const int32_t* cc = p.cache_cnt + int64_t(s) * K;
+  // Mode 1 with hot ranks: replay the fill over the hot counts first.  When
+  // the walk provably ends inside the hot ranks (n rows found and the first
+  // tail rank's cached count below their minimum, or cached counts below the
+  // threshold), the tail histogram is never read: skip building it.  Dense
+  // srcs -- the ones whose histograms are expensive -- end here.
+  bool need_tail = p.R < K && !(p.dbg & 1);
+  if (MODE == 1 && need_tail && p.R > 0) {
+    const int nmax = p.ns[q];
+    int found = 0;
+    uint32_t T = 0xffffffffu;
+    bool filled = false;
+    for (int base = 0; base < p.R; base += TN_THREADS) {
+      const int k = base + tid;
+      const uint32_t cnt = k < p.R ? uint32_t(cc[k]) : 0u;
+      const uint32_t cv = cnt >= mt ? p.hot_cnt[(int64_t(s) * p.Q + q) * p.R + k] : 0u;
+      const bool ok = cnt >= mt && cv >= mt;
+      int tot;
+      const int rank = block_rank(ok, bs, tot);
+      const bool take = ok && (nmax == 0 || found + rank < nmax);
+      uint32_t tmin;
+      int pmax;
+      block_minmax(take ? cv : 0xffffffffu, -1, bs, tmin, pmax);
+      T = min(T, uint32_t(__builtin_amdgcn_readfirstlane(int(tmin))));
+      found += __builtin_amdgcn_readfirstlane(tot);
+      if (nmax > 0 && found >= nmax) {
+        filled = true;
+        break;
+      }
+    }
+    const uint32_t c_r = uint32_t(cc[p.R]);
+    if (c_r < mt || (filled && c_r < T)) need_tail = false;
+  }
+  if (MODE == 1 && p.tail_built) {
+    if (tid == 0) p.tail_built[unit_index(p, q, s)] = need_tail ? 1 : 0;
+  }
+  if (need_tail) {
+    for (int i = tid; i < words; i += TN_THREADS) hist[i] = 0;
+  }
   __syncthreads();
 
   // histogram of cache slots over src's columns, 4 columns per thread in
@@ -273,7 +325,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
   const int64_t eb = p.entbase[s];
   const int64_t amax = ((p.slots_n - 16) & ~int64_t(7));
   const auto sl4 = gp(reinterpret_cast<const uint4*>(p.slots));
-  for (int j = 0; j < ((p.dbg & 1) ? 0 : 16); j++) {
+  for (int j = 0; j < (need_tail ? 16 : 0); j++) {
     const int n = p.src_counts[kb + j];
     if (n <= 0) continue;
     const auto vals = gp(p.src_vals + p.src_offs[kb + j]);
@@ -290,9 +342,13 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
       uint4 w0[4], w1[4];
 #pragma unroll
       for (int r = 0; r < 4; r++) {
+        // exec-masked: columns without (tail) slots fetch nothing
         a[r] = min((eb + int64_t(e0[r])) & ~int64_t(7), amax);
-        w0[r] = sl4[a[r] >> 3];
-        w1[r] = sl4[(a[r] >> 3) + 1];
+        const int64_t hi = eb + int64_t(e1[r]) - a[r];
+        w0[r] = make_uint4(0, 0, 0, 0);
+        w1[r] = make_uint4(0, 0, 0, 0);
+        if (e1[r] > e0[r]) w0[r] = sl4[a[r] >> 3];
+        if (hi > 8) w1[r] = sl4[(a[r] >> 3) + 1];
       }
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -334,16 +390,14 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
     }
   }
   __syncthreads();
-  if (MODE == 1 && p.hist_out) {
+  if (MODE == 1 && p.hist_out && need_tail) {
     // keep the histogram for the ids= re-count (topn_gather_kernel)
     uint32_t* ho = p.hist_out + unit_hist_base(p, q, s, words);
     for (int i = tid; i < words; i += TN_THREADS) ho[i] = hist[i];
   }
 
-  const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
   if (MODE == 1 && (p.dbg & 2)) return;
   if constexpr (MODE == 1) {
-    const int32_t* cc = p.cache_cnt + int64_t(s) * K;
     const int32_t* ca = p.cache_acc + int64_t(s) * K;
     int32_t* acc = p.acc + int64_t(q) * p.A;
     const int nmax = p.ns[q];
@@ -354,7 +408,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
     for (int base = 0; base < K; base += TN_THREADS) {
       const int k = base + tid;
       const uint32_t cnt = k < K ? uint32_t(cc[k]) : 0u;
-      const uint32_t cv = k < K ? hist_get(hist, L, k) : 0u;
+      const uint32_t cv = cnt >= mt ? slot_count(p, hist, L, q, s, k) : 0u;
       const bool ok = cnt >= mt && cv >= mt;
       int tot;
       const int rank = block_rank(ok, bs, tot);
@@ -379,7 +433,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
       for (int base = P + 1; base < K; base += TN_THREADS) {
         const int k = base + tid;
         if (k < K && uint32_t(cc[k]) >= T) {
-          const uint32_t cv = hist_get(hist, L, k);
+          const uint32_t cv = slot_count(p, hist, L, q, s, k);
           if (cv >= T) atomicAdd(acc + ca[k], int32_t(cv));
         }
         if (uint32_t(cc[min(base + TN_THREADS, K) - 1]) < T) break;
@@ -393,7 +447,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
       const int k = sm[a];
       uint32_t c = 0;
       if (k >= 0) {
-        c = hist_get(hist, L, k);
+        c = slot_count(p, hist, L, q, s, k);
       } else {
         const int d = p.a2dense[a];
         if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
@@ -408,7 +462,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
 __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
   const uint32_t unit = tn_xcd_remap(blockIdx.x, gridDim.x);
   const int q = int(unit % p.Q), s = int(unit / p.Q);
-  const HistLayout L(p.K, p.H32, p.H16);
+  const HistLayout L(p.K - p.R, p.H32, p.H16);
   const auto h = gp(p.hist_in + unit_hist_base(p, q, s, L.words));
   const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
   const int32_t* sm = p.slotmap + int64_t(s) * p.A;
@@ -418,8 +472,12 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
     const int a = p.pair_idx[i];
     const int k = sm[a];
     uint32_t c = 0;
-    if (k >= 0) {
-      c = hist_get(h, L, k);
+    if (k >= 0 && (k < p.R || !p.tail_built || p.tail_built[unit_index(p, q, s)])) {
+      c = slot_count(p, h, L, q, s, k);
+    } else if (k >= 0) {
+      // phase 1 skipped this unit's tail histogram: count the row exactly
+      c = src_row_count(p.v, s, int(p.cache_dense[int64_t(s) * p.K + k]), p.src_counts + kb, p.src_offs + kb,
+                        p.src_vals);
     } else {
       const int d = p.a2dense[a];
       if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
@@ -428,20 +486,288 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
   }
 }
 
+
+// ---------------------------------------------------------------- hot ranks
+// The first R cache ranks of every shard hold most of the cached rows' bits
+// (Zipf: ranks < 2048 carry ~90% of them), and every query of a batch needs
+// their src counts before its heap walk can stop.  Counting them through the
+// column-major slot histogram costs |src| x (bits per column) scattered
+// slot-run reads PER QUERY; here they are counted row-major ONCE for the
+// whole batch (Q <= 16):
+//   one 1024-thread workgroup per shard; for each container key j
+//     1. an LDS table of 65536 u16 query masks (128 KB): bit q of entry x
+//        is set when src(q) has column j*2^16 + x;
+//     2. each wave streams its hot rows' key-j containers (coalesced reads
+//        of the arena payload) and sums, per query, the mask bits of the
+//        row's values: 16 per-lane counters, reduced over the wave by a
+//        17-shuffle transpose (lane l ends with query (l >> 2) & 15);
+//     3. the wave adds them into hot_cnt[s][q][k] (it owns row k for every j,
+//        so the read-modify-write needs no atomics).
+// hot_meta[s][j][k] is the row's key-j container (meta index relative to the
+// shard, -1 = none), built once with the index.
+constexpr int HOT_THREADS = 1024;
+constexpr int HOT_TAB_WORDS = 32768;
+constexpr int HOT_SMALL_N = 255;  // byte counters: at most 255 values per lane-owned container
+
+// SWAR: add the 16 bits of a query mask to 16 byte counters (4 per word):
+// a nibble times 0x00204081 puts its bits at bytes 0..3 without carries.
+__device__ __forceinline__ void swar_add(uint32_t (&c4)[4], uint32_t msk) {
+#pragma unroll
+  for (int g = 0; g < 4; g++) c4[g] += (((msk >> (4 * g)) & 15u) * 0x00204081u) & 0x01010101u;
+}
+
+__global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) {
+  extern __shared__ uint32_t tab[];
+  __shared__ int grab[2];
+  // one workgroup per (shard, key j); consecutive blocks share a shard (XCD L2)
+  const int unit = int(tn_xcd_remap(blockIdx.x, gridDim.x));
+  const int s = unit >> 4, j = unit & 15;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int Q = p.Q, R = p.R;
+  const int64_t sb = p.v.shard_base[s];
+  uint32_t* out = p.hot_cnt + int64_t(s) * Q * R;
+  // 1. query-mask table of key j
+  bool any = false;
+  for (int q = 0; q < Q; q++) any |= p.src_counts[(int64_t(q) * p.S + s) * 16 + j] > 0;
+  if (!any) return;  // block-uniform: no src has key j in this shard
+  uint4* t4 = reinterpret_cast<uint4*>(tab);
+  for (int i = tid; i < HOT_TAB_WORDS / 4; i += HOT_THREADS) t4[i] = make_uint4(0, 0, 0, 0);
+  if (tid == 0) grab[0] = grab[1] = 0;
+  __syncthreads();
+  for (int q = 0; q < Q; q++) {
+    const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
+    const int n = p.src_counts[kk];
+    if (n <= 0) continue;
+    const uint16_t* vals = p.src_vals + p.src_offs[kk];
+    if (n <= ARRAY_MAX) {
+      for (int i = tid; i < n; i += HOT_THREADS) {
+        const int x = vals[i];
+        atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+      }
+    } else {
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(vals);
+      for (int i = tid; i < 1024; i += HOT_THREADS)
+        for (uint64_t bb = w[i]; bb; bb &= bb - 1) {
+          const int x = i * 64 + __builtin_ctzll(bb);
+          atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+        }
+    }
+  }
+  __syncthreads();
+  auto mask_of = [&](int x) -> uint32_t { return tab[x >> 1] >> ((x & 1) << 4); };
+  const int32_t* hm = p.hot_meta + (int64_t(s) * 16 + j) * R;
+  const int B = min(R, p.hot_split[int64_t(s) * 16 + j]);
+
+  // 2. big containers, ranks [0, B): wave w takes ranks w + 16 i (sizes fall
+  //    with rank, so every wave gets a similar mix).  Per group of 64 of its
+  //    ranks, lane l loads rank l's container index and meta word (2 vector
+  //    loads per 64 rows); then rows stream as 512-value chunks (8 rounds of
+  //    64 consecutive values) with the NEXT chunk's loads -- possibly the next
+  //    row's first chunk -- in flight while the current one is counted.  Byte
+  //    counters per lane, a 17-shuffle transpose-reduce per row, totals in
+  //    lanes (l >> 2) & 15.
+  const int wave = tid >> 6;
+  for (int gb = wave; gb < ((p.dbg & 16) ? 0 : B); gb += 64 * (HOT_THREADS / 64)) {
+    const int kl = gb + (HOT_THREADS / 64) * lane;
+    const int cl = kl < B ? hm[kl] : -1;
+    const int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
+    uint64_t live = __ballot(cl >= 0);
+    if (!live) continue;
+    auto row_meta = [&](int r) -> int64_t {
+      const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(ml)), r));
+      const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(ml) >> 32)), r));
+      return int64_t((uint64_t(hi) << 32) | lo);
+    };
+    auto load_chunk = [&](int64_t m, int base, int (&x)[8]) {
+      const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
+      const int n = meta_n(m);
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const int i = base + 64 * t + lane;
+        x[t] = i < n ? int(pp[i]) : -1;
+      }
+    };
+    int r = __builtin_ctzll(live);
+    live &= live - 1;
+    int64_t m = row_meta(r);
+    int base = 0;
+    int cur[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) cur[t] = -1;
+    if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur);
+    uint32_t c4[4] = {0u, 0u, 0u, 0u};
+    uint32_t acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc[q] = 0;
+    auto flush = [&]() {
+#pragma unroll
+      for (int q = 0; q < 16; q++) acc[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+#pragma unroll
+      for (int g = 0; g < 4; g++) c4[g] = 0;
+    };
+    for (;;) {
+      const int ty = meta_type(m);
+      const int n = meta_n(m);
+      const bool more = ty == CT_ARRAY && base + 512 < n;
+      int rn = r, bn = base + 512;
+      int64_t mn = m;
+      const bool row_end = !more;
+      if (row_end) {
+        rn = live ? __builtin_ctzll(live) : -1;
+        bn = 0;
+        mn = rn >= 0 ? row_meta(rn) : 0;
+      }
+      int nxt[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) nxt[t] = -1;
+      if (rn >= 0 && meta_type(mn) == CT_ARRAY) load_chunk(mn, bn, nxt);
+      const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
+      if (ty == CT_ARRAY) {
+        // an array gives a lane at most 64 values: bytes cannot overflow
+#pragma unroll
+        for (int t = 0; t < 8; t++)
+          if (cur[t] >= 0) swar_add(c4, mask_of(cur[t]));
+      } else if (ty == CT_BITMAP) {
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(pp);
+        for (int i = lane; i < 1024; i += 64) {
+          for (uint64_t bb = w[i]; bb; bb &= bb - 1) swar_add(c4, mask_of(i * 64 + __builtin_ctzll(bb)));
+          if ((i >> 6) % 3 == 2) flush();  // <= 192 bits per lane between flushes
+        }
+      } else {
+        const int nr = pp[0];
+        const uint16_t* rr = pp + 8;
+        int since = 0;
+        for (int t = 0; t < nr; t++) {
+          const int a0 = rr[2 * t], b0 = rr[2 * t + 1];
+          for (int xx = a0 + lane; xx <= b0; xx += 64) {
+            swar_add(c4, mask_of(xx));
+            if (++since == 240) {
+              flush();
+              since = 0;
+            }
+          }
+        }
+      }
+      if (row_end) {
+        flush();
+        // transpose-reduce: 16 counters x 64 lanes -> one total per 4 lanes
+        const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
+        uint32_t aa[8], bq[4], c2[2];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const uint32_t mine = h5 ? acc[8 + i] : acc[i], other = h5 ? acc[i] : acc[8 + i];
+          aa[i] = mine + uint32_t(__shfl_xor(int(other), 32, 64));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t mine = h4 ? aa[4 + i] : aa[i], other = h4 ? aa[i] : aa[4 + i];
+          bq[i] = mine + uint32_t(__shfl_xor(int(other), 16, 64));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+          const uint32_t mine = h3 ? bq[2 + i] : bq[i], other = h3 ? bq[i] : bq[2 + i];
+          c2[i] = mine + uint32_t(__shfl_xor(int(other), 8, 64));
+        }
+        uint32_t d = (h2 ? c2[1] : c2[0]) + uint32_t(__shfl_xor(int(h2 ? c2[0] : c2[1]), 4, 64));
+        d += uint32_t(__shfl_xor(int(d), 2, 64));
+        d += uint32_t(__shfl_xor(int(d), 1, 64));
+        const int q = (lane >> 2) & 15;
+        const int k = gb + (HOT_THREADS / 64) * r;
+        if ((lane & 3) == 0 && q < Q && d) atomicAdd(out + int64_t(q) * R + k, d);
+#pragma unroll
+        for (int qq = 0; qq < 16; qq++) acc[qq] = 0;
+        if (rn < 0) break;
+        live &= live - 1;
+      }
+      r = rn;
+      base = bn;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < 8; t++) cur[t] = nxt[t];
+    }
+  }
+
+  // 3. small array containers (<= HOT_SMALL_N values), ranks [B, R): waves
+  //    grab groups of 64 consecutive ranks, each lane counts its own row
+  //    (8 values per 16-byte load), no reduction; atomics are coalesced
+  //    (consecutive ranks per query)
+  for (;;) {
+    int g = 0;
+    if (lane == 0) g = atomicAdd(&grab[1], 1);
+    g = __builtin_amdgcn_readfirstlane(g);
+    const int k0 = B + 64 * g;
+    if (k0 >= R || (p.dbg & 8)) break;
+    const int kl = k0 + lane;
+    const int cl = kl < R ? hm[kl] : -1;
+    const int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
+    const int nl = cl >= 0 ? meta_n(ml) : 0;
+    const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
+    uint32_t c4[4] = {0u, 0u, 0u, 0u};
+    for (int i = 0; __ballot(i < nl); i += 16) {
+      // two 16-byte loads in flight per lane (16 values)
+      uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
+      if (i < nl) w0 = pp[i >> 3];
+      if (i + 8 < nl) w1 = pp[(i >> 3) + 1];
+      const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int t = 0; t < 16; t++)
+        if (i + t < nl) swar_add(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+      if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
+    }
+  }
+}
+
+// hot_meta[s][j][k] = meta index (relative to the shard) of the key-j
+// container of the row at cache rank k < R, -1 when absent.  Thread per (s, k).
+__global__ __launch_bounds__(256) void topn_hot_meta_kernel(ViewDev v, int S, int K, int R,
+                                                            const int32_t* __restrict__ cache_dense,
+                                                            int32_t* __restrict__ hot_meta,
+                                                            int32_t* __restrict__ hot_split) {
+  const int64_t total = int64_t(S) * R;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
+       e += int64_t(gridDim.x) * blockDim.x) {
+    const int s = int(e / R), k = int(e - int64_t(s) * R);
+    const int d = cache_dense[int64_t(s) * K + k];
+    if (d < 0) continue;
+    const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+    const int64_t sb = v.shard_base[s];
+    for (uint32_t c = rp[d]; c < rp[d + 1]; c++) {
+      const int64_t m = v.meta[sb + c];
+      hot_meta[(int64_t(s) * 16 + meta_j(m)) * R + k] = int32_t(c);
+      // ranks before the split take the cooperative path (see topn_hot_kernel)
+      if (meta_type(m) != CT_ARRAY || meta_n(m) > HOT_SMALL_N) atomicMax(hot_split + int64_t(s) * 16 + meta_j(m), k + 1);
+    }
+  }
+}
+
 }  // namespace
 
-void launch_topn_index(const ViewDev& v, int S, int K, const int32_t* cache_dense, uint32_t* colcnt,
+void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
+                          int32_t* hot_split, hipStream_t st) {
+  const int64_t total = int64_t(S) * R;
+  if (total <= 0) return;
+  const int64_t want = (total + 255) / 256;
+  const int blocks = int(want < 65536 ? want : 65536);
+  hipLaunchKernelGGL(topn_hot_meta_kernel, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense, hot_meta,
+                     hot_split);
+}
+
+void launch_topn_index(const ViewDev& v, int S, int K, int k0, const int32_t* cache_dense, uint32_t* colcnt,
                        const uint32_t* colptr, const int64_t* entbase, uint16_t* slots, bool fill, hipStream_t st) {
-  const int64_t waves = int64_t(S) * K;
+  const int64_t waves = int64_t(S) * (K - k0);
   const int64_t want = (waves + 3) / 4;
   const int blocks = int(want < 256 * 64 ? want : 256 * 64);
   if (blocks <= 0) return;
   if (fill)
-    hipLaunchKernelGGL(topn_index_kernel<true>, dim3(blocks), dim3(256), 0, st, v, S, K, cache_dense, colcnt, colptr,
-                       entbase, slots);
+    hipLaunchKernelGGL(topn_index_kernel<true>, dim3(blocks), dim3(256), 0, st, v, S, K, k0, cache_dense, colcnt,
+                       colptr, entbase, slots);
   else
-    hipLaunchKernelGGL(topn_index_kernel<false>, dim3(blocks), dim3(256), 0, st, v, S, K, cache_dense, colcnt, colptr,
-                       entbase, slots);
+    hipLaunchKernelGGL(topn_index_kernel<false>, dim3(blocks), dim3(256), 0, st, v, S, K, k0, cache_dense, colcnt,
+                       colptr, entbase, slots);
 }
 
 int topn_lds_bytes(int K, int H32, int H16) {
@@ -455,10 +781,17 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
     return e ? atoi(e) : 0;
   }();
   a.dbg = dbg;
-  const int lds = topn_lds_bytes(a.K, a.H32, a.H16);
+  const int lds = topn_lds_bytes(a.K - a.R, a.H32, a.H16);
   const int64_t units = int64_t(a.Q) * a.S;
   if (units <= 0) return;
-  if (mode == 3) {
+  if (mode == 4) {
+    // hot-rank count matrix (before mode 1/2 of the same batch)
+    if (a.R <= 0) return;
+    const int tab = HOT_TAB_WORDS * 4;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, tab);
+    hipLaunchKernelGGL(topn_hot_kernel, dim3(unsigned(a.S) * 16u), dim3(HOT_THREADS), tab, st, a);
+  } else if (mode == 3) {
     hipLaunchKernelGGL(topn_gather_kernel, dim3(unsigned(units)), dim3(256), 0, st, a);
   } else if (mode == 1) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_src_kernel<1>),

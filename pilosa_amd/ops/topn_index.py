@@ -19,6 +19,7 @@ of the walk) sums one int64 per candidate with an all-reduce.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -29,6 +30,11 @@ from .device import DeviceView, GpuEngine, kernels
 
 SHARD_WIDTH = 1 << 20
 LDS_LIMIT = 160 * 1024 - 1024
+# cache ranks counted row-major for the whole batch (topn_hot_kernel); the
+# slot index / histogram cover the ranks after them
+HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "2048"))
+# queries per hot-rank launch (u16 query masks in the LDS table)
+HOT_Q = 16
 MAX_SLOTS = 65535
 # phase-1 histograms are kept for the ids= gather up to this many bytes per batch
 HIST_KEEP_BYTES = 8 << 30
@@ -48,7 +54,7 @@ class DeviceTopNIndex:
     pass the union of every rank's rows on a multi-GPU node (default: this
     view's rows)."""
 
-    def __init__(self, view: DeviceView, cache, space: Optional[np.ndarray] = None):
+    def __init__(self, view: DeviceView, cache, space: Optional[np.ndarray] = None, hot: Optional[int] = None):
         import torch
 
         ext = kernels()
@@ -81,21 +87,29 @@ class DeviceTopNIndex:
         self.cache_acc = t32(acc_i)
         self.cache_cnt = t32(np.where(valid, np.minimum(counts, 2 ** 31 - 1), 0))
         self.a2dense = t32(view.dense_many(space) if A else np.zeros(0))
+        # ranks [0, R): hot, counted row-major per batch; [R, K): slot index
+        self.R = R = max(0, min(K, HOT_RANKS if hot is None else int(hot)))
+        Kt = K - R
+        tail = counts[:, R:]
         # counter tiers from the cached counts (a src count never exceeds them)
-        n32 = int((counts >= 65536).sum(axis=1).max()) if S else 0
-        n16 = int((counts >= 256).sum(axis=1).max()) if S else 0
-        self.H32 = min(K, (n32 + 63) // 64 * 64)
-        self.H16 = max(self.H32, min(K, (n16 + 63) // 64 * 64))
-        self.lds = lds_bytes(K, self.H32, self.H16)
+        n32 = int((tail >= 65536).sum(axis=1).max()) if S and Kt else 0
+        n16 = int((tail >= 256).sum(axis=1).max()) if S and Kt else 0
+        self.H32 = min(Kt, (n32 + 63) // 64 * 64)
+        self.H16 = max(self.H32, min(Kt, (n16 + 63) // 64 * 64))
+        self.lds = lds_bytes(Kt, self.H32, self.H16)
         self.ok = self.lds <= LDS_LIMIT
         self._vd = torch.from_numpy(np.frombuffer(view.viewdev().tobytes(), dtype=np.uint8).copy())
 
         def empty(dt):
             return torch.empty(0, dtype=dt, device=dev)
 
+        self.hot_meta = torch.full((S * 16 * R,), -1, dtype=torch.int32, device=dev)
+        self.hot_split = torch.zeros(S * 16, dtype=torch.int32, device=dev)
+        if S and R:
+            ext.topn_hot_meta(self._vd, S, K, R, self.cache_dense, self.hot_meta, self.hot_split)
         colcnt = torch.zeros(S * SHARD_WIDTH, dtype=torch.int32, device=dev)
-        if S:
-            ext.topn_index(self._vd, S, K, self.cache_dense, colcnt, empty(torch.int32), empty(torch.int64),
+        if S and Kt:
+            ext.topn_index(self._vd, S, K, R, self.cache_dense, colcnt, empty(torch.int32), empty(torch.int64),
                            empty(torch.int16), False)
         self.colptr = torch.zeros((S, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
         if S:
@@ -107,9 +121,9 @@ class DeviceTopNIndex:
         self.entries = int(tot.sum().item()) if S else 0
         # +16 entries: the histogram reads each slot run as aligned 16-byte words
         self.slots = torch.zeros((self.entries + 16 + 7) // 8 * 8, dtype=torch.int16, device=dev)
-        if S:
+        if S and Kt:
             colcnt.zero_()
-            ext.topn_index(self._vd, S, K, self.cache_dense, colcnt, self.colptr, self.entbase, self.slots, True)
+            ext.topn_index(self._vd, S, K, R, self.cache_dense, colcnt, self.colptr, self.entbase, self.slots, True)
         del colcnt
         self.slotmap = torch.full((S, max(A, 1)), -1, dtype=torch.int32, device=dev)
         si, ki = torch.nonzero(self.cache_dense >= 0, as_tuple=True)
@@ -120,7 +134,7 @@ class DeviceTopNIndex:
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.cache_dense, self.cache_acc, self.cache_cnt,
                                                           self.a2dense, self.colptr, self.entbase, self.slots,
-                                                          self.slotmap))
+                                                          self.slotmap, self.hot_meta))
 
     @property
     def stale(self) -> bool:
@@ -128,7 +142,7 @@ class DeviceTopNIndex:
 
     # ------------------------------------------------------------ queries
     def _launch(self, mode: int, Q: int, src, ns_t, th_t, acc=None, pair_off=None, pair_idx=None, out=None,
-                hist=None):
+                hist=None, hot_cnt=None, tail_built=None):
         import torch
 
         dev = self.view.device
@@ -139,15 +153,33 @@ class DeviceTopNIndex:
                            self.entbase, self.slots, self.cache_cnt, self.cache_acc, self.slotmap, self.a2dense,
                            ns_t, th_t, mode, acc if acc is not None else e32,
                            pair_off if pair_off is not None else e64, pair_idx if pair_idx is not None else e32,
-                           out if out is not None else e64, hist if hist is not None else e32)
+                           out if out is not None else e64, hist if hist is not None else e32,
+                           self.R, self.hot_meta, hot_cnt if hot_cnt is not None else e32,
+                           tail_built if tail_built is not None else e32, self.cache_dense, self.hot_split)
+
+    def hot_counts(self, src, Q: int):
+        """int32[S, Q, R]: src counts of the hot cache ranks (one row-major
+        pass per 16 queries), or None without hot ranks."""
+        import torch
+
+        if not self.R or not Q or not self.S:
+            return None
+        if Q > HOT_Q:
+            raise ValueError("hot_counts: at most 16 queries per call")
+        dev = self.view.device
+        hot = torch.zeros(self.S * Q * self.R, dtype=torch.int32, device=dev)
+        z = torch.zeros(Q, dtype=torch.int32, device=dev)
+        self._launch(4, Q, src, z, z, hot_cnt=hot)
+        return hot
 
     def hist_bytes(self, Q: int) -> int:
         return self.lds * Q * self.S
 
-    def phase1(self, src, Q: int, ns: Sequence[int], thresholds: Sequence[int], keep_hist: bool = False):
+    def phase1(self, src, Q: int, ns: Sequence[int], thresholds: Sequence[int], keep_hist: bool = False,
+               hot=None):
         """acc int32[Q, A]: per query the per-shard heap results summed by row.
         ``keep_hist`` also returns the (query, shard) slot histograms so the
-        ids= re-count is a gather (else None)."""
+        ids= re-count is a gather (else None).  ``hot``: hot_counts(src, Q)."""
         import torch
 
         dev = self.view.device
@@ -155,11 +187,13 @@ class DeviceTopNIndex:
         th_t = torch.tensor(list(thresholds), dtype=torch.int32).to(dev)
         acc = torch.zeros((Q, self.A), dtype=torch.int32, device=dev)
         hist = torch.empty(self.hist_bytes(Q) // 4, dtype=torch.int32, device=dev) if keep_hist else None
+        # which units built their tail histogram (phase 2 probes the others exactly)
+        tb = torch.ones(Q * self.S, dtype=torch.int32, device=dev) if keep_hist else None
         if Q and self.S and self.A:
-            self._launch(1, Q, src, ns_t, th_t, acc=acc, hist=hist)
-        return acc, ns_t, th_t, hist
+            self._launch(1, Q, src, ns_t, th_t, acc=acc, hist=hist, hot_cnt=hot, tail_built=tb)
+        return acc, ns_t, th_t, (hist, tb) if keep_hist else None
 
-    def phase2(self, src, Q: int, ns_t, th_t, pair_q, pair_idx, hist=None):
+    def phase2(self, src, Q: int, ns_t, th_t, pair_q, pair_idx, hist=None, hot=None):
         """Exact per-shard re-count of (query, acc index) pairs, summed over
         the local shards where it reaches the threshold (ids= semantics);
         from phase 1's kept histograms when given, else rebuilt."""
@@ -171,8 +205,10 @@ class DeviceTopNIndex:
         if P and self.S:
             off = torch.zeros(Q + 1, dtype=torch.int64, device=dev)
             off[1:] = torch.cumsum(torch.bincount(pair_q, minlength=Q), 0)
-            self._launch(3 if hist is not None else 2, Q, src, ns_t, th_t, pair_off=off,
-                         pair_idx=pair_idx.to(torch.int32).contiguous(), out=out, hist=hist)
+            h, tb = hist if hist is not None else (None, None)
+            self._launch(3 if h is not None else 2, Q, src, ns_t, th_t, pair_off=off,
+                         pair_idx=pair_idx.to(torch.int32).contiguous(), out=out, hist=h, hot_cnt=hot,
+                         tail_built=tb)
         return out
 
     def _candidates(self, acc, comm):
@@ -199,11 +235,17 @@ class DeviceTopNIndex:
         Q = len(srcs)
         if Q == 0:
             return []
+        if self.R and Q > HOT_Q:
+            out: List[List[Pair]] = []
+            for i in range(0, Q, HOT_Q):
+                out += self.topn(engine, srcs[i:i + HOT_Q], ns[i:i + HOT_Q], thresholds[i:i + HOT_Q], comm)
+            return out
         src = engine.materialize_batch(srcs, self.S)
+        hot = self.hot_counts(src, Q)
         keep = self.hist_bytes(Q) <= HIST_KEEP_BYTES
-        acc, ns_t, th_t, hist = self.phase1(src, Q, ns, thresholds, keep_hist=keep)
+        acc, ns_t, th_t, hist = self.phase1(src, Q, ns, thresholds, keep_hist=keep, hot=hot)
         pair_q, pair_idx = self._candidates(acc, comm)
-        out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx, hist=hist)
+        out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx, hist=hist, hot=hot)
         if comm is not None:
             comm.all_reduce(out)
         return finish_batch_dev(self.space, Q, pair_q, pair_idx, out, ns)
@@ -218,8 +260,9 @@ class DeviceTopNIndex:
 
         dev = self.view.device
         src_t = engine.materialize_batch([src], self.S)
+        hot = self.hot_counts(src_t, 1)
         if ids is None:
-            acc, _, _, _ = self.phase1(src_t, 1, [n], [threshold])
+            acc, _, _, _ = self.phase1(src_t, 1, [n], [threshold], hot=hot)
             nz = torch.nonzero(acc[0] > 0).reshape(-1)
             a = nz.cpu().numpy()
             c = acc[0].index_select(0, nz).cpu().numpy()
@@ -231,7 +274,7 @@ class DeviceTopNIndex:
             ns_t = torch.zeros(1, dtype=torch.int32, device=dev)
             th_t = torch.tensor([threshold], dtype=torch.int32).to(dev)
             pa = torch.from_numpy(a.astype(np.int64)).to(dev)
-            out = self.phase2(src_t, 1, ns_t, th_t, torch.zeros_like(pa), pa)
+            out = self.phase2(src_t, 1, ns_t, th_t, torch.zeros_like(pa), pa, hot=hot)
             c = out.cpu().numpy()
         keep = c > 0
         ids_out = self.space[a[keep]] if len(a) else np.zeros(0, np.uint64)

@@ -40,23 +40,28 @@ def main():
     idx = DeviceTopNIndex(view, cache)
     torch.cuda.synchronize()
     out = {"shards": S, "index_build_s": round(time.perf_counter() - t0, 2), "H32": idx.H32, "H16": idx.H16,
-           "lds_bytes": idx.lds, "classes": {}}
+           "lds_bytes": idx.lds, "hot_ranks": idx.R, "slot_entries": idx.entries, "classes": {}}
     B = args.batch
     for name, rows in (("hot 0-15", range(0, 16)), ("warm 100-115", range(100, 116)),
                        ("cold 900-915", range(900, 900 + B))):
         srcs = [Leaf(view, r) for r in list(rows)[:B]]
         src = eng.materialize_batch(srcs, idx.S)
-        acc, ns_t, th_t, hist = idx.phase1(src, B, [100] * B, [1] * B, keep_hist=True)
+        hot = idx.hot_counts(src, B)
+        acc, ns_t, th_t, hist = idx.phase1(src, B, [100] * B, [1] * B, keep_hist=True, hot=hot)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
         for _ in range(args.reps):
-            idx._launch(1, B, src, ns_t, th_t, acc=acc, hist=hist)
+            hot = idx.hot_counts(src, B)
         e1.record()
+        for _ in range(args.reps):
+            idx._launch(1, B, src, ns_t, th_t, acc=acc, hist=hist[0], hot_cnt=hot, tail_built=hist[1])
+        e2.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / args.reps
+        ms_hot = e0.elapsed_time(e1) / args.reps
+        ms = e1.elapsed_time(e2) / args.reps
         nsrc = int(src[0].sum().item())
-        out["classes"][name] = {"phase1_ms": round(ms, 3), "src_bits": nsrc,
+        out["classes"][name] = {"hot_ms": round(ms_hot, 3), "phase1_ms": round(ms, 3), "src_bits": nsrc,
                                 "dbg": int(os.environ.get("PILOSA_TOPN_DBG", "0"))}
     if not int(os.environ.get("PILOSA_TOPN_DBG", "0")):
         # the bench mix (src rows Zipf over the 1000 hottest): end to end and
@@ -83,11 +88,13 @@ def main():
         t = time.perf_counter()
         src = eng.materialize_batch(srcs, idx.S)
         t = mark("materialize", t)
-        acc, ns_t, th_t, hist = idx.phase1(src, B, [100] * B, [1] * B, keep_hist=True)
+        hot = idx.hot_counts(src, B)
+        t = mark("hot", t)
+        acc, ns_t, th_t, hist = idx.phase1(src, B, [100] * B, [1] * B, keep_hist=True, hot=hot)
         t = mark("phase1", t)
         pq, pa = idx._candidates(acc, None)
         t = mark("candidates", t)
-        cnt = idx.phase2(src, B, ns_t, th_t, pq, pa, hist=hist)
+        cnt = idx.phase2(src, B, ns_t, th_t, pq, pa, hist=hist, hot=hot)
         t = mark("phase2", t)
         finish_batch_dev(idx.space, B, pq, pa, cnt, [100] * B)
         mark("finish", t)

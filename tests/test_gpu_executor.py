@@ -294,11 +294,13 @@ def test_hbm_budget_lru_eviction(envs):
     assert sum(st["containers"].values()) > 0
 
 
-@pytest.mark.parametrize("k", [5000, 100, 7])
-def test_slot_index_topn_matches_replay(envs, k):
-    """Column-major slot index + LDS-histogram heap walk (ops/topn_index.py)
-    == the exact host replay over the same device rank cache; small caches
-    exercise the ids outside a shard's cache (in-kernel exact probe)."""
+@pytest.mark.parametrize("k,hot", [(5000, 0), (5000, 37), (5000, None), (100, 0), (100, 64), (100, 100), (7, 3)])
+def test_slot_index_topn_matches_replay(envs, k, hot):
+    """Hot-rank count matrix + column-major slot index + LDS-histogram heap
+    walk (ops/topn_index.py) == the exact host replay over the same device
+    rank cache, for every split of the cache ranks between the two (hot=0:
+    histogram only, hot=k: row-major only); small caches exercise the ids
+    outside a shard's cache (in-kernel exact probe)."""
     from pilosa_amd.ops.topn import DeviceRankCache, topn_batch
     from pilosa_amd.ops.topn_index import DeviceTopNIndex
     from pilosa_amd.pql import parse_string
@@ -306,8 +308,8 @@ def test_slot_index_topn_matches_replay(envs, k):
     shards = cpu.holder.index("i").available_shards()
     hv = gpu.view_arena("i", "h", "standard", shards)
     cache = DeviceRankCache.from_view(hv, k=k)
-    idx = DeviceTopNIndex(hv, cache)
-    assert idx.ok and idx.entries > 0
+    idx = DeviceTopNIndex(hv, cache, hot=hot)
+    assert idx.ok and (idx.entries > 0 or idx.R >= min(k, cache.rows.shape[1]))
     cases = ["Row(f=2)", "Row(f=3)", "Row(g=1)", "Row(f=0)", "Row(h=0)", "Intersect(Row(f=0), Row(g=2))",
              "Union(Row(f=20), Row(f=1))"]
     srcs = [gpu.plan("i", parse_string(q).calls[0], shards) for q in cases]
