@@ -206,6 +206,19 @@ void topn_index(torch::Tensor view, int64_t S, int64_t K, int64_t k0, torch::Ten
   check_launch("topn_index");
 }
 
+void leaf_src(torch::Tensor view, torch::Tensor rows, int64_t S, torch::Tensor counts, torch::Tensor offs,
+              torch::Tensor has_run) {
+  for (auto* t : {&rows, &counts, &offs, &has_run}) check_dev(*t, "leaf_src");
+  const int64_t Q = rows.numel();
+  TORCH_CHECK(rows.scalar_type() == torch::kInt64, "rows int64[Q]");
+  TORCH_CHECK(counts.scalar_type() == torch::kInt32 && counts.numel() == Q * S * 16, "counts int32[Q*S*16]");
+  TORCH_CHECK(offs.scalar_type() == torch::kInt64 && offs.numel() == Q * S * 16, "offs int64[Q*S*16]");
+  TORCH_CHECK(has_run.scalar_type() == torch::kInt32 && has_run.numel() == 1, "has_run int32[1]");
+  pk::launch_leaf_src(viewdev_from(view), rows.data_ptr<int64_t>(), int(Q), int(S), counts.data_ptr<int32_t>(),
+                      offs.data_ptr<int64_t>(), has_run.data_ptr<int32_t>(), cur_stream(rows));
+  check_launch("leaf_src");
+}
+
 void topn_hot_meta(torch::Tensor view, int64_t S, int64_t K, int64_t R, torch::Tensor cache_dense,
                    torch::Tensor hot_meta, torch::Tensor hot_split) {
   check_dev(cache_dense, "cache_dense");
@@ -412,6 +425,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
   m.def("bsi_range_count", &bsi_range_count, "Count(Row(v <op> x)): fused BSI predicate + count");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
+  m.def("leaf_src", &leaf_src, "src containers of plain rows straight from the arena (TopN srcs)");
   m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");

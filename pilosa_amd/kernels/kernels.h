@@ -113,6 +113,10 @@ int topn_lds_bytes(int K, int H32, int H16);
 // -> out[P] (rebuilds the histograms); mode 3: ids= re-count from hist_in.
 // mode 4: hot-rank count matrix hot_cnt (row-major over the batch).
 void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
+// Src containers (counts / u16 offsets into the arena payload) of plain
+// rows; *has_run set when a run container needs materialising.
+void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_t* counts, int64_t* offs,
+                     int32_t* has_run, hipStream_t st);
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st);
 

@@ -744,7 +744,37 @@ __global__ __launch_bounds__(256) void topn_hot_meta_kernel(ViewDev v, int S, in
   }
 }
 
+// Src containers of plain-row srcs straight from the arena (no copy):
+// counts[(q*S + s)*16 + j] = n, offs = the container's u16 payload offset;
+// run containers set *has_run (the caller then materialises instead).
+__global__ __launch_bounds__(256) void leaf_src_kernel(ViewDev v, const int64_t* __restrict__ rows, int Q, int S,
+                                                       int32_t* __restrict__ counts, int64_t* __restrict__ offs,
+                                                       int32_t* __restrict__ has_run) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= int64_t(Q) * S) return;
+  const int q = int(e / S), s = int(e - int64_t(q) * S);
+  const int64_t d = rows[q];
+  if (d < 0) return;
+  const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+  const int64_t sb = v.shard_base[s];
+  for (uint32_t c = rp[d]; c < rp[d + 1]; c++) {
+    const int64_t m = v.meta[sb + c];
+    const int64_t o = (int64_t(q) * S + s) * 16 + meta_j(m);
+    counts[o] = meta_n(m);
+    offs[o] = meta_off16(m) * 8;
+    if (meta_type(m) == CT_RUN) atomicOr(has_run, 1);
+  }
+}
+
 }  // namespace
+
+void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_t* counts, int64_t* offs,
+                     int32_t* has_run, hipStream_t st) {
+  const int64_t total = int64_t(Q) * S;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(leaf_src_kernel, dim3(unsigned((total + 255) / 256)), dim3(256), 0, st, v, rows, Q, S, counts,
+                     offs, has_run);
+}
 
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st) {

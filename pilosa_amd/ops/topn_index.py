@@ -157,6 +157,27 @@ class DeviceTopNIndex:
                            self.R, self.hot_meta, hot_cnt if hot_cnt is not None else e32,
                            tail_built if tail_built is not None else e32, self.cache_dense, self.hot_split)
 
+    def materialize(self, engine: GpuEngine, srcs: Sequence[object]):
+        """Src containers of a batch: plain rows of this view are read in
+        place from the arena (leaf_src, no copy); anything else (or a row
+        with a run container) is materialised by the engine."""
+        import torch
+
+        from .device import Leaf
+
+        Q = len(srcs)
+        if Q and self.S and all(isinstance(x, Leaf) and x.view is self.view for x in srcs):
+            dev = self.view.device
+            dense = self.view.dense_many(np.array([x.row for x in srcs], dtype=np.uint64))
+            rows = torch.from_numpy(np.asarray(dense, dtype=np.int64)).to(dev)
+            counts = torch.zeros(Q * self.S * 16, dtype=torch.int32, device=dev)
+            offs = torch.zeros(Q * self.S * 16, dtype=torch.int64, device=dev)
+            has_run = torch.zeros(1, dtype=torch.int32, device=dev)
+            kernels().leaf_src(self._vd, rows, self.S, counts, offs, has_run)
+            if not int(has_run.item()):
+                return counts, offs, self.view.t_payload
+        return engine.materialize_batch(srcs, self.S)
+
     def hot_counts(self, src, Q: int):
         """int32[S, Q, R]: src counts of the hot cache ranks (one row-major
         pass per 16 queries), or None without hot ranks."""
@@ -240,7 +261,7 @@ class DeviceTopNIndex:
             for i in range(0, Q, HOT_Q):
                 out += self.topn(engine, srcs[i:i + HOT_Q], ns[i:i + HOT_Q], thresholds[i:i + HOT_Q], comm)
             return out
-        src = engine.materialize_batch(srcs, self.S)
+        src = self.materialize(engine, srcs)
         hot = self.hot_counts(src, Q)
         keep = self.hist_bytes(Q) <= HIST_KEEP_BYTES
         acc, ns_t, th_t, hist = self.phase1(src, Q, ns, thresholds, keep_hist=keep, hot=hot)
@@ -259,7 +280,7 @@ class DeviceTopNIndex:
         import torch
 
         dev = self.view.device
-        src_t = engine.materialize_batch([src], self.S)
+        src_t = self.materialize(engine, [src])
         hot = self.hot_counts(src_t, 1)
         if ids is None:
             acc, _, _, _ = self.phase1(src_t, 1, [n], [threshold], hot=hot)

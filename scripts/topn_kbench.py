@@ -86,7 +86,7 @@ def main():
             return now
         srcs = batches[1]
         t = time.perf_counter()
-        src = eng.materialize_batch(srcs, idx.S)
+        src = idx.materialize(eng, srcs)
         t = mark("materialize", t)
         hot = idx.hot_counts(src, B)
         t = mark("hot", t)
