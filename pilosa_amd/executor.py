@@ -269,9 +269,9 @@ class Executor:
                     if a:
                         sets.append({"id": cid, "attrs": a})
                 if idx.keys:
-                    for s in sets:
-                        s["key"] = self.holder.translate.translate_column_to_string(index, s["id"])
-                        s.pop("id")
+                    # ColumnAttrSet field order: id / key, then attrs (executor.go ColumnAttrSet)
+                    ts = self.holder.translate
+                    sets = [{"key": ts.translate_column_to_string(index, s["id"]), "attrs": s["attrs"]} for s in sets]
                 resp.column_attr_sets = sets
             if not opt.remote:
                 resp.results = [self._translate_result(index, idx, c, r) for c, r in zip(q.calls, results)]
@@ -728,7 +728,7 @@ class Executor:
             raise PilosaError("Row(): too many arguments")
         (fname, cond), = c.args.items()
         if not isinstance(cond, Condition):
-            raise PilosaError(f"Row(): {fname!r}: expected condition argument, got {cond}")
+            raise PilosaError(f'Row(): "{fname}": expected condition argument, got {cond}')
         f = self.holder.field(index, fname)
         if f is None:
             raise ErrFieldNotFound
@@ -912,7 +912,7 @@ class Executor:
         n, _ = c.uint_arg("n")
         f = self.holder.field(index, fname)
         if f is not None and f.type == FIELD_TYPE_INT:
-            raise PilosaError(f"cannot compute TopN() on integer field: {fname!r}")
+            raise PilosaError(f'cannot compute TopN() on integer field: "{fname}"')
         ids, _ = c.uint_slice_arg("ids")
         threshold, _ = c.uint_arg("threshold")
         tanimoto, _ = c.uint_arg("tanimotoThreshold")
@@ -931,7 +931,7 @@ class Executor:
         if frag is None:
             return []
         if frag.cache_type == "none":
-            raise PilosaError(f"cannot compute TopN(), field has no cache: {fname!r}")
+            raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
         f = self.holder.field(index, fname)
         return frag.top(TopOptions(n=n, src=src, row_ids=ids, min_threshold=threshold, filter_name=attr_name,
                                    filter_values=attr_values, tanimoto_threshold=tanimoto,
@@ -1054,22 +1054,42 @@ class Executor:
         return out
 
     @staticmethod
-    def group_by_previous(c: Call) -> Optional[Tuple[int, ...]]:
+    def group_by_start(c: Call) -> Optional[Tuple[Optional[int], ...]]:
+        """Paging start of a GroupBy, or None (no paging).
+
+        Reference groupByIterator (executor.go:3085-3145): a child with
+        ``previous=p`` seeks its row iterator to p (the last child to p + 1);
+        a child without it starts at its first row; a child whose seek lands
+        past p makes the deeper children start from their first row, and
+        deeper iterators wrap.  So a shard returns the keys lexicographically
+        >= start, with start_i = p_i (last: p + 1) and, for children without
+        ``previous`` (None here), that shard's first row of the field
+        (resolve_group_start)."""
+        k = len(c.children)
         prev = c.args.get("previous")
-        if prev is None:
-            # per-child previous (reference Rows(previous=...))
-            ps = []
-            for ch in c.children:
-                p, ok = ch.uint_arg("previous")
-                if not ok:
-                    return None
-                ps.append(p)
-            return tuple(ps)
-        if not isinstance(prev, list):
-            raise PilosaError(f"'previous' argument must be list, but got {type(prev).__name__}")
-        if len(prev) != len(c.children):
-            raise PilosaError(f"mismatched lengths for previous: {len(prev)} and children: {len(c.children)}")
-        return tuple(int(x) for x in prev)
+        if prev is not None:
+            if not isinstance(prev, list):
+                raise PilosaError(f"'previous' argument must be list, but got {type(prev).__name__}")
+            if len(prev) != k:
+                raise PilosaError(f"mismatched lengths for previous: {len(prev)} and children: {k}")
+            ps = [int(x) for x in prev]
+            return tuple(ps[:-1]) + (ps[-1] + 1,)
+        start: List[Optional[int]] = []
+        any_prev = False
+        for i, ch in enumerate(c.children):
+            p, ok = ch.uint_arg("previous")
+            any_prev |= ok
+            start.append((p + 1 if i == k - 1 else p) if ok else None)
+        return tuple(start) if any_prev else None
+
+    @staticmethod
+    def resolve_group_start(start, cands) -> Optional[Tuple[int, ...]]:
+        """group_by_start with each None replaced by the field's first
+        candidate row (sorted candidates per field)."""
+        if start is None:
+            return None
+        return tuple(s if s is not None else (int(cands[i][0]) if len(cands[i]) else -1)
+                     for i, s in enumerate(start))
 
     def _group_by_shard(self, index: str, c: Call, filt: Optional[Call], shard: int, child_rows, limit):
         cands = self.group_by_candidates(index, c, shard, child_rows)
@@ -1077,7 +1097,7 @@ class Executor:
             return []
         filt_row = self.bitmap_call_shard(index, filt, shard) if filt is not None else None
         fields = [ch.args["_field"] for ch in c.children]
-        prev = self.group_by_previous(c)
+        start = self.resolve_group_start(self.group_by_start(c), cands)
         frags = [self.holder.fragment(index, f, VIEW_STANDARD, shard) for f in fields]
         results: List[GroupCount] = []
         k = len(fields)
@@ -1085,7 +1105,7 @@ class Executor:
         def rec(level: int, acc: Optional[Row], prefix: Tuple[int, ...]):
             for rid in cands[level]:
                 key = prefix + (rid,)
-                if prev is not None and key[:len(key)] < prev[:len(key)]:
+                if start is not None and key < start[:len(key)]:
                     continue
                 r = frags[level].row(rid)
                 if level == 0 and filt_row is not None:
@@ -1094,8 +1114,6 @@ class Executor:
                 if cur.is_empty():
                     continue
                 if level == k - 1:
-                    if prev is not None and key <= prev:
-                        continue
                     results.append(GroupCount([FieldRow(fields[i], key[i]) for i in range(k)], cur.count()))
                     if len(results) >= limit:
                         return True
@@ -1396,19 +1414,20 @@ class Executor:
             if isinstance(fname, str) and fname:
                 f = idx.field(fname)
                 if f is None:
-                    raise PilosaError(f"field {fname!r} not found")
+                    raise PilosaError(f'field "{fname}" not found')
                 if f.keys():
                     key = ts.translate_row_to_string(index, fname, r.id)
                     if c.name in ("MinRow", "MaxRow"):
                         return Pair(r.id, r.count, key)
                     return Pair(0, r.count, key)
             return r
-        if isinstance(r, list) and r and isinstance(r[0], Pair):
+        # a []Pair result -- TopN's, even empty (executor.go:2832-2846)
+        if isinstance(r, list) and (c.name == "TopN" or (r and isinstance(r[0], Pair))):
             fname = c.args.get("_field")
             if isinstance(fname, str) and fname:
                 f = idx.field(fname)
                 if f is None:
-                    raise PilosaError(f"field {fname!r} not found")
+                    raise PilosaError(f'field "{fname}" not found')
                 if f.keys():
                     return [Pair(0, p.count, ts.translate_row_to_string(index, fname, p.id)) for p in r]
             return r

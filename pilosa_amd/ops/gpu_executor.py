@@ -705,7 +705,7 @@ class GpuExecutor:
         for f in frags:
             if f is not None and f.cache_type == "none":
                 from pilosa_amd.errors import PilosaError
-                raise PilosaError(f"cannot compute TopN(), field has no cache: {fname!r}")
+                raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
         # candidate (row, cached count) lists per shard, as fragment.top() would see them
         per_shard_pairs = [f._top_bitmap_pairs(ids) if f is not None else [] for f in frags]
         cand = sorted({rid for pairs in per_shard_pairs for rid, _ in pairs})
@@ -827,7 +827,18 @@ class GpuExecutor:
             fexpr = self.plan(index, filt, shards)
             if fexpr is EMPTY:
                 return []
-        prev = ex.group_by_previous(c)
+        start = ex.group_by_start(c)
+        if start is not None:
+            # a child without previous starts at ITS first row in EACH shard
+            # (reference iterator per shard): exact on the merged candidates
+            # only when such children all come after the paged ones
+            seen_none = False
+            for v in start:
+                if v is None:
+                    seen_none = True
+                elif seen_none:
+                    raise NotImplementedError
+            start = tuple(-1 if v is None else v for v in start)
         if k == 2 and len(cand[0]) * len(cand[1]) >= GROUPBY_MATRIX_MIN and \
                 (fexpr is None or type(fexpr) is Leaf) and self._matrix_fits(len(cand[0]), len(cand[1])):
             # two fields: the whole count matrix in one bit-GEMM (MFMA), then
@@ -838,9 +849,10 @@ class GpuExecutor:
                                     filt=(fexpr.view, fexpr.row) if fexpr is not None else None,
                                     chunk_bytes=self._groupby_budget() - len(cand[0]) * len(cand[1]) * 12)
             return [GroupCount([FieldRow(fields[0], ra), FieldRow(fields[1], rb)], n)
-                    for ra, rb, n in emit_groups(cand[0], cand[1], mat, prev, limit)]
+                    for ra, rb, n in emit_groups(cand[0], cand[1], mat,
+                                                 None if start is None else (start[0], start[1] - 1), limit)]
         try:
-            groups = self._pruned_groups(arenas, cand, fexpr, prev, limit)
+            groups = self._pruned_groups(arenas, cand, fexpr, start, limit)
         except CompileError:
             raise NotImplementedError
         return [GroupCount([FieldRow(fields[i], key[i]) for i in range(k)], n) for key, n in groups]
@@ -864,7 +876,7 @@ class GpuExecutor:
         need = (ra + rb) * WORDS_PER_SHARD * 8 + ra * rb * 12
         return need <= self._groupby_budget()
 
-    def _pruned_groups(self, arenas, cand, fexpr, prev, limit: int):
+    def _pruned_groups(self, arenas, cand, fexpr, start, limit: int):
         """GroupBy combinations in lexicographic order with cumulative-
         intersection pruning (reference groupByIterator, executor.go:3060-3230):
         a prefix whose intersection (with the filter) is empty is never
@@ -885,7 +897,7 @@ class GpuExecutor:
             i = 0
             while i < len(todo) and len(todo[i][0]) == lvl and len(keys) < budget:
                 pre, j = todo[i]
-                rows = self._next_rows(cand[lvl], pre, prev)
+                rows = self._next_rows(cand[lvl], pre, start)
                 take = rows[j:j + budget - len(keys)]
                 keys.extend(pre + (r,) for r in take)
                 if j + len(take) < len(rows):
@@ -902,7 +914,7 @@ class GpuExecutor:
             live = [(key, int(v)) for key, v in zip(keys, got) if v > 0]
             if lvl + 1 == k:
                 for key, v in live:
-                    if prev is not None and key <= prev:
+                    if start is not None and key < start:
                         continue
                     out.append((key, v))
                     if len(out) >= limit:
@@ -950,12 +962,13 @@ class GpuExecutor:
         return eng.launch_count(eng.prepare_progs(progs, views, views[0].S)).cpu().numpy()
 
     @staticmethod
-    def _next_rows(rows: List[int], prefix: Tuple[int, ...], prev: Optional[Tuple[int, ...]]) -> List[int]:
+    def _next_rows(rows: List[int], prefix: Tuple[int, ...], start: Optional[Tuple[int, ...]]) -> List[int]:
         """Rows of the next field for ``prefix``: while the prefix equals
-        ``prev``'s, only rows from prev's row on (paging)."""
-        if prev is None or tuple(prev[:len(prefix)]) != prefix:
+        ``start``'s, only rows from start's row on (paging,
+        Executor.group_by_start)."""
+        if start is None or tuple(start[:len(prefix)]) != prefix:
             return rows
-        lo = prev[len(prefix)]
+        lo = start[len(prefix)]
         return [r for r in rows if r >= lo]
 
 

@@ -10,6 +10,12 @@ from __future__ import annotations
 import datetime as _dt
 from typing import Any, Dict, List, Optional
 
+from pilosa_amd.errors import PilosaError
+
+
+class ArgError(PilosaError, ValueError):
+    """A call argument of the wrong type or range (pql/ast.go Call.*Arg errors)."""
+
 # tokens (pql/token.go)
 ILLEGAL, EQ, NEQ, LT, LTE, GT, GTE, BETWEEN = "ILLEGAL", "==", "!=", "<", "<=", ">", ">=", "><"
 TOKENS = (EQ, NEQ, LT, LTE, GT, GTE, BETWEEN)
@@ -35,11 +41,11 @@ class Condition:
 
     def int_slice_value(self) -> List[int]:
         if not isinstance(self.value, list):
-            raise ValueError(f"unexpected type {type(self.value).__name__} in IntSliceValue, val {self.value}")
+            raise ArgError(f"unexpected type {type(self.value).__name__} in IntSliceValue, val {self.value}")
         out = []
         for v in self.value:
             if isinstance(v, bool) or not isinstance(v, int):
-                raise ValueError(f"unexpected value type {type(v).__name__} in IntSliceValue, val {v}")
+                raise ArgError(f"unexpected value type {type(v).__name__} in IntSliceValue, val {v}")
             out.append(v)
         return out
 
@@ -71,14 +77,14 @@ class Call:
         for k in self.args:
             if not is_reserved_arg(k):
                 return k
-        raise ValueError("no field argument specified")
+        raise ArgError("no field argument specified")
 
     def bool_arg(self, key):
         if key not in self.args:
             return False, False
         v = self.args[key]
         if not isinstance(v, bool):
-            raise ValueError(f"could not convert {v} of type {type(v).__name__} to bool in Call.BoolArg")
+            raise ArgError(f"could not convert {v} of type {type(v).__name__} to bool in Call.BoolArg")
         return v, True
 
     def uint_arg(self, key):
@@ -86,9 +92,9 @@ class Call:
             return 0, False
         v = self.args[key]
         if isinstance(v, bool) or not isinstance(v, int):
-            raise ValueError(f"could not convert {v} of type {type(v).__name__} to uint64 in Call.UintArg")
+            raise ArgError(f"could not convert {v} of type {type(v).__name__} to uint64 in Call.UintArg")
         if v < 0:
-            raise ValueError(f"value for '{key}' must be positive, but got {v}")
+            raise ArgError(f"value for '{key}' must be positive, but got {v}")
         return v, True
 
     def int_arg(self, key):
@@ -96,7 +102,7 @@ class Call:
             return 0, False
         v = self.args[key]
         if isinstance(v, bool) or not isinstance(v, int):
-            raise ValueError(f"could not convert {v} of type {type(v).__name__} to int64 in Call.IntArg")
+            raise ArgError(f"could not convert {v} of type {type(v).__name__} to int64 in Call.IntArg")
         return v, True
 
     def uint_slice_arg(self, key):
@@ -104,7 +110,7 @@ class Call:
             return None, False
         v = self.args[key]
         if not isinstance(v, list) or not all(isinstance(x, int) and not isinstance(x, bool) for x in v):
-            raise ValueError(f"unexpected type {type(v).__name__} in UintSliceArg, val {v}")
+            raise ArgError(f"unexpected type {type(v).__name__} in UintSliceArg, val {v}")
         return [int(x) for x in v], True
 
     def call_arg(self, key):
@@ -112,7 +118,7 @@ class Call:
             return None, False
         v = self.args[key]
         if not isinstance(v, Call):
-            raise ValueError(f"could not convert {v} of type {type(v).__name__} to Call in Call.CallArg")
+            raise ArgError(f"could not convert {v} of type {type(v).__name__} to Call in Call.CallArg")
         return v, True
 
     def has_condition_arg(self) -> bool:

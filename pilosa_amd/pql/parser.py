@@ -360,7 +360,7 @@ class Parser:
     def _int(s: str) -> int:
         v = int(s)
         if v < _INT64_MIN or v > _INT64_MAX:
-            raise ParseError(f"{INT_OUT_OF_RANGE}: strconv.ParseInt: parsing {s!r}: value out of range")
+            raise ParseError(f'{INT_OUT_OF_RANGE}: strconv.ParseInt: parsing "{s}": value out of range')
         return v
 
     def _num(self, s: str):

@@ -8,9 +8,45 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+_SHM_TMP = None
+
+
+def _shm_tmp():
+    """Test data dirs on /dev/shm when it exists: the tests' many small
+    files, fsyncs and sqlite commits cost ~30 ms each on an overlay /tmp.
+    Stale dirs of dead test processes are removed first."""
+    import shutil
+    import tempfile
+    base = "/dev/shm"
+    if os.environ.get("PILOSA_TEST_TMP") == "keep" or not os.path.isdir(base) or not os.access(base, os.W_OK):
+        return None
+    for name in os.listdir(base):
+        if name.startswith("pilosa_amd_tests_"):
+            try:
+                pid = int(name.rsplit("_", 1)[1])
+                os.kill(pid, 0)
+            except (ValueError, ProcessLookupError):
+                shutil.rmtree(os.path.join(base, name), ignore_errors=True)
+            except PermissionError:
+                pass
+    d = os.path.join(base, f"pilosa_amd_tests_{os.getpid()}")
+    os.makedirs(d, exist_ok=True)
+    tempfile.tempdir = d
+    os.environ["TMPDIR"] = d
+    return d
+
+
 def pytest_configure(config):
+    global _SHM_TMP
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")
+    _SHM_TMP = _shm_tmp()
+
+
+def pytest_unconfigure(config):
+    if _SHM_TMP:
+        import shutil
+        shutil.rmtree(_SHM_TMP, ignore_errors=True)
 
 
 def _gpu_available():
