@@ -825,7 +825,8 @@ class Fragment:
         return sort_pairs(results)
 
     def _top_bitmap_pairs(self, row_ids: Sequence[int]) -> List[Tuple[int, int]]:
-        if self.cache_type == CACHE_TYPE_NONE and not row_ids:
+        # no cache: nothing, even for explicit ids (fragment.go topBitmapPairs)
+        if self.cache_type == CACHE_TYPE_NONE:
             return list(self.cache.top())
         if not row_ids:
             with self.mu:

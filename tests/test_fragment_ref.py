@@ -1,0 +1,415 @@
+"""Expectations ported from the reference fragment tests
+(/root/reference/fragment_internal_test.go), one test per reference function
+(line ranges cited); run against models/fragment.py on the CPU."""
+import io
+import os
+import random
+import shutil
+import tempfile
+
+import numpy as np
+import pytest
+
+from pilosa_amd.models.cache import CACHE_TYPE_LRU, CACHE_TYPE_NONE, CACHE_TYPE_RANKED
+from pilosa_amd.models.fragment import Fragment, TopOptions
+from pilosa_amd.models.row import Row
+
+SW = 1 << 20
+
+
+class _Frags:
+    def __init__(self):
+        self.dirs = []
+        self.frags = []
+
+    def open(self, shard=0, cache_type=CACHE_TYPE_RANKED, cache_size=50000, **kw):
+        """mustOpenFragment (fragment_internal_test.go:1985-2010)."""
+        d = tempfile.mkdtemp(prefix="frag_")
+        self.dirs.append(d)
+        f = Fragment(os.path.join(d, str(shard)), "i", "f", "standard", shard, cache_type=cache_type,
+                     cache_size=cache_size, **kw)
+        f.open()
+        self.frags.append(f)
+        return f
+
+    def reopen(self, f):
+        f.close()
+        g = Fragment(f.path, f.index, f.field, f.view, f.shard, cache_type=f.cache_type, cache_size=f.cache_size,
+                     max_opn=f.max_opn, mutex=f.mutex, bool_field=f.bool_field)
+        g.open()
+        self.frags.append(g)
+        return g
+
+    def close(self):
+        for f in self.frags:
+            try:
+                f.close()
+            except Exception:  # noqa: BLE001 - already closed
+                pass
+        for d in self.dirs:
+            shutil.rmtree(d, ignore_errors=True)
+
+
+@pytest.fixture
+def frags():
+    fs = _Frags()
+    yield fs
+    fs.close()
+
+
+def cols(row):
+    return [int(c) for c in row.columns()]
+
+
+# ---------------------------------------------------------------- bits (:51-220)
+def test_set_bit(frags):
+    f = frags.open()
+    f.set_bit(120, 1)
+    f.set_bit(120, 6)
+    f.set_bit(121, 0)
+    assert f.row(120).count() == 2 and f.row(121).count() == 1
+    f = frags.reopen(f)
+    assert f.row(120).count() == 2 and f.row(121).count() == 1
+
+
+def test_clear_bit(frags):
+    f = frags.open()
+    f.set_bit(1000, 1)
+    f.set_bit(1000, 2)
+    f.clear_bit(1000, 1)
+    assert f.row(1000).count() == 1
+    f = frags.reopen(f)
+    assert f.row(1000).count() == 1
+
+
+def test_rowcache_map(frags):
+    """:109-145 -- a row read before snapshots keeps its bits while the
+    fragment is rewritten underneath it."""
+    f = frags.open()
+    f.max_opn = 200
+    for i in range(f.max_opn):
+        f.set_bit(0, i * 32)
+    f.snapshot()
+    row = f.row(0)
+    for j in range(5):
+        for i in range(f.max_opn):
+            f.set_bit(0, i * 32 + j + 1)
+    assert all(row.includes(i * 32) for i in range(200))
+    assert row.count() == 200
+
+
+def test_clear_row(frags):
+    f = frags.open()
+    f.set_bit(1000, 1)
+    f.set_bit(1000, 65536)
+    f.clear_row(1000)
+    assert f.row(1000).count() == 0
+    f = frags.reopen(f)
+    assert f.row(1000).count() == 0
+
+
+def test_set_row(frags):
+    f = frags.open(shard=7)
+    f.set_bit(1000, 7 * SW + 1)
+    f.set_bit(1000, 7 * SW + 65536)
+    assert cols(f.row(1000)) == [7 * SW + 1, 7 * SW + 65536]
+    assert f.set_row(Row([7 * SW + 1, 7 * SW + 65537, 7 * SW + 140000]), 1000) is True
+    assert cols(f.row(1000)) == [7 * SW + 1, 7 * SW + 65537, 7 * SW + 140000]
+    f = frags.reopen(f)
+    assert f.row(1000).count() == 3
+
+
+# ---------------------------------------------------------------- BSI (:222-900)
+def test_set_value(frags):
+    f = frags.open()
+    assert f.set_value(100, 16, 3829) is True
+    assert f.value(100, 16) == (3829, True)
+    assert f.set_value(100, 16, 3829) is False
+    f = frags.open()
+    assert f.set_value(100, 16, 3829) is True
+    assert f.set_value(100, 16, 2028) is True
+    assert f.value(100, 16) == (2028, True)
+    f = frags.open()
+    f.set_value(100, 16, 3829)
+    assert f.clear_value(100, 16, 2028) is True
+    assert f.value(100, 16) == (0, False)
+    f = frags.open()
+    assert f.set_value(100, 10, 20) is True
+    assert f.value(101, 11) == (0, False)
+    # QuickCheck analogue: random depths / columns / values
+    rng = random.Random(7)
+    for _ in range(20):
+        depth = rng.randint(1, 62)
+        n = rng.randint(1, 99)
+        f = frags.open()
+        m = {}
+        for _ in range(rng.randint(0, 30)):
+            v = rng.getrandbits(depth)
+            m[v % n] = v
+            f.set_value(v % n, depth, v)
+        for c, v in m.items():
+            assert f.value(c, depth) == (v, True)
+
+
+def _bsi(frags, vals):
+    f = frags.open()
+    for c, v in vals:
+        f.set_value(c, 16, v)
+    return f
+
+
+def test_sum(frags):
+    f = _bsi(frags, [(1000, 382), (2000, 300), (3000, 2818), (4000, 300)])
+    assert f.sum(None, 16) == (3800, 4)
+    assert f.sum(Row([2000, 4000, 5000]), 16) == (600, 2)
+    f.clear_value(1000, 16, 23)
+    assert f.sum(None, 16) == (3800 - 382, 3)
+
+
+def test_min_max(frags):
+    f = _bsi(frags, [(1000, 382), (2000, 300), (3000, 2818), (4000, 300), (5000, 2818), (6000, 2817), (7000, 0)])
+    for filt, exp, cnt in ((None, 0, 1), ([2000, 4000, 5000], 300, 2), ([2000, 4000], 300, 2), ([1], 0, 0),
+                           ([1000], 382, 1), ([7000], 0, 1)):
+        assert f.min(Row(filt) if filt is not None else None, 16) == (exp, cnt), filt
+    for filt, exp, cnt in ((None, 2818, 2), ([2000, 4000, 5000], 2818, 1), ([2000, 4000], 300, 2), ([1], 0, 0),
+                           ([1000], 382, 1), ([7000], 0, 1)):
+        assert f.max(Row(filt) if filt is not None else None, 16) == (exp, cnt), filt
+
+
+def test_range(frags):
+    f = _bsi(frags, [(1000, 382), (2000, 300), (3000, 2818), (4000, 300)])
+    assert cols(f.range_op("==", 16, 300)) == [2000, 4000]
+    assert cols(f.range_op("!=", 16, 300)) == [1000, 3000]
+    vals = [(1000, 382), (2000, 300), (3000, 2817), (4000, 301), (5000, 1), (6000, 0)]
+    f = _bsi(frags, vals)
+    assert cols(f.range_op("<", 16, 301)) == [2000, 5000, 6000]
+    assert cols(f.range_op("<", 16, 300)) == [5000, 6000]
+    assert cols(f.range_op("<=", 16, 301)) == [2000, 4000, 5000, 6000]
+    assert cols(f.range_op("<=", 16, 300)) == [2000, 5000, 6000]
+    assert cols(f.range_op(">", 16, 300)) == [1000, 3000, 4000]
+    assert cols(f.range_op(">", 16, 301)) == [1000, 3000]
+    assert cols(f.range_op(">=", 16, 300)) == [1000, 2000, 3000, 4000]
+    assert cols(f.range_op(">=", 16, 301)) == [1000, 3000, 4000]
+    assert cols(f.range_between(16, 300, 2817)) == [1000, 2000, 3000, 4000]
+    assert cols(f.range_between(16, 301, 2817)) == [1000, 3000, 4000]
+    assert cols(f.range_between(16, 301, 2816)) == [1000, 4000]
+    assert cols(f.range_between(16, 300, 2816)) == [1000, 2000, 4000]
+
+
+# ---------------------------------------------------------------- snapshot / iteration (:901-957)
+def test_snapshot(frags):
+    f = frags.open()
+    f.set_bit(1000, 1)
+    f.set_bit(1000, 2)
+    f.clear_bit(1000, 1)
+    f.snapshot()
+    assert f.row(1000).count() == 1
+    f = frags.reopen(f)
+    assert f.row(1000).count() == 1
+
+
+def test_for_each_bit(frags):
+    f = frags.open()
+    f.set_bit(100, 20)
+    f.set_bit(2, 38)
+    f.set_bit(2, 37)
+    assert list(f.for_each_bit()) == [(2, 37), (2, 38), (100, 20)]
+
+
+# ---------------------------------------------------------------- TopN (:959-1196)
+def _set_bits(f, row, *cs):
+    for c in cs:
+        f.set_bit(row, c)
+
+
+def _pairs(ps):
+    return [(p.id, p.count) for p in ps]
+
+
+def _top3(frags, cache_type=CACHE_TYPE_RANKED):
+    f = frags.open(cache_type=cache_type)
+    _set_bits(f, 100, 1, 3, 200)
+    _set_bits(f, 101, 1)
+    _set_bits(f, 102, 1, 2)
+    f.recalculate_cache()
+    return f
+
+
+def test_top(frags):
+    f = _top3(frags)
+    assert _pairs(f.top(TopOptions(n=2))) == [(100, 3), (102, 2)]
+
+
+def test_top_filter(frags):
+    from pilosa_amd.models.attrs import MemAttrStore
+    f = _top3(frags)
+    store = MemAttrStore()
+    store.set_attrs(101, {"x": 10})
+    store.set_attrs(102, {"x": 20})
+    got = f.top(TopOptions(n=2, filter_name="x", filter_values=[10, 15, 20], attr_store=store))
+    assert _pairs(got) == [(102, 2), (101, 1)]
+
+
+def test_topn_intersect(frags):
+    f = frags.open()
+    _set_bits(f, 100, 1, 10, 11, 12)
+    _set_bits(f, 101, 1, 2, 3, 4)
+    _set_bits(f, 102, 1, 2, 4, 5, 6)
+    _set_bits(f, 103, 1000, 1001, 1002)
+    f.recalculate_cache()
+    assert _pairs(f.top(TopOptions(n=3, src=Row([1, 2, 3])))) == [(101, 3), (102, 2), (100, 1)]
+
+
+def test_topn_intersect_large(frags):
+    """:1044-1094 -- rows 0..999, row i has columns 0..i-1, imported as one
+    roaring bitmap."""
+    from pilosa_amd import _roaring
+    f = frags.open()
+    i = np.arange(1000, dtype=np.uint64)
+    rows = np.repeat(i, i.astype(np.int64))
+    colsv = np.concatenate([np.arange(k, dtype=np.uint64) for k in range(1000)])
+    bm = _roaring.Bitmap(np.sort(rows * np.uint64(SW) + colsv))
+    f.import_roaring(bm.to_bytes())
+    f.recalculate_cache()
+    src = Row(list(range(980, 1000)))
+    assert _pairs(f.top(TopOptions(n=10, src=src))) == [(999 - k, 19 - k) for k in range(10)]
+
+
+def test_topn_ids(frags):
+    f = frags.open()
+    _set_bits(f, 100, 1, 2, 3)
+    _set_bits(f, 101, 4, 5, 6, 7)
+    _set_bits(f, 102, 8, 9, 10, 11, 12)
+    assert _pairs(f.top(TopOptions(row_ids=[100, 101, 200]))) == [(101, 4), (100, 3)]
+
+
+def test_topn_nop_cache(frags):
+    f = frags.open(cache_type=CACHE_TYPE_NONE, cache_size=0)
+    _set_bits(f, 100, 1, 2, 3)
+    _set_bits(f, 101, 4, 5, 6, 7)
+    _set_bits(f, 102, 8, 9, 10, 11, 12)
+    assert f.top(TopOptions(row_ids=[100, 101, 200])) == []
+
+
+def test_topn_cache_size(frags):
+    f = frags.open(cache_size=3)
+    _set_bits(f, 100, 1, 2, 3)
+    _set_bits(f, 101, 4, 5, 6, 7)
+    _set_bits(f, 102, 8, 9, 10, 11, 12)
+    _set_bits(f, 103, 8, 9, 10, 11, 12, 13)
+    _set_bits(f, 104, 8, 9, 10, 11, 12, 13, 14)
+    _set_bits(f, 105, 10, 11)
+    f.recalculate_cache()
+    got = _pairs(f.top(TopOptions(n=5)))
+    assert len(got) <= 3 and got == [(104, 7), (103, 6), (102, 5)]
+
+
+# ---------------------------------------------------------------- blocks (:1198-1271)
+def test_checksum(frags):
+    from pilosa_amd.models.fragment import HASH_BLOCK_SIZE
+    f = frags.open()
+    orig = f.checksum()
+    f.set_bit(1, 200)
+    f.set_bit(HASH_BLOCK_SIZE * 2, 200)
+    assert f.checksum() != orig
+
+
+def test_blocks(frags):
+    f = frags.open()
+    f.set_bit(0, 0)
+    prev = f.blocks()
+    assert prev[0][1]
+    f.set_bit(20, 0)
+    blocks = f.blocks()
+    assert blocks[0][1] != prev[0][1]
+    prev = blocks
+    f.set_bit(20, 100)
+    assert f.blocks()[0][1] != prev[0][1]
+
+
+def test_blocks_empty(frags):
+    f = frags.open()
+    f.set_bit(100, 1)
+    blocks = f.blocks()
+    assert len(blocks) == 1 and blocks[0][0] == 1
+
+
+# ---------------------------------------------------------------- cache persistence (:1273-1356)
+def test_lru_cache_persistence(frags):
+    from pilosa_amd.models.cache import LRUCache
+    f = frags.open(cache_type=CACHE_TYPE_LRU)
+    for i in range(1000):
+        f.set_bit(i, 0)
+    assert isinstance(f.cache, LRUCache) and len(f.cache) == 1000
+    f = frags.reopen(f)
+    assert isinstance(f.cache, LRUCache) and len(f.cache) == 1000
+
+
+def test_rank_cache_persistence():
+    """:1305-1356 -- through Index -> Field -> View like the reference."""
+    from pilosa_amd.models.cache import RankCache
+    from tests.helpers import Env
+    env = Env()
+    try:
+        env.create_index("i")
+        env.field("i", "f", type="set", cache_type="ranked", cache_size=50000)
+        f = env.holder.field("i", "f")
+        for i in range(1000):
+            f.set_bit(i, 0)
+        frag = env.holder.fragment("i", "f", "standard", 0)
+        assert isinstance(frag.cache, RankCache) and len(frag.cache) == 1000
+        env.reopen()
+        frag = env.holder.fragment("i", "f", "standard", 0)
+        assert isinstance(frag.cache, RankCache) and len(frag.cache) == 1000
+    finally:
+        env.close()
+
+
+# ---------------------------------------------------------------- tar (:1358-1410)
+def test_write_to_read_from(frags):
+    f0 = frags.open()
+    f0.set_bit(1000, 1)
+    f0.set_bit(1000, 2)
+    f0.clear_bit(1000, 1)
+    assert len(f0.cache) == 1
+    buf = io.BytesIO()
+    f0.write_to(buf)
+    wn = buf.tell()
+    buf.seek(0)
+    f1 = frags.open()
+    f1.read_from(buf)
+    assert buf.tell() == wn
+    assert len(f1.cache) == 1
+    assert cols(f1.row(1000)) == [2]
+    f1 = frags.reopen(f1)
+    assert len(f1.cache) == 1 and cols(f1.row(1000)) == [2]
+
+
+# ---------------------------------------------------------------- Tanimoto (:1463-1509)
+def _tani(frags):
+    f = frags.open()
+    _set_bits(f, 100, 1, 3, 2, 200)
+    _set_bits(f, 101, 1, 3)
+    _set_bits(f, 102, 1, 2, 10, 12)
+    f.recalculate_cache()
+    return f
+
+
+def test_tanimoto(frags):
+    f = _tani(frags)
+    assert _pairs(f.top(TopOptions(tanimoto_threshold=50, src=Row([1, 2, 3])))) == [(100, 3), (101, 2)]
+
+
+def test_zero_tanimoto(frags):
+    f = _tani(frags)
+    assert _pairs(f.top(TopOptions(tanimoto_threshold=0, src=Row([1, 2, 3])))) == [(100, 3), (101, 2), (102, 2)]
+
+
+def test_snapshot_run(frags):
+    f = frags.open()
+    for i in range(1, 3):
+        f.set_bit(1000, i)
+    f.snapshot()
+    assert f.row(1000).count() == 2
+    f = frags.reopen(f)
+    assert f.row(1000).count() == 2
