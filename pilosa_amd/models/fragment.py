@@ -768,6 +768,11 @@ class Fragment:
             out = out[:limit]
         return out
 
+    def row_iterator(self, wrap: bool, row_filter: Optional[Sequence[int]] = None) -> "RowIterator":
+        """Iterator over the non-empty rows (fragment.go rowIterator, the
+        GroupBy building block): next() -> (row, id, wrapped)."""
+        return RowIterator(self, wrap, row_filter)
+
     # ------------------------------------------------------------ TopN
     def top(self, opt: TopOptions) -> List[Pair]:
         pairs = self._top_bitmap_pairs(opt.row_ids)
@@ -1075,6 +1080,32 @@ class Fragment:
 
     def check(self) -> str:
         return self.storage.check()
+
+
+class RowIterator:
+    """fragment.go:2714-2778 rowIterator: rows in id order; a wrapping
+    iterator restarts from the first row (wrapped=True) after the last, a
+    non-wrapping one then returns (None, 0, True)."""
+
+    def __init__(self, frag: "Fragment", wrap: bool, row_filter: Optional[Sequence[int]] = None):
+        self.f = frag
+        self.wrap = wrap
+        self.ids = frag.rows(0, row_filter=row_filter)
+        self.cur = 0
+
+    def seek(self, row_id: int):
+        self.cur = int(np.searchsorted(np.asarray(self.ids, dtype=np.uint64), np.uint64(row_id)))
+
+    def next(self):
+        wrapped = False
+        if self.cur >= len(self.ids):
+            if not self.wrap or not self.ids:
+                return None, 0, True
+            self.cur = 0
+            wrapped = True
+        rid = self.ids[self.cur]
+        self.cur += 1
+        return self.f.row(rid), rid, wrapped
 
 
 def _wrap_i64(v: int) -> int:

@@ -413,3 +413,306 @@ def test_snapshot_run(frags):
     assert f.row(1000).count() == 2
     f = frags.reopen(f)
     assert f.row(1000).count() == 2
+
+
+# ---------------------------------------------------------------- mutex / imports (:1538-2000)
+def test_set_mutex(frags):
+    f = frags.open(mutex=True)
+    f.set_bit(1, 100)
+    assert cols(f.row(1)) == [100]
+    f.set_bit(2, 100)
+    assert cols(f.row(1)) == [] and cols(f.row(2)) == [100]
+
+
+IMPORT_CASES = {
+    # (set rows, set cols, set expectation, clear rows, clear cols, clear expectation) per kind
+    "set": [
+        ([1, 1, 1, 1], [0, 1, 2, 3], {1: [0, 1, 2, 3]}, [], [], {1: [0, 1, 2, 3]}),
+        ([1, 1, 1, 1, 2, 2, 2, 2], [0, 1, 2, 3, 0, 1, 2, 3], {1: [0, 1, 2, 3], 2: [0, 1, 2, 3]},
+         [1, 1, 2], [1, 2, 3], {1: [0, 3], 2: [0, 1, 2]}),
+        ([1, 1, 1, 1, 2], [0, 1, 2, 3, 1], {1: [0, 1, 2, 3], 2: [1]}, [1, 1, 1, 1], [0, 1, 2, 3], {1: [], 2: [1]}),
+        ([1, 1, 1, 1, 2, 2, 1], [0, 1, 2, 3, 1, 8, 1], {1: [0, 1, 2, 3], 2: [1, 8]}, [1, 1], [0, 0],
+         {1: [1, 2, 3], 2: [1, 8]}),
+        ([1, 2, 3], [8, 8, 8], {1: [8], 2: [8], 3: [8]}, [1, 2, 3], [9, 9, 9], {1: [8], 2: [8], 3: [8]}),
+    ],
+    "mutex": [
+        ([1, 1, 1, 1], [0, 1, 2, 3], {1: [0, 1, 2, 3]}, [], [], {1: [0, 1, 2, 3]}),
+        ([1, 1, 1, 1, 2, 2, 2, 2], [0, 1, 2, 3, 0, 1, 2, 3], {1: [], 2: [0, 1, 2, 3]}, [1, 1, 2], [1, 2, 3],
+         {1: [], 2: [0, 1, 2]}),
+        ([1, 1, 1, 1, 2], [0, 1, 2, 3, 1], {1: [0, 2, 3], 2: [1]}, [1, 1, 1, 1], [0, 1, 2, 3], {1: [], 2: [1]}),
+        ([1, 1, 1, 1, 2, 2, 1], [0, 1, 2, 3, 1, 8, 1], {1: [0, 1, 2, 3], 2: [8]}, [1, 1], [0, 0],
+         {1: [1, 2, 3], 2: [8]}),
+        ([1, 2, 3], [8, 8, 8], {1: [], 2: [], 3: [8]}, [1, 2, 3], [9, 9, 9], {1: [], 2: [], 3: [8]}),
+    ],
+    "bool": [
+        ([1, 1, 1, 1], [0, 1, 2, 3], {1: [0, 1, 2, 3]}, [], [], {1: [0, 1, 2, 3]}),
+        ([0, 0, 0, 0, 1, 1, 1, 1], [0, 1, 2, 3, 0, 1, 2, 3], {0: [], 1: [0, 1, 2, 3]}, [1, 1, 2], [1, 2, 3],
+         {0: [], 1: [0, 3], 2: []}),
+        ([0, 0, 0, 0, 1], [0, 1, 2, 3, 1], {0: [0, 2, 3], 1: [1]}, [1, 1, 1, 1], [0, 1, 2, 3],
+         {0: [0, 2, 3], 1: []}),
+        ([1, 1, 1, 1, 0, 0, 1], [0, 1, 2, 3, 1, 8, 1], {0: [8], 1: [0, 1, 2, 3]}, [1, 1], [0, 0],
+         {0: [8], 1: [1, 2, 3]}),
+        ([0, 1, 2], [8, 8, 8], {0: [], 1: [], 2: [8]}, [1, 2, 3], [9, 9, 9], {0: [], 1: [], 2: [8]}),
+    ],
+}
+
+
+@pytest.mark.parametrize("kind", ["set", "mutex", "bool"])
+def test_import(frags, kind):
+    """:1570-1700 (ImportSet), :1703-1819 (ImportMutex), :1821-1940 (ImportBool)."""
+    for i, (sr, sc, sexp, cr, cc, cexp) in enumerate(IMPORT_CASES[kind]):
+        f = frags.open(mutex=kind == "mutex", bool_field=kind == "bool")
+        f.bulk_import(sr, sc)
+        for k, v in sexp.items():
+            assert cols(f.row(k)) == v, (kind, i, "set", k)
+        f.bulk_import(cr, cc, clear=True)
+        for k, v in cexp.items():
+            assert cols(f.row(k)) == v, (kind, i, "clear", k)
+
+
+def test_concurrent_import(frags):
+    """:1687-1700"""
+    import threading
+    f = frags.open()
+    errs = []
+
+    def imp(r, c):
+        try:
+            f.bulk_import(r, c)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=imp, args=([1, 2], [1, 2])), threading.Thread(target=imp, args=([3, 4], [3, 4]))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs
+    assert [cols(f.row(r)) for r in (1, 2, 3, 4)] == [[1], [2], [3], [4]]
+
+
+# ---------------------------------------------------------------- rows / roaring import (:2634-2915)
+def test_rows_iteration(frags):
+    f = frags.open()
+    for i in range(100, 200):
+        f.set_bit(i, i % 2)
+    assert f.rows(0) == list(range(100, 200))
+    assert f.rows(0, column=1) == [i for i in range(100, 200) if i % 2]
+    f = frags.open()
+    f.set_bit(1, 66000)
+    f.set_bit(2, 66000)
+    f.set_bit(2, 166000)
+    assert f.rows(0) == [1, 2] and f.rows(0, column=66000) == [1, 2]
+    f = frags.open()
+    expected = []
+    for r in range(1, 10000, 100):
+        expected.append(r)
+        for c in range(1, SW - 1, 10000 * 7):  # the reference's grid, every 7th column step
+            f.set_bit(r, c)
+            assert f.rows(0, column=c) == expected
+        assert f.rows(0) == expected
+
+
+def _calc_expected(*inputs):
+    rows = {}
+    for inp in inputs:
+        for v in inp:
+            rows.setdefault(v // SW, set()).add(v % SW)
+    return {r: sorted(c) for r, c in rows.items()}
+
+
+def test_roaring_import(frags):
+    from pilosa_amd import _roaring
+    cases = [[[0], [1]],
+             [[0, 65535, 65536, 65537, 65538, 65539, 130000], [1000, 67000, 130000]],
+             [[0, 65535, 65536, 65537, 65538, 65539, 130000], [0, 65535, 65536, 65537, 65538, 65539, 130000]],
+             [[0, 65535, 65536, SW + 1, SW * 2 + 1], [1, SW + 2, SW * 2 + 2]]]
+    for case in cases:
+        f = frags.open()
+        for num, inp in enumerate(case):
+            f.import_roaring(_roaring.Bitmap(np.array(sorted(inp), dtype=np.uint64)).to_bytes())
+            for row, want in _calc_expected(*case[:num + 1]).items():
+                assert cols(f.row(row)) == want
+
+
+def _calc_top(rows, colsv):
+    d = {}
+    for r, c in zip(rows, colsv):
+        d.setdefault(r, set()).add(c)
+    return sorted(((r, len(c)) for r, c in d.items()), key=lambda p: -p[1])
+
+
+def test_roaring_import_topn(frags):
+    from pilosa_amd import _roaring
+    f = frags.open()
+    rows, cs = [4, 4, 4, 4], [0, 1, 2, 3]
+    f.bulk_import(rows, cs)
+    assert _pairs(f.top(TopOptions())) == _calc_top(rows, cs)
+    r2, c2 = [5, 5, 5, 5, 5], [0, 1, 2, 3, 4]
+    f.bulk_import(r2, c2)
+    rows, cs = rows + r2, cs + c2
+    assert _pairs(f.top(TopOptions())) == _calc_top(rows, cs)
+    bits = [0, 65535, 65536, SW + 1, SW + 2, SW * 2 + 1]
+    f.import_roaring(_roaring.Bitmap(np.array(bits, dtype=np.uint64)).to_bytes())
+    assert _pairs(f.top(TopOptions())) == _calc_top(rows + [b // SW for b in bits], cs + [b % SW for b in bits])
+
+
+def test_fragment_row_iterator(frags):
+    """:2915-3031"""
+    for wrap in (False, True):
+        for ids in ([0, 1, 2, 3], [1, 3, 5, 7]):
+            f = frags.open()
+            for r in ids:
+                f.set_bit(r, 0)
+            it = f.row_iterator(wrap)
+            for k in range(len(ids) + (1 if wrap else 0)):
+                row, rid, wrapped = it.next()
+                assert rid == ids[k % len(ids)]
+                assert wrapped == (k >= len(ids))
+                assert cols(row) == [0]
+            if not wrap:
+                row, rid, wrapped = it.next()
+                assert row is None and rid == 0 and wrapped
+
+
+def test_union_in_place_mapped(frags):
+    """:3033-3097 -- a bitmap written into the fragment, then unioned in
+    place with another: the count is between the larger input and the sum."""
+    from pilosa_amd import _roaring
+    rng0, rng1 = np.random.default_rng(2), np.random.default_rng(1)
+    d0 = np.unique(rng0.integers(0, 1 << 28, 1_000_000, dtype=np.uint64))
+    d1 = np.unique(rng1.integers(0, 1 << 28, 1_000_000, dtype=np.uint64))
+    f = frags.open(cache_type=CACHE_TYPE_NONE, cache_size=0)
+    f.import_roaring(_roaring.Bitmap(d0).to_bytes())
+    assert f.storage.count() == len(d0)
+    f.import_roaring(_roaring.Bitmap(d1).to_bytes())
+    n = f.storage.count()
+    assert max(len(d0), len(d1)) <= n <= len(d0) + len(d1)
+    assert n == len(np.union1d(d0, d1))
+    f = frags.reopen(f)
+    assert f.storage.count() == n
+
+
+# ---------------------------------------------------------------- BSI positions / restart (:3099-3433)
+def test_positions_for_value(frags):
+    f = frags.open(cache_type=CACHE_TYPE_NONE, cache_size=0)
+    for col, depth, val, to_set, to_clear in (
+            (0, 1, 0, [0], [SW, SW * 2]),
+            (0, 3, 0, [0], [SW, SW * 2, SW * 3, SW * 4]),
+            (1, 3, 0, [1], [SW + 1, SW * 2 + 1, SW * 3 + 1, SW * 4 + 1]),
+            (0, 1, 1, [0, SW * 2], [SW]),
+            (0, 4, 10, [0, SW * 3, SW * 5], [SW, SW * 2, SW * 4]),
+            (0, 5, 10, [0, SW * 3, SW * 5], [SW, SW * 2, SW * 4, SW * 6])):
+        s, c = f._positions_for_values(np.array([col]), np.array([val]), depth, False)
+        assert sorted(int(x) for x in s) == to_set and sorted(int(x) for x in c) == to_clear, (col, depth, val)
+
+
+@pytest.mark.parametrize("max_opn", [0, 10000])
+def test_import_clear_restart(frags, max_opn):
+    """:3181-3290 -- import, reopen, reopen on a second fragment object,
+    clear import, reopen: the rows are exactly as expected every time, and
+    the op count survives restarts while it fits under max_opn."""
+    cases = [([1], [1]), ([1, 2, 3, 4, 5, 6, 7, 8, 9, 1], [1, 2, 3, 4, 5, 6, 7, 8, 9, 500000]),
+             ([0] * 10, [0, 65535, 65536, 131071, 131072, 196607, 196608, 262143, 262144, 1000000]),
+             ([1, 2, 20, 200, 2000, 200000], [1] * 6)]
+    for rows, cs in cases:
+        exp = {}
+        for r, c in zip(rows, cs):
+            exp.setdefault(r, set()).add(c)
+        exp_opn = sum(len(v) for v in exp.values())
+
+        def check(fr, want):
+            for r, cset in want.items():
+                assert set(cols(fr.row(r))) == cset, (r, max_opn)
+        f = frags.open(max_opn=max_opn)
+        f.bulk_import(rows, cs)
+        if exp_opn <= max_opn:
+            assert f.opn == exp_opn
+        check(f, exp)
+        f = frags.reopen(f)
+        if exp_opn <= max_opn:
+            assert f.opn == exp_opn
+        check(f, exp)
+        f2 = frags.reopen(f)
+        check(f2, exp)
+        f2.bulk_import(rows, cs, clear=True)
+        cleared = {r: set() for r in exp}
+        check(f2, cleared)
+        f3 = frags.reopen(f2)
+        check(f3, cleared)
+
+
+def test_import_value_concurrent(frags):
+    import threading
+    f = frags.open()
+    errs = []
+
+    def work(i):
+        rng = random.Random(i)
+        try:
+            for j in range(10):
+                f.import_value([j], [rng.randrange(1000)], 10, clear=i % 2 == 0)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs
+
+
+@pytest.mark.parametrize("max_opn", [0, 10000])
+def test_import_multiple_values(frags, max_opn):
+    """:3361-3406 -- the last value of a column in one import wins."""
+    f = frags.open(max_opn=max_opn)
+    f.import_value([0, 0], [97, 100], 7)
+    assert f.value(0, 7) == (100, True)
+
+
+def test_fragment_concurrent_read_write(frags):
+    import threading
+    f = frags.open()
+    errs = []
+
+    def writer():
+        try:
+            for i in range(1000):
+                f.set_bit(i % 4, i)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    t = threading.Thread(target=writer)
+    t.start()
+    acc = 0
+    for i in range(100):
+        acc += f.row(i % 4).count()
+    t.join()
+    assert not errs
+    assert sum(f.row(r).count() for r in range(4)) == 1000
+
+
+# ---------------------------------------------------------------- anti-entropy merge (fragment.go:1873-1991)
+def test_merge_block_majority_vote(frags):
+    """mergeBlock: a pair is set when at least (n+1)/2 of the n block copies
+    (local + replicas) have it; each copy's diff brings it to the consensus.
+    (The reference appends a clear to its *sets* slice -- a bug at
+    fragment.go:1969-1970; the cases below never mix sets and clears for
+    one copy, so both agree.)"""
+    f = frags.open()
+    f.set_bit(1, 10)   # local + r1 -> stays
+    f.set_bit(2, 20)   # local only -> cleared locally
+    f.set_bit(150, 5)  # other block: untouched
+    r1 = ([1, 3], [10, 30])          # has (1,10), (3,30)
+    r2 = ([3, 4, 250], [30, 40, 1])  # (3,30) with r1 -> set everywhere; (250, 1) is outside block 0
+    sets, clears = f.merge_block(0, [r1, r2])
+    assert cols(f.row(1)) == [10] and cols(f.row(2)) == [] and cols(f.row(3)) == [30]
+    assert cols(f.row(150)) == [5]
+    assert [list(map(list, s)) for s in sets] == [[[], []], [[1], [10]]]
+    assert [list(map(list, c)) for c in clears] == [[[], []], [[4], [40]]]
+    # even split of 2 copies: set wins
+    f = frags.open()
+    f.set_bit(7, 70)
+    sets, clears = f.merge_block(0, [([], [])])
+    assert cols(f.row(7)) == [70]
+    assert [list(map(list, s)) for s in sets] == [[[7], [70]]]
+    with pytest.raises(Exception):
+        f.merge_block(0, [([1, 2], [1])])
