@@ -17,15 +17,20 @@ from __future__ import annotations
 
 import json
 import os
+import random
 import struct
 import threading
+import time
+import urllib.request
 import uuid
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 from urllib.parse import urlparse
 
 DEFAULT_PARTITION_N = 256
 STATE_STARTING, STATE_DEGRADED, STATE_NORMAL, STATE_RESIZING = "STARTING", "DEGRADED", "NORMAL", "RESIZING"
 NODE_READY, NODE_DOWN = "READY", "DOWN"
+RESIZE_ACTION_ADD, RESIZE_ACTION_REMOVE = "ADD", "REMOVE"
+RESIZE_JOB_RUNNING, RESIZE_JOB_DONE, RESIZE_JOB_ABORTED = "RUNNING", "DONE", "ABORTED"
 
 _FNV64_OFFSET = 0xcbf29ce484222325
 _FNV64_PRIME = 0x100000001b3
@@ -123,12 +128,104 @@ class Node:
         return f"Node({self.id}@{self.uri}, {self.state}{', coord' if self.is_coordinator else ''})"
 
 
+# ---------------------------------------------------------------- Nodes helpers
+# (reference cluster.go Nodes: IDs / Filter / FilterURI / Contains / Clone)
+def node_ids(nodes: Sequence[Node]) -> List[str]:
+    return [n.id for n in nodes]
+
+
+def filter_nodes(nodes: Sequence[Node], drop: Node) -> List[Node]:
+    return [n for n in nodes if n.id != drop.id]
+
+
+def filter_nodes_uri(nodes: Sequence[Node], uri: URI) -> List[Node]:
+    return [n for n in nodes if n.uri != uri]
+
+
+def contains_node(nodes: Sequence[Node], n: Node) -> bool:
+    return any(x.id == n.id for x in nodes)
+
+
+def clone_nodes(nodes: Sequence[Node]) -> List[Node]:
+    return [Node(n.id, URI(n.uri.scheme, n.uri.host, n.uri.port), n.is_coordinator, n.state, n.gpus)
+            for n in nodes]
+
+
+def confirm_node_down(uri: URI, retries: int = 10, sleep: float = 1.0, timeout: float = 2.0,
+                      logger=None) -> bool:
+    """Guard against false leave events: a node is only DOWN when ``/version``
+    fails ``retries`` times in a row (reference confirmNodeDown,
+    cluster.go:1699-1726; 10 tries, 1 s apart, 2 s timeout each)."""
+    url = f"{uri.scheme}://{uri.host_port()}/version"
+    for i in range(retries):
+        try:
+            with urllib.request.urlopen(url, timeout=timeout) as resp:
+                if resp.status == 200:
+                    return False
+        except Exception as e:  # noqa: BLE001 - any failure counts as a miss
+            if logger is not None:
+                logger.printf("NodeLeave confirm with %s %d. err: '%s'", uri.host_port(), i, e)
+        if i + 1 < retries:
+            time.sleep(sleep)
+    return True
+
+
+class ResizeJob:
+    """One coordinator-driven resize (reference resizeJob, cluster.go:1420-1545).
+
+    ``ids`` maps every node that must finish its ResizeInstruction to whether
+    it has reported completion: on ADD the existing nodes plus the new one, on
+    REMOVE every node except the one leaving."""
+
+    def __init__(self, existing: Sequence[Node], node: Node, action: str, job_id: Optional[int] = None):
+        if action == RESIZE_ACTION_REMOVE:
+            self.ids = {n.id: False for n in existing if n.id != node.id}
+        elif action == RESIZE_ACTION_ADD:
+            self.ids = {n.id: False for n in existing}
+            self.ids[node.id] = False
+        else:
+            raise ValueError(f"invalid resize action: {action}")
+        self.id = job_id if job_id is not None else random.getrandbits(63)
+        self.action = action
+        self.node = node
+        self.nodes: List[Node] = []       # membership once the job commits
+        self.state = RESIZE_JOB_RUNNING
+        self.errors: List[str] = []
+        self.done = threading.Event()
+
+    @property
+    def pending(self) -> set:
+        return {k for k, v in self.ids.items() if not v}
+
+    @property
+    def leaving(self) -> Optional[str]:
+        return self.node.id if self.action == RESIZE_ACTION_REMOVE else None
+
+    def mark(self, node_id: str, error: str = "") -> bool:
+        """Record one node's completion; True once every node has reported."""
+        if error:
+            self.errors.append(error)
+        if node_id in self.ids:
+            self.ids[node_id] = True
+        return self.is_complete()
+
+    def is_complete(self) -> bool:
+        return all(self.ids.values())
+
+    def finish(self, state: str):
+        self.state = state
+        self.done.set()
+
+
 class Topology:
     """Persisted node-id list (``.topology``, protobuf Topology)."""
 
     def __init__(self, cluster_id: str = "", node_ids: Optional[List[str]] = None):
         self.cluster_id = cluster_id or str(uuid.uuid4())
         self.node_ids = sorted(node_ids or [])
+
+    def contains_id(self, nid: str) -> bool:
+        return nid in self.node_ids
 
     def save(self, path: str):
         from pilosa_amd.wire import pb
@@ -157,6 +254,9 @@ class Cluster:
         self.state = STATE_STARTING
         self.path = path
         self.topology = Topology.load(os.path.join(path, ".topology")) if path else None
+        # a persisted topology with nodes in it means a restarting cluster that
+        # must regain agreement before it serves (cluster.go:1660-1694)
+        self.topology_loaded = self.topology is not None and bool(self.topology.node_ids)
         if self.topology is None:
             self.topology = Topology(node_ids=[node.id])
         self.mu = threading.RLock()
@@ -164,8 +264,54 @@ class Cluster:
         node.is_coordinator = True
         self.on_state_change = None
 
+    @classmethod
+    def from_nodes(cls, nodes: Sequence[Node], replica_n: int = 1, partition_n: int = DEFAULT_PARTITION_N,
+                   hasher=None, local: Optional[Node] = None) -> "Cluster":
+        """An in-memory cluster over ``nodes`` (no topology file), as a resize
+        plan's from/to side or a test fixture."""
+        nodes = sorted(nodes, key=lambda n: n.id)
+        c = cls(local or nodes[0], replica_n=replica_n, partition_n=partition_n, hasher=hasher)
+        c.nodes = list(nodes)
+        c.topology.node_ids = [n.id for n in nodes]
+        return c
+
     # ------------------------------------------------------------ membership
-    def set_nodes(self, nodes: Sequence[Node], coordinator_id: Optional[str] = None):
+    def node_ids(self) -> List[str]:
+        return [n.id for n in self.nodes]
+
+    def check_coordinator_topology(self):
+        """The coordinator of a restarting cluster must be in its own persisted
+        topology (cluster.go:1686-1689)."""
+        from pilosa_amd.errors import PilosaError
+        if self.topology_loaded and not self.topology.contains_id(self.node.id):
+            raise PilosaError(f"coordinator {self.node.id} is not in topology: "
+                              f"[{' '.join(self.topology.node_ids)}]")
+
+    def need_topology_agreement(self) -> bool:
+        """STARTING/DEGRADED and the live node set differs from the persisted
+        topology (cluster.go:1013)."""
+        return self.state in (STATE_STARTING, STATE_DEGRADED) and self.topology.node_ids != self.node_ids()
+
+    def previous_node(self) -> Optional[Node]:
+        """The node before this one on the ID-sorted ring (cluster.go:1983)."""
+        if len(self.nodes) <= 1:
+            return None
+        for i, n in enumerate(self.nodes):
+            if n.id == self.node.id:
+                return self.nodes[i - 1]
+        return None
+
+    def update_coordinator(self, n: Node) -> bool:
+        """Point the coordinator at ``n``; True if it changed (cluster.go:356)."""
+        with self.mu:
+            changed = self.coordinator_id != n.id
+            self.set_coordinator(n.id)
+            return changed
+
+    def set_nodes(self, nodes: Sequence[Node], coordinator_id: Optional[str] = None, exact: bool = False):
+        """Adopt a membership list. ``exact`` (a coordinator's status push)
+        also drops topology entries the status no longer lists, as
+        mergeClusterStatus removes them (cluster.go:1890-1930)."""
         with self.mu:
             by_id = {n.id: n for n in nodes}
             by_id[self.node.id] = by_id.get(self.node.id, self.node)
@@ -174,7 +320,8 @@ class Cluster:
                 self.coordinator_id = coordinator_id
             for n in self.nodes:
                 n.is_coordinator = n.id == self.coordinator_id
-            self.topology.node_ids = sorted(set(self.topology.node_ids) | {n.id for n in self.nodes})
+            ids = {n.id for n in self.nodes}
+            self.topology.node_ids = sorted(ids if exact else set(self.topology.node_ids) | ids)
             self.save_topology()
 
     def add_node(self, n: Node):
@@ -251,11 +398,12 @@ class Cluster:
         h = fnv64a(index.encode() + struct.pack(">Q", int(shard)))
         return h % self.partition_n
 
-    def partition_nodes(self, pid: int, nodes: Optional[List[Node]] = None) -> List[Node]:
+    def partition_nodes(self, pid: int, nodes: Optional[List[Node]] = None,
+                        replica_n: Optional[int] = None) -> List[Node]:
         nodes = self.nodes if nodes is None else nodes
         if not nodes:
             return []
-        rn = self.replica_n
+        rn = self.replica_n if replica_n is None else replica_n
         if rn > len(nodes):
             rn = len(nodes)
         elif rn == 0:
@@ -273,27 +421,81 @@ class Cluster:
     def contains_shards(self, index: str, shards: Sequence[int], node: Node) -> List[int]:
         return [s for s in shards if any(n.id == node.id for n in self.shard_nodes(index, s))]
 
-    def frag_sources(self, to_nodes: List[Node], holder_schema: Dict[str, Dict[str, List[str]]],
-                     available: Dict[str, List[int]]) -> Dict[str, List[dict]]:
-        """For a resize from self.nodes to ``to_nodes``: per destination node
-        id, the fragments it must fetch and from which current owner
-        (cluster.go:760-844 fragSources)."""
-        out: Dict[str, List[dict]] = {n.id: [] for n in to_nodes}
-        from_nodes = list(self.nodes)
-        for index, fields in holder_schema.items():
-            for shard in available.get(index, []):
-                pid = self.partition(index, shard)
-                old = {n.id for n in self.partition_nodes(pid, from_nodes)}
-                new = self.partition_nodes(pid, sorted(to_nodes, key=lambda n: n.id))
-                src = [n for n in self.partition_nodes(pid, from_nodes) if n.state != NODE_DOWN] or \
-                    self.partition_nodes(pid, from_nodes)
-                for dst in new:
-                    if dst.id in old:
-                        continue
-                    for field, views in fields.items():
-                        for view in views:
-                            out[dst.id].append({"node": src[0].to_json(), "index": index, "field": field,
-                                                "view": view, "shard": shard})
+    # ------------------------------------------------------------ resize planning
+    def frag_combos(self, index: str, shards: Sequence[int], field_views: Dict[str, List[str]],
+                    replica_n: Optional[int] = None) -> Dict[str, List[Tuple[str, str, int]]]:
+        """Per node id, every (field, view, shard) it holds for ``index``
+        (cluster.go:702 fragCombos)."""
+        out: Dict[str, List[Tuple[str, str, int]]] = {}
+        for shard in sorted(shards):
+            for n in self.partition_nodes(self.partition(index, shard), replica_n=replica_n):
+                lst = out.setdefault(n.id, [])
+                for field in sorted(field_views):
+                    for view in field_views[field]:
+                        lst.append((field, view, shard))
+        return out
+
+    def frags_by_host(self, schema: Dict[str, Dict[str, List[str]]], available: Dict[str, Sequence[int]],
+                      replica_n: Optional[int] = None) -> Dict[str, List[Tuple[str, str, str, int]]]:
+        """frag_combos over every index: node id -> [(index, field, view, shard)]."""
+        out: Dict[str, List[Tuple[str, str, str, int]]] = {}
+        for index in sorted(schema):
+            for nid, frags in self.frag_combos(index, available.get(index, []), schema[index],
+                                               replica_n).items():
+                out.setdefault(nid, []).extend((index,) + f for f in frags)
+        return out
+
+    def diff(self, other: "Cluster") -> Tuple[str, str]:
+        """(action, node id) for a one-node membership change (cluster.go:721)."""
+        from pilosa_amd.errors import PilosaError
+        nf, nt = len(self.nodes), len(other.nodes)
+        if nf == nt:
+            raise PilosaError("clusters are the same size")
+        if nf < nt:
+            if nt - nf > 1:
+                raise PilosaError("adding more than one node at a time is not supported")
+            mine = set(self.node_ids())
+            return RESIZE_ACTION_ADD, next(n.id for n in other.nodes if n.id not in mine)
+        if nf - nt > 1:
+            raise PilosaError("removing more than one node at a time is not supported")
+        theirs = set(other.node_ids())
+        return RESIZE_ACTION_REMOVE, next(n.id for n in self.nodes if n.id not in theirs)
+
+    def frag_sources(self, to: Union["Cluster", List[Node]], holder_schema: Dict[str, Dict[str, List[str]]],
+                     available: Dict[str, Sequence[int]]) -> Dict[str, List[dict]]:
+        """For a resize from this membership to ``to``: per destination node
+        id, the fragments it lacks and which current node serves each
+        (cluster.go:760-844 fragSources).
+
+        Adding a node only ever reads primaries (a replica-1 view of the old
+        cluster); removing one reads whichever surviving node holds the
+        fragment, so ReplicaN must be high enough to cover the leaver."""
+        from pilosa_amd.errors import PilosaError
+        if not isinstance(to, Cluster):
+            to = Cluster.from_nodes(to, replica_n=self.replica_n, partition_n=self.partition_n,
+                                    hasher=self.hasher)
+        action, diff_id = self.diff(to)
+        src_rn = 1 if action == RESIZE_ACTION_ADD and self.replica_n > 1 else None
+        have = self.frags_by_host(holder_schema, available)
+        want = to.frags_by_host(holder_schema, available)
+        src_by_frag: Dict[tuple, str] = {}
+        for nid, frags in sorted(self.frags_by_host(holder_schema, available, src_rn).items()):
+            if action == RESIZE_ACTION_REMOVE and nid == diff_id:
+                continue
+            for fr in frags:
+                src_by_frag.setdefault(fr, nid)
+        out: Dict[str, List[dict]] = {n.id: [] for n in to.nodes}
+        for nid, frags in want.items():
+            held = set(have.get(nid, ()))
+            for fr in frags:
+                if fr in held:
+                    continue
+                src = src_by_frag.get(fr)
+                if src is None:
+                    raise PilosaError("not enough data to perform resize (replica factor may need to be increased)")
+                index, field, view, shard = fr
+                out[nid].append({"node": self.node_by_id(src).to_json(), "index": index, "field": field,
+                                 "view": view, "shard": shard})
         return out
 
     def status(self) -> dict:

@@ -22,7 +22,7 @@ from pilosa_amd.errors import (APIMethodNotAllowedError, BadRequestError, Confli
 from pilosa_amd.executor import ExecOptions, QueryResponse
 from pilosa_amd.models.field import FieldOptions
 from pilosa_amd.models.fragment import SHARD_WIDTH
-from pilosa_amd.parallel.cluster import STATE_DEGRADED, STATE_NORMAL, STATE_RESIZING, STATE_STARTING
+from pilosa_amd.parallel.cluster import STATE_DEGRADED, STATE_NORMAL, STATE_RESIZING, STATE_STARTING, URI, Node
 from pilosa_amd.pql import ParseError, parse_string
 from pilosa_amd.utils import tracing
 
@@ -420,13 +420,18 @@ class API:
         return old, n
 
     def remove_node(self, node_id: str):
+        """Start a REMOVE resize (api.go:1225 RemoveNode -> cluster.nodeLeave).
+        A node only in the persisted topology (already gone) can be removed too."""
         self.validate("RemoveNode")
-        if not self.cluster.is_coordinator():
-            raise ErrNodeNotCoordinator
         n = self.cluster.node_by_id(node_id)
         if n is None:
-            raise ErrNodeIDNotExists
-        self.server.resize_remove_node(n)
+            if not self.cluster.topology.contains_id(node_id):
+                raise NotFoundError(f"finding node to remove: {ErrNodeIDNotExists}")
+            n = Node(node_id, URI())
+        try:
+            self.server.node_leave(n)
+        except PilosaError as e:
+            raise PilosaError(f"calling node leave: {e}") from e
         return n
 
     def resize_abort(self):

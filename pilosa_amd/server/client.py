@@ -26,6 +26,7 @@ class ClientError(PilosaError):
     def __init__(self, status, msg):
         super().__init__(f"server error {status}: {msg}")
         self.status = status
+        self.body = msg
 
 
 class InternalClient:

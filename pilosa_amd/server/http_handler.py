@@ -518,10 +518,19 @@ class Handler:
     def post_remove_node(self, req):
         try:
             body = json.loads(req.body)
-            n = self.api.remove_node(body["id"])
-            req.send_json({"remove": n.to_json()})
-        except (PilosaError, KeyError, ValueError) as e:
-            req.send(400, json.dumps({"error": str(e)}), JSON)
+            node_id = body["id"]
+        except (KeyError, ValueError, TypeError) as e:
+            req.send(400, str(e) + "\n", "text/plain; charset=utf-8")
+            return
+        try:
+            n = self.api.remove_node(node_id)
+        except NotFoundError as e:
+            req.send(404, f"removing node: {e}\n", "text/plain; charset=utf-8")
+            return
+        except PilosaError as e:
+            req.send(500, f"removing node: {e}\n", "text/plain; charset=utf-8")
+            return
+        req.send_json({"remove": n.to_json()})
 
     def post_set_coordinator(self, req):
         try:

@@ -29,8 +29,10 @@ import numpy as np
 from pilosa_amd.executor import Executor
 from pilosa_amd.models.field import FieldOptions
 from pilosa_amd.models.holder import Holder
-from pilosa_amd.parallel.cluster import (NODE_DOWN, NODE_READY, STATE_NORMAL, STATE_RESIZING, STATE_STARTING,
-                                         Cluster, JumpHasher, ModHasher, Node, URI)
+from pilosa_amd.errors import PilosaError
+from pilosa_amd.parallel.cluster import (NODE_DOWN, NODE_READY, RESIZE_ACTION_ADD, RESIZE_ACTION_REMOVE,
+                                         RESIZE_JOB_ABORTED, RESIZE_JOB_DONE, STATE_DEGRADED, STATE_NORMAL,
+                                         STATE_RESIZING, STATE_STARTING, Cluster, JumpHasher, ModHasher, Node, ResizeJob, URI)
 from pilosa_amd.server.api import API
 from pilosa_amd.server.client import InternalClient
 from pilosa_amd.server.http_handler import Handler, make_http_server
@@ -107,7 +109,8 @@ class Server:
         self._closing = threading.Event()
         self._threads: List[threading.Thread] = []
         self._misses: Dict[str, int] = {}
-        self._resize: Optional[dict] = None
+        self._resize: Optional[ResizeJob] = None
+        self.join_error: Optional[str] = None
         self.mu = threading.RLock()
 
     # ------------------------------------------------------------ lifecycle
@@ -147,8 +150,14 @@ class Server:
         t = threading.Thread(target=self.httpd.serve_forever, name="http", daemon=True)
         t.start()
         self._threads.append(t)
+        if self.is_coordinator_cfg and not self.cluster_disabled:
+            try:
+                self.cluster.check_coordinator_topology()
+            except PilosaError:
+                self.close()
+                raise
         if self.cluster_disabled or (not self.hosts and self.coordinator_uri is None):
-            self.cluster.set_state(STATE_NORMAL)
+            self.cluster.set_state(STATE_NORMAL if not self.cluster.need_topology_agreement() else STATE_STARTING)
         elif self.is_coordinator_cfg:
             self.cluster.set_coordinator(self.node.id)
             self._start_loop(self._membership_loop, "membership")
@@ -347,22 +356,32 @@ class Server:
 
     # ------------------------------------------------------------ membership
     def _join(self):
-        target = self.coordinator_uri or (self.hosts[0] if self.hosts else None)
-        if target is None:
+        """Announce this node to the cluster through the first seed that
+        answers (the coordinator URI, then the configured hosts); a seed that
+        is not the coordinator forwards the join (gossip seeds, server.go)."""
+        seeds = ([self.coordinator_uri] if self.coordinator_uri else []) + \
+            [h for h in self.hosts if h != self.node.uri and h != self.coordinator_uri]
+        if not seeds:
             self.cluster.set_state(STATE_NORMAL)
             return
         deadline = time.time() + 30
+        msg = {"type": "NodeJoin", "node": self.node.to_json(), "status": self._node_status()}
         while not self._closing.is_set():
-            try:
-                tmp = Node("?", target)
-                self.client.send_message(tmp, {"type": "NodeJoin", "node": self.node.to_json(),
-                                               "status": self._node_status()})
-                return
-            except Exception as e:  # noqa: BLE001
-                if time.time() > deadline:
-                    self.logger.printf("join %s failed: %s", target, e)
+            err = None
+            for target in seeds:
+                try:
+                    self.client.send_message(Node("?", target), msg)
                     return
-                time.sleep(0.2)
+                except Exception as e:  # noqa: BLE001
+                    if "not in topology" in str(e):    # refused by the coordinator: retrying cannot help
+                        self.join_error = getattr(e, "body", str(e))
+                        self.logger.printf("join %s refused: %s", target, e)
+                        return
+                    err = e
+            if time.time() > deadline:
+                self.logger.printf("join %s failed: %s", seeds, err)
+                return
+            time.sleep(0.2)
 
     def _node_status(self) -> dict:
         return {"node": self.node.to_json(), "schema": self.holder.schema(),
@@ -386,6 +405,9 @@ class Server:
                 self.client.send_message(c, {"type": "NodeJoin", "node": n.to_json()})
             return
         with self.mu:
+            if self.cluster.need_topology_agreement() and not self.cluster.topology.contains_id(n.id):
+                # a restarting cluster only admits the nodes of its persisted topology (cluster.go:1775)
+                raise PilosaError(f"host is not in topology: {n.id}")
             known = self.cluster.node_by_id(n.id)
             if known is not None:
                 known.uri = n.uri
@@ -418,7 +440,7 @@ class Server:
         coord = st.get("coordinator") or next((d["id"] for d in st.get("nodes", []) if d.get("isCoordinator")),
                                                None)
         self.cluster.topology.cluster_id = st.get("clusterID", self.cluster.topology.cluster_id)
-        self.cluster.set_nodes(nodes, coord)
+        self.cluster.set_nodes(nodes, coord, exact=True)
         me = self.cluster.node_by_id(self.node.id)
         if me is not None:
             me.state = NODE_READY
@@ -453,29 +475,33 @@ class Server:
         layout = self._holder_layout()
         avail = {n: idx.available_shards() for n, idx in self.holder.indexes.items()}
         sources = self.cluster.frag_sources(new_nodes, layout, avail)
-        job_id = int(time.time() * 1000)
-        self._resize = {"id": job_id, "pending": {n.id for n in new_nodes}, "nodes": new_nodes,
-                        "leaving": leaving.id if leaving else None, "errors": []}
+        action = RESIZE_ACTION_ADD if joining is not None else RESIZE_ACTION_REMOVE
+        job = ResizeJob(self.cluster.nodes, joining if joining is not None else leaving, action,
+                        job_id=int(time.time() * 1000))
+        job.nodes = list(new_nodes)
+        self._resize = job
         self.cluster.set_state(STATE_RESIZING)
         status = self.cluster.status()
         for n in new_nodes:
-            msg = {"type": "ResizeInstruction", "jobID": job_id, "node": n.to_json(),
+            msg = {"type": "ResizeInstruction", "jobID": job.id, "node": n.to_json(),
                    "coordinator": self.node.to_json(), "sources": sources.get(n.id, []),
-                   "schema": self.holder.schema(), "status": status}
+                   "schema": self.holder.schema(), "status": status, "nodeStatus": self._node_status()}
             try:
                 if n.id == self.node.id:
                     threading.Thread(target=self._follow_resize, args=(msg,), daemon=True).start()
                 else:
                     self.client.send_message(n, msg)
             except Exception as e:  # noqa: BLE001
-                self._resize["errors"].append(str(e))
-                self._resize["pending"].discard(n.id)
+                job.mark(n.id, str(e))
 
     def _follow_resize(self, msg: dict):
         err = ""
         try:
             self.cluster.set_state(STATE_RESIZING)
             self.holder.apply_schema(msg.get("schema", []))
+            if msg.get("nodeStatus"):
+                # the coordinator's view of which shards exist cluster-wide
+                self._merge_node_status(msg["nodeStatus"])
             for src in msg.get("sources", []):
                 sn = Node.from_json(src["node"])
                 data = self.client.fragment_data(sn.uri, src["index"], src["field"], src["view"], src["shard"])
@@ -495,24 +521,40 @@ class Server:
     def _resize_complete(self, msg: dict):
         with self.mu:
             job = self._resize
-            if job is None or msg.get("jobID") != job["id"]:
+            if job is None or msg.get("jobID") != job.id:
                 return
-            if msg.get("error"):
-                job["errors"].append(msg["error"])
-            job["pending"].discard(msg["node"]["id"])
-            if job["pending"]:
+            if not job.mark(msg["node"]["id"], msg.get("error") or ""):
                 return
             self._resize = None
-            if job["errors"]:
-                self.logger.printf("resize job %s failed: %s", job["id"], job["errors"][0])
+            if job.errors:
+                self.logger.printf("resize job %s failed: %s", job.id, job.errors[0])
             else:
-                self.cluster.set_nodes(job["nodes"], self.cluster.coordinator_id)
-                if job.get("leaving"):
-                    self.cluster.remove_node(job["leaving"])
+                self.cluster.set_nodes(job.nodes, self.cluster.coordinator_id)
+                if job.leaving:
+                    self.cluster.remove_node(job.leaving)
             self.cluster.state = STATE_NORMAL
             self._publish_status()
             self.clean_holder()
             self.broadcast({"type": "RecalculateCaches"})
+            job.finish(RESIZE_JOB_ABORTED if job.errors else RESIZE_JOB_DONE)
+
+    def node_leave(self, n: Node):
+        """Coordinator-side checks before removing a node (cluster.go:1841-1880)."""
+        c = self.cluster
+        if not c.is_coordinator():
+            co = c.coordinator()
+            raise PilosaError("node removal requests are only valid on the coordinator node: "
+                              f"{co.id if co else c.coordinator_id}")
+        if c.state not in (STATE_NORMAL, STATE_DEGRADED):
+            raise PilosaError(f"cluster must be '{STATE_NORMAL}' to remove a node but is '{c.state}'")
+        if not c.topology.contains_id(n.id) and c.node_by_id(n.id) is None:
+            raise PilosaError(f"Node is not a member of the cluster: {n.id}")
+        if n.id == self.node.id:
+            raise PilosaError("coordinator cannot be removed; first, make a different node the new coordinator")
+        try:
+            self.resize_remove_node(n)
+        except PilosaError as e:
+            raise PilosaError(f"generating job: {e}") from e
 
     def resize_remove_node(self, n: Node):
         remaining = [x for x in self.cluster.nodes if x.id != n.id]
@@ -527,6 +569,7 @@ class Server:
         with self.mu:
             if self._resize is None:
                 return False
+            self._resize.finish(RESIZE_JOB_ABORTED)
             self._resize = None
             self.cluster.state = STATE_NORMAL
             self._publish_status()
@@ -541,6 +584,8 @@ class Server:
                     for shard in list(v.fragments):
                         if not self.cluster.owns_shard(self.node.id, idx.name, shard):
                             v.delete_fragment(shard)
+                            # still available in the cluster: its owner holds it now
+                            f.add_remote_available_shards([shard])
         if self.gpu is not None:
             self.gpu.invalidate()
 
