@@ -83,7 +83,7 @@ def cmd_server(args, stdout, stderr) -> int:
     bind = cfg.get("bind")
     if bind.startswith(":"):
         bind = "0.0.0.0" + bind
-    hosts = cfg.get("cluster.hosts")
+    hosts = list(cfg.get("cluster.hosts")) + [h for h in cfg.get("gossip.seeds") if h not in cfg.get("cluster.hosts")]
     srv = Server(cfg.data_dir(), bind=bind, replica_n=cfg.get("cluster.replicas"), hosts=hosts,
                  coordinator=cfg.get("cluster.coordinator") or not hosts,
                  coordinator_uri=cfg.get("cluster.coordinator-uri") or (hosts[0] if hosts and
@@ -93,6 +93,7 @@ def cmd_server(args, stdout, stderr) -> int:
                  max_writes=cfg.get("max-writes-per-request"),
                  anti_entropy_interval=cfg.duration("anti-entropy.interval"),
                  probe_interval=cfg.duration("gossip.probe-interval"),
+                 gossip_interval=cfg.duration("gossip.push-pull-interval"),
                  long_query_time=cfg.duration("cluster.long-query-time"), stats=cfg.get("metric.service")
                  if cfg.get("metric.service") != "none" else "expvar", logger=logger,
                  cluster_disabled=cfg.get("cluster.disabled"), mesh_block=cfg.get("gpu.shard-block"),

@@ -260,6 +260,9 @@ class Server {
     }
     for (auto& th : workers_) th.join();
     workers_.clear();
+    // a stopped server refuses new connections (workers closed the open ones)
+    if (lfd_ >= 0) ::close(lfd_);
+    lfd_ = -1;
     for (int e : epfds_) ::close(e);
     for (int w : wakefds_) ::close(w);
     epfds_.clear();

@@ -32,6 +32,7 @@ class ClientError(PilosaError):
 class InternalClient:
     def __init__(self, timeout: float = 30.0, skip_verify: bool = False):
         self.timeout = timeout
+        self.local_node: Optional[dict] = None   # sender identity for messages that carry one
         self.skip_verify = skip_verify
         self._local = threading.local()
 
@@ -190,8 +191,11 @@ class InternalClient:
 
     # ------------------------------------------------------------ messages
     def send_message(self, node, msg: dict):
-        self.do(node.uri, "POST", "/internal/cluster/message", json.dumps(msg).encode(),
-                {"Content-Type": "application/json"})
+        """POST one cluster message in the reference's wire format: a type
+        byte + protobuf (http/client.go:1017 SendMessage, wire/messages.py)."""
+        from pilosa_amd.wire import messages
+        self.do(node.uri, "POST", "/internal/cluster/message", messages.encode(msg, self.local_node),
+                {"Content-Type": messages.CONTENT_TYPE, "Accept": "application/json"})
 
     def export_csv(self, uri, index, field, shard) -> str:
         return self.do(uri, "GET", "/export", query={"index": index, "field": field, "shard": shard},

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import re
+import socket
 import threading
 import time
 import traceback
@@ -453,14 +454,23 @@ class Handler:
         req.send(204, "", "text/plain")
 
     def post_cluster_message(self, req):
+        """Type byte + protobuf body (http/handler.go:1474); a JSON body is
+        also taken, for tooling.  Failures are 400s, as in the reference."""
+        from pilosa_amd.wire import messages
+        ctype = (req.headers.get("Content-Type") or "").split(";")[0].strip()
         try:
-            msg = json.loads(req.body)
+            if ctype == messages.CONTENT_TYPE:
+                msg = messages.decode(req.body)
+            elif ctype == "application/json":
+                msg = json.loads(req.body)
+            else:
+                raise HTTPError(415, "Unsupported media type")
         except ValueError as e:
             raise HTTPError(400, str(e))
         try:
             self.api.cluster_message(msg)
-        except PilosaError as e:
-            raise HTTPError(500, str(e))
+        except (PilosaError, KeyError, ValueError) as e:
+            raise HTTPError(400, str(e))
         req.send_json({})
 
     def get_translate_data(self, req):
@@ -649,6 +659,32 @@ def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
         # listen backlog (socketserver's default of 5 drops SYNs under
         # 100+ concurrent clients)
         request_queue_size = 1024
+
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            self._conns = set()
+            self._conns_mu = threading.Lock()
+
+        def process_request(self, request, client_address):
+            with self._conns_mu:
+                self._conns.add(request)
+            super().process_request(request, client_address)
+
+        def shutdown_request(self, request):
+            with self._conns_mu:
+                self._conns.discard(request)
+            super().shutdown_request(request)
+
+        def server_close(self):
+            # a closed node must not keep answering on keep-alive connections
+            super().server_close()
+            with self._conns_mu:
+                conns, self._conns = list(self._conns), set()
+            for c in conns:
+                try:
+                    c.shutdown(socket.SHUT_RDWR)
+                except OSError:
+                    pass
 
     srv = _Srv((host, int(port)), _H)
     srv.daemon_threads = True

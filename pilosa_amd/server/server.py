@@ -58,7 +58,8 @@ class Server:
                  translation_primary_url: str = "", tls_certificate: str = "", tls_key: str = "",
                  tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
                  gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
-                 lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None):
+                 lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None,
+                 gossip_interval: float = 30.0):
         self.data_dir = data_dir
         # native epoll front end (native/httpd.cpp) unless TLS is configured
         if native_http is None:
@@ -80,6 +81,9 @@ class Server:
         self.long_query_time = long_query_time
         self.anti_entropy_interval = anti_entropy_interval
         self.probe_interval = probe_interval
+        self.gossip_interval = gossip_interval
+        self._gossip_i = 0
+        self._gossip_misses: Dict[str, int] = {}
         self.hosts = [URI.parse(h) for h in (hosts or [])]
         self.coordinator_uri = URI.parse(coordinator_uri) if coordinator_uri else None
         self.is_coordinator_cfg = coordinator
@@ -136,6 +140,7 @@ class Server:
         port = self.httpd.server_address[1]
         adv = host if host not in ("", "0.0.0.0") else "127.0.0.1"
         self.node = Node(nid, URI(scheme, adv, port), state=NODE_READY)
+        self.client.local_node = self.node.to_json()
         self.cluster = Cluster(self.node, replica_n=self.replica_n, hasher=self.hasher, path=self.data_dir)
         self.cluster.on_state_change = lambda s: self.logger.debugf("cluster state -> %s", s)
         self._init_gpu()
@@ -164,6 +169,8 @@ class Server:
             self.cluster.set_state(self.cluster.determine_state())
         else:
             self._join()
+        if not self.cluster_disabled and self.gossip_interval > 0:
+            self._start_loop(self._gossip_loop, "gossip")
         if self.replica_n > 1 and self.anti_entropy_interval > 0:
             self._start_loop(self._anti_entropy_loop, "anti-entropy")
         self._start_loop(self._runtime_loop, "runtime")
@@ -326,6 +333,16 @@ class Server:
             f = h.field(msg["index"], msg["field"])
             if f is not None and f.view(msg["view"]) is not None:
                 f.delete_view(msg["view"])
+        elif t == "CreateView":
+            f = h.field(msg["index"], msg["field"])
+            if f is None:
+                raise PilosaError(f"local field not found: {msg['field']}")
+            f.create_view_if_not_exists(msg["view"])
+        elif t == "NodeState":
+            if self.cluster.set_node_state(msg["nodeID"], msg["state"]) and self.cluster.is_coordinator():
+                self._publish_status()
+        elif t == "NodeUpdate":
+            pass    # intentionally not implemented, as in the reference (cluster.go:1762)
         elif t == "CreateShard":
             f = h.field(msg["index"], msg["field"])
             if f is not None:
@@ -467,6 +484,39 @@ class Server:
             if changed or new_state != self.cluster.state:
                 self._publish_status()
 
+    def _gossip_loop(self):
+        """Push-pull of NodeStatus between every pair of nodes (the role of
+        memberlist's LocalState/MergeRemoteState, gossip/gossip.go:295-443):
+        each round this node pushes its schema + available shards to the next
+        peer, and receives every peer's push in turn.  A peer that misses
+        three pushes and then fails confirm_node_down is reported DOWN to the
+        coordinator, so failures are seen by non-coordinators too."""
+        from pilosa_amd.parallel.cluster import confirm_node_down
+        while not self._closing.wait(self.gossip_interval):
+            peers = [n for n in self.cluster.nodes if n.id != self.node.id]
+            if not peers:
+                continue
+            n = peers[self._gossip_i % len(peers)]
+            self._gossip_i += 1
+            try:
+                self.probe_client.send_message(n, {"type": "NodeStatus", "status": self._node_status()})
+                self._gossip_misses[n.id] = 0
+            except Exception as e:  # noqa: BLE001
+                miss = self._gossip_misses[n.id] = self._gossip_misses.get(n.id, 0) + 1
+                if miss < 3 or n.state == NODE_DOWN or self.cluster.is_coordinator():
+                    continue    # the coordinator's own membership loop owns its verdicts
+                if not confirm_node_down(n.uri, retries=2, sleep=min(self.probe_interval, 1.0), timeout=2.0):
+                    continue
+                self.logger.printf("gossip: node %s unreachable (%s)", n.id, e)
+                coord = self.cluster.coordinator()
+                if coord is not None and coord.id not in (n.id, self.node.id):
+                    try:
+                        self.client.send_message(coord, {"type": "NodeState", "nodeID": n.id, "state": NODE_DOWN})
+                    except Exception as e2:  # noqa: BLE001
+                        self.logger.printf("gossip: reporting %s down: %s", n.id, e2)
+                else:
+                    self._node_down(n.id)
+
     # ------------------------------------------------------------ resize
     def _holder_layout(self) -> Dict[str, Dict[str, List[str]]]:
         return {n: {f.name: sorted(f.views) for f in idx.fields.values()} for n, idx in self.holder.indexes.items()}
@@ -572,8 +622,7 @@ class Server:
             self._resize.finish(RESIZE_JOB_ABORTED)
             self._resize = None
             self.cluster.state = STATE_NORMAL
-            self._publish_status()
-            self.broadcast({"type": "ResizeAbort"})
+            self._publish_status()     # followers leave RESIZING through the status push
             return True
 
     def clean_holder(self):

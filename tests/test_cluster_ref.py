@@ -519,3 +519,36 @@ def test_cluster_resize_remove_node_with_replicas():
     finally:
         for s in reversed(servers):
             s.close()
+
+
+# ---------------------------------------------------------------- gossip (NodeStatus push-pull)
+@pytestmark_timeout
+def test_gossip_spreads_schema_and_detects_failure_on_non_coordinator():
+    def mk(nid, coord=None, probe=0.2):
+        s = Server(tempfile.mkdtemp(), bind="127.0.0.1:0", node_id=nid, gpu="off", coordinator=coord is None,
+                   coordinator_uri=None if coord is None else coord.uri.normalize(), probe_interval=probe,
+                   logger=CaptureLogger(), hasher="mod", native_http=False, gossip_interval=0.1)
+        if coord is None:
+            s.hosts = [URI.parse("127.0.0.1:1")]
+        return s.open()
+    # the coordinator's own prober is slowed right down: only gossip can notice the failure in time
+    m0 = mk("node0", probe=3600)
+    m1 = m2 = None
+    try:
+        m0.probe_interval = 0.2
+        m1, m2 = mk("node1", m0), mk("node2", m0)
+        m0.probe_interval = 3600
+        assert _all_normal([m0, m1, m2], 3)
+        # a schema change made on node2 alone (no broadcast) reaches everyone through gossip
+        m2.api.create_index("g", remote=True)
+        assert _wait(lambda: m0.holder.index("g") is not None and m1.holder.index("g") is not None)
+        m2.close()
+        assert _wait(lambda: m0.cluster.node_by_id("node2").state == "DOWN", timeout=30)
+        assert m0.cluster.state == "DEGRADED" or m0.cluster.state == "STARTING"
+    finally:
+        for s in (m2, m1, m0):
+            if s is not None:
+                try:
+                    s.close()
+                except Exception:  # noqa: BLE001 - m2 closed above
+                    pass
