@@ -1406,7 +1406,7 @@ class Executor:
             if idx.keys:
                 out = Row()
                 out.attrs = r.attrs
-                out.keys = [ts.translate_column_to_string(index, int(col)) for col in r.columns()]
+                out.keys = ts.translate_columns_to_strings(index, [int(c) for c in r.columns()])
                 return out
             return r
         if isinstance(r, Pair):
@@ -1449,7 +1449,7 @@ class Executor:
             if f is None:
                 raise ErrFieldNotFound
             if f.keys():
-                return RowIdentifiers(keys=[ts.translate_row_to_string(index, fname, x) for x in r])
+                return RowIdentifiers(keys=ts.translate_rows_to_strings(index, fname, [int(x) for x in r]))
             return RowIdentifiers(rows=r)
         if c.name == "GroupBy" and isinstance(r, list):
             return r

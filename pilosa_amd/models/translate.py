@@ -1,72 +1,122 @@
 """String key <-> uint64 id translation (reference: translate.go).
 
 IDs are assigned in order starting at 1, per index for column keys and per
-(index, field) for row keys (translate.go:496-585, :675).  The store is an
-append-only log replayed on open; replicas are read-only and tail the
-primary's log from an offset (translate.go:423-474 ``replicate``) via
-:meth:`TranslateFile.read_from` / :meth:`apply_log`.
+(index, field) for row keys (translate.go:496-585, :675).  Storage is the
+native store in ``native/translate.cpp``: the reference's on-disk log of
+varint-framed ``LogEntry`` records (translate.go:716-866), memory-mapped,
+with a Robin-Hood key index that points into the mapping (translate.go:
+880-1037), so a Pilosa data directory's ``.keys`` file opens as is and the
+replication stream (``/internal/translate/data``) is byte-compatible.
 
-Log record (little endian): u8 type (1 column, 2 row) | u16 len(index) |
-index | u16 len(field) | field | u64 id | u32 len(key) | key.
+Replicas are read-only and tail the primary's log from an offset
+(translate.go:423-474 ``replicate``) via :meth:`TranslateFile.read_from` /
+:meth:`apply_log`; keys they do not know yet are forwarded to the primary.
+
+Files written by earlier pilosa_amd builds (fixed-width little-endian
+records) are converted to the log format on open.
 """
 from __future__ import annotations
 
 import os
 import struct
 import threading
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Iterator, List, Optional, Sequence, Tuple
 
-from pilosa_amd.errors import ErrTranslateStoreReadOnly, ErrTranslatingKeyNotFound
+from pilosa_amd.errors import ErrTranslateStoreReadOnly
 
 T_COLUMN, T_ROW = 1, 2
 
 
-def _encode(t: int, index: str, field: str, id: int, key: str) -> bytes:
-    ib, fb, kb = index.encode(), field.encode(), key.encode()
-    return (struct.pack("<BH", t, len(ib)) + ib + struct.pack("<H", len(fb)) + fb +
-            struct.pack("<QI", id, len(kb)) + kb)
+def _native():
+    try:
+        from pilosa_amd import _translate
+    except ImportError as e:  # pragma: no cover - build() makes it
+        raise ImportError("pilosa_amd._translate is not built; run __graft_entry__.build()") from e
+    return _translate
 
 
-def _decode_all(data: bytes, off: int = 0):
-    n = len(data)
-    while off < n:
-        if off + 3 > n:
-            break
+# ---------------------------------------------------------------- LogEntry codec
+def _uvarint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def encode_entry(t: int, index: str, field: str, ids: Sequence[int], keys: Sequence[str]) -> bytes:
+    """One LogEntry exactly as LogEntry.WriteTo (translate.go:795-850)."""
+    ib, fb = index.encode(), (field.encode() if t == T_ROW else b"")
+    body = bytearray([t]) + _uvarint(len(ib)) + ib + _uvarint(len(fb)) + fb + _uvarint(len(ids))
+    for i, k in zip(ids, keys):
+        kb = k.encode() if isinstance(k, str) else bytes(k)
+        body += _uvarint(int(i)) + _uvarint(len(kb)) + kb
+    return _uvarint(len(body)) + bytes(body)
+
+
+# ---------------------------------------------------------------- legacy format
+def _legacy_records(data: bytes) -> Iterator[Tuple[int, str, str, int, str]]:
+    off, n = 0, len(data)
+    while off + 3 <= n:
         t, il = struct.unpack_from("<BH", data, off)
         p = off + 3
-        if p + il + 2 > n:
-            break
+        if t not in (T_COLUMN, T_ROW) or p + il + 2 > n:
+            return
         index = data[p:p + il].decode()
         p += il
         (fl,) = struct.unpack_from("<H", data, p)
         p += 2
         if p + fl + 12 > n:
-            break
+            return
         field = data[p:p + fl].decode()
         p += fl
-        id, kl = struct.unpack_from("<QI", data, p)
+        id_, kl = struct.unpack_from("<QI", data, p)
         p += 12
         if p + kl > n:
-            break
-        key = data[p:p + kl].decode()
-        p += kl
-        yield p, t, index, field, id, key
-        off = p
+            return
+        yield t, index, field, id_, data[p:p + kl].decode()
+        off = p + kl
+
+
+def _migrate_legacy(path: str) -> bool:
+    """Rewrite a pre-log-format file in place; True if one was converted.
+
+    The log format can never start with byte 1 or 2 (the smallest entry is 4
+    bytes long), the legacy format always does."""
+    if not os.path.exists(path) or os.path.getsize(path) == 0:
+        return False
+    with open(path, "rb") as fh:
+        data = fh.read()
+    if data[0] not in (T_COLUMN, T_ROW):
+        return False
+    out, run = bytearray(), None
+    for t, index, field, id_, key in _legacy_records(data):
+        k = (t, index, field)
+        if run is None or run[0] != k:
+            if run is not None:
+                out += encode_entry(*run[0], run[1], run[2])
+            run = (k, [], [])
+        run[1].append(id_)
+        run[2].append(key)
+    if run is not None:
+        out += encode_entry(*run[0], run[1], run[2])
+    tmp = path + ".migrate"
+    with open(tmp, "wb") as fh:
+        fh.write(out)
+        fh.flush()
+        os.fsync(fh.fileno())
+    os.replace(tmp, path)
+    return True
 
 
 class TranslateFile:
-    def __init__(self, path: Optional[str] = None, read_only: bool = False):
+    def __init__(self, path: Optional[str] = None, read_only: bool = False, map_size: int = 0):
         self.path = path
-        self.read_only = read_only
+        self._read_only = read_only
+        self.map_size = map_size
         self.mu = threading.RLock()
-        self._cols: Dict[str, Dict[str, int]] = {}
-        self._col_ids: Dict[str, Dict[int, str]] = {}
-        self._rows: Dict[Tuple[str, str], Dict[str, int]] = {}
-        self._row_ids: Dict[Tuple[str, str], Dict[int, str]] = {}
-        self._log: List[bytes] = []  # in-memory copy when no path
-        self._fh = None
-        self.size = 0
-        self._next: Dict[Tuple[str, str], int] = {}  # (index, field or "") -> next id
+        self._s = None
         # read-only replicas: (index, field or None, keys) -> ids resolved by
         # the primary (http translate proxy, reference http/translator.go)
         self.forward = None
@@ -75,144 +125,84 @@ class TranslateFile:
         with self.mu:
             if self.path:
                 os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-                if os.path.exists(self.path):
-                    with open(self.path, "rb") as fh:
-                        data = fh.read()
-                    end = self.apply_log(data, persist=False)
-                    if end != len(data):  # truncate a torn tail
-                        with open(self.path, "r+b") as fh:
-                            fh.truncate(end)
-                self._fh = open(self.path, "ab", buffering=0)
+                _migrate_legacy(self.path)
+            self._s = _native().Store(self.path or "", self._read_only, int(self.map_size))
+            self._s.open()
         return self
 
     def close(self):
         with self.mu:
-            if self._fh is not None:
-                self._fh.close()
-                self._fh = None
+            if self._s is not None:
+                self._s.close()
+                self._s = None
 
-    # ------------------------------------------------------------ internals
-    def _apply(self, t, index, field, id, key):
-        if t == T_COLUMN:
-            self._cols.setdefault(index, {})[key] = id
-            self._col_ids.setdefault(index, {})[id] = key
-            nk = (index, "")
-        else:
-            self._rows.setdefault((index, field), {})[key] = id
-            self._row_ids.setdefault((index, field), {})[id] = key
-            nk = (index, field)
-        if id >= self._next.get(nk, 1):
-            self._next[nk] = id + 1
+    def reopen(self):
+        self.close()
+        return self.open()
 
-    def _append(self, rec: bytes):
-        if self._fh is not None:
-            self._fh.write(rec)
-        else:
-            self._log.append(rec)
-        self.size += len(rec)
+    @property
+    def read_only(self) -> bool:
+        return self._read_only
 
+    @read_only.setter
+    def read_only(self, v: bool):
+        self._read_only = bool(v)
+        if self._s is not None:
+            self._s.read_only = self._read_only
+
+    @property
+    def size(self) -> int:
+        return self._s.size() if self._s is not None else 0
+
+    # ------------------------------------------------------------ replication
     def apply_log(self, data: bytes, persist: bool = True) -> int:
-        """Apply log records (replica tailing); returns bytes consumed."""
-        end = 0
-        with self.mu:
-            start = 0
-            for p, t, index, field, id, key in _decode_all(data):
-                self._apply(t, index, field, id, key)
-                if persist:
-                    self._append(data[start:p])
-                else:
-                    self.size += p - start
-                start = p
-                end = p
-        return end
+        """Append + index whole log entries (replica tailing); returns the
+        bytes consumed (a torn trailing entry is left for the next read)."""
+        return self._s.apply_log(bytes(data))
 
     def read_from(self, offset: int) -> bytes:
         """Log bytes from ``offset`` (served at /internal/translate/data)."""
-        with self.mu:
-            if self.path:
-                if self._fh is not None:
-                    self._fh.flush()
-                with open(self.path, "rb") as fh:
-                    fh.seek(offset)
-                    return fh.read()
-            return b"".join(self._log)[offset:]
+        return self._s.read_from(int(offset))
 
-    def _next_id(self, index: str, field: str = "") -> int:
-        return self._next.get((index, field), 1)
+    def entries(self, offset: int = 0) -> List[tuple]:
+        """[(type, index, field, ids, keys, encoded_length)] from ``offset``."""
+        return self._s.entries(int(offset))
 
-    def _forward(self, index: str, field: Optional[str], keys: List[str]) -> List[int]:
-        if self.forward is None:
-            raise ErrTranslateStoreReadOnly
-        ids = self.forward(index, field, keys)
-        with self.mu:
-            for k, i in zip(keys, ids):  # visible now; the replicated log entry follows
-                self._apply(T_ROW if field else T_COLUMN, index, field or "", int(i), k)
-        return [int(i) for i in ids]
+    # ------------------------------------------------------------ generic
+    def _translate(self, t: int, index: str, field: str, keys: Sequence[str]) -> List[int]:
+        keys = [k if isinstance(k, str) else str(k) for k in keys]
+        ids = self._s.translate(t, index, field, keys, not self._read_only)
+        if self._read_only and 0 in ids:
+            if self.forward is None:
+                raise ErrTranslateStoreReadOnly
+            missing = sorted({k for k, i in zip(keys, ids) if i == 0})
+            got = dict(zip(missing, (int(x) for x in self.forward(index, field if t == T_ROW else None, missing))))
+            ids = [i or got[k] for k, i in zip(keys, ids)]
+        return list(ids)
 
     # ------------------------------------------------------------ columns
     def translate_columns_to_uint64(self, index: str, keys: Sequence[str]) -> List[int]:
-        out = []
-        keys = list(keys)
-        if self.read_only:
-            with self.mu:
-                cm = self._cols.get(index, {})
-                missing = [k for k in keys if k not in cm]
-            if missing:
-                self._forward(index, None, sorted(set(missing)))
-        with self.mu:
-            cm = self._cols.setdefault(index, {})
-            for k in keys:
-                id = cm.get(k)
-                if id is None:
-                    if self.read_only:
-                        raise ErrTranslateStoreReadOnly
-                    id = self._next_id(index)
-                    self._apply(T_COLUMN, index, "", id, k)
-                    self._append(_encode(T_COLUMN, index, "", id, k))
-                out.append(id)
-        return out
+        return self._translate(T_COLUMN, index, "", keys)
 
     def translate_column_to_string(self, index: str, id: int) -> str:
-        with self.mu:
-            k = self._col_ids.get(index, {}).get(int(id))
-        if k is None:
-            raise ErrTranslatingKeyNotFound
-        return k
+        """The key for ``id``; "" if none (TranslateColumnToString)."""
+        return self._s.keys_of(T_COLUMN, index, "", [int(id)])[0]
+
+    def translate_columns_to_strings(self, index: str, ids: Sequence[int]) -> List[str]:
+        return self._s.keys_of(T_COLUMN, index, "", [int(i) for i in ids])
 
     def column_key_id(self, index: str, key: str) -> Optional[int]:
-        with self.mu:
-            return self._cols.get(index, {}).get(key)
+        return self._s.translate(T_COLUMN, index, "", [key], False)[0] or None
 
     # ------------------------------------------------------------ rows
     def translate_rows_to_uint64(self, index: str, field: str, keys: Sequence[str]) -> List[int]:
-        out = []
-        keys = list(keys)
-        if self.read_only:
-            with self.mu:
-                rm = self._rows.get((index, field), {})
-                missing = [k for k in keys if k not in rm]
-            if missing:
-                self._forward(index, field, sorted(set(missing)))
-        with self.mu:
-            rm = self._rows.setdefault((index, field), {})
-            for k in keys:
-                id = rm.get(k)
-                if id is None:
-                    if self.read_only:
-                        raise ErrTranslateStoreReadOnly
-                    id = self._next_id(index, field)
-                    self._apply(T_ROW, index, field, id, k)
-                    self._append(_encode(T_ROW, index, field, id, k))
-                out.append(id)
-        return out
+        return self._translate(T_ROW, index, field, keys)
 
     def translate_row_to_string(self, index: str, field: str, id: int) -> str:
-        with self.mu:
-            k = self._row_ids.get((index, field), {}).get(int(id))
-        if k is None:
-            raise ErrTranslatingKeyNotFound
-        return k
+        return self._s.keys_of(T_ROW, index, field, [int(id)])[0]
+
+    def translate_rows_to_strings(self, index: str, field: str, ids: Sequence[int]) -> List[str]:
+        return self._s.keys_of(T_ROW, index, field, [int(i) for i in ids])
 
     def row_key_id(self, index: str, field: str, key: str) -> Optional[int]:
-        with self.mu:
-            return self._rows.get((index, field), {}).get(key)
+        return self._s.translate(T_ROW, index, field, [key], False)[0] or None

@@ -86,6 +86,24 @@ def build_httpd(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_translate(force: bool = False, verbose: bool = False) -> str:
+    """Key translation store (translate.cpp), pybind11 module ``_translate``."""
+    import pybind11
+
+    out = os.path.join(PKG, "_translate" + _ext_suffix())
+    srcs = [os.path.join(HERE, "translate.cpp")]
+    if not force and not _newer(out, srcs):
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-std=c++17", "-O2", "-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
+           "-I", sysconfig.get_paths()["include"], *srcs, "-o", out + ".tmp", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def hip_sources():
     return [os.path.join(KDIR, f) for f in sorted(os.listdir(KDIR))
             if f.endswith((".hip", ".cpp", ".h", ".hpp"))]
@@ -144,6 +162,7 @@ def build_all(force: bool = False, verbose: bool = False):
     r = build_roaring(force, verbose)
     build_pql(force, verbose)
     build_httpd(force, verbose)
+    build_translate(force, verbose)
     h = build_hip(force, verbose) if os.path.exists(os.path.join(KDIR, "binding.cpp")) else None
     return r, h
 
