@@ -716,3 +716,42 @@ def test_merge_block_majority_vote(frags):
     assert [list(map(list, s)) for s in sets] == [[[7], [70]]]
     with pytest.raises(Exception):
         f.merge_block(0, [([1, 2], [1])])
+
+
+# ---------------------------------------------------------------- snapshot concurrency
+def test_snapshot_does_not_stall_writers_and_keeps_their_ops(frags, monkeypatch):
+    """The snapshot's write + fsync run outside the fragment lock; writes
+    landing meanwhile go to the old op log and are carried onto the new file."""
+    import threading
+    import pilosa_amd.models.fragment as fm
+    f = frags.open()
+    for c in range(100):
+        f.set_bit(1, c)
+    entered, release = threading.Event(), threading.Event()
+    real_fsync = os.fsync
+
+    def slow_fsync(fd):
+        if not entered.is_set():
+            entered.set()
+            assert release.wait(10)
+        real_fsync(fd)
+    monkeypatch.setattr(fm.os, "fsync", slow_fsync)
+    t = threading.Thread(target=f.snapshot)
+    t.start()
+    assert entered.wait(10)
+    done = threading.Event()
+
+    def writer():   # must not block on the in-flight snapshot
+        for c in range(100, 150):
+            f.set_bit(2, c)
+        f.clear_bit(1, 0)
+        done.set()
+    w = threading.Thread(target=writer)
+    w.start()
+    assert done.wait(5), "writer stalled behind the snapshot"
+    release.set()
+    t.join(10)
+    w.join(5)
+    assert f.opn >= 0
+    g = frags.reopen(f)
+    assert cols(g.row(1)) == list(range(1, 100)) and cols(g.row(2)) == list(range(100, 150))
