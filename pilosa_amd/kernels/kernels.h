@@ -141,4 +141,16 @@ void launch_shift_dense(const uint64_t* src, int S, int64_t n, uint64_t* main_ou
 // shards [s0, s0 + ns) (j >= 0: only rows whose key-j container holds col16).
 void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_t* flags, hipStream_t st);
 
+// Device write path (write_kernels.hip).  merge: one workgroup per touched
+// container u -> scratch[u][1024] u64 bitmap + card[u]; mode 0 applies sorted
+// u16 lows dlows[dstart[u], dstart[u+1]), mode 1 the delta container dmeta[u]
+// (arena metadata into dpayload, -1 none); old_meta[u] = -1 for a new
+// container.  emit: final container u at u16 offset off16[u]*8 of payload
+// (array <= 4096 values, else bitmap) and its metadata word (-1 if empty).
+void launch_container_merge(const int64_t* old_meta, const uint16_t* payload, int64_t U, const int32_t* dstart,
+                            const uint16_t* dlows, const int64_t* dmeta, const uint16_t* dpayload, int mode,
+                            bool clear, uint64_t* scratch, int32_t* card, hipStream_t st);
+void launch_container_emit(const uint64_t* scratch, const int32_t* card, const int64_t* off16, const int32_t* jkey,
+                           int64_t U, uint16_t* payload, int64_t* meta_out, hipStream_t st);
+
 }  // namespace pk

@@ -391,7 +391,12 @@ class Fragment:
         return self.storage.contains(self._pos(row_id, col))
 
     DIRTY_LIMIT = 4096
+    DELTA_LIMIT = 1 << 24     # recorded positions per subscriber before falling back to container keys
 
+    # A dirty subscription is [rows, container keys, deltas, recorded positions]:
+    # rows / keys changed in ways only the fragment storage can describe, and
+    # the ordered write batches ("pos", sorted positions, clear) / ("roaring",
+    # Bitmap, clear) that the device can replay itself (DeviceView.apply_deltas).
     def _note_rows(self, rows):
         for k, d in self._dirty_subs.items():
             if d is not None:
@@ -408,32 +413,51 @@ class Fragment:
                 if len(d[0]) + len(d[1]) > self.DIRTY_LIMIT:
                     self._dirty_subs[k] = None
 
+    def _note_delta(self, kind: str, data, clear: bool, n: int):
+        for k, d in self._dirty_subs.items():
+            if d is None:
+                continue
+            d[2].append((kind, data, clear))
+            d[3] += n
+            if d[3] > self.DELTA_LIMIT or len(d[2]) > self.DIRTY_LIMIT:
+                # too much to replay: degrade to the containers the batches touched
+                if any(kd != "pos" for kd, _, _ in d[2]):
+                    self._dirty_subs[k] = None
+                    continue
+                for _, dd, _ in d[2]:
+                    d[1].update(np.unique(dd >> np.uint64(16)).tolist())
+                d[2].clear()
+                d[3] = 0
+                if len(d[0]) + len(d[1]) > self.DIRTY_LIMIT:
+                    self._dirty_subs[k] = None
+
     def _note_unknown(self):
         for k in self._dirty_subs:
             self._dirty_subs[k] = None
 
     def take_dirty(self, token):
-        """(rows, container keys) changed since ``token`` last asked; container
-        keys are row*16 + local key.  None = unknown -> refresh everything;
-        the first call registers the token and returns None."""
+        """(rows, container keys, deltas) changed since ``token`` last asked;
+        container keys are row*16 + local key, deltas the ordered write
+        batches.  None = unknown -> refresh everything; the first call
+        registers the token and returns None."""
         with self.mu:
             if token not in self._dirty_subs:
-                self._dirty_subs[token] = (set(), set())
+                self._dirty_subs[token] = [set(), set(), [], 0]
                 return None
             d = self._dirty_subs[token]
-            self._dirty_subs[token] = (set(), set())
-            return d
+            self._dirty_subs[token] = [set(), set(), [], 0]
+            return None if d is None else (d[0], d[1], d[2])
 
     def drop_dirty(self, token):
         with self.mu:
             self._dirty_subs.pop(token, None)
 
-    def _after_row_change(self, row_id: int, bulk: bool = False, pos: Optional[int] = None):
+    def _after_row_change(self, row_id: int, bulk: bool = False, pos: Optional[int] = None, clear: bool = False):
         if self._dirty_subs:
             if pos is None:
                 self._note_rows((row_id,))
             else:
-                self._note_container(pos)
+                self._note_delta("pos", np.array([pos], np.uint64), clear, 1)
         self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
         if self.cache_type != CACHE_TYPE_NONE:
             n = self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
@@ -444,12 +468,12 @@ class Fragment:
         if row_id > self.max_row_id:
             self.max_row_id = row_id
 
-    def _after_rows_change(self, rows: np.ndarray):
+    def _after_rows_change(self, rows: np.ndarray, note: bool = True):
         """Vectorised :meth:`_after_row_change` for bulk imports: one native
         call counts every touched row (fragment.go bulkImport cache refresh)."""
         if not len(rows):
             return
-        if self._dirty_subs:
+        if self._dirty_subs and note:
             self._note_rows(rows.tolist())
         for b in np.unique(rows // np.uint64(HASH_BLOCK_SIZE)).tolist():
             self.checksums.pop(int(b), None)
@@ -480,7 +504,7 @@ class Fragment:
         if not changed:
             return False
         self._log(OP_REMOVE, p)
-        self._after_row_change(row_id, pos=p)
+        self._after_row_change(row_id, pos=p, clear=True)
         self._increment_opn(1)
         if self.stats:
             self.stats.count("clearBit", 1)
@@ -899,15 +923,19 @@ class Fragment:
             n = self.storage.add_many(set_pos, True)
             if n:
                 self._log(OP_ADD_BATCH, values=set_pos)
+                if self._dirty_subs:
+                    self._note_delta("pos", set_pos, False, len(set_pos))
             changed += n
         if len(clear_pos):
             clear_pos = np.unique(np.asarray(clear_pos, dtype=np.uint64))
             n = self.storage.remove_many(clear_pos)
             if n:
                 self._log(OP_REMOVE_BATCH, values=clear_pos)
+                if self._dirty_subs:
+                    self._note_delta("pos", clear_pos, True, len(clear_pos))
             changed += n
         rows = row_set if isinstance(row_set, np.ndarray) else np.fromiter((int(r) for r in row_set), dtype=np.uint64)
-        self._after_rows_change(rows.astype(np.uint64, copy=False))
+        self._after_rows_change(rows.astype(np.uint64, copy=False), note=False)
         if self.cache_type != CACHE_TYPE_NONE:
             self.cache.recalculate()
         self._increment_opn(changed)
@@ -971,7 +999,9 @@ class Fragment:
     def import_roaring(self, data: bytes, clear: bool = False) -> int:
         with self.mu:
             changed, rowdelta = self.storage.import_roaring(data, clear, CONTAINERS_PER_ROW)
-            self._note_rows(int(r) for r, d in rowdelta.items() if d)
+            if changed and self._dirty_subs:
+                # the device merges the imported containers itself (K12)
+                self._note_delta("roaring", Bitmap.from_bytes(data), clear, int(changed))
             if changed:
                 self._log(OP_REMOVE_ROARING if clear else OP_ADD_ROARING, roaring=data, opn=changed)
             any_changed = False

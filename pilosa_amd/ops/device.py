@@ -387,6 +387,182 @@ class DeviceView:
         self.generation += 1
         return True
 
+    # ------------------------------------------------------------ device write path (K11/K12)
+    def _seg_keys(self, si: int):
+        """(segment base, shard metadata segment, sorted dense*16+j key of each)."""
+        base = int(self._sb_host[si])
+        rp = self._rowptr_host[si]
+        seg = self._meta_host[base:base + int(rp[-1])]
+        keys = np.repeat(np.arange(self.D, dtype=np.int64), np.diff(rp).astype(np.int64)) * 16 + (seg & 15)
+        return base, seg, keys
+
+    def apply_positions(self, si: int, positions, clear: bool = False) -> bool:
+        """Set (or clear) shard-local positions row*2^20 + col of local shard
+        ``si`` directly in the arena: container_merge / container_emit on the
+        GPU (kernels/write_kernels.hip), only the positions go over PCIe.
+        False -> the caller must refresh the shard another way."""
+        if self._cap is None or self.device.type != "cuda":
+            return False
+        p = np.unique(np.asarray(positions, dtype=np.uint64))
+        if not len(p):
+            return True
+        rows_p = p >> np.uint64(20)
+        urows = np.unique(rows_p)
+        dense_r = self.dense_many(urows)
+        if (dense_r < 0).any():
+            if clear:   # rows this view has no containers for: nothing to clear there
+                p = p[np.isin(rows_p, urows[dense_r >= 0])]
+                if not len(p):
+                    return True
+            elif not self.add_rows(urows[dense_r < 0]):
+                return False
+        ck = (p >> np.uint64(16)).astype(np.int64)
+        uk, start = np.unique(ck, return_index=True)
+        dense = self.dense_many((uk >> 4).astype(np.uint64))
+        dstart = np.append(start, len(p)).astype(np.int32)
+        return self._device_merge(si, dense, (uk & 15).astype(np.int32), 0, clear, dstart=dstart,
+                                  dlows=(p & np.uint64(0xFFFF)).astype(np.uint16))
+
+    def apply_bitmap(self, si: int, bitmap, clear: bool = False) -> bool:
+        """ImportRoaringBits on the device: OR (AND-NOT) every container of
+        ``bitmap`` (shard-local positions) into the arena, container against
+        container (mode 1 of container_merge)."""
+        from pilosa_amd import _roaring
+
+        if self._cap is None or self.device.type != "cuda":
+            return False
+        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], 16, 1)
+        n = int(sb_s[-1])
+        if not n:
+            return True
+        counts = np.diff(rp_s[0].astype(np.int64))
+        drow = np.repeat(rows_s.astype(np.uint64), counts)
+        dmeta = meta_s[:n].astype(np.int64)
+        dense = self.dense_many(drow)
+        if (dense < 0).any():
+            if clear:
+                keep = dense >= 0
+                drow, dmeta, dense = drow[keep], dmeta[keep], dense[keep]
+                if not len(drow):
+                    return True
+            else:
+                if not self.add_rows(np.unique(drow[dense < 0])):
+                    return False
+                dense = self.dense_many(drow)
+        return self._device_merge(si, dense, (dmeta & 15).astype(np.int32), 1, clear, dmeta=dmeta,
+                                  dpayload=pay_s)
+
+    def apply_deltas(self, si: int, deltas) -> bool:
+        """Replay a fragment's recorded writes in order: runs of position
+        batches with the same set/clear flag are merged into one launch."""
+        i = 0
+        while i < len(deltas):
+            kind, data, clear = deltas[i]
+            if kind == "roaring":
+                if not self.apply_bitmap(si, data, clear):
+                    return False
+                i += 1
+                continue
+            j = i + 1
+            while j < len(deltas) and deltas[j][0] == "pos" and deltas[j][2] == clear:
+                j += 1
+            pos = data if j == i + 1 else np.concatenate([d[1] for d in deltas[i:j]])
+            if not self.apply_positions(si, pos, clear):
+                return False
+            i = j
+        return True
+
+    WRITE_CHUNK = 16384   # containers per merge launch (128 MiB of bitmap scratch)
+
+    def _device_merge(self, si: int, dense: np.ndarray, j: np.ndarray, mode: int, clear: bool, dstart=None,
+                      dlows=None, dmeta=None, dpayload=None) -> bool:
+        import torch
+
+        K = kernels()
+        dev = self.device
+        base, seg, segkeys = self._seg_keys(si)
+        qk = dense.astype(np.int64) * 16 + j
+        U = len(qk)
+        if len(segkeys):
+            idx = np.minimum(np.searchsorted(segkeys, qk), len(segkeys) - 1)
+            found = segkeys[idx] == qk
+            old = np.where(found, seg[idx], -1).astype(np.int64)
+        else:
+            idx = np.zeros(U, np.int64)
+            found = np.zeros(U, bool)
+            old = np.full(U, -1, np.int64)
+        t_old = torch.from_numpy(old).to(dev)
+        t_j = torch.from_numpy(np.ascontiguousarray(j, dtype=np.int32)).to(dev)
+        empty16 = torch.empty(0, dtype=torch.int16, device=dev)
+        empty64 = torch.empty(0, dtype=torch.int64, device=dev)
+        empty32 = torch.empty(1, dtype=torch.int32, device=dev)
+        if mode == 0:
+            t_lows = torch.from_numpy(dlows.view(np.int16)).to(dev)
+        else:
+            t_dmeta = torch.from_numpy(np.ascontiguousarray(dmeta, dtype=np.int64)).to(dev)
+            t_dpay = torch.from_numpy(np.ascontiguousarray(dpayload).view(np.int16)).to(dev)
+        new_meta = np.empty(U, np.int64)
+        used = self.payload_used
+        for c0 in range(0, U, self.WRITE_CHUNK):
+            c1 = min(U, c0 + self.WRITE_CHUNK)
+            n = c1 - c0
+            scratch = torch.empty(n * 1024, dtype=torch.int64, device=dev)
+            card = torch.empty(n, dtype=torch.int32, device=dev)
+            if mode == 0:
+                a, b = int(dstart[c0]), int(dstart[c1])
+                ds = torch.from_numpy((dstart[c0:c1 + 1] - a).astype(np.int32)).to(dev)
+                K.container_merge(t_old[c0:c1], self.t_payload, ds, t_lows[a:b], empty64, empty16, 0, clear, scratch,
+                                  card)
+            else:
+                K.container_merge(t_old[c0:c1], self.t_payload, empty32, empty16, t_dmeta[c0:c1], t_dpay, 1, clear,
+                                  scratch, card)
+            c64 = card.to(torch.int64)
+            sizes = torch.where(c64 == 0, torch.zeros_like(c64),
+                                torch.where(c64 > 4096, torch.full_like(c64, 4096), (c64 + 7) // 8 * 8))
+            ends = torch.cumsum(sizes, 0)
+            tot = int(ends[-1])
+            if used + tot > int(self.t_payload.numel()):
+                return False
+            off16 = (ends - sizes + used) // 8
+            meta_out = torch.empty(n, dtype=torch.int64, device=dev)
+            K.container_emit(scratch, card, off16, t_j[c0:c1], self.t_payload, meta_out)
+            new_meta[c0:c1] = meta_out.cpu().numpy()
+            used += tot
+        # splice the new metadata words into the shard's segment
+        keep = new_meta >= 0
+        old_n = (old >> 6) & 0x1FFFF
+        old_t = (old >> 4) & 3
+        self.garbage_u16 += int(np.where(found, np.where(old_t == 2, 4096, (old_n + 7) // 8 * 8), 0).sum())
+        if not (found & ~keep).any() and not (~found & keep).any():
+            at = base + idx[found]
+            self._meta_host[at] = new_meta[found]
+            if len(at):
+                self.t_meta.index_copy_(0, torch.from_numpy(at).to(dev), torch.from_numpy(new_meta[found]).to(dev))
+        else:
+            kept = np.ones(len(seg), bool)
+            kept[idx[found & ~keep]] = False          # containers that became empty
+            ins = keep & ~found
+            repl = keep & found
+            seg2 = seg.copy()
+            seg2[idx[repl]] = new_meta[repl]
+            keys = np.concatenate([segkeys[kept], qk[ins]])
+            vals = np.concatenate([seg2[kept], new_meta[ins]])
+            order = np.argsort(keys, kind="stable")
+            keys, vals = keys[order], vals[order]
+            if len(vals) > int(self._cap[si]):
+                return False
+            rp_new = np.zeros(self.D + 1, np.int64)
+            rp_new[1:] = np.cumsum(np.bincount(keys >> 4, minlength=self.D)[:self.D])
+            full = np.zeros(int(self._cap[si]), np.int64)
+            full[:len(vals)] = vals
+            self.t_meta[base:base + len(full)].copy_(torch.from_numpy(full).to(dev))
+            self.t_rowptr.view(self.S, self.D + 1)[si].copy_(torch.from_numpy(rp_new.astype(np.int32)).to(dev))
+            self._meta_host[base:base + len(full)] = full
+            self._rowptr_host[si] = rp_new
+        self.payload_used = used
+        self.generation += 1
+        return True
+
     def needs_compaction(self) -> bool:
         """Dead payload from in-place updates exceeds half the buffer."""
         return self._cap is not None and self.garbage_u16 > int(self.t_payload.numel()) // 2

@@ -53,6 +53,15 @@ class _Empty:
 EMPTY = _Empty()
 
 
+def _delta_keys(deltas) -> set:
+    """Container keys (row*16 + key) touched by recorded write batches."""
+    out = set()
+    for kind, data, _ in deltas:
+        pos = data if kind == "pos" else data.slice()
+        out.update(np.unique(np.asarray(pos, dtype=np.uint64) >> np.uint64(16)).tolist())
+    return out
+
+
 class GpuExecutor:
     def __init__(self, holder, device="cuda:0", executor=None, hbm_budget: int = 0):
         self.holder = holder
@@ -71,6 +80,7 @@ class GpuExecutor:
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
+        self.device_writes = 0   # ... of which write batches were merged on the GPU (K11/K12)
         # cold views load from their fragment files (no host bitmaps)
         self.file_loader = os.environ.get("PILOSA_FILE_LOADER", "1") != "0"
         self.cold_loads = 0
@@ -117,8 +127,18 @@ class GpuExecutor:
                     with f.mu:
                         dirty = f.take_dirty(dv.token) if old is not None and old[0] == id(f) else None
                         if dirty is not None:
-                            ok = dv.update_rows(si, dirty[0], f.storage, keys=dirty[1])
-                            self.row_updates += ok
+                            rows, keys, deltas = dirty
+                            ok = True
+                            if deltas:
+                                # writes replayed on the device (K11/K12), only the batches cross PCIe;
+                                # otherwise the containers they touched are rebuilt from the host
+                                if dv.apply_deltas(si, deltas):
+                                    self.device_writes += 1
+                                else:
+                                    keys = set(keys) | _delta_keys(deltas)
+                            if ok and (rows or keys):
+                                ok = dv.update_rows(si, rows, f.storage, keys=keys)
+                                self.row_updates += ok
                         else:
                             ok = False
                         if not ok:
@@ -212,7 +232,7 @@ class GpuExecutor:
                 types[name] += int((t == code).sum())
         return {"arenas": len(views), "arenaBytes": self.hbm_bytes(), "containers": types,
                 "launches": self.launches, "rebuilds": self.rebuilds, "shardUpdates": self.shard_updates,
-                "rowUpdates": self.row_updates, "evictions": self.evictions, "hbmBudget": self.hbm_budget}
+                "rowUpdates": self.row_updates, "deviceWrites": self.device_writes, "evictions": self.evictions, "hbmBudget": self.hbm_budget}
 
     def invalidate(self):
         with self.mu:

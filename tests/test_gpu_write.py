@@ -1,0 +1,129 @@
+"""Device write path (K11 AddN/RemoveN, K12 ImportRoaringBits on the GPU,
+kernels/write_kernels.hip): after set / clear / roaring-import batches are
+merged into the HBM arena by container_merge + container_emit, the arena
+decodes to exactly the host roaring result (C++ CPU oracle)."""
+import numpy as np
+import pytest
+
+from pilosa_amd import _roaring as R
+from tests.helpers import SW, Env
+from tests.test_arena_patch import _decode
+from tests.test_gpu_kernels import _random_fragment
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def view():
+    import torch
+    from pilosa_amd.ops.device import DeviceView
+    rng = np.random.default_rng(11)
+    # shard 1 holds every container flavour, shards 0 and 2 must stay untouched
+    frags = [_random_fragment(rng, nrows=6, shard=0) for _ in range(3)]
+    dv = DeviceView.from_bitmaps(frags, torch.device("cuda:0"), shards=[0, 1, 2], patchable=True)
+    return dv, frags, rng
+
+
+def _check(dv, host):
+    for si, h in enumerate(host):
+        assert _decode(dv, si) == h.slice().astype(np.int64).tolist(), f"shard {si}"
+
+
+def test_set_positions_every_container_kind(view):
+    dv, host, rng = view
+    pos = np.concatenate([
+        rng.integers(0, 6 * SW, 20000),                       # into existing rows
+        np.uint64(3) * np.uint64(SW) + np.arange(5000, dtype=np.uint64),   # array -> bitmap conversions
+        np.uint64(9) * np.uint64(SW) + rng.integers(0, SW, 300),            # a brand-new row
+        np.uint64(7) * np.uint64(SW) + np.arange(65536, dtype=np.uint64),   # a full container
+    ]).astype(np.uint64)
+    assert dv.apply_positions(1, pos, clear=False)
+    host[1].add_many(np.unique(pos), True)
+    assert 9 in dv.rows.tolist()
+    _check(dv, host)
+
+
+def test_clear_positions_removes_emptied_containers(view):
+    dv, host, rng = view
+    everything = host[1].slice()
+    key0 = everything[(everything >> np.uint64(16)) == (everything[0] >> np.uint64(16))]
+    pos = np.concatenate([key0, rng.choice(everything, 5000, replace=False),
+                          np.uint64(11) * np.uint64(SW) + np.arange(10, dtype=np.uint64)])  # absent row: no-op
+    n_before = int(dv._rowptr_host[1][-1])
+    assert dv.apply_positions(1, pos, clear=True)
+    host[1].remove_many(np.unique(pos))
+    assert int(dv._rowptr_host[1][-1]) < n_before
+    _check(dv, host)
+
+
+def test_point_writes_and_mixed_batches(view):
+    dv, host, rng = view
+    for k in range(40):
+        p = np.array([int(rng.integers(0, 8 * SW))], np.uint64)
+        clear = bool(k % 3 == 0)
+        assert dv.apply_deltas(1, [("pos", p, clear)])
+        (host[1].remove_many if clear else host[1].add_many)(*((p,) if clear else (p, True)))
+    deltas = [("pos", rng.integers(0, 6 * SW, 500).astype(np.uint64), False),
+              ("pos", rng.integers(0, 6 * SW, 500).astype(np.uint64), False),
+              ("pos", rng.integers(0, 6 * SW, 800).astype(np.uint64), True)]
+    assert dv.apply_deltas(1, deltas)
+    for kind, p, clear in deltas:
+        if clear:
+            host[1].remove_many(np.unique(p))
+        else:
+            host[1].add_many(np.unique(p), True)
+    _check(dv, host)
+
+
+def test_import_roaring_containers(view):
+    dv, host, rng = view
+    src = _random_fragment(rng, nrows=8, shard=0)      # arrays, bitmaps and runs
+    assert dv.apply_bitmap(1, src, clear=False)
+    host[1] = R.Bitmap(np.union1d(host[1].slice(), src.slice()))
+    _check(dv, host)
+    cut = _random_fragment(rng, nrows=5, shard=0)
+    assert dv.apply_bitmap(1, cut, clear=True)
+    host[1] = R.Bitmap(np.setdiff1d(host[1].slice(), cut.slice()))
+    _check(dv, host)
+
+
+def test_executor_writes_merge_on_device():
+    """Set/Clear queries, bulk imports and roaring imports against a GPU-
+    resident view are replayed by the write kernels (no rebuild, no host
+    container rebuild) and every shard still decodes to its fragment."""
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    shards = [0, 1, 2, 3]
+    env = Env(gpu=lambda h: GpuExecutor(h, "cuda:0"))
+    try:
+        env.create_index("i")
+        env.field("i", "g")
+        f = env.holder.index("i").field("g")
+        rng = np.random.default_rng(3)
+        for r in range(6):
+            c = rng.choice(4 * SW, 40000, replace=False).astype(np.uint64)
+            f.import_bits(np.full(len(c), r, np.uint64), c)
+        g = env.executor.gpu
+        g.view_arena("i", "g", "standard", shards)
+        for k in range(60):
+            c, r = int(rng.integers(0, 4 * SW)), int(rng.integers(0, 8))
+            env.q("i", f"Set({c}, g={r})" if k % 3 else f"Clear({c}, g={r})")
+            if k % 9 == 0:
+                f.import_bits(np.full(3000, r, np.uint64), rng.integers(0, 4 * SW, 3000).astype(np.uint64))
+            if k % 20 == 19:
+                frag = env.holder.fragment("i", "g", "standard", 2)
+                rb = R.Bitmap(np.uint64(r) * np.uint64(SW) + rng.integers(0, SW, 5000).astype(np.uint64))
+                frag.import_roaring(rb.to_bytes(), clear=bool(k % 40 == 39))
+            dv = g.view_arena("i", "g", "standard", shards)
+        assert g.rebuilds == 1 and g.device_writes > 50
+        for si, s in enumerate(shards):
+            frag = env.holder.fragment("i", "g", "standard", s)
+            assert _decode(dv, si) == frag.storage.slice().astype(np.int64).tolist()
+        # and queries through the device agree with the host
+        before = g.launches
+        for r in range(8):
+            got = env.q("i", f"Count(Row(g={r}))")[0]
+            want = sum(env.holder.fragment("i", "g", "standard", s).row_count(r) for s in shards)
+            assert got == want
+        assert g.launches > before and g.rebuilds == 1
+    finally:
+        env.close()
