@@ -449,6 +449,19 @@ void container_emit(torch::Tensor scratch, torch::Tensor card, torch::Tensor off
   check_launch("container_emit");
 }
 
+void payload_compact(torch::Tensor meta, torch::Tensor new_off16, torch::Tensor size16, torch::Tensor src,
+                     torch::Tensor dst) {
+  const int64_t C = meta.numel();
+  TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == torch::kInt64 && meta.is_contiguous(), "meta int64[C]");
+  TORCH_CHECK(new_off16.scalar_type() == torch::kInt64 && new_off16.numel() == C, "new_off16 int64[C]");
+  TORCH_CHECK(size16.scalar_type() == torch::kInt64 && size16.numel() == C, "size16 int64[C]");
+  TORCH_CHECK(src.scalar_type() == torch::kInt16 && dst.scalar_type() == torch::kInt16, "payload int16");
+  pk::launch_payload_compact(meta.data_ptr<int64_t>(), C, new_off16.data_ptr<int64_t>(), size16.data_ptr<int64_t>(),
+                             reinterpret_cast<const uint16_t*>(src.data_ptr()),
+                             reinterpret_cast<uint16_t*>(dst.data_ptr()), cur_stream(meta));
+  check_launch("payload_compact");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -476,6 +489,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("shift_dense", &shift_dense, "Shift a dense view by n columns per shard (main + next-shard spill)");
   m.def("rows_list", &rows_list, "flag dense rows with non-empty containers (optionally holding one column)");
   m.def("container_merge", &container_merge, "device write path: old container + delta -> bitmap + cardinality");
+  m.def("payload_compact", &payload_compact, "copy live containers into a compacted payload buffer");
   m.def("container_emit", &container_emit, "device write path: bitmap -> final array/bitmap container + metadata");
   m.def("densify", &densify, "dense bit rows of an arena over a shard range");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program", py::arg("progs"),

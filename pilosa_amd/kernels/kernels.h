@@ -150,6 +150,10 @@ void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_
 void launch_container_merge(const int64_t* old_meta, const uint16_t* payload, int64_t U, const int32_t* dstart,
                             const uint16_t* dlows, const int64_t* dmeta, const uint16_t* dpayload, int mode,
                             bool clear, uint64_t* scratch, int32_t* card, hipStream_t st);
+// Copy every live container (meta type != 0) of size size16[c] 16-byte units
+// from src to new_off16[c] of dst (payload compaction).
+void launch_payload_compact(const int64_t* meta, int64_t C, const int64_t* new_off16, const int64_t* size16,
+                            const uint16_t* src, uint16_t* dst, hipStream_t st);
 void launch_container_emit(const uint64_t* scratch, const int32_t* card, const int64_t* off16, const int32_t* jkey,
                            int64_t U, uint16_t* payload, int64_t* meta_out, hipStream_t st);
 

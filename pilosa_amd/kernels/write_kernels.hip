@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace pk {
@@ -171,7 +173,35 @@ __global__ __launch_bounds__(WG) void container_emit_kernel(const uint64_t* __re
   if (tid == 0) meta_out[u] = int64_t(jkey[u]) | (int64_t(CT_ARRAY) << 4) | (int64_t(n) << 6) | (o16 << 23);
 }
 
+// Payload compaction: container c (metadata word meta[c], type 0 = unused
+// slot) is copied from its old payload offset to new_off16[c]*8 of dst; one
+// wave per container, grid-stride, 16-byte loads and stores.
+__global__ __launch_bounds__(WG) void payload_compact_kernel(const int64_t* __restrict__ meta, int64_t C,
+                                                             const int64_t* __restrict__ new_off16,
+                                                             const int64_t* __restrict__ size16,
+                                                             const uint16_t* __restrict__ src,
+                                                             uint16_t* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = int64_t(gridDim.x) * (WG / 64);
+  for (int64_t c = int64_t(blockIdx.x) * (WG / 64) + (threadIdx.x >> 6); c < C; c += waves) {
+    const int64_t m = meta[c];
+    const int64_t n16 = size16[c];
+    if (meta_type(m) == 0 || n16 == 0) continue;
+    const uint4* sp = reinterpret_cast<const uint4*>(src + meta_off16(m) * 8);
+    uint4* dp = reinterpret_cast<uint4*>(dst + new_off16[c] * 8);
+    for (int64_t i = lane; i < n16; i += 64) dp[i] = sp[i];
+  }
+}
+
 }  // namespace
+
+void launch_payload_compact(const int64_t* meta, int64_t C, const int64_t* new_off16, const int64_t* size16,
+                            const uint16_t* src, uint16_t* dst, hipStream_t st) {
+  if (C <= 0) return;
+  const int64_t blocks = std::min<int64_t>((C + 3) / 4, 256 * 64);   // 64 waves per CU worth of work in flight
+  hipLaunchKernelGGL(payload_compact_kernel, dim3(unsigned(blocks)), dim3(WG), 0, st, meta, C, new_off16, size16,
+                     src, dst);
+}
 
 void launch_container_merge(const int64_t* old_meta, const uint16_t* payload, int64_t U, const int32_t* dstart,
                             const uint16_t* dlows, const int64_t* dmeta, const uint16_t* dpayload, int mode,

@@ -286,7 +286,7 @@ class DeviceView:
         rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([part], 16, 1)
         n_part = int(sb_s[-1])
         npay = int(pay_s.shape[0]) if n_part else 0
-        if self.payload_used + npay > int(self.t_payload.numel()):
+        if self.payload_used + npay > int(self.t_payload.numel()) and not self.grow_payload(npay):
             return False
         new_meta = np.zeros(n_part, np.int64)
         if n_part:
@@ -321,7 +321,9 @@ class DeviceView:
         pieces.append(seg_old[rp_old[cur]:rp_old[-1]])
         seg = np.concatenate(pieces)
         if len(seg) > int(self._cap[si]):
-            return False
+            if not self.grow_segment(si, len(seg)):
+                return False
+            base = int(self._sb_host[si])
         rp_new = np.zeros(self.D + 1, np.int64)
         rp_new[1:] = np.cumsum(counts)
         full = np.zeros(int(self._cap[si]), np.int64)
@@ -352,7 +354,7 @@ class DeviceView:
             return False
         rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], 16, 1)
         n_new = int(sb_s[-1])
-        if n_new > int(self._cap[si]):
+        if n_new > int(self._cap[si]) and not self.grow_segment(si, n_new):
             return False
         dense = self.dense_many(rows_s) if len(rows_s) else np.zeros(0, np.int64)
         if len(dense) and (dense < 0).any():
@@ -360,7 +362,7 @@ class DeviceView:
                 return False
             dense = self.dense_many(rows_s)
         npay = int(pay_s.shape[0]) if n_new else 0
-        if self.payload_used + npay > int(self.t_payload.numel()):
+        if self.payload_used + npay > int(self.t_payload.numel()) and not self.grow_payload(npay):
             return False
         # rowptr over the view's full row directory
         counts = np.zeros(self.D, np.int64)
@@ -385,6 +387,104 @@ class DeviceView:
         self.payload_used += npay
         self.garbage_u16 += npay  # approximate: the shard's previous payload is now unreachable
         self.generation += 1
+        return True
+
+    # ------------------------------------------------------------ growth
+    def grow_segment(self, si: int, need: int) -> bool:
+        """Re-lay the metadata array so shard ``si`` has room for ``need``
+        containers: each shard's used part is copied device-to-device into
+        the new layout (the payload is untouched), so an overflowing shard
+        costs one pass over the metadata instead of a rebuild from the host."""
+        import torch
+
+        if self._cap is None:
+            return False
+        cap = self._cap.copy()
+        cap[si] = need + max(16, need // 8)
+        nsb = np.zeros(self.S + 1, np.int64)
+        nsb[1:] = np.cumsum(cap)
+        t_new = torch.zeros(max(int(nsb[-1]), 1), dtype=torch.int64, device=self.device)
+        h_new = np.zeros(max(int(nsb[-1]), 1), np.int64)
+        for s in range(self.S):
+            n = int(self._rowptr_host[s][-1])
+            if n:
+                a, b = int(self._sb_host[s]), int(nsb[s])
+                t_new[b:b + n].copy_(self.t_meta[a:a + n])
+                h_new[b:b + n] = self._meta_host[a:a + n]
+        self.t_meta, self._meta_host, self._cap = t_new, h_new, cap
+        self._sb_host = nsb
+        self.t_shard_base = torch.from_numpy(nsb.copy()).to(self.device)
+        self.container_count = int(nsb[-1])
+        self.generation += 1
+        return True
+
+    def grow_payload(self, need_u16: int) -> bool:
+        """Room for ``need_u16`` more payload values (a larger buffer, the
+        used prefix copied device-to-device)."""
+        import torch
+
+        if self._cap is None:
+            return False
+        want = self.payload_used + need_u16
+        if want <= int(self.t_payload.numel()):
+            return True
+        size = want + max(8 << 20, want // 4)
+        try:
+            t_new = torch.empty(size, dtype=self.t_payload.dtype, device=self.device)
+        except RuntimeError:   # out of device memory: the caller rebuilds
+            return False
+        t_new[:self.payload_used].copy_(self.t_payload[:self.payload_used])
+        self.t_payload = t_new
+        self.generation += 1
+        return True
+
+    def compact(self) -> bool:
+        """Drop the payload left behind by in-place updates on the device:
+        live containers are copied into a fresh, packed buffer
+        (payload_compact_kernel) and their metadata re-pointed -- instead of
+        rebuilding the view from the host fragments."""
+        import torch
+
+        if self._cap is None or self.device.type != "cuda":
+            return False
+        K = kernels()
+        dev = self.device
+        m = self.t_meta
+        C = int(m.numel())
+        sb = torch.from_numpy(np.asarray(self._sb_host, np.int64)).to(dev)
+        used = torch.from_numpy(np.array([int(r[-1]) for r in self._rowptr_host], np.int64)).to(dev)
+        pos = torch.arange(C, device=dev)
+        seg = torch.clamp(torch.bucketize(pos, sb[1:], right=True), max=self.S - 1)
+        live = (pos - sb[seg]) < used[seg]
+        del pos, seg
+        t = (m >> 4) & 3
+        n = (m >> 6) & 0x1FFFF
+        off16 = m >> 23
+        size16 = torch.where(t == 1, (n + 7) // 8, torch.where(t == 2, torch.full_like(n, 512), torch.zeros_like(n)))
+        runs = torch.nonzero(live & (t == 3)).flatten()
+        if runs.numel():
+            nr = self.t_payload[off16[runs] * 8].to(torch.int64) & 0xFFFF
+            size16[runs] = (8 + 2 * nr + 7) // 8
+        live &= t != 0
+        size16 = torch.where(live, size16, torch.zeros_like(size16))
+        ends = torch.cumsum(size16, 0)
+        total16 = int(ends[-1]) if C else 0
+        new_off16 = ends - size16
+        del ends
+        cap_u16 = total16 * 8 + max(8 << 20, total16 * 2)
+        try:
+            dst = torch.empty(cap_u16, dtype=self.t_payload.dtype, device=dev)
+        except RuntimeError:
+            return False
+        K.payload_compact(m, new_off16, size16, self.t_payload, dst)
+        new_meta = torch.where(live, (m & ((1 << 23) - 1)) | (new_off16 << 23), torch.zeros_like(m))
+        self.t_meta = new_meta
+        self._meta_host = new_meta.cpu().numpy()
+        self.t_payload = dst
+        self.payload_used = total16 * 8
+        self.garbage_u16 = 0
+        self.generation += 1
+        self.compactions = getattr(self, "compactions", 0) + 1
         return True
 
     # ------------------------------------------------------------ device write path (K11/K12)
@@ -522,7 +622,11 @@ class DeviceView:
             ends = torch.cumsum(sizes, 0)
             tot = int(ends[-1])
             if used + tot > int(self.t_payload.numel()):
-                return False
+                self.payload_used, prev = used, self.payload_used
+                grown = self.grow_payload(tot)
+                self.payload_used = prev
+                if not grown:
+                    return False
             off16 = (ends - sizes + used) // 8
             meta_out = torch.empty(n, dtype=torch.int64, device=dev)
             K.container_emit(scratch, card, off16, t_j[c0:c1], self.t_payload, meta_out)
@@ -550,7 +654,9 @@ class DeviceView:
             order = np.argsort(keys, kind="stable")
             keys, vals = keys[order], vals[order]
             if len(vals) > int(self._cap[si]):
-                return False
+                if not self.grow_segment(si, len(vals)):
+                    return False
+                base = int(self._sb_host[si])
             rp_new = np.zeros(self.D + 1, np.int64)
             rp_new[1:] = np.cumsum(np.bincount(keys >> 4, minlength=self.D)[:self.D])
             full = np.zeros(int(self._cap[si]), np.int64)

@@ -81,6 +81,7 @@ class GpuExecutor:
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
         self.device_writes = 0   # ... of which write batches were merged on the GPU (K11/K12)
+        self.device_writes_on = os.environ.get("PILOSA_DEVICE_WRITES", "1") != "0"
         # cold views load from their fragment files (no host bitmaps)
         self.file_loader = os.environ.get("PILOSA_FILE_LOADER", "1") != "0"
         self.cold_loads = 0
@@ -114,6 +115,8 @@ class GpuExecutor:
                 self._arenas.move_to_end(key)
             if hit is not None and hit[0] == sig:
                 return hit[1]
+            if hit is not None and len(hit[0]) == len(sig) and hit[1].needs_compaction():
+                hit[1].compact()   # on the device; a view that cannot be compacted is rebuilt below
             if hit is not None and len(hit[0]) == len(sig) and not hit[1].needs_compaction():
                 # only some shards changed: rewrite their segments in place
                 dv = hit[1]
@@ -132,7 +135,7 @@ class GpuExecutor:
                             if deltas:
                                 # writes replayed on the device (K11/K12), only the batches cross PCIe;
                                 # otherwise the containers they touched are rebuilt from the host
-                                if dv.apply_deltas(si, deltas):
+                                if self.device_writes_on and dv.apply_deltas(si, deltas):
                                     self.device_writes += 1
                                 else:
                                     keys = set(keys) | _delta_keys(deltas)

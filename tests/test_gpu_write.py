@@ -103,6 +103,7 @@ def test_executor_writes_merge_on_device():
             c = rng.choice(4 * SW, 40000, replace=False).astype(np.uint64)
             f.import_bits(np.full(len(c), r, np.uint64), c)
         g = env.executor.gpu
+        g.executor = env.executor
         g.view_arena("i", "g", "standard", shards)
         for k in range(60):
             c, r = int(rng.integers(0, 4 * SW)), int(rng.integers(0, 8))
@@ -120,10 +121,35 @@ def test_executor_writes_merge_on_device():
             assert _decode(dv, si) == frag.storage.slice().astype(np.int64).tolist()
         # and queries through the device agree with the host
         before = g.launches
-        for r in range(8):
-            got = env.q("i", f"Count(Row(g={r}))")[0]
-            want = sum(env.holder.fragment("i", "g", "standard", s).row_count(r) for s in shards)
+
+        def cols(s, r):
+            v = env.holder.fragment("i", "g", "standard", s).storage.slice()
+            return v[(v >> np.uint64(20)) == np.uint64(r)] & np.uint64(SW - 1)
+        for r in range(7):
+            got = env.q("i", f"Count(Intersect(Row(g={r}), Row(g={r + 1})))")[0]
+            want = sum(len(np.intersect1d(cols(s, r), cols(s, r + 1))) for s in shards)
             assert got == want
         assert g.launches > before and g.rebuilds == 1
     finally:
         env.close()
+
+
+def test_compaction_on_device(view):
+    dv, host, rng = view
+    for k in range(6):
+        p = rng.integers(0, 6 * SW, 30000).astype(np.uint64)
+        assert dv.apply_positions(k % 3, p, clear=bool(k % 2))
+        if k % 2:
+            host[k % 3].remove_many(np.unique(p))
+        else:
+            host[k % 3].add_many(np.unique(p), True)
+    before = dv.payload_used
+    assert dv.garbage_u16 > 0
+    assert dv.compact()
+    assert dv.payload_used < before and dv.garbage_u16 == 0
+    _check(dv, host)
+    # and writes keep working on the compacted buffer
+    p = rng.integers(0, 6 * SW, 5000).astype(np.uint64)
+    assert dv.apply_positions(2, p)
+    host[2].add_many(np.unique(p), True)
+    _check(dv, host)
