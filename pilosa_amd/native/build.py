@@ -31,17 +31,26 @@ def _newer(target: str, sources) -> bool:
     return any(os.path.getmtime(s) > t for s in sources)
 
 
-def build_roaring(force: bool = False, verbose: bool = False) -> str:
+def build_roaring(force: bool = False, verbose: bool = False, stats: bool = False) -> str:
+    """Host roaring core.  ``stats`` builds the instrumented variant as the
+    separate module ``_roaring_stats`` (the reference's ``roaringstats`` build
+    tag); ``PILOSA_ROARING_STATS=1`` instruments the default ``_roaring``."""
     import pybind11
 
-    out = os.path.join(PKG, "_roaring" + _ext_suffix())
+    name = "_roaring_stats" if stats else "_roaring"
+    out = os.path.join(PKG, name + _ext_suffix())
     srcs = [os.path.join(HERE, f) for f in ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp")]
     deps = srcs + [os.path.join(HERE, f) for f in ("roaring.hpp", "synth.hpp")]
     if not force and not _newer(out, deps):
         return out
     cxx = os.environ.get("CXX", "g++")
-    flags = os.environ.get("PILOSA_AMD_CXXFLAGS", "-O3 -mpopcnt -mbmi2 -mavx2")
-    cmd = [cxx, "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *flags.split(),
+    flags = os.environ.get("PILOSA_AMD_CXXFLAGS", "-O3 -mpopcnt -mbmi2 -mavx2").split()
+    if stats or os.environ.get("PILOSA_ROARING_STATS", "0") == "1":
+        flags.append("-DPILOSA_ROARING_STATS")
+    if stats:
+        # own module name and C++ namespace: both variants can load in one process
+        flags += [f"-DPILOSA_ROARING_MODULE={name}", "-Dpr=pr_stats"]
+    cmd = [cxx, "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *flags,
            "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], *srcs,
            "-o", out + ".tmp", "-lpthread"]
     if verbose:
@@ -160,6 +169,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
 
 def build_all(force: bool = False, verbose: bool = False):
     r = build_roaring(force, verbose)
+    build_roaring(force, verbose, stats=True)
     build_pql(force, verbose)
     build_httpd(force, verbose)
     build_translate(force, verbose)

@@ -31,6 +31,10 @@
 #include "synth.hpp"
 
 namespace py = pybind11;
+
+#ifndef PILOSA_ROARING_MODULE
+#define PILOSA_ROARING_MODULE _roaring
+#endif
 using pr::Bitmap;
 using pr::Container;
 
@@ -480,7 +484,15 @@ static py::tuple topn_replay(I64Arr cand_rows, I64Arr cand_cnts,
 
 void register_arena_io(py::module_& m);  // arena_io.cpp
 
-PYBIND11_MODULE(_roaring, m) {
+PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
+  m.attr("ROARING_STATS") = pr::STATS_ENABLED;
+  m.def("roaring_stats", [](bool reset) {
+    py::dict d;
+    for (int k = 0; k < pr::ST_COUNT; k++) d[pr::STAT_NAMES[k]] = pr::stats_get(pr::StatId(k));
+    if (reset) pr::stats_reset();
+    return d;
+  }, py::arg("reset") = false, "container event counters (built with PILOSA_ROARING_STATS)");
+
   m.doc() = "Host roaring core (containers, pilosa file format, op log, device arena builder)";
   m.attr("ARRAY_MAX") = pr::ARRAY_MAX;
   m.attr("RUN_MAX") = pr::RUN_MAX;

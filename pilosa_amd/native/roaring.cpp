@@ -5,6 +5,7 @@
 #include <map>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 
 namespace pr {
@@ -17,6 +18,23 @@ static inline uint64_t rd64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); re
 static inline void put16(std::string& s, uint16_t v) { s.append(reinterpret_cast<const char*>(&v), 2); }
 static inline void put32(std::string& s, uint32_t v) { s.append(reinterpret_cast<const char*>(&v), 4); }
 static inline void put64(std::string& s, uint64_t v) { s.append(reinterpret_cast<const char*>(&v), 8); }
+
+const char* const STAT_NAMES[ST_COUNT] = {
+    "NewContainer",        "arrayAdd/append",          "arrayAdd/insert", "arrayAdd/arrayToBitmap",
+    "bitmapRemove/bitmapToArray", "runAdd/convert",    "runRemove/convert", "optimize/toRun",
+    "optimize/toArray",    "optimize/toBitmap",        "optimize/unchanged", "unionInPlace",
+    "sliceContainers/Remove"};
+#ifdef PILOSA_ROARING_STATS
+static std::atomic<int64_t> g_stats[ST_COUNT];
+void stats_hit(StatId s) { g_stats[s].fetch_add(1, std::memory_order_relaxed); }
+int64_t stats_get(StatId s) { return g_stats[s].load(std::memory_order_relaxed); }
+void stats_reset() {
+  for (auto& x : g_stats) x.store(0, std::memory_order_relaxed);
+}
+#else
+int64_t stats_get(StatId) { return 0; }
+void stats_reset() {}
+#endif
 
 // ---------------------------------------------------------------- container
 
@@ -209,10 +227,13 @@ void Container::optimize() {
   if (runs <= RUN_MAX && runs <= n / 2) nt = CT_RUN;
   else if (n < ARRAY_MAX) nt = CT_ARRAY;
   else nt = CT_BITMAP;
-  if (nt == type) return;
-  if (nt == CT_RUN) to_run();
-  else if (nt == CT_ARRAY) to_array();
-  else to_bitmap();
+  if (nt == type) {
+    stats_hit(ST_OPT_UNCHANGED);
+    return;
+  }
+  if (nt == CT_RUN) { stats_hit(ST_OPT_TO_RUN); to_run(); }
+  else if (nt == CT_ARRAY) { stats_hit(ST_OPT_TO_ARRAY); to_array(); }
+  else { stats_hit(ST_OPT_TO_BITMAP); to_bitmap(); }
 }
 
 bool Container::add(uint16_t v) {
@@ -221,11 +242,13 @@ bool Container::add(uint16_t v) {
       auto it = std::lower_bound(a.begin(), a.end(), v);
       if (it != a.end() && *it == v) return false;
       if (int(a.size()) >= ARRAY_MAX) {
+        stats_hit(ST_ARRAY_ADD_TO_BITMAP);
         to_bitmap();
         b[v >> 6] |= 1ull << (v & 63);
         n++;
         return true;
       }
+      stats_hit(it == a.end() ? ST_ARRAY_ADD_APPEND : ST_ARRAY_ADD_INSERT);
       a.insert(it, v);
       n++;
       return true;
@@ -239,6 +262,7 @@ bool Container::add(uint16_t v) {
     }
     case CT_RUN: {
       if (contains(v)) return false;
+      stats_hit(ST_RUN_ADD_CONVERT);
       if (n + 1 > ARRAY_MAX) to_bitmap(); else to_array();
       return add(v);
     }
@@ -260,11 +284,15 @@ bool Container::remove(uint16_t v) {
       if (!(b[v >> 6] & m)) return false;
       b[v >> 6] &= ~m;
       n--;
-      if (n <= ARRAY_MAX / 2) to_array();
+      if (n <= ARRAY_MAX / 2) {
+        stats_hit(ST_BITMAP_REMOVE_TO_ARRAY);
+        to_array();
+      }
       return true;
     }
     case CT_RUN: {
       if (!contains(v)) return false;
+      stats_hit(ST_RUN_REMOVE_CONVERT);
       if (n - 1 > ARRAY_MAX) to_bitmap(); else to_array();
       return remove(v);
     }
@@ -565,15 +593,22 @@ int64_t c_intersection_count(const Container& x, const Container& y) {
 Container& get_or_create(Bitmap& b, uint64_t key) { return b.cs[key]; }
 
 bool Bitmap::add(uint64_t v) {
-  Container& c = cs[v >> 16];
-  return c.add(uint16_t(v & 0xffff));
+  auto it = cs.find(v >> 16);
+  if (it == cs.end()) {
+    stats_hit(ST_NEW_CONTAINER);
+    it = cs.emplace(v >> 16, Container()).first;
+  }
+  return it->second.add(uint16_t(v & 0xffff));
 }
 
 bool Bitmap::remove(uint64_t v) {
   auto it = cs.find(v >> 16);
   if (it == cs.end()) return false;
   bool ch = it->second.remove(uint16_t(v & 0xffff));
-  if (it->second.n == 0) cs.erase(it);
+  if (it->second.n == 0) {
+    stats_hit(ST_CONTAINER_REMOVED);
+    cs.erase(it);
+  }
   return ch;
 }
 
@@ -799,6 +834,7 @@ void Bitmap::union_in_place(const std::vector<const Bitmap*>& others) {
     for (auto& kv : o->cs)
       if (kv.second.n) bykey[kv.first].push_back(&kv.second);
   std::vector<uint64_t> w(BITMAP_N);
+  stats_hit(ST_UNION_IN_PLACE);
   for (auto& kv : bykey) {
     Container& dst = cs[kv.first];
     if (kv.second.size() == 1 && dst.n == 0) {

@@ -40,6 +40,37 @@ constexpr uint32_t OFFICIAL_RUN = 12347;
 
 enum : uint8_t { CT_NIL = 0, CT_ARRAY = 1, CT_BITMAP = 2, CT_RUN = 3 };
 
+// Container event counters: the reference's ``roaringstats`` build tag
+// (roaring/roaring_stats.go, statsHit call sites across roaring.go).  Built in
+// with -DPILOSA_ROARING_STATS (native/build.py ``PILOSA_ROARING_STATS=1``),
+// read and reset through _roaring.roaring_stats(); otherwise a no-op.
+enum StatId : int {
+  ST_NEW_CONTAINER,
+  ST_ARRAY_ADD_APPEND,
+  ST_ARRAY_ADD_INSERT,
+  ST_ARRAY_ADD_TO_BITMAP,
+  ST_BITMAP_REMOVE_TO_ARRAY,
+  ST_RUN_ADD_CONVERT,
+  ST_RUN_REMOVE_CONVERT,
+  ST_OPT_TO_RUN,
+  ST_OPT_TO_ARRAY,
+  ST_OPT_TO_BITMAP,
+  ST_OPT_UNCHANGED,
+  ST_UNION_IN_PLACE,
+  ST_CONTAINER_REMOVED,
+  ST_COUNT
+};
+extern const char* const STAT_NAMES[ST_COUNT];
+#ifdef PILOSA_ROARING_STATS
+void stats_hit(StatId s);
+constexpr bool STATS_ENABLED = true;
+#else
+inline void stats_hit(StatId) {}
+constexpr bool STATS_ENABLED = false;
+#endif
+int64_t stats_get(StatId s);
+void stats_reset();
+
 struct Iv {
   uint16_t start, last;
 };

@@ -566,12 +566,16 @@ class Handler:
                        for s in spans[-1000:]])
 
     def debug_pprof(self, req):
-        import sys
-        frames = sys._current_frames()
-        out = []
-        for tid, fr in frames.items():
-            out.append(f"--- thread {tid}\n" + "".join(traceback.format_stack(fr)))
-        req.send(200, "\n".join(out), "text/plain")
+        from pilosa_amd.utils import pprof
+        try:
+            body = pprof.render(req.vars.get("rest", ""), {k: v for k, v in req.query.items()})
+        except KeyError:
+            req.send(404, "Unknown profile\n", "text/plain; charset=utf-8")
+            return
+        except ValueError as e:
+            req.send(400, f"{e}\n", "text/plain; charset=utf-8")
+            return
+        req.send(200, body, "text/plain; charset=utf-8")
 
 
 class Request:
