@@ -21,7 +21,7 @@ import sys
 import threading
 from typing import Dict, List, Optional
 
-SHARD_WIDTH = 1 << 20
+from pilosa_amd.shardwidth import SHARD_WIDTH  # noqa: E402
 
 
 # ------------------------------------------------------------------ config plumbing

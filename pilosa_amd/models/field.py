@@ -26,7 +26,7 @@ from pilosa_amd.errors import (ErrBSIGroupNotFound, ErrBSIGroupValueTooHigh, Err
                                validate_name)
 from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
 from pilosa_amd.models.cache import CACHE_TYPE_LRU, CACHE_TYPE_NONE, CACHE_TYPE_RANKED, DEFAULT_CACHE_SIZE
-from pilosa_amd.models.fragment import SHARD_WIDTH
+from pilosa_amd.models.fragment import SHARD_WIDTH, SHARD_WIDTH_EXP
 from pilosa_amd.models.row import Row
 from pilosa_amd.models.timeq import valid_quantum, views_by_time
 from pilosa_amd.models.view import VIEW_BSI_PREFIX, VIEW_STANDARD, View
@@ -496,7 +496,7 @@ class Field:
         if len(rows) != len(cols):
             raise PilosaError("row/column length mismatch")
         groups: Dict[Tuple[str, int], List[int]] = {}
-        shards = (cols >> np.uint64(20)).astype(np.int64)
+        shards = (cols >> np.uint64(SHARD_WIDTH_EXP)).astype(np.int64)
         q = self.time_quantum()
         std_ok = not self.options.no_standard_view
         if timestamps is None or all(t is None for t in timestamps):
@@ -548,7 +548,7 @@ class Field:
         else:
             base_vals = vals
         view = self.create_view_if_not_exists(self.bsi_view_name())
-        shards = (cols >> np.uint64(20)).astype(np.int64)
+        shards = (cols >> np.uint64(SHARD_WIDTH_EXP)).astype(np.int64)
         changed = 0
         for s in np.unique(shards):
             idx = shards == s

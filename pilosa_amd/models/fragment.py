@@ -33,9 +33,8 @@ from pilosa_amd.models.row import Row
 
 Bitmap = _roaring.Bitmap
 
-SHARD_WIDTH_EXP = 20
-SHARD_WIDTH = 1 << SHARD_WIDTH_EXP
-CONTAINERS_PER_ROW = SHARD_WIDTH >> 16
+from pilosa_amd.shardwidth import CONTAINERS_PER_ROW, SHARD_WIDTH  # noqa: E402
+from pilosa_amd.shardwidth import EXPONENT as SHARD_WIDTH_EXP  # noqa: E402
 HASH_BLOCK_SIZE = 100
 DEFAULT_MAX_OPN = 10000
 FALSE_ROW_ID, TRUE_ROW_ID = 0, 1

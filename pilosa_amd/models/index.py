@@ -13,6 +13,7 @@ import threading
 from typing import Dict, List, Optional
 
 from pilosa_amd.errors import ErrFieldExists, ErrFieldNotFound, ErrName, validate_name
+from pilosa_amd.shardwidth import SHARD_WIDTH
 from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
 from pilosa_amd.models.cache import CACHE_TYPE_NONE
 from pilosa_amd.models.field import Field, FieldOptions
@@ -148,4 +149,4 @@ class Index:
 
     def info(self) -> dict:
         return {"name": self.name, "options": self.options_json(),
-                "fields": [f.info() for f in self.public_fields()], "shardWidth": 1 << 20}
+                "fields": [f.info() for f in self.public_fields()], "shardWidth": SHARD_WIDTH}

@@ -13,7 +13,8 @@ import numpy as np
 
 from pilosa_amd import _roaring
 
-SHARD_WIDTH = 1 << 20
+from pilosa_amd.shardwidth import EXPONENT as _EXP
+from pilosa_amd.shardwidth import SHARD_WIDTH
 Bitmap = _roaring.Bitmap
 
 
@@ -40,7 +41,7 @@ class Row:
         cols = np.asarray(cols, dtype=np.uint64)
         if len(cols) == 0:
             return
-        shards = cols >> np.uint64(20)
+        shards = cols >> np.uint64(_EXP)
         for s in np.unique(shards):
             part = cols[shards == s]
             bm = self.segments.get(int(s))
@@ -49,7 +50,7 @@ class Row:
             bm.add_many(part)
 
     def set_bit(self, col: int) -> bool:
-        s = col >> 20
+        s = col >> _EXP
         bm = self.segments.get(s)
         if bm is None:
             bm = self.segments[s] = Bitmap()
@@ -160,7 +161,7 @@ class Row:
         return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint64)
 
     def includes(self, col: int) -> bool:
-        bm = self.segments.get(col >> 20)
+        bm = self.segments.get(col >> _EXP)
         return bm is not None and bm.contains(col)
 
     def __eq__(self, other):

@@ -11,7 +11,7 @@ import shutil
 import threading
 from typing import Callable, Dict, List, Optional
 
-from pilosa_amd.models.fragment import Fragment
+from pilosa_amd.models.fragment import SHARD_WIDTH_EXP, Fragment
 from pilosa_amd.models.row import Row
 
 VIEW_STANDARD = "standard"
@@ -116,23 +116,23 @@ class View:
         return r
 
     def set_bit(self, row_id: int, col: int) -> bool:
-        return self.create_fragment_if_not_exists(col >> 20).set_bit(row_id, col)
+        return self.create_fragment_if_not_exists(col >> SHARD_WIDTH_EXP).set_bit(row_id, col)
 
     def clear_bit(self, row_id: int, col: int) -> bool:
-        f = self.fragment(col >> 20)
+        f = self.fragment(col >> SHARD_WIDTH_EXP)
         return f.clear_bit(row_id, col) if f is not None else False
 
     def value(self, col: int, bit_depth: int):
-        f = self.fragment(col >> 20)
+        f = self.fragment(col >> SHARD_WIDTH_EXP)
         if f is None:
             return 0, False
         return f.value(col, bit_depth)
 
     def set_value(self, col: int, bit_depth: int, value: int) -> bool:
-        return self.create_fragment_if_not_exists(col >> 20).set_value(col, bit_depth, value)
+        return self.create_fragment_if_not_exists(col >> SHARD_WIDTH_EXP).set_value(col, bit_depth, value)
 
     def clear_value(self, col: int, bit_depth: int, value: int) -> bool:
-        f = self.fragment(col >> 20)
+        f = self.fragment(col >> SHARD_WIDTH_EXP)
         return f.clear_value(col, bit_depth, value) if f is not None else False
 
     def sum(self, filt: Optional[Row], bit_depth: int):

@@ -64,6 +64,10 @@ def _delta_keys(deltas) -> set:
 
 class GpuExecutor:
     def __init__(self, holder, device="cuda:0", executor=None, hbm_budget: int = 0):
+        from pilosa_amd import shardwidth
+        if not shardwidth.device_supported():
+            raise NotImplementedError(f"device arenas need 2^{shardwidth.DEVICE_EXPONENT}-column shards "
+                                      f"(PILOSA_SHARD_WIDTH={shardwidth.EXPONENT})")
         self.holder = holder
         self.engine = GpuEngine(device)
         self.device = self.engine.device

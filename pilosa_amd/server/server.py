@@ -34,6 +34,7 @@ from pilosa_amd.parallel.cluster import (NODE_DOWN, NODE_READY, RESIZE_ACTION_AD
                                          RESIZE_JOB_ABORTED, RESIZE_JOB_DONE, STATE_DEGRADED, STATE_NORMAL,
                                          STATE_RESIZING, STATE_STARTING, Cluster, JumpHasher, ModHasher, Node, ResizeJob, URI)
 from pilosa_amd.server.api import API
+from pilosa_amd.shardwidth import SHARD_WIDTH
 from pilosa_amd.server.client import InternalClient
 from pilosa_amd.server.http_handler import Handler, make_http_server
 from pilosa_amd.utils.logger import NopLogger, StandardLogger
@@ -238,6 +239,14 @@ class Server:
     def _init_gpu(self):
         mode = (self.gpu_mode or "auto").lower()
         if mode in ("off", "none", "cpu"):
+            return
+        from pilosa_amd import shardwidth
+        if not shardwidth.device_supported():
+            if mode == "on":
+                raise RuntimeError(f"gpu=on needs 2^{shardwidth.DEVICE_EXPONENT}-column shards "
+                                   f"(PILOSA_SHARD_WIDTH={shardwidth.EXPONENT})")
+            self.logger.printf("shard width 2^%d: the GPU kernels are built for 2^%d-column shards, "
+                               "queries run on the host", shardwidth.EXPONENT, shardwidth.DEVICE_EXPONENT)
             return
         try:
             import torch
@@ -691,7 +700,7 @@ class Server:
                 continue
             data = [self.client.block_data(n.uri, index, field, view, shard, bid) for n in live]
             sets, clears = frag.merge_block(bid, data)
-            base = shard << 20
+            base = shard * SHARD_WIDTH
             for n, (sr, sc), (cr, cc) in zip(live, sets, clears):
                 if sr:
                     self.client.import_bits(n, index, field, shard, sr, [base + c for c in sc],

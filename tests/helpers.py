@@ -10,7 +10,7 @@ from pilosa_amd.executor import Executor
 from pilosa_amd.models.field import FieldOptions
 from pilosa_amd.models.holder import Holder
 
-SW = 1 << 20
+from pilosa_amd.shardwidth import SHARD_WIDTH as SW  # noqa: E402
 
 
 class Env:

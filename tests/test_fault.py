@@ -14,7 +14,7 @@ import urllib.request
 
 import pytest
 
-SW = 1 << 20
+from pilosa_amd.shardwidth import SHARD_WIDTH as SW  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 

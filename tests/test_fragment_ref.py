@@ -14,7 +14,7 @@ from pilosa_amd.models.cache import CACHE_TYPE_LRU, CACHE_TYPE_NONE, CACHE_TYPE_
 from pilosa_amd.models.fragment import Fragment, TopOptions
 from pilosa_amd.models.row import Row
 
-SW = 1 << 20
+from pilosa_amd.shardwidth import SHARD_WIDTH as SW  # noqa: E402
 
 
 class _Frags:
@@ -99,6 +99,8 @@ def test_rowcache_map(frags):
 
 
 def test_clear_row(frags):
+    if SW <= 1 << 16:
+        pytest.skip("uses a second container per row (columns >= 65536 in shard 0)")
     f = frags.open()
     f.set_bit(1000, 1)
     f.set_bit(1000, 65536)
@@ -109,6 +111,8 @@ def test_clear_row(frags):
 
 
 def test_set_row(frags):
+    if SW <= 1 << 16:
+        pytest.skip("uses a second container per row (columns >= 65536 in shard 0)")
     f = frags.open(shard=7)
     f.set_bit(1000, 7 * SW + 1)
     f.set_bit(1000, 7 * SW + 65536)
@@ -492,6 +496,8 @@ def test_concurrent_import(frags):
 
 # ---------------------------------------------------------------- rows / roaring import (:2634-2915)
 def test_rows_iteration(frags):
+    if SW <= 1 << 16:
+        pytest.skip("uses a second container per row (columns >= 65536 in shard 0)")
     f = frags.open()
     for i in range(100, 200):
         f.set_bit(i, i % 2)
@@ -615,6 +621,7 @@ def test_import_clear_restart(frags, max_opn):
              ([0] * 10, [0, 65535, 65536, 131071, 131072, 196607, 196608, 262143, 262144, 1000000]),
              ([1, 2, 20, 200, 2000, 200000], [1] * 6)]
     for rows, cs in cases:
+        cs = [c % SW for c in cs]   # shard 0 under any PILOSA_SHARD_WIDTH
         exp = {}
         for r, c in zip(rows, cs):
             exp.setdefault(r, set()).add(c)

@@ -13,7 +13,7 @@ from pilosa_amd.server.client import InternalClient
 from pilosa_amd.server.server import Server
 from pilosa_amd.utils.logger import CaptureLogger
 
-SW = 1 << 20
+from pilosa_amd.shardwidth import SHARD_WIDTH as SW  # noqa: E402
 
 
 def _req(srv, method, path, body=b"", headers=None):
