@@ -312,7 +312,18 @@ class Server:
             self.logger.printf("broadcast %s: %d errors, first: %s", msg.get("type"), len(errs), errs[0])
 
     def _on_create_shard(self, index, field, shard):
-        self.broadcast({"type": "CreateShard", "index": index, "field": field, "shard": shard})
+        """Announce a new shard; like view.go:239-262 the write waits for the
+        broadcast at most 50 ms and lets it finish in the background."""
+        done = threading.Event()
+
+        def send():
+            try:
+                self.broadcast({"type": "CreateShard", "index": index, "field": field, "shard": shard})
+            finally:
+                done.set()
+        threading.Thread(target=send, name="create-shard", daemon=True).start()
+        if not done.wait(0.05):
+            self.logger.debugf("broadcasting create shard took >50ms")
 
     def receive_message(self, msg: dict):
         """Dispatch of internal cluster messages (server.go:549-643)."""
