@@ -95,7 +95,6 @@ class Fragment:
         self.checksums: Dict[int, bytes] = {}
         self.opn = 0
         self.ops = 0
-        self._snap_mu = threading.Lock()   # one snapshot at a time per fragment
         self._file_gen = 0                 # bumped whenever the data file is replaced
         self._max_row_id = 0
         # lazy open: the file is only validated by its header; the storage (and
@@ -294,47 +293,50 @@ class Fragment:
 
         Writers are only blocked while the storage is serialised and while
         the file is swapped: the write + fsync of the snapshot runs outside
-        ``mu``.  Ops appended to the old file meanwhile are copied onto the
-        new one before the rename, so none is lost (the reference holds the
-        fragment lock throughout, fragment.go:2240-2290)."""
-        with self._snap_mu:
-            with self.mu:
-                if self._fh is None and not os.path.exists(self.path):
-                    return  # closed/deleted while queued
-                data = self.storage.to_bytes()
-                gen = self._file_gen
-                mark = self._file_size()
-                opn0, ops0 = self.opn, self.ops
-            tmp = self.path + ".snapshotting"
-            with open(tmp, "wb") as fh:
-                fh.write(data)
-                fh.flush()
-                os.fsync(fh.fileno())
-            with self.mu:
-                if gen != self._file_gen or (self._fh is None and not os.path.exists(self.path)):
-                    os.unlink(tmp)    # replaced (read_from) or closed meanwhile
-                    return
-                end = self._file_size()
-                if end > mark:
-                    with open(self.path, "rb") as src, open(tmp, "ab") as dst:
-                        src.seek(mark)
-                        dst.write(src.read(end - mark))
-                        dst.flush()
-                        os.fsync(dst.fileno())
-                if self._fh is not None:
-                    try:
-                        fcntl.flock(self._fh.fileno(), fcntl.LOCK_UN)
-                    except OSError:
-                        pass
-                    self._fh.close()
-                os.replace(tmp, self.path)
-                self._file_gen += 1
-                self._fh = open(self.path, "ab", buffering=0)
-                fcntl.flock(self._fh.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
-                self.opn -= opn0
-                self.ops -= ops0
-                if self.stats:
-                    self.stats.count("snapshot", 1)
+        ``mu`` (unless the caller already holds it, e.g. ``set_row``).  Ops
+        appended to the old file meanwhile are copied onto the new one before
+        the rename, so none is lost; a snapshot that finds the file replaced
+        under it (a newer snapshot, ``read_from``) discards its own.  The
+        reference holds the fragment lock throughout (fragment.go:2240-2290).
+        No second lock is taken, so a snapshot queued in the background and
+        one run synchronously under ``mu`` cannot deadlock."""
+        with self.mu:
+            if self._fh is None and not os.path.exists(self.path):
+                return  # closed/deleted while queued
+            data = self.storage.to_bytes()
+            gen = self._file_gen
+            mark = self._file_size()
+            opn0, ops0 = self.opn, self.ops
+        tmp = f"{self.path}.{os.getpid()}.{threading.get_ident()}.snapshotting"
+        with open(tmp, "wb") as fh:
+            fh.write(data)
+            fh.flush()
+            os.fsync(fh.fileno())
+        with self.mu:
+            if gen != self._file_gen or (self._fh is None and not os.path.exists(self.path)):
+                os.unlink(tmp)    # replaced (newer snapshot, read_from) or closed meanwhile
+                return
+            end = self._file_size()
+            if end > mark:
+                with open(self.path, "rb") as src, open(tmp, "ab") as dst:
+                    src.seek(mark)
+                    dst.write(src.read(end - mark))
+                    dst.flush()
+                    os.fsync(dst.fileno())
+            if self._fh is not None:
+                try:
+                    fcntl.flock(self._fh.fileno(), fcntl.LOCK_UN)
+                except OSError:
+                    pass
+                self._fh.close()
+            os.replace(tmp, self.path)
+            self._file_gen += 1
+            self._fh = open(self.path, "ab", buffering=0)
+            fcntl.flock(self._fh.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
+            self.opn -= opn0
+            self.ops -= ops0
+            if self.stats:
+                self.stats.count("snapshot", 1)
 
     def _file_size(self) -> int:
         if self._fh is not None:

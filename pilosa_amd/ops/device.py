@@ -501,106 +501,146 @@ class DeviceView:
         ``si`` directly in the arena: container_merge / container_emit on the
         GPU (kernels/write_kernels.hip), only the positions go over PCIe.
         False -> the caller must refresh the shard another way."""
-        if self._cap is None or self.device.type != "cuda":
-            return False
-        p = np.unique(np.asarray(positions, dtype=np.uint64))
-        if not len(p):
-            return True
-        rows_p = p >> np.uint64(20)
-        urows = np.unique(rows_p)
-        dense_r = self.dense_many(urows)
-        if (dense_r < 0).any():
-            if clear:   # rows this view has no containers for: nothing to clear there
-                p = p[np.isin(rows_p, urows[dense_r >= 0])]
-                if not len(p):
-                    return True
-            elif not self.add_rows(urows[dense_r < 0]):
-                return False
-        ck = (p >> np.uint64(16)).astype(np.int64)
-        uk, start = np.unique(ck, return_index=True)
-        dense = self.dense_many((uk >> 4).astype(np.uint64))
-        dstart = np.append(start, len(p)).astype(np.int32)
-        return self._device_merge(si, dense, (uk & 15).astype(np.int32), 0, clear, dstart=dstart,
-                                  dlows=(p & np.uint64(0xFFFF)).astype(np.uint16))
+        return not self.apply_deltas_multi({si: [("pos", positions, clear)]})
 
     def apply_bitmap(self, si: int, bitmap, clear: bool = False) -> bool:
         """ImportRoaringBits on the device: OR (AND-NOT) every container of
         ``bitmap`` (shard-local positions) into the arena, container against
         container (mode 1 of container_merge)."""
-        from pilosa_amd import _roaring
-
-        if self._cap is None or self.device.type != "cuda":
-            return False
-        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], 16, 1)
-        n = int(sb_s[-1])
-        if not n:
-            return True
-        counts = np.diff(rp_s[0].astype(np.int64))
-        drow = np.repeat(rows_s.astype(np.uint64), counts)
-        dmeta = meta_s[:n].astype(np.int64)
-        dense = self.dense_many(drow)
-        if (dense < 0).any():
-            if clear:
-                keep = dense >= 0
-                drow, dmeta, dense = drow[keep], dmeta[keep], dense[keep]
-                if not len(drow):
-                    return True
-            else:
-                if not self.add_rows(np.unique(drow[dense < 0])):
-                    return False
-                dense = self.dense_many(drow)
-        return self._device_merge(si, dense, (dmeta & 15).astype(np.int32), 1, clear, dmeta=dmeta,
-                                  dpayload=pay_s)
+        return not self.apply_deltas_multi({si: [("roaring", bitmap, clear)]})
 
     def apply_deltas(self, si: int, deltas) -> bool:
-        """Replay a fragment's recorded writes in order: runs of position
-        batches with the same set/clear flag are merged into one launch."""
-        i = 0
-        while i < len(deltas):
-            kind, data, clear = deltas[i]
-            if kind == "roaring":
-                if not self.apply_bitmap(si, data, clear):
-                    return False
-                i += 1
-                continue
-            j = i + 1
-            while j < len(deltas) and deltas[j][0] == "pos" and deltas[j][2] == clear:
-                j += 1
-            pos = data if j == i + 1 else np.concatenate([d[1] for d in deltas[i:j]])
-            if not self.apply_positions(si, pos, clear):
-                return False
-            i = j
-        return True
+        """Replay one shard's recorded writes in order."""
+        return not self.apply_deltas_multi({si: deltas})
+
+    @staticmethod
+    def _runs(deltas):
+        """Merge consecutive position batches with the same set/clear flag."""
+        out = []
+        for kind, data, clear in deltas:
+            if kind == "pos" and out and out[-1][0] == "pos" and out[-1][2] == clear:
+                out[-1][1].append(np.asarray(data, dtype=np.uint64))
+            elif kind == "pos":
+                out.append(("pos", [np.asarray(data, dtype=np.uint64)], clear))
+            else:
+                out.append((kind, data, clear))
+        return [(k, np.concatenate(d) if k == "pos" else d, c) for k, d, c in out]
+
+    def apply_deltas_multi(self, per_shard) -> set:
+        """Replay the recorded writes of several local shards: the r-th write
+        run of every shard goes into the same container_merge /
+        container_emit launches (grouped by kind and set/clear), so a refresh
+        costs a few launches and transfers, not a few per shard.  Returns the
+        shard indices whose replay failed (the caller rebuilds those)."""
+        if self._cap is None or self.device.type != "cuda":
+            return set(per_shard)
+        runs = {si: self._runs(d) for si, d in per_shard.items() if d}
+        failed: set = set()
+        r = 0
+        while True:
+            layer = [(si, rs[r]) for si, rs in runs.items() if r < len(rs) and si not in failed]
+            if not layer:
+                return failed
+            for kind in ("pos", "roaring"):
+                for clear in (False, True):
+                    group = [(si, data) for si, (k, data, c) in layer if k == kind and c == clear]
+                    if group:
+                        failed |= self._replay_group(group, kind, clear)
+            r += 1
+
+    def _replay_group(self, group, kind: str, clear: bool) -> set:
+        from pilosa_amd import _roaring
+
+        jobs = []   # (si, container row ids, j, mode-specific arrays)
+        for si, data in group:
+            if kind == "pos":
+                p = np.unique(np.asarray(data, dtype=np.uint64))
+                if not len(p):
+                    continue
+                ck = (p >> np.uint64(16)).astype(np.int64)
+                uk, start = np.unique(ck, return_index=True)
+                jobs.append([si, (uk >> 4).astype(np.uint64), (uk & 15).astype(np.int32),
+                             np.append(start, len(p)).astype(np.int64), (p & np.uint64(0xFFFF)).astype(np.uint16)])
+            else:
+                rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([data], 16, 1)
+                n = int(sb_s[-1])
+                if not n:
+                    continue
+                drow = np.repeat(rows_s.astype(np.uint64), np.diff(rp_s[0].astype(np.int64)))
+                dmeta = meta_s[:n].astype(np.int64)
+                jobs.append([si, drow, (dmeta & 15).astype(np.int32), dmeta, pay_s])
+        if not jobs:
+            return set()
+        # rows new to the directory: added once for the whole group (sets only)
+        allrows = np.unique(np.concatenate([jb[1] for jb in jobs]))
+        dense_all = self.dense_many(allrows)
+        if (dense_all < 0).any() and not clear:
+            if not self.add_rows(allrows[dense_all < 0]):
+                return {jb[0] for jb in jobs}
+        for jb in jobs:
+            dense = self.dense_many(jb[1])
+            if clear and (dense < 0).any():     # nothing to clear in rows this view never had
+                keep = dense >= 0
+                if kind == "pos":
+                    counts = np.diff(jb[3])
+                    lows = np.concatenate([jb[4][a:b] for a, b, k in zip(jb[3][:-1], jb[3][1:], keep) if k]) \
+                        if keep.any() else np.zeros(0, np.uint16)
+                    jb[3] = np.concatenate([[0], np.cumsum(counts[keep])]).astype(np.int64)
+                    jb[4] = lows
+                else:
+                    jb[3] = jb[3][keep]
+                jb[1], jb[2], dense = jb[1][keep], jb[2][keep], dense[keep]
+            jb.append(dense)
+        jobs = [jb for jb in jobs if len(jb[1])]
+        if not jobs:
+            return set()
+        return self._merge_jobs(jobs, 0 if kind == "pos" else 1, clear)
 
     WRITE_CHUNK = 16384   # containers per merge launch (128 MiB of bitmap scratch)
 
-    def _device_merge(self, si: int, dense: np.ndarray, j: np.ndarray, mode: int, clear: bool, dstart=None,
-                      dlows=None, dmeta=None, dpayload=None) -> bool:
+    def _merge_jobs(self, jobs, mode: int, clear: bool) -> set:
+        """Merge + emit every job's containers in shared launches, then splice
+        each shard's new metadata words into its segment."""
         import torch
 
         K = kernels()
         dev = self.device
-        base, seg, segkeys = self._seg_keys(si)
-        qk = dense.astype(np.int64) * 16 + j
-        U = len(qk)
-        if len(segkeys):
-            idx = np.minimum(np.searchsorted(segkeys, qk), len(segkeys) - 1)
-            found = segkeys[idx] == qk
-            old = np.where(found, seg[idx], -1).astype(np.int64)
-        else:
-            idx = np.zeros(U, np.int64)
-            found = np.zeros(U, bool)
-            old = np.full(U, -1, np.int64)
-        t_old = torch.from_numpy(old).to(dev)
-        t_j = torch.from_numpy(np.ascontiguousarray(j, dtype=np.int32)).to(dev)
+        seg_info, olds, js, qks = [], [], [], []
+        for jb in jobs:
+            si, dense, j = jb[0], jb[-1], jb[2]
+            base, seg, segkeys = self._seg_keys(si)
+            qk = dense.astype(np.int64) * 16 + j
+            if len(segkeys):
+                idx = np.minimum(np.searchsorted(segkeys, qk), len(segkeys) - 1)
+                found = segkeys[idx] == qk
+                old = np.where(found, seg[idx], -1).astype(np.int64)
+            else:
+                idx = np.zeros(len(qk), np.int64)
+                found = np.zeros(len(qk), bool)
+                old = np.full(len(qk), -1, np.int64)
+            seg_info.append((si, seg, segkeys, qk, idx, found, old))
+            olds.append(old)
+            js.append(j)
+        U = sum(len(o) for o in olds)
+        t_old = torch.from_numpy(np.concatenate(olds)).to(dev)
+        t_j = torch.from_numpy(np.ascontiguousarray(np.concatenate(js), dtype=np.int32)).to(dev)
         empty16 = torch.empty(0, dtype=torch.int16, device=dev)
         empty64 = torch.empty(0, dtype=torch.int64, device=dev)
         empty32 = torch.empty(1, dtype=torch.int32, device=dev)
         if mode == 0:
-            t_lows = torch.from_numpy(dlows.view(np.int16)).to(dev)
+            offs = np.cumsum([0] + [len(jb[4]) for jb in jobs])
+            dstart = np.concatenate([jb[3][:-1] + offs[k] for k, jb in enumerate(jobs)] + [[offs[-1]]]).astype(np.int64)
+            t_lows = torch.from_numpy(np.concatenate([jb[4] for jb in jobs]).view(np.int16)).to(dev)
         else:
-            t_dmeta = torch.from_numpy(np.ascontiguousarray(dmeta, dtype=np.int64)).to(dev)
-            t_dpay = torch.from_numpy(np.ascontiguousarray(dpayload).view(np.int16)).to(dev)
+            pays, metas, at16 = [], [], 0
+            for jb in jobs:
+                mm = jb[3].view(np.uint64)
+                metas.append(((mm & np.uint64((1 << 23) - 1)) | (((mm >> np.uint64(23)) + np.uint64(at16))
+                                                                 << np.uint64(23))).view(np.int64))
+                pays.append(np.ascontiguousarray(jb[4]))
+                at16 += len(jb[4]) // 8
+            t_dmeta = torch.from_numpy(np.concatenate(metas)).to(dev)
+            t_dpay = torch.from_numpy(np.concatenate(pays).view(np.int16)).to(dev)
         new_meta = np.empty(U, np.int64)
         used = self.payload_used
         for c0 in range(0, U, self.WRITE_CHUNK):
@@ -626,36 +666,47 @@ class DeviceView:
                 grown = self.grow_payload(tot)
                 self.payload_used = prev
                 if not grown:
-                    return False
+                    return {jb[0] for jb in jobs}
             off16 = (ends - sizes + used) // 8
             meta_out = torch.empty(n, dtype=torch.int64, device=dev)
             K.container_emit(scratch, card, off16, t_j[c0:c1], self.t_payload, meta_out)
             new_meta[c0:c1] = meta_out.cpu().numpy()
             used += tot
-        # splice the new metadata words into the shard's segment
-        keep = new_meta >= 0
-        old_n = (old >> 6) & 0x1FFFF
-        old_t = (old >> 4) & 3
-        self.garbage_u16 += int(np.where(found, np.where(old_t == 2, 4096, (old_n + 7) // 8 * 8), 0).sum())
-        if not (found & ~keep).any() and not (~found & keep).any():
-            at = base + idx[found]
-            self._meta_host[at] = new_meta[found]
-            if len(at):
-                self.t_meta.index_copy_(0, torch.from_numpy(at).to(dev), torch.from_numpy(new_meta[found]).to(dev))
-        else:
+        self.payload_used = used
+        failed = set()
+        at = 0
+        scatter_at, scatter_val = [], []
+        for si, seg, segkeys, qk, idx, found, old in seg_info:
+            nm = new_meta[at:at + len(qk)]
+            at += len(qk)
+            keep = nm >= 0
+            old_n = (old >> 6) & 0x1FFFF
+            old_t = (old >> 4) & 3
+            self.garbage_u16 += int(np.where(found, np.where(old_t == 2, 4096, (old_n + 7) // 8 * 8), 0).sum())
+            base = int(self._sb_host[si])
+            if not (found & ~keep).any() and not (~found & keep).any():
+                pos = base + idx[found]
+                self._meta_host[pos] = nm[found]
+                scatter_at.append(pos)
+                scatter_val.append(nm[found])
+                continue
             kept = np.ones(len(seg), bool)
             kept[idx[found & ~keep]] = False          # containers that became empty
             ins = keep & ~found
             repl = keep & found
             seg2 = seg.copy()
-            seg2[idx[repl]] = new_meta[repl]
+            seg2[idx[repl]] = nm[repl]
             keys = np.concatenate([segkeys[kept], qk[ins]])
-            vals = np.concatenate([seg2[kept], new_meta[ins]])
+            vals = np.concatenate([seg2[kept], nm[ins]])
             order = np.argsort(keys, kind="stable")
             keys, vals = keys[order], vals[order]
             if len(vals) > int(self._cap[si]):
+                if scatter_at:   # a re-layout moves segments: flush pending in-place updates first
+                    self._flush_meta_scatter(scatter_at, scatter_val)
+                    scatter_at, scatter_val = [], []
                 if not self.grow_segment(si, len(vals)):
-                    return False
+                    failed.add(si)
+                    continue
                 base = int(self._sb_host[si])
             rp_new = np.zeros(self.D + 1, np.int64)
             rp_new[1:] = np.cumsum(np.bincount(keys >> 4, minlength=self.D)[:self.D])
@@ -665,9 +716,17 @@ class DeviceView:
             self.t_rowptr.view(self.S, self.D + 1)[si].copy_(torch.from_numpy(rp_new.astype(np.int32)).to(dev))
             self._meta_host[base:base + len(full)] = full
             self._rowptr_host[si] = rp_new
-        self.payload_used = used
+        if scatter_at:
+            self._flush_meta_scatter(scatter_at, scatter_val)
         self.generation += 1
-        return True
+        return failed
+
+    def _flush_meta_scatter(self, at, val):
+        import torch
+        pos = np.concatenate(at)
+        if len(pos):
+            self.t_meta.index_copy_(0, torch.from_numpy(pos).to(self.device),
+                                    torch.from_numpy(np.concatenate(val)).to(self.device))
 
     def needs_compaction(self) -> bool:
         """Dead payload from in-place updates exceeds half the buffer."""

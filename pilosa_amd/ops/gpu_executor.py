@@ -125,6 +125,7 @@ class GpuExecutor:
                 # only some shards changed: rewrite their segments in place
                 dv = hit[1]
                 ok = True
+                pending = {}   # si -> write batches replayed on the device after the loop
                 for si, (old, new, f) in enumerate(zip(hit[0], sig, frags)):
                     if old == new:
                         continue
@@ -136,13 +137,13 @@ class GpuExecutor:
                         if dirty is not None:
                             rows, keys, deltas = dirty
                             ok = True
-                            if deltas:
-                                # writes replayed on the device (K11/K12), only the batches cross PCIe;
-                                # otherwise the containers they touched are rebuilt from the host
-                                if self.device_writes_on and dv.apply_deltas(si, deltas):
-                                    self.device_writes += 1
-                                else:
-                                    keys = set(keys) | _delta_keys(deltas)
+                            if deltas and self.device_writes_on and dv.device.type == "cuda":
+                                # writes replayed on the device (K11/K12), all shards in shared launches;
+                                # only the batches cross PCIe.  Rows rebuilt below from the current
+                                # storage may see the batches again: set/clear replays are idempotent
+                                pending[si] = deltas
+                            elif deltas:
+                                keys = set(keys) | _delta_keys(deltas)
                             if ok and (rows or keys):
                                 ok = dv.update_rows(si, rows, f.storage, keys=keys)
                                 self.row_updates += ok
@@ -150,10 +151,21 @@ class GpuExecutor:
                             ok = False
                         if not ok:
                             f.take_dirty(dv.token)
+                            pending.pop(si, None)
                             ok = dv.update_shard(si, f.storage)
                     if not ok:
                         break
                     self.shard_updates += 1
+                if ok and pending:
+                    failed = dv.apply_deltas_multi(pending)
+                    self.device_writes += len(pending) - len(failed)
+                    for si in sorted(failed):   # rebuild what the device could not take from the host
+                        f = frags[si]
+                        with f.mu:
+                            ok = dv.update_rows(si, set(), f.storage, keys=_delta_keys(pending[si])) or \
+                                dv.update_shard(si, f.storage)
+                        if not ok:
+                            break
                 if ok:
                     self._arenas[key] = (sig, dv)
                     return dv

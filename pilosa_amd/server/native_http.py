@@ -141,7 +141,7 @@ class NativeHTTPServer:
     def _generic_loop(self):
         srv, handler = self.srv, self.handler
         while not self._stop.is_set():
-            for rid, method, path, query, headers, body in srv.take(1, 100):
+            for rid, method, path, query, headers, body in srv.take(1, 500):
                 req = NativeRequest(srv, rid, method, path, query, headers, body)
                 try:
                     handler.dispatch(req)
@@ -160,7 +160,7 @@ class NativeHTTPServer:
     def _count_loop(self):
         srv = self.srv
         while not self._stop.is_set():
-            for index, ids, ncalls, text in srv.take_counts(self.max_batch, 100):
+            for index, ids, ncalls, text in srv.take_counts(self.max_batch, 500):
                 t0 = time.perf_counter()
                 counts = self._count_group(index, text, sum(ncalls))
                 self.count_s += time.perf_counter() - t0

@@ -48,3 +48,27 @@ class Env:
 
 def cols(row):
     return [int(c) for c in row.columns()]
+
+
+def free_port() -> int:
+    """A currently free TCP port below the kernel's ephemeral range.
+
+    A port taken from ``bind(0)`` and released is soon handed out again to
+    some other test's ``bind(0)`` server (xdist workers run side by side), so
+    a test that picks a port for a server started later could end up talking
+    to another test's server.  Ports below 32768 are never assigned by
+    ``bind(0)``."""
+    import random
+    import socket
+    rng = random.Random()
+    for _ in range(1000):
+        p = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port below 32000")

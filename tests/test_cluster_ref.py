@@ -225,10 +225,8 @@ def test_confirm_node_down_timeout():
 
 
 def test_confirm_node_down_down():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()   # nothing listens there any more
+    from tests.helpers import free_port
+    port = free_port()   # nothing listens there (and bind(0) servers never get it)
     assert confirm_node_down(URI("http", "127.0.0.1", port), retries=2, sleep=0.05, timeout=0.5)
 
 
@@ -432,7 +430,8 @@ def test_cluster_gossip_membership_invalid_seed_first():
     ms = []
     try:
         assert _wait(lambda: m0.cluster.state == "NORMAL")
-        dead = "http://127.0.0.1:8765"
+        from tests.helpers import free_port
+        dead = f"http://127.0.0.1:{free_port()}"
         ts = [threading.Thread(target=lambda nid=nid, h=h: ms.append(_join(m0, nid, h)))
               for nid, h in [("node1", [dead, m0.uri.normalize()]), ("node2", [m0.uri.normalize(), dead])]]
         for t in ts:

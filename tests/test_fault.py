@@ -19,11 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from tests.helpers import free_port
+    return free_port()
 
 
 def _req(port, method, path, body=None, timeout=30):
@@ -80,6 +77,15 @@ def test_paused_node_failover():
         _wait(lambda: all(n["state"] == "READY" for n in _req(ports[0], "GET", "/status")["nodes"]),
               timeout=30, what="node READY again")
         assert _req(ports[0], "POST", "/index/i/query", "Count(Row(f=1))")["results"] == [12]
+    except Exception:
+        # thread dumps of every node, to tell a stall from a slow machine
+        for p in ports:
+            try:
+                with urllib.request.urlopen(f"http://127.0.0.1:{p}/debug/pprof/goroutine?debug=1", timeout=5) as r:
+                    print(f"==== node :{p}\n" + r.read().decode()[:20000])
+            except Exception as e:  # noqa: BLE001
+                print(f"==== node :{p}: {e}")
+        raise
     finally:
         for p in procs:
             try:

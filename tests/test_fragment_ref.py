@@ -762,3 +762,38 @@ def test_snapshot_does_not_stall_writers_and_keeps_their_ops(frags, monkeypatch)
     assert f.opn >= 0
     g = frags.reopen(f)
     assert cols(g.row(1)) == list(range(1, 100)) and cols(g.row(2)) == list(range(100, 150))
+
+
+def test_background_and_inline_snapshots_do_not_deadlock(frags, monkeypatch):
+    """A queued snapshot in its write+fsync phase and a ClearRow (which
+    snapshots while holding the fragment lock) must both finish; the newer
+    inline snapshot wins and the background one discards its file."""
+    import threading
+    import pilosa_amd.models.fragment as fm
+    f = frags.open()
+    for c in range(50):
+        f.set_bit(1, c)
+        f.set_bit(2, c)
+    entered, release = threading.Event(), threading.Event()
+    real_fsync = os.fsync
+
+    def slow_fsync(fd):
+        if threading.current_thread().name == "bg-snap" and not entered.is_set():
+            entered.set()
+            assert release.wait(10)
+        real_fsync(fd)
+    monkeypatch.setattr(fm.os, "fsync", slow_fsync)
+    bg = threading.Thread(target=f.snapshot, name="bg-snap")
+    bg.start()
+    assert entered.wait(10)
+    done = threading.Event()
+    t = threading.Thread(target=lambda: (f.clear_row(1), done.set()))
+    t.start()
+    assert done.wait(10), "ClearRow deadlocked against the background snapshot"
+    release.set()
+    bg.join(10)
+    t.join(10)
+    assert not bg.is_alive()
+    g = frags.reopen(f)
+    assert cols(g.row(1)) == [] and cols(g.row(2)) == list(range(50))
+    assert not [n for n in os.listdir(os.path.dirname(f.path)) if n.endswith(".snapshotting")]

@@ -41,11 +41,8 @@ QUERIES = [
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    from tests.helpers import free_port
+    return free_port()
 
 
 def _data():
