@@ -224,9 +224,20 @@ def bench_cpu_host(args, ra, rb, nshards, nq=256):
             total += r1.intersection_count(r2)
     dt = time.perf_counter() - t0
     per_q_all_shards = dt / n * (nshards / k)
+    # our host fallback (Executor.count_shard): the rows counted in place
+    t0 = time.perf_counter()
+    total2 = 0
+    for a, b in zip(ra[:n], rb[:n]):
+        a, b = int(a), int(b)
+        for f in frags:
+            total2 += f.range_intersection_count(a * w, f, b * w, w)
+    per_q_inplace = (time.perf_counter() - t0) / n * (nshards / k)
     return {"shards_timed": k, "queries": n, "threads": 1, "checksum": total,
             "ms_per_query_all_shards_1core": round(per_q_all_shards * 1000, 3),
-            "qps_per_core": round(1.0 / per_q_all_shards, 3)}
+            "qps_per_core": round(1.0 / per_q_all_shards, 3),
+            "host_fallback_in_place": {"checksum_matches": total2 == total,
+                                       "ms_per_query_all_shards_1core": round(per_q_inplace * 1000, 3),
+                                       "qps_per_core": round(1.0 / per_q_inplace, 3)}}
 
 
 def _timed(fn, reps, world, dev):

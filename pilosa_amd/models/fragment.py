@@ -382,6 +382,22 @@ class Fragment:
         with self.mu:
             return self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
 
+    def row_intersection_count(self, row_id: int, other: "Fragment", other_row: int) -> int:
+        """|row_id ∩ other.other_row| read in place (no row extraction).
+
+        Host fast path for Count(Intersect(Row, Row)); the reference builds both
+        rows with OffsetRange and intersects them (fragment.go:559-580,
+        executor.go executeCount).  Locks are taken in a fixed order so two
+        counts over the same pair of fragments cannot deadlock."""
+        first, second = (self, other) if id(self) <= id(other) else (other, self)
+        with first.mu:
+            if second is first:
+                return self.storage.range_intersection_count(row_id * SHARD_WIDTH, other.storage,
+                                                             other_row * SHARD_WIDTH, SHARD_WIDTH)
+            with second.mu:
+                return self.storage.range_intersection_count(row_id * SHARD_WIDTH, other.storage,
+                                                             other_row * SHARD_WIDTH, SHARD_WIDTH)
+
     def _pos(self, row_id: int, col: int) -> int:
         lo = self.shard * SHARD_WIDTH
         if col < lo or col >= lo + SHARD_WIDTH:

@@ -554,6 +554,12 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
       .def("difference", &Bitmap::difference, py::call_guard<py::gil_scoped_release>())
       .def("xor", &Bitmap::xor_, py::call_guard<py::gil_scoped_release>())
       .def("intersection_count", &Bitmap::intersection_count, py::call_guard<py::gil_scoped_release>())
+      .def("range_intersection_count", &Bitmap::range_intersection_count, py::arg("a_start"), py::arg("other"),
+           py::arg("b_start"), py::arg("length"), py::call_guard<py::gil_scoped_release>())
+      .def_static("range_union_count", [](std::vector<std::pair<const Bitmap*, uint64_t>> srcs, uint64_t len) {
+        py::gil_scoped_release nogil;
+        return Bitmap::range_union_count(srcs, len);
+      }, py::arg("sources"), py::arg("length"))
       .def("union_in_place", [](Bitmap& b, std::vector<const Bitmap*> others) {
         py::gil_scoped_release nogil;
         b.union_in_place(others);

@@ -550,6 +550,22 @@ int64_t c_intersection_count(const Container& x, const Container& y) {
       }
       return c;
     }
+    if (s.size() >= 64) {
+      // scatter the larger array into a stack bitmap and probe it with the
+      // smaller one: no data-dependent branches (a merge mispredicts about
+      // every other step on random arrays)
+      uint64_t w[BITMAP_N];
+      memset(w, 0, sizeof w);
+      for (uint16_t v : l) w[v >> 6] |= 1ull << (v & 63);
+      int64_t c0 = 0, c1 = 0;
+      size_t i = 0;
+      for (; i + 2 <= s.size(); i += 2) {
+        c0 += (w[s[i] >> 6] >> (s[i] & 63)) & 1;
+        c1 += (w[s[i + 1] >> 6] >> (s[i + 1] & 63)) & 1;
+      }
+      if (i < s.size()) c0 += (w[s[i] >> 6] >> (s[i] & 63)) & 1;
+      return c0 + c1;
+    }
     size_t i = 0, j = 0;
     while (i < s.size() && j < l.size()) {
       if (s[i] < l[j]) i++;
@@ -567,7 +583,29 @@ int64_t c_intersection_count(const Container& x, const Container& y) {
     const Container& arr = x.type == CT_ARRAY ? x : y;
     const Container& oth = x.type == CT_ARRAY ? y : x;
     int64_t c = 0;
-    for (uint16_t v : arr.a) c += oth.contains(v);
+    if (oth.type == CT_BITMAP) {
+      // branch-free bit probes, 4 independent accumulators
+      const uint64_t* w = oth.b.data();
+      const uint16_t* a = arr.a.data();
+      const size_t n = arr.a.size();
+      int64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+      size_t i = 0;
+      for (; i + 4 <= n; i += 4) {
+        c0 += (w[a[i] >> 6] >> (a[i] & 63)) & 1;
+        c1 += (w[a[i + 1] >> 6] >> (a[i + 1] & 63)) & 1;
+        c2 += (w[a[i + 2] >> 6] >> (a[i + 2] & 63)) & 1;
+        c3 += (w[a[i + 3] >> 6] >> (a[i + 3] & 63)) & 1;
+      }
+      for (; i < n; i++) c0 += (w[a[i] >> 6] >> (a[i] & 63)) & 1;
+      return c0 + c1 + c2 + c3;
+    }
+    // array & run: one merge walk over the sorted values and runs
+    size_t r = 0;
+    for (uint16_t v : arr.a) {
+      while (r < oth.r.size() && oth.r[r].last < v) r++;
+      if (r == oth.r.size()) break;
+      c += oth.r[r].start <= v;
+    }
     return c;
   }
   // run with bitmap or run with run
@@ -823,6 +861,58 @@ int64_t Bitmap::intersection_count(const Bitmap& o) const {
       ++i;
       ++j;
     }
+  }
+  return c;
+}
+
+int64_t Bitmap::range_intersection_count(uint64_t a_start, const Bitmap& o, uint64_t b_start, uint64_t len) const {
+  // |rows a ∩ b| read in place: the same container walk as intersection_count,
+  // but over key windows [a_start, a_start+len) of this bitmap and
+  // [b_start, b_start+len) of `o`, so no row is extracted (the reference
+  // executor pays OffsetRange copies per row, fragment.go:559-580).
+  if ((a_start & 0xffff) || (b_start & 0xffff) || (len & 0xffff))
+    throw std::invalid_argument("range_intersection_count: starts/len must be multiples of 65536");
+  const uint64_t ak = a_start >> 16, bk = b_start >> 16, nk = len >> 16;
+  int64_t c = 0;
+  auto i = cs.lower_bound(ak);
+  auto j = o.cs.lower_bound(bk);
+  while (i != cs.end() && j != o.cs.end() && i->first - ak < nk && j->first - bk < nk) {
+    const uint64_t ri = i->first - ak, rj = j->first - bk;
+    if (ri < rj) ++i;
+    else if (ri > rj) ++j;
+    else {
+      c += c_intersection_count(i->second, j->second);
+      ++i;
+      ++j;
+    }
+  }
+  return c;
+}
+
+int64_t Bitmap::range_union_count(const std::vector<std::pair<const Bitmap*, uint64_t>>& srcs, uint64_t len) {
+  // |∪ rows| over key windows of several bitmaps (a time Row's covering views,
+  // executor.go:1444-1533) without building the union: per relative key the
+  // containers are OR-ed into one word buffer, a lone container is counted
+  // from its cardinality.
+  if (len & 0xffff) throw std::invalid_argument("range_union_count: len must be a multiple of 65536");
+  const uint64_t nk = len >> 16;
+  std::map<uint64_t, std::vector<const Container*>> bykey;
+  for (auto& s : srcs) {
+    if (s.second & 0xffff) throw std::invalid_argument("range_union_count: starts must be multiples of 65536");
+    const uint64_t sk = s.second >> 16;
+    for (auto it = s.first->cs.lower_bound(sk); it != s.first->cs.end() && it->first - sk < nk; ++it)
+      if (it->second.n) bykey[it->first - sk].push_back(&it->second);
+  }
+  int64_t c = 0;
+  std::vector<uint64_t> w(BITMAP_N);
+  for (auto& kv : bykey) {
+    if (kv.second.size() == 1) {
+      c += kv.second[0]->n;
+      continue;
+    }
+    std::fill(w.begin(), w.end(), 0);
+    for (const Container* x : kv.second) x->to_words(w.data());
+    for (int i = 0; i < BITMAP_N; i++) c += popc(w[i]);
   }
   return c;
 }

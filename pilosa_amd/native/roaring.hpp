@@ -145,6 +145,9 @@ class Bitmap {
   Bitmap difference(const Bitmap& o) const;
   Bitmap xor_(const Bitmap& o) const;
   int64_t intersection_count(const Bitmap& o) const;
+  // zero-copy row counts: key windows [start, start+len) (65536-aligned)
+  int64_t range_intersection_count(uint64_t a_start, const Bitmap& o, uint64_t b_start, uint64_t len) const;
+  static int64_t range_union_count(const std::vector<std::pair<const Bitmap*, uint64_t>>& srcs, uint64_t len);
   void union_in_place(const std::vector<const Bitmap*>& others);
   Bitmap shift(int n) const;
   Bitmap flip(uint64_t start, uint64_t end) const;
