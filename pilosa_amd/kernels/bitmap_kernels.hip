@@ -487,6 +487,164 @@ __global__ __launch_bounds__(256) void union_count_kernel(const QueryProg* __res
   if (lane == 0 && total) atomicAdd(out + q, (unsigned long long)total);
 }
 
+// Union count v2 (MODE 4, the default for Count(Union(leaves))).  v1 above
+// walks the leaves of a key one after the other: slot (LDS) -> meta (global)
+// -> payload (global) -> returning LDS atomics, i.e. two dependent global
+// round trips per (leaf, key), ~7x16 of them in series per (query, shard) for
+// a YMDH time range.  Here
+//   * the metas of every (leaf, key) are fetched in one parallel round trip
+//     (lane = (leaf, container) pair) into a wave-private LDS table;
+//   * per key, the present leaves' payloads are walked as ONE flat list of
+//     16-byte chunks (array: 8 values, bitmap: 2 words), so the loads of all
+//     leaves are in flight together (4 per lane per step); a lane finds its
+//     chunk's leaf by comparing with the leaves' chunk prefix (scalar
+//     readlanes) and fetches the leaf's meta / payload pointer with bpermutes;
+//   * values are OR-ed into the LDS bitmap with NON-returning ds_or, and the
+//     key's union is counted by one popcount pass that also re-zeroes it;
+//   * a key present in one leaf only is counted from its metadata.
+// Run containers (rare in time views) are OR-ed in a second, per-run loop.
+__device__ __forceinline__ int shfl_i32(int v, int src) { return __shfl(v, src); }
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
+  const int lo = __shfl(int(uint64_t(v)), src), hi = __shfl(int(uint64_t(v) >> 32), src);
+  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+}
+
+__global__ __launch_bounds__(256) void union_count2_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                           const ViewDev* __restrict__ views, int S,
+                                                           unsigned long long* __restrict__ out) {
+  __shared__ uint32_t lbits[WAVES_PER_BLOCK][2048];
+  __shared__ int64_t lmeta[WAVES_PER_BLOCK][MAXLEAF * 16];
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int wave = threadIdx.x >> 6;
+  const int lane = wave_lane();
+  const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
+  if (item >= int64_t(Q) * S) return;
+  const int q = int(item % Q);
+  const int s = int(item / Q);
+  const QueryProg& qp = progs[q];
+  const int nleaf = qp.nleaf;
+  uint32_t* lb = lbits[wave];
+  int64_t* mt = lmeta[wave];
+  for (int t = lane; t < MAXLEAF * 16; t += 64) mt[t] = -1;
+  {
+    uint4* lb4 = reinterpret_cast<uint4*>(lb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) lb4[i * 64 + lane] = make_uint4(0, 0, 0, 0);
+  }
+  lds_fence();
+  // (leaf, container) metas: lane -> leaf k0 + lane/16, container lane%16
+#pragma unroll
+  for (int k0 = 0; k0 < MAXLEAF; k0 += 4) {
+    const int k = k0 + (lane >> 4), idx = lane & 15;
+    if (k0 < nleaf && k < nleaf) {
+      const int64_t d = qp.leaf_row[k];
+      if (d >= 0) {
+        const ViewDev& v = views[qp.leaf_view[k]];
+        const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+        const int64_t base = v.shard_base[s];
+        const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+        if (idx < hi - lo) {
+          const int64_t m = v.meta[lo + idx];
+          mt[k * 16 + meta_j(m)] = m;
+        }
+      }
+    }
+  }
+  lds_fence();
+  bool has = false;
+  if (lane < 16)
+    for (int k = 0; k < nleaf; k++) has |= mt[k * 16 + lane] >= 0;
+  const uint32_t cand = uint32_t(__ballot(has) & 0xffff);
+  // per-leaf payload base pointer (lane k < nleaf)
+  const uint16_t* lpay = lane < nleaf ? views[qp.leaf_view[lane]].payload : nullptr;
+  int64_t total = 0;
+  unsigned long long* lb64 = reinterpret_cast<unsigned long long*>(lb);
+  for (uint32_t cm = cand; cm; cm &= cm - 1) {
+    const int j = __builtin_ctz(cm);
+    const int64_t m = lane < nleaf ? mt[lane * 16 + j] : -1;
+    const uint64_t pres = __ballot(m >= 0);
+    if (__popcll(pres) == 1) {  // one leaf holds this key: its cardinality
+      if (lane == __builtin_ctzll(pres)) total += meta_n(m);
+      continue;
+    }
+    const int type = m >= 0 ? meta_type(m) : -1;
+    const int cnt = type == CT_ARRAY ? (meta_n(m) + 7) >> 3 : (type == CT_BITMAP ? 512 : 0);
+    // inclusive scan of chunk counts over lanes 0..15
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const int t = __shfl_up(incl, d);
+      if ((lane & 15) >= d) incl += t;
+    }
+    const int pre = incl - cnt;
+    const int tot = __builtin_amdgcn_readlane(incl, 15);
+    const uint16_t* lptr = (m >= 0) ? lpay + meta_off16(m) * 8 : nullptr;
+    for (int c0 = 0; c0 < tot; c0 += 256) {
+      int c[4], leaf[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) { c[u] = c0 + u * 64 + lane; leaf[u] = 0; }
+      for (int k = 1; k < nleaf; k++) {
+        const int pk = __builtin_amdgcn_readlane(pre, k);
+#pragma unroll
+        for (int u = 0; u < 4; u++) leaf[u] += c[u] >= pk;
+      }
+      uint4 v[4];
+      int64_t mm[4];
+      int loc[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        mm[u] = shfl_i64(m, leaf[u]);
+        loc[u] = c[u] - shfl_i32(pre, leaf[u]);
+        const uint4* p = reinterpret_cast<const uint4*>(shfl_i64(int64_t(lptr), leaf[u]));
+        if (c[u] < tot) v[u] = p[loc[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (c[u] >= tot) continue;
+        if (meta_type(mm[u]) == CT_BITMAP) {
+          atomicOr(lb64 + 2 * loc[u], (unsigned long long)(uint64_t(v[u].y) << 32 | v[u].x));
+          atomicOr(lb64 + 2 * loc[u] + 1, (unsigned long long)(uint64_t(v[u].w) << 32 | v[u].z));
+        } else {
+          const int n = meta_n(mm[u]);
+          const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int t = 0; t < 8; t++) {
+            const uint32_t x = (w4[t >> 1] >> ((t & 1) * 16)) & 0xffff;
+            if (loc[u] * 8 + t < n) atomicOr(lb + (x >> 5), 1u << (x & 31));
+          }
+        }
+      }
+    }
+    // run containers of this key
+    uint64_t runs = __ballot(type == CT_RUN);
+    for (; runs; runs &= runs - 1) {
+      const int k = __builtin_ctzll(runs);
+      const uint16_t* p = reinterpret_cast<const uint16_t*>(shfl_i64(int64_t(lptr), k));
+      const int nr = p[0];
+      for (int r = lane; r < nr; r += 64) {
+        const uint32_t st = p[8 + 2 * r], e = uint32_t(p[9 + 2 * r]) + 1;
+        for (uint32_t w = st >> 6; w <= (e - 1) >> 6; w++) {
+          uint64_t mk = ~0ull;
+          if (w == (st >> 6)) mk &= ~0ull << (st & 63);
+          if (w == ((e - 1) >> 6) && (e & 63)) mk &= (1ull << (e & 63)) - 1;
+          atomicOr(lb64 + w, (unsigned long long)mk);
+        }
+      }
+    }
+    lds_fence();
+    uint4* lb4 = reinterpret_cast<uint4*>(lb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint4 w = lb4[i * 64 + lane];
+      total += __popc(w.x) + __popc(w.y) + __popc(w.z) + __popc(w.w);
+      lb4[i * 64 + lane] = make_uint4(0, 0, 0, 0);
+    }
+    lds_fence();
+  }
+  total = wave_sum_i64(total);
+  if (lane == 0 && total) atomicAdd(out + q, (unsigned long long)total);
+}
+
 // Materialize kernel: writes result containers for every (q, s, j) with
 // counts[q,s,j] > 0 at u16 offset offs[q,s,j]; array if n <= 4096 else bitmap.
 __global__ __launch_bounds__(256) void expr_materialize_kernel(const QueryProg* __restrict__ progs, int Q,
@@ -1110,11 +1268,13 @@ void launch_expr_count(const QueryProg* progs, int Q, const ViewDev* views, int 
   const int64_t items = int64_t(Q) * S;
   if (items == 0) return;
   const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
-  if (mode == 3 && per_key == nullptr && per_shard == nullptr)
+  if (mode == 4 && per_key == nullptr && per_shard == nullptr)
+    hipLaunchKernelGGL(union_count2_kernel, grid, block, 0, st, progs, Q, views, S, out);
+  else if (mode == 3 && per_key == nullptr && per_shard == nullptr)
     hipLaunchKernelGGL(union_count_kernel, grid, block, 0, st, progs, Q, views, S, out);
   else if (mode == 1 && per_key == nullptr)
     hipLaunchKernelGGL(expr_count_kernel<1>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
-  else if (mode == 2 || mode == 3)
+  else if (mode == 2 || mode == 3 || mode == 4)
     hipLaunchKernelGGL(expr_count_kernel<2>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);
   else
     hipLaunchKernelGGL(expr_count_kernel<0>, grid, block, 0, st, progs, Q, views, S, out, per_key, per_shard);

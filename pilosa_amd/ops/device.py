@@ -843,6 +843,8 @@ class GpuEngine:
         self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "6"))
         # Count(Union(leaves)) route: union_count_kernel (bitmap_kernels.hip)
         self.use_union = os.environ.get("PILOSA_UNION_KERNEL", "1") != "0"
+        # 2 = union_count2_kernel (flat chunk walk, parallel meta fetch), 1 = union_count_kernel
+        self.union_variant = int(os.environ.get("PILOSA_UNION_VARIANT", "2"))
 
     def _views_tensor(self, views: List["DeviceView"]):
         arr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
@@ -1028,7 +1030,10 @@ class GpuEngine:
                 o = self._and2_partial(tp, tv, S, n).sum(dim=(0, 1), dtype=torch.int64)
             else:
                 o = torch.zeros(n, dtype=torch.int64, device=self.device)
-                self.ext.expr_count(tp, tv, S, o, None, _KERNEL_MODE[kind])
+                mode = _KERNEL_MODE[kind]
+                if kind == KIND_UNION and self.union_variant == 2:
+                    mode = 4  # union_count2_kernel
+                self.ext.expr_count(tp, tv, S, o, None, mode)
             out.index_copy_(0, ti, o)
         return out
 
@@ -1055,6 +1060,26 @@ class GpuEngine:
         p["prog"][:, 0] = 0
         p["prog"][:, 1] = 1
         p["prog"][:, 2] = OP_AND
+        return p
+
+    @staticmethod
+    def union_programs(dense: np.ndarray) -> np.ndarray:
+        """Count(Union(Row r of view 0, Row r of view 1, ...)) records built
+        directly (vectorised) from ``dense[Q, V]`` = the dense index of each
+        query's row in each of the V batch views (slots 0..V-1), e.g. the
+        covering views of a time-range Row.  Flat OR fold, as compile_expr
+        emits it: l0 l1 | l2 | ..."""
+        dense = np.asarray(dense, np.int64)
+        Q, V = dense.shape
+        if not 1 <= V <= MAXLEAF:
+            raise CompileError("too many leaves")
+        p = np.zeros(Q, dtype=QPROG_DTYPE)
+        p["nleaf"] = V
+        p["nprog"] = 2 * V - 1
+        p["leaf_view"][:, :V] = np.arange(V)
+        p["leaf_row"][:, :V] = dense
+        prog = [0] + [x for k in range(1, V) for x in (k, OP_OR)]
+        p["prog"][:, :len(prog)] = prog
         return p
 
     def count_per_shard_progs(self, progs: np.ndarray, views: List["DeviceView"], S: int,

@@ -230,3 +230,31 @@ def test_pair_kernel_array_size_boundaries(cq, variant):
     np.testing.assert_array_equal(got, np.array(want))
     per = eng.count_per_shard(exprs)
     np.testing.assert_array_equal(per[:, 0], np.array(want))
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_union_count_kernels(setup, variant):
+    """Count(Union(...)) of 2..16 leaves on union_count_kernel (1) and
+    union_count2_kernel (2): every container mix, repeated leaves, missing
+    rows, keys held by one leaf only (the metadata shortcut)."""
+    from pilosa_amd.ops.device import Leaf, Op
+    frags, view, eng = setup
+    old = eng.union_variant
+    eng.union_variant = variant
+    try:
+        rng = np.random.default_rng(11)
+        sets = [[0, 1], [2, 3], [0, 2, 3], [1, 1, 2], [3, 7, 11, 99], list(range(12)),
+                [5, 9, 2, 6, 10, 3, 7, 11, 0, 4, 8, 1, 2, 3, 99, 98]]
+        sets += [list(rng.integers(0, 14, size=rng.integers(2, 17))) for _ in range(24)]
+        exprs = [Op("or", tuple(Leaf(view, int(r)) for r in rs)) for rs in sets]
+        got = eng.count(exprs)
+        for rs, g in zip(sets, got):
+            want = 0
+            for f in frags:
+                u = R.Bitmap()
+                for r in rs:
+                    u = u.union(_row(f, int(r)))
+                want += u.count()
+            assert g == want, (variant, rs)
+    finally:
+        eng.union_variant = old
