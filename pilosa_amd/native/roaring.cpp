@@ -455,9 +455,11 @@ std::string Container::check() const {
 
 // ---------------------------------------------------------------- pairwise
 
-static Container from_words_vec(std::vector<uint64_t>& w) {
+// word buffers of the pairwise ops live on the stack (8 KiB each): no heap
+// allocation per container pair
+static Container from_words_vec(const uint64_t* w) {
   Container c;
-  c.set_words(w.data());
+  c.set_words(w);
   return c;
 }
 
@@ -478,9 +480,9 @@ Container c_intersect(const Container& x, const Container& y) {
     out.n = int32_t(out.a.size());
     return out;
   }
-  std::vector<uint64_t> wx(BITMAP_N, 0), wy(BITMAP_N, 0);
-  x.to_words(wx.data());
-  y.to_words(wy.data());
+  uint64_t wx[BITMAP_N] = {0}, wy[BITMAP_N] = {0};
+  x.to_words(wx);
+  y.to_words(wy);
   for (int i = 0; i < BITMAP_N; i++) wx[i] &= wy[i];
   return from_words_vec(wx);
 }
@@ -495,9 +497,9 @@ Container c_union(const Container& x, const Container& y) {
     out.n = int32_t(out.a.size());
     return out;
   }
-  std::vector<uint64_t> w(BITMAP_N, 0);
-  x.to_words(w.data());
-  y.to_words(w.data());
+  uint64_t w[BITMAP_N] = {0};
+  x.to_words(w);
+  y.to_words(w);
   return from_words_vec(w);
 }
 
@@ -511,9 +513,9 @@ Container c_difference(const Container& x, const Container& y) {
     out.n = int32_t(out.a.size());
     return out;
   }
-  std::vector<uint64_t> wx(BITMAP_N, 0), wy(BITMAP_N, 0);
-  x.to_words(wx.data());
-  y.to_words(wy.data());
+  uint64_t wx[BITMAP_N] = {0}, wy[BITMAP_N] = {0};
+  x.to_words(wx);
+  y.to_words(wy);
   for (int i = 0; i < BITMAP_N; i++) wx[i] &= ~wy[i];
   return from_words_vec(wx);
 }
@@ -527,9 +529,9 @@ Container c_xor(const Container& x, const Container& y) {
     out.n = int32_t(out.a.size());
     return out;
   }
-  std::vector<uint64_t> wx(BITMAP_N, 0), wy(BITMAP_N, 0);
-  x.to_words(wx.data());
-  y.to_words(wy.data());
+  uint64_t wx[BITMAP_N] = {0}, wy[BITMAP_N] = {0};
+  x.to_words(wx);
+  y.to_words(wy);
   for (int i = 0; i < BITMAP_N; i++) wx[i] ^= wy[i];
   return from_words_vec(wx);
 }
