@@ -146,32 +146,42 @@ __device__ __forceinline__ void tile_op(Tile& a, const Tile& b) {
 // Per-wave scratch in LDS.
 struct WaveScratch {
   uint64_t lb[1024];          // 8 KiB expansion bitmap
-  int32_t slot[MAXLEAF][16];  // container index per (leaf, j), -1 absent
+  int64_t meta[MAXLEAF][16];  // container meta word per (leaf, j), -1 absent
 };
 
-// Build the slot table for every leaf of query `qp` in shard `s`; returns the
-// presence mask of each leaf in `mask[]` (wave-uniform).
+// Build the (leaf, key) meta table for query `qp` in shard `s`; returns the
+// presence mask of each leaf in `mask[]` (wave-uniform).  Lanes take
+// (leaf, container) pairs -- 4 leaves per pass, passes unrolled -- so the
+// rowptr and meta loads of all leaves are in flight together instead of one
+// leaf's dependent chain after the other's; the key loops then read metas
+// from LDS, not global memory.
 __device__ __forceinline__ void build_slots(const QueryProg& qp, const ViewDev* views, int s, WaveScratch& ws,
                                             uint32_t* mask) {
   const int lane = wave_lane();
-  for (int t = lane; t < MAXLEAF * 16; t += 64) (&ws.slot[0][0])[t] = -1;
+  for (int t = lane; t < MAXLEAF * 16; t += 64) (&ws.meta[0][0])[t] = -1;
   lds_fence();
-  for (int k = 0; k < qp.nleaf; k++) {
-    const int64_t d = qp.leaf_row[k];
-    if (d < 0) continue;
-    const ViewDev& v = views[qp.leaf_view[k]];
-    const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
-    const int64_t base = v.shard_base[s];
-    const int64_t lo = base + rp[d], hi = base + rp[d + 1];
-    if (lane < hi - lo) {
-      const int64_t ci = lo + lane;
-      ws.slot[k][meta_j(v.meta[ci])] = int32_t(ci - base);
+  const int nleaf = qp.nleaf;
+#pragma unroll
+  for (int k0 = 0; k0 < MAXLEAF; k0 += 4) {
+    const int k = k0 + (lane >> 4), idx = lane & 15;
+    if (k0 < nleaf && k < nleaf) {
+      const int64_t d = qp.leaf_row[k];
+      if (d >= 0) {
+        const ViewDev& v = views[qp.leaf_view[k]];
+        const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+        const int64_t base = v.shard_base[s];
+        const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+        if (idx < hi - lo) {
+          const int64_t m = v.meta[lo + idx];
+          ws.meta[k][meta_j(m)] = m;
+        }
+      }
     }
   }
   lds_fence();
   for (int k0 = 0; k0 < MAXLEAF; k0 += 4) {
     const int k = k0 + (lane >> 4);
-    const bool has = ws.slot[k][lane & 15] >= 0;
+    const bool has = ws.meta[k][lane & 15] >= 0;
     const uint64_t b = __ballot(has);
 #pragma unroll
     for (int i = 0; i < 4; i++) mask[k0 + i] = uint32_t((b >> (16 * i)) & 0xffff);
@@ -208,13 +218,9 @@ __device__ __forceinline__ void eval_tile(const QueryProg& qp, const ViewDev* vi
     const int op = qp.prog[pc];
     if (op < OP_AND) {
       t3 = t2; t2 = t1; t1 = acc;
-      const int32_t c = ws.slot[op][j];
-      if (c < 0) {
-        tile_zero(acc);
-      } else {
-        const ViewDev& v = views[qp.leaf_view[op]];
-        tile_load(acc, v.payload, v.meta[v.shard_base[s] + c], ws.lb);
-      }
+      const int64_t m = ws.meta[op][j];
+      if (m < 0) tile_zero(acc);
+      else tile_load(acc, views[qp.leaf_view[op]].payload, m, ws.lb);
     } else {
       // acc = t1 OP acc
       if (op == OP_AND) { tile_op<OP_AND>(t1, acc); }
@@ -320,13 +326,9 @@ constexpr int WAVES_PER_BLOCK = 4;
 // Flat fold: acc = l0; acc = acc op_i l_i.
 __device__ __forceinline__ void load_leaf(const QueryProg& qp, const ViewDev* views, int s, int j, WaveScratch& ws,
                                           int k, Tile& t) {
-  const int32_t c = ws.slot[k][j];
-  if (c < 0) {
-    tile_zero(t);
-  } else {
-    const ViewDev& v = views[qp.leaf_view[k]];
-    tile_load(t, v.payload, v.meta[v.shard_base[s] + c], ws.lb);
-  }
+  const int64_t m = ws.meta[k][j];
+  if (m < 0) tile_zero(t);
+  else tile_load(t, views[qp.leaf_view[k]].payload, m, ws.lb);
 }
 
 __device__ __forceinline__ void eval_flat(const QueryProg& qp, const ViewDev* views, int s, int j, WaveScratch& ws,
@@ -366,10 +368,8 @@ __global__ __launch_bounds__(256, MODE == 0 ? 1 : 4) void expr_count_kernel(cons
   if (cand) {
     if (qp.nprog == 1) {
       // Count(Row): metadata only
-      const ViewDev& v = views[qp.leaf_view[0]];
       if (lane < 16 && ((cand >> lane) & 1)) {
-        const int c = ws.slot[0][lane];
-        const int n = meta_n(v.meta[v.shard_base[s] + c]);
+        const int n = meta_n(ws.meta[0][lane]);
         total = n;
         if (per_key) per_key[(int64_t(q) * S + s) * 16 + lane] = n;
       }
@@ -379,8 +379,8 @@ __global__ __launch_bounds__(256, MODE == 0 ? 1 : 4) void expr_count_kernel(cons
       const ViewDev& vb = views[qp.leaf_view[1]];
       for (uint32_t cm = cand; cm; cm &= cm - 1) {
         const int j = __builtin_ctz(cm);
-        const int64_t ma = va.meta[va.shard_base[s] + ws.slot[0][j]];
-        const int64_t mb = vb.meta[vb.shard_base[s] + ws.slot[1][j]];
+        const int64_t ma = ws.meta[0][j];
+        const int64_t mb = ws.meta[1][j];
         total += and2_count(va, ma, vb, mb, ws.lb);
       }
     } else {
@@ -437,10 +437,9 @@ __global__ __launch_bounds__(256) void union_count_kernel(const QueryProg* __res
     for (int i = 0; i < 8; i++) l2[i * 64 + lane] = make_ulong2(0, 0);
     lds_fence();
     for (int k = 0; k < qp.nleaf; k++) {
-      const int32_t c = ws.slot[k][j];
-      if (c < 0) continue;
+      const int64_t m = ws.meta[k][j];
+      if (m < 0) continue;
       const ViewDev& v = views[qp.leaf_view[k]];
-      const int64_t m = v.meta[v.shard_base[s] + c];
       const uint16_t* p = v.payload + meta_off16(m) * 8;
       const int type = meta_type(m);
       if (type == CT_BITMAP) {

@@ -506,6 +506,11 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
 // hot_meta[s][j][k] is the row's key-j container (meta index relative to the
 // shard, -1 = none), built once with the index.
 constexpr int HOT_THREADS = 1024;
+// 1 = big hot-rank containers stream as one 16-byte load per lane per
+// 512-value chunk (8 values, packed until counted); 0 = 8 two-byte loads
+#ifndef HOT_VEC_LOADS
+#define HOT_VEC_LOADS 1
+#endif
 constexpr int HOT_TAB_WORDS = 32768;
 constexpr int HOT_SMALL_N = 255;  // byte counters: at most 255 values per lane-owned container
 
@@ -578,6 +583,18 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(ml) >> 32)), r));
       return int64_t((uint64_t(hi) << 32) | lo);
     };
+#if HOT_VEC_LOADS
+    // lane l takes values base + 8l .. +7 with ONE 16-byte load (the payload
+    // is 16-byte aligned and padded to 8 values); the raw words stay packed
+    // in 4 VGPRs until the chunk is counted, so the load stays in flight
+    auto load_chunk = [&](int64_t m, int base, uint4& x, int& nv) {
+      const uint4* pp4 = reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8);
+      const int i0 = base + 8 * lane;
+      nv = min(max(meta_n(m) - i0, 0), 8);
+      x = make_uint4(0, 0, 0, 0);
+      if (nv > 0) x = pp4[i0 >> 3];
+    };
+#else
     auto load_chunk = [&](int64_t m, int base, int (&x)[8]) {
       const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
       const int n = meta_n(m);
@@ -587,14 +604,21 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         x[t] = i < n ? int(pp[i]) : -1;
       }
     };
+#endif
     int r = __builtin_ctzll(live);
     live &= live - 1;
     int64_t m = row_meta(r);
     int base = 0;
+#if HOT_VEC_LOADS
+    uint4 cur = make_uint4(0, 0, 0, 0);
+    int curv = 0;
+    if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur, curv);
+#else
     int cur[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) cur[t] = -1;
     if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur);
+#endif
     uint32_t c4[4] = {0u, 0u, 0u, 0u};
     uint32_t acc[16];
 #pragma unroll
@@ -617,16 +641,29 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         bn = 0;
         mn = rn >= 0 ? row_meta(rn) : 0;
       }
+#if HOT_VEC_LOADS
+      uint4 nxt = make_uint4(0, 0, 0, 0);
+      int nxtv = 0;
+      if (rn >= 0 && meta_type(mn) == CT_ARRAY) load_chunk(mn, bn, nxt, nxtv);
+#else
       int nxt[8];
 #pragma unroll
       for (int t = 0; t < 8; t++) nxt[t] = -1;
       if (rn >= 0 && meta_type(mn) == CT_ARRAY) load_chunk(mn, bn, nxt);
+#endif
       const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
       if (ty == CT_ARRAY) {
         // an array gives a lane at most 64 values: bytes cannot overflow
+#if HOT_VEC_LOADS
+        const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+        for (int t = 0; t < 8; t++)
+          if (t < curv) swar_add(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
+#else
 #pragma unroll
         for (int t = 0; t < 8; t++)
           if (cur[t] >= 0) swar_add(c4, mask_of(cur[t]));
+#endif
       } else if (ty == CT_BITMAP) {
         const uint64_t* w = reinterpret_cast<const uint64_t*>(pp);
         for (int i = lane; i < 1024; i += 64) {
@@ -682,8 +719,13 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       r = rn;
       base = bn;
       m = mn;
+#if HOT_VEC_LOADS
+      cur = nxt;
+      curv = nxtv;
+#else
 #pragma unroll
       for (int t = 0; t < 8; t++) cur[t] = nxt[t];
+#endif
     }
   }
 
