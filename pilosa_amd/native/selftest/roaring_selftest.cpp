@@ -4,9 +4,11 @@
 // native-code analogue for our host core).  Exit status 0 = pass.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../roaring.hpp"
@@ -47,7 +49,47 @@ static std::set<uint64_t> gen(std::mt19937_64& rng, int kind) {
   return s;
 }
 
+// Concurrent readers (the executor's host pool runs roaring ops with the GIL
+// released, several threads reading the same fragment bitmaps) plus
+// per-thread writers; built with -fsanitize=thread by
+// tests/test_native_sanitizers.py.  Any shared mutable state in the core
+// (e.g. the roaringstats counters) shows up as a data race.
+static int run_threads(int nthreads) {
+  std::mt19937_64 rng(777);
+  auto sa = gen(rng, 0), sb = gen(rng, 1), sc = gen(rng, 2);
+  sa.insert(sc.begin(), sc.end());
+  const Bitmap a = from_set(sa), b = from_set(sb);
+  const int64_t want = a.intersection_count(b);
+  const int64_t want_u = a.unite(b).count();
+  const Bitmap a0 = a.offset_range(0, 0, 1 << 20), b0 = b.offset_range(0, 0, 1 << 20);
+  const int64_t want_r = a0.intersection_count(b0), want_ru = a0.unite(b0).count();
+  std::vector<int> bad(nthreads, 0);
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; t++) {
+    ts.emplace_back([&, t] {
+      std::mt19937_64 r(t);
+      Bitmap own;
+      for (int k = 0; k < 200; k++) {
+        if (a.intersection_count(b) != want) bad[t]++;
+        if (a.range_intersection_count(0, b, 0, 1 << 20) != want_r) bad[t]++;
+        if (Bitmap::range_union_count({{&a, 0}, {&b, 0}}, 1 << 20) != want_ru) bad[t]++;
+        if (a.unite(b).count() != want_u) bad[t]++;
+        own.add(r() % (1 << 20));
+        own.remove(r() % (1 << 20));
+        Bitmap o = own.intersect(a);
+        o.optimize();
+      }
+    });
+  }
+  for (auto& th : ts) th.join();
+  int n = 0;
+  for (int x : bad) n += x;
+  std::fprintf(stderr, "threads: %d failures\n", n);
+  return n ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && std::strcmp(argv[2], "threads") == 0) return run_threads(std::atoi(argv[1]));
   const int iters = argc > 1 ? std::atoi(argv[1]) : 60;
   std::mt19937_64 rng(12345);
   for (int it = 0; it < iters; it++) {
@@ -70,6 +112,23 @@ int main(int argc, char** argv) {
     EXPECT(a.unite(b).slice() == to_vec(uni));
     EXPECT(a.difference(b).slice() == to_vec(diff));
     EXPECT(a.xor_(b).slice() == to_vec(x));
+    // in-place row counts over 2^20-wide windows (rows 0 and 1 of a shard)
+    for (uint64_t ra : {0ull, 1ull})
+      for (uint64_t rb : {0ull, 1ull}) {
+        int64_t ic = 0, uc = 0;
+        std::set<uint64_t> u;
+        for (auto v : sa)
+          if (v >> 20 == ra) u.insert(v & ((1 << 20) - 1));
+        for (auto v : sb)
+          if (v >> 20 == rb) {
+            ic += u.count(v & ((1 << 20) - 1));
+          }
+        for (auto v : sb)
+          if (v >> 20 == rb) u.insert(v & ((1 << 20) - 1));
+        uc = int64_t(u.size());
+        EXPECT(a.range_intersection_count(ra << 20, b, rb << 20, 1 << 20) == ic);
+        EXPECT(Bitmap::range_union_count({{&a, ra << 20}, {&b, rb << 20}}, 1 << 20) == uc);
+      }
     // serialisation round trip (pilosa format) and op-log-free reload
     std::string bytes = a.to_bytes();
     Bitmap c;

@@ -28,3 +28,20 @@ def test_roaring_core_asan_ubsan():
     r = subprocess.run([out, "12"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "0 failures" in r.stderr
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+def test_roaring_core_threads_tsan():
+    """Concurrent readers of shared bitmaps + per-thread writers under
+    ThreadSanitizer, with the roaringstats counters compiled in (the host
+    pool runs these ops with the GIL released)."""
+    out = os.path.join(tempfile.mkdtemp(), "roaring_selftest_tsan")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-DPILOSA_ROARING_STATS", "-mpopcnt", "-mbmi2",
+           "-pthread", os.path.join(NATIVE, "selftest", "roaring_selftest.cpp"), os.path.join(NATIVE, "roaring.cpp"),
+           "-o", out]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66")
+    r = subprocess.run([out, "6", "threads"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "threads: 0 failures" in r.stderr
