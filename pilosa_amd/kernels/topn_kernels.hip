@@ -511,6 +511,10 @@ constexpr int HOT_THREADS = 1024;
 #ifndef HOT_VEC_LOADS
 #define HOT_VEC_LOADS 1
 #endif
+// 1 = with HOT_VEC_LOADS, loads run two chunks ahead of the counting
+#ifndef HOT_PF2
+#define HOT_PF2 1
+#endif
 constexpr int HOT_TAB_WORDS = 32768;
 constexpr int HOT_SMALL_N = 255;  // byte counters: at most 255 values per lane-owned container
 
@@ -559,7 +563,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     }
   }
   __syncthreads();
-  auto mask_of = [&](int x) -> uint32_t { return tab[x >> 1] >> ((x & 1) << 4); };
+  // entry x is the u16 half x of the table: one ds_read_u16, no shift/select
+  const uint16_t* tab16 = reinterpret_cast<const uint16_t*>(tab);
+  auto mask_of = [&](int x) -> uint32_t { return tab16[x]; };
   const int32_t* hm = p.hot_meta + (int64_t(s) * 16 + j) * R;
   const int B = min(R, p.hot_split[int64_t(s) * 16 + j]);
 
@@ -613,6 +619,29 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     uint4 cur = make_uint4(0, 0, 0, 0);
     int curv = 0;
     if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur, curv);
+#if HOT_PF2
+    // a load cursor runs two chunks ahead of the count cursor over the same
+    // (row, chunk) sequence: two 16-byte loads per lane stay in flight
+    int lr = r, lbase = 0;
+    int64_t lm = m;
+    uint64_t llive = live;
+    auto adv = [&]() {
+      if (lr < 0) return;
+      if (meta_type(lm) == CT_ARRAY && lbase + 512 < meta_n(lm)) {
+        lbase += 512;
+        return;
+      }
+      lr = llive ? __builtin_ctzll(llive) : -1;
+      llive &= llive - 1;
+      lbase = 0;
+      lm = lr >= 0 ? row_meta(lr) : 0;
+    };
+    adv();
+    uint4 nxt = make_uint4(0, 0, 0, 0);
+    int nxtv = 0;
+    if (lr >= 0 && meta_type(lm) == CT_ARRAY) load_chunk(lm, lbase, nxt, nxtv);
+    adv();
+#endif
 #else
     int cur[8];
 #pragma unroll
@@ -641,7 +670,12 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         bn = 0;
         mn = rn >= 0 ? row_meta(rn) : 0;
       }
-#if HOT_VEC_LOADS
+#if HOT_VEC_LOADS && HOT_PF2
+      uint4 nx2 = make_uint4(0, 0, 0, 0);
+      int nx2v = 0;
+      if (lr >= 0 && meta_type(lm) == CT_ARRAY) load_chunk(lm, lbase, nx2, nx2v);
+      adv();
+#elif HOT_VEC_LOADS
       uint4 nxt = make_uint4(0, 0, 0, 0);
       int nxtv = 0;
       if (rn >= 0 && meta_type(mn) == CT_ARRAY) load_chunk(mn, bn, nxt, nxtv);
@@ -665,10 +699,16 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
           if (cur[t] >= 0) swar_add(c4, mask_of(cur[t]));
 #endif
       } else if (ty == CT_BITMAP) {
+        // all 16 words of the lane issued before the first is counted
         const uint64_t* w = reinterpret_cast<const uint64_t*>(pp);
-        for (int i = lane; i < 1024; i += 64) {
-          for (uint64_t bb = w[i]; bb; bb &= bb - 1) swar_add(c4, mask_of(i * 64 + __builtin_ctzll(bb)));
-          if ((i >> 6) % 3 == 2) flush();  // <= 192 bits per lane between flushes
+        uint64_t wv[16];
+#pragma unroll
+        for (int it = 0; it < 16; it++) wv[it] = w[lane + 64 * it];
+#pragma unroll
+        for (int it = 0; it < 16; it++) {
+          const int i = lane + 64 * it;
+          for (uint64_t bb = wv[it]; bb; bb &= bb - 1) swar_add(c4, mask_of(i * 64 + __builtin_ctzll(bb)));
+          if (it % 3 == 2) flush();  // <= 192 bits per lane between flushes
         }
       } else {
         const int nr = pp[0];
@@ -722,6 +762,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
 #if HOT_VEC_LOADS
       cur = nxt;
       curv = nxtv;
+#if HOT_PF2
+      nxt = nx2;
+      nxtv = nx2v;
+#endif
 #else
 #pragma unroll
       for (int t = 0; t < 8; t++) cur[t] = nxt[t];
