@@ -258,3 +258,57 @@ def test_union_count_kernels(setup, variant):
             assert g == want, (variant, rs)
     finally:
         eng.union_variant = old
+
+
+def _rand_expr(rng, view, depth):
+    """Random boolean tree over rows 0..13 (12, 13 are missing rows)."""
+    from pilosa_amd.ops.device import Leaf, Op
+    if depth == 0 or rng.random() < 0.3:
+        r = int(rng.integers(0, 14))
+        return Leaf(view, r), ("row", r)
+    op = ["and", "or", "xor", "andnot"][int(rng.integers(0, 4))]
+    k = int(rng.integers(2, 4))
+    kids = [_rand_expr(rng, view, depth - 1) for _ in range(k)]
+    return Op(op, tuple(e for e, _ in kids)), (op, [t for _, t in kids])
+
+
+def _host_eval(tree, frag):
+    if tree[0] == "row":
+        return _row(frag, tree[1])
+    vals = [_host_eval(t, frag) for t in tree[1]]
+    out = vals[0]
+    for v in vals[1:]:
+        out = {"and": out.intersect, "or": out.union, "xor": out.xor, "andnot": out.difference}[tree[0]](v)
+    return out
+
+
+def test_differential_fuzz_count_and_materialize(setup):
+    """SURVEY §5.2 differential fuzzing: random expression trees through every
+    count route the planner picks (pair kernel, union kernel, flat fold,
+    generic interpreter) and through materialize, against the host roaring
+    oracle."""
+    from pilosa_amd.ops.device import CompileError
+    frags, view, eng = setup
+    rng = np.random.default_rng(2024)
+    exprs, trees = [], []
+    while len(exprs) < 160:
+        e, t = _rand_expr(rng, view, 3)
+        try:
+            from pilosa_amd.ops.device import compile_expr
+            compile_expr(e, {})
+        except CompileError:
+            continue
+        exprs.append(e)
+        trees.append(t)
+    got = eng.count(exprs)
+    for e, t, g in zip(exprs, trees, got):
+        want = sum(_host_eval(t, f).count() for f in frags if f is not None)
+        assert g == want, t
+    for e, t in list(zip(exprs, trees))[:24]:
+        bms, shards = eng.materialize(e)
+        for f, b in zip(frags, bms):
+            if f is None:
+                continue
+            want_cols = _host_eval(t, f).slice() % (1 << 20)
+            got_cols = b.slice() % (1 << 20) if b is not None else np.array([], np.uint64)
+            np.testing.assert_array_equal(np.sort(got_cols), np.sort(want_cols), err_msg=str(t))
