@@ -36,6 +36,7 @@ import argparse
 import json
 import math
 import os
+import shutil
 import sys
 import time
 
@@ -744,8 +745,25 @@ def main():
     rb = zipf_rows(rng, nq, args.rows)
     queries = [f"Count(Intersect(Row(f={a}), Row(f={b})))" for a, b in zip(ra, rb)]
 
+    fallback = None
+    if args.mode == "disk" and args.data_dir is None:
+        # every rank writes its shard range under TMPDIR: when any rank lacks
+        # the space, all ranks time the synthesised arena instead of failing
+        nshards = math.ceil(args.cols / SHARD_WIDTH)
+        lo, hi = nshards * rank // world, nshards * (rank + 1) // world
+        need = int(36e9 * (hi - lo) / 954 * (args.rows / NROWS))
+        free = shutil.disk_usage(os.environ.get("TMPDIR") or "/tmp").free
+        short = torch.tensor([1 if free < need else 0], dtype=torch.int64, device=dev)
+        if world > 1:
+            all_reduce(short, op=dist.ReduceOp.MAX)
+        if int(short.item()):
+            fallback = (f"--mode disk needs ~{need / 1e9:.1f} GB per rank under TMPDIR, a rank had "
+                        f"{free / 1e9:.1f} GB free: timed the synthesised arena instead")
+            args.mode = "synthetic"
     run = run_disk if args.mode == "disk" else run_synthetic
     elapsed, extra = run(args, world, rank, dev, queries, ra, rb)
+    if fallback:
+        extra["mode_fallback"] = fallback
     torch.cuda.empty_cache()
     if "4" in args.configs.split(","):
         extra["config4_bsi"] = bench_bsi(args, world, rank, dev)
