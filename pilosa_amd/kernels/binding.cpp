@@ -250,7 +250,7 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
   if (R > 0) {
     check_dev(hot_meta, "hot_meta");
     check_dev(hot_cnt, "hot_cnt");
-    TORCH_CHECK(Q <= 16, "hot-rank counting takes at most 16 queries per launch");
+    TORCH_CHECK(Q <= 32, "hot-rank counting takes at most 32 queries per launch");
     TORCH_CHECK(hot_meta.scalar_type() == torch::kInt32 && hot_meta.numel() == S * 16 * R, "hot_meta int32[S*16*R]");
     TORCH_CHECK(hot_cnt.scalar_type() == torch::kInt32 && hot_cnt.numel() == S * Q * R, "hot_cnt int32[S*Q*R]");
     check_dev(hot_split, "hot_split");

@@ -520,17 +520,28 @@ constexpr int HOT_SMALL_N = 255;  // byte counters: at most 255 values per lane-
 
 // SWAR: add the 16 bits of a query mask to 16 byte counters (4 per word):
 // a nibble times 0x00204081 puts its bits at bytes 0..3 without carries.
-__device__ __forceinline__ void swar_add(uint32_t (&c4)[4], uint32_t msk) {
+template <int NQ>
+__device__ __forceinline__ void swar_add(uint32_t (&c4)[NQ / 4], uint32_t msk) {
 #pragma unroll
-  for (int g = 0; g < 4; g++) c4[g] += (((msk >> (4 * g)) & 15u) * 0x00204081u) & 0x01010101u;
+  for (int g = 0; g < NQ / 4; g++) c4[g] += (((msk >> (4 * g)) & 15u) * 0x00204081u) & 0x01010101u;
 }
 
+// NQ = 16: one workgroup per (shard, key j), a u16 query mask per value of
+// the key (64K x 2 B).  NQ = 32 (17..32 queries per launch): one workgroup
+// per (shard, key, half h) with u32 masks for the key's values
+// [h*32768, h*32768 + 32768) -- the same 128 KB of LDS -- so a launch counts
+// twice the queries for the same streamed bytes (the two halves' workgroups
+// are consecutive, on one XCD: the second read of a container hits L2).
+template <int NQ>
 __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) {
   extern __shared__ uint32_t tab[];
   __shared__ int grab[2];
-  // one workgroup per (shard, key j); consecutive blocks share a shard (XCD L2)
+  // one workgroup per (shard, key j[, half]); consecutive blocks share a shard (XCD L2)
   const int unit = int(tn_xcd_remap(blockIdx.x, gridDim.x));
-  const int s = unit >> 4, j = unit & 15;
+  constexpr int HB = NQ == 32 ? 1 : 0;  // half bit
+  const int s = unit >> (4 + HB), j = (unit >> HB) & 15;
+  const int lo = HB ? (unit & 1) * 32768 : 0;
+  constexpr int NLO = HB ? 32768 : 65536;  // values per workgroup
   const int tid = threadIdx.x, lane = tid & 63;
   const int Q = p.Q, R = p.R;
   const int64_t sb = p.v.shard_base[s];
@@ -551,21 +562,30 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     if (n <= ARRAY_MAX) {
       for (int i = tid; i < n; i += HOT_THREADS) {
         const int x = vals[i];
-        atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+        if (HB) {
+          if (unsigned(x - lo) < unsigned(NLO)) atomicOr(&tab[x - lo], 1u << q);
+        } else {
+          atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+        }
       }
     } else {
       const uint64_t* w = reinterpret_cast<const uint64_t*>(vals);
-      for (int i = tid; i < 1024; i += HOT_THREADS)
+      for (int i = tid + (lo >> 6); i < (lo + NLO) >> 6; i += HOT_THREADS)
         for (uint64_t bb = w[i]; bb; bb &= bb - 1) {
           const int x = i * 64 + __builtin_ctzll(bb);
-          atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+          if (HB) atomicOr(&tab[x - lo], 1u << q);
+          else atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
         }
     }
   }
   __syncthreads();
-  // entry x is the u16 half x of the table: one ds_read_u16, no shift/select
+  // NQ 16: entry x is the u16 half x of the table (one ds_read_u16, no
+  // shift/select); NQ 32: u32 entry x - lo, 0 outside the workgroup's half
   const uint16_t* tab16 = reinterpret_cast<const uint16_t*>(tab);
-  auto mask_of = [&](int x) -> uint32_t { return tab16[x]; };
+  auto mask_of = [&](int x) -> uint32_t {
+    if (HB) return unsigned(x - lo) < unsigned(NLO) ? tab[x - lo] : 0u;
+    return tab16[x];
+  };
   const int32_t* hm = p.hot_meta + (int64_t(s) * 16 + j) * R;
   const int B = min(R, p.hot_split[int64_t(s) * 16 + j]);
 
@@ -648,15 +668,17 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     for (int t = 0; t < 8; t++) cur[t] = -1;
     if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur);
 #endif
-    uint32_t c4[4] = {0u, 0u, 0u, 0u};
-    uint32_t acc[16];
+    uint32_t c4[NQ / 4];
 #pragma unroll
-    for (int q = 0; q < 16; q++) acc[q] = 0;
+    for (int g = 0; g < NQ / 4; g++) c4[g] = 0u;
+    uint32_t acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) acc[q] = 0;
     auto flush = [&]() {
 #pragma unroll
-      for (int q = 0; q < 16; q++) acc[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+      for (int q = 0; q < NQ; q++) acc[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
 #pragma unroll
-      for (int g = 0; g < 4; g++) c4[g] = 0;
+      for (int g = 0; g < NQ / 4; g++) c4[g] = 0;
     };
     for (;;) {
       const int ty = meta_type(m);
@@ -692,22 +714,23 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
         for (int t = 0; t < 8; t++)
-          if (t < curv) swar_add(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
+          if (t < curv) swar_add<NQ>(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
 #else
 #pragma unroll
         for (int t = 0; t < 8; t++)
-          if (cur[t] >= 0) swar_add(c4, mask_of(cur[t]));
+          if (cur[t] >= 0) swar_add<NQ>(c4, mask_of(cur[t]));
 #endif
       } else if (ty == CT_BITMAP) {
         // all 16 words of the lane issued before the first is counted
-        const uint64_t* w = reinterpret_cast<const uint64_t*>(pp);
-        uint64_t wv[16];
+        constexpr int NIT = NLO / 4096;  // 64-word rounds of the workgroup's values
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(pp) + (lo >> 6);
+        uint64_t wv[NIT];
 #pragma unroll
-        for (int it = 0; it < 16; it++) wv[it] = w[lane + 64 * it];
+        for (int it = 0; it < NIT; it++) wv[it] = w[lane + 64 * it];
 #pragma unroll
-        for (int it = 0; it < 16; it++) {
-          const int i = lane + 64 * it;
-          for (uint64_t bb = wv[it]; bb; bb &= bb - 1) swar_add(c4, mask_of(i * 64 + __builtin_ctzll(bb)));
+        for (int it = 0; it < NIT; it++) {
+          const int i = (lo >> 6) + lane + 64 * it;
+          for (uint64_t bb = wv[it]; bb; bb &= bb - 1) swar_add<NQ>(c4, mask_of(i * 64 + __builtin_ctzll(bb)));
           if (it % 3 == 2) flush();  // <= 192 bits per lane between flushes
         }
       } else {
@@ -715,9 +738,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         const uint16_t* rr = pp + 8;
         int since = 0;
         for (int t = 0; t < nr; t++) {
-          const int a0 = rr[2 * t], b0 = rr[2 * t + 1];
+          const int a0 = max(int(rr[2 * t]), lo), b0 = min(int(rr[2 * t + 1]), lo + NLO - 1);
           for (int xx = a0 + lane; xx <= b0; xx += 64) {
-            swar_add(c4, mask_of(xx));
+            swar_add<NQ>(c4, mask_of(xx));
             if (++since == 240) {
               flush();
               since = 0;
@@ -727,32 +750,60 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       }
       if (row_end) {
         flush();
-        // transpose-reduce: 16 counters x 64 lanes -> one total per 4 lanes
-        const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
-        uint32_t aa[8], bq[4], c2[2];
+        // transpose-reduce: NQ counters x 64 lanes -> one total per 64/NQ
+        // lanes: each level halves the counters a lane holds and sums the
+        // exchanged half with lane ^ step (query bit = lane bit)
+        uint32_t t16[16], t8[8], t4[4], t2[2];
+        if (NQ == 32) {
+          const bool h5 = lane & 32;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const uint32_t mine = h5 ? acc[8 + i] : acc[i], other = h5 ? acc[i] : acc[8 + i];
-          aa[i] = mine + uint32_t(__shfl_xor(int(other), 32, 64));
-        }
+          for (int i = 0; i < 16; i++) {
+            const uint32_t mine = h5 ? acc[(16 + i) % NQ] : acc[i], other = h5 ? acc[i] : acc[(16 + i) % NQ];
+            t16[i] = mine + uint32_t(__shfl_xor(int(other), 32, 64));
+          }
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const uint32_t mine = h4 ? aa[4 + i] : aa[i], other = h4 ? aa[i] : aa[4 + i];
-          bq[i] = mine + uint32_t(__shfl_xor(int(other), 16, 64));
+          for (int i = 0; i < 16; i++) t16[i] = acc[i];
         }
+        {
+          const int st = NQ == 32 ? 16 : 32;
+          const bool hb = lane & st;
 #pragma unroll
-        for (int i = 0; i < 2; i++) {
-          const uint32_t mine = h3 ? bq[2 + i] : bq[i], other = h3 ? bq[i] : bq[2 + i];
-          c2[i] = mine + uint32_t(__shfl_xor(int(other), 8, 64));
+          for (int i = 0; i < 8; i++) {
+            const uint32_t mine = hb ? t16[8 + i] : t16[i], other = hb ? t16[i] : t16[8 + i];
+            t8[i] = mine + uint32_t(__shfl_xor(int(other), st, 64));
+          }
         }
-        uint32_t d = (h2 ? c2[1] : c2[0]) + uint32_t(__shfl_xor(int(h2 ? c2[0] : c2[1]), 4, 64));
-        d += uint32_t(__shfl_xor(int(d), 2, 64));
+        {
+          const int st = NQ == 32 ? 8 : 16;
+          const bool hb = lane & st;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint32_t mine = hb ? t8[4 + i] : t8[i], other = hb ? t8[i] : t8[4 + i];
+            t4[i] = mine + uint32_t(__shfl_xor(int(other), st, 64));
+          }
+        }
+        {
+          const int st = NQ == 32 ? 4 : 8;
+          const bool hb = lane & st;
+#pragma unroll
+          for (int i = 0; i < 2; i++) {
+            const uint32_t mine = hb ? t4[2 + i] : t4[i], other = hb ? t4[i] : t4[2 + i];
+            t2[i] = mine + uint32_t(__shfl_xor(int(other), st, 64));
+          }
+        }
+        const int st1 = NQ == 32 ? 2 : 4;
+        const bool h1 = lane & st1;
+        uint32_t d = (h1 ? t2[1] : t2[0]) + uint32_t(__shfl_xor(int(h1 ? t2[0] : t2[1]), st1, 64));
+        if (NQ == 16) d += uint32_t(__shfl_xor(int(d), 2, 64));
         d += uint32_t(__shfl_xor(int(d), 1, 64));
-        const int q = (lane >> 2) & 15;
+        // the query of this lane's total: bits (lane >> log2(64/NQ)) in the
+        // order the levels consumed them
+        const int q = NQ == 32 ? (lane >> 1) & 31 : (lane >> 2) & 15;
         const int k = gb + (HOT_THREADS / 64) * r;
-        if ((lane & 3) == 0 && q < Q && d) atomicAdd(out + int64_t(q) * R + k, d);
+        if ((lane & (64 / NQ - 1)) == 0 && q < Q && d) atomicAdd(out + int64_t(q) * R + k, d);
 #pragma unroll
-        for (int qq = 0; qq < 16; qq++) acc[qq] = 0;
+        for (int qq = 0; qq < NQ; qq++) acc[qq] = 0;
         if (rn < 0) break;
         live &= live - 1;
       }
@@ -788,7 +839,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     const int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
     const int nl = cl >= 0 ? meta_n(ml) : 0;
     const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
-    uint32_t c4[4] = {0u, 0u, 0u, 0u};
+    uint32_t c4[NQ / 4];
+#pragma unroll
+    for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
     for (int i = 0; __ballot(i < nl); i += 16) {
       // two 16-byte loads in flight per lane (16 values)
       uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
@@ -797,10 +850,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
       for (int t = 0; t < 16; t++)
-        if (i + t < nl) swar_add(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
+        if (i + t < nl) swar_add<NQ>(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
     }
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
+    for (int q = 0; q < NQ; q++) {
       const uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
       if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
     }
@@ -904,9 +957,15 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
     // hot-rank count matrix (before mode 1/2 of the same batch)
     if (a.R <= 0) return;
     const int tab = HOT_TAB_WORDS * 4;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, tab);
-    hipLaunchKernelGGL(topn_hot_kernel, dim3(unsigned(a.S) * 16u), dim3(HOT_THREADS), tab, st, a);
+    if (a.Q > 16) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<32>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
+      hipLaunchKernelGGL(topn_hot_kernel<32>, dim3(unsigned(a.S) * 32u), dim3(HOT_THREADS), tab, st, a);
+    } else {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
+      hipLaunchKernelGGL(topn_hot_kernel<16>, dim3(unsigned(a.S) * 16u), dim3(HOT_THREADS), tab, st, a);
+    }
   } else if (mode == 3) {
     hipLaunchKernelGGL(topn_gather_kernel, dim3(unsigned(units)), dim3(256), 0, st, a);
   } else if (mode == 1) {

@@ -33,8 +33,13 @@ LDS_LIMIT = 160 * 1024 - 1024
 # cache ranks counted row-major for the whole batch (topn_hot_kernel); the
 # slot index / histogram cover the ranks after them
 HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "2048"))
-# queries per hot-rank launch (u16 query masks in the LDS table)
-HOT_Q = 16
+# queries per hot-rank launch: up to 16 take topn_hot_kernel<16> (u16 query
+# masks of a whole key in LDS), 17..32 topn_hot_kernel<32> (u32 masks of half
+# a key per workgroup: twice the queries for the same streamed bytes).  The
+# kernel is VALU-bound on the SWAR mask adds, so the 32-query launch measured
+# 30.6 ms against 2 x 9.2 ms for two 16-query launches
+# (profiles/r02_topn/topn_kbench_b32.log): 16 stays the default.
+HOT_Q = int(os.environ.get("PILOSA_TOPN_HOT_Q", "16"))
 MAX_SLOTS = 65535
 # phase-1 histograms are kept for the ids= gather up to this many bytes per batch
 HIST_KEEP_BYTES = 8 << 30
@@ -180,13 +185,13 @@ class DeviceTopNIndex:
 
     def hot_counts(self, src, Q: int):
         """int32[S, Q, R]: src counts of the hot cache ranks (one row-major
-        pass per 16 queries), or None without hot ranks."""
+        pass per HOT_Q queries), or None without hot ranks."""
         import torch
 
         if not self.R or not Q or not self.S:
             return None
         if Q > HOT_Q:
-            raise ValueError("hot_counts: at most 16 queries per call")
+            raise ValueError(f"hot_counts: at most {HOT_Q} queries per call")
         dev = self.view.device
         hot = torch.zeros(self.S * Q * self.R, dtype=torch.int32, device=dev)
         z = torch.zeros(Q, dtype=torch.int32, device=dev)

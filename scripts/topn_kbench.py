@@ -42,7 +42,7 @@ def main():
     out = {"shards": S, "index_build_s": round(time.perf_counter() - t0, 2), "H32": idx.H32, "H16": idx.H16,
            "lds_bytes": idx.lds, "hot_ranks": idx.R, "slot_entries": idx.entries, "classes": {}}
     B = args.batch
-    for name, rows in (("hot 0-15", range(0, 16)), ("warm 100-115", range(100, 116)),
+    for name, rows in ((f"hot 0-{B - 1}", range(0, B)), (f"warm 100-{99 + B}", range(100, 100 + B)),
                        ("cold 900-915", range(900, 900 + B))):
         srcs = [Leaf(view, r) for r in list(rows)[:B]]
         src = eng.materialize_batch(srcs, idx.S)

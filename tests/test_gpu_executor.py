@@ -324,6 +324,38 @@ def test_slot_index_topn_matches_replay(envs, k, hot):
                 assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in want], (q, n)
 
 
+@pytest.mark.parametrize("hot", [None, 64])
+def test_slot_index_topn_32_query_launch(envs, hot):
+    """17..32 srcs per launch take topn_hot_kernel<32> (u32 masks of half a
+    key per workgroup): its hot counts equal two 16-query launches', and the
+    TopN answers equal the exact replay."""
+    import torch
+
+    from pilosa_amd.ops.topn import DeviceRankCache, topn_batch
+    from pilosa_amd.ops.topn_index import DeviceTopNIndex
+    from pilosa_amd.pql import parse_string
+    cpu, gpu = envs
+    shards = cpu.holder.index("i").available_shards()
+    hv = gpu.view_arena("i", "h", "standard", shards)
+    cache = DeviceRankCache.from_view(hv, k=5000)
+    idx = DeviceTopNIndex(hv, cache, hot=hot)
+    cases = ["Row(f=2)", "Row(f=3)", "Row(g=1)", "Row(f=0)", "Row(h=0)", "Intersect(Row(f=0), Row(g=2))",
+             "Union(Row(f=20), Row(f=1))", "Row(h=1)", "Row(h=2)", "Row(g=0)"] * 3
+    srcs = [gpu.plan("i", parse_string(q).calls[0], shards) for q in cases]
+    assert 16 < len(srcs) <= 32
+    src = idx.materialize(gpu.engine, srcs)
+    h32 = idx.hot_counts(src, len(srcs)).view(idx.S, len(srcs), idx.R)
+    for lo, hi in ((0, 16), (16, len(srcs))):
+        sub = idx.materialize(gpu.engine, srcs[lo:hi])
+        h16 = idx.hot_counts(sub, hi - lo).view(idx.S, hi - lo, idx.R)
+        assert torch.equal(h32[:, lo:hi], h16), (lo, hi)
+    for n, th in ((5, 1), (100, 1), (20, 40)):
+        got = idx.topn(gpu.engine, srcs, [n] * len(srcs), [th] * len(srcs))
+        want = topn_batch(gpu.engine, hv, cache, srcs, n=n, threshold=th)
+        for q, g, w in zip(cases, got, want):
+            assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in w], (q, n, th)
+
+
 def test_concurrent_counts_coalesce_on_gpu(envs):
     """Independent concurrent Count() requests share GPU launches
     (ops/coalescer.py) and each gets exactly its host result."""
