@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_executor.py -x -q -k "topn or TopN" --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_gpu_topn.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_topn.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu_topn.log
-for B in 32 16; do
+for B in ${BATCHES:-32 16}; do
   timeout -k 10 300 python -u scripts/topn_kbench.py --cols 1000000000 --batch $B > gpurun_out/topn_kbench_b$B.log 2>&1 || { tail -20 gpurun_out/topn_kbench_b$B.log; exit 1; }
   tail -1 gpurun_out/topn_kbench_b$B.log
 done

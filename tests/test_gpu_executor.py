@@ -325,13 +325,15 @@ def test_slot_index_topn_matches_replay(envs, k, hot):
 
 
 @pytest.mark.parametrize("hot", [None, 64])
-def test_slot_index_topn_32_query_launch(envs, hot):
+def test_slot_index_topn_32_query_launch(envs, hot, monkeypatch):
     """17..32 srcs per launch take topn_hot_kernel<32> (u32 masks of half a
     key per workgroup): its hot counts equal two 16-query launches', and the
     TopN answers equal the exact replay."""
     import torch
 
+    from pilosa_amd.ops import topn_index
     from pilosa_amd.ops.topn import DeviceRankCache, topn_batch
+    monkeypatch.setattr(topn_index, "HOT_Q", 32)
     from pilosa_amd.ops.topn_index import DeviceTopNIndex
     from pilosa_amd.pql import parse_string
     cpu, gpu = envs
