@@ -35,8 +35,10 @@ LDS_LIMIT = 160 * 1024 - 1024
 HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "2048"))
 # queries per hot-rank launch: up to 16 take topn_hot_kernel<16> (u16 query
 # masks of a whole key in LDS), 17..32 topn_hot_kernel<32> (u32 masks of half
-# a key per workgroup: twice the queries for the same streamed bytes).  The
-# kernel is VALU-bound on the SWAR mask adds, so the 32-query launch measured
+# a key per workgroup: twice the queries for the same streamed bytes).  Both
+# half-key workgroups still walk every value of a container (per-value work,
+# not bytes, bounds this kernel: carry-save mask counting instead of the SWAR
+# adds changed nothing, 9.44 vs 9.16 ms), so the 32-query launch measured
 # 30.6 ms against 2 x 9.2 ms for two 16-query launches
 # (profiles/r02_topn/topn_kbench_b32.log): 16 stays the default.
 HOT_Q = int(os.environ.get("PILOSA_TOPN_HOT_Q", "16"))
