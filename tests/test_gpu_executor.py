@@ -358,6 +358,27 @@ def test_slot_index_topn_32_query_launch(envs, hot, monkeypatch):
             assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in w], (q, n, th)
 
 
+def test_topn_nosrc_matches_cache_replay(envs):
+    """Ranked-cache TopN(field, n) batches on the device (sorted unique
+    candidate keys, device ids= re-count, device finish) == the per-query
+    host replay of the same device rank caches, mixed n and thresholds."""
+    from pilosa_amd.ops.topn import DeviceRankCache, finish_topn, topn_cache_phase1, topn_cache_phase2_counts
+    from pilosa_amd.ops.topn_index import DeviceTopNIndex
+    cpu, gpu = envs
+    shards = cpu.holder.index("i").available_shards()
+    hv = gpu.view_arena("i", "h", "standard", shards)
+    for k in (5000, 7):
+        cache = DeviceRankCache.from_view(hv, k=k, keep_row_counts=True)
+        idx = DeviceTopNIndex(hv, cache)
+        ns = [5, 100, 0, 1, 20, 3000]
+        ths = [1, 1, 1, 1, 40, 2]
+        got = idx.topn_nosrc(cache.row_counts, ns, ths)
+        for n, th, g in zip(ns, ths, got):
+            ids = sorted(topn_cache_phase1(cache, n, th))
+            want = finish_topn(ids, topn_cache_phase2_counts(cache, hv, ids, th), n)
+            assert [(p.id, p.count) for p in g] == [(p.id, p.count) for p in want], (k, n, th)
+
+
 def test_concurrent_counts_coalesce_on_gpu(envs):
     """Independent concurrent Count() requests share GPU launches
     (ops/coalescer.py) and each gets exactly its host result."""
