@@ -219,6 +219,14 @@ void leaf_src(torch::Tensor view, torch::Tensor rows, int64_t S, torch::Tensor c
   check_launch("leaf_src");
 }
 
+void keymask_build(torch::Tensor view, int64_t S, torch::Tensor out) {
+  check_dev(out, "keymask");
+  const pk::ViewDev v = viewdev_from(view);
+  TORCH_CHECK(out.scalar_type() == torch::kInt16 && out.numel() == S * v.D, "keymask int16[S*D]");
+  pk::launch_keymask_build(v, int(S), reinterpret_cast<uint16_t*>(out.data_ptr<int16_t>()), cur_stream(out));
+  check_launch("keymask_build");
+}
+
 void topn_hot_meta(torch::Tensor view, int64_t S, int64_t K, int64_t R, torch::Tensor cache_dense,
                    torch::Tensor hot_meta, torch::Tensor hot_split) {
   check_dev(cache_dense, "cache_dense");
@@ -481,6 +489,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_range_count", &bsi_range_count, "Count(Row(v <op> x)): fused BSI predicate + count");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("leaf_src", &leaf_src, "src containers of plain rows straight from the arena (TopN srcs)");
+  m.def("keymask_build", &keymask_build, "key-presence mask of every (shard, row) of a view");
   m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");

@@ -36,7 +36,8 @@ struct ViewDev {
   const int64_t* meta;         // [C]
   const uint16_t* payload;     // [P]
   int64_t D;
-  int64_t pad[3];
+  const uint16_t* keymask;     // [S][D] key-presence mask per (shard, row); nullptr = derive from meta
+  int64_t pad[2];
 };
 static_assert(sizeof(ViewDev) == 64, "ViewDev layout");
 
@@ -117,6 +118,7 @@ void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
 // rows; *has_run set when a run container needs materialising.
 void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_t* counts, int64_t* offs,
                      int32_t* has_run, hipStream_t st);
+void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st);
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st);
 

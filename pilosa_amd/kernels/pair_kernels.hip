@@ -83,8 +83,11 @@ __device__ __forceinline__ uint32_t row_keys(const ViewDev& v, int s, int64_t d,
   lo = 0;
   if (d < 0) return 0;
   const auto rp = gp(v.rowptr + int64_t(s) * (v.D + 1));
-  const uint32_t r0 = rp[d], r1 = rp[d + 1];
+  const uint32_t r0 = rp[d];
   lo = gp(v.shard_base)[s] + r0;
+  // the view's mask table: one 2-byte load instead of the row's metas
+  if (v.keymask) return gp(v.keymask)[int64_t(s) * v.D + d];
+  const uint32_t r1 = rp[d + 1];
   const int n = int(r1 - r0);
   if (n == 16) return 0xffffu;
   uint32_t pres = 0;
@@ -92,6 +95,20 @@ __device__ __forceinline__ uint32_t row_keys(const ViewDev& v, int s, int64_t d,
   for (int k = 0; k < 16; k++)
     if (k < n) pres |= 1u << meta_j(gp(v.meta)[lo + k]);
   return pres;
+}
+
+// keymask[s][d] = row_keys() of every (shard, dense row): built once per view
+// generation (DeviceView.ensure_keymask), it turns pair_build's up-to-16
+// scattered meta loads per row into one 2-byte load (1.4 ms of a 4096-query
+// Count(Intersect) batch on the headline index was pair_build).
+__global__ __launch_bounds__(256) void keymask_build_kernel(ViewDev v, int S, uint16_t* __restrict__ out) {
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= int64_t(S) * v.D) return;
+  const int s = int(t / v.D);
+  const int64_t d = t - int64_t(s) * v.D;
+  v.keymask = nullptr;
+  int64_t lo;
+  out[t] = uint16_t(row_keys(v, s, d, lo));
 }
 
 __global__ __launch_bounds__(256) void pair_build_kernel(const QueryProg* __restrict__ progs, int Q,
@@ -1190,6 +1207,12 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
   if (lane < nq) partial[u * Q + q0 + lane] = mine;
 }
 }  // namespace
+
+void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st) {
+  const int64_t n = int64_t(S) * v.D;
+  if (n == 0) return;
+  hipLaunchKernelGGL(keymask_build_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, v, S, out);
+}
 
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
                        int cq, int variant, hipStream_t st) {

@@ -42,7 +42,7 @@ _OPS = {"and": OP_AND, "or": OP_OR, "xor": OP_XOR, "andnot": OP_ANDNOT}
 QPROG_DTYPE = np.dtype([("nleaf", "<i4"), ("nprog", "<i4"), ("leaf_view", "<i4", (MAXLEAF,)),
                         ("leaf_row", "<i8", (MAXLEAF,)), ("prog", "u1", (MAXPROG,)), ("pad", "<i8", (3,))])
 VIEWDEV_DTYPE = np.dtype([("rowptr", "<u8"), ("shard_base", "<u8"), ("meta", "<u8"), ("payload", "<u8"),
-                          ("D", "<i8"), ("pad", "<i8", (3,))])
+                          ("D", "<i8"), ("keymask", "<u8"), ("pad", "<i8", (2,))])
 assert QPROG_DTYPE.itemsize == 256 and VIEWDEV_DTYPE.itemsize == 64
 
 _ext = None
@@ -822,7 +822,45 @@ class DeviceView:
         rec["meta"] = self.t_meta.data_ptr()
         rec["payload"] = self.t_payload.data_ptr()
         rec["D"] = self.D
+        km = getattr(self, "_keymask", None)
+        if km is not None and km[0] == self.generation:
+            rec["keymask"] = km[1].data_ptr()
         return rec
+
+    KEYMASK_MIN_INTERVAL_S = 5.0
+
+    def ensure_keymask(self) -> bool:
+        """Build the [S][D] key-presence mask table the pair kernels read
+        instead of each row's metas (pair_kernels.hip keymask_build_kernel).
+        It is tied to the view generation; after writes it is rebuilt at most
+        every KEYMASK_MIN_INTERVAL_S seconds, and a stale table is simply not
+        passed (the kernels then read metas).  Returns whether it is fresh."""
+        import time
+
+        import torch
+
+        if os.environ.get("PILOSA_KEYMASK", "1") == "0" or self.device.type != "cuda":
+            return False
+        km = getattr(self, "_keymask", None)
+        if km is not None and km[0] == self.generation:
+            return True
+        now = time.monotonic()
+        if km is not None and now - km[2] < self.KEYMASK_MIN_INTERVAL_S:
+            return False
+        n = self.S * self.D
+        if n == 0:
+            return False
+        out = km[1] if km is not None and km[1].numel() == n else torch.empty(n, dtype=torch.int16,
+                                                                               device=self.device)
+        rec = np.zeros((), dtype=VIEWDEV_DTYPE)
+        rec["rowptr"] = self.t_rowptr.data_ptr()
+        rec["shard_base"] = self.t_shard_base.data_ptr()
+        rec["meta"] = self.t_meta.data_ptr()
+        rec["payload"] = self.t_payload.data_ptr()
+        rec["D"] = self.D
+        kernels().keymask_build(torch.from_numpy(np.frombuffer(rec.tobytes(), dtype=np.uint8).copy()), self.S, out)
+        self._keymask = (self.generation, out, now)
+        return True
 
 
 # ---------------------------------------------------------------- engine
@@ -958,6 +996,8 @@ class GpuEngine:
         if is_and2.any():
             progs = self._hot_leaf_first(progs, is_and2)
             lr = progs["leaf_row"]
+            for v in views:
+                v.ensure_keymask()
         varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
         for i, v in enumerate(views):
             varr[i] = v.viewdev()
@@ -985,6 +1025,9 @@ class GpuEngine:
         torch = self.torch
         if not S or not Q:
             return (Q, S, None, [])
+        if any(int(kind) == KIND_AND2 for kind, _, _, _ in segs):
+            for v in views:
+                v.ensure_keymask()
         varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
         for i, v in enumerate(views):
             varr[i] = v.viewdev()

@@ -324,23 +324,19 @@ class DeviceTopNIndex:
         nmax = self.K if any(int(n) == 0 for n in ns) else min(self.K, max(int(n) for n in ns))
         lim = torch.tensor([int(n) if int(n) else self.K for n in ns], dtype=torch.int64).to(dev)
         mt = torch.tensor([max(1, int(t)) for t in thresholds], dtype=torch.int32).to(dev)
-        # candidates: every id some shard's first n cache entries (at or above
-        # the threshold) hold -- the set the phase-1 sums would make nonzero --
-        # as sorted unique (query, id) keys of those <= Q x S x n entries, not a
-        # dense [Q x row-space] accumulator scanned for nonzeros
-        A = max(self.A, 1)
+        # phase 1 as a dense [Q x row-space] scatter-add of the taken cache
+        # entries, candidates = its nonzeros.  (Sorted unique (query, id) keys
+        # of the <= Q x S x n taken entries instead measured 1.74-1.76 ms per
+        # 16-query batch against 1.52-1.64 ms for this, profiles/r02_final/.)
+        acc = torch.zeros((Q, max(self.A, 1)), dtype=torch.int32, device=dev)
         if self.S and self.A and nmax:
             cnt = self.cache_cnt[:, :nmax]                                       # [S, n]
             k = torch.arange(nmax, device=dev)
             take = (k[None, None, :] < lim[:, None, None]) & (cnt[None] >= mt[:, None, None])
-            keys = (torch.arange(Q, device=dev, dtype=torch.int64)[:, None, None] * A
-                    + self.cache_acc[:, :nmax].to(torch.int64)[None])
-            keys = torch.unique(keys[take])
-        else:
-            keys = torch.zeros(0, dtype=torch.int64, device=dev)
-        if comm is not None:
-            keys = comm.union(keys)
-        pq, pa = (keys // A).contiguous(), (keys % A).contiguous()
+            vals = torch.where(take, cnt[None], torch.zeros((), dtype=torch.int32, device=dev))
+            idx = self.cache_acc[:, :nmax].reshape(1, -1).expand(Q, -1).to(torch.int64)
+            acc.scatter_add_(1, idx, vals.reshape(Q, -1))
+        pq, pa = self._candidates(acc, comm)
         out = torch.zeros(pa.numel(), dtype=torch.int64, device=dev)
         if pa.numel() and self.S:
             d = self.a2dense[pa].to(torch.int64)
