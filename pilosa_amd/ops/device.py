@@ -850,6 +850,16 @@ class DeviceView:
         n = self.S * self.D
         if n == 0:
             return False
+        if km is None or km[1].numel() != n:
+            # HBM guard: the table (2 B per (shard, row)) is skipped for views
+            # whose row directory is large next to their containers, or when
+            # it would not leave the device comfortably free
+            need = 2 * n
+            if need > max(256 << 20, self.nbytes() // 4):
+                return False
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if need * 4 > free:
+                return False
         out = km[1] if km is not None and km[1].numel() == n else torch.empty(n, dtype=torch.int16,
                                                                                device=self.device)
         rec = np.zeros((), dtype=VIEWDEV_DTYPE)
