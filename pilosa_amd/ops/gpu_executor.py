@@ -536,9 +536,79 @@ class GpuExecutor:
         self.launches += 1
         return eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S)).cpu().tolist()
 
+    TIME_GROUP_MIN = 2
+
+    def _count_time_rows(self, index: str, calls: List[Call], shards: List[int]) -> Dict[int, int]:
+        """Count(Row(t=r, from=, to=)) calls of a batch that share (field,
+        from, to): one union program per call built vectorised
+        (GpuEngine.union_programs over the covering views' dense rows) and
+        one launch per group, instead of a Leaf/Op tree and compile_expr per
+        call.  Returns {call index: count}; calls it does not take (other
+        shapes, small groups, > 16 covering views) are left to the caller."""
+        from .device import MAXLEAF
+        idx = self.holder.index(index)
+        if idx is None:
+            return {}
+        groups: Dict[Tuple, List[Tuple[int, int]]] = {}
+        for i, c in enumerate(calls):
+            if len(c.children) != 1:
+                continue
+            ch = c.children[0]
+            if ch.name != "Row" or ch.children or ch.has_condition_arg() or "from" not in ch.args and "to" not in ch.args:
+                continue
+            try:
+                fname = ch.field_arg()
+                rid, ok = ch.uint_arg(fname)
+            except ValueError:
+                continue
+            if not ok or idx.field(fname) is None:
+                continue
+            groups.setdefault((fname, str(ch.args.get("from")), str(ch.args.get("to"))), []).append((i, rid, ch))
+        out: Dict[int, int] = {}
+        for (fname, _, _), members in groups.items():
+            if len(members) < self.TIME_GROUP_MIN:
+                continue
+            try:
+                vnames = self._ex().time_views(idx.field(fname), members[0][2])
+            except Exception:  # noqa: BLE001 - malformed times: the general path reports them
+                continue
+            if vnames is None:
+                continue
+            dvs = [dv for dv in (self.view_arena(index, fname, v, shards) for v in vnames) if dv is not None]
+            if not dvs:
+                for i, _, _ in members:
+                    out[i] = 0
+                continue
+            if len(dvs) > MAXLEAF or len({dv.S for dv in dvs}) != 1:
+                continue
+            rows = np.array([rid for _, rid, _ in members], dtype=np.uint64)
+            progs = GpuEngine.union_programs(np.stack([dv.dense_many(rows) for dv in dvs], axis=1))
+            self.launches += 1
+            got = self.engine.launch_count(self.engine.prepare_progs(progs, dvs, dvs[0].S)).cpu().tolist()
+            for (i, _, _), v in zip(members, got):
+                out[i] = int(v)
+        return out
+
     def try_count_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
         """Many Count() calls of one request -> one launch; calls whose tree
-        does not fit the kernel limits are counted on the host."""
+        does not fit the kernel limits are counted on the host.  Time-range
+        Row counts sharing a range take the vectorised union path first."""
+        done = self._count_time_rows(index, calls, shards) if len(calls) >= self.TIME_GROUP_MIN else {}
+        if not done:
+            return self._try_count_batch_plain(index, calls, shards)
+        rest = [i for i in range(len(calls)) if i not in done]
+        out = [0] * len(calls)
+        for i, v in done.items():
+            out[i] = v
+        if rest:
+            got = self._try_count_batch_plain(index, [calls[i] for i in rest], shards)
+            if got is None:
+                return None
+            for i, v in zip(rest, got):
+                out[i] = v
+        return out
+
+    def _try_count_batch_plain(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[int]]:
         from .device import compile_expr
         if len(calls) >= self.NATIVE_BATCH_MIN:
             got = self._count_batch_native(index, calls, shards)

@@ -600,3 +600,46 @@ def test_bsi_sum_matrix_matches_per_filter_kernel(envs, mode):
     for q, s, n in list(zip(qs, s1.cpu().tolist(), n1.cpu().tolist()))[:8]:
         want = cpu.q1("i", f"Sum({q}, field=n)" if q else "Sum(field=n)")
         assert (want.val, want.count) == (s + n * base, n), q
+
+
+def test_time_range_count_batches_match_host():
+    """Count(Row(t=r, from=, to=)) calls sharing a range go through the
+    vectorised union programs (GpuExecutor._count_time_rows, one launch per
+    range group) and equal the host executor; mixed with other calls and
+    ranges covering no view."""
+    import datetime as dt
+
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    env = Env()
+    try:
+        env.create_index("i")
+        env.field("i", "t", type="time", time_quantum="YMDH")
+        env.field("i", "f")
+        rng = np.random.default_rng(5)
+        t = env.holder.index("i").field("t")
+        rows, cs, ts = [], [], []
+        for r in range(40):
+            k = int(rng.integers(1, 3000))
+            cc = rng.choice(3 * SW, size=k, replace=False)
+            rows += [r] * k
+            cs += cc.tolist()
+            ts += [dt.datetime(2021, 1 + int(x % 3), 1 + int(x % 28), int(x % 24)) for x in cc]
+        t.import_bits(np.array(rows, np.uint64), np.array(cs, np.uint64), timestamps=ts)
+        env.holder.index("i").field("f").import_bits(np.zeros(100, np.uint64), np.arange(100, dtype=np.uint64))
+        ranges = [("2021-01-03T05:00", "2021-02-11T13:00"), ("2021-01-01T00:00", "2021-04-01T00:00"),
+                  ("2021-02-27T22:00", "2021-03-02T02:00"), ("2019-01-01T00:00", "2019-02-01T00:00")]
+        q = " ".join(f"Count(Row(t={r}, from={a}, to={b}))" for a, b in ranges for r in list(range(0, 44, 3)))
+        q += " Count(Row(f=0)) Count(Row(t=7, from=2021-01-05T00:00, to=2021-01-06T00:00))"
+        want = env.q("i", q)
+        gpu = GpuExecutor(env.holder, "cuda:0", executor=env.executor)
+        env.executor.gpu = gpu
+        try:
+            n0 = gpu.launches
+            got = env.q("i", q)
+            assert gpu.launches > n0
+        finally:
+            env.executor.gpu = None
+        assert got == want
+        assert sum(want) > 0
+    finally:
+        env.close()
