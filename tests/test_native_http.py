@@ -25,7 +25,9 @@ def _server(native: bool):
 
 
 def _raw(port, data: bytes) -> bytes:
-    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    # generous: right after a load phase the server may still be draining the
+    # load generator's backlog on a busy (xdist) machine
+    s = socket.create_connection(("127.0.0.1", port), timeout=60)
     s.sendall(data)
     out = b""
     while True:
