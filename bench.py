@@ -722,7 +722,7 @@ def main():
     ap.add_argument("--data-dir", default=None, help="disk mode: reuse/keep fragment files under this dir")
     ap.add_argument("--keep-data", action="store_true")
     ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")
-    ap.add_argument("--topn-batches", type=int, default=3,
+    ap.add_argument("--topn-batches", type=int, default=10,
                     help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
