@@ -79,6 +79,29 @@ def mutation_epoch() -> int:
     return _EPOCH[0]
 
 
+def remove_stale_snapshots(dirpath: str, names: Iterable[str]) -> int:
+    """Snapshot temp files (``<shard>.<pid>.<tid>.snapshotting``, or the old
+    fixed ``<shard>.snapshotting``) left by a process that died mid-snapshot
+    are never renamed: View.open drops them.  Files of this process may
+    belong to a snapshot still running and are kept."""
+    me = str(os.getpid())
+    n = 0
+    for nm in names:
+        if not nm.endswith(".snapshotting"):
+            continue
+        parts = nm[:-len(".snapshotting")].split(".")
+        if not parts[0].isdigit() or not all(p.isdigit() for p in parts) or len(parts) not in (1, 3):
+            continue
+        if len(parts) == 3 and parts[1] == me:
+            continue
+        try:
+            os.unlink(os.path.join(dirpath, nm))
+            n += 1
+        except OSError:
+            pass
+    return n
+
+
 class Fragment:
     def __init__(self, path: str, index: str, field: str, view: str, shard: int,
                  cache_type: str = CACHE_TYPE_RANKED, cache_size: int = DEFAULT_CACHE_SIZE,

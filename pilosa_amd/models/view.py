@@ -11,7 +11,7 @@ import shutil
 import threading
 from typing import Callable, Dict, List, Optional
 
-from pilosa_amd.models.fragment import SHARD_WIDTH_EXP, Fragment
+from pilosa_amd.models.fragment import SHARD_WIDTH_EXP, Fragment, remove_stale_snapshots
 from pilosa_amd.models.row import Row
 
 VIEW_STANDARD = "standard"
@@ -54,7 +54,9 @@ class View:
     def open(self):
         with self.mu:
             os.makedirs(self.fragments_path(), exist_ok=True)
-            for name in os.listdir(self.fragments_path()):
+            names = os.listdir(self.fragments_path())
+            remove_stale_snapshots(self.fragments_path(), names)
+            for name in names:
                 if not name.isdigit():
                     continue
                 shard = int(name)

@@ -81,6 +81,10 @@ struct Conn : std::enable_shared_from_this<Conn> {
   bool want_out = false;  // EPOLLOUT armed
   bool peer_eof = false;  // the client shut its side: answer what is queued, read no more
   bool sent_continue = false;
+  // HTTP/1.1 pipelining: a connection's requests execute one at a time, in
+  // order (as Go's net/http serves a connection); later ones wait here
+  bool busy = false;
+  std::deque<std::shared_ptr<Req>> waiting;
 };
 
 // epoll interest of a connection (conn lock held)
@@ -419,13 +423,34 @@ class Server {
       pending_.erase(it);
     }
     responses_++;
-    auto& c = r->conn;
+    auto c = r->conn;
     std::lock_guard<std::mutex> g(c->mu);
-    if (c->closed) return;
+    if (c->closed) {
+      std::lock_guard<std::mutex> pg(pmu_);
+      for (auto& w : c->waiting) pending_.erase(w->id);
+      c->waiting.clear();
+      c->busy = false;
+      return;
+    }
     c->ready.emplace(r->seq, std::make_pair(make_response(status, ctype, body.data(), body.size(), r->close_after),
                                             r->close_after));
     drain_ready(*c);
     flush(*c);
+    if (!c->waiting.empty()) {
+      auto nx = std::move(c->waiting.front());
+      c->waiting.pop_front();
+      enqueue(nx);
+    } else {
+      c->busy = false;
+    }
+  }
+
+  void enqueue(const std::shared_ptr<Req>& r) {
+    {
+      std::lock_guard<std::mutex> g(qmu_);
+      q_[r->kind].push_back(r);
+    }
+    qcv_.notify_all();
   }
 
   // move in-order ready responses into the output buffer (conn lock held)
@@ -598,7 +623,7 @@ class Server {
       bool keep = version == "HTTP/1.1";
       bool chunked = false, expect100 = false;
       size_t clen = 0;
-      bool has_len = false;
+      bool has_len = false, bad_len = false;
       std::string ctype, accept;
       for (size_t p = le + 2; p < he;) {
         size_t e = c.in.find("\r\n", p);
@@ -607,8 +632,11 @@ class Server {
         if (colon != std::string::npos && colon < e) {
           std::string k = c.in.substr(p, colon - p), v = trim(c.in.substr(colon + 1, e - colon - 1));
           if (ieq(k, "content-length")) {
+            bool digits = !v.empty() && v.size() <= 18;
+            for (char ch : v) digits = digits && ch >= '0' && ch <= '9';
+            if (!digits || (has_len && clen != size_t(strtoull(v.c_str(), nullptr, 10)))) bad_len = true;
             has_len = true;
-            clen = size_t(strtoull(v.c_str(), nullptr, 10));
+            clen = digits ? size_t(strtoull(v.c_str(), nullptr, 10)) : 0;
           } else if (ieq(k, "transfer-encoding")) {
             chunked = v.find("chunked") != std::string::npos;
           } else if (ieq(k, "connection")) {
@@ -625,17 +653,37 @@ class Server {
         }
         p = e + 2;
       }
+      // a malformed Content-Length, or both framings at once (request smuggling)
+      if (bad_len || (chunked && has_len)) {
+        native_reply(c, c.next_seq++, 400, "bad request framing\n", true);
+        ok = false;
+        break;
+      }
       // body
       size_t end = he + 4;
       if (chunked) {
         std::string body;
         size_t p = end;
-        bool complete = false, bad = false;
+        bool complete = false, bad = false, malformed = false;
         for (;;) {
           const size_t e = c.in.find("\r\n", p);
           if (e == std::string::npos) break;
-          const size_t sz = size_t(strtoull(c.in.substr(p, e - p).c_str(), nullptr, 16));
-          if (body.size() + sz > max_body_) {
+          // chunk-size line: 1..15 hex digits, optional ";ext"
+          size_t sz = 0, nd = 0, q = p;
+          for (; q < e && nd < 16; q++, nd++) {
+            const int ch = static_cast<unsigned char>(c.in[q]);
+            int v;
+            if (ch >= '0' && ch <= '9') v = ch - '0';
+            else if (ch >= 'a' && ch <= 'f') v = ch - 'a' + 10;
+            else if (ch >= 'A' && ch <= 'F') v = ch - 'A' + 10;
+            else break;
+            sz = (sz << 4) | size_t(v);
+          }
+          if (nd == 0 || nd > 15 || (q < e && c.in[q] != ';' && c.in[q] != ' ' && c.in[q] != '\t')) {
+            malformed = true;
+            break;
+          }
+          if (sz > max_body_ || body.size() > max_body_ - sz) {
             bad = true;
             break;
           }
@@ -653,9 +701,18 @@ class Server {
             }
             break;
           }
-          if (c.in.size() < e + 2 + sz + 2) break;
+          if (c.in.size() - (e + 2) < sz + 2) break;
+          if (c.in.compare(e + 2 + sz, 2, "\r\n") != 0) {
+            malformed = true;
+            break;
+          }
           body.append(c.in, e + 2, sz);
-          p = e + 2 + sz + 2;
+          p = e + 2 + sz + 2;   // strictly increases (sz + 4 >= 4 bytes per chunk)
+        }
+        if (malformed) {
+          native_reply(c, c.next_seq++, 400, "malformed chunked body\n", true);
+          ok = false;
+          break;
         }
         if (bad) {
           native_reply(c, c.next_seq++, 413, "request body too large\n", true);
@@ -706,11 +763,12 @@ class Server {
         std::lock_guard<std::mutex> g(pmu_);
         pending_.emplace(r->id, r);
       }
-      {
-        std::lock_guard<std::mutex> g(qmu_);
-        q_[r->kind].push_back(r);
+      if (c.busy) {
+        c.waiting.push_back(r);   // runs once the earlier requests are answered
+      } else {
+        c.busy = true;
+        enqueue(r);
       }
-      qcv_.notify_all();
       if (r->close_after) {
         c.closing = true;  // answer what we have, read nothing more
         break;

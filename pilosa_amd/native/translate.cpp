@@ -165,6 +165,7 @@ class Store {
   // tail is truncated away).
   int64_t open() {
     std::unique_lock<std::shared_mutex> g(mu_);
+    closed_ = false;
     if (!path_.empty()) {
       fd_ = ::open(path_.c_str(), O_RDWR | O_CREAT | O_APPEND | O_CLOEXEC, 0666);
       if (fd_ < 0) throw std::runtime_error("open " + path_ + ": " + strerror(errno));
@@ -191,6 +192,12 @@ class Store {
     map_len_ = 0;
     if (fd_ >= 0) ::close(fd_);
     fd_ = -1;
+    // a closed store answers nothing: callers racing a close()/reopen get an
+    // error instead of reading key offsets through an unmapped log
+    idx_.clear();
+    size_ = 0;
+    mem_.clear();
+    closed_ = true;
   }
 
   int64_t size() {
@@ -208,6 +215,7 @@ class Store {
     bool missing = false;
     {
       std::shared_lock<std::shared_mutex> g(mu_);
+      check_open();
       const KeyIndex* ki = find_index(type, index, field);
       for (size_t i = 0; i < keys.size(); i++) {
         ids[i] = ki ? lookup(*ki, keys[i]) : 0;
@@ -216,6 +224,7 @@ class Store {
     }
     if (!missing || !create || read_only_) return ids;
     std::unique_lock<std::shared_mutex> g(mu_);
+    check_open();
     KeyIndex& ki = index_for(type, index, field);
     std::unordered_map<std::string, uint64_t> fresh;
     std::vector<size_t> new_pos;
@@ -260,6 +269,7 @@ class Store {
   std::vector<std::string> keys_of(uint8_t type, const std::string& index, const std::string& field,
                                    const std::vector<uint64_t>& ids) {
     std::shared_lock<std::shared_mutex> g(mu_);
+    check_open();
     std::vector<std::string> out(ids.size());
     const KeyIndex* ki = find_index(type, index, field);
     if (!ki) return out;
@@ -285,6 +295,7 @@ class Store {
     }
     if (!used) return 0;
     std::unique_lock<std::shared_mutex> g(mu_);
+    check_open();
     const size_t at = size_;
     append(chunk.substr(0, used));
     replay(at, size_);
@@ -295,6 +306,7 @@ class Store {
     std::string out;
     {
       std::shared_lock<std::shared_mutex> g(mu_);
+      check_open();
       if (offset < 0) offset = 0;
       if (size_t(offset) < size_) out.assign(reinterpret_cast<const char*>(data()) + offset, size_ - size_t(offset));
     }
@@ -311,6 +323,7 @@ class Store {
   // the inspect command).
   py::list entries(int64_t offset) {
     std::shared_lock<std::shared_mutex> g(mu_);
+    check_open();
     py::list out;
     size_t at = size_t(std::max<int64_t>(offset, 0));
     const uint8_t* d = data();
@@ -334,6 +347,10 @@ class Store {
   }
 
  private:
+  void check_open() const {
+    if (closed_) throw std::runtime_error("translate store " + path_ + " is closed");
+  }
+
   const uint8_t* data() const {
     return path_.empty() ? reinterpret_cast<const uint8_t*>(mem_.data()) : reinterpret_cast<const uint8_t*>(map_);
   }
@@ -518,6 +535,7 @@ class Store {
   size_t map_len_ = 0;
   size_t size_ = 0;
   std::string mem_;
+  bool closed_ = false;
   std::unordered_map<std::string, KeyIndex> idx_;
   mutable std::shared_mutex mu_;
 };

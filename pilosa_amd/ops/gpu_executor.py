@@ -125,7 +125,15 @@ class GpuExecutor:
                 # only some shards changed: rewrite their segments in place
                 dv = hit[1]
                 ok = True
-                pending = {}   # si -> write batches replayed on the device after the loop
+                # Ordered write batches are replayed on the device FIRST (K11/K12, all
+                # shards in shared launches; only the batches cross PCIe), THEN rows and
+                # container keys that only the storage can describe (ClearRow, Store,
+                # mutex/bool vectors, ...) are rebuilt from the current storage.  A batch
+                # recorded before such a row change is therefore overwritten by the row's
+                # current state instead of being re-applied on top of it.
+                pending = {}   # si -> write batches for the device
+                rebuild = {}   # si -> (rows, container keys) rebuilt from the storage afterwards
+                whole = []     # shards whose change is unknown: full segment rewrite
                 for si, (old, new, f) in enumerate(zip(hit[0], sig, frags)):
                     if old == new:
                         continue
@@ -134,38 +142,40 @@ class GpuExecutor:
                         break
                     with f.mu:
                         dirty = f.take_dirty(dv.token) if old is not None and old[0] == id(f) else None
-                        if dirty is not None:
-                            rows, keys, deltas = dirty
-                            ok = True
-                            if deltas and self.device_writes_on and dv.device.type == "cuda":
-                                # writes replayed on the device (K11/K12), all shards in shared launches;
-                                # only the batches cross PCIe.  Rows rebuilt below from the current
-                                # storage may see the batches again: set/clear replays are idempotent
-                                pending[si] = deltas
-                            elif deltas:
-                                keys = set(keys) | _delta_keys(deltas)
-                            if ok and (rows or keys):
-                                ok = dv.update_rows(si, rows, f.storage, keys=keys)
-                                self.row_updates += ok
-                        else:
-                            ok = False
-                        if not ok:
-                            f.take_dirty(dv.token)
-                            pending.pop(si, None)
-                            ok = dv.update_shard(si, f.storage)
-                    if not ok:
-                        break
-                    self.shard_updates += 1
+                    if dirty is None:
+                        whole.append(si)
+                        continue
+                    rows, keys, deltas = dirty
+                    if deltas and self.device_writes_on and dv.device.type == "cuda":
+                        pending[si] = deltas
+                    elif deltas:
+                        keys = set(keys) | _delta_keys(deltas)
+                    rebuild[si] = (rows, keys)
                 if ok and pending:
                     failed = dv.apply_deltas_multi(pending)
                     self.device_writes += len(pending) - len(failed)
-                    for si in sorted(failed):   # rebuild what the device could not take from the host
+                    for si in failed:   # the host rebuilds what the device could not take
+                        rows, keys = rebuild[si]
+                        rebuild[si] = (rows, set(keys) | _delta_keys(pending[si]))
+                for si in sorted(rebuild) if ok else ():
+                    rows, keys = rebuild[si]
+                    if rows or keys:
                         f = frags[si]
                         with f.mu:
-                            ok = dv.update_rows(si, set(), f.storage, keys=_delta_keys(pending[si])) or \
-                                dv.update_shard(si, f.storage)
-                        if not ok:
-                            break
+                            good = dv.update_rows(si, rows, f.storage, keys=keys)
+                        self.row_updates += good
+                        if not good:
+                            whole.append(si)
+                            continue
+                    self.shard_updates += 1
+                for si in sorted(set(whole)) if ok else ():
+                    f = frags[si]
+                    with f.mu:
+                        f.take_dirty(dv.token)
+                        ok = dv.update_shard(si, f.storage)
+                    if not ok:
+                        break
+                    self.shard_updates += 1
                 if ok:
                     self._arenas[key] = (sig, dv)
                     return dv

@@ -797,3 +797,20 @@ def test_background_and_inline_snapshots_do_not_deadlock(frags, monkeypatch):
     g = frags.reopen(f)
     assert cols(g.row(1)) == [] and cols(g.row(2)) == list(range(50))
     assert not [n for n in os.listdir(os.path.dirname(f.path)) if n.endswith(".snapshotting")]
+
+
+def test_view_open_drops_stale_snapshot_files(tmp_path):
+    """Snapshot temp files of a process that died mid-snapshot are removed
+    when the view opens; other files are kept (ADVICE r02 fragment.py:310)."""
+    import os as _os
+
+    from pilosa_amd.models.fragment import remove_stale_snapshots
+    d = tmp_path / "fragments"
+    d.mkdir()
+    names = ["3", "3.cache", "3.99999999.12.snapshotting", "3.snapshotting",
+             f"3.{_os.getpid()}.7.snapshotting", "notes.snapshotting"]
+    for nm in names:
+        (d / nm).write_bytes(b"x")
+    assert remove_stale_snapshots(str(d), _os.listdir(d)) == 2
+    assert sorted(_os.listdir(d)) == sorted(["3", "3.cache", f"3.{_os.getpid()}.7.snapshotting",
+                                             "notes.snapshotting"])

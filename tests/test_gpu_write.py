@@ -134,6 +134,45 @@ def test_executor_writes_merge_on_device():
         env.close()
 
 
+def test_row_rebuilds_after_recorded_batches():
+    """Set -> ClearRow and Set -> Store between two device reads: the recorded
+    position batches are replayed BEFORE the storage-described row rebuilds,
+    so the device never re-applies a set on top of the cleared/stored row
+    (gpu_executor refresh order)."""
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    shards = [0, 1]
+    env = Env(gpu=lambda h: GpuExecutor(h, "cuda:0"))
+    try:
+        env.create_index("i")
+        env.field("i", "g")
+        f = env.holder.index("i").field("g")
+        rng = np.random.default_rng(5)
+        for r in range(4):
+            c = rng.choice(2 * SW, 5000, replace=False).astype(np.uint64)
+            f.import_bits(np.full(len(c), r, np.uint64), c)
+        g = env.executor.gpu
+        g.executor = env.executor
+        env.executor.strict_gpu = True
+        assert env.q("i", "Count(Row(g=1))")[0] > 0
+
+        def host_count(r):
+            return sum(int(env.holder.fragment("i", "g", "standard", s).storage.count_range(r * SW, (r + 1) * SW))
+                       for s in shards)
+        env.q("i", f"Set({SW + 17}, g=1)")
+        env.q("i", "ClearRow(g=1)")
+        assert env.q("i", "Count(Row(g=1))")[0] == host_count(1) == 0
+        env.q("i", f"Set({SW + 99}, g=2)")
+        env.q("i", f"Set(5, g=3)")
+        env.q("i", "Store(Row(g=0), g=2)")
+        assert env.q("i", "Count(Row(g=2))")[0] == host_count(2) == host_count(0)
+        assert env.q("i", "Count(Row(g=3))")[0] == host_count(3)
+        env.q("i", f"Set(7, g=1)")
+        assert env.q("i", "Count(Row(g=1))")[0] == host_count(1) == 1
+        assert g.rebuilds == 1
+    finally:
+        env.close()
+
+
 def test_compaction_on_device(view):
     dv, host, rng = view
     for k in range(6):

@@ -214,3 +214,51 @@ def test_concurrent_generic_requests():
         assert json.loads(rs[0][1]) == {"results": [160]}
     finally:
         srv.close()
+
+
+def test_chunk_size_and_framing_attacks_rejected():
+    """Chunk sizes are hex digits only and bounded before any arithmetic; a
+    request carrying both Content-Length and Transfer-Encoding, or a
+    non-numeric Content-Length, is refused (ADVICE r02 httpd.cpp:637)."""
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        head = b"POST /index/i/query HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+        for body in (b"ffffffffffffff9c\r\nCount(Row(f=1))\r\n0\r\n\r\n",   # wraps size_t arithmetic
+                     b"zz\r\nabc\r\n0\r\n\r\n",                              # not hex
+                     b"\r\nabc\r\n0\r\n\r\n",                                # empty size line
+                     b"3\r\nabcXY0\r\n\r\n"):                                # chunk not CRLF-terminated
+            rs = _responses(_raw(port, head + body))
+            assert rs and rs[0][0] in (400, 413), (body, rs)
+        rs = _responses(_raw(port, b"POST /index/i/query HTTP/1.1\r\nHost: x\r\nContent-Length: 3\r\n"
+                                   b"Transfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n"))
+        assert rs[0][0] == 400
+        rs = _responses(_raw(port, b"POST /index/i/query HTTP/1.1\r\nHost: x\r\nContent-Length: 1x\r\n\r\nx"))
+        assert rs[0][0] == 400
+        # the server still answers normally afterwards
+        assert _responses(_raw(port, _req("GET", "/version", close=True)))[0][0] == 200
+    finally:
+        srv.close()
+
+
+def test_pipelined_requests_run_in_order():
+    """A pipelined Set followed by Count/Row on one keep-alive connection sees
+    the write: a connection's requests execute one at a time, in order, even
+    though Count-only requests go to the batcher (ADVICE r02 httpd.cpp:709)."""
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        _raw(port, _req("POST", "/index/i", close=True))
+        _raw(port, _req("POST", "/index/i/field/f", close=True))
+        stream = b""
+        for k in range(40):
+            stream += _req("POST", "/index/i/query", f"Set({k}, f=3)".encode())
+            stream += _req("POST", "/index/i/query", b"Count(Row(f=3))")
+        stream += _req("POST", "/index/i/query", b"Row(f=3)", close=True)
+        rs = _responses(_raw(port, stream))
+        assert len(rs) == 81
+        counts = [json.loads(b)["results"][0] for s, b in rs[1:80:2]]
+        assert counts == list(range(1, 41))
+        assert json.loads(rs[80][1])["results"][0]["columns"] == list(range(40))
+    finally:
+        srv.close()

@@ -215,3 +215,22 @@ def test_in_memory_store():
     assert s.translate_rows_to_uint64("i", "f", ["a", "b"]) == [1, 2]
     assert s.read_from(0) == encode_entry(T_ROW, "i", "f", [1, 2], ["a", "b"])
     s.close()
+
+
+def test_closed_store_raises_instead_of_reading_unmapped_log(tmp_path):
+    """A translate/keys_of racing a close() gets an error, never a read
+    through the unmapped log (ADVICE r02 translate.cpp:187)."""
+    from pilosa_amd import _translate
+    s = _translate.Store(str(tmp_path / "keys"))
+    s.open()
+    ids = s.translate(_translate.T_COLUMN, "i", "", ["a", "b"], True)
+    assert list(ids) == [1, 2]
+    s.close()
+    for call in (lambda: s.translate(_translate.T_COLUMN, "i", "", ["a"], False),
+                 lambda: s.keys_of(_translate.T_COLUMN, "i", "", [1]),
+                 lambda: s.read_from(0), lambda: s.entries(0)):
+        with pytest.raises(RuntimeError):
+            call()
+    s.open()
+    assert list(s.keys_of(_translate.T_COLUMN, "i", "", [1, 2])) == ["a", "b"]
+    s.close()
