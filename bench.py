@@ -59,6 +59,14 @@ def all_reduce(t, op=None):
     return _COMM.all_reduce(t, op)
 
 
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress line on stderr (long GPU runs must keep writing)."""
+    print(f"[bench {time.time() - _T0:7.1f}s r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
 def zipf_rows(rng, n, nrows=NROWS, s=1.6, v=50.0):
     # inverse-CDF sampling of P(k) ~ (v+k)^-s, k in [0, nrows)
     k = np.arange(nrows, dtype=np.float64)
@@ -195,6 +203,141 @@ def bench_topn(args, view, eng, rng, world, rank, dev):
         out["src_paths_agree"] = [[(p.id, p.count) for p in r] for r in res_idx] == \
             [[(p.id, p.count) for p in r] for r in res_pairs]
     return out
+
+
+def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
+    """BASELINE config 3 through the product path: TopN requests go through
+    ``Executor.execute`` on the lazily opened index (PQL text -> device rank
+    caches from the fragments' .cache files + HBM arena -> both TopN phases on
+    the device, ops/topn_exec.py).  ``cache``: TopN(f, n=100); ``src``:
+    TopN(f, Row(f=a), n=100) with a from the 1000 hottest rows; every request
+    carries ``--topn-batch`` calls, ``--clients`` request threads.  With N
+    GPUs every rank runs the same requests over its shard range and the
+    candidates / re-counts merge over RCCL inside the device path (one
+    client thread: collectives in request order).  After the timed runs a
+    sample of (query, shard) phase-1 answers is re-derived by the host
+    ``fragment.top`` (which loads those fragments)."""
+    import resource
+    import threading
+
+    import torch
+    import torch.distributed as dist
+
+    from pilosa_amd.models.fragment import TopOptions
+    from pilosa_amd.pql import parse_string
+
+    n = 100
+    B, nb = args.topn_batch, args.topn_batches
+    clients = max(1, args.clients) if world == 1 else 1
+    if world > 1:
+        gpu.comm = _COMM
+    rng = np.random.default_rng(99)
+    out = {"path": "Executor.execute(PQL TopN text), lazy holder, device rank caches from .cache files",
+           "n": n, "cache_k": args.topn_cache, "batch": B, "clients": clients}
+
+    def timed(texts, first):
+        # warmup request first (builds rank caches / slot index), then nb timed requests
+        done = [None] * len(texts)
+        err = []
+        nxt = [0]
+        lock = threading.Lock()
+
+        def client(lo, hi):
+            while True:
+                with lock:
+                    i = nxt[0]
+                    if i >= hi or err:
+                        return
+                    nxt[0] += 1
+                try:
+                    done[i] = ex.execute("i", texts[i], shards=shards).results
+                except BaseException as e:  # noqa: BLE001
+                    err.append(e)
+                    return
+        t0 = time.perf_counter()
+        done[0] = ex.execute("i", texts[0], shards=shards).results
+        torch.cuda.synchronize(dev)
+        first["first_request_s"] = round(time.perf_counter() - t0, 2)
+        log(f"topn: first request {first['first_request_s']} s")
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        nxt[0] = 1
+        t0 = time.perf_counter()
+        ts = [threading.Thread(target=client, args=(1, len(texts))) for _ in range(clients)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if err:
+            raise err[0]
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        elt = torch.tensor([el], dtype=torch.float64, device=dev)
+        if world > 1:
+            all_reduce(elt, op=dist.ReduceOp.MAX)
+        el = float(elt.item())
+        last = done[-1]
+        first.update({"qps": round(B * (len(texts) - 1) / el, 2), "ms_per_request": round(el / (len(texts) - 1) * 1000, 2),
+                      "sample_top3": [(p.id, p.count) for p in last[0][:3]] if last and last[0] else []})
+        return done
+
+    l0 = gpu.launches
+    log("topn: cache-only requests")
+    cache_q = [" ".join([f"TopN(f, n={n})"] * B)] * (nb + 1)
+    out["cache"] = {}
+    res_cache = timed(cache_q, out["cache"])
+    hot = zipf_rows(rng, B * (nb + 1), 1000)
+    src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
+    src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
+    out["src"] = {}
+    log("topn: src requests")
+    res_src = timed(src_q, out["src"])
+    log("topn: verify")
+    out["device_launches"] = gpu.launches - l0
+    out["batches_declined"] = ex.topn_batch_declined
+    out["host_fallbacks"] = ex.gpu_faults
+    view = holder.view("i", "f", "standard")
+    out["fragments_cold_after_topn"] = sum(f.is_cold() for f in view.all_fragments())
+    out["fragments"] = len(view.all_fragments())
+    out["peak_host_rss_gb_after_topn"] = round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)
+    key = ("i", "f", tuple(shards))
+    rc = gpu._rank_cache_map.get(key, (None, None))[1]
+    tix = gpu._topn_indexes.get(key, (None, None, None))[1]
+    out["rank_cache_k"] = rc.K if rc is not None else 0
+    out["rank_cache_cold_shards"] = rc.cold_shards if rc is not None else 0
+    out["slot_index_bytes"] = tix.nbytes() if tix is not None else 0
+    gpu.comm = None
+    # correctness: per-shard phase-1 answers (device map step over one shard) vs
+    # the host fragment.top on sampled shards (this loads those fragments)
+    if args.verify > 0 and shards:
+        sel = sorted(set(np.linspace(0, len(shards) - 1, min(4, len(shards))).astype(int).tolist()))
+        calls = [parse_string(f"TopN(f, n={n})").calls[0]] + \
+            [parse_string(c).calls[0] for c in src_calls[B:B + 3]]
+        bad = 0
+        for si in sel:
+            s = shards[si]
+            frag = holder.fragment("i", "f", "standard", s)
+            for c in calls:
+                dev_pairs = sorted((p.id, p.count) for p in gpu.topn("i", c, [s]))
+                src = ex.bitmap_call_shard("i", c.children[0], s) if c.children else None
+                host = frag.top(TopOptions(n=n, src=src, min_threshold=1))
+                if dev_pairs != sorted((p.id, p.count) for p in host):
+                    bad += 1
+        # and the fused batch answers equal the two-phase map/reduce on the device
+        agree = [[(p.id, p.count) for p in r] for r in res_src[-1][:2]] == \
+            [[(p.id, p.count) for p in ex._topn("i", parse_string(c).calls[0], shards, _exec_opts())]
+             for c in src_calls[nb * B:nb * B + 2]] if world == 1 else None
+        out["verify"] = {"shards_checked": len(sel), "queries_per_shard": len(calls), "mismatches": bad,
+                         "fused_equals_two_phase": agree, "verified": bad == 0 and agree is not False}
+    return out
+
+
+def _exec_opts():
+    from pilosa_amd.executor import ExecOptions
+    return ExecOptions()
 
 
 def bench_cpu_host(args, ra, rb, nshards, nq=256):
@@ -405,6 +548,193 @@ def bench_time_union(args, world, rank, dev):
     return res
 
 
+TIME_VIEWS = [("standard_20200101", 1.0), ("standard_20200102", 1.0), ("standard_2020010300", 0.25),
+              ("standard_2020010301", 0.25), ("standard_2020010302", 0.25), ("standard_2020010303", 0.25),
+              ("standard_2020010304", 0.25)]
+TIME_RANGE = "from='2020-01-01T00:00', to='2020-01-03T05:00'"
+
+
+def bench_configs_disk(args, world, rank, dev, which):
+    """BASELINE configs 4 and 5 through the product path.  The fields are
+    written as Pilosa fragment files and opened with a lazy ``Holder``; every
+    query is PQL text through ``Executor.execute`` (native loader -> HBM):
+
+    * config 4: int field ``v`` (min -1000, max 1e6, bit depth 20; half the
+      columns hold a value uniform in [-1000, 1e6]) stored in its ``bsig_v``
+      view (exists / sign / magnitude rows, fragment.go:90-93):
+      ``Sum(field=v)``, ``Count(Row(v > x))``, ``Count(Row(v >< [a, b]))``,
+      ``Min/Max(field=v)`` and one request of 32 ``Sum(Row(g=r), field=v)``
+      (the executor batches it onto the bit-plane count matrix, MFMA);
+    * config 5: time field ``t`` (quantum YMDH) whose 2 day views + 5 hour
+      views cover ``from=2020-01-01T00:00 to=2020-01-03T05:00`` (the
+      reference's views_by_time_range, time.go:104-181); requests of 1024
+      ``Count(Row(t=r, from=, to=))``.
+
+    A sample of every answer is re-derived on the host executor over a few
+    shards (``verified``).  With N GPUs each rank serves its shard range and
+    the per-request answers are summed over the ranks (RCCL)."""
+    import resource
+    import tempfile
+
+    import torch
+    import torch.distributed as dist
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.field import FieldOptions
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+
+    nshards = math.ceil(args.cols / SHARD_WIDTH)
+    lo, hi = nshards * rank // world, nshards * (rank + 1) // world
+    shards = list(range(lo, hi))
+    own = args.data_dir is None
+    base = tempfile.mkdtemp(prefix=f"pilosa_cfg_r{rank}_", dir=os.environ.get("TMPDIR") or "/tmp") if own \
+        else os.path.join(args.data_dir, f"cfg_rank{rank}of{world}")
+    res = {}
+    try:
+        tag = f"{args.cols}:{args.rows}:{lo}:{hi}:{which}:v1"
+        marker = os.path.join(base, ".bench_data")
+        t0 = time.perf_counter()
+        if not (os.path.exists(marker) and open(marker).read() == tag):
+            shutil.rmtree(base, ignore_errors=True)
+            os.makedirs(base, exist_ok=True)
+            h = Holder(base).open()
+            idx = h.create_index("c", track_existence=False)
+            if "4" in which:
+                fv = idx.create_field("v", FieldOptions(type="int", min=-1000, max=1_000_000))
+                fv.options.bit_depth = 20
+                fv.bsi.bit_depth = 20
+                fv.save_meta()
+                idx.create_field("g", FieldOptions(cache_type="none"))
+            if "5" in which:
+                idx.create_field("t", FieldOptions(type="time", time_quantum="YMDH"))
+            h.close()
+
+            def frag_dir(field, view):
+                d = os.path.join(base, "c", field, "views", view, "fragments")
+                os.makedirs(d, exist_ok=True)
+                return d
+            if "4" in which:
+                _roaring.write_bsi_fragments(frag_dir("v", "bsig_v"), lo, hi, args.cols, 20, 0.5, -1000, 1_000_000,
+                                             7, args.threads)
+                _roaring.write_zipf_fragments(frag_dir("g", "standard"), lo, hi, args.cols, 1000, 1.0, 1.6, 50.0, 11,
+                                              args.threads, cache_size=0)
+            if "5" in which:
+                for k, (vname, bpc) in enumerate(TIME_VIEWS):
+                    _roaring.write_zipf_fragments(frag_dir("t", vname), lo, hi, args.cols, args.rows, bpc, 1.6, 50.0,
+                                                  100 + k, args.threads, cache_size=0)
+            with open(marker, "w") as fh:
+                fh.write(tag)
+        write_s = time.perf_counter() - t0
+        log(f"configs {which}: data ready ({write_s:.1f} s)")
+        holder = Holder(base, lazy_fragments=True).open()
+        gpu = GpuExecutor(holder, dev)
+        ex = Executor(holder, gpu=gpu)
+        gpu.executor = ex
+        ex.strict_gpu = True
+        rng = np.random.default_rng(5)
+
+        def reduce_vals(vals):
+            t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=dev)
+            if world > 1:
+                all_reduce(t)
+            return t.cpu().tolist()
+
+        def flat(r):
+            out = []
+            for x in r:
+                if hasattr(x, "val"):
+                    out += [x.val, x.count]
+                else:
+                    out.append(int(x))
+            return out
+
+        def run(texts, reps):
+            # first request loads the views (cold load timed separately), then reps timed requests
+            t0 = time.perf_counter()
+            first = ex.execute("c", texts[0], shards=shards).results
+            torch.cuda.synchronize(dev)
+            load = time.perf_counter() - t0
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            last = None
+            for k in range(reps):
+                last = reduce_vals(flat(ex.execute("c", texts[1 + k % (len(texts) - 1)], shards=shards).results))
+            torch.cuda.synchronize(dev)
+            el = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+            if world > 1:
+                all_reduce(el, op=dist.ReduceOp.MAX)
+            return float(el.item()), load, last, first
+
+        def verify(texts):
+            # host executor over a few shards (loads those fragments) vs the device on the same shards
+            sel = [shards[i] for i in sorted(set(np.linspace(0, len(shards) - 1, min(3, len(shards))).astype(int)))]
+            bad = 0
+            for q in texts:
+                d = flat(ex.execute("c", q, shards=sel).results)
+                ex.gpu = None
+                try:
+                    hst = flat(ex.execute("c", q, shards=sel).results)
+                finally:
+                    ex.gpu = gpu
+                bad += int(d != hst)
+            return {"shards": len(sel), "requests": len(texts), "mismatches": bad, "verified": bad == 0}
+
+        reps = args.config_reps
+        if "4" in which:
+            r4 = {"config": "BSI int field v (bsig_v fragment files, depth 20, fill 0.5, values [-1000, 1e6]), "
+                            "1B cols, lazy Holder + Executor.execute", "queries": {}}
+            l0 = gpu.launches
+            qs = {"Sum(field=v)": ["Sum(field=v)"] * 2,
+                  "Count(Row(v > x))": [f"Count(Row(v > {int(x)}))" for x in rng.integers(0, 1_000_000, 8)],
+                  "Count(Row(v >< [a,b]))": [f"Count(Row(v >< [{int(a)}, {int(a) + 50000}]))"
+                                             for a in rng.integers(0, 900_000, 8)],
+                  "Min(field=v)": ["Min(field=v)"] * 2, "Max(field=v)": ["Max(field=v)"] * 2}
+            frows = [[int(r) for r in rng.integers(0, 200, 32)] for _ in range(4)]
+            qs["Sum(Row(g=r), field=v) x32 per request"] = [" ".join(f"Sum(Row(g={r}), field=v)" for r in rows)
+                                                            for rows in frows]
+            for name, texts in qs.items():
+                log(f"config 4: {name}")
+                dt_, load, last, first = run(texts, reps)
+                n_calls = texts[0].count("(field") if "x32" in name else 1
+                r4["queries"][name] = {"ms_per_request": round(dt_ * 1000, 3), "qps": round(n_calls / dt_, 1),
+                                       "first_request_s": round(load, 2), "sample": last[:4]}
+            r4["device_launches"] = gpu.launches - l0
+            r4["verify"] = verify(["Sum(field=v)", qs["Count(Row(v > x))"][0], qs["Count(Row(v >< [a,b]))"][0],
+                                   "Min(field=v)", "Max(field=v)", qs["Sum(Row(g=r), field=v) x32 per request"][0]])
+            r4["fragments_cold"] = sum(f.is_cold() for f in holder.view("c", "v", "bsig_v").all_fragments())
+            res["config4_bsi"] = r4
+        if "5" in which:
+            B = 1024
+            calls5 = [[f"Count(Row(t={int(r)}, {TIME_RANGE}))" for r in zipf_rows(rng, B, args.rows)]
+                      for _ in range(4)]
+            texts = [" ".join(c) for c in calls5]
+            l0 = gpu.launches
+            log("config 5: time-range counts")
+            dt_, load, last, first = run(texts, reps)
+            res["config5_time_union"] = {
+                "config": "time field t (quantum YMDH), Count(Row(t=r, from, to)) over 2 day + 5 hour views "
+                          "(fragment files), 1M rows x 1B cols, lazy Holder + Executor.execute",
+                "covering_views": [v for v, _ in TIME_VIEWS], "batch": B, "ms_per_request": round(dt_ * 1000, 2),
+                "qps": round(B / dt_, 1), "first_request_s": round(load, 2), "sample_sum": int(sum(last)),
+                "device_launches": gpu.launches - l0,
+                "hbm_bytes_per_gpu": sum(dv.nbytes() for _, dv in gpu._arenas.values()),
+                "verify": verify([" ".join(calls5[1][:64])])}
+        res["data"] = {"write_s": round(write_s, 2), "dir_bytes": _dir_bytes(base),
+                       "peak_host_rss_gb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)}
+        holder.close()
+        ex.close()
+        del gpu
+        torch.cuda.empty_cache()
+        return res
+    finally:
+        if own and not args.keep_data:
+            shutil.rmtree(base, ignore_errors=True)
+
+
 def host_pair_counts(bitmaps, pairs):
     """Host roaring oracle: counts[q, k] = |Row(a_q) & Row(b_q)| in shard k."""
     w = SHARD_WIDTH
@@ -590,11 +920,12 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
         else os.path.join(args.data_dir, f"rank{rank}of{world}")
     extra = {"path": "Holder(lazy) + file loader -> HBM, Executor.execute(PQL text) per request", "data_dir": base}
     try:
-        tag = f"{args.cols}:{args.rows}:{lo}:{hi}:zipf1.6/50:8:seed1"
+        tag = f"{args.cols}:{args.rows}:{lo}:{hi}:zipf1.6/50:8:seed1:cache{args.topn_cache}"
         marker = os.path.join(base, ".bench_data")
         fdir = os.path.join(base, "i", "f", "views", "standard", "fragments")
         t0 = time.perf_counter()
         if not (os.path.exists(marker) and open(marker).read() == tag):
+            log("writing fragment files")
             shutil.rmtree(base, ignore_errors=True)
             os.makedirs(base, exist_ok=True)
             need = int(36e9 * (hi - lo) / 954 * (args.rows / NROWS))
@@ -607,13 +938,15 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
             h.index("i").create_field("f", FieldOptions())
             h.close()
             os.makedirs(fdir, exist_ok=True)
-            w = _roaring.write_zipf_fragments(fdir, lo, hi, args.cols, args.rows, 8.0, 1.6, 50.0, 1, args.threads)
+            w = _roaring.write_zipf_fragments(fdir, lo, hi, args.cols, args.rows, 8.0, 1.6, 50.0, 1, args.threads,
+                                              cache_size=args.topn_cache)
             with open(marker, "w") as fh:
                 fh.write(tag)
             extra["write"] = {"files": int(w["shards"]), "bytes": int(w["bytes"]), "containers": int(w["containers"]),
                               "s": round(time.perf_counter() - t0, 2)}
         else:
             extra["write"] = {"reused": True, "bytes": _dir_bytes(fdir)}
+        log("opening holder + loading the view into HBM")
         t1 = time.perf_counter()
         holder = Holder(base, lazy_fragments=True).open()
         t2 = time.perf_counter()
@@ -675,6 +1008,7 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
                 raise err[0]
 
         n0 = gpu.launches
+        log("count: warmup")
         run(0, args.warmup)
         assert gpu.launches > n0, "requests did not reach the device"
         if world > 1:
@@ -699,8 +1033,9 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
                 with open(os.path.join(fdir, str(shards[si])), "rb") as fh:
                     return _roaring.Bitmap.from_bytes(fh.read())
             extra["verify"] = verify_sample(gpu.engine, view, host_bitmap, pairs, last[:n], world, dev)
+        log("count: done")
         if args.topn_batches > 0:
-            extra["topn"] = bench_topn(args, view, gpu.engine, np.random.default_rng(99), world, rank, dev)
+            extra["topn"] = bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev)
         holder.close()
         return elapsed, extra
     finally:
@@ -765,10 +1100,14 @@ def main():
     if fallback:
         extra["mode_fallback"] = fallback
     torch.cuda.empty_cache()
-    if "4" in args.configs.split(","):
-        extra["config4_bsi"] = bench_bsi(args, world, rank, dev)
-    if "5" in args.configs.split(","):
-        extra["config5_time_union"] = bench_time_union(args, world, rank, dev)
+    which = [c for c in args.configs.split(",") if c in ("4", "5")]
+    if which and args.mode == "disk":
+        extra.update(bench_configs_disk(args, world, rank, dev, "".join(which)))
+    else:
+        if "4" in which:
+            extra["config4_bsi"] = bench_bsi(args, world, rank, dev)
+        if "5" in which:
+            extra["config5_time_union"] = bench_time_union(args, world, rank, dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         all_reduce(el, op=dist.ReduceOp.MAX)

@@ -218,6 +218,8 @@ class Executor:
         self.cluster = cluster
         self.client = client
         self.gpu = gpu            # GpuExecutor or None
+        if gpu is not None and getattr(gpu, "executor", False) is None:
+            gpu.executor = self   # plans need the executor's BSI/time/TopN helpers
         self.mesh = None          # parallel.mesh.ShardMesh on a multi-GPU node (rank 0 front end)
         # concurrent single-Count requests share GPU launches (ops/coalescer.py)
         self.coalesce = os.environ.get("PILOSA_COALESCE", "1") != "0"
@@ -230,6 +232,8 @@ class Executor:
         self.strict_gpu = False
         self.logger = None
         self._coalescer = None
+        self._topn_coalescer = None
+        self.topn_batch_declined = 0
         self.max_writes = max_writes
         self.stats = stats
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, workers), thread_name_prefix="shard")
@@ -339,6 +343,36 @@ class Executor:
                 if not mesh.failed_over:
                     raise  # a rank reported an error: the query's error
                 # a rank is gone: this process adopted its shards, answer locally
+        # many Sum() calls over one BSI field: one batched device launch
+        # (bit-plane matrix on the matrix cores from 32 filters up)
+        if self.gpu is not None and len(q.calls) > 1 and all(c.name == "Sum" for c in q.calls) and \
+                not opt.remote and not self._use_mesh(opt) and not self._has_remote(index, shards, opt):
+            try:
+                res = self.gpu.bsi_sum_batch(index, q.calls, shards)
+            except PilosaError:
+                raise
+            except Exception as err:  # noqa: BLE001 - device fault: host path below
+                self._gpu_fault(err)
+                res = None
+            if res is not None:
+                if self.stats is not None:
+                    self.stats.count_with_tags("Sum", len(res), [f"index:{index}"])
+                return res
+        # TopN requests on a local GPU: both phases of every call on the device
+        # (ops/topn_exec.py); concurrent single-TopN requests share launches
+        if self.gpu is not None and q.calls and all(c.name == "TopN" for c in q.calls) and not opt.remote and \
+                not self._use_mesh(opt) and not self._has_remote(index, shards, opt):
+            for c in q.calls:
+                self._validate_call_args(c)
+            if any("ids" in c.args for c in q.calls):
+                return [self.execute_call(index, c, shards, opt) for c in q.calls]   # phase 2 only: map step
+            if len(q.calls) == 1 and self.coalesce:
+                c = q.calls[0]
+                key = (index, tuple(shards))
+                return [self.topn_coalescer.submit(key, c, lambda: self.execute_call(index, c, shards, opt))]
+            res = self._run_topn_batch((index, tuple(shards)), q.calls)
+            if res is not None:
+                return res
         if self.gpu is not None and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \
                 not self._has_remote(index, shards, opt):
             try:
@@ -358,6 +392,35 @@ class Executor:
             from pilosa_amd.ops.coalescer import CountCoalescer
             self._coalescer = CountCoalescer(self._run_count_batch)
         return self._coalescer
+
+    @property
+    def topn_coalescer(self):
+        if self._topn_coalescer is None:
+            from pilosa_amd.ops.coalescer import CountCoalescer
+            self._topn_coalescer = CountCoalescer(self._run_topn_batch, max_batch=256)
+        return self._topn_coalescer
+
+    def _run_topn_batch(self, key, calls):
+        index, shards = key
+        if self.gpu is None:
+            return None
+        try:
+            res = self.gpu.topn_batch(index, list(calls), list(shards))
+            if res is None:
+                self.topn_batch_declined += 1
+        except PilosaError:
+            raise
+        except Exception as err:  # noqa: BLE001 - counted; each call then runs alone
+            self._gpu_fault(err)
+            return None
+        if res is not None and self.stats is not None:
+            self.stats.count_with_tags("TopN", len(res), [f"index:{index}"])
+        if res is not None and self.paranoia:
+            for c, r in zip(calls, res):
+                want = self._topn(index, c, list(shards), ExecOptions())
+                if [(p.id, p.count) for p in r] != [(p.id, p.count) for p in want]:
+                    raise AssertionError(f"paranoia: device TopN {r!r} != host TopN {want!r}")
+        return res
 
     def _run_count_batch(self, key, calls):
         index, shards, mesh = key

@@ -219,6 +219,29 @@ void leaf_src(torch::Tensor view, torch::Tensor rows, int64_t S, torch::Tensor c
   check_launch("leaf_src");
 }
 
+void row_counts(torch::Tensor view, torch::Tensor shard_of, torch::Tensor dense, torch::Tensor out) {
+  for (auto* t : {&shard_of, &dense, &out}) check_dev(*t, "row_counts");
+  const int64_t N = dense.numel();
+  TORCH_CHECK(shard_of.scalar_type() == torch::kInt32 && shard_of.numel() == N, "shard_of int32[N]");
+  TORCH_CHECK(dense.scalar_type() == torch::kInt32, "dense int32[N]");
+  TORCH_CHECK(out.scalar_type() == torch::kInt32 && out.numel() == N, "out int32[N]");
+  pk::launch_row_counts(viewdev_from(view), shard_of.data_ptr<int32_t>(), dense.data_ptr<int32_t>(), N,
+                        out.data_ptr<int32_t>(), cur_stream(dense));
+  check_launch("row_counts");
+}
+
+void row_counts_sum(torch::Tensor view, int64_t S, torch::Tensor dense, torch::Tensor threshold, torch::Tensor out) {
+  for (auto* t : {&dense, &threshold, &out}) check_dev(*t, "row_counts_sum");
+  const int64_t P = dense.numel();
+  TORCH_CHECK(dense.scalar_type() == torch::kInt32, "dense int32[P]");
+  TORCH_CHECK(threshold.scalar_type() == torch::kInt32 && threshold.numel() == P, "threshold int32[P]");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() == P, "out int64[P]");
+  TORCH_CHECK(P < (int64_t(1) << 31), "too many ids");
+  pk::launch_row_counts_sum(viewdev_from(view), int(S), dense.data_ptr<int32_t>(), threshold.data_ptr<int32_t>(),
+                            int(P), reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream(dense));
+  check_launch("row_counts_sum");
+}
+
 void keymask_build(torch::Tensor view, int64_t S, torch::Tensor out) {
   check_dev(out, "keymask");
   const pk::ViewDev v = viewdev_from(view);
@@ -489,6 +512,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_range_count", &bsi_range_count, "Count(Row(v <op> x)): fused BSI predicate + count");
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("leaf_src", &leaf_src, "src containers of plain rows straight from the arena (TopN srcs)");
+  m.def("row_counts", &row_counts, "row counts of (shard, dense row) entries (device rank caches)");
+  m.def("row_counts_sum", &row_counts_sum, "ids= re-count without src: per id the sum of shard row counts >= threshold");
   m.def("keymask_build", &keymask_build, "key-presence mask of every (shard, row) of a view");
   m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");

@@ -119,6 +119,12 @@ void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
 void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_t* counts, int64_t* offs,
                      int32_t* has_run, hipStream_t st);
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st);
+// Row counts of (shard, dense row) entries -> out[N] (device rank caches).
+void launch_row_counts(const ViewDev& v, const int32_t* shard_of, const int32_t* dense, int64_t N, int32_t* out,
+                       hipStream_t st);
+// out[p] = sum over shards of row dense[p]'s count where >= threshold[p] (ids= re-count, no src).
+void launch_row_counts_sum(const ViewDev& v, int S, const int32_t* dense, const int32_t* threshold, int P,
+                           unsigned long long* out, hipStream_t st);
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st);
 

@@ -905,6 +905,51 @@ __global__ __launch_bounds__(256) void leaf_src_kernel(ViewDev v, const int64_t*
   }
 }
 
+
+// Row cardinality of dense row d in local shard s: the metadata counts of its
+// (at most 16) containers, no payload read (fragment.go:459 CountRange).
+__device__ __forceinline__ int32_t row_card(const ViewDev& v, int s, int64_t d) {
+  if (d < 0 || d >= v.D) return 0;
+  const uint32_t* rp = v.rowptr + int64_t(s) * (v.D + 1);
+  const int64_t sb = v.shard_base[s];
+  int32_t n = 0;
+  for (uint32_t c = rp[d]; c < rp[d + 1]; c++) n += meta_n(v.meta[sb + c]);
+  return n;
+}
+
+// Rank-cache entries (shard, dense row) -> row counts (device rank caches of
+// cold fragments: the .cache file's ids with the arena's counts).
+__global__ __launch_bounds__(256) void row_counts_kernel(ViewDev v, const int32_t* __restrict__ shard_of,
+                                                         const int32_t* __restrict__ dense, int64_t N,
+                                                         int32_t* __restrict__ out) {
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < N; e += int64_t(gridDim.x) * blockDim.x)
+    out[e] = row_card(v, shard_of[e], dense[e]);
+}
+
+// ids= re-count without a src row (fragment.top with RowIDs, cache-only):
+// out[p] = sum over the local shards of row p's count where it reaches
+// threshold[p].  One 256-thread workgroup per id walks the shards; wave64
+// shuffle reduction, one store per id.
+__global__ __launch_bounds__(256) void row_counts_sum_kernel(ViewDev v, int S, const int32_t* __restrict__ dense,
+                                                             const int32_t* __restrict__ threshold, int P,
+                                                             unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long part[4];
+  const int p = blockIdx.x;
+  if (p >= P) return;
+  const int64_t d = dense[p];
+  const int32_t th = threshold[p] > 1 ? threshold[p] : 1;
+  unsigned long long acc = 0;
+  if (d >= 0)
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const int32_t n = row_card(v, s, d);
+      if (n >= th) acc += unsigned(n);
+    }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[p] = part[0] + part[1] + part[2] + part[3];
+}
+
 }  // namespace
 
 void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_t* counts, int64_t* offs,
@@ -977,6 +1022,21 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(topn_src_kernel<2>, dim3(unsigned(units)), dim3(TN_THREADS), lds, st, a);
   }
+}
+
+
+void launch_row_counts(const ViewDev& v, const int32_t* shard_of, const int32_t* dense, int64_t N, int32_t* out,
+                       hipStream_t st) {
+  if (N <= 0) return;
+  const int64_t want = (N + 255) / 256;
+  const int blocks = int(want < 256 * 64 ? want : 256 * 64);
+  hipLaunchKernelGGL(row_counts_kernel, dim3(blocks), dim3(256), 0, st, v, shard_of, dense, N, out);
+}
+
+void launch_row_counts_sum(const ViewDev& v, int S, const int32_t* dense, const int32_t* threshold, int P,
+                           unsigned long long* out, hipStream_t st) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(row_counts_sum_kernel, dim3(unsigned(P)), dim3(256), 0, st, v, S, dense, threshold, P, out);
 }
 
 }  // namespace pk

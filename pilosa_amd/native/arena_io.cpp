@@ -22,7 +22,17 @@
 //
 //   write_zipf_fragments(dir, ...)  the bench's 1M-row x 1B-column Zipf set
 //                   field written as one Pilosa-format fragment file per shard
-//                   (writeToUnoptimized layout, roaring.go:1052-1122).
+//                   (writeToUnoptimized layout, roaring.go:1052-1122), plus
+//                   the shard's `<shard>.cache` TopN rank-cache file (protobuf
+//                   Cache{IDs}, fragment.go:2397-2421): the ids of its
+//                   cache_size most populated rows, as a bulk import followed
+//                   by a cache flush leaves it.
+//
+//   read_cache_files(paths)  the ids of every `<shard>.cache` file (packed or
+//                   unpacked protobuf varints) for the device rank caches:
+//                   a cold fragment's cache is these ids with the arena's row
+//                   counts (fragment.go:459 openCache's CountRange per id),
+//                   without materialising the fragment on the host.
 #include <fcntl.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -34,6 +44,7 @@
 #include <atomic>
 #include <cerrno>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -428,9 +439,141 @@ void write_shard_file(const std::string& path, const synth::ShardOut& o, uint8_t
   if (rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename " + tmp + ": " + strerror(errno));
 }
 
+inline void put_uvarint(std::string& out, uint64_t v) {
+  while (v >= 0x80) {
+    out.push_back(char(uint8_t(v) | 0x80));
+    v >>= 7;
+  }
+  out.push_back(char(v));
+}
+
+// <shard>.cache of a synthetic shard: protobuf Cache{repeated uint64 IDs = 1}
+// (packed) with the ids of the `cache_size` rows of largest count (count desc,
+// id asc on ties), in ascending id order (rankCache.IDs, cache.go).
+void write_cache_file(const std::string& path, const synth::ShardOut& o, int64_t cache_size) {
+  const int64_t R = int64_t(o.rowptr.size()) - 1;
+  std::vector<std::pair<int64_t, int64_t>> rc;  // (-count, row)
+  for (int64_t r = 0; r < R; r++) {
+    int64_t n = 0;
+    for (uint32_t c = o.rowptr[size_t(r)]; c < o.rowptr[size_t(r + 1)]; c++) n += int64_t((uint64_t(o.meta[c]) >> 6) & 0x1ffff);
+    if (n > 0) rc.emplace_back(-n, r);
+  }
+  if (int64_t(rc.size()) > cache_size) {
+    std::nth_element(rc.begin(), rc.begin() + cache_size, rc.end());
+    rc.resize(size_t(cache_size));
+  }
+  std::vector<uint64_t> ids;
+  ids.reserve(rc.size());
+  for (auto& x : rc) ids.push_back(uint64_t(x.second));
+  std::sort(ids.begin(), ids.end());
+  std::string body;
+  for (uint64_t id : ids) put_uvarint(body, id);
+  std::string msg;
+  if (!body.empty()) {
+    msg.push_back(char(0x0A));  // field 1, wire type 2 (packed)
+    put_uvarint(msg, body.size());
+    msg += body;
+  }
+  const std::string tmp = path + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) throw std::runtime_error("open " + tmp + ": " + strerror(errno));
+  bool ok = msg.empty() || fwrite(msg.data(), 1, msg.size(), f) == msg.size();
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) throw std::runtime_error("write " + tmp + " failed");
+  if (rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename " + tmp + ": " + strerror(errno));
+}
+
+// Ids of a protobuf Cache message (field 1: packed or one varint per entry;
+// unknown fields skipped).  false on a malformed message.
+bool parse_cache_ids(const uint8_t* p, size_t n, std::vector<uint64_t>& out) {
+  size_t i = 0;
+  auto uv = [&](uint64_t* v) -> bool {
+    uint64_t x = 0;
+    for (int sh = 0; sh < 64; sh += 7) {
+      if (i >= n) return false;
+      const uint8_t b = p[i++];
+      x |= uint64_t(b & 0x7f) << sh;
+      if (!(b & 0x80)) {
+        *v = x;
+        return true;
+      }
+    }
+    return false;
+  };
+  while (i < n) {
+    uint64_t tag;
+    if (!uv(&tag)) return false;
+    const uint64_t field = tag >> 3, wt = tag & 7;
+    if (wt == 0) {
+      uint64_t v;
+      if (!uv(&v)) return false;
+      if (field == 1) out.push_back(v);
+    } else if (wt == 2) {
+      uint64_t len;
+      if (!uv(&len) || len > n - i) return false;
+      const size_t end = i + size_t(len);
+      if (field == 1) {
+        while (i < end) {
+          uint64_t v;
+          if (!uv(&v) || i > end) return false;
+          out.push_back(v);
+        }
+      }
+      i = end;
+    } else if (wt == 1) {
+      if (n - i < 8) return false;
+      i += 8;
+    } else if (wt == 5) {
+      if (n - i < 4) return false;
+      i += 4;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+// -> (offsets int64[S+1], ids uint64[N], ok bool[S]); a missing file is an
+// empty cache, a corrupt one ok=False (the caller rebuilds, as openCache does).
+py::tuple read_cache_files(const std::vector<std::string>& paths, int nthreads) {
+  const int64_t S = int64_t(paths.size());
+  std::vector<std::vector<uint64_t>> per(static_cast<size_t>(S));
+  std::vector<char> good(static_cast<size_t>(S), 1);
+  {
+    py::gil_scoped_release nogil;
+    parallel_for(S, nthreads, [&](int64_t s) {
+      const std::string& path = paths[size_t(s)];
+      if (path.empty()) return;
+      FILE* f = fopen(path.c_str(), "rb");
+      if (!f) return;  // no cache file: empty rank cache
+      std::string data;
+      char buf[1 << 16];
+      size_t r;
+      while ((r = fread(buf, 1, sizeof(buf), f)) > 0) data.append(buf, r);
+      fclose(f);
+      if (!parse_cache_ids(reinterpret_cast<const uint8_t*>(data.data()), data.size(), per[size_t(s)])) {
+        per[size_t(s)].clear();
+        good[size_t(s)] = 0;
+      }
+    });
+  }
+  py::array_t<int64_t> offs(S + 1);
+  int64_t* op = offs.mutable_data();
+  op[0] = 0;
+  for (int64_t s = 0; s < S; s++) op[s + 1] = op[s] + int64_t(per[size_t(s)].size());
+  py::array_t<uint64_t> ids(std::max<int64_t>(op[S], 0));
+  py::array_t<bool> ok(S);
+  uint64_t* ip = ids.mutable_data();
+  for (int64_t s = 0; s < S; s++) {
+    if (!per[size_t(s)].empty()) memcpy(ip + op[s], per[size_t(s)].data(), per[size_t(s)].size() * 8);
+    ok.mutable_data()[s] = good[size_t(s)] != 0;
+  }
+  return py::make_tuple(offs, ids, ok);
+}
+
 py::dict write_zipf_fragments(const std::string& dir, int64_t shard_lo, int64_t shard_hi, int64_t total_cols,
                               int64_t nrows, double bits_per_col, double zs, double zv, uint64_t seed, int nthreads,
-                              uint8_t flags) {
+                              uint8_t flags, int64_t cache_size) {
   const int64_t S = std::max<int64_t>(0, shard_hi - shard_lo);
   std::atomic<int64_t> bytes{0}, containers{0};
   {
@@ -442,6 +585,7 @@ py::dict write_zipf_fragments(const std::string& dir, int64_t shard_lo, int64_t 
       synth::gen_zipf_shard(o, shard, total_cols, dens, seed);
       if (o.meta.empty()) return;
       write_shard_file(dir + "/" + std::to_string(shard), o, flags);
+      if (cache_size > 0) write_cache_file(dir + "/" + std::to_string(shard) + ".cache", o, cache_size);
       containers += int64_t(o.meta.size());
       int64_t b = int64_t(pr::HEADER_BASE) + int64_t(o.meta.size()) * 16;
       for (int64_t m : o.meta) {
@@ -458,6 +602,30 @@ py::dict write_zipf_fragments(const std::string& dir, int64_t shard_lo, int64_t 
   return d;
 }
 
+// The synthetic BSI int field of BASELINE config 4 as Pilosa-format fragment
+// files of its bsig_<field> view (one per shard).
+py::dict write_bsi_fragments(const std::string& dir, int64_t shard_lo, int64_t shard_hi, int64_t total_cols, int depth,
+                             double fill, int64_t vmin, int64_t vmax, uint64_t seed, int nthreads, uint8_t flags) {
+  if (depth < 1 || depth > 62) throw std::invalid_argument("depth must be in 1..62");
+  const int64_t S = std::max<int64_t>(0, shard_hi - shard_lo);
+  std::atomic<int64_t> containers{0};
+  {
+    py::gil_scoped_release nogil;
+    parallel_for(S, nthreads, [&](int64_t k) {
+      synth::ShardOut o;
+      const int64_t shard = shard_lo + k;
+      synth::gen_bsi_shard(o, shard, total_cols, depth, fill, vmin, vmax, seed);
+      if (o.meta.empty()) return;
+      write_shard_file(dir + "/" + std::to_string(shard), o, flags);
+      containers += int64_t(o.meta.size());
+    });
+  }
+  py::dict d;
+  d["shards"] = S;
+  d["containers"] = containers.load();
+  return d;
+}
+
 }  // namespace
 
 void register_arena_io(py::module_& m) {
@@ -471,5 +639,13 @@ void register_arena_io(py::module_& m) {
   m.def("write_zipf_fragments", &write_zipf_fragments, py::arg("dir"), py::arg("shard_lo"), py::arg("shard_hi"),
         py::arg("total_cols"), py::arg("nrows"), py::arg("bits_per_col") = 8.0, py::arg("zipf_s") = 1.6,
         py::arg("zipf_v") = 50.0, py::arg("seed") = 1, py::arg("nthreads") = 16, py::arg("flags") = 1,
-        "Write the synthetic Zipf set field as one Pilosa-format fragment file per shard (<dir>/<shard>)");
+        py::arg("cache_size") = 50000,
+        "Write the synthetic Zipf set field as one Pilosa-format fragment file per shard (<dir>/<shard>) "
+        "and its rank-cache file (<dir>/<shard>.cache, cache_size most populated rows; 0 = none)");
+  m.def("write_bsi_fragments", &write_bsi_fragments, py::arg("dir"), py::arg("shard_lo"), py::arg("shard_hi"),
+        py::arg("total_cols"), py::arg("depth"), py::arg("fill"), py::arg("vmin"), py::arg("vmax"), py::arg("seed") = 1,
+        py::arg("nthreads") = 16, py::arg("flags") = 1,
+        "Write a synthetic BSI int field (exists, sign, magnitude planes) as Pilosa-format fragment files");
+  m.def("read_cache_files", &read_cache_files, py::arg("paths"), py::arg("nthreads") = 16,
+        "Ids of <shard>.cache rank-cache files -> (offsets int64[S+1], ids uint64[N], ok bool[S])");
 }

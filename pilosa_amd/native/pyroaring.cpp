@@ -284,31 +284,7 @@ static py::tuple gen_bsi_arena(int64_t shard_lo, int64_t shard_hi, int64_t total
   const int64_t R = depth + 2;
   std::vector<ShardOut> outs(S);
   auto work = [&](int64_t si) {
-    const int64_t shard = shard_lo + si;
-    const int64_t cols = std::max<int64_t>(0, std::min<int64_t>(1 << 20, total_cols - shard * (1 << 20)));
-    ShardOut& o = outs[si];
-    o.rowptr.assign(R + 1, 0);
-    // planes[r][j][1024]
-    std::vector<uint64_t> planes(size_t(R) * 16 * 1024, 0);
-    Rng rng(mix3(seed, uint64_t(shard), 0xB51));
-    const uint64_t span = uint64_t(vmax - vmin) + 1;
-    for (int64_t c = 0; c < cols; c++) {
-      if (double(rng.next() >> 11) * (1.0 / 9007199254740992.0) >= fill) continue;
-      const int64_t v = vmin + int64_t(rng.next() % span);
-      const uint64_t u = uint64_t(v < 0 ? -v : v);
-      const int j = int(c >> 16), w = int((c & 0xffff) >> 6);
-      const uint64_t bit = 1ull << (c & 63);
-      planes[(size_t(0) * 16 + j) * 1024 + w] |= bit;
-      if (v < 0) planes[(size_t(1) * 16 + j) * 1024 + w] |= bit;
-      for (int i = 0; i < depth; i++)
-        if ((u >> i) & 1) planes[(size_t(2 + i) * 16 + j) * 1024 + w] |= bit;
-    }
-    std::vector<uint16_t> tmp;
-    for (int64_t r = 0; r < R; r++) {
-      o.rowptr[r] = uint32_t(o.meta.size());
-      for (int j = 0; j < 16; j++) o.emit_words(j, &planes[(size_t(r) * 16 + j) * 1024], tmp);
-    }
-    o.rowptr[R] = uint32_t(o.meta.size());
+    synth::gen_bsi_shard(outs[si], shard_lo + si, total_cols, depth, fill, vmin, vmax, seed);
   };
   {
     py::gil_scoped_release nogil;

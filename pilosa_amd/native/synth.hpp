@@ -149,4 +149,35 @@ inline void gen_zipf_shard(ShardOut& o, int64_t shard, int64_t total_cols, const
   o.rowptr[size_t(R)] = uint32_t(o.meta.size());
 }
 
+// One shard of a synthetic BSI int field (reference bsiExistsBit / bsiSignBit /
+// bsiOffsetBit layout, sign-magnitude): a fraction `fill` of the columns hold
+// a value uniform in [vmin, vmax]; rows 0 = exists, 1 = sign, 2+i = bit i of
+// |value|.  Deterministic per (seed, shard).
+inline void gen_bsi_shard(ShardOut& o, int64_t shard, int64_t total_cols, int depth, double fill, int64_t vmin,
+                          int64_t vmax, uint64_t seed) {
+  const int64_t cols = std::max<int64_t>(0, std::min<int64_t>(1 << 20, total_cols - shard * (1 << 20)));
+  const int64_t R = depth + 2;
+  o.rowptr.assign(size_t(R + 1), 0);
+  std::vector<uint64_t> planes(size_t(R) * 16 * 1024, 0);  // planes[r][j][1024]
+  Rng rng(mix3(seed, uint64_t(shard), 0xB51));
+  const uint64_t span = uint64_t(vmax - vmin) + 1;
+  for (int64_t c = 0; c < cols; c++) {
+    if (double(rng.next() >> 11) * (1.0 / 9007199254740992.0) >= fill) continue;
+    const int64_t v = vmin + int64_t(rng.next() % span);
+    const uint64_t u = uint64_t(v < 0 ? -v : v);
+    const int j = int(c >> 16), w = int((c & 0xffff) >> 6);
+    const uint64_t bit = 1ull << (c & 63);
+    planes[(size_t(0) * 16 + size_t(j)) * 1024 + size_t(w)] |= bit;
+    if (v < 0) planes[(size_t(1) * 16 + size_t(j)) * 1024 + size_t(w)] |= bit;
+    for (int i = 0; i < depth; i++)
+      if ((u >> i) & 1) planes[(size_t(2 + i) * 16 + size_t(j)) * 1024 + size_t(w)] |= bit;
+  }
+  std::vector<uint16_t> tmp;
+  for (int64_t r = 0; r < R; r++) {
+    o.rowptr[size_t(r)] = uint32_t(o.meta.size());
+    for (int j = 0; j < 16; j++) o.emit_words(j, &planes[(size_t(r) * 16 + size_t(j)) * 1024], tmp);
+  }
+  o.rowptr[size_t(R)] = uint32_t(o.meta.size());
+}
+
 }  // namespace synth

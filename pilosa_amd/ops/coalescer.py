@@ -44,6 +44,7 @@ class CountCoalescer:
         self.batches = 0       # launched batches
         self.batched = 0       # calls that went through a batch
         self.fallbacks = 0     # calls sent back to the regular path
+        self.last_error: Optional[BaseException] = None   # why the last batch fell back (diagnostics)
 
     def submit(self, key, call, fallback: Callable[[], Any]):
         """Result of ``call`` (via a batch, or ``fallback()``)."""
@@ -91,7 +92,8 @@ class CountCoalescer:
     def _run(self, key, batch: List[_Slot]):
         try:
             res = self.run_batch(key, [s.call for s in batch]) if len(batch) > 0 else []
-        except Exception:  # noqa: BLE001 - every call retries alone and gets its own error
+        except Exception as err:  # noqa: BLE001 - every call retries alone and gets its own error
+            self.last_error = err
             res = None
         self.batches += 1
         if res is None or len(res) != len(batch):

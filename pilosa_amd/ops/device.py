@@ -827,6 +827,11 @@ class DeviceView:
             rec["keymask"] = km[1].data_ptr()
         return rec
 
+    def viewdev_tensor(self):
+        """The ViewDev record as the uint8 host tensor the kernel bindings take."""
+        import torch
+        return torch.from_numpy(np.frombuffer(self.viewdev().tobytes(), dtype=np.uint8).copy())
+
     KEYMASK_MIN_INTERVAL_S = 5.0
 
     def ensure_keymask(self) -> bool:

@@ -92,7 +92,14 @@ class GpuExecutor:
         self.last_load: Dict = {}
         self.plan_threads = int(os.environ.get("PILOSA_PLAN_THREADS", "4"))
         self.topn_index_enabled = os.environ.get("PILOSA_TOPN_INDEX", "1") != "0"
-        self._topn_indexes: Dict[Tuple, Tuple] = {}  # (index, field, shards) -> (versions, index, built_at)
+        self._topn_indexes: Dict[Tuple, Tuple] = {}  # (index, field, shards) -> (rank caches, index, built_at)
+        self._rank_cache_map: Dict[Tuple, Tuple] = {}  # (index, field, shards) -> (signature, DeviceRankCaches)
+        # SPMD ranks of one node (parallel/collectives.Comm): TopN batches merge
+        # their candidates / re-counts node-wide (every rank runs the same calls)
+        self.comm = None
+        self._spaces: Dict[Tuple, Tuple] = {}
+        self.topn_decline = ""          # why the last topn_batch returned None (diagnostics)
+        self._topn_index_why = ""
 
     # ------------------------------------------------------------ arenas
     def view_arena(self, index: str, field: str, view: str, shards: Sequence[int]) -> Optional[DeviceView]:
@@ -269,6 +276,7 @@ class GpuExecutor:
             self._arena_epoch.clear()
             self._bsi_views.clear()
             self._topn_indexes.clear()
+            self._rank_cache_map.clear()
 
     BSI_CACHE = 8
 
@@ -812,42 +820,174 @@ class GpuExecutor:
         s, n = int(s.cpu()[0]), int(n.cpu()[0])
         return ValCount(_wrap(s + n * b.base), n)
 
+    def bsi_sum_batch(self, index: str, calls: List[Call], shards: List[int]):
+        """Many Sum(<filter>, field=v) calls of one request over one BSI field:
+        the filters are planned together and summed in one launch -- the
+        bit-plane count matrix on the matrix cores (ops/bsi.py) from
+        BSI_MATRIX_MIN filters up, else the per-filter kernel with all filters
+        in one grid.  None when a call needs the general path."""
+        from pilosa_amd.executor import ValCount, _wrap
+
+        from .bsi import BSI_MATRIX_MIN, bsi_sum_matrix
+        fname = calls[0].args.get("field")
+        if not isinstance(fname, str) or any(c.args.get("field") != fname or len(c.children) > 1 for c in calls):
+            return None
+        f = self.holder.field(index, fname)
+        if f is None or f.bsi_group(fname) is None:
+            return None
+        b = f.bsi_group(fname)
+        bv = self.view_arena(index, fname, VIEW_BSI_PREFIX + fname, shards)
+        if bv is None:
+            return [ValCount() for _ in calls]
+        filters = []
+        try:
+            for c in calls:
+                filters.append(self.plan(index, c.children[0], shards) if c.children else None)
+        except NotImplementedError:
+            return None
+        live = [i for i, x in enumerate(filters) if x is not EMPTY]
+        out = [ValCount() for _ in calls]
+        if not live:
+            return out
+        fl = [filters[i] for i in live]
+        try:
+            self.launches += 1
+            if len(fl) >= BSI_MATRIX_MIN:
+                s_t, n_t = bsi_sum_matrix(self.engine, fl, bv, b.bit_depth)
+            else:
+                s_t, n_t = self.engine.bsi_sum_async(fl, bv, b.bit_depth)
+        except CompileError:
+            return None
+        for i, sv, nv in zip(live, s_t.cpu().tolist(), n_t.cpu().tolist()):
+            out[i] = ValCount(_wrap(int(sv) + int(nv) * b.base), int(nv))
+        return out
+
     # ------------------------------------------------------------ TopN
-    def topn(self, index: str, c: Call, shards: List[int]) -> List[Pair]:
-        from pilosa_amd.models.fragment import TopOptions
+    def _topn_setup(self, index: str, c: Call, shards: List[int]):
+        """(params, frags, rank caches, view, src plan) of one TopN call, or
+        NotImplementedError for the shapes the host answers (Tanimoto and
+        attribute filters: per-row attribute reads)."""
         ex = self._ex()
         fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
-        if len(c.children) != 1 or tanimoto or (attr_name and attr_values):
-            raise NotImplementedError  # cache-only TopN is cheap on the host; exotic options stay there
-        src = self.plan(index, c.children[0], shards)
+        if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
+            raise NotImplementedError
         frags = [self.holder.fragment(index, fname, VIEW_STANDARD, s) for s in shards]
         for f in frags:
             if f is not None and f.cache_type == "none":
                 from pilosa_amd.errors import PilosaError
                 raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
-        # candidate (row, cached count) lists per shard, as fragment.top() would see them
-        per_shard_pairs = [f._top_bitmap_pairs(ids) if f is not None else [] for f in frags]
-        cand = sorted({rid for pairs in per_shard_pairs for rid, _ in pairs})
-        if not cand:
-            return []
-        if src is EMPTY:
-            return []
         rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
-        if not ids or threshold <= 1:
-            tix = self._topn_index(index, fname, shards, frags, rv)
-            if tix is not None:
+        src = self.plan(index, c.children[0], shards) if c.children else None
+        rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+        return (fname, n, ids, threshold), rc, rv, src
+
+    def topn(self, index: str, c: Call, shards: List[int]) -> List[Pair]:
+        """One TopN call's map step over the local shards (executor.go:905-930):
+        phase 1 = per-shard ``fragment.top`` results summed by row (untrimmed),
+        with ``ids=`` the per-shard exact re-count of those rows."""
+        (fname, n, ids, threshold), rc, rv, src = self._topn_setup(index, c, shards)
+        if rc is None or src is EMPTY or rc.K == 0:
+            return []
+        if src is None:
+            self.launches += 1
+            return rc.shard_pairs_nosrc(0 if ids else n, threshold, ids or None)
+        tix = self._topn_index(index, fname, shards, rc, rv)
+        if tix is not None:
+            self.launches += 1
+            return sort_pairs(tix.shard_pairs(self.engine, src, 0 if ids else n, threshold, ids or None))
+        return self._topn_pairs_path(rc, rv, src, n, ids, threshold)
+
+    def topn_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[List[Pair]]]:
+        """Whole TopN calls (phase 1, candidate union, ids= re-count, trim to
+        n: executor.go:863-903) for a batch of calls over local shards, both
+        phases on the device.  Calls of one (field, src shape) share launches:
+        cache-only calls one scatter-add + one re-count, src calls the slot
+        index (16 per hot-rank launch).  The per-field work (fragments, view,
+        rank caches, slot index) is resolved once per batch.  None when a call
+        needs the general path (the caller then runs each call alone)."""
+        ex = self._ex()
+        params = []
+        fields: Dict[str, Tuple] = {}
+        for c in calls:
+            fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
+            if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
+                self.topn_decline = f"shape ({c})"
+                return None
+            if ids:
+                self.topn_decline = "ids"
+                return None   # explicit ids= (phase 2 only): the map-step path
+            params.append((fname, n, threshold))
+            if fname not in fields:
+                frags = [self.holder.fragment(index, fname, VIEW_STANDARD, s) for s in shards]
+                for f in frags:
+                    if f is not None and f.cache_type == "none":
+                        from pilosa_amd.errors import PilosaError
+                        raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
+                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+                rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+                fields[fname] = (rv, rc)
+        srcs = []
+        try:
+            for c in calls:
+                srcs.append(self.plan(index, c.children[0], shards) if c.children else None)
+        except NotImplementedError as e:
+            self.topn_decline = f"src plan: {e!r}"
+            return None
+        groups: Dict[Tuple, List[int]] = {}
+        for i, (fname, _, _) in enumerate(params):
+            groups.setdefault((fname, srcs[i] is None), []).append(i)
+        out: List[Optional[List[Pair]]] = [None] * len(calls)
+        for (fname, nosrc), members in groups.items():
+            rv, rc = fields[fname]
+            live = [i for i in members if rc is not None and rc.K and srcs[i] is not EMPTY]
+            for i in members:
+                if i not in live:
+                    out[i] = []
+            if not live:
+                continue
+            ns = [params[i][1] for i in live]
+            ths = [params[i][2] for i in live]
+            space = self._node_space((index, fname, tuple(shards)), rv)
+            if nosrc:
                 self.launches += 1
-                return sort_pairs(tix.shard_pairs(self.engine, src, 0 if ids else n, threshold, ids or None))
-        # Each shard's fragment.top() walks its cache in order and stops once a
-        # row's cached count falls below the heap threshold, so usually only a
-        # short prefix of the (up to cache-size) candidates is ever counted.
-        # Count growing prefixes on the device (one launch per round for all
-        # shards), replay the exact heap logic on the host, and only extend
-        # the shards whose replay ran past what was counted.
+                got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space)
+            else:
+                tix = self._topn_index(index, fname, shards, rc, rv, space=space)
+                if tix is None:
+                    self.topn_decline = f"no slot index ({self._topn_index_why})"
+                    return None
+                self.launches += 1
+                got = tix.topn(self.engine, [srcs[i] for i in live], ns, ths, comm=self.comm)
+            for i, r in zip(live, got):
+                out[i] = r
+        return out
+
+    def _topn_pairs_path(self, rc, rv, src, n: int, ids, threshold: int) -> List[Pair]:
+        """Src TopN without a slot index (while it is rebuilt, or too large for
+        LDS): each shard's fragment.top() walks its cache in order and stops
+        once a row's cached count falls below the heap threshold, so usually
+        only a short prefix of the candidates is ever counted.  Growing
+        prefixes are counted on the device (one launch per round for all
+        shards), the exact heap logic is replayed natively, and only the
+        shards whose replay ran past what was counted are extended."""
+        per_shard_pairs = []
+        if ids:
+            # topBitmapPairs(rowIDs): every listed row with its count in the shard
+            want = sorted({int(x) for x in ids})
+            cnt = rc.row_counts_for(want)                      # [S, P]
+            for si in range(rc.S):
+                pr = [(r, int(k)) for r, k in zip(want, cnt[si].tolist()) if k > 0]
+                pr.sort(key=lambda p: (-p[1], p[0]))
+                per_shard_pairs.append(pr)
+        else:
+            rows, counts = rc.host_lists()
+            for si in range(rc.S):
+                live = counts[si] > 0
+                per_shard_pairs.append(list(zip(rows[si][live].tolist(), counts[si][live].tolist())))
         counted: Dict[int, np.ndarray] = {}
-        depth = [0] * len(shards)
-        k = max(256, 2 * n) if not ids else max(len(p) for p in per_shard_pairs)
-        pending = list(range(len(shards)))
+        depth = [0] * rc.S
+        k = max(256, 2 * n) if not ids else max((len(p) for p in per_shard_pairs), default=0)
+        pending = list(range(rc.S))
         total: Dict[int, int] = {}
         while pending:
             want = set()
@@ -855,22 +995,21 @@ class GpuExecutor:
                 depth[si] = min(len(per_shard_pairs[si]), max(depth[si] * 4, k))
                 want.update(rid for rid, _ in per_shard_pairs[si][:depth[si]] if rid not in counted)
             if want:
-                rows = sorted(want)
-                exprs = [Op("and", (src, Leaf(rv, r))) for r in rows]
+                rws = sorted(want)
+                exprs = [Op("and", (src, Leaf(rv, r))) for r in rws]
                 try:
                     for i in range(0, len(exprs), MAX_GROUPS_PER_LAUNCH):
                         self.launches += 1
                         m = self.engine.count_per_shard(exprs[i:i + MAX_GROUPS_PER_LAUNCH])  # [R, S]
-                        for r, row_counts in zip(rows[i:i + MAX_GROUPS_PER_LAUNCH], m):
+                        for r, row_counts in zip(rws[i:i + MAX_GROUPS_PER_LAUNCH], m):
                             counted[r] = row_counts
                 except CompileError:
                     raise NotImplementedError
             nxt = []
             for si in pending:
-                pairs = per_shard_pairs[si]
                 try:
-                    got = _replay_top(pairs, lambda rid, si=si: _counted(counted, rid, si), 0 if ids else n,
-                                      threshold)
+                    got = _replay_top(per_shard_pairs[si], lambda rid, si=si: _counted(counted, rid, si),
+                                      0 if ids else n, threshold)
                 except _NeedMore:
                     nxt.append(si)
                     continue
@@ -879,40 +1018,83 @@ class GpuExecutor:
             pending = nxt
         return sort_pairs([Pair(k2, v) for k2, v in total.items()])
 
-    def _topn_index(self, index: str, fname: str, shards: List[int], frags, rv):
-        """Device slot index (ops/topn_index.py) of the fragments' rank caches,
-        rebuilt when a cache re-ranks or the arena changes, at most once per
-        TOPN_INDEX_REBUILD_S per view (stale in between: pair-count path)."""
-        if rv is None or not self.topn_index_enabled:
+    def _rank_caches(self, index: str, fname: str, shards: List[int], frags, rv):
+        """Device rank caches of the view (ops/topn_exec.py), rebuilt when the
+        arena changes or a warm fragment's host cache re-ranks.  Cold
+        fragments contribute their .cache file ids (never loaded on the host);
+        warm ones their live host caches (recalculated as topBitmapPairs does
+        with cache.Invalidate, at most every 10 s)."""
+        from .topn_exec import DeviceRankCaches
+        key = (index, fname, tuple(shards))
+        epoch = mutation_epoch()
+        with self.mu:
+            ent = self._rank_cache_map.get(key)
+            if ent is not None and ent[2] == epoch and ent[1].view is rv and ent[1].generation == rv.generation:
+                return ent[1]
+        sig = []
+        for f in frags:
+            if f is None:
+                sig.append(None)
+            elif f.is_cold():
+                sig.append(("cold", id(f)))
+            else:
+                f.cache.invalidate()
+                sig.append(("warm", id(f), getattr(f.cache, "version", -1)))
+        sig = (id(rv), rv.generation, tuple(sig))
+        with self.mu:
+            ent = self._rank_cache_map.get(key)
+            if ent is not None and ent[0] == sig:
+                self._rank_cache_map[key] = (sig, ent[1], epoch)
+                return ent[1]
+        rc = DeviceRankCaches(rv, frags)
+        with self.mu:
+            self._rank_cache_map[key] = (sig, rc, epoch)
+        return rc
+
+    def _node_space(self, key, rv) -> Optional[np.ndarray]:
+        """Sorted union of every rank's row ids of this view (the common space
+        of the node-wide TopN candidates), or None on a single rank."""
+        if self.comm is None or rv is None:
             return None
-        from pilosa_amd.ops.topn import DeviceRankCache
+        import torch
+        sig = (id(rv), rv.generation)
+        ent = self._spaces.get(key)
+        if ent is not None and ent[0] == sig:
+            return ent[1]
+        t = torch.from_numpy(np.ascontiguousarray(rv.rows).view(np.int64).copy()).to(rv.device)
+        parts = self.comm.all_gather_var(t)
+        space = np.unique(np.concatenate([p.cpu().numpy().view(np.uint64) for p in parts])) if parts else rv.rows
+        self._spaces[key] = (sig, space)
+        return space
+
+    def _topn_index(self, index: str, fname: str, shards: List[int], rc, rv, space=None):
+        """Device slot index (ops/topn_index.py) over the rank caches ``rc``,
+        rebuilt when they change, at most once per TOPN_INDEX_REBUILD_S per
+        view (stale in between: the pair-count path)."""
+        if rv is None or rc is None or not self.topn_index_enabled or rc.K == 0:
+            self._topn_index_why = "disabled/empty"
+            return None
         from pilosa_amd.ops.topn_index import MAX_SLOTS, DeviceTopNIndex
         key = (index, fname, tuple(shards))
-        ver = tuple(getattr(f.cache, "version", -1) if f is not None else -2 for f in frags)
         ent = self._topn_indexes.get(key)
-        if ent is not None and ent[0] == ver and ent[1].view is rv and not ent[1].stale:
+        if ent is not None and ent[0] is rc and ent[1].view is rv and not ent[1].stale:
             return ent[1]
         now = time.monotonic()
         if ent is not None and now - ent[2] < TOPN_INDEX_REBUILD_S:
+            self._topn_index_why = (f"throttled: same_rc={ent[0] is rc} same_view={ent[1].view is rv} "
+                                    f"stale={ent[1].stale}")
             return None
-        lists = [list(f.cache.top()) if f is not None else [] for f in frags]
-        K = max((len(x) for x in lists), default=0)
-        if K == 0 or K > MAX_SLOTS:
+        if rc.K > MAX_SLOTS:
+            self._topn_index_why = "too many slots"
             return None
-        rows = np.zeros((len(frags), K), np.int64)
-        counts = np.zeros((len(frags), K), np.int64)
-        for si, pairs in enumerate(lists):
-            if pairs:
-                a = np.asarray(pairs, dtype=np.int64)
-                rows[si, :len(a)] = a[:, 0]
-                counts[si, :len(a)] = a[:, 1]
+        self._topn_indexes.pop(key, None)   # free the old index's HBM before building
         try:
-            tix = DeviceTopNIndex(rv, DeviceRankCache(rows, counts))
+            tix = DeviceTopNIndex(rv, rc, space=space)
         except ValueError:
             return None
         if not tix.ok:
             return None
-        self._topn_indexes[key] = (ver, tix, now)
+        self._topn_indexes[key] = (rc, tix, now)
         return tix
 
     # ------------------------------------------------------------ GroupBy

@@ -1,0 +1,271 @@
+"""Executor-path TopN on the device: rank caches built without touching the
+host fragments, and batched two-phase TopN over all local shards.
+
+Reference: executor.go:863-1000 (executeTopN: phase 1 per-shard ``top``,
+Pairs.Add over shards, phase 2 ``ids=`` re-count, trim to n),
+fragment.go:1568-1712 (``top`` / ``topBitmapPairs``), fragment.go:459
+(``openCache``: the persisted ``<shard>.cache`` ids with a CountRange each),
+cache.go:235-281 (rank cache order).
+
+MI355X design.  A lazily opened fragment is never read on the host for TopN:
+
+* its rank cache is the id list of its ``.cache`` file (read natively,
+  ``_roaring.read_cache_files``) with each row's count taken from the HBM arena
+  metadata by ``row_counts_kernel`` -- exactly what ``openCache`` computes with
+  CountRange on the mapped file;
+* a fragment already warm on the host (written to since open) contributes its
+  live host rank cache (``fragment.cache.top()``), as the reference would.
+
+The per-shard lists are ranked on the device (count desc, id asc) into
+``[S, K]`` tensors that feed both the cache-only TopN here and the src-TopN
+slot index (ops/topn_index.py).  A batch of TopN calls is answered with both
+phases on the device: phase 1 as one scatter-add of every query's per-shard
+cache prefixes, phase 2 (``ids=``) as ``row_counts_sum_kernel`` over the
+candidates, and only the trimmed ``Q x n`` pairs cross to the host.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from pilosa_amd.models.cache import Pair
+
+from .device import DeviceView, kernels
+
+# queries per cache-only phase-1 accumulator (Q x D int32 scratch)
+NOSRC_CHUNK = 64
+
+
+def rows_dev(view: DeviceView):
+    """int64 device copy of the view's sorted row directory (cached per view)."""
+    import torch
+    got = getattr(view, "_rows_dev", None)
+    if got is None or got[0] != view.generation or got[1].numel() != view.D:
+        t = torch.from_numpy(np.ascontiguousarray(view.rows).view(np.int64)).to(view.device)
+        got = (view.generation, t)
+        view._rows_dev = got
+    return got[1]
+
+
+def dense_dev(view: DeviceView, ids):
+    """Row ids (int64 device tensor) -> dense row indexes of ``view`` (int32, -1 absent)."""
+    import torch
+    D = view.D
+    if D == 0 or ids.numel() == 0:
+        return torch.full(ids.shape, -1, dtype=torch.int32, device=ids.device)
+    if int(view.rows[-1]) == D - 1:   # identity directory (rows 0..D-1)
+        return torch.where((ids >= 0) & (ids < D), ids, torch.full_like(ids, -1)).to(torch.int32)
+    rows = rows_dev(view)
+    i = torch.searchsorted(rows, ids).clamp_(max=D - 1)
+    return torch.where(rows[i] == ids, i, torch.full_like(i, -1)).to(torch.int32)
+
+
+class DeviceRankCaches:
+    """Ranked caches of every local shard of one view, on the device.
+
+    ``cache_dense`` int32[S, K] (dense row of each rank, -1 empty) and
+    ``cache_cnt`` int32[S, K] (its count, 0 empty), ranks ordered count desc
+    then row asc.  ``cold_shards`` counts the shards whose ranks came from
+    the ``.cache`` file (fragment never loaded on the host)."""
+
+    def __init__(self, view: DeviceView, frags: Sequence, nthreads: int = 16):
+        import torch
+
+        from pilosa_amd import _roaring
+        self.view = view
+        self.generation = view.generation
+        S = view.S
+        dev = view.device
+        self.S = S
+        cold = [f is not None and f.is_cold() for f in frags]
+        paths = [frags[si].cache_path() if cold[si] else "" for si in range(S)]
+        offs, ids, ok = _roaring.read_cache_files(paths, nthreads)
+        # a corrupt .cache file: the host fragment rebuilds its cache (openCache)
+        warm = [si for si in range(S) if frags[si] is not None and (not cold[si] or not ok[si])]
+        self.cold_shards = sum(1 for si in range(S) if cold[si] and ok[si])
+        lens = np.diff(offs)
+        for si in warm:
+            lens[si] = 0
+        keep = np.repeat(lens > 0, np.diff(offs)) if len(ids) else np.zeros(0, bool)
+        shard_of = np.repeat(np.arange(S, dtype=np.int32), lens)
+        ids = ids[keep] if len(ids) else ids
+        t_shard = torch.from_numpy(shard_of).to(dev)
+        t_dense = dense_dev(view, torch.from_numpy(np.ascontiguousarray(ids).view(np.int64)).to(dev))
+        t_cnt = torch.zeros(t_dense.numel(), dtype=torch.int32, device=dev)
+        if t_dense.numel():
+            kernels().row_counts(view.viewdev_tensor(), t_shard, t_dense, t_cnt)
+        if warm:
+            # host rank caches of fragments loaded on the host (their live counts)
+            hs, hd, hc = [], [], []
+            for si in warm:
+                pairs = list(frags[si].cache.top())
+                if not pairs:
+                    continue
+                a = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+                hs.append(np.full(len(a), si, np.int32))
+                hd.append(view.dense_many(a[:, 0].astype(np.uint64)).astype(np.int32))
+                hc.append(np.minimum(a[:, 1], 2 ** 31 - 1).astype(np.int32))
+            if hs:
+                t_shard = torch.cat([t_shard, torch.from_numpy(np.concatenate(hs)).to(dev)])
+                t_dense = torch.cat([t_dense, torch.from_numpy(np.concatenate(hd)).to(dev)])
+                t_cnt = torch.cat([t_cnt, torch.from_numpy(np.concatenate(hc)).to(dev)])
+        N = t_dense.numel()
+        if N == 0 or S == 0:
+            self.K = 0
+            self.cache_dense = torch.full((S, 0), -1, dtype=torch.int32, device=dev)
+            self.cache_cnt = torch.zeros((S, 0), dtype=torch.int32, device=dev)
+            return
+        # rank per shard on the device: key = count << 32 | (~dense), sorted desc
+        order = torch.argsort(t_shard.to(torch.int64) * (1 << 32) + torch.arange(N, device=dev), stable=False)
+        t_shard, t_dense, t_cnt = t_shard[order], t_dense[order], t_cnt[order]
+        per = torch.bincount(t_shard.to(torch.int64), minlength=S)
+        start = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+        start[1:] = torch.cumsum(per, 0)
+        pos = torch.arange(N, device=dev) - start[t_shard.to(torch.int64)]
+        K = int(per.max().item())
+        valid = (t_cnt > 0) & (t_dense >= 0)
+        key = torch.where(valid, (t_cnt.to(torch.int64) << 32) | (0xFFFFFFFF - t_dense.to(torch.int64)),
+                          torch.full_like(pos, -1))
+        mat = torch.full((S, K), -1, dtype=torch.int64, device=dev)
+        mat[t_shard.to(torch.int64), pos] = key
+        mat = torch.sort(mat, dim=1, descending=True).values
+        # a ranked cache keeps its cache_size best entries (rankCache.recalculate,
+        # cache.go:245-281): a .cache file may list up to 1.1x that many ids
+        sizes = [f.cache_size for f in frags if f is not None and f.cache_type == "ranked" and f.cache_size > 0]
+        if sizes and K > max(sizes):
+            mat = mat[:, :max(sizes)]
+        live = mat >= 0
+        kmax = int(live.sum(dim=1).max().item()) if K else 0
+        mat, live = mat[:, :kmax], live[:, :kmax]
+        self.K = kmax
+        self.cache_cnt = torch.where(live, mat >> 32, torch.zeros_like(mat)).to(torch.int32).contiguous()
+        self.cache_dense = torch.where(live, 0xFFFFFFFF - (mat & 0xFFFFFFFF), torch.full_like(mat, -1)) \
+            .to(torch.int32).contiguous()
+
+    def nbytes(self) -> int:
+        return 8 * self.S * self.K
+
+    def host_lists(self):
+        """(rows int64[S, K], counts int64[S, K]) on the host (tests, the
+        multi-rank slot index)."""
+        d = self.cache_dense.cpu().numpy().astype(np.int64)
+        c = self.cache_cnt.cpu().numpy().astype(np.int64)
+        rows = np.where(d >= 0, self.view.rows[np.maximum(d, 0)].astype(np.int64) if self.view.D else 0, 0)
+        return rows, c
+
+    def row_counts_for(self, ids: Sequence[int]) -> np.ndarray:
+        """int32[S, P]: each listed row's count in every local shard (0 absent)."""
+        import torch
+        P, S = len(ids), self.S
+        if not P or not S:
+            return np.zeros((S, P), np.int32)
+        dev = self.view.device
+        d = self.view.dense_many(np.asarray(ids, dtype=np.uint64)).astype(np.int32)
+        t_dense = torch.from_numpy(np.tile(d, S)).to(dev)
+        t_shard = torch.arange(S, dtype=torch.int32, device=dev).repeat_interleave(P)
+        out = torch.zeros(S * P, dtype=torch.int32, device=dev)
+        kernels().row_counts(self.view.viewdev_tensor(), t_shard, t_dense, out)
+        return out.view(S, P).cpu().numpy()
+
+    # ------------------------------------------------------------ cache-only TopN
+    def nosrc_phase1(self, ns: Sequence[int], thresholds: Sequence[int]):
+        """Per query the per-shard fill phase of fragment.top (the first n
+        cache entries at or above the threshold; the walk stops once its heap
+        holds n rows) summed by row -> (query, dense, count) candidate tensors."""
+        import torch
+        dev = self.view.device
+        Q, D = len(ns), self.view.D
+        qs, ds, cs = [], [], []
+        for q0 in range(0, Q, NOSRC_CHUNK):
+            q1 = min(Q, q0 + NOSRC_CHUNK)
+            nn = [int(n) for n in ns[q0:q1]]
+            nmax = self.K if any(n == 0 for n in nn) else min(self.K, max(nn))
+            if not nmax or not D:
+                continue
+            lim = torch.tensor([n if n else self.K for n in nn], dtype=torch.int64).to(dev)
+            mt = torch.tensor([max(1, int(t)) for t in thresholds[q0:q1]], dtype=torch.int32).to(dev)
+            cnt = self.cache_cnt[:, :nmax]
+            dn = self.cache_dense[:, :nmax]
+            k = torch.arange(nmax, device=dev)
+            take = (k[None, None, :] < lim[:, None, None]) & (cnt[None] >= mt[:, None, None]) & (dn[None] >= 0)
+            vals = torch.where(take, cnt[None], torch.zeros((), dtype=torch.int32, device=dev))
+            acc = torch.zeros((q1 - q0, D), dtype=torch.int32, device=dev)
+            acc.scatter_add_(1, dn.clamp(min=0).reshape(1, -1).expand(q1 - q0, -1).to(torch.int64),
+                             vals.reshape(q1 - q0, -1))
+            nz = torch.nonzero(acc > 0)
+            qs.append(nz[:, 0] + q0)
+            ds.append(nz[:, 1])
+            cs.append(acc[nz[:, 0], nz[:, 1]].to(torch.int64))
+        if not qs:
+            z = torch.zeros(0, dtype=torch.int64, device=dev)
+            return z, z, z
+        return torch.cat(qs), torch.cat(ds), torch.cat(cs)
+
+    def recount(self, pq, pdense, thresholds: Sequence[int]):
+        """ids= re-count without src: per (query, dense row) the sum over the
+        local shards of the row's count where it reaches the query's threshold.
+        A row asked for by several queries of the batch with one threshold is
+        counted once (the per-shard counts do not depend on the query)."""
+        import torch
+        dev = self.view.device
+        P = int(pdense.numel())
+        out = torch.zeros(P, dtype=torch.int64, device=dev)
+        if P and self.S:
+            th = torch.tensor([max(1, int(t)) for t in thresholds], dtype=torch.int64).to(dev)[pq]
+            key = (pdense.to(torch.int64) << 32) | th
+            uk, inv = torch.unique(key, return_inverse=True)
+            ud = (uk >> 32).to(torch.int32).contiguous()
+            ut = (uk & 0xFFFFFFFF).to(torch.int32).contiguous()
+            res = torch.zeros(int(uk.numel()), dtype=torch.int64, device=dev)
+            kernels().row_counts_sum(self.view.viewdev_tensor(), self.S, ud, ut, res)
+            out = res[inv]
+        return out
+
+    def topn_nosrc(self, ns: Sequence[int], thresholds: Sequence[int], comm=None,
+                   space: Optional[np.ndarray] = None) -> List[List[Pair]]:
+        """Whole TopN(field, n) calls (both phases, trimmed) for a batch.
+        ``comm`` (parallel/collectives.Comm) spans the ranks of a node; the
+        candidates then travel in ``space``, the sorted union of every rank's
+        row ids (identical on all ranks): each rank's phase-1 keys are
+        all-gathered and unioned, the ids= re-count is all-reduced."""
+        import torch
+
+        from .topn_index import finish_batch_dev
+        Q = len(ns)
+        if Q == 0:
+            return []
+        pq, pd, _ = self.nosrc_phase1(ns, thresholds)
+        if comm is None:
+            out = self.recount(pq, pd, thresholds)
+            return finish_batch_dev(self.view.rows, Q, pq, pd, out, ns)
+        dev = self.view.device
+        sp = torch.from_numpy(np.ascontiguousarray(space, dtype=np.uint64).view(np.int64)).to(dev)
+        A = max(int(sp.numel()), 1)
+        acc = torch.searchsorted(sp, rows_dev(self.view)[pd]) if pd.numel() else pd
+        keys = comm.union(pq * A + acc)
+        pq, pa = keys // A, keys % A
+        local = dense_dev(self.view, sp[pa]) if pa.numel() else pa.to(torch.int32)
+        out = self.recount(pq, local.clamp(min=-1), thresholds)
+        comm.all_reduce(out)
+        return finish_batch_dev(np.asarray(space, dtype=np.uint64), Q, pq, pa, out, ns)
+
+    def shard_pairs_nosrc(self, n: int, threshold: int, ids: Optional[Sequence[int]] = None) -> List[Pair]:
+        """One cache-only TopN call as the executor's map step sees it: phase 1
+        (untrimmed per-shard results summed by row) or the ids= re-count."""
+        import torch
+        dev = self.view.device
+        if ids is None:
+            pq, pd, pc = self.nosrc_phase1([n], [threshold])
+        else:
+            want = np.unique(np.asarray(list(ids), dtype=np.uint64))
+            d = self.view.dense_many(want)
+            d = d[d >= 0]
+            pd = torch.from_numpy(d.astype(np.int64)).to(dev)
+            pq = torch.zeros_like(pd)
+            pc = self.recount(pq, pd, [threshold])
+        keep = pc > 0
+        d_h = pd[keep].cpu().numpy()
+        c_h = pc[keep].cpu().numpy()
+        rows = self.view.rows[d_h] if len(d_h) else np.zeros(0, np.uint64)
+        return [Pair(int(r), int(c)) for r, c in zip(rows.tolist(), c_h.tolist())]

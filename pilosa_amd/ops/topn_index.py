@@ -65,42 +65,74 @@ class DeviceTopNIndex:
         import torch
 
         ext = kernels()
-        S, K = cache.rows.shape
-        if K > MAX_SLOTS:
-            raise ValueError(f"rank cache of {K} slots exceeds the u16 slot index ({MAX_SLOTS})")
-        if S != view.S:
-            raise ValueError("rank cache and view disagree on the shard count")
         dev = view.device
-        self.view, self.S, self.K = view, S, K
+        self.view = view
         self.generation = view.generation
         space = np.asarray(view.rows if space is None else space, dtype=np.uint64)
         self.space = space
         self.A = A = int(len(space))
-        counts = np.asarray(cache.counts, dtype=np.int64)
-        valid = counts > 0
-        rows = np.asarray(cache.rows, dtype=np.uint64).reshape(-1)
-        dense = view.dense_many(rows).reshape(S, K)
-        dense = np.where(valid, dense, -1)
-        acc_i = np.searchsorted(space, rows).reshape(S, K)
-        acc_i = np.minimum(acc_i, max(A - 1, 0))
-        if valid.any() and not np.array_equal(space[acc_i[valid]], rows.reshape(S, K)[valid]):
-            raise ValueError("acc space misses cached rows")
-        acc_i = np.where(valid, acc_i, 0)
 
         def t32(a):
             return torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(dev)
 
-        self.cache_dense = t32(dense)
-        self.cache_acc = t32(acc_i)
-        self.cache_cnt = t32(np.where(valid, np.minimum(counts, 2 ** 31 - 1), 0))
-        self.a2dense = t32(view.dense_many(space) if A else np.zeros(0))
+        if hasattr(cache, "cache_dense"):
+            # device rank caches (ops/topn_exec.DeviceRankCaches): no host pass
+            S, K = int(cache.cache_dense.shape[0]), int(cache.cache_dense.shape[1])
+            if S != view.S:
+                raise ValueError("rank cache and view disagree on the shard count")
+            self.cache_dense = cache.cache_dense.contiguous()
+            self.cache_cnt = cache.cache_cnt.contiguous()
+            valid_t = self.cache_dense >= 0
+            if A == view.D and (A == 0 or np.array_equal(space, view.rows)):
+                acc_t = self.cache_dense.clamp(min=0)
+                self.a2dense = torch.arange(A, dtype=torch.int32, device=dev)
+            else:
+                from .topn_exec import dense_dev, rows_dev
+                sp = torch.from_numpy(space.view(np.int64)).to(dev)
+                rid = rows_dev(view)[self.cache_dense.clamp(min=0).long()]
+                acc_t = torch.searchsorted(sp, rid).clamp_(max=max(A - 1, 0))
+                if bool((valid_t & (sp[acc_t] != rid)).any().item()):
+                    raise ValueError("acc space misses cached rows")
+                self.a2dense = dense_dev(view, sp).contiguous()
+            self.cache_acc = torch.where(valid_t, acc_t, torch.zeros_like(acc_t)).to(torch.int32).contiguous()
+            cnt_for_tiers = None
+        else:
+            S, K = cache.rows.shape
+            if S != view.S:
+                raise ValueError("rank cache and view disagree on the shard count")
+            counts = np.asarray(cache.counts, dtype=np.int64)
+            valid = counts > 0
+            rows = np.asarray(cache.rows, dtype=np.uint64).reshape(-1)
+            dense = view.dense_many(rows).reshape(S, K)
+            dense = np.where(valid, dense, -1)
+            acc_i = np.searchsorted(space, rows).reshape(S, K)
+            acc_i = np.minimum(acc_i, max(A - 1, 0))
+            if valid.any() and not np.array_equal(space[acc_i[valid]], rows.reshape(S, K)[valid]):
+                raise ValueError("acc space misses cached rows")
+            acc_i = np.where(valid, acc_i, 0)
+            self.cache_dense = t32(dense)
+            self.cache_acc = t32(acc_i)
+            self.cache_cnt = t32(np.where(valid, np.minimum(counts, 2 ** 31 - 1), 0))
+            self.a2dense = t32(view.dense_many(space) if A else np.zeros(0))
+            cnt_for_tiers = counts
+        if K > MAX_SLOTS:
+            raise ValueError(f"rank cache of {K} slots exceeds the u16 slot index ({MAX_SLOTS})")
+        self.S, self.K = S, K
         # ranks [0, R): hot, counted row-major per batch; [R, K): slot index
         self.R = R = max(0, min(K, HOT_RANKS if hot is None else int(hot)))
         Kt = K - R
-        tail = counts[:, R:]
         # counter tiers from the cached counts (a src count never exceeds them)
-        n32 = int((tail >= 65536).sum(axis=1).max()) if S and Kt else 0
-        n16 = int((tail >= 256).sum(axis=1).max()) if S and Kt else 0
+        if S and Kt:
+            if cnt_for_tiers is None:
+                tail = self.cache_cnt[:, R:]
+                n32 = int((tail >= 65536).sum(dim=1).max().item())
+                n16 = int((tail >= 256).sum(dim=1).max().item())
+            else:
+                tail = cnt_for_tiers[:, R:]
+                n32 = int((tail >= 65536).sum(axis=1).max())
+                n16 = int((tail >= 256).sum(axis=1).max())
+        else:
+            n32 = n16 = 0
         self.H32 = min(Kt, (n32 + 63) // 64 * 64)
         self.H16 = max(self.H32, min(Kt, (n16 + 63) // 64 * 64))
         self.lds = lds_bytes(Kt, self.H32, self.H16)

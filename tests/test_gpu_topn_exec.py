@@ -1,0 +1,134 @@
+"""TopN through Executor.execute on the device (ops/topn_exec.py): a lazily
+opened holder answers cache-only and src-filtered TopN from the fragments'
+``.cache`` files and the HBM arena, with every fragment still cold afterwards,
+and the answers equal the host executor's (fragment.top two-phase TopN,
+executor.go:863-1000) computed on the same data before the lazy reopen."""
+import threading
+
+import numpy as np
+import pytest
+
+from pilosa_amd.executor import Executor
+from pilosa_amd.models.holder import Holder
+from tests.helpers import SW, Env
+
+pytestmark = pytest.mark.gpu
+
+QUERIES = ["TopN(h, n=10)", "TopN(h, n=100)", "TopN(h)", "TopN(h, n=20, threshold=300)",
+           "TopN(h, Row(f=1), n=5)", "TopN(h, Row(f=0), n=50)", "TopN(h, Row(h=3), n=20)",
+           "TopN(h, Row(f=2), n=7, threshold=2)", "TopN(h, ids=[1, 5, 7, 2999])",
+           "TopN(h, Row(f=1), ids=[0, 2, 4, 6, 8])", "TopN(h, Intersect(Row(f=0), Row(f=1)), n=10)"]
+
+
+@pytest.fixture(scope="module")
+def lazy_env():
+    """(lazy holder, GPU executor, {query: host answer}, multi-call answer)."""
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    env = Env()
+    rng = np.random.default_rng(7)
+    env.create_index("i")
+    env.field("i", "f")
+    env.field("i", "h", cache_type="ranked", cache_size=2000)
+    idx = env.holder.index("i")
+    nshard = 3
+    for r in range(4):
+        k = int([0.3, 0.05, 0.01, 0.002][r] * nshard * SW)
+        idx.field("f").import_bits(np.full(k, r, np.uint64),
+                                   rng.choice(nshard * SW, size=k, replace=False).astype(np.uint64))
+    hr = (rng.zipf(1.3, size=300000) % 3000).astype(np.uint64)
+    hc = rng.integers(0, nshard * SW, size=len(hr)).astype(np.uint64)
+    idx.field("h").import_bits(hr, hc)
+    for frag in env.holder.all_fragments():
+        frag.rebuild_cache()
+        frag.flush_cache()
+    want = {q: env.q1("i", q) for q in QUERIES}
+    want_multi = env.q("i", " ".join(QUERIES[:8]))
+    env.holder.close()
+    holder = Holder(env.dir, lazy_fragments=True).open()
+    gpu = GpuExecutor(holder, "cuda:0")
+    ex = Executor(holder, gpu=gpu)
+    gpu.executor = ex
+    ex.strict_gpu = True
+    yield holder, ex, gpu, want, want_multi
+    ex.close()
+    holder.close()
+    env.executor.close()
+    import shutil
+    shutil.rmtree(env.dir, ignore_errors=True)
+
+
+def _pairs(r):
+    return [(p.id, p.count) for p in r]
+
+
+@pytest.mark.parametrize("q", QUERIES)
+def test_topn_executor_matches_host_and_stays_cold(lazy_env, q):
+    holder, ex, gpu, want, _ = lazy_env
+    n0 = gpu.launches
+    got = ex.execute("i", q).results[0]
+    assert gpu.launches > n0, "device path not taken"
+    assert _pairs(got) == _pairs(want[q])
+    frags = holder.view("i", "h", "standard").all_fragments()
+    assert frags and all(f.is_cold() for f in frags), "TopN read a fragment on the host"
+
+
+def test_multi_call_topn_request_one_batch(lazy_env):
+    holder, ex, gpu, want, want_multi = lazy_env
+    got = ex.execute("i", " ".join(QUERIES[:8])).results
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in want_multi]
+    assert all(f.is_cold() for f in holder.view("i", "h", "standard").all_fragments())
+
+
+def test_concurrent_topn_requests_coalesce(lazy_env):
+    holder, ex, gpu, want, _ = lazy_env
+    qs = [QUERIES[k % 8] for k in range(48)]
+    out = [None] * len(qs)
+    f0 = ex.topn_coalescer.fallbacks
+
+    def run(k):
+        out[k] = ex.execute("i", qs[k]).results[0]
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(len(qs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for k, q in enumerate(qs):
+        assert _pairs(out[k]) == _pairs(want[q]), q
+    assert ex.topn_coalescer.fallbacks == f0, (repr(ex.topn_coalescer.last_error), ex.topn_batch_declined, gpu.topn_decline)
+
+
+def test_rank_caches_from_cache_files_equal_host_caches(lazy_env):
+    """The device rank lists of cold fragments (.cache ids + arena counts)
+    are the host rank caches the reference's openCache builds."""
+    holder, ex, gpu, _, _ = lazy_env
+    shards = holder.index("i").available_shards()
+    rv = gpu.view_arena("i", "h", "standard", shards)
+    frags = [holder.fragment("i", "h", "standard", s) for s in shards]
+    rc = gpu._rank_caches("i", "h", shards, frags, rv)
+    assert rc.cold_shards == len(shards)
+    rows, counts = rc.host_lists()
+    from pilosa_amd import _roaring
+    for si, s in enumerate(shards):
+        with open(frags[si].path, "rb") as fh:
+            bm = _roaring.Bitmap.from_bytes(fh.read())
+        offs, ids, _ = _roaring.read_cache_files([frags[si].cache_path()])
+        host = sorted(((int(i), int(bm.count_range(int(i) * SW, (int(i) + 1) * SW))) for i in ids),
+                      key=lambda p: (-p[1], p[0]))
+        host = [p for p in host if p[1] > 0][:frags[si].cache_size]   # rankCache keeps cache_size entries
+        live = counts[si] > 0
+        assert list(zip(rows[si][live].tolist(), counts[si][live].tolist())) == host
+    assert all(f.is_cold() for f in frags)
+
+
+def test_topn_after_writes_uses_warm_caches(lazy_env):
+    """A fragment written to after open is warm: its live host cache feeds the
+    device ranks, and the answers still equal the host path."""
+    holder, ex, gpu, _, _ = lazy_env
+    ex.execute("i", "Set(5, h=2999) Set(6, h=2999) Set(7, h=2999)")
+    got = ex.execute("i", "TopN(h, n=15) TopN(h, Row(f=1), n=6)").results
+    ex.gpu = None
+    try:
+        want = ex.execute("i", "TopN(h, n=15) TopN(h, Row(f=1), n=6)").results
+    finally:
+        ex.gpu = gpu
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
