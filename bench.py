@@ -699,13 +699,13 @@ def bench_configs_disk(args, world, rank, dev, which):
             for name, texts in qs.items():
                 log(f"config 4: {name}")
                 dt_, load, last, first = run(texts, reps)
-                n_calls = texts[0].count("(field") if "x32" in name else 1
+                n_calls = texts[0].count("Sum(") if "x32" in name else 1
                 r4["queries"][name] = {"ms_per_request": round(dt_ * 1000, 3), "qps": round(n_calls / dt_, 1),
                                        "first_request_s": round(load, 2), "sample": last[:4]}
             r4["device_launches"] = gpu.launches - l0
+            r4["fragments_cold"] = sum(f.is_cold() for f in holder.view("c", "v", "bsig_v").all_fragments())
             r4["verify"] = verify(["Sum(field=v)", qs["Count(Row(v > x))"][0], qs["Count(Row(v >< [a,b]))"][0],
                                    "Min(field=v)", "Max(field=v)", qs["Sum(Row(g=r), field=v) x32 per request"][0]])
-            r4["fragments_cold"] = sum(f.is_cold() for f in holder.view("c", "v", "bsig_v").all_fragments())
             res["config4_bsi"] = r4
         if "5" in which:
             B = 1024

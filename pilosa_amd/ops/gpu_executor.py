@@ -346,35 +346,7 @@ class GpuExecutor:
             o = self.engine.bsi_minmax(filt, bv, b.bit_depth)
         except CompileError:
             raise NotImplementedError
-        out = []
-        for si in range(len(shards)):
-            k = o[si]
-            npos, nneg = int(k[:, 8].sum()), int(k[:, 9].sum())
-            if npos + nneg == 0:
-                out.append(ValCount())
-                continue
-            if which == "min":
-                if nneg:  # -(max magnitude among negatives)
-                    sel = k[k[:, 9] > 0]
-                    v = int(sel[:, 0].max())
-                    cnt = int(sel[sel[:, 0] == v][:, 1].sum())
-                    v = -v
-                else:
-                    sel = k[k[:, 8] > 0]
-                    v = int(sel[:, 2].min())
-                    cnt = int(sel[sel[:, 2] == v][:, 3].sum())
-            else:
-                if npos:
-                    sel = k[k[:, 8] > 0]
-                    v = int(sel[:, 4].max())
-                    cnt = int(sel[sel[:, 4] == v][:, 5].sum())
-                else:  # all negative: -(min magnitude), fragment.max quirk
-                    sel = k[k[:, 9] > 0]
-                    v = int(sel[:, 6].min())
-                    cnt = int(sel[sel[:, 6] == v][:, 7].sum())
-                    v = -v
-            out.append(ValCount(v + b.base, cnt))
-        return out
+        return [ValCount(v + b.base, n) if n else ValCount() for v, n in zip(*_minmax_per_shard(o, which))]
 
     def hbm_bytes(self) -> int:
         with self.mu:
@@ -1271,6 +1243,36 @@ class GpuExecutor:
             return rows
         lo = start[len(prefix)]
         return [r for r in rows if r >= lo]
+
+
+def _minmax_per_shard(o: np.ndarray, which: str):
+    """Per-shard (value, count) of the BSI min/max descents ``o`` int64[S, 16, 10]
+    (bitmap_kernels.hip bsi_minmax_kernel, per key: 0/1 max |neg| + count,
+    2/3 min pos, 4/5 max pos, 6/7 min |neg|, 8/9 any pos / any neg), vectorised
+    over the shards with fragment.min/max's sign rules (fragment.go:1145-1225);
+    count 0 = no value in the shard."""
+    big = np.iinfo(np.int64).max
+    pos = o[:, :, 8] > 0
+    neg = o[:, :, 9] > 0
+    anyp, anyn = pos.any(axis=1), neg.any(axis=1)
+
+    def pick(vcol, ccol, mask, largest):
+        v = np.where(mask, o[:, :, vcol], -1 if largest else big)
+        best = v.max(axis=1) if largest else v.min(axis=1)
+        cnt = np.where(mask & (o[:, :, vcol] == best[:, None]), o[:, :, ccol], 0).sum(axis=1)
+        return best, cnt
+
+    if which == "min":
+        vn, cn = pick(0, 1, neg, True)      # -(max magnitude among negatives)
+        vp, cp = pick(2, 3, pos, False)
+        val = np.where(anyn, -vn, vp)
+        cnt = np.where(anyn, cn, np.where(anyp, cp, 0))
+    else:
+        vp, cp = pick(4, 5, pos, True)
+        vn, cn = pick(6, 7, neg, False)     # all negative: -(min magnitude), fragment.max quirk
+        val = np.where(anyp, vp, -vn)
+        cnt = np.where(anyp, cp, np.where(anyn, cn, 0))
+    return val.tolist(), cnt.tolist()
 
 
 def _has_shift(e) -> bool:
