@@ -22,12 +22,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--shards", type=int, default=0, help="0 = full 954")
-    ap.add_argument("--cq", default="0,32,64", help="chunk sizes for variant 1")
-    ap.add_argument("--cq2", default="", help="chunk sizes for variant 2")
-    ap.add_argument("--cq3", default="", help="chunk sizes for variant 3")
+    ap.add_argument("--cq", default="0,32,64", help="pair-kernel chunk sizes (queries per wave)")
     ap.add_argument("--no-tile", action="store_true", help="skip the generic tile kernel")
     ap.add_argument("--variants", default="", help="extra kernel variants at --cq's first size, e.g. 4,5")
-    ap.add_argument("--dbg", action="store_true", help="also time the cost-isolation variants 11-15")
     args = ap.parse_args()
     import torch
 
@@ -48,14 +45,8 @@ def main():
     ref = None
     configs = [] if args.no_tile else [("tile", {"use_and2": False})]
     configs += [(f"and2_cq{c}", {"and2_cq": int(c), "and2_variant": 1}) for c in args.cq.split(",") if c]
-    configs += [(f"and2v2_cq{c}", {"and2_cq": int(c), "and2_variant": 2}) for c in args.cq2.split(",") if c]
-    configs += [(f"and2v3_cq{c}", {"and2_cq": int(c), "and2_variant": 3}) for c in args.cq3.split(",") if c]
     cq0 = int(args.cq.split(",")[0]) if args.cq else 64
     configs += [(f"and2var{v}_cq{cq0}", {"and2_cq": cq0, "and2_variant": int(v)}) for v in args.variants.split(",") if v]
-    if args.dbg:
-        configs += [("dbg_nostage", {"and2_variant": 11}), ("dbg_nocount", {"and2_variant": 12}),
-                    ("dbg_neither", {"and2_variant": 13}), ("dbg_no_b_loads", {"and2_variant": 14}),
-                    ("dbg_no_probes", {"and2_variant": 15})]
     for name, cfg in configs:
         eng = GpuEngine(dev)
         for k, v in cfg.items():
