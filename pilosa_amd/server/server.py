@@ -572,12 +572,26 @@ class Server:
             if msg.get("nodeStatus"):
                 # the coordinator's view of which shards exist cluster-wide
                 self._merge_node_status(msg["nodeStatus"])
-            for src in msg.get("sources", []):
+            # pull sources a few at a time (resizeFollower fetches per source;
+            # cluster.go:1378-1460) and stop as soon as the job is aborted: the
+            # coordinator's abort leaves RESIZING through the status push
+            from concurrent.futures import ThreadPoolExecutor
+
+            def pull(src):
+                if self._resize_aborted():
+                    raise PilosaError("resize aborted")
                 sn = Node.from_json(src["node"])
                 data = self.client.fragment_data(sn.uri, src["index"], src["field"], src["view"], src["shard"])
+                if self._resize_aborted():
+                    raise PilosaError("resize aborted")
                 f = self.holder.field(src["index"], src["field"])
                 frag = f.create_view_if_not_exists(src["view"]).create_fragment_if_not_exists(src["shard"])
                 frag.read_from(io.BytesIO(data))
+            srcs = msg.get("sources", [])
+            if srcs:
+                with ThreadPoolExecutor(max_workers=min(4, len(srcs))) as pool:
+                    for fut in [pool.submit(pull, s_) for s_ in srcs]:
+                        fut.result()
         except Exception as e:  # noqa: BLE001
             err = str(e)
         done = {"type": "ResizeInstructionComplete", "jobID": msg["jobID"], "node": self.node.to_json(),
@@ -659,24 +673,39 @@ class Server:
             self.gpu.invalidate()
 
     # ------------------------------------------------------------ anti-entropy
+    def _resize_aborted(self) -> bool:
+        return self._closing.is_set() or self.cluster.state != STATE_RESIZING
+
     def _anti_entropy_loop(self):
         while not self._closing.wait(self.anti_entropy_interval):
             if self.cluster.state != STATE_NORMAL:
                 continue
             try:
-                self.sync_holder()
+                if not self.sync_holder():
+                    self.logger.printf("anti-entropy: pass aborted (cluster state %s)", self.cluster.state)
             except Exception as e:  # noqa: BLE001
                 self.logger.printf("anti-entropy: %s", e)
 
-    def sync_holder(self):
-        """One anti-entropy pass over every local fragment and attr store."""
+    def _sync_should_abort(self) -> bool:
+        """holderSyncer.IsClosing: a pass stops once the node closes or the
+        cluster leaves NORMAL (a resize began), cluster.go:253-275,465."""
+        return self._closing.is_set() or self.cluster.state != STATE_NORMAL
+
+    def sync_holder(self) -> bool:
+        """One anti-entropy pass over every local fragment and attr store.
+        Returns False when the pass was aborted part-way."""
         for idx in list(self.holder.indexes.values()):
+            if self._sync_should_abort():
+                return False
             self._sync_attrs(idx.name, None, idx.column_attr_store)
             for f in list(idx.fields.values()):
                 self._sync_attrs(idx.name, f.name, f.row_attr_store)
                 for v in list(f.views.values()):
                     for shard, frag in list(v.fragments.items()):
+                        if self._sync_should_abort():
+                            return False
                         self._sync_fragment(idx.name, f.name, v.name, shard, frag)
+        return True
 
     def _sync_attrs(self, index, field, store):
         blocks = [{"id": b, "checksum": c.hex()} for b, c in store.blocks()]

@@ -164,3 +164,29 @@ def test_replication_and_failover():
     finally:
         for s in servers:
             s.close()
+
+
+def test_anti_entropy_pass_aborts_when_resize_begins():
+    """holderSyncer stops mid-pass once the cluster leaves NORMAL
+    (cluster.go:253-275,465): a diverged replica is left alone while the
+    cluster is RESIZING and repaired by the next pass in NORMAL."""
+    from pilosa_amd.parallel.cluster import STATE_NORMAL, STATE_RESIZING
+    servers = _cluster(2, replicas=2)
+    try:
+        s0, s1 = servers
+        c = InternalClient()
+        c.create_index(s0.uri, "i")
+        c.create_field(s0.uri, "i", "f", {"type": "set"})
+        time.sleep(0.2)
+        c.query(s0.uri, "i", "Set(1, f=3)")
+        s1.holder.fragment("i", "f", "standard", 0).set_bit(9, 5)
+        s0.cluster.set_state(STATE_RESIZING)
+        assert s0.sync_holder() is False
+        assert s0.holder.fragment("i", "f", "standard", 0).row_count(9) == 0
+        s0.cluster.set_state(STATE_NORMAL)
+        assert s0.sync_holder() is True
+        assert s0.holder.fragment("i", "f", "standard", 0).row_count(9) == \
+            s1.holder.fragment("i", "f", "standard", 0).row_count(9) == 1
+    finally:
+        for s in servers:
+            s.close()
