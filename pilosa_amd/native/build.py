@@ -113,6 +113,37 @@ def build_translate(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+HOST_MODULES = {
+    "_roaring": ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp"),
+    "_pql": ("pql_parser.cpp", "pql_compile.cpp"),
+    "_httpd": ("httpd.cpp",),
+    "_translate": ("translate.cpp",),
+}
+
+
+def build_sanitized(name: str, sanitize: str, outdir: str, verbose: bool = False) -> str:
+    """A host module built with ``-fsanitize=<sanitize>`` into ``outdir``
+    (never in-tree: the sanitizer runtime has to be preloaded into the
+    interpreter that imports it).  Used by tests/test_native_sanitizers.py."""
+    import pybind11
+
+    os.makedirs(outdir, exist_ok=True)
+    out = os.path.join(outdir, name + _ext_suffix())
+    srcs = [os.path.join(HERE, f) for f in HOST_MODULES[name]]
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={sanitize}"]
+    if "undefined" in sanitize:
+        flags.append("-fno-sanitize-recover=undefined")
+    if name == "_roaring":
+        flags += ["-mpopcnt", "-mbmi2", "-mavx2"]
+    cmd = [cxx, "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *flags, "-I", pybind11.get_include(),
+           "-I", sysconfig.get_paths()["include"], *srcs, "-o", out, "-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return out
+
+
 def hip_sources():
     return [os.path.join(KDIR, f) for f in sorted(os.listdir(KDIR))
             if f.endswith((".hip", ".cpp", ".h", ".hpp"))]

@@ -188,6 +188,42 @@ static int split_calls(const std::string& t, bool* all_count) {
   return calls;
 }
 
+// Strict UTF-8 (no overlongs, surrogates or code points past U+10FFFF): the
+// request head reaches Python as str, so anything else is refused with 400.
+static bool valid_utf8(const char* s, size_t n) {
+  const auto* p = reinterpret_cast<const unsigned char*>(s);
+  size_t i = 0;
+  while (i < n) {
+    const unsigned c = p[i];
+    if (c < 0x80) {
+      i++;
+      continue;
+    }
+    size_t len;
+    unsigned cp;
+    if ((c & 0xE0) == 0xC0) len = 2, cp = c & 0x1F;
+    else if ((c & 0xF0) == 0xE0) len = 3, cp = c & 0x0F;
+    else if ((c & 0xF8) == 0xF0) len = 4, cp = c & 0x07;
+    else return false;
+    if (i + len > n) return false;
+    for (size_t k = 1; k < len; k++) {
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (p[i + k] & 0x3F);
+    }
+    if ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && cp < 0x10000) || cp > 0x10FFFF ||
+        (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    i += len;
+  }
+  return true;
+}
+
+static py::str str_lossy(const std::string& s) {
+  PyObject* o = PyUnicode_DecodeUTF8(s.data(), Py_ssize_t(s.size()), "replace");
+  if (!o) throw py::error_already_set();
+  return py::reinterpret_steal<py::str>(o);
+}
+
 static bool accept_json(const std::string& acc) {
   if (acc.empty()) return true;
   size_t p = 0;
@@ -291,8 +327,9 @@ class Server {
     py::list out;
     for (auto& r : got) {
       py::list hs;
-      for (auto& kv : r->headers) hs.append(py::make_tuple(kv.first, kv.second));
-      out.append(py::make_tuple(r->id, r->method, r->path, r->query, hs, py::bytes(r->body)));
+      for (auto& kv : r->headers) hs.append(py::make_tuple(str_lossy(kv.first), str_lossy(kv.second)));
+      out.append(py::make_tuple(r->id, str_lossy(r->method), str_lossy(r->path), str_lossy(r->query), hs,
+                                py::bytes(r->body)));
     }
     return out;
   }
@@ -329,7 +366,7 @@ class Server {
         ids.append(got[i]->id);
         nc.append(got[i]->ncalls);
       }
-      out.append(py::make_tuple(groups[g].first, ids, nc, py::str(texts[g])));
+      out.append(py::make_tuple(str_lossy(groups[g].first), ids, nc, str_lossy(texts[g])));
     }
     return out;
   }
@@ -404,9 +441,14 @@ class Server {
   void pop(int kind, size_t max_n, int timeout_ms, std::vector<std::shared_ptr<Req>>& got) {
     std::unique_lock<std::mutex> g(qmu_);
     auto& q = q_[kind];
+    // system_clock deadline: its wait maps to pthread_cond_timedwait, which
+    // ThreadSanitizer intercepts (a steady_clock wait_for goes through
+    // pthread_cond_clockwait, which gcc-11's TSan does not, and then reports a
+    // false double lock); the wait is a short poll, so clock jumps only end it
+    // early or late by that much
     if (q.empty())
-      qcv_.wait_for(g, std::chrono::milliseconds(std::max(0, timeout_ms)),
-                    [&] { return !q.empty() || stopping_; });
+      qcv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms)),
+                      [&] { return !q.empty() || stopping_; });
     while (!q.empty() && got.size() < max_n) {
       got.push_back(std::move(q.front()));
       q.pop_front();
@@ -602,6 +644,11 @@ class Server {
           native_reply(c, c.next_seq++, 431, "request header too large\n", true);
           ok = false;
         }
+        break;
+      }
+      if (!valid_utf8(c.in.data() + off, he - off)) {
+        native_reply(c, c.next_seq++, 400, "request head is not valid UTF-8\n", true);
+        ok = false;
         break;
       }
       // request line

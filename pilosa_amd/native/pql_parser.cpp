@@ -161,7 +161,19 @@ class Parser {
   }
 
   // ------------------------------------------------------------ calls
+  // Nesting guard: the reference's PEG runs on growable goroutine stacks; a
+  // fixed native stack needs a bound (pql/parser.py MAX_NESTING, same value).
+  static constexpr int MAX_NESTING = 1000;
+  int depth_ = 0;
+  struct Nest {
+    int& d;
+    explicit Nest(int& d_) : d(d_) { ++d; }
+    ~Nest() { --d; }
+  };
+
   size_t call(size_t i, py::object& out) {
+    Nest guard(depth_);
+    if (depth_ > MAX_NESTING) parse_error("query nesting exceeds " + std::to_string(MAX_NESTING) + " levels");
     std::string name;
     size_t j = ident(i, name);
     static const char* lits[] = {"Set", "SetRowAttrs", "SetColumnAttrs", "Clear", "ClearRow",

@@ -340,13 +340,19 @@ class Store {
         keys.append(py::bytes(reinterpret_cast<const char*>(d + q), kl));
         q += kl;
       }
-      out.append(py::make_tuple(int(e.type), e.index, e.field, ids, keys, e.end - at));
+      // names come from the file: decode lossily so a damaged log can still be inspected
+      out.append(py::make_tuple(int(e.type), lossy(e.index), lossy(e.field), ids, keys, e.end - at));
       at = e.end;
     }
     return out;
   }
 
  private:
+  static py::str lossy(const std::string& s) {
+    PyObject* o = PyUnicode_DecodeUTF8(s.data(), Py_ssize_t(s.size()), "replace");
+    if (!o) throw py::error_already_set();
+    return py::reinterpret_steal<py::str>(o);
+  }
   void check_open() const {
     if (closed_) throw std::runtime_error("translate store " + path_ + " is closed");
   }

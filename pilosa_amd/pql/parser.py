@@ -14,6 +14,9 @@ from typing import Any, List, Optional, Tuple
 from .ast import BETWEEN, EQ, GT, GTE, LT, LTE, NEQ, Call, Condition, Query
 
 
+# nesting bound shared with native/pql_parser.cpp (Parser::MAX_NESTING)
+MAX_NESTING = 1000
+
 class ParseError(Exception):
     pass
 
@@ -94,6 +97,9 @@ class Parser:
                 i, c = self.call(i)
             except _Fail:
                 raise ParseError(self._err(i))
+            except RecursionError:
+                # the native parser bounds nesting at MAX_NESTING levels
+                raise ParseError(f"query nesting exceeds {MAX_NESTING} levels") from None
             calls.append(c)
             i = self.sp(i)
         return Query(calls)
