@@ -125,6 +125,10 @@ class Fragment:
         # A GPU node reads cold fragments straight into HBM instead
         # (native/arena_io.cpp), so the host never holds their containers.
         self.lazy = False
+        # cold host access: a copy-on-write mmap view of the file
+        # (_roaring.MappedBitmap) serves membership, counts, row reads, the
+        # rank cache and single-bit writes without reading the file into heap
+        self._mapped = None
         self._flags_hint = 0
         self._cache_pending = False
         self.version = 0
@@ -164,7 +168,9 @@ class Fragment:
     @property
     def cache(self):
         if self._cache_pending:
-            self._load_cold()
+            with self.mu:
+                if self._cache_pending:
+                    self._open_cache()   # counts from the mapped file (fragment.go openCache)
         return self._cache
 
     @cache.setter
@@ -173,8 +179,8 @@ class Fragment:
 
     @property
     def max_row_id(self) -> int:
-        if self._storage is None:
-            self._load_cold()
+        if self._storage is None and self._mapped is None:
+            self._cold()
         return self._max_row_id
 
     @max_row_id.setter
@@ -182,9 +188,37 @@ class Fragment:
         self._max_row_id = v
 
     def is_cold(self) -> bool:
-        """True while the storage has not been read from the file (the file
-        is exactly the fragment's state: any write loads it first)."""
+        """True while the storage has not been read into heap.  The file is
+        exactly the fragment's state: writes to a cold fragment go to the
+        mapped view's overlay and to the op log appended to the file."""
         return self._storage is None
+
+    def _cold(self):
+        """The mapped view of a cold fragment (created on first use)."""
+        with self.mu:
+            m = self._mapped
+            if m is None:
+                try:
+                    m = _roaring.MappedBitmap(self.path)
+                except Exception as e:  # noqa: BLE001
+                    raise PilosaError(f"unmarshal storage: file={self.path}, err={e}")
+                self._mapped = m
+                self.opn, self.ops = int(m.opn), int(m.ops)
+                self._max_row_id = int(m.max()) // SHARD_WIDTH if m.any() else 0
+            return m
+
+    def _rw(self):
+        """Storage for the operations the mapped view offers: the heap
+        Bitmap once materialised, else the mapped view."""
+        s = self._storage
+        return s if s is not None else self._cold()
+
+    def mapped_stats(self) -> Optional[dict]:
+        m = self._mapped
+        if m is None or self._storage is not None:
+            return None
+        return {"mapped_bytes": int(m.mapped_bytes), "containers": int(m.mapped_containers),
+                "overlay_containers": int(m.overlay_containers)}
 
     def _read_storage(self) -> Bitmap:
         with open(self.path, "rb") as fh:
@@ -201,6 +235,7 @@ class Fragment:
                 self.opn = int(bm.opn)
                 self.ops = int(bm.ops)
                 self._storage = bm
+                self._mapped = None   # the file holds every write the mapped view took
                 self._max_row_id = int(bm.max()) // SHARD_WIDTH if bm.any() else 0
             if self._cache_pending:
                 self._cache_pending = False
@@ -258,15 +293,15 @@ class Fragment:
                 m.ParseFromString(fh.read())
         except Exception:  # noqa: BLE001 - a corrupt cache is rebuilt
             return
-        st = self.storage
+        st = self._rw()
         for rid in m.IDs:
             n = st.count_range(rid * SHARD_WIDTH, (rid + 1) * SHARD_WIDTH)
             self._cache.bulk_add(rid, n)
         self._cache.invalidate()
 
     def flush_cache(self):
-        if self.cache_type == CACHE_TYPE_NONE or self._storage is None or self._cache_pending:
-            return  # cold fragment: the cache file on disk is current
+        if self.cache_type == CACHE_TYPE_NONE or self._cache_pending:
+            return  # cache never opened: the cache file on disk is current
         from pilosa_amd.wire import pb
         with self.mu:
             ids = self.cache.ids()
@@ -392,18 +427,18 @@ class Fragment:
     # ------------------------------------------------------------ rows
     def row(self, row_id: int) -> Row:
         with self.mu:
-            bm = self.storage.offset_range(self.shard * SHARD_WIDTH, row_id * SHARD_WIDTH,
+            bm = self._rw().offset_range(self.shard * SHARD_WIDTH, row_id * SHARD_WIDTH,
                                            (row_id + 1) * SHARD_WIDTH)
         return Row.from_segment(self.shard, bm)
 
     def row_bitmap(self, row_id: int) -> Bitmap:
         with self.mu:
-            return self.storage.offset_range(self.shard * SHARD_WIDTH, row_id * SHARD_WIDTH,
+            return self._rw().offset_range(self.shard * SHARD_WIDTH, row_id * SHARD_WIDTH,
                                              (row_id + 1) * SHARD_WIDTH)
 
     def row_count(self, row_id: int) -> int:
         with self.mu:
-            return self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
+            return self._rw().count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
 
     def row_intersection_count(self, row_id: int, other: "Fragment", other_row: int) -> int:
         """|row_id ∩ other.other_row| read in place (no row extraction).
@@ -428,7 +463,9 @@ class Fragment:
         return pos(row_id, col)
 
     def bit(self, row_id: int, col: int) -> bool:
-        return self.storage.contains(self._pos(row_id, col))
+        p = self._pos(row_id, col)
+        with self.mu:
+            return self._rw().contains(p)
 
     DIRTY_LIMIT = 4096
     DELTA_LIMIT = 1 << 24     # recorded positions per subscriber before falling back to container keys
@@ -500,7 +537,7 @@ class Fragment:
                 self._note_delta("pos", np.array([pos], np.uint64), clear, 1)
         self.checksums.pop(row_id // HASH_BLOCK_SIZE, None)
         if self.cache_type != CACHE_TYPE_NONE:
-            n = self.storage.count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
+            n = self._rw().count_range(row_id * SHARD_WIDTH, (row_id + 1) * SHARD_WIDTH)
             if bulk:
                 self.cache.bulk_add(row_id, n)
             else:
@@ -528,7 +565,7 @@ class Fragment:
 
     def _unprotected_set_bit(self, row_id: int, col: int) -> bool:
         p = self._pos(row_id, col)
-        changed = self.storage.add(p)
+        changed = self._rw().add(p)
         if not changed:
             return False
         self._log(OP_ADD, p)
@@ -540,7 +577,7 @@ class Fragment:
 
     def _unprotected_clear_bit(self, row_id: int, col: int) -> bool:
         p = self._pos(row_id, col)
-        changed = self.storage.remove(p)
+        changed = self._rw().remove(p)
         if not changed:
             return False
         self._log(OP_REMOVE, p)
@@ -565,7 +602,7 @@ class Fragment:
             return self._unprotected_clear_bit(row_id, col)
 
     def _vector_get(self, col: int) -> Optional[int]:
-        rows = self.storage.rows_with_column(col % SHARD_WIDTH, CONTAINERS_PER_ROW)
+        rows = self._rw().rows_with_column(col % SHARD_WIDTH, CONTAINERS_PER_ROW)
         if len(rows) > 1:
             raise PilosaError("found multiple row values for column")
         if len(rows) == 1:

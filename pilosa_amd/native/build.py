@@ -39,7 +39,7 @@ def build_roaring(force: bool = False, verbose: bool = False, stats: bool = Fals
 
     name = "_roaring_stats" if stats else "_roaring"
     out = os.path.join(PKG, name + _ext_suffix())
-    srcs = [os.path.join(HERE, f) for f in ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp")]
+    srcs = [os.path.join(HERE, f) for f in ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp", "mapped.cpp")]
     deps = srcs + [os.path.join(HERE, f) for f in ("roaring.hpp", "synth.hpp")]
     if not force and not _newer(out, deps):
         return out
@@ -114,7 +114,7 @@ def build_translate(force: bool = False, verbose: bool = False) -> str:
 
 
 HOST_MODULES = {
-    "_roaring": ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp"),
+    "_roaring": ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp", "mapped.cpp"),
     "_pql": ("pql_parser.cpp", "pql_compile.cpp"),
     "_httpd": ("httpd.cpp",),
     "_translate": ("translate.cpp",),

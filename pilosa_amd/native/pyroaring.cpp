@@ -657,6 +657,36 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
         return to_np(rows);
       }, py::arg("containers_per_row") = 16);
 
+  py::class_<pr::MappedBitmap>(m, "MappedBitmap",
+                               "Copy-on-write mmap view of a Pilosa fragment file (see roaring.hpp)")
+      .def(py::init<const std::string&>(), py::arg("path"))
+      .def("contains", &pr::MappedBitmap::contains)
+      .def("__contains__", &pr::MappedBitmap::contains)
+      .def("add", &pr::MappedBitmap::add)
+      .def("remove", &pr::MappedBitmap::remove)
+      .def("count", &pr::MappedBitmap::count)
+      .def("count_range", &pr::MappedBitmap::count_range)
+      .def("any", &pr::MappedBitmap::any)
+      .def("max", &pr::MappedBitmap::max)
+      .def("offset_range", &pr::MappedBitmap::offset_range)
+      .def("rows_with_column", [](const pr::MappedBitmap& b, uint64_t col, uint64_t cpr) {
+        return to_np(b.rows_with_column(col, cpr));
+      }, py::arg("col"), py::arg("containers_per_row") = 16)
+      .def("count_rows", [](const pr::MappedBitmap& b, u64arr rows, uint64_t cpr) {
+        const uint64_t* r = rows.data();
+        const py::ssize_t n = rows.size();
+        py::array_t<int64_t> out(n);
+        int64_t* o = out.mutable_data();
+        for (py::ssize_t i = 0; i < n; i++) o[i] = b.count_range((r[i] * cpr) << 16, ((r[i] + 1) * cpr) << 16);
+        return out;
+      }, py::arg("rows"), py::arg("containers_per_row") = 16)
+      .def_property_readonly("mapped_containers", &pr::MappedBitmap::mapped_containers)
+      .def_property_readonly("overlay_containers", &pr::MappedBitmap::overlay_containers)
+      .def_property_readonly("mapped_bytes", &pr::MappedBitmap::mapped_bytes)
+      .def_readonly("flags", &pr::MappedBitmap::flags)
+      .def_readonly("ops", &pr::MappedBitmap::ops)
+      .def_readonly("opn", &pr::MappedBitmap::opn);
+
   m.def("encode_op", [](uint8_t typ, uint64_t value, u64arr values, py::bytes roaring, uint32_t opn) {
     std::string r = roaring;
     const uint64_t* p = values.data();

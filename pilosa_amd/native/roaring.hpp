@@ -163,11 +163,65 @@ class Bitmap {
   // per-row deltas (row = key / containers_per_row)
   int64_t import_roaring(const uint8_t* data, size_t n, bool clear, uint64_t containers_per_row,
                          std::map<uint64_t, int64_t>* rowdelta);
+  // apply a Pilosa op log (13-byte ops + batches / roaring blobs) in order
+  void replay_ops(const uint8_t* data, size_t n);
 
  private:
   void parse_pilosa(const uint8_t* data, size_t n, size_t* ops_offset);
   void parse_official(const uint8_t* data, size_t n);
-  void replay_ops(const uint8_t* data, size_t n);
+};
+
+// Read-mostly view of a Pilosa fragment file through mmap (the reference's
+// frozen, mapped containers: roaring/container_stash.go:262-346,
+// roaring.go:1616-1622).  Lookups binary-search the mapped header and read
+// container payloads in place; the first write to a container copies it into
+// an owned overlay (copy-on-write), so a cold fragment that takes a few
+// writes holds only the containers those writes touched.  The file's own op
+// log is replayed into that overlay at open.  Only the operations a cold
+// fragment needs are offered (membership, counts, row extraction, single-bit
+// writes); anything else loads the whole file into a Bitmap.
+class MappedBitmap {
+ public:
+  explicit MappedBitmap(const std::string& path);
+  ~MappedBitmap();
+  MappedBitmap(const MappedBitmap&) = delete;
+  MappedBitmap& operator=(const MappedBitmap&) = delete;
+
+  bool contains(uint64_t v) const;
+  bool add(uint64_t v);
+  bool remove(uint64_t v);
+  int64_t count() const;
+  int64_t count_range(uint64_t start, uint64_t end) const;
+  bool any() const;
+  uint64_t max() const;
+  Bitmap offset_range(uint64_t offset, uint64_t start, uint64_t end) const;
+  std::vector<uint64_t> rows_with_column(uint64_t col, uint64_t cpr) const;
+  size_t mapped_containers() const { return keyn_; }
+  size_t overlay_containers() const { return touched_.size(); }
+  size_t mapped_bytes() const { return len_; }
+
+  uint8_t flags = 0;
+  int64_t ops = 0, opn = 0;
+
+ private:
+  int fd_ = -1;
+  const uint8_t* base_ = nullptr;
+  size_t len_ = 0;
+  uint32_t keyn_ = 0;
+  const uint8_t* hdr_ = nullptr;   // keyn x (key u64, type u16, n-1 u16)
+  const uint8_t* offs_ = nullptr;  // keyn x u32
+  Bitmap over_;                    // owned copies of touched containers
+  std::map<uint64_t, bool> touched_;  // keys whose authoritative copy is in over_ (absent there = empty)
+
+  uint64_t key_at(size_t i) const;
+  size_t lower(uint64_t key) const;                 // first header index with key >= key
+  int64_t find(uint64_t key) const;                 // header index of key, or -1
+  Container load(size_t i) const;                   // copy of mapped container i
+  int32_t mapped_n(size_t i) const;
+  bool span(size_t i, size_t* off, size_t* sz) const;  // payload extent of container i, false if corrupt
+  const uint8_t* payload(size_t i) const;              // checked payload pointer (throws if corrupt)
+  bool mapped_contains(size_t i, uint16_t low) const;
+  Container& cow(uint64_t key);
 };
 
 Container& get_or_create(Bitmap& b, uint64_t key);

@@ -1078,6 +1078,22 @@ class GpuEngine:
         self.ext.and2_count(tp, tv, S, pairs, partial, self.and2_cq, self.and2_variant)
         return partial.view(S, 16, n)
 
+    def to_host(self, t):
+        """Device tensor -> host tensor through a pinned buffer and an event
+        wait.  A plain ``.cpu()`` is a synchronous pageable D2H copy: the HIP
+        runtime stages it with blit kernels and holds the stream while it
+        waits, so other request threads cannot enqueue their next batch and
+        the GPU idles between batches (profiles/r03_clients)."""
+        torch = self.torch
+        if t.device.type != "cuda":
+            return t
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        return h
+
     def launch_count(self, handle):
         """Device half: launch the kernels; returns the device int64[Q] result."""
         torch = self.torch

@@ -490,7 +490,7 @@ class GpuExecutor:
         if comp.fallbacks:
             return None  # rows missing from every arena (EMPTY) etc.: planner path
         self.launches += 1
-        return [int(v) for v in self.engine.launch_count(self.engine.prepare_progs(progs, vlist, S)).cpu().tolist()]
+        return self.engine.to_host(self.engine.launch_count(self.engine.prepare_progs(progs, vlist, S))).tolist()
 
     def try_count_text(self, index: str, text: str, shards: List[int]) -> Optional[List[int]]:
         """A whole request of ``Count(<Row/set-op tree>)`` calls, compiled from
@@ -524,7 +524,7 @@ class GpuExecutor:
             return None
         Q, segs, buf = got
         self.launches += 1
-        return eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S)).cpu().tolist()
+        return eng.to_host(eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S))).tolist()
 
     TIME_GROUP_MIN = 2
 

@@ -137,7 +137,8 @@ def test_lazy_fragment_close_keeps_files_and_cache():
         env.executor.holder = env.holder
         fr = _frags(env)[0]
         assert fr.is_cold()
-        assert fr.cache.ids() and not fr.is_cold()  # the cache pulls the storage in
+        # the cache opens from the mmapped file (fragment.go openCache): still cold
+        assert fr.cache.ids() and fr.is_cold() and fr.mapped_stats() is not None
     finally:
         env.close()
 

@@ -176,3 +176,53 @@ def test_native_matches_python_on_generated_queries():
     for _ in range(300):
         src = f"Count({gen(4)})"
         assert P.parse_string(src).calls == P.parse_string_py(src).calls
+
+
+_SEEDS = ["Count(Row(f=1))", "Count(Intersect(Row(f=1), Row(g='k')))", "Set(1, f=2, 2019-01-01T00:00)",
+          "TopN(f, Row(g=1), n=5, ids=[1,2])", "Row(1 < v <= 100)", 'SetRowAttrs(f, 1, a="x\\"y", b=1.5)',
+          "Rows(f, previous=10, limit=5, column=3)", "GroupBy(Rows(f), Rows(g), limit=3, filter=Row(h=1))",
+          "Options(Count(Row(f=1)), shards=[0, 1], excludeColumns=true)", "Range(t=1, 2018-01-01T00:00, 2019-01-01T00:00)",
+          "Clear(1, f=2) ClearRow(f=3) Store(Row(f=1), g=2)", "Not(Row(f=-1))", "Row(f != null)", "Count(Shift(Row(f=1), n=2))"]
+
+
+@pytest.mark.skipif("native" not in PARSERS, reason="native parser not built")
+def test_native_matches_python_on_mutated_input_fuzz():
+    """Differential fuzz (hypothesis): byte-level mutations of valid queries.
+    The native parser and the Python spec parser must agree on accept vs
+    ParseError and, when both accept, on the AST (the reference's PEG is the
+    single grammar both implement, pql/pql.peg)."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    alphabet = st.sampled_from(list("()[],=<>!\"' .-_:abfgnvxyz0123456789TRCU\n\t") + ["\\", "é", "\x00"])
+
+    @settings(max_examples=1500, deadline=None, suppress_health_check=list(HealthCheck), derandomize=True)
+    @given(st.sampled_from(_SEEDS), st.lists(st.tuples(st.integers(0, 200), st.integers(0, 3), alphabet),
+                                             max_size=4))
+    def run(seed, edits):
+        s = list(seed)
+        for pos, op, ch in edits:
+            pos = pos % (len(s) + 1)
+            if op == 0 and pos < len(s):
+                s[pos] = ch
+            elif op == 1:
+                s.insert(pos, ch)
+            elif op == 2 and pos < len(s):
+                del s[pos]
+            else:
+                del s[pos:]
+        src = "".join(s)
+        try:
+            want = P.parse_string_py(src).calls
+        except P.ParseError:
+            want = None
+        except (ValueError, OverflowError, TypeError):
+            want = "error"
+        try:
+            got = P.parse_string(src).calls
+        except P.ParseError:
+            got = None
+        except (ValueError, OverflowError, TypeError):
+            got = "error"
+        assert got == want, src
+    run()
