@@ -969,6 +969,10 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
         nxt = [0]
         err = []
 
+        from pilosa_amd.executor import ExecOptions
+        dopt = ExecOptions()
+        dopt.device_counts = world > 1   # N>1: counts stay on the device for the all-reduce
+
         def client(end):
             while True:
                 with lock:
@@ -977,7 +981,12 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
                         return
                     nxt[0] += 1
                 try:
-                    results[i] = ex.execute("i", texts[i], shards=shards).results
+                    r = ex.execute("i", texts[i], shards=shards, opt=dopt).results
+                    if world > 1 and isinstance(r, torch.Tensor):
+                        ev = torch.cuda.Event()
+                        ev.record()      # the batch's kernels, on this thread's stream
+                        r = (r, ev)
+                    results[i] = r
                 except BaseException as e:  # noqa: BLE001
                     err.append(e)
                     return
@@ -999,9 +1008,15 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
                     if err:
                         break
                     with torch.cuda.stream(comm_stream):
-                        tt = torch.tensor(results[i], dtype=torch.int64, device=dev)
+                        r = results[i]
+                        if isinstance(r, tuple):   # device counts: reduce them in place
+                            tt, ev = r
+                            comm_stream.wait_event(ev)
+                            tt.record_stream(comm_stream)
+                        else:
+                            tt = torch.tensor(r, dtype=torch.int64, device=dev)
                         all_reduce(tt)
-                        results[i] = tt.cpu().tolist()
+                        results[i] = gpu.engine.to_host(tt).tolist()
             for t in ts:
                 t.join()
             if err:
@@ -1037,10 +1052,142 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
         if args.topn_batches > 0:
             extra["topn"] = bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev)
         holder.close()
+        if args.serve_seconds > 0 and world == 1:
+            # the server opens the same data dir itself: free this process's arena first
+            ex.close()
+            del ex, gpu, view
+            import gc
+            gc.collect()
+            torch.cuda.empty_cache()
+            extra["serving"] = bench_serving(args, base, dev)
         return elapsed, extra
     finally:
         if own and not args.keep_data:
             shutil.rmtree(base, ignore_errors=True)
+
+
+def bench_serving(args, base, dev):
+    """The server product path on the same data dir:
+    ``Server`` (lazy holder, GPU executor, native epoll HTTP front end,
+    group-commit of concurrent Count requests) under the closed-loop C++ load
+    generator: ``--serve-conns`` keep-alive connections, one
+    ``Count(Intersect(Row, Row))`` per request for ``--serve-seconds``, then a
+    Count + TopN(f, n=100) mix; sampled responses are checked against
+    ``Executor.execute``.  Then a bulk import through POST /import (protobuf
+    ImportRequest, one per shard, concurrent clients) into the cold fragments
+    (mapped copy-on-write containers), and the first query after it, which
+    replays the write batches of every shard on the device in shared launches.
+    Reference: http/handler.go:293,495 (query, import routes)."""
+    import http.client
+    import threading
+
+    from pilosa_amd import _httpd
+    from pilosa_amd.server.server import Server
+    from pilosa_amd.utils.logger import CaptureLogger
+    from pilosa_amd.wire import pb
+
+    out = {"path": "Server(data dir) -> native httpd -> Executor (group commit) -> GPU"}
+    t0 = time.perf_counter()
+    srv = Server(base, bind="127.0.0.1:0", gpu="on", logger=CaptureLogger()).open()
+    try:
+        ex = srv.executor
+        rng = np.random.default_rng(77)
+        a, b = zipf_rows(rng, 20000, args.rows), zipf_rows(rng, 20000, args.rows)
+        queries = [f"Count(Intersect(Row(f={x}), Row(f={y})))" for x, y in zip(a, b)]
+        ex.execute("i", queries[0])   # loads the view into HBM
+        out["open_and_load_s"] = round(time.perf_counter() - t0, 2)
+        port = srv.uri.port
+
+        def run(bodies, seconds, samples):
+            log(f"serving: {len(bodies)} bodies, {args.serve_conns} conns, {seconds} s")
+            res = _httpd.load("127.0.0.1", port, "/index/i/query", [q.encode() for q in bodies], args.serve_conns,
+                              4, float(seconds), samples)
+            mism = 0
+            smp = res.pop("samples", [])
+            for k, body in smp:
+                want = ex.execute("i", bodies[k]).results
+                got = json.loads(body)["results"]
+                if [r if isinstance(r, int) else [[p.id, p.count] for p in r] for r in want] != \
+                        [r if isinstance(r, int) else [[p["id"], p["count"]] for p in r] for r in got]:
+                    mism += 1
+            fe = res.pop("first_error", b"")
+            return {"req_per_s": round(res["requests"] / seconds, 1), "requests": int(res["requests"]),
+                    "errors": int(res["errors"]), "p50_ms": round(res.get("p50_ms", 0.0), 3),
+                    "p99_ms": round(res.get("p99_ms", 0.0), 3), "mean_ms": round(res.get("mean_ms", 0.0), 3),
+                    "verified": len(smp), "mismatches": mism,
+                    "first_error": fe[:200].decode(errors="replace") if fe else ""}
+        out["count"] = run(queries, args.serve_seconds, 64)
+        mix = [q if k % 10 else "TopN(f, n=100)" for k, q in enumerate(queries[:2000])]
+        out["count_topn_mix"] = dict(run(mix, max(2.0, args.serve_seconds / 2), 32), topn_fraction=0.1)
+        out["conns"] = args.serve_conns
+        out["httpd"] = srv.httpd.stats() if hasattr(srv.httpd, "stats") else None
+
+        # ---- bulk import through the HTTP API
+        nsh = min(args.import_shards, len(srv.holder.index("i").available_shards()))
+        per = args.import_bits_per_shard
+        irng = np.random.default_rng(5)
+        bodies = []
+        for s in range(nsh):
+            rows = zipf_rows(irng, per, 1000).astype(np.uint64)
+            cols = (np.uint64(s) << np.uint64(20)) + irng.integers(0, 1 << 20, size=per).astype(np.uint64)
+            bodies.append((s, rows, cols, pb.ImportRequest(Index="i", Field="f", Shard=s, RowIDs=rows.tolist(),
+                                                           ColumnIDs=cols.tolist()).SerializeToString()))
+        rss0 = _rss_gb()
+        errs = []
+        nxt = [0]
+        lock = threading.Lock()
+
+        def importer():
+            conn = http.client.HTTPConnection("127.0.0.1", port, timeout=300)
+            while True:
+                with lock:
+                    k = nxt[0]
+                    nxt[0] += 1
+                if k >= len(bodies):
+                    return
+                conn.request("POST", "/index/i/field/f/import", body=bodies[k][3],
+                             headers={"Content-Type": "application/x-protobuf", "Accept": "application/x-protobuf"})
+                r = conn.getresponse()
+                r.read()
+                if r.status != 200:
+                    errs.append(r.status)
+        log(f"import: {nsh} shards x {per} bits over HTTP")
+        t1 = time.perf_counter()
+        ts = [threading.Thread(target=importer) for _ in range(args.import_clients)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        t_imp = time.perf_counter() - t1
+        gpu = ex.gpu
+        w0 = getattr(gpu, "device_writes", 0)
+        t2 = time.perf_counter()
+        ex.execute("i", queries[1])      # first query after the import: device replay of the write batches
+        t_replay = time.perf_counter() - t2
+        frags = srv.holder.view("i", "f", "standard").all_fragments()
+        chk = []
+        for s, rows, cols, _ in bodies[:3]:
+            r = int(rows[0])
+            got = ex.execute("i", f"Count(Row(f={r}))", shards=[s]).results[0]
+            chk.append(got == srv.holder.fragment("i", "f", "standard", s).row_count(r))
+        out["import"] = {"shards": nsh, "bits": nsh * per, "s": round(t_imp, 3),
+                         "bits_per_s": round(nsh * per / t_imp, 1), "http_errors": len(errs),
+                         "clients": args.import_clients,
+                         "first_query_after_s": round(t_replay, 3),
+                         "device_write_batches": int(getattr(gpu, "device_writes", 0) - w0),
+                         "fragments_cold_after_import": sum(f.is_cold() for f in frags), "fragments": len(frags),
+                         "rss_growth_gb": round(_rss_gb() - rss0, 2), "device_matches_host": all(chk)}
+    finally:
+        srv.close()
+    return out
+
+
+def _rss_gb() -> float:
+    with open("/proc/self/status") as fh:
+        for line in fh:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) / 1e6
+    return 0.0
 
 
 def main():
@@ -1066,6 +1213,12 @@ def main():
     ap.add_argument("--configs", default=os.environ.get("PILOSA_BENCH_CONFIGS", "4,5"),
                     help="also run BASELINE configs 4 (BSI) and 5 (time union) into extra (empty = skip)")
     ap.add_argument("--config-reps", type=int, default=5)
+    ap.add_argument("--serve-seconds", type=float, default=5.0,
+                    help="disk mode, 1 GPU: native-HTTP serving run on the same data dir (0 = skip)")
+    ap.add_argument("--serve-conns", type=int, default=128)
+    ap.add_argument("--import-shards", type=int, default=64, help="serving phase: shards of the HTTP bulk import")
+    ap.add_argument("--import-bits-per-shard", type=int, default=200_000)
+    ap.add_argument("--import-clients", type=int, default=8)
     ap.add_argument("--cpu-baseline-shards", type=int, default=0,
                     help="also time the host C++ roaring executor on this many shards (extrapolated)")
     args = ap.parse_args()

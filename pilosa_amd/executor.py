@@ -41,7 +41,7 @@ MAX_INT = (1 << 63) - 1
 
 
 class ExecOptions:
-    __slots__ = ("remote", "exclude_row_attrs", "exclude_columns", "column_attrs", "mesh_local")
+    __slots__ = ("remote", "exclude_row_attrs", "exclude_columns", "column_attrs", "mesh_local", "device_counts")
 
     def __init__(self, remote=False, exclude_row_attrs=False, exclude_columns=False, column_attrs=False):
         self.remote = remote
@@ -49,10 +49,15 @@ class ExecOptions:
         self.exclude_columns = exclude_columns
         self.column_attrs = column_attrs
         self.mesh_local = False  # set on a rank's own share of a multi-GPU call
+        # a Count-only request answered in one device launch returns its counts
+        # as the device int64 tensor (callers that reduce on the device: the
+        # SPMD multi-GPU bench all-reduces it without a host round trip)
+        self.device_counts = False
 
     def copy(self):
         o = ExecOptions(self.remote, self.exclude_row_attrs, self.exclude_columns, self.column_attrs)
         o.mesh_local = self.mesh_local
+        o.device_counts = self.device_counts
         return o
 
 
@@ -145,7 +150,7 @@ class GroupCount:
 
 class QueryResponse:
     def __init__(self, results=None, column_attr_sets=None, err=None):
-        self.results = results or []
+        self.results = results if results is not None else []
         self.column_attr_sets = column_attr_sets
         self.err = err
 
@@ -246,6 +251,10 @@ class Executor:
                 opt: Optional[ExecOptions] = None) -> QueryResponse:
         with tracing.span("Executor.Execute"):
             if isinstance(q, str):
+                if self._use_mesh(opt):
+                    res = self._mesh_count_text(index, q, shards, opt)
+                    if res is not None:
+                        return QueryResponse(res)
                 fast = self._count_text_fast(index, q, shards, opt)
                 if fast is not None:
                     return QueryResponse(fast)
@@ -293,7 +302,10 @@ class Executor:
         and answered in one launch.  None = use the general path (which also
         produces every error the reference would)."""
         gpu = self.gpu
-        if gpu is None or (opt is not None and (opt.remote or opt.column_attrs)):
+        if gpu is None or (opt is not None and opt.column_attrs):
+            return None
+        dev_out = opt is not None and opt.device_counts
+        if opt is not None and opt.remote and not dev_out:
             return None
         head = text.lstrip()[:6]
         if head != "Count(" and head != "Count ":
@@ -310,7 +322,7 @@ class Executor:
         if fn is None:
             return None
         try:
-            res = fn(index, text, shards)
+            res = fn(index, text, shards, device_out=True) if dev_out else fn(index, text, shards)
         except PilosaError:
             raise
         except Exception as err:  # noqa: BLE001 - device fault: general path
@@ -319,6 +331,28 @@ class Executor:
         if res is not None and self.stats is not None:
             self.stats.count_with_tags("Count", len(res), [f"index:{index}"])
         return res
+
+    def _mesh_count_text(self, index: str, text: str, shards, opt: Optional[ExecOptions]) -> Optional[List[int]]:
+        """Multi-GPU node: a request of Count() calls goes to the ranks as
+        its PQL text (each compiles its share natively, parallel/mesh.py
+        count_text) and comes back as one all-reduced tensor; several such
+        requests are in flight at once.  None = general path."""
+        if opt is not None and (opt.remote or opt.column_attrs):
+            return None
+        head = text.lstrip()[:6]
+        if (head != "Count(" and head != "Count ") or text.count("Count") < self.COUNT_TEXT_MIN:
+            return None
+        idx = self.holder.index(index)
+        if idx is None or idx.keys or any(f.options.keys for f in idx.fields.values()):
+            return None   # key translation happens on the general path
+        shards = list(shards) if shards else (idx.available_shards() or [0])
+        mesh = self.mesh
+        try:
+            return mesh.count_text(index, text, shards)
+        except MeshError:
+            if not mesh.failed_over:
+                raise
+            return None   # a rank is gone: this process adopted its shards
 
     def _execute(self, index: str, q: Query, shards: List[int], opt: ExecOptions) -> List[Any]:
         needs = any(c.name not in ("Clear", "Set", "SetRowAttrs", "SetColumnAttrs") for c in q.calls)

@@ -358,16 +358,24 @@ class Fragment:
         reference holds the fragment lock throughout (fragment.go:2240-2290).
         No second lock is taken, so a snapshot queued in the background and
         one run synchronously under ``mu`` cannot deadlock."""
+        tmp = f"{self.path}.{os.getpid()}.{threading.get_ident()}.snapshotting"
         with self.mu:
             if self._fh is None and not os.path.exists(self.path):
                 return  # closed/deleted while queued
-            data = self.storage.to_bytes()
+            cold = self._storage is None
+            if cold:
+                # stream the mapped file + overlay straight to the new file:
+                # the fragment is never read into heap (under mu: the overlay
+                # must not change while it is written out)
+                self._cold().write_snapshot(tmp)
+            else:
+                data = self.storage.to_bytes()
             gen = self._file_gen
             mark = self._file_size()
             opn0, ops0 = self.opn, self.ops
-        tmp = f"{self.path}.{os.getpid()}.{threading.get_ident()}.snapshotting"
-        with open(tmp, "wb") as fh:
-            fh.write(data)
+        with open(tmp, "r+b" if cold else "wb") as fh:
+            if not cold:
+                fh.write(data)
             fh.flush()
             os.fsync(fh.fileno())
         with self.mu:
@@ -389,6 +397,10 @@ class Fragment:
                 self._fh.close()
             os.replace(tmp, self.path)
             self._file_gen += 1
+            if self._storage is None and self._mapped is not None:
+                # re-map the new file: the overlay is in it now (plus any ops
+                # appended meanwhile, which the new view replays)
+                self._mapped = _roaring.MappedBitmap(self.path)
             self._fh = open(self.path, "ab", buffering=0)
             fcntl.flock(self._fh.fileno(), fcntl.LOCK_EX | fcntl.LOCK_NB)
             self.opn -= opn0
@@ -555,7 +567,7 @@ class Fragment:
         for b in np.unique(rows // np.uint64(HASH_BLOCK_SIZE)).tolist():
             self.checksums.pop(int(b), None)
         if self.cache_type != CACHE_TYPE_NONE:
-            counts = self.storage.count_rows(rows, CONTAINERS_PER_ROW)
+            counts = self._rw().count_rows(rows, CONTAINERS_PER_ROW)
             add = self.cache.bulk_add
             for rid, n in zip(rows.tolist(), counts.tolist()):
                 add(rid, n)
@@ -997,7 +1009,7 @@ class Fragment:
         changed = 0
         if len(set_pos):
             set_pos = np.unique(np.asarray(set_pos, dtype=np.uint64))
-            n = self.storage.add_many(set_pos, True)
+            n = self._rw().add_many(set_pos, True)
             if n:
                 self._log(OP_ADD_BATCH, values=set_pos)
                 if self._dirty_subs:
@@ -1005,7 +1017,7 @@ class Fragment:
             changed += n
         if len(clear_pos):
             clear_pos = np.unique(np.asarray(clear_pos, dtype=np.uint64))
-            n = self.storage.remove_many(clear_pos)
+            n = self._rw().remove_many(clear_pos)
             if n:
                 self._log(OP_REMOVE_BATCH, values=clear_pos)
                 if self._dirty_subs:
@@ -1075,7 +1087,7 @@ class Fragment:
 
     def import_roaring(self, data: bytes, clear: bool = False) -> int:
         with self.mu:
-            changed, rowdelta = self.storage.import_roaring(data, clear, CONTAINERS_PER_ROW)
+            changed, rowdelta = self._rw().import_roaring(data, clear, CONTAINERS_PER_ROW)
             if changed and self._dirty_subs:
                 # the device merges the imported containers itself (K12)
                 self._note_delta("roaring", Bitmap.from_bytes(data), clear, int(changed))

@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <set>
 #include <stdexcept>
@@ -320,6 +321,131 @@ std::vector<uint64_t> MappedBitmap::rows_with_column(uint64_t col, uint64_t cpr)
   for (auto& kv : over_.cs)
     if (kv.first % cpr == ck && kv.second.n && kv.second.contains(low)) rows.insert(kv.first / cpr);
   return std::vector<uint64_t>(rows.begin(), rows.end());
+}
+
+int64_t MappedBitmap::add_many(const uint64_t* v, size_t n) {
+  int64_t changed = 0;
+  for (size_t i = 0; i < n;) {
+    const uint64_t key = v[i] >> 16;
+    size_t j = i;
+    while (j < n && (v[j] >> 16) == key) j++;
+    cow(key);
+    changed += over_.add_many(v + i, j - i);
+    i = j;
+  }
+  return changed;
+}
+
+int64_t MappedBitmap::remove_many(const uint64_t* v, size_t n) {
+  int64_t changed = 0;
+  for (size_t i = 0; i < n;) {
+    const uint64_t key = v[i] >> 16;
+    size_t j = i;
+    while (j < n && (v[j] >> 16) == key) j++;
+    if (touched_.count(key) || find(key) >= 0) {  // nothing to clear in an absent container
+      cow(key);
+      changed += over_.remove_many(v + i, j - i);
+    }
+    i = j;
+  }
+  return changed;
+}
+
+int64_t MappedBitmap::import_roaring(const uint8_t* data, size_t n, bool clear, uint64_t cpr,
+                                     std::map<uint64_t, int64_t>* rowdelta) {
+  Bitmap blob;
+  blob.from_bytes(data, n);
+  for (auto& kv : blob.cs)
+    if (kv.second.n && (!clear || touched_.count(kv.first) || find(kv.first) >= 0)) cow(kv.first);
+  // over_ now owns every container the blob can change
+  return over_.import_roaring(data, n, clear, cpr, rowdelta);
+}
+
+namespace {
+void put_le(std::string& s, uint64_t v, int bytes) {
+  for (int k = 0; k < bytes; k++) s.push_back(char((v >> (8 * k)) & 0xff));
+}
+}  // namespace
+
+size_t MappedBitmap::write_snapshot(const std::string& path) {
+  for (auto& kv : touched_) {
+    auto it = over_.cs.find(kv.first);
+    if (it != over_.cs.end() && it->second.n) it->second.optimize();
+  }
+  // merged key order: (key, mapped index or -1 for the overlay copy)
+  std::vector<std::pair<uint64_t, int64_t>> order;
+  order.reserve(keyn_ + touched_.size());
+  size_t i = 0;
+  auto ot = touched_.begin();
+  while (i < keyn_ || ot != touched_.end()) {
+    const uint64_t mk = i < keyn_ ? key_at(i) : ~0ull;
+    const uint64_t tk = ot != touched_.end() ? ot->first : ~0ull;
+    if (tk <= mk) {
+      auto c = over_.cs.find(tk);
+      if (c != over_.cs.end() && c->second.n) order.emplace_back(tk, -1);
+      ++ot;
+      if (tk == mk) i++;  // the overlay copy replaces the mapped container
+    } else {
+      order.emplace_back(mk, int64_t(i));
+      i++;
+    }
+  }
+  std::string head;
+  head.reserve(HEADER_BASE + order.size() * 16);
+  put_le(head, MAGIC | (STORAGE_VERSION << 16) | (uint32_t(flags) << 24), 4);
+  put_le(head, order.size(), 4);
+  std::vector<size_t> sizes(order.size());
+  for (size_t k = 0; k < order.size(); k++) {
+    uint16_t typ;
+    int32_t cn;
+    if (order[k].second >= 0) {
+      const size_t mi = size_t(order[k].second);
+      size_t off;
+      if (!span(mi, &off, &sizes[k])) throw std::runtime_error("write_snapshot: corrupt mapped container");
+      typ = r16(hdr_ + mi * 12 + 8);
+      cn = mapped_n(mi);
+    } else {
+      const Container& c = over_.cs.at(order[k].first);
+      typ = c.type;
+      cn = c.n;
+      sizes[k] = c.encoded_size();
+    }
+    put_le(head, order[k].first, 8);
+    put_le(head, typ, 2);
+    put_le(head, uint16_t(cn - 1), 2);
+  }
+  size_t off = HEADER_BASE + order.size() * 16;
+  for (size_t k = 0; k < order.size(); k++) {
+    if (off + sizes[k] > 0xFFFFFFFFull) throw std::runtime_error("write_snapshot: file exceeds 4 GiB offsets");
+    put_le(head, off, 4);
+    off += sizes[k];
+  }
+  FILE* fh = fopen(path.c_str(), "wb");
+  if (!fh) throw std::runtime_error("write_snapshot: open " + path + ": " + strerror(errno));
+  bool ok = fwrite(head.data(), 1, head.size(), fh) == head.size();
+  std::string buf;
+  for (size_t k = 0; k < order.size() && ok; k++) {
+    if (order[k].second >= 0) {
+      ok = fwrite(payload(size_t(order[k].second)), 1, sizes[k], fh) == sizes[k];
+      continue;
+    }
+    const Container& c = over_.cs.at(order[k].first);
+    buf.clear();
+    switch (c.type) {
+      case CT_ARRAY: buf.append(reinterpret_cast<const char*>(c.a.data()), c.a.size() * 2); break;
+      case CT_BITMAP: buf.append(reinterpret_cast<const char*>(c.b.data()), size_t(BITMAP_N) * 8); break;
+      default:
+        put_le(buf, c.r.size(), 2);
+        for (const Iv& iv : c.r) {
+          put_le(buf, iv.start, 2);
+          put_le(buf, iv.last, 2);
+        }
+    }
+    ok = fwrite(buf.data(), 1, buf.size(), fh) == buf.size();
+  }
+  if (fclose(fh) != 0) ok = false;
+  if (!ok) throw std::runtime_error("write_snapshot: short write to " + path);
+  return off;
 }
 
 }  // namespace pr

@@ -565,6 +565,29 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
         }
         return out;
       })
+      .def("container_runs", [](const Bitmap& b, uint64_t key) {
+        // (start, last) intervals of a run container; count_runs() of any other
+        // type is reported through container_run_count (debug / tests)
+        std::vector<std::pair<int, int>> out;
+        auto it = b.cs.find(key);
+        if (it == b.cs.end() || it->second.type != pr::CT_RUN) throw std::invalid_argument("no run container at key");
+        for (const auto& iv : it->second.r) out.emplace_back(iv.start, iv.last);
+        return out;
+      })
+      .def("container_run_count", [](const Bitmap& b, uint64_t key) {
+        auto it = b.cs.find(key);
+        return it == b.cs.end() ? 0 : it->second.count_runs();
+      })
+      .def("convert_container", [](Bitmap& b, uint64_t key, const std::string& to) {
+        // force the encoding of one container (the reference's arrayToRun,
+        // runToBitmap, ... conversions; debug / tests)
+        auto it = b.cs.find(key);
+        if (it == b.cs.end()) throw std::invalid_argument("no container at key");
+        if (to == "array") it->second.to_array();
+        else if (to == "bitmap") it->second.to_bitmap();
+        else if (to == "run") it->second.to_run();
+        else throw std::invalid_argument("type must be array, bitmap or run");
+      })
       .def("to_bytes", [](Bitmap& b) {
         std::string s = b.to_bytes();
         return py::bytes(s);
@@ -680,6 +703,26 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
         for (py::ssize_t i = 0; i < n; i++) o[i] = b.count_range((r[i] * cpr) << 16, ((r[i] + 1) * cpr) << 16);
         return out;
       }, py::arg("rows"), py::arg("containers_per_row") = 16)
+      .def("add_many", [](pr::MappedBitmap& b, u64arr vals, bool sorted) {
+        std::vector<uint64_t> v(vals.data(), vals.data() + vals.size());
+        if (!sorted) std::sort(v.begin(), v.end());
+        return b.add_many(v.data(), v.size());
+      }, py::arg("values"), py::arg("sorted") = false)
+      .def("remove_many", [](pr::MappedBitmap& b, u64arr vals) {
+        std::vector<uint64_t> v(vals.data(), vals.data() + vals.size());
+        std::sort(v.begin(), v.end());
+        return b.remove_many(v.data(), v.size());
+      })
+      .def("import_roaring", [](pr::MappedBitmap& b, py::bytes data, bool clear, uint64_t cpr) {
+        std::string s = data;
+        std::map<uint64_t, int64_t> rd;
+        int64_t ch = b.import_roaring(reinterpret_cast<const uint8_t*>(s.data()), s.size(), clear, cpr, &rd);
+        py::dict d;
+        for (auto& kv : rd) d[py::int_(kv.first)] = kv.second;
+        return py::make_tuple(ch, d);
+      }, py::arg("data"), py::arg("clear") = false, py::arg("containers_per_row") = 16)
+      .def("write_snapshot", &pr::MappedBitmap::write_snapshot, py::arg("path"),
+           py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("mapped_containers", &pr::MappedBitmap::mapped_containers)
       .def_property_readonly("overlay_containers", &pr::MappedBitmap::overlay_containers)
       .def_property_readonly("mapped_bytes", &pr::MappedBitmap::mapped_bytes)

@@ -196,6 +196,15 @@ class MappedBitmap {
   uint64_t max() const;
   Bitmap offset_range(uint64_t offset, uint64_t start, uint64_t end) const;
   std::vector<uint64_t> rows_with_column(uint64_t col, uint64_t cpr) const;
+  int64_t add_many(const uint64_t* v, size_t n);     // v sorted ascending
+  int64_t remove_many(const uint64_t* v, size_t n);  // v sorted ascending
+  int64_t import_roaring(const uint8_t* data, size_t n, bool clear, uint64_t cpr,
+                         std::map<uint64_t, int64_t>* rowdelta);
+  // Pilosa-format snapshot of the current state streamed to ``path``:
+  // untouched containers are copied from the map byte for byte, overlay
+  // containers are optimised and encoded (Bitmap::to_bytes layout).  Returns
+  // the bytes written.
+  size_t write_snapshot(const std::string& path);
   size_t mapped_containers() const { return keyn_; }
   size_t overlay_containers() const { return touched_.size(); }
   size_t mapped_bytes() const { return len_; }

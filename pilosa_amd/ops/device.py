@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -47,6 +48,7 @@ assert QPROG_DTYPE.itemsize == 256 and VIEWDEV_DTYPE.itemsize == 64
 
 _ext = None
 _ext_lock = threading.Lock()
+_D2H_POLL = float(os.environ.get("PILOSA_D2H_POLL", "0"))
 
 
 def kernels():
@@ -1091,7 +1093,13 @@ class GpuEngine:
         h.copy_(t, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        ev.synchronize()
+        if _D2H_POLL:
+            # poll instead of a blocking wait: other request threads keep
+            # launching while this one waits for its batch
+            while not ev.query():
+                time.sleep(_D2H_POLL)
+        else:
+            ev.synchronize()
         return h
 
     def launch_count(self, handle):

@@ -492,7 +492,7 @@ class GpuExecutor:
         self.launches += 1
         return self.engine.to_host(self.engine.launch_count(self.engine.prepare_progs(progs, vlist, S))).tolist()
 
-    def try_count_text(self, index: str, text: str, shards: List[int]) -> Optional[List[int]]:
+    def try_count_text(self, index: str, text: str, shards: List[int], device_out: bool = False):
         """A whole request of ``Count(<Row/set-op tree>)`` calls, compiled from
         the PQL text natively (no Python AST) into one launch.  None when any
         call, field or view needs the general executor path (keys, BSI and
@@ -524,7 +524,10 @@ class GpuExecutor:
             return None
         Q, segs, buf = got
         self.launches += 1
-        return eng.to_host(eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S))).tolist()
+        out = eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S))
+        # device_out: the int64[Q] device tensor, still being computed (the
+        # caller reduces it on the device, e.g. the mesh all-reduce)
+        return out if device_out else eng.to_host(out).tolist()
 
     TIME_GROUP_MIN = 2
 

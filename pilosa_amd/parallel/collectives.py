@@ -36,7 +36,7 @@ class CommError(RuntimeError):
 
 
 class Comm:
-    def __init__(self, group=None, device=None, host_copies: bool = False):
+    def __init__(self, group=None, device=None, host_copies: bool = False, ctrl_group=None):
         import torch
         import torch.distributed as dist
 
@@ -53,6 +53,10 @@ class Comm:
         self.host_copies = host_copies or (backend == "gloo" and self.device.type == "cuda")
         self.broken: Optional[BaseException] = None
         self.calls = 0
+        # command channel: a gloo group of its own, so a command broadcast is
+        # never queued behind the data collectives of batches still in flight
+        self.ctrl = ctrl_group
+        self.ctrl_device = torch.device("cpu") if ctrl_group is not None else self.device
 
     # ------------------------------------------------------------ guard
     def _guard(self, fn, *a, **kw):
@@ -86,20 +90,47 @@ class Comm:
         return t
 
     def bcast_bytes(self, op: int = 0, payload: bytes = b"", src: int = 0):
-        """Rank ``src`` sends (op, payload); every rank returns them."""
+        """Rank ``src`` sends (op, payload); every rank returns them (on the
+        command group when there is one)."""
         torch = self.torch
-        hdr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        dev = self.ctrl_device
+
+        def bc(t):
+            if self.ctrl is None:
+                return self.broadcast(t, src)
+            self._guard(self.dist.broadcast, t, src=src, group=self.ctrl)
+            return t
+        hdr = torch.zeros(2, dtype=torch.int64, device=dev)
         if self.rank == src:
             hdr[0], hdr[1] = int(op), len(payload)
-        self.broadcast(hdr, src)
+        bc(hdr)
         op_, n = (int(x) for x in hdr.cpu().tolist())
         if n == 0:
             return op_, b""
-        buf = torch.empty(n, dtype=torch.uint8, device=self.device)
+        buf = torch.empty(n, dtype=torch.uint8, device=dev)
         if self.rank == src:
             buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
-        self.broadcast(buf, src)
+        bc(buf)
         return op_, buf.cpu().numpy().tobytes()
+
+    def all_reduce_async(self, t, op=None):
+        """Start an in-place sum of ``t``; returns a handle for :meth:`wait`.
+        RCCL enqueues it behind the work already on the caller's stream and
+        the host goes on (the next batch can be planned and launched)."""
+        op = self.dist.ReduceOp.SUM if op is None else op
+        if self.host_copies:   # gloo rehearsal of a GPU run: host copies, synchronous
+            self.all_reduce(t, op)
+            return None
+        return self._guard(self.dist.all_reduce, t, op=op, group=self.group, async_op=True)
+
+    def wait(self, work):
+        """Complete a collective started by :meth:`all_reduce_async`."""
+        if work is not None:
+            self._guard(work.wait)
+
+    @staticmethod
+    def done(work) -> bool:
+        return work is None or work.is_completed()
 
     def all_gather_var(self, t) -> List:
         """1-D tensors of any length per rank -> list of per-rank tensors."""

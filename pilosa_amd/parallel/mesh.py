@@ -44,7 +44,9 @@ class MeshError(RuntimeError):
 
 
 # ---------------------------------------------------------------- transport
-OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS = range(9)
+(OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS, OP_COUNT_TEXT,
+ OP_ERRORS) = range(11)
+MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
 
 
 def _raise_remote(parts):
@@ -58,10 +60,19 @@ def _raise_remote(parts):
 class ShardMesh:
     """Shard-owner routing and collective reductions for one node's GPUs."""
 
-    def __init__(self, executor, group=None, block: int = 1, device=None, peer_dirs: Optional[Dict[int, str]] = None):
+    def __init__(self, executor, group=None, block: int = 1, device=None, peer_dirs: Optional[Dict[int, str]] = None,
+                 ctrl_group="auto"):
+        import collections
+
+        import torch.distributed as dist
+
         from .collectives import Comm
 
-        self.comm = Comm(group, device=device)
+        if ctrl_group == "auto":
+            # every rank builds its mesh in the same order, so this collective
+            # group creation lines up; commands then travel on gloo (host)
+            ctrl_group = dist.new_group(backend="gloo") if group is None and dist.get_world_size() > 1 else None
+        self.comm = Comm(group, device=device, ctrl_group=ctrl_group)
         self.torch = self.comm.torch
         self.dist = self.comm.dist
         self.group = group
@@ -76,6 +87,12 @@ class ShardMesh:
         self.peer_dirs: Dict[int, str] = dict(peer_dirs or {})
         self.failed_over = False
         self.failover_error: Optional[str] = None
+        self.seq = 0                      # count-text batches issued (front end)
+        self.in_flight = 0                # front end: batches issued, result not yet read
+        self.max_in_flight = 0
+        self._pending = collections.deque()   # worker: (tensor, work) of batches in flight
+        self._errors: Dict[int, BaseException] = {}
+        self.last_count_text_errors: List[str] = []
 
     # ------------------------------------------------------------ ownership
     def owner(self, shard: int) -> int:
@@ -128,6 +145,74 @@ class ShardMesh:
 
     def count_batch(self, index: str, calls, shards: Sequence[int]) -> List[int]:
         return self._run(OP_COUNT, index, [str(c) for c in calls], list(shards))
+
+    def count_text(self, index: str, text: str, shards: Sequence[int]) -> Optional[List[int]]:
+        """A request of Count() calls as PQL text, pipelined: the lock covers
+        only the command broadcast and the launch of this rank's share plus
+        its all-reduce (every rank issues collectives in command order); the
+        wait for the reduced counts happens outside it, so the next request's
+        broadcast, planning and kernels overlap this one's (executor.go
+        mapReduce)."""
+        from .collectives import CommError, encode
+
+        if not self.is_frontend:
+            raise MeshError("only rank 0 issues mesh commands")
+        q = text.count("Count(")
+        with self.lock:
+            if self.failed_over:
+                raise MeshError(f"mesh failed over: {self.failover_error}")
+            self.ops += 1
+            self.seq += 1
+            seq = self.seq
+            try:
+                self.comm.bcast_bytes(OP_COUNT_TEXT, encode([index, text, list(shards), q, seq]))
+                t, work = self._count_text_issue(index, text, list(shards), q, seq)
+            except CommError as e:
+                self.failover(e)
+                raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
+            self.in_flight += 1
+            self.max_in_flight = max(self.max_in_flight, self.in_flight)
+        try:
+            self.comm.wait(work)
+            out = self._host_list(t)
+        except CommError as e:
+            with self.lock:
+                self.failover(e)
+            raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
+        finally:
+            with self.lock:
+                self.in_flight -= 1
+        if out[-1]:
+            # a rank could not count it: collect the errors (logged), and let
+            # the caller run the request on the general path, which raises
+            # the reference's error for it (parse errors, unknown fields, ...)
+            from .collectives import RemoteError
+            errs = [p for p in self._run_collect(OP_ERRORS, seq) if isinstance(p, RemoteError)]
+            self.last_count_text_errors = [str(e) for e in errs]
+            return None
+        return out[:-1]
+
+    def _run_collect(self, op: int, *args) -> list:
+        """Like :meth:`_run` but returns the per-rank parts without raising
+        the remote errors among them."""
+        from .collectives import CommError, encode
+
+        with self.lock:
+            if self.failed_over:
+                raise MeshError(f"mesh failed over: {self.failover_error}")
+            try:
+                self.comm.bcast_bytes(op, encode(list(args)))
+                mine = self._errors.pop(int(args[0]), None) if op == OP_ERRORS else None
+                return self._gather(mine)
+            except CommError as e:
+                self.failover(e)
+                raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
+
+    def _host_list(self, t) -> List[int]:
+        gpu = getattr(self.executor, "gpu", None)
+        if t.device.type == "cuda" and gpu is not None and hasattr(gpu, "engine"):
+            return gpu.engine.to_host(t).tolist()
+        return t.cpu().tolist()
 
     def forward_write(self, index: str, c, shard: int, opt) -> Any:
         parts = self._run(OP_WRITE, index, str(c), int(shard), _opt_dict(opt))
@@ -205,7 +290,16 @@ class ShardMesh:
         while True:
             op, payload = self.comm.bcast_bytes()
             if op == OP_STOP:
+                while self._pending:
+                    self.comm.wait(self._pending.popleft()[1])
                 return
+            if op == OP_COUNT_TEXT:
+                index, text, shards, q, seq = decode(payload)
+                self._pending.append(self._count_text_issue(index, text, shards, q, seq))
+                # keep tensors alive until their collective is done; bound the queue
+                while self._pending and (len(self._pending) > MAX_IN_FLIGHT or self.comm.done(self._pending[0][1])):
+                    self.comm.wait(self._pending.popleft()[1])
+                continue
             self._dispatch(op, decode(payload) or [])
 
     # ------------------------------------------------------------ all ranks
@@ -252,6 +346,8 @@ class ShardMesh:
                     idx = ex.holder.index(args[0])
                     if idx is not None and idx.field(args[1]) is not None:
                         idx.delete_field(args[1])
+            elif op == OP_ERRORS:
+                mine = self._errors.pop(int(args[0]), None)
             elif op == OP_SHARDS:
                 mine = {name: idx.available_shards() for name, idx in ex.holder.indexes.items()}
                 if self.is_frontend:
@@ -267,6 +363,43 @@ class ShardMesh:
         if self.is_frontend:
             _raise_remote(parts)
         return parts
+
+    def _count_text_issue(self, index: str, text: str, shards: List[int], q: int, seq: int):
+        """This rank's counts for its own shards as a device tensor (plus an
+        error flag) and the started all-reduce of it."""
+        torch = self.torch
+        err = None
+        t = None
+        try:
+            t = self._local_count_text(index, text, self.owned(shards), q)
+            if t is None or t.numel() != q:
+                raise MeshError(f"rank {self.rank}: {0 if t is None else t.numel()} counts for {q} calls")
+        except Exception as e:  # noqa: BLE001 - flagged in the reduced tensor, text via OP_ERRORS
+            err = e
+            t = torch.zeros(q, dtype=torch.int64, device=self.device)
+        if err is not None:
+            self._errors[seq] = err
+            while len(self._errors) > 64:
+                self._errors.pop(next(iter(self._errors)))
+        flag = torch.full((1,), 1 if err is not None else 0, dtype=torch.int64, device=self.device)
+        tt = torch.cat([t.to(self.device, torch.int64), flag])
+        return tt, self.comm.all_reduce_async(tt)
+
+    def _local_count_text(self, index: str, text: str, shards: List[int], q: int):
+        torch = self.torch
+        ex = self.executor
+        if not shards:
+            return torch.zeros(q, dtype=torch.int64, device=self.device)
+        if ex.holder.index(index) is None:
+            raise MeshError(f"index not found on rank {self.rank}: {index}")
+        gpu = ex.gpu
+        if gpu is not None and hasattr(gpu, "try_count_text"):
+            res = gpu.try_count_text(index, text, shards, device_out=True)
+            if res is not None:
+                return res
+        from pilosa_amd.pql import parse_string
+        pqls = [str(c) for c in parse_string(text).calls]
+        return torch.tensor(self._local_counts(index, pqls, shards), dtype=torch.int64, device=self.device)
 
     def _local_opt(self, optd: dict):
         from pilosa_amd.executor import ExecOptions

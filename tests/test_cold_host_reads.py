@@ -88,3 +88,46 @@ def test_lazy_holder_serves_writes_and_reads_from_mapped_files():
         full.close()
     finally:
         shutil.rmtree(base, ignore_errors=True)
+
+
+def test_cold_bulk_import_and_snapshot_stay_off_heap():
+    """Bulk imports (bits, roaring) into cold fragments go through the
+    mapped overlay, and the snapshot they trigger streams the mapped file plus
+    overlay to the new file (MappedBitmap.write_snapshot): the fragments stay
+    cold, and a whole load of the new files equals a whole-load replay."""
+    base = tempfile.mkdtemp(prefix="cold_import_")
+    try:
+        _make(base)
+        rng = np.random.default_rng(9)
+        holder = Holder(base, lazy_fragments=True).open()
+        f = holder.index("i").field("f")
+        n = 60_000   # > max_opn for every shard it lands in: snapshots run
+        rows = rng.integers(0, 300, size=n).astype(np.uint64)
+        cols = rng.integers(0, 4 * SW, size=n).astype(np.uint64)
+        f.import_bits(rows, cols)
+        f.import_bits(rows[:5000], cols[:5000], clear=True)
+        frag0 = holder.fragment("i", "f", "standard", 0)
+        blob = _roaring.Bitmap(np.unique(rng.integers(0, 64 * SW, size=20000)).astype(np.uint64)).to_bytes()
+        frag0.import_roaring(blob)
+        holder.snapshot_queue.drain() if getattr(holder, "snapshot_queue", None) is not None and \
+            hasattr(holder.snapshot_queue, "drain") else None
+        for s in range(4):
+            holder.fragment("i", "f", "standard", s).snapshot()
+        frags = holder.view("i", "f", "standard").all_fragments()
+        assert all(fr.is_cold() for fr in frags)
+        counts = {r: holder.fragment("i", "f", "standard", 1).row_count(r) for r in range(0, 300, 37)}
+        holder.close()
+        full = Holder(base).open()
+        for r, c in counts.items():
+            assert full.fragment("i", "f", "standard", 1).row_count(r) == c
+        fr0 = full.fragment("i", "f", "standard", 0)
+        assert fr0.storage.check() == ""
+        clear_set = set(zip(rows[:5000].tolist(), cols[:5000].tolist()))
+        blob_bm = _roaring.Bitmap.from_bytes(blob)
+        for r, c in list(zip(rows.tolist(), cols.tolist()))[::97]:
+            sh = int(c) // SW
+            exp = (r, c) not in clear_set or (sh == 0 and blob_bm.contains(r * SW + c % SW))
+            assert full.fragment("i", "f", "standard", sh).bit(r, c) == exp
+        full.close()
+    finally:
+        shutil.rmtree(base, ignore_errors=True)

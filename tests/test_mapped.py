@@ -109,3 +109,34 @@ def test_mapped_rejects_corrupt_files():
     open(p, "wb").close()
     m = _roaring.MappedBitmap(p)
     assert not m.any() and m.count() == 0 and m.add(7) and m.contains(7)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_mapped_bulk_ops_and_streamed_snapshot(seed):
+    rng = np.random.default_rng(100 + seed)
+    d = tempfile.mkdtemp()
+    path = os.path.join(d, "0")
+    want = _with_ops(rng, _random_bitmap(rng), path)
+    m = _roaring.MappedBitmap(path)
+    for _ in range(6):
+        vals = np.unique(rng.integers(0, 70 * 65536, size=int(rng.integers(1, 5000)))).astype(np.uint64)
+        k = int(rng.integers(0, 3))
+        if k == 0:
+            assert m.add_many(vals, True) == want.add_many(vals, True)
+        elif k == 1:
+            assert m.remove_many(vals) == want.remove_many(vals)
+        else:
+            blob = _roaring.Bitmap(vals).to_bytes()
+            clear = bool(rng.integers(0, 2))
+            got, gd = m.import_roaring(blob, clear, 16)
+            exp, ed = want.import_roaring(blob, clear, 16)
+            assert got == exp and {k_: v for k_, v in gd.items() if v} == {k_: v for k_, v in ed.items() if v}
+    snap = os.path.join(d, "snap")
+    n = m.write_snapshot(snap)
+    data = open(snap, "rb").read()
+    assert n == len(data)
+    back = _roaring.Bitmap.from_bytes(data)
+    assert back.equals(want) and back.flags == want.flags
+    assert back.check() == ""
+    m2 = _roaring.MappedBitmap(snap)
+    assert m2.count() == want.count() and m2.overlay_containers == 0

@@ -222,3 +222,72 @@ def test_result_codec_round_trip():
     assert [int(c) for c in got.columns()] == [1, 5, 3 << 20] and got.attrs == {"x": 1}
     e = decode(encode(ValueError("boom")))
     assert isinstance(e, RemoteError) and "boom" in str(e)
+
+
+def _pipeline_worker(rank, world, port, outdir):
+    """Concurrent multi-Count requests through the mesh text path: several
+    batches in flight (broadcast on the gloo command group, async
+    all-reduces), answers equal to one Count per request; a request naming an
+    unknown field falls back to the general path and raises its error."""
+    import threading
+
+    import torch.distributed as dist
+
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    holder = Holder(tempfile.mkdtemp(prefix=f"meshp{rank}_")).open()
+    ex = Executor(holder)
+    mesh = ShardMesh(ex, block=1)
+    ex.mesh = mesh
+    try:
+        if rank != 0:
+            mesh.serve()
+            return
+        _setup_schema(holder)
+        mesh.apply_schema()
+        bits, vals = _data()
+        _load(ex, bits, vals, mesh)
+        rng = np.random.default_rng(3)
+        reqs = []
+        for _ in range(24):
+            qs = [f"Count(Intersect(Row(f={int(a)}), Row(g={int(b)})))" for a, b in
+                  zip(rng.integers(0, 5, 6), rng.integers(0, 4, 6))]
+            reqs.append(qs)
+        got = [None] * len(reqs)
+
+        def run(k):
+            got[k] = ex.execute("i", " ".join(reqs[k])).results
+        ts = [threading.Thread(target=run, args=(k,)) for k in range(len(reqs))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        want = [[ex.execute("i", q).results[0] for q in qs] for qs in reqs]
+        err = ""
+        try:
+            ex.execute("i", "Count(Row(f=1)) Count(Row(zz=1))")
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        with open(os.path.join(outdir, "pipe.json"), "w") as fh:
+            json.dump({"got": got, "want": want, "max_in_flight": mesh.max_in_flight, "seq": mesh.seq,
+                       "err": err, "rank_errors": mesh.last_count_text_errors}, fh)
+        mesh.stop()
+    finally:
+        ex.close()
+        holder.close()
+        dist.destroy_process_group()
+
+
+def test_mesh_count_text_pipelined(tmp_path):
+    mp.start_processes(_pipeline_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True,
+                       start_method="spawn")
+    res = json.load(open(tmp_path / "pipe.json"))
+    assert res["got"] == res["want"]
+    assert res["seq"] >= 24
+    assert res["max_in_flight"] >= 2, res["max_in_flight"]
+    assert "field not found" in res["err"] and res["rank_errors"], res
