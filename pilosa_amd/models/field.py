@@ -99,6 +99,12 @@ class FieldOptions:
     def from_json(cls, d: dict) -> "FieldOptions":
         """HTTP create-field options with per-type validation
         (http/handler.go:811-901)."""
+        if not isinstance(d, dict):
+            raise PilosaError(f"json: cannot unmarshal {type(d).__name__} into Go value of type fieldOptions")
+        known = ("type", "cacheType", "cacheSize", "min", "max", "timeQuantum", "keys", "noStandardView")
+        for k in d:
+            if k not in known:   # the reference decodes with DisallowUnknownFields
+                raise PilosaError(f'json: unknown field "{k}"')
         t = d.get("type", "") or ""
         o = cls(type=t)
         allowed = {

@@ -228,12 +228,15 @@ class Handler:
                 self._success(req, BadRequestError(e))
                 return
             for k, v in body.items():
-                if k != "options" or not isinstance(v, dict):
-                    self._success(req, BadRequestError(f"unknown key: {k}:{v}"))
+                if k == "options" and not isinstance(v, dict):
+                    self._success(req, BadRequestError("options is not map[string]interface{}"))
+                    return
+                if k != "options":
+                    self._success(req, BadRequestError(f"unknown key: {k}:{_go_fmt(v)}"))
                     return
                 for kk, vv in v.items():
                     if kk not in opts:
-                        self._success(req, BadRequestError(f"unknown key: {kk}:{vv}"))
+                        self._success(req, BadRequestError(f"unknown key: {kk}:{_go_fmt(vv)}"))
                         return
                     opts[kk] = vv
         try:
@@ -693,3 +696,16 @@ def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
     srv = _Srv((host, int(port)), _H)
     srv.daemon_threads = True
     return srv
+
+
+def _go_fmt(v) -> str:
+    """Go's %v of a decoded JSON value (the reference's error texts embed it)."""
+    if isinstance(v, dict):
+        return "map[" + " ".join(f"{k}:{_go_fmt(x)}" for k, x in sorted(v.items())) + "]"
+    if isinstance(v, list):
+        return "[" + " ".join(_go_fmt(x) for x in v) + "]"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if v is None:
+        return "<nil>"
+    return str(v)
