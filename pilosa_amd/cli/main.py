@@ -165,6 +165,7 @@ def cmd_import(args, stdout, stderr) -> int:
         print("field not found", file=stderr)
         return 1
     is_int = fld["options"].get("type") == "int"
+    is_bool = fld["options"].get("type") == "bool"
     use_col_keys = idx["options"].get("keys", False)
     use_row_keys = fld["options"].get("keys", False)
     node = Node("cli", uri)
@@ -175,8 +176,9 @@ def cmd_import(args, stdout, stderr) -> int:
         for rnum, rec in enumerate(csv.reader(fh), 1):
             if not rec or rec[0] == "":
                 continue
-            if len(rec) < 2:
-                print(f"bad column count on row {rnum}: col={len(rec)}", file=stderr)
+            err = _check_record(rec, rnum, is_int, is_bool, use_col_keys, use_row_keys)
+            if err:
+                print(err, file=stderr)
                 return 1
             buf.append(rec)
             if len(buf) >= args.buffer_size:
@@ -187,6 +189,34 @@ def cmd_import(args, stdout, stderr) -> int:
             fh.close()
     print(f"imported {total} records", file=stderr)
     return 0
+
+
+def _check_record(rec, rnum: int, is_int: bool, is_bool: bool, col_keys: bool, row_keys: bool) -> str:
+    """The reference importer's per-record checks (ctl/import.go
+    bufferBits / bufferValues): column count, numeric ids, timestamp format,
+    bool rows.  Returns the error text, "" when the record is good."""
+    if len(rec) < 2:
+        return f"bad column count on row {rnum}: col={len(rec)}"
+    if is_int:
+        if not col_keys and not rec[0].isdigit():
+            return f"invalid column id on row {rnum}: {rec[0]!r}"
+        try:
+            int(rec[1])
+        except ValueError:
+            return f"invalid value on row {rnum}: {rec[1]!r}"
+        return ""
+    if not row_keys and not rec[0].isdigit():
+        return f"invalid row id on row {rnum}: {rec[0]!r}"
+    if not col_keys and not rec[1].isdigit():
+        return f"invalid column id on row {rnum}: {rec[1]!r}"
+    if is_bool and not row_keys and int(rec[0]) not in (0, 1):
+        return "bool field imports only support values 0 and 1"
+    if len(rec) > 2 and rec[2]:
+        try:
+            dt.datetime.strptime(rec[2], "%Y-%m-%dT%H:%M")
+        except ValueError:
+            return f"invalid timestamp on row {rnum}: {rec[2]!r}"
+    return ""
 
 
 def _flush(c, node, args, buf, is_int, col_keys, row_keys) -> int:
