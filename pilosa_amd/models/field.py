@@ -192,7 +192,8 @@ class BSIGroup:
 class Field:
     def __init__(self, path: str, index: str, name: str, options: Optional[FieldOptions] = None,
                  max_opn: int = 10000, stats=None, persistent_attrs: bool = True):
-        validate_name(name) if not name.startswith("_") else None
+        if name != "_exists":   # the index's internal existence field
+            validate_name(name)
         self.path = path
         self.index = index
         self.name = name
@@ -388,6 +389,25 @@ class Field:
                 "views": [{"name": v} for v in sorted(self.views)]}
 
     # ------------------------------------------------------------ rows / bits
+    def set_time_quantum(self, q: str):
+        """Change the time quantum of a time field and persist it
+        (field.go setTimeQuantum)."""
+        if not valid_quantum(q):
+            raise ErrInvalidTimeQuantum
+        with self.mu:
+            self.options.time_quantum = q
+            self.save_meta()
+
+    def row_time(self, row_id: int, t: dt.datetime, quantum: str) -> Row:
+        """The row of the time view at ``quantum``'s finest unit that holds
+        ``t`` (field.go RowTime)."""
+        if not quantum or not valid_quantum(quantum):
+            raise ErrInvalidTimeQuantum
+        name = views_by_time(VIEW_STANDARD, t, quantum[-1])[0]
+        if self.view(name) is None:
+            raise PilosaError(f"view with quantum {quantum} not found.")
+        return self.row(row_id, name)
+
     def row(self, row_id: int, view: str = VIEW_STANDARD) -> Row:
         v = self.views.get(view)
         if v is None:

@@ -423,6 +423,15 @@ class Server {
 
   void set_count_batching(bool on) { count_batching_ = on; }
 
+  // A fixed 200 response for (method, path) with no query string, served by
+  // the epoll workers without a round trip through Python.
+  void set_static(const std::string& method, const std::string& path, const std::string& ctype, py::bytes body) {
+    std::string b = body;
+    std::lock_guard<std::mutex> g(smu_);
+    statics_[method + " " + path] = std::make_pair(ctype, std::move(b));
+    statics_empty_ = false;
+  }
+
   py::dict stats() {
     py::dict d;
     d["requests"] = requests_.load();
@@ -803,6 +812,29 @@ class Server {
                      "Access-Control-Allow-Headers: Content-Type, Accept\r\n");
         continue;
       }
+      if (r->query.empty() && !statics_empty_.load()) {
+        // fixed responses answered on the I/O thread (liveness probes: a
+        // busy Python worker pool must not make a node look dead)
+        std::string hit_ct, hit_body;
+        bool hit = false;
+        {
+          std::lock_guard<std::mutex> g(smu_);
+          auto it = statics_.find(r->method + " " + r->path);
+          if (it != statics_.end()) hit = true, hit_ct = it->second.first, hit_body = it->second.second;
+        }
+        if (hit) {
+          c.ready.emplace(r->seq, std::make_pair(make_response(200, hit_ct, hit_body.data(), hit_body.size(),
+                                                               r->close_after, nullptr),
+                                                 r->close_after));
+          drain_ready(c);
+          flush(c);
+          if (r->close_after) {
+            c.closing = true;
+            break;
+          }
+          continue;
+        }
+      }
       classify(*r, ctype, accept);
       r->conn = c.shared_from_this();
       r->id = next_id_++;
@@ -849,7 +881,9 @@ class Server {
  private:
   int lfd_ = -1, port_ = 0, nthreads_;
   size_t max_body_;
-  std::atomic<bool> running_{false}, stopping_{false}, count_batching_{true};
+  std::atomic<bool> running_{false}, stopping_{false}, count_batching_{true}, statics_empty_{true};
+  std::mutex smu_;
+  std::unordered_map<std::string, std::pair<std::string, std::string>> statics_;
   std::vector<std::thread> workers_;
   std::vector<int> epfds_, wakefds_;
   std::mutex qmu_;
@@ -1051,6 +1085,8 @@ PYBIND11_MODULE(_httpd, m) {
       .def("respond", &httpd::Server::respond)
       .def("respond_counts", &httpd::Server::respond_counts)
       .def("set_count_batching", &httpd::Server::set_count_batching)
+      .def("set_static", &httpd::Server::set_static, py::arg("method"), py::arg("path"), py::arg("content_type"),
+           py::arg("body"))
       .def("stats", &httpd::Server::stats);
   m.def("load", &httpd::load, py::arg("host"), py::arg("port"), py::arg("path"), py::arg("bodies"),
         py::arg("conns") = 128, py::arg("threads") = 4, py::arg("seconds") = 10.0, py::arg("samples") = 0,

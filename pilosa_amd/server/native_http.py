@@ -110,6 +110,14 @@ class NativeHTTPServer:
         # Count batching only pays with a device behind the executor
         server = self.handler.server
         self.srv.set_count_batching(server is None or getattr(server, "gpu", None) is not None)
+        # the liveness probe (GET /version, cluster membership) is answered by
+        # the epoll workers: a saturated worker pool cannot fail it
+        import json
+        try:
+            ver = self.handler.api.version()
+            self.srv.set_static("GET", "/version", "application/json", (json.dumps({"version": ver}) + "\n").encode())
+        except Exception:  # noqa: BLE001 - the Python route still answers
+            pass
         self.srv.start()
         for i in range(self.n_workers):
             self._spawn(self._generic_loop, f"http-worker-{i}")
