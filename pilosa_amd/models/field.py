@@ -303,9 +303,18 @@ class Field:
     def open(self):
         with self.mu:
             os.makedirs(self.path, exist_ok=True)
-            self.load_meta()
+            try:
+                self.load_meta()
+            except PilosaError:
+                raise
+            except Exception as e:  # noqa: BLE001 - a truncated / corrupt .meta
+                raise PilosaError(f"loading meta: unmarshaling: {_meta_err(e)}") from e
             self._load_available_shards()
-            self.row_attr_store.open()
+            try:
+                self.row_attr_store.open()
+            except Exception as e:  # noqa: BLE001
+                from pilosa_amd.models.index import _attr_err
+                raise PilosaError(f"opening attrstore: opening storage: {_attr_err(e)}") from e
             vdir = os.path.join(self.path, "views")
             os.makedirs(vdir, exist_ok=True)
             for name in sorted(os.listdir(vdir)):
@@ -591,3 +600,10 @@ class Field:
             frag = self.create_view_if_not_exists(name).create_fragment_if_not_exists(int(shard))
             changed += frag.import_roaring(data, clear)
         return changed
+
+
+def _meta_err(e: Exception) -> str:
+    msg = str(e)
+    if "truncated" in msg.lower() or "Truncated" in msg or "parse" in msg.lower():
+        return "unexpected EOF"
+    return msg

@@ -14,7 +14,7 @@ import threading
 import uuid
 from typing import Dict, List, Optional
 
-from pilosa_amd.errors import ErrIndexExists, ErrIndexNotFound, validate_name
+from pilosa_amd.errors import ErrIndexExists, ErrIndexNotFound, ErrName, PilosaError, validate_name
 from pilosa_amd.models.field import FieldOptions
 from pilosa_amd.models.index import Index
 from pilosa_amd.models.translate import TranslateFile
@@ -41,6 +41,7 @@ class Holder:
         self.on_create_shard = None   # (index, field, shard) -> None, set by the server (broadcast)
         self.on_schema_change = None  # () -> None, e.g. GPU arena invalidation
         self.snapshot_queue = None    # background snapshots, created by open() (holder.go:160)
+        self.logger = None            # open-time warnings (server sets its logger)
 
     # ------------------------------------------------------------ lifecycle
     def open(self, background: bool = False):
@@ -58,9 +59,15 @@ class Holder:
                 try:
                     validate_name(name)
                 except Exception:  # noqa: BLE001
+                    self._log(f"ERROR opening index: {name}, err={ErrName}")   # holder.go Open: logged, skipped
                     continue
                 idx = self._new_index(name)
-                idx.open()
+                try:
+                    idx.open()
+                except PilosaError as e:
+                    raise PilosaError(f"open index: name={name}, err={e}") from e
+                except OSError as e:
+                    raise PilosaError(f"open index: name={name}, err={e.strerror or e}") from e
                 self.indexes[name] = idx
         if background:
             self._flusher = threading.Thread(target=self._monitor_cache_flush, daemon=True)
@@ -185,7 +192,23 @@ class Holder:
             self.on_schema_change()
 
     def has_data(self) -> bool:
-        return bool(self.indexes)
+        """True when an index is open or the data dir holds an index
+        directory (holder.go HasData peeks before Open)."""
+        if self.indexes:
+            return True
+        try:
+            return any(not n.startswith(".") and os.path.isdir(os.path.join(self.path, n))
+                       for n in os.listdir(self.path))
+        except OSError:
+            return False
+
+    def _log(self, msg: str):
+        lg = getattr(self, "logger", None)
+        if lg is not None:
+            lg.printf("%s", msg)
+        else:
+            import sys
+            print(msg, file=sys.stderr)
 
     # ------------------------------------------------------------ schema
     def schema(self) -> List[dict]:

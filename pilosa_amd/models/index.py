@@ -12,7 +12,7 @@ import shutil
 import threading
 from typing import Dict, List, Optional
 
-from pilosa_amd.errors import ErrFieldExists, ErrFieldNotFound, ErrName, validate_name
+from pilosa_amd.errors import ErrFieldExists, ErrFieldNotFound, ErrName, PilosaError, validate_name
 from pilosa_amd.shardwidth import SHARD_WIDTH
 from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
 from pilosa_amd.models.cache import CACHE_TYPE_NONE
@@ -59,13 +59,19 @@ class Index:
         with self.mu:
             os.makedirs(self.path, exist_ok=True)
             self.load_meta()
-            self.column_attr_store.open()
+            try:
+                self.column_attr_store.open()
+            except Exception as e:  # noqa: BLE001
+                raise PilosaError(f"opening attrstore: opening storage: {_attr_err(e)}") from e
             for name in sorted(os.listdir(self.path)):
                 p = os.path.join(self.path, name)
                 if name.startswith(".") or not os.path.isdir(p):
                     continue
                 f = self._new_field(name, None)
-                f.open()
+                try:
+                    f.open()
+                except PilosaError as e:
+                    raise PilosaError(f"opening fields: open field: name={name}, err={e}") from e
                 self.fields[name] = f
             if self.track_existence:
                 self._open_existence_field()
@@ -150,3 +156,11 @@ class Index:
     def info(self) -> dict:
         return {"name": self.name, "options": self.options_json(),
                 "fields": [f.info() for f in self.public_fields()], "shardWidth": SHARD_WIDTH}
+
+
+def _attr_err(e: Exception) -> str:
+    """The reference's bolt wording for an unreadable attribute database."""
+    import sqlite3
+    if isinstance(e, sqlite3.DatabaseError):
+        return "invalid database"
+    return str(e)

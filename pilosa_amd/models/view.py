@@ -11,6 +11,7 @@ import shutil
 import threading
 from typing import Callable, Dict, List, Optional
 
+from pilosa_amd.errors import PilosaError
 from pilosa_amd.models.fragment import SHARD_WIDTH_EXP, Fragment, remove_stale_snapshots
 from pilosa_amd.models.row import Row
 
@@ -60,7 +61,10 @@ class View:
                 if not name.isdigit():
                     continue
                 shard = int(name)
-                frag = self._new_fragment(shard).open()
+                try:
+                    frag = self._new_fragment(shard).open()
+                except PilosaError as e:
+                    raise PilosaError(f"open fragment: shard={shard}, err=opening storage: {e}") from e
                 self.fragments[shard] = frag
         return self
 

@@ -75,6 +75,7 @@ class Server:
         if lazy_fragments is None or lazy_fragments:
             lazy_fragments = (gpu or "auto").lower() not in ("off", "none", "cpu") and _gpu_present()
         self.holder = Holder(data_dir, max_opn=max_opn, stats=self.stats, lazy_fragments=lazy_fragments)
+        self.holder.logger = self.logger
         self.client = InternalClient()
         # liveness probes use a short timeout so a hung peer is noticed quickly
         # (reference confirmNodeDown: 2 s per /version attempt, cluster.go:1699-1726)
