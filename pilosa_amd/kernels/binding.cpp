@@ -440,13 +440,14 @@ void rows_list(torch::Tensor view, int64_t s0, int64_t ns, int64_t j, int64_t co
 
 void container_merge(torch::Tensor old_meta, torch::Tensor payload, torch::Tensor dstart, torch::Tensor dlows,
                      torch::Tensor dmeta, torch::Tensor dpayload, int64_t mode, bool clear, torch::Tensor scratch,
-                     torch::Tensor card) {
+                     torch::Tensor card, torch::Tensor nruns) {
   const int64_t U = old_meta.numel();
   TORCH_CHECK(old_meta.is_cuda() && old_meta.scalar_type() == torch::kInt64 && old_meta.is_contiguous(),
               "old_meta int64[U]");
   TORCH_CHECK(payload.is_cuda() && payload.scalar_type() == torch::kInt16 && payload.is_contiguous(), "payload int16");
   TORCH_CHECK(scratch.scalar_type() == torch::kInt64 && scratch.numel() >= U * 1024, "scratch int64[U*1024]");
   TORCH_CHECK(card.scalar_type() == torch::kInt32 && card.numel() >= U, "card int32[U]");
+  TORCH_CHECK(nruns.is_cuda() && nruns.scalar_type() == torch::kInt32 && nruns.numel() >= U, "nruns int32[U]");
   TORCH_CHECK(mode == 0 || mode == 1, "mode 0 (positions) or 1 (containers)");
   if (mode == 0) {
     TORCH_CHECK(dstart.scalar_type() == torch::kInt32 && dstart.numel() == U + 1, "dstart int32[U+1]");
@@ -461,20 +462,21 @@ void container_merge(torch::Tensor old_meta, torch::Tensor payload, torch::Tenso
                              mode == 1 ? dmeta.data_ptr<int64_t>() : nullptr,
                              mode == 1 ? reinterpret_cast<const uint16_t*>(dpayload.data_ptr()) : nullptr, int(mode),
                              clear, reinterpret_cast<uint64_t*>(scratch.data_ptr<int64_t>()), card.data_ptr<int32_t>(),
-                             cur_stream(old_meta));
+                             nruns.data_ptr<int32_t>(), cur_stream(old_meta));
   check_launch("container_merge");
 }
 
-void container_emit(torch::Tensor scratch, torch::Tensor card, torch::Tensor off16, torch::Tensor jkey,
-                    torch::Tensor payload, torch::Tensor meta_out) {
+void container_emit(torch::Tensor scratch, torch::Tensor card, torch::Tensor nruns, torch::Tensor off16,
+                    torch::Tensor jkey, torch::Tensor payload, torch::Tensor meta_out) {
   const int64_t U = card.numel();
+  TORCH_CHECK(nruns.scalar_type() == torch::kInt32 && nruns.numel() == U, "nruns int32[U]");
   TORCH_CHECK(scratch.scalar_type() == torch::kInt64 && scratch.numel() >= U * 1024, "scratch int64[U*1024]");
   TORCH_CHECK(off16.scalar_type() == torch::kInt64 && off16.numel() == U, "off16 int64[U]");
   TORCH_CHECK(jkey.scalar_type() == torch::kInt32 && jkey.numel() == U, "jkey int32[U]");
   TORCH_CHECK(meta_out.scalar_type() == torch::kInt64 && meta_out.numel() == U, "meta_out int64[U]");
   TORCH_CHECK(payload.scalar_type() == torch::kInt16 && payload.is_contiguous(), "payload int16");
   pk::launch_container_emit(reinterpret_cast<const uint64_t*>(scratch.data_ptr<int64_t>()), card.data_ptr<int32_t>(),
-                            off16.data_ptr<int64_t>(), jkey.data_ptr<int32_t>(), U,
+                            nruns.data_ptr<int32_t>(), off16.data_ptr<int64_t>(), jkey.data_ptr<int32_t>(), U,
                             reinterpret_cast<uint16_t*>(payload.data_ptr()), meta_out.data_ptr<int64_t>(),
                             cur_stream(card));
   check_launch("container_emit");
@@ -524,7 +526,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rows_list", &rows_list, "flag dense rows with non-empty containers (optionally holding one column)");
   m.def("container_merge", &container_merge, "device write path: old container + delta -> bitmap + cardinality");
   m.def("payload_compact", &payload_compact, "copy live containers into a compacted payload buffer");
-  m.def("container_emit", &container_emit, "device write path: bitmap -> final array/bitmap container + metadata");
+  m.def("container_emit", &container_emit, "device write path: bitmap -> final run/array/bitmap container (Optimize rule) + metadata");
   m.def("densify", &densify, "dense bit rows of an arena over a shard range");
   m.def("bsi_sum", &bsi_sum, "bit-sliced integer sum with optional filter program", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("bsi_args"), py::arg("out_sum"), py::arg("out_cnt"),

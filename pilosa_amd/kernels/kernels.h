@@ -10,6 +10,7 @@ namespace pk {
 constexpr int MAXLEAF = 16;
 constexpr int MAXPROG = 32;
 constexpr int ARRAY_MAX = 4096;
+constexpr int RUN_MAX = 2048;
 constexpr int CT_ARRAY = 1, CT_BITMAP = 2, CT_RUN = 3;
 // opcodes: 0..MAXLEAF-1 push leaf k; then binary ops
 constexpr int OP_AND = 32, OP_OR = 33, OP_XOR = 34, OP_ANDNOT = 35;
@@ -153,16 +154,17 @@ void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_
 // container u -> scratch[u][1024] u64 bitmap + card[u]; mode 0 applies sorted
 // u16 lows dlows[dstart[u], dstart[u+1]), mode 1 the delta container dmeta[u]
 // (arena metadata into dpayload, -1 none); old_meta[u] = -1 for a new
-// container.  emit: final container u at u16 offset off16[u]*8 of payload
-// (array <= 4096 values, else bitmap) and its metadata word (-1 if empty).
+// container; nruns[u] = its number of runs.  emit: final container u at u16
+// offset off16[u]*8 of payload, encoded by the reference's Optimize rule
+// (run / array / bitmap), and its metadata word (-1 if empty).
 void launch_container_merge(const int64_t* old_meta, const uint16_t* payload, int64_t U, const int32_t* dstart,
                             const uint16_t* dlows, const int64_t* dmeta, const uint16_t* dpayload, int mode,
-                            bool clear, uint64_t* scratch, int32_t* card, hipStream_t st);
+                            bool clear, uint64_t* scratch, int32_t* card, int32_t* nruns, hipStream_t st);
 // Copy every live container (meta type != 0) of size size16[c] 16-byte units
 // from src to new_off16[c] of dst (payload compaction).
 void launch_payload_compact(const int64_t* meta, int64_t C, const int64_t* new_off16, const int64_t* size16,
                             const uint16_t* src, uint16_t* dst, hipStream_t st);
-void launch_container_emit(const uint64_t* scratch, const int32_t* card, const int64_t* off16, const int32_t* jkey,
-                           int64_t U, uint16_t* payload, int64_t* meta_out, hipStream_t st);
+void launch_container_emit(const uint64_t* scratch, const int32_t* card, const int32_t* nruns, const int64_t* off16,
+                           const int32_t* jkey, int64_t U, uint16_t* payload, int64_t* meta_out, hipStream_t st);
 
 }  // namespace pk

@@ -12,12 +12,15 @@
 //          applies the delta -- sorted u16 lows (positions mode) or a whole
 //          delta container (roaring mode) -- with OR or AND-NOT, and writes
 //          the bitmap plus its cardinality to scratch;
-//   emit:  after an exclusive scan of the output sizes (array <= 4096 values,
-//          padded to 8; bitmap 4096 u16; empty containers vanish), one
-//          workgroup per container writes the final container at the tail of
-//          the arena payload -- bitmap words copied, or the array's values
-//          produced by a workgroup prefix sum over per-thread popcounts --
-//          and its new metadata word.
+//   emit:  the container's encoding follows the reference's Optimize rule
+//          (roaring.go:2289-2338): run when runs <= 2048 and runs <= n/2,
+//          else array when n < 4096, else bitmap.  After an exclusive scan of
+//          the output sizes (run: 8-u16 header + (start, last) pairs; array:
+//          n values; both padded to 8; bitmap 4096 u16; empty containers
+//          vanish), one workgroup per container writes it at the tail of the
+//          arena payload -- bitmap words copied, the array's values or the
+//          runs' starts and lasts placed by workgroup prefix sums over
+//          per-thread popcounts -- and its new metadata word.
 //
 // The host then splices the new metadata words into the shard's segment.  Only
 // the write batch (8 B per position) crosses PCIe, never container payloads.
@@ -79,9 +82,10 @@ __global__ __launch_bounds__(WG) void container_merge_kernel(const int64_t* __re
                                                              const int64_t* __restrict__ dmeta,
                                                              const uint16_t* __restrict__ dpayload,
                                                              uint64_t* __restrict__ scratch,
-                                                             int32_t* __restrict__ card) {
+                                                             int32_t* __restrict__ card,
+                                                             int32_t* __restrict__ nruns) {
   __shared__ uint64_t bm[1024];
-  __shared__ int32_t red[WG / 64];
+  __shared__ int32_t red[WG / 64], redr[WG / 64];
   const int tid = threadIdx.x;
   const int64_t u = blockIdx.x;
   for (int i = tid; i < 1024; i += WG) bm[i] = 0;
@@ -103,23 +107,54 @@ __global__ __launch_bounds__(WG) void container_merge_kernel(const int64_t* __re
     if (dm >= 0) apply_container<CLEAR>(bm, dpayload, dm);
   }
   __syncthreads();
-  int c = 0;
+  int c = 0, r = 0;
   uint64_t* out = scratch + u * 1024;
 #pragma unroll
   for (int k = 0; k < WORDS_PER_THREAD; k++) {
     const int i = k * WG + tid;  // coalesced
     const uint64_t w = bm[i];
+    const uint64_t prev_top = i ? (bm[i - 1] >> 63) : 0ull;
     out[i] = w;
     c += __popcll(w);
+    r += __popcll(w & ~((w << 1) | prev_top));   // run starts: set bits whose predecessor is clear
   }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
-  if ((tid & 63) == 0) red[tid >> 6] = c;
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_down(c, o, 64);
+    r += __shfl_down(r, o, 64);
+  }
+  if ((tid & 63) == 0) red[tid >> 6] = c, redr[tid >> 6] = r;
   __syncthreads();
-  if (tid == 0) card[u] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) {
+    card[u] = red[0] + red[1] + red[2] + red[3];
+    nruns[u] = redr[0] + redr[1] + redr[2] + redr[3];
+  }
+}
+
+// The reference's Optimize choice for a container of n bits in `runs` runs.
+__device__ __forceinline__ int emit_type(int n, int runs) {
+  if (runs <= RUN_MAX && runs <= n / 2) return CT_RUN;
+  return n < ARRAY_MAX ? CT_ARRAY : CT_BITMAP;
+}
+
+// Exclusive workgroup scan of one int per thread (Hillis-Steele in LDS).
+__device__ __forceinline__ int wg_exclusive_scan(int32_t* scan, int v) {
+  const int tid = threadIdx.x;
+  scan[tid] = v;
+  __syncthreads();
+  for (int o = 1; o < WG; o <<= 1) {
+    const int x = tid >= o ? scan[tid - o] : 0;
+    __syncthreads();
+    scan[tid] += x;
+    __syncthreads();
+  }
+  const int at = scan[tid] - v;
+  __syncthreads();
+  return at;
 }
 
 __global__ __launch_bounds__(WG) void container_emit_kernel(const uint64_t* __restrict__ scratch,
                                                             const int32_t* __restrict__ card,
+                                                            const int32_t* __restrict__ nruns,
                                                             const int64_t* __restrict__ off16,
                                                             const int32_t* __restrict__ jkey,
                                                             uint16_t* __restrict__ payload,
@@ -134,7 +169,44 @@ __global__ __launch_bounds__(WG) void container_emit_kernel(const uint64_t* __re
     return;
   }
   const int64_t o16 = off16[u];
-  if (n > ARRAY_MAX) {
+  const int type = emit_type(n, nruns[u]);
+  if (type == CT_RUN) {
+    // thread t owns words [4t, 4t+4): run starts (bit set, predecessor clear)
+    // and lasts (bit set, successor clear) are numbered by two prefix sums;
+    // the k-th start and the k-th last form run k
+    uint64_t w[WORDS_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < WORDS_PER_THREAD; k++) w[k] = src[tid * WORDS_PER_THREAD + k];
+    const uint64_t before = tid ? src[tid * WORDS_PER_THREAD - 1] : 0ull;
+    const uint64_t after = tid + 1 < WG ? src[(tid + 1) * WORDS_PER_THREAD] : 0ull;
+    uint64_t st[WORDS_PER_THREAD], la[WORDS_PER_THREAD];
+    int cs = 0, cl = 0;
+#pragma unroll
+    for (int k = 0; k < WORDS_PER_THREAD; k++) {
+      const uint64_t prev_top = (k ? w[k - 1] : before) >> 63;
+      const uint64_t next_low = (k + 1 < WORDS_PER_THREAD ? w[k + 1] : after) & 1ull;
+      st[k] = w[k] & ~((w[k] << 1) | prev_top);
+      la[k] = w[k] & ~((w[k] >> 1) | (next_low << 63));
+      cs += __popcll(st[k]);
+      cl += __popcll(la[k]);
+    }
+    int as = wg_exclusive_scan(scan, cs);
+    int al = wg_exclusive_scan(scan, cl);
+    uint16_t* dst = payload + o16 * 8;
+#pragma unroll
+    for (int k = 0; k < WORDS_PER_THREAD; k++) {
+      const int base = (tid * WORDS_PER_THREAD + k) * 64;
+      for (uint64_t x = st[k]; x; x &= x - 1) dst[8 + 2 * (as++)] = uint16_t(base + __ffsll((long long)x) - 1);
+      for (uint64_t x = la[k]; x; x &= x - 1) dst[9 + 2 * (al++)] = uint16_t(base + __ffsll((long long)x) - 1);
+    }
+    const int nr = nruns[u];
+    const int used = 8 + 2 * nr, padded = (used + 7) & ~7;
+    if (tid < 8) dst[tid] = tid == 0 ? uint16_t(nr) : uint16_t(0);
+    if (tid < padded - used) dst[used + tid] = 0;
+    if (tid == 0) meta_out[u] = int64_t(jkey[u]) | (int64_t(CT_RUN) << 4) | (int64_t(n) << 6) | (o16 << 23);
+    return;
+  }
+  if (type == CT_BITMAP) {
     uint64_t* dst = reinterpret_cast<uint64_t*>(payload + o16 * 8);
     for (int i = tid; i < 1024; i += WG) dst[i] = src[i];
     if (tid == 0) meta_out[u] = int64_t(jkey[u]) | (int64_t(CT_BITMAP) << 4) | (int64_t(n) << 6) | (o16 << 23);
@@ -205,31 +277,31 @@ void launch_payload_compact(const int64_t* meta, int64_t C, const int64_t* new_o
 
 void launch_container_merge(const int64_t* old_meta, const uint16_t* payload, int64_t U, const int32_t* dstart,
                             const uint16_t* dlows, const int64_t* dmeta, const uint16_t* dpayload, int mode,
-                            bool clear, uint64_t* scratch, int32_t* card, hipStream_t st) {
+                            bool clear, uint64_t* scratch, int32_t* card, int32_t* nruns, hipStream_t st) {
   if (U <= 0) return;
   const dim3 g{unsigned(U)}, b{unsigned(WG)};
   if (mode == 0) {
     if (clear)
       hipLaunchKernelGGL((container_merge_kernel<true, 0>), g, b, 0, st, old_meta, payload, dstart, dlows, dmeta,
-                         dpayload, scratch, card);
+                         dpayload, scratch, card, nruns);
     else
       hipLaunchKernelGGL((container_merge_kernel<false, 0>), g, b, 0, st, old_meta, payload, dstart, dlows, dmeta,
-                         dpayload, scratch, card);
+                         dpayload, scratch, card, nruns);
   } else {
     if (clear)
       hipLaunchKernelGGL((container_merge_kernel<true, 1>), g, b, 0, st, old_meta, payload, dstart, dlows, dmeta,
-                         dpayload, scratch, card);
+                         dpayload, scratch, card, nruns);
     else
       hipLaunchKernelGGL((container_merge_kernel<false, 1>), g, b, 0, st, old_meta, payload, dstart, dlows, dmeta,
-                         dpayload, scratch, card);
+                         dpayload, scratch, card, nruns);
   }
 }
 
-void launch_container_emit(const uint64_t* scratch, const int32_t* card, const int64_t* off16, const int32_t* jkey,
-                           int64_t U, uint16_t* payload, int64_t* meta_out, hipStream_t st) {
+void launch_container_emit(const uint64_t* scratch, const int32_t* card, const int32_t* nruns, const int64_t* off16,
+                           const int32_t* jkey, int64_t U, uint16_t* payload, int64_t* meta_out, hipStream_t st) {
   if (U <= 0) return;
-  hipLaunchKernelGGL(container_emit_kernel, dim3(unsigned(U)), dim3(WG), 0, st, scratch, card, off16, jkey, payload,
-                     meta_out);
+  hipLaunchKernelGGL(container_emit_kernel, dim3(unsigned(U)), dim3(WG), 0, st, scratch, card, nruns, off16, jkey,
+                     payload, meta_out);
 }
 
 }  // namespace pk

@@ -650,17 +650,22 @@ class DeviceView:
             n = c1 - c0
             scratch = torch.empty(n * 1024, dtype=torch.int64, device=dev)
             card = torch.empty(n, dtype=torch.int32, device=dev)
+            nruns = torch.empty(n, dtype=torch.int32, device=dev)
             if mode == 0:
                 a, b = int(dstart[c0]), int(dstart[c1])
                 ds = torch.from_numpy((dstart[c0:c1 + 1] - a).astype(np.int32)).to(dev)
                 K.container_merge(t_old[c0:c1], self.t_payload, ds, t_lows[a:b], empty64, empty16, 0, clear, scratch,
-                                  card)
+                                  card, nruns)
             else:
                 K.container_merge(t_old[c0:c1], self.t_payload, empty32, empty16, t_dmeta[c0:c1], t_dpay, 1, clear,
-                                  scratch, card)
-            c64 = card.to(torch.int64)
+                                  scratch, card, nruns)
+            c64, r64 = card.to(torch.int64), nruns.to(torch.int64)
+            # the reference's Optimize choice (write_kernels.hip emit_type):
+            # run if runs <= 2048 and runs <= n/2, array if n < 4096, else bitmap
+            is_run = (r64 <= 2048) & (r64 <= c64 // 2)
             sizes = torch.where(c64 == 0, torch.zeros_like(c64),
-                                torch.where(c64 > 4096, torch.full_like(c64, 4096), (c64 + 7) // 8 * 8))
+                                torch.where(is_run, (8 + 2 * r64 + 7) // 8 * 8,
+                                            torch.where(c64 < 4096, (c64 + 7) // 8 * 8, torch.full_like(c64, 4096))))
             ends = torch.cumsum(sizes, 0)
             tot = int(ends[-1])
             if used + tot > int(self.t_payload.numel()):
@@ -671,7 +676,7 @@ class DeviceView:
                     return {jb[0] for jb in jobs}
             off16 = (ends - sizes + used) // 8
             meta_out = torch.empty(n, dtype=torch.int64, device=dev)
-            K.container_emit(scratch, card, off16, t_j[c0:c1], self.t_payload, meta_out)
+            K.container_emit(scratch, card, nruns, off16, t_j[c0:c1], self.t_payload, meta_out)
             new_meta[c0:c1] = meta_out.cpu().numpy()
             used += tot
         self.payload_used = used
@@ -684,7 +689,9 @@ class DeviceView:
             keep = nm >= 0
             old_n = (old >> 6) & 0x1FFFF
             old_t = (old >> 4) & 3
-            self.garbage_u16 += int(np.where(found, np.where(old_t == 2, 4096, (old_n + 7) // 8 * 8), 0).sum())
+            # a run container's size is in its header, not its metadata: count the header only
+            self.garbage_u16 += int(np.where(found, np.where(old_t == 2, 4096, np.where(old_t == 3, 8, (old_n + 7) // 8 * 8)),
+                                             0).sum())
             base = int(self._sb_host[si])
             if not (found & ~keep).any() and not (~found & keep).any():
                 pos = base + idx[found]

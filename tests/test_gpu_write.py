@@ -192,3 +192,42 @@ def test_compaction_on_device(view):
     assert dv.apply_positions(2, p)
     host[2].add_many(np.unique(p), True)
     _check(dv, host)
+
+
+def _types(dv, si):
+    """{container key: encoding} of shard si as the arena holds it."""
+    rp = dv._rowptr_host[si]
+    base = int(dv._sb_host[si])
+    out = {}
+    for d in range(dv.D):
+        row = int(dv.rows[d])
+        for ci in range(base + rp[d], base + rp[d + 1]):
+            m = int(dv._meta_host[ci])
+            out[row * 16 + (m & 15)] = {1: "array", 2: "bitmap", 3: "run"}[(m >> 4) & 3]
+    return out
+
+
+def test_device_writes_emit_optimized_container_types(view):
+    """K9: containers the device writes are encoded by the reference's
+    Optimize rule (run / array / bitmap, roaring.go:2289-2338), exactly as the
+    host roaring core optimises the same container (runs from a long range,
+    arrays below 4096 bits, bitmaps at 4096 and above)."""
+    dv, host, rng = view
+    pos = np.concatenate([
+        np.uint64(20) * np.uint64(SW) + np.arange(30000, dtype=np.uint64),                    # one long run
+        np.uint64(21) * np.uint64(SW) + np.arange(0, 60000, 3, dtype=np.uint64),              # bitmap, many runs
+        np.uint64(22) * np.uint64(SW) + np.sort(rng.choice(65536, 300, replace=False)).astype(np.uint64),  # array
+        np.uint64(23) * np.uint64(SW) + np.arange(0, 8192, 2, dtype=np.uint64),               # exactly 4096 bits
+        np.uint64(24) * np.uint64(SW) + (np.arange(2000, dtype=np.uint64) * np.uint64(32))[:, None].repeat(4, 1).ravel()
+        + np.tile(np.arange(4, dtype=np.uint64), 2000),                                        # 2000 runs of 4
+    ]).astype(np.uint64)
+    assert dv.apply_positions(1, pos, clear=False)
+    host[1].add_many(np.unique(pos), True)
+    _check(dv, host)
+    opt = host[1].clone()
+    opt.optimize()
+    want = {k: t for k, t, _ in opt.container_info()}
+    got = _types(dv, 1)
+    for k in (20 * 16, 21 * 16, 22 * 16, 23 * 16, 24 * 16):
+        assert got[k] == want[k], (k, got[k], want[k])
+    assert got[20 * 16] == "run" and got[22 * 16] == "array" and got[23 * 16] == "bitmap"
