@@ -80,6 +80,8 @@ def cmd_server(args, stdout, stderr) -> int:
         return M.run_worker(cfg.data_dir(), gpu_mode=cfg.get("gpu.mode"), block=cfg.get("gpu.shard-block"),
                             timeout_s=cfg.duration("gpu.rccl-timeout"),
                             logger=logger)
+    from pilosa_amd.utils import syswrap
+    syswrap.set_max_map_count(cfg.get("max-map-count"))   # server.Command: syswrap.SetMaxMapCount
     bind = cfg.get("bind")
     if bind.startswith(":"):
         bind = "0.0.0.0" + bind

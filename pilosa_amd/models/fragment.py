@@ -194,18 +194,30 @@ class Fragment:
         return self._storage is None
 
     def _cold(self):
-        """The mapped view of a cold fragment (created on first use)."""
+        """The mapped view of a cold fragment (created on first use).  Past
+        the process's map-count cap (utils/syswrap.py) the file is read into
+        heap instead, as the reference falls back when mmap is refused."""
         with self.mu:
             m = self._mapped
             if m is None:
+                from pilosa_amd.utils import syswrap
+                if not syswrap.try_acquire():
+                    return self._load_cold()
                 try:
                     m = _roaring.MappedBitmap(self.path)
                 except Exception as e:  # noqa: BLE001
+                    syswrap.release()
                     raise PilosaError(f"unmarshal storage: file={self.path}, err={e}")
                 self._mapped = m
                 self.opn, self.ops = int(m.opn), int(m.ops)
                 self._max_row_id = int(m.max()) // SHARD_WIDTH if m.any() else 0
             return m
+
+    def _drop_mapped(self):
+        if self._mapped is not None:
+            from pilosa_amd.utils import syswrap
+            self._mapped = None
+            syswrap.release()
 
     def _rw(self):
         """Storage for the operations the mapped view offers: the heap
@@ -235,7 +247,7 @@ class Fragment:
                 self.opn = int(bm.opn)
                 self.ops = int(bm.ops)
                 self._storage = bm
-                self._mapped = None   # the file holds every write the mapped view took
+                self._drop_mapped()   # the file holds every write the mapped view took
                 self._max_row_id = int(bm.max()) // SHARD_WIDTH if bm.any() else 0
             if self._cache_pending:
                 self._cache_pending = False
@@ -317,6 +329,7 @@ class Fragment:
                 self.flush_cache()
             except OSError:
                 pass
+            self._drop_mapped()
             if self._fh is not None:
                 try:
                     fcntl.flock(self._fh.fileno(), fcntl.LOCK_UN)

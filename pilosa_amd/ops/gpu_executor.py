@@ -98,6 +98,7 @@ class GpuExecutor:
         # their candidates / re-counts node-wide (every rank runs the same calls)
         self.comm = None
         self._spaces: Dict[Tuple, Tuple] = {}
+        self._frag_lists: Dict[Tuple, Tuple] = {}   # (index, field, shards) -> (epoch, fragments)
         self.topn_decline = ""          # why the last topn_batch returned None (diagnostics)
         self._topn_index_why = ""
 
@@ -277,6 +278,7 @@ class GpuExecutor:
             self._bsi_views.clear()
             self._topn_indexes.clear()
             self._rank_cache_map.clear()
+            self._frag_lists.clear()
 
     BSI_CACHE = 8
 
@@ -846,11 +848,7 @@ class GpuExecutor:
         fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
         if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
             raise NotImplementedError
-        frags = [self.holder.fragment(index, fname, VIEW_STANDARD, s) for s in shards]
-        for f in frags:
-            if f is not None and f.cache_type == "none":
-                from pilosa_amd.errors import PilosaError
-                raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
+        frags = self._topn_frags(index, fname, shards)
         rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
         src = self.plan(index, c.children[0], shards) if c.children else None
         rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
@@ -893,11 +891,7 @@ class GpuExecutor:
                 return None   # explicit ids= (phase 2 only): the map-step path
             params.append((fname, n, threshold))
             if fname not in fields:
-                frags = [self.holder.fragment(index, fname, VIEW_STANDARD, s) for s in shards]
-                for f in frags:
-                    if f is not None and f.cache_type == "none":
-                        from pilosa_amd.errors import PilosaError
-                        raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
+                frags = self._topn_frags(index, fname, shards)
                 rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
                 rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
                 fields[fname] = (rv, rc)
@@ -936,6 +930,24 @@ class GpuExecutor:
             for i, r in zip(live, got):
                 out[i] = r
         return out
+
+    def _topn_frags(self, index: str, fname: str, shards: List[int]):
+        """The field's standard-view fragments of ``shards`` (cache type
+        checked), memoised while no fragment is created, written or dropped
+        (the mutation epoch): a TopN request over ~1k shards would otherwise
+        spend a millisecond on holder lookups alone."""
+        key = (index, fname, tuple(shards))
+        epoch = mutation_epoch()
+        ent = self._frag_lists.get(key)
+        if ent is not None and ent[0] == epoch:
+            return ent[1]
+        frags = [self.holder.fragment(index, fname, VIEW_STANDARD, s) for s in shards]
+        for f in frags:
+            if f is not None and f.cache_type == "none":
+                from pilosa_amd.errors import PilosaError
+                raise PilosaError(f'cannot compute TopN(), field has no cache: "{fname}"')
+        self._frag_lists[key] = (epoch, frags)
+        return frags
 
     def _topn_pairs_path(self, rc, rv, src, n: int, ids, threshold: int) -> List[Pair]:
         """Src TopN without a slot index (while it is rebuilt, or too large for

@@ -187,15 +187,18 @@ class DeviceRankCaches:
             mt = torch.tensor([max(1, int(t)) for t in thresholds[q0:q1]], dtype=torch.int32).to(dev)
             cnt = self.cache_cnt[:, :nmax]
             dn = self.cache_dense[:, :nmax]
+            # accumulate over the candidate rows only (the union of the shards'
+            # first nmax cache entries), not a dense [queries x D] row space
+            u, inv = torch.unique(dn.clamp(min=-1), return_inverse=True)
+            U = int(u.numel())
             k = torch.arange(nmax, device=dev)
             take = (k[None, None, :] < lim[:, None, None]) & (cnt[None] >= mt[:, None, None]) & (dn[None] >= 0)
             vals = torch.where(take, cnt[None], torch.zeros((), dtype=torch.int32, device=dev))
-            acc = torch.zeros((q1 - q0, D), dtype=torch.int32, device=dev)
-            acc.scatter_add_(1, dn.clamp(min=0).reshape(1, -1).expand(q1 - q0, -1).to(torch.int64),
-                             vals.reshape(q1 - q0, -1))
+            acc = torch.zeros((q1 - q0, U), dtype=torch.int32, device=dev)
+            acc.scatter_add_(1, inv.reshape(1, -1).expand(q1 - q0, -1), vals.reshape(q1 - q0, -1))
             nz = torch.nonzero(acc > 0)
             qs.append(nz[:, 0] + q0)
-            ds.append(nz[:, 1])
+            ds.append(u[nz[:, 1]].to(torch.int64))
             cs.append(acc[nz[:, 0], nz[:, 1]].to(torch.int64))
         if not qs:
             z = torch.zeros(0, dtype=torch.int64, device=dev)

@@ -402,9 +402,9 @@ def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) 
     lim = torch.tensor([int(n) if int(n) else (1 << 62) for n in ns], dtype=torch.int64).to(dev)
     rank = torch.arange(pq.numel(), device=dev) - bounds[pq]
     sel = rank < lim[pq]
-    q_h = pq[sel].cpu().numpy()
-    a_h = pa[sel].cpu().numpy()
-    c_h = cnt[sel].cpu().numpy()
+    # one device -> host copy for the kept pairs
+    qac = torch.stack([pq[sel].to(torch.int64), pa[sel], cnt[sel].to(torch.int64)]).cpu().numpy()
+    q_h, a_h, c_h = qac[0], qac[1], qac[2]
     ids = space[a_h]
     out: List[List[Pair]] = [[] for _ in range(Q)]
     for qq, i, c in zip(q_h.tolist(), ids.tolist(), c_h.tolist()):

@@ -131,3 +131,28 @@ def test_cold_bulk_import_and_snapshot_stay_off_heap():
         full.close()
     finally:
         shutil.rmtree(base, ignore_errors=True)
+
+
+def test_map_count_cap_falls_back_to_heap():
+    """syswrap: past max-map-count a cold fragment is read into heap instead
+    of mapped (reference syswrap/mmap.go ErrMaxMapCountReached), and closing
+    fragments gives their map slots back."""
+    from pilosa_amd.utils import syswrap
+    base = tempfile.mkdtemp(prefix="cold_cap_")
+    old_max = syswrap.max_map_count()
+    try:
+        _make(base)
+        holder = Holder(base, lazy_fragments=True).open()
+        frags = holder.view("i", "f", "standard").all_fragments()
+        c0 = syswrap.map_count()
+        syswrap.set_max_map_count(c0 + 2)
+        for fr in frags[:3]:
+            fr.row_count(1)
+        assert [fr.mapped_stats() is not None for fr in frags[:3]] == [True, True, False]
+        assert frags[0].is_cold() and frags[1].is_cold() and not frags[2].is_cold()
+        assert syswrap.map_count() == c0 + 2
+        holder.close()
+        assert syswrap.map_count() == c0
+    finally:
+        syswrap.set_max_map_count(old_max)
+        shutil.rmtree(base, ignore_errors=True)
