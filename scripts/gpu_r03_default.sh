@@ -14,4 +14,5 @@ print("topn", json.dumps({k: e["topn"][k] for k in ("cache", "src", "fragments_c
 print("cfg4", json.dumps(e.get("config4_bsi"))[:2500])
 print("cfg5", json.dumps(e.get("config5_time_union"))[:1500])
 print("data", e.get("data"))
+print("serving", json.dumps(e.get("serving"))[:3000])
 PY
