@@ -392,6 +392,20 @@ class Executor:
                 if self.stats is not None:
                     self.stats.count_with_tags("Sum", len(res), [f"index:{index}"])
                 return res
+        # TopN requests on a multi-GPU node: every rank's device runs both
+        # phases, candidates and re-counts merge over the collectives
+        if self._use_mesh(opt) and q.calls and all(c.name == "TopN" for c in q.calls) and not opt.remote and \
+                not self._has_remote(index, shards, opt) and not any("ids" in c.args for c in q.calls):
+            for c in q.calls:
+                self._validate_call_args(c)
+            try:
+                res = self.mesh.topn_batch(index, q.calls, shards)
+            except MeshError:
+                if not self.mesh.failed_over:
+                    raise
+                res = None
+            if res is not None:
+                return res
         # TopN requests on a local GPU: both phases of every call on the device
         # (ops/topn_exec.py); concurrent single-TopN requests share launches
         if self.gpu is not None and q.calls and all(c.name == "TopN" for c in q.calls) and not opt.remote and \

@@ -29,6 +29,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from pilosa_amd.errors import PilosaError
 from pilosa_amd.models.cache import Pair, sort_pairs
 from pilosa_amd.models.fragment import SHARD_WIDTH, mutation_epoch
 from pilosa_amd.models.index import EXISTENCE_FIELD_NAME
@@ -930,6 +931,35 @@ class GpuExecutor:
             for i, r in zip(live, got):
                 out[i] = r
         return out
+
+    def topn_batch_ready(self, index: str, calls: List[Call], shards: List[int]) -> bool:
+        """Would :meth:`topn_batch` answer these calls on the device, with
+        every call taking part in the batch's collectives?  Resolves (and
+        builds) what it needs -- rank caches, slot index -- without any
+        collective, so the ranks of a node can agree on the answer first
+        (parallel/mesh.py OP_TOPN)."""
+        if not shards:
+            return False
+        ex = self._ex()
+        try:
+            for c in calls:
+                fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
+                if ids or tanimoto or (attr_name and attr_values) or len(c.children) > 1:
+                    return False
+                frags = self._topn_frags(index, fname, shards)
+                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+                if rv is None:
+                    return False
+                rc = self._rank_caches(index, fname, shards, frags, rv)
+                if rc is None or not rc.K:
+                    return False
+                if c.children:
+                    src = self.plan(index, c.children[0], shards)
+                    if src is EMPTY or self._topn_index(index, fname, shards, rc, rv) is None:
+                        return False
+        except (NotImplementedError, PilosaError):
+            return False
+        return True
 
     def _topn_frags(self, index: str, fname: str, shards: List[int]):
         """The field's standard-view fragments of ``shards`` (cache type

@@ -45,7 +45,7 @@ class MeshError(RuntimeError):
 
 # ---------------------------------------------------------------- transport
 (OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS, OP_COUNT_TEXT,
- OP_ERRORS) = range(11)
+ OP_ERRORS, OP_TOPN) = range(12)
 MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
 
 
@@ -93,6 +93,7 @@ class ShardMesh:
         self._pending = collections.deque()   # worker: (tensor, work) of batches in flight
         self._errors: Dict[int, BaseException] = {}
         self.last_count_text_errors: List[str] = []
+        self.topn_tensor_batches = 0
 
     # ------------------------------------------------------------ ownership
     def owner(self, shard: int) -> int:
@@ -208,6 +209,19 @@ class ShardMesh:
                 self.failover(e)
                 raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
 
+    def topn_batch(self, index: str, calls, shards: Sequence[int]):
+        """Whole TopN calls on every rank's GPU with the node-wide merge on
+        tensors (ops/topn_exec.py / topn_index.py with ``comm``): the ranks
+        all-gather and union their phase-1 candidate keys and all-reduce the
+        ids= re-counts, so the answers come back complete on every rank
+        (executor.go:863-903 over RCCL instead of per-shard pair lists).  The
+        ranks first agree (one all-reduce of a flag) that each can run the
+        batch on its device; None = use the general path."""
+        res = self._run(OP_TOPN, index, [str(c) for c in calls], list(shards))
+        if res is not None:
+            self.topn_tensor_batches += 1
+        return res
+
     def _host_list(self, t) -> List[int]:
         gpu = getattr(self.executor, "gpu", None)
         if t.device.type == "cuda" and gpu is not None and hasattr(gpu, "engine"):
@@ -322,6 +336,8 @@ class ShardMesh:
                 if self.is_frontend:
                     _raise_remote(parts)
             return out[:-1]
+        if op == OP_TOPN:
+            return self._topn_batch_local(*args)
         mine = None
         try:
             if op == OP_CALL:
@@ -363,6 +379,34 @@ class ShardMesh:
         if self.is_frontend:
             _raise_remote(parts)
         return parts
+
+    def _topn_batch_local(self, index: str, pqls: List[str], shards: List[int]):
+        from pilosa_amd.pql import parse_string
+
+        torch = self.torch
+        ex = self.executor
+        gpu = ex.gpu
+        own = self.owned(shards)
+        ok = False
+        calls = []
+        try:
+            calls = [parse_string(p).calls[0] for p in pqls]
+            ok = gpu is not None and ex.holder.index(index) is not None and gpu.topn_batch_ready(index, calls, own)
+        except Exception:  # noqa: BLE001 - a rank that cannot take part declines
+            ok = False
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=self.device)
+        self.comm.all_reduce(flag)
+        if int(flag.item()):
+            return None
+        prev = gpu.comm
+        gpu.comm = self.comm
+        try:
+            res = gpu.topn_batch(index, calls, own)
+        finally:
+            gpu.comm = prev
+        if res is None:   # every rank checked readiness: a decline now would desynchronise
+            raise MeshError(f"rank {self.rank}: TopN batch declined after the readiness check")
+        return res
 
     def _count_text_issue(self, index: str, text: str, shards: List[int], q: int, seq: int):
         """This rank's counts for its own shards as a device tensor (plus an
