@@ -33,7 +33,10 @@
 // staging (v7, 18.5 ms: lower occupancy, probes unchanged) and lane-interleaved
 // u16 probes (v8, 24.0 ms: 5x the load instructions although LDS conflicts
 // fell from 0.52 to 0.33 of the LDS cycles) and an XOR-swizzled LDS bitmap
-// (18.8 ms, see lds_swz).
+// (18.8 ms, see lds_swz); every load of a container issued before any of it
+// is consumed (v9, 20.9 ms: one round trip per array instead of one per
+// 512 values, but slower -- the chunked walk is not latency-bound,
+// profiles/r03_v9/).
 //
 // Reference hot loops replaced: roaring/roaring.go:3078-3215 intersectionCount*
 // and executor.go:1230-1290 (executeCount over executeIntersect).
@@ -555,21 +558,25 @@ void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st
 // for API stability; every value runs v6.
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
                        int cq, int variant, hipStream_t st) {
-  (void)variant;
   const int64_t items = int64_t(Q) * S;
   if (items == 0) return;
   hipLaunchKernelGGL(pair_build_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, progs, Q, views, S,
                      pairs);
   const int64_t units = int64_t(S) * 16;
   if (cq <= 0) cq = Q <= 2048 ? 32 : 64;
-  switch (cq) {
-    case 16: { const int64_t wv = units * ((Q + 15) / 16);
-      hipLaunchKernelGGL(and2_pairs_v6_kernel<16>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); } break;
-    case 32: { const int64_t wv = units * ((Q + 31) / 32);
-      hipLaunchKernelGGL(and2_pairs_v6_kernel<32>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); } break;
-    default: { const int64_t wv = units * ((Q + 63) / 64);
-      hipLaunchKernelGGL(and2_pairs_v6_kernel<64>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); } break;
+  (void)variant;
+#define PK_LAUNCH(CQV)                                                                                      \
+  {                                                                                                         \
+    const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                       \
+    hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, \
+                       pairs, partial);                                                                     \
   }
+  switch (cq) {
+    case 16: PK_LAUNCH(16) break;
+    case 32: PK_LAUNCH(32) break;
+    default: PK_LAUNCH(64) break;
+  }
+#undef PK_LAUNCH
 }
 
 }  // namespace pk

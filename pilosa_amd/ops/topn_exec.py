@@ -238,6 +238,8 @@ class DeviceRankCaches:
         Q = len(ns)
         if Q == 0:
             return []
+        if comm is None and self.view.D and self.S < 2048:   # counts < 2^31: composite int64 key
+            return self._topn_nosrc_dense(ns, thresholds)
         pq, pd, _ = self.nosrc_phase1(ns, thresholds)
         if comm is None:
             out = self.recount(pq, pd, thresholds)
@@ -252,6 +254,79 @@ class DeviceRankCaches:
         out = self.recount(pq, local.clamp(min=-1), thresholds)
         comm.all_reduce(out)
         return finish_batch_dev(np.asarray(space, dtype=np.uint64), Q, pq, pa, out, ns)
+
+    def _candidates(self, nmax: int):
+        """(u, inv) = torch.unique of the first ``nmax`` ranks of every shard:
+        the candidate rows of a cache-only phase 1 (dense ids, -1 = empty) and
+        each rank's candidate index.  A property of the rank caches, memoised
+        per prefix length (this object is rebuilt when the caches change)."""
+        import torch
+        memo = self.__dict__.setdefault("_cand", {})
+        got = memo.get(nmax)
+        if got is None:
+            u, inv = torch.unique(self.cache_dense[:, :nmax].clamp(min=-1), return_inverse=True)
+            got = (u, inv.reshape(-1))
+            memo[nmax] = got
+        return got
+
+    def _topn_nosrc_dense(self, ns: Sequence[int], thresholds: Sequence[int]) -> List[List[Pair]]:
+        """Single-rank cache-only TopN batch without a host round trip until
+        the end: phase 1 accumulates every query's cache prefixes into a
+        [Q, candidates] matrix, phase 2 re-counts each candidate row once per
+        distinct threshold (row_counts_sum), and one top-k over the composite
+        key (count desc, id asc) trims each query to n; only the Q x n pairs
+        are copied to the host.  Same answers as nosrc_phase1 + recount +
+        finish_batch_dev, with no data-dependent shapes (no syncs) on the way."""
+        import torch
+        dev = self.view.device
+        Q = len(ns)
+        nn = [int(n) for n in ns]
+        nmax = self.K if any(n == 0 for n in nn) else min(self.K, max(nn))
+        if not nmax:
+            return [[] for _ in range(Q)]
+        u, inv = self._candidates(nmax)
+        U = int(u.numel())
+        ths = [max(1, int(t)) for t in thresholds]
+        uniq_t = sorted(set(ths))
+        lim_mt = torch.tensor([[n if n else self.K for n in nn], ths], dtype=torch.int64).to(dev, non_blocking=True)
+        lim, mt = lim_mt[0], lim_mt[1].to(torch.int32)
+        cnt = self.cache_cnt[:, :nmax]
+        dn = self.cache_dense[:, :nmax]
+        k = torch.arange(nmax, device=dev)
+        take = (k[None, None, :] < lim[:, None, None]) & (cnt[None] >= mt[:, None, None]) & (dn[None] >= 0)
+        vals = torch.where(take, cnt[None], torch.zeros((), dtype=torch.int32, device=dev))
+        acc = torch.zeros((Q, U), dtype=torch.int32, device=dev)
+        acc.scatter_add_(1, inv.reshape(1, -1).expand(Q, -1), vals.reshape(Q, -1))
+        # phase 2: every candidate row re-counted once per distinct threshold
+        ud = u.clamp(min=0).to(torch.int32).contiguous()
+        res = torch.zeros((len(uniq_t), U), dtype=torch.int64, device=dev)
+        for ti, t in enumerate(uniq_t):
+            kernels().row_counts_sum(self.view.viewdev_tensor(), self.S, ud,
+                                     torch.full((U,), t, dtype=torch.int32, device=dev), res[ti])
+        if len(uniq_t) == 1:
+            tot = res[0][None, :].expand(Q, -1)
+        else:
+            tsel = torch.tensor([uniq_t.index(t) for t in ths], dtype=torch.int64).to(dev)
+            tot = res[tsel]
+        live = (acc > 0) & (u >= 0)[None, :]
+        score = torch.where(live, tot, torch.zeros((), dtype=torch.int64, device=dev))
+        # composite key: count desc, then dense (= row id) asc
+        key = (score << 32) | (0xFFFFFFFF - u.clamp(min=0).to(torch.int64))[None, :]
+        key = torch.where(score > 0, key, torch.full((), -1, dtype=torch.int64, device=dev))
+        kk = min(U, nmax if all(nn) else U)
+        top = torch.topk(key, kk, dim=1, sorted=True).values
+        h = top.cpu().numpy()
+        rows = self.view.rows
+        out: List[List[Pair]] = []
+        for q in range(Q):
+            r = h[q]
+            r = r[r >= 0]
+            if nn[q]:
+                r = r[:nn[q]]
+            d = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
+            ids = rows[d] if len(d) else np.zeros(0, np.uint64)
+            out.append([Pair(int(i), int(c)) for i, c in zip(ids.tolist(), (r >> 32).tolist())])
+        return out
 
     def shard_pairs_nosrc(self, n: int, threshold: int, ids: Optional[Sequence[int]] = None) -> List[Pair]:
         """One cache-only TopN call as the executor's map step sees it: phase 1

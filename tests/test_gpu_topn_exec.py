@@ -132,3 +132,20 @@ def test_topn_after_writes_uses_warm_caches(lazy_env):
     finally:
         ex.gpu = gpu
     assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
+
+
+def test_nosrc_dense_batch_equals_two_phase(lazy_env):
+    """The sync-free cache-only batch (one [Q, candidates] accumulator, one
+    re-count per threshold, one top-k) answers exactly as phase 1 + ids=
+    re-count + finish_batch_dev, for mixed n (0 = all) and thresholds."""
+    from pilosa_amd.ops.topn_index import finish_batch_dev
+    holder, ex, gpu, want, _ = lazy_env
+    ex.execute("i", "TopN(h, n=10)")
+    rc = next(iter(gpu._rank_cache_map.values()))[1]
+    ns = [10, 100, 0, 20, 1, 7, 100, 3]
+    ths = [1, 1, 1, 300, 1, 2, 50, 1]
+    got = rc._topn_nosrc_dense(ns, ths)
+    pq, pd, _ = rc.nosrc_phase1(ns, ths)
+    ref = finish_batch_dev(rc.view.rows, len(ns), pq, pd, rc.recount(pq, pd, ths), ns)
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in ref]
+    assert _pairs(got[0]) == _pairs(want["TopN(h, n=10)"])
