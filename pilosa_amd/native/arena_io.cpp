@@ -103,7 +103,7 @@ struct Shard {
   const uint8_t* offs = nullptr; // keyn x u32
   int64_t containers = 0;        // with n > 0
   int64_t payload = 0;           // arena u16
-  uint64_t last_row = 0;
+  uint64_t last_key = 0;         // highest container key (row << key_shift | j)
   bool replayed = false;
 
   void release() {
@@ -118,7 +118,12 @@ struct Shard {
 
 class FragmentLoader {
  public:
-  FragmentLoader(std::vector<std::string> paths, int nthreads) : nthreads_(std::max(1, nthreads)) {
+  // key_shift = log2(containers per row) = shard-width exponent - 16: 4 for
+  // 2^20-column shards; 0..3 for narrower shards, whose rows then fill only
+  // the first 2^key_shift of the arena's 16 container slots per row.
+  FragmentLoader(std::vector<std::string> paths, int nthreads, int key_shift = 4)
+      : nthreads_(std::max(1, nthreads)), ks_(key_shift), jm_((uint64_t(1) << key_shift) - 1) {
+    if (key_shift < 0 || key_shift > 4) throw std::invalid_argument("FragmentLoader: key_shift must be in [0, 4]");
     shards_.resize(paths.size());
     for (size_t i = 0; i < paths.size(); i++) {
       shards_[i] = std::make_unique<Shard>();
@@ -155,7 +160,7 @@ class FragmentLoader {
       uint64_t maxrow = 0;
       bool any = false;
       for (auto& sp : shards_)
-        if (sp->containers) any = true, maxrow = std::max(maxrow, sp->last_row);
+        if (sp->containers) any = true, maxrow = std::max(maxrow, sp->last_key >> ks_);
       if (any && maxrow < (uint64_t(1) << 31)) {
         // presence bits, set in parallel (fetch_or), then compacted in order
         const size_t W = size_t(maxrow / 64 + 1);
@@ -165,7 +170,7 @@ class FragmentLoader {
           const Shard& sh = *shards_[size_t(s)];
           uint64_t prev = ~0ull;
           for (uint32_t i = 0; i < sh.keyn; i++) {
-            const uint64_t r = rd64(sh.hdr + size_t(i) * 12) >> 4;
+            const uint64_t r = rd64(sh.hdr + size_t(i) * 12) >> ks_;
             if (r == prev) continue;
             prev = r;
             bits[r >> 6].fetch_or(1ull << (r & 63), std::memory_order_relaxed);
@@ -178,7 +183,7 @@ class FragmentLoader {
         for (auto& sp : shards_) {
           uint64_t prev = ~0ull;
           for (uint32_t i = 0; i < sp->keyn; i++) {
-            const uint64_t r = rd64(sp->hdr + size_t(i) * 12) >> 4;
+            const uint64_t r = rd64(sp->hdr + size_t(i) * 12) >> ks_;
             if (r != prev) out.push_back(r), prev = r;
           }
         }
@@ -227,7 +232,7 @@ class FragmentLoader {
           const uint64_t key = rd64(h);
           const int type = rd16(h + 8);
           const int64_t n = int64_t(rd16(h + 10)) + 1;
-          const uint64_t r = key >> 4;
+          const uint64_t r = key >> ks_;
           if (identity) {
             while (d <= int64_t(r) && d < D) rps[d++] = uint32_t(ci);
           } else {
@@ -235,7 +240,7 @@ class FragmentLoader {
             if (d < D && rows_[size_t(d)] == r) rps[d++] = uint32_t(ci);
           }
           const int64_t nr = type == pr::CT_RUN ? int64_t(rd16(sh.map + rd32(sh.offs + size_t(i) * 4))) : 0;
-          ms[ci++] = int64_t((key & 15) | (uint64_t(type) << 4) | (uint64_t(n) << 6) | (uint64_t(pi / 8) << 23));
+          ms[ci++] = int64_t((key & jm_) | (uint64_t(type) << 4) | (uint64_t(n) << 6) | (uint64_t(pi / 8) << 23));
           pi += arena_u16(type, n, nr);
         }
         while (d <= D) rps[d++] = uint32_t(ci);
@@ -296,6 +301,8 @@ class FragmentLoader {
   std::vector<uint64_t> rows_;
   bool scanned_ = false, have_rows_ = false;
   int nthreads_;
+  int ks_;
+  uint64_t jm_;
 
   void need_scan() const {
     if (!scanned_) throw std::runtime_error("FragmentLoader: scan() first");
@@ -385,7 +392,7 @@ class FragmentLoader {
     if (end != n) return false;  // op log follows: replay path
     sh.containers = keyn;
     sh.payload = P;
-    sh.last_row = keyn ? prev >> 4 : 0;
+    sh.last_key = keyn ? prev : 0;
     return true;
   }
 };
@@ -630,7 +637,8 @@ py::dict write_bsi_fragments(const std::string& dir, int64_t shard_lo, int64_t s
 
 void register_arena_io(py::module_& m) {
   py::class_<FragmentLoader>(m, "FragmentLoader")
-      .def(py::init<std::vector<std::string>, int>(), py::arg("paths"), py::arg("nthreads") = 16)
+      .def(py::init<std::vector<std::string>, int, int>(), py::arg("paths"), py::arg("nthreads") = 16,
+           py::arg("key_shift") = 4)
       .def("scan", &FragmentLoader::scan)
       .def("rows", &FragmentLoader::rows)
       .def("fill_index", &FragmentLoader::fill_index, py::arg("slack") = 0.0, py::arg("min_slack") = 0)

@@ -74,7 +74,11 @@ static void write_payload(const Container& c, uint16_t* dst) {
 }
 
 static py::tuple build_arena(std::vector<py::object> shards, uint64_t cpr, int nthreads) {
-  if (cpr != 16) throw std::invalid_argument("build_arena: only 16 containers per row (ShardWidth 2^20) supported");
+  // cpr = containers per row of the source bitmaps (ShardWidth / 2^16): 16
+  // for 2^20-column shards, 1..8 for narrower ones (their rows use the first
+  // cpr of the arena's 16 container slots)
+  if (cpr == 0 || cpr > 16 || (cpr & (cpr - 1)))
+    throw std::invalid_argument("build_arena: containers per row must be a power of two <= 16");
   size_t S = shards.size();
   std::vector<const Bitmap*> bms(S, nullptr);
   for (size_t s = 0; s < S; s++)

@@ -270,8 +270,10 @@ class DeviceView:
 
         if self._cap is None:
             return False
+        from pilosa_amd import shardwidth
         rows = set(int(r) for r in rows)
-        keys = sorted(int(k) for k in keys if (int(k) >> 4) not in rows)
+        keys = sorted(int(shardwidth.device_key(int(k))) for k in keys)   # arena keys row*16 + j
+        keys = [k for k in keys if (k >> 4) not in rows]
         if not rows and not keys:
             return True
         touched = sorted(rows | {k >> 4 for k in keys})
@@ -280,9 +282,12 @@ class DeviceView:
             if not self.add_rows([r for r, d in dense_of.items() if d < 0]):
                 return False
             dense_of = dict(zip(touched, self.dense_many(np.array(touched, np.uint64)).tolist()))
-        sw, cw = 1 << 20, 1 << 16
-        parts = [storage.offset_range(r * sw, r * sw, (r + 1) * sw) for r in sorted(rows)]
-        parts += [storage.offset_range(k * cw, k * cw, (k + 1) * cw) for k in keys]
+        # storage positions are row * ShardWidth + column; the arena's rows are
+        # 2^20 columns wide (identity for 2^20-column shards)
+        sw, dw, cw = shardwidth.SHARD_WIDTH, 1 << 20, 1 << 16
+        parts = [storage.offset_range(r * dw, r * sw, (r + 1) * sw) for r in sorted(rows)]
+        parts += [storage.offset_range(k * cw, shardwidth.host_key(k) * cw, (shardwidth.host_key(k) + 1) * cw)
+                  for k in keys]
         part = _roaring.Bitmap()
         part.union_in_place(parts)
         rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([part], 16, 1)
@@ -354,7 +359,8 @@ class DeviceView:
 
         if self._cap is None:
             return False
-        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], 16, 1)
+        from pilosa_amd import shardwidth
+        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], shardwidth.CONTAINERS_PER_ROW, 1)
         n_new = int(sb_s[-1])
         if n_new > int(self._cap[si]) and not self.grow_segment(si, n_new):
             return False
@@ -499,7 +505,7 @@ class DeviceView:
         return base, seg, keys
 
     def apply_positions(self, si: int, positions, clear: bool = False) -> bool:
-        """Set (or clear) shard-local positions row*2^20 + col of local shard
+        """Set (or clear) shard-local positions row * ShardWidth + col of local shard
         ``si`` directly in the arena: container_merge / container_emit on the
         GPU (kernels/write_kernels.hip), only the positions go over PCIe.
         False -> the caller must refresh the shard another way."""
@@ -551,7 +557,8 @@ class DeviceView:
             r += 1
 
     def _replay_group(self, group, kind: str, clear: bool) -> set:
-        from pilosa_amd import _roaring
+        from pilosa_amd import _roaring, shardwidth
+        ks, cpr = shardwidth.KEY_SHIFT, shardwidth.CONTAINERS_PER_ROW
 
         jobs = []   # (si, container row ids, j, mode-specific arrays)
         for si, data in group:
@@ -559,12 +566,12 @@ class DeviceView:
                 p = np.unique(np.asarray(data, dtype=np.uint64))
                 if not len(p):
                     continue
-                ck = (p >> np.uint64(16)).astype(np.int64)
+                ck = (p >> np.uint64(16)).astype(np.int64)    # host container keys
                 uk, start = np.unique(ck, return_index=True)
-                jobs.append([si, (uk >> 4).astype(np.uint64), (uk & 15).astype(np.int32),
+                jobs.append([si, (uk >> ks).astype(np.uint64), (uk & (cpr - 1)).astype(np.int32),
                              np.append(start, len(p)).astype(np.int64), (p & np.uint64(0xFFFF)).astype(np.uint16)])
             else:
-                rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([data], 16, 1)
+                rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([data], cpr, 1)
                 n = int(sb_s[-1])
                 if not n:
                     continue
@@ -795,10 +802,14 @@ class DeviceView:
         return self
 
     @classmethod
-    def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=(), patchable: bool = False):
-        from pilosa_amd import _roaring
+    def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=(), patchable: bool = False,
+                     cpr: Optional[int] = None):
+        """Arena of per-shard bitmaps of shard-local positions row * ShardWidth
+        + column (``cpr`` containers per row, default the shard width's)."""
+        from pilosa_amd import _roaring, shardwidth
 
-        rows, rowptr, sb, meta, payload = _roaring.build_arena(list(bitmaps), 16, 8)
+        cpr = shardwidth.CONTAINERS_PER_ROW if cpr is None else int(cpr)
+        rows, rowptr, sb, meta, payload = _roaring.build_arena(list(bitmaps), cpr, 8)
         if patchable:
             return cls.patchable(rows, rowptr, sb, meta, payload, device, shards)
         return cls(rows, rowptr, sb, meta, payload, device, shards)
@@ -1251,6 +1262,8 @@ class GpuEngine:
         o = offs.cpu().numpy()
         pay = outp.cpu().numpy().view(np.uint16)
         shards = views[0].shards
+        from pilosa_amd import shardwidth
+        cpr = shardwidth.CONTAINERS_PER_ROW
         result = []
         for s in range(S):
             cs = c[s * 16:(s + 1) * 16]
@@ -1258,7 +1271,7 @@ class GpuEngine:
             if len(nz) == 0:
                 result.append(None)
                 continue
-            keys = (np.uint64(shards[s]) * np.uint64(16) + nz.astype(np.uint64)).astype(np.uint64)
+            keys = (np.uint64(shards[s]) * np.uint64(cpr) + nz.astype(np.uint64)).astype(np.uint64)
             types = np.where(cs[nz] > 4096, 2, 1).astype(np.uint8)
             result.append(_roaring.bitmap_from_containers(keys, types, cs[nz].astype(np.int32),
                                                           o[s * 16 + nz].astype(np.int64), pay))
@@ -1345,7 +1358,8 @@ class GpuEngine:
         if column is None:
             self.ext.rows_list(vd, 0, view.S, -1, 0, flags)
         else:
-            shard, off = divmod(int(column), 1 << 20)
+            from pilosa_amd import shardwidth
+            shard, off = divmod(int(column), shardwidth.SHARD_WIDTH)
             if shard not in view.shards:
                 return np.zeros(0, np.uint64)
             si = view.shards.index(shard)

@@ -67,7 +67,8 @@ class GpuExecutor:
     def __init__(self, holder, device="cuda:0", executor=None, hbm_budget: int = 0):
         from pilosa_amd import shardwidth
         if not shardwidth.device_supported():
-            raise NotImplementedError(f"device arenas need 2^{shardwidth.DEVICE_EXPONENT}-column shards "
+            raise NotImplementedError(f"device arenas hold shards of 2^{shardwidth.MIN_EXPONENT}.."
+                                      f"2^{shardwidth.DEVICE_EXPONENT} columns "
                                       f"(PILOSA_SHARD_WIDTH={shardwidth.EXPONENT})")
         self.holder = holder
         self.engine = GpuEngine(device)
@@ -419,8 +420,10 @@ class GpuExecutor:
             child = self.plan(index, c.children[0], shards)
             if k == 0 or child is EMPTY:
                 return child
-            if k >= SHARD_WIDTH or _has_shift(child):
-                raise NotImplementedError  # multi-shard carries: host path
+            if k >= SHARD_WIDTH or _has_shift(child) or SHARD_WIDTH != 1 << 20:
+                # multi-shard carries, or shards narrower than the device
+                # shard (shift_dense carries at 2^20 columns): host path
+                raise NotImplementedError
             try:
                 self.launches += 2
                 main, spill = self.engine.shift_views(child, k)

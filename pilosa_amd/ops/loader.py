@@ -39,7 +39,8 @@ def load_view(paths: Sequence[str], shards: Sequence[int], device, patchable: bo
         nthreads = min(16, os.cpu_count() or 8)
     device = torch.device(device)
     t0 = time.perf_counter()
-    ld = _roaring.FragmentLoader([p or "" for p in paths], int(nthreads))
+    from pilosa_amd import shardwidth
+    ld = _roaring.FragmentLoader([p or "" for p in paths], int(nthreads), shardwidth.KEY_SHIFT)
     info = ld.scan()
     rows = ld.rows()
     t_scan = time.perf_counter()

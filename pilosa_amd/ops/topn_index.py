@@ -28,7 +28,7 @@ from pilosa_amd.models.cache import Pair
 
 from .device import DeviceView, GpuEngine, kernels
 
-SHARD_WIDTH = 1 << 20
+SHARD_WIDTH = 1 << 20   # device shard width: columns of one arena shard (16 container slots per row)
 LDS_LIMIT = 160 * 1024 - 1024
 # cache ranks counted row-major for the whole batch (topn_hot_kernel); the
 # slot index / histogram cover the ranks after them

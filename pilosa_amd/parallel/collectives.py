@@ -19,9 +19,11 @@ Every collective runs under the process group's timeout (``init(timeout=)``;
 RCCL aborts the communicator when it expires), and a failure marks the Comm
 broken so callers can fail over instead of hanging.
 
-Partial results are encoded with msgpack (a schema-less binary format; no
-code is executed on decode) with extension types for the executor's result
-objects.
+Partial call results travel as typed int64 tensors (``encode_partial``:
+ValCount, Pair, TopN pairs, row ids, GroupBy matrices, Row segments as
+roaring bytes); results with strings and errors fall back to msgpack (a
+schema-less binary format; no code is executed on decode) with extension
+types for the executor's result objects, packed into the same tensor.
 """
 from __future__ import annotations
 
@@ -163,6 +165,14 @@ class Comm:
         parts = self.all_gather_var(t.to(self.device))
         return [p.cpu().numpy().tobytes() for p in parts]
 
+    def gather_partials(self, obj) -> list:
+        """Every rank's partial call result, on every rank: the typed int64
+        encoding (encode_partial) of each rank travels in ONE variable-length
+        all-gather of device tensors (RCCL over xGMI on a GPU node)."""
+        torch = self.torch
+        t = torch.from_numpy(encode_partial(obj)).to(self.device)
+        return [decode_partial(p.cpu().numpy()) for p in self.all_gather_var(t)]
+
     def barrier(self):
         self.all_reduce(self.torch.zeros(1, dtype=self.torch.int64, device=self.device))
 
@@ -270,6 +280,129 @@ def decode(data: bytes):
     if not data:
         return None
     return msgpack.unpackb(data, ext_hook=_ext_hook, strict_map_key=False, raw=False)
+
+
+# ---------------------------------------------------------------- typed partials
+# A rank's partial result of one call as a flat int64 tensor, so the mesh
+# moves call results as tensors (one all_gather_var, i.e. RCCL on the GPU
+# box) and the front end decodes them with numpy views instead of walking a
+# msgpack object tree.  Layout: [tag, ...payload].  Shapes with strings (keys,
+# attributes), errors and anything else ride as TAG_MSGPACK (the bytes
+# packed into int64 words), so every rank always takes part in the same one
+# collective whatever it produced (the reference's QueryResponse per node,
+# internal/public.proto, reduced by executor.go mapReduce).
+(TAG_NONE, TAG_MSGPACK, TAG_VALCOUNT, TAG_PAIR, TAG_PAIRS, TAG_ROWIDS, TAG_GROUPS, TAG_ROW,
+ TAG_INT, TAG_BOOL) = range(10)
+
+
+def _bytes_to_words(b: bytes) -> np.ndarray:
+    pad = (-len(b)) % 8
+    return np.frombuffer(b + b"\0" * pad, dtype=np.int64)
+
+
+def _words_to_bytes(w: np.ndarray, n: int) -> bytes:
+    return np.ascontiguousarray(w, dtype=np.int64).tobytes()[:n]
+
+
+def encode_partial(obj) -> np.ndarray:
+    """One rank's partial result -> int64[...] (see the TAG_ layout)."""
+    from pilosa_amd.executor import GroupCount, RowIdentifiers, ValCount
+    from pilosa_amd.models.cache import Pair
+    from pilosa_amd.models.row import Row
+
+    def msg():
+        b = encode(obj)
+        return np.concatenate([np.array([TAG_MSGPACK, len(b)], np.int64), _bytes_to_words(b)])
+
+    if obj is None:
+        return np.array([TAG_NONE], np.int64)
+    if isinstance(obj, bool):
+        return np.array([TAG_BOOL, int(obj)], np.int64)
+    if isinstance(obj, (int, np.integer)) and -(1 << 63) <= int(obj) < (1 << 63):
+        return np.array([TAG_INT, int(obj)], np.int64)
+    if isinstance(obj, ValCount):
+        return np.array([TAG_VALCOUNT, obj.val, obj.count], np.int64)
+    if isinstance(obj, Pair) and not getattr(obj, "key", ""):
+        return np.array([TAG_PAIR, obj.id, obj.count], np.uint64).view(np.int64)
+    if isinstance(obj, list) and all(isinstance(p, Pair) and not getattr(p, "key", "") for p in obj):
+        flat = np.array([(p.id, p.count) for p in obj], np.uint64).reshape(-1).view(np.int64) if obj else \
+            np.zeros(0, np.int64)
+        return np.concatenate([np.array([TAG_PAIRS, len(obj)], np.int64), flat])
+    if isinstance(obj, list) and all(isinstance(x, (int, np.integer)) for x in obj):
+        a = np.asarray(obj, dtype=np.uint64).view(np.int64) if obj else np.zeros(0, np.int64)
+        return np.concatenate([np.array([TAG_ROWIDS, len(obj)], np.int64), a])
+    if isinstance(obj, list) and obj and all(isinstance(g, GroupCount) for g in obj):
+        fields = [fr.field for fr in obj[0].group]
+        k = len(fields)
+        if all(len(g.group) == k and all(fr.field == f and not fr.row_key for fr, f in zip(g.group, fields))
+               for g in obj):
+            names = encode(fields)
+            mat = np.array([[fr.row_id for fr in g.group] + [g.count] for g in obj], np.uint64).view(np.int64)
+            return np.concatenate([np.array([TAG_GROUPS, len(obj), k, len(names)], np.int64), _bytes_to_words(names),
+                                   mat.reshape(-1)])
+        return msg()
+    if isinstance(obj, Row) and not obj.keys and not obj.attrs:
+        segs = [(int(s), bm.to_bytes()) for s, bm in sorted(obj.segments.items())]
+        head = [TAG_ROW, len(segs)]
+        for s, b in segs:
+            head += [s, len(b)]
+        return np.concatenate([np.array(head, np.int64)] + [_bytes_to_words(b) for _, b in segs])
+    if isinstance(obj, RowIdentifiers) and not obj.keys:
+        a = np.asarray(obj.rows, dtype=np.uint64).view(np.int64) if obj.rows else np.zeros(0, np.int64)
+        return np.concatenate([np.array([TAG_ROWIDS, -1 - len(obj.rows)], np.int64), a])
+    return msg()
+
+
+def decode_partial(w: np.ndarray):
+    """Inverse of :func:`encode_partial`."""
+    from pilosa_amd import _roaring
+    from pilosa_amd.executor import FieldRow, GroupCount, RowIdentifiers, ValCount
+    from pilosa_amd.models.cache import Pair
+    from pilosa_amd.models.row import Row
+
+    w = np.asarray(w, dtype=np.int64)
+    if len(w) == 0:
+        return None
+    tag = int(w[0])
+    if tag == TAG_NONE:
+        return None
+    if tag == TAG_BOOL:
+        return bool(w[1])
+    if tag == TAG_INT:
+        return int(w[1])
+    if tag == TAG_MSGPACK:
+        return decode(_words_to_bytes(w[2:], int(w[1])))
+    if tag == TAG_VALCOUNT:
+        return ValCount(int(w[1]), int(w[2]))
+    if tag == TAG_PAIR:
+        return Pair(int(w[1:2].view(np.uint64)[0]), int(w[2]))
+    if tag == TAG_PAIRS:
+        n = int(w[1])
+        a = w[2:2 + 2 * n].view(np.uint64).reshape(n, 2)
+        return [Pair(int(i), int(c)) for i, c in a.tolist()]
+    if tag == TAG_ROWIDS:
+        n = int(w[1])
+        if n < 0:   # RowIdentifiers
+            m = -1 - n
+            return RowIdentifiers(w[2:2 + m].view(np.uint64).tolist())
+        return w[2:2 + n].view(np.uint64).tolist()
+    if tag == TAG_GROUPS:
+        n, k, nb = int(w[1]), int(w[2]), int(w[3])
+        nw = (nb + 7) // 8
+        fields = decode(_words_to_bytes(w[4:4 + nw], nb))
+        mat = w[4 + nw:4 + nw + n * (k + 1)].view(np.uint64).reshape(n, k + 1).tolist()
+        return [GroupCount([FieldRow(f, r) for f, r in zip(fields, row[:k])], row[k]) for row in mat]
+    if tag == TAG_ROW:
+        ns = int(w[1])
+        hdr = w[2:2 + 2 * ns].reshape(ns, 2)
+        o = 2 + 2 * ns
+        segs = {}
+        for s, nb in hdr.tolist():
+            nw = (nb + 7) // 8
+            segs[int(s)] = _roaring.Bitmap.from_bytes(_words_to_bytes(w[o:o + nw], nb))
+            o += nw
+        return Row(segments=segs)
+    raise ValueError(f"unknown partial tag {tag}")
 
 
 def pairs_to_arrays(totals: Sequence[dict]):

@@ -16,9 +16,13 @@ hop with a process group (backend ``nccl`` = RCCL over xGMI on the GPU box,
   with ``remote`` semantics (TopN phase-1 pairs, unmerged row segments), and
   the partial results are reduced with collectives: ``all_reduce(SUM)`` of
   int64 tensors for Count / batched Counts (an error flag rides in the same
-  tensor), a variable-length byte all-gather of msgpack-encoded partials
-  folded with the executor's own reduce function for everything else (TopN
-  pairs, Rows, GroupBy, MinRow/MaxRow, Min/Max, Row segments).
+  tensor), whole TopN batches on the device with a candidate union and an
+  all-reduced re-count (OP_TOPN), and for every other call one
+  variable-length all-gather of each rank's partial as a typed int64 tensor
+  (collectives.encode_partial: ValCount, Pair, TopN pairs, Rows ids, GroupBy
+  matrices, Row segments as roaring bytes) folded with the executor's own
+  reduce function; results carrying strings (keys, attributes) ride as
+  msgpack bytes inside the same tensor.
 * writes and imports are routed to the owning rank only.
 
 Transport is tensors only (parallel/collectives.py): a command is an int64
@@ -36,7 +40,6 @@ from __future__ import annotations
 import threading
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
-SHARD_WIDTH = 1 << 20
 
 
 class MeshError(RuntimeError):
@@ -109,10 +112,8 @@ class ShardMesh:
 
     # ------------------------------------------------------------ plumbing
     def _gather(self, obj) -> list:
-        """Every rank's partial result (msgpack over a byte all-gather)."""
-        from .collectives import decode, encode
-
-        return [decode(b) for b in self.comm.gather_bytes(encode(obj))]
+        """Every rank's partial result (typed int64 tensors, one all-gather)."""
+        return self.comm.gather_partials(obj)
 
     def _run(self, op: int, *args):
         """Front end: broadcast the command and take part in it like any rank.

@@ -244,9 +244,9 @@ class Server:
         from pilosa_amd import shardwidth
         if not shardwidth.device_supported():
             if mode == "on":
-                raise RuntimeError(f"gpu=on needs 2^{shardwidth.DEVICE_EXPONENT}-column shards "
-                                   f"(PILOSA_SHARD_WIDTH={shardwidth.EXPONENT})")
-            self.logger.printf("shard width 2^%d: the GPU kernels are built for 2^%d-column shards, "
+                raise RuntimeError(f"gpu=on needs shards of 2^{shardwidth.MIN_EXPONENT}..2^"
+                                   f"{shardwidth.DEVICE_EXPONENT} columns (PILOSA_SHARD_WIDTH={shardwidth.EXPONENT})")
+            self.logger.printf("shard width 2^%d: the device arenas hold shards of at most 2^%d columns, "
                                "queries run on the host", shardwidth.EXPONENT, shardwidth.DEVICE_EXPONENT)
             return
         try:

@@ -187,7 +187,8 @@ def test_device_rank_cache_topn_batch_matches_host(envs):
     # the device cache order equals the fragments' rank caches (all rows fit)
     for si, s in enumerate(shards):
         frag = cpu.holder.fragment("i", "h", "standard", s)
-        host = [(p[0], p[1]) for p in frag._top_bitmap_pairs([])]
+        # (at narrow shard widths the run of f=20 reaches a shard h never has)
+        host = [(p[0], p[1]) for p in frag._top_bitmap_pairs([])] if frag is not None else []
         dev = [(int(r), int(c)) for r, c in zip(cache.rows[si], cache.counts[si]) if c > 0]
         assert dev == host
     cases = [("Row(f=2)", 5), ("Row(f=3)", 300), ("Row(g=1)", 1000), ("Row(f=0)", 50)]
@@ -566,7 +567,7 @@ def test_groupby_two_million_row_fields_limit():
         env.field("i", "b")
         n = 1_000_000
         rows = np.arange(n, dtype=np.uint64)
-        cols = (rows * np.uint64(3)) % np.uint64(4 * SW)
+        cols = (rows * np.uint64(3)) % np.uint64(4 << 20)   # no two rows share a column (any shard width)
         idx = env.holder.index("i")
         idx.field("a").import_bits(rows, cols)
         idx.field("b").import_bits(rows, cols)
