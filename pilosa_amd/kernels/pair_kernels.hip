@@ -36,7 +36,10 @@
 // (18.8 ms, see lds_swz); every load of a container issued before any of it
 // is consumed (v9, 20.9 ms: one round trip per array instead of one per
 // 512 values, but slower -- the chunked walk is not latency-bound,
-// profiles/r03_v9/).
+// profiles/r03_v9/).  Occupancy: the kernel holds 20 waves/CU (8 KiB LDS and
+// 84 VGPRs per wave); padding LDS to 16 / 12 waves/CU measured 17.9 / 23.3 ms
+// against 16.7 (profiles/r03_occ/), so sharing one bitmap between two waves
+// to reach 32 waves/CU would buy well under the 12->16 step.
 //
 // Reference hot loops replaced: roaring/roaring.go:3078-3215 intersectionCount*
 // and executor.go:1230-1290 (executeCount over executeIntersect).
