@@ -309,6 +309,31 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     out["rank_cache_k"] = rc.K if rc is not None else 0
     out["rank_cache_cold_shards"] = rc.cold_shards if rc is not None else 0
     out["slot_index_bytes"] = tix.nbytes() if tix is not None else 0
+    if world == 1 and shards:
+        # a write burst into one shard (an existing row gains 8k bits and
+        # climbs that shard's rank cache): the next src request refreshes the
+        # slot index in place (only that shard re-indexed) instead of falling
+        # back to the pair-count path while a full rebuild is throttled
+        fw = holder.index("i").field("f")
+        wcols = np.uint64(shards[0]) * np.uint64(SHARD_WIDTH) + np.arange(0, SHARD_WIDTH, 128, dtype=np.uint64)
+        r0, d0 = gpu.topn_index_refreshes, ex.topn_batch_declined
+        t0 = time.perf_counter()
+        fw.import_bits(np.full(len(wcols), NROWS - 1, np.uint64), wcols)
+        t1 = time.perf_counter()
+        ex.execute("i", src_q[1], shards=shards)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        tt = [time.perf_counter()]
+        for q in src_q[2:6]:
+            ex.execute("i", q, shards=shards)
+        torch.cuda.synchronize(dev)
+        tt.append(time.perf_counter())
+        out["after_write"] = {"bits": int(len(wcols)), "row": NROWS - 1, "shard": shards[0],
+                              "import_s": round(t1 - t0, 3), "first_src_request_s": round(t2 - t1, 3),
+                              "next_src_ms_per_request": round((tt[1] - tt[0]) / 4 * 1000, 2),
+                              "index_refreshes": gpu.topn_index_refreshes - r0,
+                              "batches_declined": ex.topn_batch_declined - d0}
+        log(f"topn: after a write burst {out['after_write']}")
     gpu.comm = None
     # correctness: per-shard phase-1 answers (device map step over one shard) vs
     # the host fragment.top on sampled shards (this loads those fragments)
@@ -894,6 +919,32 @@ def _dir_bytes(path):
     return tot
 
 
+def _evict_page_cache(root: str) -> dict:
+    """fsync + POSIX_FADV_DONTNEED every file under ``root`` so the next read
+    of the index comes from the device, as after a restart (an unprivileged
+    process may drop clean pages of its own files).  Returns what it did."""
+    t0 = time.perf_counter()
+    files = nbytes = 0
+    for dp, _, fns in os.walk(root):
+        for fn in fns:
+            path = os.path.join(dp, fn)
+            try:
+                fd = os.open(path, os.O_RDONLY)
+            except OSError:
+                continue
+            try:
+                os.fsync(fd)
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                files += 1
+                nbytes += os.fstat(fd).st_size
+            except OSError:
+                pass
+            finally:
+                os.close(fd)
+    return {"evicted_files": files, "evicted_bytes": nbytes, "s": round(time.perf_counter() - t0, 2),
+            "how": "fsync + posix_fadvise(DONTNEED) per file before the load"}
+
+
 def run_disk(args, world, rank, dev, queries, ra, rb):
     """Product path: Pilosa-format fragment files on disk -> Holder (lazy) ->
     HBM via the native file loader -> Executor.execute(PQL text)."""
@@ -946,6 +997,10 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
                               "s": round(time.perf_counter() - t0, 2)}
         else:
             extra["write"] = {"reused": True, "bytes": _dir_bytes(fdir)}
+        if args.cold_load:
+            # resume from disk, not from the page cache the write just filled:
+            # every fragment file is synced and dropped from the cache first
+            extra["page_cache"] = _evict_page_cache(base)
         log("opening holder + loading the view into HBM")
         t1 = time.perf_counter()
         holder = Holder(base, lazy_fragments=True).open()
@@ -1202,6 +1257,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--clients", type=int, default=3, help="disk mode: concurrent request threads")
     ap.add_argument("--data-dir", default=None, help="disk mode: reuse/keep fragment files under this dir")
+    ap.add_argument("--cold-load", type=int, default=1,
+                    help="disk mode: drop the fragment files from the page cache before loading (1) or not (0)")
     ap.add_argument("--keep-data", action="store_true")
     ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")
     ap.add_argument("--topn-batches", type=int, default=10,

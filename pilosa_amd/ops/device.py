@@ -195,6 +195,12 @@ class DeviceView:
         self.container_count = int(shard_base[-1])
         self._row_index = None
         self.generation = 0          # bumped by in-place shard updates
+        # what changed since a given generation, for incremental dependents
+        # (the TopN slot index refreshes only the shards whose bits changed):
+        # shard_gen[si] counts content changes of shard si, rows_gen changes
+        # of the dense row directory
+        self.shard_gen = np.zeros(self.S, np.int64)
+        self.rows_gen = 0
         self._sb_host = np.asarray(shard_base, dtype=np.int64).copy()
         self._cap = None             # per-shard meta capacity (patchable arenas)
         self.payload_used = int(payload.shape[0])
@@ -257,6 +263,7 @@ class DeviceView:
         self.D = D2
         self._row_index = None
         self.generation += 1
+        self.rows_gen += 1
         return True
 
     def update_rows(self, si: int, rows, storage, keys=()) -> bool:
@@ -346,6 +353,7 @@ class DeviceView:
         self.payload_used += npay
         self.garbage_u16 += npay
         self.generation += 1
+        self.shard_gen[si] += 1
         return True
 
     def update_shard(self, si: int, bitmap) -> bool:
@@ -395,6 +403,7 @@ class DeviceView:
         self.payload_used += npay
         self.garbage_u16 += npay  # approximate: the shard's previous payload is now unreachable
         self.generation += 1
+        self.shard_gen[si] += 1
         return True
 
     # ------------------------------------------------------------ growth
@@ -735,6 +744,8 @@ class DeviceView:
         if scatter_at:
             self._flush_meta_scatter(scatter_at, scatter_val)
         self.generation += 1
+        for jb in jobs:
+            self.shard_gen[jb[0]] += 1
         return failed
 
     def _flush_meta_scatter(self, at, val):
@@ -764,6 +775,8 @@ class DeviceView:
         self.container_count = int(container_count)
         self._row_index = None
         self.generation = 0
+        self.shard_gen = np.zeros(self.S, np.int64)
+        self.rows_gen = 0
         self._cap = None
         self.payload_used = int(t_payload.numel())
         self.garbage_u16 = 0
@@ -791,6 +804,8 @@ class DeviceView:
         self.container_count = int(shard_base[-1])
         self._row_index = None
         self.generation = 0
+        self.shard_gen = np.zeros(self.S, np.int64)
+        self.rows_gen = 0
         self._sb_host = np.asarray(shard_base, dtype=np.int64).copy()
         self.payload_used = int(payload_used)
         self.garbage_u16 = 0

@@ -83,6 +83,7 @@ class GpuExecutor:
         self._bsi_views: Dict[Tuple, DeviceView] = {}  # predicate results (small LRU)
         self.mu = threading.RLock()
         self.launches = 0
+        self.topn_index_refreshes = 0   # slot indexes brought up to date in place after writes
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
@@ -871,7 +872,10 @@ class GpuExecutor:
         tix = self._topn_index(index, fname, shards, rc, rv)
         if tix is not None:
             self.launches += 1
-            return sort_pairs(tix.shard_pairs(self.engine, src, 0 if ids else n, threshold, ids or None))
+            try:
+                return sort_pairs(tix.shard_pairs(self.engine, src, 0 if ids else n, threshold, ids or None))
+            except CompileError:
+                raise NotImplementedError   # src too large for one device program: host path
         return self._topn_pairs_path(rc, rv, src, n, ids, threshold)
 
     def topn_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[List[Pair]]]:
@@ -930,7 +934,11 @@ class GpuExecutor:
                     self.topn_decline = f"no slot index ({self._topn_index_why})"
                     return None
                 self.launches += 1
-                got = tix.topn(self.engine, [srcs[i] for i in live], ns, ths, comm=self.comm)
+                try:
+                    got = tix.topn(self.engine, [srcs[i] for i in live], ns, ths, comm=self.comm)
+                except CompileError:
+                    self.topn_decline = "src too large for one device program"
+                    return None
             for i, r in zip(live, got):
                 out[i] = r
         return out
@@ -1099,6 +1107,13 @@ class GpuExecutor:
         ent = self._topn_indexes.get(key)
         if ent is not None and ent[0] is rc and ent[1].view is rv and not ent[1].stale:
             return ent[1]
+        if ent is not None and ent[1].view is rv and space is None:
+            # after writes: re-index only the changed shards, in place (no
+            # throttle, no fall back to the pair-count path)
+            if ent[1].refresh(rv, rc):
+                self._topn_indexes[key] = (rc, ent[1], ent[2])
+                self.topn_index_refreshes += 1
+                return ent[1]
         now = time.monotonic()
         if ent is not None and now - ent[2] < TOPN_INDEX_REBUILD_S:
             self._topn_index_why = (f"throttled: same_rc={ent[0] is rc} same_view={ent[1].view is rv} "

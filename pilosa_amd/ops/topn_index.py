@@ -154,10 +154,13 @@ class DeviceTopNIndex:
         if S:
             self.colptr[:, 1:] = torch.cumsum(colcnt.view(S, SHARD_WIDTH), dim=1, dtype=torch.int32)
         tot = self.colptr[:, SHARD_WIDTH].to(torch.int64)
+        # each shard's slot region has 1/8 spare room, so a shard whose
+        # cached rows change can be re-indexed in place (refresh)
+        self.cap = tot + tot // 8 + 64
         self.entbase = torch.zeros(max(S, 1), dtype=torch.int64, device=dev)
         if S > 1:
-            self.entbase[1:S] = torch.cumsum(tot, 0)[:-1]
-        self.entries = int(tot.sum().item()) if S else 0
+            self.entbase[1:S] = torch.cumsum(self.cap, 0)[:-1]
+        self.entries = int(self.cap.sum().item()) if S else 0
         # +16 entries: the histogram reads each slot run as aligned 16-byte words
         self.slots = torch.zeros((self.entries + 16 + 7) // 8 * 8, dtype=torch.int16, device=dev)
         if S and Kt:
@@ -169,6 +172,98 @@ class DeviceTopNIndex:
         self.slotmap[si, self.cache_acc[si, ki].long()] = ki.to(torch.int32)
         if A == 0:
             self.slotmap = self.slotmap[:, :0].contiguous()
+        # what this index reflects (refresh compares them with the view's)
+        self.shard_gen = view.shard_gen.copy()
+        self.rows_gen = view.rows_gen
+        self.refreshes = 0
+        self.refreshed_shards = 0
+
+    def refresh(self, view: DeviceView, cache, max_frac: float = 0.25) -> bool:
+        """Bring the index up to date in place after writes, re-indexing only
+        the shards whose bits changed (the view's shard generations) or whose
+        cached row order changed (``cache``: the rebuilt DeviceRankCaches):
+        hot-rank metadata, column counts, slot region (within its spare room)
+        and slot map of those shards, through the same kernels over a
+        gathered sub-view.  False = the caller rebuilds the whole index (row
+        directory changed, cache width changed, too many shards, a region
+        overflowed)."""
+        import torch
+
+        if (view is not self.view or view.rows_gen != self.rows_gen or not hasattr(cache, "cache_dense")
+                or tuple(cache.cache_dense.shape) != (self.S, self.K) or self.A != view.D
+                or not (self.A == 0 or np.array_equal(self.space, view.rows))):
+            return False
+        S, K, R = self.S, self.K, self.R
+        dev = view.device
+        new_dense = cache.cache_dense.contiguous()
+        changed = torch.from_numpy(view.shard_gen != self.shard_gen).to(dev)
+        changed |= (new_dense != self.cache_dense).any(dim=1)
+        C = torch.nonzero(changed).reshape(-1)
+        nc = int(C.numel())
+        if nc > max(1, int(S * max_frac)):
+            return False
+        ext = kernels()
+        if nc:
+            D1 = view.D + 1
+            sub = np.zeros((), dtype=view.viewdev().dtype)
+            sub[()] = view.viewdev()
+            rp_sub = view.t_rowptr.view(S, D1).index_select(0, C).contiguous()
+            sb_sub = torch.cat([view.t_shard_base.index_select(0, C), view.t_shard_base[-1:]]).contiguous()
+            sub["rowptr"] = rp_sub.data_ptr()
+            sub["shard_base"] = sb_sub.data_ptr()
+            sub["keymask"] = 0
+            vd_sub = torch.from_numpy(np.frombuffer(sub.tobytes(), dtype=np.uint8).copy())
+            cd_sub = new_dense.index_select(0, C).contiguous()
+            Kt = K - R
+            colcnt = torch.zeros(nc * SHARD_WIDTH, dtype=torch.int32, device=dev)
+            if Kt:
+                ext.topn_index(vd_sub, nc, K, R, cd_sub, colcnt, torch.empty(0, dtype=torch.int32, device=dev),
+                               torch.empty(0, dtype=torch.int64, device=dev),
+                               torch.empty(0, dtype=torch.int16, device=dev), False)
+            cp_sub = torch.zeros((nc, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
+            cp_sub[:, 1:] = torch.cumsum(colcnt.view(nc, SHARD_WIDTH), dim=1, dtype=torch.int32)
+            if bool((cp_sub[:, SHARD_WIDTH].to(torch.int64) > self.cap.index_select(0, C)).any().item()):
+                return False
+            eb_sub = self.entbase.index_select(0, C).contiguous()
+            if Kt:
+                colcnt.zero_()
+                ext.topn_index(vd_sub, nc, K, R, cd_sub, colcnt, cp_sub, eb_sub, self.slots, True)
+            del colcnt
+            self.colptr.index_copy_(0, C, cp_sub)
+            if R:
+                hm_sub = torch.full((nc * 16 * R,), -1, dtype=torch.int32, device=dev)
+                hs_sub = torch.zeros(nc * 16, dtype=torch.int32, device=dev)
+                ext.topn_hot_meta(vd_sub, nc, K, R, cd_sub, hm_sub, hs_sub)
+                self.hot_meta.view(S, 16 * R).index_copy_(0, C, hm_sub.view(nc, 16 * R))
+                self.hot_split.view(S, 16).index_copy_(0, C, hs_sub.view(nc, 16))
+        # the rank caches of every shard (counts of unchanged shards may move
+        # too), their acc indexes, the slot map rows and the counter tiers
+        self.cache_dense = new_dense
+        self.cache_cnt = cache.cache_cnt.contiguous()
+        valid_t = self.cache_dense >= 0
+        acc_t = self.cache_dense.clamp(min=0)
+        self.cache_acc = torch.where(valid_t, acc_t, torch.zeros_like(acc_t)).to(torch.int32).contiguous()
+        if nc and self.A:
+            self.slotmap.index_fill_(0, C, -1)
+            si, ki = torch.nonzero(valid_t.index_select(0, C), as_tuple=True)
+            self.slotmap[C[si], self.cache_acc[C[si], ki].long()] = ki.to(torch.int32)
+        Kt = K - R
+        if S and Kt:
+            tail = self.cache_cnt[:, R:]
+            n32 = int((tail >= 65536).sum(dim=1).max().item())
+            n16 = int((tail >= 256).sum(dim=1).max().item())
+        else:
+            n32 = n16 = 0
+        self.H32 = min(Kt, (n32 + 63) // 64 * 64)
+        self.H16 = max(self.H32, min(Kt, (n16 + 63) // 64 * 64))
+        self.lds = lds_bytes(Kt, self.H32, self.H16)
+        self.ok = self.lds <= LDS_LIMIT
+        self._vd = torch.from_numpy(np.frombuffer(view.viewdev().tobytes(), dtype=np.uint8).copy())
+        self.generation = view.generation
+        self.shard_gen = view.shard_gen.copy()
+        self.refreshes += 1
+        self.refreshed_shards += nc
+        return self.ok
 
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.cache_dense, self.cache_acc, self.cache_cnt,

@@ -149,3 +149,27 @@ def test_nosrc_dense_batch_equals_two_phase(lazy_env):
     ref = finish_batch_dev(rc.view.rows, len(ns), pq, pd, rc.recount(pq, pd, ths), ns)
     assert [_pairs(r) for r in got] == [_pairs(r) for r in ref]
     assert _pairs(got[0]) == _pairs(want["TopN(h, n=10)"])
+
+
+def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
+    """A write burst into one shard (new bits, and a tail row pushed up the
+    rank order) re-indexes only that shard's slot region in place: the next
+    src TopN is answered by the slot index (no throttled rebuild, no
+    pair-count fallback) and equals the host path."""
+    holder, ex, gpu, _, _ = lazy_env
+    q = "TopN(h, Row(f=1), n=8) TopN(h, Row(f=0), n=5)"
+    ex.execute("i", q)                      # index built over the current caches
+    r0 = gpu.topn_index_refreshes
+    d0 = ex.topn_batch_declined
+    cols = np.arange(2 * SW + 1000, 2 * SW + 61000, 7, dtype=np.uint64)
+    holder.index("i").field("h").import_bits(np.full(len(cols), 2998, np.uint64), cols)
+    ex.execute("i", "Set(%d, h=7) Clear(%d, h=7)" % (2 * SW + 3, 2 * SW + 3))
+    got = ex.execute("i", q).results
+    assert gpu.topn_index_refreshes > r0, gpu._topn_index_why if hasattr(gpu, "_topn_index_why") else ""
+    assert ex.topn_batch_declined == d0
+    ex.gpu = None
+    try:
+        want = ex.execute("i", q).results
+    finally:
+        ex.gpu = gpu
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
