@@ -968,7 +968,9 @@ class GpuExecutor:
                     src = self.plan(index, c.children[0], shards)
                     if src is EMPTY or self._topn_index(index, fname, shards, rc, rv) is None:
                         return False
-        except (NotImplementedError, PilosaError):
+                    if not (type(src) is Leaf and src.view is rv):
+                        self.engine.compile_batch([src])   # a src too large for one program declines here
+        except (NotImplementedError, PilosaError, CompileError):
             return False
         return True
 
