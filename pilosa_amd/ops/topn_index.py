@@ -20,6 +20,8 @@ of the walk) sums one int64 per candidate with an all-reduce.
 from __future__ import annotations
 
 import os
+import threading
+from contextlib import contextmanager
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -45,6 +47,53 @@ HOT_Q = int(os.environ.get("PILOSA_TOPN_HOT_Q", "16"))
 MAX_SLOTS = 65535
 # phase-1 histograms are kept for the ids= gather up to this many bytes per batch
 HIST_KEEP_BYTES = 8 << 30
+
+
+class _RWLock:
+    """Readers (TopN batches using an index) share it; a writer (an in-place
+    refresh after writes) waits for them and holds new ones back.  A
+    thread's nested read (topn over several hot-rank launches) re-enters."""
+
+    def __init__(self):
+        self._c = threading.Condition()
+        self._readers = 0
+        self._writer = False
+        self._waiting = 0
+        self._local = threading.local()
+
+    @contextmanager
+    def read(self):
+        depth = getattr(self._local, "d", 0)
+        if depth == 0:
+            with self._c:
+                while self._writer or self._waiting:
+                    self._c.wait()
+                self._readers += 1
+        self._local.d = depth + 1
+        try:
+            yield
+        finally:
+            self._local.d = depth
+            if depth == 0:
+                with self._c:
+                    self._readers -= 1
+                    if not self._readers:
+                        self._c.notify_all()
+
+    @contextmanager
+    def write(self):
+        with self._c:
+            self._waiting += 1
+            while self._writer or self._readers:
+                self._c.wait()
+            self._waiting -= 1
+            self._writer = True
+        try:
+            yield
+        finally:
+            with self._c:
+                self._writer = False
+                self._c.notify_all()
 
 
 def lds_bytes(K: int, H32: int, H16: int) -> int:
@@ -177,8 +226,14 @@ class DeviceTopNIndex:
         self.rows_gen = view.rows_gen
         self.refreshes = 0
         self.refreshed_shards = 0
+        self.rw = _RWLock()
 
     def refresh(self, view: DeviceView, cache, max_frac: float = 0.25) -> bool:
+        """See :meth:`_refresh`; waits for the batches using this index."""
+        with self.rw.write():
+            return self._refresh(view, cache, max_frac)
+
+    def _refresh(self, view: DeviceView, cache, max_frac: float = 0.25) -> bool:
         """Bring the index up to date in place after writes, re-indexing only
         the shards whose bits changed (the view's shard generations) or whose
         cached row order changed (``cache``: the rebuilt DeviceRankCaches):
@@ -383,6 +438,11 @@ class DeviceTopNIndex:
 
     def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
              comm=None) -> List[List[Pair]]:
+        with self.rw.read():
+            return self._topn(engine, srcs, ns, thresholds, comm)
+
+    def _topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
+             comm=None) -> List[List[Pair]]:
         """TopN(field, src_q, n=ns[q], threshold=thresholds[q]) for a batch.
         ``comm`` (parallel/collectives.Comm) spans the ranks of a node: the
         candidate union and the phase-2 sums go through it; every rank must
@@ -406,6 +466,11 @@ class DeviceTopNIndex:
         return finish_batch_dev(self.space, Q, pair_q, pair_idx, out, ns)
 
     def shard_pairs(self, engine: GpuEngine, src, n: int, threshold: int,
+                    ids: Optional[Sequence[int]] = None) -> List[Pair]:
+        with self.rw.read():
+            return self._shard_pairs(engine, src, n, threshold, ids)
+
+    def _shard_pairs(self, engine: GpuEngine, src, n: int, threshold: int,
                     ids: Optional[Sequence[int]] = None) -> List[Pair]:
         """One TopN call over the local shards as the executor's map step
         sees it (executor.go:905-930): without ``ids`` the per-shard heap
@@ -436,6 +501,10 @@ class DeviceTopNIndex:
         return [Pair(int(i), int(v)) for i, v in zip(ids_out.tolist(), c[keep].tolist())]
 
     def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None) -> List[List[Pair]]:
+        with self.rw.read():
+            return self._topn_nosrc(row_counts, ns, thresholds, comm)
+
+    def _topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None) -> List[List[Pair]]:
         """TopN(field, n) without a src row for a batch, all on the device.
         Phase 1: per shard the first n cache entries at or above the
         threshold (fragment.top stops once its heap holds n rows), summed by

@@ -173,3 +173,48 @@ def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
     finally:
         ex.gpu = gpu
     assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
+
+
+def test_src_topn_concurrent_with_write_bursts(lazy_env):
+    """Request threads keep running src TopN while another thread writes
+    bursts into one shard: the in-place index refreshes wait for the batches
+    in flight (reader/writer lock), nothing fails, and afterwards the answers
+    equal the host path."""
+    holder, ex, gpu, _, _ = lazy_env
+    q = "TopN(h, Row(f=1), n=8) TopN(h, Row(f=2), n=4)"
+    errs = []
+    stop = threading.Event()
+
+    def reader():
+        try:
+            while not stop.is_set():
+                ex.execute("i", q)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    def writer():
+        try:
+            rng = np.random.default_rng(11)
+            for k in range(6):
+                cols = (np.uint64(SW) + rng.choice(SW, 3000, replace=False).astype(np.uint64))
+                holder.index("i").field("h").import_bits(np.full(len(cols), 2990 + k, np.uint64), cols)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+    rs = [threading.Thread(target=reader) for _ in range(3)]
+    w = threading.Thread(target=writer)
+    for t in rs:
+        t.start()
+    w.start()
+    w.join(timeout=120)
+    stop.set()
+    for t in rs:
+        t.join(timeout=120)
+    assert not errs, errs[:2]
+    assert not w.is_alive() and not any(t.is_alive() for t in rs)
+    got = ex.execute("i", q).results
+    ex.gpu = None
+    try:
+        want = ex.execute("i", q).results
+    finally:
+        ex.gpu = gpu
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
