@@ -759,6 +759,9 @@ class Server:
                 self.stats.gauge("maxrss_kb", ru.ru_maxrss)
                 self.stats.gauge("open_files", len(os.listdir("/proc/self/fd")))
                 self.stats.gauge("threads", threading.active_count())
+                gcn = getattr(self, "gc_notifier", None)
+                if gcn is not None:
+                    gcn.flush()
                 if self.gpu is not None:
                     st = self.gpu.stats()
                     self.stats.gauge("gpu.arena_bytes", st["arenaBytes"])

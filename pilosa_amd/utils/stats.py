@@ -43,7 +43,9 @@ class NopStatsClient:
 
 class _Registry:
     def __init__(self):
-        self.mu = threading.Lock()
+        # reentrant: a finalizer or gc callback that records a stat while its
+        # thread is inside one of these updates must not deadlock the process
+        self.mu = threading.RLock()
         self.counters: Dict[Tuple[str, Tuple[str, ...]], float] = defaultdict(float)
         self.gauges: Dict[Tuple[str, Tuple[str, ...]], float] = {}
         self.hist: Dict[Tuple[str, Tuple[str, ...]], List[float]] = defaultdict(list)

@@ -125,6 +125,13 @@ def test_gc_notifier_counts_collections():
     try:
         gc.collect()
         assert n.collections >= 1
+        assert n.flush() >= 1
+        assert st.expvar()["garbage_collection"] >= 1
+        # a collection triggered while the registry lock is held must not
+        # deadlock (the callback takes no lock)
+        with st.reg.mu:
+            gc.collect()
+        assert n.flush() >= 1
     finally:
         n.stop()
 
