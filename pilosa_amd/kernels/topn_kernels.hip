@@ -506,15 +506,6 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
 // hot_meta[s][j][k] is the row's key-j container (meta index relative to the
 // shard, -1 = none), built once with the index.
 constexpr int HOT_THREADS = 1024;
-// 1 = big hot-rank containers stream as one 16-byte load per lane per
-// 512-value chunk (8 values, packed until counted); 0 = 8 two-byte loads
-#ifndef HOT_VEC_LOADS
-#define HOT_VEC_LOADS 1
-#endif
-// 1 = with HOT_VEC_LOADS, loads run two chunks ahead of the counting
-#ifndef HOT_PF2
-#define HOT_PF2 1
-#endif
 constexpr int HOT_TAB_WORDS = 32768;
 constexpr int HOT_SMALL_N = 255;  // byte counters: at most 255 values per lane-owned container
 
@@ -609,39 +600,34 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(ml) >> 32)), r));
       return int64_t((uint64_t(hi) << 32) | lo);
     };
-#if HOT_VEC_LOADS
     // lane l takes values base + 8l .. +7 with ONE 16-byte load (the payload
-    // is 16-byte aligned and padded to 8 values); the raw words stay packed
-    // in 4 VGPRs until the chunk is counted, so the load stays in flight
+    // is 16-byte aligned and padded to 8 values)
+    // Branch-free: every lane always loads a valid chunk (its own, or the
+    // container's last / the payload's first when it has none) and zeroes
+    // it after, so the load is never behind a branch and the compiler can
+    // count the loads in flight instead of draining them all (vmcnt(0)).
+    // m == 0 (no container to prefetch) reads the payload's first chunk.
     auto load_chunk = [&](int64_t m, int base, uint4& x, int& nv) {
       const uint4* pp4 = reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8);
       const int i0 = base + 8 * lane;
-      nv = min(max(meta_n(m) - i0, 0), 8);
-      x = make_uint4(0, 0, 0, 0);
-      if (nv > 0) x = pp4[i0 >> 3];
-    };
-#else
-    auto load_chunk = [&](int64_t m, int base, int (&x)[8]) {
-      const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
       const int n = meta_n(m);
-#pragma unroll
-      for (int t = 0; t < 8; t++) {
-        const int i = base + 64 * t + lane;
-        x[t] = i < n ? int(pp[i]) : -1;
-      }
+      nv = min(max(n - i0, 0), 8);
+      x = pp4[min(i0, max(n - 1, 0)) >> 3];
+      if (nv <= 0) x = make_uint4(0, 0, 0, 0);
     };
-#endif
     int r = __builtin_ctzll(live);
     live &= live - 1;
     int64_t m = row_meta(r);
     int base = 0;
-#if HOT_VEC_LOADS
-    uint4 cur = make_uint4(0, 0, 0, 0);
-    int curv = 0;
-    if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur, curv);
-#if HOT_PF2
-    // a load cursor runs two chunks ahead of the count cursor over the same
-    // (row, chunk) sequence: two 16-byte loads per lane stay in flight
+    // Three chunk buffers rotate through the unrolled loop below: a load
+    // cursor runs two (row, chunk) steps ahead of the count cursor and each
+    // step loads into the buffer the step before last consumed.  No buffer is
+    // ever copied into another, so the wait before a chunk is counted is for
+    // THAT chunk's load only (a rotating copy of in-flight registers made the
+    // compiler wait for the newest prefetch before every chunk).
+    uint4 b0 = make_uint4(0, 0, 0, 0), b1 = make_uint4(0, 0, 0, 0), b2 = make_uint4(0, 0, 0, 0);
+    int v0 = 0, v1 = 0, v2 = 0;
+    load_chunk(meta_type(m) == CT_ARRAY ? m : 0, 0, b0, v0);
     int lr = r, lbase = 0;
     int64_t lm = m;
     uint64_t llive = live;
@@ -657,17 +643,8 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       lm = lr >= 0 ? row_meta(lr) : 0;
     };
     adv();
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    int nxtv = 0;
-    if (lr >= 0 && meta_type(lm) == CT_ARRAY) load_chunk(lm, lbase, nxt, nxtv);
+    load_chunk(lr >= 0 && meta_type(lm) == CT_ARRAY ? lm : 0, lbase, b1, v1);
     adv();
-#endif
-#else
-    int cur[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) cur[t] = -1;
-    if (meta_type(m) == CT_ARRAY) load_chunk(m, 0, cur);
-#endif
     uint32_t c4[NQ / 4];
 #pragma unroll
     for (int g = 0; g < NQ / 4; g++) c4[g] = 0u;
@@ -680,7 +657,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
 #pragma unroll
       for (int g = 0; g < NQ / 4; g++) c4[g] = 0;
     };
-    for (;;) {
+    // one (row, chunk) step: count `cur`, load two steps ahead into `ldb`;
+    // false once the wave's last row is done
+    auto step = [&](const uint4& cur, const int curv, uint4& ldb, int& ldv) -> bool {
       const int ty = meta_type(m);
       const int n = meta_n(m);
       const bool more = ty == CT_ARRAY && base + 512 < n;
@@ -692,45 +671,44 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         bn = 0;
         mn = rn >= 0 ? row_meta(rn) : 0;
       }
-#if HOT_VEC_LOADS && HOT_PF2
-      uint4 nx2 = make_uint4(0, 0, 0, 0);
-      int nx2v = 0;
-      if (lr >= 0 && meta_type(lm) == CT_ARRAY) load_chunk(lm, lbase, nx2, nx2v);
+      load_chunk(lr >= 0 && meta_type(lm) == CT_ARRAY ? lm : 0, lbase, ldb, ldv);
       adv();
-#elif HOT_VEC_LOADS
-      uint4 nxt = make_uint4(0, 0, 0, 0);
-      int nxtv = 0;
-      if (rn >= 0 && meta_type(mn) == CT_ARRAY) load_chunk(mn, bn, nxt, nxtv);
-#else
-      int nxt[8];
-#pragma unroll
-      for (int t = 0; t < 8; t++) nxt[t] = -1;
-      if (rn >= 0 && meta_type(mn) == CT_ARRAY) load_chunk(mn, bn, nxt);
-#endif
       const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
       if (ty == CT_ARRAY) {
-        // an array gives a lane at most 64 values: bytes cannot overflow
-#if HOT_VEC_LOADS
+        // an array gives a lane at most 64 values: bytes cannot overflow.
+        // All 8 table reads issue before any is consumed (one LDS wait per
+        // chunk); values past the array read entry 0 and count nothing.
         const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+        uint32_t mk[8];
 #pragma unroll
-        for (int t = 0; t < 8; t++)
-          if (t < curv) swar_add<NQ>(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
-#else
+        for (int t = 0; t < 8; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
 #pragma unroll
-        for (int t = 0; t < 8; t++)
-          if (cur[t] >= 0) swar_add<NQ>(c4, mask_of(cur[t]));
-#endif
+        for (int t = 0; t < 8; t++) swar_add<NQ>(c4, t < curv ? mk[t] : 0u);
       } else if (ty == CT_BITMAP) {
-        // all 16 words of the lane issued before the first is counted
+        // all 16 words of the lane issued before the first is counted; set
+        // bits are taken four at a time (four table reads in flight)
         constexpr int NIT = NLO / 4096;  // 64-word rounds of the workgroup's values
+        constexpr int HALF = NIT / 2;     // words loaded per batch (register budget)
         const uint64_t* w = reinterpret_cast<const uint64_t*>(pp) + (lo >> 6);
-        uint64_t wv[NIT];
-#pragma unroll
-        for (int it = 0; it < NIT; it++) wv[it] = w[lane + 64 * it];
+        uint64_t wv[HALF];
 #pragma unroll
         for (int it = 0; it < NIT; it++) {
+          if (it % HALF == 0) {
+#pragma unroll
+            for (int h = 0; h < HALF; h++) wv[h] = w[lane + 64 * (it + h)];
+          }
           const int i = (lo >> 6) + lane + 64 * it;
-          for (uint64_t bb = wv[it]; bb; bb &= bb - 1) swar_add<NQ>(c4, mask_of(i * 64 + __builtin_ctzll(bb)));
+          for (uint64_t bb = wv[it % HALF]; bb;) {
+            uint32_t mk[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const bool v = bb != 0;
+              mk[k] = v ? mask_of(i * 64 + __builtin_ctzll(bb)) : 0u;
+              bb &= bb - 1;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) swar_add<NQ>(c4, mk[k]);
+          }
           if (it % 3 == 2) flush();  // <= 192 bits per lane between flushes
         }
       } else {
@@ -738,8 +716,8 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         const uint16_t* rr = pp + 8;
         int since = 0;
         for (int t = 0; t < nr; t++) {
-          const int a0 = max(int(rr[2 * t]), lo), b0 = min(int(rr[2 * t + 1]), lo + NLO - 1);
-          for (int xx = a0 + lane; xx <= b0; xx += 64) {
+          const int a0 = max(int(rr[2 * t]), lo), b0_ = min(int(rr[2 * t + 1]), lo + NLO - 1);
+          for (int xx = a0 + lane; xx <= b0_; xx += 64) {
             swar_add<NQ>(c4, mask_of(xx));
             if (++since == 240) {
               flush();
@@ -804,25 +782,21 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         if ((lane & (64 / NQ - 1)) == 0 && q < Q && d) atomicAdd(out + int64_t(q) * R + k, d);
 #pragma unroll
         for (int qq = 0; qq < NQ; qq++) acc[qq] = 0;
-        if (rn < 0) break;
+        if (rn < 0) return false;
         live &= live - 1;
       }
       r = rn;
       base = bn;
       m = mn;
-#if HOT_VEC_LOADS
-      cur = nxt;
-      curv = nxtv;
-#if HOT_PF2
-      nxt = nx2;
-      nxtv = nx2v;
-#endif
-#else
-#pragma unroll
-      for (int t = 0; t < 8; t++) cur[t] = nxt[t];
-#endif
+      return true;
+    };
+    for (;;) {
+      if (!step(b0, v0, b2, v2)) break;
+      if (!step(b1, v1, b0, v0)) break;
+      if (!step(b2, v2, b1, v1)) break;
     }
   }
+
 
   // 3. small array containers (<= HOT_SMALL_N values), ranks [B, R): waves
   //    grab groups of 64 consecutive ranks, each lane counts its own row
@@ -843,14 +817,17 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
 #pragma unroll
     for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
     for (int i = 0; __ballot(i < nl); i += 16) {
-      // two 16-byte loads in flight per lane (16 values)
+      // two 16-byte loads in flight per lane (16 values); all 16 table reads
+      // issue before any is consumed (values past the row count nothing)
       uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
       if (i < nl) w0 = pp[i >> 3];
       if (i + 8 < nl) w1 = pp[(i >> 3) + 1];
       const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      uint32_t mk[16];
 #pragma unroll
-      for (int t = 0; t < 16; t++)
-        if (i + t < nl) swar_add<NQ>(c4, mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu)));
+      for (int t = 0; t < 16; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
+#pragma unroll
+      for (int t = 0; t < 16; t++) swar_add<NQ>(c4, i + t < nl ? mk[t] : 0u);
     }
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
