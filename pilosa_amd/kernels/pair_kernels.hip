@@ -39,7 +39,11 @@
 // profiles/r03_v9/).  Occupancy: the kernel holds 20 waves/CU (8 KiB LDS and
 // 84 VGPRs per wave); padding LDS to 16 / 12 waves/CU measured 17.9 / 23.3 ms
 // against 16.7 (profiles/r03_occ/), so sharing one bitmap between two waves
-// to reach 32 waves/CU would buy well under the 12->16 step.
+// to reach 32 waves/CU would buy well under the 12->16 step.  One-ahead
+// prefetch in the multi-chunk array walks (two rotating register buffers,
+// branch-free clamped loads, the stage's first load before the LDS clear)
+// measured 23.5 vs 16.7 ms (profiles/r03_pf/): like v9, issuing the array
+// loads earlier made the kernel slower, not faster.
 //
 // Reference hot loops replaced: roaring/roaring.go:3078-3215 intersectionCount*
 // and executor.go:1230-1290 (executeCount over executeIntersect).
