@@ -313,7 +313,7 @@ class DeviceRankCaches:
         # composite key: count desc, then dense (= row id) asc
         key = (score << 32) | (0xFFFFFFFF - u.clamp(min=0).to(torch.int64))[None, :]
         key = torch.where(score > 0, key, torch.full((), -1, dtype=torch.int64, device=dev))
-        kk = min(U, nmax if all(nn) else U)
+        kk = min(U, max(nn)) if all(nn) else U   # a query keeps up to n rows (n may exceed the cache width)
         top = torch.topk(key, kk, dim=1, sorted=True).values
         h = top.cpu().numpy()
         rows = self.view.rows

@@ -142,8 +142,8 @@ def test_nosrc_dense_batch_equals_two_phase(lazy_env):
     holder, ex, gpu, want, _ = lazy_env
     ex.execute("i", "TopN(h, n=10)")
     rc = next(iter(gpu._rank_cache_map.values()))[1]
-    ns = [10, 100, 0, 20, 1, 7, 100, 3]
-    ths = [1, 1, 1, 300, 1, 2, 50, 1]
+    ns = [10, 100, 0, 20, 1, 7, 100, 3, rc.K + 500]   # the last asks for more rows than a cache holds
+    ths = [1, 1, 1, 300, 1, 2, 50, 1, 1]
     got = rc._topn_nosrc_dense(ns, ths)
     pq, pd, _ = rc.nosrc_phase1(ns, ths)
     ref = finish_batch_dev(rc.view.rows, len(ns), pq, pd, rc.recount(pq, pd, ths), ns)
