@@ -187,6 +187,12 @@ class Fragment:
     def max_row_id(self, v: int):
         self._max_row_id = v
 
+    def cache_is_live(self) -> bool:
+        """True once the rank cache has been opened in memory (a write opens
+        it, mapped fragments included): from then on it, not the persisted
+        ``.cache`` file, is the fragment's ranking."""
+        return self.cache_type != CACHE_TYPE_NONE and not self._cache_pending
+
     def is_cold(self) -> bool:
         """True while the storage has not been read into heap.  The file is
         exactly the fragment's state: writes to a cold fragment go to the

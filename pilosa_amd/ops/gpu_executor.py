@@ -1065,7 +1065,7 @@ class GpuExecutor:
         for f in frags:
             if f is None:
                 sig.append(None)
-            elif f.is_cold():
+            elif f.is_cold() and not f.cache_is_live():
                 sig.append(("cold", id(f)))
             else:
                 f.cache.invalidate()

@@ -78,7 +78,10 @@ class DeviceRankCaches:
         S = view.S
         dev = view.device
         self.S = S
-        cold = [f is not None and f.is_cold() for f in frags]
+        # the persisted .cache ids serve a fragment whose cache was never
+        # opened; once a write opened it (mapped fragments too) the live host
+        # cache is the ranking, as fragment.top would use
+        cold = [f is not None and f.is_cold() and not f.cache_is_live() for f in frags]
         paths = [frags[si].cache_path() if cold[si] else "" for si in range(S)]
         offs, ids, ok = _roaring.read_cache_files(paths, nthreads)
         # a corrupt .cache file: the host fragment rebuilds its cache (openCache)

@@ -134,6 +134,28 @@ def test_topn_after_writes_uses_warm_caches(lazy_env):
     assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
 
 
+def test_single_bit_writes_to_cold_fragment_reach_device_ranks(lazy_env):
+    """Set on a mapped (cold) fragment goes to the mapped overlay and opens
+    the fragment's in-memory rank cache while the fragment stays cold: from
+    then on the live cache, not the stale ``.cache`` file, ranks that shard,
+    so a new row written there shows up in the device TopN."""
+    holder, ex, gpu, _, _ = lazy_env
+    frag = holder.fragment("i", "h", "standard", 1)
+    ex.execute("i", "TopN(h)")     # device ranks built while the shard is file-backed
+    ex.execute("i", " ".join(f"Set({SW + 10 + k}, h=5000)" for k in range(60)))
+    assert frag.is_cold() and frag.cache_is_live()
+    frag.cache.recalculate()       # past the rank cache's 10 s recalculation throttle
+    qs = "TopN(h) TopN(h, n=2500) TopN(h, Row(f=0), n=3000)"
+    got = ex.execute("i", qs).results
+    ex.gpu = None
+    try:
+        want = ex.execute("i", qs).results
+    finally:
+        ex.gpu = gpu
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
+    assert 5000 in [p.id for p in got[0]]
+
+
 def test_nosrc_dense_batch_equals_two_phase(lazy_env):
     """The sync-free cache-only batch (one [Q, candidates] accumulator, one
     re-count per threshold, one top-k) answers exactly as phase 1 + ids=
@@ -158,6 +180,7 @@ def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
     pair-count fallback) and equals the host path."""
     holder, ex, gpu, _, _ = lazy_env
     q = "TopN(h, Row(f=1), n=8) TopN(h, Row(f=0), n=5)"
+    gpu._topn_indexes.clear()               # earlier tests may have left a throttled entry
     ex.execute("i", q)                      # index built over the current caches
     r0 = gpu.topn_index_refreshes
     d0 = ex.topn_batch_declined
