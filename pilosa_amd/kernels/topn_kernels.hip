@@ -674,7 +674,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       load_chunk(lr >= 0 && meta_type(lm) == CT_ARRAY ? lm : 0, lbase, ldb, ldv);
       adv();
       const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
-      if (ty == CT_ARRAY) {
+      if (ty == CT_ARRAY && !(p.dbg & 64)) {
         // an array gives a lane at most 64 values: bytes cannot overflow.
         // All 8 table reads issue before any is consumed (one LDS wait per
         // chunk); values past the array read entry 0 and count nothing.
@@ -684,7 +684,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         for (int t = 0; t < 8; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
 #pragma unroll
         for (int t = 0; t < 8; t++) swar_add<NQ>(c4, t < curv ? mk[t] : 0u);
-      } else if (ty == CT_BITMAP) {
+      } else if (ty == CT_BITMAP && !(p.dbg & 32)) {
         // all 16 words of the lane issued before the first is counted; set
         // bits are taken four at a time (four table reads in flight)
         constexpr int NIT = NLO / 4096;  // 64-word rounds of the workgroup's values
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
           }
           if (it % 3 == 2) flush();  // <= 192 bits per lane between flushes
         }
-      } else {
+      } else if (ty == CT_RUN) {
         const int nr = pp[0];
         const uint16_t* rr = pp + 8;
         int since = 0;
@@ -801,38 +801,65 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   // 3. small array containers (<= HOT_SMALL_N values), ranks [B, R): waves
   //    grab groups of 64 consecutive ranks, each lane counts its own row
   //    (8 values per 16-byte load), no reduction; atomics are coalesced
-  //    (consecutive ranks per query)
-  for (;;) {
-    int g = 0;
-    if (lane == 0) g = atomicAdd(&grab[1], 1);
-    g = __builtin_amdgcn_readfirstlane(g);
-    const int k0 = B + 64 * g;
-    if (k0 >= R || (p.dbg & 8)) break;
-    const int kl = k0 + lane;
-    const int cl = kl < R ? hm[kl] : -1;
-    const int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
-    const int nl = cl >= 0 ? meta_n(ml) : 0;
-    const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
-    uint32_t c4[NQ / 4];
-#pragma unroll
-    for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
-    for (int i = 0; __ballot(i < nl); i += 16) {
-      // two 16-byte loads in flight per lane (16 values); all 16 table reads
-      // issue before any is consumed (values past the row count nothing)
+  //    (consecutive ranks per query).  A row here has a handful of values, so
+  //    the rank -> meta -> payload chain of loads is the cost: groups are
+  //    claimed two ahead and the next group's meta word and the one after's
+  //    meta index are loaded with the current group's payload (one round trip
+  //    per group instead of three).
+  if (!(p.dbg & 8)) {
+    auto claim = [&]() -> int {
+      int g = 0;
+      if (lane == 0) g = atomicAdd(&grab[1], 1);
+      return __builtin_amdgcn_readfirstlane(g);
+    };
+    auto rank_meta = [&](int g) -> int {
+      const int kl = B + 64 * g + lane;
+      return kl < R ? hm[kl] : -1;
+    };
+    int g = claim();
+    int cl = rank_meta(g);
+    int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
+    int gn = claim();
+    int cln = rank_meta(gn);
+    while (B + 64 * g < R) {
+      const int kl = B + 64 * g + lane;
+      const int nl = cl >= 0 ? meta_n(ml) : 0;
+      const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
       uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
-      if (i < nl) w0 = pp[i >> 3];
-      if (i + 8 < nl) w1 = pp[(i >> 3) + 1];
-      const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      uint32_t mk[16];
+      if (0 < nl) w0 = pp[0];
+      if (8 < nl) w1 = pp[1];
+      const int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
+      const int gnn = claim();
+      const int clnn = rank_meta(gnn);
+      uint32_t c4[NQ / 4];
 #pragma unroll
-      for (int t = 0; t < 16; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
+      for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
+      for (int i = 0; __ballot(i < nl); i += 16) {
+        // two 16-byte loads per lane (16 values); all 16 table reads issue
+        // before any is consumed (values past the row count nothing)
+        if (i > 0) {
+          w0 = make_uint4(0, 0, 0, 0);
+          w1 = make_uint4(0, 0, 0, 0);
+          if (i < nl) w0 = pp[i >> 3];
+          if (i + 8 < nl) w1 = pp[(i >> 3) + 1];
+        }
+        const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        uint32_t mk[16];
 #pragma unroll
-      for (int t = 0; t < 16; t++) swar_add<NQ>(c4, i + t < nl ? mk[t] : 0u);
-    }
+        for (int t = 0; t < 16; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
 #pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      const uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
-      if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
+        for (int t = 0; t < 16; t++) swar_add<NQ>(c4, i + t < nl ? mk[t] : 0u);
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; q++) {
+        const uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+        if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
+      }
+      g = gn;
+      cl = cln;
+      ml = mln;
+      gn = gnn;
+      cln = clnn;
     }
   }
 }

@@ -33,8 +33,11 @@ from .device import DeviceView, GpuEngine, kernels
 SHARD_WIDTH = 1 << 20   # device shard width: columns of one arena shard (16 container slots per row)
 LDS_LIMIT = 160 * 1024 - 1024
 # cache ranks counted row-major for the whole batch (topn_hot_kernel); the
-# slot index / histogram cover the ranks after them
-HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "2048"))
+# slot index / histogram cover the ranks after them.  Bench src mix, 16-query
+# batch on the 954-shard headline index (profiles/r03_hotpart): 2048 -> hot
+# 9.05 + tail histogram 3.17 ms; 4096 -> 10.03 + 1.40 ms (13.0 vs 13.9 ms per
+# batch end to end); 8192 -> hot 12.7 ms, worse
+HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "4096"))
 # queries per hot-rank launch: up to 16 take topn_hot_kernel<16> (u16 query
 # masks of a whole key in LDS), 17..32 topn_hot_kernel<32> (u32 masks of half
 # a key per workgroup: twice the queries for the same streamed bytes).  Both
@@ -550,6 +553,31 @@ def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) 
     the kept Q x n pairs cross to the host."""
     import torch
 
+    if pq.numel() == 0:
+        return [[] for _ in range(Q)]
+    bq, ba = max(1, int(Q - 1).bit_length()), max(1, int(len(space) - 1).bit_length())
+    if bq + 31 + ba <= 63:
+        # one sort of a composite key (query, ~count, acc index): acc indexes
+        # are in id order, so this is (query, count desc, id asc) with no
+        # masking sync; zero counts sort last in their query and are dropped
+        # with the trim
+        c = cnt.to(torch.int64).clamp_(0, (1 << 31) - 1)
+        key = (pq.to(torch.int64) << (31 + ba)) | (((1 << 31) - 1 - c) << ba) | pa.to(torch.int64)
+        key = torch.sort(key)[0]
+        q_s = key >> (31 + ba)
+        c_s = ((1 << 31) - 1) - ((key >> ba) & ((1 << 31) - 1))
+        bounds = torch.searchsorted(q_s, torch.arange(Q + 1, device=key.device, dtype=torch.int64))
+        lim = torch.tensor([int(n) if int(n) else (1 << 62) for n in ns], dtype=torch.int64).to(key.device)
+        rank = torch.arange(key.numel(), device=key.device) - bounds[q_s]
+        sel = (rank < lim[q_s]) & (c_s > 0)
+        kept = key[sel].cpu().numpy()
+        q_h = kept >> (31 + ba)
+        c_h = ((1 << 31) - 1) - ((kept >> ba) & ((1 << 31) - 1))
+        ids = space[kept & ((1 << ba) - 1)]
+        out: List[List[Pair]] = [[] for _ in range(Q)]
+        for qq, i, cc in zip(q_h.tolist(), ids.tolist(), c_h.tolist()):
+            out[qq].append(Pair(int(i), int(cc)))
+        return out
     keep = cnt > 0
     pq, pa, cnt = pq[keep], pa[keep], cnt[keep]
     if pq.numel() == 0:
