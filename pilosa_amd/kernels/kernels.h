@@ -107,7 +107,8 @@ struct TopNLaunch {
   uint32_t* hot_cnt;              // [S][Q][R] src counts of the hot ranks (mode 4 writes, 1-3 read)
   int32_t* tail_built;            // [Q*S] mode 1: 1 = unit's tail histogram built (kept), 0 = skipped
   const int32_t* cache_dense;     // [S][K] dense row of each cache slot (mode 3 exact probes)
-  int dbg;                        // profiling builds: bit 0 skip histogram, bit 1 skip walk
+  int dbg;                        // PILOSA_TOPN_DBG cost isolation: 1 skip histogram, 2 skip walk, 8 skip small hot rows,
+                                  // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays (answers then wrong)
 };
 // LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).
 int topn_lds_bytes(int K, int H32, int H16);
