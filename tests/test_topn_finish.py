@@ -36,3 +36,35 @@ def test_finish_dev_empty():
     assert finish_batch_dev(space, 3, e, e, e, [1, 2, 3]) == [[], [], []]
     z = torch.zeros(4, dtype=torch.int64)
     assert finish_batch_dev(space, 2, z, z, z, [1, 1]) == [[], []]
+
+
+def test_finish_dev_composite_key_and_fallback_agree(monkeypatch):
+    """The one-sort composite-key finish (query | ~count | acc index packed in
+    an int64) and the three-stable-sort path it falls back to when the key
+    would not fit give the host answer, for random batches with large counts
+    and n past the candidate count."""
+    rng = np.random.default_rng(11)
+    for t in range(60):
+        Q = int(rng.integers(1, 40))
+        space = np.sort(rng.choice(1 << 50, int(rng.integers(1, 5000)), replace=False)).astype(np.uint64)
+        A = len(space)
+        key = np.unique(rng.integers(0, Q, 3000) * A + rng.integers(0, A, 3000))
+        pq, pa = key // A, key % A
+        cnt = rng.integers(0, 1 << 31, len(pq)) if t % 2 else rng.integers(0, 5, len(pq))
+        ns = [int(x) for x in rng.integers(0, 120, Q)]
+        want = _as_lists(finish_batch(space, Q, pq, pa, cnt, ns))
+        got = finish_batch_dev(space, Q, torch.from_numpy(pq).to(torch.int32), torch.from_numpy(pa).to(torch.int32),
+                               torch.from_numpy(cnt).to(torch.int64), ns)
+        assert _as_lists(got) == want
+    # a space too large for the packed key takes the sort-chain path
+    big = np.arange(1 << 33, (1 << 33) + 64, dtype=np.uint64)
+    pq = torch.tensor([0, 0, 1], dtype=torch.int64)
+    pa = torch.tensor([3, 5, 3], dtype=torch.int64)
+    cnt = torch.tensor([7, 9, 1], dtype=torch.int64)
+
+    class Huge(np.ndarray):
+        def __len__(self):
+            return 1 << 40
+    huge = big.view(Huge)
+    assert _as_lists(finish_batch_dev(huge, 2, pq, pa, cnt, [0, 0])) == \
+        _as_lists(finish_batch(big, 2, pq.numpy(), pa.numpy(), cnt.numpy(), [0, 0]))
