@@ -795,6 +795,31 @@ def verify_sample(eng, view, host_bitmap, pairs, answered, world, dev, nshards_c
             "mismatch_totals": bad_total, "verified": bad_shard == 0 and bad_total == 0}
 
 
+def _launch_ranks(args) -> int:
+    """``bench.py --gpus N`` without a launcher: check that N devices are
+    visible (counting them does not initialise the GPU), then run this
+    script under torch.distributed.run with one rank per GPU as a child
+    process and return its exit code.  PILOSA_BENCH_REHEARSE=1 allows N
+    ranks on fewer GPUs (gloo rehearsal, never for reported numbers)."""
+    import subprocess
+
+    rehearse = os.environ.get("PILOSA_BENCH_REHEARSE") == "1"
+    if not rehearse:
+        import torch
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            print(f"bench: --gpus {args.gpus} but {visible} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[2:9])} ...")
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
 def setup_dist():
     import torch
     import torch.distributed as dist
@@ -808,6 +833,8 @@ def setup_dist():
     if rehearse:
         local_rank = 0
     dev = torch.device("cuda", local_rank)
+    if world > 1 and not rehearse and local_rank >= torch.cuda.device_count():
+        raise SystemExit(f"bench: rank {rank} has LOCAL_RANK {local_rank} but {torch.cuda.device_count()} GPU(s)")
     if world > 1:
         from pilosa_amd.parallel.collectives import Comm, init
         torch.cuda.set_device(local_rank)
@@ -945,6 +972,41 @@ def _evict_page_cache(root: str) -> dict:
             "how": "fsync + posix_fadvise(DONTNEED) per file before the load"}
 
 
+def _write_index(args, base, lo, hi):
+    """The headline index's fragment files for shards [lo, hi) under
+    ``base`` (reused when the marker matches).  Returns (fragment dir,
+    what was done)."""
+    from pilosa_amd import _roaring
+    from pilosa_amd.models.field import FieldOptions
+    from pilosa_amd.models.holder import Holder
+
+    tag = f"{args.cols}:{args.rows}:{lo}:{hi}:zipf1.6/50:8:seed1:cache{args.topn_cache}"
+    marker = os.path.join(base, ".bench_data")
+    fdir = os.path.join(base, "i", "f", "views", "standard", "fragments")
+    t0 = time.perf_counter()
+    if os.path.exists(marker) and open(marker).read() == tag:
+        return fdir, {"reused": True, "bytes": _dir_bytes(fdir)}
+    log("writing fragment files")
+    shutil.rmtree(base, ignore_errors=True)
+    os.makedirs(base, exist_ok=True)
+    need = int(36e9 * (hi - lo) / 954 * (args.rows / NROWS))
+    free = shutil.disk_usage(base).free
+    if free < need:
+        raise SystemExit(f"bench --mode disk: {free / 1e9:.1f} GB free in {base}, need ~{need / 1e9:.1f} GB "
+                         "(set --data-dir or use --mode synthetic)")
+    h = Holder(base).open()
+    h.create_index("i", keys=False, track_existence=True)
+    h.index("i").create_field("f", FieldOptions())
+    h.close()
+    os.makedirs(fdir, exist_ok=True)
+    w = _roaring.write_zipf_fragments(fdir, lo, hi, args.cols, args.rows, 8.0, 1.6, 50.0, 1, args.threads,
+                                      cache_size=args.topn_cache)
+    with open(marker, "w") as fh:
+        fh.write(tag)
+    return fdir, {"files": int(w["shards"]), "bytes": int(w["bytes"]), "containers": int(w["containers"]),
+                  "s": round(time.perf_counter() - t0, 2)}
+
+
 def run_disk(args, world, rank, dev, queries, ra, rb):
     """Product path: Pilosa-format fragment files on disk -> Holder (lazy) ->
     HBM via the native file loader -> Executor.execute(PQL text)."""
@@ -971,32 +1033,7 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
         else os.path.join(args.data_dir, f"rank{rank}of{world}")
     extra = {"path": "Holder(lazy) + file loader -> HBM, Executor.execute(PQL text) per request", "data_dir": base}
     try:
-        tag = f"{args.cols}:{args.rows}:{lo}:{hi}:zipf1.6/50:8:seed1:cache{args.topn_cache}"
-        marker = os.path.join(base, ".bench_data")
-        fdir = os.path.join(base, "i", "f", "views", "standard", "fragments")
-        t0 = time.perf_counter()
-        if not (os.path.exists(marker) and open(marker).read() == tag):
-            log("writing fragment files")
-            shutil.rmtree(base, ignore_errors=True)
-            os.makedirs(base, exist_ok=True)
-            need = int(36e9 * (hi - lo) / 954 * (args.rows / NROWS))
-            free = shutil.disk_usage(base).free
-            if free < need:
-                raise SystemExit(f"bench --mode disk: {free / 1e9:.1f} GB free in {base}, need ~{need / 1e9:.1f} GB "
-                                 "(set --data-dir or use --mode synthetic)")
-            h = Holder(base).open()
-            h.create_index("i", keys=False, track_existence=True)
-            h.index("i").create_field("f", FieldOptions())
-            h.close()
-            os.makedirs(fdir, exist_ok=True)
-            w = _roaring.write_zipf_fragments(fdir, lo, hi, args.cols, args.rows, 8.0, 1.6, 50.0, 1, args.threads,
-                                              cache_size=args.topn_cache)
-            with open(marker, "w") as fh:
-                fh.write(tag)
-            extra["write"] = {"files": int(w["shards"]), "bytes": int(w["bytes"]), "containers": int(w["containers"]),
-                              "s": round(time.perf_counter() - t0, 2)}
-        else:
-            extra["write"] = {"reused": True, "bytes": _dir_bytes(fdir)}
+        fdir, extra["write"] = _write_index(args, base, lo, hi)
         if args.cold_load:
             # resume from disk, not from the page cache the write just filled:
             # every fragment file is synced and dropped from the cache first
@@ -1119,6 +1156,227 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
     finally:
         if own and not args.keep_data:
             shutil.rmtree(base, ignore_errors=True)
+
+
+def _mesh_root(args, world) -> str:
+    """Parent dir of every rank's data dir in a multi-GPU run (deterministic
+    per job, so rank 0 can read the other ranks' fragment files to verify)."""
+    if args.data_dir is not None:
+        return args.data_dir
+    return os.path.join(os.environ.get("TMPDIR") or "/tmp", f"pilosa_bench_{os.environ.get('MASTER_PORT', '0')}")
+
+
+def run_disk_mesh(args, world, rank, dev, queries, ra, rb):
+    """N>1 product path, as ``pilosa_amd server`` runs under torchrun: one
+    process per GPU, each with its own holder over the fragment files of a
+    contiguous shard range (ShardMesh ownership ``(s // block) % world``
+    with ``block = ceil(shards / world)``), loaded into its HBM by the file
+    loader.  Rank 0 is the front end: every request is
+    ``Executor.execute(PQL text)``, which sends it through the mesh
+    (parallel/mesh.py) -- Count requests as ``count_text`` (broadcast, each
+    rank compiles and counts its share natively, device all-reduce, several
+    requests in flight), TopN requests as ``OP_TOPN`` batches (candidate
+    union + all-reduced re-count on the devices, pipelined).  Ranks > 0 run
+    ``ShardMesh.serve``.  The timed region is bracketed by ``mesh.sync()``
+    (every rank drains its in-flight requests, synchronises its device and
+    meets the others); the time is the max over ranks.
+    Reference: executor.go:2458-2555 (mapReduce over nodes)."""
+    import resource
+    import threading
+
+    import torch
+
+    from pilosa_amd import _roaring
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    nshards = math.ceil(args.cols / SHARD_WIDTH)
+    block = -(-nshards // world)
+    own = [s for s in range(nshards) if (s // block) % world == rank]
+    lo, hi = (own[0], own[-1] + 1) if own else (0, 0)
+    all_shards = list(range(nshards))
+    root = _mesh_root(args, world)
+    rank_dir = lambda r: os.path.join(root, f"rank{r}of{world}")   # noqa: E731
+    base = rank_dir(rank)
+    extra = {"path": "ShardMesh product path: rank 0 Executor.execute(PQL text) -> mesh count_text / OP_TOPN; "
+                     "every rank: Holder(lazy) + file loader -> HBM",
+             "data_dir": base, "block": block}
+    holder = ex = None
+    try:
+        fdir, extra["write"] = _write_index(args, base, lo, hi)
+        if args.cold_load:
+            extra["page_cache"] = _evict_page_cache(base)
+        t1 = time.perf_counter()
+        holder = Holder(base, lazy_fragments=True).open()
+        gpu = GpuExecutor(holder, dev)
+        ex = Executor(holder, gpu=gpu)
+        gpu.executor = ex
+        ex.strict_gpu = True
+        view = gpu.view_arena("i", "f", "standard", own) if own else None
+        torch.cuda.synchronize(dev)
+        load_s = time.perf_counter() - t1
+        mesh = ShardMesh(ex, block=block, device=dev)
+        if rank != 0:
+            log(f"mesh worker: {len(own)} shards loaded in {load_s:.2f} s, serving")
+            mesh.serve()
+            return 0.0, {}
+        ex.mesh = mesh
+        per_rank = {r: len(v.get("i", [])) for r, v in mesh.shard_counts().items()}
+        extra.update({"load_s_rank0": round(load_s, 2), "load": gpu.last_load,
+                      "hbm_bytes_rank0": view.nbytes() if view is not None else 0,
+                      "shards": nshards, "shards_per_rank": per_rank})
+        assert sum(per_rank.values()) == nshards, per_rank
+
+        texts = [" ".join(queries[i * args.batch:(i + 1) * args.batch]) for i in range(args.warmup + args.steps)]
+        results = [None] * len(texts)
+        lock = threading.Lock()
+        nxt = [0]
+        err = []
+
+        def client(end):
+            while True:
+                with lock:
+                    i = nxt[0]
+                    if i >= end or err:
+                        return
+                    nxt[0] += 1
+                try:
+                    results[i] = ex.execute("i", texts[i], shards=all_shards).results
+                except BaseException as e:  # noqa: BLE001
+                    err.append(e)
+                    return
+
+        def run(first, n):
+            nxt[0] = first
+            ts = [threading.Thread(target=client, args=(first + n,)) for _ in range(max(1, args.clients))]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            if err:
+                raise err[0]
+
+        seq0 = mesh.seq
+        log("mesh count: warmup")
+        run(0, args.warmup)
+        t_a = mesh.sync()
+        run(args.warmup, args.steps)
+        t_b = mesh.sync()
+        elapsed = max(b - a for a, b in zip(t_a, t_b)) / 1e9
+        last = results[args.warmup + args.steps - 1]
+        extra.update({"clients": args.clients, "mean_count": float(np.mean(last)),
+                      "mesh_count_requests": mesh.seq - seq0, "mesh_max_in_flight": mesh.max_in_flight,
+                      "per_rank_elapsed_s": [round((b - a) / 1e9, 4) for a, b in zip(t_a, t_b)],
+                      "gpu_faults": ex.gpu_faults,
+                      "peak_host_rss_gb_rank0": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)})
+        log(f"mesh count: {args.steps} steps in {elapsed:.3f} s")
+        if args.verify > 0:
+            # per-shard answers through the mesh (the owner rank counts, the
+            # others add zero) vs the host roaring core over that shard's file
+            # in its owner's data dir
+            b0 = (args.warmup + args.steps - 1) * args.batch
+            n = min(args.verify, args.batch)
+            pairs = [(int(a), int(b)) for a, b in zip(ra[b0:b0 + n], rb[b0:b0 + n])]
+            sel = sorted(set(np.linspace(0, nshards - 1, min(8, nshards)).astype(int).tolist()))
+            text = " ".join(queries[b0:b0 + n])
+            bad = 0
+            for s in sel:
+                got = ex.execute("i", text, shards=[s]).results
+                path = os.path.join(rank_dir((s // block) % world), "i", "f", "views", "standard", "fragments", str(s))
+                with open(path, "rb") as fh:
+                    bm = _roaring.Bitmap.from_bytes(fh.read())
+                want = host_pair_counts([bm], pairs)[:, 0]
+                bad += int((np.asarray(got, np.int64) != want).sum())
+            extra["verify"] = {"queries": n, "shards_checked": len(sel), "mismatch_shard_counts": bad,
+                               "answered_by": "owner rank through the mesh", "verified": bad == 0,
+                               "verified_all_ranks": bad == 0}
+        if args.topn_batches > 0:
+            extra["topn"] = bench_topn_mesh(args, ex, mesh, all_shards)
+        mesh.stop()
+        return elapsed, extra
+    finally:
+        if ex is not None:
+            ex.close()
+        if holder is not None:
+            holder.close()
+        if args.data_dir is None and not args.keep_data:
+            shutil.rmtree(base, ignore_errors=True)
+
+
+def bench_topn_mesh(args, ex, mesh, all_shards):
+    """BASELINE config 3 on N GPUs: TopN requests through rank 0's
+    ``Executor.execute`` -> ``ShardMesh.topn_batch`` (OP_TOPN: each rank's
+    device runs both phases over its shards, candidates union over the
+    ranks, re-counts all-reduced; up to MAX_IN_FLIGHT batches in flight)
+    from ``--clients`` request threads.  The fused answers are checked
+    against the two-phase map/reduce through the mesh (OP_CALL per phase)."""
+    import threading
+
+    from pilosa_amd.executor import ExecOptions
+    from pilosa_amd.pql import parse_string
+
+    n = 100
+    B, nb = args.topn_batch, args.topn_batches
+    rng = np.random.default_rng(99)
+    out = {"path": "rank 0 Executor.execute(TopN text) -> ShardMesh OP_TOPN", "n": n, "batch": B,
+           "clients": args.clients}
+
+    def timed(texts, rec):
+        done = [None] * len(texts)
+        t0 = time.perf_counter()
+        done[0] = ex.execute("i", texts[0], shards=all_shards).results
+        rec["first_request_s"] = round(time.perf_counter() - t0, 2)
+        nxt = [1]
+        lock = threading.Lock()
+        err = []
+
+        def client():
+            while True:
+                with lock:
+                    i = nxt[0]
+                    if i >= len(texts) or err:
+                        return
+                    nxt[0] += 1
+                try:
+                    done[i] = ex.execute("i", texts[i], shards=all_shards).results
+                except BaseException as e:  # noqa: BLE001
+                    err.append(e)
+                    return
+        mesh.max_in_flight = 0
+        b0 = mesh.topn_tensor_batches
+        t_a = mesh.sync()
+        ts = [threading.Thread(target=client) for _ in range(max(1, args.clients))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        t_b = mesh.sync()
+        if err:
+            raise err[0]
+        el = max(b - a for a, b in zip(t_a, t_b)) / 1e9
+        rec.update({"qps": round(B * (len(texts) - 1) / el, 2), "ms_per_request": round(el / (len(texts) - 1) * 1000, 2),
+                    "device_batches": mesh.topn_tensor_batches - b0, "max_in_flight": mesh.max_in_flight,
+                    "sample_top3": [(p.id, p.count) for p in done[-1][0][:3]] if done[-1] and done[-1][0] else []})
+        return done
+
+    log("mesh topn: cache-only requests")
+    out["cache"] = {}
+    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nb + 1), out["cache"])
+    hot = zipf_rows(rng, B * (nb + 1), 1000)
+    src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
+    src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
+    out["src"] = {}
+    log("mesh topn: src requests")
+    res = timed(src_q, out["src"])
+    if args.verify > 0:
+        calls = [parse_string(c).calls[0] for c in src_calls[nb * B:nb * B + 2]] + [parse_string(f"TopN(f, n={n})").calls[0]]
+        fused = [[(p.id, p.count) for p in r] for r in res[-1][:2]] + \
+            [[(p.id, p.count) for p in ex.execute("i", f"TopN(f, n={n})", shards=all_shards).results[0]]]
+        two_phase = [[(p.id, p.count) for p in ex._topn("i", c, all_shards, ExecOptions())] for c in calls]
+        out["verify"] = {"fused_equals_two_phase_mesh": fused == two_phase, "verified": fused == two_phase}
+    return out
 
 
 def bench_serving(args, base, dev):
@@ -1280,6 +1538,17 @@ def main():
                     help="also time the host C++ roaring executor on this many shards (extrapolated)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # launched without a launcher: start one rank per GPU ourselves
+        # (nothing here has touched the GPU: no exec from a GPU process)
+        raise SystemExit(_launch_ranks(args))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={env_world} but --gpus {args.gpus}: launch one rank per GPU "
+                         "(torch.distributed.run --nproc-per-node N ... --gpus N)")
+
     import torch
     import torch.distributed as dist
 
@@ -1305,8 +1574,11 @@ def main():
             fallback = (f"--mode disk needs ~{need / 1e9:.1f} GB per rank under TMPDIR, a rank had "
                         f"{free / 1e9:.1f} GB free: timed the synthesised arena instead")
             args.mode = "synthetic"
-    run = run_disk if args.mode == "disk" else run_synthetic
+    mesh_mode = args.mode == "disk" and world > 1
+    run = run_disk_mesh if mesh_mode else run_disk if args.mode == "disk" else run_synthetic
     elapsed, extra = run(args, world, rank, dev, queries, ra, rb)
+    if world > 1:
+        extra.update({"backend": dist.get_backend(), "world_size": dist.get_world_size()})
     if fallback:
         extra["mode_fallback"] = fallback
     torch.cuda.empty_cache()
@@ -1324,7 +1596,7 @@ def main():
     elapsed = float(el.item())
     ms = elapsed / args.steps * 1000.0
     qps = args.batch * args.steps / elapsed
-    if "verify" in extra:
+    if "verify" in extra and not mesh_mode:   # mesh mode: rank 0 verified through the mesh
         ok = torch.tensor([0 if extra["verify"]["verified"] else 1], dtype=torch.int64, device=dev)
         if world > 1:
             all_reduce(ok)
@@ -1341,7 +1613,9 @@ def main():
                        + ("; written as Pilosa fragment files and loaded from disk" if args.mode == "disk" else ""),
                "config": {"model": f"set field f, {size} ({nshards} shards)", "global_batch": args.batch,
                           "seq_len": args.cols,
-                          "parallelism": f"shard-range x{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+                          "parallelism": f"shard-range x{world}" + (
+                              f" (ShardMesh over {extra.get('backend')})" if mesh_mode else
+                              " + RCCL all-reduce" if world > 1 else "")},
                "verified": extra.get("verify", {}).get("verified_all_ranks"),
                "mode": args.mode, "extra": extra}
         print(json.dumps(rec), flush=True)

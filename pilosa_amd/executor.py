@@ -36,6 +36,7 @@ from pilosa_amd.parallel.mesh import MeshError
 from pilosa_amd.utils import tracing
 
 DEFAULT_FIELD = "general"
+_FANOUT_LOCK = threading.Lock()
 DEFAULT_MIN_THRESHOLD = 1
 MAX_INT = (1 << 63) - 1
 
@@ -245,6 +246,9 @@ class Executor:
 
     def close(self):
         self.pool.shutdown(wait=False)
+        pool = self.__dict__.get("_fanout")
+        if pool is not None:
+            pool.shutdown(wait=False)
 
     # ================================================================ entry
     def execute(self, index: str, q, shards: Optional[Sequence[int]] = None,
@@ -595,7 +599,16 @@ class Executor:
         internal client with failover to replicas (executor.go:2458-2518)."""
         by_node = self._shards_by_node(index, shards, opt)
         result = None
-        remote_jobs = []
+        # every remote node is queried at once (one request in flight per
+        # node, like the reference's goroutine per node, executor.go:2530-2552)
+        # while the local shards run here; the wall time is the slowest node's,
+        # not the sum.  Partials are folded in node order (deterministic).
+        remote = []
+        if not opt.remote:
+            for node, nshards in by_node.items():
+                if node is not None and (self.cluster is None or node.id != self.cluster.node.id):
+                    remote.append(self.fanout.submit(self._remote_with_failover, index, c, node, nshards, opt,
+                                                     map_fn, reduce_fn, local_fn, {node.id}))
         for node, nshards in by_node.items():
             if node is None or (self.cluster is not None and node.id == self.cluster.node.id):
                 if self._use_mesh(opt):
@@ -608,12 +621,23 @@ class Executor:
                             raise
                         # failed over: this process now holds every local shard
                 result = reduce_fn(result, self._map_local(nshards, map_fn, reduce_fn, local_fn))
-            elif not opt.remote:
-                remote_jobs.append((node, nshards))
-        for node, nshards in remote_jobs:
-            result = reduce_fn(result, self._remote_with_failover(index, c, node, nshards, opt, map_fn, reduce_fn,
-                                                                  local_fn, {node.id}))
+        for fut in remote:
+            result = reduce_fn(result, fut.result())
         return result
+
+    @property
+    def fanout(self) -> cf.ThreadPoolExecutor:
+        """Threads that carry the remote node requests of map/reduce (and
+        their replica retries); separate from the shard pool so a fan-out
+        never waits behind local shard jobs."""
+        pool = self.__dict__.get("_fanout")
+        if pool is None:
+            with _FANOUT_LOCK:
+                pool = self.__dict__.get("_fanout")
+                if pool is None:
+                    pool = cf.ThreadPoolExecutor(max_workers=32, thread_name_prefix="fanout")
+                    self._fanout = pool
+        return pool
 
     def _use_mesh(self, opt) -> bool:
         return self.mesh is not None and self.mesh.world > 1 and not getattr(opt, "mesh_local", False)
@@ -642,12 +666,16 @@ class Executor:
                 if not cands:
                     raise err
                 regroup.setdefault(cands[0], []).append(s)
+            # the failed node's shards, regrouped by their next replica: those
+            # replicas are asked at once as well
+            futs = [self.fanout.submit(self._remote_with_failover, index, c, n2, ss, opt, map_fn, reduce_fn,
+                                       local_fn, tried | {n2.id})
+                    for n2, ss in regroup.items() if n2.id != self.cluster.node.id]
             for n2, ss in regroup.items():
                 if n2.id == self.cluster.node.id:
                     result = reduce_fn(result, self._map_local(ss, map_fn, reduce_fn, local_fn))
-                else:
-                    result = reduce_fn(result, self._remote_with_failover(index, c, n2, ss, opt, map_fn, reduce_fn,
-                                                                          local_fn, tried | {n2.id}))
+            for f in futs:
+                result = reduce_fn(result, f.result())
             return result
 
     def _map_local(self, shards: List[int], map_fn, reduce_fn, local_fn):

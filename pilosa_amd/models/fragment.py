@@ -386,8 +386,12 @@ class Fragment:
                 # stream the mapped file + overlay straight to the new file:
                 # the fragment is never read into heap (under mu: the overlay
                 # must not change while it is written out)
-                self._cold().write_snapshot(tmp)
-            else:
+                st = self._cold()
+                if self._storage is not None:
+                    cold = False   # past the map-count cap _cold() read it into heap
+                else:
+                    st.write_snapshot(tmp)
+            if not cold:
                 data = self.storage.to_bytes()
             gen = self._file_gen
             mark = self._file_size()
@@ -1218,6 +1222,7 @@ class Fragment:
                 if ti.name == "data":
                     with self.mu:
                         self.storage = Bitmap.from_bytes(payload)
+                        self._drop_mapped()   # the old mapping views the replaced inode
                         self._note_unknown()
                         tmp = self.path + ".snapshotting"
                         with open(tmp, "wb") as fh:

@@ -70,19 +70,19 @@ MappedBitmap::MappedBitmap(const std::string& path) {
     throw std::runtime_error("stat " + path + ": " + strerror(errno));
   }
   len_ = size_t(st.st_size);
+  void* p = len_ ? mmap(nullptr, len_, PROT_READ, MAP_SHARED, fd_, 0) : nullptr;
+  const int err = errno;
+  // the mapping stays valid without the descriptor: one fd per fragment
+  // (Fragment's own append handle), as the reference keeps
+  ::close(fd_);
+  fd_ = -1;
   if (len_ == 0) return;  // empty fragment
-  void* p = mmap(nullptr, len_, PROT_READ, MAP_SHARED, fd_, 0);
-  if (p == MAP_FAILED) {
-    ::close(fd_);
-    throw std::runtime_error("mmap " + path + ": " + strerror(errno));
-  }
+  if (p == MAP_FAILED) throw std::runtime_error("mmap " + path + ": " + strerror(err));
   base_ = static_cast<const uint8_t*>(p);
   madvise(p, len_, MADV_RANDOM);
   auto fail = [&](const std::string& msg) {
     munmap(const_cast<uint8_t*>(base_), len_);
-    ::close(fd_);
     base_ = nullptr;
-    fd_ = -1;
     throw std::runtime_error(msg);
   };
   if (len_ < size_t(HEADER_BASE)) fail("data too small");

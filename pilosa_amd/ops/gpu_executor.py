@@ -878,14 +878,16 @@ class GpuExecutor:
                 raise NotImplementedError   # src too large for one device program: host path
         return self._topn_pairs_path(rc, rv, src, n, ids, threshold)
 
-    def topn_batch(self, index: str, calls: List[Call], shards: List[int]) -> Optional[List[List[Pair]]]:
+    def topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False):
         """Whole TopN calls (phase 1, candidate union, ids= re-count, trim to
         n: executor.go:863-903) for a batch of calls over local shards, both
         phases on the device.  Calls of one (field, src shape) share launches:
         cache-only calls one scatter-add + one re-count, src calls the slot
         index (16 per hot-rank launch).  The per-field work (fragments, view,
         rank caches, slot index) is resolved once per batch.  None when a call
-        needs the general path (the caller then runs each call alone)."""
+        needs the general path (the caller then runs each call alone).
+        ``defer`` (with ``self.comm``): a pending result whose last
+        collectives are still in flight (parallel/collectives.Pending)."""
         ex = self._ex()
         params = []
         fields: Dict[str, Tuple] = {}
@@ -914,6 +916,7 @@ class GpuExecutor:
         for i, (fname, _, _) in enumerate(params):
             groups.setdefault((fname, srcs[i] is None), []).append(i)
         out: List[Optional[List[Pair]]] = [None] * len(calls)
+        parts: List[Tuple[List[int], object]] = []
         for (fname, nosrc), members in groups.items():
             rv, rc = fields[fname]
             live = [i for i in members if rc is not None and rc.K and srcs[i] is not EMPTY]
@@ -927,7 +930,7 @@ class GpuExecutor:
             space = self._node_space((index, fname, tuple(shards)), rv)
             if nosrc:
                 self.launches += 1
-                got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space)
+                got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space, defer=defer)
             else:
                 tix = self._topn_index(index, fname, shards, rc, rv, space=space)
                 if tix is None:
@@ -935,13 +938,21 @@ class GpuExecutor:
                     return None
                 self.launches += 1
                 try:
-                    got = tix.topn(self.engine, [srcs[i] for i in live], ns, ths, comm=self.comm)
+                    got = tix.topn(self.engine, [srcs[i] for i in live], ns, ths, comm=self.comm, defer=defer)
                 except CompileError:
                     self.topn_decline = "src too large for one device program"
                     return None
-            for i, r in zip(live, got):
-                out[i] = r
-        return out
+            parts.append((live, got))
+
+        def fill(results):
+            for (live, _), got in zip(parts, results):
+                for i, r in zip(live, got):
+                    out[i] = r
+            return out
+        if defer:
+            from pilosa_amd.parallel.collectives import PendingAll
+            return PendingAll([g for _, g in parts], fill)
+        return fill([g for _, g in parts])
 
     def topn_batch_ready(self, index: str, calls: List[Call], shards: List[int]) -> bool:
         """Would :meth:`topn_batch` answer these calls on the device, with
@@ -966,7 +977,8 @@ class GpuExecutor:
                     return False
                 if c.children:
                     src = self.plan(index, c.children[0], shards)
-                    if src is EMPTY or self._topn_index(index, fname, shards, rc, rv) is None:
+                    space = self._node_space((index, fname, tuple(shards)), rv)
+                    if src is EMPTY or self._topn_index(index, fname, shards, rc, rv, space=space) is None:
                         return False
                     if not (type(src) is Leaf and src.view is rv):
                         self.engine.compile_batch([src])   # a src too large for one program declines here
@@ -1068,8 +1080,9 @@ class GpuExecutor:
             elif f.is_cold() and not f.cache_is_live():
                 sig.append(("cold", id(f)))
             else:
-                f.cache.invalidate()
-                sig.append(("warm", id(f), getattr(f.cache, "version", -1)))
+                with f.mu:   # writers update the rank cache under f.mu (fragment.go:1709-1712)
+                    f.cache.invalidate()
+                    sig.append(("warm", id(f), getattr(f.cache, "version", -1)))
         sig = (id(rv), rv.generation, tuple(sig))
         with self.mu:
             ent = self._rank_cache_map.get(key)
@@ -1083,19 +1096,48 @@ class GpuExecutor:
 
     def _node_space(self, key, rv) -> Optional[np.ndarray]:
         """Sorted union of every rank's row ids of this view (the common space
-        of the node-wide TopN candidates), or None on a single rank."""
+        of the node-wide TopN candidates), or None on a single rank.  Never
+        runs a collective: the mesh refreshes the spaces of a TopN batch
+        collectively first (:meth:`node_space_stale` on every rank, one
+        all-reduced vote, then :meth:`refresh_node_spaces` on every rank), so
+        a write that moved only one rank's view cannot make the ranks pair
+        different collectives."""
         if self.comm is None or rv is None:
             return None
-        import torch
-        sig = (id(rv), rv.generation)
         ent = self._spaces.get(key)
-        if ent is not None and ent[0] == sig:
-            return ent[1]
-        t = torch.from_numpy(np.ascontiguousarray(rv.rows).view(np.int64).copy()).to(rv.device)
-        parts = self.comm.all_gather_var(t)
-        space = np.unique(np.concatenate([p.cpu().numpy().view(np.uint64) for p in parts])) if parts else rv.rows
-        self._spaces[key] = (sig, space)
-        return space
+        if ent is None:
+            raise NotImplementedError("node row space not gathered (mesh refresh missing)")
+        return ent[1]
+
+    def node_space_stale(self, index: str, fname: str, shards: List[int]) -> bool:
+        """Does this rank's copy of the node row space of (index, fname) miss
+        changes of its own view?  Local check only (see :meth:`_node_space`)."""
+        key = (index, fname, tuple(shards))
+        rv = self.view_arena(index, fname, VIEW_STANDARD, shards) if shards else None
+        sig = (id(rv), rv.rows_gen) if rv is not None else None
+        ent = self._spaces.get(key)
+        return ent is None or ent[0] != sig
+
+    def refresh_node_spaces(self, index: str, fnames: Sequence[str], shards: List[int], comm) -> None:
+        """Collective on every rank, fields in the same order: all-gather the
+        ranks' row directories of each field's standard view and keep their
+        sorted union as the node row space (a rank without the view adds
+        nothing).  Every rank takes part in every gather whatever fails
+        locally."""
+        import torch
+        for fname in fnames:
+            key = (index, fname, tuple(shards))
+            rv = None
+            try:
+                rv = self.view_arena(index, fname, VIEW_STANDARD, shards) if shards else None
+            except Exception:  # noqa: BLE001 - contribute no rows, decline in the readiness vote
+                rv = None
+            rows = np.ascontiguousarray(rv.rows if rv is not None else np.zeros(0, np.uint64), dtype=np.uint64)
+            t = torch.from_numpy(rows.view(np.int64).copy()).to(comm.device)
+            parts = comm.all_gather_var(t)
+            space = np.unique(np.concatenate([p.cpu().numpy().view(np.uint64) for p in parts])) if parts else rows
+            sig = (id(rv), rv.rows_gen) if rv is not None else None
+            self._spaces[key] = (sig, space)
 
     def _topn_index(self, index: str, fname: str, shards: List[int], rc, rv, space=None):
         """Device slot index (ops/topn_index.py) over the rank caches ``rc``,
@@ -1107,7 +1149,9 @@ class GpuExecutor:
         from pilosa_amd.ops.topn_index import MAX_SLOTS, DeviceTopNIndex
         key = (index, fname, tuple(shards))
         ent = self._topn_indexes.get(key)
-        if ent is not None and ent[0] is rc and ent[1].view is rv and not ent[1].stale:
+        want = rv.rows if space is None else space
+        same_space = ent is not None and (ent[1].space is want or np.array_equal(ent[1].space, want))
+        if ent is not None and ent[0] is rc and ent[1].view is rv and not ent[1].stale and same_space:
             return ent[1]
         if ent is not None and ent[1].view is rv and space is None:
             # after writes: re-index only the changed shards, in place (no

@@ -102,7 +102,8 @@ class DeviceRankCaches:
             # host rank caches of fragments loaded on the host (their live counts)
             hs, hd, hc = [], [], []
             for si in warm:
-                pairs = list(frags[si].cache.top())
+                with frags[si].mu:
+                    pairs = list(frags[si].cache.top())
                 if not pairs:
                     continue
                 a = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
@@ -229,13 +230,16 @@ class DeviceRankCaches:
         return out
 
     def topn_nosrc(self, ns: Sequence[int], thresholds: Sequence[int], comm=None,
-                   space: Optional[np.ndarray] = None) -> List[List[Pair]]:
+                   space: Optional[np.ndarray] = None, defer: bool = False):
         """Whole TopN(field, n) calls (both phases, trimmed) for a batch.
         ``comm`` (parallel/collectives.Comm) spans the ranks of a node; the
         candidates then travel in ``space``, the sorted union of every rank's
         row ids (identical on all ranks): each rank's phase-1 keys are
-        all-gathered and unioned, the ids= re-count is all-reduced."""
+        all-gathered and unioned, the ids= re-count is all-reduced (left in
+        flight with ``defer``: a pending result, parallel/collectives.Pending)."""
         import torch
+
+        from pilosa_amd.parallel.collectives import Pending
 
         from .topn_index import finish_batch_dev
         Q = len(ns)
@@ -255,8 +259,9 @@ class DeviceRankCaches:
         pq, pa = keys // A, keys % A
         local = dense_dev(self.view, sp[pa]) if pa.numel() else pa.to(torch.int32)
         out = self.recount(pq, local.clamp(min=-1), thresholds)
-        comm.all_reduce(out)
-        return finish_batch_dev(np.asarray(space, dtype=np.uint64), Q, pq, pa, out, ns)
+        sp_h = np.asarray(space, dtype=np.uint64)
+        pend = Pending(comm, comm.all_reduce_async(out), lambda: finish_batch_dev(sp_h, Q, pq, pa, out, ns), keep=out)
+        return pend if defer else pend.result()
 
     def _candidates(self, nmax: int):
         """(u, inv) = torch.unique of the first ``nmax`` ranks of every shard:

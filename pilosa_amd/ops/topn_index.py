@@ -440,33 +440,41 @@ class DeviceTopNIndex:
         return (keys // A).contiguous(), (keys % A).contiguous()
 
     def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
-             comm=None) -> List[List[Pair]]:
+             comm=None, defer: bool = False):
         with self.rw.read():
-            return self._topn(engine, srcs, ns, thresholds, comm)
+            return self._topn(engine, srcs, ns, thresholds, comm, defer)
 
     def _topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],
-             comm=None) -> List[List[Pair]]:
+             comm=None, defer: bool = False):
         """TopN(field, src_q, n=ns[q], threshold=thresholds[q]) for a batch.
         ``comm`` (parallel/collectives.Comm) spans the ranks of a node: the
         candidate union and the phase-2 sums go through it; every rank must
-        call with the same batch."""
+        call with the same batch.  ``defer``: return a pending result with
+        the phase-2 all-reduce still in flight (parallel/mesh.py keeps
+        several TopN batches in flight)."""
+        from pilosa_amd.parallel.collectives import Pending, PendingAll
         Q = len(srcs)
         if Q == 0:
             return []
         if self.R and Q > HOT_Q:
-            out: List[List[Pair]] = []
-            for i in range(0, Q, HOT_Q):
-                out += self.topn(engine, srcs[i:i + HOT_Q], ns[i:i + HOT_Q], thresholds[i:i + HOT_Q], comm)
-            return out
+            parts = [self._topn(engine, srcs[i:i + HOT_Q], ns[i:i + HOT_Q], thresholds[i:i + HOT_Q], comm, defer)
+                     for i in range(0, Q, HOT_Q)]
+            cat = lambda rs: [p for r in rs for p in r]   # noqa: E731
+            return PendingAll(parts, cat) if defer else cat(parts)
         src = self.materialize(engine, srcs)
         hot = self.hot_counts(src, Q)
         keep = self.hist_bytes(Q) <= HIST_KEEP_BYTES
         acc, ns_t, th_t, hist = self.phase1(src, Q, ns, thresholds, keep_hist=keep, hot=hot)
         pair_q, pair_idx = self._candidates(acc, comm)
         out = self.phase2(src, Q, ns_t, th_t, pair_q, pair_idx, hist=hist, hot=hot)
-        if comm is not None:
-            comm.all_reduce(out)
-        return finish_batch_dev(self.space, Q, pair_q, pair_idx, out, ns)
+        space = self.space
+
+        def finish():
+            return finish_batch_dev(space, Q, pair_q, pair_idx, out, ns)
+        if comm is None:
+            return finish()
+        pend = Pending(comm, comm.all_reduce_async(out), finish, keep=out)
+        return pend if defer else pend.result()
 
     def shard_pairs(self, engine: GpuEngine, src, n: int, threshold: int,
                     ids: Optional[Sequence[int]] = None) -> List[Pair]:
@@ -503,11 +511,11 @@ class DeviceTopNIndex:
         ids_out = self.space[a[keep]] if len(a) else np.zeros(0, np.uint64)
         return [Pair(int(i), int(v)) for i, v in zip(ids_out.tolist(), c[keep].tolist())]
 
-    def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None) -> List[List[Pair]]:
+    def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None):
         with self.rw.read():
             return self._topn_nosrc(row_counts, ns, thresholds, comm)
 
-    def _topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None) -> List[List[Pair]]:
+    def _topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None):
         """TopN(field, n) without a src row for a batch, all on the device.
         Phase 1: per shard the first n cache entries at or above the
         threshold (fragment.top stops once its heap holds n rows), summed by

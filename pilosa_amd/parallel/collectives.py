@@ -153,6 +153,31 @@ class Comm:
         self._guard(self.dist.all_gather, ho, self._on(pad), group=self.group)
         return [x[:k].to(t.device) for x, k in zip(ho, lens)]
 
+    def all_gather_var_async(self, t) -> "Pending":
+        """Like :meth:`all_gather_var`, with the data all-gather left in
+        flight: the sizes travel first (one tiny synchronous all-gather, so
+        every rank pads alike), then the padded all-gather is started and
+        the returned :class:`Pending` yields the per-rank tensors."""
+        torch = self.torch
+        t = t.reshape(-1)
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        hs = [self._on(x) for x in sizes]
+        self._guard(self.dist.all_gather, hs, self._on(n), group=self.group)
+        lens = [int(x.item()) for x in hs]
+        m = max(lens) if lens else 0
+        if m == 0:
+            return Pending(self, None, lambda: [t[:0] for _ in range(self.world)])
+        pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+        pad[:t.numel()] = t
+        outs = [torch.empty(m, dtype=t.dtype, device=t.device) for _ in range(self.world)]
+        if self.host_copies:   # gloo rehearsal of a GPU run: host copies, synchronous
+            ho = [self._on(x) for x in outs]
+            self._guard(self.dist.all_gather, ho, self._on(pad), group=self.group)
+            return Pending(self, None, lambda: [x[:k].to(t.device) for x, k in zip(ho, lens)])
+        work = self._guard(self.dist.all_gather, outs, pad, group=self.group, async_op=True)
+        return Pending(self, work, lambda: [x[:k] for x, k in zip(outs, lens)], keep=(pad, outs))
+
     def union(self, t):
         """Sorted distinct values of ``t`` over all ranks (same on every rank)."""
         parts = self.all_gather_var(t)
@@ -175,6 +200,58 @@ class Comm:
 
     def barrier(self):
         self.all_reduce(self.torch.zeros(1, dtype=self.torch.int64, device=self.device))
+
+
+class Pending:
+    """A result whose last collective is still in flight (the mesh keeps
+    several requests in flight: parallel/mesh.py).  ``wait()`` completes the
+    collective only (what a worker rank needs before it drops the tensors);
+    ``result()`` also runs ``finish`` (decode / trim on the front end).
+    Nothing after the collective's start may issue another collective, so
+    completions can run in any order, outside the mesh lock."""
+
+    __slots__ = ("_comm", "_work", "_finish", "_keep")
+
+    def __init__(self, comm, work, finish, keep=None):
+        self._comm, self._work, self._finish, self._keep = comm, work, finish, keep
+
+    def wait(self):
+        if self._work is not None:
+            w, self._work = self._work, None
+            self._comm.wait(w)
+        self._keep = None
+
+    def done(self) -> bool:
+        return self._work is None or Comm.done(self._work)
+
+    def result(self):
+        self.wait()
+        return self._finish()
+
+
+class PendingAll:
+    """Several :class:`Pending` parts finished together by ``combine``."""
+
+    __slots__ = ("parts", "combine")
+
+    def __init__(self, parts, combine):
+        self.parts, self.combine = list(parts), combine
+
+    def wait(self):
+        for p in self.parts:
+            if hasattr(p, "wait"):
+                p.wait()
+
+    def done(self) -> bool:
+        return all(p.done() for p in self.parts if hasattr(p, "done"))
+
+    def result(self):
+        return self.combine([p.result() if hasattr(p, "result") else p for p in self.parts])
+
+
+def resolve(x):
+    """The value of a possibly pending result."""
+    return x.result() if callable(getattr(x, "result", None)) and callable(getattr(x, "wait", None)) else x
 
 
 def init(backend: Optional[str] = None, local_rank: int = 0, timeout_s: float = 120.0):

@@ -28,7 +28,13 @@ hop with a process group (backend ``nccl`` = RCCL over xGMI on the GPU box,
 Transport is tensors only (parallel/collectives.py): a command is an int64
 header plus a uint8 payload tensor, no pickled objects.  Collectives are
 issued strictly in the same order on every rank, so the front end serialises
-mesh operations with a lock.  Every collective has the process group's
+the ISSUE of mesh operations with a lock: the command broadcast, this rank's
+share of the work and the start of the operation's last collective.  Count
+batches, general calls (OP_CALL) and TopN batches (OP_TOPN) leave that last
+collective in flight (a ``collectives.Pending``) and complete it -- wait,
+decode, reduce, trim -- outside the lock, so up to MAX_IN_FLIGHT requests per
+rank overlap (the reference runs every query's mapReduce independently,
+executor.go:2458-2518).  Every collective has the process group's
 timeout; when one fails (a rank died or hung) the front end fails over: it
 adopts the other ranks' fragment files from their data dirs into its own
 holder (lazily opened, loaded into its HBM on first use) and keeps serving
@@ -48,7 +54,7 @@ class MeshError(RuntimeError):
 
 # ---------------------------------------------------------------- transport
 (OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS, OP_COUNT_TEXT,
- OP_ERRORS, OP_TOPN) = range(12)
+ OP_ERRORS, OP_TOPN, OP_SYNC, OP_RECALC) = range(14)
 MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
 
 
@@ -139,7 +145,8 @@ class ShardMesh:
         partial results with ``reduce_fn`` (the executor's reduce step)."""
         if c.name == "Count":
             return self._run(OP_COUNT, index, [str(c)], list(shards))[0]
-        parts = self._run(OP_CALL, index, str(c), list(shards), _opt_dict(opt))
+        parts = self._run_pipelined(OP_CALL, index, str(c), list(shards), _opt_dict(opt))
+        _raise_remote(parts)
         result = None
         for p in parts:
             result = reduce_fn(result, p)
@@ -218,10 +225,40 @@ class ShardMesh:
         (executor.go:863-903 over RCCL instead of per-shard pair lists).  The
         ranks first agree (one all-reduce of a flag) that each can run the
         batch on its device; None = use the general path."""
-        res = self._run(OP_TOPN, index, [str(c) for c in calls], list(shards))
+        res = self._run_pipelined(OP_TOPN, index, [str(c) for c in calls], list(shards))
         if res is not None:
             self.topn_tensor_batches += 1
         return res
+
+    def _run_pipelined(self, op: int, *args):
+        """Front end: broadcast + issue under the lock (this rank's share
+        and the start of the last collective), completion outside it, so
+        the next request's issue overlaps this one's transfer and decode."""
+        from .collectives import CommError, encode, resolve
+
+        if not self.is_frontend:
+            raise MeshError("only rank 0 issues mesh commands")
+        with self.lock:
+            if self.failed_over:
+                raise MeshError(f"mesh failed over: {self.failover_error}")
+            self.ops += 1
+            try:
+                self.comm.bcast_bytes(op, encode(list(args)))
+                h = self._issue(op, list(args))
+            except CommError as e:
+                self.failover(e)
+                raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
+            self.in_flight += 1
+            self.max_in_flight = max(self.max_in_flight, self.in_flight)
+        try:
+            return resolve(h)
+        except CommError as e:
+            with self.lock:
+                self.failover(e)
+            raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
+        finally:
+            with self.lock:
+                self.in_flight -= 1
 
     def _host_list(self, t) -> List[int]:
         gpu = getattr(self.executor, "gpu", None)
@@ -253,6 +290,18 @@ class ShardMesh:
         """Available shards per rank (status/debug)."""
         parts = self._run(OP_SHARDS)
         return {r: p for r, p in enumerate(parts)}
+
+    def recalculate_caches(self):
+        """Every rank re-ranks its fragments' caches now (the reference's
+        /recalculate-caches, holder.go:544, on each GPU's holder)."""
+        self._run(OP_RECALC)
+
+    def sync(self) -> List[int]:
+        """Quiesce the node: every rank completes its requests in flight and
+        synchronises its device, then the ranks meet (one gather).  Returns
+        each rank's monotonic clock (ns) at that point, so the time between
+        two syncs can be taken as the max over ranks (bench.py)."""
+        return [int(x) for x in self._run(OP_SYNC)]
 
     def stop(self):
         if self.is_frontend and not self.failed_over:
@@ -306,14 +355,22 @@ class ShardMesh:
             op, payload = self.comm.bcast_bytes()
             if op == OP_STOP:
                 while self._pending:
-                    self.comm.wait(self._pending.popleft()[1])
+                    self._pending.popleft().wait()
                 return
-            if op == OP_COUNT_TEXT:
-                index, text, shards, q, seq = decode(payload)
-                self._pending.append(self._count_text_issue(index, text, shards, q, seq))
-                # keep tensors alive until their collective is done; bound the queue
-                while self._pending and (len(self._pending) > MAX_IN_FLIGHT or self.comm.done(self._pending[0][1])):
-                    self.comm.wait(self._pending.popleft()[1])
+            if op in (OP_COUNT_TEXT, OP_CALL, OP_TOPN):
+                args = decode(payload) or []
+                if op == OP_COUNT_TEXT:
+                    index, text, shards, q, seq = args
+                    t, work = self._count_text_issue(index, text, shards, q, seq)
+                    from .collectives import Pending
+                    h = Pending(self.comm, work, lambda: None, keep=t)
+                else:
+                    h = self._issue(op, args)
+                if hasattr(h, "wait"):
+                    # keep tensors alive until their collective is done; bound the queue
+                    self._pending.append(h)
+                while self._pending and (len(self._pending) > MAX_IN_FLIGHT or self._pending[0].done()):
+                    self._pending.popleft().wait()
                 continue
             self._dispatch(op, decode(payload) or [])
 
@@ -337,14 +394,9 @@ class ShardMesh:
                 if self.is_frontend:
                     _raise_remote(parts)
             return out[:-1]
-        if op == OP_TOPN:
-            return self._topn_batch_local(*args)
         mine = None
         try:
-            if op == OP_CALL:
-                index, pql, shards, optd = args
-                mine = self._local_call(index, pql, self.owned(shards), optd)
-            elif op == OP_WRITE:
+            if op == OP_WRITE:
                 index, pql, shard, optd = args
                 if self.owner(shard) == self.rank:
                     mine = self._local_call(index, pql, [shard], optd)
@@ -365,6 +417,15 @@ class ShardMesh:
                         idx.delete_field(args[1])
             elif op == OP_ERRORS:
                 mine = self._errors.pop(int(args[0]), None)
+            elif op == OP_RECALC:
+                ex.holder.recalculate_caches()
+            elif op == OP_SYNC:
+                while self._pending:
+                    self._pending.popleft().wait()
+                if self.device.type == "cuda":
+                    self.torch.cuda.synchronize(self.device)
+                import time
+                mine = time.perf_counter_ns()
             elif op == OP_SHARDS:
                 mine = {name: idx.available_shards() for name, idx in ex.holder.indexes.items()}
                 if self.is_frontend:
@@ -381,30 +442,86 @@ class ShardMesh:
             _raise_remote(parts)
         return parts
 
+    def _issue(self, op: int, args: list):
+        """This rank's share of a pipelined operation, up to the start of its
+        last collective: a Pending (or a plain value when nothing is left in
+        flight).  Any failure of the local work travels as the rank's partial
+        (OP_CALL) or as a declined readiness vote (OP_TOPN), never as a
+        missing collective."""
+        from .collectives import decode_partial, encode_partial
+
+        if op == OP_TOPN:
+            return self._topn_batch_local(*args)
+        if op != OP_CALL:
+            raise MeshError(f"mesh command {op!r} is not pipelined")
+        index, pql, shards, optd = args
+        try:
+            mine = self._local_call(index, pql, self.owned(shards), optd)
+        except Exception as e:  # noqa: BLE001 - reported through the gather below
+            mine = e
+        t = self.torch.from_numpy(encode_partial(mine)).to(self.device)
+        return _Chain(self.comm.all_gather_var_async(t), lambda ps: [decode_partial(p.cpu().numpy()) for p in ps])
+
+    def _refresh_spaces(self, index: str, fnames: List[str], own: List[int]):
+        """Collective vote + refresh of the node row spaces of a TopN batch:
+        every rank reports whether its copy is stale (a write moved its own
+        view), and if ANY rank says so every rank re-gathers, field by field
+        in the same order -- the decision is never rank-local."""
+        torch = self.torch
+        gpu = self.executor.gpu
+        stale = 0
+        try:
+            if gpu is not None and hasattr(gpu, "node_space_stale"):
+                stale = int(any(gpu.node_space_stale(index, f, own) for f in fnames))
+        except Exception:  # noqa: BLE001 - a rank that cannot tell asks for a refresh
+            stale = 1
+        flag = torch.tensor([stale], dtype=torch.int64, device=self.device)
+        self.comm.all_reduce(flag)
+        if not int(flag.item()):
+            return
+        if gpu is not None and hasattr(gpu, "refresh_node_spaces"):
+            gpu.refresh_node_spaces(index, fnames, own, self.comm)
+        else:
+            for _ in fnames:   # take part with no rows
+                self.comm.all_gather_var(torch.zeros(0, dtype=torch.int64, device=self.device))
+
     def _topn_batch_local(self, index: str, pqls: List[str], shards: List[int]):
         from pilosa_amd.pql import parse_string
 
         torch = self.torch
         ex = self.executor
         gpu = ex.gpu
+        from pilosa_amd.executor import DEFAULT_FIELD
+
         own = self.owned(shards)
         ok = False
         calls = []
         try:
             calls = [parse_string(p).calls[0] for p in pqls]
-            ok = gpu is not None and ex.holder.index(index) is not None and gpu.topn_batch_ready(index, calls, own)
-        except Exception:  # noqa: BLE001 - a rank that cannot take part declines
-            ok = False
-        flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=self.device)
-        self.comm.all_reduce(flag)
-        if int(flag.item()):
-            return None
-        prev = gpu.comm
-        gpu.comm = self.comm
+        except Exception:  # noqa: BLE001 - the same text fails on every rank
+            calls = []
+        # the batch's fields come from the command text: every rank lists the
+        # same ones in the same order for the collective space refresh
+        fnames = sorted({str(c.args.get("_field") or DEFAULT_FIELD) for c in calls})
+        prev = gpu.comm if gpu is not None else None
+        if gpu is not None:
+            gpu.comm = self.comm
         try:
-            res = gpu.topn_batch(index, calls, own)
+            if fnames:
+                self._refresh_spaces(index, fnames, own)
+            try:
+                ok = bool(calls) and gpu is not None and ex.holder.index(index) is not None and \
+                    gpu.topn_batch_ready(index, calls, own)
+            except Exception:  # noqa: BLE001 - a rank that cannot take part declines
+                ok = False
+            flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=self.device)
+            self.comm.all_reduce(flag)
+            if int(flag.item()):
+                return None
+            res = gpu.topn_batch(index, calls, own, defer=True)
         finally:
-            gpu.comm = prev
+            if gpu is not None:
+                gpu.comm = prev
         if res is None:   # every rank checked readiness: a decline now would desynchronise
             raise MeshError(f"rank {self.rank}: TopN batch declined after the readiness check")
         return res
@@ -508,6 +625,24 @@ class ShardMesh:
             f.import_roaring(shard, p["views"], p.get("clear", False))
         else:
             raise MeshError(f"unknown import kind {what!r}")
+
+
+class _Chain:
+    """A pending result post-processed by ``fn`` on completion."""
+
+    __slots__ = ("p", "fn")
+
+    def __init__(self, p, fn):
+        self.p, self.fn = p, fn
+
+    def wait(self):
+        self.p.wait()
+
+    def done(self) -> bool:
+        return self.p.done()
+
+    def result(self):
+        return self.fn(self.p.result())
 
 
 def _plain(v):

@@ -365,7 +365,11 @@ class API:
 
     def recalculate_caches(self, remote: bool = False):
         self.validate("RecalculateCaches")
-        self.holder.recalculate_caches()
+        mesh = getattr(self.executor, "mesh", None)
+        if mesh is not None and mesh.world > 1:
+            mesh.recalculate_caches()   # every GPU's holder (rank 0's included)
+        else:
+            self.holder.recalculate_caches()
         if not remote:
             self.server.broadcast({"type": "RecalculateCaches"})
 

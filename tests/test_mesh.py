@@ -291,3 +291,64 @@ def test_mesh_count_text_pipelined(tmp_path):
     assert res["seq"] >= 24
     assert res["max_in_flight"] >= 2, res["max_in_flight"]
     assert "field not found" in res["err"] and res["rank_errors"], res
+
+
+CALL_QUERIES = ["TopN(f, n=3)", "TopN(f, Row(g=3), n=2)", "Sum(Row(f=1), field=v)", "Rows(f)",
+                "GroupBy(Rows(f), Rows(g))", "MaxRow(field=f)", "Min(field=v)", "Row(f=2)"]
+
+
+def _call_pipeline_worker(rank, world, port, outdir):
+    """Concurrent general calls (TopN, Sum, Rows, GroupBy, ...) through the
+    mesh: each request's OP_CALL is issued under the front-end lock and
+    completed (all-gather wait, decode, reduce) outside it, so requests
+    overlap; answers equal the same calls run one at a time."""
+    import threading
+
+    import torch.distributed as dist
+
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    holder = Holder(tempfile.mkdtemp(prefix=f"meshc{rank}_")).open()
+    ex = Executor(holder)
+    mesh = ShardMesh(ex, block=1)
+    ex.mesh = mesh
+    try:
+        if rank != 0:
+            mesh.serve()
+            return
+        _setup_schema(holder)
+        mesh.apply_schema()
+        bits, vals = _data()
+        _load(ex, bits, vals, mesh)
+        want = {q: _canon(ex.execute("i", q).results) for q in CALL_QUERIES}
+        reqs = [CALL_QUERIES[k % len(CALL_QUERIES)] for k in range(48)]
+        got = [None] * len(reqs)
+
+        def run(k):
+            got[k] = _canon(ex.execute("i", reqs[k]).results)
+        ts = [threading.Thread(target=run, args=(k,)) for k in range(len(reqs))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        with open(os.path.join(outdir, "calls.json"), "w") as fh:
+            json.dump({"ok": [got[k] == want[reqs[k]] for k in range(len(reqs))],
+                       "max_in_flight": mesh.max_in_flight}, fh)
+        mesh.stop()
+    finally:
+        ex.close()
+        holder.close()
+        dist.destroy_process_group()
+
+
+def test_mesh_general_calls_pipelined(tmp_path):
+    mp.start_processes(_call_pipeline_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True,
+                       start_method="spawn")
+    res = json.load(open(tmp_path / "calls.json"))
+    assert all(res["ok"]), res["ok"]
+    assert res["max_in_flight"] >= 2, res["max_in_flight"]
