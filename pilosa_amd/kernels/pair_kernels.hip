@@ -552,6 +552,165 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
   }
   if (lane < nq) partial[u * Q + q0 + lane] = mine;
 }
+// ---- v10: one wave per (unit, chunk of CQ queries) as v6, but a run of
+// queries that share the staged row A is counted as ONE flat stream.
+//
+// v6 handles one pair at a time: readlanes, a type dispatch, one probe pass
+// with most lanes idle for the typical 30-300-value partner, and a wave_sum,
+// for each of the 58.6M pairs of a 4096-query batch.  Here, after A is
+// staged, the run's array partners are laid end to end as 16-byte chunks
+// (8 values): an inclusive wave scan of their chunk counts gives each pair's
+// first chunk, and every iteration gives each lane the next chunk of the
+// stream, whatever pair it belongs to.  The lane->pair map of an iteration
+// is a popcount: the pairs' first chunks are bits of a boundary bitmap in
+// LDS, so pair(lane) = pairs started before the window + mbcnt of the
+// window's 64 boundary bits up to the lane.  Per-pair sums are kept in a
+// register while a lane stays on one pair and flushed with a non-returning
+// LDS add when it moves on; each pair's lane reads its total at the end.
+// Bitmap / run partners (rare) keep v6's per-pair wave-cooperative count.
+extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+}
+
+constexpr int V10_WIN = 2048;  // chunks per boundary window: 64 dwords, one per lane
+
+template <int CQ>
+__global__ __launch_bounds__(64, 5) void and2_pairs_v10_kernel(const QueryProg* __restrict__ progs, int Q,
+                                                              const ViewDev* __restrict__ views, int S,
+                                                              const uint2* __restrict__ pairs,
+                                                              int32_t* __restrict__ partial) {
+  __shared__ uint64_t lb[1024];          // the staged container, as a bitmap
+  __shared__ uint4 tbl[64];              // per array partner: payload pointer, first chunk, n
+  __shared__ uint32_t bnd[V10_WIN / 32];  // first-chunk bits of the current window
+  __shared__ int32_t cnt[64];            // per array partner: its count
+  const int lane = lane_id();
+  const int64_t gw = int64_t(xcd_remap_blocks(blockIdx.x, gridDim.x));
+  const int nch = (Q + CQ - 1) / CQ;
+  const int64_t u = gw / nch;
+  if (u >= int64_t(S) * 16) return;
+  const int q0 = int(gw % nch) * CQ;
+  const int nq = min(CQ, Q - q0);
+
+  uint32_t ea = NONE;
+  int vai = -1;
+  int64_t ma = 0, mb = 0;
+  uint64_t pal = 0, pbl = 0;
+  if (lane < nq) {
+    const uint2 e = pairs[u * Q + q0 + lane];
+    if (e.x != NONE) {
+      ea = e.x;
+      vai = progs[q0 + lane].leaf_view[0];
+      const int vbi = progs[q0 + lane].leaf_view[1];
+      ma = gp(views[vai].meta)[e.x];
+      mb = gp(views[vbi].meta)[e.y];
+      pal = reinterpret_cast<uint64_t>(payload_of(views[vai], ma));
+      pbl = reinterpret_cast<uint64_t>(payload_of(views[vbi], mb));
+    }
+  }
+  const bool valid = ea != NONE;
+  const int tB = meta_type(mb);
+  const int nB = meta_n(mb);
+  const uint32_t* bm32 = reinterpret_cast<const uint32_t*>(lb);
+  uint64_t todo = __ballot(valid);
+  int mine = 0;
+  while (todo) {
+    const int i = __builtin_ctzll(todo);
+    const uint32_t a = __builtin_amdgcn_readlane(ea, i);
+    const int va = __builtin_amdgcn_readlane(vai, i);
+    // the batch is sorted by (A, B): a run's lanes are consecutive among the valid ones
+    const uint64_t run = __ballot(valid && ea == a && vai == va) & todo;
+    todo &= ~run;
+    const int64_t mA = rl64(ma, i);
+    const uint16_t* pA = reinterpret_cast<const uint16_t*>(rl_u64(pal, i));
+    const int tA = meta_type(mA);
+    if ((run & (run - 1)) == 0) {
+      // a pair of its own: v6's shortcuts that need no staging, else stage the smaller array
+      const int64_t mB = rl64(mb, i);
+      const uint16_t* pB = reinterpret_cast<const uint16_t*>(rl_u64(pbl, i));
+      const int tb = meta_type(mB);
+      int c;
+      if (tA == CT_BITMAP && tb == CT_BITMAP) {
+        c = and_global_bitmaps(reinterpret_cast<const uint64_t*>(pA), reinterpret_cast<const uint64_t*>(pB));
+      } else if (tA == CT_ARRAY && tb == CT_BITMAP && meta_n(mA) <= SMALL_ARRAY_N) {
+        c = probe_small<false>(gp(reinterpret_cast<const uint32_t*>(pB)), pA, meta_n(mA));
+      } else if (tA == CT_ARRAY && (tb == CT_BITMAP || (tb == CT_ARRAY && meta_n(mB) < meta_n(mA)))) {
+        lds_wait();
+        stage(lb, pB, mB);
+        c = count_vs_lds(lb, pA, mA);
+      } else {
+        lds_wait();
+        stage(lb, pA, mA);
+        c = count_vs_lds(lb, pB, mB);
+      }
+      c = wave_sum(c);
+      if (lane == i) mine = c;
+      continue;
+    }
+    lds_wait();  // previous readers of lb / tbl / cnt are done before they are rewritten
+    stage(lb, pA, mA);
+    const bool inrun = (run >> lane) & 1;
+    const uint64_t am = __ballot(inrun && tB == CT_ARRAY);
+    // bitmap / run partners: one at a time, wave-cooperative
+    for (uint64_t other = run & ~am; other; other &= other - 1) {
+      const int j = __builtin_ctzll(other);
+      int c = count_vs_lds(lb, reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j));
+      c = wave_sum(c);
+      if (lane == j) mine = c;
+    }
+    if (!am) continue;
+    // array partners: one flat stream of 16-byte chunks
+    const bool isArr = (am >> lane) & 1;
+    const int n8 = isArr ? (nB + 7) >> 3 : 0;
+    const int incl = __ockl_wfscan_add_i32(n8, true);
+    const int start = incl - n8;
+    const int T = __builtin_amdgcn_readlane(incl, 63);
+    const int ord = int(mbcnt64(am));
+    if (isArr) {
+      tbl[ord] = make_uint4(uint32_t(pbl), uint32_t(pbl >> 32), uint32_t(start), uint32_t(nB));
+      cnt[ord] = 0;
+    }
+    const int bit0 = int(bm32[0] & 1u);  // hits of a zero-valued pad probe
+    int kb = -1, curk = -1, acc = 0;
+    for (int w0 = 0; w0 < T; w0 += V10_WIN) {
+      bnd[lane] = 0u;
+      lds_wait();
+      if (isArr && start >= w0 && start < w0 + V10_WIN)
+        atomicOr(&bnd[(start - w0) >> 5], 1u << (start & 31));
+      lds_wait();
+      const int wend = min(T, w0 + V10_WIN);
+      for (int b = w0; b < wend; b += 64) {
+        const uint32_t wi = uint32_t(b - w0) >> 5;
+        const uint64_t M = (uint64_t(__builtin_amdgcn_readfirstlane(bnd[wi + 1])) << 32) |
+                           uint32_t(__builtin_amdgcn_readfirstlane(bnd[wi]));
+        const int k = kb + int(mbcnt64(M)) + int((M >> lane) & 1u);
+        kb += __popcll(M);
+        const int t = b + lane;
+        if (t < wend) {
+          const uint4 e = tbl[k];
+          const int c = t - int(e.z);
+          const auto p4 = gp(reinterpret_cast<const uint4*>((uint64_t(e.y) << 32) | e.x));
+          const uint4 v4 = p4[c];
+          const int rem = int(e.w) - c * 8;
+          int cc = probe8<true>(bm32, v4);
+          if (rem < 8) cc -= bit0 * (8 - rem);
+          if (k != curk) {
+            if (curk >= 0) atomicAdd(&cnt[curk], acc);
+            curk = k;
+            acc = cc;
+          } else {
+            acc += cc;
+          }
+        }
+      }
+    }
+    if (curk >= 0) atomicAdd(&cnt[curk], acc);
+    lds_wait();
+    if (isArr) mine = cnt[ord];
+  }
+  if (lane < nq) partial[u * Q + q0 + lane] = mine;
+}
 }  // namespace
 
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st) {
@@ -560,9 +719,9 @@ void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st
   hipLaunchKernelGGL(keymask_build_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, v, S, out);
 }
 
-// pair_build then and2_pairs_v6; `cq` = queries per wave (16 / 32 / 64; <= 0
-// picks by batch size: 32 for Q <= 2048, 64 above).  `variant` is accepted
-// for API stability; every value runs v6.
+// pair_build then the pair kernel; `cq` = queries per wave (16 / 32 / 64; <= 0
+// picks by batch size: 32 for Q <= 2048, 64 above).  `variant` 10 runs the
+// flat-stream kernel (and2_pairs_v10), anything else v6.
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
                        int cq, int variant, hipStream_t st) {
   const int64_t items = int64_t(Q) * S;
@@ -571,12 +730,15 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                      pairs);
   const int64_t units = int64_t(S) * 16;
   if (cq <= 0) cq = Q <= 2048 ? 32 : 64;
-  (void)variant;
-#define PK_LAUNCH(CQV)                                                                                      \
-  {                                                                                                         \
-    const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                       \
-    hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, \
-                       pairs, partial);                                                                     \
+#define PK_LAUNCH(CQV)                                                                                       \
+  {                                                                                                          \
+    const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                        \
+    if (variant == 10)                                                                                       \
+      hipLaunchKernelGGL(and2_pairs_v10_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, \
+                         pairs, partial);                                                                    \
+    else                                                                                                     \
+      hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
+                         pairs, partial);                                                                    \
   }
   switch (cq) {
     case 16: PK_LAUNCH(16) break;

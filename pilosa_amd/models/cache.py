@@ -18,6 +18,8 @@ import threading
 import time
 from typing import Dict, Iterable, List, Tuple
 
+import numpy as np
+
 THRESHOLD_FACTOR = 1.1
 CACHE_TYPE_RANKED = "ranked"
 CACHE_TYPE_LRU = "lru"
@@ -134,7 +136,8 @@ class RankCache:
         self.max_entries = int(max_entries)
         self.threshold_buffer = int(THRESHOLD_FACTOR * self.max_entries)
         self.entries: Dict[int, int] = {}
-        self.rankings: List[Tuple[int, int]] = []
+        self._ranked = (np.zeros(0, np.uint64), np.zeros(0, np.int64))
+        self._rankings: List[Tuple[int, int]] = []
         self.version = 0  # bumped whenever top() can change (device TopN index validity)
         self.threshold_value = 0
         self.update_time = 0.0
@@ -152,6 +155,15 @@ class RankCache:
             if n < self.threshold_value:
                 return
             self.entries[id] = n
+
+    def bulk_add_many(self, ids, counts):
+        """bulk_add for arrays of (row id, count) at once (bulk imports,
+        cache open): one dict update instead of a call per row."""
+        ids = np.asarray(ids, dtype=np.uint64)
+        counts = np.asarray(counts, dtype=np.int64)
+        with self._lock:
+            keep = counts >= self.threshold_value
+            self.entries.update(zip(ids[keep].tolist(), counts[keep].tolist()))
 
     def get(self, id):
         with self._lock:
@@ -178,20 +190,34 @@ class RankCache:
         self._recalculate()
 
     def _recalculate(self):
-        rankings = sorted(self.entries.items(), key=lambda kv: (-kv[1], kv[0]))
-        remove = []
-        if len(rankings) > self.max_entries:
-            self.threshold_value = rankings[self.max_entries][1]
-            remove = rankings[self.max_entries:]
-            rankings = rankings[: self.max_entries]
+        # count desc, then id asc (cache.go:245-281), sorted with numpy
+        n = len(self.entries)
+        ids = np.fromiter(self.entries.keys(), dtype=np.uint64, count=n)
+        cnt = np.fromiter(self.entries.values(), dtype=np.int64, count=n)
+        order = np.lexsort((ids, -cnt))
+        ids, cnt = ids[order], cnt[order]
+        if n > self.max_entries:
+            self.threshold_value = int(cnt[self.max_entries])
+            if n > self.threshold_buffer:
+                for id in ids[self.max_entries:].tolist():
+                    self.entries.pop(id, None)
+            ids, cnt = ids[:self.max_entries], cnt[:self.max_entries]
         else:
             self.threshold_value = 1
-        self.rankings = rankings
+        # the (id, count) list is built when someone reads it (top()): a bulk
+        # import re-ranks after every batch, TopN reads far less often
+        self._ranked = (ids, cnt)
+        self._rankings = None
         self.version += 1
         self.update_time = time.monotonic()
-        if len(self.entries) > self.threshold_buffer:
-            for id, _ in remove:
-                self.entries.pop(id, None)
+
+    @property
+    def rankings(self) -> List[Tuple[int, int]]:
+        r = self._rankings
+        if r is None:
+            ids, cnt = self._ranked
+            r = self._rankings = list(zip(ids.tolist(), cnt.tolist()))
+        return r
 
     def top(self):
         return self.rankings

@@ -304,17 +304,18 @@ class Fragment:
         p = self.cache_path()
         if not os.path.exists(p):
             return
-        from pilosa_amd.wire import pb
-        m = pb.Cache()
-        try:
-            with open(p, "rb") as fh:
-                m.ParseFromString(fh.read())
-        except Exception:  # noqa: BLE001 - a corrupt cache is rebuilt
+        # the protobuf Cache message read natively (a corrupt one is rebuilt)
+        _, ids, ok = _roaring.read_cache_files([p], 1)
+        if not ok[0]:
             return
         st = self._rw()
-        for rid in m.IDs:
-            n = st.count_range(rid * SHARD_WIDTH, (rid + 1) * SHARD_WIDTH)
-            self._cache.bulk_add(rid, n)
+        ids = np.asarray(ids, dtype=np.uint64)
+        if len(ids) and hasattr(self._cache, "bulk_add_many"):
+            # one native call counts every cached row (openCache's CountRange per id)
+            self._cache.bulk_add_many(ids, st.count_rows(ids, CONTAINERS_PER_ROW))
+        else:
+            for rid in ids.tolist():
+                self._cache.bulk_add(rid, st.count_range(rid * SHARD_WIDTH, (rid + 1) * SHARD_WIDTH))
         self._cache.invalidate()
 
     def flush_cache(self):
@@ -591,9 +592,13 @@ class Fragment:
             self.checksums.pop(int(b), None)
         if self.cache_type != CACHE_TYPE_NONE:
             counts = self._rw().count_rows(rows, CONTAINERS_PER_ROW)
-            add = self.cache.bulk_add
-            for rid, n in zip(rows.tolist(), counts.tolist()):
-                add(rid, n)
+            bulk = getattr(self.cache, "bulk_add_many", None)
+            if bulk is not None:
+                bulk(rows, counts)
+            else:
+                add = self.cache.bulk_add
+                for rid, n in zip(rows.tolist(), counts.tolist()):
+                    add(rid, n)
         mx = int(rows.max())
         if mx > self.max_row_id:
             self.max_row_id = mx

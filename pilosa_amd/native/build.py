@@ -39,7 +39,8 @@ def build_roaring(force: bool = False, verbose: bool = False, stats: bool = Fals
 
     name = "_roaring_stats" if stats else "_roaring"
     out = os.path.join(PKG, name + _ext_suffix())
-    srcs = [os.path.join(HERE, f) for f in ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp", "mapped.cpp")]
+    srcs = [os.path.join(HERE, f) for f in ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp", "mapped.cpp",
+                                          "wire_decode.cpp")]
     deps = srcs + [os.path.join(HERE, f) for f in ("roaring.hpp", "synth.hpp")]
     if not force and not _newer(out, deps):
         return out

@@ -12,8 +12,13 @@
 // Accepted subset (everything else is flagged for the general path, so
 // semantics are never approximated here):
 //   query := ws 'Count' ws '(' ws expr ws ')' ws EOF
-//   expr  := ('Row'|'Bitmap') ws '(' ws field ws '=' ws uint ws ')'
+//   expr  := ('Row'|'Bitmap') ws '(' ws field ws '=' ws uint [range] ws ')'
 //          | ('Intersect'|'Union'|'Difference'|'Xor') ws '(' ws expr (ws ',' ws expr)* ws ')'
+//   range := (ws ',' ws ('from'|'to') ws '=' ws time)+      each key at most once
+// A Row with a time range is the union of the row over the range's covering
+// views (executor.go:1444-1533 with time.go:104-181 viewsByTimeRange): the
+// caller resolves each distinct (field, from, to) to those views' slots
+// (count_text_ranges), and the leaf compiles to leaf0 leaf1 OR leaf2 OR ...
 // Reference semantics: executor.go:585-680 (bitmap call tree), 1668-1790
 // (Intersect/Union/Difference/Xor folding left to right).
 #include <pybind11/numpy.h>
@@ -68,11 +73,86 @@ struct View {
 
 struct Unsupported {};
 
+// (field, from, to) of a time-range Row -> slots of its covering views
+using RangeMap = std::unordered_map<std::string, std::vector<int>>;
+static const RangeMap kNoRanges;
+constexpr char kAbsent = '\x01';  // from/to not given
+
+static std::string range_key(const std::string& field, const std::string& from, const std::string& to) {
+  return field + '\x1f' + from + '\x1f' + to;
+}
+
+// A time value: a quoted string ('...' or "...", no escapes) or a bare
+// timestamp token; the text between the quotes is returned.
+static bool scan_time(std::string_view s, size_t& i, std::string& out) {
+  if (i >= s.size()) return false;
+  const char q = s[i];
+  if (q == '\'' || q == '"') {
+    const size_t e = s.find(q, i + 1);
+    if (e == std::string_view::npos) return false;
+    out.assign(s.substr(i + 1, e - i - 1));
+    i = e + 1;
+    return true;
+  }
+  const size_t b = i;
+  while (i < s.size() && (std::isalnum(static_cast<unsigned char>(s[i])) || s[i] == ':' || s[i] == '-' || s[i] == '.'))
+    i++;
+  if (i == b) return false;
+  out.assign(s.substr(b, i - b));
+  return true;
+}
+
+static void skip_ws(std::string_view s, size_t& i) {
+  while (i < s.size() && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++;
+}
+
+static bool key_word(std::string_view s, size_t& i, const char* w) {
+  const size_t n = std::strlen(w);
+  if (s.compare(i, n, w) != 0) return false;
+  if (i + n < s.size() && (std::isalnum(static_cast<unsigned char>(s[i + n])) || s[i + n] == '_')) return false;
+  i += n;
+  return true;
+}
+
+// `, from=<t>, to=<t>` after a Row's row id, up to and including the
+// closing ')'.  false = not this shape (the caller takes the general path).
+static bool scan_range(std::string_view s, size_t& i, std::string& from, std::string& to) {
+  bool hf = false, ht = false;
+  from.assign(1, kAbsent);
+  to.assign(1, kAbsent);
+  for (;;) {
+    skip_ws(s, i);
+    if (key_word(s, i, "from")) {
+      if (hf) return false;
+      hf = true;
+      skip_ws(s, i);
+      if (i >= s.size() || s[i++] != '=') return false;
+      skip_ws(s, i);
+      if (!scan_time(s, i, from)) return false;
+    } else if (key_word(s, i, "to")) {
+      if (ht) return false;
+      ht = true;
+      skip_ws(s, i);
+      if (i >= s.size() || s[i++] != '=') return false;
+      skip_ws(s, i);
+      if (!scan_time(s, i, to)) return false;
+    } else {
+      return false;
+    }
+    skip_ws(s, i);
+    if (i < s.size() && s[i] == ')') {
+      i++;
+      return true;
+    }
+    if (i >= s.size() || s[i++] != ',') return false;
+  }
+}
+
 class Compiler {
  public:
   Compiler(std::string_view s, const std::unordered_map<std::string, int>& fields, const std::vector<View>& views,
-           QueryProg& out)
-      : s_(s), fields_(fields), views_(views), outp_(&out) {}
+           QueryProg& out, const RangeMap& ranges = kNoRanges)
+      : s_(s), fields_(fields), views_(views), outp_(&out), ranges_(ranges) {}
 
   bool run() {
     if (!call()) return false;
@@ -111,7 +191,18 @@ class Compiler {
   const std::unordered_map<std::string, int>& fields_;
   const std::vector<View>& views_;
   QueryProg* outp_;
+  const RangeMap& ranges_;
   int nleaf_ = 0, nprog_ = 0, depth_ = 0;
+
+  // leaf index of (view slot, dense row), added if new
+  int leaf_of(int slot, int64_t d) {
+    for (int x = 0; x < nleaf_; x++)
+      if (outp_->leaf_view[x] == slot && outp_->leaf_row[x] == d) return x;
+    if (nleaf_ >= MAXLEAF) return -1;
+    outp_->leaf_view[nleaf_] = slot;
+    outp_->leaf_row[nleaf_] = d;
+    return nleaf_++;
+  }
 
   void ws() {
     while (i_ < s_.size() && (s_[i_] == ' ' || s_[i_] == '\t' || s_[i_] == '\n' || s_[i_] == '\r')) i_++;
@@ -158,21 +249,32 @@ class Compiler {
     }
     if (i_ < s_.size() && s_[i_] == '.') return false;  // float
     ws();
+    if (ch(',')) {
+      // time range: the row over the covering views, OR-folded
+      std::string from, to;
+      if (!scan_range(s_, i_, from, to)) return false;
+      auto rt = ranges_.find(range_key(field, from, to));
+      if (rt == ranges_.end() || rt->second.empty()) return false;
+      bool first = true;
+      for (int slot : rt->second) {
+        if (slot < 0 || slot >= int(views_.size())) return false;
+        const int k = leaf_of(slot, views_[slot].dense(row));
+        if (k < 0 || ++depth_ > MAXDEPTH) return false;
+        if (!emit(uint8_t(k))) return false;
+        if (!first) {
+          if (!emit(OP_OR)) return false;
+          depth_--;
+        }
+        first = false;
+      }
+      return true;
+    }
     if (!ch(')')) return false;
     auto it = fields_.find(field);
     if (it == fields_.end()) return false;
     const int slot = it->second;
-    const int64_t d = views_[slot].dense(row);
-    int k = -1;
-    for (int x = 0; x < nleaf_; x++)
-      if (outp_->leaf_view[x] == slot && outp_->leaf_row[x] == d) k = x;
-    if (k < 0) {
-      if (nleaf_ >= MAXLEAF) return false;
-      k = nleaf_++;
-      outp_->leaf_view[k] = slot;
-      outp_->leaf_row[k] = d;
-    }
-    if (++depth_ > MAXDEPTH) return false;
+    const int k = leaf_of(slot, views_[slot].dense(row));
+    if (k < 0 || ++depth_ > MAXDEPTH) return false;
     return emit(uint8_t(k));
   }
 
@@ -294,7 +396,7 @@ static bool is_flat(const QueryProg& p) {
 
 py::object plan_count_text(const std::string& text, const std::unordered_map<std::string, int>& fields,
                            const std::vector<py::array_t<uint64_t, py::array::c_style | py::array::forcecast>>& dirs,
-                           bool use_and2, bool use_union, int nthreads) {
+                           bool use_and2, bool use_union, int nthreads, const RangeMap& ranges) {
   std::vector<View> views;
   views.reserve(dirs.size());
   for (const auto& d : dirs) {
@@ -306,6 +408,9 @@ py::object plan_count_text(const std::string& text, const std::unordered_map<std
   }
   for (const auto& kv : fields)
     if (kv.second < 0 || kv.second >= int(views.size())) throw std::out_of_range("field slot out of range");
+  for (const auto& kv : ranges)
+    for (int slot : kv.second)
+      if (slot < 0 || slot >= int(views.size())) throw std::out_of_range("range view slot out of range");
   std::vector<QueryProg> progs;
   std::vector<int> kind;
   bool ok = true;
@@ -325,9 +430,14 @@ py::object plan_count_text(const std::string& text, const std::unordered_map<std
         bool seen = false;
         for (; i < n; i++) {
           const char c = text[i];
-          if (c == '"' || c == '\'') {  // quoted strings: never in the native subset
-            ok = false;
-            break;
+          if (c == '"' || c == '\'') {  // quoted (time values): parentheses inside do not count
+            const size_t e = text.find(c, i + 1);
+            if (e == std::string::npos) {
+              ok = false;
+              break;
+            }
+            i = e;
+            continue;
           }
           if (c == '(') depth++, seen = true;
           else if (c == ')' && --depth == 0) {
@@ -354,7 +464,7 @@ py::object plan_count_text(const std::string& text, const std::unordered_map<std
       auto work = [&](size_t lo, size_t hi) {
         for (size_t q = lo; q < hi; q++) {
           Compiler c(std::string_view(text).substr(calls[q].first, calls[q].second - calls[q].first), fields, views,
-                     progs[q]);
+                     progs[q], ranges);
           good[q] = c.run() ? 1 : 0;
         }
       };
@@ -497,10 +607,72 @@ std::vector<std::string> count_text_fields(const std::string& text) {
     while (j < n && (std::isalnum(static_cast<unsigned char>(text[j])) || text[j] == '_' || text[j] == '-')) j++;
     if (j == f0) continue;
     std::string f = text.substr(f0, j - f0);
+    // a time-range Row (`f=<id>, from=..`) needs its covering views, not the
+    // standard view: count_text_ranges lists it
+    size_t k = j;
+    skip_ws(text, k);
+    if (k < n && text[k] == '=') {
+      k++;
+      skip_ws(text, k);
+      while (k < n && std::isdigit(static_cast<unsigned char>(text[k]))) k++;
+      skip_ws(text, k);
+      if (k < n && text[k] == ',') {
+        i = j;
+        continue;
+      }
+    }
     bool seen = false;
     for (const auto& x : out) seen = seen || x == f;
     if (!seen) out.push_back(std::move(f));
     i = j;
+  }
+  return out;
+}
+
+// Distinct (field, from, to) of the time-range Row leaves of a request, in
+// first-seen order; from / to are None when not given.  The caller maps
+// each to its covering views (plan_count_text's `ranges`, keyed by
+// range_key with "\x01" for an absent bound).
+py::list count_text_ranges(const std::string& text) {
+  py::list out;
+  std::vector<std::string> seen;
+  const std::string_view s(text);
+  const size_t n = s.size();
+  for (size_t i = 0; i + 4 < n; i++) {
+    if (s[i] != 'R' || s.compare(i, 3, "Row") != 0) continue;
+    if (i > 0 && (std::isalnum(static_cast<unsigned char>(s[i - 1])) || s[i - 1] == '_')) continue;
+    size_t j = i + 3;
+    skip_ws(s, j);
+    if (j >= n || s[j] != '(') continue;
+    j++;
+    skip_ws(s, j);
+    const size_t f0 = j;
+    while (j < n && (std::isalnum(static_cast<unsigned char>(s[j])) || s[j] == '_' || s[j] == '-')) j++;
+    if (j == f0) continue;
+    const std::string field(s.substr(f0, j - f0));
+    size_t k = j;
+    skip_ws(s, k);
+    if (k >= n || s[k] != '=') continue;
+    k++;
+    skip_ws(s, k);
+    const size_t d0 = k;
+    while (k < n && std::isdigit(static_cast<unsigned char>(s[k]))) k++;
+    if (k == d0) continue;
+    skip_ws(s, k);
+    if (k >= n || s[k] != ',') continue;
+    k++;
+    std::string from, to;
+    if (!scan_range(s, k, from, to)) continue;
+    const std::string key = range_key(field, from, to);
+    bool dup = false;
+    for (const auto& x : seen) dup = dup || x == key;
+    if (!dup) {
+      seen.push_back(key);
+      py::object pf = from == std::string(1, kAbsent) ? py::object(py::none()) : py::object(py::str(from));
+      py::object pt = to == std::string(1, kAbsent) ? py::object(py::none()) : py::object(py::str(to));
+      out.append(py::make_tuple(field, pf, pt));
+    }
+    i = k - 1;
   }
   return out;
 }
@@ -512,8 +684,11 @@ void register_compile(py::module_& m) {
         "Compile a request of top-level Count(<Row/Intersect/Union/Difference/Xor tree>) calls straight to "
         "QueryProg records; (progs uint8[Q*256], Q), or None when a call needs the general path");
   m.def("count_text_fields", &count_text_fields, py::arg("text"));
+  m.def("count_text_ranges", &count_text_ranges, py::arg("text"),
+        "Distinct (field, from, to) of the time-range Row(f=<id>, from=, to=) leaves of a request");
   m.def("plan_count_text", &plan_count_text, py::arg("text"), py::arg("fields"), py::arg("dirs"),
         py::arg("use_and2") = true, py::arg("use_union") = true, py::arg("nthreads") = 4,
+        py::arg("ranges") = RangeMap{},
         "Compile + classify + order a request of Count() calls into one H2D-ready buffer; "
         "(Q, [(kind, n, progs_off, order_off)], buf) or None");
   m.def("compile_counts", &compile_counts, py::arg("queries"), py::arg("fields"), py::arg("dirs"),

@@ -463,6 +463,7 @@ static py::tuple topn_replay(I64Arr cand_rows, I64Arr cand_cnts,
 }
 
 void register_arena_io(py::module_& m);  // arena_io.cpp
+void register_wire_decode(py::module_& m);  // wire_decode.cpp
 
 PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
   m.attr("ROARING_STATS") = pr::STATS_ENABLED;
@@ -764,4 +765,5 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
         py::arg("seed") = 1, py::arg("nthreads") = 8);
   m.def("arena_shard_bitmap", &arena_shard_bitmap);
   register_arena_io(m);
+  register_wire_decode(m);
 }

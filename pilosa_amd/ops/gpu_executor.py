@@ -519,14 +519,16 @@ class GpuExecutor:
             if dv is None:
                 return None
             views[name] = dv
-        if not views:
-            return None
         vlist = list(views.values())
+        fields = {n: i for i, n in enumerate(views)}
+        ranges = self._text_ranges(idx, index, text, shards, vlist) if ("from" in text or "to" in text) else {}
+        if ranges is None or not vlist:
+            return None
         eng = self.engine
         use_and2 = eng.use_and2 and max(v.container_count for v in vlist) < 0xFFFFFFFF
         # rows absent from a view compile to dense -1 (empty leaf)
-        got = _pql.plan_count_text(text, {n: i for i, n in enumerate(views)}, [v.rows for v in vlist],
-                                   use_and2, eng.use_union, self.plan_threads)
+        got = _pql.plan_count_text(text, fields, [v.rows for v in vlist], use_and2, eng.use_union, self.plan_threads,
+                                   ranges)
         if got is None:
             return None
         Q, segs, buf = got
@@ -535,6 +537,43 @@ class GpuExecutor:
         # device_out: the int64[Q] device tensor, still being computed (the
         # caller reduces it on the device, e.g. the mesh all-reduce)
         return out if device_out else eng.to_host(out).tolist()
+
+    def _text_ranges(self, idx, index: str, text: str, shards: List[int], vlist: List[DeviceView]):
+        """The time-range Row(t=<id>, from=, to=) leaves of a request text
+        (native scan), each resolved to the slots of its covering views'
+        arenas, which are appended to ``vlist`` (executor time_views ->
+        views_by_time_range, time.go:104-181).  {range key: [slots]} for
+        plan_count_text, or None when a range needs the general path."""
+        from pilosa_amd import _pql
+        from pilosa_amd.models.field import FIELD_TYPE_TIME
+        from pilosa_amd.pql.ast import Call
+        out: Dict[str, List[int]] = {}
+        slot_of: Dict[Tuple[str, str], int] = {}
+        ex = self._ex()
+        for fname, fr, to in _pql.count_text_ranges(text):
+            f = idx.field(fname)
+            if f is None or f.type != FIELD_TYPE_TIME or f.options.keys:
+                return None
+            args = {k: v for k, v in (("from", fr), ("to", to)) if v is not None}
+            try:
+                vnames = ex.time_views(f, Call("Row", args))
+            except Exception:  # noqa: BLE001 - malformed times: the general path reports them
+                return None
+            if not vnames:
+                return None
+            slots = []
+            for v in vnames:
+                if (fname, v) not in slot_of:
+                    dv = self.view_arena(index, fname, v, shards)
+                    if dv is None:
+                        continue
+                    slot_of[(fname, v)] = len(vlist)
+                    vlist.append(dv)
+                slots.append(slot_of[(fname, v)])
+            if not slots:
+                return None
+            out[f"{fname}\x1f{chr(1) if fr is None else fr}\x1f{chr(1) if to is None else to}"] = slots
+        return out
 
     TIME_GROUP_MIN = 2
 
@@ -584,7 +623,7 @@ class GpuExecutor:
             rows = np.array([rid for _, rid, _ in members], dtype=np.uint64)
             progs = GpuEngine.union_programs(np.stack([dv.dense_many(rows) for dv in dvs], axis=1))
             self.launches += 1
-            got = self.engine.launch_count(self.engine.prepare_progs(progs, dvs, dvs[0].S)).cpu().tolist()
+            got = self.engine.to_host(self.engine.launch_count(self.engine.prepare_progs(progs, dvs, dvs[0].S))).tolist()
             for (i, _, _), v in zip(members, got):
                 out[i] = int(v)
         return out

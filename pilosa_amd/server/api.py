@@ -223,22 +223,25 @@ class API:
         f = idx.field(field)
         if f is None:
             raise NotFoundError(ErrFieldNotFound)
-        row_ids, col_ids = list(row_ids), list(col_ids)
+        # numpy arrays (the native request decoder) stay arrays on the id path
+        row_ids = row_ids if isinstance(row_ids, np.ndarray) else list(row_ids)
+        col_ids = col_ids if isinstance(col_ids, np.ndarray) else list(col_ids)
         if not ignore_key_check:
             if f.keys():
-                if row_ids:
+                if len(row_ids):
                     raise BadRequestError("row ids cannot be used because field uses string keys")
                 row_ids = self.holder.translate.translate_rows_to_uint64(index, field, list(row_keys))
             if idx.keys:
-                if col_ids:
+                if len(col_ids):
                     raise BadRequestError("column ids cannot be used because index uses string keys")
                 col_ids = self.holder.translate.translate_columns_to_uint64(index, list(col_keys))
             if idx.keys or f.keys():
+                row_ids, col_ids = [int(x) for x in row_ids], [int(x) for x in col_ids]
                 by_shard: Dict[int, List[int]] = {}
                 for i, c in enumerate(col_ids):
                     by_shard.setdefault(c // SHARD_WIDTH, []).append(i)
                 for s, ii in sorted(by_shard.items()):
-                    ts = [timestamps[i] for i in ii] if timestamps else []
+                    ts = [int(timestamps[i]) for i in ii] if len(timestamps) else []
                     self._route_import(index, field, s, [row_ids[i] for i in ii], [col_ids[i] for i in ii], ts,
                                        clear)
                 return
@@ -257,12 +260,12 @@ class API:
     def _local_import(self, idx, f, rows, cols, timestamps, clear):
         import datetime as dt
         if len(cols) and self._mesh_route(idx.name, f.name, "bits", int(cols[0]) // SHARD_WIDTH,
-                                          {"rows": list(rows), "cols": list(cols), "clear": clear,
+                                          {"rows": rows, "cols": cols, "clear": clear,
                                            "timestamps": _ts_list(timestamps)}):
             return
         tss = None
-        if timestamps and any(timestamps):
-            tss = [dt.datetime.utcfromtimestamp(t / 1e9) if t else None for t in timestamps]
+        if len(timestamps) and np.any(np.asarray(timestamps, dtype=np.int64) != 0):
+            tss = [dt.datetime.utcfromtimestamp(t / 1e9) if t else None for t in np.asarray(timestamps).tolist()]
         if not clear and idx.existence_field() is not None and len(cols):
             idx.existence_field().import_bits(np.zeros(len(cols), np.uint64), np.asarray(cols, np.uint64))
         f.import_bits(rows, cols, tss, clear=clear)
@@ -274,10 +277,10 @@ class API:
         f = idx.field(field)
         if f is None:
             raise NotFoundError(ErrFieldNotFound)
-        col_ids = list(col_ids)
-        values = list(values)
+        col_ids = col_ids if isinstance(col_ids, np.ndarray) else list(col_ids)
+        values = values if isinstance(values, np.ndarray) else list(values)
         if not ignore_key_check and idx.keys:
-            if col_ids:
+            if len(col_ids):
                 raise BadRequestError("column ids cannot be used because index uses string keys")
             col_ids = self.holder.translate.translate_columns_to_uint64(index, list(col_keys))
             by_shard: Dict[int, List[int]] = {}
@@ -297,7 +300,7 @@ class API:
 
     def _local_import_values(self, idx, f, cols, vals, clear):
         if len(cols) and self._mesh_route(idx.name, f.name, "values", int(cols[0]) // SHARD_WIDTH,
-                                          {"cols": list(cols), "values": list(vals), "clear": clear}):
+                                          {"cols": cols, "values": vals, "clear": clear}):
             return
         if not clear and idx.existence_field() is not None and len(cols):
             idx.existence_field().import_bits(np.zeros(len(cols), np.uint64), np.asarray(cols, np.uint64))
@@ -447,6 +450,6 @@ class API:
 def _ts_list(timestamps):
     """Import timestamps (ns since epoch) -> datetimes, as Field.import_bits takes."""
     import datetime as dt
-    if not timestamps or not any(timestamps):
+    if timestamps is None or not len(timestamps) or not np.any(np.asarray(timestamps, dtype=np.int64) != 0):
         return None
-    return [dt.datetime.utcfromtimestamp(t / 1e9) if t else None for t in timestamps]
+    return [dt.datetime.utcfromtimestamp(t / 1e9) if t else None for t in np.asarray(timestamps).tolist()]

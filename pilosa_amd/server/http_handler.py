@@ -17,6 +17,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Callable, Dict, List, Optional, Tuple
 from urllib.parse import parse_qs, urlparse
 
+from pilosa_amd import _roaring
 from pilosa_amd.errors import (APIMethodNotAllowedError, BadRequestError, ConflictError, ErrClusterDoesNotOwnShard,
                                ErrFieldNotFound, ErrFragmentNotFound, ErrIndexNotFound, ErrTooManyWrites,
                                NotFoundError, PilosaError)
@@ -340,16 +341,18 @@ class Handler:
         except PilosaError as e:
             raise HTTPError(404 if isinstance(e, NotFoundError) else 500, str(e))
         try:
+            # packed id / value lists decoded natively straight into numpy
+            # (native/wire_decode.cpp), not through protobuf repeated fields
+            try:
+                m = _roaring.decode_import_request(req.body, f.type == "int")
+            except RuntimeError as e:
+                raise HTTPError(400, f"decoding request: {e}")
             if f.type == "int":
-                m = pb.ImportValueRequest()
-                m.ParseFromString(req.body)
-                self.api.import_values(index, field, m.Shard, list(m.ColumnIDs), list(m.Values), list(m.ColumnKeys),
+                self.api.import_values(index, field, m["Shard"], m["ColumnIDs"], m["Values"], m["ColumnKeys"],
                                        clear=clear, ignore_key_check=ignore)
             else:
-                m = pb.ImportRequest()
-                m.ParseFromString(req.body)
-                self.api.import_bits(index, field, m.Shard, list(m.RowIDs), list(m.ColumnIDs), list(m.RowKeys),
-                                     list(m.ColumnKeys), list(m.Timestamps), clear=clear, ignore_key_check=ignore)
+                self.api.import_bits(index, field, m["Shard"], m["RowIDs"], m["ColumnIDs"], m["RowKeys"],
+                                     m["ColumnKeys"], m["Timestamps"], clear=clear, ignore_key_check=ignore)
         except PilosaError as e:
             if str(e) == str(ErrClusterDoesNotOwnShard):
                 raise HTTPError(412, str(e))

@@ -22,3 +22,8 @@ for n in (1, 4):
     print("  topn cache", {k: t.get("cache", {}).get(k) for k in ("qps", "sample_top3", "max_in_flight")},
           "src", {k: t.get("src", {}).get(k) for k in ("qps", "sample_top3", "max_in_flight")}, "verify", t.get("verify"))
 PY
+# pair kernel: v10 (flat stream per staged run) vs v6, correctness + timing
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "and2 or array_size" --timeout 300 --timeout-method thread > $O/pytest_pairs.log 2>&1 || { tail -c 4000 $O/pytest_pairs.log; exit 1; }
+tail -2 $O/pytest_pairs.log
+timeout -k 10 600 python -u scripts/kbench.py --batch 4096 --reps 5 --cq 64 --no-tile --variants 10 > $O/kbench.log 2>&1 || { tail -c 3000 $O/kbench.log; exit 1; }
+tail -3 $O/kbench.log

@@ -126,10 +126,12 @@ def test_and2_pair_kernels_match_tile_kernel(setup):
         exprs.append(Op("and", (Leaf(va, min(a, 5) if va is view2 else a), Leaf(view, b))))
         ra = min(a, 5) if va is view2 else a
         want.append(sum(_row(x, ra).intersection_count(_row(f, b)) for x, f in zip(fa, frags)))
-    for cq in (0, 16, 32, 64):
-        e2 = GpuEngine(view.device)
-        e2.and2_cq = cq
-        np.testing.assert_array_equal(e2.count(exprs), np.array(want))
+    for var in (6, 10):
+        for cq in (0, 16, 32, 64):
+            e2 = GpuEngine(view.device)
+            e2.and2_cq = cq
+            e2.and2_variant = var
+            np.testing.assert_array_equal(e2.count(exprs), np.array(want), err_msg=f"variant {var} cq {cq}")
     old = GpuEngine(view.device)
     old.use_and2 = False
     np.testing.assert_array_equal(old.count(exprs), np.array(want))
@@ -185,8 +187,9 @@ def test_bitgemm_count_matrix_matches_host(mode):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("variant", [6, 10])
 @pytest.mark.parametrize("cq", [16, 32, 64])
-def test_pair_kernel_array_size_boundaries(cq):
+def test_pair_kernel_array_size_boundaries(cq, variant):
     """Array containers of 1, 63, 64, 65, 255, 256, 257 (the small-probe
     boundary), 511, 512, 513 and 4096 values against bitmap, array and run
     rows, each paired once (one-off: the gather / LDS-staged-bitmap branches)
@@ -215,6 +218,7 @@ def test_pair_kernel_array_size_boundaries(cq):
     view = DeviceView.from_bitmaps([frag], dev)
     eng = GpuEngine(dev)
     eng.and2_cq = cq
+    eng.and2_variant = variant
     pairs = []
     for a in range(len(rows)):
         for b in range(len(rows)):

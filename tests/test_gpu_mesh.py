@@ -101,6 +101,10 @@ def _distinct_rows_data():
 def _topn_worker(rank, world, port, outdir):
     import threading
 
+    # rebuild the slot index as soon as the node row space moves (the 10 s
+    # re-rank throttle would send the src batches to the general path)
+    os.environ["PILOSA_TOPN_INDEX_REBUILD_S"] = "0"
+
     import torch.distributed as dist
 
     from pilosa_amd.executor import Executor

@@ -150,3 +150,40 @@ def test_plan_count_text_matches_numpy_planner(views):
     assert seen.all()
     assert _pql.plan_count_text("Count(Row(f=1)) TopN(f)", fields, dirs, True, True, 4) is None
     assert _pql.plan_count_text("Count(Row(f=\"a\"))", fields, dirs, True, True, 4) is None
+
+
+def test_plan_count_text_time_ranges(views):
+    """Time-range Row leaves compile natively into the union of the row over
+    the range's covering views (the slots the caller resolved per distinct
+    (field, from, to)), quoted and bare times, either bound alone, mixed
+    with plain rows; an unresolved range or a malformed one is refused."""
+    from pilosa_amd import _pql
+    from pilosa_amd.ops.device import OP_OR
+    fields = {"f": 0}
+    dirs = [views["f"].rows, views["g"].rows, views["f"].rows, views["g"].rows]
+    text = ("Count(Row(t=3, from='2020-01-01T00:00', to='2020-01-03T05:00')) "
+            "Count(Row(t=9,to=2020-01-02T00:00)) Count(Row(f=4)) "
+            "Count(Intersect(Row(f=2), Row(t=27, from=\"2020-01-01T00:00\", to='2020-01-03T05:00')))")
+    assert _pql.count_text_fields(text) == ["f"]
+    rs = _pql.count_text_ranges(text)
+    assert rs == [("t", "2020-01-01T00:00", "2020-01-03T05:00"), ("t", None, "2020-01-02T00:00")]
+    k1 = "t\x1f2020-01-01T00:00\x1f2020-01-03T05:00"
+    k2 = "t\x1f\x01\x1f2020-01-02T00:00"
+    ranges = {k1: [1, 2, 3], k2: [1]}
+    Q, segs, buf = _pql.plan_count_text(text, fields, dirs, True, True, 1, ranges)
+    assert Q == 4
+    progs = {}
+    for kind, n, po, oo in segs:
+        for p, q in zip(buf[po:po + n * 256].view(QPROG_DTYPE), buf[oo:oo + n * 8].view(np.int64)):
+            progs[int(q)] = (kind, p)
+    kind, p = progs[0]
+    assert kind == 4 and int(p["nleaf"]) == 3 and list(p["prog"][:5]) == [0, 1, OP_OR, 2, OP_OR]
+    assert list(p["leaf_view"][:3]) == [1, 2, 3]
+    assert list(p["leaf_row"][:3]) == [views["g"].dense_many(np.array([3], np.uint64))[0], 3, 0]
+    kind, p = progs[1]
+    assert kind == 1 and int(p["leaf_view"][0]) == 1 and int(p["leaf_row"][0]) == 1   # g row 9 -> dense 1
+    kind, p = progs[3]
+    assert int(p["nleaf"]) == 4 and int(p["nprog"]) == 7   # f2 AND (t27@1 OR t27@2 OR t27@3)
+    assert _pql.plan_count_text(text, fields, dirs, True, True, 1, {k1: [1, 2, 3]}) is None   # k2 unresolved
+    for bad in ("Count(Row(t=3, from='2020-01-01))", "Count(Row(t=3, from=1, from=2))", "Count(Row(t=3, at=1))"):
+        assert _pql.plan_count_text(bad, fields, dirs, True, True, 1, ranges) is None, bad
