@@ -285,10 +285,16 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         return done
 
     l0 = gpu.launches
-    log("topn: cache-only requests")
-    cache_q = [" ".join([f"TopN(f, n={n})"] * B)] * (nb + 1)
-    out["cache"] = {}
+    log("topn: cache-only requests (distinct calls)")
+    # every call of every request distinct: n and threshold vary, so no
+    # phase-2 re-count or candidate set is shared between calls by repetition
+    cache_calls = _distinct_topn_calls(B * (nb + 1))
+    cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
+    out["cache"] = {"calls": "TopN(f, n in {10,50,100,500}, threshold in {1,1000,5000,20000}), all distinct"}
     res_cache = timed(cache_q, out["cache"])
+    log("topn: cache-only requests (the same call repeated, round-3 figure)")
+    out["cache_repeated"] = {}
+    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nb + 1), out["cache_repeated"])
     hot = zipf_rows(rng, B * (nb + 1), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
@@ -340,6 +346,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     if args.verify > 0 and shards:
         sel = sorted(set(np.linspace(0, len(shards) - 1, min(4, len(shards))).astype(int).tolist()))
         calls = [parse_string(f"TopN(f, n={n})").calls[0]] + \
+            [parse_string(c).calls[0] for c in cache_calls[:3]] + \
             [parse_string(c).calls[0] for c in src_calls[B:B + 3]]
         bad = 0
         for si in sel:
@@ -352,11 +359,27 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
                 if dev_pairs != sorted((p.id, p.count) for p in host):
                     bad += 1
         # and the fused batch answers equal the two-phase map/reduce on the device
-        agree = [[(p.id, p.count) for p in r] for r in res_src[-1][:2]] == \
+        agree = [[(p.id, p.count) for p in r] for r in res_src[-1][:2] + res_cache[-1][:4]] == \
             [[(p.id, p.count) for p in ex._topn("i", parse_string(c).calls[0], shards, _exec_opts())]
-             for c in src_calls[nb * B:nb * B + 2]] if world == 1 else None
+             for c in src_calls[nb * B:nb * B + 2] + cache_calls[nb * B:nb * B + 4]] if world == 1 else None
         out["verify"] = {"shards_checked": len(sel), "queries_per_shard": len(calls), "mismatches": bad,
                          "fused_equals_two_phase": agree, "verified": bad == 0 and agree is not False}
+    return out
+
+
+TOPN_NS = (10, 50, 100, 500)
+TOPN_THRESHOLDS = (1, 1000, 5000, 20000)
+
+
+def _distinct_topn_calls(k: int):
+    """k cache-only TopN calls, no two alike within a request: n and
+    threshold cycle through TOPN_NS x TOPN_THRESHOLDS, and the n values get
+    a per-call offset so every (n, threshold) pair differs."""
+    out = []
+    for i in range(k):
+        n = TOPN_NS[i % len(TOPN_NS)] + (i // 16) % 7
+        t = TOPN_THRESHOLDS[(i // len(TOPN_NS)) % len(TOPN_THRESHOLDS)]
+        out.append(f"TopN(f, n={n}, threshold={t})")
     return out
 
 
@@ -1361,9 +1384,10 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
                     "sample_top3": [(p.id, p.count) for p in done[-1][0][:3]] if done[-1] and done[-1][0] else []})
         return done
 
-    log("mesh topn: cache-only requests")
-    out["cache"] = {}
-    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nb + 1), out["cache"])
+    log("mesh topn: cache-only requests (distinct calls)")
+    cache_calls = _distinct_topn_calls(B * (nb + 1))
+    out["cache"] = {"calls": "TopN(f, n in {10,50,100,500}, threshold in {1,1000,5000,20000}), all distinct"}
+    timed([" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nb + 1)], out["cache"])
     hot = zipf_rows(rng, B * (nb + 1), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
@@ -1430,7 +1454,8 @@ def bench_serving(args, base, dev):
                     "verified": len(smp), "mismatches": mism,
                     "first_error": fe[:200].decode(errors="replace") if fe else ""}
         out["count"] = run(queries, args.serve_seconds, 64)
-        mix = [q if k % 10 else "TopN(f, n=100)" for k, q in enumerate(queries[:2000])]
+        tcalls = _distinct_topn_calls(2000)
+        mix = [q if k % 10 else tcalls[k] for k, q in enumerate(queries[:2000])]
         out["count_topn_mix"] = dict(run(mix, max(2.0, args.serve_seconds / 2), 32), topn_fraction=0.1)
         out["conns"] = args.serve_conns
         out["httpd"] = srv.httpd.stats() if hasattr(srv.httpd, "stats") else None

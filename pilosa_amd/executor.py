@@ -326,7 +326,8 @@ class Executor:
         if fn is None:
             return None
         try:
-            res = fn(index, text, shards, device_out=True) if dev_out else fn(index, text, shards)
+            with tracing.span("Executor.countTextNative", shards=len(shards)):
+                res = fn(index, text, shards, device_out=True) if dev_out else fn(index, text, shards)
         except PilosaError:
             raise
         except Exception as err:  # noqa: BLE001 - device fault: general path
@@ -352,7 +353,8 @@ class Executor:
         shards = list(shards) if shards else (idx.available_shards() or [0])
         mesh = self.mesh
         try:
-            return mesh.count_text(index, text, shards)
+            with tracing.span("Executor.meshCountText", shards=len(shards)):
+                return mesh.count_text(index, text, shards)
         except MeshError:
             if not mesh.failed_over:
                 raise
@@ -597,6 +599,10 @@ class Executor:
         """Group shards by owner node; local shards via ``local_fn`` (one
         batched GPU call) or the per-shard ``map_fn``; remote ones via the
         internal client with failover to replicas (executor.go:2458-2518)."""
+        with tracing.span("Executor.mapReduce", call=c.name, shards=len(shards)):
+            return self._map_reduce(index, shards, c, opt, map_fn, reduce_fn, local_fn)
+
+    def _map_reduce(self, index, shards, c, opt, map_fn, reduce_fn, local_fn):
         by_node = self._shards_by_node(index, shards, opt)
         result = None
         # every remote node is queried at once (one request in flight per
@@ -607,8 +613,8 @@ class Executor:
         if not opt.remote:
             for node, nshards in by_node.items():
                 if node is not None and (self.cluster is None or node.id != self.cluster.node.id):
-                    remote.append(self.fanout.submit(self._remote_with_failover, index, c, node, nshards, opt,
-                                                     map_fn, reduce_fn, local_fn, {node.id}))
+                    remote.append(self.fanout.submit(tracing.bind(self._remote_with_failover), index, c, node,
+                                                     nshards, opt, map_fn, reduce_fn, local_fn, {node.id}))
         for node, nshards in by_node.items():
             if node is None or (self.cluster is not None and node.id == self.cluster.node.id):
                 if self._use_mesh(opt):
@@ -620,7 +626,8 @@ class Executor:
                         if not mesh.failed_over:
                             raise
                         # failed over: this process now holds every local shard
-                result = reduce_fn(result, self._map_local(nshards, map_fn, reduce_fn, local_fn))
+                with tracing.span("Executor.mapperLocal", shards=len(nshards)):
+                    result = reduce_fn(result, self._map_local(nshards, map_fn, reduce_fn, local_fn))
         for fut in remote:
             result = reduce_fn(result, fut.result())
         return result
@@ -656,7 +663,8 @@ class Executor:
 
     def _remote_with_failover(self, index, c, node, nshards, opt, map_fn, reduce_fn, local_fn, tried):
         try:
-            results = self.client.query_node(node, index, str(c), nshards)
+            with tracing.span("Executor.remoteExec", node=node.id, shards=len(nshards)):
+                results = self.client.query_node(node, index, str(c), nshards)
             return results[0] if results else None
         except Exception as err:  # noqa: BLE001 - retry on replicas
             result = None
@@ -668,8 +676,8 @@ class Executor:
                 regroup.setdefault(cands[0], []).append(s)
             # the failed node's shards, regrouped by their next replica: those
             # replicas are asked at once as well
-            futs = [self.fanout.submit(self._remote_with_failover, index, c, n2, ss, opt, map_fn, reduce_fn,
-                                       local_fn, tried | {n2.id})
+            futs = [self.fanout.submit(tracing.bind(self._remote_with_failover), index, c, n2, ss, opt, map_fn,
+                                       reduce_fn, local_fn, tried | {n2.id})
                     for n2, ss in regroup.items() if n2.id != self.cluster.node.id]
             for n2, ss in regroup.items():
                 if n2.id == self.cluster.node.id:

@@ -576,8 +576,10 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
 
 constexpr int V10_WIN = 2048;  // chunks per boundary window: 64 dwords, one per lane
 
-template <int CQ>
-__global__ __launch_bounds__(64, 5) void and2_pairs_v10_kernel(const QueryProg* __restrict__ progs, int Q,
+// DBG (cost isolation only, wrong answers): 1 = no probes, 2 = no staging,
+// 3 = no chunk loads, 4 = singletons skipped
+template <int CQ, int PF, int DBG = 0>
+__global__ __launch_bounds__(64, 4) void and2_pairs_v10_kernel(const QueryProg* __restrict__ progs, int Q,
                                                               const ViewDev* __restrict__ views, int S,
                                                               const uint2* __restrict__ pairs,
                                                               int32_t* __restrict__ partial) {
@@ -625,6 +627,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v10_kernel(const QueryProg* 
     const int64_t mA = rl64(ma, i);
     const uint16_t* pA = reinterpret_cast<const uint16_t*>(rl_u64(pal, i));
     const int tA = meta_type(mA);
+    if (DBG == 4 && (run & (run - 1)) == 0) continue;
     if ((run & (run - 1)) == 0) {
       // a pair of its own: v6's shortcuts that need no staging, else stage the smaller array
       const int64_t mB = rl64(mb, i);
@@ -649,7 +652,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v10_kernel(const QueryProg* 
       continue;
     }
     lds_wait();  // previous readers of lb / tbl / cnt are done before they are rewritten
-    stage(lb, pA, mA);
+    if (DBG != 2) stage(lb, pA, mA);
     const bool inrun = (run >> lane) & 1;
     const uint64_t am = __ballot(inrun && tB == CT_ARRAY);
     // bitmap / run partners: one at a time, wave-cooperative
@@ -673,34 +676,68 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v10_kernel(const QueryProg* 
     }
     const int bit0 = int(bm32[0] & 1u);  // hits of a zero-valued pad probe
     int kb = -1, curk = -1, acc = 0;
+#pragma unroll 1
     for (int w0 = 0; w0 < T; w0 += V10_WIN) {
       bnd[lane] = 0u;
       lds_wait();
       if (isArr && start >= w0 && start < w0 + V10_WIN)
         atomicOr(&bnd[(start - w0) >> 5], 1u << (start & 31));
       lds_wait();
+      // the window's boundary words live in a VGPR (lane w = word w): each
+      // iteration takes its 64 bits with two readlanes, no LDS round trip
+      const uint32_t bw = bnd[lane];
       const int wend = min(T, w0 + V10_WIN);
-      for (int b = w0; b < wend; b += 64) {
-        const uint32_t wi = uint32_t(b - w0) >> 5;
-        const uint64_t M = (uint64_t(__builtin_amdgcn_readfirstlane(bnd[wi + 1])) << 32) |
-                           uint32_t(__builtin_amdgcn_readfirstlane(bnd[wi]));
-        const int k = kb + int(mbcnt64(M)) + int((M >> lane) & 1u);
+      const int iters = (wend - w0 + 63) >> 6;
+      // software pipeline: the mapping and chunk load of iteration it+PF are
+      // issued before iteration it's chunk is probed (PF register slots,
+      // statically indexed by unrolling the slot loop)
+      auto fetch = [&](int it, uint4& v, int& k, int& rem) {
+        const uint64_t M = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(bw), 2 * it + 1))) << 32) |
+                           uint32_t(__builtin_amdgcn_readlane(int(bw), 2 * it));
+        k = kb + int(mbcnt64(M)) + int((M >> lane) & 1u);
         kb += __popcll(M);
-        const int t = b + lane;
+        const int t = w0 + it * 64 + lane;
+        v = make_uint4(0, 0, 0, 0);
+        rem = -1;
         if (t < wend) {
           const uint4 e = tbl[k];
           const int c = t - int(e.z);
-          const auto p4 = gp(reinterpret_cast<const uint4*>((uint64_t(e.y) << 32) | e.x));
-          const uint4 v4 = p4[c];
-          const int rem = int(e.w) - c * 8;
-          int cc = probe8<true>(bm32, v4);
-          if (rem < 8) cc -= bit0 * (8 - rem);
-          if (k != curk) {
-            if (curk >= 0) atomicAdd(&cnt[curk], acc);
-            curk = k;
-            acc = cc;
-          } else {
-            acc += cc;
+          if (DBG == 3)
+            v = make_uint4(uint32_t(c) * 0x10001u, e.x, e.y, uint32_t(t));
+          else
+            v = gp(reinterpret_cast<const uint4*>((uint64_t(e.y) << 32) | e.x))[c];
+          rem = int(e.w) - c * 8;
+        }
+      };
+      uint4 bv[PF];
+      int bk[PF], brem[PF];
+#pragma unroll
+      for (int sl = 0; sl < PF; sl++) {
+        bk[sl] = -1;
+        brem[sl] = -1;
+        bv[sl] = make_uint4(0, 0, 0, 0);
+        if (sl < iters) fetch(sl, bv[sl], bk[sl], brem[sl]);
+      }
+#pragma unroll 1
+      for (int it0 = 0; it0 < iters; it0 += PF) {
+#pragma unroll
+        for (int sl = 0; sl < PF; sl++) {
+          const int it = it0 + sl;
+          if (it >= iters) break;
+          const uint4 cv = bv[sl];
+          const int ck = bk[sl], crem = brem[sl];
+          brem[sl] = -1;
+          if (it + PF < iters) fetch(it + PF, bv[sl], bk[sl], brem[sl]);
+          if (crem >= 0) {
+            int cc = DBG == 1 ? int(cv.x ^ cv.y ^ cv.z ^ cv.w) & 7 : probe8<true>(bm32, cv);
+            if (crem < 8) cc -= bit0 * (8 - crem);
+            if (ck != curk) {
+              if (curk >= 0) atomicAdd(&cnt[curk], acc);
+              curk = ck;
+              acc = cc;
+            } else {
+              acc += cc;
+            }
           }
         }
       }
@@ -713,6 +750,17 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v10_kernel(const QueryProg* 
 }
 }  // namespace
 
+template <int CQ>
+void launch_v10_dbg(int dbg, int64_t wv, const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs,
+                    int32_t* partial, hipStream_t st) {
+  switch (dbg) {
+    case 1: hipLaunchKernelGGL((and2_pairs_v10_kernel<CQ, 2, 1>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 2: hipLaunchKernelGGL((and2_pairs_v10_kernel<CQ, 2, 2>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 3: hipLaunchKernelGGL((and2_pairs_v10_kernel<CQ, 2, 3>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    default: hipLaunchKernelGGL((and2_pairs_v10_kernel<CQ, 2, 4>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+  }
+}
+
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st) {
   const int64_t n = int64_t(S) * v.D;
   if (n == 0) return;
@@ -721,7 +769,8 @@ void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st
 
 // pair_build then the pair kernel; `cq` = queries per wave (16 / 32 / 64; <= 0
 // picks by batch size: 32 for Q <= 2048, 64 above).  `variant` 10 runs the
-// flat-stream kernel (and2_pairs_v10), anything else v6.
+// flat-stream kernel (and2_pairs_v10) with 1 chunk prefetched, 11 / 12 with 2
+// / 3, anything else v6.
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
                        int cq, int variant, hipStream_t st) {
   const int64_t items = int64_t(Q) * S;
@@ -734,8 +783,16 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   {                                                                                                          \
     const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                        \
     if (variant == 10)                                                                                       \
-      hipLaunchKernelGGL(and2_pairs_v10_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, \
-                         pairs, partial);                                                                    \
+      hipLaunchKernelGGL((and2_pairs_v10_kernel<CQV, 1>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, \
+                         S, pairs, partial);                                                                 \
+    else if (variant == 11)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v10_kernel<CQV, 2>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, \
+                         S, pairs, partial);                                                                 \
+    else if (variant == 12)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v10_kernel<CQV, 3>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, \
+                         S, pairs, partial);                                                                 \
+    else if (variant >= 21 && variant <= 24)                                                                 \
+      launch_v10_dbg<CQV>(variant - 20, wv, progs, Q, views, S, pairs, partial, st);                         \
     else                                                                                                     \
       hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
                          pairs, partial);                                                                    \

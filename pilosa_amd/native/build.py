@@ -115,7 +115,7 @@ def build_translate(force: bool = False, verbose: bool = False) -> str:
 
 
 HOST_MODULES = {
-    "_roaring": ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp", "mapped.cpp"),
+    "_roaring": ("roaring.cpp", "pyroaring.cpp", "arena_io.cpp", "mapped.cpp", "wire_decode.cpp"),
     "_pql": ("pql_parser.cpp", "pql_compile.cpp"),
     "_httpd": ("httpd.cpp",),
     "_translate": ("translate.cpp",),

@@ -295,6 +295,32 @@ def drive_arena(m, rng: random.Random):
                 bm.count()
             except Exception:  # noqa: BLE001
                 pass
+        # the import-request decoder over valid, truncated and mutated bodies
+        # (hand-encoded ImportRequest: packed and unpacked ids, keys, unknown fields)
+        def varint(v):
+            out = bytearray()
+            while True:
+                b7 = v & 0x7F
+                v >>= 7
+                out.append(b7 | (0x80 if v else 0))
+                if not v:
+                    return bytes(out)
+
+        def field(fn, wt, payload):
+            return varint(fn << 3 | wt) + (varint(len(payload)) + payload if wt == 2 else payload)
+        ids = b"".join(varint(rng.randrange(1 << 40)) for _ in range(500))
+        body = (field(1, 2, b"i") + field(2, 2, b"f") + field(3, 0, varint(7)) + field(4, 2, ids) +
+                field(5, 2, ids) + field(5, 0, varint(3)) + field(7, 2, b"key") + field(9, 0, varint(1)) +
+                field(6, 2, b"".join(varint((1 << 64) - 5) for _ in range(3))))
+        got = m.decode_import_request(body)
+        assert got["Shard"] == 7 and len(got["RowIDs"]) == 500 and len(got["ColumnIDs"]) == 501
+        for k in range(300):
+            b = body[:rng.randrange(len(body))] if k % 2 else mutate(rng, body, 4)
+            for vals in (False, True):
+                try:
+                    m.decode_import_request(b, vals)
+                except Exception:  # noqa: BLE001 - RuntimeError is the contract
+                    pass
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -311,9 +337,13 @@ def drive_pql(m, rng: random.Random):
               "Count(Row(f > 10))", "Count(Row(-5 < f < 10))", "Row(f=1, from='2018-01-01T00:00', to='2019-01-01T00:00')",
               "Rows(f, previous=10, limit=5)", "GroupBy(Rows(f), Rows(g), limit=3)", "Options(Count(Row(f=1)), shards=[0,1])",
               "Count(Intersect(Row(f=1), Row(f=1)))", "Sum(Row(f=1), field=v)", "Count(Shift(Row(f=1), n=2))"]
+    corpus += ["Count(Row(t=3, from='2020-01-01T00:00', to='2020-01-03T05:00')) Count(Row(t=4, to=2020-01-02))",
+               "Count(Intersect(Row(f=2), Row(t=9, from=\"2020-01-01T00:00\")))"]
     fields = {"f": 0, "g": 1}
     dirs = [np.array(sorted(rng.sample(range(1000), 300)), np.uint64),
             np.array(sorted(rng.sample(range(1000), 200)), np.uint64)]
+    ranges = {"t\x1f2020-01-01T00:00\x1f2020-01-03T05:00": [0, 1], "t\x1f\x01\x1f2020-01-02": [1],
+              "t\x1f2020-01-01T00:00\x1f\x01": [0]}
     texts = list(corpus)
     for _ in range(600):
         texts.append(mutate(rng, rng.choice(corpus).encode(), 5).decode("latin-1"))
@@ -325,8 +355,9 @@ def drive_pql(m, rng: random.Random):
                           for _ in range(3000)))
 
     def one(t):
-        for fn in (lambda: m.parse_calls(t), lambda: m.count_text_fields(t),
+        for fn in (lambda: m.parse_calls(t), lambda: m.count_text_fields(t), lambda: m.count_text_ranges(t),
                    lambda: m.plan_count_text(t, fields, dirs, True, True, 4),
+                   lambda: m.plan_count_text(t, fields, dirs, True, True, 4, ranges),
                    lambda: m.compile_counts([t, t], fields, dirs),
                    lambda: m.compile_count_text(t, fields, dirs)):
             try:

@@ -20,6 +20,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from pilosa_amd.utils import tracing
+
 MAXLEAF = 16
 MAXPROG = 32
 OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 32, 33, 34, 35
@@ -1114,6 +1116,10 @@ class GpuEngine:
         return partial.view(S, 16, n)
 
     def to_host(self, t):
+        with tracing.span("GpuEngine.d2h", gpu=True):
+            return self._to_host(t)
+
+    def _to_host(self, t):
         """Device tensor -> host tensor through a pinned buffer and an event
         wait.  A plain ``.cpu()`` is a synchronous pageable D2H copy: the HIP
         runtime stages it with blit kernels and holds the stream while it
@@ -1137,6 +1143,10 @@ class GpuEngine:
 
     def launch_count(self, handle):
         """Device half: launch the kernels; returns the device int64[Q] result."""
+        with tracing.span("GpuEngine.launchCount", gpu=True, queries=handle[0], shards=handle[1]):
+            return self._launch_count(handle)
+
+    def _launch_count(self, handle):
         torch = self.torch
         Q, S, tv, parts = handle
         out = torch.zeros(Q, dtype=torch.int64, device=self.device)

@@ -30,6 +30,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from pilosa_amd.errors import PilosaError
+from pilosa_amd.utils import tracing
 from pilosa_amd.models.cache import Pair, sort_pairs
 from pilosa_amd.models.fragment import SHARD_WIDTH, mutation_epoch
 from pilosa_amd.models.index import EXISTENCE_FIELD_NAME
@@ -196,7 +197,8 @@ class GpuExecutor:
                         f.drop_dirty(hit[1].token)
             token = object()  # dirty-row subscription of the new arena
             self._evict_for(key)
-            dv = self._load_cold(frags, shards, token, key) if self.file_loader else None
+            with tracing.span("GpuExecutor.loadView", gpu=True, field=field, view=view, shards=len(shards)):
+                dv = self._load_cold(frags, shards, token, key) if self.file_loader else None
             if dv is None:
                 bms = []
                 for f in frags:
@@ -527,8 +529,9 @@ class GpuExecutor:
         eng = self.engine
         use_and2 = eng.use_and2 and max(v.container_count for v in vlist) < 0xFFFFFFFF
         # rows absent from a view compile to dense -1 (empty leaf)
-        got = _pql.plan_count_text(text, fields, [v.rows for v in vlist], use_and2, eng.use_union, self.plan_threads,
-                                   ranges)
+        with tracing.span("GpuExecutor.planCountText"):
+            got = _pql.plan_count_text(text, fields, [v.rows for v in vlist], use_and2, eng.use_union,
+                                       self.plan_threads, ranges)
         if got is None:
             return None
         Q, segs, buf = got
@@ -918,6 +921,10 @@ class GpuExecutor:
         return self._topn_pairs_path(rc, rv, src, n, ids, threshold)
 
     def topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False):
+        with tracing.span("GpuExecutor.topnBatch", gpu=True, calls=len(calls)):
+            return self._topn_batch(index, calls, shards, defer)
+
+    def _topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False):
         """Whole TopN calls (phase 1, candidate union, ids= re-count, trim to
         n: executor.go:863-903) for a batch of calls over local shards, both
         phases on the device.  Calls of one (field, src shape) share launches:

@@ -32,6 +32,8 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
+from pilosa_amd.utils import tracing
+
 
 class CommError(RuntimeError):
     """A collective failed or timed out; the mesh must fail over."""
@@ -66,6 +68,13 @@ class Comm:
             raise CommError(f"communicator broken: {self.broken}")
         self.calls += 1
         try:
+            if tracing.enabled():
+                # one span per collective; RCCL ones are HIP-event timed (the
+                # collective kernel on the device), async ones time the issue
+                dev = self.device.type == "cuda" and not self.host_copies and kw.get("group") is not self.ctrl
+                with tracing.span(f"Comm.{getattr(fn, '__name__', 'op')}", gpu=dev and not kw.get("async_op"),
+                                  ranks=self.world, control=kw.get("group") is self.ctrl):
+                    return fn(*a, **kw)
             return fn(*a, **kw)
         except Exception as e:  # noqa: BLE001 - timeouts / peer loss surface here
             self.broken = e

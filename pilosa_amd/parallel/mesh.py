@@ -46,6 +46,7 @@ from __future__ import annotations
 import threading
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
+from pilosa_amd.utils import tracing
 
 
 class MeshError(RuntimeError):
@@ -56,6 +57,10 @@ class MeshError(RuntimeError):
 (OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS, OP_COUNT_TEXT,
  OP_ERRORS, OP_TOPN, OP_SYNC, OP_RECALC) = range(14)
 MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
+_OP_NAMES = {OP_STOP: "stop", OP_COUNT: "count", OP_CALL: "call", OP_WRITE: "write", OP_IMPORT: "import",
+             OP_SCHEMA: "schema", OP_DEL_INDEX: "deleteIndex", OP_DEL_FIELD: "deleteField", OP_SHARDS: "shards",
+             OP_COUNT_TEXT: "countText", OP_ERRORS: "errors", OP_TOPN: "topn", OP_SYNC: "sync",
+             OP_RECALC: "recalculateCaches"}
 
 
 def _raise_remote(parts):
@@ -128,12 +133,12 @@ class ShardMesh:
 
         if not self.is_frontend:
             raise MeshError("only rank 0 issues mesh commands")
-        with self.lock:
+        with self.lock, tracing.span(f"Mesh.{_OP_NAMES.get(op, op)}"):
             if self.failed_over:
                 raise MeshError(f"mesh failed over: {self.failover_error}")
             self.ops += 1
             try:
-                self.comm.bcast_bytes(op, encode(list(args)))
+                self.comm.bcast_bytes(op, encode([tracing.context()] + list(args)))
                 return self._dispatch(op, list(args))
             except CommError as e:
                 self.failover(e)
@@ -167,14 +172,14 @@ class ShardMesh:
         if not self.is_frontend:
             raise MeshError("only rank 0 issues mesh commands")
         q = text.count("Count(")
-        with self.lock:
+        with self.lock, tracing.span("Mesh.countTextIssue", calls=q):
             if self.failed_over:
                 raise MeshError(f"mesh failed over: {self.failover_error}")
             self.ops += 1
             self.seq += 1
             seq = self.seq
             try:
-                self.comm.bcast_bytes(OP_COUNT_TEXT, encode([index, text, list(shards), q, seq]))
+                self.comm.bcast_bytes(OP_COUNT_TEXT, encode([tracing.context(), index, text, list(shards), q, seq]))
                 t, work = self._count_text_issue(index, text, list(shards), q, seq)
             except CommError as e:
                 self.failover(e)
@@ -182,8 +187,9 @@ class ShardMesh:
             self.in_flight += 1
             self.max_in_flight = max(self.max_in_flight, self.in_flight)
         try:
-            self.comm.wait(work)
-            out = self._host_list(t)
+            with tracing.span("Mesh.countTextWait", gpu=True):
+                self.comm.wait(work)
+                out = self._host_list(t)
         except CommError as e:
             with self.lock:
                 self.failover(e)
@@ -210,7 +216,7 @@ class ShardMesh:
             if self.failed_over:
                 raise MeshError(f"mesh failed over: {self.failover_error}")
             try:
-                self.comm.bcast_bytes(op, encode(list(args)))
+                self.comm.bcast_bytes(op, encode([tracing.context()] + list(args)))
                 mine = self._errors.pop(int(args[0]), None) if op == OP_ERRORS else None
                 return self._gather(mine)
             except CommError as e:
@@ -238,12 +244,13 @@ class ShardMesh:
 
         if not self.is_frontend:
             raise MeshError("only rank 0 issues mesh commands")
-        with self.lock:
+        name = _OP_NAMES.get(op, op)
+        with self.lock, tracing.span(f"Mesh.{name}Issue"):
             if self.failed_over:
                 raise MeshError(f"mesh failed over: {self.failover_error}")
             self.ops += 1
             try:
-                self.comm.bcast_bytes(op, encode(list(args)))
+                self.comm.bcast_bytes(op, encode([tracing.context()] + list(args)))
                 h = self._issue(op, list(args))
             except CommError as e:
                 self.failover(e)
@@ -251,7 +258,8 @@ class ShardMesh:
             self.in_flight += 1
             self.max_in_flight = max(self.max_in_flight, self.in_flight)
         try:
-            return resolve(h)
+            with tracing.span(f"Mesh.{name}Complete", gpu=True):
+                return resolve(h)
         except CommError as e:
             with self.lock:
                 self.failover(e)
@@ -357,22 +365,27 @@ class ShardMesh:
                 while self._pending:
                     self._pending.popleft().wait()
                 return
-            if op in (OP_COUNT_TEXT, OP_CALL, OP_TOPN):
-                args = decode(payload) or []
-                if op == OP_COUNT_TEXT:
-                    index, text, shards, q, seq = args
-                    t, work = self._count_text_issue(index, text, shards, q, seq)
-                    from .collectives import Pending
-                    h = Pending(self.comm, work, lambda: None, keep=t)
-                else:
-                    h = self._issue(op, args)
-                if hasattr(h, "wait"):
-                    # keep tensors alive until their collective is done; bound the queue
-                    self._pending.append(h)
-                while self._pending and (len(self._pending) > MAX_IN_FLIGHT or self._pending[0].done()):
-                    self._pending.popleft().wait()
-                continue
-            self._dispatch(op, decode(payload) or [])
+            args = decode(payload) or [""]
+            ctx, args = args[0], args[1:]
+            with tracing.remote_parent(ctx), tracing.span(f"Mesh.serve.{_OP_NAMES.get(op, op)}", rank=self.rank):
+                self._serve_one(op, args)
+
+    def _serve_one(self, op: int, args: list):
+        if op not in (OP_COUNT_TEXT, OP_CALL, OP_TOPN):
+            self._dispatch(op, args)
+            return
+        if op == OP_COUNT_TEXT:
+            from .collectives import Pending
+            index, text, shards, q, seq = args
+            t, work = self._count_text_issue(index, text, shards, q, seq)
+            h = Pending(self.comm, work, lambda: None, keep=t)
+        else:
+            h = self._issue(op, args)
+        if hasattr(h, "wait"):
+            # keep tensors alive until their collective is done; bound the queue
+            self._pending.append(h)
+        while self._pending and (len(self._pending) > MAX_IN_FLIGHT or self._pending[0].done()):
+            self._pending.popleft().wait()
 
     # ------------------------------------------------------------ all ranks
     def _dispatch(self, op: int, args: list):

@@ -566,10 +566,12 @@ class Handler:
 
     def debug_traces(self, req):
         t = tracing.global_tracer()
+        tid = req.query.get("trace")
+        if tid and hasattr(t, "tree"):
+            req.send_json(t.tree(tid, wait=False))   # one trace as a span tree
+            return
         spans = getattr(t, "spans", [])
-        req.send_json([{"name": s.name, "trace": s.trace_id, "span": s.span_id, "parent": s.parent_id,
-                        "ms": round(s.duration * 1000, 3), "tags": {k: str(v) for k, v in s.tags.items()}}
-                       for s in spans[-1000:]])
+        req.send_json([s.to_dict(wait=False) for s in spans[-1000:]])
 
     def debug_pprof(self, req):
         from pilosa_amd.utils import pprof
