@@ -241,7 +241,8 @@ class Executor:
         self._topn_coalescer = None
         self.topn_batch_declined = 0
         self.max_writes = max_writes
-        self.stats = stats
+        # per-call counters go to the holder's client unless given one (executor.go:298-340)
+        self.stats = stats if stats is not None else getattr(holder, "stats", None)
         self.pool = cf.ThreadPoolExecutor(max_workers=max(1, workers), thread_name_prefix="shard")
 
     def close(self):
@@ -858,6 +859,8 @@ class Executor:
         if views is None:
             frag = self.holder.fragment(index, fname, VIEW_STANDARD, shard)
             return frag.row(rid) if frag is not None else Row()
+        if f.stats is not None:
+            f.stats.count("range", 1)   # executor.go:1530
         rows = []
         for v in views:
             frag = self.holder.fragment(index, fname, v, shard)
@@ -923,6 +926,8 @@ class Executor:
         frag = self.holder.fragment(index, f.name, VIEW_BSI_PREFIX + f.name, shard)
         if frag is None:
             return Row()
+        if f.stats is not None:
+            f.stats.count("range:bsigroup", 1)   # executor.go:1662
         if kind == "notnull":
             return frag.not_null()
         if kind == "between":
@@ -1504,6 +1509,8 @@ class Executor:
             raise PilosaError("SetRowAttrs() row field 'row' required")
         attrs = {k: v for k, v in c.args.items() if k not in ("_field", "_row")}
         f.row_attr_store.set_attrs(rid, attrs)
+        if f.stats is not None:
+            f.stats.count("SetRowAttrs", 1)   # executor.go:2242
         self._broadcast_call(index, [c], opt)
 
     def _bulk_set_row_attrs(self, index, calls: List[Call], opt):
@@ -1520,7 +1527,10 @@ class Executor:
             attrs = {k: v for k, v in c.args.items() if k not in ("_field", "_row")}
             m.setdefault(fname, {}).setdefault(rid, {}).update(attrs)
         for fname, fm in m.items():
-            self.holder.field(index, fname).row_attr_store.set_bulk_attrs(fm)
+            f = self.holder.field(index, fname)
+            f.row_attr_store.set_bulk_attrs(fm)
+            if f.stats is not None:
+                f.stats.count("SetRowAttrs", 1)   # executor.go:2336
         self._broadcast_call(index, calls, opt)
         return [None] * len(calls)
 
@@ -1533,6 +1543,8 @@ class Executor:
             raise PilosaError("reading SetColumnAttrs() col errs")
         attrs = {k: v for k, v in c.args.items() if k not in ("_col", "field")}
         idx.column_attr_store.set_attrs(col, attrs)
+        if idx.stats is not None:
+            idx.stats.count("SetProfileAttrs", 1)   # executor.go:2390
         self._broadcast_call(index, [c], opt)
 
     # ================================================================ translation

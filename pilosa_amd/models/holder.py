@@ -125,8 +125,10 @@ class Holder:
 
     # ------------------------------------------------------------ indexes
     def _new_index(self, name: str, keys=False, track_existence=True) -> Index:
+        # the index (and its fields, views, fragments) count under "index:<name>" (holder.go:442)
+        st = self.stats.with_tags(f"index:{name}") if self.stats is not None else None
         idx = Index(os.path.join(self.path, name), name, keys=keys, track_existence=track_existence,
-                    max_opn=self.max_opn, stats=self.stats, persistent_attrs=self.persistent_attrs)
+                    max_opn=self.max_opn, stats=st, persistent_attrs=self.persistent_attrs)
         idx.on_create_shard = self._index_created_shard
         idx.snapshot_queue = self.snapshot_queue
         idx.lazy_fragments = self.lazy_fragments

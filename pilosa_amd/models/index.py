@@ -148,7 +148,10 @@ class Index:
         s = set()
         for f in list(self.fields.values()):
             s |= set(f.available_shards())
-        return sorted(s)
+        out = sorted(s)
+        if self.stats is not None and out:
+            self.stats.gauge("maxShard", out[-1])   # index.go:257
+        return out
 
     def options_json(self) -> dict:
         return {"keys": self.keys, "trackExistence": self.track_existence}

@@ -18,13 +18,13 @@ from __future__ import annotations
 import json
 import os
 import random
+import re
 import struct
 import threading
 import time
 import urllib.request
 import uuid
 from typing import Dict, List, Optional, Sequence, Tuple, Union
-from urllib.parse import urlparse
 
 DEFAULT_PARTITION_N = 256
 STATE_STARTING, STATE_DEGRADED, STATE_NORMAL, STATE_RESIZING = "STARTING", "DEGRADED", "NORMAL", "RESIZING"
@@ -67,7 +67,16 @@ class JumpHasher:
         return jump_hash(key, n)
 
 
+_SCHEME_RE = re.compile(r"^[+a-z]+$")
+_HOST_RE = re.compile(r"^[0-9a-z.-]+$|^\[[:0-9a-fA-F]+\]$")
+_ADDRESS_RE = re.compile(r"^(([+a-z]+)://)?([0-9a-z.-]+|\[[:0-9a-fA-F]+\])?(:([0-9]+))?$")
+
+
 class URI:
+    """scheme://host:port of a node (reference uri.go): an address parses
+    with the reference's grammar (scheme and port optional, IPv6 hosts in
+    brackets, defaults http / localhost / 10101); ``normalize`` drops a
+    ``+protobuf``-style scheme suffix."""
     __slots__ = ("scheme", "host", "port")
 
     def __init__(self, scheme="http", host="localhost", port=10101):
@@ -75,13 +84,43 @@ class URI:
 
     @classmethod
     def parse(cls, s: str) -> "URI":
-        if "://" not in s:
-            s = "http://" + s
-        u = urlparse(s)
-        return cls(u.scheme or "http", u.hostname or "localhost", u.port or 10101)
+        """NewURIFromAddress (uri.go parseAddress); ValueError when invalid."""
+        m = _ADDRESS_RE.match(s)
+        if m is None:
+            raise ValueError(f"invalid address: {s!r}")
+        port = 10101
+        if m.group(5):
+            port = int(m.group(5))
+            if port > 65535:
+                raise ValueError("port must be in range 0 - 65535")
+        return cls(m.group(2) or "http", m.group(3) or "localhost", port)
+
+    @classmethod
+    def from_host_port(cls, host: str, port: int) -> "URI":
+        """NewURIFromHostPort: the default scheme with a validated host."""
+        u = cls()
+        u.set_host(host)
+        u.set_port(port)
+        return u
+
+    def set_scheme(self, scheme: str):
+        if not _SCHEME_RE.match(scheme):
+            raise ValueError("invalid scheme")
+        self.scheme = scheme
+
+    def set_host(self, host: str):
+        if not _HOST_RE.match(host):
+            raise ValueError("invalid host")
+        self.host = host
+
+    def set_port(self, port: int):
+        self.port = int(port)
 
     def normalize(self) -> str:
-        return f"{self.scheme}://{self.host}:{self.port}"
+        return f"{self.scheme.split('+', 1)[0]}://{self.host}:{self.port}"
+
+    def path(self, p: str) -> str:
+        return self.normalize() + p
 
     def host_port(self) -> str:
         return f"{self.host}:{self.port}"

@@ -89,6 +89,16 @@ class API:
             return resp
 
     # ------------------------------------------------------------ schema
+    def _count(self, name: str, index: Optional[str] = None):
+        """Schema events on the holder's stats client (api.go:183,227,274,461,493)."""
+        st = self.holder.stats
+        if st is None:
+            return
+        if index is None:
+            st.count(name, 1)
+        else:
+            st.count_with_tags(name, 1, [f"index:{index}"])
+
     def create_index(self, name: str, keys: bool = False, track_existence: bool = True, remote: bool = False):
         self.validate("CreateIndex")
         try:
@@ -97,6 +107,7 @@ class API:
             if e is ErrIndexExists:
                 raise ConflictError(e)
             raise BadRequestError(e)
+        self._count("createIndex")
         self._mesh_schema()
         if not remote:
             self.server.broadcast({"type": "CreateIndex", "index": name,
@@ -116,6 +127,7 @@ class API:
             self.holder.delete_index(name)
         except PilosaError as e:
             raise NotFoundError(e)
+        self._count("deleteIndex")
         if self.server.gpu is not None:
             self.server.gpu.invalidate()
         if getattr(self.server, "mesh", None) is not None:
@@ -134,6 +146,7 @@ class API:
             if e is ErrFieldExists:
                 raise ConflictError(e)
             raise BadRequestError(e)
+        self._count("createField", index)
         self._mesh_schema()
         if not remote:
             self.server.broadcast({"type": "CreateField", "index": index, "field": name,
@@ -159,6 +172,7 @@ class API:
             idx.delete_field(name)
         except PilosaError as e:
             raise NotFoundError(e)
+        self._count("deleteField", index)
         if self.server.gpu is not None:
             self.server.gpu.invalidate()
         if getattr(self.server, "mesh", None) is not None:
@@ -170,6 +184,7 @@ class API:
         self.validate("DeleteAvailableShard")
         f = self.field(index, field)
         f.remove_available_shard(shard)
+        self._count("deleteAvailableShard", index)
         if not remote:
             self.server.broadcast({"type": "DeleteAvailableShard", "index": index, "field": field, "shard": shard})
 

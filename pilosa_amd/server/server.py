@@ -210,6 +210,7 @@ class Server:
 
     def _refresh_diagnostics(self):
         d = self.diagnostics
+        d.set("Version", d.version)
         d.set("Host", self.uri.host)
         d.set("Cluster", ",".join(n.id for n in self.cluster.nodes))
         d.set("NumNodes", len(self.cluster.nodes))

@@ -17,6 +17,93 @@ from typing import Iterable, List, Optional
 import numpy as np
 
 
+# ---- slice helpers (roaring/naive.go): the oracle's operations on plain
+# lists of uint64 values; inputs may be unsorted and hold duplicates, every
+# set result comes back sorted and distinct
+def sort_slice(a: List[int]) -> List[int]:
+    a.sort()
+    return a
+
+
+def remove_slice_duplicates(a: Iterable[int]) -> List[int]:
+    return sorted(set(a))
+
+
+def intersect_slice(a: Iterable[int], b: Iterable[int]) -> List[int]:
+    return sorted(set(a) & set(b))
+
+
+def union_slice(a: Iterable[int], b: Iterable[int]) -> List[int]:
+    return sorted(set(a) | set(b))
+
+
+def difference_slice(a: Iterable[int], b: Iterable[int]) -> List[int]:
+    return sorted(set(a) - set(b))
+
+
+def xor_slice(a: Iterable[int], b: Iterable[int]) -> List[int]:
+    return sorted(set(a) ^ set(b))
+
+
+def max_in_slice(a: Iterable[int]) -> int:
+    return max(a, default=0)
+
+
+def shift_slice(a: Iterable[int], n: int) -> List[int]:
+    return sorted(int(x) + n for x in set(a))
+
+
+def for_each_in_slice(a: Iterable[int], fn) -> None:
+    for x in a:           # in the slice's own order
+        fn(x)
+
+
+def for_each_in_range_slice(a: Iterable[int], start: int, end: int, fn) -> None:
+    for x in a:           # values in [start, end), in the slice's own order
+        if start <= x < end:
+            fn(x)
+
+
+def contained_in_slice(a: List[int], v: int):
+    """(index of v in the slice as given, found)"""
+    for i, x in enumerate(a):
+        if x == v:
+            return i, True
+    return -1, False
+
+
+def add_n_to_slice(a: Iterable[int], *b: int):
+    """(sorted union, number of values of b that were not in a)"""
+    s = set(a)
+    n = len(s)
+    s.update(b)
+    return sorted(s), len(s) - n
+
+
+def remove_n_from_slice(a: Iterable[int], *b: int):
+    """(sorted difference, number of values removed)"""
+    s = set(a)
+    n = len(s)
+    s.difference_update(b)
+    return sorted(s), n - len(s)
+
+
+def count_range_slice(a: Iterable[int], start: int, end: int) -> int:
+    return sum(1 for x in set(a) if start <= x < end)
+
+
+def range_slice(a: Iterable[int], start: int, end: int) -> List[int]:
+    return sorted(x for x in set(a) if start <= x < end)
+
+
+def flip_slice(a: Iterable[int], start: int, end: int) -> List[int]:
+    """Flip [start, end] inclusive (Bitmap.Flip); start > end flips nothing."""
+    s = set(a)
+    if start <= end:
+        s ^= set(range(start, end + 1))
+    return sorted(s)
+
+
 class NaiveBitmap:
     def __init__(self, values: Iterable[int] = ()):
         self.v: List[int] = sorted(set(int(x) for x in values))

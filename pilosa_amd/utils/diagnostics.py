@@ -17,6 +17,17 @@ from pilosa_amd import __version__
 from pilosa_amd.utils.sysinfo import SystemInfo
 
 
+def version_segments(v: str):
+    """'v1.2.3-rc1' -> [1, 2, 3] (diagnostics.go versionSegments)."""
+    out = []
+    for x in v.strip("v").split("-", 1)[0].split("."):
+        try:
+            out.append(int(x))
+        except ValueError:
+            out.append(0)
+    return out
+
+
 def compare_versions(a: str, b: str) -> int:
     """semver-ish compare of 'vX.Y.Z[-suffix]' strings (-1, 0, 1)."""
     def parts(v):
@@ -46,8 +57,13 @@ class DiagnosticsCollector:
         self._thread: Optional[threading.Thread] = None
 
     def set(self, name: str, value):
+        if isinstance(value, str) and value == "":
+            return   # empty strings are not recorded (diagnostics.go Set)
         with self.mu:
             self.metrics[name] = value
+
+    def set_version(self, v: str):
+        self.version = v
 
     def enrich_with_os(self):
         s = self.sysinfo
@@ -88,18 +104,20 @@ class DiagnosticsCollector:
         self.set("BSIFieldCount", int_fields)
         self.set("TimeQuantumFieldCount", time_fields)
 
-    def payload(self) -> bytes:
+    def encode(self) -> bytes:
+        """The recorded metrics as the JSON document (diagnostics.go encode)."""
         with self.mu:
-            m = dict(self.metrics)
-        m["Version"] = self.version
-        m["Uptime"] = int(time.time() - self.start_time)
-        return json.dumps(m, sort_keys=True).encode()
+            return json.dumps(self.metrics, sort_keys=True).encode()
+
+    payload = encode
 
     def flush(self) -> bool:
-        """POST the document to the configured endpoint (no-op without one)."""
+        """Record Uptime, then POST the document to the configured endpoint
+        (no-op without one; diagnostics.go Flush)."""
+        self.set("Uptime", int(time.time() - self.start_time))
         if not self.host:
             return False
-        req = urllib.request.Request(self.host, data=self.payload(), method="POST",
+        req = urllib.request.Request(self.host, data=self.encode(), method="POST",
                                      headers={"Content-Type": "application/json"})
         try:
             with urllib.request.urlopen(req, timeout=10) as r:
@@ -110,11 +128,39 @@ class DiagnosticsCollector:
                 self.logger.debugf("diagnostics flush: %s", e)
             return False
 
-    def check_version(self, latest: str) -> Optional[str]:
-        """Message when ``latest`` is newer than this build (diagnostics.go:120-150)."""
-        if latest and compare_versions(latest, self.version) > 0:
-            return f"you are running Pilosa-AMD {self.version}, a newer version ({latest}) is available"
+    def compare_version(self, value: str) -> Optional[str]:
+        """The upgrade message when release ``value`` is newer than this
+        build -- major, minor or patch -- else None (diagnostics.go:135-148)."""
+        cur, loc = (version_segments(value) + [0, 0, 0])[:3], (version_segments(self.version) + [0, 0, 0])[:3]
+        url = "https://github.com/pilosa/pilosa/releases"
+        if loc[0] < cur[0]:
+            return f"you are running Pilosa {self.version}, a newer version ({value}) is available: {url}"
+        if loc[1] < cur[1] and loc[0] == cur[0]:
+            return f"you are running Pilosa {self.version}, the latest minor release is {value}: {url}"
+        if loc[2] < cur[2] and loc[0] == cur[0] and loc[1] == cur[1]:
+            return f"there is a new patch release of Pilosa available: {value}: {url}"
         return None
+
+    def check_version(self, latest: str) -> Optional[str]:
+        """Message when ``latest`` is newer than this build."""
+        return self.compare_version(latest) if latest else None
+
+    version_url = ""
+    _last_version = ""
+
+    def check_version_url(self) -> None:
+        """GET ``version_url`` ({"version": ...}) and log the upgrade message
+        once per new release seen (diagnostics.go CheckVersion)."""
+        with urllib.request.urlopen(self.version_url, timeout=10) as r:
+            if r.status != 200:
+                raise RuntimeError(f"http: status={r.status}")
+            v = json.loads(r.read() or b"{}").get("version", "")
+        if v == self._last_version:
+            return
+        self._last_version = v
+        msg = self.compare_version(v)
+        if msg and self.logger is not None:
+            self.logger.printf("%s\n", msg)
 
     def start(self, refresh: Callable[[], None]):
         def loop():

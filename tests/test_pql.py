@@ -226,3 +226,12 @@ def test_native_matches_python_on_mutated_input_fuzz():
             got = "error"
         assert got == want, src
     run()
+
+
+@pytest.mark.parametrize("src", ["Row(a==foo, a==bar)", "Row(a=foo, a=bar)", "Row(a>5, a>6)", "Row(a=7, a=8)",
+                                 "Row(a=[7], a=[7,8])"])
+def test_duplicate_arg_error(parse, src):
+    """pqlpeg_test.go TestDuplicateArgError: the exact reference message."""
+    with pytest.raises(ParseError) as e:
+        parse(src)
+    assert str(e.value) == "duplicate argument provided: a"

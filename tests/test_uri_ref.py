@@ -1,0 +1,89 @@
+"""Reference uri_internal_test.go, ported (13 tests): address grammar,
+defaults, normalisation, setters and their validation."""
+import pytest
+
+from pilosa_amd.parallel.cluster import URI
+
+VALID = [  # uri_internal_test.go validFixture
+    ("http+protobuf://index1.pilosa.com:3333", "http+protobuf", "index1.pilosa.com", 3333),
+    ("index1.pilosa.com:3333", "http", "index1.pilosa.com", 3333),
+    ("https://index1.pilosa.com", "https", "index1.pilosa.com", 10101),
+    ("index1.pilosa.com", "http", "index1.pilosa.com", 10101),
+    ("https://:3333", "https", "localhost", 3333),
+    (":3333", "http", "localhost", 3333),
+    ("[::1]", "http", "[::1]", 10101),
+    ("[::1]:3333", "http", "[::1]", 3333),
+    ("[fd42:4201:f86b:7e09:216:3eff:fefa:ed80]:3333", "http", "[fd42:4201:f86b:7e09:216:3eff:fefa:ed80]", 3333),
+    ("https://[fd42:4201:f86b:7e09:216:3eff:fefa:ed80]:3333", "https", "[fd42:4201:f86b:7e09:216:3eff:fefa:ed80]", 3333),
+]
+INVALID = ["foo:bar", "http://foo:", "foo:", ":bar", "http://pilosa.com:129999999999999999999999993",
+           "fd42:4201:f86b:7e09:216:3eff:fefa:ed80", ":65536"]
+
+
+def _cmp(u, scheme, host, port):
+    assert (u.scheme, u.host, u.port) == (scheme, host, port)
+
+
+def test_default_uri():                          # TestDefaultURI
+    _cmp(URI(), "http", "localhost", 10101)
+
+
+def test_uri_with_host_port():                   # TestURIWithHostPort
+    _cmp(URI.from_host_port("index1.pilosa.com", 3333), "http", "index1.pilosa.com", 3333)
+
+
+def test_uri_with_invalid_host_port():           # TestURIWithInvalidHostPort
+    with pytest.raises(ValueError):
+        URI.from_host_port("index?.pilosa.com", 3333)
+
+
+@pytest.mark.parametrize("addr,scheme,host,port", VALID)
+def test_new_uri_from_address(addr, scheme, host, port):   # TestNewURIFromAddress
+    _cmp(URI.parse(addr), scheme, host, port)
+
+
+@pytest.mark.parametrize("addr", INVALID)
+def test_new_uri_from_address_invalid(addr):     # TestNewURIFromAddressInvalidAddress
+    with pytest.raises(ValueError):
+        URI.parse(addr)
+
+
+def test_normalized_address():                   # TestNormalizedAddress
+    assert URI.parse("http+protobuf://big-data.pilosa.com:6888").normalize() == "http://big-data.pilosa.com:6888"
+
+
+def test_uri_path():                             # TestURIPath
+    u = URI.parse("http+protobuf://big-data.pilosa.com:6888")
+    assert u.path("/index/foo") == "http://big-data.pilosa.com:6888/index/foo"
+
+
+def test_set_scheme():                           # TestSetScheme
+    u = URI()
+    u.set_scheme("fun")
+    assert u.scheme == "fun"
+
+
+def test_set_host():                             # TestSetHost
+    u = URI()
+    u.set_host("10.20.30.40")
+    assert u.host == "10.20.30.40"
+
+
+def test_set_port():                             # TestSetPort
+    u = URI()
+    u.set_port(9999)
+    assert u.port == 9999
+
+
+def test_set_invalid_scheme():                   # TestSetInvalidScheme
+    with pytest.raises(ValueError):
+        URI().set_scheme("?invalid")
+
+
+def test_set_invalid_host():                     # TestSetInvalidHost
+    with pytest.raises(ValueError):
+        URI().set_host("index?.pilosa.com")
+
+
+def test_host_port():                            # TestHostPort
+    assert URI.from_host_port("i.pilosa.com", 15001).host_port() == "i.pilosa.com:15001"
