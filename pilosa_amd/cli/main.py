@@ -268,8 +268,11 @@ def _flush(c, node, args, buf, is_int, col_keys, row_keys) -> int:
 # ------------------------------------------------------------------ export
 def cmd_export(args, stdout, stderr) -> int:
     from pilosa_amd.server.client import InternalClient
-    if not args.index or not args.field:
-        print("index and field required", file=stderr)
+    if not args.index:
+        print("index required", file=stderr)      # pilosa.ErrIndexRequired
+        return 1
+    if not args.field:
+        print("field required", file=stderr)      # pilosa.ErrFieldRequired
         return 1
     uri = _client_uri(args.host)
     c = InternalClient()
@@ -287,31 +290,49 @@ def cmd_export(args, stdout, stderr) -> int:
 
 # ------------------------------------------------------------------ check / inspect
 def cmd_check(args, stdout, stderr) -> int:
+    """ctl/check.go: fragment files (no extension) are unmarshalled and
+    consistency-checked; .cache and .snapshotting files are skipped with a
+    note; the first file that cannot be read ends the run with its error."""
     from pilosa_amd import _roaring
-    rc = 0
     for p in args.paths:
-        if p.endswith(".cache") or p.endswith(".snapshotting"):
-            print(f"{p}: ignoring", file=stdout)
+        ext = os.path.splitext(p)[1]
+        if ext == ".cache":
+            print(f"{p}: ignoring cache file", file=stdout)
+            continue
+        if ext == ".snapshotting":
+            print(f"{p}: ignoring snapshot file", file=stdout)
+            continue
+        if ext:
             continue
         try:
             with open(p, "rb") as fh:
-                bm = _roaring.Bitmap.from_bytes(fh.read())
-            errs = bm.check()
+                data = fh.read()
+        except OSError as e:
+            print(f"checking bitmap: opening file: {e}", file=stderr)
+            return 1
+        try:
+            bm = _roaring.Bitmap.from_bytes(data)
         except Exception as e:  # noqa: BLE001
-            errs = str(e)
-        if errs:
-            rc = 1
-            print(f"{p}: {errs.strip()}", file=stdout)
-        else:
-            print(f"{p}: ok", file=stdout)
-    return rc
+            print(f"checking bitmap: unmarshalling: reading roaring header: {e}", file=stderr)
+            return 1
+        errs = bm.check()
+        for line in (errs or "").strip().splitlines():
+            print(f"{p}: {line}", file=stdout)
+        print(f"{p}: ok", file=stdout)
+    return 0
 
 
 def cmd_inspect(args, stdout, stderr) -> int:
     from collections import Counter
 
     from pilosa_amd import _roaring
-    with open(args.path, "rb") as fh:
+    if not args.path:
+        print("path required", file=stderr)
+        return 1
+    if len(args.path) > 1:
+        print("only one path allowed", file=stderr)
+        return 1
+    with open(args.path[0], "rb") as fh:
         data = fh.read()
     bm = _roaring.Bitmap.from_bytes(data)
     info = bm.container_info()
@@ -370,7 +391,7 @@ def build_parser() -> argparse.ArgumentParser:
     ck = sub.add_parser("check", help="consistency check of fragment files")
     ck.add_argument("paths", nargs="+")
     ins = sub.add_parser("inspect", help="inspect a fragment file")
-    ins.add_argument("path")
+    ins.add_argument("path", nargs="*")
     ins.add_argument("--limit", type=int, default=100)
     cf = sub.add_parser("config", help="print the resolved configuration")
     cf.add_argument("-c", "--config", default=None)

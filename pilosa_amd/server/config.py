@@ -16,45 +16,70 @@ DURATION_UNITS = {"ns": 1e-9, "us": 1e-6, "µs": 1e-6, "ms": 1e-3, "s": 1.0, "m"
 
 
 def parse_duration(v) -> float:
-    """Go-style durations ('1m30s', '500ms', '10m') -> seconds."""
+    """Go ``time.ParseDuration`` ('1m30s', '500ms', '-1.5h') -> seconds
+    (toml/toml.go Duration.UnmarshalText); the reference's error texts."""
     if isinstance(v, (int, float)):
         return float(v)
     s = str(v).strip()
+    orig = s
     if not s:
         return 0.0
-    total, num = 0.0, ""
-    i = 0
+    neg = s[0] == "-"
+    if s[0] in "+-":
+        s = s[1:]
+    if s == "0":
+        return 0.0
+    if not s:
+        raise ValueError(f"time: invalid duration {orig}")
+    total, i = 0.0, 0
     while i < len(s):
-        ch = s[i]
-        if ch.isdigit() or ch == ".":
-            num += ch
-            i += 1
-            continue
-        unit = ""
-        while i < len(s) and not (s[i].isdigit() or s[i] == "."):
-            unit += s[i]
-            i += 1
-        if unit not in DURATION_UNITS or not num:
-            raise ValueError(f"invalid duration: {v!r}")
+        j = i
+        while j < len(s) and (s[j].isdigit() or s[j] == "."):
+            j += 1
+        num = s[i:j]
+        if not num or num == "." or num.count(".") > 1:
+            raise ValueError(f"time: invalid duration {orig}")
+        k = j
+        while k < len(s) and not (s[k].isdigit() or s[k] == "."):
+            k += 1
+        unit = s[j:k]
+        if not unit:
+            raise ValueError(f"time: missing unit in duration {orig}")
+        if unit not in DURATION_UNITS:
+            raise ValueError(f"time: unknown unit {unit} in duration {orig}")
         total += float(num) * DURATION_UNITS[unit]
-        num = ""
-    if num:
-        if total == 0 and float(num) == 0:
-            return 0.0
-        raise ValueError(f"missing unit in duration {v!r}")
-    return total
+        i = k
+    return -total if neg else total
 
 
 def format_duration(sec: float) -> str:
-    if sec == 0:
+    """Go ``time.Duration.String``: '3m2s', '1h0m0s', '1.5s', '500ms', '0s'."""
+    ns = int(round(sec * 1e9))
+    if ns == 0:
         return "0s"
-    if sec % 3600 == 0:
-        return f"{int(sec // 3600)}h0m0s"
-    if sec % 60 == 0:
-        return f"{int(sec // 60)}m0s"
-    if sec >= 1 and float(sec).is_integer():
-        return f"{int(sec)}s"
-    return f"{int(round(sec * 1000))}ms"
+    sign = "-" if ns < 0 else ""
+    ns = abs(ns)
+
+    def frac(v: int, unit: int) -> str:
+        w, f = divmod(v, unit)
+        if not f:
+            return str(w)
+        digits = len(str(unit)) - 1
+        return f"{w}.{str(f).rjust(digits, '0').rstrip('0')}"
+    if ns < 1000:
+        return f"{sign}{ns}ns"
+    if ns < 1_000_000:
+        return f"{sign}{frac(ns, 1000)}\u00b5s"
+    if ns < 1_000_000_000:
+        return f"{sign}{frac(ns, 1_000_000)}ms"
+    h, rem = divmod(ns, 3600 * 1_000_000_000)
+    m, rem = divmod(rem, 60 * 1_000_000_000)
+    out = f"{frac(rem, 1_000_000_000)}s"
+    if h:
+        return f"{sign}{h}h{m}m{out}"
+    if m:
+        return f"{sign}{m}m{out}"
+    return sign + out
 
 
 DEFAULTS: Dict[str, Any] = {
