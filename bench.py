@@ -1499,6 +1499,7 @@ def bench_serving(args, base, dev):
         t_imp = time.perf_counter() - t1
         gpu = ex.gpu
         w0 = getattr(gpu, "device_writes", 0)
+        wl0 = getattr(gpu, "device_write_launches", 0)
         t2 = time.perf_counter()
         ex.execute("i", queries[1])      # first query after the import: device replay of the write batches
         t_replay = time.perf_counter() - t2
@@ -1513,6 +1514,7 @@ def bench_serving(args, base, dev):
                          "clients": args.import_clients,
                          "first_query_after_s": round(t_replay, 3),
                          "device_write_batches": int(getattr(gpu, "device_writes", 0) - w0),
+                         "device_write_launches": int(getattr(gpu, "device_write_launches", 0) - wl0),
                          "fragments_cold_after_import": sum(f.is_cold() for f in frags), "fragments": len(frags),
                          "rss_growth_gb": round(_rss_gb() - rss0, 2), "device_matches_host": all(chk)}
     finally:

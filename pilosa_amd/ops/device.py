@@ -207,6 +207,7 @@ class DeviceView:
         self._cap = None             # per-shard meta capacity (patchable arenas)
         self.payload_used = int(payload.shape[0])
         self.garbage_u16 = 0
+        self.write_launches = 0      # container_merge / container_emit launches (device write replay)
 
     # ------------------------------------------------------------ patchable layout
     @classmethod
@@ -695,6 +696,7 @@ class DeviceView:
             off16 = (ends - sizes + used) // 8
             meta_out = torch.empty(n, dtype=torch.int64, device=dev)
             K.container_emit(scratch, card, nruns, off16, t_j[c0:c1], self.t_payload, meta_out)
+            self.write_launches += 2   # one merge + one emit launch for every shard of the group
             new_meta[c0:c1] = meta_out.cpu().numpy()
             used += tot
         self.payload_used = used

@@ -89,6 +89,7 @@ class GpuExecutor:
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
         self.device_writes = 0   # ... of which write batches were merged on the GPU (K11/K12)
+        self.device_write_launches = 0   # ... in this many merge/emit launches (all shards of a refresh share them)
         self.device_writes_on = os.environ.get("PILOSA_DEVICE_WRITES", "1") != "0"
         # cold views load from their fragment files (no host bitmaps)
         self.file_loader = os.environ.get("PILOSA_FILE_LOADER", "1") != "0"
@@ -164,8 +165,10 @@ class GpuExecutor:
                         keys = set(keys) | _delta_keys(deltas)
                     rebuild[si] = (rows, keys)
                 if ok and pending:
+                    wl0 = dv.write_launches
                     failed = dv.apply_deltas_multi(pending)
                     self.device_writes += len(pending) - len(failed)
+                    self.device_write_launches += dv.write_launches - wl0
                     for si in failed:   # the host rebuilds what the device could not take
                         rows, keys = rebuild[si]
                         rebuild[si] = (rows, set(keys) | _delta_keys(pending[si]))
@@ -274,7 +277,8 @@ class GpuExecutor:
                 types[name] += int((t == code).sum())
         return {"arenas": len(views), "arenaBytes": self.hbm_bytes(), "containers": types,
                 "launches": self.launches, "rebuilds": self.rebuilds, "shardUpdates": self.shard_updates,
-                "rowUpdates": self.row_updates, "deviceWrites": self.device_writes, "evictions": self.evictions, "hbmBudget": self.hbm_budget}
+                "rowUpdates": self.row_updates, "deviceWrites": self.device_writes,
+                "deviceWriteLaunches": self.device_write_launches, "evictions": self.evictions, "hbmBudget": self.hbm_budget}
 
     def invalidate(self):
         with self.mu:

@@ -231,3 +231,36 @@ def test_device_writes_emit_optimized_container_types(view):
     for k in (20 * 16, 21 * 16, 22 * 16, 23 * 16, 24 * 16):
         assert got[k] == want[k], (k, got[k], want[k])
     assert got[20 * 16] == "run" and got[22 * 16] == "array" and got[23 * 16] == "bitmap"
+
+
+def test_device_write_replay_shares_launches_across_shards():
+    """A bulk import request per shard (16 shards, as POST /import sends them)
+    is replayed on the device at the next read in shared launches: one
+    container_merge + container_emit pair for the whole refresh, not one per
+    shard (reference fragment.go:1995-2156 imports shard by shard)."""
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+
+    shards = list(range(16))
+    env = Env(gpu=lambda h: GpuExecutor(h, "cuda:0"))
+    try:
+        env.create_index("i")
+        env.field("i", "g")
+        f = env.holder.index("i").field("g")
+        rng = np.random.default_rng(7)
+        c = rng.choice(16 * SW, 200000, replace=False).astype(np.uint64)
+        f.import_bits(rng.integers(0, 5, len(c)).astype(np.uint64), c)
+        g = env.executor.gpu
+        g.executor = env.executor
+        g.view_arena("i", "g", "standard", shards)
+        w0, l0 = g.device_writes, g.device_write_launches
+        for s in shards:
+            cols = np.uint64(s) * np.uint64(SW) + rng.integers(0, SW, 5000).astype(np.uint64)
+            f.import_bits(rng.integers(0, 8, len(cols)).astype(np.uint64), cols)
+        dv = g.view_arena("i", "g", "standard", shards)
+        assert g.device_writes - w0 == 16
+        assert g.device_write_launches - l0 <= 4, g.device_write_launches - l0
+        for si, s in enumerate(shards):
+            frag = env.holder.fragment("i", "g", "standard", s)
+            assert _decode(dv, si) == frag.storage.slice().astype(np.int64).tolist()
+    finally:
+        env.close()
