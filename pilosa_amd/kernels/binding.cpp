@@ -230,6 +230,40 @@ void row_counts(torch::Tensor view, torch::Tensor shard_of, torch::Tensor dense,
   check_launch("row_counts");
 }
 
+void topn_cache_counts(torch::Tensor view, int64_t S, torch::Tensor u, torch::Tensor cm) {
+  for (auto* t : {&u, &cm}) check_dev(*t, "topn_cache_counts");
+  const int64_t U = u.numel();
+  TORCH_CHECK(u.scalar_type() == torch::kInt32, "u int32[U]");
+  TORCH_CHECK(cm.scalar_type() == torch::kInt32 && cm.numel() == U * S, "cm int32[U, S]");
+  pk::launch_topn_cache_counts(viewdev_from(view), int(S), u.data_ptr<int32_t>(), int(U), cm.data_ptr<int32_t>(),
+                               cur_stream(u));
+  check_launch("topn_cache_counts");
+}
+
+void topn_cache_batch(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch::Tensor u, torch::Tensor cm,
+                      torch::Tensor prm, int64_t Q, int64_t T, torch::Tensor member, torch::Tensor tot,
+                      torch::Tensor out) {
+  for (auto* t : {&cnt, &inv, &u, &cm, &prm, &member, &tot, &out}) check_dev(*t, "topn_cache_batch");
+  TORCH_CHECK(cnt.scalar_type() == torch::kInt32 && cnt.dim() == 2, "cnt int32[S, K]");
+  const int64_t S = cnt.size(0), K = cnt.size(1), U = u.numel();
+  TORCH_CHECK(nmax >= 0 && nmax <= K, "nmax out of range");
+  TORCH_CHECK(inv.scalar_type() == torch::kInt32 && inv.numel() == S * nmax, "inv int32[S * nmax]");
+  TORCH_CHECK(u.scalar_type() == torch::kInt32, "u int32[U]");
+  TORCH_CHECK(cm.scalar_type() == torch::kInt32 && cm.numel() == U * S, "cm int32[U, S]");
+  TORCH_CHECK(prm.scalar_type() == torch::kInt32 && prm.numel() == 4 * Q + T, "prm int32[4Q + T]");
+  TORCH_CHECK(member.scalar_type() == torch::kUInt8 && member.numel() == Q * U, "member uint8[Q, U]");
+  TORCH_CHECK(tot.scalar_type() == torch::kInt64 && tot.numel() == T * U, "tot int64[T, U]");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.dim() == 2 && out.size(0) == Q, "out int64[Q, KK+1]");
+  TORCH_CHECK(Q < 65536 && T > 0 && U < (int64_t(1) << 31), "topn_cache_batch sizes");
+  const int64_t KK = out.size(1) - 1;
+  pk::launch_topn_cache_batch(cnt.data_ptr<int32_t>(), int(K), int(S), int(nmax), inv.data_ptr<int32_t>(),
+                              u.data_ptr<int32_t>(), cm.data_ptr<int32_t>(), prm.data_ptr<int32_t>(), int(Q), int(T),
+                              int(U), int(KK), member.data_ptr<uint8_t>(),
+                              reinterpret_cast<long long*>(tot.data_ptr<int64_t>()),
+                              reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(cnt));
+  check_launch("topn_cache_batch");
+}
+
 void row_counts_sum(torch::Tensor view, int64_t S, torch::Tensor dense, torch::Tensor threshold, torch::Tensor out) {
   for (auto* t : {&dense, &threshold, &out}) check_dev(*t, "row_counts_sum");
   const int64_t P = dense.numel();
@@ -515,6 +549,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
   m.def("leaf_src", &leaf_src, "src containers of plain rows straight from the arena (TopN srcs)");
   m.def("row_counts", &row_counts, "row counts of (shard, dense row) entries (device rank caches)");
+  m.def("topn_cache_counts", &topn_cache_counts, "cache-only TopN: [candidate x shard] row counts");
+  m.def("topn_cache_batch", &topn_cache_batch, "cache-only TopN batch: membership, totals, per-query top-n");
   m.def("row_counts_sum", &row_counts_sum, "ids= re-count without src: per id the sum of shard row counts >= threshold");
   m.def("keymask_build", &keymask_build, "key-presence mask of every (shard, row) of a view");
   m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");

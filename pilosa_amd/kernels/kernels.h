@@ -127,6 +127,13 @@ void launch_row_counts(const ViewDev& v, const int32_t* shard_of, const int32_t*
 // out[p] = sum over shards of row dense[p]'s count where >= threshold[p] (ids= re-count, no src).
 void launch_row_counts_sum(const ViewDev& v, int S, const int32_t* dense, const int32_t* threshold, int P,
                            unsigned long long* out, hipStream_t st);
+// Cache-only TopN: cm[j*S + s] = candidate u[j]'s count in shard s (memoised per rank-cache prefix).
+void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, int32_t* cm, hipStream_t st);
+// Cache-only TopN batch: membership, per-threshold totals and per-query top-n
+// (prm = lim[Q] | mt[Q] | tsel[Q] | nq[Q] | th[T]; out[Q, KK+1], column 0 = rows kept or -2 on overflow).
+void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
+                             const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
+                             long long* tot, long long* out, hipStream_t st);
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st);
 

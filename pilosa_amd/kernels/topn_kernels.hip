@@ -1044,4 +1044,144 @@ void launch_row_counts_sum(const ViewDev& v, int S, const int32_t* dense, const 
   hipLaunchKernelGGL(row_counts_sum_kernel, dim3(unsigned(P)), dim3(256), 0, st, v, S, dense, threshold, P, out);
 }
 
+// ---------------------------------------------------------------------------
+// Cache-only TopN batch (TopN(field, n) without a src row): the reference
+// runs, per shard, fragment.top's fill phase over the rank cache
+// (fragment.go:1436-1530 with src == nil) and then re-counts the union of
+// the candidates with ids= (executor.go executeTopN phase 2).  On the device
+// the whole batch is three kernels over the rank caches already resident in
+// HBM: a per-query membership bitmap over the candidate rows, one total per
+// (distinct threshold, candidate) from the memoised [candidate x shard]
+// count matrix, and one workgroup per query that compacts its members into
+// LDS, bitonic-sorts the composite key (count desc, row asc) and writes the
+// first n.  No data-dependent host round trips between them.
+namespace {
+
+constexpr int TC_CAP = 8192;   // members per query sorted in LDS (64 KB of keys)
+
+__global__ __launch_bounds__(256) void topn_cache_counts_kernel(ViewDev v, int S, const int32_t* __restrict__ u,
+                                                                int64_t N, int32_t* __restrict__ cm) {
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < N; e += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t j = e / S;
+    cm[e] = row_card(v, int(e - j * S), u[j]);
+  }
+}
+
+// member[q, inv[s*nmax + k]] = 1 for the first lim[q] ranks of shard s whose
+// cached count reaches mt[q]
+__global__ __launch_bounds__(256) void topn_cache_member_kernel(const int32_t* __restrict__ cnt, int K, int S, int nmax,
+                                                                const int32_t* __restrict__ inv,
+                                                                const int32_t* __restrict__ prm, int Q, int U,
+                                                                uint8_t* __restrict__ member) {
+  const int q = blockIdx.y;
+  const int L = min(prm[q], nmax);
+  const int32_t m = prm[Q + q];
+  const int64_t N = int64_t(S) * nmax;
+  uint8_t* mq = member + int64_t(q) * U;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < N; e += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t s = e / nmax;
+    const int k = int(e - s * nmax);
+    if (k < L && cnt[s * K + k] >= m) mq[inv[e]] = 1;
+  }
+}
+
+// tot[t*U + j] = sum over shards of cm[j*S + s] where it reaches th[t]; one
+// wave per (threshold, candidate), coalesced over the shard axis
+__global__ __launch_bounds__(256) void topn_cache_totals_kernel(const int32_t* __restrict__ cm, int S, int U,
+                                                                const int32_t* __restrict__ th, int T,
+                                                                long long* __restrict__ tot) {
+  const int w = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
+  const int lane = int(threadIdx.x & 63);
+  if (w >= T * U) return;
+  const int t = w / U;
+  const int j = w - t * U;
+  const int32_t m = th[t];
+  const int32_t* row = cm + int64_t(j) * S;
+  int acc = 0;
+  for (int s = lane; s < S; s += 64) {
+    const int32_t n = row[s];
+    acc += n >= m ? n : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) tot[w] = acc;
+}
+
+__global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* __restrict__ member,
+                                                                const long long* __restrict__ tot,
+                                                                const int32_t* __restrict__ u,
+                                                                const int32_t* __restrict__ prm, int Q, int U, int KK,
+                                                                long long* __restrict__ out) {
+  __shared__ long long keys[TC_CAP];
+  __shared__ int nmem;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid == 0) nmem = 0;
+  __syncthreads();
+  const uint8_t* mq = member + int64_t(q) * U;
+  const long long* tq = tot + int64_t(prm[2 * Q + q]) * U;
+  for (int j = tid; j < U; j += 256) {
+    if (!mq[j]) continue;
+    const int32_t d = u[j];
+    const long long sc = tq[j];
+    if (d < 0 || sc <= 0) continue;
+    const int p = atomicAdd(&nmem, 1);
+    if (p < TC_CAP) keys[p] = (sc << 32) | (0xFFFFFFFFll - d);
+  }
+  __syncthreads();
+  const int M = nmem;
+  long long* o = out + int64_t(q) * (KK + 1);
+  if (M > TC_CAP) {   // uniform over the workgroup: the host redoes this batch
+    if (tid == 0) o[0] = -2;
+    return;
+  }
+  int P = 1;
+  while (P < M) P <<= 1;
+  for (int i = M + tid; i < P; i += 256) keys[i] = -1;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1)
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = tid; i < P; i += 256) {
+        const int ixj = i ^ jj;
+        if (ixj > i) {
+          const long long a = keys[i], b = keys[ixj];
+          if (((i & k) == 0) ? (a < b) : (a > b)) {
+            keys[i] = b;
+            keys[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  const int lim = min(min(M, prm[3 * Q + q]), KK);
+  if (tid == 0) o[0] = lim;
+  for (int i = tid; i < lim; i += 256) o[1 + i] = keys[i];
+}
+
+}  // namespace
+
+void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, int32_t* cm, hipStream_t st) {
+  const int64_t N = int64_t(U) * S;
+  if (N <= 0) return;
+  const int64_t want = (N + 255) / 256;
+  const int blocks = int(want < 65536 ? want : 65536);
+  hipLaunchKernelGGL(topn_cache_counts_kernel, dim3(blocks), dim3(256), 0, st, v, S, u, N, cm);
+}
+
+void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
+                             const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
+                             long long* tot, long long* out, hipStream_t st) {
+  if (Q <= 0 || U <= 0) return;
+  const int64_t N = int64_t(S) * nmax;
+  if (N > 0) {
+    const int64_t want = (N + 255) / 256;
+    const int bx = int(want < 1024 ? want : 1024);
+    hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
+                       member);
+  }
+  const int64_t waves = int64_t(T) * U;
+  hipLaunchKernelGGL(topn_cache_totals_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm, S, U,
+                     prm + 4 * Q, T, tot);
+  hipLaunchKernelGGL(topn_cache_select_kernel, dim3(Q), dim3(256), 0, st, member, tot, u, prm, Q, U, KK, out);
+}
+
 }  // namespace pk

@@ -105,6 +105,12 @@ struct Shard {
   int64_t payload = 0;           // arena u16
   uint64_t last_key = 0;         // highest container key (row << key_shift | j)
   bool replayed = false;
+  // shards wider than 2^20 columns: this entry is device sub-shard `sub` of
+  // the file (its containers c with (c >> 4) & sub_mask == sub), -1 = all
+  int64_t sub = -1;
+  uint64_t sub_mask = 0;
+
+  bool keep(uint64_t key) const { return sub < 0 || ((key >> 4) & sub_mask) == uint64_t(sub); }
 
   void release() {
     if (map && owned.empty()) munmap(const_cast<uint8_t*>(map), len);
@@ -120,14 +126,26 @@ class FragmentLoader {
  public:
   // key_shift = log2(containers per row) = shard-width exponent - 16: 4 for
   // 2^20-column shards; 0..3 for narrower shards, whose rows then fill only
-  // the first 2^key_shift of the arena's 16 container slots per row.
-  FragmentLoader(std::vector<std::string> paths, int nthreads, int key_shift = 4)
-      : nthreads_(std::max(1, nthreads)), ks_(key_shift), jm_((uint64_t(1) << key_shift) - 1) {
-    if (key_shift < 0 || key_shift > 4) throw std::invalid_argument("FragmentLoader: key_shift must be in [0, 4]");
+  // the first 2^key_shift of the arena's 16 container slots per row; 5..16
+  // for wider shards, whose files each serve 2^(key_shift-4) device
+  // sub-shards of 2^20 columns: ``subs[i]`` names the sub-shard entry i loads
+  // (container c of a row goes to sub-shard c >> 4, arena slot c & 15).
+  FragmentLoader(std::vector<std::string> paths, int nthreads, int key_shift = 4, std::vector<int64_t> subs = {})
+      : nthreads_(std::max(1, nthreads)), ks_(key_shift), jm_((uint64_t(1) << std::min(key_shift, 4)) - 1) {
+    if (key_shift < 0 || key_shift > 16) throw std::invalid_argument("FragmentLoader: key_shift must be in [0, 16]");
+    if (key_shift > 4 && subs.size() != paths.size())
+      throw std::invalid_argument("FragmentLoader: key_shift > 4 needs one sub-shard index per path");
+    if (key_shift <= 4 && !subs.empty()) throw std::invalid_argument("FragmentLoader: subs only for key_shift > 4");
+    const uint64_t mask = key_shift > 4 ? (uint64_t(1) << (key_shift - 4)) - 1 : 0;
     shards_.resize(paths.size());
     for (size_t i = 0; i < paths.size(); i++) {
       shards_[i] = std::make_unique<Shard>();
       shards_[i]->path = paths[i];
+      if (key_shift > 4) {
+        if (subs[i] < 0 || uint64_t(subs[i]) > mask) throw std::invalid_argument("FragmentLoader: sub-shard out of range");
+        shards_[i]->sub = subs[i];
+        shards_[i]->sub_mask = mask;
+      }
     }
   }
 
@@ -170,7 +188,9 @@ class FragmentLoader {
           const Shard& sh = *shards_[size_t(s)];
           uint64_t prev = ~0ull;
           for (uint32_t i = 0; i < sh.keyn; i++) {
-            const uint64_t r = rd64(sh.hdr + size_t(i) * 12) >> ks_;
+            const uint64_t key = rd64(sh.hdr + size_t(i) * 12);
+            if (!sh.keep(key)) continue;
+            const uint64_t r = key >> ks_;
             if (r == prev) continue;
             prev = r;
             bits[r >> 6].fetch_or(1ull << (r & 63), std::memory_order_relaxed);
@@ -183,7 +203,9 @@ class FragmentLoader {
         for (auto& sp : shards_) {
           uint64_t prev = ~0ull;
           for (uint32_t i = 0; i < sp->keyn; i++) {
-            const uint64_t r = rd64(sp->hdr + size_t(i) * 12) >> ks_;
+            const uint64_t key = rd64(sp->hdr + size_t(i) * 12);
+            if (!sp->keep(key)) continue;
+            const uint64_t r = key >> ks_;
             if (r != prev) out.push_back(r), prev = r;
           }
         }
@@ -230,6 +252,7 @@ class FragmentLoader {
         for (uint32_t i = 0; i < sh.keyn; i++) {
           const uint8_t* h = sh.hdr + size_t(i) * 12;
           const uint64_t key = rd64(h);
+          if (!sh.keep(key)) continue;
           const int type = rd16(h + 8);
           const int64_t n = int64_t(rd16(h + 10)) + 1;
           const uint64_t r = key >> ks_;
@@ -268,6 +291,7 @@ class FragmentLoader {
         uint16_t* dst = op + base[size_t(k)];
         for (uint32_t i = 0; i < sh.keyn; i++) {
           const uint8_t* h = sh.hdr + size_t(i) * 12;
+          if (!sh.keep(rd64(h))) continue;
           const int type = rd16(h + 8);
           const int64_t n = int64_t(rd16(h + 10)) + 1;
           const uint8_t* src = sh.map + rd32(sh.offs + size_t(i) * 4);
@@ -361,8 +385,8 @@ class FragmentLoader {
     sh.hdr = sh.map + pr::HEADER_BASE;
     sh.offs = sh.hdr + size_t(keyn) * 12;
     size_t end = size_t(pr::HEADER_BASE) + size_t(keyn) * 16;
-    int64_t P = 0;
-    uint64_t prev = 0;
+    int64_t P = 0, kept = 0;
+    uint64_t prev = 0, last = 0;
     for (uint32_t i = 0; i < keyn; i++) {
       const uint8_t* h = sh.hdr + size_t(i) * 12;
       const uint64_t key = rd64(h);
@@ -387,12 +411,15 @@ class FragmentLoader {
       }
       if (off + sz > n) fail(sh, "container overruns data");
       end = off + sz;
+      if (!sh.keep(key)) continue;
       P += arena_u16(type, cn, nr);
+      kept++;
+      last = key;
     }
     if (end != n) return false;  // op log follows: replay path
-    sh.containers = keyn;
+    sh.containers = kept;
     sh.payload = P;
-    sh.last_key = keyn ? prev : 0;
+    sh.last_key = last;
     return true;
   }
 };
@@ -637,8 +664,8 @@ py::dict write_bsi_fragments(const std::string& dir, int64_t shard_lo, int64_t s
 
 void register_arena_io(py::module_& m) {
   py::class_<FragmentLoader>(m, "FragmentLoader")
-      .def(py::init<std::vector<std::string>, int, int>(), py::arg("paths"), py::arg("nthreads") = 16,
-           py::arg("key_shift") = 4)
+      .def(py::init<std::vector<std::string>, int, int, std::vector<int64_t>>(), py::arg("paths"),
+           py::arg("nthreads") = 16, py::arg("key_shift") = 4, py::arg("subs") = std::vector<int64_t>{})
       .def("scan", &FragmentLoader::scan)
       .def("rows", &FragmentLoader::rows)
       .def("fill_index", &FragmentLoader::fill_index, py::arg("slack") = 0.0, py::arg("min_slack") = 0)

@@ -309,6 +309,21 @@ Bitmap MappedBitmap::offset_range(uint64_t offset, uint64_t start, uint64_t end)
   return out;
 }
 
+Bitmap MappedBitmap::sub_shard(int key_shift, uint64_t sub) const {
+  if (key_shift < 4 || key_shift > 16) throw std::invalid_argument("sub_shard: key_shift must be in [4, 16]");
+  const uint64_t mask = (uint64_t(1) << (key_shift - 4)) - 1;
+  if (sub > mask) throw std::invalid_argument("sub_shard: sub-shard out of range");
+  Bitmap out;
+  auto rekey = [&](uint64_t k) { return ((k >> key_shift) << 4) | (k & 15); };
+  for (size_t i = 0; i < keyn_; i++) {
+    const uint64_t k = key_at(i);
+    if (((k >> 4) & mask) == sub && !touched_.count(k)) out.cs.emplace(rekey(k), load(i));
+  }
+  for (auto& kv : over_.cs)
+    if (kv.second.n && ((kv.first >> 4) & mask) == sub) out.cs[rekey(kv.first)] = kv.second;
+  return out;
+}
+
 std::vector<uint64_t> MappedBitmap::rows_with_column(uint64_t col, uint64_t cpr) const {
   const uint64_t ck = col >> 16;
   const uint16_t low = uint16_t(col & 0xffff);

@@ -530,6 +530,7 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
       .def("slice", [](const Bitmap& b) { return to_np(b.slice()); })
       .def("slice_range", [](const Bitmap& b, uint64_t s, uint64_t e) { return to_np(b.slice_range(s, e)); })
       .def("offset_range", &Bitmap::offset_range)
+      .def("sub_shard", &Bitmap::sub_shard, py::arg("key_shift"), py::arg("sub"))
       .def("intersect", &Bitmap::intersect, py::call_guard<py::gil_scoped_release>())
       .def("union", &Bitmap::unite, py::call_guard<py::gil_scoped_release>())
       .def("difference", &Bitmap::difference, py::call_guard<py::gil_scoped_release>())
@@ -697,6 +698,7 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
       .def("any", &pr::MappedBitmap::any)
       .def("max", &pr::MappedBitmap::max)
       .def("offset_range", &pr::MappedBitmap::offset_range)
+      .def("sub_shard", &pr::MappedBitmap::sub_shard, py::arg("key_shift"), py::arg("sub"))
       .def("rows_with_column", [](const pr::MappedBitmap& b, uint64_t col, uint64_t cpr) {
         return to_np(b.rows_with_column(col, cpr));
       }, py::arg("col"), py::arg("containers_per_row") = 16)

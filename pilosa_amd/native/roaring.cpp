@@ -777,6 +777,17 @@ Bitmap Bitmap::offset_range(uint64_t offset, uint64_t start, uint64_t end) const
   return out;
 }
 
+Bitmap Bitmap::sub_shard(int key_shift, uint64_t sub) const {
+  if (key_shift < 4 || key_shift > 16) throw std::invalid_argument("sub_shard: key_shift must be in [4, 16]");
+  const uint64_t mask = (uint64_t(1) << (key_shift - 4)) - 1;
+  if (sub > mask) throw std::invalid_argument("sub_shard: sub-shard out of range");
+  Bitmap out;
+  for (auto& kv : cs)
+    if (kv.second.n && ((kv.first >> 4) & mask) == sub)
+      out.cs.emplace_hint(out.cs.end(), ((kv.first >> key_shift) << 4) | (kv.first & 15), kv.second);
+  return out;
+}
+
 Bitmap Bitmap::intersect(const Bitmap& o) const {
   Bitmap out;
   auto i = cs.begin();

@@ -140,6 +140,9 @@ class Bitmap {
   std::vector<uint64_t> slice() const;
   std::vector<uint64_t> slice_range(uint64_t start, uint64_t end) const;
   Bitmap offset_range(uint64_t offset, uint64_t start, uint64_t end) const;
+  // device sub-shard `sub` of a shard wider than 2^20 columns (key = row <<
+  // key_shift | c): containers with c >> 4 == sub, re-keyed row * 16 + (c & 15)
+  Bitmap sub_shard(int key_shift, uint64_t sub) const;
   Bitmap intersect(const Bitmap& o) const;
   Bitmap unite(const Bitmap& o) const;
   Bitmap difference(const Bitmap& o) const;
@@ -195,6 +198,7 @@ class MappedBitmap {
   bool any() const;
   uint64_t max() const;
   Bitmap offset_range(uint64_t offset, uint64_t start, uint64_t end) const;
+  Bitmap sub_shard(int key_shift, uint64_t sub) const;
   std::vector<uint64_t> rows_with_column(uint64_t col, uint64_t cpr) const;
   int64_t add_many(const uint64_t* v, size_t n);     // v sorted ascending
   int64_t remove_many(const uint64_t* v, size_t n);  // v sorted ascending

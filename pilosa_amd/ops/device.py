@@ -181,6 +181,10 @@ class DeviceView:
     """One field-view's containers for a contiguous range of local shards,
     resident on one GPU."""
 
+    # container_merge / container_emit launches (device write replay); a class
+    # default so the __new__-built views (from_device, from_host_index) count too
+    write_launches = 0
+
     def __init__(self, rows, rowptr, shard_base, meta, payload, device, shards: Sequence[int] = ()):
         import torch
 
@@ -293,10 +297,13 @@ class DeviceView:
                 return False
             dense_of = dict(zip(touched, self.dense_many(np.array(touched, np.uint64)).tolist()))
         # storage positions are row * ShardWidth + column; the arena's rows are
-        # 2^20 columns wide (identity for 2^20-column shards)
+        # 2^20 columns wide (identity for 2^20-column shards); a wider shard's
+        # device sub-shard takes columns [sub * 2^20, (sub + 1) * 2^20) of it
         sw, dw, cw = shardwidth.SHARD_WIDTH, 1 << 20, 1 << 16
-        parts = [storage.offset_range(r * dw, r * sw, (r + 1) * sw) for r in sorted(rows)]
-        parts += [storage.offset_range(k * cw, shardwidth.host_key(k) * cw, (shardwidth.host_key(k) + 1) * cw)
+        sub = int(self.shards[si]) % shardwidth.DEVICE_SUBSHARDS if shardwidth.WIDE else 0
+        base, span = sub * dw, min(sw, dw)
+        parts = [storage.offset_range(r * dw, r * sw + base, r * sw + base + span) for r in sorted(rows)]
+        parts += [storage.offset_range(k * cw, shardwidth.host_key(k, sub) * cw, (shardwidth.host_key(k, sub) + 1) * cw)
                   for k in keys]
         part = _roaring.Bitmap()
         part.union_in_place(parts)
@@ -371,7 +378,8 @@ class DeviceView:
         if self._cap is None:
             return False
         from pilosa_amd import shardwidth
-        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], shardwidth.CONTAINERS_PER_ROW, 1)
+        # (a wider shard's sub-shard arrives re-keyed to 2^20 columns: ARENA_CPR)
+        rows_s, rp_s, sb_s, meta_s, pay_s = _roaring.build_arena([bitmap], shardwidth.ARENA_CPR, 1)
         n_new = int(sb_s[-1])
         if n_new > int(self._cap[si]) and not self.grow_segment(si, n_new):
             return False
@@ -824,10 +832,12 @@ class DeviceView:
     def from_bitmaps(cls, bitmaps: Sequence[Optional[object]], device, shards=(), patchable: bool = False,
                      cpr: Optional[int] = None):
         """Arena of per-shard bitmaps of shard-local positions row * ShardWidth
-        + column (``cpr`` containers per row, default the shard width's)."""
+        + column (``cpr`` containers per row, default the shard width's; a
+        wider shard's sub-shards arrive re-keyed to 2^20 columns,
+        ``Bitmap.sub_shard``)."""
         from pilosa_amd import _roaring, shardwidth
 
-        cpr = shardwidth.CONTAINERS_PER_ROW if cpr is None else int(cpr)
+        cpr = shardwidth.ARENA_CPR if cpr is None else int(cpr)
         rows, rowptr, sb, meta, payload = _roaring.build_arena(list(bitmaps), cpr, 8)
         if patchable:
             return cls.patchable(rows, rowptr, sb, meta, payload, device, shards)
@@ -1290,7 +1300,7 @@ class GpuEngine:
         pay = outp.cpu().numpy().view(np.uint16)
         shards = views[0].shards
         from pilosa_amd import shardwidth
-        cpr = shardwidth.CONTAINERS_PER_ROW
+        cpr = shardwidth.ARENA_CPR   # device shard ids: global key = shard * cpr + slot
         result = []
         for s in range(S):
             cs = c[s * 16:(s + 1) * 16]
@@ -1386,7 +1396,7 @@ class GpuEngine:
             self.ext.rows_list(vd, 0, view.S, -1, 0, flags)
         else:
             from pilosa_amd import shardwidth
-            shard, off = divmod(int(column), shardwidth.SHARD_WIDTH)
+            shard, off = divmod(int(column), shardwidth.ARENA_WIDTH)   # device shard
             if shard not in view.shards:
                 return np.zeros(0, np.uint64)
             si = view.shards.index(shard)

@@ -29,6 +29,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from pilosa_amd import shardwidth
 from pilosa_amd.errors import PilosaError
 from pilosa_amd.utils import tracing
 from pilosa_amd.models.cache import Pair, sort_pairs
@@ -64,9 +65,77 @@ def _delta_keys(deltas) -> set:
     return out
 
 
+class SubFragment:
+    """Device sub-shard ``sub`` of a fragment wider than the device shard
+    (shard width 2^21..2^32, pilosa_amd/shardwidth.py): what the arena
+    builder reads of a fragment -- lock, version, file, dirty rows -- with
+    its own dirty subscription per sub-shard and only the container keys of
+    its sub-shard.  Write batches are not replayed on the device at these
+    widths: their containers are rebuilt from the storage instead."""
+    __slots__ = ("frag", "sub")
+
+    def __init__(self, frag, sub: int):
+        self.frag = frag
+        self.sub = int(sub)
+
+    @property
+    def mu(self):
+        return self.frag.mu
+
+    @property
+    def version(self):
+        return self.frag.version
+
+    @property
+    def path(self):
+        return self.frag.path
+
+    @property
+    def storage(self):
+        return self.frag.storage
+
+    def is_cold(self) -> bool:
+        return self.frag.is_cold()
+
+    def device_storage(self):
+        """This sub-shard's containers re-keyed to the arena (row * 16 + slot)."""
+        return self.frag.storage.sub_shard(shardwidth.KEY_SHIFT, self.sub)
+
+    def take_dirty(self, token):
+        d = self.frag.take_dirty((token, self.sub))
+        if d is None:
+            return None
+        rows, keys, deltas = d
+        keys = set(keys) | _delta_keys(deltas)
+        return rows, {k for k in keys if shardwidth.sub_of_key(k) == self.sub}, []
+
+    def drop_dirty(self, token):
+        self.frag.drop_dirty((token, self.sub))
+
+
+def _device_frags(v, shards) -> list:
+    """The arena's per-device-shard fragments of holder view ``v`` for host
+    ``shards`` (sub-shard proxies above 2^20 columns)."""
+    if not shardwidth.WIDE:
+        return [v.fragment(s) for s in shards]
+    out = []
+    for s in shards:
+        f = v.fragment(s)
+        out.extend(SubFragment(f, i) if f is not None else None for i in range(shardwidth.DEVICE_SUBSHARDS))
+    return out
+
+
+def _fid(f) -> int:
+    """Identity of the fragment behind an arena shard (proxies are per call)."""
+    return id(f.frag) if isinstance(f, SubFragment) else id(f)
+
+
+def _dev_storage(f):
+    return f.device_storage() if isinstance(f, SubFragment) else f.storage
+
+
 class GpuExecutor:
     def __init__(self, holder, device="cuda:0", executor=None, hbm_budget: int = 0):
-        from pilosa_amd import shardwidth
         if not shardwidth.device_supported():
             raise NotImplementedError(f"device arenas hold shards of 2^{shardwidth.MIN_EXPONENT}.."
                                       f"2^{shardwidth.DEVICE_EXPONENT} columns "
@@ -123,8 +192,8 @@ class GpuExecutor:
         v = self.holder.view(index, field, view)
         if v is None:
             return None
-        frags = [v.fragment(s) for s in shards]
-        sig = tuple((id(f), f.version) if f is not None else None for f in frags)
+        frags = _device_frags(v, shards)
+        sig = tuple((_fid(f), f.version) if f is not None else None for f in frags)
         with self.mu:
             self._arena_epoch[key] = epoch
             hit = self._arenas.get(key)
@@ -154,7 +223,7 @@ class GpuExecutor:
                         ok = False
                         break
                     with f.mu:
-                        dirty = f.take_dirty(dv.token) if old is not None and old[0] == id(f) else None
+                        dirty = f.take_dirty(dv.token) if old is not None and old[0] == _fid(f) else None
                     if dirty is None:
                         whole.append(si)
                         continue
@@ -187,7 +256,7 @@ class GpuExecutor:
                     f = frags[si]
                     with f.mu:
                         f.take_dirty(dv.token)
-                        ok = dv.update_shard(si, f.storage)
+                        ok = dv.update_shard(si, _dev_storage(f))
                     if not ok:
                         break
                     self.shard_updates += 1
@@ -200,8 +269,9 @@ class GpuExecutor:
                         f.drop_dirty(hit[1].token)
             token = object()  # dirty-row subscription of the new arena
             self._evict_for(key)
+            dshards = shardwidth.device_shards(shards)
             with tracing.span("GpuExecutor.loadView", gpu=True, field=field, view=view, shards=len(shards)):
-                dv = self._load_cold(frags, shards, token, key) if self.file_loader else None
+                dv = self._load_cold(frags, dshards, token, key) if self.file_loader else None
             if dv is None:
                 bms = []
                 for f in frags:
@@ -210,8 +280,8 @@ class GpuExecutor:
                     else:
                         with f.mu:
                             f.take_dirty(token)  # register before the contents are read
-                            bms.append(f.storage)
-                dv = DeviceView.from_bitmaps(bms, self.device, shards=list(shards), patchable=True)
+                            bms.append(_dev_storage(f))
+                dv = DeviceView.from_bitmaps(bms, self.device, shards=dshards, patchable=True)
             dv.token = token
             self.rebuilds += 1
             self._arenas[key] = (sig, dv)
@@ -239,8 +309,9 @@ class GpuExecutor:
             for f in live:
                 f.take_dirty(token)
             info: Dict = {}
+            subs = [f.sub if f is not None else 0 for f in frags] if shardwidth.WIDE else None
             dv = load_view([f.path if f is not None else "" for f in frags], shards, self.device, patchable=True,
-                           stats=info)
+                           stats=info, subs=subs)
         self.cold_loads += 1
         self.last_load = dict(info, view=list(key[:3]))
         return dv
@@ -261,8 +332,7 @@ class GpuExecutor:
         v = self.holder.view(key[0], key[1], key[2])
         if v is None or getattr(dv, "token", None) is None:
             return
-        for s in key[3]:
-            f = v.fragment(s)
+        for f in _device_frags(v, key[3]):
             if f is not None:
                 f.drop_dirty(dv.token)
 
@@ -811,6 +881,8 @@ class GpuExecutor:
                 cnt[found] = m[first[found], np.nonzero(found)[0]]
                 open_ &= ~found
                 lo, chunk = hi, chunk * 4
+        if shardwidth.WIDE:
+            rid, cnt = _fold_subshards(rid, cnt, is_min, filtered=len(c.children) == 1)
         out = None
         for r, n_ in zip(rid.tolist(), cnt.tolist()):
             v = Pair(r, n_)
@@ -896,6 +968,9 @@ class GpuExecutor:
         NotImplementedError for the shapes the host answers (Tanimoto and
         attribute filters: per-row attribute reads)."""
         ex = self._ex()
+        if shardwidth.WIDE:
+            # rank caches are per (wide) fragment; the device ranks per 2^20 sub-shard
+            raise NotImplementedError
         fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
         if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
             raise NotImplementedError
@@ -939,6 +1014,9 @@ class GpuExecutor:
         ``defer`` (with ``self.comm``): a pending result whose last
         collectives are still in flight (parallel/collectives.Pending)."""
         ex = self._ex()
+        if shardwidth.WIDE:
+            self.topn_decline = f"shard width 2^{shardwidth.EXPONENT}"
+            return None
         params = []
         fields: Dict[str, Tuple] = {}
         for c in calls:
@@ -1010,7 +1088,7 @@ class GpuExecutor:
         builds) what it needs -- rank caches, slot index -- without any
         collective, so the ranks of a node can agree on the answer first
         (parallel/mesh.py OP_TOPN)."""
-        if not shards:
+        if not shards or shardwidth.WIDE:
             return False
         ex = self._ex()
         try:
@@ -1402,6 +1480,22 @@ class GpuExecutor:
             return rows
         lo = start[len(prefix)]
         return [r for r in rows if r >= lo]
+
+
+def _fold_subshards(rid: np.ndarray, cnt: np.ndarray, is_min: bool, filtered: bool):
+    """Per-device-shard MinRow/MaxRow pairs -> per host shard (shards wider
+    than 2^20 columns): the first (last) row over the shard's sub-shards,
+    with the filtered count summed over the sub-shards that found it."""
+    M = shardwidth.DEVICE_SUBSHARDS
+    r, c = rid.reshape(-1, M), cnt.reshape(-1, M)
+    big = np.iinfo(np.int64).max
+    live = c > 0
+    key = np.where(live, r, big if is_min else -1)
+    best = key.min(axis=1) if is_min else key.max(axis=1)
+    hit = live & (r == best[:, None])
+    n = (np.where(hit, c, 0).sum(axis=1) if filtered else hit.any(axis=1).astype(np.int64))
+    ok = live.any(axis=1)
+    return np.where(ok, best, 0), np.where(ok, n, 0)
 
 
 def _minmax_per_shard(o: np.ndarray, which: str):

@@ -28,9 +28,11 @@ PAYLOAD_SLACK, PAYLOAD_MIN_SLACK_U16 = 0.25, 8 << 20
 
 def load_view(paths: Sequence[str], shards: Sequence[int], device, patchable: bool = True,
               nthreads: Optional[int] = None, chunk_bytes: int = 256 << 20,
-              stats: Optional[Dict] = None) -> DeviceView:
+              stats: Optional[Dict] = None, subs: Optional[Sequence[int]] = None) -> DeviceView:
     """Build a :class:`DeviceView` over ``shards`` from their fragment files
-    (``""`` or a missing path = empty shard)."""
+    (``""`` or a missing path = empty shard).  Above 2^20 columns per shard
+    ``shards`` are device shard ids and ``subs[i]`` the sub-shard of
+    ``paths[i]`` that arena shard i holds (pilosa_amd/shardwidth.py)."""
     import torch
 
     from pilosa_amd import _roaring
@@ -40,7 +42,10 @@ def load_view(paths: Sequence[str], shards: Sequence[int], device, patchable: bo
     device = torch.device(device)
     t0 = time.perf_counter()
     from pilosa_amd import shardwidth
-    ld = _roaring.FragmentLoader([p or "" for p in paths], int(nthreads), shardwidth.KEY_SHIFT)
+    if shardwidth.WIDE and subs is None:
+        raise ValueError(f"load_view: shard width 2^{shardwidth.EXPONENT} needs the sub-shard of every path")
+    ld = _roaring.FragmentLoader([p or "" for p in paths], int(nthreads), shardwidth.KEY_SHIFT,
+                                 [int(x) for x in subs] if shardwidth.WIDE else [])
     info = ld.scan()
     rows = ld.rows()
     t_scan = time.perf_counter()

@@ -21,7 +21,10 @@ The per-shard lists are ranked on the device (count desc, id asc) into
 slot index (ops/topn_index.py).  A batch of TopN calls is answered with both
 phases on the device: phase 1 as one scatter-add of every query's per-shard
 cache prefixes, phase 2 (``ids=``) as ``row_counts_sum_kernel`` over the
-candidates, and only the trimmed ``Q x n`` pairs cross to the host.
+candidates, and only the trimmed ``Q x n`` pairs cross to the host.  On one
+rank the whole batch is the three ``topn_cache_*`` kernels
+(``_topn_nosrc_fused``): membership, per-threshold totals from a memoised
+candidate x shard count matrix, and a per-query LDS bitonic top-n.
 """
 from __future__ import annotations
 
@@ -35,6 +38,8 @@ from .device import DeviceView, kernels
 
 # queries per cache-only phase-1 accumulator (Q x D int32 scratch)
 NOSRC_CHUNK = 64
+# largest [candidate x shard] count matrix the fused cache-only path memoises
+FUSED_MAX_CELLS = 1 << 25
 
 
 def rows_dev(view: DeviceView):
@@ -246,7 +251,8 @@ class DeviceRankCaches:
         if Q == 0:
             return []
         if comm is None and self.view.D and self.S < 2048:   # counts < 2^31: composite int64 key
-            return self._topn_nosrc_dense(ns, thresholds)
+            got = self._topn_nosrc_fused(ns, thresholds)
+            return got if got is not None else self._topn_nosrc_dense(ns, thresholds)
         pq, pd, _ = self.nosrc_phase1(ns, thresholds)
         if comm is None:
             out = self.recount(pq, pd, thresholds)
@@ -276,6 +282,72 @@ class DeviceRankCaches:
             got = (u, inv.reshape(-1))
             memo[nmax] = got
         return got
+
+    def _fused_memo(self, nmax: int):
+        """(u int32[U], inv int32[S*nmax], cm int32[U, S]) for a prefix length:
+        the candidate rows, each rank's candidate index and every candidate's
+        count in every shard.  Fixed for this object (rebuilt when the view's
+        generation moves), so a batch pays none of it after the first."""
+        import torch
+        memo = self.__dict__.setdefault("_fused", {})
+        got = memo.get(nmax)
+        if got is None:
+            u, inv = self._candidates(nmax)
+            U = int(u.numel())
+            if U * self.S > FUSED_MAX_CELLS:
+                got = False
+            else:
+                u32 = u.to(torch.int32).contiguous()
+                cm = torch.empty((U, self.S), dtype=torch.int32, device=self.view.device)
+                kernels().topn_cache_counts(self.view.viewdev_tensor(), self.S, u32, cm)
+                got = (u32, inv.to(torch.int32).contiguous(), cm)
+            memo[nmax] = got
+        return got
+
+    def _topn_nosrc_fused(self, ns: Sequence[int], thresholds: Sequence[int]) -> Optional[List[List[Pair]]]:
+        """Cache-only TopN batch in three hand-written kernels
+        (kernels/topn_kernels.hip topn_cache_*): membership of every query's
+        cache prefixes, one total per (distinct threshold, candidate) from the
+        memoised count matrix, and a per-query LDS bitonic top-n.  One H2D of
+        the batch parameters, one D2H of the Q x n keys.  None when the
+        candidate set is too large for it (the torch path then runs)."""
+        import torch
+        Q = len(ns)
+        nn = [int(n) for n in ns]
+        nmax = self.K if any(n == 0 for n in nn) else min(self.K, max(nn))
+        if not nmax:
+            return [[] for _ in range(Q)]
+        memo = self._fused_memo(nmax)
+        if memo is False:
+            return None
+        u32, inv32, cm = memo
+        U = int(u32.numel())
+        dev = self.view.device
+        ths = [max(1, int(t)) for t in thresholds]
+        uniq_t = sorted(set(ths))
+        KK = min(U, max(nn)) if all(nn) else U
+        prm = np.empty(4 * Q + len(uniq_t), np.int32)
+        prm[:Q] = [n if n else self.K for n in nn]
+        prm[Q:2 * Q] = ths
+        prm[2 * Q:3 * Q] = [uniq_t.index(t) for t in ths]
+        prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
+        prm[4 * Q:] = uniq_t
+        prm_d = torch.from_numpy(prm).to(dev, non_blocking=True)
+        member = torch.zeros((Q, U), dtype=torch.uint8, device=dev)
+        tot = torch.empty((len(uniq_t), U), dtype=torch.int64, device=dev)
+        out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
+        kernels().topn_cache_batch(self.cache_cnt, nmax, inv32, u32, cm, prm_d, Q, len(uniq_t), member, tot, out)
+        h = out.cpu().numpy()
+        if (h[:, 0] < 0).any():     # a query with more members than one workgroup sorts
+            return None
+        rows = self.view.rows
+        res: List[List[Pair]] = []
+        for q in range(Q):
+            r = h[q, 1:1 + int(h[q, 0])]
+            d = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
+            ids = rows[d] if len(d) else np.zeros(0, np.uint64)
+            res.append([Pair(int(i), int(c)) for i, c in zip(ids.tolist(), (r >> 32).tolist())])
+        return res
 
     def _topn_nosrc_dense(self, ns: Sequence[int], thresholds: Sequence[int]) -> List[List[Pair]]:
         """Single-rank cache-only TopN batch without a host round trip until

@@ -12,9 +12,14 @@ containers per row) maps onto them one to one: its containers fill the first
 2^(e-16) slots of each row, container keys are translated at the host/device
 boundary (``device_key`` / ``host_key``: the loader, build_arena, the write
 replay, row results) and a shard's columns stay ``shard * ShardWidth + x``.
-Wider shards (21..32) would need several device shards per shard; a node
-with such a width answers from the host roaring path (server.Server disables
-the GPU executor and says so in its log).
+A wider shard (exponent 21..32) is split into ``DEVICE_SUBSHARDS`` =
+2^(e-20) device sub-shards of 2^20 columns: host shard s becomes device
+shards s*M .. s*M + M-1 (``device_shards``), container c of a row goes to
+sub-shard c >> 4, arena slot c & 15.  Global columns then stay
+``device_shard * 2^20 + x``, so every kernel, row result and per-shard count
+works unchanged on device shard ids; the GPU executor maps host shards to
+device shards at the arena boundary (ops/gpu_executor.py ``SubFragment``) and
+the native file loader reads one sub-shard of a file per arena shard.
 """
 from __future__ import annotations
 
@@ -43,22 +48,47 @@ CONTAINERS_PER_ROW = SHARD_WIDTH >> 16
 
 KEY_SHIFT = EXPONENT - 16   # log2(containers per row)
 
+# device shards per shard (2^(e-20) above 2^20 columns, else 1), the arena's
+# columns per device shard and its containers per row
+DEVICE_SUBSHARDS = 1 << max(0, EXPONENT - DEVICE_EXPONENT)
+WIDE = DEVICE_SUBSHARDS > 1
+ARENA_WIDTH = min(SHARD_WIDTH, 1 << DEVICE_EXPONENT)
+ARENA_CPR = ARENA_WIDTH >> 16
+
 
 def device_supported() -> bool:
-    """True when the GPU arenas can hold this shard width (2^16..2^20)."""
-    return MIN_EXPONENT <= EXPONENT <= DEVICE_EXPONENT
+    """True when the GPU arenas can hold this shard width: 2^16..2^20 map one
+    to one, wider shards as 2^(e-20) device sub-shards each."""
+    return MIN_EXPONENT <= EXPONENT <= MAX_EXPONENT
+
+
+def device_shards(shards):
+    """Host shard ids -> the device shard ids of the arena (identity up to 2^20)."""
+    if not WIDE:
+        return [int(s) for s in shards]
+    M = DEVICE_SUBSHARDS
+    return [int(s) * M + i for s in shards for i in range(M)]
 
 
 def device_key(k):
-    """Host container key (row << KEY_SHIFT | j) -> arena key (row * 16 + j).
+    """Host container key (row << KEY_SHIFT | j) -> arena key (row * 16 + j;
+    above 2^20 columns j is the slot within the key's sub-shard, c & 15).
     Works on ints and uint64 numpy arrays."""
     if KEY_SHIFT == 4:
         return k
-    return ((k >> KEY_SHIFT) << 4) | (k & (CONTAINERS_PER_ROW - 1))
+    return ((k >> KEY_SHIFT) << 4) | (k & (ARENA_CPR - 1))
 
 
-def host_key(k):
-    """Arena key (row * 16 + j, j < CONTAINERS_PER_ROW) -> host container key."""
+def sub_of_key(k):
+    """Device sub-shard of a host container key (0 up to 2^20 columns)."""
+    return (k >> 4) & (DEVICE_SUBSHARDS - 1) if WIDE else 0 * k
+
+
+def host_key(k, sub: int = 0):
+    """Arena key (row * 16 + j, j < ARENA_CPR) of sub-shard ``sub`` -> host
+    container key."""
     if KEY_SHIFT == 4:
         return k
+    if WIDE:
+        return ((k >> 4) << KEY_SHIFT) | (sub << 4) | (k & 15)
     return ((k >> 4) << KEY_SHIFT) | (k & 15)

@@ -1,8 +1,11 @@
-"""Device arenas at shard widths narrower than the device shard (2^16 and
-2^18 columns, reference shardwidth/16.go..20.go): the GPU executor's
+"""Device arenas at shard widths other than the device shard's 2^20 columns
+(reference shardwidth/16.go..32.go): narrower (2^16, 2^18): the GPU executor's
 differential suite and the executor-path TopN suite run unchanged at that
 width in a fresh interpreter (the width is fixed per process, like the
 reference's build tag), every answer compared with the host executor.
+Wider (2^22, the reference CI's SHARD_WIDTH=22): every shard is 4 device
+sub-shards and the executor differential suite runs unchanged (TopN answers
+from the host at these widths: rank caches are per wide fragment).
 Shift is excluded: its device carry works at 2^20 columns only, so at
 other widths it runs on the host (ops/gpu_executor.py)."""
 import os
@@ -22,6 +25,17 @@ def test_gpu_suites_at_narrow_width(exp):
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
                         "--timeout", "300", "--timeout-method", "thread", "-k", "not shift and not Shift",
                         "tests/test_gpu_executor.py", "tests/test_gpu_topn_exec.py"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=850)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and "skipped" not in r.stdout.splitlines()[-1], r.stdout[-1000:]
+
+
+@pytest.mark.timeout(900)
+def test_gpu_executor_suite_at_wide_width():
+    env = dict(os.environ, PILOSA_SHARD_WIDTH="22")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        "--timeout", "300", "--timeout-method", "thread", "-k", "not shift and not Shift",
+                        "tests/test_gpu_executor.py"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=850)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert " passed" in r.stdout and "skipped" not in r.stdout.splitlines()[-1], r.stdout[-1000:]

@@ -173,6 +173,33 @@ def test_nosrc_dense_batch_equals_two_phase(lazy_env):
     assert _pairs(got[0]) == _pairs(want["TopN(h, n=10)"])
 
 
+def test_nosrc_fused_kernels_equal_torch_batch(lazy_env, monkeypatch):
+    """The hand-written cache-only batch (topn_cache_member / totals / select
+    kernels) answers exactly as the torch batch and the two-phase reference,
+    for mixed n (0 = all, n beyond the cache width) and thresholds; the
+    executor's TopN runs through it; an oversized candidate set declines to
+    the torch batch."""
+    from pilosa_amd.ops import topn_exec
+    from pilosa_amd.ops.topn_index import finish_batch_dev
+    holder, ex, gpu, want, _ = lazy_env
+    ex.execute("i", "TopN(h, n=10)")
+    rc = next(iter(gpu._rank_cache_map.values()))[1]
+    ns = [10, 100, 0, 20, 1, 7, 100, 3, rc.K + 500, 50, 50]
+    ths = [1, 1, 1, 300, 1, 2, 50, 1, 1, 5000, 20]
+    got = rc._topn_nosrc_fused(ns, ths)
+    assert got is not None
+    dense = rc._topn_nosrc_dense(ns, ths)
+    pq, pd, _ = rc.nosrc_phase1(ns, ths)
+    ref = finish_batch_dev(rc.view.rows, len(ns), pq, pd, rc.recount(pq, pd, ths), ns)
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in dense] == [_pairs(r) for r in ref]
+    assert _pairs(got[0]) == _pairs(want["TopN(h, n=10)"])
+    assert rc.__dict__.get("_fused"), "fused memo never built"
+    rc.__dict__.pop("_fused", None)
+    monkeypatch.setattr(topn_exec, "FUSED_MAX_CELLS", 0)
+    assert rc._topn_nosrc_fused(ns, ths) is None
+    assert [_pairs(r) for r in rc.topn_nosrc(ns, ths)] == [_pairs(r) for r in ref]
+
+
 def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
     """A write burst into one shard (new bits, and a tail row pushed up the
     rank order) re-indexes only that shard's slot region in place: the next
