@@ -92,6 +92,7 @@ def cmd_server(args, stdout, stderr) -> int:
                                                                          not cfg.get("cluster.coordinator")
                                                                          else None),
                  gpu=cfg.get("gpu.mode"), workers=cfg.get("worker-pool-size"),
+                 allowed_origins=list(cfg.get("handler.allowed-origins") or []),
                  max_writes=cfg.get("max-writes-per-request"),
                  anti_entropy_interval=cfg.duration("anti-entropy.interval"),
                  probe_interval=cfg.duration("gossip.probe-interval"),

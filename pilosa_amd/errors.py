@@ -44,6 +44,25 @@ def _e(msg):
     return PilosaError(msg)
 
 
+def cause(err: BaseException) -> BaseException:
+    """errors.Cause: the innermost error behind :func:`wrap` layers."""
+    while getattr(err, "cause", None) is not None and err.cause is not err:
+        err = err.cause
+    return err
+
+
+def wrap(err: BaseException, prefix: str) -> PilosaError:
+    """errors.Wrap: ``"<prefix>: <err>"`` of the same class (so the same HTTP
+    status), with the original reachable through :func:`cause`."""
+    cls = type(err) if isinstance(err, PilosaError) else PilosaError
+    out = cls.__new__(cls)
+    Exception.__init__(out, f"{prefix}: {err}")
+    if hasattr(err, "err"):
+        out.err = err.err
+    out.cause = err
+    return out
+
+
 ErrHostRequired = _e("host required")
 ErrIndexRequired = _e("index required")
 ErrIndexExists = _e("index already exists")

@@ -23,7 +23,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 from pilosa_amd import _roaring
 from pilosa_amd.errors import (BadRequestError, ErrBSIGroupNotFound, ErrFieldNotFound, ErrIndexNotFound,
-                               ErrIndexRequired, ErrTooManyWrites, PilosaError)
+                               ErrIndexRequired, ErrTooManyWrites, PilosaError, wrap)
 from pilosa_amd.models.cache import Pair, pairs_add, sort_pairs
 from pilosa_amd.models.field import FIELD_TYPE_BOOL, FIELD_TYPE_INT, FIELD_TYPE_SET, FIELD_TYPE_TIME
 from pilosa_amd.models.fragment import FALSE_ROW_ID, SHARD_WIDTH, TRUE_ROW_ID, TopOptions
@@ -746,8 +746,11 @@ class Executor:
             return prev
 
         local = (lambda ss: self.gpu.bitmap(index, c, ss)) if self.gpu is not None else None
-        row = self.map_reduce(index, shards, c, opt, lambda s: self.bitmap_call_shard(index, c, s), reduce_fn,
-                              local) or Row()
+        try:
+            row = self.map_reduce(index, shards, c, opt, lambda s: self.bitmap_call_shard(index, c, s), reduce_fn,
+                                  local) or Row()
+        except PilosaError as e:
+            raise wrap(e, "map reduce") from e   # executor.go:606
         if c.name == "Row" and not c.has_condition_arg():
             if opt.exclude_row_attrs:
                 row.attrs = {}

@@ -128,11 +128,9 @@ class FieldOptions:
             o.cache_size = int(d.get("cacheSize", DEFAULT_CACHE_SIZE))
             o.keys = bool(d.get("keys", False))
         elif t == FIELD_TYPE_INT:
-            if "min" not in d:
-                raise PilosaError("min is required for field type int")
-            if "max" not in d:
-                raise PilosaError("max is required for field type int")
-            o.min, o.max = int(d["min"]), int(d["max"])
+            # an absent bound is unbounded (http/handler.go:774-782)
+            o.min = int(d["min"]) if "min" in d else -(1 << 63)
+            o.max = int(d["max"]) if "max" in d else (1 << 63) - 1
             if o.min > o.max:
                 raise PilosaError("int field min cannot be greater than max")
             o.keys = bool(d.get("keys", False))

@@ -64,6 +64,7 @@ struct Req {
   int ncalls = 0;
   std::string method, path, query, index, body;
   std::vector<std::pair<std::string, std::string>> headers;
+  std::string cors;   // CORS response headers when the Origin is allowed (else empty)
 };
 
 struct Conn : std::enable_shared_from_this<Conn> {
@@ -149,7 +150,7 @@ static std::string make_response(int status, const std::string& ctype, const cha
   }
   r += "Content-Length: ";
   r += std::to_string(n);
-  r += "\r\nAccess-Control-Allow-Origin: *\r\n";
+  r += "\r\n";
   if (extra) r += extra;
   if (close) r += "Connection: close\r\n";
   r += "\r\n";
@@ -411,9 +412,9 @@ class Server {
     size_t k = 0;
     std::string body;
     for (size_t i = 0; i < ids.size(); i++) {
-      body.assign("{\"results\": [");
+      body.assign("{\"results\":[");   // Go's encoding/json: no spaces
       for (int c = 0; c < ncalls[i]; c++, k++) {
-        if (c) body += ", ";
+        if (c) body += ",";
         body += std::to_string(counts[k]);
       }
       body += "]}\n";
@@ -422,6 +423,9 @@ class Server {
   }
 
   void set_count_batching(bool on) { count_batching_ = on; }
+
+  // origins allowed by CORS (set before start())
+  void set_cors(const std::vector<std::string>& origins) { cors_origins_ = origins; }
 
   // A fixed 200 response for (method, path) with no query string, served by
   // the epoll workers without a round trip through Python.
@@ -483,7 +487,8 @@ class Server {
       c->busy = false;
       return;
     }
-    c->ready.emplace(r->seq, std::make_pair(make_response(status, ctype, body.data(), body.size(), r->close_after),
+    c->ready.emplace(r->seq, std::make_pair(make_response(status, ctype, body.data(), body.size(), r->close_after,
+                                                          r->cors.empty() ? nullptr : r->cors.c_str()),
                                             r->close_after));
     drain_ready(*c);
     flush(*c);
@@ -680,7 +685,7 @@ class Server {
       bool chunked = false, expect100 = false;
       size_t clen = 0;
       bool has_len = false, bad_len = false;
-      std::string ctype, accept;
+      std::string ctype, accept, origin, preflight;
       for (size_t p = le + 2; p < he;) {
         size_t e = c.in.find("\r\n", p);
         if (e == std::string::npos || e > he) e = he;
@@ -704,6 +709,10 @@ class Server {
             ctype = v;
           } else if (ieq(k, "accept")) {
             accept = v;
+          } else if (ieq(k, "origin")) {
+            origin = v;
+          } else if (ieq(k, "access-control-request-method")) {
+            preflight = v;
           }
           r->headers.emplace_back(std::move(k), std::move(v));
         }
@@ -806,10 +815,16 @@ class Server {
       r->seq = c.next_seq++;
       r->close_after = !keep;
       requests_++;
-      if (r->method == "OPTIONS") {
-        native_reply(c, r->seq, 200, "", r->close_after,
-                     "Access-Control-Allow-Methods: GET, POST, DELETE, PATCH, OPTIONS\r\n"
-                     "Access-Control-Allow-Headers: Content-Type, Accept\r\n");
+      // CORS (http/handler.go OptHandlerAllowedOrigins): only for configured
+      // origins; a preflight from one is answered here, any other OPTIONS goes
+      // to the route table (405 / 404, as without CORS)
+      if (!origin.empty() && !cors_origins_.empty() &&
+          std::find(cors_origins_.begin(), cors_origins_.end(), origin) != cors_origins_.end())
+        r->cors = "Access-Control-Allow-Origin: " + origin + "\r\nVary: Origin\r\n";
+      if (r->method == "OPTIONS" && !r->cors.empty() && !preflight.empty()) {
+        const std::string extra = r->cors + "Access-Control-Allow-Methods: " + preflight +
+                                  "\r\nAccess-Control-Allow-Headers: Content-Type\r\n";
+        native_reply(c, r->seq, 200, "", r->close_after, extra.c_str());
         continue;
       }
       if (r->query.empty() && !statics_empty_.load()) {
@@ -824,7 +839,8 @@ class Server {
         }
         if (hit) {
           c.ready.emplace(r->seq, std::make_pair(make_response(200, hit_ct, hit_body.data(), hit_body.size(),
-                                                               r->close_after, nullptr),
+                                                               r->close_after,
+                                                               r->cors.empty() ? nullptr : r->cors.c_str()),
                                                  r->close_after));
           drain_ready(c);
           flush(c);
@@ -882,6 +898,7 @@ class Server {
   int lfd_ = -1, port_ = 0, nthreads_;
   size_t max_body_;
   std::atomic<bool> running_{false}, stopping_{false}, count_batching_{true}, statics_empty_{true};
+  std::vector<std::string> cors_origins_;
   std::mutex smu_;
   std::unordered_map<std::string, std::pair<std::string, std::string>> statics_;
   std::vector<std::thread> workers_;
@@ -1085,6 +1102,7 @@ PYBIND11_MODULE(_httpd, m) {
       .def("respond", &httpd::Server::respond)
       .def("respond_counts", &httpd::Server::respond_counts)
       .def("set_count_batching", &httpd::Server::set_count_batching)
+      .def("set_cors", &httpd::Server::set_cors, py::arg("origins"))
       .def("set_static", &httpd::Server::set_static, py::arg("method"), py::arg("path"), py::arg("content_type"),
            py::arg("body"))
       .def("stats", &httpd::Server::stats);

@@ -7,6 +7,7 @@ panic recovery (:323) mirror the reference.
 """
 from __future__ import annotations
 
+import base64
 import json
 import re
 import socket
@@ -17,10 +18,11 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Callable, Dict, List, Optional, Tuple
 from urllib.parse import parse_qs, urlparse
 
+from pilosa_amd.utils import gojson
 from pilosa_amd import _roaring
 from pilosa_amd.errors import (APIMethodNotAllowedError, BadRequestError, ConflictError, ErrClusterDoesNotOwnShard,
                                ErrFieldNotFound, ErrFragmentNotFound, ErrIndexNotFound, ErrTooManyWrites,
-                               NotFoundError, PilosaError)
+                               ErrNodeNotCoordinator, ErrResizeNotRunning, NotFoundError, PilosaError, cause)
 from pilosa_amd.models.field import FieldOptions
 from pilosa_amd.server.api import QueryRequest
 from pilosa_amd.server.encoding import response_to_json, response_to_pb
@@ -69,6 +71,7 @@ class Handler:
         self.server = server
         self.logger = logger
         self.stats = stats
+        self.allowed_origins: List[str] = []   # CORS (http/handler.go OptHandlerAllowedOrigins)
         self.routes: List[Tuple[str, re.Pattern, Callable, str]] = []
         r = self._route
         r("GET", r"/", self.home, "Home")
@@ -147,13 +150,15 @@ class Handler:
         if spec is None:
             return
         required, optional = spec
+        # the reference answers with a JSON error body through http.Error
+        # (http/handler.go queryArgValidator)
         for k in required:
             if k not in req.query:
-                raise HTTPError(400, f"{k} is required")
+                raise HTTPError(400, gojson.dumps({"error": f"{k} is required"}))
         allowed = set(required) | set(optional)
         for k in req.query:
             if k not in allowed:
-                raise HTTPError(400, f"{k} is not a valid argument")
+                raise HTTPError(400, gojson.dumps({"error": f"{k} is not a valid argument"}))
 
     # ------------------------------------------------------------ helpers
     @staticmethod
@@ -175,7 +180,7 @@ class Handler:
         if err is None:
             req.send_json({"success": True})
             return
-        req.send(_status_for(err), json.dumps({"success": False, "error": {"message": str(err)}}) + "\n",
+        req.send(_status_for(err), gojson.encode_line({"success": False, "error": {"message": str(err)}}),
                  "text/plain; charset=utf-8")
 
     # ------------------------------------------------------------ handlers
@@ -185,7 +190,7 @@ class Handler:
 
     def get_schema(self, req):
         self._require_json(req)
-        req.send_json({"indexes": self.api.schema()})
+        req.send_json({"indexes": self.api.schema() or None})   # Go: a nil slice encodes as null
 
     def post_schema(self, req):
         try:
@@ -309,7 +314,7 @@ class Handler:
         try:
             resp = self.api.query(qr)
         except PilosaError as e:
-            status = 413 if str(e) == str(ErrTooManyWrites) else 400
+            status = 413 if str(cause(e)) == str(ErrTooManyWrites) else 400
             if isinstance(e, APIMethodNotAllowedError):
                 status = 405
             self._write_query_error(req, status, e)
@@ -318,13 +323,13 @@ class Handler:
             self._write_query_error(req, 400, e)
             return
         if self._accept_json(req):
-            req.send(200, json.dumps(response_to_json(resp)) + "\n", JSON)
+            req.send(200, gojson.encode_line(response_to_json(resp)), JSON)
         else:
             req.send(200, response_to_pb(resp, getattr(resp, "calls", None)), "application/protobuf")
 
     def _write_query_error(self, req, status, err):
         if self._accept_json(req):
-            req.send(status, json.dumps({"error": str(err)}) + "\n", JSON)
+            req.send(status, gojson.encode_line({"error": str(err)}), JSON)
         else:
             req.send(status, pb.QueryResponse(Err=str(err)).SerializeToString(), "application/protobuf")
 
@@ -372,6 +377,8 @@ class Handler:
                                     remote=req.query.get("remote") == "true")
         except NotFoundError as e:
             raise HTTPError(404, str(e))
+        except BadRequestError as e:
+            raise HTTPError(400, str(e))
         except PilosaError as e:
             raise HTTPError(500, str(e))
         req.send(200, pb.ImportResponse(Err="").SerializeToString(), PROTO)
@@ -497,12 +504,16 @@ class Handler:
             body = json.loads(req.body)
         except ValueError as e:
             raise HTTPError(400, str(e))
-        theirs = {int(b["id"]): b["checksum"] for b in body.get("blocks", [])}
+        # attrBlocks checksums are Go []byte: base64 in JSON (attr.go:80-83)
+        try:
+            theirs = {int(b["id"]): base64.b64decode(b.get("checksum") or "") for b in body.get("blocks", [])}
+        except (ValueError, TypeError, KeyError) as e:
+            raise HTTPError(400, str(e))
         out = {}
         for bid, chk in store.blocks():
-            if theirs.get(bid) != chk.hex():
+            if theirs.get(bid) != chk:
                 for i, a in store.block_data(bid).items():
-                    out[str(i)] = a
+                    out[str(i)] = dict(sorted(a.items()))   # a Go map encodes with sorted keys
         req.send_json({"attrs": out})
 
     def post_index_attr_diff(self, req):
@@ -525,11 +536,20 @@ class Handler:
             self._success(req, e)
 
     def post_resize_abort(self, req):
+        # http/handler.go handlePostClusterResizeAbort: not the coordinator ->
+        # 400, no job running -> 200 with the message, anything else (the
+        # method is not allowed in this cluster state) -> 500
+        self._require_json(req)
         try:
             self.api.resize_abort()
-            req.send_json({"info": "resize job aborted"})
+            req.send_json({"info": ""})
         except PilosaError as e:
-            req.send(400, json.dumps({"error": str(e)}), JSON)
+            if e is ErrNodeNotCoordinator:
+                raise HTTPError(400, str(e))
+            if e is ErrResizeNotRunning:
+                req.send_json({"info": str(e)})
+                return
+            raise HTTPError(500, str(e))
 
     def post_remove_node(self, req):
         try:
@@ -554,7 +574,7 @@ class Handler:
             old, new = self.api.set_coordinator(body["id"])
             req.send_json({"old": old.to_json() if old else None, "new": new.to_json()})
         except (PilosaError, KeyError, ValueError) as e:
-            req.send(400, json.dumps({"error": str(e)}), JSON)
+            req.send(400, gojson.encode_line({"error": str(e)}), JSON)
 
     def debug_vars(self, req):
         st = self.stats
@@ -587,7 +607,7 @@ class Handler:
 
 
 class Request:
-    __slots__ = ("method", "path", "query", "headers", "body", "vars", "_h", "sent")
+    __slots__ = ("method", "path", "query", "headers", "body", "vars", "_h", "sent", "cors")
 
     def __init__(self, h: BaseHTTPRequestHandler, method: str):
         u = urlparse(h.path)
@@ -600,22 +620,28 @@ class Request:
         self.vars = {}
         self._h = h
         self.sent = False
+        self.cors = ""     # the allowed Origin echoed back (CORS), else ""
 
-    def send(self, status: int, body, ctype: str):
+    def send(self, status: int, body, ctype: str, extra: Tuple = ()):
         if isinstance(body, str):
             body = body.encode()
         h = self._h
         h.send_response(status)
-        h.send_header("Content-Type", ctype)
+        if ctype:
+            h.send_header("Content-Type", ctype)
         h.send_header("Content-Length", str(len(body)))
-        h.send_header("Access-Control-Allow-Origin", "*")
+        if self.cors:
+            h.send_header("Access-Control-Allow-Origin", self.cors)
+            h.send_header("Vary", "Origin")
+        for k, v in extra:
+            h.send_header(k, v)
         h.end_headers()
         if body:
             h.wfile.write(body)
         self.sent = True
 
     def send_json(self, obj, status: int = 200):
-        self.send(status, json.dumps(obj) + "\n", JSON)
+        self.send(status, gojson.encode_line(obj), JSON)
 
 
 def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
@@ -636,6 +662,14 @@ def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
             req = None
             try:
                 req = Request(self, method)
+                origin = self.headers.get("Origin")
+                if origin and origin in handler.allowed_origins:
+                    req.cors = origin
+                    want = self.headers.get("Access-Control-Request-Method")
+                    if method == "OPTIONS" and want:   # CORS preflight
+                        req.send(200, b"", "", (("Access-Control-Allow-Methods", want),
+                                                ("Access-Control-Allow-Headers", "Content-Type")))
+                        return
                 handler.dispatch(req)
             except HTTPError as e:
                 if req is not None and not req.sent:
@@ -660,12 +694,7 @@ def make_http_server(handler: Handler, bind: str) -> ThreadingHTTPServer:
             self._do("PATCH")
 
         def do_OPTIONS(self):
-            self.send_response(200)
-            self.send_header("Access-Control-Allow-Origin", "*")
-            self.send_header("Access-Control-Allow-Methods", "GET, POST, DELETE, PATCH, OPTIONS")
-            self.send_header("Access-Control-Allow-Headers", "Content-Type, Accept")
-            self.send_header("Content-Length", "0")
-            self.end_headers()
+            self._do("OPTIONS")   # preflight for an allowed origin, else 405 / 404 from the routes
 
     class _Srv(ThreadingHTTPServer):
         # listen backlog (socketserver's default of 5 drops SYNs under

@@ -22,6 +22,7 @@ import traceback
 from typing import Dict, List, Optional
 from urllib.parse import parse_qs
 
+from pilosa_amd.utils import gojson
 from pilosa_amd.server.http_handler import Handler, HTTPError
 
 
@@ -79,7 +80,7 @@ class NativeRequest:
 
     def send_json(self, obj, status: int = 200):
         import json
-        self.send(status, json.dumps(obj) + "\n", "application/json")
+        self.send(status, gojson.encode_line(obj), "application/json")
 
 
 class NativeHTTPServer:
@@ -97,6 +98,7 @@ class NativeHTTPServer:
         self.handler = handler
         self.srv = _httpd.Server(host, int(port), io_threads)
         self.server_address = (host, self.srv.port())
+        self.srv.set_cors(list(getattr(handler, "allowed_origins", None) or []))
         self.n_workers, self.n_batchers, self.max_batch = workers, batchers, max_batch
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
@@ -115,7 +117,7 @@ class NativeHTTPServer:
         import json
         try:
             ver = self.handler.api.version()
-            self.srv.set_static("GET", "/version", "application/json", (json.dumps({"version": ver}) + "\n").encode())
+            self.srv.set_static("GET", "/version", "application/json", (gojson.encode_line({"version": ver})).encode())
         except Exception:  # noqa: BLE001 - the Python route still answers
             pass
         self.srv.start()

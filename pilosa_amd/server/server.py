@@ -18,6 +18,7 @@ runs the background loops:
 """
 from __future__ import annotations
 
+import base64
 import io
 import os
 import threading
@@ -60,8 +61,10 @@ class Server:
                  tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
                  gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
                  lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None,
-                 gossip_interval: float = 30.0):
+                 gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None):
         self.data_dir = data_dir
+        # CORS origins ([handler] allowed-origins); none = no CORS headers at all
+        self.allowed_origins = list(allowed_origins or [])
         # native epoll front end (native/httpd.cpp) unless TLS is configured
         if native_http is None:
             native_http = os.environ.get("PILOSA_NATIVE_HTTP", "1") != "0"
@@ -125,6 +128,7 @@ class Server:
         nid = self._node_id or self.holder.load_node_id()
         host, _, port = self.bind.rpartition(":")
         handler = Handler(self.api, self, self.logger, self.stats)
+        handler.allowed_origins = self.allowed_origins
         self.httpd = None
         if self.native_http:
             from pilosa_amd.server import native_http
@@ -710,7 +714,7 @@ class Server:
         return True
 
     def _sync_attrs(self, index, field, store):
-        blocks = [{"id": b, "checksum": c.hex()} for b, c in store.blocks()]
+        blocks = [{"id": b, "checksum": base64.b64encode(c).decode()} for b, c in store.blocks()]
         for n in self.cluster.nodes:
             if n.id == self.node.id or n.state != NODE_READY:
                 continue
@@ -729,7 +733,7 @@ class Server:
         remote_blocks = {}
         for n in owners:
             try:
-                remote_blocks[n.id] = {b["id"]: bytes.fromhex(b["checksum"])
+                remote_blocks[n.id] = {b["id"]: base64.b64decode(b["checksum"] or "")
                                        for b in self.client.fragment_blocks(n.uri, index, field, view, shard)}
             except Exception:  # noqa: BLE001
                 remote_blocks[n.id] = None

@@ -4,7 +4,7 @@ cites its source lines.  Same data, same queries, same expected results and
 error texts, run through this framework's Holder + Executor on the CPU."""
 import pytest
 
-from pilosa_amd.errors import PilosaError
+from pilosa_amd.errors import PilosaError, cause
 from tests.helpers import SW, Env, cols
 
 
@@ -42,9 +42,12 @@ def set_bits(env, index, field, bits, **fopts):
 
 
 def err_of(env, index, q):
+    """The error's cause (errors.Cause in the reference tests: a top-level
+    bitmap call's error arrives wrapped in "map reduce: ", executor.go:606)."""
+    from pilosa_amd.errors import cause
     with pytest.raises(PilosaError) as ei:
         env.q(index, q)
-    return str(ei.value)
+    return str(cause(ei.value))
 
 
 # ---------------------------------------------------------------- Row (:57-133)
@@ -541,7 +544,7 @@ def _bsi_checks(env, call, gt_below_min):
     assert c(f"Row(edge > {gt_below_min})") == [0, 1]
     with pytest.raises(PilosaError) as ei:
         env.q("i", f"{call}(bad_field >= 20)")
-    assert str(ei.value) == str(ErrFieldNotFound)
+    assert str(cause(ei.value)) == str(ErrFieldNotFound)   # errors.Cause
 
 
 def test_execute_row_bsi_group(envs):
@@ -911,7 +914,7 @@ def test_execute_group_by(envs):
     from pilosa_amd.errors import ErrFieldNotFound
     with pytest.raises(PilosaError) as ei:
         env.q("i", "GroupBy(Rows(missing))")
-    assert str(ei.value) == str(ErrFieldNotFound)
+    assert str(cause(ei.value)) == str(ErrFieldNotFound)
 
     def g(q):
         return [([(fr[0], fr[1]) for fr in grp], n) for grp, n in _groups(env.q1("i", q))]

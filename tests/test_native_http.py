@@ -119,9 +119,11 @@ def test_pipelining_chunked_close_options_continue():
                   + _req("POST", "/index/i/query", b"Count(Row(f=9))", close=True)
                   + _req("GET", "/version"))  # after Connection: close: never answered
         rs = _responses(_raw(port, stream))
-        assert [s for s, _ in rs] == [200, 200, 200, 200, 200]
+        # OPTIONS without configured CORS origins: the route table's 405, as
+        # the reference's router answers (server/handler_test.go "CORS" :830)
+        assert [s for s, _ in rs] == [200, 200, 405, 200, 200]
         assert json.loads(rs[0][1]) == {"results": [2]} and json.loads(rs[1][1]) == {"results": [2]}
-        assert rs[2][1] == b"" and b"version" in rs[3][1]
+        assert b"version" in rs[3][1]
         assert json.loads(rs[4][1]) == {"results": [0]}
         # Expect: 100-continue: the interim response arrives before the body is sent
         s = socket.create_connection(("127.0.0.1", port), timeout=10)
@@ -136,7 +138,7 @@ def test_pipelining_chunked_close_options_continue():
             if not x:
                 break
             out += x
-        assert _responses(out) == [(200, b'{"results": [2]}\n')]
+        assert _responses(out) == [(200, b'{"results":[2]}\n')]
         # malformed request line
         assert _responses(_raw(port, b"BROKEN\r\n\r\n"))[0][0] == 400
     finally:
@@ -182,7 +184,7 @@ def test_count_group_commit_and_fallback():
         # a group the fast path declines (unknown field) goes to the general
         # path: same error as the stdlib server, other groups unaffected
         rs = _responses(_raw(port, _req("POST", "/index/i/query", b"Count(Row(nope=1))", close=True)))
-        assert rs[0] == (400, b"{\"error\": \"field not found\"}\n")
+        assert rs[0] == (400, b"{\"error\":\"executing: field not found\"}\n")
         assert srv.httpd.stats()["requeued"] >= 1
     finally:
         srv.close()
