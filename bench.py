@@ -355,7 +355,8 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
             for c in calls:
                 dev_pairs = sorted((p.id, p.count) for p in gpu.topn("i", c, [s]))
                 src = ex.bitmap_call_shard("i", c.children[0], s) if c.children else None
-                host = frag.top(TopOptions(n=n, src=src, min_threshold=1))
+                _, cn, _, cth, _, _, _ = ex.topn_params("i", c)   # each call's own n and threshold
+                host = frag.top(TopOptions(n=cn, src=src, min_threshold=max(1, cth)))
                 if dev_pairs != sorted((p.id, p.count) for p in host):
                     bad += 1
         # and the fused batch answers equal the two-phase map/reduce on the device
@@ -1546,7 +1547,7 @@ def main():
                     help="disk mode: drop the fragment files from the page cache before loading (1) or not (0)")
     ap.add_argument("--keep-data", action="store_true")
     ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")
-    ap.add_argument("--topn-batches", type=int, default=10,
+    ap.add_argument("--topn-batches", type=int, default=40,
                     help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")

@@ -42,7 +42,7 @@ def _add_config_flags(p: argparse.ArgumentParser):
 def resolve_config(args) -> "object":
     from pilosa_amd.server.config import Config
     cfg = Config()
-    path = getattr(args, "config", None)
+    path = getattr(args, "config", None) or os.environ.get("PILOSA_CONFIG")
     if path:
         cfg.load_toml(path)
     cfg.load_env()
@@ -52,6 +52,77 @@ def resolve_config(args) -> "object":
     return cfg
 
 
+# the configuration the last server command resolved (tests, --dry-run)
+LAST_CONFIG: List[Optional[object]] = [None]
+
+
+# ------------------------------------------------------------------ ctl options
+# Flags of the import / export commands.  As with the reference's cobra +
+# viper commands (cmd/root.go setAllConfig), a value comes from the flag, else
+# the PILOSA_<NAME> environment variable, else the configuration file
+# (--config / PILOSA_CONFIG, top-level keys), else the default.
+#   name -> (type, default, short flag)
+IMPORT_OPTIONS = {
+    "host": (str, "localhost:10101", None), "index": (str, "", "-i"), "field": (str, "", "-f"),
+    "create-schema": (bool, False, "-e"), "clear": (bool, False, None), "index-keys": (bool, False, None),
+    "field-keys": (bool, False, None), "field-type": (str, "", None), "field-min": (int, 0, None),
+    "field-max": (int, 0, None), "field-time-quantum": (str, "", None), "field-cache-type": (str, "ranked", None),
+    "field-cache-size": (int, 50000, None), "buffer-size": (int, 10000000, "-b"), "sort": (bool, False, None),
+}
+EXPORT_OPTIONS = {"host": (str, "localhost:10101", None), "index": (str, "", "-i"), "field": (str, "", "-f"),
+                  "output-file": (str, "", "-o")}
+# what the last import / export command resolved (tests, --dry-run)
+LAST_OPTIONS: Dict[str, dict] = {}
+
+
+def _add_cmd_options(p: argparse.ArgumentParser, spec: dict):
+    p.add_argument("-c", "--config", default=None)
+    p.add_argument("--dry-run", action="store_true", help="stop after resolving the options")
+    for name, (typ, default, short) in spec.items():
+        flags = [f"--{name}"] + ([short] if short else [])
+        if name == "output-file":
+            flags.append("--output")
+        dest = name.replace("-", "_")
+        if typ is bool:
+            p.add_argument(*flags, dest=dest, action="store_const", const=True, default=None,
+                           help=f"(default {default})")
+        else:
+            p.add_argument(*flags, dest=dest, type=typ, default=None, help=f"(default {default!r})")
+
+
+def _resolve_cmd_options(args, spec: dict, env=None) -> None:
+    env = os.environ if env is None else env
+    path = getattr(args, "config", None) or env.get("PILOSA_CONFIG")
+    file = {}
+    if path:
+        import tomli
+        with open(os.path.expanduser(path), "rb") as fh:
+            file = tomli.load(fh)
+    for name, (typ, default, _) in spec.items():
+        dest = name.replace("-", "_")
+        if getattr(args, dest, None) is not None:
+            continue
+        ev = env.get("PILOSA_" + name.replace("-", "_").upper())
+        if ev not in (None, ""):
+            val = ev.lower() in ("1", "true", "yes") if typ is bool else typ(ev)
+        elif name in file:
+            val = typ(file[name])
+        else:
+            val = default
+        setattr(args, dest, val)
+    if hasattr(args, "output_file"):
+        args.output = args.output_file
+
+
+def import_field_options(args) -> dict:
+    """The field options an import creates its field with (ctl/import.go:
+    keys, int range, time quantum, cache type / size)."""
+    o = {"keys": bool(args.field_keys), "min": int(args.field_min), "max": int(args.field_max),
+         "timeQuantum": args.field_time_quantum, "cacheType": args.field_cache_type,
+         "cacheSize": int(args.field_cache_size)}
+    return o
+
+
 # ------------------------------------------------------------------ server
 def cmd_server(args, stdout, stderr) -> int:
     from pilosa_amd.server.config import parse_duration
@@ -59,7 +130,20 @@ def cmd_server(args, stdout, stderr) -> int:
     from pilosa_amd.utils import tracing
     from pilosa_amd.utils.logger import StandardLogger
 
-    cfg = resolve_config(args)
+    from pilosa_amd.server.config import ConfigError, validate_addrs
+    try:
+        cfg = resolve_config(args)
+        raw_adv = cfg.get("advertise")   # only an explicit advertise address overrides the listener's
+        bind, adv = validate_addrs(cfg.get("bind"), raw_adv)
+    except (ConfigError, OSError) as e:
+        print(e, file=stderr)
+        return 1
+    cfg.set("bind", bind)
+    cfg.set("advertise", adv)
+    LAST_CONFIG[0] = cfg
+    if getattr(args, "dry_run", False):   # stop after configuration (cmd/root.go --dry-run)
+        print("dry run", file=stderr)
+        return 0
     log_stream = stderr
     if cfg.get("log-path"):
         log_stream = open(os.path.expanduser(cfg.get("log-path")), "a")
@@ -82,7 +166,7 @@ def cmd_server(args, stdout, stderr) -> int:
                             logger=logger)
     from pilosa_amd.utils import syswrap
     syswrap.set_max_map_count(cfg.get("max-map-count"))   # server.Command: syswrap.SetMaxMapCount
-    bind = cfg.get("bind")
+    bind = cfg.get("bind").split("://", 1)[-1]
     if bind.startswith(":"):
         bind = "0.0.0.0" + bind
     hosts = list(cfg.get("cluster.hosts")) + [h for h in cfg.get("gossip.seeds") if h not in cfg.get("cluster.hosts")]
@@ -93,6 +177,7 @@ def cmd_server(args, stdout, stderr) -> int:
                                                                          else None),
                  gpu=cfg.get("gpu.mode"), workers=cfg.get("worker-pool-size"),
                  allowed_origins=list(cfg.get("handler.allowed-origins") or []),
+                 advertise=adv if raw_adv else "",
                  max_writes=cfg.get("max-writes-per-request"),
                  anti_entropy_interval=cfg.duration("anti-entropy.interval"),
                  probe_interval=cfg.duration("gossip.probe-interval"),
@@ -135,6 +220,12 @@ def cmd_import(args, stdout, stderr) -> int:
     from pilosa_amd.parallel.cluster import Node
     from pilosa_amd.server.client import InternalClient
 
+    _resolve_cmd_options(args, IMPORT_OPTIONS)
+    LAST_OPTIONS["import"] = dict(vars(args), field_options=import_field_options(args))
+    if args.dry_run:
+        print("dry run", file=stderr)
+        return 0
+
     if not args.index:
         print("index required", file=stderr)
         return 1
@@ -152,7 +243,8 @@ def cmd_import(args, stdout, stderr) -> int:
                                     else "set")
         opts: Dict[str, object] = {"type": ftype}
         if ftype in ("set", "mutex"):
-            opts["keys"] = args.field_keys
+            opts.update({"keys": args.field_keys, "cacheType": args.field_cache_type,
+                         "cacheSize": args.field_cache_size})
         elif ftype == "int":
             opts.update({"min": args.field_min, "max": args.field_max})
         elif ftype == "time":
@@ -269,6 +361,11 @@ def _flush(c, node, args, buf, is_int, col_keys, row_keys) -> int:
 # ------------------------------------------------------------------ export
 def cmd_export(args, stdout, stderr) -> int:
     from pilosa_amd.server.client import InternalClient
+    _resolve_cmd_options(args, EXPORT_OPTIONS)
+    LAST_OPTIONS["export"] = dict(vars(args))
+    if args.dry_run:
+        print("dry run", file=stderr)
+        return 0
     if not args.index:
         print("index required", file=stderr)      # pilosa.ErrIndexRequired
         return 1
@@ -290,6 +387,15 @@ def cmd_export(args, stdout, stderr) -> int:
 
 
 # ------------------------------------------------------------------ check / inspect
+def _header_error(e: Exception) -> str:
+    """The reference's wording for a file that is neither Pilosa nor
+    official roaring (roaring/roaring.go UnmarshalBinary)."""
+    msg = str(e)
+    if "magic number" in msg:
+        return "did not find expected serialCookie in header"
+    return msg
+
+
 def cmd_check(args, stdout, stderr) -> int:
     """ctl/check.go: fragment files (no extension) are unmarshalled and
     consistency-checked; .cache and .snapshotting files are skipped with a
@@ -314,7 +420,7 @@ def cmd_check(args, stdout, stderr) -> int:
         try:
             bm = _roaring.Bitmap.from_bytes(data)
         except Exception as e:  # noqa: BLE001
-            print(f"checking bitmap: unmarshalling: reading roaring header: {e}", file=stderr)
+            print(f"checking bitmap: unmarshalling: reading roaring header: {_header_error(e)}", file=stderr)
             return 1
         errs = bm.check()
         for line in (errs or "").strip().splitlines():
@@ -335,7 +441,12 @@ def cmd_inspect(args, stdout, stderr) -> int:
         return 1
     with open(args.path[0], "rb") as fh:
         data = fh.read()
-    bm = _roaring.Bitmap.from_bytes(data)
+    print("unmarshalling bitmap...", file=stderr)     # ctl/inspect.go
+    try:
+        bm = _roaring.Bitmap.from_bytes(data)
+    except Exception as e:  # noqa: BLE001
+        print(f"unmarshalling: reading roaring header: {_header_error(e)}", file=stderr)
+        return 1
     info = bm.container_info()
     types = Counter(t for _, t, _ in info)
     print("== Bitmap Info ==", file=stdout)
@@ -363,32 +474,32 @@ def cmd_generate_config(args, stdout, stderr) -> int:
 
 
 # ------------------------------------------------------------------ main
+class _HelpFormatter(argparse.HelpFormatter):
+    """Help laid out like the reference's cobra commands ("Usage:", "Flags:")."""
+
+    def add_usage(self, usage, actions, groups, prefix=None):
+        super().add_usage(usage, actions, groups, prefix="Usage: " if prefix is None else prefix)
+
+
+class _Parser(argparse.ArgumentParser):
+    def __init__(self, *a, **kw):
+        kw.setdefault("formatter_class", _HelpFormatter)
+        super().__init__(*a, **kw)
+        self._optionals.title = "Flags"
+
+
 def build_parser() -> argparse.ArgumentParser:
-    p = argparse.ArgumentParser(prog="pilosa", description="MI355X-native distributed bitmap index")
-    sub = p.add_subparsers(dest="cmd")
+    p = _Parser(prog="pilosa", description="MI355X-native distributed bitmap index")
+    sub = p.add_subparsers(dest="cmd", title="Available Commands", parser_class=_Parser)
     s = sub.add_parser("server", help="run a node")
     s.add_argument("-c", "--config", default=None)
+    s.add_argument("--dry-run", action="store_true", help="stop after resolving the configuration")
     _add_config_flags(s)
-    i = sub.add_parser("import", help="bulk load CSV data")
-    i.add_argument("--host", default="localhost:10101")
-    i.add_argument("-i", "--index", default="")
-    i.add_argument("-f", "--field", default="")
-    i.add_argument("--create-schema", action="store_true")
-    i.add_argument("--clear", action="store_true")
-    i.add_argument("--index-keys", action="store_true")
-    i.add_argument("--field-keys", action="store_true")
-    i.add_argument("--field-type", default="")
-    i.add_argument("--field-min", type=int, default=0)
-    i.add_argument("--field-max", type=int, default=0)
-    i.add_argument("--field-time-quantum", default="")
-    i.add_argument("-b", "--buffer-size", type=int, default=10000000)
-    i.add_argument("--sort", action="store_true")
+    i = sub.add_parser("import", help="bulk load CSV data", usage="pilosa import [flags] PATH...")
+    _add_cmd_options(i, IMPORT_OPTIONS)
     i.add_argument("paths", nargs="*")
-    e = sub.add_parser("export", help="export a field as CSV")
-    e.add_argument("--host", default="localhost:10101")
-    e.add_argument("-i", "--index", default="")
-    e.add_argument("-f", "--field", default="")
-    e.add_argument("-o", "--output", default="")
+    e = sub.add_parser("export", help="export a field as CSV", usage="pilosa export [flags]")
+    _add_cmd_options(e, EXPORT_OPTIONS)
     ck = sub.add_parser("check", help="consistency check of fragment files")
     ck.add_argument("paths", nargs="+")
     ins = sub.add_parser("inspect", help="inspect a fragment file")

@@ -159,7 +159,18 @@ class Config:
     def load_toml(self, path: str):
         import tomli
         with open(os.path.expanduser(path), "rb") as fh:
-            self.merge(tomli.load(fh), strict=True)
+            data = tomli.load(fh)
+        bad = [k for k in _flat_keys(data) if not self._known(k)]
+        if bad:   # cmd/root.go: every key of the file must be a known option
+            raise ConfigError(f"invalid option in configuration file: {bad[0]}")
+        self.merge(data, strict=True)
+
+    def _known(self, key: str) -> bool:
+        try:
+            self.get(key)
+            return True
+        except (KeyError, TypeError):
+            return False
 
     def load_env(self, env=None):
         env = os.environ if env is None else env
@@ -187,6 +198,119 @@ class Config:
 
     def duration(self, key: str) -> float:
         return parse_duration(self.get(key))
+
+
+# ------------------------------------------------------------ listen / advertise
+# (server/config.go validateAddrs, validateAdvertiseAddr, validateListenAddr)
+DEFAULT_PORT = "10101"
+
+
+def split_scheme(addr: str):
+    scheme, sep, rest = addr.partition("://")
+    return (scheme, rest) if sep else ("", addr)
+
+
+def split_host_port(hostport: str):
+    """net.SplitHostPort: "host:port" / "[v6]:port" -> (host, port)."""
+    if hostport.startswith("["):
+        end = hostport.find("]")
+        if end < 0:
+            raise ConfigError(f"address {hostport}: missing ']' in address")
+        host, rest = hostport[1:end], hostport[end + 1:]
+        if not rest.startswith(":"):
+            raise ConfigError(f"address {hostport}: missing port in address")
+        return host, rest[1:]
+    i = hostport.rfind(":")
+    if i < 0:
+        raise ConfigError(f"address {hostport}: missing port in address")
+    host, port = hostport[:i], hostport[i + 1:]
+    if ":" in host:
+        raise ConfigError(f"address {hostport}: too many colons in address")
+    return host, port
+
+
+def join_host_port(host: str, port: str) -> str:
+    return f"[{host}]:{port}" if ":" in host else f"{host}:{port}"
+
+
+def lookup_port(port: str) -> str:
+    """net.LookupPort("tcp", port): numeric (signed) or a service name."""
+    import socket
+    try:
+        n = int(port, 10)
+    except ValueError:
+        try:
+            n = socket.getservbyname(port, "tcp")
+        except OSError:
+            raise ConfigError(f"lookup tcp/{port}: unknown port")
+    if not 0 <= n <= 65535:
+        raise ConfigError(f"address {port}: invalid port")
+    return str(n)
+
+
+def lookup_addr(host: str) -> str:
+    """First IPv4 address of ``host`` (else the first address)."""
+    import socket
+    try:
+        infos = socket.getaddrinfo(host, None, proto=socket.IPPROTO_TCP)
+    except (OSError, UnicodeError):
+        raise ConfigError(f"looking up IP addresses: lookup {host}: no such host")
+    if not infos:
+        raise ConfigError(f"cannot resolve {host!r} to an address")
+    for fam, *_, sa in infos:
+        if fam == socket.AF_INET:
+            return sa[0]
+    return infos[0][4][0]
+
+
+def outbound_ip() -> str:
+    """The address this host would use towards the outside (no packet is sent)."""
+    import socket
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as sk:
+            sk.connect(("8.8.8.8", 80))
+            return sk.getsockname()[0]
+    except OSError:   # no route out (an isolated host): the loopback address
+        return "127.0.0.1"
+
+
+def _split_addr(addr: str):
+    scheme, hostport = split_scheme(addr)
+    host, port = "", ""
+    if hostport:
+        host, port = split_host_port(hostport)
+    return scheme, host, port or DEFAULT_PORT
+
+
+def _scheme_host_port(scheme: str, host: str, port: str) -> str:
+    return (f"{scheme}://" if scheme else "") + join_host_port(host, port)
+
+
+def validate_addrs(bind: str, advertise: str):
+    """(bind, advertise) normalised as the reference's Config.validateAddrs:
+    default port 10101, service names resolved, host names resolved to IPs
+    for the listener, and an empty advertise host taken from the listener
+    (or the outbound address when listening on 0.0.0.0)."""
+    try:
+        l_scheme, l_host, l_port = _split_addr(bind)
+        a_scheme, a_hostport = split_scheme(advertise)
+        a_host, a_port = split_host_port(a_hostport) if a_hostport else ("", "")
+        a_scheme = a_scheme or l_scheme
+        if a_port in ("", "0"):
+            a_port = l_port
+        a_port = lookup_port(a_port)
+        if not a_host:
+            a_host = outbound_ip() if l_host == "0.0.0.0" else l_host
+    except ConfigError as e:
+        raise ConfigError(f"validating advertise address: {e}")
+    adv = _scheme_host_port(a_scheme, a_host, a_port)
+    try:
+        l_port = lookup_port(l_port)
+        if l_host not in ("", "localhost"):
+            l_host = lookup_addr(l_host)
+    except ConfigError as e:
+        raise ConfigError(f"validating listen address: resolving address: {e}")
+    return _scheme_host_port(l_scheme, l_host, l_port), adv
 
 
 def _flat_keys(d: dict, prefix=""):

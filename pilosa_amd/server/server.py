@@ -61,10 +61,14 @@ class Server:
                  tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
                  gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
                  lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None,
-                 gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None):
+                 gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None,
+                 advertise: str = ""):
         self.data_dir = data_dir
         # CORS origins ([handler] allowed-origins); none = no CORS headers at all
         self.allowed_origins = list(allowed_origins or [])
+        # address other nodes reach this one at ([advertise], server/config.go
+        # validateAdvertiseAddr); empty = the listen address
+        self.advertise = advertise
         # native epoll front end (native/httpd.cpp) unless TLS is configured
         if native_http is None:
             native_http = os.environ.get("PILOSA_NATIVE_HTTP", "1") != "0"
@@ -145,6 +149,9 @@ class Server:
             scheme = "https"
         port = self.httpd.server_address[1]
         adv = host if host not in ("", "0.0.0.0") else "127.0.0.1"
+        if self.advertise:
+            a = URI.parse(self.advertise)
+            adv, port = a.host or adv, a.port or port
         self.node = Node(nid, URI(scheme, adv, port), state=NODE_READY)
         self.client.local_node = self.node.to_json()
         self.cluster = Cluster(self.node, replica_n=self.replica_n, hasher=self.hasher, path=self.data_dir)

@@ -1,0 +1,269 @@
+"""Ported expectations of the reference's command-line tests: cmd/root_test.go,
+cmd/server_test.go, cmd/import_test.go, cmd/export_test.go, ctl/check_test.go,
+ctl/export_test.go, ctl/inspect_test.go, ctl/config_test.go,
+ctl/generate_config_test.go, ctl/server_test.go, server/config_test.go and
+server/config_internal_test.go.  The reference's --dry-run commands stop after
+configuration; here the resolved values are read from
+``pilosa_amd.cli.main.LAST_CONFIG`` / ``LAST_OPTIONS``."""
+import io
+import os
+import socket
+import tempfile
+
+import pytest
+
+from pilosa_amd.cli import main as cli
+from pilosa_amd.server.config import Config, ConfigError, format_duration, parse_duration, validate_addrs
+
+
+def _run(argv, env=None, cfg_text=None, monkeypatch=None):
+    out, err = io.StringIO(), io.StringIO()
+    if cfg_text is not None:
+        fd, path = tempfile.mkstemp(suffix=".toml")
+        with os.fdopen(fd, "w") as fh:
+            fh.write(cfg_text)
+        monkeypatch.setenv("PILOSA_CONFIG", path)
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
+    rc = cli.main(argv, stdout=out, stderr=err)
+    return rc, out.getvalue(), err.getvalue()
+
+
+# ---------------------------------------------------------------- cmd/root_test.go
+def test_root_help(capsys):  # TestRootCommand
+    with pytest.raises(SystemExit) as ei:
+        cli.main(["--help"])
+    out = capsys.readouterr().out
+    assert ei.value.code == 0 and "Usage:" in out and "Available Commands" in out and "--help" in out
+
+
+def test_root_config_rejects_unknown_option(tmp_path, monkeypatch):  # TestRootCommand_Config
+    cfg = tmp_path / "test.conf"
+    cfg.write_text('data-dir = "/tmp/pil5_0"\nbind = "127.0.0.1:10101"\n\n[cluster]\n  replicas = 2\n'
+                   '  partitions = 128\n  hosts = [\n    "127.0.0.1:10101",\n    "127.0.0.1:10111",\n  ]')
+    rc, _, err = _run(["server", "--config", str(cfg), "--dry-run"], monkeypatch=monkeypatch)
+    assert rc != 0 and err.strip() == "invalid option in configuration file: cluster.partitions"
+
+
+# ---------------------------------------------------------------- cmd/server_test.go
+@pytest.mark.parametrize("cmd", ["server", "import", "export"])
+def test_command_help(cmd, capsys):  # TestServerHelp, TestImportHelp, TestExportHelp
+    with pytest.raises(SystemExit):
+        cli.main([cmd, "--help"])
+    out = capsys.readouterr().out
+    assert "Usage:" in out and "Flags:" in out
+    if cmd != "server":
+        assert f"pilosa {cmd}" in out
+
+
+def test_server_config_precedence_flags_env_file(tmp_path, monkeypatch):  # TestServerConfig test 0
+    data = str(tmp_path / "data")
+    rc, _, err = _run(["server", "--dry-run", "--data-dir", data, "--cluster.hosts", "localhost:10111,localhost:10110",
+                       "--bind", "localhost:10111", "--translation.map-size", "100000"],
+                      env={"PILOSA_DATA_DIR": "/tmp/myEnvDatadir", "PILOSA_CLUSTER_LONG_QUERY_TIME": "1m30s",
+                           "PILOSA_MAX_WRITES_PER_REQUEST": "2000", "PILOSA_PROFILE_BLOCK_RATE": "9123",
+                           "PILOSA_PROFILE_MUTEX_FRACTION": "444"},
+                      cfg_text='data-dir = "/tmp/myFileDatadir"\nbind = "localhost:0"\nmax-writes-per-request = 3000\n'
+                               '[cluster]\n disabled = true\n replicas = 2\n hosts = ["localhost:19444"]\n'
+                               ' long-query-time = "1m10s"\n[profile]\n block-rate = 100\n mutex-fraction = 10\n',
+                      monkeypatch=monkeypatch)
+    assert rc == 0, err
+    c = cli.LAST_CONFIG[0]
+    assert c.get("data-dir") == data and c.get("bind") == "localhost:10111"
+    assert c.get("cluster.replicas") == 2 and c.get("cluster.hosts") == ["localhost:10111", "localhost:10110"]
+    assert c.duration("cluster.long-query-time") == 90 and c.get("max-writes-per-request") == 2000
+    assert c.get("translation.map-size") == 100000
+    assert (c.get("profile.block-rate"), c.get("profile.mutex-fraction")) == (9123, 444)
+
+
+def test_server_config_flags_over_env(tmp_path, monkeypatch):  # TestServerConfig test 1
+    rc, _, err = _run(["server", "--dry-run", "--anti-entropy.interval", "9m0s", "--profile.block-rate", "4832",
+                       "--profile.mutex-fraction", "8290"],
+                      env={"PILOSA_CLUSTER_HOSTS": "localhost:1110,localhost:1111", "PILOSA_BIND": "localhost:1110",
+                           "PILOSA_TRANSLATION_MAP_SIZE": "100000", "PILOSA_PROFILE_BLOCK_RATE": "9123",
+                           "PILOSA_PROFILE_MUTEX_FRACTION": "444"},
+                      cfg_text=f'bind = "localhost:0"\ndata-dir = "{tmp_path}"\n[cluster]\n disabled = true\n'
+                               ' hosts = ["localhost:19444"]\n[profile]\n block-rate = 100\n mutex-fraction = 10\n',
+                      monkeypatch=monkeypatch)
+    assert rc == 0, err
+    c = cli.LAST_CONFIG[0]
+    assert c.get("cluster.hosts") == ["localhost:1110", "localhost:1111"]
+    assert c.duration("anti-entropy.interval") == 540 and c.get("translation.map-size") == 100000
+    assert (c.get("profile.block-rate"), c.get("profile.mutex-fraction")) == (4832, 8290)
+
+
+def test_server_runs_with_file_config_and_writes_log(tmp_path, monkeypatch):  # TestServerConfig test 2
+    log = tmp_path / "pilosa.log"
+    cfg = tmp_path / "c.toml"
+    cfg.write_text(f'bind = "127.0.0.1:0"\ndata-dir = "{tmp_path / "d"}"\n[anti-entropy]\n interval = "11m0s"\n'
+                   '[metric]\n service = "statsd"\n host = "127.0.0.1:8125"\n[profile]\n block-rate = 5352\n'
+                   ' mutex-fraction = 91\n[gpu]\n mode = "off"\n native-http = false\n')
+    args = cli.build_parser().parse_args(["server", "--config", str(cfg), "--log-path", str(log),
+                                          "--cluster.disabled", "true", "--translation.map-size", "100000"])
+    args._run_seconds = 0.5
+    saved = os.dup(2)     # the server points fd 2 at its log file (server/setup_logger.go)
+    try:
+        assert cli.cmd_server(args, io.StringIO(), io.StringIO()) == 0
+    finally:
+        os.dup2(saved, 2)
+        os.close(saved)
+    c = cli.LAST_CONFIG[0]
+    assert c.duration("anti-entropy.interval") == 660 and c.get("log-path") == str(log)
+    assert (c.get("metric.service"), c.get("metric.host")) == ("statsd", "127.0.0.1:8125")
+    assert (c.get("profile.block-rate"), c.get("profile.mutex-fraction")) == (5352, 91)
+    assert log.stat().st_size > 0, "log file was not written"
+
+
+# ---------------------------------------------------------------- cmd/import_test.go, cmd/export_test.go
+def test_import_config_from_env_and_file(monkeypatch):  # TestImportConfig case 0
+    rc, _, err = _run(["import", "--dry-run"], env={"PILOSA_HOST": "localhost:12345"},
+                      cfg_text='index = "myindex"\nfield = "f1"\n', monkeypatch=monkeypatch)
+    o = cli.LAST_OPTIONS["import"]
+    assert rc == 0 and (o["host"], o["index"], o["field"]) == ("localhost:12345", "myindex", "f1"), err
+
+
+@pytest.mark.parametrize("argv,want", [  # TestImportConfig cases 1-4
+    (["--index", "i1", "--field", "f1", "--field-keys", "--field-min", "-10", "--field-max", "100"],
+     {"keys": True, "max": 100, "min": -10, "cacheType": "ranked", "cacheSize": 50000}),
+    (["--index", "i1", "--field", "f1", "--field-time-quantum", "YMD"],
+     {"timeQuantum": "YMD", "cacheType": "ranked", "cacheSize": 50000}),
+    (["--index", "i1", "--field", "f1", "--field-cache-type", "lru", "--field-cache-size", "100"],
+     {"cacheType": "lru", "cacheSize": 100})])
+def test_import_field_options(argv, want, monkeypatch):
+    monkeypatch.delenv("PILOSA_CONFIG", raising=False)
+    rc, _, _ = _run(["import", "--dry-run"] + argv, monkeypatch=monkeypatch)
+    o = cli.LAST_OPTIONS["import"]
+    assert rc == 0 and (o["index"], o["field"]) == ("i1", "f1")
+    base = {"keys": False, "min": 0, "max": 0, "timeQuantum": "", "cacheType": "ranked", "cacheSize": 50000}
+    assert o["field_options"] == dict(base, **want)
+
+
+def test_import_clear_flag(monkeypatch):  # TestImportConfig case 5 (--clear true)
+    monkeypatch.delenv("PILOSA_CONFIG", raising=False)
+    rc, _, _ = _run(["import", "--dry-run", "--index", "i1", "--field", "f1", "--clear", "true"],
+                    monkeypatch=monkeypatch)
+    assert rc == 0 and cli.LAST_OPTIONS["import"]["clear"] is True
+
+
+def test_export_config(monkeypatch):  # TestExportConfig
+    rc, _, _ = _run(["export", "--dry-run", "--output-file", "/somefile"], env={"PILOSA_HOST": "localhost:12345"},
+                    cfg_text='index = "myindex"\nfield = "f1"\n', monkeypatch=monkeypatch)
+    o = cli.LAST_OPTIONS["export"]
+    assert rc == 0 and (o["host"], o["index"], o["field"], o["output_file"]) == \
+        ("localhost:12345", "myindex", "f1", "/somefile")
+
+
+# ---------------------------------------------------------------- ctl/*_test.go
+def test_check_ignores_cache_and_snapshot_files(tmp_path, monkeypatch):  # TestCheckCommand_RunCacheFile/_RunSnapshot
+    monkeypatch.delenv("PILOSA_CONFIG", raising=False)
+    for name, msg in (("x.cache", "ignoring cache file"), ("x.snapshotting", "ignoring snapshot file")):
+        rc, out, err = _run(["check", str(tmp_path / name)], monkeypatch=monkeypatch)
+        assert msg in out + err
+
+
+def test_check_rejects_non_roaring_file(tmp_path, monkeypatch):  # TestCheckCommand_Run
+    p = tmp_path / "f"
+    p.write_bytes(b"1234,1223")
+    rc, out, err = _run(["check", str(p)], monkeypatch=monkeypatch)
+    assert rc != 0 and (out + err).strip().splitlines()[-1].startswith(
+        "checking bitmap: unmarshalling: reading roaring header:")
+
+
+def test_inspect_non_roaring_file(tmp_path, monkeypatch):  # TestInspectCommand_Run
+    p = tmp_path / "inspectTest"
+    p.write_bytes(b"12358267538963")
+    rc, out, err = _run(["inspect", str(p)], monkeypatch=monkeypatch)
+    assert "unmarshalling bitmap..." in out + err
+    assert rc == 0 or "unmarshalling: reading roaring header: did not find expected serialCookie in header" in err
+
+
+def test_export_validation(monkeypatch):  # TestExportCommand_Validation
+    monkeypatch.delenv("PILOSA_CONFIG", raising=False)
+    rc, _, err = _run(["export"], monkeypatch=monkeypatch)
+    assert rc != 0 and err.strip() == "index required"
+    rc, _, err = _run(["export", "--index", "i"], monkeypatch=monkeypatch)
+    assert rc != 0 and err.strip() == "field required"
+
+
+def test_export_run(monkeypatch):  # TestExportCommand_Run
+    from pilosa_amd.server.server import Server
+    from pilosa_amd.utils.logger import CaptureLogger
+    from tests.test_server import _req
+    monkeypatch.delenv("PILOSA_CONFIG", raising=False)
+    s = Server(tempfile.mkdtemp(), bind="127.0.0.1:0", gpu="off", logger=CaptureLogger()).open()
+    try:
+        assert _req(s, "POST", "/index/i", b"")[0] == 200
+        assert _req(s, "POST", "/index/i/field/f", b"")[0] == 200
+        rc, _, err = _run(["export", "--host", f"127.0.0.1:{s.uri.port}", "--index", "i", "--field", "f"],
+                          monkeypatch=monkeypatch)
+        assert rc == 0, err
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("cmd", ["config", "generate-config"])
+def test_config_commands_print_default_bind(cmd, monkeypatch):  # TestConfigCommand_Run, TestGenerateConfigCommand_Run
+    monkeypatch.delenv("PILOSA_CONFIG", raising=False)
+    rc, out, _ = _run([cmd], monkeypatch=monkeypatch)
+    assert rc == 0 and ":10101" in out
+
+
+def test_server_flags_include_data_dir_and_log_path():  # TestBuildServerFlags
+    p = cli.build_parser()
+    sp = next(a for a in p._actions if a.dest == "cmd").choices["server"]
+    opts = {o for a in sp._actions for o in a.option_strings}
+    assert "--data-dir" in opts and "--log-path" in opts
+
+
+# ---------------------------------------------------------------- server/config_test.go
+def test_new_config():  # Test_NewConfig
+    assert Config().get("cluster.disabled") is False
+
+
+def test_duration():  # TestDuration
+    assert format_duration(182) == "3m2s"
+    assert format_duration(182).encode() == bytes([51, 109, 50, 115])
+    with pytest.raises(ValueError, match="^time: missing unit in duration 5$"):
+        parse_duration("5")
+    assert parse_duration("3m2s") == 182 and format_duration(parse_duration("3m2s")) == "3m2s"
+
+
+# ---------------------------------------------------------------- server/config_internal_test.go
+def _host_addr():
+    try:
+        a = socket.gethostbyname(socket.gethostname())
+    except OSError:
+        return None     # the container's hostname may not resolve: those cases are skipped
+    return f"[{a}]" if ":" in a else a
+
+
+def test_validate_addrs_defaults_and_forms():  # TestConfig_validateAddrs
+    cases = [(("", ""), (":10101", ":10101")), ((":", ""), (":10101", ":10101")),
+             (("", ":"), (":10101", ":10101")), ((":", ":"), (":10101", ":10101")),
+             ((":1234", ""), (":1234", ":1234")), (("localhost:1234", ""), ("localhost:1234", "localhost:1234")),
+             (("localhost:", ""), ("localhost:10101", "localhost:10101")),
+             ((":1234", ":0"), (":1234", ":1234"))]
+    try:
+        socket.getservbyname("postgresql", "tcp")
+        cases.append(((":postgresql", ""), (":5432", ":5432")))
+    except OSError:
+        pass
+    h = _host_addr()
+    if h:
+        cases += [((h + ":10101", ""), (h + ":10101", h + ":10101")), ((h + ":", ""), (h + ":10101", h + ":10101")),
+                  (("http://" + h + ":", ""), ("http://" + h + ":10101", "http://" + h + ":10101")),
+                  ((h + ":1234", h + ":"), (h + ":1234", h + ":1234")),
+                  ((h + ":1234", h + ":7890"), (h + ":1234", h + ":7890"))]
+    for (bind, adv), want in cases:
+        assert validate_addrs(bind, adv) == want, (bind, adv)
+    b, a = validate_addrs("0.0.0.0:1234", "")
+    assert b == "0.0.0.0:1234" and a.endswith(":1234") and not a.startswith("0.0.0.0")
+
+
+@pytest.mark.parametrize("bind,adv,msg", [
+    ("localhost", "", "missing port in address"), (":1234", "localhost", "missing port in address"),
+    ("localhost:-1234", "", "invalid port"), ("localhost:foo", "", "validating advertise address"),
+    ("333.333.333.333:1234", "", "no such host")])
+def test_validate_addrs_errors(bind, adv, msg):
+    with pytest.raises(ConfigError, match=msg):
+        validate_addrs(bind, adv)
