@@ -1174,28 +1174,30 @@ class Fragment:
 
     def merge_block(self, block_id: int, data: List[Tuple[Sequence[int], Sequence[int]]]):
         """Majority-vote merge of replica block data (fragment.go:1873-1991).
-        Returns (sets, clears) diffs per remote replica."""
+        Returns (sets, clears) diffs per remote replica.  The reference walks
+        the replicas' sorted pair iterators in lockstep; here every replica's
+        pairs become sorted position arrays (models/iterator.py) and the vote
+        is one counted union over them."""
+        from pilosa_amd.models.iterator import pairs_to_positions
         lr, lc = self.block_data(block_id)
-        sets_all = [set(zip(lr.tolist(), lc.tolist()))]
-        max_row = (block_id + 1) * HASH_BLOCK_SIZE
+        lo, hi = block_id * HASH_BLOCK_SIZE, (block_id + 1) * HASH_BLOCK_SIZE
+        sets_all = [pairs_to_positions(lr, lc)]
         for rows, cols in data:
             if len(rows) != len(cols):
                 raise PilosaError(f"pair set mismatch: {len(rows)} != {len(cols)}")
-            sets_all.append({(int(r), int(c)) for r, c in zip(rows, cols)
-                             if block_id * HASH_BLOCK_SIZE <= int(r) < max_row and int(c) < SHARD_WIDTH})
+            r = np.asarray(rows, dtype=np.uint64)
+            c = np.asarray(cols, dtype=np.uint64)
+            keep = (r >= np.uint64(lo)) & (r < np.uint64(hi)) & (c < np.uint64(SHARD_WIDTH))
+            sets_all.append(pairs_to_positions(r[keep], c[keep]))
         majority = (len(sets_all) + 1) // 2
-        universe = sorted(set().union(*sets_all))
-        sets = [([], []) for _ in sets_all]
-        clears = [([], []) for _ in sets_all]
-        for pr in universe:
-            have = [pr in s for s in sets_all]
-            new = sum(have) >= majority
-            for i, h in enumerate(have):
-                if h == new:
-                    continue
-                tgt = sets[i] if new else clears[i]
-                tgt[0].append(pr[0])
-                tgt[1].append(pr[1])
+        uniq, cnt = np.unique(np.concatenate(sets_all), return_counts=True)
+        want = uniq[cnt >= majority]
+        w = np.uint64(SHARD_WIDTH)
+
+        def split(p):
+            return (p // w).tolist(), (p % w).tolist()
+        sets = [split(np.setdiff1d(want, have, assume_unique=True)) for have in sets_all]
+        clears = [split(np.setdiff1d(have, want, assume_unique=True)) for have in sets_all]
         with self.mu:
             for r, c in zip(*sets[0]):
                 self._unprotected_set_bit(r, self.shard * SHARD_WIDTH + c)

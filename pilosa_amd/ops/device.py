@@ -625,7 +625,9 @@ class DeviceView:
             return set()
         return self._merge_jobs(jobs, 0 if kind == "pos" else 1, clear)
 
-    WRITE_CHUNK = 16384   # containers per merge launch (128 MiB of bitmap scratch)
+    # containers per merge launch: 2 GiB of bitmap scratch (8 KiB each) on a
+    # 288 GB device, so an import request's whole batch of shards shares a few launches
+    WRITE_CHUNK = 1 << 18
 
     def _merge_jobs(self, jobs, mode: int, clear: bool) -> set:
         """Merge + emit every job's containers in shared launches, then splice

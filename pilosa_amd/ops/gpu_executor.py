@@ -427,7 +427,13 @@ class GpuExecutor:
             o = self.engine.bsi_minmax(filt, bv, b.bit_depth)
         except CompileError:
             raise NotImplementedError
-        return [ValCount(v + b.base, n) if n else ValCount() for v, n in zip(*_minmax_per_shard(o, which))]
+        vals, cnts = _minmax_per_shard(o, which)
+        if shardwidth.WIDE:
+            # per fragment: the extreme over its sub-shards, counted over all of them
+            # (fragment.min/max counts every column of the wide shard holding it)
+            vals, cnts = _fold_subshards_value(np.asarray(vals, np.int64), np.asarray(cnts, np.int64),
+                                               which == "min")
+        return [ValCount(int(v) + b.base, int(n)) if n else ValCount() for v, n in zip(vals, cnts)]
 
     def hbm_bytes(self) -> int:
         with self.mu:
@@ -968,9 +974,6 @@ class GpuExecutor:
         NotImplementedError for the shapes the host answers (Tanimoto and
         attribute filters: per-row attribute reads)."""
         ex = self._ex()
-        if shardwidth.WIDE:
-            # rank caches are per (wide) fragment; the device ranks per 2^20 sub-shard
-            raise NotImplementedError
         fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
         if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
             raise NotImplementedError
@@ -1014,9 +1017,6 @@ class GpuExecutor:
         ``defer`` (with ``self.comm``): a pending result whose last
         collectives are still in flight (parallel/collectives.Pending)."""
         ex = self._ex()
-        if shardwidth.WIDE:
-            self.topn_decline = f"shard width 2^{shardwidth.EXPONENT}"
-            return None
         params = []
         fields: Dict[str, Tuple] = {}
         for c in calls:
@@ -1088,7 +1088,7 @@ class GpuExecutor:
         builds) what it needs -- rank caches, slot index -- without any
         collective, so the ranks of a node can agree on the answer first
         (parallel/mesh.py OP_TOPN)."""
-        if not shards or shardwidth.WIDE:
+        if not shards:
             return False
         ex = self._ex()
         try:
@@ -1170,7 +1170,9 @@ class GpuExecutor:
                 try:
                     for i in range(0, len(exprs), MAX_GROUPS_PER_LAUNCH):
                         self.launches += 1
-                        m = self.engine.count_per_shard(exprs[i:i + MAX_GROUPS_PER_LAUNCH])  # [R, S]
+                        m = self.engine.count_per_shard(exprs[i:i + MAX_GROUPS_PER_LAUNCH])  # [R, arena shards]
+                        if rc.M > 1:   # per fragment: the sum over its sub-shards
+                            m = m.reshape(len(m), rc.S, rc.M).sum(axis=2)
                         for r, row_counts in zip(rws[i:i + MAX_GROUPS_PER_LAUNCH], m):
                             counted[r] = row_counts
                 except CompileError:
@@ -1273,6 +1275,11 @@ class GpuExecutor:
         view (stale in between: the pair-count path)."""
         if rv is None or rc is None or not self.topn_index_enabled or rc.K == 0:
             self._topn_index_why = "disabled/empty"
+            return None
+        if rc.M > 1:
+            # the slot index walks each fragment's ranks over one 2^20-column
+            # arena shard; wider fragments take the pair-count path
+            self._topn_index_why = f"shard width 2^{shardwidth.EXPONENT}"
             return None
         from pilosa_amd.ops.topn_index import MAX_SLOTS, DeviceTopNIndex
         key = (index, fname, tuple(shards))
@@ -1496,6 +1503,20 @@ def _fold_subshards(rid: np.ndarray, cnt: np.ndarray, is_min: bool, filtered: bo
     n = (np.where(hit, c, 0).sum(axis=1) if filtered else hit.any(axis=1).astype(np.int64))
     ok = live.any(axis=1)
     return np.where(ok, best, 0), np.where(ok, n, 0)
+
+
+def _fold_subshards_value(vals: np.ndarray, cnts: np.ndarray, is_min: bool):
+    """Per-device-shard (value, count) -> per fragment wider than 2^20
+    columns: the min (max) value over its sub-shards with the counts of
+    every sub-shard holding that value summed."""
+    M = shardwidth.DEVICE_SUBSHARDS
+    v, c = vals.reshape(-1, M), cnts.reshape(-1, M)
+    live = c > 0
+    big = np.iinfo(np.int64).max
+    key = np.where(live, v, big if is_min else -big)
+    best = key.min(axis=1) if is_min else key.max(axis=1)
+    n = np.where(live & (v == best[:, None]), c, 0).sum(axis=1)
+    return np.where(n > 0, best, 0), n
 
 
 def _minmax_per_shard(o: np.ndarray, which: str):

@@ -80,7 +80,13 @@ class DeviceRankCaches:
         from pilosa_amd import _roaring
         self.view = view
         self.generation = view.generation
-        S = view.S
+        # one rank cache per fragment; a fragment wider than 2^20 columns is
+        # M device sub-shards of the arena (pilosa_amd/shardwidth.py), whose
+        # row counts are summed per fragment
+        S = len(frags)
+        if S and view.S % S:
+            raise ValueError(f"DeviceRankCaches: {view.S} arena shards for {S} fragments")
+        self.M = view.S // S if S else 1
         dev = view.device
         self.S = S
         # the persisted .cache ids serve a fragment whose cache was never
@@ -100,9 +106,7 @@ class DeviceRankCaches:
         ids = ids[keep] if len(ids) else ids
         t_shard = torch.from_numpy(shard_of).to(dev)
         t_dense = dense_dev(view, torch.from_numpy(np.ascontiguousarray(ids).view(np.int64)).to(dev))
-        t_cnt = torch.zeros(t_dense.numel(), dtype=torch.int32, device=dev)
-        if t_dense.numel():
-            kernels().row_counts(view.viewdev_tensor(), t_shard, t_dense, t_cnt)
+        t_cnt = self._counts(t_shard, t_dense)
         if warm:
             # host rank caches of fragments loaded on the host (their live counts)
             hs, hd, hc = [], [], []
@@ -155,6 +159,34 @@ class DeviceRankCaches:
     def nbytes(self) -> int:
         return 8 * self.S * self.K
 
+    def _counts(self, t_shard, t_dense):
+        """int32 count of each (fragment index, dense row) entry over the
+        fragment's arena shards (row_counts_kernel)."""
+        import torch
+        N = int(t_dense.numel())
+        dev = self.view.device
+        if not N:
+            return torch.zeros(0, dtype=torch.int32, device=dev)
+        M = self.M
+        if M > 1:
+            t_shard = (t_shard.to(torch.int32)[:, None] * M +
+                       torch.arange(M, dtype=torch.int32, device=dev)[None, :]).reshape(-1).contiguous()
+            t_dense = t_dense.to(torch.int32).repeat_interleave(M).contiguous()
+        out = torch.zeros(N * M, dtype=torch.int32, device=dev)
+        kernels().row_counts(self.view.viewdev_tensor(), t_shard.contiguous(), t_dense.contiguous(), out)
+        return out if M == 1 else out.view(N, M).sum(dim=1, dtype=torch.int32)
+
+    def _count_matrix(self, u32):
+        """int32[U, S]: every candidate row's count in every fragment."""
+        import torch
+        U = int(u32.numel())
+        D = self.view.S
+        cm = torch.empty((U, D), dtype=torch.int32, device=self.view.device)
+        kernels().topn_cache_counts(self.view.viewdev_tensor(), D, u32, cm)
+        if self.M > 1:
+            cm = cm.view(U, self.S, self.M).sum(dim=2, dtype=torch.int32).contiguous()
+        return cm
+
     def host_lists(self):
         """(rows int64[S, K], counts int64[S, K]) on the host (tests, the
         multi-rank slot index)."""
@@ -173,9 +205,7 @@ class DeviceRankCaches:
         d = self.view.dense_many(np.asarray(ids, dtype=np.uint64)).astype(np.int32)
         t_dense = torch.from_numpy(np.tile(d, S)).to(dev)
         t_shard = torch.arange(S, dtype=torch.int32, device=dev).repeat_interleave(P)
-        out = torch.zeros(S * P, dtype=torch.int32, device=dev)
-        kernels().row_counts(self.view.viewdev_tensor(), t_shard, t_dense, out)
-        return out.view(S, P).cpu().numpy()
+        return self._counts(t_shard, t_dense).view(S, P).cpu().numpy()
 
     # ------------------------------------------------------------ cache-only TopN
     def nosrc_phase1(self, ns: Sequence[int], thresholds: Sequence[int]):
@@ -229,8 +259,12 @@ class DeviceRankCaches:
             uk, inv = torch.unique(key, return_inverse=True)
             ud = (uk >> 32).to(torch.int32).contiguous()
             ut = (uk & 0xFFFFFFFF).to(torch.int32).contiguous()
-            res = torch.zeros(int(uk.numel()), dtype=torch.int64, device=dev)
-            kernels().row_counts_sum(self.view.viewdev_tensor(), self.S, ud, ut, res)
+            if self.M == 1:
+                res = torch.zeros(int(uk.numel()), dtype=torch.int64, device=dev)
+                kernels().row_counts_sum(self.view.viewdev_tensor(), self.S, ud, ut, res)
+            else:   # the threshold applies to a fragment's count, summed over its sub-shards
+                cm = self._count_matrix(ud)
+                res = torch.where(cm >= ut.clamp(min=1)[:, None], cm, torch.zeros_like(cm)).sum(dim=1)
             out = res[inv]
         return out
 
@@ -294,13 +328,11 @@ class DeviceRankCaches:
         if got is None:
             u, inv = self._candidates(nmax)
             U = int(u.numel())
-            if U * self.S > FUSED_MAX_CELLS:
+            if U * self.view.S > FUSED_MAX_CELLS:
                 got = False
             else:
                 u32 = u.to(torch.int32).contiguous()
-                cm = torch.empty((U, self.S), dtype=torch.int32, device=self.view.device)
-                kernels().topn_cache_counts(self.view.viewdev_tensor(), self.S, u32, cm)
-                got = (u32, inv.to(torch.int32).contiguous(), cm)
+                got = (u32, inv.to(torch.int32).contiguous(), self._count_matrix(u32))
             memo[nmax] = got
         return got
 
@@ -380,7 +412,11 @@ class DeviceRankCaches:
         # phase 2: every candidate row re-counted once per distinct threshold
         ud = u.clamp(min=0).to(torch.int32).contiguous()
         res = torch.zeros((len(uniq_t), U), dtype=torch.int64, device=dev)
+        cm = self._count_matrix(ud) if self.M > 1 else None   # per fragment over its sub-shards
         for ti, t in enumerate(uniq_t):
+            if cm is not None:
+                res[ti] = torch.where(cm >= t, cm, torch.zeros_like(cm)).sum(dim=1)
+                continue
             kernels().row_counts_sum(self.view.viewdev_tensor(), self.S, ud,
                                      torch.full((U,), t, dtype=torch.int32, device=dev), res[ti])
         if len(uniq_t) == 1:

@@ -4,8 +4,9 @@ differential suite and the executor-path TopN suite run unchanged at that
 width in a fresh interpreter (the width is fixed per process, like the
 reference's build tag), every answer compared with the host executor.
 Wider (2^22, the reference CI's SHARD_WIDTH=22): every shard is 4 device
-sub-shards and the executor differential suite runs unchanged (TopN answers
-from the host at these widths: rank caches are per wide fragment).
+sub-shards and the executor and TopN suites run unchanged (rank caches stay
+per fragment with counts summed over its sub-shards; src TopN takes the
+pair-count path instead of the 2^20-column slot index).
 Shift is excluded: its device carry works at 2^20 columns only, so at
 other widths it runs on the host (ops/gpu_executor.py)."""
 import os
@@ -35,7 +36,9 @@ def test_gpu_executor_suite_at_wide_width():
     env = dict(os.environ, PILOSA_SHARD_WIDTH="22")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
                         "--timeout", "300", "--timeout-method", "thread", "-k", "not shift and not Shift",
-                        "tests/test_gpu_executor.py"],
+                        "tests/test_gpu_executor.py", "tests/test_gpu_topn_exec.py"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=850)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout and "skipped" not in r.stdout.splitlines()[-1], r.stdout[-1000:]
+    last = r.stdout.splitlines()[-1]
+    # one skip allowed: the slot-index refresh test (src TopN uses the pair path here)
+    assert " passed" in last and ("skipped" not in last or "1 skipped" in last), r.stdout[-1000:]

@@ -10,6 +10,7 @@ import pytest
 
 from pilosa_amd.executor import Executor
 from pilosa_amd.models.holder import Holder
+from pilosa_amd import shardwidth
 from tests.helpers import SW, Env
 
 pytestmark = pytest.mark.gpu
@@ -94,7 +95,9 @@ def test_concurrent_topn_requests_coalesce(lazy_env):
         t.join()
     for k, q in enumerate(qs):
         assert _pairs(out[k]) == _pairs(want[q]), q
-    assert ex.topn_coalescer.fallbacks == f0, (repr(ex.topn_coalescer.last_error), ex.topn_batch_declined, gpu.topn_decline)
+    if not shardwidth.WIDE:   # wider shards: src calls take the per-call pair-count path by design
+        assert ex.topn_coalescer.fallbacks == f0, (repr(ex.topn_coalescer.last_error), ex.topn_batch_declined,
+                                                   gpu.topn_decline)
 
 
 def test_rank_caches_from_cache_files_equal_host_caches(lazy_env):
@@ -200,6 +203,8 @@ def test_nosrc_fused_kernels_equal_torch_batch(lazy_env, monkeypatch):
     assert [_pairs(r) for r in rc.topn_nosrc(ns, ths)] == [_pairs(r) for r in ref]
 
 
+@pytest.mark.skipif(shardwidth.WIDE, reason="the slot index is per 2^20-column arena shard: wider "
+                    "fragments answer src TopN through the pair-count path")
 def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
     """A write burst into one shard (new bits, and a tail row pushed up the
     rank order) re-indexes only that shard's slot region in place: the next
