@@ -99,7 +99,8 @@ class Server:
         self.cluster_disabled = cluster_disabled
         self._node_id = node_id
         self.replica_n = replica_n
-        self.hasher = ModHasher() if hasher == "mod" else JumpHasher()
+        # "jump" (the reference's default), "mod", or a hasher object with hash(key, n)
+        self.hasher = hasher if hasattr(hasher, "hash") else ModHasher() if hasher == "mod" else JumpHasher()
         self.gpu = None
         self.gpu_mode = gpu
         self.gpu_device = gpu_device
@@ -189,6 +190,8 @@ class Server:
         self._start_loop(self._runtime_loop, "runtime")
         if self.translation_primary is not None:
             self._start_translate_replica()
+        elif not self.cluster_disabled:
+            self._start_translate_follower()
         from pilosa_amd.utils.gcnotify import GCNotifier
         self.gc_notifier = GCNotifier(self.stats).start()
         from pilosa_amd.utils.diagnostics import DiagnosticsCollector
@@ -218,6 +221,44 @@ class Server:
                     self.logger.debugf("translate replication: %s", e)
                 self._closing.wait(0.5)
         self._start_loop(loop, "translate-replica")
+
+    def _start_translate_follower(self):
+        """Without a configured primary, the cluster's coordinator is the
+        translate primary: every other node tails its key log and forwards
+        keys it has not seen, so ids agree cluster-wide and any node answers
+        with keys (the reference replicates the translate log between nodes
+        on membership changes, cluster.go:1969-1971, translate.go:197-240).
+        Re-evaluated as the coordinator changes."""
+        ts = self.holder.translate
+        state = {"primary": None}
+
+        def primary_uri():
+            c = self.cluster.coordinator() if self.cluster is not None else None
+            return None if c is None or c.id == self.node.id else c.uri
+
+        def forward(index, field, keys):
+            uri = state["primary"]
+            if uri is None:
+                raise PilosaError("translate primary unavailable")
+            return self.client.translate_keys(uri, index, field, keys)
+
+        def loop():
+            while not self._closing.is_set():
+                uri = primary_uri()
+                if uri != state["primary"]:
+                    state["primary"] = uri
+                    ts.read_only = uri is not None
+                    ts.forward = forward if uri is not None else None
+                if uri is not None:
+                    try:
+                        data = self.client.translate_data(uri, ts.size)
+                        if data:
+                            ts.apply_log(data)
+                            continue
+                    except Exception as e:  # noqa: BLE001 - coordinator briefly unavailable
+                        self.logger.debugf("translate replication: %s", e)
+                self._closing.wait(0.2)
+        self._start_loop(loop, "translate-follower")
 
     def _refresh_diagnostics(self):
         d = self.diagnostics

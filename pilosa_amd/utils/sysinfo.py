@@ -85,6 +85,18 @@ class SystemInfo:
             return int(self._ps.virtual_memory().used)
         return 0
 
+    def mem_free(self) -> int:
+        if self._ps is not None:
+            return int(self._ps.virtual_memory().free)
+        with open("/proc/meminfo") as fh:
+            for line in fh:
+                if line.startswith("MemFree:"):
+                    return int(line.split()[1]) * 1024
+        return 0
+
+    def cpu_arch(self) -> str:
+        return platform.machine()
+
     def gpus(self) -> list:
         """Visible GPUs (name, HBM bytes) without initialising HIP in a
         process that has not touched the GPU yet."""
@@ -104,5 +116,6 @@ class SystemInfo:
         return {"hostname": self.hostname(), "platform": self.platform(), "family": self.family(),
                 "osVersion": self.os_version(), "kernelVersion": self.kernel_version(), "cpuModel": self.cpu_model(),
                 "cpuPhysicalCores": self.cpu_cores(), "cpuLogicalCores": self.cpu_threads(),
-                "cpuMHz": self.cpu_mhz(), "memory": self.mem_total(), "memoryUsed": self.mem_used(),
+                "cpuMHz": self.cpu_mhz(), "cpuArch": self.cpu_arch(), "memory": self.mem_total(),
+                "memoryUsed": self.mem_used(), "memoryFree": self.mem_free(),
                 "uptime": self.uptime()}

@@ -5,7 +5,6 @@ content types.  The cases run in the reference's order against one server,
 since later cases depend on the state earlier ones leave behind."""
 import base64
 import json
-import math
 import tempfile
 
 import pytest
@@ -21,7 +20,7 @@ PB = {"Content-Type": "application/x-protobuf", "Accept": "application/x-protobu
 ROARING = bytes.fromhex("3B3001000100000900010000000100010009000100")
 
 
-@pytest.fixture(scope="module")
+@pytest.fixture
 def node():
     s = Server(tempfile.mkdtemp(), bind="127.0.0.1:0", gpu="off", logger=CaptureLogger()).open()
     yield s
@@ -43,12 +42,12 @@ def _schema_field(srv, index, name):
     return None
 
 
-def test_not_found_and_empty_schema(node):  # "Not Found" :88, "SchemaEmpty" :96
+def _not_found_and_empty_schema(node):  # "Not Found" :88, "SchemaEmpty" :96
     assert _req(node, "GET", "/no_such_path")[0] == 404
     assert _req(node, "GET", "/schema") == (200, b'{"indexes":null}\n')
 
 
-def test_post_schema(node):  # "PostSchema" :109
+def _post_schema(node):  # "PostSchema" :109
     body = ('{"indexes":[{"name":"blah","options":{"keys":false,"trackExistence":true},"fields":[{"name":"f1",'
             '"options":{"type":"set","cacheType":"ranked","cacheSize":50000,"keys":false}}],"shardWidth":1048576}]}')
     st, out = _req(node, "POST", "/schema", body.encode())
@@ -57,7 +56,7 @@ def test_post_schema(node):  # "PostSchema" :109
     assert _req(node, "DELETE", "/index/blah")[0] == 200
 
 
-def test_info(node):  # "Info" :138
+def _info(node):  # "Info" :138
     st, body = _req(node, "GET", "/info")
     assert st == 200
     d = _json(body)
@@ -75,7 +74,7 @@ def _populate(node):
     return i0, i1
 
 
-def test_schema_and_import_roaring(node):  # "Schema" :190, "ImportRoaring" :204, "...FieldTypeFail" :232
+def _schema_and_import_roaring(node):  # "Schema" :190, "ImportRoaring" :204, "...FieldTypeFail" :232
     i0, _ = _populate(node)
     target = ('{"indexes":[{"name":"i0","options":{"keys":false,"trackExistence":false},"fields":['
               '{"name":"f0","options":{"type":"set","cacheType":"ranked","cacheSize":50000,"keys":false}},'
@@ -95,7 +94,7 @@ def test_schema_and_import_roaring(node):  # "Schema" :190, "ImportRoaring" :204
     assert st == 400
 
 
-def test_status_and_abort_without_resize(node):  # "Status" :260, "Abort no resize job" :275
+def _status_and_abort_without_resize(node):  # "Status" :260, "Abort no resize job" :275
     st, body = _req(node, "GET", "/status")
     assert st == 200
     d = _json(body)
@@ -112,7 +111,7 @@ def _bits(node):
         f1.set_bit(40, c)
 
 
-def test_max_shard_and_shard_args(node):  # "Max Shard" :295 .. "Query params err" :352
+def _max_shard_and_shard_args(node):  # "Max Shard" :295 .. "Query params err" :352
     _bits(node)
     assert _req(node, "GET", "/internal/shards/max") == (200, b'{"standard":{"i0":3,"i1":0}}\n')
     assert _req(node, "POST", "/index/i0/query?shards=0,1", b"Count(Row(f0=30))") == (200, b'{"results":[2]}\n')
@@ -126,7 +125,7 @@ def test_max_shard_and_shard_args(node):  # "Max Shard" :295 .. "Query params er
         (400, b'{"error":"db is not a valid argument"}\n')
 
 
-def test_uint64_protobuf_and_content_types(node):  # "Uint64 protobuf" :362, "Shards args protobuf" :315
+def _uint64_protobuf_and_content_types(node):  # "Uint64 protobuf" :362, "Shards args protobuf" :315
     import urllib.request
     r = urllib.request.Request(f"http://127.0.0.1:{node.uri.port}/index/i0/query", data=b"Count(Row(f0=30))",
                                method="POST", headers={"Accept": "application/x-protobuf"})
@@ -142,7 +141,7 @@ def test_uint64_protobuf_and_content_types(node):  # "Uint64 protobuf" :362, "Sh
         assert resp.headers["Content-Type"] == "application/json"
 
 
-def test_row_json_and_attrs(node):  # "Row JSON" :381, "ColumnAttrs_JSON" :400
+def _row_json_and_attrs(node):  # "Row JSON" :381, "ColumnAttrs_JSON" :400
     cols = (SW + 1, SW + 2, 3 * SW + 4)
     assert _req(node, "POST", "/index/i0/query", b"Row(f0=30)") == \
         (200, ('{"results":[{"attrs":{},"columns":[%d,%d,%d]}]}\n' % cols).encode())
@@ -162,7 +161,7 @@ def _attrs(m):
     return out
 
 
-def test_row_protobuf(node):  # "Row pbuf" :411, "Row columnattrs protobuf" :436
+def _row_protobuf(node):  # "Row pbuf" :411, "Row columnattrs protobuf" :436
     cols = [SW + 1, SW + 2, 3 * SW + 4]
     st, body = _req(node, "POST", "/index/i0/query", b"Row(f0=30)", {"Accept": "application/x-protobuf"})
     m = pb.QueryResponse()
@@ -179,7 +178,7 @@ def test_row_protobuf(node):  # "Row pbuf" :411, "Row columnattrs protobuf" :436
     assert len(a) == 2 and a[0].ID == SW + 1 and _attrs(a[0].Attrs) == {"x": "y"}
 
 
-def test_query_pairs_and_errors(node):  # "Query Pairs JSON" :484 .. "Query empty" :538
+def _query_pairs_and_errors(node):  # "Query Pairs JSON" :484 .. "Query empty" :538
     assert _req(node, "POST", "/index/i0/query", b"TopN(f0, n=2)") == \
         (200, b'{"results":[[{"id":30,"count":3},{"id":31,"count":1}]]}\n')
     st, body = _req(node, "POST", "/index/i0/query", b"TopN(f0, n=2)", {"Accept": "application/x-protobuf"})
@@ -195,18 +194,16 @@ def test_query_pairs_and_errors(node):  # "Query Pairs JSON" :484 .. "Query empt
     assert _req(node, "POST", "/index/i0/query", b"")[1] == b'{"results":[]}\n'
 
 
-@pytest.mark.parametrize("name,opts,lo,hi", [  # "Query int field unbounded" :546, "... min" :575, "... max" :604
-    ("f-int-ubound", '{"options":{"type":"int"}}', -2 ** 63, 2 ** 63 - 1),
-    ("f-int-ubound-min", '{"options":{"type":"int", "max": 10}}', -2 ** 63, 10),
-    ("f-int-ubound-max", '{"options":{"type":"int", "min": -10}}', -10, 2 ** 63 - 1)])
-def test_int_field_unbounded(node, name, opts, lo, hi):
-    assert _req(node, "POST", f"/index/i0/field/{name}", opts.encode())[0] == 200
-    f = _schema_field(node, "i0", name)
-    assert f is not None and (f["options"]["min"], f["options"]["max"]) == (lo, hi)
-    assert math.isfinite(lo)
+def _int_field_unbounded(node):  # "Query int field unbounded" :546, "... min" :575, "... max" :604
+    for name, opts, lo, hi in (("f-int-ubound", '{"options":{"type":"int"}}', -2 ** 63, 2 ** 63 - 1),
+                               ("f-int-ubound-min", '{"options":{"type":"int", "max": 10}}', -2 ** 63, 10),
+                               ("f-int-ubound-max", '{"options":{"type":"int", "min": -10}}', -10, 2 ** 63 - 1)):
+        assert _req(node, "POST", f"/index/i0/field/{name}", opts.encode())[0] == 200
+        f = _schema_field(node, "i0", name)
+        assert f is not None and (f["options"]["min"], f["options"]["max"]) == (lo, hi)
 
 
-def test_int_field_min_above_max_and_methods(node):  # :633, "Method not allowed" :644, "Err Parse" :652
+def _int_field_min_above_max_and_methods(node):  # :633, "Method not allowed" :644, "Err Parse" :652
     assert _req(node, "POST", "/index/i0/field/f-int-ubound-err",
                 b'{"options":{"type":"int", "min": 10, "max": -10}}')[0] == 400
     assert _req(node, "GET", "/index/i0/query")[0] == 405
@@ -218,7 +215,7 @@ def test_int_field_min_above_max_and_methods(node):  # :633, "Method not allowed
     assert st == 400 and body.startswith(b'{"error":"parsing: ') and body.endswith(b'"}\n')
 
 
-def test_delete_index_and_field(node):  # "delete index" :662, "Field delete" :677
+def _delete_index_and_field(node):  # "delete index" :662, "Field delete" :677
     node.holder.create_index_if_not_exists("i", track_existence=False)
     assert _req(node, "DELETE", "/index/i") == (200, b'{"success":true}\n')
     assert node.holder.index("i") is None
@@ -234,7 +231,7 @@ def _diff_body(store):
     return json.dumps({"blocks": blks}).encode()
 
 
-def test_attr_diffs(node):  # "AttrStore Diff" :702, "field attrstore diff" :743
+def _attr_diffs(node):  # "AttrStore Diff" :702, "field attrstore diff" :743
     i = node.holder.create_index_if_not_exists("i", track_existence=False)
     for k, v in ((1, {"foo": 1, "bar": 2}), (100, {"x": "y"}), (200, {"snowman": "\u2603"})):
         i.column_attr_store.set_attrs(k, v)
@@ -248,7 +245,7 @@ def test_attr_diffs(node):  # "AttrStore Diff" :702, "field attrstore diff" :743
         (200, want)
 
 
-def test_version_fragment_nodes_expvars_recalculate(node):  # "Version" :771 .. "Recalculate Caches" :822
+def _version_fragment_nodes_expvars_recalculate(node):  # "Version" :771 .. "Recalculate Caches" :822
     from pilosa_amd import __version__
     assert _req(node, "GET", "/version") == (200, ('{"version":"%s"}\n' % __version__.lstrip("v")).encode())
     st, body = _req(node, "GET", "/internal/fragment/nodes?index=i&shard=0")
@@ -257,6 +254,27 @@ def test_version_fragment_nodes_expvars_recalculate(node):  # "Version" :771 .. 
     assert _req(node, "GET", "/internal/fragment/nodes?shard=0")[0] == 400
     assert _req(node, "GET", "/debug/vars")[0] == 200
     assert _req(node, "POST", "/recalculate-caches")[0] == 204
+
+
+def test_handler_endpoints(node):
+    """The reference's subtests, in its order (later cases build on earlier state)."""
+    _not_found_and_empty_schema(node)
+    _post_schema(node)
+    _info(node)
+    _schema_and_import_roaring(node)
+    _status_and_abort_without_resize(node)
+    _max_shard_and_shard_args(node)
+    _uint64_protobuf_and_content_types(node)
+    _row_json_and_attrs(node)
+    _row_protobuf(node)
+    _query_pairs_and_errors(node)
+    _int_field_unbounded(node)
+    _int_field_min_above_max_and_methods(node)
+    _delete_index_and_field(node)
+    _attr_diffs(node)
+    _version_fragment_nodes_expvars_recalculate(node)
+    _index_handlers(node)
+    _translate_keys(node)
 
 
 def test_cors_preflight():  # "CORS" :830
@@ -277,7 +295,7 @@ def test_cors_preflight():  # "CORS" :830
         s.close()
 
 
-def test_index_handlers(node):  # "index handlers" :860
+def _index_handlers(node):  # "index handlers" :860
     ok = (200, b'{"success":true}\n')
     assert _req(node, "POST", "/index/idx1", b"") == ok
     assert _req(node, "POST", "/index/idx1", b"") == \
@@ -293,7 +311,7 @@ def test_index_handlers(node):  # "index handlers" :860
         (404, b'{"success":false,"error":{"message":"deleting index: index not found"}}\n')
 
 
-def test_translate_keys(node):  # "translate keys" :942
+def _translate_keys(node):  # "translate keys" :942
     ok = (200, b'{"success":true}\n')
     assert _req(node, "POST", "/index/i1-tr", b'{"options":{"keys":true}}') == ok
     assert _req(node, "POST", "/index/i1-tr/field/f1", b'{"options":{"keys":true}}') == ok
