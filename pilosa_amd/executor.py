@@ -421,11 +421,17 @@ class Executor:
                 self._validate_call_args(c)
             if any("ids" in c.args for c in q.calls):
                 return [self.execute_call(index, c, shards, opt) for c in q.calls]   # phase 2 only: map step
+            key = (index, tuple(shards))
             if len(q.calls) == 1 and self.coalesce:
                 c = q.calls[0]
-                key = (index, tuple(shards))
                 return [self.topn_coalescer.submit(key, c, lambda: self.execute_call(index, c, shards, opt))]
-            res = self._run_topn_batch((index, tuple(shards)), q.calls)
+            if self.coalesce:
+                # concurrent multi-call requests share launches too (the hot-rank
+                # kernel counts up to 32 queries per streamed container)
+                return self.topn_coalescer.submit_many(
+                    key, q.calls, lambda: self._run_topn_batch(key, q.calls) or
+                    [self.execute_call(index, c, shards, opt) for c in q.calls])
+            res = self._run_topn_batch(key, q.calls)
             if res is not None:
                 return res
         if self.gpu is not None and len(q.calls) > 1 and all(c.name == "Count" for c in q.calls) and \

@@ -975,12 +975,24 @@ class GpuExecutor:
         attribute filters: per-row attribute reads)."""
         ex = self._ex()
         fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
-        if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
+        if len(c.children) > 1:
             raise NotImplementedError
         frags = self._topn_frags(index, fname, shards)
         rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
         src = self.plan(index, c.children[0], shards) if c.children else None
         rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+        keep = None
+        if attr_name and attr_values:
+            # fragment.top's attribute filter (fragment.go:1586-1600): rows whose
+            # attribute value is one of the listed ones
+            from pilosa_amd.models.fragment import _hashable
+            store = self.holder.field(index, fname).row_attr_store
+            want = {_hashable(v) for v in attr_values}
+
+            def keep(rid, store=store, want=want, name=attr_name):
+                a = store.attrs(rid)
+                return bool(a) and a.get(name) is not None and _hashable(a.get(name)) in want
+        self._topn_filters = (tanimoto if src is not None else 0, keep)
         return (fname, n, ids, threshold), rc, rv, src
 
     def topn(self, index: str, c: Call, shards: List[int]) -> List[Pair]:
@@ -988,8 +1000,13 @@ class GpuExecutor:
         phase 1 = per-shard ``fragment.top`` results summed by row (untrimmed),
         with ``ids=`` the per-shard exact re-count of those rows."""
         (fname, n, ids, threshold), rc, rv, src = self._topn_setup(index, c, shards)
+        tan, keep = self._topn_filters
         if rc is None or src is EMPTY or rc.K == 0:
             return []
+        if tan or keep is not None:
+            # Tanimoto / attribute filters: device counts, the exact heap walk
+            # with both filters replayed on the host (fragment.go:1568-1700)
+            return self._topn_pairs_path(rc, rv, src, n, ids, threshold, tan=tan, keep=keep)
         if src is None:
             self.launches += 1
             return rc.shard_pairs_nosrc(0 if ids else n, threshold, ids or None)
@@ -1132,7 +1149,7 @@ class GpuExecutor:
         self._frag_lists[key] = (epoch, frags)
         return frags
 
-    def _topn_pairs_path(self, rc, rv, src, n: int, ids, threshold: int) -> List[Pair]:
+    def _topn_pairs_path(self, rc, rv, src, n: int, ids, threshold: int, tan: int = 0, keep=None) -> List[Pair]:
         """Src TopN without a slot index (while it is rebuilt, or too large for
         LDS): each shard's fragment.top() walks its cache in order and stops
         once a row's cached count falls below the heap threshold, so usually
@@ -1154,6 +1171,19 @@ class GpuExecutor:
             for si in range(rc.S):
                 live = counts[si] > 0
                 per_shard_pairs.append(list(zip(rows[si][live].tolist(), counts[si][live].tolist())))
+        if src is None:
+            # cache-only with an attribute filter: the cached counts are the counts
+            self.launches += 1
+            total: Dict[int, int] = {}
+            for si in range(rc.S):
+                for p in _replay_top(per_shard_pairs[si], None, 0 if ids else n, threshold, keep=keep):
+                    total[p.id] = total.get(p.id, 0) + p.count
+            return sort_pairs([Pair(k2, v) for k2, v in total.items()])
+        src_counts = None
+        if tan:
+            self.launches += 1
+            sc = self.engine.count_per_shard([src])[0]        # |src| per arena shard
+            src_counts = sc.reshape(rc.S, rc.M).sum(axis=1) if rc.M > 1 else sc
         counted: Dict[int, np.ndarray] = {}
         depth = [0] * rc.S
         k = max(256, 2 * n) if not ids else max((len(p) for p in per_shard_pairs), default=0)
@@ -1181,7 +1211,8 @@ class GpuExecutor:
             for si in pending:
                 try:
                     got = _replay_top(per_shard_pairs[si], lambda rid, si=si: _counted(counted, rid, si),
-                                      0 if ids else n, threshold)
+                                      0 if ids else n, threshold, tan=tan,
+                                      src_count=int(src_counts[si]) if src_counts is not None else 0, keep=keep)
                 except _NeedMore:
                     nxt.append(si)
                     continue
@@ -1603,18 +1634,40 @@ def _counted(counted: Dict[int, np.ndarray], rid: int, si: int) -> int:
     return int(row[si])
 
 
-def _replay_top(pairs: List[Tuple[int, int]], count_of, n: int, min_threshold: int) -> List[Pair]:
-    """fragment.top() heap logic with precomputed src∩row counts."""
+def _replay_top(pairs: List[Tuple[int, int]], count_of, n: int, min_threshold: int, tan: int = 0,
+                src_count: int = 0, keep=None) -> List[Pair]:
+    """fragment.top() heap logic (fragment.go:1568-1700) with precomputed
+    src∩row counts (``count_of``; None = no src, the cached counts), the
+    Tanimoto window and the attribute filter ``keep``."""
     import heapq
+    import math
     heap: List[Tuple[int, int]] = []
+    min_t = max_t = 0.0
+    if tan > 0:
+        min_t = float(src_count * tan) / 100
+        max_t = float(src_count * 100) / float(tan)
     for rid, cnt in pairs:
-        if cnt == 0 or cnt < min_threshold:
+        if cnt == 0:
+            continue
+        if tan > 0:
+            if cnt <= min_t or cnt >= max_t:
+                continue
+        elif cnt < min_threshold:
+            continue
+        if keep is not None and not keep(rid):
             continue
         if n == 0 or len(heap) < n:
-            count = count_of(rid)
-            if count == 0 or count < min_threshold:
+            count = cnt if count_of is None else count_of(rid)
+            if count == 0:
+                continue
+            if tan > 0:
+                if math.ceil(float(count * 100) / float(cnt + src_count - count)) <= tan:
+                    continue
+            elif count < min_threshold:
                 continue
             heapq.heappush(heap, (count, -rid))
+            if count_of is None and n > 0 and len(heap) == n:
+                break
             continue
         threshold = heap[0][0]
         if threshold < min_threshold or cnt < threshold:

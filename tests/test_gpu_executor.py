@@ -650,3 +650,22 @@ def test_time_range_count_batches_match_host():
         assert sum(want) > 0
     finally:
         env.close()
+
+
+@pytest.mark.parametrize("q", ["TopN(h, Row(h=3), tanimotoThreshold=10)", "TopN(h, Row(f=1), n=5, tanimotoThreshold=1)",
+                               "TopN(h, Row(h=7), n=20, tanimotoThreshold=60)",
+                               'TopN(h, Row(f=0), n=8, attrName="cat", attrValues=[1, 3])',
+                               'TopN(h, n=6, attrName="cat", attrValues=[2])',
+                               'TopN(h, Row(f=2), ids=[1, 2, 3, 4, 5, 6], attrName="cat", attrValues=[1])'])
+def test_topn_tanimoto_and_attr_filters_on_device(envs, q):
+    """fragment.top's Tanimoto window and attribute filter (fragment.go:
+    1586-1650) on the device path: counts on the GPU, the heap walk with both
+    filters replayed exactly."""
+    cpu, gpu = envs
+    if not getattr(test_topn_tanimoto_and_attr_filters_on_device, "_attrs", False):
+        for rid in range(40):
+            cpu.q("i", f"SetRowAttrs(h, {rid}, cat={1 + rid % 3})")
+        test_topn_tanimoto_and_attr_filters_on_device._attrs = True
+    want = cpu.q1("i", q)
+    got = _dev(cpu, gpu, lambda: cpu.q1("i", q))
+    assert [(p.id, p.count) for p in got] == [(p.id, p.count) for p in want]
