@@ -1457,7 +1457,19 @@ def bench_serving(args, base, dev):
         out["count"] = run(queries, args.serve_seconds, 64)
         tcalls = _distinct_topn_calls(2000)
         mix = [q if k % 10 else tcalls[k] for k, q in enumerate(queries[:2000])]
+        prof = None
+        if args.serve_profile:
+            # every server thread's stacks sampled during the mix (/debug/pprof/profile)
+            from pilosa_amd.utils import pprof
+            holder_ = {}
+            prof = threading.Thread(target=lambda: holder_.setdefault(
+                "p", pprof.cpu_profile(seconds=max(2.0, args.serve_seconds / 2), hz=250)), daemon=True)
+            prof.start()
         out["count_topn_mix"] = dict(run(mix, max(2.0, args.serve_seconds / 2), 32), topn_fraction=0.1)
+        if prof is not None:
+            prof.join()
+            with open(args.serve_profile, "w") as fh:
+                fh.write(holder_.get("p", ""))
         out["conns"] = args.serve_conns
         out["httpd"] = srv.httpd.stats() if hasattr(srv.httpd, "stats") else None
 
@@ -1559,6 +1571,7 @@ def main():
     ap.add_argument("--serve-seconds", type=float, default=5.0,
                     help="disk mode, 1 GPU: native-HTTP serving run on the same data dir (0 = skip)")
     ap.add_argument("--serve-conns", type=int, default=128)
+    ap.add_argument("--serve-profile", default="", help="write folded stacks of the server during the mix here")
     ap.add_argument("--import-shards", type=int, default=64, help="serving phase: shards of the HTTP bulk import")
     ap.add_argument("--import-bits-per-shard", type=int, default=200_000)
     ap.add_argument("--import-clients", type=int, default=8)

@@ -1,0 +1,10 @@
+#!/bin/bash
+# pair kernel A/B: v6 vs v6 + next-pair A prefetch (variant 13)
+set -o pipefail
+O=gpurun_out/r04_f
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "and2 or array_size" --timeout 300 --timeout-method thread > $O/pytest_pairs.log 2>&1 || { tail -c 4000 $O/pytest_pairs.log; exit 1; }
+tail -2 $O/pytest_pairs.log
+timeout -k 10 600 python -u scripts/kbench.py --batch 4096 --reps 5 --cq 64 --no-tile --variants 13 > $O/kbench.log 2>&1 || { tail -c 3000 $O/kbench.log; exit 1; }
+tail -4 $O/kbench.log
+bash scripts/gpu_r04_e.sh
