@@ -425,12 +425,10 @@ class Executor:
             if len(q.calls) == 1 and self.coalesce:
                 c = q.calls[0]
                 return [self.topn_coalescer.submit(key, c, lambda: self.execute_call(index, c, shards, opt))]
-            if self.coalesce:
-                # concurrent multi-call requests share launches too (the hot-rank
-                # kernel counts up to 32 queries per streamed container)
-                return self.topn_coalescer.submit_many(
-                    key, q.calls, lambda: self._run_topn_batch(key, q.calls) or
-                    [self.execute_call(index, c, shards, opt) for c in q.calls])
+            # multi-call requests run as their own batch: merging concurrent
+            # ones serialised them and lost the CPU/GPU overlap between requests
+            # (cache-only 15.4k -> 5.2k q/s, src unchanged; 32-query hot-rank
+            # launches are slower than two 16-query ones: profiles/r04_e/)
             res = self._run_topn_batch(key, q.calls)
             if res is not None:
                 return res

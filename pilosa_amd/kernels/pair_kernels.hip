@@ -491,9 +491,10 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
   lds_wait();
 }
 
-// APF: the next pair's A chunk is prefetched too when that pair switches to a
-// new A that is an array of <= 512 values (41.6M of the 58.6M pairs of the
-// headline batch are array x array), so staging it waits on no global load.
+// APF (variant 13): the next pair's A chunk is prefetched too when that pair
+// switches to a new A that is an array of <= 512 values (41.6M of the 58.6M
+// pairs of the headline batch are array x array), so staging it waits on no
+// global load.  Measured 17.7 vs 16.7 ms (profiles/r04_f/): not the default.
 template <int CQ, bool APF = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,

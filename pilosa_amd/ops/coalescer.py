@@ -25,14 +25,13 @@ _FALLBACK = object()
 
 
 class _Slot:
-    __slots__ = ("call", "event", "result", "lead", "owner")
+    __slots__ = ("call", "event", "result", "lead")
 
-    def __init__(self, call, owner=None):
+    def __init__(self, call):
         self.call = call
         self.event = threading.Event()
         self.result: Any = None
         self.lead = False
-        self.owner = owner or self   # the slot whose request thread waits (the last of its request)
 
 
 class CountCoalescer:
@@ -68,34 +67,6 @@ class CountCoalescer:
             return fallback()
         return slot.result
 
-    def submit_many(self, key, calls: Sequence[Any], fallback: Callable[[], List[Any]]) -> List[Any]:
-        """Results of a request's ``calls``, batched (contiguously, in order)
-        with whatever other requests are pending for ``key``; ``fallback()``
-        answers the whole request when any of its calls cannot batch."""
-        if not calls:
-            return []
-        last = _Slot(calls[-1])
-        slots = [_Slot(c, owner=last) for c in calls[:-1]] + [last]
-        with self._lock:
-            self._pending.setdefault(key, []).extend(slots)
-            if key not in self._busy:
-                self._busy.add(key)
-                last.lead = True
-        while True:
-            if last.lead:
-                last.lead = False
-                self._lead(key, last)
-            last.event.wait()
-            if last.lead:
-                last.event.clear()
-                continue
-            break
-        for s in slots:
-            s.event.wait()
-        if any(s.result is _FALLBACK for s in slots):
-            return fallback()
-        return [s.result for s in slots]
-
     def _lead(self, key, mine: _Slot):
         """Run batches for ``key`` until ``mine`` is answered, then pass the
         lead to a waiting request (or release the key)."""
@@ -110,7 +81,7 @@ class CountCoalescer:
                 rest = self._pending.get(key) or []
                 if mine.event.is_set() or not rest:
                     if rest:
-                        nxt = rest[0].owner
+                        nxt = rest[0]
                         nxt.lead = True
                         nxt.event.set()
                     else:

@@ -75,41 +75,3 @@ def test_keys_are_batched_separately():
     assert out == [(i % 3, i) for i in range(24)]
     assert all(len(c) <= 4 and all(x % 3 == k for x in c) for k, c in seen)
 
-
-def test_submit_many_batches_requests_together_in_order():
-    """Multi-call requests join one batch contiguously; each gets its own
-    results in call order; the lead passes to a request's last slot."""
-    import threading
-    import time as _t
-
-    from pilosa_amd.ops.coalescer import CountCoalescer
-    sizes = []
-
-    def run(key, calls):
-        sizes.append(len(calls))
-        _t.sleep(0.01)
-        return [c * 10 for c in calls]
-    co = CountCoalescer(run, max_batch=64)
-    out = {}
-
-    def req(k):
-        calls = [k * 100 + i for i in range(1 + k % 5)]
-        if k % 3 == 0:
-            out[k] = [co.submit("k", calls[0], lambda: None)]
-            calls = calls[:1]
-        else:
-            out[k] = co.submit_many("k", calls, lambda: None)
-        assert out[k] == [c * 10 for c in calls]
-    ts = [threading.Thread(target=req, args=(k,)) for k in range(40)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    assert len(out) == 40 and max(sizes) > 5, sizes
-
-
-def test_submit_many_falls_back_as_a_request():
-    from pilosa_amd.ops.coalescer import CountCoalescer
-    co = CountCoalescer(lambda key, calls: None)
-    assert co.submit_many("k", [1, 2, 3], lambda: ["alone"]) == ["alone"]
-    assert co.fallbacks == 3
