@@ -200,6 +200,8 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_all(force: bool = False, verbose: bool = False):
+    from pilosa_amd import buildinfo
+    buildinfo.write()      # version / build time / release / enterprise of this build
     r = build_roaring(force, verbose)
     build_roaring(force, verbose, stats=True)
     build_pql(force, verbose)

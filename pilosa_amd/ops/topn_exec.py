@@ -155,6 +155,9 @@ class DeviceRankCaches:
         self.cache_cnt = torch.where(live, mat >> 32, torch.zeros_like(mat)).to(torch.int32).contiguous()
         self.cache_dense = torch.where(live, 0xFFFFFFFF - (mat & 0xFFFFFFFF), torch.full_like(mat, -1)) \
             .to(torch.int32).contiguous()
+        if dev.type == "cuda":   # the side stream of cache-only batches starts after this point
+            self._ready = torch.cuda.Event()
+            self._ready.record()
 
     def nbytes(self) -> int:
         return 8 * self.S * self.K
@@ -343,12 +346,41 @@ class DeviceRankCaches:
         memoised count matrix, and a per-query LDS bitonic top-n.  One H2D of
         the batch parameters, one D2H of the Q x n keys.  None when the
         candidate set is too large for it (the torch path then runs)."""
+        import contextlib
+
         import torch
         Q = len(ns)
         nn = [int(n) for n in ns]
         nmax = self.K if any(n == 0 for n in nn) else min(self.K, max(nn))
         if not nmax:
             return [[] for _ in range(Q)]
+        ctx = contextlib.nullcontext()
+        if self.view.device.type == "cuda":
+            # its own stream: a serving mix's TopN batch does not queue behind the
+            # Count batches of other requests on the default stream
+            st = self.__dict__.get("_stream")
+            if st is None:
+                st = self._stream = torch.cuda.Stream(device=self.view.device)
+            st.wait_event(self._ready)
+            ctx = torch.cuda.stream(st)
+        mu = self.__dict__.get("_mu")
+        if mu is None:
+            import threading
+            mu = self.__dict__.setdefault("_mu", threading.Lock())
+        with mu, ctx:   # one batch at a time owns the stream's pinned parameter buffer
+            return self._topn_nosrc_fused_on(ns, nn, nmax, thresholds)
+
+    def _pinned_i32(self, n: int):
+        """Reusable pinned int32 host buffer of at least ``n`` (batch parameters)."""
+        import torch
+        buf = self.__dict__.get("_pin")
+        if buf is None or buf.numel() < n:
+            buf = self._pin = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
+        return buf[:n]
+
+    def _topn_nosrc_fused_on(self, ns, nn, nmax, thresholds):
+        import torch
+        Q = len(ns)
         memo = self._fused_memo(nmax)
         if memo is False:
             return None
@@ -358,13 +390,14 @@ class DeviceRankCaches:
         ths = [max(1, int(t)) for t in thresholds]
         uniq_t = sorted(set(ths))
         KK = min(U, max(nn)) if all(nn) else U
-        prm = np.empty(4 * Q + len(uniq_t), np.int32)
+        pin = self._pinned_i32(4 * Q + len(uniq_t)) if dev.type == "cuda" else None
+        prm = pin.numpy() if pin is not None else np.empty(4 * Q + len(uniq_t), np.int32)
         prm[:Q] = [n if n else self.K for n in nn]
         prm[Q:2 * Q] = ths
         prm[2 * Q:3 * Q] = [uniq_t.index(t) for t in ths]
         prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
         prm[4 * Q:] = uniq_t
-        prm_d = torch.from_numpy(prm).to(dev, non_blocking=True)
+        prm_d = (pin if pin is not None else torch.from_numpy(prm)).to(dev, non_blocking=True)
         member = torch.zeros((Q, U), dtype=torch.uint8, device=dev)
         tot = torch.empty((len(uniq_t), U), dtype=torch.int64, device=dev)
         out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)

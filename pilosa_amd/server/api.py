@@ -445,7 +445,8 @@ class API:
                 "cpuType": si.cpu_model(), "memory": si.mem_total(), "version": __version__, "gpus": gpu}
 
     def version(self) -> str:
-        return __version__.lstrip("v")   # handler.go: strings.TrimPrefix(pilosa.Version, "v")
+        from pilosa_amd import buildinfo
+        return buildinfo.VERSION.lstrip("v")   # handler.go: strings.TrimPrefix(pilosa.Version, "v")
 
     def set_coordinator(self, node_id: str):
         self.validate("SetCoordinator")

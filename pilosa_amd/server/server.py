@@ -58,7 +58,7 @@ class Server:
                  long_query_time: float = 60.0, stats: str = "expvar", logger=None, hasher: str = "jump",
                  max_opn: int = 10000, cluster_disabled: bool = False, mesh_block: int = 1,
                  translation_primary_url: str = "", tls_certificate: str = "", tls_key: str = "",
-                 tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: float = 3600.0,
+                 tls_skip_verify: bool = False, diagnostics_host: str = "", diagnostics_interval: Optional[float] = None,
                  gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
                  lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None,
                  gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None,
@@ -111,7 +111,11 @@ class Server:
         self.tls_certificate, self.tls_key = tls_certificate, tls_key
         self.client.skip_verify = self.probe_client.skip_verify = tls_skip_verify
         self.diagnostics = None
-        self.diagnostics_host, self.diagnostics_interval = diagnostics_host, diagnostics_interval
+        from pilosa_amd import buildinfo
+        # release builds report hourly, others not at all (server/release.go, default.go)
+        self.diagnostics_host = diagnostics_host
+        self.diagnostics_interval = buildinfo.DEFAULT_DIAGNOSTICS_INTERVAL if diagnostics_interval is None \
+            else diagnostics_interval
         self.gc_notifier = None
         self.workers = workers
         self.max_writes = max_writes
@@ -196,7 +200,7 @@ class Server:
         self.gc_notifier = GCNotifier(self.stats).start()
         from pilosa_amd.utils.diagnostics import DiagnosticsCollector
         self.diagnostics = DiagnosticsCollector(self.diagnostics_host, self.diagnostics_interval, self.logger)
-        if self.diagnostics_host:
+        if self.diagnostics_host and self.diagnostics_interval > 0:
             self.diagnostics.start(self._refresh_diagnostics)
         return self
 

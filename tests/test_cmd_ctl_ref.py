@@ -267,3 +267,18 @@ def test_validate_addrs_defaults_and_forms():  # TestConfig_validateAddrs
 def test_validate_addrs_errors(bind, adv, msg):
     with pytest.raises(ConfigError, match=msg):
         validate_addrs(bind, adv)
+
+
+# ---------------------------------------------------------------- build-time knobs (Makefile:9-19)
+def test_build_info_knobs(tmp_path, monkeypatch):
+    """Version / build time / enterprise / release recorded at build time
+    (the reference's ldflags); a release build reports diagnostics hourly,
+    others not at all (server/release.go vs server/default.go)."""
+    import json
+    from pilosa_amd import buildinfo
+    monkeypatch.setattr(buildinfo, "PATH", str(tmp_path / "_buildinfo.json"))
+    info = buildinfo.write({"PILOSA_VERSION": "v9.9.9", "PILOSA_RELEASE": "1", "PILOSA_ENTERPRISE": "1"})
+    assert info["version"] == "v9.9.9" and info["enterprise"] == "1" and info["release"] is True
+    assert buildinfo._load() == json.loads((tmp_path / "_buildinfo.json").read_text()) == info
+    assert info["build_time"].endswith("+0000")
+    assert buildinfo.DEFAULT_DIAGNOSTICS_INTERVAL == (3600.0 if buildinfo.RELEASE else 0.0)
