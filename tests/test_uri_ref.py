@@ -87,3 +87,24 @@ def test_set_invalid_host():                     # TestSetInvalidHost
 
 def test_host_port():                            # TestHostPort
     assert URI.from_host_port("i.pilosa.com", 15001).host_port() == "i.pilosa.com:15001"
+
+
+# ---------------------------------------------------------------- pilosa_test.go TestAddressWithDefaults
+# The reference lists ":", "localhost:", "127.0.0.1:" and "1.2.3.4:" as
+# defaulting to port 10101, but its address grammar (uri.go addressRegexp)
+# rejects a bare trailing colon and the test's error branch accepts any error
+# when no error text is given: the reference answers "invalid address", and
+# so does this URI.
+@pytest.mark.parametrize("addr,want", [
+    ("", "localhost:10101"), ("localhost", "localhost:10101"), ("127.0.0.1:10101", "127.0.0.1:10101"),
+    (":10101", "localhost:10101"), (":55555", "localhost:55555"), ("1.2.3.4", "1.2.3.4:10101"),
+    ("1.2.3.4:55555", "1.2.3.4:55555")])
+def test_address_with_defaults(addr, want):
+    u = URI() if addr == "" else URI.parse(addr)     # AddressWithDefaults: "" is the default URI
+    assert u.host_port() == want
+
+
+@pytest.mark.parametrize("addr", ["[invalid][addr]:port", ":", "localhost:", "127.0.0.1:", "1.2.3.4:"])
+def test_address_with_defaults_invalid(addr):
+    with pytest.raises(ValueError, match="invalid address"):
+        URI.parse(addr)
