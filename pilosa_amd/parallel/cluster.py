@@ -367,6 +367,9 @@ class Cluster:
         with self.mu:
             if any(x.id == n.id for x in self.nodes):
                 return
+            # a joining node describes itself as it sees itself (its own
+            # coordinator until it joins); here only the cluster's counts
+            n.is_coordinator = n.id == self.coordinator_id
             self.nodes = sorted(self.nodes + [n], key=lambda x: x.id)
             if n.id not in self.topology.node_ids:
                 self.topology.node_ids = sorted(self.topology.node_ids + [n.id])

@@ -343,3 +343,18 @@ def test_cluster_exhausting_connections():  # TestClusterExhaustingConnections :
         assert c.query(cl.nodes[0].uri, "testidx", "Count(Row(testfield=0))")["results"] == [500]
     finally:
         cl.close()
+
+
+# ---------------------------------------------------------------- test/pilosa_test.go TestNewCluster
+def test_new_cluster_agrees_on_coordinator_and_status():
+    c = _Cluster(3)
+    try:
+        coords = [[n for n in m.api.hosts() if n.is_coordinator] for m in c.nodes]
+        assert all(len(x) == 1 for x in coords)
+        assert len({x[0].id for x in coords}) == 1, "nodes disagree on the coordinator"
+        from tests.test_server import _req
+        st, body = _req(c.nodes[0], "GET", "/status", headers={"Accept": "application/json"})
+        d = json.loads(body)
+        assert st == 200 and len(d["nodes"]) == 3 and d["state"] == "NORMAL"
+    finally:
+        c.close()
