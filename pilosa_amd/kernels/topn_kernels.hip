@@ -507,7 +507,11 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
 // shard, -1 = none), built once with the index.
 constexpr int HOT_THREADS = 1024;
 constexpr int HOT_TAB_WORDS = 32768;
-constexpr int HOT_SMALL_N = 255;  // byte counters: at most 255 values per lane-owned container
+// Lane-owned (small) containers: at most SMALLN values.  255 fits the byte
+// counters outright; 1023 (PILOSA_TOPN_SMALL_N=1023) flushes them into u32
+// totals every 240 values, so mid-size rows skip the wave-cooperative path's
+// per-row transpose-reduce.
+constexpr int HOT_SMALL_N = 255;
 
 // SWAR: add the 16 bits of a query mask to 16 byte counters (4 per word):
 // a nibble times 0x00204081 puts its bits at bytes 0..3 without carries.
@@ -523,7 +527,7 @@ __device__ __forceinline__ void swar_add(uint32_t (&c4)[NQ / 4], uint32_t msk) {
 // [h*32768, h*32768 + 32768) -- the same 128 KB of LDS -- so a launch counts
 // twice the queries for the same streamed bytes (the two halves' workgroups
 // are consecutive, on one XCD: the second read of a container hits L2).
-template <int NQ>
+template <int NQ, int SMALLN = HOT_SMALL_N>
 __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) {
   extern __shared__ uint32_t tab[];
   __shared__ int grab[2];
@@ -835,6 +839,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       uint32_t c4[NQ / 4];
 #pragma unroll
       for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
+      uint32_t big[SMALLN > 255 ? NQ : 1];
+#pragma unroll
+      for (int q = 0; q < (SMALLN > 255 ? NQ : 1); q++) big[q] = 0u;
+      int since = 0;
       for (int i = 0; __ballot(i < nl); i += 16) {
         // two 16-byte loads per lane (16 values); all 16 table reads issue
         // before any is consumed (values past the row count nothing)
@@ -850,10 +858,18 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         for (int t = 0; t < 16; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
 #pragma unroll
         for (int t = 0; t < 16; t++) swar_add<NQ>(c4, i + t < nl ? mk[t] : 0u);
+        if (SMALLN > 255 && ++since == 15) {   // wave-uniform: <= 240 values per byte counter
+          since = 0;
+#pragma unroll
+          for (int q = 0; q < (SMALLN > 255 ? NQ : 1); q++) big[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+#pragma unroll
+          for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
+        }
       }
 #pragma unroll
       for (int q = 0; q < NQ; q++) {
-        const uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+        uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+        if (SMALLN > 255) c += big[SMALLN > 255 ? q : 0];
         if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
       }
       g = gn;
@@ -867,6 +883,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
 
 // hot_meta[s][j][k] = meta index (relative to the shard) of the key-j
 // container of the row at cache rank k < R, -1 when absent.  Thread per (s, k).
+template <int SMALLN>
 __global__ __launch_bounds__(256) void topn_hot_meta_kernel(ViewDev v, int S, int K, int R,
                                                             const int32_t* __restrict__ cache_dense,
                                                             int32_t* __restrict__ hot_meta,
@@ -883,7 +900,7 @@ __global__ __launch_bounds__(256) void topn_hot_meta_kernel(ViewDev v, int S, in
       const int64_t m = v.meta[sb + c];
       hot_meta[(int64_t(s) * 16 + meta_j(m)) * R + k] = int32_t(c);
       // ranks before the split take the cooperative path (see topn_hot_kernel)
-      if (meta_type(m) != CT_ARRAY || meta_n(m) > HOT_SMALL_N) atomicMax(hot_split + int64_t(s) * 16 + meta_j(m), k + 1);
+      if (meta_type(m) != CT_ARRAY || meta_n(m) > SMALLN) atomicMax(hot_split + int64_t(s) * 16 + meta_j(m), k + 1);
     }
   }
 }
@@ -965,14 +982,28 @@ void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_
                      offs, has_run);
 }
 
+// lane-owned container bound of the hot-rank kernels (255 or 1023), fixed per
+// process: the split the meta kernel records must match the counting kernel's
+static int hot_small_n() {
+  static const int n = [] {
+    const char* e = getenv("PILOSA_TOPN_SMALL_N");
+    return e && atoi(e) > 255 ? 1023 : 255;
+  }();
+  return n;
+}
+
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st) {
   const int64_t total = int64_t(S) * R;
   if (total <= 0) return;
   const int64_t want = (total + 255) / 256;
   const int blocks = int(want < 65536 ? want : 65536);
-  hipLaunchKernelGGL(topn_hot_meta_kernel, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense, hot_meta,
-                     hot_split);
+  if (hot_small_n() > 255)
+    hipLaunchKernelGGL(topn_hot_meta_kernel<1023>, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense,
+                       hot_meta, hot_split);
+  else
+    hipLaunchKernelGGL(topn_hot_meta_kernel<255>, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense,
+                       hot_meta, hot_split);
 }
 
 void launch_topn_index(const ViewDev& v, int S, int K, int k0, const int32_t* cache_dense, uint32_t* colcnt,
@@ -1011,6 +1042,10 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<32>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, tab);
       hipLaunchKernelGGL(topn_hot_kernel<32>, dim3(unsigned(a.S) * 32u), dim3(HOT_THREADS), tab, st, a);
+    } else if (hot_small_n() > 255) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<16, 1023>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
+      hipLaunchKernelGGL((topn_hot_kernel<16, 1023>), dim3(unsigned(a.S) * 16u), dim3(HOT_THREADS), tab, st, a);
     } else {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<16>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, tab);

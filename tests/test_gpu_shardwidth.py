@@ -43,3 +43,17 @@ def test_gpu_executor_suite_at_wide_width():
     # skips allowed: the slot-index refresh test (src TopN uses the pair path
     # here) and the two engine-level ops/topn.py tests (per arena shard)
     assert " passed" in last and ("skipped" not in last or "3 skipped" in last), r.stdout[-1000:]
+
+
+@pytest.mark.timeout(600)
+def test_gpu_topn_suites_with_wide_lane_owned_rows():
+    """The hot-rank TopN kernel with lane-owned containers up to 1023 values
+    (PILOSA_TOPN_SMALL_N=1023: byte counters flushed every 240 values) answers
+    the slot-index and executor TopN suites exactly."""
+    env = dict(os.environ, PILOSA_TOPN_SMALL_N="1023")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        "--timeout", "300", "--timeout-method", "thread", "-k", "slot_index or topn or TopN",
+                        "tests/test_gpu_executor.py", "tests/test_gpu_topn_exec.py"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=580)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout.splitlines()[-1], r.stdout[-1000:]
