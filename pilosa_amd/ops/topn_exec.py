@@ -28,6 +28,7 @@ candidate x shard count matrix, and a per-query LDS bitonic top-n.
 """
 from __future__ import annotations
 
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -40,6 +41,30 @@ from .device import DeviceView, kernels
 NOSRC_CHUNK = 64
 # largest [candidate x shard] count matrix the fused cache-only path memoises
 FUSED_MAX_CELLS = 1 << 25
+
+
+_TLS = threading.local()
+
+
+def _thread_stream(device):
+    """This thread's TopN side stream on ``device`` (created on first use)."""
+    import torch
+    d = _TLS.__dict__.setdefault("streams", {})
+    st = d.get(device)
+    if st is None:
+        st = d[device] = torch.cuda.Stream(device=device)
+    return st
+
+
+def _thread_pinned_i32(n: int):
+    """This thread's reusable pinned int32 host buffer of at least ``n``.  A
+    batch's parameters are copied from it on the thread's own stream and the
+    batch ends in a blocking D2H, so the next batch may overwrite it."""
+    import torch
+    buf = getattr(_TLS, "pin", None)
+    if buf is None or buf.numel() < n:
+        buf = _TLS.pin = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
+    return buf[:n]
 
 
 def rows_dev(view: DeviceView):
@@ -336,6 +361,9 @@ class DeviceRankCaches:
             else:
                 u32 = u.to(torch.int32).contiguous()
                 got = (u32, inv.to(torch.int32).contiguous(), self._count_matrix(u32))
+                if self.view.device.type == "cuda":
+                    # built on this thread's stream; other threads' streams read it
+                    torch.cuda.current_stream(self.view.device).synchronize()
             memo[nmax] = got
         return got
 
@@ -356,27 +384,14 @@ class DeviceRankCaches:
             return [[] for _ in range(Q)]
         ctx = contextlib.nullcontext()
         if self.view.device.type == "cuda":
-            # its own stream: a serving mix's TopN batch does not queue behind the
-            # Count batches of other requests on the default stream
-            st = self.__dict__.get("_stream")
-            if st is None:
-                st = self._stream = torch.cuda.Stream(device=self.view.device)
+            # a side stream per serving thread: a serving mix's TopN batch does not
+            # queue behind the Count batches of other requests on the default
+            # stream, nor behind another thread's TopN batch
+            st = _thread_stream(self.view.device)
             st.wait_event(self._ready)
             ctx = torch.cuda.stream(st)
-        mu = self.__dict__.get("_mu")
-        if mu is None:
-            import threading
-            mu = self.__dict__.setdefault("_mu", threading.Lock())
-        with mu, ctx:   # one batch at a time owns the stream's pinned parameter buffer
+        with ctx:
             return self._topn_nosrc_fused_on(ns, nn, nmax, thresholds)
-
-    def _pinned_i32(self, n: int):
-        """Reusable pinned int32 host buffer of at least ``n`` (batch parameters)."""
-        import torch
-        buf = self.__dict__.get("_pin")
-        if buf is None or buf.numel() < n:
-            buf = self._pin = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
-        return buf[:n]
 
     def _topn_nosrc_fused_on(self, ns, nn, nmax, thresholds):
         import torch
@@ -390,7 +405,7 @@ class DeviceRankCaches:
         ths = [max(1, int(t)) for t in thresholds]
         uniq_t = sorted(set(ths))
         KK = min(U, max(nn)) if all(nn) else U
-        pin = self._pinned_i32(4 * Q + len(uniq_t)) if dev.type == "cuda" else None
+        pin = _thread_pinned_i32(4 * Q + len(uniq_t)) if dev.type == "cuda" else None
         prm = pin.numpy() if pin is not None else np.empty(4 * Q + len(uniq_t), np.int32)
         prm[:Q] = [n if n else self.K for n in nn]
         prm[Q:2 * Q] = ths

@@ -670,14 +670,3 @@ def test_topn_tanimoto_and_attr_filters_on_device(envs, q):
     got = _dev(cpu, gpu, lambda: cpu.q1("i", q))
     assert [(p.id, p.count) for p in got] == [(p.id, p.count) for p in want]
 
-
-def test_generated_queries_match_host(envs):
-    """Random nested Count queries (testing/querygen.py, the reference's
-    internal/test query generator) answered on the device equal the host."""
-    from pilosa_amd.testing.querygen import QueryGenerator
-    cpu, gpu = envs
-    qs = QueryGenerator(["f", "g"], rows=13, seed=11, depth=3).queries(60)
-    text = " ".join(qs)
-    want = cpu.q("i", text)
-    got = _dev(cpu, gpu, lambda: cpu.q("i", text))
-    assert got == want

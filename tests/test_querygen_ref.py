@@ -20,8 +20,8 @@ def test_generator_builds_parsed_ast(text, built):
 
 
 def test_random_queries_parse_and_round_trip():
-    g = QueryGenerator(["f", "g"], rows=50, seed=7, depth=3)
-    for q in g.queries(200):
+    g = QueryGenerator(seed=7, set_fields=["f", "g"], int_fields=["v"], time_fields=["t"], max_row=50)
+    for q in g.queries(200, depth=3):
         parsed = parse_string(q)
-        assert len(parsed.calls) == 1 and parsed.calls[0].name == "Count"
+        assert len(parsed.calls) == 1
         assert parse_string(str(parsed)).calls == parsed.calls
