@@ -1038,7 +1038,11 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
     // hot-rank count matrix (before mode 1/2 of the same batch)
     if (a.R <= 0) return;
     const int tab = HOT_TAB_WORDS * 4;
-    if (a.Q > 16) {
+    if (a.Q > 16 && hot_small_n() > 255) {   // the split must match the meta kernel's bound
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<32, 1023>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
+      hipLaunchKernelGGL((topn_hot_kernel<32, 1023>), dim3(unsigned(a.S) * 32u), dim3(HOT_THREADS), tab, st, a);
+    } else if (a.Q > 16) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<32>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, tab);
       hipLaunchKernelGGL(topn_hot_kernel<32>, dim3(unsigned(a.S) * 32u), dim3(HOT_THREADS), tab, st, a);

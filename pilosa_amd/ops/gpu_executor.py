@@ -970,9 +970,9 @@ class GpuExecutor:
 
     # ------------------------------------------------------------ TopN
     def _topn_setup(self, index: str, c: Call, shards: List[int]):
-        """(params, frags, rank caches, view, src plan) of one TopN call, or
-        NotImplementedError for the shapes the host answers (Tanimoto and
-        attribute filters: per-row attribute reads)."""
+        """(params, rank caches, view, src plan, (tanimoto, attribute filter))
+        of one TopN call, or NotImplementedError for the shapes the host
+        answers (more than one child)."""
         ex = self._ex()
         fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
         if len(c.children) > 1:
@@ -992,15 +992,13 @@ class GpuExecutor:
             def keep(rid, store=store, want=want, name=attr_name):
                 a = store.attrs(rid)
                 return bool(a) and a.get(name) is not None and _hashable(a.get(name)) in want
-        self._topn_filters = (tanimoto if src is not None else 0, keep)
-        return (fname, n, ids, threshold), rc, rv, src
+        return (fname, n, ids, threshold), rc, rv, src, (tanimoto if src is not None else 0, keep)
 
     def topn(self, index: str, c: Call, shards: List[int]) -> List[Pair]:
         """One TopN call's map step over the local shards (executor.go:905-930):
         phase 1 = per-shard ``fragment.top`` results summed by row (untrimmed),
         with ``ids=`` the per-shard exact re-count of those rows."""
-        (fname, n, ids, threshold), rc, rv, src = self._topn_setup(index, c, shards)
-        tan, keep = self._topn_filters
+        (fname, n, ids, threshold), rc, rv, src, (tan, keep) = self._topn_setup(index, c, shards)
         if rc is None or src is EMPTY or rc.K == 0:
             return []
         if tan or keep is not None:

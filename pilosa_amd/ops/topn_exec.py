@@ -28,6 +28,7 @@ candidate x shard count matrix, and a per-query LDS bitonic top-n.
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import List, Optional, Sequence
 
@@ -44,6 +45,8 @@ FUSED_MAX_CELLS = 1 << 25
 
 
 _TLS = threading.local()
+# cache-only TopN batches on a per-thread side stream (0: the current stream)
+SIDE_STREAM = os.environ.get("PILOSA_TOPN_SIDE_STREAM", "1") != "0"
 
 
 def _thread_stream(device):
@@ -383,7 +386,7 @@ class DeviceRankCaches:
         if not nmax:
             return [[] for _ in range(Q)]
         ctx = contextlib.nullcontext()
-        if self.view.device.type == "cuda":
+        if self.view.device.type == "cuda" and SIDE_STREAM:
             # a side stream per serving thread: a serving mix's TopN batch does not
             # queue behind the Count batches of other requests on the default
             # stream, nor behind another thread's TopN batch
