@@ -288,13 +288,14 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     log("topn: cache-only requests (distinct calls)")
     # every call of every request distinct: n and threshold vary, so no
     # phase-2 re-count or candidate set is shared between calls by repetition
-    cache_calls = _distinct_topn_calls(B * (nb + 1))
-    cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
+    nbc = max(nb, args.topn_cache_batches)   # cache-only requests are ~1 ms: a longer window
+    cache_calls = _distinct_topn_calls(B * (nbc + 1))
+    cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nbc + 1)]
     out["cache"] = {"calls": "TopN(f, n in {10,50,100,500}, threshold in {1,1000,5000,20000}), all distinct"}
     res_cache = timed(cache_q, out["cache"])
     log("topn: cache-only requests (the same call repeated, round-3 figure)")
     out["cache_repeated"] = {}
-    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nb + 1), out["cache_repeated"])
+    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nbc + 1), out["cache_repeated"])
     hot = zipf_rows(rng, B * (nb + 1), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
@@ -362,7 +363,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         # and the fused batch answers equal the two-phase map/reduce on the device
         agree = [[(p.id, p.count) for p in r] for r in res_src[-1][:2] + res_cache[-1][:4]] == \
             [[(p.id, p.count) for p in ex._topn("i", parse_string(c).calls[0], shards, _exec_opts())]
-             for c in src_calls[nb * B:nb * B + 2] + cache_calls[nb * B:nb * B + 4]] if world == 1 else None
+             for c in src_calls[nb * B:nb * B + 2] + cache_calls[nbc * B:nbc * B + 4]] if world == 1 else None
         out["verify"] = {"shards_checked": len(sel), "queries_per_shard": len(calls), "mismatches": bad,
                          "fused_equals_two_phase": agree, "verified": bad == 0 and agree is not False}
     return out
@@ -1561,6 +1562,8 @@ def main():
     ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")
     ap.add_argument("--topn-batches", type=int, default=40,
                     help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
+    ap.add_argument("--topn-cache-batches", type=int, default=240,
+                    help="timed cache-only TopN requests (at least --topn-batches)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
     ap.add_argument("--topn-pairs-batches", type=int, default=1,

@@ -44,30 +44,45 @@ NOSRC_CHUNK = 64
 FUSED_MAX_CELLS = 1 << 25
 
 
-_TLS = threading.local()
-# cache-only TopN batches on a per-thread side stream (0: the current stream)
+# cache-only TopN batches on a side stream (0: the current stream)
 SIDE_STREAM = os.environ.get("PILOSA_TOPN_SIDE_STREAM", "1") != "0"
 
 
-def _thread_stream(device):
-    """This thread's TopN side stream on ``device`` (created on first use)."""
-    import torch
-    d = _TLS.__dict__.setdefault("streams", {})
-    st = d.get(device)
-    if st is None:
-        st = d[device] = torch.cuda.Stream(device=device)
-    return st
+class _Lane:
+    """A side stream and a pinned int32 parameter buffer, owned by one batch
+    at a time.  The batch copies its parameters from the buffer on the
+    stream and ends in a blocking D2H, so the next owner may overwrite it."""
+
+    def __init__(self, device):
+        import torch
+        self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+        self.pin = None
+
+    def pinned_i32(self, n: int):
+        import torch
+        if self.pin is None or self.pin.numel() < n:
+            self.pin = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
+        return self.pin[:n]
 
 
-def _thread_pinned_i32(n: int):
-    """This thread's reusable pinned int32 host buffer of at least ``n``.  A
-    batch's parameters are copied from it on the thread's own stream and the
-    batch ends in a blocking D2H, so the next batch may overwrite it."""
-    import torch
-    buf = getattr(_TLS, "pin", None)
-    if buf is None or buf.numel() < n:
-        buf = _TLS.pin = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
-    return buf[:n]
+_LANES: dict = {}
+_LANES_MU = threading.Lock()
+
+
+def _lane_take(device) -> "_Lane":
+    """A free lane of ``device`` (a new one when all are taken): concurrent
+    batches run on their own streams, and a serving thread pays no stream or
+    pinned-buffer creation after the first batches."""
+    with _LANES_MU:
+        free = _LANES.setdefault(device, [])
+        if free:
+            return free.pop()
+    return _Lane(device)
+
+
+def _lane_give(device, lane: "_Lane") -> None:
+    with _LANES_MU:
+        _LANES.setdefault(device, []).append(lane)
 
 
 def rows_dev(view: DeviceView):
@@ -365,7 +380,7 @@ class DeviceRankCaches:
                 u32 = u.to(torch.int32).contiguous()
                 got = (u32, inv.to(torch.int32).contiguous(), self._count_matrix(u32))
                 if self.view.device.type == "cuda":
-                    # built on this thread's stream; other threads' streams read it
+                    # built on this batch's stream; other batches' streams read it
                     torch.cuda.current_stream(self.view.device).synchronize()
             memo[nmax] = got
         return got
@@ -377,26 +392,29 @@ class DeviceRankCaches:
         memoised count matrix, and a per-query LDS bitonic top-n.  One H2D of
         the batch parameters, one D2H of the Q x n keys.  None when the
         candidate set is too large for it (the torch path then runs)."""
-        import contextlib
-
         import torch
         Q = len(ns)
         nn = [int(n) for n in ns]
         nmax = self.K if any(n == 0 for n in nn) else min(self.K, max(nn))
         if not nmax:
             return [[] for _ in range(Q)]
-        ctx = contextlib.nullcontext()
-        if self.view.device.type == "cuda" and SIDE_STREAM:
-            # a side stream per serving thread: a serving mix's TopN batch does not
-            # queue behind the Count batches of other requests on the default
-            # stream, nor behind another thread's TopN batch
-            st = _thread_stream(self.view.device)
-            st.wait_event(self._ready)
-            ctx = torch.cuda.stream(st)
-        with ctx:
-            return self._topn_nosrc_fused_on(ns, nn, nmax, thresholds)
+        dev = self.view.device
+        if dev.type != "cuda":
+            return self._topn_nosrc_fused_on(ns, nn, nmax, thresholds, None)
+        lane = _lane_take(dev)
+        if not SIDE_STREAM:
+            res = self._topn_nosrc_fused_on(ns, nn, nmax, thresholds, lane)
+        else:
+            # a serving mix's TopN batch does not queue behind the Count batches
+            # of other requests on the default stream, nor behind another
+            # request's TopN batch
+            lane.stream.wait_event(self._ready)
+            with torch.cuda.stream(lane.stream):
+                res = self._topn_nosrc_fused_on(ns, nn, nmax, thresholds, lane)
+        _lane_give(dev, lane)   # not after an error: its copies may still be in flight
+        return res
 
-    def _topn_nosrc_fused_on(self, ns, nn, nmax, thresholds):
+    def _topn_nosrc_fused_on(self, ns, nn, nmax, thresholds, lane):
         import torch
         Q = len(ns)
         memo = self._fused_memo(nmax)
@@ -408,7 +426,7 @@ class DeviceRankCaches:
         ths = [max(1, int(t)) for t in thresholds]
         uniq_t = sorted(set(ths))
         KK = min(U, max(nn)) if all(nn) else U
-        pin = _thread_pinned_i32(4 * Q + len(uniq_t)) if dev.type == "cuda" else None
+        pin = lane.pinned_i32(4 * Q + len(uniq_t)) if lane is not None else None
         prm = pin.numpy() if pin is not None else np.empty(4 * Q + len(uniq_t), np.int32)
         prm[:Q] = [n if n else self.K for n in nn]
         prm[Q:2 * Q] = ths
