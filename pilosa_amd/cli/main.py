@@ -388,12 +388,9 @@ def cmd_export(args, stdout, stderr) -> int:
 
 # ------------------------------------------------------------------ check / inspect
 def _header_error(e: Exception) -> str:
-    """The reference's wording for a file that is neither Pilosa nor
-    official roaring (roaring/roaring.go UnmarshalBinary)."""
-    msg = str(e)
-    if "magic number" in msg:
-        return "did not find expected serialCookie in header"
-    return msg
+    """The decoder's message, already in the reference's wording and prefixes
+    (roaring/roaring.go UnmarshalBinary: "reading roaring header: ...")."""
+    return str(e)
 
 
 def cmd_check(args, stdout, stderr) -> int:
@@ -420,7 +417,7 @@ def cmd_check(args, stdout, stderr) -> int:
         try:
             bm = _roaring.Bitmap.from_bytes(data)
         except Exception as e:  # noqa: BLE001
-            print(f"checking bitmap: unmarshalling: reading roaring header: {_header_error(e)}", file=stderr)
+            print(f"checking bitmap: unmarshalling: {_header_error(e)}", file=stderr)
             return 1
         errs = bm.check()
         for line in (errs or "").strip().splitlines():
@@ -445,7 +442,7 @@ def cmd_inspect(args, stdout, stderr) -> int:
     try:
         bm = _roaring.Bitmap.from_bytes(data)
     except Exception as e:  # noqa: BLE001
-        print(f"unmarshalling: reading roaring header: {_header_error(e)}", file=stderr)
+        print(f"unmarshalling: {_header_error(e)}", file=stderr)
         return 1
     info = bm.container_info()
     types = Counter(t for _, t, _ in info)

@@ -1155,8 +1155,12 @@ void Bitmap::parse_pilosa(const uint8_t* data, size_t n, size_t* ops_offset) {
     throw std::runtime_error("wrong roaring version, file is v" + std::to_string(data[2]) + ", server requires v0");
   flags = data[3];
   uint32_t keyn = rd32(data + 4);
+  // the reference's wording (roaring.go:1581-1583), its count included (keyN / 12)
+  if (size_t(HEADER_BASE) + size_t(keyn) * 12 > n)
+    throw std::runtime_error("malformed bitmap, key-cardinality not provided for " + std::to_string(keyn / 12) +
+                             " containers");
   if (size_t(HEADER_BASE) + size_t(keyn) * 16 > n)
-    throw std::runtime_error("malformed bitmap, key-cardinality not provided for " + std::to_string(keyn) + " containers");
+    throw std::runtime_error("malformed bitmap, offsets not provided for " + std::to_string(keyn) + " containers");
   cs.clear();
   const uint8_t* hdr = data + HEADER_BASE;
   const uint8_t* offs = hdr + size_t(keyn) * 12;
@@ -1204,7 +1208,13 @@ void Bitmap::parse_pilosa(const uint8_t* data, size_t n, size_t* ops_offset) {
 }
 
 void Bitmap::parse_official(const uint8_t* data, size_t n) {
-  if (n < 8) throw std::runtime_error("buffer too small, expecting at least 8 bytes");
+  // errors in the header read "reading roaring header: ...", errors past it
+  // "reading offsets from official roaring format: ..." (roaring.go:5141-5245)
+  auto header_err = [](const std::string& m) { return std::runtime_error("reading roaring header: " + m); };
+  auto offset_err = [](const std::string& m) {
+    return std::runtime_error("reading offsets from official roaring format: " + m);
+  };
+  if (n < 8) throw header_err("buffer too small, expecting at least 8 bytes, was " + std::to_string(n));
   uint32_t cookie = rd32(data);
   size_t pos = 4;
   uint32_t size;
@@ -1217,20 +1227,24 @@ void Bitmap::parse_official(const uint8_t* data, size_t n) {
     have_runs = true;
     size = (cookie >> 16) + 1;
     size_t rb = (size + 7) / 8;
-    if (pos + rb > n) throw std::runtime_error("malformed bitmap, is-run bitmap overruns buffer");
+    if (pos + rb > n) throw header_err("malformed bitmap, is-run bitmap overruns buffer at " + std::to_string(pos + rb));
     isrun = data + pos;
     pos += rb;
   } else {
-    throw std::runtime_error("did not find expected serialCookie in header");
+    throw header_err("did not find expected serialCookie in header");
   }
-  if (size > 65536) throw std::runtime_error("it is logically impossible to have more than (1<<16) containers");
-  if (pos + size_t(size) * 4 > n) throw std::runtime_error("malformed bitmap, key-cardinality slice overruns buffer");
+  if (size > 65536) throw header_err("it is logically impossible to have more than (1<<16) containers");
+  if (pos + size_t(size) * 4 >= n)
+    throw header_err("malformed bitmap, key-cardinality slice overruns buffer at " + std::to_string(pos + size_t(size) * 4));
   const uint8_t* hdr = data + pos;
   pos += size_t(size) * 4;
   const uint8_t* offs = nullptr;
   if (!have_runs || size >= 4) {
+    if (pos + size_t(size) * 4 > n) throw offset_err("offset incomplete: len=" + std::to_string((n - pos) % 4));
     offs = data + pos;
     pos += size_t(size) * 4;
+  } else if (pos + 2 > n) {
+    throw offset_err("offset incomplete: len=" + std::to_string(n));
   }
   cs.clear();
   size_t cur = pos;
@@ -1238,14 +1252,18 @@ void Bitmap::parse_official(const uint8_t* data, size_t n) {
     uint16_t key = rd16(hdr + i * 4);
     int32_t card = int32_t(rd16(hdr + i * 4 + 2)) + 1;
     bool run = have_runs && (isrun[i / 8] >> (i % 8)) & 1;
-    if (offs) cur = rd32(offs + i * 4);
+    if (offs) {
+      cur = rd32(offs + i * 4);
+      if (cur >= n)
+        throw offset_err("offset out of bounds: off=" + std::to_string(cur) + ", len=" + std::to_string(n));
+    }
     Container c;
     c.n = card;
     if (run) {
-      if (cur + 2 > n) throw std::runtime_error("run container overruns buffer");
+      if (cur + 2 > n) throw offset_err("run container overruns buffer");
       uint16_t nr = rd16(data + cur);
       cur += 2;
-      if (cur + size_t(nr) * 4 > n) throw std::runtime_error("run container overruns buffer");
+      if (cur + size_t(nr) * 4 > n) throw offset_err("run container overruns buffer");
       c.type = CT_RUN;
       c.r.resize(nr);
       for (uint16_t k = 0; k < nr; k++) {
@@ -1255,13 +1273,13 @@ void Bitmap::parse_official(const uint8_t* data, size_t n) {
       }
       cur += size_t(nr) * 4;
     } else if (card <= ARRAY_MAX) {
-      if (cur + size_t(card) * 2 > n) throw std::runtime_error("array container overruns buffer");
+      if (cur + size_t(card) * 2 > n) throw offset_err("array container overruns buffer");
       c.type = CT_ARRAY;
       c.a.resize(card);
       memcpy(c.a.data(), data + cur, size_t(card) * 2);
       cur += size_t(card) * 2;
     } else {
-      if (cur + BITMAP_N * 8 > n) throw std::runtime_error("bitmap container overruns buffer");
+      if (cur + BITMAP_N * 8 > n) throw offset_err("bitmap container overruns buffer");
       c.type = CT_BITMAP;
       c.b.resize(BITMAP_N);
       memcpy(c.b.data(), data + cur, BITMAP_N * 8);
@@ -1385,16 +1403,16 @@ void Bitmap::from_bytes(const uint8_t* data, size_t n) {
     cs.clear();
     return;
   }
-  if (n < HEADER_BASE) throw std::runtime_error("invalid data: not long enough to be a roaring header");
-  uint32_t magic = rd16(data);
-  if (magic == MAGIC) {
-    size_t off = 0;
-    parse_pilosa(data, n, &off);
-    replay_ops(data + off, n - off);
-  } else if (magic == OFFICIAL_NORUN || magic == OFFICIAL_RUN) {
-    parse_official(data, n);
+  if (n >= 2 && rd16(data) == MAGIC) {
+    try {
+      size_t off = 0;
+      parse_pilosa(data, n, &off);
+      replay_ops(data + off, n - off);
+    } catch (const std::runtime_error& e) {
+      throw std::runtime_error(std::string("unmarshaling as pilosa roaring: ") + e.what());
+    }
   } else {
-    throw std::runtime_error("unknown roaring magic number " + std::to_string(magic));
+    parse_official(data, n);   // anything else is read as the official format
   }
 }
 

@@ -487,13 +487,10 @@ def test_unmarshal_official_roaring_file():  # TestUnmarshalRoaringWithNoErrors 
 
 
 def test_unmarshal_roaring_with_errors():  # TestUnmarshalRoaringWithErrors :3404
-    # the reference only pins the message when decoding fails: an empty
-    # container set may decode as an empty bitmap instead
-    for hx in ("3A30000000000000", "3B30000000000000"):
-        try:
-            assert Bitmap.from_bytes(bytes.fromhex(hx)).count() == 0
-        except RuntimeError as e:
-            assert "malformed bitmap, key-cardinality slice overruns buffer" in str(e)
+    for hx, at in (("3A30000000000000", 8), ("3B30000000000000", 9)):
+        with pytest.raises(RuntimeError) as ei:
+            Bitmap.from_bytes(bytes.fromhex(hx))
+        assert str(ei.value) == f"reading roaring header: malformed bitmap, key-cardinality slice overruns buffer at {at}"
     assert Bitmap.from_bytes(bytes.fromhex("3C30000000000000")).count() == 0   # Pilosa format, no containers
 
 
