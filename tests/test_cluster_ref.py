@@ -6,7 +6,9 @@ TestCluster_Coordinator, TestCluster_Topology, TestCluster_ResizeStates,
 TestCluster_UpdateCoordinator, TestCluster_confirmNodeDown*).
 
 The server-level cases run real in-process nodes over loopback HTTP (the
-reference's in-memory cluster harness has no equivalent here)."""
+reference's in-memory cluster harness, utils_internal_test.go's
+NewTestCluster / ClusterCluster with a mod hasher, is the in-process
+``Cluster.from_nodes(..., hasher=ModHasher())`` here)."""
 import http.server
 import os
 import random
