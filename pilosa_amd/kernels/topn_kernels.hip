@@ -541,31 +541,49 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   const int Q = p.Q, R = p.R;
   const int64_t sb = p.v.shard_base[s];
   uint32_t* out = p.hot_cnt + int64_t(s) * Q * R;
-  // 1. query-mask table of key j
-  bool any = false;
-  for (int q = 0; q < Q; q++) any |= p.src_counts[(int64_t(q) * p.S + s) * 16 + j] > 0;
-  if (!any) return;  // block-uniform: no src has key j in this shard
+  // 1. query-mask table of key j.  One wave per query (wave w takes queries
+  //    w, w + 16): each lane issues 8 independent value loads before its 8
+  //    LDS ORs, so the table costs a few load round trips instead of one per
+  //    (query, 1024 values) -- the CU holds only this workgroup and waits out
+  //    every round trip of the build (1.55 ms of a 16-query launch with the
+  //    thread-per-value loop over queries, profiles/r03_hotsplit/).
+  const int wave = tid >> 6;
+  {
+    int has = 0;
+    if (tid < Q) has = p.src_counts[(int64_t(tid) * p.S + s) * 16 + j] > 0;
+    if (!__syncthreads_or(has)) return;  // block-uniform: no src has key j in this shard
+  }
   uint4* t4 = reinterpret_cast<uint4*>(tab);
   for (int i = tid; i < HOT_TAB_WORDS / 4; i += HOT_THREADS) t4[i] = make_uint4(0, 0, 0, 0);
   if (tid == 0) grab[0] = grab[1] = 0;
   __syncthreads();
-  for (int q = 0; q < Q; q++) {
+  for (int q = wave; q < Q; q += HOT_THREADS / 64) {
     const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
     const int n = p.src_counts[kk];
     if (n <= 0) continue;
-    const uint16_t* vals = p.src_vals + p.src_offs[kk];
+    const auto vals = gp(p.src_vals + p.src_offs[kk]);
     if (n <= ARRAY_MAX) {
-      for (int i = tid; i < n; i += HOT_THREADS) {
-        const int x = vals[i];
-        if (HB) {
-          if (unsigned(x - lo) < unsigned(NLO)) atomicOr(&tab[x - lo], 1u << q);
-        } else {
-          atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+      for (int i0 = 0; i0 < n; i0 += 64 * 8) {
+        int xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int i = i0 + 64 * u + lane;
+          xv[u] = i < n ? int(vals[i]) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int x = xv[u];
+          if (x < 0) continue;
+          if (HB) {
+            if (unsigned(x - lo) < unsigned(NLO)) atomicOr(&tab[x - lo], 1u << q);
+          } else {
+            atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+          }
         }
       }
     } else {
-      const uint64_t* w = reinterpret_cast<const uint64_t*>(vals);
-      for (int i = tid + (lo >> 6); i < (lo + NLO) >> 6; i += HOT_THREADS)
+      const auto w = reinterpret_cast<const TN_GLOBAL uint64_t*>(vals);
+      for (int i = lane + (lo >> 6); i < (lo + NLO) >> 6; i += 64)
         for (uint64_t bb = w[i]; bb; bb &= bb - 1) {
           const int x = i * 64 + __builtin_ctzll(bb);
           if (HB) atomicOr(&tab[x - lo], 1u << q);
@@ -592,7 +610,6 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //    row's first chunk -- in flight while the current one is counted.  Byte
   //    counters per lane, a 17-shuffle transpose-reduce per row, totals in
   //    lanes (l >> 2) & 15.
-  const int wave = tid >> 6;
   for (int gb = wave; gb < ((p.dbg & 16) ? 0 : B); gb += 64 * (HOT_THREADS / 64)) {
     const int kl = gb + (HOT_THREADS / 64) * lane;
     const int cl = kl < B ? hm[kl] : -1;
