@@ -235,8 +235,9 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     out = {"path": "Executor.execute(PQL TopN text), lazy holder, device rank caches from .cache files",
            "n": n, "cache_k": args.topn_cache, "batch": B, "clients": clients}
 
-    def timed(texts, first):
-        # warmup request first (builds rank caches / slot index), then nb timed requests
+    def timed(texts, first, profile=""):
+        # warmup request first (builds rank caches / slot index), then nb timed requests;
+        # ``profile``: folded stacks of every thread over the first 0.3 s of the timed run
         done = [None] * len(texts)
         err = []
         nxt = [0]
@@ -263,6 +264,22 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
             dist.barrier()
         torch.cuda.synchronize(dev)
         nxt[0] = 1
+        prof = None
+        gc_t = [0.0, 0, None]   # pause seconds, collections, start of the current one
+        if profile:
+            import gc
+
+            def gc_cb(phase, info):
+                if phase == "start":
+                    gc_t[2] = time.perf_counter()
+                elif gc_t[2] is not None:
+                    gc_t[0] += time.perf_counter() - gc_t[2]
+                    gc_t[1] += 1
+            gc.callbacks.append(gc_cb)
+            from pilosa_amd.utils import pprof
+            prof_out = {}
+            prof = threading.Thread(target=lambda: prof_out.setdefault("p", pprof.cpu_profile(0.3, 500)), daemon=True)
+            prof.start()
         t0 = time.perf_counter()
         ts = [threading.Thread(target=client, args=(1, len(texts))) for _ in range(clients)]
         for t in ts:
@@ -275,6 +292,13 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        if prof is not None:
+            gc.callbacks.remove(gc_cb)
+            first["gc_pause_s"] = round(gc_t[0], 4)
+            first["gc_collections"] = gc_t[1]
+            prof.join()
+            with open(profile, "w") as fh:
+                fh.write(prof_out.get("p", ""))
         elt = torch.tensor([el], dtype=torch.float64, device=dev)
         if world > 1:
             all_reduce(elt, op=dist.ReduceOp.MAX)
@@ -292,7 +316,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     cache_calls = _distinct_topn_calls(B * (nbc + 1))
     cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nbc + 1)]
     out["cache"] = {"calls": "TopN(f, n in {10,50,100,500}, threshold in {1,1000,5000,20000}), all distinct"}
-    res_cache = timed(cache_q, out["cache"])
+    res_cache = timed(cache_q, out["cache"], os.environ.get("PILOSA_BENCH_TOPN_PROFILE", ""))
     log("topn: cache-only requests (the same call repeated, round-3 figure)")
     out["cache_repeated"] = {}
     timed([" ".join([f"TopN(f, n={n})"] * B)] * (nbc + 1), out["cache_repeated"])
