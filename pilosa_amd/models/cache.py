@@ -49,6 +49,34 @@ class Pair:
         return f"Pair({self.id}, {self.count}{', ' + repr(self.key) if self.key else ''})"
 
 
+def pairs_from_arrays(ids, counts) -> List[Pair]:
+    """``[Pair(id, count), ...]`` from parallel id / count sequences, built in
+    bulk by the native core when it is loaded (pyroaring ``make_pairs``: the
+    same objects, ~0.1 us each instead of ~0.5 us through ``__init__``; a
+    16-call TopN request returns thousands of pairs)."""
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    counts = np.ascontiguousarray(counts, dtype=np.int64)
+    fast = _make_pairs()
+    if fast is not None:
+        got = fast(Pair, ids, counts)
+        if got is not None:
+            return got
+    return [Pair(i, c) for i, c in zip(ids.tolist(), counts.tolist())]
+
+
+_MAKE_PAIRS = []
+
+
+def _make_pairs():
+    if not _MAKE_PAIRS:
+        try:
+            from pilosa_amd import _roaring
+            _MAKE_PAIRS.append(getattr(_roaring, "make_pairs", None))
+        except ImportError:
+            _MAKE_PAIRS.append(None)
+    return _MAKE_PAIRS[0]
+
+
 def sort_pairs(pairs: List[Pair]) -> List[Pair]:
     return sorted(pairs, key=lambda p: (-p.count, p.id))
 

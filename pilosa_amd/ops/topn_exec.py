@@ -34,7 +34,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from pilosa_amd.models.cache import Pair
+from pilosa_amd.models.cache import Pair, pairs_from_arrays
 
 from .device import DeviceView, kernels
 
@@ -447,7 +447,7 @@ class DeviceRankCaches:
             r = h[q, 1:1 + int(h[q, 0])]
             d = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
             ids = rows[d] if len(d) else np.zeros(0, np.uint64)
-            res.append([Pair(int(i), int(c)) for i, c in zip(ids.tolist(), (r >> 32).tolist())])
+            res.append(pairs_from_arrays(ids, r >> 32))
         return res
 
     def _topn_nosrc_dense(self, ns: Sequence[int], thresholds: Sequence[int]) -> List[List[Pair]]:
@@ -510,7 +510,7 @@ class DeviceRankCaches:
                 r = r[:nn[q]]
             d = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
             ids = rows[d] if len(d) else np.zeros(0, np.uint64)
-            out.append([Pair(int(i), int(c)) for i, c in zip(ids.tolist(), (r >> 32).tolist())])
+            out.append(pairs_from_arrays(ids, r >> 32))
         return out
 
     def shard_pairs_nosrc(self, n: int, threshold: int, ids: Optional[Sequence[int]] = None) -> List[Pair]:
@@ -531,4 +531,4 @@ class DeviceRankCaches:
         d_h = pd[keep].cpu().numpy()
         c_h = pc[keep].cpu().numpy()
         rows = self.view.rows[d_h] if len(d_h) else np.zeros(0, np.uint64)
-        return [Pair(int(r), int(c)) for r, c in zip(rows.tolist(), c_h.tolist())]
+        return pairs_from_arrays(rows, c_h)

@@ -26,7 +26,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from pilosa_amd.models.cache import Pair
+from pilosa_amd.models.cache import Pair, pairs_from_arrays
 
 from .device import DeviceView, GpuEngine, kernels
 
@@ -509,7 +509,7 @@ class DeviceTopNIndex:
             c = out.cpu().numpy()
         keep = c > 0
         ids_out = self.space[a[keep]] if len(a) else np.zeros(0, np.uint64)
-        return [Pair(int(i), int(v)) for i, v in zip(ids_out.tolist(), c[keep].tolist())]
+        return pairs_from_arrays(ids_out, c[keep])
 
     def topn_nosrc(self, row_counts, ns: Sequence[int], thresholds: Sequence[int], comm=None):
         with self.rw.read():
@@ -627,5 +627,5 @@ def finish_batch(space: np.ndarray, Q: int, pq: np.ndarray, pa: np.ndarray, cnt:
         n = int(ns[q])
         if n:
             hi = min(hi, lo + n)
-        out.append([Pair(int(i), int(c)) for i, c in zip(ids[lo:hi].tolist(), cnt[lo:hi].tolist())])
+        out.append(pairs_from_arrays(ids[lo:hi], cnt[lo:hi]))
     return out
