@@ -259,6 +259,10 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         done[0] = ex.execute("i", texts[0], shards=shards).results
         torch.cuda.synchronize(dev)
         first["first_request_s"] = round(time.perf_counter() - t0, 2)
+        # what the server's Refreezer does after warm-up: the rank caches and
+        # slot index the first request built leave the collector's walk
+        from pilosa_amd.utils import gctune
+        gctune.freeze_long_lived()
         log(f"topn: first request {first['first_request_s']} s")
         if world > 1:
             dist.barrier()
@@ -1166,6 +1170,10 @@ def run_disk(args, world, rank, dev, queries, ra, rb):
         n0 = gpu.launches
         log("count: warmup")
         run(0, args.warmup)
+        # the server's GC policy (utils/gctune.py): start-up objects frozen
+        from pilosa_amd.utils import gctune
+        gctune.configure()
+        gctune.freeze_long_lived()
         assert gpu.launches > n0, "requests did not reach the device"
         if world > 1:
             dist.barrier()

@@ -196,8 +196,15 @@ class Server:
             self._start_translate_replica()
         elif not self.cluster_disabled:
             self._start_translate_follower()
+        from pilosa_amd.utils import gctune
         from pilosa_amd.utils.gcnotify import GCNotifier
         self.gc_notifier = GCNotifier(self.stats).start()
+        # long-lived objects out of the collector's walk (utils/gctune.py)
+        self._refreezer = None
+        if gctune.enabled():
+            gctune.configure()
+            gctune.freeze_long_lived()
+            self._refreezer = gctune.Refreezer()
         from pilosa_amd.utils.diagnostics import DiagnosticsCollector
         self.diagnostics = DiagnosticsCollector(self.diagnostics_host, self.diagnostics_interval, self.logger)
         if self.diagnostics_host and self.diagnostics_interval > 0:
@@ -819,6 +826,9 @@ class Server:
                 gcn = getattr(self, "gc_notifier", None)
                 if gcn is not None:
                     gcn.flush()
+                rf = getattr(self, "_refreezer", None)
+                if rf is not None:
+                    rf.tick()
                 if self.gpu is not None:
                     st = self.gpu.stats()
                     self.stats.gauge("gpu.arena_bytes", st["arenaBytes"])

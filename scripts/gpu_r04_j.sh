@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/r04_j
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 2 --warmup 1 \
+timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 2 --warmup 1 \
     --configs none --serve-seconds 0 --topn-batches 40 > $O/bench.log 2> $O/bench.err || { tail -c 2000 $O/bench.err; exit 1; }
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1)
 cp "$f" $O/kernel_stats.csv

@@ -41,6 +41,8 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")
     _SHM_TMP = _shm_tmp()
+    # servers opened by tests do not freeze the collector (utils/gctune.py)
+    os.environ.setdefault("PILOSA_GC_FREEZE", "0")
 
 
 def pytest_unconfigure(config):
