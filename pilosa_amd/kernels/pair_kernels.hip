@@ -254,7 +254,12 @@ __device__ __forceinline__ int probe8(BM bm, const uint4 v4) {
 // (variant 14): one AND clears bits 0-4 of both halves of a dword, after which
 // a value's word byte address is ONE op per half (bfe of bits 3..15, or a
 // shift by 19) instead of a shift and a mask.  The AND is inline asm so the
-// compiler cannot fold it back into the two per-half masks.
+// compiler cannot fold it back into the two per-half masks.  28 instead of 32
+// VALU ops per 8 probes, but measured 17.18 vs 16.74 ms per 4096-query batch
+// (the asm also stops the probe loop's unroll; profiles/r04_l/): rejected.
+// The same run: 32 / 16 queries per wave (fewer units in flight per XCD, a
+// smaller L2 footprint) 17.5 / 19.9 ms -- less A reuse costs more than the
+// L2 gains.
 __device__ __forceinline__ int probe8_lean(const uint32_t* bm, const uint4 v4) {
   const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
   const char* base = reinterpret_cast<const char*>(bm);
