@@ -33,7 +33,10 @@
 // staging (v7, 18.5 ms: lower occupancy, probes unchanged) and lane-interleaved
 // u16 probes (v8, 24.0 ms: 5x the load instructions although LDS conflicts
 // fell from 0.52 to 0.33 of the LDS cycles) and an XOR-swizzled LDS bitmap
-// (18.8 ms, see lds_swz); every load of a container issued before any of it
+// (18.8 ms, see lds_swz); one-op LDS word addressing per probe half through
+// an inline-asm mask (28 instead of 32 VALU per 8 probes, but 17.2 ms: the asm
+// stopped the probe loop's unroll; 32 / 16 queries per wave 17.5 / 19.9 ms,
+// profiles/r04_l/); every load of a container issued before any of it
 // is consumed (v9, 20.9 ms: one round trip per array instead of one per
 // 512 values, but slower -- the chunked walk is not latency-bound,
 // profiles/r03_v9/).  Occupancy: the kernel holds 20 waves/CU (8 KiB LDS and
@@ -250,34 +253,6 @@ __device__ __forceinline__ int probe8(BM bm, const uint4 v4) {
   return c;
 }
 
-// probe8 against the plain (unswizzled) LDS bitmap with cheaper addressing
-// (variant 14): one AND clears bits 0-4 of both halves of a dword, after which
-// a value's word byte address is ONE op per half (bfe of bits 3..15, or a
-// shift by 19) instead of a shift and a mask.  The AND is inline asm so the
-// compiler cannot fold it back into the two per-half masks.  28 instead of 32
-// VALU ops per 8 probes, but measured 17.18 vs 16.74 ms per 4096-query batch
-// (the asm also stops the probe loop's unroll; profiles/r04_l/): rejected.
-// The same run: 32 / 16 queries per wave (fewer units in flight per XCD, a
-// smaller L2 footprint) 17.5 / 19.9 ms -- less A reuse costs more than the
-// L2 gains.
-__device__ __forceinline__ int probe8_lean(const uint32_t* bm, const uint4 v4) {
-  const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
-  const char* base = reinterpret_cast<const char*>(bm);
-  uint32_t x[8];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t wm;
-    asm("v_and_b32 %0, 0xffe0ffe0, %1" : "=v"(wm) : "v"(w[k]));
-    x[2 * k] = *reinterpret_cast<const uint32_t*>(base + __builtin_amdgcn_ubfe(wm, 3u, 13u));
-    x[2 * k + 1] = *reinterpret_cast<const uint32_t*>(base + (wm >> 19));
-  }
-  int c = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-    c += int(__builtin_amdgcn_ubfe(x[2 * k], w[k], 1u)) + int(__builtin_amdgcn_ubfe(x[2 * k + 1], w[k] >> 16, 1u));
-  return c;
-}
-
 // Hits of `slots - n` zero-valued pad probes: bit 0 of the bitmap times the
 // number of probed slots that were not array values (counted on lane 0 only,
 // so the wave sum subtracts it once).  Dword 0 is not moved by the swizzle.
@@ -441,7 +416,7 @@ __device__ __forceinline__ uint4 load_bhead(const uint16_t* p, int64_t m) {
 }
 
 // |B & staged| with B's head (load_bhead) already in registers
-template <bool SWZ, bool LEAN = false>
+template <bool SWZ>
 __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t* p, int64_t m, const uint4 head) {
   const int lane = lane_id();
   const int t = meta_type(m);
@@ -453,11 +428,7 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
       return int(__builtin_amdgcn_ubfe(bm_word<SWZ>(bm, v), v, 1u)) - pad_hits(bm, 64, n);
     }
     const int n8 = (n + 7) >> 3;
-    if (n <= 512) {
-      const uint4 h = lane < n8 ? head : make_uint4(0, 0, 0, 0);
-      if constexpr (LEAN) return probe8_lean(bm, h) - pad_hits(bm, 512, n);
-      else return probe8<SWZ>(bm, h) - pad_hits(bm, 512, n);
-    }
+    if (n <= 512) return probe8<SWZ>(bm, lane < n8 ? head : make_uint4(0, 0, 0, 0)) - pad_hits(bm, 512, n);
     // bigger arrays: chunk `lane` is the head, the rest pipelined as probe_pipe
     const auto p4 = gp(reinterpret_cast<const uint4*>(p));
     const int iters = (n8 + 63) >> 6;
@@ -469,8 +440,7 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
       const int ne8 = e8 + 64;
       uint4 nxt = make_uint4(0, 0, 0, 0);
       if (ne8 < n8) nxt = p4[ne8];
-      if constexpr (LEAN) c += probe8_lean(bm, cur);
-      else c += probe8<SWZ>(bm, cur);
+      c += probe8<SWZ>(bm, cur);
       cur = nxt;
       e8 = ne8;
     }
@@ -528,7 +498,7 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // switches to a new A that is an array of <= 512 values (41.6M of the 58.6M
 // pairs of the headline batch are array x array), so staging it waits on no
 // global load.  Measured 17.7 vs 16.7 ms (profiles/r04_f/): not the default.
-template <int CQ, bool APF = false, bool LEAN = false>
+template <int CQ, bool APF = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -601,7 +571,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       }
       int c;
       if (a == cached && va == cached_v) {
-        c = count_vs_head<true, LEAN>(lb, pB, mB, head);
+        c = count_vs_head<true>(lb, pB, mB, head);
       } else {
         const bool next_same = j >= 0 && __builtin_amdgcn_readlane(ea, j) == a &&
                                __builtin_amdgcn_readlane(vai, j) == va;
@@ -623,7 +593,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
             stage(lb, pA, mA);
           cached = a;
           cached_v = va;
-          c = count_vs_head<true, LEAN>(lb, pB, mB, head);
+          c = count_vs_head<true>(lb, pB, mB, head);
         }
       }
       c = wave_sum(c);
@@ -879,9 +849,6 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
     else if (variant == 13)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q,    \
                          views, S, pairs, partial);                                                          \
-    else if (variant == 14)                                                                                  \
-      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, \
-                         Q, views, S, pairs, partial);                                                       \
     else                                                                                                     \
       hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
                          pairs, partial);                                                                    \
