@@ -203,6 +203,43 @@ def test_nosrc_fused_kernels_equal_torch_batch(lazy_env, monkeypatch):
     assert [_pairs(r) for r in rc.topn_nosrc(ns, ths)] == [_pairs(r) for r in ref]
 
 
+def test_nosrc_fused_concurrent_batches_on_lanes(lazy_env):
+    """Concurrent cache-only batches each check out a (side stream, pinned
+    parameter buffer) lane: 8 threads x 12 batches of different n / threshold
+    mixes answer exactly as the same batches run one at a time, and the lanes
+    are reused (the pool never holds more than the concurrency)."""
+    from pilosa_amd.ops import topn_exec
+    holder, ex, gpu, _, _ = lazy_env
+    ex.execute("i", "TopN(h, n=10)")
+    rc = next(iter(gpu._rank_cache_map.values()))[1]
+    rng = np.random.default_rng(5)
+    batches = []
+    for _ in range(96):
+        q = int(rng.integers(1, 17))
+        batches.append(([int(x) for x in rng.choice([0, 1, 5, 10, 50, 100, 400], q)],
+                        [int(x) for x in rng.choice([1, 2, 20, 300], q)]))
+    want = [[_pairs(r) for r in rc._topn_nosrc_fused(ns, ths)] for ns, ths in batches]
+    n0 = len(topn_exec._LANES.get(rc.view.device, []))
+    got = [None] * len(batches)
+    err = []
+
+    def worker(w):
+        try:
+            for k in range(w, len(batches), 8):
+                got[k] = [_pairs(r) for r in rc._topn_nosrc_fused(*batches[k])]
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not err, err[0]
+    assert got == want
+    lanes = topn_exec._LANES.get(rc.view.device, [])
+    assert 1 <= len(lanes) <= n0 + 8
+
+
 @pytest.mark.skipif(shardwidth.WIDE, reason="the slot index is per 2^20-column arena shard: wider "
                     "fragments answer src TopN through the pair-count path")
 def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
