@@ -13,7 +13,9 @@ concurrent collector):
   * objects that are alive after start-up or a warm-up are moved out of the
     collector's generations (``gc.freeze``), so collections walk only what
     was allocated since;
-  * gen-0 collections run every ``THRESHOLD0`` allocations instead of 700;
+  * gen-0 collections run every ``THRESHOLD0`` net allocations instead of 700
+    (10k: a collection of that many young objects stays well under a
+    millisecond, so it does not show in request tail latency);
   * :class:`Refreezer` re-freezes survivors periodically (after a young
     collection, so short-lived cycles are reclaimed first) and runs one full
     unfrozen collection every ``full_every`` seconds, so cyclic garbage that
@@ -25,7 +27,7 @@ import gc
 import os
 import time
 
-THRESHOLD0 = 50_000
+THRESHOLD0 = 10_000
 
 
 def enabled() -> bool:
