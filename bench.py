@@ -1280,6 +1280,9 @@ def run_disk_mesh(args, world, rank, dev, queries, ra, rb):
             mesh.serve()
             return 0.0, {}
         ex.mesh = mesh
+        from pilosa_amd.utils import gctune   # the front end's GC policy (Server.open does the same)
+        gctune.configure()
+        gctune.freeze_long_lived()
         per_rank = {r: len(v.get("i", [])) for r, v in mesh.shard_counts().items()}
         extra.update({"load_s_rank0": round(load_s, 2), "load": gpu.last_load,
                       "hbm_bytes_rank0": view.nbytes() if view is not None else 0,

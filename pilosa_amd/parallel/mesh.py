@@ -357,9 +357,20 @@ class ShardMesh:
     # ------------------------------------------------------------ worker loop
     def serve(self):
         """Ranks > 0: execute broadcast commands until ``stop``."""
+        from pilosa_amd.utils import gctune
+
         from .collectives import decode
 
+        refreeze = None
+        if gctune.enabled():
+            # this rank's holder and arena are built: keep them out of the
+            # cyclic collector's walk (utils/gctune.py), as the front end does
+            gctune.configure()
+            gctune.freeze_long_lived()
+            refreeze = gctune.Refreezer()
         while True:
+            if refreeze is not None:
+                refreeze.tick()
             op, payload = self.comm.bcast_bytes()
             if op == OP_STOP:
                 while self._pending:
