@@ -36,7 +36,9 @@
 // (18.8 ms, see lds_swz); one-op LDS word addressing per probe half through
 // an inline-asm mask (28 instead of 32 VALU per 8 probes, but 17.2 ms: the asm
 // stopped the probe loop's unroll; 32 / 16 queries per wave 17.5 / 19.9 ms,
-// profiles/r04_l/); every load of a container issued before any of it
+// profiles/r04_l/); non-temporal loads for B containers whose row occurs once
+// in the batch (host-marked, so they would not evict reused containers from
+// L2: 17.4 vs 16.7 ms, profiles/r04_o/); every load of a container issued before any of it
 // is consumed (v9, 20.9 ms: one round trip per array instead of one per
 // 512 values, but slower -- the chunked walk is not latency-bound,
 // profiles/r03_v9/).  Occupancy: the kernel holds 20 waves/CU (8 KiB LDS and
@@ -404,33 +406,20 @@ __device__ __forceinline__ int popc_and4(const uint4 a, const uint4 b) {
 // pair, so a tail pair (most pairs) waits for nothing; the in-order vmcnt wait
 // for anything loaded later also covers the prefetch, which by then has had
 // the previous pair's work to arrive.
-// Non-temporal 16-byte load (variant 15): streamed once, so it should not
-// evict the unit's reused containers from L2.
-typedef uint32_t pk_u32x4 __attribute__((ext_vector_type(4)));
-template <class P>
-__device__ __forceinline__ uint4 ld_nt4(P a) {
-  const pk_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const PK_GLOBAL pk_u32x4*>(a));
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-__device__ __forceinline__ uint4 load_bhead(const uint16_t* p, int64_t m, bool nt = false) {
+__device__ __forceinline__ uint4 load_bhead(const uint16_t* p, int64_t m) {
   const int lane = lane_id();
   const int t = meta_type(m);
   if (t == CT_ARRAY && meta_n(m) <= 64) {
-    const auto a = gp(p) + min(lane, meta_n(m) - 1);
-    const uint32_t v = uint32_t(nt ? __builtin_nontemporal_load(a) : *a);
+    const uint32_t v = uint32_t(gp(p)[min(lane, meta_n(m) - 1)]);
     return make_uint4(v, 0, 0, 0);
   }
   const int last = t == CT_BITMAP ? 511 : (t == CT_ARRAY ? ((meta_n(m) + 7) >> 3) - 1 : 0);
-  const auto a = gp(reinterpret_cast<const uint4*>(p)) + min(lane, last);
-  if (nt) return ld_nt4(a);
-  return *a;
+  return gp(reinterpret_cast<const uint4*>(p))[min(lane, last)];
 }
 
 // |B & staged| with B's head (load_bhead) already in registers
 template <bool SWZ>
-__device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t* p, int64_t m, const uint4 head,
-                                             bool nt = false) {
+__device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t* p, int64_t m, const uint4 head) {
   const int lane = lane_id();
   const int t = meta_type(m);
   const uint32_t* bm = reinterpret_cast<const uint32_t*>(lb);
@@ -452,10 +441,7 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
     for (int it = 0; it < iters; it++) {
       const int ne8 = e8 + 64;
       uint4 nxt = make_uint4(0, 0, 0, 0);
-      if (ne8 < n8) {
-        if (nt) nxt = ld_nt4(p4 + ne8);
-        else nxt = p4[ne8];
-      }
+      if (ne8 < n8) nxt = p4[ne8];
       c += probe8<SWZ>(bm, cur);
       cur = nxt;
       e8 = ne8;
@@ -463,18 +449,14 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
     return c - pad_hits(bm, iters * 512, n);
   }
   if (t == CT_BITMAP) {
-    const auto g0 = gp(reinterpret_cast<const uint4*>(p));
-    auto g = [&](int k) -> uint4 {
-      if (nt) return ld_nt4(g0 + k);
-      return g0[k];
-    };
+    const auto g = gp(reinterpret_cast<const uint4*>(p));
     const uint4* l4 = reinterpret_cast<const uint4*>(lb);
     auto li = [&](int k) { return SWZ ? lds_swzc(uint32_t(k * 64 + lane)) : uint32_t(k * 64 + lane); };
     int c = popc_and4(l4[li(0)], head);
     {
       uint4 b[4], x[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) b[k] = g((1 + k) * 64 + lane);
+      for (int k = 0; k < 4; k++) b[k] = g[(1 + k) * 64 + lane];
 #pragma unroll
       for (int k = 0; k < 4; k++) x[k] = l4[li(1 + k)];
 #pragma unroll
@@ -483,7 +465,7 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
     {
       uint4 b[3], x[3];
 #pragma unroll
-      for (int k = 0; k < 3; k++) b[k] = g((5 + k) * 64 + lane);
+      for (int k = 0; k < 3; k++) b[k] = g[(5 + k) * 64 + lane];
 #pragma unroll
       for (int k = 0; k < 3; k++) x[k] = l4[li(5 + k)];
 #pragma unroll
@@ -518,7 +500,7 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // switches to a new A that is an array of <= 512 values (41.6M of the 58.6M
 // pairs of the headline batch are array x array), so staging it waits on no
 // global load.  Measured 17.7 vs 16.7 ms (profiles/r04_f/): not the default.
-template <int CQ, bool APF = false, bool NTB = false>
+template <int CQ, bool APF = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -536,21 +518,18 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
   int vai = -1;
   int64_t ma = 0, mb = 0;
   uint64_t pal = 0, pbl = 0;
-  int ntl = 0;  // NTB: this query's B row occurs once in the batch (QueryProg.pad[0] bit 0)
   if (lane < nq) {
     const uint2 e = pairs[u * Q + q0 + lane];
     if (e.x != NONE) {
       ea = e.x;
       vai = progs[q0 + lane].leaf_view[0];
       const int vbi = progs[q0 + lane].leaf_view[1];
-      if (NTB) ntl = int(progs[q0 + lane].pad[0] & 1);
       ma = gp(views[vai].meta)[e.x];
       mb = gp(views[vbi].meta)[e.y];
       pal = reinterpret_cast<uint64_t>(payload_of(views[vai], ma));
       pbl = reinterpret_cast<uint64_t>(payload_of(views[vbi], mb));
     }
   }
-  auto bnt = [&](int k) { return NTB && __builtin_amdgcn_readlane(ntl, k) != 0; };
   uint64_t todo = __ballot(ea != NONE);
   int mine = 0;
   if (todo) {
@@ -558,7 +537,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
     int cached_v = -1;
     int i = __builtin_ctzll(todo);
     todo &= todo - 1;
-    uint4 pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, i)), rl64(mb, i), bnt(i));
+    uint4 pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, i)), rl64(mb, i));
     // A chunk of the pair about to run (APF), valid when apre_ok
     auto small_array = [](int64_t m) { return meta_type(m) == CT_ARRAY && meta_n(m) <= 512; };
     auto load_ahead = [&](int k) {
@@ -583,7 +562,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       const uint4 head = pre;
       const uint4 ahead = apre;
       const bool aok = apre_ok;
-      if (j >= 0) pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j), bnt(j));
+      if (j >= 0) pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j));
       if (APF) {
         apre_ok = false;
         if (j >= 0 && !(__builtin_amdgcn_readlane(ea, j) == a && __builtin_amdgcn_readlane(vai, j) == va) &&
@@ -594,7 +573,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       }
       int c;
       if (a == cached && va == cached_v) {
-        c = count_vs_head<true>(lb, pB, mB, head, bnt(i));
+        c = count_vs_head<true>(lb, pB, mB, head);
       } else {
         const bool next_same = j >= 0 && __builtin_amdgcn_readlane(ea, j) == a &&
                                __builtin_amdgcn_readlane(vai, j) == va;
@@ -616,7 +595,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
             stage(lb, pA, mA);
           cached = a;
           cached_v = va;
-          c = count_vs_head<true>(lb, pB, mB, head, bnt(i));
+          c = count_vs_head<true>(lb, pB, mB, head);
         }
       }
       c = wave_sum(c);
@@ -872,9 +851,6 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
     else if (variant == 13)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q,    \
                          views, S, pairs, partial);                                                          \
-    else if (variant == 15)                                                                                  \
-      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, \
-                         Q, views, S, pairs, partial);                                                       \
     else                                                                                                     \
       hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
                          pairs, partial);                                                                    \

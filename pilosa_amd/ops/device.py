@@ -135,22 +135,6 @@ def compile_expr(expr, view_index: Dict[int, int]):
     return leaf_views, leaf_rows, prog
 
 
-def _mark_single_use_b(progs: np.ndarray) -> np.ndarray:
-    """QueryProg.pad[0] bit 0 = this Count(Intersect(a, b)) query's B row
-    (leaf 1: the colder one after ``_hot_leaf_first``) occurs once in the
-    batch as either leaf: the pair kernel then streams B's containers with
-    non-temporal loads so they do not evict the unit's reused containers from
-    L2 (pair kernel variant 15)."""
-    lr, lv = progs["leaf_row"], progs["leaf_view"]
-    key = np.concatenate([lv[:, 0].astype(np.int64) << 40 | lr[:, 0], lv[:, 1].astype(np.int64) << 40 | lr[:, 1]])
-    u, cnt = np.unique(key, return_counts=True)
-    kb = key[len(progs):]
-    single = cnt[np.searchsorted(u, kb)] == 1
-    progs = progs.copy()
-    progs["pad"][:, 0] = single.astype(np.int64)
-    return progs
-
-
 def _canonical_and2(progs: np.ndarray) -> np.ndarray:
     """Intersect(Row(a), Row(a)) compiles to one leaf with prog [0, 0, AND];
     give it a second (identical) leaf so it takes the pair-kernel route."""
@@ -1255,8 +1239,6 @@ class GpuEngine:
                 bool(np.all((np_ == 3) & (pg[:, 0] == 0) & (pg[:, 1] == 1) & (pg[:, 2] == OP_AND))):
             progs = self._hot_leaf_first(progs, np.ones(Q, bool))
             lr = progs["leaf_row"]
-            if self.and2_variant == 15:
-                progs = _mark_single_use_b(progs)
             order = np.lexsort((lr[:, 1], lr[:, 0]))
             tv, tp, to = self._h2d_many([varr.view(np.uint8), np.ascontiguousarray(progs[order]).view(np.uint8),
                                          order.astype(np.int64)])

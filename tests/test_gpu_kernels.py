@@ -126,7 +126,7 @@ def test_and2_pair_kernels_match_tile_kernel(setup):
         exprs.append(Op("and", (Leaf(va, min(a, 5) if va is view2 else a), Leaf(view, b))))
         ra = min(a, 5) if va is view2 else a
         want.append(sum(_row(x, ra).intersection_count(_row(f, b)) for x, f in zip(fa, frags)))
-    for var in (6, 10, 12, 13, 15):
+    for var in (6, 10, 12, 13):
         for cq in (0, 16, 32, 64):
             e2 = GpuEngine(view.device)
             e2.and2_cq = cq

@@ -187,17 +187,3 @@ def test_plan_count_text_time_ranges(views):
     assert _pql.plan_count_text(text, fields, dirs, True, True, 1, {k1: [1, 2, 3]}) is None   # k2 unresolved
     for bad in ("Count(Row(t=3, from='2020-01-01))", "Count(Row(t=3, from=1, from=2))", "Count(Row(t=3, at=1))"):
         assert _pql.plan_count_text(bad, fields, dirs, True, True, 1, ranges) is None, bad
-
-
-def test_single_use_b_marking():
-    """Pair-kernel variant 15's host flag: B (leaf 1) rows that occur once in
-    the batch, as either leaf, get QueryProg.pad[0] bit 0."""
-    import numpy as np
-
-    from pilosa_amd.ops.device import QPROG_DTYPE, _mark_single_use_b
-    p = np.zeros(5, dtype=QPROG_DTYPE)
-    p["leaf_row"][:, :2] = [[1, 2], [1, 3], [4, 2], [5, 6], [6, 7]]
-    p["leaf_view"][:, 1] = [0, 0, 0, 0, 1]    # row 7 of view 1
-    q = _mark_single_use_b(p)
-    assert q["pad"][:, 0].tolist() == [0, 1, 0, 0, 1]
-    assert (p["pad"] == 0).all()            # the input batch is not modified
