@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/r04_p
 mkdir -p $O
 D=/tmp/pilosa_r04p
-for R in 3072 4096 6144; do
+for R in ${RS:-2048 2560 3072 3584}; do
   timeout -k 10 600 env PILOSA_TOPN_HOT=$R python -u bench.py --steps 2 --warmup 1 --configs none --serve-seconds 0 \
       --topn-batches 40 --topn-cache-batches 40 --data-dir $D --keep-data > $O/bench_R$R.log 2> $O/bench_R$R.err \
       || { tail -c 2000 $O/bench_R$R.err; exit 1; }
