@@ -36,8 +36,10 @@ LDS_LIMIT = 160 * 1024 - 1024
 # slot index / histogram cover the ranks after them.  Bench src mix, 16-query
 # batch on the 954-shard headline index (profiles/r03_hotpart): 2048 -> hot
 # 9.05 + tail histogram 3.17 ms; 4096 -> 10.03 + 1.40 ms (13.0 vs 13.9 ms per
-# batch end to end); 8192 -> hot 12.7 ms, worse
-HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "4096"))
+# batch end to end); 8192 -> hot 12.7 ms, worse.  Round 4 (current kernels,
+# through the executor, profiles/r04_p/): 2048 / 2560 / 3072 / 3584 / 4096 /
+# 6144 -> 1,194 / 1,223 / 1,264-1,278 / 1,261 / 1,196 / 1,203 src q/s.
+HOT_RANKS = int(os.environ.get("PILOSA_TOPN_HOT", "3072"))
 # queries per hot-rank launch: up to 16 take topn_hot_kernel<16> (u16 query
 # masks of a whole key in LDS), 17..32 topn_hot_kernel<32> (u32 masks of half
 # a key per workgroup: twice the queries for the same streamed bytes).  Both
