@@ -1,0 +1,15 @@
+#!/bin/bash
+# Headline Count step: request threads (--clients) sweep.
+set -o pipefail
+O=gpurun_out/r04_r
+mkdir -p $O
+D=/tmp/pilosa_r04r
+for C in ${CS:-2 3 4 6}; do
+  timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --clients $C --configs none --serve-seconds 0 \
+      --topn-batches 0 --data-dir $D --keep-data > $O/bench_c$C.log 2> $O/bench_c$C.err || { tail -c 2000 $O/bench_c$C.err; exit 1; }
+  python - "$O/bench_c$C.log" "$C" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+print("clients", sys.argv[2], "value", d["value"], "ms_per_step", d["ms_per_step"], "verified", d.get("verified"))
+PY
+done
