@@ -1589,7 +1589,9 @@ def main():
     ap.add_argument("--cols", type=int, default=TOTAL_COLS)
     ap.add_argument("--rows", type=int, default=NROWS)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--clients", type=int, default=3, help="disk mode: concurrent request threads")
+    ap.add_argument("--clients", type=int, default=2,
+                    help="disk mode: concurrent request threads (2 keeps the GPU fed: 1 / 2 / 3 / 4 / 6 threads "
+                         "measured 221k / 236-237k / 234k / 232k / 225k Count q/s, profiles/r04_r/)")
     ap.add_argument("--data-dir", default=None, help="disk mode: reuse/keep fragment files under this dir")
     ap.add_argument("--cold-load", type=int, default=1,
                     help="disk mode: drop the fragment files from the page cache before loading (1) or not (0)")
