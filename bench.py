@@ -1589,9 +1589,10 @@ def main():
     ap.add_argument("--cols", type=int, default=TOTAL_COLS)
     ap.add_argument("--rows", type=int, default=NROWS)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--clients", type=int, default=2,
-                    help="disk mode: concurrent request threads (2 keeps the GPU fed: 1 / 2 / 3 / 4 / 6 threads "
-                         "measured 221k / 236-237k / 234k / 232k / 225k Count q/s, profiles/r04_r/)")
+    ap.add_argument("--clients", type=int, default=0,
+                    help="disk mode: concurrent request threads; 0 = 2 on one GPU (1 / 2 / 3 / 4 / 6 threads "
+                         "measured 221k / 236-237k / 234k / 232k / 225k Count q/s, profiles/r04_r/), 4 on a "
+                         "mesh (every batch also waits on its collectives, so more must be in flight)")
     ap.add_argument("--data-dir", default=None, help="disk mode: reuse/keep fragment files under this dir")
     ap.add_argument("--cold-load", type=int, default=1,
                     help="disk mode: drop the fragment files from the page cache before loading (1) or not (0)")
@@ -1634,6 +1635,8 @@ def main():
     import torch.distributed as dist
 
     world, rank, dev = setup_dist()
+    if args.clients <= 0:
+        args.clients = 2 if world == 1 else 4
     rng = np.random.default_rng(1234)
     nq = args.batch * (args.steps + args.warmup)
     ra = zipf_rows(rng, nq, args.rows)
