@@ -114,7 +114,8 @@ void bsi_range_count(torch::Tensor views, int64_t S, torch::Tensor bsi_args, int
   check_launch("bsi_range_count");
 }
 
-void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out) {
+void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out,
+                int64_t which) {
   check_dev(progs, "progs");
   check_dev(views, "views");
   check_dev(out, "out");
@@ -122,7 +123,7 @@ void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() >= S * 16 * 10, "out must be int64[S*16*10]");
   pk::launch_bsi_minmax(reinterpret_cast<const pk::QueryProg*>(progs.data_ptr<uint8_t>()),
                         reinterpret_cast<const pk::ViewDev*>(views.data_ptr<uint8_t>()), int(S),
-                        bsi_args_from(bsi_args), out.data_ptr<int64_t>(), cur_stream(views));
+                        bsi_args_from(bsi_args), out.data_ptr<int64_t>(), cur_stream(views), int(which));
   check_launch("bsi_minmax");
 }
 
@@ -546,7 +547,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("variant") = 1);
   m.def("bsi_range", &bsi_range, "BSI predicate -> bitmap container per (shard, key)");
   m.def("bsi_range_count", &bsi_range_count, "Count(Row(v <op> x)): fused BSI predicate + count");
-  m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key)");
+  m.def("bsi_minmax", &bsi_minmax, "BSI min/max descents per (shard, key); which: 0 both, 1 Min, 2 Max",
+        py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("bsi_args"), py::arg("out"), py::arg("which") = 0);
   m.def("leaf_src", &leaf_src, "src containers of plain rows straight from the arena (TopN srcs)");
   m.def("row_counts", &row_counts, "row counts of (shard, dense row) entries (device rank caches)");
   m.def("topn_cache_counts", &topn_cache_counts, "cache-only TopN: [candidate x shard] row counts");

@@ -1178,7 +1178,10 @@ __global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restric
 // unsigned minimum of the positives, for Max the unsigned maximum of the
 // positives and the minimum magnitude of the negatives.  out[item] = 4 x
 // (value, count); the host folds keys into shard results exactly as one
-// shard-wide descent would (the key sets partition the shard).
+// shard-wide descent would (the key sets partition the shard).  WHICH = 1
+// (Min) runs only maxU(neg) / minU(pos), 2 (Max) only maxU(pos) / minU(neg):
+// half the tiles, popcounts and wave reductions per bit (0 = all four).
+template <int WHICH>
 __global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __restrict__ progs,
                                                          const ViewDev* __restrict__ views, int S, BsiArgs bsi,
                                                          int64_t* __restrict__ out) {
@@ -1219,30 +1222,35 @@ __global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __rest
   for (int i = depth - 1; i >= 0; i--) {
     bsi_bit(c, i, r);
     Tile t;
-    // maxU(neg)
-    t = fmaxn;
-    tile_op<OP_AND>(t, r);
-    int64_t k = wave_sum_i64(tile_popc(t));
-    if (k > 0) { vmaxn |= int64_t(1) << i; fmaxn = t; cmaxn = k; }
-    else if (i == 0) cmaxn = wave_sum_i64(tile_popc(fmaxn));
-    // maxU(pos)
-    t = fmaxp;
-    tile_op<OP_AND>(t, r);
-    k = wave_sum_i64(tile_popc(t));
-    if (k > 0) { vmaxp |= int64_t(1) << i; fmaxp = t; cmaxp = k; }
-    else if (i == 0) cmaxp = wave_sum_i64(tile_popc(fmaxp));
-    // minU(pos)
-    t = fminp;
-    tile_op<OP_ANDNOT>(t, r);
-    k = wave_sum_i64(tile_popc(t));
-    if (k > 0) { fminp = t; cminp = k; }
-    else { vminp += int64_t(1) << i; if (i == 0) cminp = wave_sum_i64(tile_popc(fminp)); }
-    // minU(neg)
-    t = fminn;
-    tile_op<OP_ANDNOT>(t, r);
-    k = wave_sum_i64(tile_popc(t));
-    if (k > 0) { fminn = t; cminn = k; }
-    else { vminn += int64_t(1) << i; if (i == 0) cminn = wave_sum_i64(tile_popc(fminn)); }
+    int64_t k;
+    if (WHICH != 2) {  // maxU(neg)
+      t = fmaxn;
+      tile_op<OP_AND>(t, r);
+      k = wave_sum_i64(tile_popc(t));
+      if (k > 0) { vmaxn |= int64_t(1) << i; fmaxn = t; cmaxn = k; }
+      else if (i == 0) cmaxn = wave_sum_i64(tile_popc(fmaxn));
+    }
+    if (WHICH != 1) {  // maxU(pos)
+      t = fmaxp;
+      tile_op<OP_AND>(t, r);
+      k = wave_sum_i64(tile_popc(t));
+      if (k > 0) { vmaxp |= int64_t(1) << i; fmaxp = t; cmaxp = k; }
+      else if (i == 0) cmaxp = wave_sum_i64(tile_popc(fmaxp));
+    }
+    if (WHICH != 2) {  // minU(pos)
+      t = fminp;
+      tile_op<OP_ANDNOT>(t, r);
+      k = wave_sum_i64(tile_popc(t));
+      if (k > 0) { fminp = t; cminp = k; }
+      else { vminp += int64_t(1) << i; if (i == 0) cminp = wave_sum_i64(tile_popc(fminp)); }
+    }
+    if (WHICH != 1) {  // minU(neg)
+      t = fminn;
+      tile_op<OP_ANDNOT>(t, r);
+      k = wave_sum_i64(tile_popc(t));
+      if (k > 0) { fminn = t; cminn = k; }
+      else { vminn += int64_t(1) << i; if (i == 0) cminn = wave_sum_i64(tile_popc(fminn)); }
+    }
   }
   const int64_t npos = wave_sum_i64(tile_popc(pos)), nneg = wave_sum_i64(tile_popc(neg));
   if (lane == 0) {
@@ -1304,11 +1312,16 @@ void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t 
 }
 
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
-                       hipStream_t st) {
+                       hipStream_t st, int which) {
   const int64_t items = int64_t(S) * 16;
   if (items == 0) return;
-  hipLaunchKernelGGL(bsi_minmax_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, progs, views, S,
-                     bsi, out);
+  const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
+  if (which == 1)
+    hipLaunchKernelGGL(bsi_minmax_kernel<1>, grid, block, 0, st, progs, views, S, bsi, out);
+  else if (which == 2)
+    hipLaunchKernelGGL(bsi_minmax_kernel<2>, grid, block, 0, st, progs, views, S, bsi, out);
+  else
+    hipLaunchKernelGGL(bsi_minmax_kernel<0>, grid, block, 0, st, progs, views, S, bsi, out);
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,

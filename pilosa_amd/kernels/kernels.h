@@ -65,7 +65,7 @@ void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t 
                       int64_t* out_meta, unsigned long long* out_count, hipStream_t st);
 // BSI min/max descents per (shard, key): out int64[S*16*10] (see bitmap_kernels.hip).
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
-                       hipStream_t st);
+                       hipStream_t st, int which = 0);
 // fmode: 0 no filters, 1 flat-fold filter programs, 2 any program.
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
                     unsigned long long* out_sum, unsigned long long* out_cnt, int fmode, hipStream_t st);

@@ -1417,8 +1417,10 @@ class GpuEngine:
                                      self.BSI_OPS[op], int(p1), int(p2), out)
         return out
 
-    def bsi_minmax(self, filt: Optional[object], bsi_view: "DeviceView", depth: int) -> np.ndarray:
-        """Per (shard, key) descents -> int64[S, 16, 10] (see bsi_minmax_kernel)."""
+    def bsi_minmax(self, filt: Optional[object], bsi_view: "DeviceView", depth: int, which: str = "") -> np.ndarray:
+        """Per (shard, key) descents -> int64[S, 16, 10] (see bsi_minmax_kernel);
+        ``which`` "min" / "max" runs only that call's two descents (the other
+        columns stay 0), "" all four."""
         torch = self.torch
         S = bsi_view.S
         view_index: Dict[int, int] = {id(bsi_view): 0}
@@ -1441,7 +1443,7 @@ class GpuEngine:
         args = self.bsi_args(bsi_view, depth)
         if S and args[2] >= 0:
             tp, tv = self.upload_batch(progs, ordered)
-            self.ext.bsi_minmax(tp, tv, S, torch.from_numpy(args), out)
+            self.ext.bsi_minmax(tp, tv, S, torch.from_numpy(args), out, {"min": 1, "max": 2}.get(which, 0))
         return out.cpu().numpy().reshape(S, 16, 10)
 
     def bsi_sum_async(self, filters: Sequence[Optional[object]], bsi_view: "DeviceView", depth: int,

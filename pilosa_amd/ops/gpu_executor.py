@@ -424,7 +424,7 @@ class GpuExecutor:
                 return [ValCount() for _ in shards]
         try:
             self.launches += 1
-            o = self.engine.bsi_minmax(filt, bv, b.bit_depth)
+            o = self.engine.bsi_minmax(filt, bv, b.bit_depth, which)
         except CompileError:
             raise NotImplementedError
         vals, cnts = _minmax_per_shard(o, which)
