@@ -1078,8 +1078,12 @@ __device__ void bsi_between_unsigned(const BsiCtx& c, Tile& filt, int depth, uin
 __device__ __forceinline__ void tile_or(Tile& a, const Tile& b) { tile_op<OP_OR>(a, b); }
 
 // op: 0 EQ, 1 NEQ, 2 LT, 3 LTE, 4 GT, 5 GTE, 6 BETWEEN(p1..p2), 7 NOT NULL
-__global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restrict__ views, int S, BsiArgs bsi,
-                                                        int op, int64_t p1, int64_t p2,
+// OPC: the comparison as a template constant, so each instantiation keeps only
+// its own path's tiles live (the runtime switch over every op held 256 VGPRs,
+// one wave per SIMD).  ``op_rt`` is unused (kept for the launcher's signature).
+template <int OPC>
+__global__ __launch_bounds__(256, 2) void bsi_range_kernel(const ViewDev* __restrict__ views, int S, BsiArgs bsi,
+                                                        int op_rt, int64_t p1, int64_t p2,
                                                         uint16_t* __restrict__ out_payload,
                                                         int64_t* __restrict__ out_meta,
                                                         unsigned long long* __restrict__ out_count) {
@@ -1094,6 +1098,8 @@ __global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restric
   BsiCtx c{bsi, bv, s, j, bv.shard_base[s], bv.rowptr + int64_t(s) * (bv.D + 1), scratch[wave].lb};
   plane_index(c);
   const int depth = bsi.depth;
+  constexpr int op = OPC;
+  (void)op_rt;
   Tile b, sign, res;
   bsi_row(c, bsi.row_exists, b);
   bsi_row(c, bsi.row_sign, sign);
@@ -1136,9 +1142,9 @@ __global__ __launch_bounds__(256) void bsi_range_kernel(const ViewDev* __restric
     } else {
       Tile neg = b;
       tile_op<OP_AND>(neg, sign);
-      bsi_lt_unsigned(c, neg, depth, up, allow);
-      res = b;
+      res = b;   // the positives, taken before the descent so b and sign are dead during it
       tile_op<OP_ANDNOT>(res, sign);
+      bsi_lt_unsigned(c, neg, depth, up, allow);
       tile_or(res, neg);
     }
   } else {  // between
@@ -1307,8 +1313,17 @@ void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t 
                       int64_t* out_meta, unsigned long long* out_count, hipStream_t st) {
   const int64_t items = int64_t(S) * 16;
   if (items == 0) return;
-  hipLaunchKernelGGL(bsi_range_kernel, dim3(grid_for(items)), dim3(64 * WAVES_PER_BLOCK), 0, st, views, S, bsi, op,
-                     p1, p2, out_payload, out_meta, out_count);
+  const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
+#define PK_RANGE(OPV)                                                                                       \
+  case OPV:                                                                                                 \
+    hipLaunchKernelGGL(bsi_range_kernel<OPV>, grid, block, 0, st, views, S, bsi, op, p1, p2, out_payload,  \
+                       out_meta, out_count);                                                                \
+    break;
+  switch (op) {
+    PK_RANGE(0) PK_RANGE(1) PK_RANGE(2) PK_RANGE(3) PK_RANGE(4) PK_RANGE(5) PK_RANGE(6) PK_RANGE(7)
+    default: break;
+  }
+#undef PK_RANGE
 }
 
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
