@@ -1187,8 +1187,8 @@ __global__ __launch_bounds__(256, 2) void bsi_range_kernel(const ViewDev* __rest
 // shard-wide descent would (the key sets partition the shard).  WHICH = 1
 // (Min) runs only maxU(neg) / minU(pos), 2 (Max) only maxU(pos) / minU(neg):
 // half the tiles, popcounts and wave reductions per bit (0 = all four).
-template <int WHICH>
-__global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __restrict__ progs,
+template <int WHICH, int MINW = 2>
+__global__ __launch_bounds__(256, MINW) void bsi_minmax_kernel(const QueryProg* __restrict__ progs,
                                                          const ViewDev* __restrict__ views, int S, BsiArgs bsi,
                                                          int64_t* __restrict__ out) {
   __shared__ WaveScratch scratch[WAVES_PER_BLOCK];
@@ -1221,6 +1221,8 @@ __global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __rest
     tile_op<OP_AND>(neg, sign);
     tile_op<OP_ANDNOT>(pos, sign);
   }
+  // counted first, so pos / neg are dead once the descents' tiles take them
+  const int64_t npos = wave_sum_i64(tile_popc(pos)), nneg = wave_sum_i64(tile_popc(neg));
   // four descents share each bit-slice load: maxU(neg), minU(pos), maxU(pos), minU(neg)
   Tile fmaxn = neg, fminp = pos, fmaxp = pos, fminn = neg, r;
   int64_t vmaxn = 0, vminp = 0, vmaxp = 0, vminn = 0;
@@ -1258,7 +1260,6 @@ __global__ __launch_bounds__(256) void bsi_minmax_kernel(const QueryProg* __rest
       else { vminn += int64_t(1) << i; if (i == 0) cminn = wave_sum_i64(tile_popc(fminn)); }
     }
   }
-  const int64_t npos = wave_sum_i64(tile_popc(pos)), nneg = wave_sum_i64(tile_popc(neg));
   if (lane == 0) {
     int64_t* o = out + item * 10;
     o[0] = vmaxn; o[1] = cmaxn; o[2] = vminp; o[3] = cminp;
@@ -1331,12 +1332,20 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
   const int64_t items = int64_t(S) * 16;
   if (items == 0) return;
   const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
-  if (which == 1)
-    hipLaunchKernelGGL(bsi_minmax_kernel<1>, grid, block, 0, st, progs, views, S, bsi, out);
-  else if (which == 2)
-    hipLaunchKernelGGL(bsi_minmax_kernel<2>, grid, block, 0, st, progs, views, S, bsi, out);
-  else
-    hipLaunchKernelGGL(bsi_minmax_kernel<0>, grid, block, 0, st, progs, views, S, bsi, out);
+  // PILOSA_BSI_MINMAX_WAVES=3: 3 waves per SIMD (168 VGPRs, a few spills) instead of 2
+  static const bool w3 = [] {
+    const char* e = getenv("PILOSA_BSI_MINMAX_WAVES");
+    return e && atoi(e) == 3;
+  }();
+  if (which == 1) {
+    if (w3) hipLaunchKernelGGL((bsi_minmax_kernel<1, 3>), grid, block, 0, st, progs, views, S, bsi, out);
+    else hipLaunchKernelGGL((bsi_minmax_kernel<1, 2>), grid, block, 0, st, progs, views, S, bsi, out);
+  } else if (which == 2) {
+    if (w3) hipLaunchKernelGGL((bsi_minmax_kernel<2, 3>), grid, block, 0, st, progs, views, S, bsi, out);
+    else hipLaunchKernelGGL((bsi_minmax_kernel<2, 2>), grid, block, 0, st, progs, views, S, bsi, out);
+  } else {
+    hipLaunchKernelGGL((bsi_minmax_kernel<0, 2>), grid, block, 0, st, progs, views, S, bsi, out);
+  }
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
