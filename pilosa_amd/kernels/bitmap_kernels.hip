@@ -1332,20 +1332,14 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
   const int64_t items = int64_t(S) * 16;
   if (items == 0) return;
   const dim3 grid(grid_for(items)), block(64 * WAVES_PER_BLOCK);
-  // PILOSA_BSI_MINMAX_WAVES=3: 3 waves per SIMD (168 VGPRs, a few spills) instead of 2
-  static const bool w3 = [] {
-    const char* e = getenv("PILOSA_BSI_MINMAX_WAVES");
-    return e && atoi(e) == 3;
-  }();
-  if (which == 1) {
-    if (w3) hipLaunchKernelGGL((bsi_minmax_kernel<1, 3>), grid, block, 0, st, progs, views, S, bsi, out);
-    else hipLaunchKernelGGL((bsi_minmax_kernel<1, 2>), grid, block, 0, st, progs, views, S, bsi, out);
-  } else if (which == 2) {
-    if (w3) hipLaunchKernelGGL((bsi_minmax_kernel<2, 3>), grid, block, 0, st, progs, views, S, bsi, out);
-    else hipLaunchKernelGGL((bsi_minmax_kernel<2, 2>), grid, block, 0, st, progs, views, S, bsi, out);
-  } else {
+  // 2 waves per SIMD; 3 (168 VGPRs, 224 B of spills) measured the same
+  // (1.29 vs 1.31 ms per Min, profiles/r04_u/)
+  if (which == 1)
+    hipLaunchKernelGGL((bsi_minmax_kernel<1, 2>), grid, block, 0, st, progs, views, S, bsi, out);
+  else if (which == 2)
+    hipLaunchKernelGGL((bsi_minmax_kernel<2, 2>), grid, block, 0, st, progs, views, S, bsi, out);
+  else
     hipLaunchKernelGGL((bsi_minmax_kernel<0, 2>), grid, block, 0, st, progs, views, S, bsi, out);
-  }
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
