@@ -55,14 +55,29 @@ class _Lane:
 
     def __init__(self, device):
         import torch
+        self.device = device
         self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self.pin = None
+        self._bufs = {}
 
     def pinned_i32(self, n: int):
         import torch
         if self.pin is None or self.pin.numel() < n:
             self.pin = torch.empty(max(n, 1024), dtype=torch.int32, pin_memory=True)
         return self.pin[:n]
+
+    def buf(self, name: str, n: int, dtype, pinned: bool = False):
+        """A reusable 1-D buffer of at least ``n`` elements (device, or pinned
+        host): a batch's member / totals / answer tensors and their host copy
+        cost no allocator calls once the lane is warm."""
+        import torch
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            size = max(n, 1024) + (max(n, 1024) >> 1)
+            b = (torch.empty(size, dtype=dtype, pin_memory=True) if pinned
+                 else torch.empty(size, dtype=dtype, device=self.device))
+            self._bufs[name] = b
+        return b[:n]
 
 
 _LANES: dict = {}
@@ -433,12 +448,28 @@ class DeviceRankCaches:
         prm[2 * Q:3 * Q] = [uniq_t.index(t) for t in ths]
         prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
         prm[4 * Q:] = uniq_t
-        prm_d = (pin if pin is not None else torch.from_numpy(prm)).to(dev, non_blocking=True)
-        member = torch.zeros((Q, U), dtype=torch.uint8, device=dev)
-        tot = torch.empty((len(uniq_t), U), dtype=torch.int64, device=dev)
-        out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
-        kernels().topn_cache_batch(self.cache_cnt, nmax, inv32, u32, cm, prm_d, Q, len(uniq_t), member, tot, out)
-        h = out.cpu().numpy()
+        T = len(uniq_t)
+        if lane is not None:
+            prm_d = lane.buf("prm", len(prm), torch.int32)
+            prm_d.copy_(pin, non_blocking=True)
+            member = lane.buf("member", Q * U, torch.uint8).view(Q, U)
+            member.zero_()
+            tot = lane.buf("tot", T * U, torch.int64).view(T, U)
+            out = lane.buf("out", Q * (KK + 1), torch.int64).view(Q, KK + 1)
+        else:
+            prm_d = torch.from_numpy(prm).to(dev)
+            member = torch.zeros((Q, U), dtype=torch.uint8, device=dev)
+            tot = torch.empty((T, U), dtype=torch.int64, device=dev)
+            out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
+        kernels().topn_cache_batch(self.cache_cnt, nmax, inv32, u32, cm, prm_d, Q, T, member, tot, out)
+        if lane is not None:
+            # answers to the lane's pinned buffer, then wait for this stream only
+            hb = lane.buf("out_h", out.numel(), torch.int64, pinned=True)
+            hb.copy_(out.view(-1), non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            h = hb.numpy().reshape(Q, KK + 1)
+        else:
+            h = out.cpu().numpy()
         if (h[:, 0] < 0).any():     # a query with more members than one workgroup sorts
             return None
         rows = self.view.rows
