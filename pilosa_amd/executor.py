@@ -679,16 +679,18 @@ class Executor:
                 if not cands:
                     raise err
                 regroup.setdefault(cands[0], []).append(s)
-            # the failed node's shards, regrouped by their next replica: those
-            # replicas are asked at once as well
-            futs = [self.fanout.submit(tracing.bind(self._remote_with_failover), index, c, n2, ss, opt, map_fn,
-                                       reduce_fn, local_fn, tried | {n2.id})
-                    for n2, ss in regroup.items() if n2.id != self.cluster.node.id]
+            # the failed node's shards, regrouped by their next replica.  The
+            # retries run inline on this worker: this call already holds a
+            # fan-out thread, and waiting on futures queued to the same pool
+            # starves it when many remote calls fail together (a node dying
+            # under load), hanging every map/reduce on the node.
             for n2, ss in regroup.items():
                 if n2.id == self.cluster.node.id:
-                    result = reduce_fn(result, self._map_local(ss, map_fn, reduce_fn, local_fn))
-            for f in futs:
-                result = reduce_fn(result, f.result())
+                    part = self._map_local(ss, map_fn, reduce_fn, local_fn)
+                else:
+                    part = self._remote_with_failover(index, c, n2, ss, opt, map_fn, reduce_fn, local_fn,
+                                                      tried | {n2.id})
+                result = reduce_fn(result, part)
             return result
 
     def _map_local(self, shards: List[int], map_fn, reduce_fn, local_fn):

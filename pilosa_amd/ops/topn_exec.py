@@ -345,7 +345,9 @@ class DeviceRankCaches:
         Q = len(ns)
         if Q == 0:
             return []
-        if comm is None and self.view.D and self.S < 2048:   # counts < 2^31: composite int64 key
+        # the fused kernels total int32 counts: the node's columns (every device
+        # sub-shard of every fragment, 2^20 each) must stay below 2^31
+        if comm is None and self.view.D and self.view.S < 2048:
             got = self._topn_nosrc_fused(ns, thresholds)
             return got if got is not None else self._topn_nosrc_dense(ns, thresholds)
         pq, pd, _ = self.nosrc_phase1(ns, thresholds)
@@ -416,6 +418,12 @@ class DeviceRankCaches:
         dev = self.view.device
         if dev.type != "cuda":
             return self._topn_nosrc_fused_on(ns, nn, nmax, thresholds, None)
+        # the memo (candidate x shard count matrix) reads the arena: build it on
+        # the arena's own stream, where in-place arena writes (update_rows,
+        # apply_deltas_multi, grow_segment) are ordered, and wait for it before
+        # any side stream reads it.  Later batches find it built.
+        if self._fused_memo(nmax) is False:
+            return None
         lane = _lane_take(dev)
         if not SIDE_STREAM:
             res = self._topn_nosrc_fused_on(ns, nn, nmax, thresholds, lane)

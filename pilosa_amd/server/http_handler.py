@@ -350,7 +350,7 @@ class Handler:
             # (native/wire_decode.cpp), not through protobuf repeated fields
             try:
                 m = _roaring.decode_import_request(req.body, f.type == "int")
-            except RuntimeError as e:
+            except (RuntimeError, ValueError) as e:   # ValueError: invalid UTF-8 in a name or key
                 raise HTTPError(400, f"decoding request: {e}")
             if f.type == "int":
                 self.api.import_values(index, field, m["Shard"], m["ColumnIDs"], m["Values"], m["ColumnKeys"],

@@ -94,3 +94,25 @@ def test_fanout_failover_to_replicas():
     # fail and move to their replica n2, which answers 20
     assert got == 2 + 20
     assert ("n1", (1, 4)) in client.calls and ("n2", (1, 4)) in client.calls, client.calls
+
+
+def test_fanout_failover_does_not_starve_the_pool():
+    """with every fan-out worker busy on a failing node, the
+    replica retries must not wait on futures queued to that same pool.  A
+    pool of one thread and one failing node with one replica used to hang."""
+    import concurrent.futures as cf
+
+    client = _SlowClient(0.01, fail={"n1"})
+    ex, holder = _executor(client, replicas=True)
+    ex._fanout = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fanout-test")
+    done = []
+    t = threading.Thread(target=lambda: done.append(
+        ex.execute("i", "Count(Row(f=1))", shards=list(range(6))).results[0]), daemon=True)
+    try:
+        t.start()
+        t.join(10)
+        assert not t.is_alive(), "fan-out pool starved by replica retries"
+        assert done == [2 + 20]
+    finally:
+        ex.close()
+        holder.close()

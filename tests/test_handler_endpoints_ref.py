@@ -322,3 +322,12 @@ def _translate_keys(node):  # "translate keys" :942
         m = pb.TranslateKeysResponse()
         m.ParseFromString(out)
         assert st == 200 and list(m.IDs) == want
+
+
+def test_import_invalid_utf8_is_bad_request(node):
+    """an import body whose Index / key strings are not UTF-8 is a
+    400 (the reference's unmarshal error), not a 500."""
+    _populate(node)
+    body = b"\x0a\x02\xff\xfe" + b"\x12\x02f1"      # Index = b'\xff\xfe', Field = "f1"
+    st, _ = _req(node, "POST", "/index/i0/field/f1/import", body, PB)
+    assert st == 400
