@@ -848,6 +848,34 @@ def verify_sample(eng, view, host_bitmap, pairs, answered, world, dev, nshards_c
             "mismatch_totals": bad_total, "verified": bad_shard == 0 and bad_total == 0}
 
 
+def kfd_gpu_count(root: str = "/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs visible to this process, counted without any HIP call (the
+    launcher must not initialise the GPU before it starts the ranks): KFD
+    topology nodes with SIMDs are GPUs (CPU nodes report ``simd_count 0``),
+    limited by ROCR/HIP/CUDA_VISIBLE_DEVICES.  None when the topology is
+    unreadable."""
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(root, d, "properties")) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def _launch_ranks(args) -> int:
     """``bench.py --gpus N`` without a launcher: check that N devices are
     visible (counting them does not initialise the GPU), then run this
@@ -858,8 +886,11 @@ def _launch_ranks(args) -> int:
 
     rehearse = os.environ.get("PILOSA_BENCH_REHEARSE") == "1"
     if not rehearse:
-        import torch
-        visible = torch.cuda.device_count()
+        visible = kfd_gpu_count()
+        if visible is None:
+            print("bench: cannot count GPUs from the KFD topology (/sys/class/kfd); launch the ranks with "
+                  "torch.distributed.run yourself", file=sys.stderr, flush=True)
+            return 2
         if visible < args.gpus:
             print(f"bench: --gpus {args.gpus} but {visible} GPU(s) visible", file=sys.stderr, flush=True)
             return 2
@@ -873,7 +904,7 @@ def _launch_ranks(args) -> int:
     return subprocess.call(cmd, env=dict(os.environ))
 
 
-def setup_dist():
+def setup_dist(mesh: bool = False):
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -888,7 +919,7 @@ def setup_dist():
     dev = torch.device("cuda", local_rank)
     if world > 1 and not rehearse and local_rank >= torch.cuda.device_count():
         raise SystemExit(f"bench: rank {rank} has LOCAL_RANK {local_rank} but {torch.cuda.device_count()} GPU(s)")
-    if world > 1:
+    if world > 1 or mesh:
         from pilosa_amd.parallel.collectives import Comm, init
         torch.cuda.set_device(local_rank)
         init("gloo" if rehearse else "nccl", local_rank, timeout_s=600)
@@ -1274,7 +1305,7 @@ def run_disk_mesh(args, world, rank, dev, queries, ra, rb):
         view = gpu.view_arena("i", "f", "standard", own) if own else None
         torch.cuda.synchronize(dev)
         load_s = time.perf_counter() - t1
-        mesh = ShardMesh(ex, block=block, device=dev)
+        mesh = ShardMesh(ex, block=block, device=dev, force=getattr(args, "mesh", False))
         if rank != 0:
             log(f"mesh worker: {len(own)} shards loaded in {load_s:.2f} s, serving")
             mesh.serve()
@@ -1616,6 +1647,8 @@ def main():
     ap.add_argument("--import-shards", type=int, default=64, help="serving phase: shards of the HTTP bulk import")
     ap.add_argument("--import-bits-per-shard", type=int, default=200_000)
     ap.add_argument("--import-clients", type=int, default=8)
+    ap.add_argument("--mesh", action="store_true",
+                    help="run the multi-GPU product path (ShardMesh over RCCL, one rank per GPU) even at --gpus 1")
     ap.add_argument("--cpu-baseline-shards", type=int, default=0,
                     help="also time the host C++ roaring executor on this many shards (extrapolated)")
     args = ap.parse_args()
@@ -1623,7 +1656,7 @@ def main():
     if args.gpus < 1:
         raise SystemExit("bench: --gpus must be >= 1")
     env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and args.gpus > 1:
+    if env_world is None and (args.gpus > 1 or args.mesh):
         # launched without a launcher: start one rank per GPU ourselves
         # (nothing here has touched the GPU: no exec from a GPU process)
         raise SystemExit(_launch_ranks(args))
@@ -1634,7 +1667,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world, rank, dev = setup_dist()
+    world, rank, dev = setup_dist(mesh=args.mesh)
     if args.clients <= 0:
         args.clients = 2 if world == 1 else 4
     rng = np.random.default_rng(1234)
@@ -1658,10 +1691,10 @@ def main():
             fallback = (f"--mode disk needs ~{need / 1e9:.1f} GB per rank under TMPDIR, a rank had "
                         f"{free / 1e9:.1f} GB free: timed the synthesised arena instead")
             args.mode = "synthetic"
-    mesh_mode = args.mode == "disk" and world > 1
+    mesh_mode = args.mode == "disk" and (world > 1 or args.mesh)
     run = run_disk_mesh if mesh_mode else run_disk if args.mode == "disk" else run_synthetic
     elapsed, extra = run(args, world, rank, dev, queries, ra, rb)
-    if world > 1:
+    if world > 1 or args.mesh:
         extra.update({"backend": dist.get_backend(), "world_size": dist.get_world_size()})
     if fallback:
         extra["mode_fallback"] = fallback
@@ -1703,7 +1736,7 @@ def main():
                "verified": extra.get("verify", {}).get("verified_all_ranks"),
                "mode": args.mode, "extra": extra}
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

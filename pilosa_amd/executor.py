@@ -405,10 +405,11 @@ class Executor:
                 not self._has_remote(index, shards, opt) and not any("ids" in c.args for c in q.calls):
             for c in q.calls:
                 self._validate_call_args(c)
+            mesh = self.mesh
             try:
-                res = self.mesh.topn_batch(index, q.calls, shards)
+                res = mesh.topn_batch(index, q.calls, shards)
             except MeshError:
-                if not self.mesh.failed_over:
+                if not mesh.failed_over:   # (failover detaches self.mesh)
                     raise
                 res = None
             if res is not None:
@@ -652,7 +653,9 @@ class Executor:
         return pool
 
     def _use_mesh(self, opt) -> bool:
-        return self.mesh is not None and self.mesh.world > 1 and not getattr(opt, "mesh_local", False)
+        mesh = self.mesh
+        return mesh is not None and (mesh.world > 1 or getattr(mesh, "always", False)) and \
+            not getattr(opt, "mesh_local", False)
 
     def _shards_by_node(self, index, shards, opt) -> Dict[Any, List[int]]:
         if self.cluster is None or opt.remote:

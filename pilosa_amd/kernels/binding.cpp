@@ -265,6 +265,47 @@ void topn_cache_batch(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch:
   check_launch("topn_cache_batch");
 }
 
+// A mesh rank's cache-only partial: ``buf`` int32[(Q*U + 3) / 4 + T*U] holds
+// the membership bytes (uint8[Q, U], padded to whole words) then the int32
+// partial totals [T, U]; the ranks all-reduce (sum) it as one tensor.
+void topn_cache_partial(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch::Tensor cm, torch::Tensor prm,
+                        int64_t Q, int64_t T, int64_t U, torch::Tensor buf) {
+  for (auto* t : {&cnt, &inv, &cm, &prm, &buf}) check_dev(*t, "topn_cache_partial");
+  TORCH_CHECK(cnt.scalar_type() == torch::kInt32 && cnt.dim() == 2, "cnt int32[S, K]");
+  const int64_t S = cnt.size(0), K = cnt.size(1);
+  TORCH_CHECK(nmax >= 0 && nmax <= K, "nmax out of range");
+  TORCH_CHECK(inv.scalar_type() == torch::kInt32 && inv.numel() == S * nmax, "inv int32[S * nmax]");
+  TORCH_CHECK(cm.scalar_type() == torch::kInt32 && cm.numel() == U * S, "cm int32[U, S]");
+  TORCH_CHECK(prm.scalar_type() == torch::kInt32 && prm.numel() == 4 * Q + T, "prm int32[4Q + T]");
+  const int64_t mw = (Q * U + 3) / 4;
+  TORCH_CHECK(buf.scalar_type() == torch::kInt32 && buf.numel() == mw + T * U, "buf int32[member words + T*U]");
+  TORCH_CHECK(Q < 65536 && T > 0 && U > 0 && U < (int64_t(1) << 31), "topn_cache_partial sizes");
+  int32_t* b = buf.data_ptr<int32_t>();
+  pk::launch_topn_cache_partial(cnt.data_ptr<int32_t>(), int(K), int(S), int(nmax), inv.data_ptr<int32_t>(),
+                                cm.data_ptr<int32_t>(), prm.data_ptr<int32_t>(), int(Q), int(T), int(U),
+                                reinterpret_cast<uint8_t*>(b), b + mw, cur_stream(buf));
+  check_launch("topn_cache_partial");
+}
+
+// Per-query top-n over the all-reduced partial buffer (member bytes > 0 =
+// a candidate of that query on some rank; node totals int32).
+void topn_cache_select32(torch::Tensor buf, torch::Tensor ids, torch::Tensor prm, int64_t Q, int64_t T,
+                         torch::Tensor out) {
+  for (auto* t : {&buf, &ids, &prm, &out}) check_dev(*t, "topn_cache_select32");
+  const int64_t U = ids.numel();
+  const int64_t mw = (Q * U + 3) / 4;
+  TORCH_CHECK(ids.scalar_type() == torch::kInt32, "ids int32[U]");
+  TORCH_CHECK(buf.scalar_type() == torch::kInt32 && buf.numel() == mw + T * U, "buf int32[member words + T*U]");
+  TORCH_CHECK(prm.scalar_type() == torch::kInt32 && prm.numel() == 4 * Q + T, "prm int32[4Q + T]");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.dim() == 2 && out.size(0) == Q, "out int64[Q, KK+1]");
+  TORCH_CHECK(Q < 65536 && U > 0 && U < (int64_t(1) << 31), "topn_cache_select32 sizes");
+  const int32_t* b = buf.data_ptr<int32_t>();
+  pk::launch_topn_cache_select32(reinterpret_cast<const uint8_t*>(b), b + mw, ids.data_ptr<int32_t>(),
+                                 prm.data_ptr<int32_t>(), int(Q), int(U), int(out.size(1) - 1),
+                                 reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(buf));
+  check_launch("topn_cache_select32");
+}
+
 void row_counts_sum(torch::Tensor view, int64_t S, torch::Tensor dense, torch::Tensor threshold, torch::Tensor out) {
   for (auto* t : {&dense, &threshold, &out}) check_dev(*t, "row_counts_sum");
   const int64_t P = dense.numel();
@@ -448,7 +489,7 @@ void expr_dense(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
 }
 
 void shift_dense(torch::Tensor src, int64_t S, int64_t n, torch::Tensor main_out, torch::Tensor main_meta,
-                 torch::Tensor spill_out, torch::Tensor spill_meta) {
+                 torch::Tensor spill_out, torch::Tensor spill_meta, int64_t M) {
   for (auto* t : {&src, &main_out, &spill_out}) {
     check_dev(*t, "shift payload");
     TORCH_CHECK(t->scalar_type() == torch::kInt16 && t->numel() == S * 16 * 4096, "shift payload int16[S*16*4096]");
@@ -457,9 +498,10 @@ void shift_dense(torch::Tensor src, int64_t S, int64_t n, torch::Tensor main_out
     check_dev(*t, "shift meta");
     TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == S * 16, "shift meta int64[S*16]");
   }
-  TORCH_CHECK(n > 0 && n < (int64_t(1) << 20), "shift needs 0 < n < 2^20");
+  TORCH_CHECK(M >= 1 && S % M == 0, "shift: S must be a whole number of M-sub-shard shards");
+  TORCH_CHECK(n > 0 && n < (M << 20), "shift needs 0 < n < the shard width (M * 2^20)");
   auto u64 = [](torch::Tensor& t) { return reinterpret_cast<uint64_t*>(t.data_ptr<int16_t>()); };
-  pk::launch_shift_dense(u64(src), int(S), n, u64(main_out), main_meta.data_ptr<int64_t>(), u64(spill_out),
+  pk::launch_shift_dense(u64(src), int(S), int(M), n, u64(main_out), main_meta.data_ptr<int64_t>(), u64(spill_out),
                          spill_meta.data_ptr<int64_t>(), cur_stream(src));
   check_launch("shift_dense");
 }
@@ -553,6 +595,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_counts", &row_counts, "row counts of (shard, dense row) entries (device rank caches)");
   m.def("topn_cache_counts", &topn_cache_counts, "cache-only TopN: [candidate x shard] row counts");
   m.def("topn_cache_batch", &topn_cache_batch, "cache-only TopN batch: membership, totals, per-query top-n");
+  m.def("topn_cache_partial", &topn_cache_partial, "mesh cache-only TopN: one rank's membership + partial totals");
+  m.def("topn_cache_select32", &topn_cache_select32, "mesh cache-only TopN: per-query top-n of the reduced buffer");
   m.def("row_counts_sum", &row_counts_sum, "ids= re-count without src: per id the sum of shard row counts >= threshold");
   m.def("keymask_build", &keymask_build, "key-presence mask of every (shard, row) of a view");
   m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");
@@ -560,7 +604,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
   m.def("bitgemm", &bitgemm, "row-pair intersection count matrix of dense bit rows (mode 1 MFMA i8, 0 VALU)");
   m.def("expr_dense", &expr_dense, "evaluate expressions into dense one-row views (bitmap per shard/key)");
-  m.def("shift_dense", &shift_dense, "Shift a dense view by n columns per shard (main + next-shard spill)");
+  m.def("shift_dense", &shift_dense, "Shift a dense view by n columns per shard (main + next-shard spill)",
+        py::arg("src"), py::arg("S"), py::arg("n"), py::arg("main_out"), py::arg("main_meta"), py::arg("spill_out"),
+        py::arg("spill_meta"), py::arg("M") = 1);
   m.def("rows_list", &rows_list, "flag dense rows with non-empty containers (optionally holding one column)");
   m.def("container_merge", &container_merge, "device write path: old container + delta -> bitmap + cardinality");
   m.def("payload_compact", &payload_compact, "copy live containers into a compacted payload buffer");

@@ -134,6 +134,11 @@ void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, 
 void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
                              const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
                              long long* tot, long long* out, hipStream_t st);
+void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* cm,
+                               const int32_t* prm, int Q, int T, int U, uint8_t* member, int32_t* tot,
+                               hipStream_t st);
+void launch_topn_cache_select32(const uint8_t* member, const int32_t* tot, const int32_t* ids, const int32_t* prm,
+                                int Q, int U, int KK, long long* out, hipStream_t st);
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st);
 
@@ -152,7 +157,7 @@ void launch_expr_dense(const QueryProg* progs, int Q, const ViewDev* views, int 
 // Shift a dense view (u64[S][16384]) up by n (0 < n < 2^20) columns per shard:
 // main_out = bits that stay in the shard, spill_out = bits carried into the
 // next shard (both dense, with metadata like launch_expr_dense).
-void launch_shift_dense(const uint64_t* src, int S, int64_t n, uint64_t* main_out, int64_t* main_meta,
+void launch_shift_dense(const uint64_t* src, int S, int M, int64_t n, uint64_t* main_out, int64_t* main_meta,
                         uint64_t* spill_out, int64_t* spill_meta, hipStream_t st);
 // Rows listing: flags[d] = 1 for dense rows with a non-empty container in
 // shards [s0, s0 + ns) (j >= 0: only rows whose key-j container holds col16).

@@ -500,7 +500,11 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // switches to a new A that is an array of <= 512 values (41.6M of the 58.6M
 // pairs of the headline batch are array x array), so staging it waits on no
 // global load.  Measured 17.7 vs 16.7 ms (profiles/r04_f/): not the default.
-template <int CQ, bool APF = false>
+// DBG (cost attribution only, wrong answers): 1 = control
+// skeleton (pair table, metas, B-head prefetch, readlanes, wave_sum; no
+// staging, no counting), 2 = no wave_sum, 3 = no staging, 4 = no counting,
+// 5 = skeleton without the B-head loads
+template <int CQ, bool APF = false, int DBG = 0>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -562,7 +566,10 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       const uint4 head = pre;
       const uint4 ahead = apre;
       const bool aok = apre_ok;
-      if (j >= 0) pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j));
+      if (DBG == 5)
+        pre = make_uint4(uint32_t(j), 0, 0, 0);
+      else if (j >= 0)
+        pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j));
       if (APF) {
         apre_ok = false;
         if (j >= 0 && !(__builtin_amdgcn_readlane(ea, j) == a && __builtin_amdgcn_readlane(vai, j) == va) &&
@@ -572,8 +579,35 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
         }
       }
       int c;
-      if (a == cached && va == cached_v) {
-        c = count_vs_head<true>(lb, pB, mB, head);
+      if (DBG == 1 || DBG == 5) {
+        c = int(head.x & 1u) + int(tA == tB);
+      } else if (a == cached && va == cached_v) {
+        c = DBG == 4 ? int(head.x & 1u) : count_vs_head<true>(lb, pB, mB, head);
+      } else if (DBG == 3 || DBG == 4) {
+        // staging skipped (3: count against whatever lb holds) or counting
+        // skipped (4: stage only), with v6's branch structure
+        const bool next_same = j >= 0 && __builtin_amdgcn_readlane(ea, j) == a &&
+                               __builtin_amdgcn_readlane(vai, j) == va;
+        if (DBG == 4 && !(!next_same && tA == CT_BITMAP && tB == CT_BITMAP) &&
+            !(!next_same && tA == CT_ARRAY && tB == CT_BITMAP && meta_n(mA) <= SMALL_ARRAY_N)) {
+          lds_wait();
+          if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
+            stage(lb, pB, mB);
+            cached = NONE;
+            cached_v = -1;
+          } else {
+            stage(lb, pA, mA);
+            cached = a;
+            cached_v = va;
+          }
+          c = int(head.x & 1u);
+        } else if (DBG == 4) {
+          c = int(head.x & 1u);
+        } else {
+          cached = a;
+          cached_v = va;
+          c = count_vs_head<true>(lb, pB, mB, head);
+        }
       } else {
         const bool next_same = j >= 0 && __builtin_amdgcn_readlane(ea, j) == a &&
                                __builtin_amdgcn_readlane(vai, j) == va;
@@ -598,8 +632,12 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
           c = count_vs_head<true>(lb, pB, mB, head);
         }
       }
-      c = wave_sum(c);
-      if (lane == i) mine = c;
+      if (DBG == 2) {
+        mine += c;
+      } else {
+        c = wave_sum(c);
+        if (lane == i) mine = c;
+      }
       if (j < 0) break;
       i = j;
       todo &= todo - 1;
@@ -816,6 +854,18 @@ void launch_v10_dbg(int dbg, int64_t wv, const QueryProg* progs, int Q, const Vi
   }
 }
 
+template <int CQ>
+void launch_v6_dbg(int dbg, int64_t wv, const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs,
+                   int32_t* partial, hipStream_t st) {
+  switch (dbg) {
+    case 1: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 1>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 2: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 2>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 3: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 3>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 4: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 4>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    default: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 5>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+  }
+}
+
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st) {
   const int64_t n = int64_t(S) * v.D;
   if (n == 0) return;
@@ -848,6 +898,8 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                          S, pairs, partial);                                                                 \
     else if (variant >= 21 && variant <= 24)                                                                 \
       launch_v10_dbg<CQV>(variant - 20, wv, progs, Q, views, S, pairs, partial, st);                         \
+    else if (variant >= 31 && variant <= 35)                                                                 \
+      launch_v6_dbg<CQV>(variant - 30, wv, progs, Q, views, S, pairs, partial, st);                          \
     else if (variant == 13)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q,    \
                          views, S, pairs, partial);                                                          \

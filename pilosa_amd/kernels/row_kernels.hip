@@ -8,6 +8,8 @@
 // a dense one-row view (expr_dense_kernel: one 8 KiB bitmap per (shard, key),
 // i.e. 16384 words per shard), then one pass moves every word: target word T
 // takes source words T - n/64 and T - n/64 - 1, funnel-shifted by n % 64.
+// A shard wider than 2^20 columns is M consecutive device sub-shards whose
+// words form one row, so carries cross sub-shard boundaries in that pass.
 // Targets past the shard's last column form the "spill" view: the bits a
 // per-shard evaluation carries into the next shard's segment (row.go keeps
 // them in the shard's segment; Row.Merge folds them into shard s + 1).  One
@@ -30,7 +32,13 @@ namespace {
 
 constexpr int SHARD_WORDS = 16 * 1024;
 
-__global__ __launch_bounds__(256) void shift_dense_kernel(const uint64_t* __restrict__ src, int S, int64_t n,
+// M = device sub-shards per shard (shards wider than 2^20 columns,
+// pilosa_amd/shardwidth.py): the M sub-shards of a shard are consecutive in
+// the view and form one M * 16384-word row, so a word carried past a
+// sub-shard's end lands in the next sub-shard of the same shard; only words
+// carried past the SHARD's end form the spill, whose sub-shard m part
+// belongs to sub-shard m of the next shard.  M = 1 at widths <= 2^20.
+__global__ __launch_bounds__(256) void shift_dense_kernel(const uint64_t* __restrict__ src, int S, int M, int64_t n,
                                                           uint64_t* __restrict__ main_out,
                                                           int64_t* __restrict__ main_meta,
                                                           uint64_t* __restrict__ spill_out,
@@ -43,17 +51,22 @@ __global__ __launch_bounds__(256) void shift_dense_kernel(const uint64_t* __rest
   const int k = int(item & 15);
   const int64_t nw = n >> 6;
   const int sh = int(n & 63);
-  const uint64_t* sp = src + int64_t(s) * SHARD_WORDS;
+  const int m = s % M;
+  const int64_t row_words = int64_t(M) * SHARD_WORDS;            // the whole shard's row
+  const uint64_t* sp = src + int64_t(s - m) * SHARD_WORDS;        // its first sub-shard
   uint64_t* dst = (half ? spill_out : main_out) + int64_t(s) * SHARD_WORDS + k * 1024;
+  // target word t of this wave, counted from the shard's first word (the
+  // spill continues past the shard's end)
+  const int64_t t0 = int64_t(half) * row_words + int64_t(m) * SHARD_WORDS + k * 1024;
   int c = 0;
 #pragma unroll 4
   for (int i = 0; i < 16; i++) {
     const int w = i * 64 + lane;
-    const int64_t a = int64_t(half) * SHARD_WORDS + k * 1024 + w - nw;
-    const uint64_t x = (a >= 0 && a < SHARD_WORDS) ? sp[a] : 0ull;
+    const int64_t a = t0 + w - nw;
+    const uint64_t x = (a >= 0 && a < row_words) ? sp[a] : 0ull;
     uint64_t r = x;
     if (sh) {
-      const uint64_t y = (a - 1 >= 0 && a - 1 < SHARD_WORDS) ? sp[a - 1] : 0ull;
+      const uint64_t y = (a - 1 >= 0 && a - 1 < row_words) ? sp[a - 1] : 0ull;
       r = (x << sh) | (y >> (64 - sh));
     }
     dst[w] = r;
@@ -120,11 +133,11 @@ __global__ __launch_bounds__(256) void rows_kernel(ViewDev v, int s0, int ns, in
 
 }  // namespace
 
-void launch_shift_dense(const uint64_t* src, int S, int64_t n, uint64_t* main_out, int64_t* main_meta,
+void launch_shift_dense(const uint64_t* src, int S, int M, int64_t n, uint64_t* main_out, int64_t* main_meta,
                         uint64_t* spill_out, int64_t* spill_meta, hipStream_t st) {
   const int64_t waves = int64_t(S) * 32;
-  if (waves == 0) return;
-  hipLaunchKernelGGL(shift_dense_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, src, S, n, main_out,
+  if (waves == 0 || M <= 0 || S % M) return;
+  hipLaunchKernelGGL(shift_dense_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, src, S, M, n, main_out,
                      main_meta, spill_out, spill_meta);
 }
 

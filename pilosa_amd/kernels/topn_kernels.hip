@@ -1142,10 +1142,13 @@ __global__ __launch_bounds__(256) void topn_cache_member_kernel(const int32_t* _
 }
 
 // tot[t*U + j] = sum over shards of cm[j*S + s] where it reaches th[t]; one
-// wave per (threshold, candidate), coalesced over the shard axis
+// wave per (threshold, candidate), coalesced over the shard axis.  TT = long
+// long on one rank; int on a mesh rank, whose partial totals travel in the
+// batch's one int32 all-reduce (parallel/mesh.py OP_TOPN)
+template <class TT>
 __global__ __launch_bounds__(256) void topn_cache_totals_kernel(const int32_t* __restrict__ cm, int S, int U,
                                                                 const int32_t* __restrict__ th, int T,
-                                                                long long* __restrict__ tot) {
+                                                                TT* __restrict__ tot) {
   const int w = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
   const int lane = int(threadIdx.x & 63);
   if (w >= T * U) return;
@@ -1159,11 +1162,12 @@ __global__ __launch_bounds__(256) void topn_cache_totals_kernel(const int32_t* _
     acc += n >= m ? n : 0;
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  if (lane == 0) tot[w] = acc;
+  if (lane == 0) tot[w] = TT(acc);
 }
 
+template <class TT>
 __global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* __restrict__ member,
-                                                                const long long* __restrict__ tot,
+                                                                const TT* __restrict__ tot,
                                                                 const int32_t* __restrict__ u,
                                                                 const int32_t* __restrict__ prm, int Q, int U, int KK,
                                                                 long long* __restrict__ out) {
@@ -1174,11 +1178,11 @@ __global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* _
   if (tid == 0) nmem = 0;
   __syncthreads();
   const uint8_t* mq = member + int64_t(q) * U;
-  const long long* tq = tot + int64_t(prm[2 * Q + q]) * U;
+  const TT* tq = tot + int64_t(prm[2 * Q + q]) * U;
   for (int j = tid; j < U; j += 256) {
     if (!mq[j]) continue;
     const int32_t d = u[j];
-    const long long sc = tq[j];
+    const long long sc = (long long)tq[j];
     if (d < 0 || sc <= 0) continue;
     const int p = atomicAdd(&nmem, 1);
     if (p < TC_CAP) keys[p] = (sc << 32) | (0xFFFFFFFFll - d);
@@ -1235,9 +1239,37 @@ void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const i
                        member);
   }
   const int64_t waves = int64_t(T) * U;
-  hipLaunchKernelGGL(topn_cache_totals_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm, S, U,
-                     prm + 4 * Q, T, tot);
-  hipLaunchKernelGGL(topn_cache_select_kernel, dim3(Q), dim3(256), 0, st, member, tot, u, prm, Q, U, KK, out);
+  hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm, S,
+                     U, prm + 4 * Q, T, tot);
+  hipLaunchKernelGGL(topn_cache_select_kernel<long long>, dim3(Q), dim3(256), 0, st, member, tot, u, prm, Q, U, KK,
+                     out);
+}
+
+// A mesh rank's share of a cache-only batch over the NODE candidate space:
+// membership bytes and int32 partial totals, side by side in the buffer the
+// ranks all-reduce (member as bytes: a sum over < 256 ranks cannot carry into
+// the next byte).  The select runs after the all-reduce, on the front end.
+void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* cm,
+                               const int32_t* prm, int Q, int T, int U, uint8_t* member, int32_t* tot,
+                               hipStream_t st) {
+  if (Q <= 0 || U <= 0) return;
+  const int64_t N = int64_t(S) * nmax;
+  if (N > 0) {
+    const int64_t want = (N + 255) / 256;
+    const int bx = int(want < 1024 ? want : 1024);
+    hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
+                       member);
+  }
+  const int64_t waves = int64_t(T) * U;
+  if (S > 0)
+    hipLaunchKernelGGL(topn_cache_totals_kernel<int>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm, S, U,
+                       prm + 4 * Q, T, tot);
+}
+
+void launch_topn_cache_select32(const uint8_t* member, const int32_t* tot, const int32_t* ids, const int32_t* prm,
+                                int Q, int U, int KK, long long* out, hipStream_t st) {
+  if (Q <= 0 || U <= 0) return;
+  hipLaunchKernelGGL(topn_cache_select_kernel<int>, dim3(Q), dim3(256), 0, st, member, tot, ids, prm, Q, U, KK, out);
 }
 
 }  // namespace pk

@@ -134,6 +134,12 @@ def _dev_storage(f):
     return f.device_storage() if isinstance(f, SubFragment) else f.storage
 
 
+def _nreq(ns) -> int:
+    """The cache prefix a cache-only group needs: its largest n (0 = all)."""
+    ns = [int(n) for n in ns]
+    return 0 if any(n == 0 for n in ns) else max(ns)
+
+
 class GpuExecutor:
     def __init__(self, holder, device="cuda:0", executor=None, hbm_budget: int = 0):
         if not shardwidth.device_supported():
@@ -172,6 +178,10 @@ class GpuExecutor:
         # their candidates / re-counts node-wide (every rank runs the same calls)
         self.comm = None
         self._spaces: Dict[Tuple, Tuple] = {}
+        # (index, field, shards, nreq) -> (rank-cache serial, NodeCandidates or None):
+        # node candidate spaces of mesh cache-only batches (refreshed collectively)
+        self._cand_spaces: Dict[Tuple, Tuple] = {}
+        self.topn_mesh_fused = 0        # mesh cache-only groups answered in one all-reduce
         self._frag_lists: Dict[Tuple, Tuple] = {}   # (index, field, shards) -> (epoch, fragments)
         self.topn_decline = ""          # why the last topn_batch returned None (diagnostics)
         self._topn_index_why = ""
@@ -1073,7 +1083,17 @@ class GpuExecutor:
             space = self._node_space((index, fname, tuple(shards)), rv)
             if nosrc:
                 self.launches += 1
-                got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space, defer=defer)
+                cand = None
+                if self.comm is not None:
+                    ent = self._cand_spaces.get((index, fname, tuple(shards), _nreq(ns)))
+                    # node-consistent: every rank refreshed in the same vote, and
+                    # the entry's fit check used node-wide sizes
+                    cand = ent[1] if ent is not None and ent[0] == rc.serial else None
+                if cand is not None:
+                    self.topn_mesh_fused += 1
+                    got = rc.topn_nosrc_mesh(ns, ths, self.comm, cand, defer=defer)
+                else:
+                    got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space, defer=defer)
             else:
                 tix = self._topn_index(index, fname, shards, rc, rv, space=space)
                 if tix is None:
@@ -1297,6 +1317,65 @@ class GpuExecutor:
             space = np.unique(np.concatenate([p.cpu().numpy().view(np.uint64) for p in parts])) if parts else rows
             sig = (id(rv), rv.rows_gen) if rv is not None else None
             self._spaces[key] = (sig, space)
+
+    def _cand_groups(self, index: str, calls: List[Call]) -> List[Tuple[str, int]]:
+        """(field, nreq) of the batch's cache-only groups, sorted (the same
+        on every rank: derived from the command text)."""
+        ex = self._ex()
+        ns: Dict[str, List[int]] = {}
+        for c in calls:
+            if c.children:
+                continue
+            fname, n = ex.topn_params(index, c)[:2]
+            ns.setdefault(fname, []).append(int(n))
+        return sorted((f, _nreq(v)) for f, v in ns.items())
+
+    def topn_cand_stale(self, index: str, calls: List[Call], shards: List[int]) -> bool:
+        """Does this rank miss the node candidate space of a cache-only group
+        of the batch (never built, or built from rank caches since replaced)?
+        Local check; the mesh votes on it (parallel/mesh.py OP_TOPN)."""
+        for fname, nreq in self._cand_groups(index, calls):
+            frags = self._topn_frags(index, fname, shards)
+            rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+            rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+            ent = self._cand_spaces.get((index, fname, tuple(shards), nreq))
+            if rc is None or ent is None or ent[0] != rc.serial:
+                return True
+        return False
+
+    def refresh_cand_spaces(self, index: str, calls: List[Call], shards: List[int], comm) -> None:
+        """Collective on every rank, groups in the same order: all-gather each
+        rank's local candidate rows of a cache-only group (with its fragment
+        and device-shard counts) and keep, per group, the node candidate space
+        and this rank's tensors over it (DeviceRankCaches.node_candidates).
+        The fused one-all-reduce path is enabled only when it fits on every
+        rank (int32 node totals, the count-matrix cap): a node-wide decision."""
+        import torch
+
+        from .topn_exec import FUSED_MAX_CELLS
+        for fname, nreq in self._cand_groups(index, calls):
+            rc = None
+            rows = np.zeros(0, np.uint64)
+            try:
+                frags = self._topn_frags(index, fname, shards)
+                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+                rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+                if rc is not None:
+                    rows = rc.local_candidate_rows(nreq)
+            except Exception:  # noqa: BLE001 - take part with nothing; the fit check fails below
+                rc = None
+            head = np.array([rc.S if rc is not None else -1, rc.view.S if rc is not None else 0], np.int64)
+            t = torch.from_numpy(np.concatenate([head, rows.view(np.int64)])).to(comm.device)
+            parts = [p.cpu().numpy() for p in comm.all_gather_var(t)]
+            space = np.unique(np.concatenate([p[2:].view(np.uint64) for p in parts])) if parts else rows
+            s_frag = [int(p[0]) for p in parts]
+            fits = min(s_frag) >= 0 and len(space) * max(s_frag) <= FUSED_MAX_CELLS and \
+                sum(int(p[1]) for p in parts) < 2048 and len(space) > 0
+            key = (index, fname, tuple(shards), nreq)
+            if rc is None:
+                self._cand_spaces.pop(key, None)
+                continue
+            self._cand_spaces[key] = (rc.serial, rc.node_candidates(nreq, space) if fits else None)
 
     def _topn_index(self, index: str, fname: str, shards: List[int], rc, rv, space=None):
         """Device slot index (ops/topn_index.py) over the rank caches ``rc``,

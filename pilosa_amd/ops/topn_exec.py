@@ -28,6 +28,7 @@ candidate x shard count matrix, and a per-query LDS bitonic top-n.
 """
 from __future__ import annotations
 
+import itertools
 import os
 import threading
 from typing import List, Optional, Sequence
@@ -124,6 +125,37 @@ def dense_dev(view: DeviceView, ids):
     return torch.where(rows[i] == ids, i, torch.full_like(i, -1)).to(torch.int32)
 
 
+_RC_SERIAL = itertools.count(1)
+
+
+class NodeCandidates:
+    """One rank's view of a node candidate space (mesh cache-only TopN):
+    ``space`` the sorted node-wide candidate row ids, ``nmax`` the local
+    cache prefix, ``inv`` int32[S * nmax] the node index of each local rank
+    slot, ``cm`` int32[U, S] each candidate's count per local fragment,
+    ``ids`` arange(U) (the select kernel's tie-break ids)."""
+
+    __slots__ = ("space", "nmax", "inv", "cm", "ids")
+
+    def __init__(self, space, nmax, inv, cm, ids):
+        self.space, self.nmax, self.inv, self.cm, self.ids = space, int(nmax), inv, cm, ids
+
+
+def _select_from_buffer(buf, Q: int, T: int, U: int, q: int, t: int, lim: int) -> np.ndarray:
+    """Query q's top composite keys (count << 32 | ~index) from an all-reduced
+    partial buffer, with torch (the select kernel's LDS overflow case)."""
+    import torch
+    mw = (Q * U + 3) // 4
+    member = buf[:mw].view(torch.uint8)[q * U:(q + 1) * U]
+    tot = buf[mw + t * U:mw + (t + 1) * U].to(torch.int64)
+    idx = torch.arange(U, device=buf.device, dtype=torch.int64)
+    key = torch.where((member > 0) & (tot > 0), (tot << 32) | (0xFFFFFFFF - idx), torch.full_like(tot, -1))
+    k = min(int(lim), U)
+    top = torch.topk(key, k).values if k else key[:0]
+    h = top.cpu().numpy()
+    return h[h >= 0]
+
+
 class DeviceRankCaches:
     """Ranked caches of every local shard of one view, on the device.
 
@@ -138,6 +170,7 @@ class DeviceRankCaches:
         from pilosa_amd import _roaring
         self.view = view
         self.generation = view.generation
+        self.serial = next(_RC_SERIAL)   # identity of this ranking (mesh candidate spaces key on it)
         # one rank cache per fragment; a fragment wider than 2^20 columns is
         # M device sub-shards of the arena (pilosa_amd/shardwidth.py), whose
         # row counts are summed per fragment
@@ -358,7 +391,7 @@ class DeviceRankCaches:
         sp = torch.from_numpy(np.ascontiguousarray(space, dtype=np.uint64).view(np.int64)).to(dev)
         A = max(int(sp.numel()), 1)
         acc = torch.searchsorted(sp, rows_dev(self.view)[pd]) if pd.numel() else pd
-        keys = comm.union(pq * A + acc)
+        keys = comm.union(pq * A + acc, tag="topn_nosrc")
         pq, pa = keys // A, keys % A
         local = dense_dev(self.view, sp[pa]) if pa.numel() else pa.to(torch.int32)
         out = self.recount(pq, local.clamp(min=-1), thresholds)
@@ -401,6 +434,101 @@ class DeviceRankCaches:
                     torch.cuda.current_stream(self.view.device).synchronize()
             memo[nmax] = got
         return got
+
+    # ------------------------------------------------------------ mesh (node-wide) cache-only batches
+    def local_nmax(self, nreq: int) -> int:
+        """This rank's cache prefix for a batch whose largest n is ``nreq``
+        (0: some call takes every cached row)."""
+        return self.K if nreq == 0 else min(self.K, int(nreq))
+
+    def local_candidate_rows(self, nreq: int) -> np.ndarray:
+        """Sorted row ids of every row in the first local_nmax(nreq) ranks of
+        any local shard: this rank's share of the node candidate space."""
+        nmax = self.local_nmax(nreq)
+        if not nmax or not self.S:
+            return np.zeros(0, np.uint64)
+        u, _ = self._candidates(nmax)
+        d = u[u >= 0].cpu().numpy().astype(np.int64)
+        return np.asarray(self.view.rows[d], dtype=np.uint64) if len(d) else np.zeros(0, np.uint64)
+
+    def node_candidates(self, nreq: int, space: np.ndarray) -> "NodeCandidates":
+        """The local tensors of a mesh cache-only batch over the node
+        candidate space ``space`` (sorted union of every rank's
+        local_candidate_rows(nmax), identical on all ranks): each local rank
+        slot's node index and each node candidate's count per local fragment
+        (0 where this rank does not hold the row)."""
+        import torch
+        dev = self.view.device
+        U = len(space)
+        nmax = self.local_nmax(nreq)
+        if not nmax or not self.S:
+            return NodeCandidates(space, 0, torch.zeros(0, dtype=torch.int32, device=dev),
+                                  torch.zeros((U, self.S), dtype=torch.int32, device=dev),
+                                  torch.arange(U, dtype=torch.int32, device=dev))
+        u, inv = self._candidates(nmax)
+        u_h = u.cpu().numpy().astype(np.int64)
+        present = u_h >= 0
+        node_of_u = np.zeros(len(u_h), np.int64)
+        if present.any():
+            node_of_u[present] = np.searchsorted(space, self.view.rows[u_h[present]])
+        inv_node = torch.from_numpy(node_of_u).to(dev)[inv].to(torch.int32).contiguous()
+        cm = torch.zeros((U, self.S), dtype=torch.int32, device=dev)
+        if present.any() and self.S:
+            loc = self._count_matrix(torch.from_numpy(u_h[present].astype(np.int32)).to(dev))
+            cm[torch.from_numpy(node_of_u[present]).to(dev)] = loc
+        return NodeCandidates(space, nmax, inv_node, cm, torch.arange(U, dtype=torch.int32, device=dev))
+
+    def topn_nosrc_mesh(self, ns: Sequence[int], thresholds: Sequence[int], comm, cand: "NodeCandidates",
+                        defer: bool = False):
+        """Cache-only TopN batch across the ranks of a node in ONE collective:
+        every rank writes its membership bytes and int32 partial totals over
+        the node candidate space into one buffer (topn_cache_partial), the
+        ranks all-reduce it, and the front end runs the per-query LDS top-n
+        on the sum (topn_cache_select32).  The union of the per-shard
+        candidate lists is the sum's nonzero membership, and a total summed
+        per shard where it reaches the threshold is the node's ids= re-count
+        (executor.go:863-903), so no candidate union or re-count round trip
+        is needed."""
+        import torch
+
+        from pilosa_amd.parallel.collectives import Pending
+        Q = len(ns)
+        nn = [int(n) for n in ns]
+        U = len(cand.space)
+        dev = self.view.device
+        ths = [max(1, int(t)) for t in thresholds]
+        uniq_t = sorted(set(ths))
+        T = len(uniq_t)
+        KK = min(U, max(nn)) if all(nn) else U
+        prm = np.empty(4 * Q + T, np.int32)
+        prm[:Q] = [n if n else self.K for n in nn]
+        prm[Q:2 * Q] = ths
+        prm[2 * Q:3 * Q] = [uniq_t.index(t) for t in ths]
+        prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
+        prm[4 * Q:] = uniq_t
+        prm_d = torch.from_numpy(prm).to(dev, non_blocking=False)
+        mw = (Q * U + 3) // 4
+        buf = torch.zeros(mw + T * U, dtype=torch.int32, device=dev)
+        if cand.nmax and U:
+            kernels().topn_cache_partial(self.cache_cnt, cand.nmax, cand.inv, cand.cm, prm_d, Q, T, U, buf)
+        space = cand.space
+        ids = cand.ids
+
+        def finish():
+            out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
+            kernels().topn_cache_select32(buf, ids, prm_d, Q, T, out)
+            h = out.cpu().numpy()
+            res: List[List[Pair]] = []
+            for q in range(Q):
+                if h[q, 0] < 0:     # more members than one workgroup sorts: torch over the reduced buffer
+                    r = _select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
+                else:
+                    r = h[q, 1:1 + int(h[q, 0])]
+                j = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
+                res.append(pairs_from_arrays(space[j] if len(j) else np.zeros(0, np.uint64), r >> 32))
+            return res
+        pend = Pending(comm, comm.all_reduce_async(buf), finish, keep=(buf, prm_d))
+        return pend if defer else pend.result()
 
     def _topn_nosrc_fused(self, ns: Sequence[int], thresholds: Sequence[int]) -> Optional[List[List[Pair]]]:
         """Cache-only TopN batch in three hand-written kernels

@@ -438,7 +438,7 @@ class DeviceTopNIndex:
         if comm is None:
             return nz[:, 0].contiguous(), nz[:, 1].contiguous()
         A = max(self.A, 1)
-        keys = comm.union(nz[:, 0].to(torch.int64) * A + nz[:, 1].to(torch.int64))
+        keys = comm.union(nz[:, 0].to(torch.int64) * A + nz[:, 1].to(torch.int64), tag="topn_src")
         return (keys // A).contiguous(), (keys % A).contiguous()
 
     def topn(self, engine: GpuEngine, srcs: Sequence[object], ns: Sequence[int], thresholds: Sequence[int],

@@ -35,6 +35,10 @@ import numpy as np
 from pilosa_amd.utils import tracing
 
 
+BCAST_INLINE = 4080          # command payload bytes carried in the header broadcast
+UNION_MIN_CAP = 1024         # initial per-rank pad of a speculative union gather
+
+
 class CommError(RuntimeError):
     """A collective failed or timed out; the mesh must fail over."""
 
@@ -55,8 +59,12 @@ class Comm:
         self.device = torch.device(device)
         # gloo rehearsal of a GPU run: collectives on host copies
         self.host_copies = host_copies or (backend == "gloo" and self.device.type == "cuda")
+        self.backend = backend
         self.broken: Optional[BaseException] = None
         self.calls = 0
+        self.data_calls = 0       # collectives on the data group (device tensors on RCCL)
+        self.union_retries = 0    # speculative union gathers that overflowed their pad
+        self._union_cap: dict = {}
         # command channel: a gloo group of its own, so a command broadcast is
         # never queued behind the data collectives of batches still in flight
         self.ctrl = ctrl_group
@@ -67,6 +75,8 @@ class Comm:
         if self.broken is not None:
             raise CommError(f"communicator broken: {self.broken}")
         self.calls += 1
+        if "group" in kw and (self.ctrl is None or kw["group"] is not self.ctrl):
+            self.data_calls += 1
         try:
             if tracing.enabled():
                 # one span per collective; RCCL ones are HIP-event timed (the
@@ -111,13 +121,25 @@ class Comm:
                 return self.broadcast(t, src)
             self._guard(self.dist.broadcast, t, src=src, group=self.ctrl)
             return t
-        hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+        # one fixed-size broadcast carries (op, length) and a payload of up to
+        # BCAST_INLINE bytes (every TopN batch, most calls); longer payloads
+        # (Count texts of thousands of calls) follow in a second broadcast
+        words = 2 + BCAST_INLINE // 8
         if self.rank == src:
-            hdr[0], hdr[1] = int(op), len(payload)
+            h = np.zeros(words, np.int64)
+            h[0], h[1] = int(op), len(payload)
+            if len(payload) <= BCAST_INLINE:
+                h[2:].view(np.uint8)[:len(payload)] = np.frombuffer(payload, np.uint8)
+            hdr = torch.from_numpy(h).to(dev)
+        else:
+            hdr = torch.empty(words, dtype=torch.int64, device=dev)
         bc(hdr)
-        op_, n = (int(x) for x in hdr.cpu().tolist())
+        hh = hdr.cpu().numpy()
+        op_, n = int(hh[0]), int(hh[1])
         if n == 0:
             return op_, b""
+        if n <= BCAST_INLINE:
+            return op_, hh[2:].view(np.uint8)[:n].tobytes()
         buf = torch.empty(n, dtype=torch.uint8, device=dev)
         if self.rank == src:
             buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
@@ -187,10 +209,48 @@ class Comm:
         work = self._guard(self.dist.all_gather, outs, pad, group=self.group, async_op=True)
         return Pending(self, work, lambda: [x[:k] for x, k in zip(outs, lens)], keep=(pad, outs))
 
-    def union(self, t):
-        """Sorted distinct values of ``t`` over all ranks (same on every rank)."""
-        parts = self.all_gather_var(t)
-        return self.torch.unique(self.torch.cat(parts)) if parts else t
+    def union(self, t, tag: str = "union"):
+        """Sorted distinct values of int64 ``t`` over all ranks (the same on
+        every rank).  One all-gather in the steady state: every rank sends
+        ``[count, values..., padding]`` padded to a capacity all ranks share
+        (per ``tag``), so no size exchange has to finish -- with its host
+        sync -- before the data moves.  Every rank reads every count from the
+        gather, so the ranks agree when one overflowed the pad: they then
+        re-gather at the exact size (one more collective) and raise the
+        capacity alike for the next call."""
+        torch = self.torch
+        t = t.reshape(-1).to(torch.int64)
+        n = int(t.numel())
+        cap = self._union_cap.get(tag, (UNION_MIN_CAP, 0))
+        cap, quiet = cap
+        buf = torch.empty(cap + 1, dtype=torch.int64, device=t.device)
+        buf[0] = n
+        k = min(n, cap)
+        if k:
+            buf[1:1 + k] = t[:k]
+        out = torch.empty(self.world * (cap + 1), dtype=torch.int64, device=t.device)
+        ho = self._on(out)
+        self._guard(self.dist.all_gather_into_tensor, ho, self._on(buf), group=self.group)
+        ho = ho.view(self.world, cap + 1)
+        counts = ho[:, 0].cpu().numpy()
+        mx = int(counts.max()) if len(counts) else 0
+        # capacity for the next call: grow past the largest count (with room),
+        # halve after a long quiet spell well below it; same on every rank
+        if mx > cap:
+            ncap = 1 << max(UNION_MIN_CAP.bit_length() - 1, int(mx + mx // 4).bit_length())
+            self._union_cap[tag] = (ncap, 0)
+        elif mx * 8 < cap and cap > UNION_MIN_CAP:
+            quiet += 1
+            self._union_cap[tag] = (cap // 2, 0) if quiet >= 32 else (cap, quiet)
+        else:
+            self._union_cap[tag] = (cap, 0)
+        if mx > cap:
+            self.union_retries += 1
+            parts = self.all_gather_var(t)
+            return torch.unique(torch.cat(parts)) if parts else t
+        ho = ho.to(t.device)
+        keep = torch.arange(cap, device=t.device)[None, :] < ho[:, :1]
+        return torch.unique(ho[:, 1:][keep])
 
     def gather_bytes(self, payload: bytes) -> List[bytes]:
         """Every rank's bytes, on every rank (small control-plane payloads)."""

@@ -75,7 +75,7 @@ class ShardMesh:
     """Shard-owner routing and collective reductions for one node's GPUs."""
 
     def __init__(self, executor, group=None, block: int = 1, device=None, peer_dirs: Optional[Dict[int, str]] = None,
-                 ctrl_group="auto"):
+                 ctrl_group="auto", force: bool = False):
         import collections
 
         import torch.distributed as dist
@@ -84,8 +84,11 @@ class ShardMesh:
 
         if ctrl_group == "auto":
             # every rank builds its mesh in the same order, so this collective
-            # group creation lines up; commands then travel on gloo (host)
-            ctrl_group = dist.new_group(backend="gloo") if group is None and dist.get_world_size() > 1 else None
+            # group creation lines up; commands then travel on gloo (host).  An
+            # RCCL mesh always gets one (a world-size-1 RCCL mesh too: the
+            # 1-GPU rehearsal of the node's transport, ``force``)
+            multi = dist.get_world_size() > 1 or dist.get_backend() == "nccl"
+            ctrl_group = dist.new_group(backend="gloo") if group is None and multi else None
         self.comm = Comm(group, device=device, ctrl_group=ctrl_group)
         self.torch = self.comm.torch
         self.dist = self.comm.dist
@@ -108,6 +111,10 @@ class ShardMesh:
         self._errors: Dict[int, BaseException] = {}
         self.last_count_text_errors: List[str] = []
         self.topn_tensor_batches = 0
+        # route calls through the mesh even at world size 1 (the executor
+        # otherwise answers a 1-rank node directly): runs the RCCL transport
+        # on a 1-GPU box, bench.py --mesh
+        self.always = bool(force)
 
     # ------------------------------------------------------------ ownership
     def owner(self, shard: int) -> int:
@@ -486,23 +493,25 @@ class ShardMesh:
         t = self.torch.from_numpy(encode_partial(mine)).to(self.device)
         return _Chain(self.comm.all_gather_var_async(t), lambda ps: [decode_partial(p.cpu().numpy()) for p in ps])
 
-    def _refresh_spaces(self, index: str, fnames: List[str], own: List[int]):
-        """Collective vote + refresh of the node row spaces of a TopN batch:
-        every rank reports whether its copy is stale (a write moved its own
-        view), and if ANY rank says so every rank re-gathers, field by field
-        in the same order -- the decision is never rank-local."""
+    def _refresh_spaces(self, index: str, fnames: List[str], own: List[int], vote: bool = True):
+        """Collective refresh of the node row spaces of a TopN batch: every
+        rank reports whether its copy is stale (a write moved its own view),
+        and if ANY rank says so every rank re-gathers, field by field in the
+        same order -- the decision is never rank-local.  ``vote=False``: the
+        ranks already agreed to refresh (the folded OP_TOPN vote)."""
         torch = self.torch
         gpu = self.executor.gpu
-        stale = 0
-        try:
-            if gpu is not None and hasattr(gpu, "node_space_stale"):
-                stale = int(any(gpu.node_space_stale(index, f, own) for f in fnames))
-        except Exception:  # noqa: BLE001 - a rank that cannot tell asks for a refresh
-            stale = 1
-        flag = torch.tensor([stale], dtype=torch.int64, device=self.device)
-        self.comm.all_reduce(flag)
-        if not int(flag.item()):
-            return
+        if vote:
+            stale = 0
+            try:
+                if gpu is not None and hasattr(gpu, "node_space_stale"):
+                    stale = int(any(gpu.node_space_stale(index, f, own) for f in fnames))
+            except Exception:  # noqa: BLE001 - a rank that cannot tell asks for a refresh
+                stale = 1
+            flag = torch.tensor([stale], dtype=torch.int64, device=self.device)
+            self.comm.all_reduce(flag)
+            if not int(flag.item()):
+                return
         if gpu is not None and hasattr(gpu, "refresh_node_spaces"):
             gpu.refresh_node_spaces(index, fnames, own, self.comm)
         else:
@@ -530,18 +539,47 @@ class ShardMesh:
         prev = gpu.comm if gpu is not None else None
         if gpu is not None:
             gpu.comm = self.comm
-        try:
-            if fnames:
-                self._refresh_spaces(index, fnames, own)
+
+        def ready() -> bool:
             try:
-                ok = bool(calls) and gpu is not None and ex.holder.index(index) is not None and \
+                return bool(calls) and gpu is not None and ex.holder.index(index) is not None and \
                     gpu.topn_batch_ready(index, calls, own)
             except Exception:  # noqa: BLE001 - a rank that cannot take part declines
-                ok = False
-            flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=self.device)
-            self.comm.all_reduce(flag)
-            if int(flag.item()):
+                return False
+        try:
+            # ONE all-reduce (MAX) of [space stale, decline]: the refresh vote
+            # and the readiness vote folded together.  A rank whose own copy of
+            # a node row space is stale cannot judge readiness yet (the slot
+            # index depends on the space): it votes stale only, and then every
+            # rank refreshes and votes readiness again (a second all-reduce,
+            # only after writes moved a row directory).
+            stale = 0
+            try:
+                if gpu is not None and hasattr(gpu, "node_space_stale") and fnames:
+                    stale = int(any(gpu.node_space_stale(index, f, own) for f in fnames))
+            except Exception:  # noqa: BLE001 - a rank that cannot tell asks for a refresh
+                stale = 1
+            decline = 0 if stale else (0 if ready() else 1)
+            # cache-only groups also need this rank's node candidate space
+            # (built from its current rank caches): stale = refresh them too
+            cand = 1 if stale else 0
+            if not stale and not decline and hasattr(gpu, "topn_cand_stale"):
+                try:
+                    cand = int(gpu.topn_cand_stale(index, calls, own))
+                except Exception:  # noqa: BLE001 - a rank that cannot tell asks for a refresh
+                    cand = 1
+            flag = torch.tensor([stale, decline, cand], dtype=torch.int64, device=self.device)
+            self.comm.all_reduce(flag, op=self.dist.ReduceOp.MAX)
+            voted_stale, voted_decline, voted_cand = (int(x) for x in flag.cpu().tolist())
+            if voted_stale:
+                self._refresh_spaces(index, fnames, own, vote=False)
+                flag = torch.tensor([0 if ready() else 1], dtype=torch.int64, device=self.device)
+                self.comm.all_reduce(flag, op=self.dist.ReduceOp.MAX)
+                voted_decline = int(flag.item())
+            if voted_decline:
                 return None
+            if (voted_stale or voted_cand) and hasattr(gpu, "refresh_cand_spaces"):
+                gpu.refresh_cand_spaces(index, calls, own, self.comm)
             res = gpu.topn_batch(index, calls, own, defer=True)
         finally:
             if gpu is not None:

@@ -189,3 +189,58 @@ def test_gpu_mesh_topn_distinct_row_spaces_and_writes(tmp_path):
         assert g == want_after[k % len(TOPN_QUERIES)], k
     assert res["concurrent_batches"] >= 20, res
     assert res["max_in_flight"] >= 2, res
+
+
+def test_gpu_mesh_cache_only_fused_one_collective(tmp_path):
+    """The cache-only groups of the TopN batches above ran the node-wide
+    fused path (one all-reduce of membership + partial totals per batch) on
+    both ranks; answers are checked by the two tests above."""
+    mp.start_processes(_fused_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    res = json.load(open(tmp_path / "gfused.json"))
+    assert res["fused"] >= 4, res
+    assert res["per_batch"] and max(res["per_batch"]) <= 2, res
+
+
+def _fused_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    holder = Holder(tempfile.mkdtemp(prefix=f"gfused{rank}_")).open()
+    gpu = GpuExecutor(holder, "cuda:0")
+    ex = Executor(holder, gpu=gpu)
+    gpu.executor = ex
+    ex.strict_gpu = True
+    mesh = ShardMesh(ex, block=1, device="cuda:0")
+    ex.mesh = mesh
+    try:
+        if rank != 0:
+            mesh.serve()
+            return
+        _setup_schema(holder)
+        mesh.apply_schema()
+        bits, vals = _distinct_rows_data()
+        _load(ex, bits, vals, mesh)
+        mesh.recalculate_caches()
+        shards = list(range(6))
+        ex.execute("i", "TopN(f, n=5) TopN(f, n=2, threshold=3)", shards=shards)
+        per_batch = []
+        for q in ("TopN(f, n=5) TopN(f, n=2, threshold=3)", "TopN(f, n=3)", "TopN(f)", "TopN(f, n=1) TopN(f)"):
+            ex.execute("i", q, shards=shards)   # first of each prefix length refreshes its space
+            c0 = mesh.comm.data_calls
+            ex.execute("i", q, shards=shards)
+            per_batch.append(mesh.comm.data_calls - c0)
+        with open(os.path.join(outdir, "gfused.json"), "w") as fh:
+            json.dump({"fused": gpu.topn_mesh_fused, "per_batch": per_batch}, fh)
+        mesh.stop()
+    finally:
+        ex.close()
+        holder.close()
+        dist.destroy_process_group()
