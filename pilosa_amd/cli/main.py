@@ -130,11 +130,12 @@ def cmd_server(args, stdout, stderr) -> int:
     from pilosa_amd.utils import tracing
     from pilosa_amd.utils.logger import StandardLogger
 
-    from pilosa_amd.server.config import ConfigError, validate_addrs
+    from pilosa_amd.server.config import ConfigError, validate_addrs, validate_gossip
     try:
         cfg = resolve_config(args)
         raw_adv = cfg.get("advertise")   # only an explicit advertise address overrides the listener's
         bind, adv = validate_addrs(cfg.get("bind"), raw_adv)
+        validate_gossip(cfg)
     except (ConfigError, OSError) as e:
         print(e, file=stderr)
         return 1
@@ -181,6 +182,11 @@ def cmd_server(args, stdout, stderr) -> int:
                  max_writes=cfg.get("max-writes-per-request"),
                  anti_entropy_interval=cfg.duration("anti-entropy.interval"),
                  probe_interval=cfg.duration("gossip.probe-interval"),
+                 probe_timeout=cfg.duration("gossip.probe-timeout"),
+                 suspicion_mult=float(cfg.get("gossip.suspicion-mult")),
+                 indirect_checks=int(cfg.get("gossip.nodes")),
+                 to_the_dead_time=cfg.duration("gossip.to-the-dead-time"),
+                 stream_timeout=cfg.duration("gossip.stream-timeout"),
                  gossip_interval=cfg.duration("gossip.push-pull-interval"),
                  long_query_time=cfg.duration("cluster.long-query-time"), stats=cfg.get("metric.service")
                  if cfg.get("metric.service") != "none" else "expvar", logger=logger,

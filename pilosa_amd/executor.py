@@ -24,7 +24,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 from pilosa_amd import _roaring
 from pilosa_amd.errors import (BadRequestError, ErrBSIGroupNotFound, ErrFieldNotFound, ErrIndexNotFound,
                                ErrIndexRequired, ErrTooManyWrites, PilosaError, wrap)
-from pilosa_amd.models.cache import Pair, pairs_add, sort_pairs
+from pilosa_amd.models.cache import Pair, PairArray, pairs_add, sort_pairs
 from pilosa_amd.models.field import FIELD_TYPE_BOOL, FIELD_TYPE_INT, FIELD_TYPE_SET, FIELD_TYPE_TIME
 from pilosa_amd.models.fragment import FALSE_ROW_ID, SHARD_WIDTH, TRUE_ROW_ID, TopOptions
 from pilosa_amd.models.index import EXISTENCE_FIELD_NAME
@@ -211,6 +211,8 @@ def _results_equal(a, b) -> bool:
     if isinstance(a, Row) or isinstance(b, Row):
         a = a if not isinstance(a, Row) else list(a.columns())
         b = b if not isinstance(b, Row) else list(b.columns())
+    a = a.to_list() if isinstance(a, PairArray) else a
+    b = b.to_list() if isinstance(b, PairArray) else b
     if isinstance(a, list) and isinstance(b, list) and all(isinstance(x, Pair) for x in a + b):
         # TopN partials: the host reduce keeps insertion order, the device sorts
         return sorted((p.id, p.count) for p in a) == sorted((p.id, p.count) for p in b)
@@ -263,7 +265,9 @@ class Executor:
                 fast = self._count_text_fast(index, q, shards, opt)
                 if fast is not None:
                     return QueryResponse(fast)
+                text = q
                 q = parse_string(q)
+                q.source = text
             if not index:
                 raise ErrIndexRequired
             idx = self.holder.index(index)
@@ -406,8 +410,12 @@ class Executor:
             for c in q.calls:
                 self._validate_call_args(c)
             mesh = self.mesh
+            # the request text as sent (ranks parse it once) unless key
+            # translation rewrote calls in place
+            idx = self.holder.index(index)
+            plain = idx is not None and not idx.keys and not any(f.options.keys for f in idx.fields.values())
             try:
-                res = mesh.topn_batch(index, q.calls, shards)
+                res = mesh.topn_batch(index, q.calls, shards, text=q.source if plain else None)
             except MeshError:
                 if not mesh.failed_over:   # (failover detaches self.mesh)
                     raise
@@ -1658,7 +1666,7 @@ class Executor:
                     return Pair(0, r.count, key)
             return r
         # a []Pair result -- TopN's, even empty (executor.go:2832-2846)
-        if isinstance(r, list) and (c.name == "TopN" or (r and isinstance(r[0], Pair))):
+        if isinstance(r, PairArray) or isinstance(r, list) and (c.name == "TopN" or (r and isinstance(r[0], Pair))):
             fname = c.args.get("_field")
             if isinstance(fname, str) and fname:
                 f = idx.field(fname)

@@ -504,7 +504,19 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // skeleton (pair table, metas, B-head prefetch, readlanes, wave_sum; no
 // staging, no counting), 2 = no wave_sum, 3 = no staging, 4 = no counting,
 // 5 = skeleton without the B-head loads
-template <int CQ, bool APF = false, int DBG = 0>
+//
+// SB > 0 (v16): right after A is staged, every pair of A's run whose B is an
+// array of <= SB values is counted LANE-parallel in one pass -- each such
+// lane walks its own B (16-byte chunks) against the staged bitmap -- instead
+// of one wave-cooperative iteration per pair (readlanes, type dispatch, a
+// probe pass with most lanes idle, a wave_sum).  27 % of the headline batch's
+// pairs have B <= 64 values (scripts/pair_stats.py).
+//
+// PD = B-head prefetch depth: the heads of the next PD pairs are in flight
+// while the current pair is counted (PD = 1: the shipped v6).  The control
+// skeleton (DBG 1) with v6's occupancy spends 4.6 of its 7.5 ms waiting on
+// these heads (profiles/r05_pairs/).
+template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -536,12 +548,27 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
   }
   uint64_t todo = __ballot(ea != NONE);
   int mine = 0;
+  if (DBG) lb[lane] = 0;   // cost-attribution variants keep v6's 8 KiB LDS (and occupancy)
   if (todo) {
     uint32_t cached = NONE;
     int cached_v = -1;
     int i = __builtin_ctzll(todo);
     todo &= todo - 1;
-    uint4 pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, i)), rl64(mb, i));
+    // pf[k]: head of the k-th pair from the current one (k = 0: pair i)
+    uint4 pf[PD];
+    pf[0] = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, i)), rl64(mb, i));
+    {
+      uint64_t t = todo;
+#pragma unroll
+      for (int k = 1; k < PD; k++) {
+        pf[k] = make_uint4(0, 0, 0, 0);
+        if (t) {
+          const int jk = __builtin_ctzll(t);
+          t &= t - 1;
+          pf[k] = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, jk)), rl64(mb, jk));
+        }
+      }
+    }
     // A chunk of the pair about to run (APF), valid when apre_ok
     auto small_array = [](int64_t m) { return meta_type(m) == CT_ARRAY && meta_n(m) <= 512; };
     auto load_ahead = [&](int k) {
@@ -562,14 +589,23 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       const uint16_t* pA = reinterpret_cast<const uint16_t*>(rl_u64(pal, i));
       const uint16_t* pB = reinterpret_cast<const uint16_t*>(rl_u64(pbl, i));
       const int tA = meta_type(mA), tB = meta_type(mB);
-      const int j = todo ? __builtin_ctzll(todo) : -1;
-      const uint4 head = pre;
+      int j = todo ? __builtin_ctzll(todo) : -1;
+      const uint4 head = pf[0];
       const uint4 ahead = apre;
       const bool aok = apre_ok;
-      if (DBG == 5)
-        pre = make_uint4(uint32_t(j), 0, 0, 0);
-      else if (j >= 0)
-        pre = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j));
+#pragma unroll
+      for (int k = 0; k + 1 < PD; k++) pf[k] = pf[k + 1];
+      {
+        // the pair PD - 1 places after j enters the ring
+        uint64_t t = todo;
+#pragma unroll
+        for (int k = 1; k < PD; k++) t &= t - 1;
+        const int jn = t ? __builtin_ctzll(t) : -1;
+        if (DBG == 5)
+          pf[PD - 1] = make_uint4(uint32_t(jn), 0, 0, 0);
+        else if (jn >= 0)
+          pf[PD - 1] = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, jn)), rl64(mb, jn));
+      }
       if (APF) {
         apre_ok = false;
         if (j >= 0 && !(__builtin_amdgcn_readlane(ea, j) == a && __builtin_amdgcn_readlane(vai, j) == va) &&
@@ -578,7 +614,8 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
           apre_ok = true;
         }
       }
-      int c;
+      int c = 0;
+      bool done_i = false;   // pair i answered by the lane-parallel small-B pass
       if (DBG == 1 || DBG == 5) {
         c = int(head.x & 1u) + int(tA == tB);
       } else if (a == cached && va == cached_v) {
@@ -629,10 +666,41 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
             stage(lb, pA, mA);
           cached = a;
           cached_v = va;
-          c = count_vs_head<true>(lb, pB, mB, head);
+          if constexpr (SB > 0) {
+            const uint64_t runm = __ballot(ea == a && vai == va) & (todo | (1ull << i));
+            const uint64_t sm = runm & __ballot(meta_type(mb) == CT_ARRAY && meta_n(mb) <= SB);
+            if (PD == 1 && (sm & (sm - 1))) {   // two or more: one lane-parallel pass
+              const uint32_t* bm32 = reinterpret_cast<const uint32_t*>(lb);
+              if ((sm >> lane) & 1) {
+                const int nb = meta_n(mb);
+                const int n8 = (nb + 7) >> 3;
+                const auto p4 = gp(reinterpret_cast<const uint4*>(pbl));
+                // every chunk's load in flight before the first probe (one round trip)
+                uint4 v[SB > 0 ? SB / 8 : 1];
+#pragma unroll
+                for (int k = 0; k < SB / 8; k++) {
+                  v[k] = make_uint4(0, 0, 0, 0);
+                  if (k < n8) v[k] = p4[k];
+                }
+                int cnt = 0;
+#pragma unroll
+                for (int k = 0; k < SB / 8; k++) cnt += probe8<true>(bm32, v[k]);
+                mine = cnt - int(bm32[0] & 1u) * ((SB / 8) * 8 - nb);   // zero pad slots
+              }
+              todo &= ~sm;
+              done_i = (sm >> i) & 1;
+              if (j >= 0 && ((sm >> j) & 1)) {
+                // the prefetched next pair was answered here: prefetch the new next
+                j = todo ? __builtin_ctzll(todo) : -1;
+                if (j >= 0) pf[0] = load_bhead(reinterpret_cast<const uint16_t*>(rl_u64(pbl, j)), rl64(mb, j));
+              }
+            }
+          }
+          if (!done_i) c = count_vs_head<true>(lb, pB, mB, head);
         }
       }
-      if (DBG == 2) {
+      if (done_i) {
+      } else if (DBG == 2) {
         mine += c;
       } else {
         c = wave_sum(c);
@@ -642,6 +710,10 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       i = j;
       todo &= todo - 1;
     }
+  }
+  if (DBG) {
+    lds_wait();
+    mine += int(lb[lane] & 1u);
   }
   if (lane < nq) partial[u * Q + q0 + lane] = mine;
 }
@@ -862,7 +934,9 @@ void launch_v6_dbg(int dbg, int64_t wv, const QueryProg* progs, int Q, const Vie
     case 2: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 2>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
     case 3: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 3>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
     case 4: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 4>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
-    default: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 5>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 5: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 5>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    case 6: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 1, 0, 2>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
+    default: hipLaunchKernelGGL((and2_pairs_v6_kernel<CQ, false, 1, 0, 3>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial); break;
   }
 }
 
@@ -898,7 +972,22 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                          S, pairs, partial);                                                                 \
     else if (variant >= 21 && variant <= 24)                                                                 \
       launch_v10_dbg<CQV>(variant - 20, wv, progs, Q, views, S, pairs, partial, st);                         \
-    else if (variant >= 31 && variant <= 35)                                                                 \
+    else if (variant == 16)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 32>), dim3(unsigned(wv)), dim3(64), 0, st, progs, \
+                         Q, views, S, pairs, partial);                                                       \
+    else if (variant == 17)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 16>), dim3(unsigned(wv)), dim3(64), 0, st, progs, \
+                         Q, views, S, pairs, partial);                                                       \
+    else if (variant == 18)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 2>), dim3(unsigned(wv)), dim3(64), 0, st,     \
+                         progs, Q, views, S, pairs, partial);                                                \
+    else if (variant == 19)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 3>), dim3(unsigned(wv)), dim3(64), 0, st,     \
+                         progs, Q, views, S, pairs, partial);                                                \
+    else if (variant == 20)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 4>), dim3(unsigned(wv)), dim3(64), 0, st,     \
+                         progs, Q, views, S, pairs, partial);                                                \
+    else if (variant >= 31 && variant <= 37)                                                                 \
       launch_v6_dbg<CQV>(variant - 30, wv, progs, Q, views, S, pairs, partial, st);                          \
     else if (variant == 13)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q,    \

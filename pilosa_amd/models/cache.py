@@ -64,6 +64,75 @@ def pairs_from_arrays(ids, counts) -> List[Pair]:
     return [Pair(i, c) for i, c in zip(ids.tolist(), counts.tolist())]
 
 
+class PairArray:
+    """A TopN result kept columnar: ``ids`` (uint64) and ``counts`` (int64)
+    in result order.  It behaves like the ``[Pair, ...]`` list the reference
+    returns (len, indexing, slicing, iteration, equality with a list of
+    Pairs) but builds Pair objects only when someone iterates or indexes it:
+    a 16-call cache-only TopN request returns ~3k pairs, and creating them
+    was 40 % of its host time (profiles/r05_topn/).  The HTTP / protobuf /
+    collective encoders read the arrays directly."""
+
+    __slots__ = ("ids", "counts", "_items")
+
+    def __init__(self, ids, counts):
+        self.ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        self.counts = np.ascontiguousarray(counts, dtype=np.int64)
+        if len(self.ids) != len(self.counts):
+            raise ValueError("PairArray: ids and counts differ in length")
+        self._items = None
+
+    def to_list(self) -> List["Pair"]:
+        if self._items is None:
+            fast = _make_pairs()
+            got = fast(Pair, self.ids, self.counts) if fast is not None else None
+            if got is None:
+                got = [Pair(i, c) for i, c in zip(self.ids.tolist(), self.counts.tolist())]
+            self._items = got
+        return self._items
+
+    def __len__(self):
+        return len(self.ids)
+
+    def __bool__(self):
+        return len(self.ids) > 0
+
+    def __iter__(self):
+        return iter(self.to_list())
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return PairArray(self.ids[i], self.counts[i])
+        return self.to_list()[i]
+
+    def __eq__(self, other):
+        if isinstance(other, PairArray):
+            return np.array_equal(self.ids, other.ids) and np.array_equal(self.counts, other.counts)
+        if isinstance(other, (list, tuple)):
+            return len(other) == len(self) and all(a == b for a, b in zip(self.to_list(), other))
+        return NotImplemented
+
+    def __repr__(self):
+        return f"PairArray({self.to_list()!r})"
+
+    def to_json(self):
+        return [{"id": i, "count": c} for i, c in zip(self.ids.tolist(), self.counts.tolist())]
+
+    def json_bytes(self) -> bytes:
+        """The JSON array text (Go's layout), natively when the core is loaded."""
+        try:
+            from pilosa_amd import _roaring
+            return _roaring.pairs_json(self.ids, self.counts)
+        except (ImportError, AttributeError):
+            import json
+            return json.dumps(self.to_json(), separators=(",", ":")).encode()
+
+
+def pair_array(ids, counts) -> "PairArray":
+    """A final TopN result from parallel id / count arrays (see PairArray)."""
+    return PairArray(ids, counts)
+
+
 _MAKE_PAIRS = []
 
 

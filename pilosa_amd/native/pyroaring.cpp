@@ -474,6 +474,28 @@ void register_wire_decode(py::module_& m);  // wire_decode.cpp
 // filled directly (the member descriptors' offsets), so the objects are the
 // same as __init__ would build.  Returns None when the type does not have the
 // expected slot layout (the caller then builds them in Python).
+// A TopN result's JSON array, [{"id":1,"count":2},...], written straight
+// from the id / count arrays (Go's encoding/json layout: compact, field order
+// id, count), so a columnar result never becomes Python objects on the way
+// out of the HTTP handler.
+static py::bytes pairs_json(u64arr ids, I64Arr counts) {
+  const ssize_t n = ids.size();
+  if (counts.size() != n) throw std::invalid_argument("pairs_json: ids and counts differ in length");
+  const uint64_t* pi = ids.data();
+  const int64_t* pc = counts.data();
+  std::string out;
+  out.reserve(size_t(n) * 32 + 2);
+  out.push_back('[');
+  char buf[64];
+  for (ssize_t i = 0; i < n; i++) {
+    const int k = snprintf(buf, sizeof buf, "%s{\"id\":%llu,\"count\":%lld}", i ? "," : "",
+                           (unsigned long long)pi[i], (long long)pc[i]);
+    out.append(buf, size_t(k));
+  }
+  out.push_back(']');
+  return py::bytes(out);
+}
+
 static py::object make_pairs(py::object type, u64arr ids, I64Arr counts) {
   if (!PyType_Check(type.ptr())) throw std::invalid_argument("make_pairs: not a type");
   PyTypeObject* tp = reinterpret_cast<PyTypeObject*>(type.ptr());
@@ -800,6 +822,7 @@ PYBIND11_MODULE(PILOSA_ROARING_MODULE, m) {
   }, py::arg("typ"), py::arg("value") = 0, py::arg("values") = u64arr(0), py::arg("roaring") = py::bytes(""),
      py::arg("opn") = 0);
   m.def("make_pairs", &make_pairs, py::arg("type"), py::arg("ids"), py::arg("counts"));
+  m.def("pairs_json", &pairs_json, py::arg("ids"), py::arg("counts"));
   m.def("fnv32a", [](py::bytes data) {
     std::string s = data;
     return pr::fnv32a(reinterpret_cast<const uint8_t*>(s.data()), s.size());

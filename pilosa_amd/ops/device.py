@@ -1375,14 +1375,20 @@ class GpuEngine:
     def shift_views(self, expr, n: int) -> Tuple["DeviceView", "DeviceView"]:
         """Shift(expr, n) for 0 < n < ShardWidth (row_kernels.hip): the part
         that stays in each shard, and the spill each shard carries into the
-        next shard's segment (row.go:217-239, roaring.go:944-977)."""
+        next shard's segment (row.go:217-239, roaring.go:944-977).  Above
+        2^20 columns a shard's device sub-shards carry into each other and
+        the spill of sub-shard m lands in sub-shard m of the next shard."""
         torch = self.torch
         src = self.dense_view(expr)
         S = src.S
         outs = [torch.empty(S * 16 * 4096, dtype=torch.int16, device=self.device) for _ in range(2)]
         metas = [torch.empty(S * 16, dtype=torch.int64, device=self.device) for _ in range(2)]
         if S:
-            self.ext.shift_dense(src.t_payload, S, int(n), outs[0], metas[0], outs[1], metas[1])
+            from pilosa_amd import shardwidth
+            # a shard wider than 2^20 columns is M consecutive device sub-shards:
+            # carries cross them inside the shard (row_kernels.hip)
+            self.ext.shift_dense(src.t_payload, S, int(n), outs[0], metas[0], outs[1], metas[1],
+                                 shardwidth.DEVICE_SUBSHARDS)
         return (self._one_row_view(outs[0], metas[0], src.shards),
                 self._one_row_view(outs[1], metas[1], src.shards))
 

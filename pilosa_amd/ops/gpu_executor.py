@@ -513,9 +513,10 @@ class GpuExecutor:
             child = self.plan(index, c.children[0], shards)
             if k == 0 or child is EMPTY:
                 return child
-            if k >= SHARD_WIDTH or _has_shift(child) or SHARD_WIDTH != 1 << 20:
+            if k >= SHARD_WIDTH or _has_shift(child) or SHARD_WIDTH < 1 << 20:
                 # multi-shard carries, or shards narrower than the device
-                # shard (shift_dense carries at 2^20 columns): host path
+                # shard (shift_dense carries at whole 2^20-column device
+                # shards; wider shards carry across their sub-shards): host path
                 raise NotImplementedError
             try:
                 self.launches += 2
@@ -796,10 +797,11 @@ class GpuExecutor:
                 row.segments[int(s)] = bm
         # bits a shard's Shift carried past its last column belong to the
         # next shard's segment (Row.Merge in the reference's reduce)
+        M = shardwidth.DEVICE_SUBSHARDS   # spill of device shard s belongs to s + M (the next shard)
         for s, bm in zip(spill[1], spill[0]):
             if bm is not None and bm.any():
                 part = _rebase_spill(bm)
-                t = int(s) + 1
+                t = int(s) + M
                 row.segments[t] = row.segments[t].union(part) if t in row.segments else part
         return row
 
@@ -1041,11 +1043,9 @@ class GpuExecutor:
         needs the general path (the caller then runs each call alone).
         ``defer`` (with ``self.comm``): a pending result whose last
         collectives are still in flight (parallel/collectives.Pending)."""
-        ex = self._ex()
+        allp, finfo = self._batch_info(index, calls, shards)
         params = []
-        fields: Dict[str, Tuple] = {}
-        for c in calls:
-            fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
+        for c, (fname, n, ids, threshold, tanimoto, attr_name, attr_values) in zip(calls, allp):
             if tanimoto or (attr_name and attr_values) or len(c.children) > 1:
                 self.topn_decline = f"shape ({c})"
                 return None
@@ -1053,11 +1053,7 @@ class GpuExecutor:
                 self.topn_decline = "ids"
                 return None   # explicit ids= (phase 2 only): the map-step path
             params.append((fname, n, threshold))
-            if fname not in fields:
-                frags = self._topn_frags(index, fname, shards)
-                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
-                rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
-                fields[fname] = (rv, rc)
+        fields = {f: (rv, rc) for f, (_, rv, rc) in finfo.items()}
         srcs = []
         try:
             for c in calls:
@@ -1125,18 +1121,13 @@ class GpuExecutor:
         (parallel/mesh.py OP_TOPN)."""
         if not shards:
             return False
-        ex = self._ex()
         try:
-            for c in calls:
-                fname, n, ids, threshold, tanimoto, attr_name, attr_values = ex.topn_params(index, c)
+            allp, finfo = self._batch_info(index, calls, shards)
+            for c, (fname, n, ids, threshold, tanimoto, attr_name, attr_values) in zip(calls, allp):
                 if ids or tanimoto or (attr_name and attr_values) or len(c.children) > 1:
                     return False
-                frags = self._topn_frags(index, fname, shards)
-                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
-                if rv is None:
-                    return False
-                rc = self._rank_caches(index, fname, shards, frags, rv)
-                if rc is None or not rc.K:
+                _, rv, rc = finfo[fname]
+                if rv is None or rc is None or not rc.K:
                     return False
                 if c.children:
                     src = self.plan(index, c.children[0], shards)
@@ -1318,26 +1309,61 @@ class GpuExecutor:
             sig = (id(rv), rv.rows_gen) if rv is not None else None
             self._spaces[key] = (sig, space)
 
-    def _cand_groups(self, index: str, calls: List[Call]) -> List[Tuple[str, int]]:
-        """(field, nreq) of the batch's cache-only groups, sorted (the same
-        on every rank: derived from the command text)."""
+    def _batch_info(self, index: str, calls: List[Call], shards: List[int]):
+        """(params per call, {field: (fragments, view, rank caches)}) of a
+        TopN batch, resolved once per batch: the mesh asks for readiness,
+        staleness and the batch itself on the same ``calls`` list (a 16-call
+        request used to resolve its one field ~50 times).  Thread-local,
+        keyed by the identity of ``calls`` / ``shards`` and the mutation
+        epoch."""
+        tl = self.__dict__.setdefault("_tl", threading.local())
+        ent = getattr(tl, "batch", None)
+        epoch = mutation_epoch()
+        if ent is not None and ent[0] is calls and ent[1] == index and ent[2] is shards and ent[3] == epoch:
+            return ent[4]
+        params = self._batch_params(index, calls)
+        fields: Dict[str, Tuple] = {}
+        for p in params:
+            fname = p[0]
+            if fname not in fields:
+                frags = self._topn_frags(index, fname, shards)
+                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+                rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+                fields[fname] = (frags, rv, rc)
+        info = (params, fields)
+        tl.batch = (calls, index, shards, epoch, info)
+        return info
+
+    def _batch_params(self, index: str, calls: List[Call]):
+        """topn_params of every call of a batch (schema + text only, the same
+        on every rank), memoised per ``calls`` list like _batch_info."""
+        tl = self.__dict__.setdefault("_tl", threading.local())
+        ent = getattr(tl, "params", None)
+        if ent is not None and ent[0] is calls and ent[1] == index:
+            return ent[2]
         ex = self._ex()
+        params = [ex.topn_params(index, c) for c in calls]
+        tl.params = (calls, index, params)
+        return params
+
+    def _cand_groups(self, index: str, calls: List[Call], shards: List[int]) -> List[Tuple[str, int]]:
+        """(field, nreq) of the batch's cache-only groups, sorted (the same
+        on every rank: derived from the command text and schema only)."""
+        params = self._batch_params(index, calls)
         ns: Dict[str, List[int]] = {}
-        for c in calls:
+        for c, p in zip(calls, params):
             if c.children:
                 continue
-            fname, n = ex.topn_params(index, c)[:2]
-            ns.setdefault(fname, []).append(int(n))
+            ns.setdefault(p[0], []).append(int(p[1]))
         return sorted((f, _nreq(v)) for f, v in ns.items())
 
     def topn_cand_stale(self, index: str, calls: List[Call], shards: List[int]) -> bool:
         """Does this rank miss the node candidate space of a cache-only group
         of the batch (never built, or built from rank caches since replaced)?
         Local check; the mesh votes on it (parallel/mesh.py OP_TOPN)."""
-        for fname, nreq in self._cand_groups(index, calls):
-            frags = self._topn_frags(index, fname, shards)
-            rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
-            rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+        _, finfo = self._batch_info(index, calls, shards)
+        for fname, nreq in self._cand_groups(index, calls, shards):
+            rc = finfo[fname][2]
             ent = self._cand_spaces.get((index, fname, tuple(shards), nreq))
             if rc is None or ent is None or ent[0] != rc.serial:
                 return True
@@ -1353,13 +1379,11 @@ class GpuExecutor:
         import torch
 
         from .topn_exec import FUSED_MAX_CELLS
-        for fname, nreq in self._cand_groups(index, calls):
+        for fname, nreq in self._cand_groups(index, calls, shards):
             rc = None
             rows = np.zeros(0, np.uint64)
             try:
-                frags = self._topn_frags(index, fname, shards)
-                rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
-                rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+                rc = self._batch_info(index, calls, shards)[1][fname][2]
                 if rc is not None:
                     rows = rc.local_candidate_rows(nreq)
             except Exception:  # noqa: BLE001 - take part with nothing; the fit check fails below

@@ -35,7 +35,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from pilosa_amd.models.cache import Pair, pairs_from_arrays
+from pilosa_amd.models.cache import Pair, pair_array, pairs_from_arrays
 
 from .device import DeviceView, kernels
 
@@ -525,7 +525,7 @@ class DeviceRankCaches:
                 else:
                     r = h[q, 1:1 + int(h[q, 0])]
                 j = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
-                res.append(pairs_from_arrays(space[j] if len(j) else np.zeros(0, np.uint64), r >> 32))
+                res.append(pair_array(space[j] if len(j) else np.zeros(0, np.uint64), r >> 32))
             return res
         pend = Pending(comm, comm.all_reduce_async(buf), finish, keep=(buf, prm_d))
         return pend if defer else pend.result()
@@ -614,7 +614,7 @@ class DeviceRankCaches:
             r = h[q, 1:1 + int(h[q, 0])]
             d = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
             ids = rows[d] if len(d) else np.zeros(0, np.uint64)
-            res.append(pairs_from_arrays(ids, r >> 32))
+            res.append(pair_array(ids, r >> 32))
         return res
 
     def _topn_nosrc_dense(self, ns: Sequence[int], thresholds: Sequence[int]) -> List[List[Pair]]:
@@ -677,7 +677,7 @@ class DeviceRankCaches:
                 r = r[:nn[q]]
             d = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
             ids = rows[d] if len(d) else np.zeros(0, np.uint64)
-            out.append(pairs_from_arrays(ids, r >> 32))
+            out.append(pair_array(ids, r >> 32))
         return out
 
     def shard_pairs_nosrc(self, n: int, threshold: int, ids: Optional[Sequence[int]] = None) -> List[Pair]:

@@ -26,7 +26,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from pilosa_amd.models.cache import Pair, pairs_from_arrays
+from pilosa_amd.models.cache import Pair, pair_array, pairs_from_arrays
 
 from .device import DeviceView, GpuEngine, kernels
 
@@ -629,5 +629,5 @@ def finish_batch(space: np.ndarray, Q: int, pq: np.ndarray, pa: np.ndarray, cnt:
         n = int(ns[q])
         if n:
             hi = min(hi, lo + n)
-        out.append(pairs_from_arrays(ids[lo:hi], cnt[lo:hi]))
+        out.append(pair_array(ids[lo:hi], cnt[lo:hi]))
     return out

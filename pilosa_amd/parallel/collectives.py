@@ -453,7 +453,7 @@ def _words_to_bytes(w: np.ndarray, n: int) -> bytes:
 def encode_partial(obj) -> np.ndarray:
     """One rank's partial result -> int64[...] (see the TAG_ layout)."""
     from pilosa_amd.executor import GroupCount, RowIdentifiers, ValCount
-    from pilosa_amd.models.cache import Pair
+    from pilosa_amd.models.cache import Pair, PairArray
     from pilosa_amd.models.row import Row
 
     def msg():
@@ -470,6 +470,9 @@ def encode_partial(obj) -> np.ndarray:
         return np.array([TAG_VALCOUNT, obj.val, obj.count], np.int64)
     if isinstance(obj, Pair) and not getattr(obj, "key", ""):
         return np.array([TAG_PAIR, obj.id, obj.count], np.uint64).view(np.int64)
+    if isinstance(obj, PairArray):
+        flat = np.stack([obj.ids, obj.counts.view(np.uint64)], axis=1).reshape(-1).view(np.int64)
+        return np.concatenate([np.array([TAG_PAIRS, len(obj)], np.int64), flat])
     if isinstance(obj, list) and all(isinstance(p, Pair) and not getattr(p, "key", "") for p in obj):
         flat = np.array([(p.id, p.count) for p in obj], np.uint64).reshape(-1).view(np.int64) if obj else \
             np.zeros(0, np.int64)

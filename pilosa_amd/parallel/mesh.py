@@ -230,7 +230,7 @@ class ShardMesh:
                 self.failover(e)
                 raise MeshError(f"mesh collective failed, failed over to rank 0: {e}") from e
 
-    def topn_batch(self, index: str, calls, shards: Sequence[int]):
+    def topn_batch(self, index: str, calls, shards: Sequence[int], text: Optional[str] = None):
         """Whole TopN calls on every rank's GPU with the node-wide merge on
         tensors (ops/topn_exec.py / topn_index.py with ``comm``): the ranks
         all-gather and union their phase-1 candidate keys and all-reduce the
@@ -238,7 +238,8 @@ class ShardMesh:
         (executor.go:863-903 over RCCL instead of per-shard pair lists).  The
         ranks first agree (one all-reduce of a flag) that each can run the
         batch on its device; None = use the general path."""
-        res = self._run_pipelined(OP_TOPN, index, [str(c) for c in calls], list(shards))
+        res = self._run_pipelined(OP_TOPN, index, text if text is not None else [str(c) for c in calls],
+                                  list(shards))
         if res is not None:
             self.topn_tensor_batches += 1
         return res
@@ -527,10 +528,12 @@ class ShardMesh:
         from pilosa_amd.executor import DEFAULT_FIELD
 
         own = self.owned(shards)
-        ok = False
         calls = []
         try:
-            calls = [parse_string(p).calls[0] for p in pqls]
+            # one request text (parsed once) or the calls printed one by one
+            calls = parse_string(pqls).calls if isinstance(pqls, str) else [parse_string(p).calls[0] for p in pqls]
+            if not all(c.name == "TopN" for c in calls):
+                calls = []
         except Exception:  # noqa: BLE001 - the same text fails on every rank
             calls = []
         # the batch's fields come from the command text: every rank lists the

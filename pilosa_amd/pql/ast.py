@@ -178,10 +178,13 @@ def format_value(v: Any) -> str:
 
 
 class Query:
-    __slots__ = ("calls",)
+    __slots__ = ("calls", "source")
 
-    def __init__(self, calls: Optional[List[Call]] = None):
+    def __init__(self, calls: Optional[List[Call]] = None, source: Optional[str] = None):
         self.calls: List[Call] = calls or []
+        # the PQL text it was parsed from (the mesh forwards it as is, so
+        # the ranks parse one request once instead of per re-printed call)
+        self.source = source
 
     def write_call_n(self) -> int:
         return sum(1 for c in self.calls if c.name in ("Set", "Clear", "SetRowAttrs", "SetColumnAttrs"))

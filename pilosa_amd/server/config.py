@@ -200,6 +200,39 @@ class Config:
         return parse_duration(self.get(key))
 
 
+# ------------------------------------------------------------ gossip
+def validate_gossip(cfg: "Config") -> None:
+    """The ``[gossip]`` keys this build acts on (parallel/swim.py failure
+    detection, NodeStatus push-pull) must hold usable values: positive
+    probe interval / timeout, suspicion multiplier >= 1, indirect probers
+    >= 0, a port number, durations that parse.  Gossip travels over the
+    node's HTTP(S) port, so ``gossip.key`` (memberlist's symmetric
+    encryption key file) is refused: use ``[tls]`` to encrypt cluster
+    traffic instead of silently running unencrypted."""
+    try:
+        pi = cfg.duration("gossip.probe-interval")
+        pt = cfg.duration("gossip.probe-timeout")
+        for k in ("gossip.push-pull-interval", "gossip.interval", "gossip.to-the-dead-time", "gossip.stream-timeout"):
+            if cfg.duration(k) < 0:
+                raise ConfigError(f"{k} must not be negative")
+    except ValueError as e:
+        raise ConfigError(f"gossip: {e}")
+    if pi <= 0:
+        raise ConfigError("gossip.probe-interval must be positive")
+    if pt <= 0:
+        raise ConfigError("gossip.probe-timeout must be positive")
+    if float(cfg.get("gossip.suspicion-mult")) < 1:
+        raise ConfigError("gossip.suspicion-mult must be at least 1")
+    if int(cfg.get("gossip.nodes")) < 0:
+        raise ConfigError("gossip.nodes must not be negative")
+    port = str(cfg.get("gossip.port"))
+    if not port.isdigit() or not 0 <= int(port) <= 65535:
+        raise ConfigError(f"gossip.port: invalid port {port!r}")
+    if cfg.get("gossip.key"):
+        raise ConfigError("gossip.key: gossip runs over the node's HTTP port in this build; "
+                          "encrypt cluster traffic with [tls] instead")
+
+
 # ------------------------------------------------------------ listen / advertise
 # (server/config.go validateAddrs, validateAdvertiseAddr, validateListenAddr)
 DEFAULT_PORT = "10101"

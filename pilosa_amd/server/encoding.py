@@ -5,7 +5,7 @@ from __future__ import annotations
 from typing import Any, List, Optional
 
 from pilosa_amd.executor import FieldRow, GroupCount, QueryResponse, RowIdentifiers, ValCount
-from pilosa_amd.models.cache import Pair
+from pilosa_amd.models.cache import Pair, PairArray
 from pilosa_amd.models.row import Row
 from pilosa_amd.wire import (ATTR_TYPE_BOOL, ATTR_TYPE_FLOAT, ATTR_TYPE_INT, ATTR_TYPE_STRING,
                              QUERY_RESULT_TYPE_BOOL, QUERY_RESULT_TYPE_GROUPCOUNTS, QUERY_RESULT_TYPE_NIL,
@@ -21,11 +21,24 @@ def result_to_json(r: Any):
         return r
     if isinstance(r, int):
         return r
-    if isinstance(r, (Row, ValCount, Pair, RowIdentifiers, GroupCount, FieldRow)):
+    if isinstance(r, (Row, ValCount, Pair, RowIdentifiers, GroupCount, FieldRow, PairArray)):
         return r.to_json()
     if isinstance(r, list):
         return [result_to_json(x) for x in r]
     return r
+
+
+def response_json_bytes(resp: QueryResponse) -> bytes:
+    """The query response body as Go's json.Encoder writes it (trailing
+    newline).  Columnar TopN results (PairArray) are written straight from
+    their arrays; everything else through the generic encoder."""
+    from pilosa_amd.utils import gojson
+    if resp.err is not None or resp.column_attr_sets or \
+            not any(isinstance(r, PairArray) for r in resp.results):
+        return gojson.encode_line(response_to_json(resp)).encode()
+    parts = [r.json_bytes() if isinstance(r, PairArray) else gojson.dumps(result_to_json(r)).encode()
+             for r in resp.results]
+    return b'{"results":[' + b",".join(parts) + b"]}\n"
 
 
 def response_to_json(resp: QueryResponse) -> dict:
@@ -96,6 +109,10 @@ def result_to_pb(r: Any, call_name: str = ""):
         m.RowIdentifiers.Rows.extend(r.rows)
         if r.keys:
             m.RowIdentifiers.Keys.extend(r.keys)
+    elif isinstance(r, PairArray):
+        m.Type = QUERY_RESULT_TYPE_PAIRS
+        for i, c in zip(r.ids.tolist(), r.counts.tolist()):
+            m.Pairs.add(ID=i, Count=c)
     elif isinstance(r, list) and (not r and call_name == "TopN" or r and isinstance(r[0], Pair)):
         m.Type = QUERY_RESULT_TYPE_PAIRS
         for p in r:

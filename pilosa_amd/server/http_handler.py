@@ -25,7 +25,7 @@ from pilosa_amd.errors import (APIMethodNotAllowedError, BadRequestError, Confli
                                ErrNodeNotCoordinator, ErrResizeNotRunning, NotFoundError, PilosaError, cause)
 from pilosa_amd.models.field import FieldOptions
 from pilosa_amd.server.api import QueryRequest
-from pilosa_amd.server.encoding import response_to_json, response_to_pb
+from pilosa_amd.server.encoding import response_json_bytes, response_to_json, response_to_pb
 from pilosa_amd.utils import tracing
 from pilosa_amd.wire import pb
 
@@ -100,6 +100,7 @@ class Handler:
         r("GET", r"/status", self.get_status, "GetStatus")
         r("GET", r"/version", self.get_version, "GetVersion")
         r("POST", r"/internal/cluster/message", self.post_cluster_message, "PostClusterMessage")
+        r("POST", r"/internal/probe", self.post_probe, "PostProbe")
         r("GET", r"/internal/fragment/block/data", self.get_fragment_block_data, "GetFragmentBlockData")
         r("GET", r"/internal/fragment/blocks", self.get_fragment_blocks, "GetFragmentBlocks")
         r("GET", r"/internal/fragment/data", self.get_fragment_data, "GetFragmentData")
@@ -323,7 +324,7 @@ class Handler:
             self._write_query_error(req, 400, e)
             return
         if self._accept_json(req):
-            req.send(200, gojson.encode_line(response_to_json(resp)), JSON)
+            req.send(200, response_json_bytes(resp), JSON)
         else:
             req.send(200, response_to_pb(resp, getattr(resp, "calls", None)), "application/protobuf")
 
@@ -465,6 +466,19 @@ class Handler:
     def post_recalculate(self, req):
         self.api.recalculate_caches()
         req.send(204, "", "text/plain")
+
+    def post_probe(self, req):
+        """Indirect liveness probe for a peer's failure detector
+        (parallel/swim.py): probe ``uri`` within ``timeout`` seconds and say
+        whether it answered (memberlist's indirect ping)."""
+        try:
+            body = json.loads(req.body or b"{}")
+            uri, timeout = str(body["uri"]), float(body.get("timeout", 0.5))
+        except (ValueError, KeyError, TypeError) as e:
+            raise HTTPError(400, f"probe request: {e}")
+        srv = self.server
+        ok = bool(srv.probe_for_peer(uri, timeout)) if srv is not None else False
+        req.send_json({"ok": ok})
 
     def post_cluster_message(self, req):
         """Type byte + protobuf body (http/handler.go:1474); a JSON body is

@@ -4,10 +4,14 @@ holder.go syncer/cleaner, gossip/).
 Wires holder + cluster + executor (+ GPU executor) + API + HTTP handler and
 runs the background loops:
 
-* membership: the coordinator probes every node's ``/version``
-  (probe interval, N misses -> DOWN, like confirmNodeDown cluster.go:1699)
-  and pushes the cluster status; joining nodes announce themselves to the
-  coordinator (replaces memberlist gossip, which is not available here);
+* membership: every node runs SWIM-style failure detection
+  (parallel/swim.py, the ``[gossip]`` probe-interval / probe-timeout /
+  suspicion-mult / nodes keys that drive memberlist in the reference):
+  direct ``/version`` probes, indirect probes through peers
+  (``/internal/probe``), suspicion timeout -> DOWN; the coordinator applies
+  the verdicts and pushes the cluster status; joining nodes announce
+  themselves to the coordinator; NodeStatus push-pull gossip spreads schema
+  and shards;
 * resize: node join/leave with data -> coordinator computes per-node fragment
   sources (cluster.frag_sources), nodes stream fragments over HTTP, report
   completion, coordinator commits the topology, nodes drop fragments they no
@@ -50,6 +54,27 @@ def _gpu_present() -> bool:
         return False
 
 
+def _ssl_ctx(skip_verify: bool):
+    import ssl
+    if not skip_verify:
+        return None
+    ctx = ssl.create_default_context()
+    ctx.check_hostname = False
+    ctx.verify_mode = ssl.CERT_NONE
+    return ctx
+
+
+def _probe_version(uri, timeout: float, skip_verify: bool = False) -> bool:
+    """One liveness probe: GET /version answered 200 within ``timeout``."""
+    from urllib import request as _rq
+    url = f"{uri.scheme}://{uri.host_port()}/version"
+    try:
+        with _rq.urlopen(url, timeout=timeout, context=_ssl_ctx(skip_verify) if uri.scheme == "https" else None) as r:
+            return r.status == 200
+    except Exception:  # noqa: BLE001 - any failure is a missed ack
+        return False
+
+
 class Server:
     def __init__(self, data_dir: str, bind: str = "127.0.0.1:10101", node_id: Optional[str] = None,
                  replica_n: int = 1, hosts: Optional[List[str]] = None, coordinator: bool = True,
@@ -62,7 +87,8 @@ class Server:
                  gpu_device: Optional[int] = None, hbm_budget: int = 0, mesh_timeout_s: float = 120.0,
                  lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None,
                  gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None,
-                 advertise: str = ""):
+                 advertise: str = "", probe_timeout: float = 0.5, suspicion_mult: float = 4,
+                 indirect_checks: int = 3, to_the_dead_time: float = 30.0, stream_timeout: float = 10.0):
         self.data_dir = data_dir
         # CORS origins ([handler] allowed-origins); none = no CORS headers at all
         self.allowed_origins = list(allowed_origins or [])
@@ -87,9 +113,20 @@ class Server:
         # liveness probes use a short timeout so a hung peer is noticed quickly
         # (reference confirmNodeDown: 2 s per /version attempt, cluster.go:1699-1726)
         self.probe_client = InternalClient(timeout=2.0)
+        # NodeStatus push-pull ([gossip] stream-timeout, memberlist TCPTimeout)
+        self.stream_client = InternalClient(timeout=stream_timeout)
         self.long_query_time = long_query_time
         self.anti_entropy_interval = anti_entropy_interval
         self.probe_interval = probe_interval
+        # [gossip] failure detection (parallel/swim.py, memberlist's settings in
+        # the reference, gossip/gossip.go:269-272)
+        self.probe_timeout = probe_timeout
+        self.suspicion_mult = suspicion_mult
+        self.indirect_checks = indirect_checks
+        self.to_the_dead_time = to_the_dead_time
+        self.stream_timeout = stream_timeout
+        self.failure_detector = None
+        self._down_since: Dict[str, float] = {}
         self.gossip_interval = gossip_interval
         self._gossip_i = 0
         self._gossip_misses: Dict[str, int] = {}
@@ -109,7 +146,7 @@ class Server:
         self.mesh_block = mesh_block
         self.translation_primary = URI.parse(translation_primary_url) if translation_primary_url else None
         self.tls_certificate, self.tls_key = tls_certificate, tls_key
-        self.client.skip_verify = self.probe_client.skip_verify = tls_skip_verify
+        self.client.skip_verify = self.probe_client.skip_verify = self.stream_client.skip_verify = tls_skip_verify
         self.diagnostics = None
         from pilosa_amd import buildinfo
         # release builds report hourly, others not at all (server/release.go, default.go)
@@ -138,6 +175,7 @@ class Server:
         host, _, port = self.bind.rpartition(":")
         handler = Handler(self.api, self, self.logger, self.stats)
         handler.allowed_origins = self.allowed_origins
+        self.handler = handler
         self.httpd = None
         if self.native_http:
             from pilosa_amd.server import native_http
@@ -183,10 +221,11 @@ class Server:
             self.cluster.set_state(STATE_NORMAL if not self.cluster.need_topology_agreement() else STATE_STARTING)
         elif self.is_coordinator_cfg:
             self.cluster.set_coordinator(self.node.id)
-            self._start_loop(self._membership_loop, "membership")
             self.cluster.set_state(self.cluster.determine_state())
         else:
             self._join()
+        if not self.cluster_disabled and self.probe_interval > 0:
+            self._start_loop(self._swim_loop, "swim")
         if not self.cluster_disabled and self.gossip_interval > 0:
             self._start_loop(self._gossip_loop, "gossip")
         if self.replica_n > 1 and self.anti_entropy_interval > 0:
@@ -548,59 +587,93 @@ class Server:
             me.state = NODE_READY
         self.cluster.set_state(st.get("state", STATE_NORMAL))
 
-    def _membership_loop(self):
-        while not self._closing.wait(self.probe_interval):
-            if not self.cluster.is_coordinator():
-                continue
-            changed = False
-            for n in list(self.cluster.nodes):
-                if n.id == self.node.id:
+    def _swim_loop(self):
+        """Failure detection on every node (parallel/swim.py: direct probe,
+        indirect probes through ``indirect_checks`` peers, suspicion timeout
+        from ``suspicion_mult``).  The coordinator applies the verdicts and
+        publishes the cluster status; another node reports a DOWN verdict to
+        the coordinator (NodeState), as memberlist's leave event reaches the
+        reference's coordinator.  A DOWN node that answers again is READY."""
+        from pilosa_amd.parallel.swim import DOWN, FailureDetector
+        det = FailureDetector(self.node.id, self._swim_probe, self._swim_indirect,
+                              probe_interval=self.probe_interval, probe_timeout=self.probe_timeout,
+                              suspicion_mult=self.suspicion_mult, indirect_checks=self.indirect_checks)
+        self.failure_detector = det
+        try:
+            while not self._closing.wait(self.probe_interval):
+                det.probe_interval, det.probe_timeout = self.probe_interval, self.probe_timeout
+                nodes = list(self.cluster.nodes)
+                if len(nodes) < 2:
                     continue
-                try:
-                    self.probe_client.version(n.uri)
-                    self._misses[n.id] = 0
-                    if n.state != NODE_READY:
-                        changed |= self.cluster.set_node_state(n.id, NODE_READY)
-                except Exception:  # noqa: BLE001
-                    self._misses[n.id] = self._misses.get(n.id, 0) + 1
-                    if self._misses[n.id] >= 3 and n.state != NODE_DOWN:
-                        changed |= self.cluster.set_node_state(n.id, NODE_DOWN)
-            new_state = self.cluster.determine_state()
-            if changed or new_state != self.cluster.state:
-                self._publish_status()
+                coord = self.cluster.is_coordinator()
+                changed = False
+                for nid, ev in det.tick(nodes):
+                    if ev == DOWN:
+                        self.logger.printf("swim: node %s unreachable past the suspicion timeout", nid)
+                        self._down_since[nid] = time.monotonic()
+                        if coord:
+                            changed |= self.cluster.set_node_state(nid, NODE_DOWN)
+                        else:
+                            self._report_down(nid)
+                    else:
+                        self._down_since.pop(nid, None)
+                        if coord:
+                            changed |= self.cluster.set_node_state(nid, NODE_READY)
+                if coord:
+                    new_state = self.cluster.determine_state()
+                    if changed or new_state != self.cluster.state:
+                        self._publish_status()
+        finally:
+            det.close()
+
+    def _swim_probe(self, node, timeout: float) -> bool:
+        """Direct probe: the node's /version within ``timeout``."""
+        return _probe_version(node.uri, timeout, self.probe_client.skip_verify)
+
+    def _swim_indirect(self, helper, target, timeout: float) -> bool:
+        """Indirect probe: ask ``helper`` to probe ``target`` (POST
+        /internal/probe), memberlist's indirect ping."""
+        import json as _json
+        from urllib import request as _rq
+        url = f"{helper.uri.scheme}://{helper.uri.host_port()}/internal/probe"
+        body = _json.dumps({"uri": target.uri.normalize(), "timeout": timeout}).encode()
+        req = _rq.Request(url, data=body, method="POST", headers={"Content-Type": "application/json"})
+        with _rq.urlopen(req, timeout=timeout * 2 + 0.5, context=_ssl_ctx(self.probe_client.skip_verify)) as r:
+            return bool(_json.loads(r.read() or b"{}").get("ok"))
+
+    def probe_for_peer(self, uri: str, timeout: float) -> bool:
+        """A peer's indirect probe of ``uri`` through this node."""
+        return _probe_version(URI.parse(uri), min(float(timeout), 5.0), self.probe_client.skip_verify)
+
+    def _report_down(self, nid: str):
+        coord = self.cluster.coordinator()
+        if coord is not None and coord.id not in (nid, self.node.id):
+            try:
+                self.client.send_message(coord, {"type": "NodeState", "nodeID": nid, "state": NODE_DOWN})
+            except Exception as e:  # noqa: BLE001
+                self.logger.printf("swim: reporting %s down: %s", nid, e)
+        else:
+            self._node_down(nid)
 
     def _gossip_loop(self):
         """Push-pull of NodeStatus between every pair of nodes (the role of
         memberlist's LocalState/MergeRemoteState, gossip/gossip.go:295-443):
         each round this node pushes its schema + available shards to the next
-        peer, and receives every peer's push in turn.  A peer that misses
-        three pushes and then fails confirm_node_down is reported DOWN to the
-        coordinator, so failures are seen by non-coordinators too."""
-        from pilosa_amd.parallel.cluster import confirm_node_down
+        peer, and receives every peer's push in turn.  Failure detection is
+        the SWIM loop's; a peer DOWN for longer than ``to_the_dead_time``
+        stops receiving pushes (memberlist's GossipToTheDeadTime)."""
         while not self._closing.wait(self.gossip_interval):
-            peers = [n for n in self.cluster.nodes if n.id != self.node.id]
+            now = time.monotonic()
+            peers = [n for n in self.cluster.nodes if n.id != self.node.id and
+                     not (n.state == NODE_DOWN and now - self._down_since.get(n.id, now) > self.to_the_dead_time)]
             if not peers:
                 continue
             n = peers[self._gossip_i % len(peers)]
             self._gossip_i += 1
             try:
-                self.probe_client.send_message(n, {"type": "NodeStatus", "status": self._node_status()})
-                self._gossip_misses[n.id] = 0
-            except Exception as e:  # noqa: BLE001
-                miss = self._gossip_misses[n.id] = self._gossip_misses.get(n.id, 0) + 1
-                if miss < 3 or n.state == NODE_DOWN or self.cluster.is_coordinator():
-                    continue    # the coordinator's own membership loop owns its verdicts
-                if not confirm_node_down(n.uri, retries=2, sleep=min(self.probe_interval, 1.0), timeout=2.0):
-                    continue
-                self.logger.printf("gossip: node %s unreachable (%s)", n.id, e)
-                coord = self.cluster.coordinator()
-                if coord is not None and coord.id not in (n.id, self.node.id):
-                    try:
-                        self.client.send_message(coord, {"type": "NodeState", "nodeID": n.id, "state": NODE_DOWN})
-                    except Exception as e2:  # noqa: BLE001
-                        self.logger.printf("gossip: reporting %s down: %s", n.id, e2)
-                else:
-                    self._node_down(n.id)
+                self.stream_client.send_message(n, {"type": "NodeStatus", "status": self._node_status()})
+            except Exception as e:  # noqa: BLE001 - the SWIM loop judges liveness
+                self._gossip_misses[n.id] = self._gossip_misses.get(n.id, 0) + 1
 
     # ------------------------------------------------------------ resize
     def _holder_layout(self) -> Dict[str, Dict[str, List[str]]]:

@@ -473,6 +473,10 @@ SHIFT_QUERIES = [
     "Xor(Shift(Row(f=2), n=1000000), Row(f=3))", "Union(Shift(Row(f=0), n=64), Shift(Row(f=1), n=7))",
     "Count(Shift(Intersect(Row(f=0), Row(f=1)), n=1048575))", "Shift(Row(f=3), n=0)",
 ]
+if SW > (1 << 21):
+    # wide shards (PILOSA_SHARD_WIDTH=22): carries across 1..3 device sub-shards
+    SHIFT_QUERIES += ["Shift(Row(f=20), n=1048576)", "Count(Shift(Row(f=0), n=3000000))",
+                      "Xor(Shift(Row(f=1), n=2097153), Row(f=0))", "Shift(Row(f=3), n=4194303)"]
 
 
 @pytest.mark.parametrize("q", SHIFT_QUERIES)

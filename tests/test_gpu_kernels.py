@@ -126,7 +126,7 @@ def test_and2_pair_kernels_match_tile_kernel(setup):
         exprs.append(Op("and", (Leaf(va, min(a, 5) if va is view2 else a), Leaf(view, b))))
         ra = min(a, 5) if va is view2 else a
         want.append(sum(_row(x, ra).intersection_count(_row(f, b)) for x, f in zip(fa, frags)))
-    for var in (6, 10, 12, 13):
+    for var in (6, 10, 12, 13, 16, 17, 18, 19, 20):
         for cq in (0, 16, 32, 64):
             e2 = GpuEngine(view.device)
             e2.and2_cq = cq
@@ -187,7 +187,7 @@ def test_bitgemm_count_matrix_matches_host(mode):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("variant", [6, 10, 12])
+@pytest.mark.parametrize("variant", [6, 10, 12, 16, 17, 18, 19, 20])
 @pytest.mark.parametrize("cq", [16, 32, 64])
 def test_pair_kernel_array_size_boundaries(cq, variant):
     """Array containers of 1, 63, 64, 65, 255, 256, 257 (the small-probe

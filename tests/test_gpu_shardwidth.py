@@ -7,8 +7,8 @@ Wider (2^22, the reference CI's SHARD_WIDTH=22): every shard is 4 device
 sub-shards and the executor and TopN suites run unchanged (rank caches stay
 per fragment with counts summed over its sub-shards; src TopN takes the
 pair-count path instead of the 2^20-column slot index).
-Shift is excluded: its device carry works at 2^20 columns only, so at
-other widths it runs on the host (ops/gpu_executor.py)."""
+Shift carries across the sub-shards of a wide shard on the device; at the
+narrow widths it runs on the host (ops/gpu_executor.py) and is excluded."""
 import os
 import subprocess
 import sys
@@ -33,9 +33,11 @@ def test_gpu_suites_at_narrow_width(exp):
 
 @pytest.mark.timeout(900)
 def test_gpu_executor_suite_at_wide_width():
+    """Shift included: the device carries across the 4 sub-shards of a 2^22
+    shard, and its test asserts a device launch (no host fallback)."""
     env = dict(os.environ, PILOSA_SHARD_WIDTH="22")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
-                        "--timeout", "300", "--timeout-method", "thread", "-k", "not shift and not Shift",
+                        "--timeout", "300", "--timeout-method", "thread",
                         "tests/test_gpu_executor.py", "tests/test_gpu_topn_exec.py"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=850)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
