@@ -714,9 +714,10 @@ def bench_configs_disk(args, world, rank, dev, which):
         rng = np.random.default_rng(5)
 
         def reduce_vals(vals):
+            if world == 1:   # nothing to combine: no device round trip inside the timed loop
+                return [int(v) for v in vals]
             t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=dev)
-            if world > 1:
-                all_reduce(t)
+            all_reduce(t)
             return t.cpu().tolist()
 
         def flat(r):

@@ -490,6 +490,45 @@ class Executor:
                     raise AssertionError(f"paranoia: device TopN {r!r} != host TopN {want!r}")
         return res
 
+    def _topn_text_fast(self, index: str, text: str, shards=None) -> Optional[List[Any]]:
+        """Serving fast path for a text made only of cache-only TopN calls
+        (the concurrent TopN requests the native HTTP front end groups): the
+        text is parsed once and every call runs in ONE device batch (one
+        OP_TOPN mesh batch on a multi-GPU node), results columnar
+        (PairArray).  None = the general path, which also produces every
+        error the reference would (executor.go:863-930)."""
+        idx = self.holder.index(index)
+        if idx is None or idx.keys or any(f.options.keys for f in idx.fields.values()):
+            return None
+        opt = ExecOptions()
+        mesh = self.mesh if self._use_mesh(opt) else None
+        if mesh is None and self.gpu is None:
+            return None
+        try:
+            calls = parse_string(text).calls
+        except Exception:  # noqa: BLE001 - the general path reports the parse error
+            return None
+        if not calls or any(c.name != "TopN" or c.children or "ids" in c.args for c in calls):
+            return None
+        try:
+            for c in calls:
+                self._validate_call_args(c)
+        except PilosaError:
+            return None
+        shards = list(shards) if shards else (idx.available_shards() or [0])
+        if self._has_remote(index, shards, opt):
+            return None
+        if mesh is not None:
+            try:
+                res = mesh.topn_batch(index, calls, shards, text=text)
+            except MeshError:
+                return None
+        else:
+            res = self._run_topn_batch((index, tuple(shards)), calls)
+        if res is None or len(res) != len(calls) or any(r is None for r in res):
+            return None
+        return res
+
     def _run_count_batch(self, key, calls):
         index, shards, mesh = key
         if mesh:
@@ -1090,10 +1129,7 @@ class Executor:
             red = lambda p, v: (p or ValCount()).larger(v or ValCount())  # noqa: E731
 
         def local(ss):
-            r = None
-            for vc in self.gpu.bsi_minmax(index, c, ss, which):
-                r = red(r, vc)
-            return r
+            return self.gpu.bsi_minmax(index, c, ss, which)   # already folded over ss
         r = self.map_reduce(index, shards, c, opt, map_fn, red, local if self.gpu is not None else None) or ValCount()
         return r if r.count else ValCount()
 

@@ -4,7 +4,7 @@
 // negotiation :977-1052).
 //
 // Parsing, connection handling and response writing run on native threads
-// without the GIL.  Requests reach Python through two queues:
+// without the GIL.  Requests reach Python through three queues:
 //
 //   * kind 1 -- "count batchable": POST /index/{i}/query with a JSON-acceptable
 //     Accept header, no query arguments, a non-protobuf body made only of
@@ -14,6 +14,10 @@
 //     compile + one device launch (executor._count_text_fast); the counts go
 //     back in one respond_counts() call that formats {"results": [...]} here.
 //     A group Python cannot answer that way is requeue()d as kind 0.
+//   * kind 2 -- "topn batchable" (when enabled): the same shape made only of
+//     flat TopN(...) calls (no nested call: cache-only TopN).  take_topn()
+//     groups them like take_counts(), so the concurrent TopN requests of a
+//     serving mix become one device batch (executor._topn_text_fast).
 //   * kind 0 -- everything else: take() returns (id, method, path, query,
 //     headers, body) and Python's route table answers with respond().
 //
@@ -160,15 +164,19 @@ static std::string make_response(int status, const std::string& ctype, const cha
 
 // Top-level calls of a PQL text (the planner's split, native/pql_compile.cpp
 // plan_count_text): -1 when quoted strings or unbalanced parentheses appear,
-// else the number of calls; *all_count = every call starts with "Count(".
-static int split_calls(const std::string& t, bool* all_count) {
+// else the number of calls; *all_count = every call starts with "Count(";
+// *all_topn = every call is a flat "TopN(...)" (no nested call: the cache-only
+// shape the TopN group commit answers).
+static int split_calls(const std::string& t, bool* all_count, bool* all_topn = nullptr) {
   size_t i = 0, n = t.size();
   int calls = 0;
   *all_count = true;
+  if (all_topn) *all_topn = true;
   while (i < n) {
     while (i < n && (t[i] == ' ' || t[i] == '\t' || t[i] == '\n' || t[i] == '\r')) i++;
     if (i >= n) break;
     if (t.compare(i, 6, "Count(") != 0) *all_count = false;
+    if (all_topn && t.compare(i, 5, "TopN(") != 0) *all_topn = false;
     int depth = 0;
     bool seen = false;
     for (; i < n; i++) {
@@ -176,6 +184,7 @@ static int split_calls(const std::string& t, bool* all_count) {
       if (c == '"' || c == '\'') return -1;
       if (c == '(') {
         depth++;
+        if (depth > 1 && all_topn) *all_topn = false;
         seen = true;
       } else if (c == ')' && --depth == 0) {
         i++;
@@ -310,8 +319,7 @@ class Server {
     wakefds_.clear();
     {
       std::lock_guard<std::mutex> g(qmu_);
-      q_[0].clear();
-      q_[1].clear();
+      for (auto& q : q_) q.clear();
     }
     qcv_.notify_all();
     std::lock_guard<std::mutex> g(pmu_);
@@ -336,13 +344,15 @@ class Server {
   }
 
   // kind-1 requests grouped by index: [(index, [ids], [ncalls], text)]
-  py::list take_counts(int max_n, int timeout_ms) {
+  py::list take_counts(int max_n, int timeout_ms) { return take_grouped(1, max_n, timeout_ms); }
+
+  py::list take_grouped(int kind, int max_n, int timeout_ms) {
     std::vector<std::shared_ptr<Req>> got;
     std::vector<std::pair<std::string, std::vector<size_t>>> groups;
     std::vector<std::string> texts;
     {
       py::gil_scoped_release nogil;
-      pop(1, size_t(std::max(1, max_n)), timeout_ms, got);
+      pop(kind, size_t(std::max(1, max_n)), timeout_ms, got);
       for (size_t i = 0; i < got.size(); i++) {
         size_t g = 0;
         while (g < groups.size() && groups[g].first != got[i]->index) g++;
@@ -371,6 +381,9 @@ class Server {
     }
     return out;
   }
+
+  // kind-2 requests (flat TopN calls), grouped by index like take_counts
+  py::list take_topn(int max_n, int timeout_ms) { return take_grouped(2, max_n, timeout_ms); }
 
   // Give count requests back to the general path (kind 0).
   void requeue(const std::vector<uint64_t>& ids) {
@@ -423,6 +436,7 @@ class Server {
   }
 
   void set_count_batching(bool on) { count_batching_ = on; }
+  void set_topn_batching(bool on) { topn_batching_ = on; }
 
   // origins allowed by CORS (set before start())
   void set_cors(const std::vector<std::string>& origins) { cors_origins_ = origins; }
@@ -440,11 +454,13 @@ class Server {
     py::dict d;
     d["requests"] = requests_.load();
     d["count_requests"] = count_requests_.load();
+    d["topn_requests"] = topn_requests_.load();
     d["connections"] = connections_.load();
     d["responses"] = responses_.load();
     std::lock_guard<std::mutex> g(qmu_);
     d["queued_generic"] = q_[0].size();
     d["queued_counts"] = q_[1].size();
+    d["queued_topn"] = q_[2].size();
     return d;
   }
 
@@ -873,10 +889,13 @@ class Server {
     return ok;
   }
 
-  // kind 1 when the request is a JSON Count-only query with no arguments
+  // kind 1 when the request is a JSON Count-only query with no arguments,
+  // kind 2 when it is only flat TopN(...) calls (cache-only TopN batching)
   void classify(Req& r, const std::string& ctype, const std::string& accept) {
     r.kind = 0;
-    if (!count_batching_ || r.method != "POST" || !r.query.empty() || ctype == "application/x-protobuf" || !accept_json(accept)) return;
+    if ((!count_batching_ && !topn_batching_) || r.method != "POST" || !r.query.empty() ||
+        ctype == "application/x-protobuf" || !accept_json(accept))
+      return;
     std::string p = r.path;
     while (p.size() > 1 && p.back() == '/') p.pop_back();
     static const std::string pre = "/index/", suf = "/query";
@@ -885,19 +904,27 @@ class Server {
       return;
     std::string name = p.substr(pre.size(), p.size() - pre.size() - suf.size());
     if (name.empty() || name.find('/') != std::string::npos) return;
-    bool all_count = false;
-    const int n = split_calls(r.body, &all_count);
-    if (n <= 0 || !all_count) return;
-    r.kind = 1;
+    bool all_count = false, all_topn = false;
+    const int n = split_calls(r.body, &all_count, &all_topn);
+    if (n <= 0) return;
+    if (all_count && count_batching_) {
+      r.kind = 1;
+      count_requests_++;
+    } else if (all_topn && topn_batching_) {
+      r.kind = 2;
+      topn_requests_++;
+    } else {
+      return;
+    }
     r.ncalls = n;
     r.index = std::move(name);
-    count_requests_++;
   }
 
  private:
   int lfd_ = -1, port_ = 0, nthreads_;
   size_t max_body_;
-  std::atomic<bool> running_{false}, stopping_{false}, count_batching_{true}, statics_empty_{true};
+  std::atomic<bool> running_{false}, stopping_{false}, count_batching_{true}, topn_batching_{false},
+      statics_empty_{true};
   std::vector<std::string> cors_origins_;
   std::mutex smu_;
   std::unordered_map<std::string, std::pair<std::string, std::string>> statics_;
@@ -905,11 +932,11 @@ class Server {
   std::vector<int> epfds_, wakefds_;
   std::mutex qmu_;
   std::condition_variable qcv_;
-  std::deque<std::shared_ptr<Req>> q_[2];
+  std::deque<std::shared_ptr<Req>> q_[3];
   std::mutex pmu_;
   std::unordered_map<uint64_t, std::shared_ptr<Req>> pending_;
   std::atomic<uint64_t> next_id_{1};
-  std::atomic<uint64_t> requests_{0}, count_requests_{0}, connections_{0}, responses_{0};
+  std::atomic<uint64_t> requests_{0}, count_requests_{0}, topn_requests_{0}, connections_{0}, responses_{0};
 };
 
 
@@ -1098,6 +1125,8 @@ PYBIND11_MODULE(_httpd, m) {
       .def("stop", &httpd::Server::stop, py::call_guard<py::gil_scoped_release>())
       .def("take", &httpd::Server::take, py::arg("max_n") = 1, py::arg("timeout_ms") = 100)
       .def("take_counts", &httpd::Server::take_counts, py::arg("max_n") = 1 << 16, py::arg("timeout_ms") = 100)
+      .def("take_topn", &httpd::Server::take_topn, py::arg("max_n") = 1 << 16, py::arg("timeout_ms") = 100)
+      .def("set_topn_batching", &httpd::Server::set_topn_batching)
       .def("requeue", &httpd::Server::requeue)
       .def("respond", &httpd::Server::respond)
       .def("respond_counts", &httpd::Server::respond_counts)

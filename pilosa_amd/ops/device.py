@@ -954,7 +954,29 @@ class GpuEngine:
         arr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
         for i, v in enumerate(views):
             arr[i] = v.viewdev()
-        return self._h2d(arr.view(np.uint8))
+        # the same view table (same arenas, same buffers) is uploaded once:
+        # a BSI / single-view request otherwise pays one H2D for it per call
+        key = arr.tobytes()
+        memo = self.__dict__.setdefault("_vt_memo", {})
+        hit = memo.get(key)
+        torch = self.torch
+        cuda = self.device.type == "cuda"
+        if hit is not None:
+            t, ev = hit
+            if cuda:   # another stream may read it: after the upload, and not recycled under it
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                t.record_stream(cur)
+            return t
+        t = self._h2d(arr.view(np.uint8))
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        if len(memo) >= 64:
+            memo.pop(next(iter(memo)))
+        memo[key] = (t, ev)
+        return t
 
     def compile_batch(self, exprs: Sequence[object]):
         view_index: Dict[int, int] = {}
@@ -1318,7 +1340,13 @@ class GpuEngine:
 
     @staticmethod
     def bsi_args(bsi_view: "DeviceView", depth: int, slot: int = 0) -> np.ndarray:
-        """cpu int64[67]: view slot, depth, dense rows of exists / sign / bit i."""
+        """cpu int64[67]: view slot, depth, dense rows of exists / sign / bit i
+        (memoised per view generation)."""
+        key = (bsi_view.generation, depth, slot)
+        memo = bsi_view.__dict__.setdefault("_bsi_args", {}) if hasattr(bsi_view, "__dict__") else {}
+        hit = memo.get(key)
+        if hit is not None:
+            return hit.copy()
         args = np.full(67, -1, dtype=np.int64)
         args[0] = slot
         args[1] = depth
@@ -1326,6 +1354,8 @@ class GpuEngine:
         args[3] = bsi_view.dense(1)
         for i in range(min(depth, 63)):
             args[4 + i] = bsi_view.dense(2 + i)
+        memo.clear()
+        memo[key] = args.copy()
         return args
 
     BSI_OPS = {"==": 0, "!=": 1, "<": 2, "<=": 3, ">": 4, ">=": 5, "between": 6, "notnull": 7}
@@ -1450,7 +1480,7 @@ class GpuEngine:
         if S and args[2] >= 0:
             tp, tv = self.upload_batch(progs, ordered)
             self.ext.bsi_minmax(tp, tv, S, torch.from_numpy(args), out, {"min": 1, "max": 2}.get(which, 0))
-        return out.cpu().numpy().reshape(S, 16, 10)
+        return self.to_host(out).numpy().reshape(S, 16, 10)
 
     def bsi_sum_async(self, filters: Sequence[Optional[object]], bsi_view: "DeviceView", depth: int,
                       matrix: Optional[bool] = None):

@@ -416,8 +416,11 @@ class GpuExecutor:
         return Leaf(rv, 0)
 
     def bsi_minmax(self, index: str, c: Call, shards: List[int], which: str):
-        """Min/Max -> per-shard ValCounts in shard order (the executor folds
-        them with ValCount.smaller/larger, like its per-shard map)."""
+        """Min/Max over the local shards -> ONE ValCount, folded vectorised
+        exactly as the executor's per-shard reduce folds them in shard order
+        (ValCount.smaller / larger keep the FIRST shard holding the extreme,
+        with that shard's count: executor.go ValCount.Smaller).  Building and
+        reducing ~1k per-shard objects in Python took most of the request."""
         from pilosa_amd.executor import ValCount
         fname = c.args.get("field")
         f = self.holder.field(index, fname) if isinstance(fname, str) else None
@@ -426,12 +429,12 @@ class GpuExecutor:
         b = f.bsi_group(fname)
         bv = self.view_arena(index, fname, VIEW_BSI_PREFIX + fname, shards)
         if bv is None:
-            return [ValCount() for _ in shards]
+            return ValCount()
         filt = None
         if len(c.children) == 1:
             filt = self.plan(index, c.children[0], shards)
             if filt is EMPTY:
-                return [ValCount() for _ in shards]
+                return ValCount()
         try:
             self.launches += 1
             o = self.engine.bsi_minmax(filt, bv, b.bit_depth, which)
@@ -443,7 +446,13 @@ class GpuExecutor:
             # (fragment.min/max counts every column of the wide shard holding it)
             vals, cnts = _fold_subshards_value(np.asarray(vals, np.int64), np.asarray(cnts, np.int64),
                                                which == "min")
-        return [ValCount(int(v) + b.base, int(n)) if n else ValCount() for v, n in zip(vals, cnts)]
+        vals, cnts = np.asarray(vals, np.int64), np.asarray(cnts, np.int64)
+        live = cnts > 0
+        if not live.any():
+            return ValCount()
+        best = vals[live].min() if which == "min" else vals[live].max()
+        k = int(np.flatnonzero(live & (vals == best))[0])
+        return ValCount(int(vals[k]) + b.base, int(cnts[k]))
 
     def hbm_bytes(self) -> int:
         with self.mu:
@@ -916,6 +925,8 @@ class GpuExecutor:
         return out or Pair(0, 0)
 
     def bsi_sum(self, index: str, c: Call, shards: List[int]):
+        import torch
+
         from pilosa_amd.executor import ValCount, _wrap
         fname = c.args.get("field")
         f = self.holder.field(index, fname) if isinstance(fname, str) else None
@@ -935,7 +946,7 @@ class GpuExecutor:
             s, n = self.engine.bsi_sum_async([filt], bv, b.bit_depth)
         except CompileError:
             raise NotImplementedError
-        s, n = int(s.cpu()[0]), int(n.cpu()[0])
+        s, n = (int(x) for x in self.engine.to_host(torch.stack([s[:1], n[:1]])).view(-1).tolist())
         return ValCount(_wrap(s + n * b.base), n)
 
     def bsi_sum_batch(self, index: str, calls: List[Call], shards: List[int]):

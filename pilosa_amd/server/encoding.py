@@ -28,6 +28,14 @@ def result_to_json(r: Any):
     return r
 
 
+def result_json_bytes(r) -> bytes:
+    """One result as Go's encoding/json writes it (PairArray natively)."""
+    from pilosa_amd.utils import gojson
+    if isinstance(r, PairArray):
+        return r.json_bytes()
+    return gojson.dumps(result_to_json(r)).encode()
+
+
 def response_json_bytes(resp: QueryResponse) -> bytes:
     """The query response body as Go's json.Encoder writes it (trailing
     newline).  Columnar TopN results (PairArray) are written straight from
@@ -36,8 +44,7 @@ def response_json_bytes(resp: QueryResponse) -> bytes:
     if resp.err is not None or resp.column_attr_sets or \
             not any(isinstance(r, PairArray) for r in resp.results):
         return gojson.encode_line(response_to_json(resp)).encode()
-    parts = [r.json_bytes() if isinstance(r, PairArray) else gojson.dumps(result_to_json(r)).encode()
-             for r in resp.results]
+    parts = [result_json_bytes(r) for r in resp.results]
     return b'{"results":[' + b",".join(parts) + b"]}\n"
 
 

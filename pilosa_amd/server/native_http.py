@@ -88,7 +88,7 @@ class NativeHTTPServer:
     ``server_address``, ``serve_forever()``, ``shutdown()``, ``server_close()``."""
 
     def __init__(self, handler: Handler, bind: str, io_threads: int = 4, workers: int = 16,
-                 batchers: int = 3, max_batch: int = 1 << 16):
+                 batchers: int = 3, max_batch: int = 1 << 16, topn_batchers: int = 2):
         from pilosa_amd import _httpd
 
         host, _, port = bind.rpartition(":")
@@ -100,6 +100,10 @@ class NativeHTTPServer:
         self.server_address = (host, self.srv.port())
         self.srv.set_cors(list(getattr(handler, "allowed_origins", None) or []))
         self.n_workers, self.n_batchers, self.max_batch = workers, batchers, max_batch
+        self.n_topn_batchers = topn_batchers
+        self.topn_batches = 0
+        self.topn_batched_requests = 0
+        self.topn_requeued = 0
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         self.batches = 0
@@ -112,6 +116,8 @@ class NativeHTTPServer:
         # Count batching only pays with a device behind the executor
         server = self.handler.server
         self.srv.set_count_batching(server is None or getattr(server, "gpu", None) is not None)
+        # cache-only TopN requests too: one device batch per group of them
+        self.srv.set_topn_batching(server is not None and getattr(server, "gpu", None) is not None)
         # the liveness probe (GET /version, cluster membership) is answered by
         # the epoll workers: a saturated worker pool cannot fail it
         import json
@@ -125,6 +131,8 @@ class NativeHTTPServer:
             self._spawn(self._generic_loop, f"http-worker-{i}")
         for i in range(self.n_batchers):
             self._spawn(self._count_loop, f"http-count-{i}")
+        for i in range(self.n_topn_batchers):
+            self._spawn(self._topn_loop, f"http-topn-{i}")
         self._stop.wait()
 
     def _spawn(self, fn, name):
@@ -144,7 +152,9 @@ class NativeHTTPServer:
     def stats(self) -> dict:
         d = dict(self.srv.stats())
         d.update(batches=self.batches, batched_requests=self.batched_requests, requeued=self.requeued,
-                 count_ms_per_batch=round(1000 * self.count_s / max(self.batches, 1), 3))
+                 count_ms_per_batch=round(1000 * self.count_s / max(self.batches, 1), 3),
+                 topn_batches=self.topn_batches, topn_batched_requests=self.topn_batched_requests,
+                 topn_requeued=self.topn_requeued)
         return d
 
     # ------------------------------------------------------------ loops
@@ -181,6 +191,44 @@ class NativeHTTPServer:
                 self.batches += 1
                 self.batched_requests += len(ids)
                 srv.respond_counts(ids, ncalls, counts)
+
+    def _topn_loop(self):
+        """Concurrent flat-TopN requests of an index, answered as ONE device
+        batch (Executor._topn_text_fast: the calls of every request in one
+        fused cache-only launch); bodies are formatted from the columnar
+        results without building Pair objects.  A group the fast path cannot
+        answer goes back to the general queue."""
+        srv = self.srv
+        from pilosa_amd.server.encoding import result_json_bytes
+        while not self._stop.is_set():
+            for index, ids, ncalls, text in srv.take_topn(self.max_batch, 500):
+                res = self._topn_group(index, text, sum(ncalls))
+                if res is None:
+                    self.topn_requeued += len(ids)
+                    srv.requeue(ids)
+                    continue
+                self.topn_batches += 1
+                self.topn_batched_requests += len(ids)
+                k = 0
+                for rid, nc in zip(ids, ncalls):
+                    body = b'{"results":[' + b",".join(result_json_bytes(r) for r in res[k:k + nc]) + b"]}\n"
+                    k += nc
+                    srv.respond(rid, 200, "application/json", body)
+
+    def _topn_group(self, index: str, text: str, ncalls: int):
+        server = self.handler.server
+        api = self.handler.api
+        ex = getattr(server, "executor", None) if server is not None else None
+        if ex is None or api is None:
+            return None
+        try:
+            api.validate("Query")
+            res = ex._topn_text_fast(index, text)
+        except Exception:  # noqa: BLE001 - the general path reports it
+            return None
+        if res is None or len(res) != ncalls:
+            return None
+        return res
 
     def _count_group(self, index: str, text: str, ncalls: int) -> Optional[List[int]]:
         server = self.handler.server

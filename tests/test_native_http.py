@@ -264,3 +264,44 @@ def test_pipelined_requests_run_in_order():
         assert json.loads(rs[80][1])["results"][0]["columns"] == list(range(40))
     finally:
         srv.close()
+
+
+def test_topn_group_commit_and_fallback():
+    """Concurrent flat-TopN requests are taken as one group per index
+    (native/httpd.cpp kind 2) and answered by ONE fast-path call; a group
+    the fast path declines goes to the general path with identical answers."""
+    from pilosa_amd import _httpd
+    from pilosa_amd.pql import parse_string
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        for m, p, b in SCRIPT[:4]:
+            _raw(port, _req(m, p, b, close=True))
+        ex = srv.executor
+        texts = []
+
+        def fast(index, text, shards=None):
+            texts.append(text)
+            return ex.execute(index, parse_string(text)).results
+        ex._topn_text_fast = fast
+        srv.httpd.srv.set_topn_batching(True)
+        bodies = [b"TopN(f, n=2)", b"TopN(f, n=1) TopN(f)", b"TopN(f, n=5, threshold=2)"]
+        # the general path's answers (stdlib JSON encoding of the same results)
+        want = [json.loads(_responses(_raw(port, _req("POST", "/index/i/query", b, close=True)))[0][1])["results"]
+                for b in bodies]
+        assert want[0] and want[0][0], want
+        res = _httpd.load("127.0.0.1", port, "/index/i/query", bodies, 24, 4, 1.0, 300)
+        assert res["errors"] == 0 and res["requests"] >= 6
+        for k, body in res["samples"]:
+            assert json.loads(body)["results"] == want[k], (k, body)
+        st = srv.httpd.stats()
+        assert st["topn_requests"] >= res["requests"] and st["topn_batched_requests"] > 0
+        assert any(t.count("TopN(") > 3 for t in texts), "no multi-request TopN group was formed"
+        # nested calls (a src row) are not batched; a declined group falls back
+        rs = _responses(_raw(port, _req("POST", "/index/i/query", b"TopN(f, Row(f=2), n=1)", close=True)))
+        assert rs[0][0] == 200 and len(json.loads(rs[0][1])["results"]) == 1
+        ex._topn_text_fast = lambda index, text, shards=None: None
+        rs = _responses(_raw(port, _req("POST", "/index/i/query", b"TopN(nope, n=1)", close=True)))
+        assert rs[0][0] == 400 and srv.httpd.stats()["topn_requeued"] >= 1
+    finally:
+        srv.close()
