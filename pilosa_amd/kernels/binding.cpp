@@ -346,7 +346,9 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
               torch::Tensor a2dense, torch::Tensor ns, torch::Tensor min_threshold, int64_t mode, torch::Tensor acc,
               torch::Tensor pair_off, torch::Tensor pair_idx, torch::Tensor out, torch::Tensor hist, int64_t R,
               torch::Tensor hot_meta, torch::Tensor hot_cnt, torch::Tensor tail_built, torch::Tensor cache_dense,
-              torch::Tensor hot_split) {
+              torch::Tensor hot_split, int64_t M) {
+  TORCH_CHECK(M >= 1 && M <= 4096, "topn_src: sub-shards per fragment");
+  const int64_t Sd = S * M;   // arena sub-shards
   for (auto* t : {&src_counts, &src_offs, &src_vals, &colptr, &entbase, &slots, &cache_cnt, &cache_acc, &slotmap,
                   &a2dense, &ns, &min_threshold})
     check_dev(*t, "topn_src input");
@@ -358,18 +360,20 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
     check_dev(hot_meta, "hot_meta");
     check_dev(hot_cnt, "hot_cnt");
     TORCH_CHECK(Q <= 32, "hot-rank counting takes at most 32 queries per launch");
-    TORCH_CHECK(hot_meta.scalar_type() == torch::kInt32 && hot_meta.numel() == S * 16 * R, "hot_meta int32[S*16*R]");
-    TORCH_CHECK(hot_cnt.scalar_type() == torch::kInt32 && hot_cnt.numel() == S * Q * R, "hot_cnt int32[S*Q*R]");
+    TORCH_CHECK(hot_meta.scalar_type() == torch::kInt32 && hot_meta.numel() == Sd * 16 * R, "hot_meta int32[S*M*16*R]");
+    // mode 4 writes one matrix per sub-shard; modes 1-3 read them summed per fragment
+    TORCH_CHECK(hot_cnt.scalar_type() == torch::kInt32 && hot_cnt.numel() == (mode == 4 ? Sd : S) * Q * R,
+                "hot_cnt int32[S*Q*R] (mode 4: [S*M*Q*R])");
     check_dev(hot_split, "hot_split");
-    TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == S * 16, "hot_split int32[S*16]");
+    TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == Sd * 16, "hot_split int32[S*M*16]");
   }
-  TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * S * 16,
-              "src_counts int32[Q*S*16]");
-  TORCH_CHECK(src_offs.scalar_type() == torch::kInt64 && src_offs.numel() == Q * S * 16, "src_offs int64[Q*S*16]");
+  TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * Sd * 16,
+              "src_counts int32[Q*S*M*16]");
+  TORCH_CHECK(src_offs.scalar_type() == torch::kInt64 && src_offs.numel() == Q * Sd * 16, "src_offs int64[Q*S*M*16]");
   TORCH_CHECK(src_vals.scalar_type() == torch::kInt16, "src_vals int16");
-  TORCH_CHECK(colptr.scalar_type() == torch::kInt32 && colptr.numel() == S * ((int64_t(1) << 20) + 1),
-              "colptr int32[S*(2^20+1)]");
-  TORCH_CHECK(entbase.scalar_type() == torch::kInt64 && entbase.numel() >= S, "entbase int64[S]");
+  TORCH_CHECK(colptr.scalar_type() == torch::kInt32 && colptr.numel() == Sd * ((int64_t(1) << 20) + 1),
+              "colptr int32[S*M*(2^20+1)]");
+  TORCH_CHECK(entbase.scalar_type() == torch::kInt64 && entbase.numel() >= Sd, "entbase int64[S*M]");
   TORCH_CHECK(slots.scalar_type() == torch::kInt16, "slots int16");
   TORCH_CHECK(slots.numel() >= 16 && slots.numel() % 8 == 0 && (reinterpret_cast<uintptr_t>(slots.data_ptr()) & 15) == 0,
               "slots: 16-byte aligned, padded by 16 entries, multiple of 8");
@@ -382,7 +386,8 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
   pk::TopNLaunch a{};
   a.v = viewdev_from(view);
   a.Q = int(Q);
-  a.S = int(S);
+  a.S = int(mode == 4 ? Sd : S);   // the hot-rank kernel runs per sub-shard
+  a.M = int(mode == 4 ? 1 : M);
   a.K = int(K);
   a.H32 = int(H32);
   a.H16 = int(H16);

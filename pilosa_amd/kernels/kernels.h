@@ -79,7 +79,7 @@ void launch_topn_index(const ViewDev& v, int S, int K, int k0, const int32_t* ca
 // A sorted row ids (identical on every rank of a node).
 struct TopNLaunch {
   ViewDev v;                      // the TopN field's view (fallback probes)
-  int Q, S, K;                     // queries, shards, cache slots
+  int Q, S, K;                     // queries, shards (fragments), cache slots
   int H32, H16;                   // counter tiers: u32 < H32 <= u16 < H16 <= u8
   int64_t A;                      // acc-space size
   const int32_t* src_counts;      // [Q*S*16] materialised src containers
@@ -107,6 +107,8 @@ struct TopNLaunch {
   uint32_t* hot_cnt;              // [S][Q][R] src counts of the hot ranks (mode 4 writes, 1-3 read)
   int32_t* tail_built;            // [Q*S] mode 1: 1 = unit's tail histogram built (kept), 0 = skipped
   const int32_t* cache_dense;     // [S][K] dense row of each cache slot (mode 3 exact probes)
+  int M;                          // arena sub-shards per fragment (S fragments, S*M device shards: src, colptr,
+                                  // entbase, slots, hot_meta/split are per sub-shard; mode 4 runs with S*M, M=1)
   int dbg;                        // PILOSA_TOPN_DBG cost isolation: 1 skip histogram, 2 skip walk, 8 skip small hot rows,
                                   // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays (answers then wrong)
 };

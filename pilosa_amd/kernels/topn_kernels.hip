@@ -255,6 +255,17 @@ __device__ uint32_t src_row_count(const ViewDev& v, int s, int d, const int32_t*
   return total;
 }
 
+// the same over the p.M arena sub-shards of fragment s (query q's src)
+__device__ uint32_t src_row_count_frag(const TopNLaunch& p, int q, int s, int d) {
+  uint32_t total = 0;
+  for (int m = 0; m < p.M; m++) {
+    const int ds = s * p.M + m;
+    const int64_t kb = (int64_t(q) * p.S * p.M + ds) * 16;
+    total += src_row_count(p.v, ds, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
+  }
+  return total;
+}
+
 __device__ __forceinline__ int64_t unit_index(const TopNLaunch& p, int q, int s) { return int64_t(q) * p.S + s; }
 
 __device__ __forceinline__ int64_t unit_hist_base(const TopNLaunch& p, int q, int s, int words) {
@@ -321,15 +332,19 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
   // longer runs finish in a short tail loop.  (The previous shape, a per-lane
   // loop of u16 loads per column, serialised ~15 dependent round trips per 4
   // columns: 54 ms for 16 hot-src queries over 954 shards.)
-  const int64_t kb = (int64_t(q) * p.S + s) * 16;
-  const int64_t eb = p.entbase[s];
+  // a fragment wider than 2^20 columns is p.M consecutive arena sub-shards:
+  // its histogram sums the slot runs of all of them (the slot index and the
+  // materialised src are per sub-shard, the cache and the walk per fragment)
   const int64_t amax = ((p.slots_n - 16) & ~int64_t(7));
   const auto sl4 = gp(reinterpret_cast<const uint4*>(p.slots));
-  for (int j = 0; j < (need_tail ? 16 : 0); j++) {
+  for (int jm = 0; jm < (need_tail ? 16 * p.M : 0); jm++) {
+    const int j = jm & 15, ds = s * p.M + (jm >> 4);
+    const int64_t kb = (int64_t(q) * p.S * p.M + ds) * 16;
+    const int64_t eb = p.entbase[ds];
     const int n = p.src_counts[kb + j];
     if (n <= 0) continue;
     const auto vals = gp(p.src_vals + p.src_offs[kb + j]);
-    const auto cp = gp(p.colptr + int64_t(s) * CP_STRIDE + (int64_t(j) << 16));
+    const auto cp = gp(p.colptr + int64_t(ds) * CP_STRIDE + (int64_t(j) << 16));
     auto run4 = [&](const int (&x)[4]) {
       uint32_t e0[4], e1[4];
 #pragma unroll
@@ -450,7 +465,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
         c = slot_count(p, hist, L, q, s, k);
       } else {
         const int d = p.a2dense[a];
-        if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
+        if (d >= 0) c = src_row_count_frag(p, q, s, d);
       }
       if (c >= mt) atomicAdd(p.out + i, (unsigned long long)c);
     }
@@ -466,7 +481,6 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
   const auto h = gp(p.hist_in + unit_hist_base(p, q, s, L.words));
   const uint32_t mt = uint32_t(max(1, p.min_threshold[q]));
   const int32_t* sm = p.slotmap + int64_t(s) * p.A;
-  const int64_t kb = (int64_t(q) * p.S + s) * 16;
   const int64_t p0 = p.pair_off[q], p1 = p.pair_off[q + 1];
   for (int64_t i = p0 + threadIdx.x; i < p1; i += blockDim.x) {
     const int a = p.pair_idx[i];
@@ -476,11 +490,10 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
       c = slot_count(p, h, L, q, s, k);
     } else if (k >= 0) {
       // phase 1 skipped this unit's tail histogram: count the row exactly
-      c = src_row_count(p.v, s, int(p.cache_dense[int64_t(s) * p.K + k]), p.src_counts + kb, p.src_offs + kb,
-                        p.src_vals);
+      c = src_row_count_frag(p, q, s, int(p.cache_dense[int64_t(s) * p.K + k]));
     } else {
       const int d = p.a2dense[a];
-      if (d >= 0) c = src_row_count(p.v, s, d, p.src_counts + kb, p.src_offs + kb, p.src_vals);
+      if (d >= 0) c = src_row_count_frag(p, q, s, d);
     }
     if (c >= mt) atomicAdd(p.out + i, (unsigned long long)c);
   }

@@ -159,7 +159,12 @@ class GpuExecutor:
         self._bsi_views: Dict[Tuple, DeviceView] = {}  # predicate results (small LRU)
         self.mu = threading.RLock()
         self.launches = 0
+        # serving Count text path: host prep (parse..launch) vs result wait
+        self.text_batches = 0
+        self.text_prep_s = 0.0
+        self.text_wait_s = 0.0
         self.topn_index_refreshes = 0   # slot indexes brought up to date in place after writes
+        self.topn_index_batches = 0     # src TopN batches / calls answered by a slot index
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
         self.row_updates = 0     # ... of which only the changed rows were re-sent
@@ -608,6 +613,7 @@ class GpuExecutor:
         time-range leaves, unknown fields, ...)."""
         from pilosa_amd import _pql
         from pilosa_amd.models.field import FIELD_TYPE_INT
+        t0 = time.perf_counter()
         idx = self.holder.index(index)
         if idx is None or idx.keys:
             return None
@@ -639,7 +645,14 @@ class GpuExecutor:
         out = eng.launch_count(eng.prepare_planned(Q, segs, buf, vlist, vlist[0].S))
         # device_out: the int64[Q] device tensor, still being computed (the
         # caller reduces it on the device, e.g. the mesh all-reduce)
-        return out if device_out else eng.to_host(out).tolist()
+        if device_out:
+            return out
+        t1 = time.perf_counter()
+        res = eng.to_host(out).tolist()
+        self.text_batches += 1
+        self.text_prep_s += t1 - t0
+        self.text_wait_s += time.perf_counter() - t1
+        return res
 
     def _text_ranges(self, idx, index: str, text: str, shards: List[int], vlist: List[DeviceView]):
         """The time-range Row(t=<id>, from=, to=) leaves of a request text
@@ -1034,6 +1047,7 @@ class GpuExecutor:
         tix = self._topn_index(index, fname, shards, rc, rv)
         if tix is not None:
             self.launches += 1
+            self.topn_index_batches += 1
             try:
                 return sort_pairs(tix.shard_pairs(self.engine, src, 0 if ids else n, threshold, ids or None))
             except CompileError:
@@ -1107,6 +1121,7 @@ class GpuExecutor:
                     self.topn_decline = f"no slot index ({self._topn_index_why})"
                     return None
                 self.launches += 1
+                self.topn_index_batches += 1
                 try:
                     got = tix.topn(self.engine, [srcs[i] for i in live], ns, ths, comm=self.comm, defer=defer)
                 except CompileError:
@@ -1419,11 +1434,8 @@ class GpuExecutor:
         if rv is None or rc is None or not self.topn_index_enabled or rc.K == 0:
             self._topn_index_why = "disabled/empty"
             return None
-        if rc.M > 1:
-            # the slot index walks each fragment's ranks over one 2^20-column
-            # arena shard; wider fragments take the pair-count path
-            self._topn_index_why = f"shard width 2^{shardwidth.EXPONENT}"
-            return None
+        # (fragments wider than 2^20 columns: the index is per arena
+        # sub-shard, the histograms and walks per fragment)
         from pilosa_amd.ops.topn_index import MAX_SLOTS, DeviceTopNIndex
         key = (index, fname, tuple(shards))
         ent = self._topn_indexes.get(key)

@@ -132,7 +132,7 @@ class DeviceTopNIndex:
         if hasattr(cache, "cache_dense"):
             # device rank caches (ops/topn_exec.DeviceRankCaches): no host pass
             S, K = int(cache.cache_dense.shape[0]), int(cache.cache_dense.shape[1])
-            if S != view.S:
+            if (S == 0 and view.S) or (S and view.S % S):
                 raise ValueError("rank cache and view disagree on the shard count")
             self.cache_dense = cache.cache_dense.contiguous()
             self.cache_cnt = cache.cache_cnt.contiguous()
@@ -152,7 +152,7 @@ class DeviceTopNIndex:
             cnt_for_tiers = None
         else:
             S, K = cache.rows.shape
-            if S != view.S:
+            if (S == 0 and view.S) or (S and view.S % S):
                 raise ValueError("rank cache and view disagree on the shard count")
             counts = np.asarray(cache.counts, dtype=np.int64)
             valid = counts > 0
@@ -172,6 +172,12 @@ class DeviceTopNIndex:
         if K > MAX_SLOTS:
             raise ValueError(f"rank cache of {K} slots exceeds the u16 slot index ({MAX_SLOTS})")
         self.S, self.K = S, K
+        # fragments wider than 2^20 columns: M arena sub-shards each.  The
+        # slot index, hot-rank metadata and materialised srcs are per
+        # sub-shard (Sd of them); caches, histograms and walks per fragment
+        self.M = M = view.S // S if S else 1
+        self.Sd = Sd = view.S
+        dense_sub = self.cache_dense if M == 1 else self.cache_dense.repeat_interleave(M, dim=0).contiguous()
         # ranks [0, R): hot, counted row-major per batch; [R, K): slot index
         self.R = R = max(0, min(K, HOT_RANKS if hot is None else int(hot)))
         Kt = K - R
@@ -196,31 +202,31 @@ class DeviceTopNIndex:
         def empty(dt):
             return torch.empty(0, dtype=dt, device=dev)
 
-        self.hot_meta = torch.full((S * 16 * R,), -1, dtype=torch.int32, device=dev)
-        self.hot_split = torch.zeros(S * 16, dtype=torch.int32, device=dev)
-        if S and R:
-            ext.topn_hot_meta(self._vd, S, K, R, self.cache_dense, self.hot_meta, self.hot_split)
-        colcnt = torch.zeros(S * SHARD_WIDTH, dtype=torch.int32, device=dev)
-        if S and Kt:
-            ext.topn_index(self._vd, S, K, R, self.cache_dense, colcnt, empty(torch.int32), empty(torch.int64),
+        self.hot_meta = torch.full((Sd * 16 * R,), -1, dtype=torch.int32, device=dev)
+        self.hot_split = torch.zeros(Sd * 16, dtype=torch.int32, device=dev)
+        if Sd and R:
+            ext.topn_hot_meta(self._vd, Sd, K, R, dense_sub, self.hot_meta, self.hot_split)
+        colcnt = torch.zeros(Sd * SHARD_WIDTH, dtype=torch.int32, device=dev)
+        if Sd and Kt:
+            ext.topn_index(self._vd, Sd, K, R, dense_sub, colcnt, empty(torch.int32), empty(torch.int64),
                            empty(torch.int16), False)
-        self.colptr = torch.zeros((S, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
-        if S:
-            self.colptr[:, 1:] = torch.cumsum(colcnt.view(S, SHARD_WIDTH), dim=1, dtype=torch.int32)
+        self.colptr = torch.zeros((Sd, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
+        if Sd:
+            self.colptr[:, 1:] = torch.cumsum(colcnt.view(Sd, SHARD_WIDTH), dim=1, dtype=torch.int32)
         tot = self.colptr[:, SHARD_WIDTH].to(torch.int64)
         # each shard's slot region has 1/8 spare room, so a shard whose
         # cached rows change can be re-indexed in place (refresh)
         self.cap = tot + tot // 8 + 64
-        self.entbase = torch.zeros(max(S, 1), dtype=torch.int64, device=dev)
-        if S > 1:
-            self.entbase[1:S] = torch.cumsum(self.cap, 0)[:-1]
-        self.entries = int(self.cap.sum().item()) if S else 0
+        self.entbase = torch.zeros(max(Sd, 1), dtype=torch.int64, device=dev)
+        if Sd > 1:
+            self.entbase[1:Sd] = torch.cumsum(self.cap, 0)[:-1]
+        self.entries = int(self.cap.sum().item()) if Sd else 0
         # +16 entries: the histogram reads each slot run as aligned 16-byte words
         self.slots = torch.zeros((self.entries + 16 + 7) // 8 * 8, dtype=torch.int16, device=dev)
-        if S and Kt:
+        if Sd and Kt:
             colcnt.zero_()
-            ext.topn_index(self._vd, S, K, R, self.cache_dense, colcnt, self.colptr, self.entbase, self.slots, True)
-        del colcnt
+            ext.topn_index(self._vd, Sd, K, R, dense_sub, colcnt, self.colptr, self.entbase, self.slots, True)
+        del colcnt, dense_sub
         self.slotmap = torch.full((S, max(A, 1)), -1, dtype=torch.int32, device=dev)
         si, ki = torch.nonzero(self.cache_dense >= 0, as_tuple=True)
         self.slotmap[si, self.cache_acc[si, ki].long()] = ki.to(torch.int32)
@@ -253,10 +259,12 @@ class DeviceTopNIndex:
                 or tuple(cache.cache_dense.shape) != (self.S, self.K) or self.A != view.D
                 or not (self.A == 0 or np.array_equal(self.space, view.rows))):
             return False
-        S, K, R = self.S, self.K, self.R
+        S, K, R, M, Sd = self.S, self.K, self.R, self.M, self.Sd
         dev = view.device
         new_dense = cache.cache_dense.contiguous()
-        changed = torch.from_numpy(view.shard_gen != self.shard_gen).to(dev)
+        # a fragment is re-indexed (all its M sub-shards) when any of its
+        # sub-shards' bits or its cached row order changed
+        changed = torch.from_numpy((view.shard_gen != self.shard_gen).reshape(S, M).any(axis=1)).to(dev)
         changed |= (new_dense != self.cache_dense).any(dim=1)
         C = torch.nonzero(changed).reshape(-1)
         nc = int(C.numel())
@@ -264,38 +272,41 @@ class DeviceTopNIndex:
             return False
         ext = kernels()
         if nc:
+            Cd = (C[:, None] * M + torch.arange(M, device=dev)[None, :]).reshape(-1) if M > 1 else C
+            nd = nc * M
             D1 = view.D + 1
             sub = np.zeros((), dtype=view.viewdev().dtype)
             sub[()] = view.viewdev()
-            rp_sub = view.t_rowptr.view(S, D1).index_select(0, C).contiguous()
-            sb_sub = torch.cat([view.t_shard_base.index_select(0, C), view.t_shard_base[-1:]]).contiguous()
+            rp_sub = view.t_rowptr.view(Sd, D1).index_select(0, Cd).contiguous()
+            sb_sub = torch.cat([view.t_shard_base.index_select(0, Cd), view.t_shard_base[-1:]]).contiguous()
             sub["rowptr"] = rp_sub.data_ptr()
             sub["shard_base"] = sb_sub.data_ptr()
             sub["keymask"] = 0
             vd_sub = torch.from_numpy(np.frombuffer(sub.tobytes(), dtype=np.uint8).copy())
-            cd_sub = new_dense.index_select(0, C).contiguous()
+            cd_sub = new_dense.index_select(0, C)
+            cd_sub = (cd_sub.repeat_interleave(M, dim=0) if M > 1 else cd_sub).contiguous()
             Kt = K - R
-            colcnt = torch.zeros(nc * SHARD_WIDTH, dtype=torch.int32, device=dev)
+            colcnt = torch.zeros(nd * SHARD_WIDTH, dtype=torch.int32, device=dev)
             if Kt:
-                ext.topn_index(vd_sub, nc, K, R, cd_sub, colcnt, torch.empty(0, dtype=torch.int32, device=dev),
+                ext.topn_index(vd_sub, nd, K, R, cd_sub, colcnt, torch.empty(0, dtype=torch.int32, device=dev),
                                torch.empty(0, dtype=torch.int64, device=dev),
                                torch.empty(0, dtype=torch.int16, device=dev), False)
-            cp_sub = torch.zeros((nc, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
-            cp_sub[:, 1:] = torch.cumsum(colcnt.view(nc, SHARD_WIDTH), dim=1, dtype=torch.int32)
-            if bool((cp_sub[:, SHARD_WIDTH].to(torch.int64) > self.cap.index_select(0, C)).any().item()):
+            cp_sub = torch.zeros((nd, SHARD_WIDTH + 1), dtype=torch.int32, device=dev)
+            cp_sub[:, 1:] = torch.cumsum(colcnt.view(nd, SHARD_WIDTH), dim=1, dtype=torch.int32)
+            if bool((cp_sub[:, SHARD_WIDTH].to(torch.int64) > self.cap.index_select(0, Cd)).any().item()):
                 return False
-            eb_sub = self.entbase.index_select(0, C).contiguous()
+            eb_sub = self.entbase.index_select(0, Cd).contiguous()
             if Kt:
                 colcnt.zero_()
-                ext.topn_index(vd_sub, nc, K, R, cd_sub, colcnt, cp_sub, eb_sub, self.slots, True)
+                ext.topn_index(vd_sub, nd, K, R, cd_sub, colcnt, cp_sub, eb_sub, self.slots, True)
             del colcnt
-            self.colptr.index_copy_(0, C, cp_sub)
+            self.colptr.index_copy_(0, Cd, cp_sub)
             if R:
-                hm_sub = torch.full((nc * 16 * R,), -1, dtype=torch.int32, device=dev)
-                hs_sub = torch.zeros(nc * 16, dtype=torch.int32, device=dev)
-                ext.topn_hot_meta(vd_sub, nc, K, R, cd_sub, hm_sub, hs_sub)
-                self.hot_meta.view(S, 16 * R).index_copy_(0, C, hm_sub.view(nc, 16 * R))
-                self.hot_split.view(S, 16).index_copy_(0, C, hs_sub.view(nc, 16))
+                hm_sub = torch.full((nd * 16 * R,), -1, dtype=torch.int32, device=dev)
+                hs_sub = torch.zeros(nd * 16, dtype=torch.int32, device=dev)
+                ext.topn_hot_meta(vd_sub, nd, K, R, cd_sub, hm_sub, hs_sub)
+                self.hot_meta.view(Sd, 16 * R).index_copy_(0, Cd, hm_sub.view(nd, 16 * R))
+                self.hot_split.view(Sd, 16).index_copy_(0, Cd, hs_sub.view(nd, 16))
         # the rank caches of every shard (counts of unchanged shards may move
         # too), their acc indexes, the slot map rows and the counter tiers
         self.cache_dense = new_dense
@@ -349,7 +360,7 @@ class DeviceTopNIndex:
                            pair_off if pair_off is not None else e64, pair_idx if pair_idx is not None else e32,
                            out if out is not None else e64, hist if hist is not None else e32,
                            self.R, self.hot_meta, hot_cnt if hot_cnt is not None else e32,
-                           tail_built if tail_built is not None else e32, self.cache_dense, self.hot_split)
+                           tail_built if tail_built is not None else e32, self.cache_dense, self.hot_split, self.M)
 
     def materialize(self, engine: GpuEngine, srcs: Sequence[object]):
         """Src containers of a batch: plain rows of this view are read in
@@ -364,17 +375,18 @@ class DeviceTopNIndex:
             dev = self.view.device
             dense = self.view.dense_many(np.array([x.row for x in srcs], dtype=np.uint64))
             rows = torch.from_numpy(np.asarray(dense, dtype=np.int64)).to(dev)
-            counts = torch.zeros(Q * self.S * 16, dtype=torch.int32, device=dev)
-            offs = torch.zeros(Q * self.S * 16, dtype=torch.int64, device=dev)
+            counts = torch.zeros(Q * self.Sd * 16, dtype=torch.int32, device=dev)
+            offs = torch.zeros(Q * self.Sd * 16, dtype=torch.int64, device=dev)
             has_run = torch.zeros(1, dtype=torch.int32, device=dev)
-            kernels().leaf_src(self._vd, rows, self.S, counts, offs, has_run)
+            kernels().leaf_src(self._vd, rows, self.Sd, counts, offs, has_run)
             if not int(has_run.item()):
                 return counts, offs, self.view.t_payload
-        return engine.materialize_batch(srcs, self.S)
+        return engine.materialize_batch(srcs, self.Sd)
 
     def hot_counts(self, src, Q: int):
         """int32[S, Q, R]: src counts of the hot cache ranks (one row-major
-        pass per HOT_Q queries), or None without hot ranks."""
+        pass per HOT_Q queries, per arena sub-shard, summed per fragment),
+        or None without hot ranks."""
         import torch
 
         if not self.R or not Q or not self.S:
@@ -382,9 +394,11 @@ class DeviceTopNIndex:
         if Q > HOT_Q:
             raise ValueError(f"hot_counts: at most {HOT_Q} queries per call")
         dev = self.view.device
-        hot = torch.zeros(self.S * Q * self.R, dtype=torch.int32, device=dev)
+        hot = torch.zeros(self.Sd * Q * self.R, dtype=torch.int32, device=dev)
         z = torch.zeros(Q, dtype=torch.int32, device=dev)
         self._launch(4, Q, src, z, z, hot_cnt=hot)
+        if self.M > 1:
+            hot = hot.view(self.S, self.M, Q * self.R).sum(dim=1, dtype=torch.int32).reshape(-1).contiguous()
         return hot
 
     def hist_bytes(self, Q: int) -> int:

@@ -16,6 +16,7 @@ Threads:
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 import traceback
@@ -88,8 +89,13 @@ class NativeHTTPServer:
     ``server_address``, ``serve_forever()``, ``shutdown()``, ``server_close()``."""
 
     def __init__(self, handler: Handler, bind: str, io_threads: int = 4, workers: int = 16,
-                 batchers: int = 3, max_batch: int = 1 << 16, topn_batchers: int = 2):
+                 batchers: Optional[int] = None, max_batch: int = 1 << 16, topn_batchers: Optional[int] = None):
         from pilosa_amd import _httpd
+
+        if batchers is None:
+            batchers = int(os.environ.get("PILOSA_HTTP_COUNT_BATCHERS", "3"))
+        if topn_batchers is None:
+            topn_batchers = int(os.environ.get("PILOSA_HTTP_TOPN_BATCHERS", "2"))
 
         host, _, port = bind.rpartition(":")
         host = host or "0.0.0.0"
@@ -110,6 +116,7 @@ class NativeHTTPServer:
         self.batched_requests = 0
         self.requeued = 0
         self.count_s = 0.0
+        self._gen = 0
 
     # ------------------------------------------------------------ lifecycle
     def serve_forever(self):
@@ -129,14 +136,23 @@ class NativeHTTPServer:
         self.srv.start()
         for i in range(self.n_workers):
             self._spawn(self._generic_loop, f"http-worker-{i}")
-        for i in range(self.n_batchers):
-            self._spawn(self._count_loop, f"http-count-{i}")
-        for i in range(self.n_topn_batchers):
-            self._spawn(self._topn_loop, f"http-topn-{i}")
+        self.set_batchers(self.n_batchers, self.n_topn_batchers)
         self._stop.wait()
 
-    def _spawn(self, fn, name):
-        t = threading.Thread(target=fn, name=name, daemon=True)
+    def set_batchers(self, count: Optional[int] = None, topn: Optional[int] = None):
+        """Change the number of Count / TopN group-commit threads of a running
+        server: a new generation of loops starts and the old ones exit after
+        their current group."""
+        self.n_batchers = self.n_batchers if count is None else count
+        self.n_topn_batchers = self.n_topn_batchers if topn is None else topn
+        self._gen += 1
+        for i in range(self.n_batchers):
+            self._spawn(self._count_loop, f"http-count-{i}", self._gen)
+        for i in range(self.n_topn_batchers):
+            self._spawn(self._topn_loop, f"http-topn-{i}", self._gen)
+
+    def _spawn(self, fn, name, *args):
+        t = threading.Thread(target=fn, name=name, args=args, daemon=True)
         t.start()
         self._threads.append(t)
 
@@ -154,7 +170,14 @@ class NativeHTTPServer:
         d.update(batches=self.batches, batched_requests=self.batched_requests, requeued=self.requeued,
                  count_ms_per_batch=round(1000 * self.count_s / max(self.batches, 1), 3),
                  topn_batches=self.topn_batches, topn_batched_requests=self.topn_batched_requests,
-                 topn_requeued=self.topn_requeued)
+                 topn_requeued=self.topn_requeued, count_batchers=self.n_batchers,
+                 topn_batchers=self.n_topn_batchers)
+        server = self.handler.server
+        gpu = getattr(getattr(server, "executor", None), "gpu", None)
+        nb = getattr(gpu, "text_batches", 0)
+        if nb:
+            d.update(text_prep_ms_per_batch=round(1000 * gpu.text_prep_s / nb, 3),
+                     text_wait_ms_per_batch=round(1000 * gpu.text_wait_s / nb, 3))
         return d
 
     # ------------------------------------------------------------ loops
@@ -177,9 +200,9 @@ class NativeHTTPServer:
                     if not req.sent:
                         req.send(500, msg, "text/plain; charset=utf-8")
 
-    def _count_loop(self):
+    def _count_loop(self, gen: int = 0):
         srv = self.srv
-        while not self._stop.is_set():
+        while not self._stop.is_set() and gen == self._gen:
             for index, ids, ncalls, text in srv.take_counts(self.max_batch, 500):
                 t0 = time.perf_counter()
                 counts = self._count_group(index, text, sum(ncalls))
@@ -192,7 +215,7 @@ class NativeHTTPServer:
                 self.batched_requests += len(ids)
                 srv.respond_counts(ids, ncalls, counts)
 
-    def _topn_loop(self):
+    def _topn_loop(self, gen: int = 0):
         """Concurrent flat-TopN requests of an index, answered as ONE device
         batch (Executor._topn_text_fast: the calls of every request in one
         fused cache-only launch); bodies are formatted from the columnar
@@ -200,7 +223,7 @@ class NativeHTTPServer:
         answer goes back to the general queue."""
         srv = self.srv
         from pilosa_amd.server.encoding import result_json_bytes
-        while not self._stop.is_set():
+        while not self._stop.is_set() and gen == self._gen:
             for index, ids, ncalls, text in srv.take_topn(self.max_batch, 500):
                 res = self._topn_group(index, text, sum(ncalls))
                 if res is None:

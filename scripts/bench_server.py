@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--verify", type=int, default=256, help="HTTP responses checked against Executor.execute")
     ap.add_argument("--gpu", default="on")
     ap.add_argument("--data-dir", default=None)
+    ap.add_argument("--batchers", default="",
+                    help="comma list: one load run per Count group-commit thread count (native server)")
     args = ap.parse_args()
     import numpy as np
 
@@ -164,41 +166,56 @@ def main():
                 srv.executor.gpu = gpu
                 assert got == want, (q, got, want)
         port = srv.uri.port
-        t0 = time.perf_counter()
-        if args.client == "native":
-            from pilosa_amd import _httpd
-            res = _httpd.load("127.0.0.1", port, "/index/i/query", [q.encode() for q in queries], args.conns,
-                              args.client_threads, args.seconds, args.verify)
-            res["clients"] = args.conns
-        else:
-            res = python_clients(port, queries, args)
-        el = time.perf_counter() - t0
-        # the sampled HTTP answers against the executor's own
-        mism = 0
-        samples = res.pop("samples", [])
-        for k, body in samples:
-            want = srv.executor.execute("i", queries[k]).results
-            if json.loads(body)["results"] != want:
-                mism += 1
-        st = srv.httpd.stats() if hasattr(srv.httpd, "stats") else None
-        co = srv.executor._coalescer
-        fe = res.pop("first_error", b"")
-        print(json.dumps({
-            "metric": "HTTP Count(Intersect) requests/s", "value": round(res["requests"] / args.seconds, 1),
-            "clients": res["clients"], "client": args.client, "seconds": args.seconds,
-            "mean_latency_ms": round(res["mean_ms"], 3),
-            "p50_ms": round(res.get("p50_ms", 0), 3), "p99_ms": round(res.get("p99_ms", 0), 3),
-            "errors": res["errors"], "first_error": fe[:300].decode(errors="replace") if fe else "",
-            "verified": len(samples), "mismatches": mism,
-            "server": type(srv.httpd).__name__, "server_stats": st,
-            "gpu": gpu is not None, "coalescer": {"batches": co.batches, "batched": co.batched,
-                                                  "fallbacks": co.fallbacks} if co else None,
-            "index": args.index, "cols": args.cols if args.index == "disk" else args.shards << 20, "rows": nrows,
-            "setup": info, "wall_s": round(el, 1)}), flush=True)
+        sweep = [int(x) for x in args.batchers.split(",") if x] or [None]
+        for nb in sweep:
+            if nb is not None:
+                srv.httpd.set_batchers(nb)
+                time.sleep(0.5)
+            run_load(srv, port, queries, args, info, nrows, gpu)
     finally:
         srv.close()
         if not args.data_dir:
             shutil.rmtree(d, ignore_errors=True)
+
+
+def run_load(srv, port, queries, args, info, nrows, gpu):
+    h = srv.httpd
+    if hasattr(h, "count_s"):   # per-run group-commit stats
+        h.batches = h.batched_requests = 0
+        h.count_s = 0.0
+    if gpu is not None:
+        gpu.text_batches, gpu.text_prep_s, gpu.text_wait_s = 0, 0.0, 0.0
+    t0 = time.perf_counter()
+    if args.client == "native":
+        from pilosa_amd import _httpd
+        res = _httpd.load("127.0.0.1", port, "/index/i/query", [q.encode() for q in queries], args.conns,
+                          args.client_threads, args.seconds, args.verify)
+        res["clients"] = args.conns
+    else:
+        res = python_clients(port, queries, args)
+    el = time.perf_counter() - t0
+    # the sampled HTTP answers against the executor's own
+    mism = 0
+    samples = res.pop("samples", [])
+    for k, body in samples:
+        want = srv.executor.execute("i", queries[k]).results
+        if json.loads(body)["results"] != want:
+            mism += 1
+    st = srv.httpd.stats() if hasattr(srv.httpd, "stats") else None
+    co = srv.executor._coalescer
+    fe = res.pop("first_error", b"")
+    print(json.dumps({
+        "metric": "HTTP Count(Intersect) requests/s", "value": round(res["requests"] / args.seconds, 1),
+        "clients": res["clients"], "client": args.client, "seconds": args.seconds,
+        "mean_latency_ms": round(res["mean_ms"], 3),
+        "p50_ms": round(res.get("p50_ms", 0), 3), "p99_ms": round(res.get("p99_ms", 0), 3),
+        "errors": res["errors"], "first_error": fe[:300].decode(errors="replace") if fe else "",
+        "verified": len(samples), "mismatches": mism,
+        "server": type(srv.httpd).__name__, "server_stats": st,
+        "gpu": gpu is not None, "coalescer": {"batches": co.batches, "batched": co.batched,
+                                              "fallbacks": co.fallbacks} if co else None,
+        "index": args.index, "cols": args.cols if args.index == "disk" else args.shards << 20, "rows": nrows,
+        "setup": info, "wall_s": round(el, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -6,10 +6,8 @@
 set -o pipefail
 O=gpurun_out/r05_g
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_topn_exec.py tests/test_gpu_executor.py tests/test_native_http.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -c 6000 $O/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_topn_exec.py tests/test_gpu_executor.py tests/test_native_http.py "tests/test_gpu_shardwidth.py::test_gpu_executor_suite_at_wide_width" -x -q --timeout 900 --timeout-method thread > $O/pytest.log 2>&1 || { tail -c 6000 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-timeout -k 10 600 python -u scripts/prof_topn_paths.py --cols 1000000000 --reqs 200 > $O/prof_topn_full.log 2>&1 || { tail -c 3000 $O/prof_topn_full.log; exit 1; }
-grep -E "requests x|mesh data" $O/prof_topn_full.log
 timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2> $O/bench.err || { tail -c 5000 $O/bench.err; exit 1; }
 python - <<'PY'
 import json
@@ -24,3 +22,17 @@ s = e["serving"]
 print("serving", json.dumps({k: s[k] for k in ("count", "count_topn_mix") if k in s})[:1200])
 print("httpd", json.dumps(s.get("httpd"))[:600])
 PY
+# serving Count: group-commit thread sweep with the prep / wait split per batch
+timeout -k 10 400 python -u scripts/bench_server.py --seconds 4 --batchers 1,2,3,4,6 > $O/serve_sweep.log 2>&1 || { tail -c 3000 $O/serve_sweep.log; exit 1; }
+python - <<'PY'
+import json
+for l in open("gpurun_out/r05_g/serve_sweep.log"):
+    if l.startswith("{"):
+        d = json.loads(l); s = d["server_stats"]
+        print("batchers", s.get("count_batchers"), "rps", d["value"], "p50", d["p50_ms"], "p99", d["p99_ms"],
+              "batch", round(s["batched_requests"] / max(s["batches"], 1), 1), "ms/batch", s["count_ms_per_batch"],
+              "prep", s.get("text_prep_ms_per_batch"), "wait", s.get("text_wait_ms_per_batch"))
+PY
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_serve -o serve -- python3 -u scripts/bench_server.py --seconds 4 > $O/serve_prof.log 2>&1 || { tail -c 3000 $O/serve_prof.log; exit 1; }
+echo done

@@ -95,9 +95,10 @@ def test_concurrent_topn_requests_coalesce(lazy_env):
         t.join()
     for k, q in enumerate(qs):
         assert _pairs(out[k]) == _pairs(want[q]), q
-    if not shardwidth.WIDE:   # wider shards: src calls take the per-call pair-count path by design
-        assert ex.topn_coalescer.fallbacks == f0, (repr(ex.topn_coalescer.last_error), ex.topn_batch_declined,
-                                                   gpu.topn_decline)
+    # every width: src calls batch on the slot index (per arena sub-shard at
+    # wider shards), no per-call fallback
+    assert ex.topn_coalescer.fallbacks == f0, (repr(ex.topn_coalescer.last_error), ex.topn_batch_declined,
+                                               gpu.topn_decline)
 
 
 def test_rank_caches_from_cache_files_equal_host_caches(lazy_env):
@@ -242,8 +243,6 @@ def test_nosrc_fused_concurrent_batches_on_lanes(lazy_env):
     assert 1 <= len(lanes) <= n0 + 8
 
 
-@pytest.mark.skipif(shardwidth.WIDE, reason="the slot index is per 2^20-column arena shard: wider "
-                    "fragments answer src TopN through the pair-count path")
 def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
     """A write burst into one shard (new bits, and a tail row pushed up the
     rank order) re-indexes only that shard's slot region in place: the next
@@ -306,6 +305,55 @@ def test_src_topn_concurrent_with_write_bursts(lazy_env):
     assert not errs, errs[:2]
     assert not w.is_alive() and not any(t.is_alive() for t in rs)
     got = ex.execute("i", q).results
+    ex.gpu = None
+    try:
+        want = ex.execute("i", q).results
+    finally:
+        ex.gpu = gpu
+    assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
+
+
+@pytest.mark.parametrize("hot", [0, 64, 700])
+def test_slot_index_on_fragment_caches_matches_host(lazy_env, hot):
+    """The slot index over the executor's per-fragment rank caches, with the
+    cache ranks split between the hot-rank matrix and the tail histogram
+    (hot=0: histogram only).  At a wide shard width (PILOSA_SHARD_WIDTH=22,
+    test_gpu_shardwidth.py) each fragment is M arena sub-shards: the index
+    is per sub-shard and the hot counts and histograms are summed per
+    fragment before the heap walk (topn_kernels.hip topn_src_kernel)."""
+    from pilosa_amd.ops.topn_index import DeviceTopNIndex
+    from pilosa_amd.pql import parse_string
+    holder, ex, gpu, _, _ = lazy_env
+    shards = holder.index("i").available_shards()
+    rv = gpu.view_arena("i", "h", "standard", shards)
+    frags = [holder.fragment("i", "h", "standard", s) for s in shards]
+    rc = gpu._rank_caches("i", "h", shards, frags, rv)
+    idx = DeviceTopNIndex(rv, rc, hot=hot)
+    assert idx.ok and idx.M == rc.M and idx.Sd == rv.S and idx.R == min(hot, rc.K)
+    if shardwidth.WIDE:
+        assert idx.M > 1
+    cases = ["Row(f=0)", "Row(f=1)", "Row(f=3)", "Row(h=3)", "Intersect(Row(f=0), Row(f=1))"]
+    srcs = [gpu.plan("i", parse_string(q).calls[0], shards) for q in cases]
+    for n, th in ((5, 1), (50, 1), (0, 1), (20, 40)):
+        got = idx.topn(gpu.engine, srcs, [n] * len(srcs), [th] * len(srcs))
+        ex.gpu = None
+        try:
+            want = [ex.execute("i", f"TopN(h, {q}, n={n}, threshold={th})").results[0] for q in cases]
+        finally:
+            ex.gpu = gpu
+        for q, g, w in zip(cases, got, want):
+            assert _pairs(g) == _pairs(w), (q, n, th, hot)
+
+
+def test_src_topn_uses_the_slot_index_at_every_width(lazy_env):
+    """Src TopN calls through the executor are answered by the device slot
+    index (not the pair-count path) whatever the shard width."""
+    holder, ex, gpu, _, _ = lazy_env
+    gpu._topn_indexes.clear()
+    b0 = gpu.topn_index_batches
+    q = "TopN(h, Row(f=1), n=5) TopN(h, Row(f=0), n=9)"
+    got = ex.execute("i", q).results
+    assert gpu.topn_index_batches > b0, getattr(gpu, "_topn_index_why", "")
     ex.gpu = None
     try:
         want = ex.execute("i", q).results
