@@ -127,6 +127,18 @@ void bsi_minmax(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   check_launch("bsi_minmax");
 }
 
+void bsi_minmax_fold(torch::Tensor o, int64_t F, int64_t G, int64_t is_min, torch::Tensor out) {
+  check_dev(o, "o");
+  check_dev(out, "out");
+  TORCH_CHECK(o.scalar_type() == torch::kInt64 && o.is_contiguous() && o.numel() == F * G * 10 && G > 0,
+              "o must be int64[F*G*10]");
+  TORCH_CHECK(F < (int64_t(1) << 31) - 1, "bsi_minmax_fold: fragment count");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() >= 3, "out must be int64[3]");
+  pk::launch_bsi_minmax_fold(o.data_ptr<int64_t>(), int(F), int(G), int(is_min), out.data_ptr<int64_t>(),
+                             cur_stream(o));
+  check_launch("bsi_minmax_fold");
+}
+
 void bsi_sum(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor bsi_args, torch::Tensor out_sum,
              torch::Tensor out_cnt, int64_t fmode) {
   check_dev(progs, "progs");
@@ -606,6 +618,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("keymask_build", &keymask_build, "key-presence mask of every (shard, row) of a view");
   m.def("topn_hot_meta", &topn_hot_meta, "key-j container of every hot cache rank of the TopN index");
   m.def("topn_index", &topn_index, "build pass of the device TopN slot index (count or fill)");
+  m.def("bsi_minmax_fold", &bsi_minmax_fold, "fold BSI min/max descents into one (value, count, found)");
   m.def("topn_src", &topn_src, "src-filtered TopN over the slot index: mode 1 heap walk, mode 2/3 ids= re-count (rebuilt / kept histograms)");
   m.def("bitgemm", &bitgemm, "row-pair intersection count matrix of dense bit rows (mode 1 MFMA i8, 0 VALU)");
   m.def("expr_dense", &expr_dense, "evaluate expressions into dense one-row views (bitmap per shard/key)");

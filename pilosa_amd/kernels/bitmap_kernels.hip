@@ -1268,6 +1268,86 @@ __global__ __launch_bounds__(256, MINW) void bsi_minmax_kernel(const QueryProg* 
   }
 }
 
+// Fold of the per-key descents into the call's ONE (value, count), on the
+// device (one small D2H instead of the [S, 16, 10] table): per fragment (its
+// G = 16 * sub-shards keys) fragment.min/max's sign rules -- Min: the largest
+// |negative| if any negative, else the smallest positive; Max: the largest
+// positive if any, else the smallest |negative| (fragment.go:1145-1225) --
+// with the counts of every key holding that value summed; across fragments
+// the extreme, counted in the FIRST fragment holding it (executor.go
+// ValCount.Smaller / Larger keep the earlier shard's).  One 1024-thread block;
+// out = {value, count, found}.
+constexpr int FOLD_THREADS = 1024;
+__global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int64_t* __restrict__ o, int F, int G,
+                                                                      int is_min, int64_t* __restrict__ out) {
+  __shared__ int64_t sv[FOLD_THREADS / 64];
+  __shared__ int sf[FOLD_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t BIG = 0x7fffffffffffffffLL;
+  // this thread's best (value, fragment) over its fragments; key = value
+  // for Min, -value for Max (smaller key wins; ties: lower fragment)
+  int64_t bkey = BIG, bval = 0, bcnt = 0;
+  int bfrag = 0x7fffffff;
+  for (int f = tid; f < F; f += FOLD_THREADS) {
+    const int64_t* e = o + int64_t(f) * G * 10;
+    bool anyp = false, anyn = false;
+    for (int g = 0; g < G; g++) {
+      anyp |= e[g * 10 + 8] > 0;
+      anyn |= e[g * 10 + 9] > 0;
+    }
+    if (!anyp && !anyn) continue;
+    // column pair and sign of the fragment's candidate: Min: neg -> max |neg| (0/1),
+    // else min pos (2/3); Max: pos -> max pos (4/5), else min |neg| (6/7)
+    const bool use_neg = is_min ? anyn : !anyp;
+    const int vc = is_min ? (anyn ? 0 : 2) : (anyp ? 4 : 6);
+    const bool largest = vc == 0 || vc == 4;
+    const int mcol = use_neg ? 9 : 8;
+    int64_t best = largest ? -1 : BIG, cnt = 0;
+    for (int g = 0; g < G; g++) {
+      if (e[g * 10 + mcol] <= 0) continue;
+      const int64_t v = e[g * 10 + vc];
+      if (largest ? v > best : v < best) { best = v; cnt = 0; }
+      if (v == best) cnt += e[g * 10 + vc + 1];
+    }
+    const int64_t val = use_neg ? -best : best;
+    const int64_t key = is_min ? val : -val;
+    if (key < bkey || (key == bkey && f < bfrag)) { bkey = key; bval = val; bcnt = cnt; bfrag = f; }
+  }
+  // block argmin of (key, fragment): wave shuffles, then LDS across waves
+  int64_t k = bkey;
+  int fr = bfrag;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t k2 = __shfl_xor(k, off, 64);
+    const int f2 = __shfl_xor(fr, off, 64);
+    if (k2 < k || (k2 == k && f2 < fr)) { k = k2; fr = f2; }
+  }
+  if (lane == 0) { sv[wave] = k; sf[wave] = fr; }
+  __syncthreads();
+  if (wave == 0) {
+    k = lane < FOLD_THREADS / 64 ? sv[lane] : BIG;
+    fr = lane < FOLD_THREADS / 64 ? sf[lane] : 0x7fffffff;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t k2 = __shfl_xor(k, off, 64);
+      const int f2 = __shfl_xor(fr, off, 64);
+      if (k2 < k || (k2 == k && f2 < fr)) { k = k2; fr = f2; }
+    }
+    if (lane == 0) { sv[0] = k; sf[0] = fr; }
+  }
+  __syncthreads();
+  // the owner of the winning fragment writes it (vector stores)
+  if (sf[0] == bfrag && bfrag != 0x7fffffff && sv[0] == bkey) {
+    out[0] = bval;
+    out[1] = bcnt;
+    out[2] = 1;
+  } else if (tid == 0 && sf[0] == 0x7fffffff) {
+    out[0] = 0;
+    out[1] = 0;
+    out[2] = 0;
+  }
+}
+
 }  // namespace pk
 
 // ------------------------------------------------------------ launchers
@@ -1340,6 +1420,10 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
     hipLaunchKernelGGL((bsi_minmax_kernel<2, 2>), grid, block, 0, st, progs, views, S, bsi, out);
   else
     hipLaunchKernelGGL((bsi_minmax_kernel<0, 2>), grid, block, 0, st, progs, views, S, bsi, out);
+}
+
+void launch_bsi_minmax_fold(const int64_t* o, int F, int G, int is_min, int64_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(bsi_minmax_fold_kernel, dim3(1), dim3(FOLD_THREADS), 0, st, o, F, G, is_min, out);
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,

@@ -1457,6 +1457,22 @@ class GpuEngine:
         """Per (shard, key) descents -> int64[S, 16, 10] (see bsi_minmax_kernel);
         ``which`` "min" / "max" runs only that call's two descents (the other
         columns stay 0), "" all four."""
+        return self.to_host(self._bsi_minmax_dev(filt, bsi_view, depth, which)).numpy().reshape(bsi_view.S, 16, 10)
+
+    def bsi_minmax_folded(self, filt: Optional[object], bsi_view: "DeviceView", depth: int, which: str,
+                          sub: int = 1) -> Tuple[int, int, bool]:
+        """Min / Max of the call folded on the device (bsi_minmax_fold_kernel):
+        (value, count, found) with fragments of ``sub`` arena sub-shards."""
+        torch = self.torch
+        o = self._bsi_minmax_dev(filt, bsi_view, depth, which)
+        out = torch.zeros(3, dtype=torch.int64, device=self.device)
+        S = bsi_view.S
+        if S:
+            self.ext.bsi_minmax_fold(o, S // sub, 16 * sub, 1 if which == "min" else 0, out)
+        v, c, found = self.to_host(out).tolist()
+        return int(v), int(c), bool(found)
+
+    def _bsi_minmax_dev(self, filt: Optional[object], bsi_view: "DeviceView", depth: int, which: str = ""):
         torch = self.torch
         S = bsi_view.S
         view_index: Dict[int, int] = {id(bsi_view): 0}
@@ -1480,7 +1496,7 @@ class GpuEngine:
         if S and args[2] >= 0:
             tp, tv = self.upload_batch(progs, ordered)
             self.ext.bsi_minmax(tp, tv, S, torch.from_numpy(args), out, {"min": 1, "max": 2}.get(which, 0))
-        return self.to_host(out).numpy().reshape(S, 16, 10)
+        return out
 
     def bsi_sum_async(self, filters: Sequence[Optional[object]], bsi_view: "DeviceView", depth: int,
                       matrix: Optional[bool] = None):

@@ -378,6 +378,14 @@ class GpuExecutor:
 
     def _bsi_count(self, index: str, c: Call, shards: Sequence[int]) -> Optional[int]:
         """Count(Row(v <op> x)) in one fused predicate+count launch."""
+        n = self._bsi_count_async(index, c, shards)
+        if n is None or isinstance(n, int):
+            return n
+        return int(self.engine.to_host(n)[0])
+
+    def _bsi_count_async(self, index: str, c: Call, shards: Sequence[int]):
+        """The fused count launched: device int64[1], an int when known
+        without a launch, None for the plain (NOT NULL) path."""
         f, b, kind, args = self._ex().bsi_predicate(index, c)
         if kind == "empty":
             return 0
@@ -391,7 +399,7 @@ class GpuExecutor:
         else:
             op, p1, p2 = args[0], int(args[1]), 0
         self.launches += 1
-        return int(self.engine.bsi_range_count_async(bv, b.bit_depth, op, p1, p2).item())
+        return self.engine.bsi_range_count_async(bv, b.bit_depth, op, p1, p2)
 
     def bsi_leaf(self, index: str, c: Call, shards: Sequence[int]):
         """Row(v <op> x) -> Leaf over a device-evaluated predicate view
@@ -440,24 +448,18 @@ class GpuExecutor:
             filt = self.plan(index, c.children[0], shards)
             if filt is EMPTY:
                 return ValCount()
+        # per fragment (a wide one: all keys of its sub-shards, fragment.min/max
+        # counts every column of the shard holding the value), then the first
+        # fragment holding the extreme -- folded on the device, 3 int64 back
+        sub = shardwidth.DEVICE_SUBSHARDS if shardwidth.WIDE else 1
         try:
             self.launches += 1
-            o = self.engine.bsi_minmax(filt, bv, b.bit_depth, which)
+            v, n, found = self.engine.bsi_minmax_folded(filt, bv, b.bit_depth, which, sub)
         except CompileError:
             raise NotImplementedError
-        vals, cnts = _minmax_per_shard(o, which)
-        if shardwidth.WIDE:
-            # per fragment: the extreme over its sub-shards, counted over all of them
-            # (fragment.min/max counts every column of the wide shard holding it)
-            vals, cnts = _fold_subshards_value(np.asarray(vals, np.int64), np.asarray(cnts, np.int64),
-                                               which == "min")
-        vals, cnts = np.asarray(vals, np.int64), np.asarray(cnts, np.int64)
-        live = cnts > 0
-        if not live.any():
+        if not found or n <= 0:
             return ValCount()
-        best = vals[live].min() if which == "min" else vals[live].max()
-        k = int(np.flatnonzero(live & (vals == best))[0])
-        return ValCount(int(vals[k]) + b.base, int(cnts[k]))
+        return ValCount(v + b.base, n)
 
     def hbm_bytes(self) -> int:
         with self.mu:
@@ -769,15 +771,34 @@ class GpuExecutor:
             got = self._count_batch_native(index, calls, shards)
             if got is not None:
                 return got
+        # Count(Row(v <op> x)) calls: the fused predicate+count kernel each
+        # (no predicate view written and re-read), one D2H for all of them
+        fused: Dict[int, object] = {}
         try:
             exprs = []
-            for c in calls:
+            for i, c in enumerate(calls):
                 if len(c.children) != 1:
                     return None
-                exprs.append(self.plan(index, c.children[0], shards))
+                ch = c.children[0]
+                if ch.name in ("Row", "Range") and ch.has_condition_arg():
+                    n = self._bsi_count_async(index, ch, shards)
+                    if n is not None:
+                        fused[i] = n
+                        exprs.append(EMPTY)
+                        continue
+                exprs.append(self.plan(index, ch, shards))
         except NotImplementedError:
             return None
         out = [0] * len(exprs)
+        if fused:
+            dev = [(i, t) for i, t in fused.items() if not isinstance(t, int)]
+            for i, t in fused.items():
+                if isinstance(t, int):
+                    out[i] = t
+            if dev:
+                got = self.engine.to_host(self.engine.torch.cat([t for _, t in dev])).tolist()
+                for (i, _), v in zip(dev, got):
+                    out[i] = int(v)
         live = []
         for i, e in enumerate(exprs):
             if e is EMPTY:
@@ -1660,11 +1681,12 @@ def _fold_subshards(rid: np.ndarray, cnt: np.ndarray, is_min: bool, filtered: bo
     return np.where(ok, best, 0), np.where(ok, n, 0)
 
 
-def _fold_subshards_value(vals: np.ndarray, cnts: np.ndarray, is_min: bool):
+def _fold_subshards_value(vals: np.ndarray, cnts: np.ndarray, is_min: bool, M: Optional[int] = None):
     """Per-device-shard (value, count) -> per fragment wider than 2^20
     columns: the min (max) value over its sub-shards with the counts of
-    every sub-shard holding that value summed."""
-    M = shardwidth.DEVICE_SUBSHARDS
+    every sub-shard holding that value summed.  (The host reference of
+    bsi_minmax_fold_kernel, tests/test_gpu_kernels.py.)"""
+    M = shardwidth.DEVICE_SUBSHARDS if M is None else M
     v, c = vals.reshape(-1, M), cnts.reshape(-1, M)
     live = c > 0
     big = np.iinfo(np.int64).max

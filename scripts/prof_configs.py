@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--no-profile", action="store_true", help="no cProfile (under rocprofv3)")
     a = ap.parse_args()
     import torch
 
@@ -33,10 +34,13 @@ def main():
                               config_reps=a.reps)
     dev = torch.device("cuda", 0)
     pr = cProfile.Profile()
-    pr.enable()
+    if not a.no_profile:
+        pr.enable()
     res = bench.bench_configs_disk(args, 1, 0, dev, a.which)
     pr.disable()
     print(json.dumps(res), flush=True)
+    if a.no_profile:
+        return
     for key in ("tottime", "cumulative"):
         s = io.StringIO()
         pstats.Stats(pr, stream=s).sort_stats(key).print_stats(a.top)

@@ -158,6 +158,16 @@ def test_bsi_on_device_matches_host(envs, q):
     assert got == want
 
 
+def test_bsi_counts_in_one_request_match_host(envs):
+    """A request of many Count() calls mixing BSI conditions (fused
+    predicate+count launches, one D2H) with plain trees: == host."""
+    cpu, gpu = envs
+    text = " ".join(q for q in BSI_QUERIES if q.startswith("Count("))
+    want = cpu.q("i", text)
+    got = _dev(cpu, gpu, lambda: cpu.q("i", text))
+    assert got == want
+
+
 def test_bsi_rows_match_host(envs):
     cpu, gpu = envs
     for q in ("Row(n > 99000)", "Row(n >< [-3, 3])", "Row(m < -4990)"):

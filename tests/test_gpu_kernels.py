@@ -313,3 +313,40 @@ def test_differential_fuzz_count_and_materialize(setup):
             want_cols = _host_eval(t, f).slice() % (1 << 20)
             got_cols = b.slice() % (1 << 20) if b is not None else np.array([], np.uint64)
             np.testing.assert_array_equal(np.sort(got_cols), np.sort(want_cols), err_msg=str(t))
+
+
+@pytest.mark.parametrize("which", ["min", "max"])
+@pytest.mark.parametrize("F,sub", [(1, 1), (37, 1), (2500, 1), (9, 4)])
+def test_bsi_minmax_fold_kernel_matches_host_fold(which, F, sub):
+    """bsi_minmax_fold_kernel == the host fold it replaced (per-shard sign
+    rules, sub-shard fold, first fragment holding the extreme) on random
+    descent tables with ties, empty keys and all-negative fragments."""
+    import torch
+
+    from pilosa_amd.ops.device import kernels
+    from pilosa_amd.ops.gpu_executor import _fold_subshards_value, _minmax_per_shard
+    rng = np.random.default_rng(F * 7 + sub + (which == "min"))
+    S = F * sub
+    o = np.zeros((S, 16, 10), np.int64)
+    o[:, :, 8] = rng.random((S, 16)) < 0.5          # any positive in the key
+    o[:, :, 9] = rng.random((S, 16)) < 0.3          # any negative
+    for c in (0, 2, 4, 6):
+        o[:, :, c] = rng.integers(0, 6, (S, 16))    # few values: many ties
+        o[:, :, c + 1] = rng.integers(1, 50, (S, 16))
+    dead = rng.random(S) < 0.2                      # whole shards without values
+    o[dead, :, 8:] = 0
+    vals, cnts = _minmax_per_shard(o, which)
+    vals, cnts = np.asarray(vals, np.int64), np.asarray(cnts, np.int64)
+    if sub > 1:
+        vals, cnts = _fold_subshards_value(vals, cnts, which == "min", M=sub)
+    live = cnts > 0
+    if live.any():
+        best = vals[live].min() if which == "min" else vals[live].max()
+        k = int(np.flatnonzero(live & (vals == best))[0])
+        want = [int(vals[k]), int(cnts[k]), 1]
+    else:
+        want = [0, 0, 0]
+    dev = torch.device("cuda", 0)
+    out = torch.full((3,), -7, dtype=torch.int64, device=dev)
+    kernels().bsi_minmax_fold(torch.from_numpy(o.reshape(-1)).to(dev), F, 16 * sub, int(which == "min"), out)
+    assert out.cpu().tolist() == want
