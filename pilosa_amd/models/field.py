@@ -26,7 +26,7 @@ from pilosa_amd.errors import (ErrBSIGroupNotFound, ErrBSIGroupValueTooHigh, Err
                                validate_name)
 from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
 from pilosa_amd.models.cache import CACHE_TYPE_LRU, CACHE_TYPE_NONE, CACHE_TYPE_RANKED, DEFAULT_CACHE_SIZE
-from pilosa_amd.models.fragment import SHARD_WIDTH, SHARD_WIDTH_EXP
+from pilosa_amd.models.fragment import SHARD_WIDTH, SHARD_WIDTH_EXP, bump_shard_epoch
 from pilosa_amd.models.row import Row
 from pilosa_amd.models.timeq import valid_quantum, views_by_time
 from pilosa_amd.models.view import VIEW_BSI_PREFIX, VIEW_STANDARD, View
@@ -296,6 +296,7 @@ class Field:
                 data = fh.read()
             if data:
                 self.remote_available_shards |= {int(x) for x in _roaring.Bitmap.from_bytes(data).slice()}
+                bump_shard_epoch()
 
     # ------------------------------------------------------------ lifecycle
     def open(self):
@@ -323,6 +324,7 @@ class Field:
                         for frag in v.all_fragments():
                             frag.upgrade_bsi_v2(self.bsi.bit_depth)
                     self.views[name] = v
+                    bump_shard_epoch()
                     self.local_shards |= set(v.fragments)
         return self
 
@@ -331,6 +333,7 @@ class Field:
             for v in self.views.values():
                 v.close()
             self.views.clear()
+            bump_shard_epoch()
             self.row_attr_store.close()
 
     def delete(self):
@@ -350,11 +353,13 @@ class Field:
             if v is None:
                 v = self._new_view(name).open()
                 self.views[name] = v
+                bump_shard_epoch()
             return v
 
     def delete_view(self, name: str):
         with self.mu:
             v = self.views.pop(name, None)
+            bump_shard_epoch()
             if v is None:
                 raise ErrInvalidView
             v.delete()
@@ -379,11 +384,13 @@ class Field:
     def add_remote_available_shards(self, shards: Iterable[int]):
         with self.mu:
             self.remote_available_shards |= {int(s) for s in shards}
+            bump_shard_epoch()
             self._save_available_shards()
 
     def remove_available_shard(self, shard: int):
         with self.mu:
             self.remote_available_shards.discard(int(shard))
+            bump_shard_epoch()
             self._save_available_shards()
 
     def bsi_group(self, name: Optional[str] = None) -> Optional[BSIGroup]:

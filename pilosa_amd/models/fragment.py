@@ -79,6 +79,19 @@ def mutation_epoch() -> int:
     return _EPOCH[0]
 
 
+# bumped whenever the set of fragments, views or fields (or a field's remote
+# available shards) changes: Index.available_shards is memoised on it
+_SHARD_EPOCH = [0]
+
+
+def bump_shard_epoch():
+    _SHARD_EPOCH[0] += 1
+
+
+def shard_epoch() -> int:
+    return _SHARD_EPOCH[0]
+
+
 def remove_stale_snapshots(dirpath: str, names: Iterable[str]) -> int:
     """Snapshot temp files (``<shard>.<pid>.<tid>.snapshotting``, or the old
     fixed ``<shard>.snapshotting``) left by a process that died mid-snapshot

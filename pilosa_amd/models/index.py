@@ -17,6 +17,7 @@ from pilosa_amd.shardwidth import SHARD_WIDTH
 from pilosa_amd.models.attrs import MemAttrStore, SQLiteAttrStore
 from pilosa_amd.models.cache import CACHE_TYPE_NONE
 from pilosa_amd.models.field import Field, FieldOptions
+from pilosa_amd.models.fragment import bump_shard_epoch, shard_epoch
 
 EXISTENCE_FIELD_NAME = "_exists"
 
@@ -73,6 +74,7 @@ class Index:
                 except PilosaError as e:
                     raise PilosaError(f"opening fields: open field: name={name}, err={e}") from e
                 self.fields[name] = f
+                bump_shard_epoch()
             if self.track_existence:
                 self._open_existence_field()
         return self
@@ -86,6 +88,7 @@ class Index:
             for f in self.fields.values():
                 f.close()
             self.fields.clear()
+            bump_shard_epoch()
             self.column_attr_store.close()
 
     def delete(self):
@@ -109,6 +112,7 @@ class Index:
         f.save_meta()
         f.open()
         self.fields[name] = f
+        bump_shard_epoch()
         return f
 
     def create_field(self, name: str, opts: Optional[FieldOptions] = None) -> Field:
@@ -140,15 +144,24 @@ class Index:
     def delete_field(self, name: str):
         with self.mu:
             f = self.fields.pop(name, None)
+            bump_shard_epoch()
             if f is None:
                 raise ErrFieldNotFound
             f.delete()
 
     def available_shards(self) -> List[int]:
+        # memoised on the shard epoch (bumped by every fragment / view /
+        # field / remote-shard change): the walk over ~1k fragments per
+        # request was a visible share of a serving request
+        ep = shard_epoch()
+        memo = self.__dict__.get("_avail_memo")
+        if memo is not None and memo[0] == ep:
+            return list(memo[1])
         s = set()
         for f in list(self.fields.values()):
             s |= set(f.available_shards())
         out = sorted(s)
+        self._avail_memo = (ep, tuple(out))
         if self.stats is not None and out:
             self.stats.gauge("maxShard", out[-1])   # index.go:257
         return out

@@ -12,7 +12,7 @@ import threading
 from typing import Callable, Dict, List, Optional
 
 from pilosa_amd.errors import PilosaError
-from pilosa_amd.models.fragment import SHARD_WIDTH_EXP, Fragment, remove_stale_snapshots
+from pilosa_amd.models.fragment import SHARD_WIDTH_EXP, Fragment, bump_shard_epoch, remove_stale_snapshots
 from pilosa_amd.models.row import Row
 
 VIEW_STANDARD = "standard"
@@ -66,6 +66,7 @@ class View:
                 except PilosaError as e:
                     raise PilosaError(f"open fragment: shard={shard}, err=opening storage: {e}") from e
                 self.fragments[shard] = frag
+                bump_shard_epoch()
         return self
 
     def close(self):
@@ -73,6 +74,7 @@ class View:
             for f in self.fragments.values():
                 f.close()
             self.fragments.clear()
+            bump_shard_epoch()
 
     def fragment(self, shard: int) -> Optional[Fragment]:
         return self.fragments.get(shard)
@@ -91,6 +93,7 @@ class View:
                 return f
             f = self._new_fragment(shard).open()
             self.fragments[shard] = f
+            bump_shard_epoch()
         if self.field_obj is not None:
             self.field_obj._note_shard(shard)
         if self.on_create_shard is not None:
@@ -100,6 +103,7 @@ class View:
     def delete_fragment(self, shard: int):
         with self.mu:
             f = self.fragments.pop(shard, None)
+            bump_shard_epoch()
             if f is None:
                 from pilosa_amd.errors import ErrFragmentNotFound
                 raise ErrFragmentNotFound
