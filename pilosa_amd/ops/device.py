@@ -931,6 +931,23 @@ class DeviceView:
 
 # ---------------------------------------------------------------- engine
 
+class DeviceRowBlock:
+    """A row result's containers on the device: per (shard, key) count
+    (int32[S*16]; > 4096 = bitmap) and u16 offset (int64[S*16]) into a u16
+    payload, for the device shards ``shards``; ``spill`` is the block of the
+    bits a Shift carried past each shard's last column (or None).  A rank of
+    a multi-GPU node sends its Row partial as these tensors (no host Row, no
+    roaring serialisation, parallel/collectives.encode_row_block)."""
+
+    __slots__ = ("shards", "counts", "offs", "payload", "spill")
+
+    def __init__(self, shards, counts, offs, payload, spill=None):
+        self.shards, self.counts, self.offs, self.payload, self.spill = list(shards), counts, offs, payload, spill
+
+    def host(self):
+        return (self.counts.cpu().numpy(), self.offs.cpu().numpy(), self.payload.cpu().numpy().view(np.uint16))
+
+
 class GpuEngine:
     """Batched query execution on one GPU (all views must share the shard list)."""
 
@@ -1311,22 +1328,24 @@ class GpuEngine:
             raise CompileError(f"expressions span {S2} shards, expected {S}")
         return self._materialize(progs, views, S)
 
-    def materialize(self, expr) -> Tuple[List[object], List[int]]:
-        """Evaluate one expression to per-shard host Bitmaps (row results)."""
-        from pilosa_amd import _roaring
-
+    def materialize_block(self, expr) -> Optional["DeviceRowBlock"]:
+        """Evaluate one expression into device result containers, left in HBM
+        (a rank's Row partial travels as these blocks, parallel/mesh.py)."""
         progs, views, S = self.compile_batch([expr])
         if not S:
-            return [], []
+            return None
         counts, offs, outp = self._materialize(progs, views, S)
-        c = counts.cpu().numpy()
-        o = offs.cpu().numpy()
-        pay = outp.cpu().numpy().view(np.uint16)
-        shards = views[0].shards
+        return DeviceRowBlock([int(x) for x in views[0].shards], counts, offs, outp)
+
+    @staticmethod
+    def block_bitmaps(shards: Sequence[int], c: np.ndarray, o: np.ndarray, pay: np.ndarray) -> List[object]:
+        """Host Bitmaps of result containers (counts ``c``, u16 offsets ``o``
+        per (shard, key), u16 payload ``pay``), one per shard (None = empty)."""
+        from pilosa_amd import _roaring
         from pilosa_amd import shardwidth
         cpr = shardwidth.ARENA_CPR   # device shard ids: global key = shard * cpr + slot
         result = []
-        for s in range(S):
+        for s in range(len(shards)):
             cs = c[s * 16:(s + 1) * 16]
             nz = np.nonzero(cs)[0]
             if len(nz) == 0:
@@ -1336,7 +1355,15 @@ class GpuEngine:
             types = np.where(cs[nz] > 4096, 2, 1).astype(np.uint8)
             result.append(_roaring.bitmap_from_containers(keys, types, cs[nz].astype(np.int32),
                                                           o[s * 16 + nz].astype(np.int64), pay))
-        return result, shards
+        return result
+
+    def materialize(self, expr) -> Tuple[List[object], List[int]]:
+        """Evaluate one expression to per-shard host Bitmaps (row results)."""
+        blk = self.materialize_block(expr)
+        if blk is None:
+            return [], []
+        c, o, pay = blk.host()
+        return self.block_bitmaps(blk.shards, c, o, pay), blk.shards
 
     @staticmethod
     def bsi_args(bsi_view: "DeviceView", depth: int, slot: int = 0) -> np.ndarray:

@@ -822,33 +822,33 @@ class GpuExecutor:
         return out
 
     def bitmap(self, index: str, c: Call, shards: List[int]) -> Row:
+        blk = self.bitmap_block(index, c, shards)
+        if blk is None:
+            return Row()
+        c_, o, pay = blk.host()
+        spill = ([], [])
+        if blk.spill is not None:
+            sc, so, sp = blk.spill.host()
+            spill = (self.engine.block_bitmaps(blk.spill.shards, sc, so, sp), blk.spill.shards)
+        return row_from_bitmaps(self.engine.block_bitmaps(blk.shards, c_, o, pay), blk.shards, *spill)
+
+    def bitmap_block(self, index: str, c: Call, shards: List[int]):
+        """The call's result containers left on the device (DeviceRowBlock,
+        spill block attached for Shift), None when empty."""
         e = self.plan(index, c, shards)
         if e is EMPTY:
-            return Row()
+            return None
         try:
             self.launches += 1
-            bms, shard_list = self.engine.materialize(e)
-            spill = ([], [])
-            if _has_shift(e):
+            blk = self.engine.materialize_block(e)
+            if blk is not None and _has_shift(e):
                 se = spill_expr(e)
                 if se is not EMPTY:
                     self.launches += 1
-                    spill = self.engine.materialize(se)
+                    blk.spill = self.engine.materialize_block(se)
         except CompileError:
             raise NotImplementedError
-        row = Row()
-        for s, bm in zip(shard_list, bms):
-            if bm is not None and bm.any():
-                row.segments[int(s)] = bm
-        # bits a shard's Shift carried past its last column belong to the
-        # next shard's segment (Row.Merge in the reference's reduce)
-        M = shardwidth.DEVICE_SUBSHARDS   # spill of device shard s belongs to s + M (the next shard)
-        for s, bm in zip(spill[1], spill[0]):
-            if bm is not None and bm.any():
-                part = _rebase_spill(bm)
-                t = int(s) + M
-                row.segments[t] = row.segments[t].union(part) if t in row.segments else part
-        return row
+        return blk
 
     def rows(self, index: str, fname: str, c: Call, shards: List[int]) -> List[int]:
         """Rows(field, previous=, column=, limit=, from=, to=) over the local
@@ -1758,6 +1758,23 @@ def spill_expr(e):
     if not kids:
         return EMPTY
     return kids[0] if len(kids) == 1 else Op(e.op, tuple(kids))
+
+
+def row_from_bitmaps(bms, shard_list, spill_bms=(), spill_shards=()) -> Row:
+    """A Row from per-device-shard result Bitmaps; the bits a shard's Shift
+    carried past its last column belong to the next shard's segment (Row.Merge
+    in the reference's reduce)."""
+    row = Row()
+    for s, bm in zip(shard_list, bms):
+        if bm is not None and bm.any():
+            row.segments[int(s)] = bm
+    M = shardwidth.DEVICE_SUBSHARDS   # spill of device shard s belongs to s + M (the next shard)
+    for s, bm in zip(spill_shards, spill_bms):
+        if bm is not None and bm.any():
+            part = _rebase_spill(bm)
+            t = int(s) + M
+            row.segments[t] = row.segments[t].union(part) if t in row.segments else part
+    return row
 
 
 def _rebase_spill(bm):

@@ -438,7 +438,31 @@ def decode(data: bytes):
 # collective whatever it produced (the reference's QueryResponse per node,
 # internal/public.proto, reduced by executor.go mapReduce).
 (TAG_NONE, TAG_MSGPACK, TAG_VALCOUNT, TAG_PAIR, TAG_PAIRS, TAG_ROWIDS, TAG_GROUPS, TAG_ROW,
- TAG_INT, TAG_BOOL) = range(10)
+ TAG_INT, TAG_BOOL, TAG_DEVROW) = range(11)
+
+
+def encode_row_block(blk, device):
+    """A rank's Row partial left on its GPU (ops/device.DeviceRowBlock) ->
+    one device int64 tensor, built with device copies only: [TAG_DEVROW,
+    nblocks] then per block (the row, then its Shift spill) [S, payload
+    words, shards[S], counts (int32 pairs), u16 offsets[S*16], payload].
+    The rank never copies its row to the host or serialises it; the front
+    end decodes every rank's containers with one D2H (decode_partial)."""
+    import torch
+
+    parts = []
+    blocks = [b for b in (blk, blk.spill) if b is not None]
+    parts.append(torch.tensor([TAG_DEVROW, len(blocks)], dtype=torch.int64))
+    dev_parts = []
+    for b in blocks:
+        S = len(b.shards)
+        pay = b.payload.reshape(-1)
+        if pay.numel() % 4:
+            pay = torch.cat([pay, pay.new_zeros(4 - pay.numel() % 4)])
+        hdr = torch.tensor([S, pay.numel() // 4] + list(b.shards), dtype=torch.int64)
+        dev_parts += [hdr.to(device, non_blocking=True), b.counts.reshape(-1).contiguous().view(torch.int64),
+                      b.offs.reshape(-1).to(torch.int64), pay.contiguous().view(torch.int64)]
+    return torch.cat([parts[0].to(device, non_blocking=True)] + dev_parts)
 
 
 def _bytes_to_words(b: bytes) -> np.ndarray:
@@ -541,6 +565,24 @@ def decode_partial(w: np.ndarray):
         fields = decode(_words_to_bytes(w[4:4 + nw], nb))
         mat = w[4 + nw:4 + nw + n * (k + 1)].view(np.uint64).reshape(n, k + 1).tolist()
         return [GroupCount([FieldRow(f, r) for f, r in zip(fields, row[:k])], row[k]) for row in mat]
+    if tag == TAG_DEVROW:
+        from pilosa_amd.ops.device import GpuEngine
+        from pilosa_amd.ops.gpu_executor import row_from_bitmaps
+        o = 2
+        out = []
+        for _ in range(int(w[1])):
+            S, npw = int(w[o]), int(w[o + 1])
+            shards = w[o + 2:o + 2 + S].tolist()
+            o += 2 + S
+            c = w[o:o + S * 8].view(np.int32)
+            o += S * 8
+            offs = w[o:o + S * 16]
+            o += S * 16
+            pay = w[o:o + npw].view(np.uint16)
+            o += npw
+            out.append((GpuEngine.block_bitmaps(shards, c, offs, pay), shards))
+        spill = out[1] if len(out) > 1 else ((), ())
+        return row_from_bitmaps(out[0][0], out[0][1], *spill)
     if tag == TAG_ROW:
         ns = int(w[1])
         hdr = w[2:2 + 2 * ns].reshape(ns, 2)

@@ -20,7 +20,9 @@ hop with a process group (backend ``nccl`` = RCCL over xGMI on the GPU box,
   all-reduced re-count (OP_TOPN), and for every other call one
   variable-length all-gather of each rank's partial as a typed int64 tensor
   (collectives.encode_partial: ValCount, Pair, TopN pairs, Rows ids, GroupBy
-  matrices, Row segments as roaring bytes) folded with the executor's own
+  matrices; a GPU rank's Row as its device result containers,
+  collectives.encode_row_block, decoded with one D2H on the front end)
+  folded with the executor's own
   reduce function; results carrying strings (keys, attributes) ride as
   msgpack bytes inside the same tensor.
 * writes and imports are routed to the owning rank only.
@@ -57,6 +59,8 @@ class MeshError(RuntimeError):
 (OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS, OP_COUNT_TEXT,
  OP_ERRORS, OP_TOPN, OP_SYNC, OP_RECALC) = range(14)
 MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
+# bitmap calls whose rank partial can travel as device container blocks
+_ROW_CALLS = ("Row", "Range", "Bitmap", "Intersect", "Union", "Difference", "Xor", "Not", "Shift")
 _OP_NAMES = {OP_STOP: "stop", OP_COUNT: "count", OP_CALL: "call", OP_WRITE: "write", OP_IMPORT: "import",
              OP_SCHEMA: "schema", OP_DEL_INDEX: "deleteIndex", OP_DEL_FIELD: "deleteField", OP_SHARDS: "shards",
              OP_COUNT_TEXT: "countText", OP_ERRORS: "errors", OP_TOPN: "topn", OP_SYNC: "sync",
@@ -107,6 +111,7 @@ class ShardMesh:
         self.seq = 0                      # count-text batches issued (front end)
         self.in_flight = 0                # front end: batches issued, result not yet read
         self.max_in_flight = 0
+        self.row_blocks = 0      # Row partials sent as device container blocks
         self._pending = collections.deque()   # worker: (tensor, work) of batches in flight
         self._errors: Dict[int, BaseException] = {}
         self.last_count_text_errors: List[str] = []
@@ -480,7 +485,7 @@ class ShardMesh:
         flight).  Any failure of the local work travels as the rank's partial
         (OP_CALL) or as a declined readiness vote (OP_TOPN), never as a
         missing collective."""
-        from .collectives import decode_partial, encode_partial
+        from .collectives import decode_partial, encode_partial, encode_row_block
 
         if op == OP_TOPN:
             return self._topn_batch_local(*args)
@@ -491,7 +496,11 @@ class ShardMesh:
             mine = self._local_call(index, pql, self.owned(shards), optd)
         except Exception as e:  # noqa: BLE001 - reported through the gather below
             mine = e
-        t = self.torch.from_numpy(encode_partial(mine)).to(self.device)
+        from pilosa_amd.ops.device import DeviceRowBlock
+        if isinstance(mine, DeviceRowBlock):
+            t = encode_row_block(mine, self.device)
+        else:
+            t = self.torch.from_numpy(encode_partial(mine)).to(self.device)
         return _Chain(self.comm.all_gather_var_async(t), lambda ps: [decode_partial(p.cpu().numpy()) for p in ps])
 
     def _refresh_spaces(self, index: str, fnames: List[str], own: List[int], vote: bool = True):
@@ -645,6 +654,21 @@ class ShardMesh:
         c = parse_string(pql).calls[0]
         if not shards and c.name not in ("Set", "Clear", "SetRowAttrs", "SetColumnAttrs"):
             return None
+        if c.name in _ROW_CALLS and ex.gpu is not None and hasattr(ex.gpu, "bitmap_block"):
+            # a Row partial stays on the device: its containers go straight
+            # into the all-gather (collectives.encode_row_block); the front end
+            # attaches row attributes after the reduce, as for any partial.
+            # Anything the device declines (or any error) takes the regular
+            # path below, which reports exactly what the executor would.
+            try:
+                blk = ex.gpu.bitmap_block(index, c, list(shards))
+                self.row_blocks += 1
+                if blk is not None:
+                    return blk
+                from pilosa_amd.models.row import Row
+                return Row()
+            except Exception:  # noqa: BLE001 - the regular path answers (or raises the real error)
+                pass
         return ex.execute_call(index, c, shards, self._local_opt(optd))
 
     def _local_counts(self, index: str, pqls: List[str], shards: List[int]) -> List[int]:

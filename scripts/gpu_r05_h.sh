@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 5, call H: the cache-only TopN request path at full scale (954
+# shards) -- host profile and kernel trace -- and BSI config 4 under a kernel
+# trace plus a FETCH_SIZE pass (HBM roofline of Sum / range / Min / Max).
+set -o pipefail
+O=gpurun_out/r05_h
+mkdir -p $O
+timeout -k 10 600 python -u scripts/prof_topn_paths.py --cols 1000000000 --reqs 200 --paths local > $O/prof_topn_full.log 2>&1 || { tail -c 3000 $O/prof_topn_full.log; exit 1; }
+grep -E "requests x|ms per" $O/prof_topn_full.log | head -5
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_topn -o topn -- python3 -u scripts/prof_topn_paths.py --cols 1000000000 --reqs 200 --paths local --top 5 > $O/prof_topn_trace.log 2>&1 || { tail -c 3000 $O/prof_topn_trace.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o c4 -- python3 -u scripts/prof_configs.py --which 4 --reps 20 --no-profile > $O/prof_c4.log 2>&1 || { tail -c 3000 $O/prof_c4.log; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_c4 -o c4 -- python3 -u scripts/prof_configs.py --which 4 --reps 3 --no-profile > $O/pmc_c4.log 2>&1 || { tail -c 3000 $O/pmc_c4.log; exit 1; }
+echo done

@@ -5,7 +5,8 @@ it).  Every mesh operation runs its real collectives over RCCL:
 
 * Count texts (OP_COUNT_TEXT: native compile + device all-reduce, pipelined);
 * general calls (OP_CALL: typed int64 partials in one all-gather) -- Sum,
-  Min/Max, Row, Rows, GroupBy, BSI ranges;
+  Min/Max, Rows, GroupBy, BSI ranges; Row-valued calls as the rank's device
+  result containers (collectives.encode_row_block);
 * whole TopN batches (OP_TOPN: folded vote, then for cache-only calls one
   all-reduce of membership + partial totals over the node candidate space,
   for src calls a speculative union all-gather and the re-count
@@ -72,7 +73,9 @@ def _worker(rank, world, port, outdir):
             return {"got": got, "want": want, **stats}
 
         out["counts"] = both([COUNTS])
-        out["calls"] = both(QUERIES)
+        r0 = mesh.row_blocks
+        out["calls"] = both(QUERIES + ["Shift(Row(f=1), n=5)", "Union(Row(f=1), Row(g=2))"])
+        out["row_blocks"] = mesh.row_blocks - r0
         out["topn"] = both(TOPN)
         # steady-state TopN batch: its data collectives on RCCL
         run(["TopN(f, n=4) TopN(f, n=2)"])      # builds the node candidate space for n=4
@@ -116,6 +119,8 @@ def test_rccl_world1_mesh_matches_local(tmp_path):
     assert res["counts"]["count_text"] >= 1, "Count text did not take the mesh count_text path"
     assert res["counts"]["collectives"] >= 1
     assert res["calls"]["collectives"] >= len(QUERIES), "general calls did not gather partials over RCCL"
+    # Row / Difference / Not / Shift / Union partials travelled as device container blocks
+    assert res["row_blocks"] >= 5, res["row_blocks"]
     assert res["topn"]["topn_tensor"] >= 3 and res["after_write"]["topn_tensor"] >= 3, res
     # steady state: the folded vote + ONE all-reduce for a cache-only batch;
     # vote + candidate union + re-count all-reduce for a src batch
