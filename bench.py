@@ -317,10 +317,15 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     # every call of every request distinct: n and threshold vary, so no
     # phase-2 re-count or candidate set is shared between calls by repetition
     nbc = max(nb, args.topn_cache_batches)   # cache-only requests are ~1 ms: a longer window
-    cache_calls = _distinct_topn_calls(B * (nbc + 1))
+    cache_calls = _wide_topn_calls(B * (nbc + 1), seed=17)
     cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nbc + 1)]
-    out["cache"] = {"calls": "TopN(f, n in {10,50,100,500}, threshold in {1,1000,5000,20000}), all distinct"}
+    out["cache"] = {"calls": f"TopN(f, n=log-uniform 1..1000, threshold one of {len(WIDE_THRESHOLDS)} values "
+                             "1..50000), random per call: distinct within and across requests"}
     res_cache = timed(cache_q, out["cache"], os.environ.get("PILOSA_BENCH_TOPN_PROFILE", ""))
+    log("topn: cache-only requests (round-4 cycling set: 4 n x 4 thresholds)")
+    cyc = _distinct_topn_calls(B * (nbc + 1))
+    out["cache_cycling"] = {"calls": "TopN(f, n in {10,50,100,500} + offset, threshold in {1,1000,5000,20000})"}
+    timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nbc + 1)], out["cache_cycling"])
     log("topn: cache-only requests (the same call repeated, round-3 figure)")
     out["cache_repeated"] = {}
     timed([" ".join([f"TopN(f, n={n})"] * B)] * (nbc + 1), out["cache_repeated"])
@@ -399,6 +404,21 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
 
 TOPN_NS = (10, 50, 100, 500)
 TOPN_THRESHOLDS = (1, 1000, 5000, 20000)
+
+
+# >= 64 distinct thresholds, geometric from 1 to 50000
+WIDE_THRESHOLDS = tuple(sorted({max(1, int(round(50000 ** (i / 79)))) for i in range(80)}))
+
+
+def _wide_topn_calls(k: int, seed: int = 17):
+    """k cache-only TopN calls with n log-uniform over 1..1000 and the
+    threshold drawn from WIDE_THRESHOLDS (>= 64 values), independently per
+    call: no candidate set, threshold total or re-count repeats by
+    construction across a run."""
+    rng = np.random.default_rng(seed)
+    ns = np.exp(rng.uniform(0, np.log(1000), size=k)).astype(np.int64) + 1
+    th = rng.choice(np.asarray(WIDE_THRESHOLDS), size=k)
+    return [f"TopN(f, n={int(n)}, threshold={int(t)})" for n, t in zip(ns, th)]
 
 
 def _distinct_topn_calls(k: int):
@@ -1454,9 +1474,13 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
         return done
 
     log("mesh topn: cache-only requests (distinct calls)")
-    cache_calls = _distinct_topn_calls(B * (nb + 1))
-    out["cache"] = {"calls": "TopN(f, n in {10,50,100,500}, threshold in {1,1000,5000,20000}), all distinct"}
+    cache_calls = _wide_topn_calls(B * (nb + 1), seed=17)
+    out["cache"] = {"calls": f"TopN(f, n=log-uniform 1..1000, threshold one of {len(WIDE_THRESHOLDS)} values "
+                             "1..50000), random per call"}
     timed([" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nb + 1)], out["cache"])
+    cyc = _distinct_topn_calls(B * (nb + 1))
+    out["cache_cycling"] = {"calls": "TopN(f, n in {10,50,100,500} + offset, threshold in {1,1000,5000,20000})"}
+    timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nb + 1)], out["cache_cycling"])
     hot = zipf_rows(rng, B * (nb + 1), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]

@@ -6,7 +6,7 @@
 set -o pipefail
 O=gpurun_out/r05_g
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_topn_exec.py tests/test_gpu_executor.py tests/test_native_http.py tests/test_gpu_kernels.py "tests/test_gpu_shardwidth.py::test_gpu_executor_suite_at_wide_width" -x -q --timeout 900 --timeout-method thread > $O/pytest.log 2>&1 || { tail -c 6000 $O/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_topn_exec.py tests/test_gpu_executor.py tests/test_native_http.py tests/test_gpu_kernels.py tests/test_gpu_rccl_mesh.py "tests/test_gpu_shardwidth.py::test_gpu_executor_suite_at_wide_width" -x -q --timeout 900 --timeout-method thread > $O/pytest.log 2>&1 || { tail -c 6000 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2> $O/bench.err || { tail -c 5000 $O/bench.err; exit 1; }
 python - <<'PY'

@@ -11,4 +11,13 @@ export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_topn -o topn -- python3 -u scripts/prof_topn_paths.py --cols 1000000000 --reqs 200 --paths local --top 5 > $O/prof_topn_trace.log 2>&1 || { tail -c 3000 $O/prof_topn_trace.log; exit 1; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o c4 -- python3 -u scripts/prof_configs.py --which 4 --reps 20 --no-profile > $O/prof_c4.log 2>&1 || { tail -c 3000 $O/prof_c4.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_c4 -o c4 -- python3 -u scripts/prof_configs.py --which 4 --reps 3 --no-profile > $O/pmc_c4.log 2>&1 || { tail -c 3000 $O/pmc_c4.log; exit 1; }
+# hot-rank TopN kernel counters (round-5 evidence for the src TopN bound)
+timeout -k 10 300 python3 -u scripts/topn_kbench.py --reps 1 > $O/topn_kbench.log 2>&1 || { tail -c 2000 $O/topn_kbench.log; exit 1; }
+i=0
+for SET in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
+           "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM"; do
+  i=$((i+1))
+  timeout -s KILL 240 rocprofv3 --pmc $SET --kernel-include-regex "topn_hot_kernel" --output-format csv -d $O/hotpmc -o set$i -- python3 scripts/topn_kbench.py --reps 1 > $O/hotpmc_set$i.log 2>&1 || { tail -20 $O/hotpmc_set$i.log; exit 1; }
+  echo "hot pmc pass $i done"
+done
 echo done

@@ -40,7 +40,10 @@ def main():
     idx = DeviceTopNIndex(view, cache)
     torch.cuda.synchronize()
     out = {"shards": S, "index_build_s": round(time.perf_counter() - t0, 2), "H32": idx.H32, "H16": idx.H16,
-           "lds_bytes": idx.lds, "hot_ranks": idx.R, "slot_entries": idx.entries, "classes": {}}
+           "lds_bytes": idx.lds, "hot_ranks": idx.R, "slot_entries": idx.entries, "classes": {},
+           # set bits of the hot-rank rows: the values one hot-rank launch streams
+           # (each counted for all its queries; PMC instructions / this = per value)
+           "hot_values_per_launch": int(np.asarray(cache.counts)[:, :idx.R].astype(np.int64).sum())}
     B = args.batch
     for name, rows in ((f"hot 0-{B - 1}", range(0, B)), (f"warm 100-{99 + B}", range(100, 100 + B)),
                        ("cold 900-915", range(900, 900 + B))):
