@@ -135,9 +135,13 @@ def _dev_storage(f):
 
 
 def _nreq(ns) -> int:
-    """The cache prefix a cache-only group needs: its largest n (0 = all)."""
+    """The cache prefix a cache-only group needs: its largest n rounded up to
+    a power of two (0 = all).  Rounded so batches of varied n share one node
+    candidate space / count-matrix memo per bucket instead of one per
+    distinct n (the membership kernel still stops each call at its own n)."""
+    from .topn_exec import prefix_bucket
     ns = [int(n) for n in ns]
-    return 0 if any(n == 0 for n in ns) else max(ns)
+    return 0 if any(n == 0 for n in ns) else prefix_bucket(max(ns))
 
 
 class GpuExecutor:

@@ -45,6 +45,15 @@ NOSRC_CHUNK = 64
 FUSED_MAX_CELLS = 1 << 25
 
 
+def prefix_bucket(n: int) -> int:
+    """Cache prefix length for a batch whose largest n is ``n``: the next
+    power of two (at least 16).  Candidate sets and count matrices are
+    memoised per prefix, so a stream of calls with varied n builds a handful
+    of them instead of one per distinct n."""
+    n = max(1, int(n))
+    return max(16, 1 << (n - 1).bit_length())
+
+
 # cache-only TopN batches on a side stream (0: the current stream)
 SIDE_STREAM = os.environ.get("PILOSA_TOPN_SIDE_STREAM", "1") != "0"
 
@@ -540,7 +549,7 @@ class DeviceRankCaches:
         import torch
         Q = len(ns)
         nn = [int(n) for n in ns]
-        nmax = self.K if any(n == 0 for n in nn) else min(self.K, max(nn))
+        nmax = self.K if any(n == 0 for n in nn) else min(self.K, prefix_bucket(max(nn)))
         if not nmax:
             return [[] for _ in range(Q)]
         dev = self.view.device

@@ -360,3 +360,21 @@ def test_src_topn_uses_the_slot_index_at_every_width(lazy_env):
     finally:
         ex.gpu = gpu
     assert [_pairs(r) for r in got] == [_pairs(r) for r in want]
+
+
+def test_cache_only_batch_with_varied_n_matches_host(lazy_env):
+    """Cache-only calls whose n spans several prefix buckets (the count
+    matrix / candidate memo is per power-of-two prefix) in one request, and
+    again in another order: == the host answers."""
+    holder, ex, gpu, _, _ = lazy_env
+    calls = ["TopN(h, n=3)", "TopN(h, n=17, threshold=5)", "TopN(h, n=700)", "TopN(h, n=129, threshold=40)",
+             "TopN(h, n=1)", "TopN(h, n=33)"]
+    for order in (calls, calls[::-1], calls[2:] + calls[:2]):
+        q = " ".join(order)
+        got = ex.execute("i", q).results
+        ex.gpu = None
+        try:
+            want = ex.execute("i", q).results
+        finally:
+            ex.gpu = gpu
+        assert [_pairs(r) for r in got] == [_pairs(r) for r in want], q
