@@ -1563,10 +1563,19 @@ class GpuEngine:
         for vid, slot in view_index.items():
             ordered[slot] = views[vid]
         args = self.bsi_args(bsi_view, depth)
-        out_sum = torch.zeros(len(filters), dtype=torch.int64, device=self.device)
-        out_cnt = torch.zeros(len(filters), dtype=torch.int64, device=self.device)
+        outs = torch.zeros(2 * len(filters), dtype=torch.int64, device=self.device)
+        out_sum, out_cnt = outs[:len(filters)], outs[len(filters):]
         if bsi_view.S and args[2] >= 0:
-            tp, tv = self.upload_batch(progs, ordered)
+            if not exprs and len(filters) == 1:
+                # Sum(field=v): the one empty program is a constant, uploaded once
+                tp = self.__dict__.get("_empty_prog")
+                if tp is None:   # a synchronous copy: any stream may read it afterwards
+                    tp = self._empty_prog = torch.from_numpy(progs.view(np.uint8).copy()).to(self.device)
+                    if self.device.type == "cuda":
+                        torch.cuda.current_stream(self.device).synchronize()
+                tv = self._views_tensor(ordered)
+            else:
+                tp, tv = self.upload_batch(progs, ordered)
             # filter flavour: none / flat folds (2 tiles) / any program (tile stack)
             nprog = progs["nprog"]
             if not (nprog > 0).any():
