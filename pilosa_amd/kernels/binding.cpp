@@ -181,6 +181,21 @@ void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   check_launch("and2_pairs");
 }
 
+void partial_sum_scatter(torch::Tensor partial, int64_t U, int64_t n, torch::Tensor ti, torch::Tensor out) {
+  check_dev(partial, "partial");
+  check_dev(ti, "ti");
+  check_dev(out, "out");
+  TORCH_CHECK(partial.scalar_type() == torch::kInt32 && partial.is_contiguous() && partial.numel() >= U * n,
+              "partial must be int32[U*n]");
+  TORCH_CHECK(ti.scalar_type() == torch::kInt64 && ti.numel() == n, "ti must be int64[n]");
+  TORCH_CHECK(out.scalar_type() == torch::kInt64, "out must be int64");
+  TORCH_CHECK(n < (int64_t(1) << 31) && U < (int64_t(1) << 40), "partial_sum_scatter sizes");
+  // scatter indexes outside out are dropped in the kernel
+  pk::launch_partial_sum_scatter(partial.data_ptr<int32_t>(), U, int(n), ti.data_ptr<int64_t>(),
+                                 out.data_ptr<int64_t>(), out.numel(), cur_stream(partial));
+  check_launch("partial_sum_scatter");
+}
+
 pk::ViewDev viewdev_from(const torch::Tensor& vd) {
   TORCH_CHECK(!vd.is_cuda() && vd.numel() * vd.element_size() == int64_t(sizeof(pk::ViewDev)),
               "view must be a cpu tensor holding one ViewDev (64 bytes)");
@@ -601,6 +616,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("mode") = 0,
         py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
+  m.def("partial_sum_scatter", &partial_sum_scatter, "out[ti[q]] += column sums of int32[U][n] partials");
   m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 0,
         py::arg("variant") = 1);

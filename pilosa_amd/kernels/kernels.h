@@ -56,6 +56,9 @@ void launch_expr_materialize(const QueryProg* progs, int Q, const ViewDev* views
                              const int64_t* offs, uint16_t* outp, hipStream_t st);
 // Count(Intersect(a, b)) via key-major pair kernels (pair_kernels.hip):
 // pairs = uint2[S*16*Q] scratch, partial = int32[S*16*Q] per-(shard,key,query) counts.
+// out[ti[q]] += sum over the U rows of partial[U][n] (pair-kernel partials)
+void launch_partial_sum_scatter(const int32_t* partial, int64_t U, int n, const int64_t* ti, int64_t* out,
+                                int64_t nout, hipStream_t st);
 void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs, int32_t* partial,
                        int cq, int variant, hipStream_t st);
 // BSI predicate -> one bitmap container per (shard, key): payload u16[S*16*4096], meta int64[S*16].

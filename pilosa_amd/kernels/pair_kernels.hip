@@ -997,11 +997,49 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                          pairs, partial);                                                                    \
   }
   switch (cq) {
+    case 4: PK_LAUNCH(4) break;
+    case 8: PK_LAUNCH(8) break;
     case 16: PK_LAUNCH(16) break;
     case 32: PK_LAUNCH(32) break;
     default: PK_LAUNCH(64) break;
   }
 #undef PK_LAUNCH
+}
+
+// Column sums of the pair kernel's per-(unit, query) partials (int32[U][n])
+// scattered straight into the batch result: out[ti[q]] += sum_u partial[u][q].
+// Replaces a strided torch reduction (~67 us for a 36-query serving batch,
+// profiles/r05_serve/) plus an index_copy.  Block = 64 columns x 4 row lanes
+// over a 128-row chunk; one int64 atomic per (block, column).
+__global__ __launch_bounds__(256) void partial_sum_scatter_kernel(const int32_t* __restrict__ partial, int64_t U,
+                                                                  int n, const int64_t* __restrict__ ti,
+                                                                  unsigned long long* __restrict__ out,
+                                                                  int64_t nout) {
+  __shared__ long long acc[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int q = int(blockIdx.x) * 64 + tx;
+  const int64_t r0 = int64_t(blockIdx.y) * 128;
+  const int64_t r1 = r0 + 128 < U ? r0 + 128 : U;
+  long long a = 0;
+  if (q < n) {
+#pragma unroll 8
+    for (int64_t r = r0 + ty; r < r1; r += 4) a += partial[r * n + q];
+  }
+  acc[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && q < n) {
+    const long long t = acc[0][tx] + acc[1][tx] + acc[2][tx] + acc[3][tx];
+    const int64_t o = ti[q];
+    if (t && o >= 0 && o < nout) atomicAdd(out + o, (unsigned long long)t);
+  }
+}
+
+void launch_partial_sum_scatter(const int32_t* partial, int64_t U, int n, const int64_t* ti, int64_t* out,
+                                int64_t nout, hipStream_t st) {
+  if (U <= 0 || n <= 0) return;
+  const dim3 grid(unsigned((n + 63) / 64), unsigned((U + 127) / 128));
+  hipLaunchKernelGGL(partial_sum_scatter_kernel, grid, dim3(256), 0, st, partial, U, n, ti,
+                     reinterpret_cast<unsigned long long*>(out), nout);
 }
 
 }  // namespace pk

@@ -1205,7 +1205,10 @@ class GpuEngine:
         out = torch.zeros(Q, dtype=torch.int64, device=self.device)
         for tp, ti, kind, n in parts:
             if kind == KIND_AND2:
-                o = self._and2_partial(tp, tv, S, n).sum(dim=(0, 1), dtype=torch.int64)
+                # column sums scattered into out by one kernel (a strided torch
+                # reduce + index_copy cost ~70 us per small serving batch)
+                self.ext.partial_sum_scatter(self._and2_partial(tp, tv, S, n).view(-1), S * 16, n, ti, out)
+                continue
             else:
                 o = torch.zeros(n, dtype=torch.int64, device=self.device)
                 mode = _KERNEL_MODE[kind]

@@ -350,3 +350,31 @@ def test_bsi_minmax_fold_kernel_matches_host_fold(which, F, sub):
     out = torch.full((3,), -7, dtype=torch.int64, device=dev)
     kernels().bsi_minmax_fold(torch.from_numpy(o.reshape(-1)).to(dev), F, 16 * sub, int(which == "min"), out)
     assert out.cpu().tolist() == want
+
+
+@pytest.mark.parametrize("U,n", [(1, 1), (15264, 36), (300, 130), (1000, 4096)])
+def test_partial_sum_scatter_matches_torch(U, n):
+    """partial_sum_scatter (pair-kernel partial column sums scattered into
+    the batch result) == torch sum + index_copy; out-of-range targets are
+    dropped."""
+    import torch
+
+    from pilosa_amd.ops.device import kernels
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(U + n)
+    part = torch.randint(0, 1 << 20, (U, n), generator=g, dtype=torch.int32)
+    ti = torch.randperm(n + 3, generator=g)[:n].to(torch.int64)
+    want = torch.zeros(n + 3, dtype=torch.int64)
+    want.index_copy_(0, ti, part.to(torch.int64).sum(dim=0))
+    keep = ti < n + 3
+    out = torch.zeros(n + 3, dtype=torch.int64, device=dev)
+    kernels().partial_sum_scatter(part.to(dev).view(-1), U, n, ti.to(dev), out)
+    assert torch.equal(out.cpu(), want) and bool(keep.all())
+    # a target outside out is dropped, not written
+    bad = ti.clone()
+    bad[0] = n + 100
+    out2 = torch.zeros(n + 3, dtype=torch.int64, device=dev)
+    kernels().partial_sum_scatter(part.to(dev).view(-1), U, n, bad.to(dev), out2)
+    want2 = want.clone()
+    want2[ti[0]] = 0
+    assert torch.equal(out2.cpu(), want2)
