@@ -516,7 +516,13 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // while the current pair is counted (PD = 1: the shipped v6).  The control
 // skeleton (DBG 1) with v6's occupancy spends 4.6 of its 7.5 ms waiting on
 // these heads (profiles/r05_pairs/).
-template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1>
+//
+// ONE (v38): pairs whose A is not reused by the next pair ("one-off": nearly
+// every pair of a small serving batch) skip staging A when it costs more than
+// it saves: a bitmap A is probed in place by B's values (its prefetched head,
+// global gathers, no 8 KiB LDS copy), and of two arrays the smaller one is
+// staged and the larger probes it.
+template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1, bool ONE = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -653,6 +659,25 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
         } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP && meta_n(mA) <= SMALL_ARRAY_N) {
           c = probe_small<false>(gp(reinterpret_cast<const uint32_t*>(pB)), pA, meta_n(mA));
         } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
+          lds_wait();
+          stage(lb, pB, mB);
+          cached = NONE;
+          cached_v = -1;
+          c = count_vs_lds(lb, pA, mA);
+        } else if (ONE && !next_same && tA == CT_BITMAP && tB == CT_ARRAY) {
+          // B's values probe A where it lies (B's head chunk is in registers)
+          const auto gA = gp(reinterpret_cast<const uint32_t*>(pA));
+          const int nb = meta_n(mB);
+          if (nb <= 64) {
+            const uint32_t v = lane < nb ? head.x : 0u;
+            c = int(__builtin_amdgcn_ubfe(gA[v >> 5], v, 1u)) - pad_hits(gA, 64, nb);
+          } else if (nb <= 512) {
+            c = probe8<false>(gA, lane < ((nb + 7) >> 3) ? head : make_uint4(0, 0, 0, 0)) - pad_hits(gA, 512, nb);
+          } else {
+            c = probe_pipe<false>(gA, pB, nb);
+          }
+        } else if (ONE && !next_same && tA == CT_ARRAY && tB == CT_ARRAY && meta_n(mB) < meta_n(mA)) {
+          // the smaller array is staged, the larger one probes it
           lds_wait();
           stage(lb, pB, mB);
           cached = NONE;
@@ -989,6 +1014,9 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                          progs, Q, views, S, pairs, partial);                                                \
     else if (variant >= 31 && variant <= 37)                                                                 \
       launch_v6_dbg<CQV>(variant - 30, wv, progs, Q, views, S, pairs, partial, st);                          \
+    else if (variant == 38)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true>), dim3(unsigned(wv)), dim3(64), 0, st, \
+                         progs, Q, views, S, pairs, partial);                                                \
     else if (variant == 13)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q,    \
                          views, S, pairs, partial);                                                          \

@@ -93,7 +93,7 @@ class NativeHTTPServer:
         from pilosa_amd import _httpd
 
         if batchers is None:
-            batchers = int(os.environ.get("PILOSA_HTTP_COUNT_BATCHERS", "3"))
+            batchers = int(os.environ.get("PILOSA_HTTP_COUNT_BATCHERS", "2"))
         if topn_batchers is None:
             topn_batchers = int(os.environ.get("PILOSA_HTTP_TOPN_BATCHERS", "2"))
 

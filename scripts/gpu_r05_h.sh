@@ -8,9 +8,9 @@ O=gpurun_out/r05_h
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_executor.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -c 5000 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-timeout -k 10 400 python -u scripts/kbench.py --batch 32 --reps 20 --cq 32,16,8,4 --variants 31,33,34,35 > $O/kbench_b32.log 2>&1 || { tail -c 3000 $O/kbench_b32.log; exit 1; }
+timeout -k 10 400 python -u scripts/kbench.py --batch 32 --reps 20 --cq 32,16,8,4 --variants 38,38@16,38@8,31,33,34,35 > $O/kbench_b32.log 2>&1 || { tail -c 3000 $O/kbench_b32.log; exit 1; }
 grep -v "^{" $O/kbench_b32.log
-timeout -k 10 400 python -u scripts/kbench.py --batch 96 --reps 20 --cq 32,16,8,4 > $O/kbench_b96.log 2>&1 || { tail -c 3000 $O/kbench_b96.log; exit 1; }
+timeout -k 10 400 python -u scripts/kbench.py --batch 96 --reps 20 --cq 32,16,8,4 --variants 38,38@16,38@8 > $O/kbench_b96.log 2>&1 || { tail -c 3000 $O/kbench_b96.log; exit 1; }
 grep -v "^{" $O/kbench_b96.log
 for CQ in 16 8 4; do
   PILOSA_AND2_CQ=$CQ timeout -k 10 300 python -u scripts/bench_server.py --seconds 4 --batchers 1,2,3 > $O/serve_cq$CQ.log 2>&1 || { tail -c 3000 $O/serve_cq$CQ.log; exit 1; }

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--shards", type=int, default=0, help="0 = full 954")
     ap.add_argument("--cq", default="0,32,64", help="pair-kernel chunk sizes (queries per wave)")
     ap.add_argument("--no-tile", action="store_true", help="skip the generic tile kernel")
-    ap.add_argument("--variants", default="", help="extra kernel variants at --cq's first size, e.g. 4,5")
+    ap.add_argument("--variants", default="", help="extra kernel variants at --cq's first size, e.g. 4,5 (38@8: at 8 queries per wave)")
     args = ap.parse_args()
     import torch
 
@@ -46,7 +46,12 @@ def main():
     configs = [] if args.no_tile else [("tile", {"use_and2": False})]
     configs += [(f"and2_cq{c}", {"and2_cq": int(c), "and2_variant": 1}) for c in args.cq.split(",") if c]
     cq0 = int(args.cq.split(",")[0]) if args.cq else 64
-    configs += [(f"and2var{v}_cq{cq0}", {"and2_cq": cq0, "and2_variant": int(v)}) for v in args.variants.split(",") if v]
+    for v in args.variants.split(","):
+        if not v:
+            continue
+        vv, _, cq = v.partition("@")   # "38@8": variant 38 at 8 queries per wave
+        cq = int(cq) if cq else cq0
+        configs.append((f"and2var{vv}_cq{cq}", {"and2_cq": cq, "and2_variant": int(vv)}))
     for name, cfg in configs:
         eng = GpuEngine(dev)
         for k, v in cfg.items():
