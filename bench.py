@@ -1664,7 +1664,7 @@ def main():
                     help="also time the pair-count src TopN path on this many batches (0 = skip)")
     ap.add_argument("--configs", default=os.environ.get("PILOSA_BENCH_CONFIGS", "4,5"),
                     help="also run BASELINE configs 4 (BSI) and 5 (time union) into extra (empty = skip)")
-    ap.add_argument("--config-reps", type=int, default=5)
+    ap.add_argument("--config-reps", type=int, default=20)
     ap.add_argument("--serve-seconds", type=float, default=5.0,
                     help="disk mode, 1 GPU: native-HTTP serving run on the same data dir (0 = skip)")
     ap.add_argument("--serve-conns", type=int, default=128)

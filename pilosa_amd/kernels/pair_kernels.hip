@@ -174,7 +174,12 @@ __device__ __forceinline__ void lds_clear(uint64_t* lb) {
   for (int i = 0; i < 8; i++) l2[i * 64 + lane] = make_ulong2(0, 0);
 }
 
-// Stage a container of any type into lb as a (swizzled) bitmap.
+// Stage a container of any type into lb as a (swizzled) bitmap.  BST
+// (batched staging): an array's chunks are all loaded (4 per lane per round
+// trip) before the LDS clear and the scatter, instead of one dependent load
+// per 512 values -- a 4096-value array was 8 serial round trips, and staging
+// was ~60 % of a 32-query batch's pair-kernel time (profiles/r05_serve/).
+template <bool BST = false>
 __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m) {
   const int lane = lane_id();
   const int type = meta_type(m);
@@ -189,9 +194,45 @@ __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m
     lds_wait();
     return;
   }
+  uint32_t* l32 = reinterpret_cast<uint32_t*>(lb);
+  if (BST && type == CT_ARRAY) {
+    const int n = meta_n(m);
+    const auto p4 = gp(reinterpret_cast<const uint4*>(p));
+    const int n8 = (n + 7) >> 3;
+    bool cleared = false;
+    for (int b = 0; b < n8; b += 4 * 64) {
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int e8 = b + k * 64 + lane;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (e8 < n8) v[k] = p4[e8];
+      }
+      if (!cleared) {   // the clear overlaps the first round of loads
+        lds_clear(lb);
+        lds_wait();
+        cleared = true;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int e8 = b + k * 64 + lane;
+        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        const int rem = n - e8 * 8;
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          const uint32_t x = (w[t >> 1] >> ((t & 1) * 16)) & 0xffff;
+          if (e8 < n8) atomicOr(l32 + lds_swz(x >> 5), t < rem ? (1u << (x & 31)) : 0u);
+        }
+      }
+    }
+    if (!cleared) {
+      lds_clear(lb);
+    }
+    lds_wait();
+    return;
+  }
   lds_clear(lb);
   lds_wait();
-  uint32_t* l32 = reinterpret_cast<uint32_t*>(lb);
   if (type == CT_ARRAY) {
     const int n = meta_n(m);
     const auto p4 = gp(reinterpret_cast<const uint4*>(p));
@@ -522,7 +563,7 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // it saves: a bitmap A is probed in place by B's values (its prefetched head,
 // global gathers, no 8 KiB LDS copy), and of two arrays the smaller one is
 // staged and the larger probes it.
-template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1, bool ONE = false>
+template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1, bool ONE = false, bool BST = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -635,11 +676,11 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
             !(!next_same && tA == CT_ARRAY && tB == CT_BITMAP && meta_n(mA) <= SMALL_ARRAY_N)) {
           lds_wait();
           if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
-            stage(lb, pB, mB);
+            stage<BST>(lb, pB, mB);
             cached = NONE;
             cached_v = -1;
           } else {
-            stage(lb, pA, mA);
+            stage<BST>(lb, pA, mA);
             cached = a;
             cached_v = va;
           }
@@ -660,7 +701,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
           c = probe_small<false>(gp(reinterpret_cast<const uint32_t*>(pB)), pA, meta_n(mA));
         } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
           lds_wait();
-          stage(lb, pB, mB);
+          stage<BST>(lb, pB, mB);
           cached = NONE;
           cached_v = -1;
           c = count_vs_lds(lb, pA, mA);
@@ -679,7 +720,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
         } else if (ONE && !next_same && tA == CT_ARRAY && tB == CT_ARRAY && meta_n(mB) < meta_n(mA)) {
           // the smaller array is staged, the larger one probes it
           lds_wait();
-          stage(lb, pB, mB);
+          stage<BST>(lb, pB, mB);
           cached = NONE;
           cached_v = -1;
           c = count_vs_lds(lb, pA, mA);
@@ -688,7 +729,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
           if (APF && aok && small_array(mA))
             stage_array_head(lb, mA, ahead);
           else
-            stage(lb, pA, mA);
+            stage<BST>(lb, pA, mA);
           cached = a;
           cached_v = va;
           if constexpr (SB > 0) {
@@ -1014,6 +1055,12 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                          progs, Q, views, S, pairs, partial);                                                \
     else if (variant >= 31 && variant <= 37)                                                                 \
       launch_v6_dbg<CQV>(variant - 30, wv, progs, Q, views, S, pairs, partial, st);                          \
+    else if (variant == 39)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, false, true>), dim3(unsigned(wv)), dim3(64), 0, \
+                         st, progs, Q, views, S, pairs, partial);                                            \
+    else if (variant == 40)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true, true>), dim3(unsigned(wv)), dim3(64), 0, \
+                         st, progs, Q, views, S, pairs, partial);                                            \
     else if (variant == 38)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true>), dim3(unsigned(wv)), dim3(64), 0, st, \
                          progs, Q, views, S, pairs, partial);                                                \

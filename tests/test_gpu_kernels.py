@@ -187,7 +187,7 @@ def test_bitgemm_count_matrix_matches_host(mode):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("variant", [6, 10, 12, 16, 17, 18, 19, 20, 38])
+@pytest.mark.parametrize("variant", [6, 10, 12, 16, 17, 18, 19, 20, 38, 39, 40])
 @pytest.mark.parametrize("cq", [4, 8, 16, 32, 64])
 def test_pair_kernel_array_size_boundaries(cq, variant):
     """Array containers of 1, 63, 64, 65, 255, 256, 257 (the small-probe
