@@ -850,6 +850,7 @@ __global__ __launch_bounds__(256) void bsi_sum_keys_kernel(const QueryProg* __re
   auto lane_find = [&](int64_t d) -> int64_t {
     if (d < 0) return -1;
     const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+    if (hi - lo == 16) return lo + j;   // every key present (dense planes): no meta walk
     for (int64_t c = lo; c < hi; c++)
       if (meta_j(bv.meta[c]) == j) return c;
     return -1;
@@ -876,18 +877,43 @@ __global__ __launch_bounds__(256) void bsi_sum_keys_kernel(const QueryProg* __re
   if (cs >= 0) tile_load(sign, bv.payload, bv.meta[cs], ws.lb);
   else tile_zero(sign);
   int64_t acc_sum = 0;
-  for (int i = 0; i < bsi.depth; i++) {
-    const int64_t cb = rl_i64(mine, i);
-    if (cb < 0) continue;
-    tile_load(bits, bv.payload, bv.meta[cb], ws.lb);
+  // planes double-buffered: the next present plane's tile is in flight
+  // while the current one is counted (one load round trip per plane, not
+  // a wait before every plane)
+  const uint64_t present = __ballot(mine >= 0) & (bsi.depth >= 64 ? ~0ull : ((1ull << bsi.depth) - 1));
+  auto count_plane = [&](const Tile& t, int i) {
     int pc = 0, nc = 0;
 #pragma unroll
     for (int w = 0; w < 8; w++) {
-      const uint64_t bx = bits.w[w].x & consider.w[w].x, by = bits.w[w].y & consider.w[w].y;
+      const uint64_t bx = t.w[w].x & consider.w[w].x, by = t.w[w].y & consider.w[w].y;
       pc += __popcll(bx & ~sign.w[w].x) + __popcll(by & ~sign.w[w].y);
       nc += __popcll(bx & sign.w[w].x) + __popcll(by & sign.w[w].y);
     }
     acc_sum += int64_t(uint64_t(int64_t(pc - nc)) << i);
+  };
+  Tile bits2;
+  uint64_t left = present;
+  int cur = left ? __builtin_ctzll(left) : -1;
+  if (cur >= 0) {
+    left &= left - 1;
+    tile_load(bits, bv.payload, bv.meta[rl_i64(mine, cur)], ws.lb);
+  }
+  while (cur >= 0) {
+    int nxt = left ? __builtin_ctzll(left) : -1;
+    if (nxt >= 0) {
+      left &= left - 1;
+      tile_load(bits2, bv.payload, bv.meta[rl_i64(mine, nxt)], ws.lb);
+    }
+    count_plane(bits, cur);
+    cur = nxt;
+    if (cur < 0) break;
+    nxt = left ? __builtin_ctzll(left) : -1;
+    if (nxt >= 0) {
+      left &= left - 1;
+      tile_load(bits, bv.payload, bv.meta[rl_i64(mine, nxt)], ws.lb);
+    }
+    count_plane(bits2, cur);
+    cur = nxt;
   }
   const int64_t tsum = wave_sum_i64(acc_sum);
   const int64_t tcnt = wave_sum_i64(acc_cnt);
@@ -927,6 +953,10 @@ __device__ __forceinline__ void plane_index(BsiCtx& c) {
   int64_t found = -1;
   if (d >= 0) {
     const int64_t lo = c.base + c.rp[d], hi = c.base + c.rp[d + 1];
+    if (hi - lo == 16) {   // every key present (dense planes): no meta walk
+      c.planes = lo + c.j;
+      return;
+    }
     for (int64_t ci = lo; ci < hi; ci++)
       if (meta_j(c.bv.meta[ci]) == c.j) {
         found = ci;

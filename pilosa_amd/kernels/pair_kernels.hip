@@ -1023,7 +1023,12 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   hipLaunchKernelGGL(pair_build_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, progs, Q, views, S,
                      pairs);
   const int64_t units = int64_t(S) * 16;
-  if (cq <= 0) cq = Q <= 2048 ? 32 : 64;
+  // serving-size batches (<= 128 queries: almost every pair is one-off):
+  // 8 queries per wave, one-off pairs probed in place / smaller array staged,
+  // batched array staging (variant 40) -- 68.7k vs 61.1k req/s with 2
+  // group-commit threads (profiles/r05_serve/).  Bigger batches keep v6.
+  if (variant == 6 && cq <= 0 && Q <= 128) variant = 40;
+  if (cq <= 0) cq = Q <= 128 ? 8 : (Q <= 2048 ? 32 : 64);
 #define PK_LAUNCH(CQV)                                                                                       \
   {                                                                                                          \
     const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                        \
