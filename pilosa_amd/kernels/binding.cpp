@@ -181,6 +181,22 @@ void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
   check_launch("and2_pairs");
 }
 
+pk::ViewDev viewdev_from(const torch::Tensor& vd);
+
+void shadow_build(torch::Tensor view, int64_t S, torch::Tensor rows, torch::Tensor shadow) {
+  check_dev(rows, "rows");
+  check_dev(shadow, "shadow");
+  TORCH_CHECK(rows.scalar_type() == torch::kInt32, "rows must be int32[R]");
+  const int64_t R = rows.numel();
+  TORCH_CHECK(shadow.scalar_type() == torch::kInt64 && shadow.is_contiguous() && shadow.numel() == R * S * 16 * 1024,
+              "shadow must be int64[R*S*16*1024]");
+  pk::ViewDev v = viewdev_from(view);
+  TORCH_CHECK(R >= 0 && R < (int64_t(1) << 20) && S > 0, "shadow_build sizes");
+  pk::launch_shadow_build(v, int(S), rows.data_ptr<int32_t>(), int(R), reinterpret_cast<uint64_t*>(shadow.data_ptr<int64_t>()),
+                          cur_stream(shadow));
+  check_launch("shadow_build");
+}
+
 void partial_sum_scatter(torch::Tensor partial, int64_t U, int64_t n, torch::Tensor ti, torch::Tensor out) {
   check_dev(partial, "partial");
   check_dev(ti, "ti");
@@ -616,6 +632,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("mode") = 0,
         py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
+  m.def("shadow_build", &shadow_build, "dense bitmap shadows of hot rows for the pair kernels");
   m.def("partial_sum_scatter", &partial_sum_scatter, "out[ti[q]] += column sums of int32[U][n] partials");
   m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 0,

@@ -38,7 +38,11 @@ struct ViewDev {
   const uint16_t* payload;     // [P]
   int64_t D;
   const uint16_t* keymask;     // [S][D] key-presence mask per (shard, row); nullptr = derive from meta
-  int64_t pad[2];
+  // dense bitmap shadows of the view's hottest rows (pair kernels): row d's
+  // key-j container in shard s as a 1024-word bitmap at
+  // shadow + ((shadow_slot[d] * S + s) * 16 + j) * 1024; nullptr / -1 = none
+  const uint64_t* shadow;
+  const int32_t* shadow_slot;  // [D]
 };
 static_assert(sizeof(ViewDev) == 64, "ViewDev layout");
 
@@ -127,6 +131,8 @@ void launch_topn_src(const TopNLaunch& a, int mode, hipStream_t st);
 // rows; *has_run set when a run container needs materialising.
 void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_t* counts, int64_t* offs,
                      int32_t* has_run, hipStream_t st);
+// shadow[r][s][j] = row rows[r]'s key-j container of shard s as a bitmap
+void launch_shadow_build(const ViewDev& v, int S, const int32_t* rows, int R, uint64_t* shadow, hipStream_t st);
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st);
 // Row counts of (shard, dense row) entries -> out[N] (device rank caches).
 void launch_row_counts(const ViewDev& v, const int32_t* shard_of, const int32_t* dense, int64_t N, int32_t* out,

@@ -517,6 +517,101 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
   return runs_in_lds(lb, p);
 }
 
+// ---- dense shadows (SHD): a hot row's container as a 1024-word bitmap in
+// HBM (DeviceView.ensure_shadow, shadow_build_kernel), so staging it is one
+// coalesced 8 KiB copy and a one-off pair reads it in place.
+
+// copy a global bitmap into the LDS bitmap (one round trip: all 8 loads first)
+__device__ __forceinline__ void stage_bitmap(uint64_t* lb, const uint64_t* g) {
+  const int lane = lane_id();
+  const auto g2 = gp(reinterpret_cast<const ulong2*>(g));
+  ulong2* l2 = reinterpret_cast<ulong2*>(lb);
+  ulong2 t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = g2[i * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < 8; i++) l2[lds_swzc(uint32_t(i * 64 + lane))] = t[i];
+  lds_wait();
+}
+
+// |B & A| for A a bitmap in global memory (a shadow), B any container with
+// its head already in registers; a run B goes through the LDS bitmap
+__device__ __forceinline__ int count_global_vs_head(uint64_t* lb, const uint64_t* gA, const uint16_t* pB, int64_t mB,
+                                                    const uint4 head) {
+  const int lane = lane_id();
+  const int t = meta_type(mB);
+  if (t == CT_ARRAY) {
+    const auto g32 = gp(reinterpret_cast<const uint32_t*>(gA));
+    const int nb = meta_n(mB);
+    if (nb <= 64) {
+      const uint32_t v = lane < nb ? head.x : 0u;
+      return int(__builtin_amdgcn_ubfe(g32[v >> 5], v, 1u)) - pad_hits(g32, 64, nb);
+    }
+    if (nb <= 512) return probe8<false>(g32, lane < ((nb + 7) >> 3) ? head : make_uint4(0, 0, 0, 0)) - pad_hits(g32, 512, nb);
+    return probe_pipe<false>(g32, pB, nb);
+  }
+  if (t == CT_BITMAP) {
+    const auto a4 = gp(reinterpret_cast<const uint4*>(gA));
+    const auto b4 = gp(reinterpret_cast<const uint4*>(pB));
+    int c;
+    {   // two halves keep the kernel inside its 96-VGPR budget (5 waves/SIMD)
+      uint4 x[4], y[3];
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = a4[k * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < 3; k++) y[k] = b4[(k + 1) * 64 + lane];
+      c = popc_and4(x[0], head);
+#pragma unroll
+      for (int k = 0; k < 3; k++) c += popc_and4(x[k + 1], y[k]);
+    }
+    {
+      uint4 x[4], y[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = a4[(k + 4) * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < 4; k++) y[k] = b4[(k + 4) * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < 4; k++) c += popc_and4(x[k], y[k]);
+    }
+    return c;
+  }
+  lds_wait();
+  stage_bitmap(lb, gA);
+  return runs_in_lds(lb, pB);
+}
+
+// shadow[r][s][j]: row rows[r]'s key-j container of shard s as a bitmap (zeros
+// where absent).  One wave per (r, s, j): built in LDS by stage(), copied out.
+__global__ __launch_bounds__(64) void shadow_build_kernel(ViewDev v, int S, const int32_t* __restrict__ rows, int R,
+                                                          uint64_t* __restrict__ shadow) {
+  __shared__ uint64_t lb[1024];
+  const int64_t w = int64_t(blockIdx.x) + int64_t(blockIdx.y) * 65535;
+  if (w >= int64_t(R) * S * 16) return;
+  const int j = int(w & 15);
+  const int64_t rs = w >> 4;
+  const int s = int(rs % S);
+  const int r = int(rs / S);
+  const int lane = lane_id();
+  ulong2* dst = reinterpret_cast<ulong2*>(shadow + w * 1024);
+  const int64_t d = rows[r];
+  int64_t c = -1;
+  if (d >= 0) {
+    int64_t lo;
+    const uint32_t pres = row_keys(v, s, d, lo);
+    if ((pres >> j) & 1) c = lo + __popc(pres & ((1u << j) - 1));
+  }
+  if (c < 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) dst[i * 64 + lane] = make_ulong2(0, 0);
+    return;
+  }
+  const int64_t m = gp(v.meta)[c];
+  stage<true>(lb, payload_of(v, m), m);
+  const ulong2* l2 = reinterpret_cast<const ulong2*>(lb);
+#pragma unroll
+  for (int i = 0; i < 8; i++) dst[i * 64 + lane] = l2[lds_swzc(uint32_t(i * 64 + lane))];
+}
+
 // Array A of <= 512 values staged from its chunk already in registers (one
 // 16-byte chunk per lane, loaded while the previous pair was counted).
 __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const uint4 v4) {
@@ -563,7 +658,8 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // it saves: a bitmap A is probed in place by B's values (its prefetched head,
 // global gathers, no 8 KiB LDS copy), and of two arrays the smaller one is
 // staged and the larger probes it.
-template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1, bool ONE = false, bool BST = false>
+template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1, bool ONE = false, bool BST = false,
+          bool SHD = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -581,6 +677,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
   int vai = -1;
   int64_t ma = 0, mb = 0;
   uint64_t pal = 0, pbl = 0;
+  uint64_t sha = 0;   // SHD: A's bitmap shadow for this unit (0 = none)
   if (lane < nq) {
     const uint2 e = pairs[u * Q + q0 + lane];
     if (e.x != NONE) {
@@ -591,6 +688,10 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       mb = gp(views[vbi].meta)[e.y];
       pal = reinterpret_cast<uint64_t>(payload_of(views[vai], ma));
       pbl = reinterpret_cast<uint64_t>(payload_of(views[vbi], mb));
+      if (SHD && views[vai].shadow_slot != nullptr && meta_type(ma) != CT_BITMAP) {
+        const int sl = gp(views[vai].shadow_slot)[progs[q0 + lane].leaf_row[0]];
+        if (sl >= 0) sha = reinterpret_cast<uint64_t>(views[vai].shadow + ((int64_t(sl) * S + (u >> 4)) * 16 + (u & 15)) * 1024);
+      }
     }
   }
   uint64_t todo = __ballot(ea != NONE);
@@ -699,6 +800,23 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
           c = and_global_bitmaps(reinterpret_cast<const uint64_t*>(pA), reinterpret_cast<const uint64_t*>(pB));
         } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP && meta_n(mA) <= SMALL_ARRAY_N) {
           c = probe_small<false>(gp(reinterpret_cast<const uint32_t*>(pB)), pA, meta_n(mA));
+        } else if (SHD && rl_u64(sha, i) != 0) {
+          // A has a dense shadow: a run of pairs copies it into LDS in one
+          // round trip; a one-off pair reads it in place
+          const uint64_t* gA = reinterpret_cast<const uint64_t*>(rl_u64(sha, i));
+          if (next_same) {
+            lds_wait();
+            stage_bitmap(lb, gA);
+            cached = a;
+            cached_v = va;
+            c = count_vs_head<true>(lb, pB, mB, head);
+          } else {
+            c = count_global_vs_head(lb, gA, pB, mB, head);
+            if (tB == CT_RUN) {
+              cached = NONE;
+              cached_v = -1;
+            }
+          }
         } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
           lds_wait();
           stage<BST>(lb, pB, mB);
@@ -1006,6 +1124,13 @@ void launch_v6_dbg(int dbg, int64_t wv, const QueryProg* progs, int Q, const Vie
   }
 }
 
+void launch_shadow_build(const ViewDev& v, int S, const int32_t* rows, int R, uint64_t* shadow, hipStream_t st) {
+  const int64_t w = int64_t(R) * S * 16;
+  if (w <= 0) return;
+  const dim3 grid(unsigned(w < 65535 ? w : 65535), unsigned((w + 65534) / 65535));
+  hipLaunchKernelGGL(shadow_build_kernel, grid, dim3(64), 0, st, v, S, rows, R, shadow);
+}
+
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st) {
   const int64_t n = int64_t(S) * v.D;
   if (n == 0) return;
@@ -1028,6 +1153,7 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   // batched array staging (variant 40) -- 68.7k vs 61.1k req/s with 2
   // group-commit threads (profiles/r05_serve/).  Bigger batches keep v6.
   if (variant == 6 && cq <= 0 && Q <= 128) variant = 40;
+  if (variant == 41 && cq <= 0 && Q <= 128) variant = 42;   // the same with dense shadows
   if (cq <= 0) cq = Q <= 128 ? 8 : (Q <= 2048 ? 32 : 64);
 #define PK_LAUNCH(CQV)                                                                                       \
   {                                                                                                          \
@@ -1060,6 +1186,12 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                          progs, Q, views, S, pairs, partial);                                                \
     else if (variant >= 31 && variant <= 37)                                                                 \
       launch_v6_dbg<CQV>(variant - 30, wv, progs, Q, views, S, pairs, partial, st);                          \
+    else if (variant == 41)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, false, false, true>), dim3(unsigned(wv)),  \
+                         dim3(64), 0, st, progs, Q, views, S, pairs, partial);                               \
+    else if (variant == 42)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true, true, true>), dim3(unsigned(wv)),    \
+                         dim3(64), 0, st, progs, Q, views, S, pairs, partial);                               \
     else if (variant == 39)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, false, true>), dim3(unsigned(wv)), dim3(64), 0, \
                          st, progs, Q, views, S, pairs, partial);                                            \

@@ -45,7 +45,7 @@ _OPS = {"and": OP_AND, "or": OP_OR, "xor": OP_XOR, "andnot": OP_ANDNOT}
 QPROG_DTYPE = np.dtype([("nleaf", "<i4"), ("nprog", "<i4"), ("leaf_view", "<i4", (MAXLEAF,)),
                         ("leaf_row", "<i8", (MAXLEAF,)), ("prog", "u1", (MAXPROG,)), ("pad", "<i8", (3,))])
 VIEWDEV_DTYPE = np.dtype([("rowptr", "<u8"), ("shard_base", "<u8"), ("meta", "<u8"), ("payload", "<u8"),
-                          ("D", "<i8"), ("keymask", "<u8"), ("pad", "<i8", (2,))])
+                          ("D", "<i8"), ("keymask", "<u8"), ("shadow", "<u8"), ("shadow_slot", "<u8")])
 assert QPROG_DTYPE.itemsize == 256 and VIEWDEV_DTYPE.itemsize == 64
 
 _ext = None
@@ -876,7 +876,87 @@ class DeviceView:
         km = getattr(self, "_keymask", None)
         if km is not None and km[0] == self.generation:
             rec["keymask"] = km[1].data_ptr()
+        sh = getattr(self, "_shadow", None)
+        if sh is not None and sh[0] == self.generation:
+            rec["shadow"] = sh[1].data_ptr()
+            rec["shadow_slot"] = sh[2].data_ptr()
         return rec
+
+    def shadow_fresh(self) -> bool:
+        sh = getattr(self, "_shadow", None)
+        return sh is not None and sh[0] == self.generation
+
+    # dense bitmap shadows of the hottest rows (pair_kernels.hip SHD): up to
+    # SHADOW_ROWS rows, within SHADOW_MAX_BYTES and a quarter of free HBM
+    SHADOW_ROWS = int(os.environ.get("PILOSA_SHADOW_ROWS", "256"))
+    SHADOW_MAX_BYTES = int(os.environ.get("PILOSA_SHADOW_MAX_GB", "40")) << 30
+    SHADOW_MIN_INTERVAL_S = 30.0
+    SHADOW_SAMPLE_SHARDS = 8
+
+    def _hot_dense_rows(self, R: int) -> np.ndarray:
+        """The R dense rows with the most bits over a sample of shards
+        (a hot row of a Zipf-like field is hot in every shard)."""
+        D1 = self.D + 1
+        picks = sorted(set(np.linspace(0, self.S - 1, min(self.S, self.SHADOW_SAMPLE_SHARDS)).astype(int).tolist()))
+        tot = np.zeros(self.D, np.int64)
+        sb = self._sb_host
+        for si in picks:
+            rp = self.t_rowptr[si * D1:(si + 1) * D1].cpu().numpy().astype(np.int64)
+            n = int(rp[-1])
+            if n == 0:
+                continue
+            m = self.t_meta[int(sb[si]):int(sb[si]) + n].cpu().numpy()
+            card = (m >> 6) & 0x1FFFF
+            row = np.repeat(np.arange(self.D, dtype=np.int64), np.diff(rp))
+            tot += np.bincount(row, weights=card, minlength=self.D).astype(np.int64)
+        R = min(R, int((tot > 0).sum()))
+        if R <= 0:
+            return np.zeros(0, np.int32)
+        top = np.argpartition(-tot, R - 1)[:R]
+        return np.sort(top).astype(np.int32)
+
+    def ensure_shadow(self) -> bool:
+        """Build (or refresh, at most every SHADOW_MIN_INTERVAL_S after
+        writes) the dense bitmap shadows of this view's hottest rows: each
+        row's container of every (shard, key) as a 1024-word bitmap in HBM,
+        so the pair kernels stage it with one coalesced copy or read it in
+        place.  A stale shadow is simply not passed.  Returns whether it is
+        fresh."""
+        import time
+
+        import torch
+
+        if self.SHADOW_ROWS <= 0 or self.device.type != "cuda" or not self.S or not self.D:
+            return False
+        sh = getattr(self, "_shadow", None)
+        if sh is not None and sh[0] == self.generation:
+            return True
+        now = time.monotonic()
+        if sh is not None and now - sh[3] < self.SHADOW_MIN_INTERVAL_S:
+            return False
+        if sh is None and getattr(self, "_shadow_declined", None) == self.generation:
+            return False
+        per_row = self.S * 16 * 8192
+        free, _ = torch.cuda.mem_get_info(self.device)
+        R = min(self.SHADOW_ROWS, self.D, int(min(free // 4, self.SHADOW_MAX_BYTES) // per_row))
+        rows = self._hot_dense_rows(R) if R >= 8 else np.zeros(0, np.int32)
+        if len(rows) < 8:
+            self._shadow_declined = self.generation
+            return False
+        R = len(rows)
+        buf = sh[1] if sh is not None and sh[1].numel() == R * self.S * 16 * 1024 else None
+        if buf is None:
+            self._shadow = None
+            buf = torch.empty(R * self.S * 16 * 1024, dtype=torch.int64, device=self.device)
+        slot = torch.full((self.D,), -1, dtype=torch.int32)
+        slot[torch.from_numpy(rows.astype(np.int64))] = torch.arange(R, dtype=torch.int32)
+        slot = slot.to(self.device)
+        self.ensure_keymask()
+        kernels().shadow_build(self.viewdev_tensor(), self.S, torch.from_numpy(rows).to(self.device), buf)
+        # readers on any stream see a complete shadow
+        torch.cuda.current_stream(self.device).synchronize()
+        self._shadow = (self.generation, buf, slot, now, rows)
+        return True
 
     def viewdev_tensor(self):
         """The ViewDev record as the uint8 host tensor the kernel bindings take."""
@@ -962,6 +1042,8 @@ class GpuEngine:
         self.use_and2 = os.environ.get("PILOSA_AND2", "1") != "0"
         self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "0"))  # 0 = by batch size
         self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "6"))
+        # dense bitmap shadows of hot rows for the pair kernels (DeviceView.ensure_shadow)
+        self.use_shadow = os.environ.get("PILOSA_SHADOW", "1") != "0"
         # Count(Union(leaves)) route: union_count_kernel (bitmap_kernels.hip)
         self.use_union = os.environ.get("PILOSA_UNION_KERNEL", "1") != "0"
         # 2 = union_count2_kernel (flat chunk walk, parallel meta fetch), 1 = union_count_kernel
@@ -1103,6 +1185,7 @@ class GpuEngine:
             lr = progs["leaf_row"]
             for v in views:
                 v.ensure_keymask()
+        shd = bool(is_and2.any()) and self.use_shadow and any([v.ensure_shadow() for v in views])
         varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
         for i, v in enumerate(views):
             varr[i] = v.viewdev()
@@ -1120,7 +1203,7 @@ class GpuEngine:
         dev = self._h2d_many(host)
         tv = dev[0]
         parts = [(dev[1 + 2 * i], dev[2 + 2 * i].view(torch.int64), k, n) for i, (k, n) in enumerate(meta)]
-        return (Q, S, tv, parts)
+        return (Q, S, tv, parts, shd)
 
     def prepare_planned(self, Q: int, segs, buf: np.ndarray, views: List["DeviceView"], S: int):
         """:meth:`prepare_progs` for a batch planned natively
@@ -1130,9 +1213,11 @@ class GpuEngine:
         torch = self.torch
         if not S or not Q:
             return (Q, S, None, [])
+        shd = False
         if any(int(kind) == KIND_AND2 for kind, _, _, _ in segs):
             for v in views:
                 v.ensure_keymask()
+            shd = self.use_shadow and any([v.ensure_shadow() for v in views])
         varr = np.zeros(len(views), dtype=VIEWDEV_DTYPE)
         for i, v in enumerate(views):
             varr[i] = v.viewdev()
@@ -1140,7 +1225,7 @@ class GpuEngine:
         parts = []
         for kind, n, po, oo in segs:
             parts.append((tb[po:po + n * QPROG_DTYPE.itemsize], tb[oo:oo + n * 8].view(torch.int64), int(kind), int(n)))
-        return (Q, S, tv, parts)
+        return (Q, S, tv, parts, shd)
 
     @staticmethod
     def _hot_leaf_first(progs: np.ndarray, sel: np.ndarray) -> np.ndarray:
@@ -1160,12 +1245,15 @@ class GpuEngine:
                 col[swap, 0], col[swap, 1] = col[swap, 1].copy(), col[swap, 0].copy()
         return progs
 
-    def _and2_partial(self, tp, tv, S: int, n: int):
-        """Per-(shard, key, query) Count(Intersect) partials -> int32[S, 16, n]."""
+    def _and2_partial(self, tp, tv, S: int, n: int, shd: bool = False):
+        """Per-(shard, key, query) Count(Intersect) partials -> int32[S, 16, n].
+        ``shd``: a view of the batch carries dense shadows (variant 41; the
+        launcher takes 42 for serving-size batches)."""
         torch = self.torch
         pairs = torch.empty(S * 16 * n * 2, dtype=torch.int32, device=self.device)
         partial = torch.empty(S * 16 * n, dtype=torch.int32, device=self.device)
-        self.ext.and2_count(tp, tv, S, pairs, partial, self.and2_cq, self.and2_variant)
+        variant = 41 if shd and self.and2_variant == 6 else self.and2_variant
+        self.ext.and2_count(tp, tv, S, pairs, partial, self.and2_cq, variant)
         return partial.view(S, 16, n)
 
     def to_host(self, t):
@@ -1201,13 +1289,14 @@ class GpuEngine:
 
     def _launch_count(self, handle):
         torch = self.torch
-        Q, S, tv, parts = handle
+        Q, S, tv, parts = handle[:4]
+        shd = len(handle) > 4 and handle[4]
         out = torch.zeros(Q, dtype=torch.int64, device=self.device)
         for tp, ti, kind, n in parts:
             if kind == KIND_AND2:
                 # column sums scattered into out by one kernel (a strided torch
                 # reduce + index_copy cost ~70 us per small serving batch)
-                self.ext.partial_sum_scatter(self._and2_partial(tp, tv, S, n).view(-1), S * 16, n, ti, out)
+                self.ext.partial_sum_scatter(self._and2_partial(tp, tv, S, n, shd).view(-1), S * 16, n, ti, out)
                 continue
             else:
                 o = torch.zeros(n, dtype=torch.int64, device=self.device)

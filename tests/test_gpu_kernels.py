@@ -187,14 +187,16 @@ def test_bitgemm_count_matrix_matches_host(mode):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("variant", [6, 10, 12, 16, 17, 18, 19, 20, 38, 39, 40])
+@pytest.mark.parametrize("variant", [-6, 6, 10, 12, 16, 17, 18, 19, 20, 38, 39, 40, 41, 42])
 @pytest.mark.parametrize("cq", [4, 8, 16, 32, 64])
 def test_pair_kernel_array_size_boundaries(cq, variant):
     """Array containers of 1, 63, 64, 65, 255, 256, 257 (the small-probe
     boundary), 511, 512, 513 and 4096 values against bitmap, array and run
     rows, each paired once (one-off: the gather / LDS-staged-bitmap branches)
     and many times in a row (the staged, reused-row branch), including value 0
-    (the pad-correction path) -> host intersection_count."""
+    (the pad-correction path) -> host intersection_count.  The view has >= 8
+    rows, so it gets dense shadows (DeviceView.ensure_shadow): variants 6 / 41
+    / 42 read them, -6 is v6 with them switched off."""
     import torch
 
     from pilosa_amd.ops.device import DeviceView, GpuEngine, Leaf, Op
@@ -218,7 +220,9 @@ def test_pair_kernel_array_size_boundaries(cq, variant):
     view = DeviceView.from_bitmaps([frag], dev)
     eng = GpuEngine(dev)
     eng.and2_cq = cq
-    eng.and2_variant = variant
+    eng.and2_variant = abs(variant)
+    # -6: v6 with the dense shadows off; 6 takes them (variant 41) once built
+    eng.use_shadow = variant != -6
     pairs = []
     for a in range(len(rows)):
         for b in range(len(rows)):
@@ -229,6 +233,7 @@ def test_pair_kernel_array_size_boundaries(cq, variant):
     want = [_row(frag, a).intersection_count(_row(frag, b)) for a, b in pairs]
     got = eng.count(exprs)
     np.testing.assert_array_equal(got, np.array(want))
+    assert view.shadow_fresh() == (variant != -6)
     per = eng.count_per_shard(exprs)
     np.testing.assert_array_equal(per[:, 0], np.array(want))
 
@@ -378,3 +383,42 @@ def test_partial_sum_scatter_matches_torch(U, n):
     want2 = want.clone()
     want2[ti[0]] = 0
     assert torch.equal(out2.cpu(), want2)
+
+
+def test_dense_shadows_match_arena_containers():
+    """shadow_build_kernel: every shadowed (row, shard, key) is the row's
+    container of that key as a bitmap (zeros where the row has none); rows are
+    the hottest by bit count; a write leaves the shadow stale (not passed)."""
+    import torch
+
+    from pilosa_amd.ops.device import DeviceView
+    rng = np.random.default_rng(5)
+    frags = []
+    for s in range(3):
+        rows = rng.zipf(1.5, 60000) % 40
+        cols = rng.integers(0, 1 << 20, 60000)
+        frags.append(R.Bitmap((rows.astype(np.uint64) << np.uint64(20)) + cols.astype(np.uint64)))
+        frags[-1].optimize()
+    dev = torch.device("cuda:0")
+    view = DeviceView.from_bitmaps(frags, dev)
+    assert view.ensure_shadow()
+    gen, buf, slot, _, rows = view._shadow
+    sh = buf.view(len(rows), view.S, 16, 1024).cpu().numpy()
+    counts = [sum(int(f.count_range(int(d_row) << 20, (int(d_row) + 1) << 20)) for f in frags) for d_row in view.rows]
+    assert set(rows.tolist()) <= set(range(view.D)) and len(rows) >= 8
+    # every shard sampled here (S <= SHADOW_SAMPLE_SHARDS): exactly the hottest rows (up to ties)
+    assert sum(counts[d] for d in rows.tolist()) == sum(sorted(counts, reverse=True)[:len(rows)])
+    for r, d in enumerate(rows.tolist()):
+        rid = int(view.rows[d])
+        for s in range(view.S):
+            for j in range(16):
+                lo = (rid << 20) + (j << 16)
+                want = np.zeros(65536, bool)
+                got_cols = frags[s].slice_range(lo, lo + 65536) if hasattr(frags[s], "slice_range") else \
+                    np.asarray([c for c in frags[s].slice() if lo <= c < lo + 65536], np.uint64)
+                want[(np.asarray(got_cols, np.int64) - lo)] = True
+                bits = np.unpackbits(sh[r, s, j].view(np.uint8), bitorder="little").astype(bool)
+                assert np.array_equal(bits, want), (r, s, j)
+    assert slot.cpu().numpy()[rows].tolist() == list(range(len(rows)))
+    view.generation += 1                       # a write: the shadow is not passed until rebuilt
+    assert not view.shadow_fresh() and int(view.viewdev()["shadow"]) == 0
