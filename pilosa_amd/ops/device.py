@@ -846,8 +846,10 @@ class DeviceView:
         return cls(rows, rowptr, sb, meta, payload, device, shards)
 
     def nbytes(self) -> int:
-        return sum(t.numel() * t.element_size() for t in (self.t_rowptr, self.t_shard_base, self.t_meta,
-                                                          self.t_payload))
+        n = sum(t.numel() * t.element_size() for t in (self.t_rowptr, self.t_shard_base, self.t_meta,
+                                                       self.t_payload))
+        sh = getattr(self, "_shadow", None)
+        return n + (sh[1].numel() * 8 + sh[2].numel() * 4 if sh is not None else 0)
 
     def dense(self, row: int) -> int:
         """row id -> dense index (-1 if the row has no containers on this GPU)."""
@@ -991,7 +993,9 @@ class DeviceView:
             # whose row directory is large next to their containers, or when
             # it would not leave the device comfortably free
             need = 2 * n
-            if need > max(256 << 20, self.nbytes() // 4):
+            sh = getattr(self, "_shadow", None)
+            arena = self.nbytes() - (sh[1].numel() * 8 + sh[2].numel() * 4 if sh is not None else 0)
+            if need > max(256 << 20, arena // 4):
                 return False
             free, _ = torch.cuda.mem_get_info(self.device)
             if need * 4 > free:
@@ -1043,7 +1047,10 @@ class GpuEngine:
         self.and2_cq = int(os.environ.get("PILOSA_AND2_CQ", "0"))  # 0 = by batch size
         self.and2_variant = int(os.environ.get("PILOSA_AND2_VARIANT", "6"))
         # dense bitmap shadows of hot rows for the pair kernels (DeviceView.ensure_shadow)
-        self.use_shadow = os.environ.get("PILOSA_SHADOW", "1") != "0"
+        # (off by default: measured slower -- headline 16.66 vs 16.45 ms, serving
+        # 61.5k vs 69.3k req/s, profiles/r05_serve/ -- the staged LDS probes beat
+        # reading a 8 KiB shadow in place, and the hot A rows are mostly bitmaps)
+        self.use_shadow = os.environ.get("PILOSA_SHADOW", "0") != "0"
         # Count(Union(leaves)) route: union_count_kernel (bitmap_kernels.hip)
         self.use_union = os.environ.get("PILOSA_UNION_KERNEL", "1") != "0"
         # 2 = union_count2_kernel (flat chunk walk, parallel meta fetch), 1 = union_count_kernel
