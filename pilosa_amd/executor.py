@@ -265,6 +265,17 @@ class Executor:
                 fast = self._count_text_fast(index, q, shards, opt)
                 if fast is not None:
                     return QueryResponse(fast)
+                # a request of several cache-only TopN calls: parsed once, one
+                # device batch, columnar results (single calls keep the
+                # cross-request coalescer of the general path)
+                if opt is None and (self.gpu is not None or self.mesh is not None) and \
+                        q.lstrip().startswith("TopN(") and q.count("TopN(") >= 2:
+                    try:
+                        fast = self._topn_text_fast(index, q, shards)
+                    except PilosaError:
+                        fast = None   # the general path reports it
+                    if fast is not None:
+                        return QueryResponse(fast)
                 text = q
                 q = parse_string(q)
                 q.source = text

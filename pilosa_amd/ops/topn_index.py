@@ -578,7 +578,7 @@ def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) 
     import torch
 
     if pq.numel() == 0:
-        return [[] for _ in range(Q)]
+        return [pair_array(np.zeros(0, np.uint64), np.zeros(0, np.int64)) for _ in range(Q)]
     bq, ba = max(1, int(Q - 1).bit_length()), max(1, int(len(space) - 1).bit_length())
     if bq + 31 + ba <= 63:
         # one sort of a composite key (query, ~count, acc index): acc indexes
@@ -595,13 +595,8 @@ def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) 
         rank = torch.arange(key.numel(), device=key.device) - bounds[q_s]
         sel = (rank < lim[q_s]) & (c_s > 0)
         kept = key[sel].cpu().numpy()
-        q_h = kept >> (31 + ba)
-        c_h = ((1 << 31) - 1) - ((kept >> ba) & ((1 << 31) - 1))
-        ids = space[kept & ((1 << ba) - 1)]
-        out: List[List[Pair]] = [[] for _ in range(Q)]
-        for qq, i, cc in zip(q_h.tolist(), ids.tolist(), c_h.tolist()):
-            out[qq].append(Pair(int(i), int(cc)))
-        return out
+        return _split_by_query(Q, kept >> (31 + ba), space[kept & ((1 << ba) - 1)],
+                               ((1 << 31) - 1) - ((kept >> ba) & ((1 << 31) - 1)))
     keep = cnt > 0
     pq, pa, cnt = pq[keep], pa[keep], cnt[keep]
     if pq.numel() == 0:
@@ -620,12 +615,17 @@ def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) 
     sel = rank < lim[pq]
     # one device -> host copy for the kept pairs
     qac = torch.stack([pq[sel].to(torch.int64), pa[sel], cnt[sel].to(torch.int64)]).cpu().numpy()
-    q_h, a_h, c_h = qac[0], qac[1], qac[2]
-    ids = space[a_h]
-    out: List[List[Pair]] = [[] for _ in range(Q)]
-    for qq, i, c in zip(q_h.tolist(), ids.tolist(), c_h.tolist()):
-        out[qq].append(Pair(int(i), int(c)))
-    return out
+    return _split_by_query(Q, qac[0], space[qac[1]], qac[2])
+
+
+def _split_by_query(Q: int, q_h: np.ndarray, ids: np.ndarray, cnt: np.ndarray) -> List["PairArray"]:
+    """Per-query columnar results from (query, id, count) rows sorted by
+    query (each query's rows already in result order): a Pair object per
+    kept row was ~1.7 ms of a 16-query src TopN batch."""
+    b = np.searchsorted(q_h, np.arange(Q + 1))
+    ids = np.asarray(ids, dtype=np.uint64)
+    cnt = np.asarray(cnt, dtype=np.int64)
+    return [pair_array(ids[b[q]:b[q + 1]], cnt[b[q]:b[q + 1]]) for q in range(Q)]
 
 
 def finish_batch(space: np.ndarray, Q: int, pq: np.ndarray, pa: np.ndarray, cnt: np.ndarray,
