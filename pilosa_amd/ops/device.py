@@ -1630,6 +1630,20 @@ class GpuEngine:
         Batches of BSI_MATRIX_MIN+ filters run as one bit-plane count matrix
         on the matrix cores (ops/bsi.py); ``matrix`` forces either path."""
         torch = self.torch
+        if len(filters) == 1 and filters[0] is None:
+            # Sum(field=v): no program to compile or upload (a constant one)
+            args = self.bsi_args(bsi_view, depth)
+            outs = torch.zeros(2, dtype=torch.int64, device=self.device)
+            if bsi_view.S and args[2] >= 0:
+                tp = self.__dict__.get("_empty_prog")
+                if tp is None:   # a synchronous copy: any stream may read it afterwards
+                    tp = self._empty_prog = torch.from_numpy(
+                        pack_programs([([], [], [])]).view(np.uint8).copy()).to(self.device)
+                    if self.device.type == "cuda":
+                        torch.cuda.current_stream(self.device).synchronize()
+                self.ext.bsi_sum(tp, self._views_tensor([bsi_view]), bsi_view.S, torch.from_numpy(args),
+                                 outs[:1], outs[1:], 0)
+            return outs[:1], outs[1:]
         if matrix is None:
             from .bsi import BSI_MATRIX_MIN
             matrix = len(filters) >= BSI_MATRIX_MIN
@@ -1665,16 +1679,7 @@ class GpuEngine:
         outs = torch.zeros(2 * len(filters), dtype=torch.int64, device=self.device)
         out_sum, out_cnt = outs[:len(filters)], outs[len(filters):]
         if bsi_view.S and args[2] >= 0:
-            if not exprs and len(filters) == 1:
-                # Sum(field=v): the one empty program is a constant, uploaded once
-                tp = self.__dict__.get("_empty_prog")
-                if tp is None:   # a synchronous copy: any stream may read it afterwards
-                    tp = self._empty_prog = torch.from_numpy(progs.view(np.uint8).copy()).to(self.device)
-                    if self.device.type == "cuda":
-                        torch.cuda.current_stream(self.device).synchronize()
-                tv = self._views_tensor(ordered)
-            else:
-                tp, tv = self.upload_batch(progs, ordered)
+            tp, tv = self.upload_batch(progs, ordered)
             # filter flavour: none / flat folds (2 tiles) / any program (tile stack)
             nprog = progs["nprog"]
             if not (nprog > 0).any():

@@ -986,7 +986,8 @@ class GpuExecutor:
             s, n = self.engine.bsi_sum_async([filt], bv, b.bit_depth)
         except CompileError:
             raise NotImplementedError
-        s, n = (int(x) for x in self.engine.to_host(torch.stack([s[:1], n[:1]])).view(-1).tolist())
+        base = s._base if s._base is not None and s._base.numel() == 2 and n._base is s._base else None
+        s, n = (int(x) for x in self.engine.to_host(base if base is not None else torch.stack([s[:1], n[:1]])).view(-1).tolist())
         return ValCount(_wrap(s + n * b.base), n)
 
     def bsi_sum_batch(self, index: str, calls: List[Call], shards: List[int]):

@@ -139,7 +139,7 @@ BSI_QUERIES = [
     "Count(Row(m == -20))", "Count(Row(m < -4000))", "Count(Row(n > 200000))",
     "Min(field=n)", "Max(field=n)", "Min(Row(f=1), field=n)", "Max(Row(f=2), field=n)",
     "Min(field=m)", "Max(field=m)", "Max(Row(f=0), field=m)", "Min(Row(n > 90000), field=n)",
-    "Sum(Row(n < 0), field=n)",
+    "Sum(Row(n < 0), field=n)", "Sum(field=n)", "Sum(field=m)",
 ]
 
 
