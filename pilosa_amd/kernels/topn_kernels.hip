@@ -1178,6 +1178,38 @@ __global__ __launch_bounds__(256) void topn_cache_totals_kernel(const int32_t* _
   if (lane == 0) tot[w] = TT(acc);
 }
 
+// The same totals for up to 16 thresholds in ONE pass over the count matrix:
+// one wave per candidate, every count compared against all thresholds in
+// registers (the per-threshold kernel re-read the [U x S] matrix T times:
+// ~1.2 GB for 16 distinct thresholds over a 20k-candidate prefix).
+template <class TT>
+__global__ __launch_bounds__(256) void topn_cache_totals16_kernel(const int32_t* __restrict__ cm, int S, int U,
+                                                                  const int32_t* __restrict__ th, int T,
+                                                                  TT* __restrict__ tot) {
+  const int j = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
+  const int lane = int(threadIdx.x & 63);
+  if (j >= U) return;
+  int32_t thr[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) thr[t] = t < T ? th[t] : 0x7fffffff;
+  int acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) acc[t] = 0;
+  const int32_t* row = cm + int64_t(j) * S;
+  for (int s = lane; s < S; s += 64) {
+    const int32_t n = row[s];
+#pragma unroll
+    for (int t = 0; t < 16; t++) acc[t] += n >= thr[t] ? n : 0;
+  }
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    if (t >= T) break;
+    int v = acc[t];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) tot[int64_t(t) * U + j] = TT(v);
+  }
+}
+
 template <class TT>
 __global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* __restrict__ member,
                                                                 const TT* __restrict__ tot,
@@ -1252,8 +1284,12 @@ void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const i
                        member);
   }
   const int64_t waves = int64_t(T) * U;
-  hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm, S,
-                     U, prm + 4 * Q, T, tot);
+  if (T <= 16)
+    hipLaunchKernelGGL(topn_cache_totals16_kernel<long long>, dim3(unsigned((U + 3) / 4)), dim3(256), 0, st, cm, S,
+                       U, prm + 4 * Q, T, tot);
+  else
+    hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm,
+                       S, U, prm + 4 * Q, T, tot);
   hipLaunchKernelGGL(topn_cache_select_kernel<long long>, dim3(Q), dim3(256), 0, st, member, tot, u, prm, Q, U, KK,
                      out);
 }
@@ -1274,7 +1310,10 @@ void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const
                        member);
   }
   const int64_t waves = int64_t(T) * U;
-  if (S > 0)
+  if (S > 0 && T <= 16)
+    hipLaunchKernelGGL(topn_cache_totals16_kernel<int>, dim3(unsigned((U + 3) / 4)), dim3(256), 0, st, cm, S, U,
+                       prm + 4 * Q, T, tot);
+  else if (S > 0)
     hipLaunchKernelGGL(topn_cache_totals_kernel<int>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm, S, U,
                        prm + 4 * Q, T, tot);
 }

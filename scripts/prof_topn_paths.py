@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--topn-cache", type=int, default=50000)
     ap.add_argument("--paths", default="local,mesh")
     ap.add_argument("--top", type=int, default=35)
+    ap.add_argument("--wide", action="store_true", help="the bench's wide call set (n 1..1000, 72 thresholds)")
     args = ap.parse_args()
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": os.environ.get("MASTER_PORT", "29561"),
                        "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
@@ -49,7 +50,8 @@ def main():
     gpu.executor = ex
     ex.strict_gpu = True
     shards = list(range(nshards))
-    calls = bench._distinct_topn_calls(16 * (args.reqs + 20))
+    calls = bench._wide_topn_calls(16 * (args.reqs + 20)) if args.wide else \
+        bench._distinct_topn_calls(16 * (args.reqs + 20))
     texts = [" ".join(calls[i * 16:(i + 1) * 16]) for i in range(args.reqs + 20)]
 
     def run_path(name):
