@@ -1308,8 +1308,13 @@ __global__ __launch_bounds__(256, MINW) void bsi_minmax_kernel(const QueryProg* 
 // ValCount.Smaller / Larger keep the earlier shard's).  One 1024-thread block;
 // out = {value, count, found}.
 constexpr int FOLD_THREADS = 1024;
-__global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int64_t* __restrict__ o, int F, int G,
+// GT: the keys per fragment as a compile-time constant (16: every key's
+// loads issue together -- the runtime-G loop serialised them, 44 us per call)
+// or 0 (runtime G, wide shards)
+template <int GT>
+__global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int64_t* __restrict__ o, int F, int Grt,
                                                                       int is_min, int64_t* __restrict__ out) {
+  const int G = GT > 0 ? GT : Grt;
   __shared__ int64_t sv[FOLD_THREADS / 64];
   __shared__ int sf[FOLD_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1321,6 +1326,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int
   for (int f = tid; f < F; f += FOLD_THREADS) {
     const int64_t* e = o + int64_t(f) * G * 10;
     bool anyp = false, anyn = false;
+#pragma unroll
     for (int g = 0; g < G; g++) {
       anyp |= e[g * 10 + 8] > 0;
       anyn |= e[g * 10 + 9] > 0;
@@ -1333,6 +1339,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int
     const bool largest = vc == 0 || vc == 4;
     const int mcol = use_neg ? 9 : 8;
     int64_t best = largest ? -1 : BIG, cnt = 0;
+#pragma unroll
     for (int g = 0; g < G; g++) {
       if (e[g * 10 + mcol] <= 0) continue;
       const int64_t v = e[g * 10 + vc];
@@ -1453,7 +1460,10 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
 }
 
 void launch_bsi_minmax_fold(const int64_t* o, int F, int G, int is_min, int64_t* out, hipStream_t st) {
-  hipLaunchKernelGGL(bsi_minmax_fold_kernel, dim3(1), dim3(FOLD_THREADS), 0, st, o, F, G, is_min, out);
+  if (G == 16)
+    hipLaunchKernelGGL(bsi_minmax_fold_kernel<16>, dim3(1), dim3(FOLD_THREADS), 0, st, o, F, G, is_min, out);
+  else
+    hipLaunchKernelGGL(bsi_minmax_fold_kernel<0>, dim3(1), dim3(FOLD_THREADS), 0, st, o, F, G, is_min, out);
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,
