@@ -286,7 +286,8 @@ void topn_cache_counts(torch::Tensor view, int64_t S, torch::Tensor u, torch::Te
 
 void topn_cache_batch(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch::Tensor u, torch::Tensor cm,
                       torch::Tensor prm, int64_t Q, int64_t T, torch::Tensor member, torch::Tensor tot,
-                      torch::Tensor out) {
+                      torch::Tensor out, int64_t nlim) {
+  TORCH_CHECK(nlim >= 0 && nlim <= nmax, "nlim: 0 (= nmax) .. nmax");
   for (auto* t : {&cnt, &inv, &u, &cm, &prm, &member, &tot, &out}) check_dev(*t, "topn_cache_batch");
   TORCH_CHECK(cnt.scalar_type() == torch::kInt32 && cnt.dim() == 2, "cnt int32[S, K]");
   const int64_t S = cnt.size(0), K = cnt.size(1), U = u.numel();
@@ -304,7 +305,7 @@ void topn_cache_batch(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch:
                               u.data_ptr<int32_t>(), cm.data_ptr<int32_t>(), prm.data_ptr<int32_t>(), int(Q), int(T),
                               int(U), int(KK), member.data_ptr<uint8_t>(),
                               reinterpret_cast<long long*>(tot.data_ptr<int64_t>()),
-                              reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(cnt));
+                              reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(cnt), int(nlim));
   check_launch("topn_cache_batch");
 }
 

@@ -146,7 +146,7 @@ void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, 
 // (prm = lim[Q] | mt[Q] | tsel[Q] | nq[Q] | th[T]; out[Q, KK+1], column 0 = rows kept or -2 on overflow).
 void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
                              const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
-                             long long* tot, long long* out, hipStream_t st);
+                             long long* tot, long long* out, hipStream_t st, int nlim = 0);
 void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* cm,
                                const int32_t* prm, int Q, int T, int U, uint8_t* member, int32_t* tot,
                                hipStream_t st);

@@ -1138,19 +1138,22 @@ __global__ __launch_bounds__(256) void topn_cache_counts_kernel(ViewDev v, int S
 
 // member[q, inv[s*nmax + k]] = 1 for the first lim[q] ranks of shard s whose
 // cached count reaches mt[q]
+// nmax = the memoised prefix (inv's row stride); nlim <= nmax = the ranks this
+// batch can take (its largest n): a batch reuses a longer prefix's memo
+// without walking the ranks beyond its own n
 __global__ __launch_bounds__(256) void topn_cache_member_kernel(const int32_t* __restrict__ cnt, int K, int S, int nmax,
                                                                 const int32_t* __restrict__ inv,
                                                                 const int32_t* __restrict__ prm, int Q, int U,
-                                                                uint8_t* __restrict__ member) {
+                                                                uint8_t* __restrict__ member, int nlim) {
   const int q = blockIdx.y;
-  const int L = min(prm[q], nmax);
+  const int L = min(prm[q], nlim);
   const int32_t m = prm[Q + q];
-  const int64_t N = int64_t(S) * nmax;
+  const int64_t N = int64_t(S) * nlim;
   uint8_t* mq = member + int64_t(q) * U;
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < N; e += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t s = e / nmax;
-    const int k = int(e - s * nmax);
-    if (k < L && cnt[s * K + k] >= m) mq[inv[e]] = 1;
+    const int64_t s = e / nlim;
+    const int k = int(e - s * nlim);
+    if (k < L && cnt[s * K + k] >= m) mq[inv[s * nmax + k]] = 1;
   }
 }
 
@@ -1274,14 +1277,15 @@ void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, 
 
 void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
                              const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
-                             long long* tot, long long* out, hipStream_t st) {
+                             long long* tot, long long* out, hipStream_t st, int nlim) {
   if (Q <= 0 || U <= 0) return;
-  const int64_t N = int64_t(S) * nmax;
+  if (nlim <= 0 || nlim > nmax) nlim = nmax;
+  const int64_t N = int64_t(S) * nlim;
   if (N > 0) {
     const int64_t want = (N + 255) / 256;
     const int bx = int(want < 1024 ? want : 1024);
     hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
-                       member);
+                       member, nlim);
   }
   const int64_t waves = int64_t(T) * U;
   if (T <= 16)
@@ -1307,7 +1311,7 @@ void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const
     const int64_t want = (N + 255) / 256;
     const int bx = int(want < 1024 ? want : 1024);
     hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
-                       member);
+                       member, nmax);
   }
   const int64_t waves = int64_t(T) * U;
   if (S > 0 && T <= 16)

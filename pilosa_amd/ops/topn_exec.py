@@ -431,6 +431,11 @@ class DeviceRankCaches:
         memo = self.__dict__.setdefault("_fused", {})
         got = memo.get(nmax)
         if got is None:
+            # a longer prefix's memo serves too (its candidates are a superset;
+            # the member kernel stops at this batch's ranks)
+            longer = [k for k, v in memo.items() if k > nmax and v is not False]
+            if longer:
+                return memo[min(longer)]
             u, inv = self._candidates(nmax)
             U = int(u.numel())
             if U * self.view.S > FUSED_MAX_CELLS:
@@ -581,6 +586,7 @@ class DeviceRankCaches:
         if memo is False:
             return None
         u32, inv32, cm = memo
+        stride = int(inv32.numel()) // max(self.S, 1)   # the memo's prefix length (>= nmax)
         U = int(u32.numel())
         dev = self.view.device
         ths = [max(1, int(t)) for t in thresholds]
@@ -606,7 +612,7 @@ class DeviceRankCaches:
             member = torch.zeros((Q, U), dtype=torch.uint8, device=dev)
             tot = torch.empty((T, U), dtype=torch.int64, device=dev)
             out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
-        kernels().topn_cache_batch(self.cache_cnt, nmax, inv32, u32, cm, prm_d, Q, T, member, tot, out)
+        kernels().topn_cache_batch(self.cache_cnt, stride, inv32, u32, cm, prm_d, Q, T, member, tot, out, nmax)
         if lane is not None:
             # answers to the lane's pinned buffer, then wait for this stream only
             hb = lane.buf("out_h", out.numel(), torch.int64, pinned=True)

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--topn-cache", type=int, default=50000)
     ap.add_argument("--paths", default="local,mesh")
     ap.add_argument("--top", type=int, default=35)
+    ap.add_argument("--clients", default="1", help="comma list of request-thread counts to time (e.g. 1,2,3)")
     ap.add_argument("--wide", action="store_true", help="the bench's wide call set (n 1..1000, 72 thresholds)")
     args = ap.parse_args()
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": os.environ.get("MASTER_PORT", "29561"),
@@ -58,13 +59,29 @@ def main():
         for t in texts[:20]:
             ex.execute("i", t, shards=shards)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for t in texts[20:]:
-            ex.execute("i", t, shards=shards)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        print(f"{name}: {args.reqs} requests x 16 calls: {dt / args.reqs * 1000:.3f} ms/request, "
-              f"{16 * args.reqs / dt:.0f} q/s", flush=True)
+        import threading
+        for nc in [int(x) for x in args.clients.split(",") if x]:
+            nxt = [20]
+            lock = threading.Lock()
+
+            def client():
+                while True:
+                    with lock:
+                        i = nxt[0]
+                        if i >= len(texts):
+                            return
+                        nxt[0] += 1
+                    ex.execute("i", texts[i], shards=shards)
+            t0 = time.perf_counter()
+            ts = [threading.Thread(target=client) for _ in range(nc)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            print(f"{name}: {args.reqs} requests x 16 calls, {nc} request thread(s): "
+                  f"{dt / args.reqs * 1000:.3f} ms/request, {16 * args.reqs / dt:.0f} q/s", flush=True)
         pr = cProfile.Profile()
         pr.enable()
         for t in texts[20:]:
