@@ -228,7 +228,10 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
 
     n = 100
     B, nb = args.topn_batch, args.topn_batches
-    clients = max(1, args.clients) if world == 1 else 1
+    # request threads of the TopN phase: with 2, the two threads' Python halves
+    # convoy on the GIL (cache-only 0.358 ms/request vs 0.216 with 1 and 0.232
+    # with 3, profiles/r05_topn/prof_topn_wide_threads.log)
+    clients = max(1, args.topn_clients) if world == 1 else 1
     if world > 1:
         gpu.comm = _COMM
     rng = np.random.default_rng(99)
@@ -1660,6 +1663,7 @@ def main():
                     help="timed cache-only TopN requests (at least --topn-batches)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
+    ap.add_argument("--topn-clients", type=int, default=3, help="request threads of the TopN phase")
     ap.add_argument("--topn-pairs-batches", type=int, default=1,
                     help="also time the pair-count src TopN path on this many batches (0 = skip)")
     ap.add_argument("--configs", default=os.environ.get("PILOSA_BENCH_CONFIGS", "4,5"),
