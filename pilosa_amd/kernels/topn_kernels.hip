@@ -1127,6 +1127,10 @@ void launch_row_counts_sum(const ViewDev& v, int S, const int32_t* dense, const 
 namespace {
 
 constexpr int TC_CAP = 8192;   // members per query sorted in LDS (64 KB of keys)
+// threads of the per-query select: 16 waves on the query's CU -- the bitonic
+// stages loop over up to TC_CAP keys, 4x fewer iterations per thread than 256
+// (the select was ~half of a wide cache-only batch's GPU time)
+constexpr int TC_THREADS = 1024;
 
 __global__ __launch_bounds__(256) void topn_cache_counts_kernel(ViewDev v, int S, const int32_t* __restrict__ u,
                                                                 int64_t N, int32_t* __restrict__ cm) {
@@ -1214,7 +1218,7 @@ __global__ __launch_bounds__(256) void topn_cache_totals16_kernel(const int32_t*
 }
 
 template <class TT>
-__global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* __restrict__ member,
+__global__ __launch_bounds__(TC_THREADS) void topn_cache_select_kernel(const uint8_t* __restrict__ member,
                                                                 const TT* __restrict__ tot,
                                                                 const int32_t* __restrict__ u,
                                                                 const int32_t* __restrict__ prm, int Q, int U, int KK,
@@ -1227,7 +1231,7 @@ __global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* _
   __syncthreads();
   const uint8_t* mq = member + int64_t(q) * U;
   const TT* tq = tot + int64_t(prm[2 * Q + q]) * U;
-  for (int j = tid; j < U; j += 256) {
+  for (int j = tid; j < U; j += TC_THREADS) {
     if (!mq[j]) continue;
     const int32_t d = u[j];
     const long long sc = (long long)tq[j];
@@ -1244,11 +1248,11 @@ __global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* _
   }
   int P = 1;
   while (P < M) P <<= 1;
-  for (int i = M + tid; i < P; i += 256) keys[i] = -1;
+  for (int i = M + tid; i < P; i += TC_THREADS) keys[i] = -1;
   __syncthreads();
   for (int k = 2; k <= P; k <<= 1)
     for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      for (int i = tid; i < P; i += 256) {
+      for (int i = tid; i < P; i += TC_THREADS) {
         const int ixj = i ^ jj;
         if (ixj > i) {
           const long long a = keys[i], b = keys[ixj];
@@ -1262,7 +1266,7 @@ __global__ __launch_bounds__(256) void topn_cache_select_kernel(const uint8_t* _
     }
   const int lim = min(min(M, prm[3 * Q + q]), KK);
   if (tid == 0) o[0] = lim;
-  for (int i = tid; i < lim; i += 256) o[1 + i] = keys[i];
+  for (int i = tid; i < lim; i += TC_THREADS) o[1 + i] = keys[i];
 }
 
 }  // namespace
@@ -1280,6 +1284,8 @@ void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const i
                              long long* tot, long long* out, hipStream_t st, int nlim) {
   if (Q <= 0 || U <= 0) return;
   if (nlim <= 0 || nlim > nmax) nlim = nmax;
+  // the membership bytes start clear (was a separate torch fill launched from Python)
+  (void)hipMemsetAsync(member, 0, size_t(Q) * size_t(U), st);
   const int64_t N = int64_t(S) * nlim;
   if (N > 0) {
     const int64_t want = (N + 255) / 256;
@@ -1294,8 +1300,8 @@ void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const i
   else
     hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm,
                        S, U, prm + 4 * Q, T, tot);
-  hipLaunchKernelGGL(topn_cache_select_kernel<long long>, dim3(Q), dim3(256), 0, st, member, tot, u, prm, Q, U, KK,
-                     out);
+  hipLaunchKernelGGL(topn_cache_select_kernel<long long>, dim3(Q), dim3(TC_THREADS), 0, st, member, tot, u, prm, Q, U,
+                     KK, out);
 }
 
 // A mesh rank's share of a cache-only batch over the NODE candidate space:
@@ -1325,7 +1331,8 @@ void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const
 void launch_topn_cache_select32(const uint8_t* member, const int32_t* tot, const int32_t* ids, const int32_t* prm,
                                 int Q, int U, int KK, long long* out, hipStream_t st) {
   if (Q <= 0 || U <= 0) return;
-  hipLaunchKernelGGL(topn_cache_select_kernel<int>, dim3(Q), dim3(256), 0, st, member, tot, ids, prm, Q, U, KK, out);
+  hipLaunchKernelGGL(topn_cache_select_kernel<int>, dim3(Q), dim3(TC_THREADS), 0, st, member, tot, ids, prm, Q, U, KK,
+                     out);
 }
 
 }  // namespace pk

@@ -517,7 +517,8 @@ class DeviceRankCaches:
         prm = np.empty(4 * Q + T, np.int32)
         prm[:Q] = [n if n else self.K for n in nn]
         prm[Q:2 * Q] = ths
-        prm[2 * Q:3 * Q] = [uniq_t.index(t) for t in ths]
+        tix = {t: i for i, t in enumerate(uniq_t)}
+        prm[2 * Q:3 * Q] = [tix[t] for t in ths]
         prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
         prm[4 * Q:] = uniq_t
         prm_d = torch.from_numpy(prm).to(dev, non_blocking=False)
@@ -596,20 +597,20 @@ class DeviceRankCaches:
         prm = pin.numpy() if pin is not None else np.empty(4 * Q + len(uniq_t), np.int32)
         prm[:Q] = [n if n else self.K for n in nn]
         prm[Q:2 * Q] = ths
-        prm[2 * Q:3 * Q] = [uniq_t.index(t) for t in ths]
+        tix = {t: i for i, t in enumerate(uniq_t)}
+        prm[2 * Q:3 * Q] = [tix[t] for t in ths]
         prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
         prm[4 * Q:] = uniq_t
         T = len(uniq_t)
         if lane is not None:
             prm_d = lane.buf("prm", len(prm), torch.int32)
             prm_d.copy_(pin, non_blocking=True)
-            member = lane.buf("member", Q * U, torch.uint8).view(Q, U)
-            member.zero_()
+            member = lane.buf("member", Q * U, torch.uint8).view(Q, U)   # cleared by the launcher
             tot = lane.buf("tot", T * U, torch.int64).view(T, U)
             out = lane.buf("out", Q * (KK + 1), torch.int64).view(Q, KK + 1)
         else:
             prm_d = torch.from_numpy(prm).to(dev)
-            member = torch.zeros((Q, U), dtype=torch.uint8, device=dev)
+            member = torch.empty((Q, U), dtype=torch.uint8, device=dev)   # cleared by the launcher
             tot = torch.empty((T, U), dtype=torch.int64, device=dev)
             out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
         kernels().topn_cache_batch(self.cache_cnt, stride, inv32, u32, cm, prm_d, Q, T, member, tot, out, nmax)
