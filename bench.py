@@ -238,9 +238,12 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     out = {"path": "Executor.execute(PQL TopN text), lazy holder, device rank caches from .cache files",
            "n": n, "cache_k": args.topn_cache, "batch": B, "clients": clients}
 
-    def timed(texts, first, profile=""):
-        # warmup request first (builds rank caches / slot index), then nb timed requests;
-        # ``profile``: folded stacks of every thread over the first 0.3 s of the timed run
+    def timed(texts, first, profile="", nclients=None, warm=1):
+        # ``warm`` untimed requests first (the first builds rank caches / slot
+        # index / prefix memos), then the rest timed with ``nclients`` request
+        # threads; ``profile``: folded stacks of every thread over the first
+        # 0.3 s of the timed run
+        nclients = clients if nclients is None else nclients
         done = [None] * len(texts)
         err = []
         nxt = [0]
@@ -262,6 +265,9 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         done[0] = ex.execute("i", texts[0], shards=shards).results
         torch.cuda.synchronize(dev)
         first["first_request_s"] = round(time.perf_counter() - t0, 2)
+        for i in range(1, warm):
+            done[i] = ex.execute("i", texts[i], shards=shards).results
+        torch.cuda.synchronize(dev)
         # what the server's Refreezer does after warm-up: the rank caches and
         # slot index the first request built leave the collector's walk
         from pilosa_amd.utils import gctune
@@ -270,7 +276,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        nxt[0] = 1
+        nxt[0] = warm
         prof = None
         gc_t = [0.0, 0, None]   # pause seconds, collections, start of the current one
         if profile:
@@ -288,7 +294,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
             prof = threading.Thread(target=lambda: prof_out.setdefault("p", pprof.cpu_profile(0.3, 500)), daemon=True)
             prof.start()
         t0 = time.perf_counter()
-        ts = [threading.Thread(target=client, args=(1, len(texts))) for _ in range(clients)]
+        ts = [threading.Thread(target=client, args=(warm, len(texts))) for _ in range(nclients)]
         for t in ts:
             t.start()
         for t in ts:
@@ -311,7 +317,8 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
             all_reduce(elt, op=dist.ReduceOp.MAX)
         el = float(elt.item())
         last = done[-1]
-        first.update({"qps": round(B * (len(texts) - 1) / el, 2), "ms_per_request": round(el / (len(texts) - 1) * 1000, 2),
+        first.update({"qps": round(B * (len(texts) - warm) / el, 2), "ms_per_request": round(el / (len(texts) - warm) * 1000, 2),
+                      "request_threads": nclients, "warm_requests": warm,
                       "sample_top3": [(p.id, p.count) for p in last[0][:3]] if last and last[0] else []})
         return done
 
@@ -320,18 +327,24 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     # every call of every request distinct: n and threshold vary, so no
     # phase-2 re-count or candidate set is shared between calls by repetition
     nbc = max(nb, args.topn_cache_batches)   # cache-only requests are ~1 ms: a longer window
-    cache_calls = _wide_topn_calls(B * (nbc + 1), seed=17)
-    cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nbc + 1)]
+    W = 8   # untimed: the prefix-bucket memos of the rank caches are built once
+    cache_calls = _wide_topn_calls(B * (nbc + W), seed=17)
+    cache_q = [" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nbc + W)]
     out["cache"] = {"calls": f"TopN(f, n=log-uniform 1..1000, threshold one of {len(WIDE_THRESHOLDS)} values "
                              "1..50000), random per call: distinct within and across requests"}
-    res_cache = timed(cache_q, out["cache"], os.environ.get("PILOSA_BENCH_TOPN_PROFILE", ""))
+    # cache-only requests are host-bound Python: one request thread (2-3 threads
+    # convoy on the GIL, profiles/r05_topn/prof_topn_wide_threads.log)
+    res_cache = timed(cache_q, out["cache"], os.environ.get("PILOSA_BENCH_TOPN_PROFILE", ""),
+                      nclients=args.topn_cache_clients, warm=W)
     log("topn: cache-only requests (round-4 cycling set: 4 n x 4 thresholds)")
-    cyc = _distinct_topn_calls(B * (nbc + 1))
+    cyc = _distinct_topn_calls(B * (nbc + W))
     out["cache_cycling"] = {"calls": "TopN(f, n in {10,50,100,500} + offset, threshold in {1,1000,5000,20000})"}
-    timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nbc + 1)], out["cache_cycling"])
+    timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nbc + W)], out["cache_cycling"],
+          nclients=args.topn_cache_clients, warm=W)
     log("topn: cache-only requests (the same call repeated, round-3 figure)")
     out["cache_repeated"] = {}
-    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nbc + 1), out["cache_repeated"])
+    timed([" ".join([f"TopN(f, n={n})"] * B)] * (nbc + W), out["cache_repeated"], nclients=args.topn_cache_clients,
+          warm=W)
     hot = zipf_rows(rng, B * (nb + 1), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
@@ -399,7 +412,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         # and the fused batch answers equal the two-phase map/reduce on the device
         agree = [[(p.id, p.count) for p in r] for r in res_src[-1][:2] + res_cache[-1][:4]] == \
             [[(p.id, p.count) for p in ex._topn("i", parse_string(c).calls[0], shards, _exec_opts())]
-             for c in src_calls[nb * B:nb * B + 2] + cache_calls[nbc * B:nbc * B + 4]] if world == 1 else None
+             for c in src_calls[nb * B:nb * B + 2] + cache_calls[(len(cache_q) - 1) * B:(len(cache_q) - 1) * B + 4]] if world == 1 else None
         out["verify"] = {"shards_checked": len(sel), "queries_per_shard": len(calls), "mismatches": bad,
                          "fused_equals_two_phase": agree, "verified": bad == 0 and agree is not False}
     return out
@@ -1663,7 +1676,8 @@ def main():
                     help="timed cache-only TopN requests (at least --topn-batches)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")
     ap.add_argument("--topn-cache", type=int, default=50000, help="rank-cache size per shard (reference default)")
-    ap.add_argument("--topn-clients", type=int, default=3, help="request threads of the TopN phase")
+    ap.add_argument("--topn-clients", type=int, default=3, help="request threads of the src TopN phase")
+    ap.add_argument("--topn-cache-clients", type=int, default=1, help="request threads of the cache-only TopN phases")
     ap.add_argument("--topn-pairs-batches", type=int, default=1,
                     help="also time the pair-count src TopN path on this many batches (0 = skip)")
     ap.add_argument("--configs", default=os.environ.get("PILOSA_BENCH_CONFIGS", "4,5"),
