@@ -1191,7 +1191,20 @@ class Executor:
                             lambda p, v: pairs_add(p or [], v or []), local)
         return sort_pairs(r or [])
 
+    _TOPN_PLAIN_ARGS = frozenset(("_field", "n", "threshold"))
+
     def topn_params(self, index: str, c: Call):
+        a = c.args
+        if not c.children and a.keys() <= self._TOPN_PLAIN_ARGS:
+            # TopN(f, n=.., threshold=..): the common serving shape, without
+            # the generic argument accessors (16 of these per request)
+            n, th = a.get("n", 0), a.get("threshold", 0)
+            if type(n) is int and type(th) is int and n >= 0 and th >= 0:
+                fname = a.get("_field") or DEFAULT_FIELD
+                f = self.holder.field(index, fname)
+                if f is not None and f.type == FIELD_TYPE_INT:
+                    raise PilosaError(f'cannot compute TopN() on integer field: "{fname}"')
+                return fname, n, [], th or DEFAULT_MIN_THRESHOLD, 0, "", []
         fname = c.args.get("_field") or DEFAULT_FIELD
         n, _ = c.uint_arg("n")
         f = self.holder.field(index, fname)
