@@ -271,7 +271,9 @@ class Executor:
                 if opt is None and (self.gpu is not None or self.mesh is not None) and \
                         q.lstrip().startswith("TopN(") and q.count("TopN(") >= 2:
                     try:
-                        fast = self._topn_text_fast(index, q, shards)
+                        fast = self._topn_plain_fast(index, q, shards)
+                        if fast is None:
+                            fast = self._topn_text_fast(index, q, shards)
                     except PilosaError:
                         fast = None   # the general path reports it
                     if fast is not None:
@@ -499,6 +501,46 @@ class Executor:
                 want = self._topn(index, c, list(shards), ExecOptions())
                 if [(p.id, p.count) for p in r] != [(p.id, p.count) for p in want]:
                     raise AssertionError(f"paranoia: device TopN {r!r} != host TopN {want!r}")
+        return res
+
+    def _topn_plain_fast(self, index: str, text: str, shards=None) -> Optional[List[Any]]:
+        """Single-GPU fast path for a request of plain cache-only calls of one
+        field -- TopN(f[, n=][, threshold=]) -- recognised natively
+        (native/pql_compile.cpp topn_plain): no Call objects or per-call
+        argument handling, one fused device batch (ops/topn_exec.py).  None =
+        the parse-based paths."""
+        gpu = self.gpu
+        if gpu is None or self._use_mesh(None) or not hasattr(gpu, "topn_plain_batch"):
+            return None
+        from pilosa_amd import _pql
+        got = _pql.topn_plain(text)
+        if got is None:
+            return None
+        fields, ns, ths = got
+        fname = fields[0]
+        if any(f != fname for f in fields):
+            return None
+        idx = self.holder.index(index)
+        if idx is None or idx.keys:
+            return None
+        f = idx.field(fname)
+        if f is None or f.type == FIELD_TYPE_INT or f.options.keys or f.options.cache_type == "none":
+            return None
+        shards = list(shards) if shards else (idx.available_shards() or [0])
+        if self._has_remote(index, shards, ExecOptions()):
+            return None
+        ths = [t or DEFAULT_MIN_THRESHOLD for t in ths]
+        try:
+            res = gpu.topn_plain_batch(index, fname, ns, ths, shards)
+        except PilosaError:
+            return None
+        except Exception as err:  # noqa: BLE001 - device fault: the general path answers
+            self._gpu_fault(err)
+            return None
+        if res is None or len(res) != len(ns):
+            return None
+        if self.stats is not None:
+            self.stats.count_with_tags("TopN", len(res), [f"index:{index}"])
         return res
 
     def _topn_text_fast(self, index: str, text: str, shards=None) -> Optional[List[Any]]:

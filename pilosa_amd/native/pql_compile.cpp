@@ -629,6 +629,73 @@ std::vector<std::string> count_text_fields(const std::string& text) {
   return out;
 }
 
+// A request made only of plain cache-only TopN calls -- TopN(<field>
+// [, n=<uint>] [, threshold=<uint>]) in any argument order, separated by
+// whitespace -- as (field per call, n per call, threshold per call; 0 =
+// absent), or None for anything else (the general parser then runs).  The
+// serving fast path for cache-only TopN requests needs no Call objects.
+py::object topn_plain(const std::string& text) {
+  std::vector<std::string> fields;
+  std::vector<int64_t> ns, ths;
+  const size_t n = text.size();
+  size_t i = 0;
+  auto ident = [&](size_t& k) -> std::string {
+    const size_t f0 = k;
+    while (k < n && (std::isalnum(static_cast<unsigned char>(text[k])) || text[k] == '_' || text[k] == '-')) k++;
+    return text.substr(f0, k - f0);
+  };
+  auto uint = [&](size_t& k, int64_t& v) -> bool {
+    const size_t d0 = k;
+    v = 0;
+    while (k < n && std::isdigit(static_cast<unsigned char>(text[k]))) {
+      if (v > (INT64_MAX - 9) / 10) return false;
+      v = v * 10 + (text[k] - '0');
+      k++;
+    }
+    return k > d0;
+  };
+  for (;;) {
+    skip_ws(text, i);
+    if (i >= n) break;
+    if (text.compare(i, 5, "TopN(") != 0) return py::none();
+    i += 5;
+    skip_ws(text, i);
+    std::string f = ident(i);
+    if (f.empty() || !(std::isalpha(static_cast<unsigned char>(f[0])))) return py::none();
+    skip_ws(text, i);
+    int64_t nv = 0, tv = 0;
+    bool has_n = false, has_t = false;
+    while (i < n && text[i] == ',') {
+      i++;
+      skip_ws(text, i);
+      const std::string key = ident(i);
+      skip_ws(text, i);
+      if (i >= n || text[i] != '=') return py::none();
+      i++;
+      skip_ws(text, i);
+      int64_t v;
+      if (!uint(i, v)) return py::none();
+      if (key == "n" && !has_n) {
+        nv = v;
+        has_n = true;
+      } else if (key == "threshold" && !has_t) {
+        tv = v;
+        has_t = true;
+      } else {
+        return py::none();
+      }
+      skip_ws(text, i);
+    }
+    if (i >= n || text[i] != ')') return py::none();
+    i++;
+    fields.push_back(std::move(f));
+    ns.push_back(nv);
+    ths.push_back(tv);
+  }
+  if (fields.empty()) return py::none();
+  return py::make_tuple(fields, ns, ths);
+}
+
 // Distinct (field, from, to) of the time-range Row leaves of a request, in
 // first-seen order; from / to are None when not given.  The caller maps
 // each to its covering views (plan_count_text's `ranges`, keyed by
@@ -684,6 +751,8 @@ void register_compile(py::module_& m) {
         "Compile a request of top-level Count(<Row/Intersect/Union/Difference/Xor tree>) calls straight to "
         "QueryProg records; (progs uint8[Q*256], Q), or None when a call needs the general path");
   m.def("count_text_fields", &count_text_fields, py::arg("text"));
+  m.def("topn_plain", &topn_plain, py::arg("text"),
+        "(fields, n, threshold) per call of a request of plain TopN(<field>[, n=][, threshold=]) calls, or None");
   m.def("count_text_ranges", &count_text_ranges, py::arg("text"),
         "Distinct (field, from, to) of the time-range Row(f=<id>, from=, to=) leaves of a request");
   m.def("plan_count_text", &plan_count_text, py::arg("text"), py::arg("fields"), py::arg("dirs"),

@@ -1082,6 +1082,30 @@ class GpuExecutor:
                 raise NotImplementedError   # src too large for one device program: host path
         return self._topn_pairs_path(rc, rv, src, n, ids, threshold)
 
+    def topn_plain_batch(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: List[int]):
+        """Cache-only TopN(fname, n=ns[i], threshold=ths[i]) calls over the
+        local shards in one fused batch (Executor._topn_plain_fast): the
+        field's view and rank caches are resolved once per mutation epoch."""
+        if self.comm is not None:
+            return None
+        key = (index, fname, tuple(shards))
+        epoch = mutation_epoch()
+        memo = self.__dict__.setdefault("_plain_memo", {})
+        ent = memo.get(key)
+        if ent is None or ent[0] != epoch:
+            frags = self._topn_frags(index, fname, shards)
+            rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
+            rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
+            if len(memo) > 64:
+                memo.clear()
+            ent = memo[key] = (epoch, rv, rc)
+        _, rv, rc = ent
+        if rc is None or not rc.K:
+            return [[] for _ in ns]
+        self.launches += 1
+        with tracing.span("GpuExecutor.topnPlainBatch", gpu=True, calls=len(ns)):
+            return rc.topn_nosrc(list(ns), list(ths))
+
     def topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False):
         with tracing.span("GpuExecutor.topnBatch", gpu=True, calls=len(calls)):
             return self._topn_batch(index, calls, shards, defer)

@@ -372,6 +372,7 @@ def test_cache_only_batch_with_varied_n_matches_host(lazy_env):
     for order in (calls, calls[::-1], calls[2:] + calls[:2]):
         q = " ".join(order)
         got = ex.execute("i", q).results
+        assert gpu.__dict__.get("_plain_memo"), "the plain cache-only TopN path was not taken"
         ex.gpu = None
         try:
             want = ex.execute("i", q).results
