@@ -246,7 +246,9 @@ class NativeHTTPServer:
             return None
         try:
             api.validate("Query")
-            res = ex._topn_text_fast(index, text)
+            res = ex._topn_plain_fast(index, text)
+            if res is None:
+                res = ex._topn_text_fast(index, text)
         except Exception:  # noqa: BLE001 - the general path reports it
             return None
         if res is None or len(res) != ncalls:
