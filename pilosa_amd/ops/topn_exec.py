@@ -67,6 +67,7 @@ class _Lane:
         import torch
         self.device = device
         self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+        self.run_stream = self.stream   # the stream the current batch runs on
         self.pin = None
         self._bufs = {}
 
@@ -569,8 +570,10 @@ class DeviceRankCaches:
             return None
         lane = _lane_take(dev)
         if not SIDE_STREAM:
+            lane.run_stream = torch.cuda.current_stream(dev)
             res = self._topn_nosrc_fused_on(ns, nn, nmax, thresholds, lane)
         else:
+            lane.run_stream = lane.stream
             # a serving mix's TopN batch does not queue behind the Count batches
             # of other requests on the default stream, nor behind another
             # request's TopN batch
@@ -618,7 +621,7 @@ class DeviceRankCaches:
             # answers to the lane's pinned buffer, then wait for this stream only
             hb = lane.buf("out_h", out.numel(), torch.int64, pinned=True)
             hb.copy_(out.view(-1), non_blocking=True)
-            torch.cuda.current_stream(dev).synchronize()
+            lane.run_stream.synchronize()   # the stream this batch ran on (no current-stream lookup)
             h = hb.numpy().reshape(Q, KK + 1)
         else:
             h = out.cpu().numpy()
