@@ -18,6 +18,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import datetime as dt
 import os
+import re
 import threading
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -39,6 +40,10 @@ DEFAULT_FIELD = "general"
 _FANOUT_LOCK = threading.Lock()
 DEFAULT_MIN_THRESHOLD = 1
 MAX_INT = (1 << 63) - 1
+
+
+# a request that is one unfiltered BSI aggregate: Sum|Min|Max(field=<name>)
+_BSI_AGG_RE = re.compile(r"\s*(Sum|Min|Max)\(\s*field\s*=\s*([A-Za-z][A-Za-z0-9_-]*)\s*\)\s*$")
 
 
 class ExecOptions:
@@ -265,6 +270,15 @@ class Executor:
                 fast = self._count_text_fast(index, q, shards, opt)
                 if fast is not None:
                     return QueryResponse(fast)
+                # Sum / Min / Max(field=f) alone: straight to the call, no parse
+                # tree or request dispatch (a BSI aggregate is ~0.5 ms of device
+                # streaming; the generic layers were a visible share on top)
+                if opt is None and self.gpu is not None:
+                    m = _BSI_AGG_RE.match(q)
+                    if m is not None:
+                        fast = self._bsi_agg_fast(index, m.group(1), m.group(2), shards)
+                        if fast is not None:
+                            return QueryResponse([fast])
                 # a request of several cache-only TopN calls: parsed once, one
                 # device batch, columnar results (single calls keep the
                 # cross-request coalescer of the general path)
@@ -502,6 +516,19 @@ class Executor:
                 if [(p.id, p.count) for p in r] != [(p.id, p.count) for p in want]:
                     raise AssertionError(f"paranoia: device TopN {r!r} != host TopN {want!r}")
         return res
+
+    def _bsi_agg_fast(self, index: str, name: str, fname: str, shards=None):
+        """``Sum|Min|Max(field=fname)`` as the request's only call: the same
+        execute_call the general path reaches, without building the request
+        from a parse tree.  None = the general path."""
+        idx = self.holder.index(index)
+        if idx is None or idx.keys:
+            return None
+        f = idx.field(fname)
+        if f is None or f.bsi_group(fname) is None:
+            return None   # the general path reports it
+        c = Call(name, {"field": fname})
+        return self.execute_call(index, c, list(shards) if shards else (idx.available_shards() or [0]), ExecOptions())
 
     def _topn_plain_fast(self, index: str, text: str, shards=None) -> Optional[List[Any]]:
         """Single-GPU fast path for a request of plain cache-only calls of one

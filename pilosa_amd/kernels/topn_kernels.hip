@@ -1161,6 +1161,31 @@ __global__ __launch_bounds__(256) void topn_cache_member_kernel(const int32_t* _
   }
 }
 
+// The same membership with one thread per (shard, rank) for every query of
+// the batch (Q <= 256): the rank's count and candidate index are read once
+// instead of once per query (the per-query grid re-read them Q times).
+__global__ __launch_bounds__(256) void topn_cache_member_q_kernel(const int32_t* __restrict__ cnt, int K, int S,
+                                                                  int nmax, const int32_t* __restrict__ inv,
+                                                                  const int32_t* __restrict__ prm, int Q, int U,
+                                                                  uint8_t* __restrict__ member, int nlim) {
+  __shared__ int32_t lim[256], thr[256];
+  for (int q = threadIdx.x; q < Q; q += blockDim.x) {
+    lim[q] = min(prm[q], nlim);
+    thr[q] = prm[Q + q];
+  }
+  __syncthreads();
+  const int64_t N = int64_t(S) * nlim;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < N; e += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t s = e / nlim;
+    const int k = int(e - s * nlim);
+    const int32_t c = cnt[s * K + k];
+    if (c <= 0) continue;
+    const int j = inv[s * nmax + k];
+    for (int q = 0; q < Q; q++)
+      if (k < lim[q] && c >= thr[q]) member[int64_t(q) * U + j] = 1;
+  }
+}
+
 // tot[t*U + j] = sum over shards of cm[j*S + s] where it reaches th[t]; one
 // wave per (threshold, candidate), coalesced over the shard axis.  TT = long
 // long on one rank; int on a mesh rank, whose partial totals travel in the
@@ -1290,8 +1315,12 @@ void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const i
   if (N > 0) {
     const int64_t want = (N + 255) / 256;
     const int bx = int(want < 1024 ? want : 1024);
-    hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
-                       member, nlim);
+    if (Q <= 256)
+      hipLaunchKernelGGL(topn_cache_member_q_kernel, dim3(unsigned(want < 8192 ? want : 8192)), dim3(256), 0, st, cnt,
+                         K, S, nmax, inv, prm, Q, U, member, nlim);
+    else
+      hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
+                         member, nlim);
   }
   const int64_t waves = int64_t(T) * U;
   if (T <= 16)
