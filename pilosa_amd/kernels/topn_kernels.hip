@@ -717,8 +717,15 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         uint32_t mk[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
+        if (__ballot(curv < 8) == 0) {
+          // every lane holds 8 values (the inner chunks of a big array, which
+          // carry most of the values): no per-value pad select
 #pragma unroll
-        for (int t = 0; t < 8; t++) swar_add<NQ>(c4, t < curv ? mk[t] : 0u);
+          for (int t = 0; t < 8; t++) swar_add<NQ>(c4, mk[t]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; t++) swar_add<NQ>(c4, t < curv ? mk[t] : 0u);
+        }
       } else if (ty == CT_BITMAP && !(p.dbg & 32)) {
         // all 16 words of the lane issued before the first is counted; set
         // bits are taken four at a time (four table reads in flight)
