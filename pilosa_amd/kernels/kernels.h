@@ -118,8 +118,12 @@ struct TopNLaunch {
   const int32_t* cache_dense;     // [S][K] dense row of each cache slot (mode 3 exact probes)
   int M;                          // arena sub-shards per fragment (S fragments, S*M device shards: src, colptr,
                                   // entbase, slots, hot_meta/split are per sub-shard; mode 4 runs with S*M, M=1)
+  int tbuild_min;                 // mode 4: bitmap srcs of >= this many bits build the table by transpose
   int dbg;                        // PILOSA_TOPN_DBG cost isolation: 1 skip histogram, 2 skip walk, 8 skip small hot rows,
-                                  // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays (answers then wrong)
+                                  // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays, 128 byte-counter
+                                  // (swar) hot counting, 256 no lane-owned atomics, 512 table skips bitmap srcs, 1024
+                                  // bitmap srcs by LDS atomics (not the transposed build)
+                                  // (answers then wrong, except 128 and 1024)
 };
 // LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).
 int topn_lds_bytes(int K, int H32, int H16);

@@ -520,10 +520,10 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
 // shard, -1 = none), built once with the index.
 constexpr int HOT_THREADS = 1024;
 constexpr int HOT_TAB_WORDS = 32768;
-// Lane-owned (small) containers: at most SMALLN values.  255 fits the byte
-// counters outright; 1023 (PILOSA_TOPN_SMALL_N=1023) flushes them into u32
-// totals every 240 values, so mid-size rows skip the wave-cooperative path's
-// per-row transpose-reduce.
+// Lane-owned (small) containers: at most SMALLN values (PILOSA_TOPN_SMALL_N
+// = 255, 1023 or 4096 = every array).  Counts are carry-save planes that a
+// lane turns into per-query totals every 240 values, so bigger rows lane-owned
+// skip the wave-cooperative path's per-row transpose-reduce.
 constexpr int HOT_SMALL_N = 255;
 
 // SWAR: add the 16 bits of a query mask to 16 byte counters (4 per word):
@@ -532,6 +532,104 @@ template <int NQ>
 __device__ __forceinline__ void swar_add(uint32_t (&c4)[NQ / 4], uint32_t msk) {
 #pragma unroll
   for (int g = 0; g < NQ / 4; g++) c4[g] += (((msk >> (4 * g)) & 15u) * 0x00204081u) & 0x01010101u;
+}
+
+// Bit-sliced (carry-save) counting.  A "word" is a query mask: for NQ = 16
+// the masks of two values packed as lo | hi << 16 (bit q and bit 16 + q both
+// count query q), for NQ = 32 one value's u32 mask.  pl[k] holds bit k of 32
+// per-bit counters; adding W words is a Harley-Seal tree of carry-save
+// adders (3 ops each: xor3, xor, bfi) whose last carry ripples up to plane
+// MAXP - 1 (2 ops a plane).  That is ~2.5 ops per value against the 12-14 of
+// spreading every mask into byte counters (swar_add); the planes are turned
+// into counts once per row (hs_counts).
+__device__ __forceinline__ void csa(uint32_t& s, uint32_t& c, uint32_t a, uint32_t b) {
+  // s + a + b = (s ^ a ^ b) + 2 * maj(s, a, b)
+  const uint32_t u = s ^ a;
+  c = (u & b) | (~u & s);
+  s = u ^ b;
+}
+template <int K0, int MAXP>
+__device__ __forceinline__ void hs_ripple(uint32_t (&pl)[8], uint32_t c) {
+#pragma unroll
+  for (int k = K0; k < MAXP; k++) {
+    const uint32_t t = pl[k] & c;
+    pl[k] ^= c;
+    c = t;
+  }
+}
+template <int W, int MAXP>
+__device__ __forceinline__ void hs_add(uint32_t (&pl)[8], const uint32_t* w) {
+  uint32_t a, b, c2a, c2b;
+  if constexpr (W == 2) {
+    csa(pl[0], a, w[0], w[1]);
+    hs_ripple<1, MAXP>(pl, a);
+  } else if constexpr (W == 4) {
+    csa(pl[0], a, w[0], w[1]);
+    csa(pl[0], b, w[2], w[3]);
+    csa(pl[1], c2a, a, b);
+    hs_ripple<2, MAXP>(pl, c2a);
+  } else {
+    static_assert(W == 8 || W == 16, "hs_add: W in {2, 4, 8, 16}");
+    uint32_t c3a, c3b, c4;
+#pragma unroll
+    for (int h = 0; h < W / 8; h++) {
+      const uint32_t* v = w + 8 * h;
+      csa(pl[0], a, v[0], v[1]);
+      csa(pl[0], b, v[2], v[3]);
+      csa(pl[1], c2a, a, b);
+      csa(pl[0], a, v[4], v[5]);
+      csa(pl[0], b, v[6], v[7]);
+      csa(pl[1], c2b, a, b);
+      csa(pl[2], h ? c3b : c3a, c2a, c2b);
+    }
+    if constexpr (W == 8) {
+      hs_ripple<3, MAXP>(pl, c3a);
+    } else {
+      csa(pl[3], c4, c3a, c3b);
+      hs_ripple<4, MAXP>(pl, c4);
+    }
+  }
+}
+// Add the counters held in planes pl[0..NP) to acc[NQ] and clear the planes.
+// An 8x8 bit transpose inside every byte (3 delta-swap rounds over the 8
+// plane words) leaves in byte b of word c the 8-bit count of bit 8b + c; a
+// v_dot4 then sums the bytes that belong to one query into acc.
+template <int NQ, int NP>
+__device__ __forceinline__ void hs_counts(uint32_t (&pl)[8], uint32_t (&acc)[NQ]) {
+#pragma unroll
+  for (int k = NP; k < 8; k++) pl[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t t = ((pl[k] >> 4) ^ pl[k + 4]) & 0x0f0f0f0fu;
+    pl[k + 4] ^= t;
+    pl[k] ^= t << 4;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (k & 2) continue;
+    const uint32_t t = ((pl[k] >> 2) ^ pl[k + 2]) & 0x33333333u;
+    pl[k + 2] ^= t;
+    pl[k] ^= t << 2;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+    const uint32_t t = ((pl[k] >> 1) ^ pl[k + 1]) & 0x55555555u;
+    pl[k + 1] ^= t;
+    pl[k] ^= t << 1;
+  }
+  // word c: bytes = counts of bits c, 8 + c, 16 + c, 24 + c
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    if (NQ == 16) {
+      // bits q and 16 + q are both query q
+      acc[c] = __builtin_amdgcn_udot4(pl[c], 0x00010001u, acc[c], false);
+      acc[8 + c] = __builtin_amdgcn_udot4(pl[c], 0x01000100u, acc[8 + c], false);
+    } else {
+#pragma unroll
+      for (int b = 0; b < 4; b++) acc[(8 * b + c) % NQ] = __builtin_amdgcn_udot4(pl[c], 1u << (8 * b), acc[(8 * b + c) % NQ], false);
+    }
+    pl[c] = 0;
+  }
 }
 
 // NQ = 16: one workgroup per (shard, key j), a u16 query mask per value of
@@ -554,6 +652,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   const int Q = p.Q, R = p.R;
   const int64_t sb = p.v.shard_base[s];
   uint32_t* out = p.hot_cnt + int64_t(s) * Q * R;
+  const bool hs = !(p.dbg & 128);  // 128: byte-counter (swar_add) array counting
   // 1. query-mask table of key j.  One wave per query (wave w takes queries
   //    w, w + 16): each lane issues 8 independent value loads before its 8
   //    LDS ORs, so the table costs a few load round trips instead of one per
@@ -561,14 +660,49 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //    every round trip of the build (1.55 ms of a 16-query launch with the
   //    thread-per-value loop over queries, profiles/r03_hotsplit/).
   const int wave = tid >> 6;
+  // bit q: src q's key-j container is a bitmap (the same mask in every wave)
+  uint32_t bmq;
   {
-    int has = 0;
-    if (tid < Q) has = p.src_counts[(int64_t(tid) * p.S + s) * 16 + j] > 0;
-    if (!__syncthreads_or(has)) return;  // block-uniform: no src has key j in this shard
+    const int nq = lane < Q ? p.src_counts[(int64_t(lane) * p.S + s) * 16 + j] : 0;
+    bmq = uint32_t(__ballot(nq > ARRAY_MAX && nq >= p.tbuild_min));
+    if (!__syncthreads_or(tid < Q && nq > 0)) return;  // block-uniform: no src has key j in this shard
   }
-  uint4* t4 = reinterpret_cast<uint4*>(tab);
-  for (int i = tid; i < HOT_TAB_WORDS / 4; i += HOT_THREADS) t4[i] = make_uint4(0, 0, 0, 0);
   if (tid == 0) grab[0] = grab[1] = 0;
+  if (bmq && !(p.dbg & 1024)) {
+    // bitmap srcs: every table word is written once as the transpose of the
+    // bitmaps' bits (thread-owned words, 32 loads in flight per query)
+    // instead of one LDS atomic per set bit -- a dense src row is 30-50k bits
+    // per key, which serialised ~500 atomics per lane.  Array srcs OR in below.
+    constexpr int PER = HOT_TAB_WORDS / HOT_THREADS;  // 32 table words per thread
+    const int sh = HB ? (tid & 31) : ((2 * tid) & 31);
+    uint32_t e[PER];
+#pragma unroll
+    for (int t = 0; t < PER; t++) e[t] = 0u;
+    for (uint32_t m = bmq; m; m &= m - 1) {
+      const int q = __builtin_ctz(m);
+      const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
+      const auto w32 = reinterpret_cast<const TN_GLOBAL uint32_t*>(gp(p.src_vals + p.src_offs[kk]));
+      uint32_t v[PER];
+#pragma unroll
+      for (int t = 0; t < PER; t++)
+        v[t] = HB ? w32[((lo + tid) >> 5) + 32 * t] : w32[(tid >> 4) + 64 * t];
+#pragma unroll
+      for (int t = 0; t < PER; t++) {
+        if (HB) {
+          e[t] |= ((v[t] >> sh) & 1u) << q;           // entry x = lo + tid + 1024 t
+        } else {
+          const uint32_t b2 = (v[t] >> sh) & 3u;      // entries x = 2 (tid + 1024 t) + {0, 1}
+          e[t] |= ((b2 & 1u) << q) | ((b2 >> 1) << (16 + q));
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < PER; t++) tab[tid + HOT_THREADS * t] = e[t];
+  } else {
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    for (int i = tid; i < HOT_TAB_WORDS / 4; i += HOT_THREADS) t4[i] = make_uint4(0, 0, 0, 0);
+    bmq = 0;
+  }
   __syncthreads();
   for (int q = wave; q < Q; q += HOT_THREADS / 64) {
     const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
@@ -594,7 +728,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
           }
         }
       }
-    } else {
+    } else if (!((bmq >> q) & 1u) && !(p.dbg & 512)) {
       const auto w = reinterpret_cast<const TN_GLOBAL uint64_t*>(vals);
       for (int i = lane + (lo >> 6); i < (lo + NLO) >> 6; i += 64)
         for (uint64_t bb = w[i]; bb; bb &= bb - 1) {
@@ -686,6 +820,12 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     uint32_t acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; q++) acc[q] = 0;
+    // array rows: carry-save planes (a lane sees <= 64 values of a row:
+    // 6 planes hold 32 per packed half, 7 hold 64)
+    constexpr int HW = NQ == 16 ? 4 : 8, COOP_P = NQ == 16 ? 6 : 7;
+    uint32_t pl[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) pl[k] = 0;
     auto flush = [&]() {
 #pragma unroll
       for (int q = 0; q < NQ; q++) acc[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
@@ -717,7 +857,20 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         uint32_t mk[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
-        if (__ballot(curv < 8) == 0) {
+        if (hs) {
+          // carry-save planes, counted once at the row's end
+          uint32_t hw[HW];
+          if (__ballot(curv < 8) == 0) {
+#pragma unroll
+            for (int k = 0; k < HW; k++) hw[k] = NQ == 16 ? mk[2 * k] | (mk[2 * k + 1] << 16) : mk[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < HW; k++)
+              hw[k] = NQ == 16 ? (2 * k < curv ? mk[2 * k] : 0u) | (2 * k + 1 < curv ? mk[2 * k + 1] << 16 : 0u)
+                               : (k < curv ? mk[k] : 0u);
+          }
+          hs_add<HW, COOP_P>(pl, hw);
+        } else if (__ballot(curv < 8) == 0) {
           // every lane holds 8 values (the inner chunks of a big array, which
           // carry most of the values): no per-value pad select
 #pragma unroll
@@ -770,6 +923,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       }
       if (row_end) {
         flush();
+        if (hs && ty == CT_ARRAY) hs_counts<NQ, COOP_P>(pl, acc);
         // transpose-reduce: NQ counters x 64 lanes -> one total per 64/NQ
         // lanes: each level halves the counters a lane holds and sums the
         // exchanged half with lane ^ step (query bit = lane bit)
@@ -867,9 +1021,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const int kl = B + 64 * g + lane;
       const int nl = cl >= 0 ? meta_n(ml) : 0;
       const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
-      uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
-      if (0 < nl) w0 = pp[0];
-      if (8 < nl) w1 = pp[1];
+      // every lane loads (clamped to its row's last chunk; values past the
+      // row are masked when counted), so no load sits behind a branch
+      const int lastc = max(nl - 1, 0) >> 3;
+      uint4 w0 = pp[0], w1 = pp[min(1, lastc)];
       const int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
       const int gnn = claim();
       const int clnn = rank_meta(gnn);
@@ -879,20 +1034,40 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       uint32_t big[SMALLN > 255 ? NQ : 1];
 #pragma unroll
       for (int q = 0; q < (SMALLN > 255 ? NQ : 1); q++) big[q] = 0u;
+      uint32_t lpl[8], lcnt[NQ];
+#pragma unroll
+      for (int k = 0; k < 8; k++) lpl[k] = 0u;
+#pragma unroll
+      for (int q = 0; q < NQ; q++) lcnt[q] = 0u;
       int since = 0;
-      for (int i = 0; __ballot(i < nl); i += 16) {
-        // two 16-byte loads per lane (16 values); all 16 table reads issue
-        // before any is consumed (values past the row count nothing)
-        if (i > 0) {
-          w0 = make_uint4(0, 0, 0, 0);
-          w1 = make_uint4(0, 0, 0, 0);
-          if (i < nl) w0 = pp[i >> 3];
-          if (i + 8 < nl) w1 = pp[(i >> 3) + 1];
-        }
-        const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      // 16 values per lane per step; two buffers alternate so the next
+      // step's loads are in flight while this one is counted
+      auto body = [&](const uint4& x0, const uint4& x1, const int i) {
+        const uint32_t wd[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         uint32_t mk[16];
 #pragma unroll
         for (int t = 0; t < 16; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
+        if (hs) {
+          // carry-save planes (<= 240 values per lane between counts: 8
+          // planes hold them), counted at the row's end
+          constexpr int LW = NQ == 16 ? 8 : 16;
+          uint32_t hw[LW];
+          if (__ballot(i + 16 > nl) == 0) {
+#pragma unroll
+            for (int k = 0; k < LW; k++) hw[k] = NQ == 16 ? mk[2 * k] | (mk[2 * k + 1] << 16) : mk[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < LW; k++)
+              hw[k] = NQ == 16 ? (i + 2 * k < nl ? mk[2 * k] : 0u) | (i + 2 * k + 1 < nl ? mk[2 * k + 1] << 16 : 0u)
+                               : (i + k < nl ? mk[k] : 0u);
+          }
+          hs_add<LW, 8>(lpl, hw);
+          if (SMALLN > 255 && ++since == 15) {
+            since = 0;
+            hs_counts<NQ, 8>(lpl, lcnt);
+          }
+          return;
+        }
 #pragma unroll
         for (int t = 0; t < 16; t++) swar_add<NQ>(c4, i + t < nl ? mk[t] : 0u);
         if (SMALLN > 255 && ++since == 15) {   // wave-uniform: <= 240 values per byte counter
@@ -902,12 +1077,32 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
 #pragma unroll
           for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
         }
+      };
+      uint4 n0, n1;
+      for (int i = 0;;) {
+        if (!__ballot(i < nl)) break;
+        n0 = pp[min((i >> 3) + 2, lastc)];
+        n1 = pp[min((i >> 3) + 3, lastc)];
+        body(w0, w1, i);
+        i += 16;
+        if (!__ballot(i < nl)) break;
+        w0 = pp[min((i >> 3) + 2, lastc)];
+        w1 = pp[min((i >> 3) + 3, lastc)];
+        body(n0, n1, i);
+        i += 16;
       }
+      if (hs) {
+        hs_counts<NQ, 8>(lpl, lcnt);
 #pragma unroll
-      for (int q = 0; q < NQ; q++) {
-        uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
-        if (SMALLN > 255) c += big[SMALLN > 255 ? q : 0];
-        if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
+        for (int q = 0; q < NQ; q++)
+          if (q < Q && lcnt[q] && (!(p.dbg & 256) || lcnt[q] == 0x7fffffffu)) atomicAdd(out + int64_t(q) * R + kl, lcnt[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+          uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
+          if (SMALLN > 255) c += big[SMALLN > 255 ? q : 0];
+          if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
+        }
       }
       g = gn;
       cl = cln;
@@ -1019,14 +1214,23 @@ void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_
                      offs, has_run);
 }
 
-// lane-owned container bound of the hot-rank kernels (255 or 1023), fixed per
-// process: the split the meta kernel records must match the counting kernel's
+// lane-owned container bound of the hot-rank kernels (255, 1023 or 4096 =
+// every array), fixed per process: the split the meta kernel records must
+// match the counting kernel's
 static int hot_small_n() {
   static const int n = [] {
     const char* e = getenv("PILOSA_TOPN_SMALL_N");
-    return e && atoi(e) > 255 ? 1023 : 255;
+    const int v = e ? atoi(e) : 0;
+    return v > 1023 ? 4096 : v > 255 ? 1023 : 255;
   }();
   return n;
+}
+
+template <int SMALLN>
+static void launch_hot_meta_t(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
+                              int32_t* hot_split, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(topn_hot_meta_kernel<SMALLN>, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense, hot_meta,
+                     hot_split);
 }
 
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
@@ -1035,12 +1239,20 @@ void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* 
   if (total <= 0) return;
   const int64_t want = (total + 255) / 256;
   const int blocks = int(want < 65536 ? want : 65536);
-  if (hot_small_n() > 255)
-    hipLaunchKernelGGL(topn_hot_meta_kernel<1023>, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense,
-                       hot_meta, hot_split);
-  else
-    hipLaunchKernelGGL(topn_hot_meta_kernel<255>, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense,
-                       hot_meta, hot_split);
+  switch (hot_small_n()) {
+    case 4096: launch_hot_meta_t<4096>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st); break;
+    case 1023: launch_hot_meta_t<1023>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st); break;
+    default: launch_hot_meta_t<255>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st);
+  }
+}
+
+template <int NQ, int SMALLN>
+static void launch_hot_t(const TopNLaunch& a, hipStream_t st) {
+  const int tab = HOT_TAB_WORDS * 4;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<NQ, SMALLN>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, tab);
+  hipLaunchKernelGGL((topn_hot_kernel<NQ, SMALLN>), dim3(unsigned(a.S) * unsigned(NQ)), dim3(HOT_THREADS), tab, st,
+                     a);
 }
 
 void launch_topn_index(const ViewDev& v, int S, int K, int k0, const int32_t* cache_dense, uint32_t* colcnt,
@@ -1068,29 +1280,25 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
     return e ? atoi(e) : 0;
   }();
   a.dbg = dbg;
+  // bitmap srcs at least this dense take the transposed table build, the
+  // rest one LDS atomic per set bit
+  static const int tbuild_min = [] {
+    const char* e = getenv("PILOSA_TOPN_TBUILD_MIN");
+    return e ? atoi(e) : 4097;
+  }();
+  a.tbuild_min = tbuild_min;
   const int lds = topn_lds_bytes(a.K - a.R, a.H32, a.H16);
   const int64_t units = int64_t(a.Q) * a.S;
   if (units <= 0) return;
   if (mode == 4) {
     // hot-rank count matrix (before mode 1/2 of the same batch)
     if (a.R <= 0) return;
-    const int tab = HOT_TAB_WORDS * 4;
-    if (a.Q > 16 && hot_small_n() > 255) {   // the split must match the meta kernel's bound
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<32, 1023>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
-      hipLaunchKernelGGL((topn_hot_kernel<32, 1023>), dim3(unsigned(a.S) * 32u), dim3(HOT_THREADS), tab, st, a);
-    } else if (a.Q > 16) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<32>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
-      hipLaunchKernelGGL(topn_hot_kernel<32>, dim3(unsigned(a.S) * 32u), dim3(HOT_THREADS), tab, st, a);
-    } else if (hot_small_n() > 255) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<16, 1023>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
-      hipLaunchKernelGGL((topn_hot_kernel<16, 1023>), dim3(unsigned(a.S) * 16u), dim3(HOT_THREADS), tab, st, a);
-    } else {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(topn_hot_kernel<16>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, tab);
-      hipLaunchKernelGGL(topn_hot_kernel<16>, dim3(unsigned(a.S) * 16u), dim3(HOT_THREADS), tab, st, a);
+    // the split must match the meta kernel's bound (hot_small_n)
+    const bool q32 = a.Q > 16;
+    switch (hot_small_n()) {
+      case 4096: q32 ? launch_hot_t<32, 4096>(a, st) : launch_hot_t<16, 4096>(a, st); break;
+      case 1023: q32 ? launch_hot_t<32, 1023>(a, st) : launch_hot_t<16, 1023>(a, st); break;
+      default: q32 ? launch_hot_t<32, 255>(a, st) : launch_hot_t<16, 255>(a, st);
     }
   } else if (mode == 3) {
     hipLaunchKernelGGL(topn_gather_kernel, dim3(unsigned(units)), dim3(256), 0, st, a);

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Hot-rank TopN kernel in isolation (ops/topn_index.py hot_counts) for
-profiling: --shards of the Zipf arena, 16 src rows, --reps launches."""
+profiling: --shards of the Zipf arena, 16 src rows (--src first row, or "mix"
+for the bench's Zipf draw), --reps launches."""
 import argparse
 import json
 import os
@@ -33,8 +34,14 @@ def main():
     eng = GpuEngine(dev)
     cache = DeviceRankCache.from_view(view, k=50000)
     idx = DeviceTopNIndex(view, cache)
-    base = int(args.src)
-    src = eng.materialize_batch([Leaf(view, base + i) for i in range(16)], S)
+    if args.src == "mix":   # the bench's src rows: Zipf over the 1000 hottest
+        import numpy as np
+
+        from bench import zipf_rows
+        rows = [int(r) for r in zipf_rows(np.random.default_rng(99), 16, 1000)]
+    else:
+        rows = [int(args.src) + i for i in range(16)]
+    src = eng.materialize_batch([Leaf(view, r) for r in rows], S)
     idx.hot_counts(src, 16)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
