@@ -378,7 +378,7 @@ void topn_hot_meta(torch::Tensor view, int64_t S, int64_t K, int64_t R, torch::T
   TORCH_CHECK(R >= 0 && R <= K, "hot ranks 0 <= R <= K");
   TORCH_CHECK(hot_meta.scalar_type() == torch::kInt32 && hot_meta.numel() == S * 16 * R, "hot_meta int32[S*16*R]");
   check_dev(hot_split, "hot_split");
-  TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == S * 16, "hot_split int32[S*16]");
+  TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == S * 32, "hot_split int32[S*16*2]");
   pk::launch_topn_hot_meta(viewdev_from(view), int(S), int(K), int(R), cache_dense.data_ptr<int32_t>(),
                            hot_meta.data_ptr<int32_t>(), hot_split.data_ptr<int32_t>(), cur_stream(cache_dense));
   check_launch("topn_hot_meta");
@@ -409,7 +409,7 @@ void topn_src(torch::Tensor view, int64_t Q, int64_t S, int64_t K, int64_t H32, 
     TORCH_CHECK(hot_cnt.scalar_type() == torch::kInt32 && hot_cnt.numel() == (mode == 4 ? Sd : S) * Q * R,
                 "hot_cnt int32[S*Q*R] (mode 4: [S*M*Q*R])");
     check_dev(hot_split, "hot_split");
-    TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == Sd * 16, "hot_split int32[S*M*16]");
+    TORCH_CHECK(hot_split.scalar_type() == torch::kInt32 && hot_split.numel() == Sd * 32, "hot_split int32[S*M*16*2]");
   }
   TORCH_CHECK(src_counts.scalar_type() == torch::kInt32 && src_counts.numel() == Q * Sd * 16,
               "src_counts int32[Q*S*M*16]");

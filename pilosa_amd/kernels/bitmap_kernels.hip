@@ -837,89 +837,128 @@ __global__ __launch_bounds__(256) void bsi_sum_keys_kernel(const QueryProg* __re
   const int wave = threadIdx.x >> 6;
   const int lane = wave_lane();
   const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
-  if (item >= int64_t(Q) * S * 16) return;
-  const int q = int(item % Q);
-  const int j = int((item / Q) & 15);
-  const int s = int(item / (int64_t(Q) * 16));
-  const QueryProg& qp = progs[q];
-  WaveScratch& ws = scratch[wave];
-  const ViewDev& bv = views[bsi.view];
-  const uint32_t* rp = bv.rowptr + int64_t(s) * (bv.D + 1);
-  const int64_t base = bv.shard_base[s];
-  // container index of dense row d at key j (or -1), evaluated per lane
-  auto lane_find = [&](int64_t d) -> int64_t {
-    if (d < 0) return -1;
-    const int64_t lo = base + rp[d], hi = base + rp[d + 1];
-    if (hi - lo == 16) return lo + j;   // every key present (dense planes): no meta walk
-    for (int64_t c = lo; c < hi; c++)
-      if (meta_j(bv.meta[c]) == j) return c;
-    return -1;
-  };
-  // lane i < depth (<= 63): bit plane i; lanes 0 / 1 then resolve exists /
-  // sign in a second parallel lookup
-  const int64_t mine = lane < bsi.depth ? lane_find(bsi.bit_row[lane]) : -1;
-  const int64_t extra = lane == 0 ? lane_find(bsi.row_exists) : (lane == 1 ? lane_find(bsi.row_sign) : -1);
-  const int64_t ce = rl_i64(extra, 0);
-  if (ce < 0) return;
-  Tile consider, sign, bits;
-  tile_load(consider, bv.payload, bv.meta[ce], ws.lb);
-  if (FMODE != 0 && qp.nprog) {
-    uint32_t mask[MAXLEAF];
-    build_slots(qp, views, s, ws, mask);
-    if (!((candidate_mask(qp, mask) >> j) & 1)) return;
-    Tile f;
-    if (FMODE == 1) eval_flat(qp, views, s, j, ws, f);
-    else eval_tile(qp, views, s, j, ws, f);
-    tile_op<OP_AND>(consider, f);
-  }
-  const int64_t acc_cnt = tile_popc(consider);
-  const int64_t cs = rl_i64(extra, 1);
-  if (cs >= 0) tile_load(sign, bv.payload, bv.meta[cs], ws.lb);
-  else tile_zero(sign);
-  int64_t acc_sum = 0;
-  // planes double-buffered: the next present plane's tile is in flight
-  // while the current one is counted (one load round trip per plane, not
-  // a wait before every plane)
-  const uint64_t present = __ballot(mine >= 0) & (bsi.depth >= 64 ? ~0ull : ((1ull << bsi.depth) - 1));
-  auto count_plane = [&](const Tile& t, int i) {
-    int pc = 0, nc = 0;
-#pragma unroll
+  const bool live = item < int64_t(Q) * S * 16;
+  const int q = live ? int(item % Q) : -1;
+  // the wave's (sum, count); the block folds its waves' results into one
+  // atomic pair per query: 15k waves hitting the same two words serialise
+  // at one L2 channel
+  int64_t tsum = 0, tcnt = 0;
+  auto work = [&]() {
+    const int j = int((item / Q) & 15);
+    const int s = int(item / (int64_t(Q) * 16));
+    const QueryProg& qp = progs[q];
+    WaveScratch& ws = scratch[wave];
+    const ViewDev& bv = views[bsi.view];
+    const uint32_t* rp = bv.rowptr + int64_t(s) * (bv.D + 1);
+    const int64_t base = bv.shard_base[s];
+    // container index of dense row d at key j (or -1), evaluated per lane
+    auto lane_find = [&](int64_t d) -> int64_t {
+      if (d < 0) return -1;
+      const int64_t lo = base + rp[d], hi = base + rp[d + 1];
+      if (hi - lo == 16) return lo + j;   // every key present (dense planes): no meta walk
+      for (int64_t c = lo; c < hi; c++)
+        if (meta_j(bv.meta[c]) == j) return c;
+      return -1;
+    };
+    // lane i < depth (<= 63): bit plane i; lanes 0 / 1 then resolve exists /
+    // sign in a second parallel lookup
+    const int64_t mine = lane < bsi.depth ? lane_find(bsi.bit_row[lane]) : -1;
+    const int64_t extra = lane == 0 ? lane_find(bsi.row_exists) : (lane == 1 ? lane_find(bsi.row_sign) : -1);
+    const int64_t ce = rl_i64(extra, 0);
+    if (ce < 0) return;
+    Tile consider, sign, bits;
+    tile_load(consider, bv.payload, bv.meta[ce], ws.lb);
+    if (FMODE != 0 && qp.nprog) {
+      uint32_t mask[MAXLEAF];
+      build_slots(qp, views, s, ws, mask);
+      if (!((candidate_mask(qp, mask) >> j) & 1)) return;
+      Tile f;
+      if (FMODE == 1) eval_flat(qp, views, s, j, ws, f);
+      else eval_tile(qp, views, s, j, ws, f);
+      tile_op<OP_AND>(consider, f);
+    }
+    const int64_t acc_cnt = tile_popc(consider);
+    const int64_t cs = rl_i64(extra, 1);
+    if (cs >= 0) tile_load(sign, bv.payload, bv.meta[cs], ws.lb);
+    else tile_zero(sign);
+    // consider splits into its non-negative and negative columns once per key
+    // (consider <- consider & ~sign, sign <- consider & sign); a key with no
+    // negative column (the usual case: the sign row is sparse) then counts one
+    // AND + popcount per plane word instead of two
+    uint64_t anyneg = 0;
+  #pragma unroll
     for (int w = 0; w < 8; w++) {
-      const uint64_t bx = t.w[w].x & consider.w[w].x, by = t.w[w].y & consider.w[w].y;
-      pc += __popcll(bx & ~sign.w[w].x) + __popcll(by & ~sign.w[w].y);
-      nc += __popcll(bx & sign.w[w].x) + __popcll(by & sign.w[w].y);
+      const ulong2 c = consider.w[w], g = sign.w[w];
+      consider.w[w] = make_ulong2(c.x & ~g.x, c.y & ~g.y);
+      sign.w[w] = make_ulong2(c.x & g.x, c.y & g.y);
+      anyneg |= sign.w[w].x | sign.w[w].y;
     }
-    acc_sum += int64_t(uint64_t(int64_t(pc - nc)) << i);
+    const bool neg = __ballot(anyneg != 0) != 0;
+    int64_t acc_sum = 0;
+    // planes double-buffered: the next present plane's tile is in flight
+    // while the current one is counted (one load round trip per plane, not
+    // a wait before every plane)
+    const uint64_t present = __ballot(mine >= 0) & (bsi.depth >= 64 ? ~0ull : ((1ull << bsi.depth) - 1));
+    auto count_plane = [&](const Tile& t, int i) {
+      int pc = 0, nc = 0;
+  #pragma unroll
+      for (int w = 0; w < 8; w++) pc += __popcll(t.w[w].x & consider.w[w].x) + __popcll(t.w[w].y & consider.w[w].y);
+      if (neg) {
+  #pragma unroll
+        for (int w = 0; w < 8; w++) nc += __popcll(t.w[w].x & sign.w[w].x) + __popcll(t.w[w].y & sign.w[w].y);
+      }
+      acc_sum += int64_t(uint64_t(int64_t(pc - nc)) << i);
+    };
+    Tile bits2;
+    uint64_t left = present;
+    int cur = left ? __builtin_ctzll(left) : -1;
+    if (cur >= 0) {
+      left &= left - 1;
+      tile_load(bits, bv.payload, bv.meta[rl_i64(mine, cur)], ws.lb);
+    }
+    while (cur >= 0) {
+      int nxt = left ? __builtin_ctzll(left) : -1;
+      if (nxt >= 0) {
+        left &= left - 1;
+        tile_load(bits2, bv.payload, bv.meta[rl_i64(mine, nxt)], ws.lb);
+      }
+      count_plane(bits, cur);
+      cur = nxt;
+      if (cur < 0) break;
+      nxt = left ? __builtin_ctzll(left) : -1;
+      if (nxt >= 0) {
+        left &= left - 1;
+        tile_load(bits, bv.payload, bv.meta[rl_i64(mine, nxt)], ws.lb);
+      }
+      count_plane(bits2, cur);
+      cur = nxt;
+    }
+    tsum = wave_sum_i64(acc_sum);
+    tcnt = wave_sum_i64(acc_cnt);
   };
-  Tile bits2;
-  uint64_t left = present;
-  int cur = left ? __builtin_ctzll(left) : -1;
-  if (cur >= 0) {
-    left &= left - 1;
-    tile_load(bits, bv.payload, bv.meta[rl_i64(mine, cur)], ws.lb);
-  }
-  while (cur >= 0) {
-    int nxt = left ? __builtin_ctzll(left) : -1;
-    if (nxt >= 0) {
-      left &= left - 1;
-      tile_load(bits2, bv.payload, bv.meta[rl_i64(mine, nxt)], ws.lb);
-    }
-    count_plane(bits, cur);
-    cur = nxt;
-    if (cur < 0) break;
-    nxt = left ? __builtin_ctzll(left) : -1;
-    if (nxt >= 0) {
-      left &= left - 1;
-      tile_load(bits, bv.payload, bv.meta[rl_i64(mine, nxt)], ws.lb);
-    }
-    count_plane(bits2, cur);
-    cur = nxt;
-  }
-  const int64_t tsum = wave_sum_i64(acc_sum);
-  const int64_t tcnt = wave_sum_i64(acc_cnt);
+  if (live) work();
+  __shared__ long long red_s[WAVES_PER_BLOCK], red_c[WAVES_PER_BLOCK];
+  __shared__ int red_q[WAVES_PER_BLOCK];
   if (lane == 0) {
-    if (tsum) atomicAdd(out_sum + q, (unsigned long long)tsum);
-    if (tcnt) atomicAdd(out_cnt + q, (unsigned long long)tcnt);
+    red_s[wave] = tsum;
+    red_c[wave] = tcnt;
+    red_q[wave] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < WAVES_PER_BLOCK; w++) {
+      const int qw = red_q[w];
+      if (qw < 0) continue;
+      long long ss = red_s[w], cc = red_c[w];
+      for (int w2 = w + 1; w2 < WAVES_PER_BLOCK; w2++)
+        if (red_q[w2] == qw) {
+          ss += red_s[w2];
+          cc += red_c[w2];
+          red_q[w2] = -1;
+        }
+      if (ss) atomicAdd(out_sum + qw, (unsigned long long)ss);
+      if (cc) atomicAdd(out_cnt + qw, (unsigned long long)cc);
+    }
   }
 }
 

@@ -112,7 +112,8 @@ struct TopNLaunch {
   const uint32_t* hist_in;        // mode 3: histograms kept by mode 1
   int R;                          // hot ranks [0, R) counted by mode 4; slot index / histogram cover [R, K)
   const int32_t* hot_meta;        // [S][16][R] key-j container of each hot row (meta index in shard), -1
-  const int32_t* hot_split;       // [S][16] ranks before it hold the big (cooperative) containers
+  const int32_t* hot_split;       // [S][16][2] ranks before [0] hold containers over the lane-owned bound,
+                                  // before [1] the cooperative ones (bitmaps, runs, arrays > HOT_MID_N)
   uint32_t* hot_cnt;              // [S][Q][R] src counts of the hot ranks (mode 4 writes, 1-3 read)
   int32_t* tail_built;            // [Q*S] mode 1: 1 = unit's tail histogram built (kept), 0 = skipped
   const int32_t* cache_dense;     // [S][K] dense row of each cache slot (mode 3 exact probes)
@@ -121,8 +122,8 @@ struct TopNLaunch {
   int tbuild_min;                 // mode 4: bitmap srcs of >= this many bits build the table by transpose
   int dbg;                        // PILOSA_TOPN_DBG cost isolation: 1 skip histogram, 2 skip walk, 8 skip small hot rows,
                                   // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays, 128 byte-counter
-                                  // (swar) hot counting, 256 no lane-owned atomics, 512 table skips bitmap srcs, 1024
-                                  // bitmap srcs by LDS atomics (not the transposed build)
+                                  // (swar) hot counting, 256 no lane-owned / mid atomics, 512 table skips bitmap srcs, 1024
+                                  // bitmap srcs by LDS atomics (not the transposed build), 2048 skip mid-size rows
                                   // (answers then wrong, except 128 and 1024)
 };
 // LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).

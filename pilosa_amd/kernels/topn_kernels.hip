@@ -33,6 +33,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace pk {
@@ -525,6 +527,10 @@ constexpr int HOT_TAB_WORDS = 32768;
 // lane turns into per-query totals every 240 values, so bigger rows lane-owned
 // skip the wave-cooperative path's per-row transpose-reduce.
 constexpr int HOT_SMALL_N = 255;
+// largest array of the quarter-wave (mid) path: a lane of a 16-lane quarter
+// then holds <= 128 of a row's values (7 carry-save planes per packed half
+// for NQ 16, 8 per query for NQ 32); the default bound is HOT_MID_N
+constexpr int HOT_MID_MAX = 2048, HOT_MID_N = 1024;
 
 // SWAR: add the 16 bits of a query mask to 16 byte counters (4 per word):
 // a nibble times 0x00204081 puts its bits at bytes 0..3 without carries.
@@ -654,7 +660,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   uint32_t* out = p.hot_cnt + int64_t(s) * Q * R;
   const bool hs = !(p.dbg & 128);  // 128: byte-counter (swar_add) array counting
   // 1. query-mask table of key j.  One wave per query (wave w takes queries
-  //    w, w + 16): each lane issues 8 independent value loads before its 8
+  //    w, w + 16): each lane issues 16 independent value loads before its 16
   //    LDS ORs, so the table costs a few load round trips instead of one per
   //    (query, 1024 values) -- the CU holds only this workgroup and waits out
   //    every round trip of the build (1.55 ms of a 16-query launch with the
@@ -710,15 +716,16 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     if (n <= 0) continue;
     const auto vals = gp(p.src_vals + p.src_offs[kk]);
     if (n <= ARRAY_MAX) {
-      for (int i0 = 0; i0 < n; i0 += 64 * 8) {
-        int xv[8];
+      // 16 value loads per lane in flight (a 4096-value array in 4 round trips)
+      for (int i0 = 0; i0 < n; i0 += 64 * 16) {
+        int xv[16];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           const int i = i0 + 64 * u + lane;
           xv[u] = i < n ? int(vals[i]) : -1;
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           const int x = xv[u];
           if (x < 0) continue;
           if (HB) {
@@ -747,9 +754,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     return tab16[x];
   };
   const int32_t* hm = p.hot_meta + (int64_t(s) * 16 + j) * R;
-  const int B = min(R, p.hot_split[int64_t(s) * 16 + j]);
+  const int B = min(R, p.hot_split[(int64_t(s) * 16 + j) * 2]);
+  const int B1 = min(B, p.hot_split[(int64_t(s) * 16 + j) * 2 + 1]);
 
-  // 2. big containers, ranks [0, B): wave w takes ranks w + 16 i (sizes fall
+  // 2. big containers, ranks [0, B1): wave w takes ranks w + 16 i (sizes fall
   //    with rank, so every wave gets a similar mix).  Per group of 64 of its
   //    ranks, lane l loads rank l's container index and meta word (2 vector
   //    loads per 64 rows); then rows stream as 512-value chunks (8 rounds of
@@ -757,9 +765,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //    row's first chunk -- in flight while the current one is counted.  Byte
   //    counters per lane, a 17-shuffle transpose-reduce per row, totals in
   //    lanes (l >> 2) & 15.
-  for (int gb = wave; gb < ((p.dbg & 16) ? 0 : B); gb += 64 * (HOT_THREADS / 64)) {
+  for (int gb = wave; gb < ((p.dbg & 16) ? 0 : B1); gb += 64 * (HOT_THREADS / 64)) {
     const int kl = gb + (HOT_THREADS / 64) * lane;
-    const int cl = kl < B ? hm[kl] : -1;
+    const int cl = kl < B1 ? hm[kl] : -1;
     const int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
     uint64_t live = __ballot(cl >= 0);
     if (!live) continue;
@@ -922,8 +930,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         }
       }
       if (row_end) {
-        flush();
+        // an array row counted carry-save left the byte counters at zero
         if (hs && ty == CT_ARRAY) hs_counts<NQ, COOP_P>(pl, acc);
+        else flush();
         // transpose-reduce: NQ counters x 64 lanes -> one total per 64/NQ
         // lanes: each level halves the counters a lane holds and sums the
         // exchanged half with lane ^ step (query bit = lane bit)
@@ -990,6 +999,82 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       if (!step(b0, v0, b2, v2)) break;
       if (!step(b1, v1, b0, v0)) break;
       if (!step(b2, v2, b1, v1)) break;
+    }
+  }
+
+
+  // 2b. mid-size arrays (lane-owned bound < n <= PILOSA_TOPN_MID_N), ranks [B1, B):
+  //     a 16-lane quarter wave per row, 4 rows per wave (wave w takes the
+  //     rank quads B1 + 4 (w + 16 i)).  Lane l of a quarter counts values
+  //     8l..8l+7 of every 128-value round (one 16-byte load, the next round's
+  //     in flight) into carry-save planes; at the row's end the planes become
+  //     counts and a 4-level transpose-reduce over the quarter leaves query l
+  //     (NQ 16; 2l and 2l + 1 for NQ 32) in lane l.  The cooperative path
+  //     spends a 6-level reduction of every row over the whole wave, which
+  //     rows of a few hundred values cannot amortise.
+  if (!(p.dbg & 2048)) {
+    constexpr int MW = NQ == 16 ? 4 : 8, MID_P = NQ == 16 ? 7 : 8;
+    const int sl = lane & 15;
+    for (int g4 = B1 + 4 * wave; g4 < B; g4 += 4 * (HOT_THREADS / 64)) {
+      const int k = g4 + (lane >> 4);
+      const int c = k < B ? hm[k] : -1;
+      const int64_t m = c >= 0 ? p.v.meta[sb + c] : 0;
+      const int n = c >= 0 ? meta_n(m) : 0;  // arrays only in this rank range
+      const uint4* pp = reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8);
+      const int lastc = max(n - 1, 0) >> 3;
+      uint32_t mpl[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) mpl[t] = 0u;
+      auto count8 = [&](const uint4& x, const int i0) {
+        const int nv = n - i0;  // values of this lane's chunk in the row (<= 0: none)
+        const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+        uint32_t mk[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
+        uint32_t hw[MW];
+        if (__ballot(nv < 8) == 0) {
+#pragma unroll
+          for (int w = 0; w < MW; w++) hw[w] = NQ == 16 ? mk[2 * w] | (mk[2 * w + 1] << 16) : mk[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < MW; w++)
+            hw[w] = NQ == 16 ? (2 * w < nv ? mk[2 * w] : 0u) | (2 * w + 1 < nv ? mk[2 * w + 1] << 16 : 0u)
+                             : (w < nv ? mk[w] : 0u);
+        }
+        hs_add<MW, MID_P>(mpl, hw);
+      };
+      uint4 x0 = pp[min(sl, lastc)], x1;
+      for (int r = 0;;) {
+        if (!__ballot(128 * r < n)) break;
+        x1 = pp[min(16 * (r + 1) + sl, lastc)];
+        count8(x0, 128 * r + 8 * sl);
+        r++;
+        if (!__ballot(128 * r < n)) break;
+        x0 = pp[min(16 * (r + 1) + sl, lastc)];
+        count8(x1, 128 * r + 8 * sl);
+        r++;
+      }
+      uint32_t a[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; q++) a[q] = 0u;
+      hs_counts<NQ, MID_P>(mpl, a);
+      // level st: lanes with bit st keep the upper half of the counters and
+      // add their partner's copy of it (the query index takes the lane bit)
+#pragma unroll
+      for (int st = 8, sz = NQ; st >= 1; st >>= 1, sz >>= 1) {
+        const bool hb = lane & st;
+#pragma unroll
+        for (int i = 0; i < NQ / 2; i++) {
+          if (i >= sz / 2) break;
+          const uint32_t mine = hb ? a[sz / 2 + i] : a[i], other = hb ? a[i] : a[sz / 2 + i];
+          a[i] = mine + uint32_t(__shfl_xor(int(other), st, 64));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < NQ / 16; e++) {
+        const int q = NQ == 16 ? sl : 2 * sl + e;
+        if (q < Q && a[e] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + k, a[e]);
+      }
     }
   }
 
@@ -1119,7 +1204,7 @@ template <int SMALLN>
 __global__ __launch_bounds__(256) void topn_hot_meta_kernel(ViewDev v, int S, int K, int R,
                                                             const int32_t* __restrict__ cache_dense,
                                                             int32_t* __restrict__ hot_meta,
-                                                            int32_t* __restrict__ hot_split) {
+                                                            int32_t* __restrict__ hot_split, int midn) {
   const int64_t total = int64_t(S) * R;
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
        e += int64_t(gridDim.x) * blockDim.x) {
@@ -1132,7 +1217,11 @@ __global__ __launch_bounds__(256) void topn_hot_meta_kernel(ViewDev v, int S, in
       const int64_t m = v.meta[sb + c];
       hot_meta[(int64_t(s) * 16 + meta_j(m)) * R + k] = int32_t(c);
       // ranks before the split take the cooperative path (see topn_hot_kernel)
-      if (meta_type(m) != CT_ARRAY || meta_n(m) > SMALLN) atomicMax(hot_split + int64_t(s) * 16 + meta_j(m), k + 1);
+      int32_t* hs = hot_split + (int64_t(s) * 16 + meta_j(m)) * 2;
+      if (meta_type(m) != CT_ARRAY || meta_n(m) > SMALLN) atomicMax(hs, k + 1);
+      // ranks before hs[1] take the wave-cooperative path; [hs[1], hs[0]) the
+      // quarter-wave path of mid-size arrays
+      if (meta_type(m) != CT_ARRAY || meta_n(m) > midn) atomicMax(hs + 1, k + 1);
     }
   }
 }
@@ -1226,11 +1315,22 @@ static int hot_small_n() {
   return n;
 }
 
+// mid-size arrays (lane-owned bound < n <= this) are counted by 16-lane
+// quarter waves, 4 rows per wave (PILOSA_TOPN_MID_N; 0 = none: the
+// cooperative path takes them)
+static int hot_mid_n() {
+  static const int n = [] {
+    const char* e = getenv("PILOSA_TOPN_MID_N");
+    return e ? std::max(0, std::min(atoi(e), HOT_MID_MAX)) : HOT_MID_N;
+  }();
+  return n;
+}
+
 template <int SMALLN>
 static void launch_hot_meta_t(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                               int32_t* hot_split, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(topn_hot_meta_kernel<SMALLN>, dim3(blocks), dim3(256), 0, st, v, S, K, R, cache_dense, hot_meta,
-                     hot_split);
+                     hot_split, std::max(hot_mid_n(), SMALLN));
 }
 
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,

@@ -203,7 +203,8 @@ class DeviceTopNIndex:
             return torch.empty(0, dtype=dt, device=dev)
 
         self.hot_meta = torch.full((Sd * 16 * R,), -1, dtype=torch.int32, device=dev)
-        self.hot_split = torch.zeros(Sd * 16, dtype=torch.int32, device=dev)
+        # per (sub-shard, key): [0] ranks before it are cooperative or mid-size, [1] cooperative
+        self.hot_split = torch.zeros(Sd * 16 * 2, dtype=torch.int32, device=dev)
         if Sd and R:
             ext.topn_hot_meta(self._vd, Sd, K, R, dense_sub, self.hot_meta, self.hot_split)
         colcnt = torch.zeros(Sd * SHARD_WIDTH, dtype=torch.int32, device=dev)
@@ -303,10 +304,10 @@ class DeviceTopNIndex:
             self.colptr.index_copy_(0, Cd, cp_sub)
             if R:
                 hm_sub = torch.full((nd * 16 * R,), -1, dtype=torch.int32, device=dev)
-                hs_sub = torch.zeros(nd * 16, dtype=torch.int32, device=dev)
+                hs_sub = torch.zeros(nd * 16 * 2, dtype=torch.int32, device=dev)
                 ext.topn_hot_meta(vd_sub, nd, K, R, cd_sub, hm_sub, hs_sub)
                 self.hot_meta.view(Sd, 16 * R).index_copy_(0, Cd, hm_sub.view(nd, 16 * R))
-                self.hot_split.view(Sd, 16).index_copy_(0, Cd, hs_sub.view(nd, 16))
+                self.hot_split.view(Sd, 32).index_copy_(0, Cd, hs_sub.view(nd, 32))
         # the rank caches of every shard (counts of unchanged shards may move
         # too), their acc indexes, the slot map rows and the counter tiers
         self.cache_dense = new_dense

@@ -4,11 +4,12 @@ a plain PyTorch fp32 reference on the headline's container mix.
 A Zipf arena with the bench's density profile (bits_per_col 8, s 1.6, v 50)
 puts bitmap containers at the top ranks, 1k-4k-value arrays after them and
 short arrays in the tail, so one launch runs the wave-cooperative path
-(bitmaps, big arrays) and the lane-owned path (short arrays) of the kernel,
-with carry-save or byte counters (PILOSA_TOPN_DBG bit 128), at every
-lane-owned bound (PILOSA_TOPN_SMALL_N).  The reference builds each shard's
-hot rows and src rows as dense 0/1 fp32 matrices per 2^16-column key and
-multiplies them (exact: counts < 2^24).
+(bitmaps, big arrays), the quarter-wave path (mid-size arrays) and the
+lane-owned path (short arrays) of the kernel, with carry-save or byte
+counters (PILOSA_TOPN_DBG bit 128), at every lane-owned and mid-size bound
+(PILOSA_TOPN_SMALL_N / PILOSA_TOPN_MID_N).  The reference builds each
+shard's hot rows and src rows as dense 0/1 fp32 matrices per 2^16-column key
+and multiplies them (exact: counts < 2^24).
 """
 import os
 import subprocess
@@ -122,8 +123,12 @@ def test_hot_counts_equal_dense_reference(nq, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("env", [{"PILOSA_TOPN_SMALL_N": "1023"}, {"PILOSA_TOPN_SMALL_N": "4096"},
-                                 {"PILOSA_TOPN_DBG": "128"}, {"PILOSA_TOPN_DBG": "128", "PILOSA_TOPN_SMALL_N": "1023"}],
-                         ids=["small1023", "small4096", "bytecounters", "bytecounters1023"])
+                                 {"PILOSA_TOPN_MID_N": "0"}, {"PILOSA_TOPN_MID_N": "512"},
+                                 {"PILOSA_TOPN_MID_N": "2048"},
+                                 {"PILOSA_TOPN_DBG": "128"}, {"PILOSA_TOPN_DBG": "128", "PILOSA_TOPN_SMALL_N": "1023"},
+                                 {"PILOSA_TOPN_DBG": "1024"}],
+                         ids=["small1023", "small4096", "nomid", "mid512", "mid2048", "bytecounters", "bytecounters1023",
+                              "atomicbuild"])
 def test_hot_counts_equal_dense_reference_at_every_bound(env):
     """The same check with other lane-owned bounds and with the byte-counter
     (swar) counting: both settings are fixed per process."""
