@@ -1161,8 +1161,10 @@ __global__ __launch_bounds__(256, 2) void bsi_range_kernel(const ViewDev* __rest
   const int wave = threadIdx.x >> 6;
   const int lane = wave_lane();
   const int64_t item = int64_t(blk) * WAVES_PER_BLOCK + wave;
-  if (item >= int64_t(S) * 16) return;
-  const int s = int(item >> 4), j = int(item & 15);
+  const bool live = item < int64_t(S) * 16;
+  if (!live && !out_count) return;  // (the count path's block barrier needs every wave)
+  const int64_t it = live ? item : 0;
+  const int s = int(it >> 4), j = int(it & 15);
   const ViewDev& bv = views[bsi.view];
   BsiCtx c{bsi, bv, s, j, bv.shard_base[s], bv.rowptr + int64_t(s) * (bv.D + 1), scratch[wave].lb};
   plane_index(c);
@@ -1238,7 +1240,16 @@ __global__ __launch_bounds__(256, 2) void bsi_range_kernel(const ViewDev* __rest
   }
   const int64_t n = wave_sum_i64(tile_popc(res));
   if (out_count) {  // Count(Row(v <op> x)): no predicate view is written
-    if (lane == 0 && n) atomicAdd(out_count, (unsigned long long)n);
+    // the block's waves fold into one atomic: every wave of the launch
+    // adding to the same word serialises at one L2 channel
+    // (through each wave's own scratch word 0, free by now: no extra LDS)
+    if (lane == 0) scratch[wave].lb[0] = live ? uint64_t(n) : 0ull;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long t = 0;
+      for (int w = 0; w < WAVES_PER_BLOCK; w++) t += scratch[w].lb[0];
+      if (t) atomicAdd(out_count, t);
+    }
     return;
   }
   ulong2* dst = reinterpret_cast<ulong2*>(out_payload + item * 4096);

@@ -121,10 +121,10 @@ struct TopNLaunch {
                                   // entbase, slots, hot_meta/split are per sub-shard; mode 4 runs with S*M, M=1)
   int tbuild_min;                 // mode 4: bitmap srcs of >= this many bits build the table by transpose
   int dbg;                        // PILOSA_TOPN_DBG cost isolation: 1 skip histogram, 2 skip walk, 8 skip small hot rows,
-                                  // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays, 128 byte-counter
-                                  // (swar) hot counting, 256 no lane-owned / mid atomics, 512 table skips bitmap srcs, 1024
+                                  // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays,
+                                  // 256 no lane-owned / mid atomics, 512 table skips bitmap srcs, 1024
                                   // bitmap srcs by LDS atomics (not the transposed build), 2048 skip mid-size rows
-                                  // (answers then wrong, except 128 and 1024)
+                                  // (answers then wrong, except 1024)
 };
 // LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).
 int topn_lds_bytes(int K, int H32, int H16);

@@ -523,22 +523,14 @@ __global__ __launch_bounds__(256) void topn_gather_kernel(TopNLaunch p) {
 constexpr int HOT_THREADS = 1024;
 constexpr int HOT_TAB_WORDS = 32768;
 // Lane-owned (small) containers: at most SMALLN values (PILOSA_TOPN_SMALL_N
-// = 255, 1023 or 4096 = every array).  Counts are carry-save planes that a
+// = 63, 255, 1023 or 4096 = every array).  Counts are carry-save planes that a
 // lane turns into per-query totals every 240 values, so bigger rows lane-owned
 // skip the wave-cooperative path's per-row transpose-reduce.
 constexpr int HOT_SMALL_N = 255;
 // largest array of the quarter-wave (mid) path: a lane of a 16-lane quarter
 // then holds <= 128 of a row's values (7 carry-save planes per packed half
 // for NQ 16, 8 per query for NQ 32); the default bound is HOT_MID_N
-constexpr int HOT_MID_MAX = 2048, HOT_MID_N = 1024;
-
-// SWAR: add the 16 bits of a query mask to 16 byte counters (4 per word):
-// a nibble times 0x00204081 puts its bits at bytes 0..3 without carries.
-template <int NQ>
-__device__ __forceinline__ void swar_add(uint32_t (&c4)[NQ / 4], uint32_t msk) {
-#pragma unroll
-  for (int g = 0; g < NQ / 4; g++) c4[g] += (((msk >> (4 * g)) & 15u) * 0x00204081u) & 0x01010101u;
-}
+constexpr int HOT_MID_MAX = 2048, HOT_MID_N = 2048;
 
 // Bit-sliced (carry-save) counting.  A "word" is a query mask: for NQ = 16
 // the masks of two values packed as lo | hi << 16 (bit q and bit 16 + q both
@@ -546,8 +538,9 @@ __device__ __forceinline__ void swar_add(uint32_t (&c4)[NQ / 4], uint32_t msk) {
 // per-bit counters; adding W words is a Harley-Seal tree of carry-save
 // adders (3 ops each: xor3, xor, bfi) whose last carry ripples up to plane
 // MAXP - 1 (2 ops a plane).  That is ~2.5 ops per value against the 12-14 of
-// spreading every mask into byte counters (swar_add); the planes are turned
-// into counts once per row (hs_counts).
+// spreading every mask into byte counters (a nibble times 0x00204081, the
+// round-4 kernel: profiles/r05_hotcsa/); the planes are turned into counts
+// once per row (hs_counts).
 __device__ __forceinline__ void csa(uint32_t& s, uint32_t& c, uint32_t a, uint32_t b) {
   // s + a + b = (s ^ a ^ b) + 2 * maj(s, a, b)
   const uint32_t u = s ^ a;
@@ -658,7 +651,6 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   const int Q = p.Q, R = p.R;
   const int64_t sb = p.v.shard_base[s];
   uint32_t* out = p.hot_cnt + int64_t(s) * Q * R;
-  const bool hs = !(p.dbg & 128);  // 128: byte-counter (swar_add) array counting
   // 1. query-mask table of key j.  One wave per query (wave w takes queries
   //    w, w + 16): each lane issues 16 independent value loads before its 16
   //    LDS ORs, so the table costs a few load round trips instead of one per
@@ -822,24 +814,16 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     adv();
     load_chunk(lr >= 0 && meta_type(lm) == CT_ARRAY ? lm : 0, lbase, b1, v1);
     adv();
-    uint32_t c4[NQ / 4];
-#pragma unroll
-    for (int g = 0; g < NQ / 4; g++) c4[g] = 0u;
     uint32_t acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; q++) acc[q] = 0;
-    // array rows: carry-save planes (a lane sees <= 64 values of a row:
-    // 6 planes hold 32 per packed half, 7 hold 64)
+    // carry-save planes: an array row gives a lane <= 64 values (6 planes
+    // hold 32 per packed half, 7 hold 64); bitmap rows use all 8 (<= 192
+    // bits between counts), runs too (<= 240 values)
     constexpr int HW = NQ == 16 ? 4 : 8, COOP_P = NQ == 16 ? 6 : 7;
     uint32_t pl[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) pl[k] = 0;
-    auto flush = [&]() {
-#pragma unroll
-      for (int q = 0; q < NQ; q++) acc[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
-#pragma unroll
-      for (int g = 0; g < NQ / 4; g++) c4[g] = 0;
-    };
     // one (row, chunk) step: count `cur`, load two steps ahead into `ldb`;
     // false once the wave's last row is done
     auto step = [&](const uint4& cur, const int curv, uint4& ldb, int& ldv) -> bool {
@@ -865,33 +849,25 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         uint32_t mk[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
-        if (hs) {
-          // carry-save planes, counted once at the row's end
-          uint32_t hw[HW];
-          if (__ballot(curv < 8) == 0) {
+        // carry-save planes, counted once at the row's end; when every
+        // lane holds 8 values (the inner chunks of a big array, which carry
+        // most of the values) no per-value pad select
+        uint32_t hw[HW];
+        if (__ballot(curv < 8) == 0) {
 #pragma unroll
-            for (int k = 0; k < HW; k++) hw[k] = NQ == 16 ? mk[2 * k] | (mk[2 * k + 1] << 16) : mk[k];
-          } else {
-#pragma unroll
-            for (int k = 0; k < HW; k++)
-              hw[k] = NQ == 16 ? (2 * k < curv ? mk[2 * k] : 0u) | (2 * k + 1 < curv ? mk[2 * k + 1] << 16 : 0u)
-                               : (k < curv ? mk[k] : 0u);
-          }
-          hs_add<HW, COOP_P>(pl, hw);
-        } else if (__ballot(curv < 8) == 0) {
-          // every lane holds 8 values (the inner chunks of a big array, which
-          // carry most of the values): no per-value pad select
-#pragma unroll
-          for (int t = 0; t < 8; t++) swar_add<NQ>(c4, mk[t]);
+          for (int k = 0; k < HW; k++) hw[k] = NQ == 16 ? mk[2 * k] | (mk[2 * k + 1] << 16) : mk[k];
         } else {
 #pragma unroll
-          for (int t = 0; t < 8; t++) swar_add<NQ>(c4, t < curv ? mk[t] : 0u);
+          for (int k = 0; k < HW; k++)
+            hw[k] = NQ == 16 ? (2 * k < curv ? mk[2 * k] : 0u) | (2 * k + 1 < curv ? mk[2 * k + 1] << 16 : 0u)
+                             : (k < curv ? mk[k] : 0u);
         }
+        hs_add<HW, COOP_P>(pl, hw);
       } else if (ty == CT_BITMAP && !(p.dbg & 32)) {
-        // all 16 words of the lane issued before the first is counted; set
+        // the lane's words load a quarter at a time (register budget); set
         // bits are taken four at a time (four table reads in flight)
         constexpr int NIT = NLO / 4096;  // 64-word rounds of the workgroup's values
-        constexpr int HALF = NIT / 2;     // words loaded per batch (register budget)
+        constexpr int HALF = NIT / 4;     // words loaded per batch
         const uint64_t* w = reinterpret_cast<const uint64_t*>(pp) + (lo >> 6);
         uint64_t wv[HALF];
 #pragma unroll
@@ -909,10 +885,14 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
               mk[k] = v ? mask_of(i * 64 + __builtin_ctzll(bb)) : 0u;
               bb &= bb - 1;
             }
-#pragma unroll
-            for (int k = 0; k < 4; k++) swar_add<NQ>(c4, mk[k]);
+            if (NQ == 16) {
+              const uint32_t hw[2] = {mk[0] | (mk[1] << 16), mk[2] | (mk[3] << 16)};
+              hs_add<2, 8>(pl, hw);
+            } else {
+              hs_add<4, 8>(pl, mk);
+            }
           }
-          if (it % 3 == 2) flush();  // <= 192 bits per lane between flushes
+          if (it % 3 == 2) hs_counts<NQ, 8>(pl, acc);  // <= 192 bits per lane between counts
         }
       } else if (ty == CT_RUN) {
         const int nr = pp[0];
@@ -920,19 +900,19 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         int since = 0;
         for (int t = 0; t < nr; t++) {
           const int a0 = max(int(rr[2 * t]), lo), b0_ = min(int(rr[2 * t + 1]), lo + NLO - 1);
+          // one value at a time (runs are rare among hot rows): a half-adder
+          // ripple; a lane counts its planes every 240 values
           for (int xx = a0 + lane; xx <= b0_; xx += 64) {
-            swar_add<NQ>(c4, mask_of(xx));
+            hs_ripple<0, 8>(pl, mask_of(xx));
             if (++since == 240) {
-              flush();
+              hs_counts<NQ, 8>(pl, acc);
               since = 0;
             }
           }
         }
       }
       if (row_end) {
-        // an array row counted carry-save left the byte counters at zero
-        if (hs && ty == CT_ARRAY) hs_counts<NQ, COOP_P>(pl, acc);
-        else flush();
+        hs_counts<NQ, 8>(pl, acc);
         // transpose-reduce: NQ counters x 64 lanes -> one total per 64/NQ
         // lanes: each level halves the counters a lane holds and sums the
         // exchanged half with lane ^ step (query bit = lane bit)
@@ -1113,12 +1093,6 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
       const int gnn = claim();
       const int clnn = rank_meta(gnn);
-      uint32_t c4[NQ / 4];
-#pragma unroll
-      for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
-      uint32_t big[SMALLN > 255 ? NQ : 1];
-#pragma unroll
-      for (int q = 0; q < (SMALLN > 255 ? NQ : 1); q++) big[q] = 0u;
       uint32_t lpl[8], lcnt[NQ];
 #pragma unroll
       for (int k = 0; k < 8; k++) lpl[k] = 0u;
@@ -1132,35 +1106,23 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         uint32_t mk[16];
 #pragma unroll
         for (int t = 0; t < 16; t++) mk[t] = mask_of(int((wd[t >> 1] >> ((t & 1) << 4)) & 0xffffu));
-        if (hs) {
-          // carry-save planes (<= 240 values per lane between counts: 8
-          // planes hold them), counted at the row's end
-          constexpr int LW = NQ == 16 ? 8 : 16;
-          uint32_t hw[LW];
-          if (__ballot(i + 16 > nl) == 0) {
+        // carry-save planes (<= 240 values per lane between counts: 8
+        // planes hold them), counted at the row's end
+        constexpr int LW = NQ == 16 ? 8 : 16;
+        uint32_t hw[LW];
+        if (__ballot(i + 16 > nl) == 0) {
 #pragma unroll
-            for (int k = 0; k < LW; k++) hw[k] = NQ == 16 ? mk[2 * k] | (mk[2 * k + 1] << 16) : mk[k];
-          } else {
+          for (int k = 0; k < LW; k++) hw[k] = NQ == 16 ? mk[2 * k] | (mk[2 * k + 1] << 16) : mk[k];
+        } else {
 #pragma unroll
-            for (int k = 0; k < LW; k++)
-              hw[k] = NQ == 16 ? (i + 2 * k < nl ? mk[2 * k] : 0u) | (i + 2 * k + 1 < nl ? mk[2 * k + 1] << 16 : 0u)
-                               : (i + k < nl ? mk[k] : 0u);
-          }
-          hs_add<LW, 8>(lpl, hw);
-          if (SMALLN > 255 && ++since == 15) {
-            since = 0;
-            hs_counts<NQ, 8>(lpl, lcnt);
-          }
-          return;
+          for (int k = 0; k < LW; k++)
+            hw[k] = NQ == 16 ? (i + 2 * k < nl ? mk[2 * k] : 0u) | (i + 2 * k + 1 < nl ? mk[2 * k + 1] << 16 : 0u)
+                             : (i + k < nl ? mk[k] : 0u);
         }
-#pragma unroll
-        for (int t = 0; t < 16; t++) swar_add<NQ>(c4, i + t < nl ? mk[t] : 0u);
-        if (SMALLN > 255 && ++since == 15) {   // wave-uniform: <= 240 values per byte counter
+        hs_add<LW, 8>(lpl, hw);
+        if (SMALLN > 255 && ++since == 15) {  // wave-uniform
           since = 0;
-#pragma unroll
-          for (int q = 0; q < (SMALLN > 255 ? NQ : 1); q++) big[q] += (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
-#pragma unroll
-          for (int g2 = 0; g2 < NQ / 4; g2++) c4[g2] = 0u;
+          hs_counts<NQ, 8>(lpl, lcnt);
         }
       };
       uint4 n0, n1;
@@ -1176,19 +1138,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         body(n0, n1, i);
         i += 16;
       }
-      if (hs) {
-        hs_counts<NQ, 8>(lpl, lcnt);
+      hs_counts<NQ, 8>(lpl, lcnt);
 #pragma unroll
-        for (int q = 0; q < NQ; q++)
-          if (q < Q && lcnt[q] && (!(p.dbg & 256) || lcnt[q] == 0x7fffffffu)) atomicAdd(out + int64_t(q) * R + kl, lcnt[q]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          uint32_t c = (c4[q >> 2] >> ((q & 3) << 3)) & 255u;
-          if (SMALLN > 255) c += big[SMALLN > 255 ? q : 0];
-          if (q < Q && c) atomicAdd(out + int64_t(q) * R + kl, c);
-        }
-      }
+      for (int q = 0; q < NQ; q++)
+        if (q < Q && lcnt[q] && (!(p.dbg & 256) || lcnt[q] == 0x7fffffffu)) atomicAdd(out + int64_t(q) * R + kl, lcnt[q]);
       g = gn;
       cl = cln;
       ml = mln;
@@ -1303,14 +1256,14 @@ void launch_leaf_src(const ViewDev& v, const int64_t* rows, int Q, int S, int32_
                      offs, has_run);
 }
 
-// lane-owned container bound of the hot-rank kernels (255, 1023 or 4096 =
-// every array), fixed per process: the split the meta kernel records must
+// lane-owned container bound of the hot-rank kernels (63, 255, 1023 or 4096
+// = every array), fixed per process: the split the meta kernel records must
 // match the counting kernel's
 static int hot_small_n() {
   static const int n = [] {
     const char* e = getenv("PILOSA_TOPN_SMALL_N");
     const int v = e ? atoi(e) : 0;
-    return v > 1023 ? 4096 : v > 255 ? 1023 : 255;
+    return v > 1023 ? 4096 : v > 255 ? 1023 : (v > 0 && v < 255) ? 63 : 255;
   }();
   return n;
 }
@@ -1341,6 +1294,7 @@ void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* 
   const int blocks = int(want < 65536 ? want : 65536);
   switch (hot_small_n()) {
     case 4096: launch_hot_meta_t<4096>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st); break;
+    case 63: launch_hot_meta_t<63>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st); break;
     case 1023: launch_hot_meta_t<1023>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st); break;
     default: launch_hot_meta_t<255>(v, S, K, R, cache_dense, hot_meta, hot_split, blocks, st);
   }
@@ -1397,6 +1351,7 @@ void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
     const bool q32 = a.Q > 16;
     switch (hot_small_n()) {
       case 4096: q32 ? launch_hot_t<32, 4096>(a, st) : launch_hot_t<16, 4096>(a, st); break;
+      case 63: q32 ? launch_hot_t<32, 63>(a, st) : launch_hot_t<16, 63>(a, st); break;
       case 1023: q32 ? launch_hot_t<32, 1023>(a, st) : launch_hot_t<16, 1023>(a, st); break;
       default: q32 ? launch_hot_t<32, 255>(a, st) : launch_hot_t<16, 255>(a, st);
     }

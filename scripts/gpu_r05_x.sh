@@ -8,7 +8,7 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_hot_counts.py -x -v --timeo
 tail -1 $O/pytest_hot.log
 timeout -k 10 900 python -u -m pytest tests/test_gpu_executor.py -x -q --timeout 300 --timeout-method thread -k "bsi or Sum or sum" > $O/pytest_bsi.log 2>&1 || { tail -c 5000 $O/pytest_bsi.log; exit 1; }
 tail -1 $O/pytest_bsi.log
-for cfg in "mid1024:" "mid2048:PILOSA_TOPN_MID_N=2048" "mid1536:PILOSA_TOPN_MID_N=1536"; do
+for cfg in "base:" "mid2048:PILOSA_TOPN_MID_N=2048" "small63:PILOSA_TOPN_SMALL_N=63" "hot4096:PILOSA_TOPN_HOT=4096" "hot2048:PILOSA_TOPN_HOT=2048"; do
   name=${cfg%%:*}; ev=${cfg#*:}
   timeout -k 10 300 env $ev python3 -u scripts/topn_kbench.py --reps 3 > $O/kb_$name.log 2>&1 || { tail -c 2000 $O/kb_$name.log; exit 1; }
   echo "$name: $(python3 -c "import json;d=json.loads(open('$O/kb_$name.log').read().strip().splitlines()[-1]);print([c['hot_ms'] for c in d['classes'].values()], d.get('mix',{}).get('e2e_ms_per_batch'), d.get('mix',{}).get('parts_ms',{}).get('hot'))")"

@@ -5,9 +5,9 @@ A Zipf arena with the bench's density profile (bits_per_col 8, s 1.6, v 50)
 puts bitmap containers at the top ranks, 1k-4k-value arrays after them and
 short arrays in the tail, so one launch runs the wave-cooperative path
 (bitmaps, big arrays), the quarter-wave path (mid-size arrays) and the
-lane-owned path (short arrays) of the kernel, with carry-save or byte
-counters (PILOSA_TOPN_DBG bit 128), at every lane-owned and mid-size bound
-(PILOSA_TOPN_SMALL_N / PILOSA_TOPN_MID_N).  The reference builds each
+lane-owned path (short arrays) of the kernel, at every lane-owned and
+mid-size bound (PILOSA_TOPN_SMALL_N / PILOSA_TOPN_MID_N) and with either
+table build (PILOSA_TOPN_DBG bit 1024).  The reference builds each
 shard's hot rows and src rows as dense 0/1 fp32 matrices per 2^16-column key
 and multiplies them (exact: counts < 2^24).
 """
@@ -122,16 +122,15 @@ def test_hot_counts_equal_dense_reference(nq, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env", [{"PILOSA_TOPN_SMALL_N": "1023"}, {"PILOSA_TOPN_SMALL_N": "4096"},
+@pytest.mark.parametrize("env", [{"PILOSA_TOPN_SMALL_N": "63"}, {"PILOSA_TOPN_SMALL_N": "1023"},
+                                 {"PILOSA_TOPN_SMALL_N": "4096"},
                                  {"PILOSA_TOPN_MID_N": "0"}, {"PILOSA_TOPN_MID_N": "512"},
                                  {"PILOSA_TOPN_MID_N": "2048"},
-                                 {"PILOSA_TOPN_DBG": "128"}, {"PILOSA_TOPN_DBG": "128", "PILOSA_TOPN_SMALL_N": "1023"},
                                  {"PILOSA_TOPN_DBG": "1024"}],
-                         ids=["small1023", "small4096", "nomid", "mid512", "mid2048", "bytecounters", "bytecounters1023",
-                              "atomicbuild"])
+                         ids=["small63", "small1023", "small4096", "nomid", "mid512", "mid2048", "atomicbuild"])
 def test_hot_counts_equal_dense_reference_at_every_bound(env):
-    """The same check with other lane-owned bounds and with the byte-counter
-    (swar) counting: both settings are fixed per process."""
+    """The same check with other lane-owned and mid-size bounds and the
+    atomic table build: each setting is fixed per process."""
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
                         "--timeout", "300", "--timeout-method", "thread",
                         "tests/test_gpu_hot_counts.py::test_hot_counts_equal_dense_reference"],

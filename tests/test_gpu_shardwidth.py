@@ -50,7 +50,7 @@ def test_gpu_executor_suite_at_wide_width():
 @pytest.mark.timeout(600)
 def test_gpu_topn_suites_with_wide_lane_owned_rows():
     """The hot-rank TopN kernel with lane-owned containers up to 1023 values
-    (PILOSA_TOPN_SMALL_N=1023: byte counters flushed every 240 values) answers
+    (PILOSA_TOPN_SMALL_N=1023: carry-save planes counted every 240 values) answers
     the slot-index and executor TopN suites exactly."""
     env = dict(os.environ, PILOSA_TOPN_SMALL_N="1023")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
