@@ -1373,6 +1373,47 @@ __global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int
   // for Min, -value for Max (smaller key wins; ties: lower fragment)
   int64_t bkey = BIG, bval = 0, bcnt = 0;
   int bfrag = 0x7fffffff;
+  if (GT == 16) {
+    // 16 lanes per fragment, lane g on key g: its 10 words are 5 coalesced
+    // 16-byte loads (a thread per fragment striding 80 bytes per key touched
+    // 64 cache lines per load instruction: 47 us per call), two fragments
+    // per group in flight; the group's extreme and count by shuffles
+    const int g = tid & 15;
+    auto fold = [&](const longlong2 w0, const longlong2 w1, const longlong2 w2, const longlong2 w3,
+                    const longlong2 w4, const int f) {
+      const bool live = f < F;
+      const bool anyp = (uint64_t(__ballot(live && w4.x > 0)) >> (lane & 48)) & 0xFFFFu;
+      const bool anyn = (uint64_t(__ballot(live && w4.y > 0)) >> (lane & 48)) & 0xFFFFu;
+      if (!anyp && !anyn) return;  // group-uniform
+      const bool use_neg = is_min ? anyn : !anyp;
+      const int vc = is_min ? (anyn ? 0 : 2) : (anyp ? 4 : 6);
+      const bool largest = vc == 0 || vc == 4;
+      const bool valid = (use_neg ? w4.y : w4.x) > 0;
+      const longlong2 xc = vc == 0 ? w0 : vc == 2 ? w1 : vc == 4 ? w2 : w3;  // (value, count)
+      int64_t best = valid ? int64_t(xc.x) : (largest ? int64_t(-1) : BIG);
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) {
+        const int64_t b2 = __shfl_xor(best, off, 64);
+        best = largest ? (b2 > best ? b2 : best) : (b2 < best ? b2 : best);
+      }
+      int64_t cnt = valid && int64_t(xc.x) == best ? int64_t(xc.y) : 0;
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+      const int64_t val = use_neg ? -best : best;
+      const int64_t key = is_min ? val : -val;
+      if (g == 0 && (key < bkey || (key == bkey && f < bfrag))) { bkey = key; bval = val; bcnt = cnt; bfrag = f; }
+    };
+    const int grp = tid >> 4;  // 64 groups
+    for (int f0 = grp; f0 < F; f0 += 2 * (FOLD_THREADS / 16)) {
+      const int f1 = f0 + FOLD_THREADS / 16;
+      const longlong2* e0 = reinterpret_cast<const longlong2*>(o + (int64_t(f0) * 16 + g) * 10);
+      const longlong2* e1 = reinterpret_cast<const longlong2*>(o + (int64_t(f1 < F ? f1 : f0) * 16 + g) * 10);
+      const longlong2 a0 = e0[0], a1 = e0[1], a2 = e0[2], a3 = e0[3], a4 = e0[4];
+      const longlong2 b0 = e1[0], b1 = e1[1], b2 = e1[2], b3 = e1[3], b4 = e1[4];
+      fold(a0, a1, a2, a3, a4, f0);
+      fold(b0, b1, b2, b3, b4, f1);
+    }
+  } else
   for (int f = tid; f < F; f += FOLD_THREADS) {
     const int64_t* e = o + int64_t(f) * G * 10;
     bool anyp = false, anyn = false;

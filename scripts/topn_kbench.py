@@ -45,8 +45,10 @@ def main():
            # (each counted for all its queries; PMC instructions / this = per value)
            "hot_values_per_launch": int(np.asarray(cache.counts)[:, :idx.R].astype(np.int64).sum())}
     B = args.batch
+    from bench import zipf_rows
+    mix_rows = [int(r) for r in zipf_rows(np.random.default_rng(7), B, 1000)]
     for name, rows in ((f"hot 0-{B - 1}", range(0, B)), (f"warm 100-{99 + B}", range(100, 100 + B)),
-                       ("cold 900-915", range(900, 900 + B))):
+                       ("cold 900-915", range(900, 900 + B)), ("mix", mix_rows)):
         srcs = [Leaf(view, r) for r in list(rows)[:B]]
         src = eng.materialize_batch(srcs, idx.S)
         hot = idx.hot_counts(src, B)
@@ -69,7 +71,6 @@ def main():
     if not int(os.environ.get("PILOSA_TOPN_DBG", "0")):
         # the bench mix (src rows Zipf over the 1000 hottest): end to end and
         # a synchronised breakdown of one batch
-        from bench import zipf_rows
         from pilosa_amd.ops.topn_index import finish_batch_dev
         rng = np.random.default_rng(99)
         batches = [[Leaf(view, int(r)) for r in zipf_rows(rng, B, 1000)] for _ in range(args.reps + 1)]
