@@ -1006,6 +1006,19 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     int cq = quad_c(B1 + 4 * wave);
     int64_t mq = cq >= 0 ? p.v.meta[sb + cq] : 0;
     int cq1 = quad_c(B1 + 4 * wave + QSTEP);
+    // a quad's totals are added after the next quad's first round is counted
+    // (see the lane-owned path: atomics ahead of loads delay them)
+    uint32_t mpend[NQ / 16];
+    int mpk = -1;  // rank of the pending totals' quarter (-1 = none; wave-uniform validity)
+    auto mflush = [&]() {
+      if (mpk < 0) return;
+#pragma unroll
+      for (int e = 0; e < NQ / 16; e++) {
+        const int q = NQ == 16 ? sl : 2 * sl + e;
+        if (q < Q && mpend[e] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + mpk, mpend[e]);
+      }
+      mpk = -1;
+    };
     for (int g4 = B1 + 4 * wave; g4 < B; g4 += QSTEP) {
       const int k = g4 + (lane >> 4);
       const int64_t m = mq;
@@ -1041,6 +1054,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         if (!__ballot(128 * r < n)) break;
         x1 = pp[min(16 * (r + 1) + sl, lastc)];
         count8(x0, 128 * r + 8 * sl);
+        mflush();
         r++;
         if (!__ballot(128 * r < n)) break;
         x0 = pp[min(16 * (r + 1) + sl, lastc)];
@@ -1063,12 +1077,12 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
           a[i] = mine + uint32_t(__shfl_xor(int(other), st, 64));
         }
       }
+      mflush();  // (a quad without values)
 #pragma unroll
-      for (int e = 0; e < NQ / 16; e++) {
-        const int q = NQ == 16 ? sl : 2 * sl + e;
-        if (q < Q && a[e] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + k, a[e]);
-      }
+      for (int e = 0; e < NQ / 16; e++) mpend[e] = a[e];
+      mpk = k;
     }
+    mflush();
   }
 
 
@@ -1095,6 +1109,19 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
     int gn = claim();
     int cln = rank_meta(gn);
+    // a group's counts are added one group later, after the next group's
+    // first loads have been consumed: vmcnt counts atomics with loads, so
+    // atomics issued just before a group's loads made those loads wait out
+    // the atomics' round trip too
+    uint32_t pend[NQ];
+    int pk = -1;  // rank of the pending counts (wave-uniform: -1 = none)
+    auto flush_pend = [&]() {
+      if (pk < 0) return;
+#pragma unroll
+      for (int q = 0; q < NQ; q++)
+        if (q < Q && pend[q] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + pk + lane, pend[q]);
+      pk = -1;
+    };
     while (B + 64 * g < R) {
       const int kl = B + 64 * g + lane;
       const int nl = cl >= 0 ? meta_n(ml) : 0;
@@ -1148,6 +1175,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         n0 = pp[min((i >> 3) + 2, lastc)];
         n1 = pp[min((i >> 3) + 3, lastc)];
         body(w0, w1, i);
+        flush_pend();
         i += 16;
         if (!__ballot(i < nl)) break;
         w0 = pp[min((i >> 3) + 2, lastc)];
@@ -1156,15 +1184,17 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
         i += 16;
       }
       hs_counts<NQ, 8>(lpl, lcnt);
+      flush_pend();  // (a group without values)
 #pragma unroll
-      for (int q = 0; q < NQ; q++)
-        if (q < Q && lcnt[q] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + kl, lcnt[q]);
+      for (int q = 0; q < NQ; q++) pend[q] = lcnt[q];
+      pk = B + 64 * g;
       g = gn;
       cl = cln;
       ml = mln;
       gn = gnn;
       cln = clnn;
     }
+    flush_pend();
   }
 }
 
