@@ -124,7 +124,7 @@ struct TopNLaunch {
                                   // 16 skip big hot rows, 32 skip their bitmaps, 64 skip their arrays,
                                   // 256 no lane-owned / mid atomics, 512 table skips bitmap srcs, 1024
                                   // bitmap srcs by LDS atomics (not the transposed build), 2048 skip mid-size rows, 4096
-                                  // lane-owned rows load but do not count
+                                  // lane-owned rows load but do not count, 8192 phase 1 adds nothing to acc
                                   // (answers then wrong, except 1024)
 };
 // LDS bytes of the (query, shard) slot histogram (u32 / u16 / u8 tiers).

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
       int tot;
       const int rank = block_rank(ok, bs, tot);
       const bool take = ok && (nmax == 0 || found + rank < nmax);
-      if (take) atomicAdd(acc + ca[k], int32_t(cv));
+      if (take && !(p.dbg & 8192)) atomicAdd(acc + ca[k], int32_t(cv));
       uint32_t tmin;
       int pmax;
       block_minmax(take ? cv : 0xffffffffu, take ? k : -1, bs, tmin, pmax);
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
         const int k = base + tid;
         if (k < K && uint32_t(cc[k]) >= T) {
           const uint32_t cv = slot_count(p, hist, L, q, s, k);
-          if (cv >= T) atomicAdd(acc + ca[k], int32_t(cv));
+          if (cv >= T && !(p.dbg & 8192)) atomicAdd(acc + ca[k], int32_t(cv));
         }
         if (uint32_t(cc[min(base + TN_THREADS, K) - 1]) < T) break;
       }
@@ -653,9 +653,10 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   uint32_t* out = p.hot_cnt + int64_t(s) * Q * R;
   // 1. query-mask table of key j: bitmap srcs as a transpose of their bits
   //    (every table word written once), then array srcs OR'd in with LDS
-  //    atomics, every thread taking one value of every query (loads of all
-  //    queries in flight together) -- the CU holds only this workgroup and
-  //    waits out every round trip of the build (profiles/r05_hotcsa/).
+  //    atomics, one wave per query (wave w takes queries w, w + 16), 16
+  //    value loads per lane in flight.  (Spreading every query's values over
+  //    the whole workgroup instead measured slower: mix 7.6 vs 6.9 ms,
+  //    profiles/r05_hotcsa/.)
   const int wave = tid >> 6;
   // bit q: src q's key-j container is a bitmap (the same mask in every wave)
   uint32_t bmq;
@@ -701,58 +702,40 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     bmq = 0;
   }
   __syncthreads();
-  // array srcs: the whole workgroup spreads every query's values, thread t
-  // taking value t of each (NQ loads in flight, one round trip for arrays of
-  // <= 1024 values) -- a wave per query waited out up to 4 serial rounds for
-  // the largest array while the other waves idled at the barrier
-  auto or_value = [&](int x, int q) {
-    if (HB) {
-      if (unsigned(x - lo) < unsigned(NLO)) atomicOr(&tab[x - lo], 1u << q);
-    } else {
-      atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
-    }
-  };
-  {
-    int xv[NQ];
-    int more = 0;  // bit q: array src q has values past the first 1024
-#pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      xv[q] = -1;
-      if (q >= Q) continue;
-      const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
-      const int n = p.src_counts[kk];
-      if (n <= 0 || n > ARRAY_MAX) continue;
-      if (n > HOT_THREADS) more |= 1 << q;
-      if (tid < n) xv[q] = int(gp(p.src_vals + p.src_offs[kk])[tid]);
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; q++)
-      if (xv[q] >= 0) or_value(xv[q], q);
-    for (; more; more &= more - 1) {
-      const int q = __builtin_ctz(more);
-      const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
-      const int n = p.src_counts[kk];
-      const auto vals = gp(p.src_vals + p.src_offs[kk]);
-      int yv[3];
-#pragma unroll
-      for (int u = 0; u < 3; u++) {
-        const int i = tid + HOT_THREADS * (u + 1);
-        yv[u] = i < n ? int(vals[i]) : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < 3; u++)
-        if (yv[u] >= 0) or_value(yv[u], q);
-    }
-  }
-  // bitmap srcs left to LDS atomics (PILOSA_TOPN_DBG 1024, or below the
-  // transposed build's density bound): a wave per query
   for (int q = wave; q < Q; q += HOT_THREADS / 64) {
     const int64_t kk = (int64_t(q) * p.S + s) * 16 + j;
     const int n = p.src_counts[kk];
-    if (n <= ARRAY_MAX || ((bmq >> q) & 1u) || (p.dbg & 512)) continue;
-    const auto w = reinterpret_cast<const TN_GLOBAL uint64_t*>(gp(p.src_vals + p.src_offs[kk]));
-    for (int i = lane + (lo >> 6); i < (lo + NLO) >> 6; i += 64)
-      for (uint64_t bb = w[i]; bb; bb &= bb - 1) or_value(i * 64 + __builtin_ctzll(bb), q);
+    if (n <= 0) continue;
+    const auto vals = gp(p.src_vals + p.src_offs[kk]);
+    if (n <= ARRAY_MAX) {
+      // 16 value loads per lane in flight (a 4096-value array in 4 round trips)
+      for (int i0 = 0; i0 < n; i0 += 64 * 16) {
+        int xv[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int i = i0 + 64 * u + lane;
+          xv[u] = i < n ? int(vals[i]) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+          const int x = xv[u];
+          if (x < 0) continue;
+          if (HB) {
+            if (unsigned(x - lo) < unsigned(NLO)) atomicOr(&tab[x - lo], 1u << q);
+          } else {
+            atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+          }
+        }
+      }
+    } else if (!((bmq >> q) & 1u) && !(p.dbg & 512)) {
+      const auto w = reinterpret_cast<const TN_GLOBAL uint64_t*>(vals);
+      for (int i = lane + (lo >> 6); i < (lo + NLO) >> 6; i += 64)
+        for (uint64_t bb = w[i]; bb; bb &= bb - 1) {
+          const int x = i * 64 + __builtin_ctzll(bb);
+          if (HB) atomicOr(&tab[x - lo], 1u << q);
+          else atomicOr(&tab[x >> 1], 1u << (q + ((x & 1) << 4)));
+        }
+    }
   }
   __syncthreads();
   // NQ 16: entry x is the u16 half x of the table (one ds_read_u16, no
