@@ -1104,11 +1104,24 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const int kl = B + 64 * g + lane;
       return kl < R ? hm[kl] : -1;
     };
+    // the rank -> container -> meta -> payload chain runs ahead of the
+    // counting: a group's payload loads with the previous group, the meta
+    // word two groups ahead, the container index three ahead
     int g = claim();
     int cl = rank_meta(g);
     int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
     int gn = claim();
     int cln = rank_meta(gn);
+    int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
+    int gnn = claim();
+    int clnn = rank_meta(gnn);
+    auto payload_of = [&](int64_t m) { return gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8)); };
+    uint4 pw0, pw1;  // the current group's first chunk pair, loaded a group ahead
+    {
+      const auto pp0 = payload_of(ml);
+      pw0 = pp0[0];
+      pw1 = pp0[min(1, max((cl >= 0 ? meta_n(ml) : 0) - 1, 0) >> 3)];
+    }
     // a group's counts are added one group later, after the next group's
     // first loads have been consumed: vmcnt counts atomics with loads, so
     // atomics issued just before a group's loads made those loads wait out
@@ -1125,14 +1138,19 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     while (B + 64 * g < R) {
       const int kl = B + 64 * g + lane;
       const int nl = cl >= 0 ? meta_n(ml) : 0;
-      const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
+      const auto pp = payload_of(ml);
       // every lane loads (clamped to its row's last chunk; values past the
       // row are masked when counted), so no load sits behind a branch
       const int lastc = max(nl - 1, 0) >> 3;
-      uint4 w0 = pp[0], w1 = pp[min(1, lastc)];
-      const int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
-      const int gnn = claim();
-      const int clnn = rank_meta(gnn);
+      uint4 w0 = pw0, w1 = pw1;
+      {
+        const auto ppn = payload_of(mln);
+        pw0 = ppn[0];
+        pw1 = ppn[min(1, max((cln >= 0 ? meta_n(mln) : 0) - 1, 0) >> 3)];
+      }
+      const int64_t mlnn = clnn >= 0 ? p.v.meta[sb + clnn] : 0;
+      const int g3 = claim();
+      const int cl3 = rank_meta(g3);
       uint32_t lpl[8], lcnt[NQ];
 #pragma unroll
       for (int k = 0; k < 8; k++) lpl[k] = 0u;
@@ -1193,6 +1211,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       ml = mln;
       gn = gnn;
       cln = clnn;
+      mln = mlnn;
+      gnn = g3;
+      clnn = cl3;
     }
     flush_pend();
   }
