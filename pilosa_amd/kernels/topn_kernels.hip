@@ -995,9 +995,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   if (!(p.dbg & 2048)) {
     constexpr int MW = NQ == 16 ? 4 : 8, MID_P = NQ == 16 ? 7 : 8;
     const int sl = lane & 15;
-    // the rank -> container -> meta chain runs a quad ahead (the next quad's
-    // meta word and the one after's container index load with this quad's
-    // payload): one exposed round trip per quad instead of three
+    // the rank -> container -> meta -> payload chain runs ahead: a quad's
+    // first chunk loads with the quad before, its meta word two quads
+    // ahead, its container index three ahead
     constexpr int QSTEP = 4 * (HOT_THREADS / 64);
     auto quad_c = [&](int g4) -> int {
       const int kq = g4 + (lane >> 4);
@@ -1006,6 +1006,14 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     int cq = quad_c(B1 + 4 * wave);
     int64_t mq = cq >= 0 ? p.v.meta[sb + cq] : 0;
     int cq1 = quad_c(B1 + 4 * wave + QSTEP);
+    int64_t mq1 = cq1 >= 0 ? p.v.meta[sb + cq1] : 0;
+    int cq2 = quad_c(B1 + 4 * wave + 2 * QSTEP);
+    // a quad's first chunk loads with the quad before it
+    auto first_chunk = [&](int c, int64_t m) -> uint4 {
+      const int nn = c >= 0 ? meta_n(m) : 0;
+      return reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8)[min(sl, max(nn - 1, 0) >> 3)];
+    };
+    uint4 px0 = first_chunk(cq, mq);
     // a quad's totals are added after the next quad's first round is counted
     // (see the lane-owned path: atomics ahead of loads delay them)
     uint32_t mpend[NQ / 16];
@@ -1025,10 +1033,14 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const int n = cq >= 0 ? meta_n(m) : 0;  // arrays only in this rank range
       const uint4* pp = reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8);
       const int lastc = max(n - 1, 0) >> 3;
-      uint4 x0 = pp[min(sl, lastc)], x1;
-      mq = cq1 >= 0 ? p.v.meta[sb + cq1] : 0;
+      uint4 x0 = px0, x1;
+      px0 = first_chunk(cq1, mq1);
+      const int64_t mq2 = cq2 >= 0 ? p.v.meta[sb + cq2] : 0;
       cq = cq1;
-      cq1 = quad_c(g4 + 2 * QSTEP);
+      mq = mq1;
+      cq1 = cq2;
+      mq1 = mq2;
+      cq2 = quad_c(g4 + 3 * QSTEP);
       uint32_t mpl[8];
 #pragma unroll
       for (int t = 0; t < 8; t++) mpl[t] = 0u;
@@ -1104,24 +1116,11 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       const int kl = B + 64 * g + lane;
       return kl < R ? hm[kl] : -1;
     };
-    // the rank -> container -> meta -> payload chain runs ahead of the
-    // counting: a group's payload loads with the previous group, the meta
-    // word two groups ahead, the container index three ahead
     int g = claim();
     int cl = rank_meta(g);
     int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
     int gn = claim();
     int cln = rank_meta(gn);
-    int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
-    int gnn = claim();
-    int clnn = rank_meta(gnn);
-    auto payload_of = [&](int64_t m) { return gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(m) * 8)); };
-    uint4 pw0, pw1;  // the current group's first chunk pair, loaded a group ahead
-    {
-      const auto pp0 = payload_of(ml);
-      pw0 = pp0[0];
-      pw1 = pp0[min(1, max((cl >= 0 ? meta_n(ml) : 0) - 1, 0) >> 3)];
-    }
     // a group's counts are added one group later, after the next group's
     // first loads have been consumed: vmcnt counts atomics with loads, so
     // atomics issued just before a group's loads made those loads wait out
@@ -1138,19 +1137,14 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     while (B + 64 * g < R) {
       const int kl = B + 64 * g + lane;
       const int nl = cl >= 0 ? meta_n(ml) : 0;
-      const auto pp = payload_of(ml);
+      const auto pp = gp(reinterpret_cast<const uint4*>(p.v.payload + meta_off16(ml) * 8));
       // every lane loads (clamped to its row's last chunk; values past the
       // row are masked when counted), so no load sits behind a branch
       const int lastc = max(nl - 1, 0) >> 3;
-      uint4 w0 = pw0, w1 = pw1;
-      {
-        const auto ppn = payload_of(mln);
-        pw0 = ppn[0];
-        pw1 = ppn[min(1, max((cln >= 0 ? meta_n(mln) : 0) - 1, 0) >> 3)];
-      }
-      const int64_t mlnn = clnn >= 0 ? p.v.meta[sb + clnn] : 0;
-      const int g3 = claim();
-      const int cl3 = rank_meta(g3);
+      uint4 w0 = pp[0], w1 = pp[min(1, lastc)];
+      const int64_t mln = cln >= 0 ? p.v.meta[sb + cln] : 0;
+      const int gnn = claim();
+      const int clnn = rank_meta(gnn);
       uint32_t lpl[8], lcnt[NQ];
 #pragma unroll
       for (int k = 0; k < 8; k++) lpl[k] = 0u;
@@ -1211,9 +1205,6 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       ml = mln;
       gn = gnn;
       cln = clnn;
-      mln = mlnn;
-      gnn = g3;
-      clnn = cl3;
     }
     flush_pend();
   }
