@@ -134,8 +134,9 @@ void bsi_minmax_fold(torch::Tensor o, int64_t F, int64_t G, int64_t is_min, torc
               "o must be int64[F*G*10]");
   TORCH_CHECK(F < (int64_t(1) << 31) - 1, "bsi_minmax_fold: fragment count");
   TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.numel() >= 3, "out must be int64[3]");
+  torch::Tensor part = torch::empty({((F + 63) / 64) * 4}, o.options());
   pk::launch_bsi_minmax_fold(o.data_ptr<int64_t>(), int(F), int(G), int(is_min), out.data_ptr<int64_t>(),
-                             cur_stream(o));
+                             part.data_ptr<int64_t>(), cur_stream(o));
   check_launch("bsi_minmax_fold");
 }
 

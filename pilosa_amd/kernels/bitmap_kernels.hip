@@ -1476,6 +1476,107 @@ __global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_kernel(const int
   }
 }
 
+// Multi-block fold (16 keys per fragment): block b takes fragments
+// 64 b .. 64 b + 63, one per 16-lane group (the same per-fragment rules as
+// bsi_minmax_fold_kernel), and writes its winner as part[4 b ..] = {key,
+// value, count, fragment} (key = value for Min, -value for Max; BIG = none).
+__global__ __launch_bounds__(FOLD_THREADS) void bsi_minmax_fold_part_kernel(const int64_t* __restrict__ o, int F,
+                                                                           int is_min, int64_t* __restrict__ part) {
+  __shared__ int64_t sv[FOLD_THREADS / 64];
+  __shared__ int sf[FOLD_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = tid & 15;
+  const int64_t BIG = 0x7fffffffffffffffLL;
+  const int f = int(blockIdx.x) * (FOLD_THREADS / 16) + (tid >> 4);
+  const longlong2* e = reinterpret_cast<const longlong2*>(o + (int64_t(f < F ? f : 0) * 16 + g) * 10);
+  const longlong2 w0 = e[0], w1 = e[1], w2 = e[2], w3 = e[3], w4 = e[4];
+  const bool live = f < F;
+  const bool anyp = (uint64_t(__ballot(live && w4.x > 0)) >> (lane & 48)) & 0xFFFFu;
+  const bool anyn = (uint64_t(__ballot(live && w4.y > 0)) >> (lane & 48)) & 0xFFFFu;
+  int64_t key = BIG, val = 0, cnt = 0;
+  if (anyp || anyn) {  // group-uniform
+    const bool use_neg = is_min ? anyn : !anyp;
+    const int vc = is_min ? (anyn ? 0 : 2) : (anyp ? 4 : 6);
+    const bool largest = vc == 0 || vc == 4;
+    const bool valid = (use_neg ? w4.y : w4.x) > 0;
+    const longlong2 xc = vc == 0 ? w0 : vc == 2 ? w1 : vc == 4 ? w2 : w3;
+    int64_t best = valid ? int64_t(xc.x) : (largest ? int64_t(-1) : BIG);
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      const int64_t b2 = __shfl_xor(best, off, 64);
+      best = largest ? (b2 > best ? b2 : best) : (b2 < best ? b2 : best);
+    }
+    int64_t c = valid && int64_t(xc.x) == best ? int64_t(xc.y) : 0;
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    val = use_neg ? -best : best;
+    key = is_min ? val : -val;
+    cnt = c;
+  }
+  // block argmin of (key, fragment) over the groups' lane 0
+  int64_t k = g == 0 ? key : BIG;
+  int fr = g == 0 && key != BIG ? f : 0x7fffffff;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t k2 = __shfl_xor(k, off, 64);
+    const int f2 = __shfl_xor(fr, off, 64);
+    if (k2 < k || (k2 == k && f2 < fr)) { k = k2; fr = f2; }
+  }
+  if (lane == 0) { sv[wave] = k; sf[wave] = fr; }
+  __syncthreads();
+  if (wave == 0) {
+    k = lane < FOLD_THREADS / 64 ? sv[lane] : BIG;
+    fr = lane < FOLD_THREADS / 64 ? sf[lane] : 0x7fffffff;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t k2 = __shfl_xor(k, off, 64);
+      const int f2 = __shfl_xor(fr, off, 64);
+      if (k2 < k || (k2 == k && f2 < fr)) { k = k2; fr = f2; }
+    }
+    if (lane == 0) { sv[0] = k; sf[0] = fr; }
+  }
+  __syncthreads();
+  int64_t* pb = part + int64_t(blockIdx.x) * 4;
+  if (sf[0] == 0x7fffffff) {
+    if (tid == 0) { pb[0] = BIG; pb[1] = 0; pb[2] = 0; pb[3] = 0x7fffffff; }
+  } else if (g == 0 && f == sf[0] && key == sv[0]) {
+    pb[0] = key; pb[1] = val; pb[2] = cnt; pb[3] = f;
+  }
+}
+
+// The blocks' winners -> out = {value, count, found}: smallest key, ties to
+// the lower fragment (the first shard holding the extreme).
+__global__ __launch_bounds__(256) void bsi_minmax_fold_final_kernel(const int64_t* __restrict__ part, int nb,
+                                                                   int64_t* __restrict__ out) {
+  __shared__ int64_t sk[4], sv[4], sc[4];
+  __shared__ int sfr[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t BIG = 0x7fffffffffffffffLL;
+  int64_t k = BIG, v = 0, c = 0;
+  int fr = 0x7fffffff;
+  for (int b = tid; b < nb; b += 256) {
+    const int64_t k2 = part[int64_t(b) * 4], f2 = part[int64_t(b) * 4 + 3];
+    if (k2 < k || (k2 == k && int(f2) < fr)) {
+      k = k2; fr = int(f2); v = part[int64_t(b) * 4 + 1]; c = part[int64_t(b) * 4 + 2];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t k2 = __shfl_xor(k, off, 64), v2 = __shfl_xor(v, off, 64), c2 = __shfl_xor(c, off, 64);
+    const int f2 = __shfl_xor(fr, off, 64);
+    if (k2 < k || (k2 == k && f2 < fr)) { k = k2; fr = f2; v = v2; c = c2; }
+  }
+  if (lane == 0) { sk[wave] = k; sv[wave] = v; sc[wave] = c; sfr[wave] = fr; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; w++)
+      if (sk[w] < k || (sk[w] == k && sfr[w] < fr)) { k = sk[w]; fr = sfr[w]; v = sv[w]; c = sc[w]; }
+    const bool found = fr != 0x7fffffff;
+    out[0] = found ? v : 0;
+    out[1] = found ? c : 0;
+    out[2] = found ? 1 : 0;
+  }
+}
+
 }  // namespace pk
 
 // ------------------------------------------------------------ launchers
@@ -1550,11 +1651,19 @@ void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiA
     hipLaunchKernelGGL((bsi_minmax_kernel<0, 2>), grid, block, 0, st, progs, views, S, bsi, out);
 }
 
-void launch_bsi_minmax_fold(const int64_t* o, int F, int G, int is_min, int64_t* out, hipStream_t st) {
-  if (G == 16)
+void launch_bsi_minmax_fold(const int64_t* o, int F, int G, int is_min, int64_t* out, int64_t* part,
+                            hipStream_t st) {
+  if (G == 16 && part && F > FOLD_THREADS / 16) {
+    // one fragment per 16-lane group over ceil(F / 64) blocks, then the
+    // blocks' winners (one load round trip each instead of ~8 in one block)
+    const int nb = (F + FOLD_THREADS / 16 - 1) / (FOLD_THREADS / 16);
+    hipLaunchKernelGGL(bsi_minmax_fold_part_kernel, dim3(nb), dim3(FOLD_THREADS), 0, st, o, F, is_min, part);
+    hipLaunchKernelGGL(bsi_minmax_fold_final_kernel, dim3(1), dim3(256), 0, st, part, nb, out);
+  } else if (G == 16) {
     hipLaunchKernelGGL(bsi_minmax_fold_kernel<16>, dim3(1), dim3(FOLD_THREADS), 0, st, o, F, G, is_min, out);
-  else
+  } else {
     hipLaunchKernelGGL(bsi_minmax_fold_kernel<0>, dim3(1), dim3(FOLD_THREADS), 0, st, o, F, G, is_min, out);
+  }
 }
 
 void launch_bsi_sum(const QueryProg* progs, int Q, const ViewDev* views, int S, BsiArgs bsi,

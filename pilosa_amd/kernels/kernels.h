@@ -72,7 +72,9 @@ void launch_bsi_range(const ViewDev* views, int S, BsiArgs bsi, int op, int64_t 
                       int64_t* out_meta, unsigned long long* out_count, hipStream_t st);
 // BSI min/max descents per (shard, key): out int64[S*16*10] (see bitmap_kernels.hip).
 // the [F fragments x G keys x 10] descents -> out int64[3] {value, count, found}
-void launch_bsi_minmax_fold(const int64_t* o, int F, int G, int is_min, int64_t* out, hipStream_t st);
+// part: int64[4 * ceil(F / 64)] scratch of the multi-block fold (G == 16), or nullptr
+void launch_bsi_minmax_fold(const int64_t* o, int F, int G, int is_min, int64_t* out, int64_t* part,
+                            hipStream_t st);
 void launch_bsi_minmax(const QueryProg* progs, const ViewDev* views, int S, BsiArgs bsi, int64_t* out,
                        hipStream_t st, int which = 0);
 // fmode: 0 no filters, 1 flat-fold filter programs, 2 any program.

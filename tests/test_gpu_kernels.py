@@ -321,7 +321,7 @@ def test_differential_fuzz_count_and_materialize(setup):
 
 
 @pytest.mark.parametrize("which", ["min", "max"])
-@pytest.mark.parametrize("F,sub", [(1, 1), (37, 1), (2500, 1), (9, 4)])
+@pytest.mark.parametrize("F,sub", [(1, 1), (37, 1), (65, 1), (2500, 1), (9, 4)])
 def test_bsi_minmax_fold_kernel_matches_host_fold(which, F, sub):
     """bsi_minmax_fold_kernel == the host fold it replaced (per-shard sign
     rules, sub-shard fold, first fragment holding the extreme) on random
