@@ -754,9 +754,9 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //    ranks, lane l loads rank l's container index and meta word (2 vector
   //    loads per 64 rows); then rows stream as 512-value chunks (8 rounds of
   //    64 consecutive values) with the NEXT chunk's loads -- possibly the next
-  //    row's first chunk -- in flight while the current one is counted.  Byte
-  //    counters per lane, a 17-shuffle transpose-reduce per row, totals in
-  //    lanes (l >> 2) & 15.
+  //    row's first chunk -- in flight while the current one is counted.
+  //    Carry-save planes per lane, counted at the row's end, then a
+  //    17-shuffle transpose-reduce per row, totals in lanes (l >> 2) & 15.
   for (int gb = wave; gb < ((p.dbg & 16) ? 0 : B1); gb += 64 * (HOT_THREADS / 64)) {
     const int kl = gb + (HOT_THREADS / 64) * lane;
     const int cl = kl < B1 ? hm[kl] : -1;
@@ -842,7 +842,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       adv();
       const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
       if (ty == CT_ARRAY && !(p.dbg & 64)) {
-        // an array gives a lane at most 64 values: bytes cannot overflow.
+        // an array gives a lane at most 64 values (6-7 carry-save planes).
         // All 8 table reads issue before any is consumed (one LDS wait per
         // chunk); values past the array read entry 0 and count nothing.
         const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
