@@ -184,7 +184,7 @@ def cmd_server(args, stdout, stderr) -> int:
                  probe_interval=cfg.duration("gossip.probe-interval"),
                  probe_timeout=cfg.duration("gossip.probe-timeout"),
                  suspicion_mult=float(cfg.get("gossip.suspicion-mult")),
-                 indirect_checks=int(cfg.get("gossip.nodes")),
+                 gossip_nodes=int(cfg.get("gossip.nodes")),
                  to_the_dead_time=cfg.duration("gossip.to-the-dead-time"),
                  stream_timeout=cfg.duration("gossip.stream-timeout"),
                  gossip_interval=cfg.duration("gossip.push-pull-interval"),

@@ -561,8 +561,10 @@ class Executor:
             res = gpu.topn_plain_batch(index, fname, ns, ths, shards)
         except PilosaError:
             return None
-        except Exception as err:  # noqa: BLE001 - device fault: the general path answers
+        except RuntimeError as err:   # HIP / torch device error: counted, the general path answers
             self._gpu_fault(err)
+            return None
+        except Exception:  # noqa: BLE001 - not a device fault (e.g. an argument the fast path cannot hold)
             return None
         if res is None or len(res) != len(ns):
             return None

@@ -146,32 +146,51 @@ class TranslateFile:
 
     @read_only.setter
     def read_only(self, v: bool):
-        self._read_only = bool(v)
-        if self._s is not None:
-            self._s.read_only = self._read_only
+        with self.mu:
+            self._read_only = bool(v)
+            if self._s is not None:
+                self._s.read_only = self._read_only
+
+    # Every access to the native store holds ``mu``: ``close``/``reopen`` swap
+    # ``_s`` under it, and a reader that fetched ``_s`` before a close would
+    # otherwise call into a closed (or None) store (translate.go:1039-1124
+    # holds the store's RWMutex the same way).
+    def _live(self):
+        s = self._s
+        if s is None:
+            raise RuntimeError("translate store is closed")
+        return s
 
     @property
     def size(self) -> int:
-        return self._s.size() if self._s is not None else 0
+        with self.mu:
+            return self._s.size() if self._s is not None else 0
 
     # ------------------------------------------------------------ replication
     def apply_log(self, data: bytes, persist: bool = True) -> int:
         """Append + index whole log entries (replica tailing); returns the
-        bytes consumed (a torn trailing entry is left for the next read)."""
-        return self._s.apply_log(bytes(data))
+        bytes consumed (a torn trailing entry is left for the next read).
+        A closed store consumes nothing."""
+        data = bytes(data)
+        with self.mu:
+            return self._s.apply_log(data) if self._s is not None else 0
 
     def read_from(self, offset: int) -> bytes:
-        """Log bytes from ``offset`` (served at /internal/translate/data)."""
-        return self._s.read_from(int(offset))
+        """Log bytes from ``offset`` (served at /internal/translate/data);
+        empty while the store is closed (the replica retries)."""
+        with self.mu:
+            return self._s.read_from(int(offset)) if self._s is not None else b""
 
     def entries(self, offset: int = 0) -> List[tuple]:
         """[(type, index, field, ids, keys, encoded_length)] from ``offset``."""
-        return self._s.entries(int(offset))
+        with self.mu:
+            return self._s.entries(int(offset)) if self._s is not None else []
 
     # ------------------------------------------------------------ generic
     def _translate(self, t: int, index: str, field: str, keys: Sequence[str]) -> List[int]:
         keys = [k if isinstance(k, str) else str(k) for k in keys]
-        ids = self._s.translate(t, index, field, keys, not self._read_only)
+        with self.mu:
+            ids = self._live().translate(t, index, field, keys, not self._read_only)
         if self._read_only and 0 in ids:
             if self.forward is None:
                 raise ErrTranslateStoreReadOnly
@@ -180,29 +199,38 @@ class TranslateFile:
             ids = [i or got[k] for k, i in zip(keys, ids)]
         return list(ids)
 
+    def _keys_of(self, t: int, index: str, field: str, ids: Sequence[int]) -> List[str]:
+        ids = [int(i) for i in ids]
+        with self.mu:
+            return self._live().keys_of(t, index, field, ids)
+
+    def _key_id(self, t: int, index: str, field: str, key: str) -> Optional[int]:
+        with self.mu:
+            return self._live().translate(t, index, field, [key], False)[0] or None
+
     # ------------------------------------------------------------ columns
     def translate_columns_to_uint64(self, index: str, keys: Sequence[str]) -> List[int]:
         return self._translate(T_COLUMN, index, "", keys)
 
     def translate_column_to_string(self, index: str, id: int) -> str:
         """The key for ``id``; "" if none (TranslateColumnToString)."""
-        return self._s.keys_of(T_COLUMN, index, "", [int(id)])[0]
+        return self._keys_of(T_COLUMN, index, "", [id])[0]
 
     def translate_columns_to_strings(self, index: str, ids: Sequence[int]) -> List[str]:
-        return self._s.keys_of(T_COLUMN, index, "", [int(i) for i in ids])
+        return self._keys_of(T_COLUMN, index, "", ids)
 
     def column_key_id(self, index: str, key: str) -> Optional[int]:
-        return self._s.translate(T_COLUMN, index, "", [key], False)[0] or None
+        return self._key_id(T_COLUMN, index, "", key)
 
     # ------------------------------------------------------------ rows
     def translate_rows_to_uint64(self, index: str, field: str, keys: Sequence[str]) -> List[int]:
         return self._translate(T_ROW, index, field, keys)
 
     def translate_row_to_string(self, index: str, field: str, id: int) -> str:
-        return self._s.keys_of(T_ROW, index, field, [int(id)])[0]
+        return self._keys_of(T_ROW, index, field, [id])[0]
 
     def translate_rows_to_strings(self, index: str, field: str, ids: Sequence[int]) -> List[str]:
-        return self._s.keys_of(T_ROW, index, field, [int(i) for i in ids])
+        return self._keys_of(T_ROW, index, field, ids)
 
     def row_key_id(self, index: str, field: str, key: str) -> Optional[int]:
-        return self._s.translate(T_ROW, index, field, [key], False)[0] or None
+        return self._key_id(T_ROW, index, field, key)

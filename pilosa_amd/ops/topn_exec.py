@@ -55,6 +55,18 @@ def prefix_bucket(n: int) -> int:
 
 
 # cache-only TopN batches on a side stream (0: the current stream)
+I32_MAX = (1 << 31) - 1
+
+
+def clamp_topn_params(ns: Sequence[int], thresholds: Sequence[int]):
+    """n and threshold as the int32 kernel parameters hold them.  The PQL
+    grammar takes both up to 2^63-1; an n at or above 2^31 keeps every
+    candidate and a threshold there admits no shard count of a 2^20..2^31
+    column shard, so clamping changes no answer (an unclamped
+    value overflowed the parameter array and was counted as a device fault)."""
+    return ([min(int(n), I32_MAX) for n in ns], [min(max(int(t), 0), I32_MAX) for t in thresholds])
+
+
 SIDE_STREAM = os.environ.get("PILOSA_TOPN_SIDE_STREAM", "1") != "0"
 
 
@@ -388,6 +400,7 @@ class DeviceRankCaches:
         Q = len(ns)
         if Q == 0:
             return []
+        ns, thresholds = clamp_topn_params(ns, thresholds)
         # the fused kernels total int32 counts: the node's columns (every device
         # sub-shard of every fragment, 2^20 each) must stay below 2^31
         if comm is None and self.view.D and self.view.S < 2048:
@@ -507,6 +520,7 @@ class DeviceRankCaches:
         import torch
 
         from pilosa_amd.parallel.collectives import Pending
+        ns, thresholds = clamp_topn_params(ns, thresholds)
         Q = len(ns)
         nn = [int(n) for n in ns]
         U = len(cand.space)

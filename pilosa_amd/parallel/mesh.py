@@ -774,6 +774,11 @@ def adopt_holder_dir(holder, data_dir: str) -> int:
                     pv.fragments.pop(shard)
                     f.local_shards.add(int(shard))
                     n += 1
+    if n:
+        # the peer Holder.open bumped the epoch before the move: bump it again
+        # so no available_shards() memo taken meanwhile hides the adopted shards
+        from pilosa_amd.models.fragment import bump_shard_epoch
+        bump_shard_epoch()
     return n
 
 

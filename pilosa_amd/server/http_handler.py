@@ -477,8 +477,10 @@ class Handler:
         except (ValueError, KeyError, TypeError) as e:
             raise HTTPError(400, f"probe request: {e}")
         srv = self.server
-        ok = bool(srv.probe_for_peer(uri, timeout)) if srv is not None else False
-        req.send_json({"ok": ok})
+        ok = srv.probe_for_peer(uri, timeout) if srv is not None else False
+        if ok is None:
+            raise HTTPError(400, "probe request: uri is not a member of this cluster")
+        req.send_json({"ok": bool(ok)})
 
     def post_cluster_message(self, req):
         """Type byte + protobuf body (http/handler.go:1474); a JSON body is

@@ -88,7 +88,8 @@ class Server:
                  lazy_fragments: Optional[bool] = None, native_http: Optional[bool] = None,
                  gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None,
                  advertise: str = "", probe_timeout: float = 0.5, suspicion_mult: float = 4,
-                 indirect_checks: int = 3, to_the_dead_time: float = 30.0, stream_timeout: float = 10.0):
+                 indirect_checks: int = 3, to_the_dead_time: float = 30.0, stream_timeout: float = 10.0,
+                 gossip_nodes: int = 3):
         self.data_dir = data_dir
         # CORS origins ([handler] allowed-origins); none = no CORS headers at all
         self.allowed_origins = list(allowed_origins or [])
@@ -123,6 +124,10 @@ class Server:
         self.probe_timeout = probe_timeout
         self.suspicion_mult = suspicion_mult
         self.indirect_checks = indirect_checks
+        # [gossip] nodes: peers each push-pull round sends this node's state to
+        # (memberlist GossipNodes, gossip/gossip.go:273 -- the fan-out, not the
+        # indirect-probe count, which stays memberlist's fixed 3)
+        self.gossip_nodes = max(1, int(gossip_nodes))
         self.to_the_dead_time = to_the_dead_time
         self.stream_timeout = stream_timeout
         self.failure_detector = None
@@ -641,9 +646,19 @@ class Server:
         with _rq.urlopen(req, timeout=timeout * 2 + 0.5, context=_ssl_ctx(self.probe_client.skip_verify)) as r:
             return bool(_json.loads(r.read() or b"{}").get("ok"))
 
-    def probe_for_peer(self, uri: str, timeout: float) -> bool:
-        """A peer's indirect probe of ``uri`` through this node."""
-        return _probe_version(URI.parse(uri), min(float(timeout), 5.0), self.probe_client.skip_verify)
+    def probe_for_peer(self, uri: str, timeout: float) -> Optional[bool]:
+        """A peer's indirect probe of ``uri`` through this node.  Only a
+        member of this cluster is probed (memberlist's indirect ping targets
+        known members only); None for any other address, so the route cannot
+        be used to reach arbitrary hosts.  The timeout is capped
+        at 2 s."""
+        try:
+            target = URI.parse(uri)
+        except Exception:  # noqa: BLE001 - not an address
+            return None
+        if not any(n.uri == target for n in self.cluster.nodes if n.id != self.node.id):
+            return None
+        return _probe_version(target, max(0.0, min(float(timeout), 2.0)), self.probe_client.skip_verify)
 
     def _report_down(self, nid: str):
         coord = self.cluster.coordinator()
@@ -659,7 +674,7 @@ class Server:
         """Push-pull of NodeStatus between every pair of nodes (the role of
         memberlist's LocalState/MergeRemoteState, gossip/gossip.go:295-443):
         each round this node pushes its schema + available shards to the next
-        peer, and receives every peer's push in turn.  Failure detection is
+        ``gossip_nodes`` peers in turn, and receives every peer's push in turn.  Failure detection is
         the SWIM loop's; a peer DOWN for longer than ``to_the_dead_time``
         stops receiving pushes (memberlist's GossipToTheDeadTime)."""
         while not self._closing.wait(self.gossip_interval):
@@ -668,12 +683,16 @@ class Server:
                      not (n.state == NODE_DOWN and now - self._down_since.get(n.id, now) > self.to_the_dead_time)]
             if not peers:
                 continue
-            n = peers[self._gossip_i % len(peers)]
-            self._gossip_i += 1
-            try:
-                self.stream_client.send_message(n, {"type": "NodeStatus", "status": self._node_status()})
-            except Exception as e:  # noqa: BLE001 - the SWIM loop judges liveness
-                self._gossip_misses[n.id] = self._gossip_misses.get(n.id, 0) + 1
+            status = None
+            for _ in range(min(self.gossip_nodes, len(peers))):
+                n = peers[self._gossip_i % len(peers)]
+                self._gossip_i += 1
+                try:
+                    if status is None:
+                        status = self._node_status()
+                    self.stream_client.send_message(n, {"type": "NodeStatus", "status": status})
+                except Exception as e:  # noqa: BLE001 - the SWIM loop judges liveness
+                    self._gossip_misses[n.id] = self._gossip_misses.get(n.id, 0) + 1
 
     # ------------------------------------------------------------ resize
     def _holder_layout(self) -> Dict[str, Dict[str, List[str]]]:

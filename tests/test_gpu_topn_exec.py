@@ -18,7 +18,9 @@ pytestmark = pytest.mark.gpu
 QUERIES = ["TopN(h, n=10)", "TopN(h, n=100)", "TopN(h)", "TopN(h, n=20, threshold=300)",
            "TopN(h, Row(f=1), n=5)", "TopN(h, Row(f=0), n=50)", "TopN(h, Row(h=3), n=20)",
            "TopN(h, Row(f=2), n=7, threshold=2)", "TopN(h, ids=[1, 5, 7, 2999])",
-           "TopN(h, Row(f=1), ids=[0, 2, 4, 6, 8])", "TopN(h, Intersect(Row(f=0), Row(f=1)), n=10)"]
+           "TopN(h, Row(f=1), ids=[0, 2, 4, 6, 8])", "TopN(h, Intersect(Row(f=0), Row(f=1)), n=10)",
+           # n / threshold beyond int32: clamped, not a device fault
+           "TopN(h, n=3000000000)", "TopN(h, n=3000000000, threshold=5000000000)"]
 
 
 @pytest.fixture(scope="module")
@@ -69,6 +71,7 @@ def test_topn_executor_matches_host_and_stays_cold(lazy_env, q):
     got = ex.execute("i", q).results[0]
     assert gpu.launches > n0, "device path not taken"
     assert _pairs(got) == _pairs(want[q])
+    assert ex.gpu_faults == 0
     frags = holder.view("i", "h", "standard").all_fragments()
     assert frags and all(f.is_cold() for f in frags), "TopN read a fragment on the host"
 

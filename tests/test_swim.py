@@ -150,3 +150,34 @@ def test_paused_node_detected_within_the_gossip_bound():
         for s in (m2, m1, m0):
             if s is not None:
                 s.close()
+
+
+@pytest.mark.timeout(60)
+def test_indirect_probe_route_only_probes_members():
+    """POST /internal/probe reaches cluster members only: any other address
+    is a 400, so the route cannot scan ports or reach arbitrary hosts."""
+    import json
+    import urllib.error
+    import urllib.request
+    m0 = _server("node0")
+    m1 = None
+    try:
+        m1 = _server("node1", m0)
+        assert _wait(lambda: len(m0.cluster.nodes) == 2 and len(m1.cluster.nodes) == 2, 20)
+
+        def probe(uri):
+            req = urllib.request.Request(m0.uri.normalize() + "/internal/probe",
+                                         data=json.dumps({"uri": uri, "timeout": 30}).encode(), method="POST")
+            try:
+                with urllib.request.urlopen(req, timeout=10) as r:
+                    return r.status, json.loads(r.read())
+            except urllib.error.HTTPError as e:
+                return e.code, None
+        assert probe(m1.uri.normalize()) == (200, {"ok": True})
+        assert probe("http://127.0.0.1:1")[0] == 400
+        assert probe("http://10.255.255.1:80")[0] == 400
+        assert probe(m0.uri.normalize())[0] == 400     # not itself either
+    finally:
+        for s in (m1, m0):
+            if s is not None:
+                s.close()

@@ -234,3 +234,45 @@ def test_closed_store_raises_instead_of_reading_unmapped_log(tmp_path):
     s.open()
     assert list(s.keys_of(_translate.T_COLUMN, "i", "", [1, 2])) == ["a", "b"]
     s.close()
+
+
+def test_reopen_races_concurrent_readers(tmp_path):
+    """close/reopen swaps the native store under the lock; readers running
+    concurrently (the /internal/translate/data handler, a replica's tail
+    loop) see a closed store as empty and never a None store."""
+    primary = TranslateFile(str(tmp_path / "p")).open()
+    replica = TranslateFile(str(tmp_path / "r"), read_only=True).open()
+    primary.translate_columns_to_uint64("i", [f"k{j}" for j in range(64)])
+    stop = threading.Event()
+    errors = []
+
+    def reader():
+        try:
+            while not stop.is_set():
+                data = primary.read_from(replica.size)
+                if data:
+                    replica.apply_log(data)
+                primary.entries(0)
+                _ = primary.size
+                replica.read_from(replica.size)
+        except Exception as e:  # pragma: no cover - the failure being tested
+            errors.append(e)
+    ths = [threading.Thread(target=reader, daemon=True) for _ in range(3)]
+    for t in ths:
+        t.start()
+    try:
+        for _ in range(10_000):
+            primary.reopen()
+            replica.reopen()
+    finally:
+        stop.set()
+        for t in ths:
+            t.join(5)
+    assert not errors, errors[:3]
+    assert primary.translate_column_to_string("i", 64) == "k63"
+    closed = TranslateFile(str(tmp_path / "c")).open()
+    closed.close()
+    assert closed.read_from(0) == b"" and closed.apply_log(b"xx") == 0
+    assert closed.entries() == [] and closed.size == 0
+    primary.close()
+    replica.close()
