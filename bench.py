@@ -1451,15 +1451,21 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
     n = 100
     B, nb = args.topn_batch, args.topn_batches
     rng = np.random.default_rng(99)
-    out = {"path": "rank 0 Executor.execute(TopN text) -> ShardMesh OP_TOPN", "n": n, "batch": B,
-           "clients": args.clients}
+    out = {"path": "rank 0 Executor.execute(TopN text) -> ShardMesh OP_TOPN_PLAIN (cache-only) / OP_TOPN (src)",
+           "n": n, "batch": B, "clients": {"cache": args.topn_cache_clients, "src": args.topn_clients}}
 
-    def timed(texts, rec):
+    def timed(texts, rec, warm=1, profile="", nclients=1):
         done = [None] * len(texts)
         t0 = time.perf_counter()
         done[0] = ex.execute("i", texts[0], shards=all_shards).results
         rec["first_request_s"] = round(time.perf_counter() - t0, 2)
-        nxt = [1]
+        # untimed warm requests, as the 1-GPU phases take: the node candidate
+        # spaces of the requests' n buckets are built once
+        for i in range(1, warm):
+            done[i] = ex.execute("i", texts[i], shards=all_shards).results
+        from pilosa_amd.utils import gctune
+        gctune.freeze_long_lived()
+        nxt = [warm]
         lock = threading.Lock()
         err = []
 
@@ -1476,9 +1482,17 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
                     err.append(e)
                     return
         mesh.max_in_flight = 0
-        b0 = mesh.topn_tensor_batches
+        b0 = mesh.topn_tensor_batches + mesh.topn_plain_batches
+        r0 = mesh.topn_plain_refreshes
+        prof = None
+        if profile:
+            from pilosa_amd.utils import pprof
+            prof_out = {}
+            prof = threading.Thread(target=lambda: prof_out.setdefault("p", pprof.cpu_profile(0.3, 500)),
+                                    daemon=True)
+            prof.start()
         t_a = mesh.sync()
-        ts = [threading.Thread(target=client) for _ in range(max(1, args.clients))]
+        ts = [threading.Thread(target=client) for _ in range(max(1, nclients))]
         for t in ts:
             t.start()
         for t in ts:
@@ -1486,28 +1500,40 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
         t_b = mesh.sync()
         if err:
             raise err[0]
+        if prof is not None:
+            prof.join()
+            with open(profile, "w") as fh:
+                fh.write(prof_out.get("p", ""))
         el = max(b - a for a, b in zip(t_a, t_b)) / 1e9
-        rec.update({"qps": round(B * (len(texts) - 1) / el, 2), "ms_per_request": round(el / (len(texts) - 1) * 1000, 2),
-                    "device_batches": mesh.topn_tensor_batches - b0, "max_in_flight": mesh.max_in_flight,
+        nt = len(texts) - warm
+        rec.update({"qps": round(B * nt / el, 2), "ms_per_request": round(el / nt * 1000, 2), "warm_requests": warm,
+                    "device_batches": mesh.topn_tensor_batches + mesh.topn_plain_batches - b0,
+                    "space_refreshes": mesh.topn_plain_refreshes - r0, "max_in_flight": mesh.max_in_flight,
                     "sample_top3": [(p.id, p.count) for p in done[-1][0][:3]] if done[-1] and done[-1][0] else []})
         return done
 
     log("mesh topn: cache-only requests (distinct calls)")
-    cache_calls = _wide_topn_calls(B * (nb + 1), seed=17)
+    # the same request counts and warm-up as the 1-GPU phases (bench_topn)
+    nbc, W = max(nb, args.topn_cache_batches), 8
+    cache_calls = _wide_topn_calls(B * (nbc + W), seed=17)
     out["cache"] = {"calls": f"TopN(f, n=log-uniform 1..1000, threshold one of {len(WIDE_THRESHOLDS)} values "
                              "1..50000), random per call"}
-    timed([" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nb + 1)], out["cache"])
-    cyc = _distinct_topn_calls(B * (nb + 1))
+    timed([" ".join(cache_calls[i * B:(i + 1) * B]) for i in range(nbc + W)], out["cache"], warm=W,
+          profile=os.environ.get("PILOSA_BENCH_TOPN_PROFILE", ""), nclients=args.topn_cache_clients)
+    cyc = _distinct_topn_calls(B * (nbc + W))
     out["cache_cycling"] = {"calls": "TopN(f, n in {10,50,100,500} + offset, threshold in {1,1000,5000,20000})"}
-    timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nb + 1)], out["cache_cycling"])
-    hot = zipf_rows(rng, B * (nb + 1), 1000)
+    timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nbc + W)], out["cache_cycling"], warm=W,
+          nclients=args.topn_cache_clients)
+    WS = 3
+    hot = zipf_rows(rng, B * (nb + WS), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
-    src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + 1)]
+    src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + WS)]
     out["src"] = {}
     log("mesh topn: src requests")
-    res = timed(src_q, out["src"])
+    res = timed(src_q, out["src"], warm=WS, nclients=args.topn_clients)
     if args.verify > 0:
-        calls = [parse_string(c).calls[0] for c in src_calls[nb * B:nb * B + 2]] + [parse_string(f"TopN(f, n={n})").calls[0]]
+        last = (nb + WS - 1) * B
+        calls = [parse_string(c).calls[0] for c in src_calls[last:last + 2]] + [parse_string(f"TopN(f, n={n})").calls[0]]
         fused = [[(p.id, p.count) for p in r] for r in res[-1][:2]] + \
             [[(p.id, p.count) for p in ex.execute("i", f"TopN(f, n={n})", shards=all_shards).results[0]]]
         two_phase = [[(p.id, p.count) for p in ex._topn("i", c, all_shards, ExecOptions())] for c in calls]

@@ -531,13 +531,15 @@ class Executor:
         return self.execute_call(index, c, list(shards) if shards else (idx.available_shards() or [0]), ExecOptions())
 
     def _topn_plain_fast(self, index: str, text: str, shards=None) -> Optional[List[Any]]:
-        """Single-GPU fast path for a request of plain cache-only calls of one
-        field -- TopN(f[, n=][, threshold=]) -- recognised natively
+        """Fast path for a request of plain cache-only calls of one field --
+        TopN(f[, n=][, threshold=]) -- recognised natively
         (native/pql_compile.cpp topn_plain): no Call objects or per-call
-        argument handling, one fused device batch (ops/topn_exec.py).  None =
-        the parse-based paths."""
+        argument handling, one fused device batch (ops/topn_exec.py), or on
+        a multi-GPU node one mesh batch of a single all-reduce
+        (ShardMesh.topn_plain).  None = the parse-based paths."""
         gpu = self.gpu
-        if gpu is None or self._use_mesh(None) or not hasattr(gpu, "topn_plain_batch"):
+        mesh = self.mesh if self._use_mesh(None) else None
+        if mesh is None and (gpu is None or not hasattr(gpu, "topn_plain_batch")):
             return None
         from pilosa_amd import _pql
         got = _pql.topn_plain(text)
@@ -557,6 +559,17 @@ class Executor:
         if self._has_remote(index, shards, ExecOptions()):
             return None
         ths = [t or DEFAULT_MIN_THRESHOLD for t in ths]
+        if mesh is not None:
+            # every rank's GPU, one all-reduce per batch (parallel/mesh.py OP_TOPN_PLAIN)
+            try:
+                res = mesh.topn_plain(index, fname, ns, ths, shards)
+            except MeshError:
+                return None
+            if res is None or len(res) != len(ns):
+                return None
+            if self.stats is not None:
+                self.stats.count_with_tags("TopN", len(res), [f"index:{index}"])
+            return res
         try:
             res = gpu.topn_plain_batch(index, fname, ns, ths, shards)
         except PilosaError:

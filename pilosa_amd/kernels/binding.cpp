@@ -310,44 +310,60 @@ void topn_cache_batch(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch:
   check_launch("topn_cache_batch");
 }
 
-// A mesh rank's cache-only partial: ``buf`` int32[(Q*U + 3) / 4 + T*U] holds
-// the membership bytes (uint8[Q, U], padded to whole words) then the int32
-// partial totals [T, U]; the ranks all-reduce (sum) it as one tensor.
-void topn_cache_partial(torch::Tensor cnt, int64_t nmax, torch::Tensor inv, torch::Tensor cm, torch::Tensor prm,
-                        int64_t Q, int64_t T, int64_t U, torch::Tensor buf) {
-  for (auto* t : {&cnt, &inv, &cm, &prm, &buf}) check_dev(*t, "topn_cache_partial");
-  TORCH_CHECK(cnt.scalar_type() == torch::kInt32 && cnt.dim() == 2, "cnt int32[S, K]");
-  const int64_t S = cnt.size(0), K = cnt.size(1);
-  TORCH_CHECK(nmax >= 0 && nmax <= K, "nmax out of range");
-  TORCH_CHECK(inv.scalar_type() == torch::kInt32 && inv.numel() == S * nmax, "inv int32[S * nmax]");
-  TORCH_CHECK(cm.scalar_type() == torch::kInt32 && cm.numel() == U * S, "cm int32[U, S]");
-  TORCH_CHECK(prm.scalar_type() == torch::kInt32 && prm.numel() == 4 * Q + T, "prm int32[4Q + T]");
+// A mesh rank's cache-only partial: ``buf`` int32[(Q*U + 3) / 4 + T*U + 2] holds
+// the membership bytes (uint8[Q, U], padded to whole words), the int32 partial
+// totals [T, U], then the flag words [stale, declined]; the ranks all-reduce
+// (sum) it as one tensor.  A rank that cannot take part (``stale`` /
+// ``declined``) passes no cache tensors (empty ``cnt``) and sends zeros plus
+// its flags.
+void topn_cache_partial(torch::Tensor cnt, int64_t nmax, int64_t nlim, torch::Tensor inv, torch::Tensor cm,
+                        torch::Tensor prm, int64_t Q, int64_t T, int64_t U, torch::Tensor buf, int64_t stale,
+                        int64_t declined) {
+  check_dev(buf, "topn_cache_partial");
   const int64_t mw = (Q * U + 3) / 4;
-  TORCH_CHECK(buf.scalar_type() == torch::kInt32 && buf.numel() == mw + T * U, "buf int32[member words + T*U]");
+  TORCH_CHECK(buf.scalar_type() == torch::kInt32 && buf.numel() == mw + T * U + 2,
+              "buf int32[member words + T*U + 2]");
   TORCH_CHECK(Q < 65536 && T > 0 && U > 0 && U < (int64_t(1) << 31), "topn_cache_partial sizes");
   int32_t* b = buf.data_ptr<int32_t>();
-  pk::launch_topn_cache_partial(cnt.data_ptr<int32_t>(), int(K), int(S), int(nmax), inv.data_ptr<int32_t>(),
-                                cm.data_ptr<int32_t>(), prm.data_ptr<int32_t>(), int(Q), int(T), int(U),
-                                reinterpret_cast<uint8_t*>(b), b + mw, cur_stream(buf));
+  const bool part = !stale && !declined && cnt.numel() > 0;
+  int64_t S = 0, K = 0;
+  if (part) {
+    for (auto* t : {&cnt, &inv, &cm, &prm}) check_dev(*t, "topn_cache_partial");
+    TORCH_CHECK(cnt.scalar_type() == torch::kInt32 && cnt.dim() == 2, "cnt int32[S, K]");
+    S = cnt.size(0);
+    K = cnt.size(1);
+    TORCH_CHECK(nmax >= 0 && nmax <= K, "nmax out of range");
+    TORCH_CHECK(inv.scalar_type() == torch::kInt32 && inv.numel() == S * nmax, "inv int32[S * nmax]");
+    TORCH_CHECK(cm.scalar_type() == torch::kInt32 && cm.numel() == U * S, "cm int32[U, S]");
+    TORCH_CHECK(prm.scalar_type() == torch::kInt32 && prm.numel() == 4 * Q + T, "prm int32[4Q + T]");
+  }
+  pk::launch_topn_cache_partial(part ? cnt.data_ptr<int32_t>() : nullptr, int(K), int(S), int(nmax), int(nlim),
+                                part ? inv.data_ptr<int32_t>() : nullptr, part ? cm.data_ptr<int32_t>() : nullptr,
+                                part ? prm.data_ptr<int32_t>() : nullptr, int(Q), int(T), int(U),
+                                reinterpret_cast<uint8_t*>(b), b + mw, b + mw + T * U, int(stale), int(declined),
+                                cur_stream(buf));
   check_launch("topn_cache_partial");
 }
 
 // Per-query top-n over the all-reduced partial buffer (member bytes > 0 =
-// a candidate of that query on some rank; node totals int32).
+// a candidate of that query on some rank; node totals int32; out[q, 0] = -3 /
+// -4 when the reduced flags say some rank was stale / declined).
 void topn_cache_select32(torch::Tensor buf, torch::Tensor ids, torch::Tensor prm, int64_t Q, int64_t T,
                          torch::Tensor out) {
   for (auto* t : {&buf, &ids, &prm, &out}) check_dev(*t, "topn_cache_select32");
   const int64_t U = ids.numel();
   const int64_t mw = (Q * U + 3) / 4;
   TORCH_CHECK(ids.scalar_type() == torch::kInt32, "ids int32[U]");
-  TORCH_CHECK(buf.scalar_type() == torch::kInt32 && buf.numel() == mw + T * U, "buf int32[member words + T*U]");
+  TORCH_CHECK(buf.scalar_type() == torch::kInt32 && buf.numel() == mw + T * U + 2,
+              "buf int32[member words + T*U + 2]");
   TORCH_CHECK(prm.scalar_type() == torch::kInt32 && prm.numel() == 4 * Q + T, "prm int32[4Q + T]");
   TORCH_CHECK(out.scalar_type() == torch::kInt64 && out.dim() == 2 && out.size(0) == Q, "out int64[Q, KK+1]");
   TORCH_CHECK(Q < 65536 && U > 0 && U < (int64_t(1) << 31), "topn_cache_select32 sizes");
   const int32_t* b = buf.data_ptr<int32_t>();
   pk::launch_topn_cache_select32(reinterpret_cast<const uint8_t*>(b), b + mw, ids.data_ptr<int32_t>(),
                                  prm.data_ptr<int32_t>(), int(Q), int(U), int(out.size(1) - 1),
-                                 reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream(buf));
+                                 reinterpret_cast<long long*>(out.data_ptr<int64_t>()), b + mw + T * U,
+                                 cur_stream(buf));
   check_launch("topn_cache_select32");
 }
 

@@ -155,11 +155,14 @@ void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, 
 void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
                              const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
                              long long* tot, long long* out, hipStream_t st, int nlim = 0);
-void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* cm,
-                               const int32_t* prm, int Q, int T, int U, uint8_t* member, int32_t* tot,
-                               hipStream_t st);
+// Mesh cache-only TopN: one rank's buffer [member bytes | int32 totals[T, U] | flags[2]] (cleared here;
+// flags = this rank's [stale, declined] vote, which rides in the batch's one all-reduce) and the front
+// end's select over the reduced buffer (out[q, 0] = -3 / -4 when some rank was stale / declined).
+void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, int nlim, const int32_t* inv,
+                               const int32_t* cm, const int32_t* prm, int Q, int T, int U, uint8_t* member,
+                               int32_t* tot, int32_t* flags, int stale, int declined, hipStream_t st);
 void launch_topn_cache_select32(const uint8_t* member, const int32_t* tot, const int32_t* ids, const int32_t* prm,
-                                int Q, int U, int KK, long long* out, hipStream_t st);
+                                int Q, int U, int KK, long long* out, const int32_t* flags, hipStream_t st);
 void launch_topn_hot_meta(const ViewDev& v, int S, int K, int R, const int32_t* cache_dense, int32_t* hot_meta,
                           int32_t* hot_split, hipStream_t st);
 

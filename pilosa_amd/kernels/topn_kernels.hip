@@ -1576,11 +1576,18 @@ __global__ __launch_bounds__(TC_THREADS) void topn_cache_select_kernel(const uin
                                                                 const TT* __restrict__ tot,
                                                                 const int32_t* __restrict__ u,
                                                                 const int32_t* __restrict__ prm, int Q, int U, int KK,
-                                                                long long* __restrict__ out) {
+                                                                long long* __restrict__ out,
+                                                                const int32_t* __restrict__ flags) {
   __shared__ long long keys[TC_CAP];
   __shared__ int nmem;
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
+  if (flags != nullptr && (flags[0] | flags[1])) {
+    // a mesh batch some rank could not take part in (all-reduced flag words:
+    // [stale candidate space, declined]): no answer, the front end re-plans
+    if (tid == 0) out[int64_t(q) * (KK + 1)] = flags[1] ? -4 : -3;
+    return;
+  }
   if (tid == 0) nmem = 0;
   __syncthreads();
   const uint8_t* mq = member + int64_t(q) * U;
@@ -1659,23 +1666,34 @@ void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const i
     hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm,
                        S, U, prm + 4 * Q, T, tot);
   hipLaunchKernelGGL(topn_cache_select_kernel<long long>, dim3(Q), dim3(TC_THREADS), 0, st, member, tot, u, prm, Q, U,
-                     KK, out);
+                     KK, out, (const int32_t*)nullptr);
 }
 
 // A mesh rank's share of a cache-only batch over the NODE candidate space:
 // membership bytes and int32 partial totals, side by side in the buffer the
 // ranks all-reduce (member as bytes: a sum over < 256 ranks cannot carry into
-// the next byte).  The select runs after the all-reduce, on the front end.
-void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* cm,
-                               const int32_t* prm, int Q, int T, int U, uint8_t* member, int32_t* tot,
-                               hipStream_t st) {
-  if (Q <= 0 || U <= 0) return;
-  const int64_t N = int64_t(S) * nmax;
+// the next byte), then the two flag words [stale, declined] this rank votes
+// with -- the readiness vote rides in the data all-reduce, so a batch is ONE
+// collective with no host read before it.  The whole buffer is cleared here.
+// The select runs after the all-reduce, on the front end.
+void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, int nlim, const int32_t* inv,
+                               const int32_t* cm, const int32_t* prm, int Q, int T, int U, uint8_t* member,
+                               int32_t* tot, int32_t* flags, int stale, int declined, hipStream_t st) {
+  const int64_t mw = (int64_t(Q) * U + 3) / 4;
+  (void)hipMemsetAsync(member, 0, size_t(mw + int64_t(T) * U + 2) * 4, st);
+  if (stale) (void)hipMemsetD32Async(flags, stale, 1, st);
+  if (declined) (void)hipMemsetD32Async(flags + 1, declined, 1, st);
+  if (Q <= 0 || U <= 0 || stale || declined || cnt == nullptr) return;
+  if (nlim <= 0 || nlim > nmax) nlim = nmax;
+  const int64_t N = int64_t(S) * nlim;
   if (N > 0) {
     const int64_t want = (N + 255) / 256;
-    const int bx = int(want < 1024 ? want : 1024);
-    hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
-                       member, nmax);
+    if (Q <= 256)
+      hipLaunchKernelGGL(topn_cache_member_q_kernel, dim3(unsigned(want < 8192 ? want : 8192)), dim3(256), 0, st, cnt,
+                         K, S, nmax, inv, prm, Q, U, member, nlim);
+    else
+      hipLaunchKernelGGL(topn_cache_member_kernel, dim3(int(want < 1024 ? want : 1024), Q), dim3(256), 0, st, cnt, K,
+                         S, nmax, inv, prm, Q, U, member, nlim);
   }
   const int64_t waves = int64_t(T) * U;
   if (S > 0 && T <= 16)
@@ -1687,10 +1705,10 @@ void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, const
 }
 
 void launch_topn_cache_select32(const uint8_t* member, const int32_t* tot, const int32_t* ids, const int32_t* prm,
-                                int Q, int U, int KK, long long* out, hipStream_t st) {
+                                int Q, int U, int KK, long long* out, const int32_t* flags, hipStream_t st) {
   if (Q <= 0 || U <= 0) return;
   hipLaunchKernelGGL(topn_cache_select_kernel<int>, dim3(Q), dim3(TC_THREADS), 0, st, member, tot, ids, prm, Q, U, KK,
-                     out);
+                     out, flags);
 }
 
 }  // namespace pk

@@ -190,6 +190,9 @@ class GpuExecutor:
         # (index, field, shards, nreq) -> (rank-cache serial, NodeCandidates or None):
         # node candidate spaces of mesh cache-only batches (refreshed collectively)
         self._cand_spaces: Dict[Tuple, Tuple] = {}
+        # mesh plain cache-only TopN: (index, field, shard-set id, nreq) ->
+        # (generation, rank-cache serial, fits, space, NodeCandidates, ids)
+        self._plain_cands: Dict[Tuple, Tuple] = {}
         self.topn_mesh_fused = 0        # mesh cache-only groups answered in one all-reduce
         self._frag_lists: Dict[Tuple, Tuple] = {}   # (index, field, shards) -> (epoch, fragments)
         self.topn_decline = ""          # why the last topn_batch returned None (diagnostics)
@@ -1082,13 +1085,11 @@ class GpuExecutor:
                 raise NotImplementedError   # src too large for one device program: host path
         return self._topn_pairs_path(rc, rv, src, n, ids, threshold)
 
-    def topn_plain_batch(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: List[int]):
-        """Cache-only TopN(fname, n=ns[i], threshold=ths[i]) calls over the
-        local shards in one fused batch (Executor._topn_plain_fast): the
-        field's view and rank caches are resolved once per mutation epoch."""
-        if self.comm is not None:
-            return None
-        key = (index, fname, tuple(shards))
+    def _plain_rc(self, index: str, fname: str, shards: List[int], key=None):
+        """The field's standard view and rank caches over ``shards``, resolved
+        once per mutation epoch (``key`` names the shard list: the mesh's
+        shard-set id, so a 1k-shard list is not hashed per request)."""
+        key = (index, fname, tuple(shards) if key is None else key)
         epoch = mutation_epoch()
         memo = self.__dict__.setdefault("_plain_memo", {})
         ent = memo.get(key)
@@ -1099,18 +1100,131 @@ class GpuExecutor:
             if len(memo) > 64:
                 memo.clear()
             ent = memo[key] = (epoch, rv, rc)
-        _, rv, rc = ent
+        return ent[1], ent[2]
+
+    def topn_plain_batch(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: List[int]):
+        """Cache-only TopN(fname, n=ns[i], threshold=ths[i]) calls over the
+        local shards in one fused batch (Executor._topn_plain_fast): the
+        field's view and rank caches are resolved once per mutation epoch."""
+        if self.comm is not None:
+            return None
+        rv, rc = self._plain_rc(index, fname, shards)
         if rc is None or not rc.K:
             return [[] for _ in ns]
         self.launches += 1
         with tracing.span("GpuExecutor.topnPlainBatch", gpu=True, calls=len(ns)):
             return rc.topn_nosrc(list(ns), list(ths))
 
-    def topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False):
-        with tracing.span("GpuExecutor.topnBatch", gpu=True, calls=len(calls)):
-            return self._topn_batch(index, calls, shards, defer)
+    # ------------------------------------------------------------ mesh plain cache-only TopN
+    # (parallel/mesh.py OP_TOPN_PLAIN / OP_TOPN_CAND).  A node candidate space
+    # is built collectively (refresh_plain_cand, every rank, one generation
+    # number from the front end); a batch is then ONE all-reduce whose buffer
+    # size comes from the command, and each rank's vote on whether its space
+    # is current rides in that buffer (topn_exec.mesh_cache_batch).
 
-    def _topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False):
+    def plain_cand_state(self, index: str, fname: str, shards: List[int], skey, nreq: int):
+        """Front end, before issuing a batch, no collective: (generation, U,
+        fused-path fits) of the node candidate space when this rank's copy is
+        current, None when it must be refreshed first."""
+        ent = self._plain_cands.get((index, fname, skey, nreq))
+        if ent is None:
+            return None
+        try:
+            rc = self._plain_rc(index, fname, shards, skey)[1] if shards else None
+        except Exception:  # noqa: BLE001 - the refresh reports it node-wide
+            return None
+        if ent[1] != (rc.serial if rc is not None else None):
+            return None
+        return ent[0], len(ent[3]), ent[2]
+
+    def refresh_plain_cand(self, index: str, fname: str, shards: List[int], skey, nreq: int, gen: int, comm):
+        """Collective on every rank: all-gather each rank's local candidate
+        rows of the (field, nreq) group, with its fragment and device-shard
+        counts, and keep the node candidate space, this rank's tensors over
+        it and whether the fused path fits on every rank (int32 node totals,
+        the count-matrix cap) -- a node-wide decision.  Every rank takes part
+        in the gather whatever fails locally."""
+        import torch
+
+        from .topn_exec import FUSED_MAX_CELLS
+        rc = None
+        rows = np.zeros(0, np.uint64)
+        ok = True
+        try:
+            if shards:
+                rc = self._plain_rc(index, fname, shards, skey)[1]
+            if rc is not None:
+                rows = rc.local_candidate_rows(nreq)
+        except Exception:  # noqa: BLE001 - take part with nothing; the fit check fails below
+            rc, ok = None, False
+        head = np.array([rc.S if rc is not None else (0 if ok else -1),
+                         rc.view.S if rc is not None else 0], np.int64)
+        t = torch.from_numpy(np.concatenate([head, rows.view(np.int64)])).to(comm.device)
+        parts = [p.cpu().numpy() for p in comm.all_gather_var(t)]
+        space = np.unique(np.concatenate([p[2:].view(np.uint64) for p in parts])) if parts else rows
+        s_frag = [int(p[0]) for p in parts]
+        fits = bool(parts) and min(s_frag) >= 0 and len(space) * max(s_frag + [1]) <= FUSED_MAX_CELLS and \
+            sum(int(p[1]) for p in parts) < 2048 and len(space) > 0
+        cand = None
+        if fits and rc is not None:
+            try:
+                cand = rc.node_candidates(nreq, space)
+            except Exception:  # noqa: BLE001 - this rank then votes stale on every batch
+                cand = None
+        ids = torch.arange(len(space), dtype=torch.int32, device=comm.device) if fits else None
+        if len(self._plain_cands) > 256:
+            self._plain_cands.clear()
+        self._plain_cands[(index, fname, skey, nreq)] = (int(gen), rc.serial if rc is not None else None, fits,
+                                                         space, cand, ids)
+
+    def topn_plain_mesh(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: List[int],
+                        skey, nreq: int, gen: int, U: int, comm, defer: bool = True):
+        """This rank's share of a mesh cache-only batch (every rank, the
+        front end included): its partial over the node candidate space of
+        generation ``gen`` (size ``U``, from the command) plus its vote, and
+        the started all-reduce (topn_exec.mesh_cache_batch).  Never raises
+        before the collective: a failure is a declined vote."""
+        from .topn_exec import mesh_cache_batch
+        rc = None
+        ent = self._plain_cands.get((index, fname, skey, nreq))
+        stale = declined = 0
+        try:
+            if shards:
+                rc = self._plain_rc(index, fname, shards, skey)[1]
+            if ent is None or ent[0] != int(gen) or ent[1] != (rc.serial if rc is not None else None) or \
+                    len(ent[3]) != int(U) or not ent[2]:
+                stale = 1
+            elif rc is not None and ent[4] is None:
+                stale = 1   # the space fits but this rank could not build its tensors
+        except Exception:  # noqa: BLE001 - reported as a declined vote
+            declined = 1
+        space = ent[3] if ent is not None and not stale and not declined else None
+        ids = ent[5] if ent is not None and not stale and not declined else None
+        cand = ent[4] if space is not None else None
+        self.launches += 1
+        self.topn_mesh_fused += 1
+        with tracing.span("GpuExecutor.topnPlainMesh", gpu=True, calls=len(ns)):
+            return mesh_cache_batch(rc if cand is not None else None, ns, ths, comm, cand, int(U), stale=stale,
+                                    declined=declined, defer=defer, device=self.device, space=space, ids=ids)
+
+    def topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False, cands=None):
+        with tracing.span("GpuExecutor.topnBatch", gpu=True, calls=len(calls)):
+            return self._topn_batch(index, calls, shards, defer, cands)
+
+    def capture_cands(self, index: str, calls: List[Call], shards: List[int]) -> Dict[Tuple, Tuple]:
+        """The node candidate-space entries of the batch's cache-only groups,
+        taken right after the mesh vote: the batch then follows them (fused
+        or not, and with which caches) whatever this rank's caches become
+        meanwhile (a concurrent write on the front end could flip
+        its choice and unpair the node's collectives)."""
+        out = {}
+        for fname, nreq in self._cand_groups(index, calls, shards):
+            ent = self._cand_spaces.get((index, fname, tuple(shards), nreq))
+            if ent is not None:
+                out[(fname, nreq)] = ent
+        return out
+
+    def _topn_batch(self, index: str, calls: List[Call], shards: List[int], defer: bool = False, cands=None):
         """Whole TopN calls (phase 1, candidate union, ids= re-count, trim to
         n: executor.go:863-903) for a batch of calls over local shards, both
         phases on the device.  Calls of one (field, src shape) share launches:
@@ -1145,6 +1259,25 @@ class GpuExecutor:
         parts: List[Tuple[List[int], object]] = []
         for (fname, nosrc), members in groups.items():
             rv, rc = fields[fname]
+            ent = None
+            if nosrc and self.comm is not None and cands is not None:
+                ent = cands.get((fname, _nreq([params[i][1] for i in members])))
+                if ent is not None and not ent[2]:
+                    ent = None      # the space did not fit on some rank: the node takes the union path
+            if ent is not None:
+                # fused mesh group: every rank takes part, with the captured caches
+                live = list(members)
+                ns = [params[i][1] for i in live]
+                ths = [params[i][2] for i in live]
+                self.launches += 1
+                self.topn_mesh_fused += 1
+                from .topn_exec import mesh_cache_batch
+                e_rc, e_cand, _, e_space = ent[4], ent[1], ent[2], ent[3]
+                got = mesh_cache_batch(e_rc if e_cand is not None else None, ns, ths, self.comm, e_cand,
+                                       len(e_space), defer=defer, device=self.device, space=e_space,
+                                       ids=e_cand.ids if e_cand is not None else ent[5])
+                parts.append((live, got))
+                continue
             live = [i for i in members if rc is not None and rc.K and srcs[i] is not EMPTY]
             for i in members:
                 if i not in live:
@@ -1156,17 +1289,7 @@ class GpuExecutor:
             space = self._node_space((index, fname, tuple(shards)), rv)
             if nosrc:
                 self.launches += 1
-                cand = None
-                if self.comm is not None:
-                    ent = self._cand_spaces.get((index, fname, tuple(shards), _nreq(ns)))
-                    # node-consistent: every rank refreshed in the same vote, and
-                    # the entry's fit check used node-wide sizes
-                    cand = ent[1] if ent is not None and ent[0] == rc.serial else None
-                if cand is not None:
-                    self.topn_mesh_fused += 1
-                    got = rc.topn_nosrc_mesh(ns, ths, self.comm, cand, defer=defer)
-                else:
-                    got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space, defer=defer)
+                got = rc.topn_nosrc(ns, ths, comm=self.comm, space=space, defer=defer)
             else:
                 tix = self._topn_index(index, fname, shards, rc, rv, space=space)
                 if tix is None:
@@ -1443,7 +1566,7 @@ class GpuExecutor:
         for fname, nreq in self._cand_groups(index, calls, shards):
             rc = finfo[fname][2]
             ent = self._cand_spaces.get((index, fname, tuple(shards), nreq))
-            if rc is None or ent is None or ent[0] != rc.serial:
+            if ent is None or ent[0] != (rc.serial if rc is not None else None):
                 return True
         return False
 
@@ -1474,10 +1597,19 @@ class GpuExecutor:
             fits = min(s_frag) >= 0 and len(space) * max(s_frag) <= FUSED_MAX_CELLS and \
                 sum(int(p[1]) for p in parts) < 2048 and len(space) > 0
             key = (index, fname, tuple(shards), nreq)
-            if rc is None:
-                self._cand_spaces.pop(key, None)
-                continue
-            self._cand_spaces[key] = (rc.serial, rc.node_candidates(nreq, space) if fits else None)
+            cand = None
+            if fits and rc is not None:
+                try:
+                    cand = rc.node_candidates(nreq, space)
+                except Exception:  # noqa: BLE001 - contributes zeros; the batch answers without this rank
+                    cand = None
+            # (serial, candidates, fits node-wide, space, the caches they were
+            # built from, tie-break ids): every rank holds an entry after a
+            # refresh, so the fused-or-not choice is the same on every rank
+            ids = torch.arange(len(space), dtype=torch.int32, device=comm.device) if fits else None
+            if len(self._cand_spaces) > 256:
+                self._cand_spaces.clear()
+            self._cand_spaces[key] = (rc.serial if rc is not None else None, cand, fits, space, rc, ids)
 
     def _topn_index(self, index: str, fname: str, shards: List[int], rc, rv, space=None):
         """Device slot index (ops/topn_index.py) over the rank caches ``rc``,

@@ -178,6 +178,141 @@ def _select_from_buffer(buf, Q: int, T: int, U: int, q: int, t: int, lim: int) -
     return h[h >= 0]
 
 
+def cache_partial_ref(cnt, nmax: int, nlim: int, inv, cm, prm, Q: int, T: int, U: int, buf) -> None:
+    """PyTorch reference of topn_cache_partial (kernels/topn_kernels.hip) for
+    the mesh buffer [member bytes | int32 totals[T, U] | flags[2]]: the CPU
+    path of mesh_cache_batch and the numerics oracle of the kernel."""
+    import torch
+    buf.zero_()
+    mw = (Q * U + 3) // 4
+    member = buf[:mw].view(torch.uint8)[:Q * U].view(Q, U)
+    S = int(cnt.shape[0])
+    p = prm.to(torch.int64)
+    if S and nlim:
+        c = cnt[:, :nlim].to(torch.int64)                                   # [S, nlim]
+        j = inv.view(S, nmax)[:, :nlim].to(torch.int64)
+        k = torch.arange(nlim)
+        lim = torch.clamp(p[:Q], max=nlim)
+        take = (k[None, None, :] < lim[:, None, None]) & (c[None] >= p[Q:2 * Q][:, None, None]) & (c[None] > 0)
+        for q in range(Q):
+            member[q, j[take[q]]] = 1
+    th = p[4 * Q:4 * Q + T]
+    cm64 = cm.to(torch.int64).view(U, S) if S else torch.zeros((U, 0), dtype=torch.int64)
+    tot = torch.where(cm64[None] >= th[:, None, None], cm64[None], torch.zeros((), dtype=torch.int64)).sum(dim=2)
+    buf[mw:mw + T * U] = tot.reshape(-1).to(torch.int32)
+
+
+def cache_select_ref(buf, ids, prm, Q: int, T: int, KK: int):
+    """PyTorch reference of topn_cache_select32: out int64[Q, KK + 1], column
+    0 the rows kept (-3 / -4 when the reduced flags say stale / declined)."""
+    import torch
+    U = int(ids.numel())
+    mw = (Q * U + 3) // 4
+    out = torch.zeros((Q, KK + 1), dtype=torch.int64)
+    fl = buf[mw + T * U:mw + T * U + 2].tolist()
+    if fl[0] or fl[1]:
+        out[:, 0] = -4 if fl[1] else -3
+        return out
+    member = buf[:mw].view(torch.uint8)[:Q * U].view(Q, U)
+    p = prm.to(torch.int64)
+    d = ids.to(torch.int64)
+    for q in range(Q):
+        tq = buf[mw + int(p[2 * Q + q]) * U:mw + (int(p[2 * Q + q]) + 1) * U].to(torch.int64)
+        ok = (member[q] > 0) & (d >= 0) & (tq > 0)
+        keys = torch.sort((tq[ok] << 32) | (0xFFFFFFFF - d[ok]), descending=True).values
+        lim = min(int(keys.numel()), int(p[3 * Q + q]), KK)
+        out[q, 0] = lim
+        out[q, 1:1 + lim] = keys[:lim]
+    return out
+
+
+def mesh_cache_batch(rc: Optional["DeviceRankCaches"], ns: Sequence[int], thresholds: Sequence[int], comm,
+                     cand: Optional[NodeCandidates], U: int, stale: int = 0, declined: int = 0,
+                     defer: bool = False, device=None, space=None, ids=None):
+    """One rank's share of a cache-only TopN batch across the ranks of a node,
+    in ONE collective: every rank writes its membership bytes, int32 partial
+    totals over the node candidate space and two flag words -- its vote
+    [stale candidate space, declined] -- into one buffer
+    (topn_cache_partial), the ranks all-reduce it, and the front end runs the
+    per-query LDS top-n on the sum (topn_cache_select32).  The union of the
+    per-shard candidate lists is the sum's nonzero membership, and a total
+    summed per shard where it reaches the threshold is the node's ids=
+    re-count (executor.go:863-903), so no candidate union or re-count round
+    trip is needed, and the readiness vote needs no collective of its own:
+    a rank that cannot take part (no usable candidate space: ``stale``; no
+    caches or an error: ``declined``) sends zeros and its flag, and the
+    select then answers nothing (the front end refreshes the space or takes
+    the general path).  ``U`` comes from the command, so every rank's buffer
+    has the same size whatever its local state.  The result (after the
+    collective) is a list of PairArrays, or the string "stale" / "declined".
+    ``space`` / ``ids`` (the node space and the select's tie-break ids)
+    default to ``cand``'s; a rank with no local caches passes them alone."""
+    import torch
+
+    from pilosa_amd.parallel.collectives import Pending
+    ns, thresholds = clamp_topn_params(ns, thresholds)
+    Q = len(ns)
+    nn = [int(n) for n in ns]
+    dev = rc.view.device if rc is not None else (device if device is not None else comm.device)
+    ths = [max(1, int(t)) for t in thresholds]
+    uniq_t = sorted(set(ths))
+    T = len(uniq_t)
+    K = rc.K if rc is not None else 0
+    KK = min(U, max(nn)) if all(nn) else U
+    prm = np.empty(4 * Q + T, np.int32)
+    prm[:Q] = [n if n else K for n in nn]
+    prm[Q:2 * Q] = ths
+    tix = {t: i for i, t in enumerate(uniq_t)}
+    prm[2 * Q:3 * Q] = [tix[t] for t in ths]
+    prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
+    prm[4 * Q:] = uniq_t
+    prm_d = torch.from_numpy(prm).to(dev, non_blocking=True)
+    mw = (Q * U + 3) // 4
+    buf = torch.empty(mw + T * U + 2, dtype=torch.int32, device=dev)
+    part = cand is not None and not stale and not declined and rc is not None and cand.nmax > 0 and rc.S > 0
+    if part:
+        nlim = min(cand.nmax, max(int(p) for p in prm[:Q])) if Q else cand.nmax
+        if dev.type == "cuda":
+            kernels().topn_cache_partial(rc.cache_cnt, cand.nmax, nlim, cand.inv, cand.cm, prm_d, Q, T, U, buf, 0, 0)
+        else:
+            cache_partial_ref(rc.cache_cnt, cand.nmax, nlim, cand.inv, cand.cm, prm_d, Q, T, U, buf)
+    else:
+        z = torch.zeros(0, dtype=torch.int32, device=dev)
+        if dev.type == "cuda":
+            kernels().topn_cache_partial(z, 0, 0, z, z, prm_d, Q, T, U, buf, int(bool(stale)), int(bool(declined)))
+        else:
+            buf.zero_()
+            buf[-2] = int(bool(stale))
+            buf[-1] = int(bool(declined))
+    if space is None and cand is not None:
+        space = cand.space
+    if ids is None and cand is not None:
+        ids = cand.ids
+
+    def finish():
+        if ids is None or space is None:
+            return "stale"
+        if dev.type == "cuda":
+            out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
+            kernels().topn_cache_select32(buf, ids, prm_d, Q, T, out)
+        else:
+            out = cache_select_ref(buf, ids, prm_d, Q, T, KK)
+        h = out.cpu().numpy()
+        if Q and h[0, 0] <= -3:
+            return "declined" if h[0, 0] == -4 else "stale"
+        res: List[List[Pair]] = []
+        for q in range(Q):
+            if h[q, 0] < 0:     # more members than one workgroup sorts: torch over the reduced buffer
+                r = _select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
+            else:
+                r = h[q, 1:1 + int(h[q, 0])]
+            j = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
+            res.append(pair_array(space[j] if len(j) else np.zeros(0, np.uint64), r >> 32))
+        return res
+    pend = Pending(comm, comm.all_reduce_async(buf), finish, keep=(buf, prm_d))
+    return pend if defer else pend.result()
+
+
 class DeviceRankCaches:
     """Ranked caches of every local shard of one view, on the device.
 
@@ -508,57 +643,9 @@ class DeviceRankCaches:
 
     def topn_nosrc_mesh(self, ns: Sequence[int], thresholds: Sequence[int], comm, cand: "NodeCandidates",
                         defer: bool = False):
-        """Cache-only TopN batch across the ranks of a node in ONE collective:
-        every rank writes its membership bytes and int32 partial totals over
-        the node candidate space into one buffer (topn_cache_partial), the
-        ranks all-reduce it, and the front end runs the per-query LDS top-n
-        on the sum (topn_cache_select32).  The union of the per-shard
-        candidate lists is the sum's nonzero membership, and a total summed
-        per shard where it reaches the threshold is the node's ids= re-count
-        (executor.go:863-903), so no candidate union or re-count round trip
-        is needed."""
-        import torch
-
-        from pilosa_amd.parallel.collectives import Pending
-        ns, thresholds = clamp_topn_params(ns, thresholds)
-        Q = len(ns)
-        nn = [int(n) for n in ns]
-        U = len(cand.space)
-        dev = self.view.device
-        ths = [max(1, int(t)) for t in thresholds]
-        uniq_t = sorted(set(ths))
-        T = len(uniq_t)
-        KK = min(U, max(nn)) if all(nn) else U
-        prm = np.empty(4 * Q + T, np.int32)
-        prm[:Q] = [n if n else self.K for n in nn]
-        prm[Q:2 * Q] = ths
-        tix = {t: i for i, t in enumerate(uniq_t)}
-        prm[2 * Q:3 * Q] = [tix[t] for t in ths]
-        prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
-        prm[4 * Q:] = uniq_t
-        prm_d = torch.from_numpy(prm).to(dev, non_blocking=False)
-        mw = (Q * U + 3) // 4
-        buf = torch.zeros(mw + T * U, dtype=torch.int32, device=dev)
-        if cand.nmax and U:
-            kernels().topn_cache_partial(self.cache_cnt, cand.nmax, cand.inv, cand.cm, prm_d, Q, T, U, buf)
-        space = cand.space
-        ids = cand.ids
-
-        def finish():
-            out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
-            kernels().topn_cache_select32(buf, ids, prm_d, Q, T, out)
-            h = out.cpu().numpy()
-            res: List[List[Pair]] = []
-            for q in range(Q):
-                if h[q, 0] < 0:     # more members than one workgroup sorts: torch over the reduced buffer
-                    r = _select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
-                else:
-                    r = h[q, 1:1 + int(h[q, 0])]
-                j = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
-                res.append(pair_array(space[j] if len(j) else np.zeros(0, np.uint64), r >> 32))
-            return res
-        pend = Pending(comm, comm.all_reduce_async(buf), finish, keep=(buf, prm_d))
-        return pend if defer else pend.result()
+        """Cache-only TopN batch across the ranks of a node in ONE collective
+        (:func:`mesh_cache_batch` with this rank's caches)."""
+        return mesh_cache_batch(self, ns, thresholds, comm, cand, len(cand.space), defer=defer)
 
     def _topn_nosrc_fused(self, ns: Sequence[int], thresholds: Sequence[int]) -> Optional[List[List[Pair]]]:
         """Cache-only TopN batch in three hand-written kernels

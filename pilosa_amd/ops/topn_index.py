@@ -473,7 +473,7 @@ class DeviceTopNIndex:
         Q = len(srcs)
         if Q == 0:
             return []
-        if self.R and Q > HOT_Q:
+        if Q > HOT_Q:   # (the chunking depends on Q only: every rank of a node chunks alike)
             parts = [self._topn(engine, srcs[i:i + HOT_Q], ns[i:i + HOT_Q], thresholds[i:i + HOT_Q], comm, defer)
                      for i in range(0, Q, HOT_Q)]
             cat = lambda rs: [p for r in rs for p in r]   # noqa: E731

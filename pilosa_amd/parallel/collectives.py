@@ -43,6 +43,18 @@ class CommError(RuntimeError):
     """A collective failed or timed out; the mesh must fail over."""
 
 
+class MeshVote(Exception):
+    """Some rank voted against a batch inside one of its data collectives
+    (``Comm.union(vote=)``): every rank raises it after the same collective,
+    so all abandon the batch at the same point.  ``kind`` is the largest
+    vote: 1 = declined (the general path answers), 2 = a stale node row space
+    (refresh, then re-run)."""
+
+    def __init__(self, kind: int):
+        super().__init__(f"mesh batch vote {kind}")
+        self.kind = int(kind)
+
+
 class Comm:
     def __init__(self, group=None, device=None, host_copies: bool = False, ctrl_group=None):
         import torch
@@ -209,7 +221,7 @@ class Comm:
         work = self._guard(self.dist.all_gather, outs, pad, group=self.group, async_op=True)
         return Pending(self, work, lambda: [x[:k] for x, k in zip(outs, lens)], keep=(pad, outs))
 
-    def union(self, t, tag: str = "union"):
+    def union(self, t, tag: str = "union", vote: int = 0):
         """Sorted distinct values of int64 ``t`` over all ranks (the same on
         every rank).  One all-gather in the steady state: every rank sends
         ``[count, values..., padding]`` padded to a capacity all ranks share
@@ -217,14 +229,20 @@ class Comm:
         sync -- before the data moves.  Every rank reads every count from the
         gather, so the ranks agree when one overflowed the pad: they then
         re-gather at the exact size (one more collective) and raise the
-        capacity alike for the next call."""
+        capacity alike for the next call.
+
+        ``vote`` > 0: this rank cannot take part in the batch (1 declined, 2
+        its node row space is stale); it sends ``-vote`` in place of its
+        count, and every rank -- reading the counts it already reads --
+        raises :class:`MeshVote` after this one collective.  A batch's
+        readiness vote thus needs no collective of its own."""
         torch = self.torch
         t = t.reshape(-1).to(torch.int64)
-        n = int(t.numel())
+        n = int(t.numel()) if not vote else 0
         cap = self._union_cap.get(tag, (UNION_MIN_CAP, 0))
         cap, quiet = cap
         buf = torch.empty(cap + 1, dtype=torch.int64, device=t.device)
-        buf[0] = n
+        buf[0] = n if not vote else -int(vote)
         k = min(n, cap)
         if k:
             buf[1:1 + k] = t[:k]
@@ -233,6 +251,8 @@ class Comm:
         self._guard(self.dist.all_gather_into_tensor, ho, self._on(buf), group=self.group)
         ho = ho.view(self.world, cap + 1)
         counts = ho[:, 0].cpu().numpy()
+        if len(counts) and int(counts.min()) < 0:
+            raise MeshVote(-int(counts.min()))
         mx = int(counts.max()) if len(counts) else 0
         # capacity for the next call: grow past the largest count (with room),
         # halve after a long quiet spell well below it; same on every rank

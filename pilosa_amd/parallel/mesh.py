@@ -57,14 +57,18 @@ class MeshError(RuntimeError):
 
 # ---------------------------------------------------------------- transport
 (OP_STOP, OP_COUNT, OP_CALL, OP_WRITE, OP_IMPORT, OP_SCHEMA, OP_DEL_INDEX, OP_DEL_FIELD, OP_SHARDS, OP_COUNT_TEXT,
- OP_ERRORS, OP_TOPN, OP_SYNC, OP_RECALC) = range(14)
+ OP_ERRORS, OP_TOPN, OP_SYNC, OP_RECALC, OP_TOPN_PLAIN, OP_TOPN_CAND, OP_SHARDSET, OP_TOPN_SPACES) = range(18)
 MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
+MAX_SHARD_SETS = 4096  # shard lists registered with the ranks (OP_SHARDSET); more go the general way
 # bitmap calls whose rank partial can travel as device container blocks
 _ROW_CALLS = ("Row", "Range", "Bitmap", "Intersect", "Union", "Difference", "Xor", "Not", "Shift")
 _OP_NAMES = {OP_STOP: "stop", OP_COUNT: "count", OP_CALL: "call", OP_WRITE: "write", OP_IMPORT: "import",
              OP_SCHEMA: "schema", OP_DEL_INDEX: "deleteIndex", OP_DEL_FIELD: "deleteField", OP_SHARDS: "shards",
              OP_COUNT_TEXT: "countText", OP_ERRORS: "errors", OP_TOPN: "topn", OP_SYNC: "sync",
-             OP_RECALC: "recalculateCaches"}
+             OP_RECALC: "recalculateCaches", OP_TOPN_PLAIN: "topnPlain", OP_TOPN_CAND: "topnCand",
+             OP_SHARDSET: "shardSet", OP_TOPN_SPACES: "topnSpaces"}
+_VOTES = {1: "declined", 2: "stale"}
+_PIPELINED = (OP_COUNT_TEXT, OP_CALL, OP_TOPN, OP_TOPN_PLAIN)
 
 
 def _raise_remote(parts):
@@ -120,6 +124,15 @@ class ShardMesh:
         # otherwise answers a 1-rank node directly): runs the RCCL transport
         # on a 1-GPU box, bench.py --mesh
         self.always = bool(force)
+        # shard lists named by a small id, registered once with every rank
+        # (OP_SHARDSET): a request names its ~1k shards with one int, and each
+        # rank's owned subset is computed once
+        self._shardsets: Dict[tuple, tuple] = {}     # front end: shards -> (id, owned)
+        self._sets_by_id: Dict[int, tuple] = {}      # every rank: id -> (shards, owned)
+        self._cand_gen = 0                           # node candidate space generations issued
+        self.topn_plain_batches = 0
+        self.topn_plain_refreshes = 0
+        self.topn_plain_retries = 0
 
     # ------------------------------------------------------------ ownership
     def owner(self, shard: int) -> int:
@@ -243,11 +256,92 @@ class ShardMesh:
         (executor.go:863-903 over RCCL instead of per-shard pair lists).  The
         ranks first agree (one all-reduce of a flag) that each can run the
         batch on its device; None = use the general path."""
-        res = self._run_pipelined(OP_TOPN, index, text if text is not None else [str(c) for c in calls],
-                                  list(shards))
-        if res is not None:
-            self.topn_tensor_batches += 1
-        return res
+        from pilosa_amd.executor import DEFAULT_FIELD
+        payload = text if text is not None else [str(c) for c in calls]
+        for attempt in range(2):
+            res = self._run_pipelined(OP_TOPN, index, payload, list(shards))
+            if isinstance(res, str):
+                # a batch whose vote rode in its first collective: some rank
+                # declined (the general path answers) or found its node row
+                # space stale (rebuilt collectively, then the batch re-runs)
+                if res == "stale" and attempt == 0:
+                    fnames = sorted({str(c.args.get("_field") or DEFAULT_FIELD) for c in calls})
+                    self._run(OP_TOPN_SPACES, index, fnames, list(shards))
+                    continue
+                return None
+            if res is not None:
+                self.topn_tensor_batches += 1
+            return res
+        return None
+
+    def shard_set(self, shards: Sequence[int]):
+        """(id, owned shards) of a shard list, registered with every rank on
+        first use (one OP_SHARDSET command); None once MAX_SHARD_SETS lists
+        are registered (the caller then takes the general path)."""
+        key = tuple(shards)
+        got = self._shardsets.get(key)
+        if got is not None:
+            return got
+        with self.lock:
+            got = self._shardsets.get(key)
+            if got is None:
+                if len(self._shardsets) >= MAX_SHARD_SETS:
+                    return None
+                sid = len(self._shardsets) + 1
+                self._run(OP_SHARDSET, sid, list(key))
+                got = self._shardsets[key] = (sid, self._sets_by_id[sid][1])
+        return got
+
+    def topn_plain(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: Sequence[int]):
+        """A request of plain cache-only TopN calls of one field -- TopN(f[,
+        n=][, threshold=]), recognised natively on the front end
+        (Executor._topn_plain_fast) -- on every rank's GPU as ONE all-reduce
+        (OP_TOPN_PLAIN): the command carries the parsed (n, threshold)
+        arrays, the shard-set id and the node candidate space's generation
+        and size; each rank adds its partial over that space, with its vote
+        (stale / declined) folded into the same buffer, and the front end
+        selects each call's top n from the sum.  No rank parses PQL and no
+        host reads a tensor before the data collective (executor.go:863-930
+        over mapReduce :2458-2555, on RCCL).  A space that some rank finds
+        stale is rebuilt collectively (OP_TOPN_CAND) and the batch re-run
+        once.  None = the general path."""
+        from pilosa_amd.ops.gpu_executor import _nreq
+
+        gpu = getattr(self.executor, "gpu", None)
+        if gpu is None or not hasattr(gpu, "topn_plain_mesh"):
+            return None
+        ss = self.shard_set(shards)
+        if ss is None:
+            return None
+        sid, own = ss
+        nreq = _nreq(ns)
+        ns = [int(n) for n in ns]
+        ths = [int(t) for t in ths]
+        force = False
+        for attempt in range(2):
+            st = None if force else gpu.plain_cand_state(index, fname, own, sid, nreq)
+            if st is None:
+                with self.lock:
+                    self._cand_gen += 1
+                    gen = self._cand_gen
+                self.topn_plain_refreshes += 1
+                self._run(OP_TOPN_CAND, index, fname, sid, nreq, gen)
+                st = gpu.plain_cand_state(index, fname, own, sid, nreq)
+                if st is None:
+                    return None
+            gen, U, fits = st
+            if not fits:
+                return None
+            res = self._run_pipelined(OP_TOPN_PLAIN, index, fname, ns, ths, sid, nreq, gen, U)
+            if isinstance(res, str):
+                if res == "stale" and attempt == 0:
+                    self.topn_plain_retries += 1
+                    force = True   # another rank's copy was stale: rebuild the space node-wide
+                    continue
+                return None
+            self.topn_plain_batches += 1
+            return res
+        return None
 
     def _run_pipelined(self, op: int, *args):
         """Front end: broadcast + issue under the lock (this rank's share
@@ -395,7 +489,7 @@ class ShardMesh:
                 self._serve_one(op, args)
 
     def _serve_one(self, op: int, args: list):
-        if op not in (OP_COUNT_TEXT, OP_CALL, OP_TOPN):
+        if op not in _PIPELINED:
             self._dispatch(op, args)
             return
         if op == OP_COUNT_TEXT:
@@ -454,6 +548,14 @@ class ShardMesh:
                         idx.delete_field(args[1])
             elif op == OP_ERRORS:
                 mine = self._errors.pop(int(args[0]), None)
+            elif op == OP_SHARDSET:
+                sid, shards = int(args[0]), [int(x) for x in args[1]]
+                self._sets_by_id[sid] = (shards, self.owned(shards))
+            elif op == OP_TOPN_CAND:
+                self._topn_cand_refresh(*args)
+            elif op == OP_TOPN_SPACES:
+                index, fnames, shards = args
+                self._topn_spaces_refresh(index, fnames, self.owned(shards))
             elif op == OP_RECALC:
                 ex.holder.recalculate_caches()
             elif op == OP_SYNC:
@@ -489,6 +591,8 @@ class ShardMesh:
 
         if op == OP_TOPN:
             return self._topn_batch_local(*args)
+        if op == OP_TOPN_PLAIN:
+            return self._topn_plain_local(*args)
         if op != OP_CALL:
             raise MeshError(f"mesh command {op!r} is not pipelined")
         index, pql, shards, optd = args
@@ -528,8 +632,62 @@ class ShardMesh:
             for _ in fnames:   # take part with no rows
                 self.comm.all_gather_var(torch.zeros(0, dtype=torch.int64, device=self.device))
 
+    def _topn_cand_refresh(self, index: str, fname: str, sid: int, nreq: int, gen: int):
+        """OP_TOPN_CAND on every rank: exactly one candidate-row all-gather
+        whatever this rank holds (GpuExecutor.refresh_plain_cand)."""
+        gpu = self.executor.gpu
+        own = (self._sets_by_id.get(int(sid)) or ((), []))[1]
+        if gpu is not None and hasattr(gpu, "refresh_plain_cand"):
+            gpu.refresh_plain_cand(index, fname, own, int(sid), int(nreq), int(gen), self.comm)
+        else:   # take part with a failed head: the node declines the fused path
+            self.comm.all_gather_var(self.torch.tensor([-1, 0], dtype=self.torch.int64, device=self.device))
+
+    def _topn_plain_local(self, index: str, fname: str, ns: List[int], ths: List[int], sid: int, nreq: int,
+                          gen: int, U: int):
+        """This rank's share of an OP_TOPN_PLAIN batch: its partial and vote
+        in the one all-reduce (a rank without the GPU path declines, with a
+        buffer of the commanded size)."""
+        gpu = self.executor.gpu
+        ss = self._sets_by_id.get(int(sid))
+        if gpu is None or not hasattr(gpu, "topn_plain_mesh") or ss is None:
+            from pilosa_amd.ops.topn_exec import mesh_cache_batch
+            return mesh_cache_batch(None, ns, ths, self.comm, None, int(U), declined=1, defer=True,
+                                    device=self.device)
+        return gpu.topn_plain_mesh(index, fname, ns, ths, ss[1], int(sid), int(nreq), int(gen), int(U), self.comm)
+
+    def _topn_spaces_refresh(self, index: str, fnames: List[str], own: List[int]):
+        """OP_TOPN_SPACES on every rank: the node row spaces of ``fnames``
+        re-gathered (one all-gather per field, whatever this rank holds)."""
+        gpu = self.executor.gpu
+        prev = gpu.comm if gpu is not None else None
+        try:
+            if gpu is not None:
+                gpu.comm = self.comm
+            self._refresh_spaces(index, fnames, own, vote=False)
+        finally:
+            if gpu is not None:
+                gpu.comm = prev
+
+    @staticmethod
+    def _single_src_group(calls) -> bool:
+        """Every call a TopN over one src of one field, with no ids= /
+        Tanimoto / attribute filter: the batch is one slot-index group, whose
+        first collective (the candidate union) can carry the readiness vote.
+        Decided from the command text alone, so every rank decides alike."""
+        if not calls:
+            return False
+        fields = set()
+        for c in calls:
+            if c.name != "TopN" or len(c.children) != 1 or any(
+                    k in c.args for k in ("ids", "tanimotoThreshold", "attrName", "attrValues")):
+                return False
+            fields.add(str(c.args.get("_field") or ""))
+        return len(fields) == 1
+
     def _topn_batch_local(self, index: str, pqls: List[str], shards: List[int]):
         from pilosa_amd.pql import parse_string
+
+        from .collectives import MeshVote
 
         torch = self.torch
         ex = self.executor
@@ -558,19 +716,39 @@ class ShardMesh:
                     gpu.topn_batch_ready(index, calls, own)
             except Exception:  # noqa: BLE001 - a rank that cannot take part declines
                 return False
-        try:
-            # ONE all-reduce (MAX) of [space stale, decline]: the refresh vote
-            # and the readiness vote folded together.  A rank whose own copy of
-            # a node row space is stale cannot judge readiness yet (the slot
-            # index depends on the space): it votes stale only, and then every
-            # rank refreshes and votes readiness again (a second all-reduce,
-            # only after writes moved a row directory).
-            stale = 0
+
+        def space_stale() -> int:
             try:
                 if gpu is not None and hasattr(gpu, "node_space_stale") and fnames:
-                    stale = int(any(gpu.node_space_stale(index, f, own) for f in fnames))
+                    return int(any(gpu.node_space_stale(index, f, own) for f in fnames))
             except Exception:  # noqa: BLE001 - a rank that cannot tell asks for a refresh
-                stale = 1
+                return 1
+            return 0
+        try:
+            if self._single_src_group(calls):
+                # src batch: the vote rides in the candidate union (Comm.union
+                # vote=): union + re-count = 2 data collectives in the steady
+                # state.  A rank that cannot take part sends its vote in the
+                # union and every rank abandons the batch after it.
+                vote = 2 if space_stale() else (0 if ready() else 1)
+                res = None
+                try:
+                    if not vote:
+                        res = gpu.topn_batch(index, calls, own, defer=True)
+                    if res is None:   # declined before its first collective: vote in it
+                        self.comm.union(torch.zeros(0, dtype=torch.int64, device=self.device), tag="topn_src",
+                                        vote=vote or 1)
+                except MeshVote as v:
+                    return _VOTES.get(v.kind, "declined")
+                return res
+            # other shapes: ONE all-reduce (MAX) of [space stale, decline,
+            # cand]: the refresh vote and the readiness vote folded together.
+            # A rank whose own copy of a node row space is stale cannot judge
+            # readiness yet (the slot index depends on the space): it votes
+            # stale only, and then every rank refreshes and votes readiness
+            # again (a second all-reduce, only after writes moved a row
+            # directory).
+            stale = space_stale()
             decline = 0 if stale else (0 if ready() else 1)
             # cache-only groups also need this rank's node candidate space
             # (built from its current rank caches): stale = refresh them too
@@ -592,7 +770,13 @@ class ShardMesh:
                 return None
             if (voted_stale or voted_cand) and hasattr(gpu, "refresh_cand_spaces"):
                 gpu.refresh_cand_spaces(index, calls, own, self.comm)
-            res = gpu.topn_batch(index, calls, own, defer=True)
+            # the fused-or-not choice of every cache-only group is taken NOW,
+            # from the entries every rank holds after the vote (a write on
+            # another thread may replace this rank's caches before the batch
+            # runs; the captured entries keep the node's collectives paired)
+            cands = gpu.capture_cands(index, calls, own) if hasattr(gpu, "capture_cands") else None
+            res = gpu.topn_batch(index, calls, own, defer=True, cands=cands) if cands is not None else \
+                gpu.topn_batch(index, calls, own, defer=True)
         finally:
             if gpu is not None:
                 gpu.comm = prev

@@ -27,7 +27,11 @@ from tests.test_mesh import QUERIES, _canon, _data, _free_port, _load, _setup_sc
 
 pytestmark = pytest.mark.gpu
 
-TOPN = ["TopN(f, n=3)", "TopN(f, Row(g=3), n=2)", "TopN(f, n=4) TopN(f, Row(g=1), n=3) TopN(f)"]
+TOPN = ["TopN(f, n=3)", "TopN(f, Row(g=3), n=2)", "TopN(f, n=4) TopN(f, Row(g=1), n=3) TopN(f)",
+        # a plain cache-only request (native recogniser -> OP_TOPN_PLAIN)
+        "TopN(f, n=5) TopN(f, n=2, threshold=3) TopN(f)",
+        # a src request (OP_TOPN, its vote in the candidate union)
+        "TopN(f, Row(g=1), n=4) TopN(f, Row(g=2), n=2)"]
 COUNTS = "Count(Row(f=1)) Count(Intersect(Row(f=1), Row(g=2))) Count(Union(Row(f=3), Row(g=1))) Count(Row(v > 10))"
 
 
@@ -64,9 +68,10 @@ def _worker(rank, world, port, outdir):
         def both(qs):
             ex.mesh = mesh
             c0, s0, t0 = mesh.comm.data_calls, mesh.seq, mesh.topn_tensor_batches
+            p0 = mesh.topn_plain_batches
             got = run(qs)
             stats = {"collectives": mesh.comm.data_calls - c0, "count_text": mesh.seq - s0,
-                     "topn_tensor": mesh.topn_tensor_batches - t0}
+                     "topn_tensor": mesh.topn_tensor_batches - t0, "topn_plain": mesh.topn_plain_batches - p0}
             ex.mesh = None
             want = run(qs)
             ex.mesh = mesh
@@ -122,10 +127,12 @@ def test_rccl_world1_mesh_matches_local(tmp_path):
     # Row / Difference / Not / Shift / Union partials travelled as device container blocks
     assert res["row_blocks"] >= 5, res["row_blocks"]
     assert res["topn"]["topn_tensor"] >= 3 and res["after_write"]["topn_tensor"] >= 3, res
-    # steady state: the folded vote + ONE all-reduce for a cache-only batch;
-    # vote + candidate union + re-count all-reduce for a src batch
-    assert res["topn_batch_collectives"] <= 2, res["topn_batch_collectives"]
-    assert res["topn_src_batch_collectives"] <= 3, res["topn_src_batch_collectives"]
+    assert res["topn"]["topn_plain"] >= 1 and res["after_write"]["topn_plain"] >= 1, res
+    # steady state: ONE all-reduce for a plain cache-only
+    # batch (its vote in the buffer); the candidate union (carrying the vote)
+    # + the re-count all-reduce for a src batch
+    assert res["topn_batch_collectives"] == 1, res["topn_batch_collectives"]
+    assert res["topn_src_batch_collectives"] <= 2, res["topn_src_batch_collectives"]
     assert res["topn_mesh_fused"] >= 3, res["topn_mesh_fused"]
     assert res["failed_over"] and res["mesh_detached"]
     assert res["gpu_faults"] == 0

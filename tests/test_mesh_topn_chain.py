@@ -31,6 +31,7 @@ class _StubGpu:
         self.extra = extra
         self.stale = True
         self.refreshes = 0
+        self.decline = False
 
     def node_space_stale(self, index, fname, shards):
         return self.stale
@@ -43,7 +44,7 @@ class _StubGpu:
         self.refreshes += 1
 
     def topn_batch_ready(self, index, calls, shards):
-        return True
+        return not self.decline
 
     def topn_batch(self, index, calls, shards, defer=False):
         import torch
@@ -57,7 +58,9 @@ class _StubGpu:
         for q in range(Q):
             rows = {q, 10 + self.rank, 100 + q * self.rank} | {1000 + k for k in range(self.extra)}
             keys += [q * A + r for r in sorted(rows)]
-        u = comm.union(torch.tensor(keys, dtype=torch.int64), tag="stub")
+        # src calls: the slot-index path's union tag (its vote rides in it)
+        tag = "topn_src" if all(c.children for c in calls) else "stub"
+        u = comm.union(torch.tensor(keys, dtype=torch.int64), tag=tag)
         out = torch.ones(u.numel(), dtype=torch.int64)
 
         def finish():
@@ -85,6 +88,14 @@ def _worker(rank, world, port, outdir):
     mesh = ShardMesh(ex, block=1)
     ex.mesh = mesh
     ex.gpu = stub
+    state = [0]
+
+    def toggle():   # OP_RECALC: rank 1 first declines, then finds its space stale
+        state[0] += 1
+        if rank == 1:
+            stub.decline = state[0] == 1
+            stub.stale = state[0] == 2
+    holder.recalculate_caches = toggle
     try:
         if rank != 0:
             mesh.serve()
@@ -106,12 +117,39 @@ def _worker(rank, world, port, outdir):
         r1 = mesh.comm.union_retries
         big2 = ex.execute("i", q, shards=[0, 1]).results
         r2 = mesh.comm.union_retries
+        # src batches: the readiness vote rides in the candidate union, so a
+        # steady-state batch is the union + the re-count all-reduce
+        qs = "TopN(f, Row(f=1), n=5) TopN(f, Row(f=2), n=3)"
+        stub.extra = 0
+        ex.execute("i", qs, shards=[0, 1])
+        src_batch = []
+        for _ in range(3):
+            c0 = mesh.comm.data_calls
+            src_got = ex.execute("i", qs, shards=[0, 1]).results
+            src_batch.append(mesh.comm.data_calls - c0)
+        from pilosa_amd.pql import parse_string
+        calls = parse_string(qs).calls
+        # rank 1 cannot take part (its vote rides in the union): the node
+        # abandons the batch after that one collective, the general path answers
+        mesh.recalculate_caches()     # (rank 1: decline from now on)
+        c0 = mesh.comm.data_calls
+        declined = mesh.topn_batch("i", calls, [0, 1])
+        declined_calls = mesh.comm.data_calls - c0
+        # rank 1's node row space goes stale: its vote makes the node rebuild
+        # the spaces (OP_TOPN_SPACES) and re-run the batch once
+        mesh.recalculate_caches()     # (rank 1: ready again, space stale)
+        ref0 = stub.refreshes
+        stale_got = mesh.topn_batch("i", calls, [0, 1])
+        stale_refreshes = stub.refreshes - ref0
         mesh.stop()
         canon = lambda rs: [[(p.id, p.count) for p in r] for r in rs]   # noqa: E731
         with open(os.path.join(outdir, "rank0.json"), "w") as fh:
             json.dump({"first": canon(first), "got": canon(got), "per_batch": per_batch,
                        "big_len": [len(r) for r in big1], "big_same": canon(big1) == canon(big2),
                        "retries": [r1 - r0, r2 - r1], "refreshes": stub.refreshes,
+                       "src_batch": src_batch, "src_got": canon(src_got), "declined": declined is None,
+                       "declined_calls": declined_calls, "stale_got": canon(stale_got or []),
+                       "stale_refreshes": stale_refreshes,
                        "batches": mesh.topn_tensor_batches}, fh)
     finally:
         ex.close()
@@ -133,9 +171,15 @@ def test_topn_batch_collective_chain(tmp_path):
     assert res["first"] == want and res["got"] == want
     # steady state: the folded vote, one union all-gather, one re-count all-reduce
     assert res["per_batch"] == [3] * 5, res["per_batch"]
-    # the spaces were refreshed once, on both ranks, on the first (stale) batch
-    assert res["refreshes"] == 1 and r1["refreshes"] == 1
+    # the spaces were refreshed on both ranks: on the first (stale) batch,
+    # and once more after rank 1's stale vote below
+    assert res["refreshes"] == 2 and r1["refreshes"] == 2
     assert res["big_len"] == [3000 + len(w) for w in want]
     assert res["big_same"]
     assert res["retries"] == [1, 0], res["retries"]
-    assert res["batches"] == 8
+    assert res["batches"] == 8 + 4 + 1
+    # src: union (with the vote) + re-count all-reduce
+    assert res["src_batch"] == [2, 2, 2], res["src_batch"]
+    assert res["src_got"] == want
+    assert res["declined"] and res["declined_calls"] == 1
+    assert res["stale_got"] == want and res["stale_refreshes"] == 1
