@@ -184,6 +184,7 @@ void and2_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
 
 pk::ViewDev viewdev_from(const torch::Tensor& vd);
 
+#ifdef PK_KBENCH
 void shadow_build(torch::Tensor view, int64_t S, torch::Tensor rows, torch::Tensor shadow) {
   check_dev(rows, "rows");
   check_dev(shadow, "shadow");
@@ -197,6 +198,7 @@ void shadow_build(torch::Tensor view, int64_t S, torch::Tensor rows, torch::Tens
                           cur_stream(shadow));
   check_launch("shadow_build");
 }
+#endif  // PK_KBENCH
 
 void partial_sum_scatter(torch::Tensor partial, int64_t U, int64_t n, torch::Tensor ti, torch::Tensor out) {
   check_dev(partial, "partial");
@@ -650,7 +652,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("progs"), py::arg("views"), py::arg("S"), py::arg("out"), py::arg("per_key"), py::arg("mode") = 0,
         py::arg("per_shard") = py::none());
   m.def("expr_materialize", &expr_materialize, "write result containers for a batch of expressions");
+#ifdef PK_KBENCH
   m.def("shadow_build", &shadow_build, "dense bitmap shadows of hot rows for the pair kernels");
+  m.attr("KBENCH") = true;
+#else
+  m.attr("KBENCH") = false;
+#endif
   m.def("partial_sum_scatter", &partial_sum_scatter, "out[ti[q]] += column sums of int32[U][n] partials");
   m.def("and2_count", &and2_count, "Count(Intersect(a,b)) batch via key-major pair kernels", py::arg("progs"),
         py::arg("views"), py::arg("S"), py::arg("pairs"), py::arg("partial"), py::arg("cq") = 0,

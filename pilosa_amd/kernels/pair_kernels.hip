@@ -174,12 +174,40 @@ __device__ __forceinline__ void lds_clear(uint64_t* lb) {
   for (int i = 0; i < 8; i++) l2[i * 64 + lane] = make_ulong2(0, 0);
 }
 
+// ---- lane-rotated chunks (ROT): bank conflicts of the array probes.
+// A lane holds a 16-byte chunk of 8 sorted values and probe8 issues one LDS
+// read per value slot k.  With one chunk per lane the k-th values of the 32
+// lanes of a ds_read_b32 group lie one chunk apart, i.e. at a near-constant
+// stride through the bitmap: for a 512-value array lane l's slot-k value is
+// ~1024 l + 128 k, its dword ~32 l + 4 k, so all 32 lanes land on the few
+// banks around 4 k ((a/4) mod 32) and each read replays ~5-8 times
+// (SQ_LDS_BANK_CONFLICT = 52 % of the LDS-active cycles, profiles/r05_pairs/).
+// Rotating each lane's chunk by (lane & 3) dwords before the probes puts
+// lane l's slot k on value 2 ((k/2 + l) & 3) + (k & 1): four lanes in a row
+// now read values 256 apart (8 dwords, 8 banks), spreading every group over 4x
+// the banks.  The count is a sum, so the order is free; 8 v_cndmask per
+// chunk (1 VALU per probe).  Staging (ds_or scatter) gets the same rotation,
+// with its tail mask rotated alike.
+__device__ __forceinline__ uint4 rot4(const uint4 v) {
+  const int l = lane_id();
+  const uint4 a = (l & 1) ? make_uint4(v.y, v.z, v.w, v.x) : v;
+  return (l & 2) ? make_uint4(a.z, a.w, a.x, a.y) : a;
+}
+
+// valid-slot mask of a lane's chunk holding `rem` (> 0) of an array's values,
+// rotated as rot4 rotates the chunk (bit k = new slot k holds a value)
+__device__ __forceinline__ uint32_t rot_mask(int rem) {
+  const uint32_t vm = rem >= 8 ? 0xffu : ((1u << rem) - 1u);
+  const uint32_t r2 = uint32_t(lane_id() & 3) * 2u;
+  return ((vm | (vm << 8)) >> r2) & 0xffu;
+}
+
 // Stage a container of any type into lb as a (swizzled) bitmap.  BST
 // (batched staging): an array's chunks are all loaded (4 per lane per round
 // trip) before the LDS clear and the scatter, instead of one dependent load
 // per 512 values -- a 4096-value array was 8 serial round trips, and staging
 // was ~60 % of a 32-query batch's pair-kernel time (profiles/r05_serve/).
-template <bool BST = false>
+template <bool BST = false, bool ROT = false>
 __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m) {
   const int lane = lane_id();
   const int type = meta_type(m);
@@ -216,12 +244,15 @@ __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int e8 = b + k * 64 + lane;
-        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        const uint4 vk = ROT ? rot4(v[k]) : v[k];
+        const uint32_t w[4] = {vk.x, vk.y, vk.z, vk.w};
         const int rem = n - e8 * 8;
+        const uint32_t vm = ROT ? rot_mask(rem) : 0u;
 #pragma unroll
         for (int t = 0; t < 8; t++) {
           const uint32_t x = (w[t >> 1] >> ((t & 1) * 16)) & 0xffff;
-          if (e8 < n8) atomicOr(l32 + lds_swz(x >> 5), t < rem ? (1u << (x & 31)) : 0u);
+          const bool ok = ROT ? ((vm >> t) & 1u) != 0u : t < rem;
+          if (e8 < n8) atomicOr(l32 + lds_swz(x >> 5), ok ? (1u << (x & 31)) : 0u);
         }
       }
     }
@@ -238,13 +269,16 @@ __device__ __forceinline__ void stage(uint64_t* lb, const uint16_t* p, int64_t m
     const auto p4 = gp(reinterpret_cast<const uint4*>(p));
     const int n8 = (n + 7) >> 3;
     for (int e8 = lane; e8 < n8; e8 += 64) {
-      const uint4 v4 = p4[e8];
+      const uint4 raw = p4[e8];
+      const uint4 v4 = ROT ? rot4(raw) : raw;
       const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
       const int rem = n - e8 * 8;
+      const uint32_t vm = ROT ? rot_mask(rem) : 0u;
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
-        atomicOr(l32 + lds_swz(v >> 5), k < rem ? (1u << (v & 31)) : 0u);
+        const bool ok = ROT ? ((vm >> k) & 1u) != 0u : k < rem;
+        atomicOr(l32 + lds_swz(v >> 5), ok ? (1u << (v & 31)) : 0u);
       }
     }
   } else {
@@ -307,7 +341,7 @@ __device__ __forceinline__ int pad_hits(BM bm, int slots, int n) {
 // Whole-array probe with the next chunk's load issued before the current
 // chunk's LDS probes (2-deep register pipeline); lanes past the array hold zero
 // chunks; every lane probes 8 slots per iteration.
-template <bool SWZ, class BM>
+template <bool SWZ, class BM, bool ROT = false>
 __device__ __forceinline__ int probe_pipe(BM bm, const uint16_t* arr, int n) {
   const int lane = lane_id();
   const auto p4 = gp(reinterpret_cast<const uint4*>(arr));
@@ -322,7 +356,7 @@ __device__ __forceinline__ int probe_pipe(BM bm, const uint16_t* arr, int n) {
     const int ne8 = e8 + 64;
     uint4 nxt = make_uint4(0, 0, 0, 0);
     if (ne8 < n8) nxt = p4[ne8];
-    c += probe8<SWZ>(bm, cur);
+    c += probe8<SWZ>(bm, ROT ? rot4(cur) : cur);
     cur = nxt;
     e8 = ne8;
   }
@@ -415,13 +449,14 @@ __device__ __forceinline__ int probe_small(BM bm, const uint16_t* arr, int n) {
 }
 
 // |B ∩ staged| for any B container type (staged in lb)
+template <bool ROT = false>
 __device__ __forceinline__ int count_vs_lds(const uint64_t* lb, const uint16_t* p, int64_t m) {
   const int type = meta_type(m);
   if (type == CT_BITMAP) return and_lds_bitmap(lb, reinterpret_cast<const uint64_t*>(p));
   if (type == CT_ARRAY) {
     const uint32_t* bm = reinterpret_cast<const uint32_t*>(lb);
     if (meta_n(m) <= SMALL_ARRAY_N) return probe_small<true>(bm, p, meta_n(m));
-    return probe_pipe<true>(bm, p, meta_n(m));
+    return probe_pipe<true, const uint32_t*, ROT>(bm, p, meta_n(m));
   }
   return runs_in_lds(lb, p);
 }
@@ -459,7 +494,7 @@ __device__ __forceinline__ uint4 load_bhead(const uint16_t* p, int64_t m) {
 }
 
 // |B & staged| with B's head (load_bhead) already in registers
-template <bool SWZ>
+template <bool SWZ, bool ROT = false>
 __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t* p, int64_t m, const uint4 head) {
   const int lane = lane_id();
   const int t = meta_type(m);
@@ -471,7 +506,10 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
       return int(__builtin_amdgcn_ubfe(bm_word<SWZ>(bm, v), v, 1u)) - pad_hits(bm, 64, n);
     }
     const int n8 = (n + 7) >> 3;
-    if (n <= 512) return probe8<SWZ>(bm, lane < n8 ? head : make_uint4(0, 0, 0, 0)) - pad_hits(bm, 512, n);
+    if (n <= 512) {
+      const uint4 h = lane < n8 ? head : make_uint4(0, 0, 0, 0);
+      return probe8<SWZ>(bm, ROT ? rot4(h) : h) - pad_hits(bm, 512, n);
+    }
     // bigger arrays: chunk `lane` is the head, the rest pipelined as probe_pipe
     const auto p4 = gp(reinterpret_cast<const uint4*>(p));
     const int iters = (n8 + 63) >> 6;
@@ -483,7 +521,7 @@ __device__ __forceinline__ int count_vs_head(const uint64_t* lb, const uint16_t*
       const int ne8 = e8 + 64;
       uint4 nxt = make_uint4(0, 0, 0, 0);
       if (ne8 < n8) nxt = p4[ne8];
-      c += probe8<SWZ>(bm, cur);
+      c += probe8<SWZ>(bm, ROT ? rot4(cur) : cur);
       cur = nxt;
       e8 = ne8;
     }
@@ -580,6 +618,7 @@ __device__ __forceinline__ int count_global_vs_head(uint64_t* lb, const uint64_t
   return runs_in_lds(lb, pB);
 }
 
+#ifdef PK_KBENCH
 // shadow[r][s][j]: row rows[r]'s key-j container of shard s as a bitmap (zeros
 // where absent).  One wave per (r, s, j): built in LDS by stage(), copied out.
 __global__ __launch_bounds__(64) void shadow_build_kernel(ViewDev v, int S, const int32_t* __restrict__ rows, int R,
@@ -612,21 +651,27 @@ __global__ __launch_bounds__(64) void shadow_build_kernel(ViewDev v, int S, cons
   for (int i = 0; i < 8; i++) dst[i * 64 + lane] = l2[lds_swzc(uint32_t(i * 64 + lane))];
 }
 
+#endif  // PK_KBENCH
+
 // Array A of <= 512 values staged from its chunk already in registers (one
 // 16-byte chunk per lane, loaded while the previous pair was counted).
-__device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const uint4 v4) {
+template <bool ROT = false>
+__device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const uint4 v4in) {
   const int lane = lane_id();
   lds_clear(lb);
   lds_wait();
   uint32_t* l32 = reinterpret_cast<uint32_t*>(lb);
   const int n = meta_n(m);
   if (lane < ((n + 7) >> 3)) {
+    const uint4 v4 = ROT ? rot4(v4in) : v4in;
     const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
     const int rem = n - lane * 8;
+    const uint32_t vm = ROT ? rot_mask(rem) : 0u;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t v = (w[k >> 1] >> ((k & 1) * 16)) & 0xffff;
-      atomicOr(l32 + lds_swz(v >> 5), k < rem ? (1u << (v & 31)) : 0u);
+      const bool ok = ROT ? ((vm >> k) & 1u) != 0u : k < rem;
+      atomicOr(l32 + lds_swz(v >> 5), ok ? (1u << (v & 31)) : 0u);
     }
   }
   lds_wait();
@@ -659,7 +704,7 @@ __device__ __forceinline__ void stage_array_head(uint64_t* lb, int64_t m, const 
 // global gathers, no 8 KiB LDS copy), and of two arrays the smaller one is
 // staged and the larger probes it.
 template <int CQ, bool APF = false, int DBG = 0, int SB = 0, int PD = 1, bool ONE = false, bool BST = false,
-          bool SHD = false>
+          bool SHD = false, bool ROT = false>
 __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* __restrict__ progs, int Q,
                                                              const ViewDev* __restrict__ views, int S,
                                                              const uint2* __restrict__ pairs,
@@ -767,7 +812,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
       if (DBG == 1 || DBG == 5) {
         c = int(head.x & 1u) + int(tA == tB);
       } else if (a == cached && va == cached_v) {
-        c = DBG == 4 ? int(head.x & 1u) : count_vs_head<true>(lb, pB, mB, head);
+        c = DBG == 4 ? int(head.x & 1u) : count_vs_head<true, ROT>(lb, pB, mB, head);
       } else if (DBG == 3 || DBG == 4) {
         // staging skipped (3: count against whatever lb holds) or counting
         // skipped (4: stage only), with v6's branch structure
@@ -777,11 +822,11 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
             !(!next_same && tA == CT_ARRAY && tB == CT_BITMAP && meta_n(mA) <= SMALL_ARRAY_N)) {
           lds_wait();
           if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
-            stage<BST>(lb, pB, mB);
+            stage<BST, ROT>(lb, pB, mB);
             cached = NONE;
             cached_v = -1;
           } else {
-            stage<BST>(lb, pA, mA);
+            stage<BST, ROT>(lb, pA, mA);
             cached = a;
             cached_v = va;
           }
@@ -791,7 +836,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
         } else {
           cached = a;
           cached_v = va;
-          c = count_vs_head<true>(lb, pB, mB, head);
+          c = count_vs_head<true, ROT>(lb, pB, mB, head);
         }
       } else {
         const bool next_same = j >= 0 && __builtin_amdgcn_readlane(ea, j) == a &&
@@ -809,7 +854,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
             stage_bitmap(lb, gA);
             cached = a;
             cached_v = va;
-            c = count_vs_head<true>(lb, pB, mB, head);
+            c = count_vs_head<true, ROT>(lb, pB, mB, head);
           } else {
             c = count_global_vs_head(lb, gA, pB, mB, head);
             if (tB == CT_RUN) {
@@ -819,10 +864,10 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
           }
         } else if (!next_same && tA == CT_ARRAY && tB == CT_BITMAP) {
           lds_wait();
-          stage<BST>(lb, pB, mB);
+          stage<BST, ROT>(lb, pB, mB);
           cached = NONE;
           cached_v = -1;
-          c = count_vs_lds(lb, pA, mA);
+          c = count_vs_lds<ROT>(lb, pA, mA);
         } else if (ONE && !next_same && tA == CT_BITMAP && tB == CT_ARRAY) {
           // B's values probe A where it lies (B's head chunk is in registers)
           const auto gA = gp(reinterpret_cast<const uint32_t*>(pA));
@@ -838,16 +883,16 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
         } else if (ONE && !next_same && tA == CT_ARRAY && tB == CT_ARRAY && meta_n(mB) < meta_n(mA)) {
           // the smaller array is staged, the larger one probes it
           lds_wait();
-          stage<BST>(lb, pB, mB);
+          stage<BST, ROT>(lb, pB, mB);
           cached = NONE;
           cached_v = -1;
-          c = count_vs_lds(lb, pA, mA);
+          c = count_vs_lds<ROT>(lb, pA, mA);
         } else {
           lds_wait();  // previous readers of lb are done before it is rewritten
           if (APF && aok && small_array(mA))
-            stage_array_head(lb, mA, ahead);
+            stage_array_head<ROT>(lb, mA, ahead);
           else
-            stage<BST>(lb, pA, mA);
+            stage<BST, ROT>(lb, pA, mA);
           cached = a;
           cached_v = va;
           if constexpr (SB > 0) {
@@ -880,7 +925,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
               }
             }
           }
-          if (!done_i) c = count_vs_head<true>(lb, pB, mB, head);
+          if (!done_i) c = count_vs_head<true, ROT>(lb, pB, mB, head);
         }
       }
       if (done_i) {
@@ -901,6 +946,7 @@ __global__ __launch_bounds__(64, 5) void and2_pairs_v6_kernel(const QueryProg* _
   }
   if (lane < nq) partial[u * Q + q0 + lane] = mine;
 }
+#ifdef PK_KBENCH
 // ---- v10: one wave per (unit, chunk of CQ queries) as v6, but a run of
 // queries that share the staged row A is counted as ONE flat stream.
 //
@@ -1097,8 +1143,10 @@ __global__ __launch_bounds__(64, 4) void and2_pairs_v10_kernel(const QueryProg* 
   }
   if (lane < nq) partial[u * Q + q0 + lane] = mine;
 }
+#endif  // PK_KBENCH
 }  // namespace
 
+#ifdef PK_KBENCH
 template <int CQ>
 void launch_v10_dbg(int dbg, int64_t wv, const QueryProg* progs, int Q, const ViewDev* views, int S, uint2* pairs,
                     int32_t* partial, hipStream_t st) {
@@ -1131,6 +1179,8 @@ void launch_shadow_build(const ViewDev& v, int S, const int32_t* rows, int R, ui
   hipLaunchKernelGGL(shadow_build_kernel, grid, dim3(64), 0, st, v, S, rows, R, shadow);
 }
 
+#endif  // PK_KBENCH
+
 void launch_keymask_build(const ViewDev& v, int S, uint16_t* out, hipStream_t st) {
   const int64_t n = int64_t(S) * v.D;
   if (n == 0) return;
@@ -1153,8 +1203,16 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   // batched array staging (variant 40) -- 68.7k vs 61.1k req/s with 2
   // group-commit threads (profiles/r05_serve/).  Bigger batches keep v6.
   if (variant == 6 && cq <= 0 && Q <= 128) variant = 40;
+#ifdef PK_KBENCH
+  if (variant == 50 && cq <= 0 && Q <= 128) variant = 51;   // the serving variant, lane-rotated
+#endif
   if (variant == 41 && cq <= 0 && Q <= 128) variant = 42;   // the same with dense shadows
   if (cq <= 0) cq = Q <= 128 ? 8 : (Q <= 2048 ? 32 : 64);
+// The shipped build instantiates v6 and its serving variant 40 only; every
+// measured-and-rejected variant and cost-isolation skeleton (v10-v13,
+// 16-24, 31-42, 50/51) is built into the kbench module alone
+// (pilosa_amd/native/build.py --kbench, scripts/kbench.py).
+#ifdef PK_KBENCH
 #define PK_LAUNCH(CQV)                                                                                       \
   {                                                                                                          \
     const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                        \
@@ -1201,6 +1259,12 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
     else if (variant == 38)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true>), dim3(unsigned(wv)), dim3(64), 0, st, \
                          progs, Q, views, S, pairs, partial);                                                \
+    else if (variant == 50)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, false, false, false, true>),               \
+                         dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial);           \
+    else if (variant == 51)                                                                                  \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true, true, false, true>),                 \
+                         dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S, pairs, partial);           \
     else if (variant == 13)                                                                                  \
       hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, true>), dim3(unsigned(wv)), dim3(64), 0, st, progs, Q,    \
                          views, S, pairs, partial);                                                          \
@@ -1208,6 +1272,18 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
       hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
                          pairs, partial);                                                                    \
   }
+#else
+#define PK_LAUNCH(CQV)                                                                                       \
+  {                                                                                                          \
+    const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                        \
+    if (variant == 40)                                                                                       \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true, true>), dim3(unsigned(wv)), dim3(64), 0, \
+                         st, progs, Q, views, S, pairs, partial);                                            \
+    else                                                                                                     \
+      hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
+                         pairs, partial);                                                                    \
+  }
+#endif  // PK_KBENCH
   switch (cq) {
     case 4: PK_LAUNCH(4) break;
     case 8: PK_LAUNCH(8) break;

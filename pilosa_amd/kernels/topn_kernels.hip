@@ -37,6 +37,15 @@
 
 #include "kernels.h"
 
+// Cost-isolation bits of the src-TopN kernels (PILOSA_TOPN_DBG): read only
+// in the kbench module (pilosa_amd/native/build.py --kbench); the shipped
+// kernels compile every such branch out.
+#ifdef PK_KBENCH
+#define PK_DBG(p) ((p).dbg)
+#else
+#define PK_DBG(p) 0
+#endif
+
 namespace pk {
 namespace {
 
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
   // tail rank's cached count below their minimum, or cached counts below the
   // threshold), the tail histogram is never read: skip building it.  Dense
   // srcs -- the ones whose histograms are expensive -- end here.
-  bool need_tail = p.R < K && !(p.dbg & 1);
+  bool need_tail = p.R < K && !(PK_DBG(p) & 1);
   if (MODE == 1 && need_tail && p.R > 0) {
     const int nmax = p.ns[q];
     int found = 0;
@@ -413,7 +422,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
     for (int i = tid; i < words; i += TN_THREADS) ho[i] = hist[i];
   }
 
-  if (MODE == 1 && (p.dbg & 2)) return;
+  if (MODE == 1 && (PK_DBG(p) & 2)) return;
   if constexpr (MODE == 1) {
     const int32_t* ca = p.cache_acc + int64_t(s) * K;
     int32_t* acc = p.acc + int64_t(q) * p.A;
@@ -430,7 +439,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
       int tot;
       const int rank = block_rank(ok, bs, tot);
       const bool take = ok && (nmax == 0 || found + rank < nmax);
-      if (take && !(p.dbg & 8192)) atomicAdd(acc + ca[k], int32_t(cv));
+      if (take && !(PK_DBG(p) & 8192)) atomicAdd(acc + ca[k], int32_t(cv));
       uint32_t tmin;
       int pmax;
       block_minmax(take ? cv : 0xffffffffu, take ? k : -1, bs, tmin, pmax);
@@ -451,7 +460,7 @@ __global__ __launch_bounds__(TN_THREADS, 8) void topn_src_kernel(TopNLaunch p) {
         const int k = base + tid;
         if (k < K && uint32_t(cc[k]) >= T) {
           const uint32_t cv = slot_count(p, hist, L, q, s, k);
-          if (cv >= T && !(p.dbg & 8192)) atomicAdd(acc + ca[k], int32_t(cv));
+          if (cv >= T && !(PK_DBG(p) & 8192)) atomicAdd(acc + ca[k], int32_t(cv));
         }
         if (uint32_t(cc[min(base + TN_THREADS, K) - 1]) < T) break;
       }
@@ -666,7 +675,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
     if (!__syncthreads_or(tid < Q && nq > 0)) return;  // block-uniform: no src has key j in this shard
   }
   if (tid == 0) grab[0] = grab[1] = 0;
-  if (bmq && !(p.dbg & 1024)) {
+  if (bmq && !(PK_DBG(p) & 1024)) {
     // bitmap srcs: every table word is written once as the transpose of the
     // bitmaps' bits (thread-owned words, 32 loads in flight per query)
     // instead of one LDS atomic per set bit -- a dense src row is 30-50k bits
@@ -727,7 +736,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
           }
         }
       }
-    } else if (!((bmq >> q) & 1u) && !(p.dbg & 512)) {
+    } else if (!((bmq >> q) & 1u) && !(PK_DBG(p) & 512)) {
       const auto w = reinterpret_cast<const TN_GLOBAL uint64_t*>(vals);
       for (int i = lane + (lo >> 6); i < (lo + NLO) >> 6; i += 64)
         for (uint64_t bb = w[i]; bb; bb &= bb - 1) {
@@ -757,7 +766,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //    row's first chunk -- in flight while the current one is counted.
   //    Carry-save planes per lane, counted at the row's end, then a
   //    17-shuffle transpose-reduce per row, totals in lanes (l >> 2) & 15.
-  for (int gb = wave; gb < ((p.dbg & 16) ? 0 : B1); gb += 64 * (HOT_THREADS / 64)) {
+  for (int gb = wave; gb < ((PK_DBG(p) & 16) ? 0 : B1); gb += 64 * (HOT_THREADS / 64)) {
     const int kl = gb + (HOT_THREADS / 64) * lane;
     const int cl = kl < B1 ? hm[kl] : -1;
     const int64_t ml = cl >= 0 ? p.v.meta[sb + cl] : 0;
@@ -841,7 +850,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       load_chunk(lr >= 0 && meta_type(lm) == CT_ARRAY ? lm : 0, lbase, ldb, ldv);
       adv();
       const uint16_t* pp = p.v.payload + meta_off16(m) * 8;
-      if (ty == CT_ARRAY && !(p.dbg & 64)) {
+      if (ty == CT_ARRAY && !(PK_DBG(p) & 64)) {
         // an array gives a lane at most 64 values (6-7 carry-save planes).
         // All 8 table reads issue before any is consumed (one LDS wait per
         // chunk); values past the array read entry 0 and count nothing.
@@ -863,7 +872,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
                              : (k < curv ? mk[k] : 0u);
         }
         hs_add<HW, COOP_P>(pl, hw);
-      } else if (ty == CT_BITMAP && !(p.dbg & 32)) {
+      } else if (ty == CT_BITMAP && !(PK_DBG(p) & 32)) {
         // the lane's words load a quarter at a time (register budget); set
         // bits are taken four at a time (four table reads in flight)
         constexpr int NIT = NLO / 4096;  // 64-word rounds of the workgroup's values
@@ -992,7 +1001,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //     (NQ 16; 2l and 2l + 1 for NQ 32) in lane l.  The cooperative path
   //     spends a 6-level reduction of every row over the whole wave, which
   //     rows of a few hundred values cannot amortise.
-  if (!(p.dbg & 2048)) {
+  if (!(PK_DBG(p) & 2048)) {
     constexpr int MW = NQ == 16 ? 4 : 8, MID_P = NQ == 16 ? 7 : 8;
     const int sl = lane & 15;
     // the rank -> container -> meta -> payload chain runs ahead: a quad's
@@ -1023,7 +1032,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
 #pragma unroll
       for (int e = 0; e < NQ / 16; e++) {
         const int q = NQ == 16 ? sl : 2 * sl + e;
-        if (q < Q && mpend[e] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + mpk, mpend[e]);
+        if (q < Q && mpend[e] && !(PK_DBG(p) & 256)) atomicAdd(out + int64_t(q) * R + mpk, mpend[e]);
       }
       mpk = -1;
     };
@@ -1106,7 +1115,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
   //    claimed two ahead and the next group's meta word and the one after's
   //    meta index are loaded with the current group's payload (one round trip
   //    per group instead of three).
-  if (!(p.dbg & 8)) {
+  if (!(PK_DBG(p) & 8)) {
     auto claim = [&]() -> int {
       int g = 0;
       if (lane == 0) g = atomicAdd(&grab[1], 1);
@@ -1131,7 +1140,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       if (pk < 0) return;
 #pragma unroll
       for (int q = 0; q < NQ; q++)
-        if (q < Q && pend[q] && !(p.dbg & 256)) atomicAdd(out + int64_t(q) * R + pk + lane, pend[q]);
+        if (q < Q && pend[q] && !(PK_DBG(p) & 256)) atomicAdd(out + int64_t(q) * R + pk + lane, pend[q]);
       pk = -1;
     };
     while (B + 64 * g < R) {
@@ -1154,7 +1163,7 @@ __global__ __launch_bounds__(HOT_THREADS, 1) void topn_hot_kernel(TopNLaunch p) 
       // 16 values per lane per step; two buffers alternate so the next
       // step's loads are in flight while this one is counted
       auto body = [&](const uint4& x0, const uint4& x1, const int i) {
-        if (p.dbg & 4096) {  // cost isolation: loads only (keep them live)
+        if (PK_DBG(p) & 4096) {  // cost isolation: loads only (keep them live)
           lpl[0] ^= x0.x ^ x1.y;
           return;
         }
@@ -1388,11 +1397,15 @@ int topn_lds_bytes(int K, int H32, int H16) {
 
 void launch_topn_src(const TopNLaunch& a0, int mode, hipStream_t st) {
   TopNLaunch a = a0;
+#ifdef PK_KBENCH
   static const int dbg = [] {
     const char* e = getenv("PILOSA_TOPN_DBG");
     return e ? atoi(e) : 0;
   }();
   a.dbg = dbg;
+#else
+  a.dbg = 0;
+#endif
   // bitmap srcs at least this dense take the transposed table build, the
   // rest one LDS atomic per set bit
   static const int tbuild_min = [] {

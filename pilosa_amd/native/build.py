@@ -150,12 +150,17 @@ def hip_sources():
             if f.endswith((".hip", ".cpp", ".h", ".hpp"))]
 
 
-def build_hip(force: bool = False, verbose: bool = False) -> str:
-    """Compile the HIP kernels + torch binding for gfx950 with hipcc."""
+def build_hip(force: bool = False, verbose: bool = False, kbench: bool = False) -> str:
+    """Compile the HIP kernels + torch binding for gfx950 with hipcc.
+    ``kbench``: the A/B module ``_hipkernels_kbench`` (-DPK_KBENCH) that also
+    holds the measured-and-rejected kernel variants and the cost-isolation
+    skeletons (scripts/kbench.py, scripts/topn_kbench.py); the shipped
+    ``_hipkernels`` has none of them."""
     import torch
     from torch.utils import cpp_extension
 
-    out = os.path.join(PKG, "_hipkernels" + _ext_suffix())
+    name = "_hipkernels_kbench" if kbench else "_hipkernels"
+    out = os.path.join(PKG, name + _ext_suffix())
     deps = hip_sources()
     if not force and not _newer(out, deps):
         return out
@@ -167,10 +172,11 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     objs = []
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-              "-DTORCH_EXTENSION_NAME=_hipkernels", "-DTORCH_API_INCLUDE_EXTENSION_H",
+              f"-DTORCH_EXTENSION_NAME={name}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+              *(["-DPK_KBENCH"] if kbench else []),
               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               *[f"-I{p}" for p in tinc], "-I", sysconfig.get_paths()["include"]]
-    bdir = os.path.join(PKG, "native", "_obj")
+    bdir = os.path.join(PKG, "native", "_obj_kbench" if kbench else "_obj")
     os.makedirs(bdir, exist_ok=True)
     procs = []
     for s in srcs:
@@ -213,4 +219,7 @@ def build_all(force: bool = False, verbose: bool = False):
 
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    print(build_all(force=force, verbose=True))
+    if "--kbench" in sys.argv:
+        print(build_hip(force=force, verbose=True, kbench=True))
+    else:
+        print(build_all(force=force, verbose=True))

@@ -27,6 +27,9 @@ MAXPROG = 32
 OP_AND, OP_OR, OP_XOR, OP_ANDNOT = 32, 33, 34, 35
 # count-batch kernel routes
 KIND_AND2, KIND_ROW, KIND_GENERIC, KIND_FLAT, KIND_UNION = 0, 1, 2, 3, 4
+# a planned batch's repeated Count(Intersect(a, b)) calls: (from, to) result
+# copies applied after the kernels (native/pql_compile.cpp plan_count_text)
+KIND_ALIAS = 5
 # launch_expr_count modes: expr_count_kernel<0/1/2>, 3 = union_count_kernel
 _KERNEL_MODE = {KIND_ROW: 1, KIND_GENERIC: 0, KIND_FLAT: 2, KIND_UNION: 3}
 
@@ -59,8 +62,13 @@ def kernels():
     if _ext is None:
         with _ext_lock:
             if _ext is None:
+                import importlib
+
                 import torch  # noqa: F401  (loads libtorch for the extension)
-                from pilosa_amd import _hipkernels as ext
+                # PILOSA_HIPKERNELS=_hipkernels_kbench: the A/B build with the
+                # rejected variants (scripts/kbench.py); the product loads the
+                # shipped module
+                ext = importlib.import_module("pilosa_amd." + os.environ.get("PILOSA_HIPKERNELS", "_hipkernels"))
                 assert ext.QUERYPROG_BYTES == QPROG_DTYPE.itemsize
                 assert ext.VIEWDEV_BYTES == VIEWDEV_DTYPE.itemsize
                 _ext = ext
@@ -1050,7 +1058,9 @@ class GpuEngine:
         # (off by default: measured slower -- headline 16.66 vs 16.45 ms, serving
         # 61.5k vs 69.3k req/s, profiles/r05_serve/ -- the staged LDS probes beat
         # reading a 8 KiB shadow in place, and the hot A rows are mostly bitmaps)
-        self.use_shadow = os.environ.get("PILOSA_SHADOW", "0") != "0"
+        # dense shadows of hot rows (variants 41 / 42): measured slower, built
+        # into the kbench module only (profiles/r05_shadow/)
+        self.use_shadow = os.environ.get("PILOSA_SHADOW", "0") != "0" and hasattr(kernels(), "shadow_build")
         # Count(Union(leaves)) route: union_count_kernel (bitmap_kernels.hip)
         self.use_union = os.environ.get("PILOSA_UNION_KERNEL", "1") != "0"
         # 2 = union_count2_kernel (flat chunk walk, parallel meta fetch), 1 = union_count_kernel
@@ -1231,6 +1241,10 @@ class GpuEngine:
         tv, tb = self._h2d_many([varr.view(np.uint8), buf])
         parts = []
         for kind, n, po, oo in segs:
+            if int(kind) == KIND_ALIAS:
+                parts.append((tb[po:po + n * 8].view(torch.int64), tb[oo:oo + n * 8].view(torch.int64), KIND_ALIAS,
+                              int(n)))
+                continue
             parts.append((tb[po:po + n * QPROG_DTYPE.itemsize], tb[oo:oo + n * 8].view(torch.int64), int(kind), int(n)))
         return (Q, S, tv, parts, shd)
 
@@ -1300,6 +1314,9 @@ class GpuEngine:
         shd = len(handle) > 4 and handle[4]
         out = torch.zeros(Q, dtype=torch.int64, device=self.device)
         for tp, ti, kind, n in parts:
+            if kind == KIND_ALIAS:   # repeated calls: their answers copied (the last part)
+                out.index_copy_(0, ti, out.index_select(0, tp))
+                continue
             if kind == KIND_AND2:
                 # column sums scattered into out by one kernel (a strided torch
                 # reduce + index_copy cost ~70 us per small serving batch)

@@ -11,6 +11,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the A/B module: the shipped variants plus every rejected one and the
+# cost-isolation skeletons (python -m pilosa_amd.native.build --kbench)
+os.environ.setdefault("PILOSA_HIPKERNELS", "_hipkernels_kbench")
 sys.path.insert(0, ROOT)
 
 

@@ -7,7 +7,8 @@ short arrays in the tail, so one launch runs the wave-cooperative path
 (bitmaps, big arrays), the quarter-wave path (mid-size arrays) and the
 lane-owned path (short arrays) of the kernel, at every lane-owned and
 mid-size bound (PILOSA_TOPN_SMALL_N / PILOSA_TOPN_MID_N) and with either
-table build (PILOSA_TOPN_DBG bit 1024).  The reference builds each
+table build (PILOSA_TOPN_TBUILD_MIN: 65537 sends every src to the atomic
+build).  The reference builds each
 shard's hot rows and src rows as dense 0/1 fp32 matrices per 2^16-column key
 and multiplies them (exact: counts < 2^24).
 """
@@ -125,8 +126,7 @@ def test_hot_counts_equal_dense_reference(nq, monkeypatch):
 @pytest.mark.parametrize("env", [{"PILOSA_TOPN_SMALL_N": "63"}, {"PILOSA_TOPN_SMALL_N": "1023"},
                                  {"PILOSA_TOPN_SMALL_N": "4096"},
                                  {"PILOSA_TOPN_MID_N": "0"}, {"PILOSA_TOPN_MID_N": "512"},
-                                 {"PILOSA_TOPN_MID_N": "2048"},
-                                 {"PILOSA_TOPN_DBG": "1024"}],
+                                 {"PILOSA_TOPN_MID_N": "2048"}, {"PILOSA_TOPN_TBUILD_MIN": "65537"}],
                          ids=["small63", "small1023", "small4096", "nomid", "mid512", "mid2048", "atomicbuild"])
 def test_hot_counts_equal_dense_reference_at_every_bound(env):
     """The same check with other lane-owned and mid-size bounds and the

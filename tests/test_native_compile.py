@@ -115,6 +115,9 @@ def test_plan_count_text_matches_numpy_planner(views):
     rng = np.random.default_rng(5)
     qs = [f"Count({_gen(rng)})" for _ in range(2500)]
     qs += ["Count(Intersect(Row(f=3), Row(f=3)))", "Count(Row(f=7))", "Count(Union(Row(f=1), Row(g=9), Row(f=2)))"]
+    # repeats of one Count(Intersect(a, b)), either order: planned once
+    qs += ["Count(Intersect(Row(f=1), Row(g=2)))", "Count(Intersect(Row(g=2), Row(f=1)))",
+           "Count(Intersect(Row(f=1), Row(g=2)))"]
     fields = {"f": 0, "g": 1}
     dirs = [views["f"].rows, views["g"].rows]
     Q, segs, buf = _pql.plan_count_text("\n".join(qs), fields, dirs, True, True, 4)
@@ -122,7 +125,18 @@ def test_plan_count_text_matches_numpy_planner(views):
     raw, ok = _pql.compile_counts(qs, fields, dirs)
     want = raw.view(QPROG_DTYPE)
     seen = np.zeros(Q, bool)
+    leaves = lambda w: sorted([(int(w["leaf_view"][i]), int(w["leaf_row"][i])) for i in range(int(w["nleaf"]))])  # noqa: E731
+    assert segs[-1][0] == 5, "the repeated calls form a K_ALIAS segment"
     for kind, n, po, oo in segs:
+        if kind == 5:   # (from, to): to's answer is from's, the same unordered pair
+            frm, to = buf[po:po + n * 8].view(np.int64), buf[oo:oo + n * 8].view(np.int64)
+            assert seen[frm].all() and not seen[to].any()
+            seen[to] = True
+            for a, b in zip(frm, to):
+                assert leaves(want[a]) == leaves(want[b])
+            assert {len(qs) - 2, len(qs) - 1} <= set(int(t) for t in to) or \
+                {len(qs) - 3, len(qs) - 1} <= set(int(t) for t in to) or {len(qs) - 3, len(qs) - 2} <= set(int(t) for t in to)
+            continue
         progs = buf[po:po + n * 256].view(QPROG_DTYPE)
         order = buf[oo:oo + n * 8].view(np.int64)
         assert not seen[order].any()
