@@ -96,6 +96,23 @@ def build_httpd(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_shmring(force: bool = False, verbose: bool = False) -> str:
+    """The mesh command ring (native/shmring.cpp, POSIX shm + futex)."""
+    import pybind11
+    src = os.path.join(HERE, "shmring.cpp")
+    out = os.path.join(PKG, "_shmring" + _ext_suffix())
+    if not force and not _newer(out, [src]):
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-std=c++17", "-O2", "-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
+           "-I", sysconfig.get_paths()["include"], src, "-o", out + ".tmp", "-lrt"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build_translate(force: bool = False, verbose: bool = False) -> str:
     """Key translation store (translate.cpp), pybind11 module ``_translate``."""
     import pybind11
@@ -213,6 +230,7 @@ def build_all(force: bool = False, verbose: bool = False):
     build_pql(force, verbose)
     build_httpd(force, verbose)
     build_translate(force, verbose)
+    build_shmring(force, verbose)
     h = build_hip(force, verbose) if os.path.exists(os.path.join(KDIR, "binding.cpp")) else None
     return r, h
 

@@ -36,6 +36,11 @@ from pilosa_amd.utils import tracing
 
 
 BCAST_INLINE = 4080          # command payload bytes carried in the header broadcast
+RING_SLOTS = 64              # commands a reader may lag behind the front end
+RING_SLOT_BYTES = 1 << 18    # a Count text of ~5k calls fits one slot; longer ones follow on gloo
+RING_BIG = 1 << 40           # op flag: the payload follows on the command group
+RING_SPIN_US = 300.0         # a waiting rank spins this long before it sleeps on the futex
+RING_PUBLISH_TIMEOUT_S = 120.0
 UNION_MIN_CAP = 1024         # initial per-rank pad of a speculative union gather
 
 
@@ -81,6 +86,12 @@ class Comm:
         # never queued behind the data collectives of batches still in flight
         self.ctrl = ctrl_group
         self.ctrl_device = torch.device("cpu") if ctrl_group is not None else self.device
+        # commands through a shared-memory ring (native/shmring.cpp) once
+        # attach_ring() set it up: no TCP round trip per request, and an idle
+        # node's ranks wait without a collective timeout
+        self.ring = None
+        self.ring_reader = -1
+        self.ring_msgs = 0
 
     # ------------------------------------------------------------ guard
     def _guard(self, fn, *a, **kw):
@@ -122,9 +133,84 @@ class Comm:
             t.copy_(h)
         return t
 
+    def attach_ring(self, nslots: int = RING_SLOTS, slot_bytes: int = RING_SLOT_BYTES) -> bool:
+        """Collective on every rank (in the same order as the other setup
+        collectives): rank 0 creates the command ring in /dev/shm, names it
+        over the command group, the other ranks attach as readers, and all
+        agree (one all-reduce) that every rank could -- else every rank keeps
+        the gloo broadcast.  Returns whether the ring is in use."""
+        import os
+        import uuid
+        ring = None
+        name = ""
+        if self.rank == 0 and os.environ.get("PILOSA_MESH_RING", "1") != "0":
+            try:
+                from pilosa_amd import _shmring
+                name = f"/pilosa_mesh_{os.getpid()}_{uuid.uuid4().hex[:10]}"
+                ring = _shmring.Ring(name, True, nslots=nslots, slot_bytes=slot_bytes,
+                                     nreaders=max(0, self.world - 1))
+            except Exception:  # noqa: BLE001 - no ring: the gloo broadcast stays
+                ring, name = None, ""
+        _, got = self._bcast_bytes_group(0, name.encode())
+        name = got.decode()
+        ok = 1
+        if name and self.rank != 0:
+            try:
+                from pilosa_amd import _shmring
+                ring = _shmring.Ring(name, False)
+                ring.attach(self.rank - 1)
+            except Exception:  # noqa: BLE001 - e.g. another host: everyone falls back
+                ring, ok = None, 0
+        if not name:
+            ok = 0
+        flag = self.torch.tensor([ok], dtype=self.torch.int64)
+        if self.ctrl is not None:
+            self._guard(self.dist.all_reduce, flag, op=self.dist.ReduceOp.MIN, group=self.ctrl)
+        elif self.world > 1:
+            self.all_reduce(flag.to(self.device), op=self.dist.ReduceOp.MIN)
+            flag = flag.cpu()
+        if int(flag.item()) and ring is not None:
+            self.ring = ring
+            self.ring_reader = self.rank - 1
+            return True
+        return False
+
+    def close_ring(self):
+        """Front end: wake every reader with an error (shutdown / failover)."""
+        if self.ring is not None and self.rank == 0:
+            try:
+                self.ring.close()
+            except Exception:  # noqa: BLE001
+                pass
+
     def bcast_bytes(self, op: int = 0, payload: bytes = b"", src: int = 0):
-        """Rank ``src`` sends (op, payload); every rank returns them (on the
-        command group when there is one)."""
+        """Rank ``src`` sends (op, payload); every rank returns them: through
+        the shared-memory command ring when the node has one (a payload
+        larger than a slot follows on the command group), else on the
+        command group (gloo) or the data group."""
+        if self.ring is None or src != 0:
+            return self._bcast_bytes_group(op, payload, src)
+        if self.broken is not None:
+            raise CommError(f"communicator broken: {self.broken}")
+        try:
+            if self.rank == src:
+                big = len(payload) > self.ring.slot_bytes
+                self.ring.publish(int(op) | RING_BIG if big else int(op), b"" if big else bytes(payload),
+                                  RING_PUBLISH_TIMEOUT_S)
+                self.ring_msgs += 1
+                if big:
+                    self._bcast_bytes_group(op, payload, src)
+                return int(op), payload
+            o, data = self.ring.read(self.ring_reader, RING_SPIN_US)
+        except (RuntimeError, ValueError) as e:
+            self.broken = e
+            raise CommError(f"command ring failed: {e}") from e
+        self.ring_msgs += 1
+        if o & RING_BIG:
+            return self._bcast_bytes_group(o & ~RING_BIG, b"", src)
+        return int(o), data
+
+    def _bcast_bytes_group(self, op: int = 0, payload: bytes = b"", src: int = 0):
         torch = self.torch
         dev = self.ctrl_device
 

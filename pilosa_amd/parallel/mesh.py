@@ -98,6 +98,10 @@ class ShardMesh:
             multi = dist.get_world_size() > 1 or dist.get_backend() == "nccl"
             ctrl_group = dist.new_group(backend="gloo") if group is None and multi else None
         self.comm = Comm(group, device=device, ctrl_group=ctrl_group)
+        # commands travel through a shared-memory ring (native/shmring.cpp)
+        # when every rank can attach to it: set up collectively, here, where
+        # every rank builds its mesh in the same order
+        self.ring = self.comm.attach_ring()
         self.torch = self.comm.torch
         self.dist = self.comm.dist
         self.group = group
@@ -443,6 +447,7 @@ class ShardMesh:
             return
         self.failed_over = True
         self.failover_error = f"{type(err).__name__}: {err}"
+        self.comm.close_ring()   # ranks still waiting for a command stop
         ex = self.executor
         if getattr(ex, "mesh", None) is self:
             ex.mesh = None

@@ -132,7 +132,10 @@ def _worker(rank, world, port, outdir):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    # a short collective timeout: an idle spell longer than it (below) must
+    # not break the node -- ranks wait for commands on the shared-memory ring
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=5))
     holder = Holder(tempfile.mkdtemp(prefix=f"plain{rank}_")).open()
     holder.create_index("i").create_field("f")
     ex = Executor(holder)
@@ -182,6 +185,9 @@ def _worker(rank, world, port, outdir):
         after_one = canon(ex.execute("i", text(*reqs[1]), shards=SHARDS).results)
         retries_one = mesh.topn_plain_retries - r1
         v_front = {s: (1 if mesh.owner(s) == 0 else 2) for s in SHARDS}
+        import time
+        time.sleep(7)     # idle longer than the collective timeout
+        after_idle = canon(ex.execute("i", text(*reqs[1]), shards=SHARDS).results)
         mesh.stop()
         with open(os.path.join(outdir, "rank0.json"), "w") as fh:
             json.dump({"got": got, "want": want, "per_batch": per_batch, "refreshes": stub.refreshes,
@@ -189,7 +195,8 @@ def _worker(rank, world, port, outdir):
                        "want_all": _expected(*reqs[0], {s: _shard_counts(s, 1) for s in SHARDS}),
                        "retries_all": retries_all, "after_one": after_one,
                        "want_one": _expected(*reqs[1], {s: _shard_counts(s, v_front[s]) for s in SHARDS}),
-                       "retries_one": retries_one, "buckets": len({_nreq(ns) for ns, _ in reqs})}, fh)
+                       "retries_one": retries_one, "buckets": len({_nreq(ns) for ns, _ in reqs}),
+                       "ring": mesh.ring, "ring_msgs": mesh.comm.ring_msgs, "after_idle": after_idle}, fh)
     finally:
         ex.close()
         holder.close()
@@ -212,5 +219,9 @@ def test_mesh_plain_topn_one_collective_per_batch(tmp_path):
     assert res["retries_all"] == 0          # the front end saw its own write: refreshed before issuing
     assert res["after_one"] == res["want_one"]
     assert res["retries_one"] == 1          # rank 1's stale vote, folded into the all-reduce
+    # commands travelled through the shared-memory ring, and the node
+    # answered after idling past the collective timeout
+    assert res["ring"] and res["ring_msgs"] > 10
+    assert res["after_idle"] == res["want_one"]
     # one build per n bucket, one per write, on both ranks alike
     assert res["refreshes"] == r1["refreshes"] == res["buckets"] + 2
