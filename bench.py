@@ -245,6 +245,7 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
         # 0.3 s of the timed run
         nclients = clients if nclients is None else nclients
         done = [None] * len(texts)
+        lat = [0.0] * len(texts)       # per-request wall time (s)
         err = []
         nxt = [0]
         lock = threading.Lock()
@@ -257,7 +258,9 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
                         return
                     nxt[0] += 1
                 try:
+                    t_r = time.perf_counter()
                     done[i] = ex.execute("i", texts[i], shards=shards).results
+                    lat[i] = time.perf_counter() - t_r
                 except BaseException as e:  # noqa: BLE001
                     err.append(e)
                     return
@@ -317,7 +320,11 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
             all_reduce(elt, op=dist.ReduceOp.MAX)
         el = float(elt.item())
         last = done[-1]
+        lt = np.sort(np.asarray(lat[warm:])) * 1000
         first.update({"qps": round(B * (len(texts) - warm) / el, 2), "ms_per_request": round(el / (len(texts) - warm) * 1000, 2),
+                      "timed_requests": len(texts) - warm, "timed_s": round(el, 3),
+                      "p50_ms": round(float(lt[len(lt) // 2]), 2) if len(lt) else None,
+                      "p99_ms": round(float(lt[min(len(lt) - 1, int(len(lt) * 0.99))]), 2) if len(lt) else None,
                       "request_threads": nclients, "warm_requests": warm,
                       "sample_top3": [(p.id, p.count) for p in last[0][:3]] if last and last[0] else []})
         return done
@@ -348,12 +355,25 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
     # untimed: the first request builds the slot index; the next ones settle
     # the device allocator's segments for this phase's buffers
     WS = 3
-    hot = zipf_rows(rng, B * (nb + WS), 1000)
+    nbs = max(nb, args.topn_src_batches)   # >= 200 requests: ~2-3 s timed
+    hot = zipf_rows(rng, B * (nbs + WS), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
-    src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + WS)]
+    src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nbs + WS)]
     out["src"] = {}
     log("topn: src requests")
+    ib0 = gpu.topn_index_build_s if hasattr(gpu, "topn_index_build_s") else None
     res_src = timed(src_q, out["src"], warm=WS)
+    if ib0 is not None:
+        out["src"]["slot_index_build_s"] = round(gpu.topn_index_build_s - ib0, 3)
+    # the same requests from ONE thread (sequential latency, no overlap)
+    tq = src_q[WS:WS + 30]
+    torch.cuda.synchronize(dev)
+    t_1 = time.perf_counter()
+    for q in tq:
+        ex.execute("i", q, shards=shards)
+    torch.cuda.synchronize(dev)
+    out["src"]["single_thread_ms_per_request"] = round((time.perf_counter() - t_1) / max(len(tq), 1) * 1000, 2)
+    log(f"topn: src {out['src']}")
     log("topn: verify")
     out["device_launches"] = gpu.launches - l0
     out["batches_declined"] = ex.topn_batch_declined
@@ -1525,6 +1545,7 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
     timed([" ".join(cyc[i * B:(i + 1) * B]) for i in range(nbc + W)], out["cache_cycling"], warm=W,
           nclients=args.topn_cache_clients)
     WS = 3
+    nb = max(nb, args.topn_src_batches)
     hot = zipf_rows(rng, B * (nb + WS), 1000)
     src_calls = [f"TopN(f, Row(f={a}), n={n})" for a in hot]
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + WS)]
@@ -1701,6 +1722,8 @@ def main():
     ap.add_argument("--verify", type=int, default=64, help="queries re-derived on the host (0 = skip)")
     ap.add_argument("--topn-batches", type=int, default=40,
                     help="also time this many batches of TopN(f, Row(f=a), n=100) (0 = skip)")
+    ap.add_argument("--topn-src-batches", type=int, default=240,
+                    help="timed src TopN requests (at least --topn-batches)")
     ap.add_argument("--topn-cache-batches", type=int, default=240,
                     help="timed cache-only TopN requests (at least --topn-batches)")
     ap.add_argument("--topn-batch", type=int, default=16, help="TopN queries per batch")

@@ -936,7 +936,8 @@ class DeviceView:
 
         import torch
 
-        if self.SHADOW_ROWS <= 0 or self.device.type != "cuda" or not self.S or not self.D:
+        if self.SHADOW_ROWS <= 0 or self.device.type != "cuda" or not self.S or not self.D or \
+                not hasattr(kernels(), "shadow_build"):
             return False
         sh = getattr(self, "_shadow", None)
         if sh is not None and sh[0] == self.generation:

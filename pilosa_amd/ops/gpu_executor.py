@@ -168,6 +168,8 @@ class GpuExecutor:
         self.text_prep_s = 0.0
         self.text_wait_s = 0.0
         self.topn_index_refreshes = 0   # slot indexes brought up to date in place after writes
+        self.topn_index_builds = 0      # full slot-index builds, and their wall time (synchronised)
+        self.topn_index_build_s = 0.0
         self.topn_index_batches = 0     # src TopN batches / calls answered by a slot index
         self.rebuilds = 0        # full view uploads
         self.shard_updates = 0   # in-place shard segment rewrites
@@ -1643,10 +1645,16 @@ class GpuExecutor:
             self._topn_index_why = "too many slots"
             return None
         self._topn_indexes.pop(key, None)   # free the old index's HBM before building
+        t_b = time.perf_counter()
         try:
             tix = DeviceTopNIndex(rv, rc, space=space)
         except ValueError:
             return None
+        if self.device.type == "cuda":
+            import torch
+            torch.cuda.synchronize(self.device)
+        self.topn_index_build_s += time.perf_counter() - t_b
+        self.topn_index_builds += 1
         if not tix.ok:
             return None
         self._topn_indexes[key] = (rc, tix, now)

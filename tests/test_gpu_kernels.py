@@ -386,8 +386,14 @@ def test_partial_sum_scatter_matches_torch(U, n):
 def test_dense_shadows_match_arena_containers():
     """shadow_build_kernel: every shadowed (row, shard, key) is the row's
     container of that key as a bitmap (zeros where the row has none); rows are
-    the hottest by bit count; a write leaves the shadow stale (not passed)."""
+    the hottest by bit count; a write leaves the shadow stale (not passed).
+    Dense shadows measured slower and ship in the kbench module only
+    (PILOSA_HIPKERNELS=_hipkernels_kbench runs this test)."""
     import torch
+
+    from pilosa_amd.ops.device import kernels
+    if not hasattr(kernels(), "shadow_build"):
+        pytest.skip("dense shadows are built into the kbench module only")
 
     from pilosa_amd.ops.device import DeviceView
     rng = np.random.default_rng(5)
