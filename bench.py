@@ -1443,6 +1443,8 @@ def run_disk_mesh(args, world, rank, dev, queries, ra, rb):
             extra["verify"] = {"queries": n, "shards_checked": len(sel), "mismatch_shard_counts": bad,
                                "answered_by": "owner rank through the mesh", "verified": bad == 0,
                                "verified_all_ranks": bad == 0}
+        if args.mesh_breakdown > 0:
+            extra["mesh_breakdown"] = mesh_breakdown(args, ex, mesh, all_shards, queries)
         if args.topn_batches > 0:
             extra["topn"] = bench_topn_mesh(args, ex, mesh, all_shards)
         mesh.stop()
@@ -1454,6 +1456,53 @@ def run_disk_mesh(args, world, rank, dev, queries, ra, rb):
             holder.close()
         if args.data_dir is None and not args.keep_data:
             shutil.rmtree(base, ignore_errors=True)
+
+
+def mesh_breakdown(args, ex, mesh, all_shards, queries):
+    """Where a mesh request's time goes on the front end:
+    ``--mesh-breakdown N`` sequential Count batches and cache-only TopN
+    requests under a HIP-event tracer; per span name the mean host ms per
+    request and, for GPU spans, the mean device ms between the span's events
+    (command publish, native compile/plan, kernel launch, collective issue
+    and wait, D2H)."""
+    from pilosa_amd.utils import tracing
+    n = args.mesh_breakdown
+    B = args.batch
+    texts = [" ".join(queries[i * B:(i + 1) * B]) for i in range(min(n, len(queries) // B))]
+    topn = [" ".join(_wide_topn_calls(args.topn_batch, seed=900 + i)) for i in range(n)]
+    for t in topn[:2]:      # their node candidate spaces (n buckets) built untimed
+        ex.execute("i", t, shards=all_shards)
+    out = {}
+    for kind, reqs in (("count", texts), ("topn_cache", topn)):
+        if not reqs:
+            continue
+        tr = tracing.HipEventTracer(limit=200000)
+        tracing.set_global_tracer(tr)
+        try:
+            mesh.sync()
+            t0 = time.perf_counter()
+            for r in reqs:
+                ex.execute("i", r, shards=all_shards)
+            mesh.sync()
+            wall = time.perf_counter() - t0
+        finally:
+            tracing.set_global_tracer(tracing.NopTracer())
+        agg = {}
+        for sp in tr.spans:
+            a = agg.setdefault(sp.name, [0, 0.0, 0.0, 0])
+            a[0] += 1
+            a[1] += sp.duration * 1000
+            dm = sp.device_ms(wait=True)
+            if dm is not None:
+                a[2] += dm
+                a[3] += 1
+        k = len(reqs)
+        out[kind] = {"requests": k, "wall_ms_per_request": round(wall / k * 1000, 3),
+                     "spans": {name: {"per_request": round(c / k, 2), "host_ms": round(h / k, 4),
+                                      **({"device_ms": round(d / k, 4)} if nd else {})}
+                               for name, (c, h, d, nd) in sorted(agg.items(), key=lambda kv: -kv[1][1])}}
+    log(f"mesh breakdown: {json.dumps(out)[:2000]}")
+    return out
 
 
 def bench_topn_mesh(args, ex, mesh, all_shards):
@@ -1512,11 +1561,26 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
                                     daemon=True)
             prof.start()
         t_a = mesh.sync()
-        ts = [threading.Thread(target=client) for _ in range(max(1, nclients))]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+        cprof = os.environ.get("PILOSA_BENCH_CPROFILE", "") if profile else ""
+        if cprof and max(1, nclients) == 1:
+            # deterministic profile of the one request thread (host cost per call)
+            import cProfile
+            import io
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            client()
+            pr.disable()
+            sio = io.StringIO()
+            pstats.Stats(pr, stream=sio).sort_stats("cumulative").print_stats(70)
+            with open(cprof, "w") as fh:
+                fh.write(sio.getvalue())
+        else:
+            ts = [threading.Thread(target=client) for _ in range(max(1, nclients))]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
         t_b = mesh.sync()
         if err:
             raise err[0]
@@ -1742,6 +1806,8 @@ def main():
     ap.add_argument("--import-shards", type=int, default=64, help="serving phase: shards of the HTTP bulk import")
     ap.add_argument("--import-bits-per-shard", type=int, default=200_000)
     ap.add_argument("--import-clients", type=int, default=8)
+    ap.add_argument("--mesh-breakdown", type=int, default=0,
+                    help="mesh mode: trace this many Count and cache-only TopN requests (per-span time split)")
     ap.add_argument("--mesh", action="store_true",
                     help="run the multi-GPU product path (ShardMesh over RCCL, one rank per GPU) even at --gpus 1")
     ap.add_argument("--cpu-baseline-shards", type=int, default=0,

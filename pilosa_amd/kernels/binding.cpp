@@ -5,6 +5,9 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <cstring>
+#include <mutex>
+
 #include "kernels.h"
 
 namespace {
@@ -23,6 +26,48 @@ hipStream_t cur_stream(const torch::Tensor& t) {
 void check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
   TORCH_CHECK(e == hipSuccess, what, ": kernel launch failed: ", hipGetErrorString(e));
+}
+
+// Small host int32 arrays (a batch's parameters) -> a new device tensor on
+// the current stream, staged through a ring of pinned slots: one memcpy and
+// one async H2D, no allocator or Python on the way.  A slot is rewritten only
+// once the event recorded behind its previous copy has fired.
+torch::Tensor upload_i32(torch::Tensor host, int64_t device) {
+  TORCH_CHECK(!host.is_cuda() && host.scalar_type() == torch::kInt32 && host.is_contiguous(), "host int32[]");
+  constexpr int NSLOT = 64;
+  constexpr size_t SLOT_BYTES = 16384;
+  static std::mutex mu;
+  static char* ring = nullptr;
+  static hipEvent_t ev[NSLOT];
+  static bool used[NSLOT];
+  static int next = 0;
+  const size_t nb = size_t(host.numel()) * 4;
+  auto out = torch::empty({host.numel()}, torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device));
+  if (nb == 0) return out;
+  const hipStream_t st = at::hip::getCurrentHIPStream(int(device)).stream();
+  if (nb > SLOT_BYTES) {   // large: pageable copy (rare)
+    TORCH_CHECK(hipMemcpyAsync(out.data_ptr(), host.data_ptr(), nb, hipMemcpyHostToDevice, st) == hipSuccess,
+                "upload_i32 copy");
+    return out;
+  }
+  std::lock_guard<std::mutex> g(mu);
+  if (ring == nullptr) {
+    TORCH_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ring), NSLOT * SLOT_BYTES, hipHostMallocDefault) ==
+                    hipSuccess, "upload_i32 pinned ring");
+    for (int i = 0; i < NSLOT; i++) {
+      TORCH_CHECK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess, "upload_i32 event");
+      used[i] = false;
+    }
+  }
+  const int k = next;
+  next = (next + 1) % NSLOT;
+  if (used[k]) TORCH_CHECK(hipEventSynchronize(ev[k]) == hipSuccess, "upload_i32 slot wait");
+  char* slot = ring + size_t(k) * SLOT_BYTES;
+  std::memcpy(slot, host.data_ptr(), nb);
+  TORCH_CHECK(hipMemcpyAsync(out.data_ptr(), slot, nb, hipMemcpyHostToDevice, st) == hipSuccess, "upload_i32 copy");
+  TORCH_CHECK(hipEventRecord(ev[k], st) == hipSuccess, "upload_i32 record");
+  used[k] = true;
+  return out;
 }
 
 void expr_count(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tensor out,
@@ -670,6 +715,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_counts", &row_counts, "row counts of (shard, dense row) entries (device rank caches)");
   m.def("topn_cache_counts", &topn_cache_counts, "cache-only TopN: [candidate x shard] row counts");
   m.def("topn_cache_batch", &topn_cache_batch, "cache-only TopN batch: membership, totals, per-query top-n");
+  m.def("upload_i32", &upload_i32, "small host int32 array -> device through a pinned ring (current stream)");
   m.def("topn_cache_partial", &topn_cache_partial, "mesh cache-only TopN: one rank's membership + partial totals");
   m.def("topn_cache_select32", &topn_cache_select32, "mesh cache-only TopN: per-query top-n of the reduced buffer");
   m.def("row_counts_sum", &row_counts_sum, "ids= re-count without src: per id the sum of shard row counts >= threshold");

@@ -1126,18 +1126,27 @@ class GpuExecutor:
 
     def plain_cand_state(self, index: str, fname: str, shards: List[int], skey, nreq: int):
         """Front end, before issuing a batch, no collective: (generation, U,
-        fused-path fits) of the node candidate space when this rank's copy is
-        current, None when it must be refreshed first."""
-        ent = self._plain_cands.get((index, fname, skey, nreq))
-        if ent is None:
-            return None
+        fused-path fits, bucket) of a current node candidate space that
+        serves a batch needing the first ``nreq`` ranks -- that bucket's own,
+        else the smallest built longer one (the membership kernel stops each
+        call at its own n, so a longer prefix gives the same answers: a
+        stream of varied n builds one space, as the 1-GPU memos do) -- or
+        None when one must be built first."""
         try:
             rc = self._plain_rc(index, fname, shards, skey)[1] if shards else None
         except Exception:  # noqa: BLE001 - the refresh reports it node-wide
             return None
-        if ent[1] != (rc.serial if rc is not None else None):
-            return None
-        return ent[0], len(ent[3]), ent[2]
+        serial = rc.serial if rc is not None else None
+        best = None
+        for (i2, f2, k2, b), ent in self._plain_cands.items():
+            if i2 != index or f2 != fname or k2 != skey or ent[1] != serial:
+                continue
+            if b == nreq or (nreq != 0 and (b == 0 or b > nreq)):
+                if best is None or (b != 0 and (best[3] == 0 or b < best[3])) or b == nreq:
+                    best = (ent[0], len(ent[3]), ent[2], b)
+                    if b == nreq:
+                        break
+        return best
 
     def refresh_plain_cand(self, index: str, fname: str, shards: List[int], skey, nreq: int, gen: int, comm):
         """Collective on every rank: all-gather each rank's local candidate

@@ -178,6 +178,27 @@ def _select_from_buffer(buf, Q: int, T: int, U: int, q: int, t: int, lim: int) -
     return h[h >= 0]
 
 
+_TL = threading.local()
+
+
+def _to_host_pinned(t) -> np.ndarray:
+    """Device tensor -> numpy through a per-thread pinned buffer and a wait on
+    the current stream only (a pageable .cpu() goes through a blit kernel and
+    a device-wide wait).  The array is valid until this thread's next call."""
+    import torch
+    if t.device.type != "cuda":
+        return t.cpu().numpy()
+    n = t.numel()
+    hb = getattr(_TL, "hb", None)
+    if hb is None or hb.numel() < n or hb.dtype != t.dtype:
+        hb = torch.empty(max(n, 4096), dtype=t.dtype, pin_memory=True)
+        _TL.hb = hb
+    h = hb[:n]
+    h.copy_(t.reshape(-1), non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return h.numpy().reshape(t.shape)
+
+
 def cache_partial_ref(cnt, nmax: int, nlim: int, inv, cm, prm, Q: int, T: int, U: int, buf) -> None:
     """PyTorch reference of topn_cache_partial (kernels/topn_kernels.hip) for
     the mesh buffer [member bytes | int32 totals[T, U] | flags[2]]: the CPU
@@ -266,7 +287,8 @@ def mesh_cache_batch(rc: Optional["DeviceRankCaches"], ns: Sequence[int], thresh
     prm[2 * Q:3 * Q] = [tix[t] for t in ths]
     prm[3 * Q:4 * Q] = [n if n else KK for n in nn]
     prm[4 * Q:] = uniq_t
-    prm_d = torch.from_numpy(prm).to(dev, non_blocking=True)
+    prm_d = kernels().upload_i32(torch.from_numpy(prm), dev.index or 0) if dev.type == "cuda" else \
+        torch.from_numpy(prm)
     mw = (Q * U + 3) // 4
     buf = torch.empty(mw + T * U + 2, dtype=torch.int32, device=dev)
     part = cand is not None and not stale and not declined and rc is not None and cand.nmax > 0 and rc.S > 0
@@ -297,17 +319,26 @@ def mesh_cache_batch(rc: Optional["DeviceRankCaches"], ns: Sequence[int], thresh
             kernels().topn_cache_select32(buf, ids, prm_d, Q, T, out)
         else:
             out = cache_select_ref(buf, ids, prm_d, Q, T, KK)
-        h = out.cpu().numpy()
+        h = _to_host_pinned(out)
         if Q and h[0, 0] <= -3:
             return "declined" if h[0, 0] == -4 else "stale"
-        res: List[List[Pair]] = []
-        for q in range(Q):
-            if h[q, 0] < 0:     # more members than one workgroup sorts: torch over the reduced buffer
-                r = _select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
-            else:
-                r = h[q, 1:1 + int(h[q, 0])]
-            j = (0xFFFFFFFF - (r & 0xFFFFFFFF)).astype(np.int64)
-            res.append(pair_array(space[j] if len(j) else np.zeros(0, np.uint64), r >> 32))
+        lens = h[:, 0]
+        if (lens < 0).any():    # more members than one workgroup sorts: torch over the reduced buffer
+            parts = [_select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
+                     if lens[q] < 0 else h[q, 1:1 + int(lens[q])] for q in range(Q)]
+            ln = [len(r) for r in parts]
+        else:
+            ln = lens.tolist()
+            parts = [h[q, 1:1 + n] for q, n in enumerate(ln)]
+        # every query's kept keys end to end, decoded in one pass, then split
+        # (as the 1-GPU batch decodes: _topn_nosrc_fused_on)
+        keys = np.concatenate(parts) if Q else np.zeros(0, np.int64)
+        rid = space[0xFFFFFFFF - (keys & 0xFFFFFFFF)] if len(keys) else np.zeros(0, np.uint64)
+        cnt = keys >> 32
+        res, o = [], 0
+        for n in ln:
+            res.append(pair_array(rid[o:o + n], cnt[o:o + n]))
+            o += n
         return res
     pend = Pending(comm, comm.all_reduce_async(buf), finish, keep=(buf, prm_d))
     return pend if defer else pend.result()

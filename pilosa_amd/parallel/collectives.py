@@ -195,8 +195,13 @@ class Comm:
         try:
             if self.rank == src:
                 big = len(payload) > self.ring.slot_bytes
-                self.ring.publish(int(op) | RING_BIG if big else int(op), b"" if big else bytes(payload),
-                                  RING_PUBLISH_TIMEOUT_S)
+                if tracing.enabled():
+                    with tracing.span("Comm.command", ranks=self.world, bytes=len(payload)):
+                        self.ring.publish(int(op) | RING_BIG if big else int(op), b"" if big else bytes(payload),
+                                          RING_PUBLISH_TIMEOUT_S)
+                else:
+                    self.ring.publish(int(op) | RING_BIG if big else int(op), b"" if big else bytes(payload),
+                                      RING_PUBLISH_TIMEOUT_S)
                 self.ring_msgs += 1
                 if big:
                     self._bcast_bytes_group(op, payload, src)

@@ -333,10 +333,10 @@ class ShardMesh:
                 st = gpu.plain_cand_state(index, fname, own, sid, nreq)
                 if st is None:
                     return None
-            gen, U, fits = st
+            gen, U, fits, bucket = st
             if not fits:
                 return None
-            res = self._run_pipelined(OP_TOPN_PLAIN, index, fname, ns, ths, sid, nreq, gen, U)
+            res = self._run_pipelined(OP_TOPN_PLAIN, index, fname, ns, ths, sid, bucket, gen, U)
             if isinstance(res, str):
                 if res == "stale" and attempt == 0:
                     self.topn_plain_retries += 1

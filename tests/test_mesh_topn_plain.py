@@ -223,5 +223,6 @@ def test_mesh_plain_topn_one_collective_per_batch(tmp_path):
     # answered after idling past the collective timeout
     assert res["ring"] and res["ring_msgs"] > 10
     assert res["after_idle"] == res["want_one"]
-    # one build per n bucket, one per write, on both ranks alike
-    assert res["refreshes"] == r1["refreshes"] == res["buckets"] + 2
+    # at most one build per n bucket (a longer built space serves a shorter
+    # prefix) and one per write, on both ranks alike
+    assert res["refreshes"] == r1["refreshes"] <= res["buckets"] + 2
