@@ -48,6 +48,25 @@ class CommError(RuntimeError):
     """A collective failed or timed out; the mesh must fail over."""
 
 
+class GatherParts(list):
+    """The per-rank tensors of a fixed-capacity gather, with the largest
+    rank's length (the caller's capacity policy reads it)."""
+
+    def __init__(self, parts, longest: int):
+        super().__init__(parts)
+        self.longest = int(longest)
+
+
+class Overflow:
+    """A speculative fixed-capacity gather some rank did not fit into:
+    ``need`` words would have (Comm.all_gather_cap_async)."""
+
+    __slots__ = ("need",)
+
+    def __init__(self, need: int):
+        self.need = int(need)
+
+
 class MeshVote(Exception):
     """Some rank voted against a batch inside one of its data collectives
     (``Comm.union(vote=)``): every rank raises it after the same collective,
@@ -311,6 +330,41 @@ class Comm:
             return Pending(self, None, lambda: [x[:k].to(t.device) for x, k in zip(ho, lens)])
         work = self._guard(self.dist.all_gather, outs, pad, group=self.group, async_op=True)
         return Pending(self, work, lambda: [x[:k] for x, k in zip(outs, lens)], keep=(pad, outs))
+
+    def all_gather_cap_async(self, t, cap: int) -> "Pending":
+        """Variable-length 1-D int64 tensors of every rank in ONE all-gather
+        with no size exchange first: each rank sends ``[len, values...,
+        padding]`` padded to ``cap`` words (the capacity comes from the
+        command, so every rank pads alike), or ``[-len]`` when its tensor does
+        not fit.  The pending result is the list of per-rank tensors, or an
+        :class:`Overflow` naming the capacity that would fit -- the caller
+        re-issues the whole operation with it (one more command, never a
+        collective inside a completion)."""
+        torch = self.torch
+        t = t.reshape(-1).to(torch.int64)
+        n = int(t.numel())
+        cap = max(1, int(cap))
+        buf = torch.zeros(cap + 1, dtype=torch.int64, device=t.device)
+        if n <= cap:
+            buf[0] = n
+            if n:
+                buf[1:1 + n] = t
+        else:
+            buf[0] = -n
+        out = torch.empty(self.world * (cap + 1), dtype=torch.int64, device=t.device)
+
+        def finish(ho):
+            ho = ho.view(self.world, cap + 1)
+            lens = ho[:, 0].cpu().numpy()
+            if len(lens) and int(lens.min()) < 0:
+                return Overflow(int(np.abs(lens).max()))
+            return GatherParts([ho[r, 1:1 + int(k)] for r, k in enumerate(lens)], int(lens.max()) if len(lens) else 0)
+        if self.host_copies:   # gloo rehearsal of a GPU run: host copies, synchronous
+            ho = self._on(out)
+            self._guard(self.dist.all_gather_into_tensor, ho, self._on(buf), group=self.group)
+            return Pending(self, None, lambda: finish(ho))
+        work = self._guard(self.dist.all_gather_into_tensor, out, buf, group=self.group, async_op=True)
+        return Pending(self, work, lambda: finish(out), keep=(buf, out))
 
     def union(self, t, tag: str = "union", vote: int = 0):
         """Sorted distinct values of int64 ``t`` over all ranks (the same on

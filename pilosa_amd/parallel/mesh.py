@@ -60,6 +60,7 @@ class MeshError(RuntimeError):
  OP_ERRORS, OP_TOPN, OP_SYNC, OP_RECALC, OP_TOPN_PLAIN, OP_TOPN_CAND, OP_SHARDSET, OP_TOPN_SPACES) = range(18)
 MAX_IN_FLIGHT = 4     # count batches a worker keeps in flight before it waits for the oldest
 MAX_SHARD_SETS = 4096  # shard lists registered with the ranks (OP_SHARDSET); more go the general way
+CALL_MIN_CAP = 1024    # int64 words per rank of a general call's partial gather (grows per call name)
 # bitmap calls whose rank partial can travel as device container blocks
 _ROW_CALLS = ("Row", "Range", "Bitmap", "Intersect", "Union", "Difference", "Xor", "Not", "Shift")
 _OP_NAMES = {OP_STOP: "stop", OP_COUNT: "count", OP_CALL: "call", OP_WRITE: "write", OP_IMPORT: "import",
@@ -137,6 +138,8 @@ class ShardMesh:
         self.topn_plain_batches = 0
         self.topn_plain_refreshes = 0
         self.topn_plain_retries = 0
+        self._call_cap: Dict[str, int] = {}          # OP_CALL gather capacity per call name (front end)
+        self.call_retries = 0
 
     # ------------------------------------------------------------ ownership
     def owner(self, shard: int) -> int:
@@ -177,9 +180,25 @@ class ShardMesh:
     def map_local(self, index: str, c, shards: Sequence[int], opt, reduce_fn: Callable[[Any, Any], Any]):
         """Execute call ``c`` over ``shards`` on their owner ranks and fold the
         partial results with ``reduce_fn`` (the executor's reduce step)."""
+        from .collectives import Overflow
         if c.name == "Count":
             return self._run(OP_COUNT, index, [str(c)], list(shards))[0]
-        parts = self._run_pipelined(OP_CALL, index, str(c), list(shards), _opt_dict(opt))
+        pql, optd = str(c), _opt_dict(opt)
+        while True:
+            # the partials travel in ONE fixed-capacity all-gather (no size
+            # exchange, no host read before the data moves); the capacity is
+            # learnt per call name and carried in the command
+            cap, quiet = self._call_cap.get(c.name, (CALL_MIN_CAP, 0))
+            parts = self._run_pipelined(OP_CALL, index, pql, list(shards), optd, cap)
+            if not isinstance(parts, Overflow):
+                break
+            self.call_retries += 1
+            self._call_cap[c.name] = (1 << int(parts.need + parts.need // 4).bit_length(), 0)
+        # a capacity far above what the call sends is halved after a quiet
+        # spell (a one-off large Row result does not pad every later one)
+        longest = getattr(self, "_call_longest", 0)
+        if cap > CALL_MIN_CAP and longest * 8 < cap:
+            self._call_cap[c.name] = (cap // 2, 0) if quiet >= 15 else (cap, quiet + 1)
         _raise_remote(parts)
         result = None
         for p in parts:
@@ -600,17 +619,26 @@ class ShardMesh:
             return self._topn_plain_local(*args)
         if op != OP_CALL:
             raise MeshError(f"mesh command {op!r} is not pipelined")
-        index, pql, shards, optd = args
+        index, pql, shards, optd, cap = args
         try:
             mine = self._local_call(index, pql, self.owned(shards), optd)
         except Exception as e:  # noqa: BLE001 - reported through the gather below
             mine = e
         from pilosa_amd.ops.device import DeviceRowBlock
+
+        from .collectives import Overflow
         if isinstance(mine, DeviceRowBlock):
             t = encode_row_block(mine, self.device)
         else:
             t = self.torch.from_numpy(encode_partial(mine)).to(self.device)
-        return _Chain(self.comm.all_gather_var_async(t), lambda ps: [decode_partial(p.cpu().numpy()) for p in ps])
+
+        def decode(ps):
+            if isinstance(ps, Overflow):
+                return ps
+            out = [decode_partial(p.cpu().numpy()) for p in ps]
+            self._call_longest = getattr(ps, "longest", 0)
+            return out
+        return _Chain(self.comm.all_gather_cap_async(t, int(cap)), decode)
 
     def _refresh_spaces(self, index: str, fnames: List[str], own: List[int], vote: bool = True):
         """Collective refresh of the node row spaces of a TopN batch: every

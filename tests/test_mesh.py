@@ -352,3 +352,74 @@ def test_mesh_general_calls_pipelined(tmp_path):
     res = json.load(open(tmp_path / "calls.json"))
     assert all(res["ok"]), res["ok"]
     assert res["max_in_flight"] >= 2, res["max_in_flight"]
+
+
+def _call_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    from pilosa_amd.parallel.mesh import ShardMesh
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    holder = Holder(tempfile.mkdtemp(prefix=f"call{rank}_")).open()
+    ex = Executor(holder)
+    mesh = ShardMesh(ex, block=1)
+    ex.mesh = mesh
+    try:
+        if rank != 0:
+            mesh.serve()
+            return
+        _setup_schema(holder)
+        mesh.apply_schema()
+        bits, vals = _data()
+        _load(ex, bits, vals, mesh)
+        per_call = {}
+        for q in ("Sum(field=v)", "Rows(f)", "Row(f=1)", "Max(Row(f=2), field=v)", "GroupBy(Rows(f), Rows(g))"):
+            ex.execute("i", q)                 # learns the call's gather capacity
+            c0 = mesh.comm.data_calls
+            got = _canon(ex.execute("i", q).results)
+            per_call[q] = [mesh.comm.data_calls - c0, got]
+        # a capacity far too small: the ranks' partials overflow it, the front
+        # end re-issues the call once with a capacity that fits
+        mesh._call_cap["Row"] = (4, 0)
+        r0 = mesh.call_retries
+        big = _canon(ex.execute("i", "Row(f=1)").results)
+        retries = mesh.call_retries - r0
+        c0 = mesh.comm.data_calls
+        again = _canon(ex.execute("i", "Row(f=1)").results)
+        with open(os.path.join(outdir, "calls.json"), "w") as fh:
+            json.dump({"per_call": per_call, "big": big, "retries": retries, "again": again,
+                       "again_calls": mesh.comm.data_calls - c0}, fh)
+        mesh.stop()
+    finally:
+        ex.close()
+        holder.close()
+        dist.destroy_process_group()
+
+
+def test_general_call_is_one_speculative_gather(tmp_path):
+    """a general call's partials travel in ONE
+    fixed-capacity all-gather -- no size all-gather, no host read before the
+    data moves; a rank whose partial does not fit says so inside that gather
+    and the front end re-issues the call with a capacity that fits."""
+    mp.start_processes(_call_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    res = json.load(open(tmp_path / "calls.json"))
+    from pilosa_amd.executor import Executor
+    from pilosa_amd.models.holder import Holder
+    holder = Holder(tempfile.mkdtemp(prefix="call_ref_")).open()
+    ex = Executor(holder)
+    _setup_schema(holder)
+    bits, vals = _data()
+    _load(ex, bits, vals)
+    for q, (ncoll, got) in res["per_call"].items():
+        assert ncoll == 1, (q, ncoll)
+        assert got == _canon(ex.execute("i", q).results), q
+    want_row = _canon(ex.execute("i", "Row(f=1)").results)
+    ex.close()
+    holder.close()
+    assert res["retries"] == 1 and res["big"] == want_row
+    assert res["again"] == want_row and res["again_calls"] == 1
