@@ -602,7 +602,7 @@ void expr_dense(torch::Tensor progs, torch::Tensor views, int64_t S, torch::Tens
 }
 
 void shift_dense(torch::Tensor src, int64_t S, int64_t n, torch::Tensor main_out, torch::Tensor main_meta,
-                 torch::Tensor spill_out, torch::Tensor spill_meta, int64_t M) {
+                 torch::Tensor spill_out, torch::Tensor spill_meta, int64_t M, int64_t row_words) {
   for (auto* t : {&src, &main_out, &spill_out}) {
     check_dev(*t, "shift payload");
     TORCH_CHECK(t->scalar_type() == torch::kInt16 && t->numel() == S * 16 * 4096, "shift payload int16[S*16*4096]");
@@ -612,10 +612,12 @@ void shift_dense(torch::Tensor src, int64_t S, int64_t n, torch::Tensor main_out
     TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() == S * 16, "shift meta int64[S*16]");
   }
   TORCH_CHECK(M >= 1 && S % M == 0, "shift: S must be a whole number of M-sub-shard shards");
-  TORCH_CHECK(n > 0 && n < (M << 20), "shift needs 0 < n < the shard width (M * 2^20)");
+  TORCH_CHECK(row_words >= 1024 && row_words <= M * 16384 && (row_words & 1023) == 0,
+              "shift: row_words = the shard's width in 64-bit words (whole containers)");
+  TORCH_CHECK(n > 0 && n < row_words * 64, "shift needs 0 < n < the shard width");
   auto u64 = [](torch::Tensor& t) { return reinterpret_cast<uint64_t*>(t.data_ptr<int16_t>()); };
-  pk::launch_shift_dense(u64(src), int(S), int(M), n, u64(main_out), main_meta.data_ptr<int64_t>(), u64(spill_out),
-                         spill_meta.data_ptr<int64_t>(), cur_stream(src));
+  pk::launch_shift_dense(u64(src), int(S), int(M), n, row_words, u64(main_out), main_meta.data_ptr<int64_t>(),
+                         u64(spill_out), spill_meta.data_ptr<int64_t>(), cur_stream(src));
   check_launch("shift_dense");
 }
 
@@ -728,7 +730,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("expr_dense", &expr_dense, "evaluate expressions into dense one-row views (bitmap per shard/key)");
   m.def("shift_dense", &shift_dense, "Shift a dense view by n columns per shard (main + next-shard spill)",
         py::arg("src"), py::arg("S"), py::arg("n"), py::arg("main_out"), py::arg("main_meta"), py::arg("spill_out"),
-        py::arg("spill_meta"), py::arg("M") = 1);
+        py::arg("spill_meta"), py::arg("M") = 1, py::arg("row_words") = 16384);
   m.def("rows_list", &rows_list, "flag dense rows with non-empty containers (optionally holding one column)");
   m.def("container_merge", &container_merge, "device write path: old container + delta -> bitmap + cardinality");
   m.def("payload_compact", &payload_compact, "copy live containers into a compacted payload buffer");

@@ -181,8 +181,8 @@ void launch_expr_dense(const QueryProg* progs, int Q, const ViewDev* views, int 
 // Shift a dense view (u64[S][16384]) up by n (0 < n < 2^20) columns per shard:
 // main_out = bits that stay in the shard, spill_out = bits carried into the
 // next shard (both dense, with metadata like launch_expr_dense).
-void launch_shift_dense(const uint64_t* src, int S, int M, int64_t n, uint64_t* main_out, int64_t* main_meta,
-                        uint64_t* spill_out, int64_t* spill_meta, hipStream_t st);
+void launch_shift_dense(const uint64_t* src, int S, int M, int64_t n, int64_t row_words, uint64_t* main_out,
+                        int64_t* main_meta, uint64_t* spill_out, int64_t* spill_meta, hipStream_t st);
 // Rows listing: flags[d] = 1 for dense rows with a non-empty container in
 // shards [s0, s0 + ns) (j >= 0: only rows whose key-j container holds col16).
 void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_t* flags, hipStream_t st);

@@ -38,7 +38,12 @@ constexpr int SHARD_WORDS = 16 * 1024;
 // sub-shard's end lands in the next sub-shard of the same shard; only words
 // carried past the SHARD's end form the spill, whose sub-shard m part
 // belongs to sub-shard m of the next shard.  M = 1 at widths <= 2^20.
+// row_words = the host shard's width in words: M * 16384 from 2^20 columns
+// up, 2^e / 64 for a narrower 2^e-column shard, which fills only the first
+// 2^(e-16) containers of its device shard -- words carried past 2^e columns
+// form its spill, and the device containers past it stay empty.
 __global__ __launch_bounds__(256) void shift_dense_kernel(const uint64_t* __restrict__ src, int S, int M, int64_t n,
+                                                          int64_t row_words,
                                                           uint64_t* __restrict__ main_out,
                                                           int64_t* __restrict__ main_meta,
                                                           uint64_t* __restrict__ spill_out,
@@ -52,21 +57,22 @@ __global__ __launch_bounds__(256) void shift_dense_kernel(const uint64_t* __rest
   const int64_t nw = n >> 6;
   const int sh = int(n & 63);
   const int m = s % M;
-  const int64_t row_words = int64_t(M) * SHARD_WORDS;            // the whole shard's row
   const uint64_t* sp = src + int64_t(s - m) * SHARD_WORDS;        // its first sub-shard
   uint64_t* dst = (half ? spill_out : main_out) + int64_t(s) * SHARD_WORDS + k * 1024;
-  // target word t of this wave, counted from the shard's first word (the
-  // spill continues past the shard's end)
-  const int64_t t0 = int64_t(half) * row_words + int64_t(m) * SHARD_WORDS + k * 1024;
+  // word of this wave within the shard's row, and the target word counted
+  // from the shard's first word (the spill continues past the shard's end)
+  const int64_t l0 = int64_t(m) * SHARD_WORDS + k * 1024;
+  const int64_t t0 = int64_t(half) * row_words + l0;
   int c = 0;
 #pragma unroll 4
   for (int i = 0; i < 16; i++) {
     const int w = i * 64 + lane;
     const int64_t a = t0 + w - nw;
-    const uint64_t x = (a >= 0 && a < row_words) ? sp[a] : 0ull;
+    const bool in = l0 + w < row_words;                           // inside a narrow shard's width
+    const uint64_t x = (in && a >= 0 && a < row_words) ? sp[a] : 0ull;
     uint64_t r = x;
     if (sh) {
-      const uint64_t y = (a - 1 >= 0 && a - 1 < row_words) ? sp[a - 1] : 0ull;
+      const uint64_t y = (in && a - 1 >= 0 && a - 1 < row_words) ? sp[a - 1] : 0ull;
       r = (x << sh) | (y >> (64 - sh));
     }
     dst[w] = r;
@@ -133,12 +139,12 @@ __global__ __launch_bounds__(256) void rows_kernel(ViewDev v, int s0, int ns, in
 
 }  // namespace
 
-void launch_shift_dense(const uint64_t* src, int S, int M, int64_t n, uint64_t* main_out, int64_t* main_meta,
-                        uint64_t* spill_out, int64_t* spill_meta, hipStream_t st) {
+void launch_shift_dense(const uint64_t* src, int S, int M, int64_t n, int64_t row_words, uint64_t* main_out,
+                        int64_t* main_meta, uint64_t* spill_out, int64_t* spill_meta, hipStream_t st) {
   const int64_t waves = int64_t(S) * 32;
-  if (waves == 0 || M <= 0 || S % M) return;
-  hipLaunchKernelGGL(shift_dense_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, src, S, M, n, main_out,
-                     main_meta, spill_out, spill_meta);
+  if (waves == 0 || M <= 0 || S % M || row_words <= 0 || row_words > int64_t(M) * SHARD_WORDS) return;
+  hipLaunchKernelGGL(shift_dense_kernel, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, src, S, M, n, row_words,
+                     main_out, main_meta, spill_out, spill_meta);
 }
 
 void launch_rows(const ViewDev& v, int s0, int ns, int j, uint32_t col16, uint8_t* flags, hipStream_t st) {

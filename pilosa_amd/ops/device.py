@@ -1551,7 +1551,9 @@ class GpuEngine:
         that stays in each shard, and the spill each shard carries into the
         next shard's segment (row.go:217-239, roaring.go:944-977).  Above
         2^20 columns a shard's device sub-shards carry into each other and
-        the spill of sub-shard m lands in sub-shard m of the next shard."""
+        the spill of sub-shard m lands in sub-shard m of the next shard;
+        below, a 2^e-column shard's bits carried past 2^e columns (not past
+        its 2^20-column device shard) are its spill."""
         torch = self.torch
         src = self.dense_view(expr)
         S = src.S
@@ -1562,7 +1564,7 @@ class GpuEngine:
             # a shard wider than 2^20 columns is M consecutive device sub-shards:
             # carries cross them inside the shard (row_kernels.hip)
             self.ext.shift_dense(src.t_payload, S, int(n), outs[0], metas[0], outs[1], metas[1],
-                                 shardwidth.DEVICE_SUBSHARDS)
+                                 shardwidth.DEVICE_SUBSHARDS, shardwidth.SHARD_WIDTH // 64)
         return (self._one_row_view(outs[0], metas[0], src.shards),
                 self._one_row_view(outs[1], metas[1], src.shards))
 

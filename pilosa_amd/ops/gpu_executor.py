@@ -540,17 +540,31 @@ class GpuExecutor:
             child = self.plan(index, c.children[0], shards)
             if k == 0 or child is EMPTY:
                 return child
-            if k >= SHARD_WIDTH or _has_shift(child) or SHARD_WIDTH < 1 << 20:
-                # multi-shard carries, or shards narrower than the device
-                # shard (shift_dense carries at whole 2^20-column device
-                # shards; wider shards carry across their sub-shards): host path
-                raise NotImplementedError
+            # the total shift of a nested chain: its bits reach at most one
+            # shard further (one spill level), as long as it stays below the
+            # shard width (roaring.go:944-977 carries one container at a time)
+            prior = _shift_total(child)
+            if k + prior >= SHARD_WIDTH:
+                raise NotImplementedError   # carries across several shards: host path
             try:
-                self.launches += 2
-                main, spill = self.engine.shift_views(child, k)
+                if prior:
+                    # Shift(Shift(..)): the child's in-shard part shifts and
+                    # carries; its spill (already the next shard's bits) shifts
+                    # within that shard; the new spill is their union
+                    self.launches += 2
+                    main, spill = self.engine.shift_views(child, k)
+                    se = spill_expr(child)
+                    if se is not EMPTY:
+                        self.launches += 3
+                        moved, _ = self.engine.shift_views(se, k)
+                        spill = self.engine.dense_view(Op("or", (Leaf(spill, 0), Leaf(moved, 0))))
+                else:
+                    self.launches += 2
+                    main, spill = self.engine.shift_views(child, k)
             except CompileError:
                 raise NotImplementedError
             main._spill = spill
+            main._shift_total = prior + k
             return Leaf(main, 0)
         if n == "Not":
             idx = self.holder.index(index)
@@ -1904,6 +1918,16 @@ def _minmax_per_shard(o: np.ndarray, which: str):
         val = np.where(anyp, vp, -vn)
         cnt = np.where(anyp, cp, np.where(anyn, cn, 0))
     return val.tolist(), cnt.tolist()
+
+
+def _shift_total(e) -> int:
+    """The largest total Shift of the shifted leaves of a planned expression
+    (0: none)."""
+    if type(e) is Leaf:
+        return int(getattr(e.view, "_shift_total", 0) or 0) if getattr(e.view, "_spill", None) is not None else 0
+    if type(e) is Op:
+        return max((_shift_total(a) for a in e.args), default=0)
+    return 0
 
 
 def _has_shift(e) -> bool:

@@ -478,10 +478,17 @@ def test_paranoia_cross_check_on_device(envs):
 
 SHIFT_QUERIES = [
     "Count(Shift(Row(f=0), n=1))", "Shift(Row(f=20), n=5)", "Count(Intersect(Shift(Row(f=0), n=3), Row(f=1)))",
-    "Count(Union(Shift(Row(f=1), n=70000), Row(g=1)))", "Shift(Row(f=0), n=65536)",
     "Count(Not(Shift(Row(f=2), n=100)))", "Difference(Shift(Row(f=1), n=129), Row(f=0))",
-    "Xor(Shift(Row(f=2), n=1000000), Row(f=3))", "Union(Shift(Row(f=0), n=64), Shift(Row(f=1), n=7))",
-    "Count(Shift(Intersect(Row(f=0), Row(f=1)), n=1048575))", "Shift(Row(f=3), n=0)",
+    "Union(Shift(Row(f=0), n=64), Shift(Row(f=1), n=7))", "Shift(Row(f=3), n=0)",
+    # shifts relative to the shard width (every width runs them on the device,
+    # narrow 2^16 / 2^18 shards included: their spill starts at 2^e columns)
+    f"Count(Union(Shift(Row(f=1), n={SW // 2 + 4464}), Row(g=1)))", f"Shift(Row(f=0), n={SW // 16})",
+    f"Xor(Shift(Row(f=2), n={SW - 48576}), Row(f=3))", f"Count(Shift(Intersect(Row(f=0), Row(f=1)), n={SW - 1}))",
+    # nested shifts (one spill level while the total stays below the width)
+    "Shift(Shift(Row(f=0), n=5), n=7)", f"Count(Shift(Shift(Row(f=1), n={SW - 300}), n=200))",
+    "Union(Shift(Shift(Row(f=2), n=100), n=65000), Row(g=1))",
+    f"Count(Intersect(Shift(Shift(Row(f=0), n=3), n={SW // 4}), Row(f=1)))",
+    "Shift(Union(Shift(Row(f=1), n=9), Row(f=3)), n=11)",
 ]
 if SW > (1 << 21):
     # wide shards (PILOSA_SHARD_WIDTH=22): carries across 1..3 device sub-shards
@@ -492,7 +499,8 @@ if SW > (1 << 21):
 @pytest.mark.parametrize("q", SHIFT_QUERIES)
 def test_shift_on_device_matches_host(envs, q):
     """Shift(row, n) through expr_dense + shift_dense (row_kernels.hip),
-    including the bits each shard carries into the next shard's segment."""
+    including the bits each shard carries into the next shard's segment, at
+    every shard width, nested shifts included."""
     cpu, gpu = envs
     want = cpu.q1("i", q)
     cpu.executor.gpu = gpu

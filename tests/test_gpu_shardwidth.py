@@ -9,7 +9,9 @@ per fragment with counts summed over its sub-shards; src TopN runs on the
 slot index built per sub-shard, its histograms summed per fragment, and
 tests/test_gpu_topn_exec.py asserts the slot index answered).
 Shift carries across the sub-shards of a wide shard on the device; at the
-narrow widths it runs on the host (ops/gpu_executor.py) and is excluded."""
+narrow widths a shard's spill starts at its own 2^e columns (row_kernels.hip
+shift_dense row_words), so the Shift tests run there too and assert device
+launches."""
 import os
 import subprocess
 import sys
@@ -25,7 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_gpu_suites_at_narrow_width(exp):
     env = dict(os.environ, PILOSA_SHARD_WIDTH=str(exp))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
-                        "--timeout", "300", "--timeout-method", "thread", "-k", "not shift and not Shift",
+                        "--timeout", "300", "--timeout-method", "thread",
                         "tests/test_gpu_executor.py", "tests/test_gpu_topn_exec.py"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=850)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
