@@ -60,7 +60,21 @@ struct alignas(64) Header {
   std::atomic<uint32_t> sleepers;      // readers asleep on data_futex
   std::atomic<uint32_t> space_futex;   // bumped on every read (a blocked producer sleeps on it)
   char pad1[64 - 20];
+  uint64_t board_bytes;                // per-rank result bytes of a board entry (0: no board)
+  uint32_t board_ranks;                // ranks posting results (readers + the producer)
+  std::atomic<uint32_t> board_futex;   // bumped on every post (a collecting front end sleeps on it)
+  std::atomic<uint32_t> board_sleepers;
+  char pad2[64 - 20];
   Cursor cur[MAX_READERS];
+};
+
+// One rank's result for command `seq` on the results board: the one-shot
+// gather of small partials (a few bytes to a few KB: Sum/Min/Max/Rows/...)
+// that needs no collective and no device copy.  len < 0: it did not fit
+// (-len bytes would have).
+struct BoardEntry {
+  std::atomic<uint64_t> seq;   // command sequence number + 1 once posted
+  int64_t len;
 };
 
 struct Slot {
@@ -77,11 +91,13 @@ bool alive(int32_t pid) { return pid <= 0 || kill(pid, 0) == 0 || errno == EPERM
 
 class Ring {
  public:
-  Ring(const std::string& name, bool create, uint32_t nslots, uint64_t slot_bytes, uint32_t nreaders)
+  Ring(const std::string& name, bool create, uint32_t nslots, uint64_t slot_bytes, uint32_t nreaders,
+       uint64_t board_bytes)
       : name_(name), owner_(create) {
     if (create) {
       if (nslots < 2 || nreaders > MAX_READERS || slot_bytes < 64) throw std::invalid_argument("ring geometry");
-      size_ = sizeof(Header) + size_t(nslots) * slot_stride(slot_bytes);
+      size_ = sizeof(Header) + size_t(nslots) * slot_stride(slot_bytes) +
+              size_t(nslots) * (nreaders + 1) * board_stride(board_bytes);
       shm_unlink(name.c_str());
       int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
       if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
@@ -94,8 +110,13 @@ class Ring {
       h_->nslots = nslots;
       h_->nreaders = nreaders;
       h_->slot_bytes = slot_bytes;
+      h_->board_bytes = board_bytes;
+      h_->board_ranks = nreaders + 1;
       h_->producer_pid.store(int32_t(getpid()));
       for (uint32_t i = 0; i < nslots; i++) slot(i)->seq.store(0);
+      if (board_bytes)
+        for (uint32_t i = 0; i < nslots; i++)
+          for (uint32_t r = 0; r <= nreaders; r++) entry(i, r)->seq.store(0);
       std::atomic_thread_fence(std::memory_order_seq_cst);
       h_->magic = MAGIC;
     } else {
@@ -109,7 +130,8 @@ class Ring {
       size_ = size_t(st.st_size);
       map(fd);
       if (h_->magic != MAGIC) throw std::runtime_error("ring " + name + " not initialised");
-      if (size_ < sizeof(Header) + size_t(h_->nslots) * slot_stride(h_->slot_bytes))
+      if (size_ < sizeof(Header) + size_t(h_->nslots) * slot_stride(h_->slot_bytes) +
+                      size_t(h_->nslots) * h_->board_ranks * board_stride(h_->board_bytes))
         throw std::runtime_error("ring " + name + " truncated");
     }
   }
@@ -119,6 +141,7 @@ class Ring {
   }
 
   uint64_t slot_bytes() const { return h_->slot_bytes; }
+  uint64_t board_bytes() const { return h_->board_bytes; }
   uint32_t nreaders() const { return h_->nreaders; }
   uint64_t head() const { return h_->head.load(); }
 
@@ -225,7 +248,94 @@ class Ring {
     h_->cur[r].seq.store(s + 1, std::memory_order_release);
     h_->space_futex.fetch_add(1, std::memory_order_acq_rel);
     futex(&h_->space_futex, FUTEX_WAKE, 1, nullptr);
-    return py::make_tuple(op, data);
+    return py::make_tuple(op, data, s);
+  }
+
+  // any rank: its result of command `seq` (rank 0 = the producer, reader r =
+  // rank r + 1); a payload larger than board_bytes posts its size only
+  void post(uint32_t rank, uint64_t seq, py::bytes payload) {
+    if (!h_->board_bytes) throw std::runtime_error("ring has no results board");
+    if (rank >= h_->board_ranks) throw std::out_of_range("board rank");
+    std::string_view data = payload;
+    BoardEntry* e = entry(uint32_t(seq % h_->nslots), rank);
+    if (data.size() > h_->board_bytes) {
+      e->len = -int64_t(data.size());
+    } else {
+      e->len = int64_t(data.size());
+      std::memcpy(reinterpret_cast<char*>(e) + sizeof(BoardEntry), data.data(), data.size());
+    }
+    e->seq.store(seq + 1, std::memory_order_release);
+    h_->board_futex.fetch_add(1, std::memory_order_acq_rel);
+    if (h_->board_sleepers.load() != 0) futex(&h_->board_futex, FUTEX_WAKE, INT32_MAX, nullptr);
+  }
+
+  // producer: every rank's posted result of command `seq` (bytes, or the int
+  // -size of one that did not fit), waiting up to timeout_s; raises when a
+  // reader process is gone, the ring is closed or the wait times out
+  py::list collect(uint64_t seq, double timeout_s, double spin_us) {
+    if (!h_->board_bytes) throw std::runtime_error("ring has no results board");
+    const uint32_t R = h_->board_ranks;
+    const uint32_t k = uint32_t(seq % h_->nslots);
+    int why = 0, dead = -1;
+    {
+      py::gil_scoped_release nogil;
+      const auto t0 = std::chrono::steady_clock::now();
+      auto last_check = t0;
+      for (;;) {
+        bool all = true;
+        for (uint32_t r = 0; r < R && all; r++) {
+          const uint64_t v = entry(k, r)->seq.load(std::memory_order_acquire);
+          if (v > seq + 1) {   // overwritten by a later command: this result is lost
+            why = 3;
+            break;
+          }
+          all = v == seq + 1;
+        }
+        if (why || all) break;
+        const auto now = std::chrono::steady_clock::now();
+        const double el = std::chrono::duration<double>(now - t0).count();
+        if (el * 1e6 < spin_us) {
+#if defined(__x86_64__)
+          __builtin_ia32_pause();
+#endif
+          continue;
+        }
+        if (el > timeout_s) {
+          why = 1;
+          break;
+        }
+        if (std::chrono::duration<double>(now - last_check).count() > 1.0) {
+          last_check = now;
+          for (uint32_t r = 0; r < h_->nreaders && dead < 0; r++)
+            if (!alive(h_->cur[r].pid.load())) dead = int(r);
+          if (dead >= 0) {
+            why = 2;
+            break;
+          }
+        }
+        const uint32_t f = h_->board_futex.load();
+        h_->board_sleepers.fetch_add(1);
+        bool ready = true;
+        for (uint32_t r = 0; r < R && ready; r++) ready = entry(k, r)->seq.load(std::memory_order_acquire) == seq + 1;
+        if (!ready) {
+          struct timespec ts = {0, 50 * 1000 * 1000};
+          futex(&h_->board_futex, FUTEX_WAIT, f, &ts);
+        }
+        h_->board_sleepers.fetch_sub(1);
+      }
+    }
+    if (why == 1) throw std::runtime_error("results board: timed out waiting for the ranks");
+    if (why == 2) throw std::runtime_error("results board: rank " + std::to_string(dead + 1) + " is gone");
+    if (why == 3) throw std::runtime_error("results board: entry overwritten");
+    py::list out;
+    for (uint32_t r = 0; r < R; r++) {
+      BoardEntry* e = entry(k, r);
+      if (e->len < 0)
+        out.append(py::int_(e->len));
+      else
+        out.append(py::bytes(reinterpret_cast<const char*>(e) + sizeof(BoardEntry), size_t(e->len)));
+    }
+    return out;
   }
 
   // producer: readers blocked in read() raise (orderly shutdown / failover)
@@ -244,7 +354,14 @@ class Ring {
     base_ = static_cast<char*>(p);
     h_ = reinterpret_cast<Header*>(base_);
   }
+  static size_t board_stride(uint64_t board_bytes) {
+    return board_bytes ? (sizeof(BoardEntry) + size_t(board_bytes) + 63) & ~size_t(63) : 0;
+  }
   Slot* slot(uint32_t i) { return reinterpret_cast<Slot*>(base_ + sizeof(Header) + size_t(i) * slot_stride(h_->slot_bytes)); }
+  BoardEntry* entry(uint32_t i, uint32_t r) {
+    char* b = base_ + sizeof(Header) + size_t(h_->nslots) * slot_stride(h_->slot_bytes);
+    return reinterpret_cast<BoardEntry*>(b + (size_t(i) * h_->board_ranks + r) * board_stride(h_->board_bytes));
+  }
   uint64_t min_cursor() const {
     uint64_t m = h_->head.load();
     for (uint32_t r = 0; r < h_->nreaders; r++) m = std::min(m, h_->cur[r].seq.load(std::memory_order_acquire));
@@ -266,13 +383,17 @@ class Ring {
 PYBIND11_MODULE(_shmring, m) {
   m.doc() = "single-producer / multi-consumer command ring in POSIX shared memory (parallel/mesh.py)";
   py::class_<Ring>(m, "Ring")
-      .def(py::init<const std::string&, bool, uint32_t, uint64_t, uint32_t>(), py::arg("name"), py::arg("create"),
-           py::arg("nslots") = 64, py::arg("slot_bytes") = 1 << 16, py::arg("nreaders") = 1)
+      .def(py::init<const std::string&, bool, uint32_t, uint64_t, uint32_t, uint64_t>(), py::arg("name"),
+           py::arg("create"), py::arg("nslots") = 64, py::arg("slot_bytes") = 1 << 16, py::arg("nreaders") = 1,
+           py::arg("board_bytes") = 0)
+      .def("post", &Ring::post, py::arg("rank"), py::arg("seq"), py::arg("payload"))
+      .def("collect", &Ring::collect, py::arg("seq"), py::arg("timeout_s") = 120.0, py::arg("spin_us") = 200.0)
       .def("attach", &Ring::attach)
       .def("publish", &Ring::publish, py::arg("op"), py::arg("payload"), py::arg("timeout_s") = 120.0)
       .def("read", &Ring::read, py::arg("reader"), py::arg("spin_us") = 200.0)
       .def("close", &Ring::close_ring)
       .def_property_readonly("slot_bytes", &Ring::slot_bytes)
+      .def_property_readonly("board_bytes", &Ring::board_bytes)
       .def_property_readonly("nreaders", &Ring::nreaders)
       .def_property_readonly("head", &Ring::head);
 }

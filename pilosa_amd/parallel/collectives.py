@@ -41,6 +41,8 @@ RING_SLOT_BYTES = 1 << 18    # a Count text of ~5k calls fits one slot; longer o
 RING_BIG = 1 << 40           # op flag: the payload follows on the command group
 RING_SPIN_US = 300.0         # a waiting rank spins this long before it sleeps on the futex
 RING_PUBLISH_TIMEOUT_S = 120.0
+RING_BOARD_BYTES = 1 << 14   # per-rank result bytes of the results board (one-shot gather of small partials)
+BOARD_TIMEOUT_S = 120.0
 UNION_MIN_CAP = 1024         # initial per-rank pad of a speculative union gather
 
 
@@ -111,6 +113,9 @@ class Comm:
         self.ring = None
         self.ring_reader = -1
         self.ring_msgs = 0
+        self.cmd_seq = -1          # sequence number of the last command sent / received on the ring
+        self.board_gathers = 0
+        self.use_board = True      # small OP_CALL partials through the results board (when the ring has one)
         self._ar_opts: dict = {}
 
     # ------------------------------------------------------------ guard
@@ -168,7 +173,7 @@ class Comm:
                 from pilosa_amd import _shmring
                 name = f"/pilosa_mesh_{os.getpid()}_{uuid.uuid4().hex[:10]}"
                 ring = _shmring.Ring(name, True, nslots=nslots, slot_bytes=slot_bytes,
-                                     nreaders=max(0, self.world - 1))
+                                     nreaders=max(0, self.world - 1), board_bytes=RING_BOARD_BYTES)
             except Exception:  # noqa: BLE001 - no ring: the gloo broadcast stays
                 ring, name = None, ""
         _, got = self._bcast_bytes_group(0, name.encode())
@@ -217,16 +222,16 @@ class Comm:
                 big = len(payload) > self.ring.slot_bytes
                 if tracing.enabled():
                     with tracing.span("Comm.command", ranks=self.world, bytes=len(payload)):
-                        self.ring.publish(int(op) | RING_BIG if big else int(op), b"" if big else bytes(payload),
-                                          RING_PUBLISH_TIMEOUT_S)
+                        self.cmd_seq = self.ring.publish(int(op) | RING_BIG if big else int(op),
+                                                         b"" if big else bytes(payload), RING_PUBLISH_TIMEOUT_S)
                 else:
-                    self.ring.publish(int(op) | RING_BIG if big else int(op), b"" if big else bytes(payload),
-                                      RING_PUBLISH_TIMEOUT_S)
+                    self.cmd_seq = self.ring.publish(int(op) | RING_BIG if big else int(op),
+                                                     b"" if big else bytes(payload), RING_PUBLISH_TIMEOUT_S)
                 self.ring_msgs += 1
                 if big:
                     self._bcast_bytes_group(op, payload, src)
                 return int(op), payload
-            o, data = self.ring.read(self.ring_reader, RING_SPIN_US)
+            o, data, self.cmd_seq = self.ring.read(self.ring_reader, RING_SPIN_US)
         except (RuntimeError, ValueError) as e:
             self.broken = e
             raise CommError(f"command ring failed: {e}") from e
@@ -364,6 +369,31 @@ class Comm:
         work = self._guard(self.dist.all_gather, outs, pad, group=self.group, async_op=True)
         return Pending(self, work, lambda: [x[:k] for x, k in zip(outs, lens)], keep=(pad, outs))
 
+    @property
+    def board(self) -> bool:
+        """The node has a shared-memory results board (Comm.board_gather)."""
+        return self.use_board and self.ring is not None and bool(getattr(self.ring, "board_bytes", 0))
+
+    def board_gather(self, payload: bytes) -> "BoardPending":
+        """One-shot gather of a small host-side partial of the current
+        command (the one bcast_bytes last delivered) through the results
+        board in shared memory: every rank writes its bytes into its own
+        slot, the front end reads them all -- no collective, no device copy,
+        no ring of hops (tiny partials off the ring; the
+        reference's per-node reduce, executor.go:2487-2516).  Workers return
+        at once; the front end's pending result is every rank's bytes, or an
+        :class:`Overflow` when some rank's did not fit an entry."""
+        if self.broken is not None:
+            raise CommError(f"communicator broken: {self.broken}")
+        seq = self.cmd_seq
+        try:
+            self.ring.post(self.rank, seq, payload)
+        except (RuntimeError, ValueError) as e:
+            self.broken = e
+            raise CommError(f"results board failed: {e}") from e
+        self.board_gathers += 1
+        return BoardPending(self, seq if self.rank == 0 else None)
+
     def all_gather_cap_async(self, t, cap: int) -> "Pending":
         """Variable-length 1-D int64 tensors of every rank in ONE all-gather
         with no size exchange first: each rank sends ``[len, values...,
@@ -494,6 +524,35 @@ class Pending:
     def result(self):
         self.wait()
         return self._finish()
+
+
+class BoardPending:
+    """A results-board gather (Comm.board_gather): nothing to wait for on a
+    worker; on the front end ``result()`` collects every rank's bytes."""
+
+    __slots__ = ("_comm", "_seq", "_got")
+
+    def __init__(self, comm, seq):
+        self._comm, self._seq, self._got = comm, seq, None
+
+    def wait(self):
+        pass
+
+    def done(self) -> bool:
+        return True
+
+    def result(self):
+        if self._seq is None:
+            return None
+        if self._got is None:
+            try:
+                got = self._comm.ring.collect(self._seq, BOARD_TIMEOUT_S, RING_SPIN_US)
+            except (RuntimeError, ValueError) as e:
+                self._comm.broken = e
+                raise CommError(f"results board failed: {e}") from e
+            over = [-x for x in got if isinstance(x, int)]
+            self._got = Overflow(max(over) // 8 + 1) if over else got
+        return self._got
 
 
 class PendingAll:

@@ -189,11 +189,15 @@ class ShardMesh:
             # exchange, no host read before the data moves); the capacity is
             # learnt per call name and carried in the command
             cap, quiet = self._call_cap.get(c.name, (CALL_MIN_CAP, 0))
-            parts = self._run_pipelined(OP_CALL, index, pql, list(shards), optd, cap)
+            # a partial that fits the results board is gathered there (cap 0:
+            # no collective at all); larger ones in the RCCL all-gather
+            board = self.comm.board and cap * 8 <= self.comm.ring.board_bytes
+            parts = self._run_pipelined(OP_CALL, index, pql, list(shards), optd, 0 if board else cap)
             if not isinstance(parts, Overflow):
                 break
             self.call_retries += 1
-            self._call_cap[c.name] = (1 << int(parts.need + parts.need // 4).bit_length(), 0)
+            self._call_cap[c.name] = (max(cap * 2 if board else 0, 1 << int(parts.need + parts.need // 4).bit_length()),
+                                      0)
         # a capacity far above what the call sends is halved after a quiet
         # spell (a one-off large Row result does not pad every later one)
         longest = getattr(self, "_call_longest", 0)
@@ -541,6 +545,20 @@ class ShardMesh:
                 local = self._local_counts(index, pqls, self.owned(shards))
             except Exception as e:  # noqa: BLE001 - flagged in the reduced tensor below
                 err = e
+            if self.comm.board and len(pqls) <= 1024:
+                # host-side counts: the shared-memory results board, no
+                # collective (the size test is the command's, so every rank
+                # takes the same path; 1024 counts fit an entry)
+                from .collectives import RemoteError, decode, encode
+                got = self.comm.board_gather(encode([[int(x) for x in local],
+                                                     f"{type(err).__name__}: {err}" if err is not None else ""]))
+                if not self.is_frontend:
+                    return None
+                parts = [decode(b) for b in got.result()]
+                errs = [RemoteError(e) for _, e in parts if e]
+                if errs:
+                    raise MeshError(str(errs[0]))
+                return [sum(int(p[0][i]) for p in parts) for i in range(len(pqls))]
             t = torch.tensor(list(local) + [1 if err is not None else 0], dtype=torch.int64, device=self.device)
             self.comm.all_reduce(t)
             out = [int(x) for x in t.cpu().tolist()]
@@ -627,6 +645,18 @@ class ShardMesh:
         from pilosa_amd.ops.device import DeviceRowBlock
 
         from .collectives import Overflow
+        if int(cap) == 0:
+            # results board: the partial as host bytes into this rank's slot
+            import numpy as np
+            w = encode_row_block(mine, self.device).cpu().numpy() if isinstance(mine, DeviceRowBlock) else \
+                encode_partial(mine)
+
+            def decode_board(ps):
+                if isinstance(ps, Overflow) or ps is None:
+                    return ps
+                self._call_longest = max(len(b) for b in ps) // 8 if ps else 0
+                return [decode_partial(np.frombuffer(b, dtype=np.int64)) for b in ps]
+            return _Chain(self.comm.board_gather(np.ascontiguousarray(w, dtype=np.int64).tobytes()), decode_board)
         if isinstance(mine, DeviceRowBlock):
             t = encode_row_block(mine, self.device)
         else:

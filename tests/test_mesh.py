@@ -379,11 +379,16 @@ def _call_worker(rank, world, port, outdir):
         per_call = {}
         for q in ("Sum(field=v)", "Rows(f)", "Row(f=1)", "Max(Row(f=2), field=v)", "GroupBy(Rows(f), Rows(g))"):
             ex.execute("i", q)                 # learns the call's gather capacity
-            c0 = mesh.comm.data_calls
+            c0, b0 = mesh.comm.data_calls, mesh.comm.board_gathers
             got = _canon(ex.execute("i", q).results)
-            per_call[q] = [mesh.comm.data_calls - c0, got]
+            per_call[q] = [mesh.comm.data_calls - c0, mesh.comm.board_gathers - b0, got]
+        # without the results board: ONE fixed-capacity all-gather per call;
         # a capacity far too small: the ranks' partials overflow it, the front
         # end re-issues the call once with a capacity that fits
+        mesh.comm.use_board = False
+        c0 = mesh.comm.data_calls
+        rccl_sum = _canon(ex.execute("i", "Sum(field=v)").results)
+        rccl_calls = mesh.comm.data_calls - c0
         mesh._call_cap["Row"] = (4, 0)
         r0 = mesh.call_retries
         big = _canon(ex.execute("i", "Row(f=1)").results)
@@ -392,7 +397,8 @@ def _call_worker(rank, world, port, outdir):
         again = _canon(ex.execute("i", "Row(f=1)").results)
         with open(os.path.join(outdir, "calls.json"), "w") as fh:
             json.dump({"per_call": per_call, "big": big, "retries": retries, "again": again,
-                       "again_calls": mesh.comm.data_calls - c0}, fh)
+                       "again_calls": mesh.comm.data_calls - c0, "rccl_sum": rccl_sum, "rccl_calls": rccl_calls,
+                       "board": mesh.comm.board or mesh.ring}, fh)
         mesh.stop()
     finally:
         ex.close()
@@ -401,10 +407,11 @@ def _call_worker(rank, world, port, outdir):
 
 
 def test_general_call_is_one_speculative_gather(tmp_path):
-    """a general call's partials travel in ONE
-    fixed-capacity all-gather -- no size all-gather, no host read before the
-    data moves; a rank whose partial does not fit says so inside that gather
-    and the front end re-issues the call with a capacity that fits."""
+    """a general call's small partials go through
+    the shared-memory results board (no collective); otherwise they travel in
+    ONE fixed-capacity all-gather -- no size all-gather, no host read before
+    the data moves; a rank whose partial does not fit says so inside that
+    gather and the front end re-issues the call with a capacity that fits."""
     mp.start_processes(_call_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
                        start_method="spawn")
     res = json.load(open(tmp_path / "calls.json"))
@@ -415,9 +422,12 @@ def test_general_call_is_one_speculative_gather(tmp_path):
     _setup_schema(holder)
     bits, vals = _data()
     _load(ex, bits, vals)
-    for q, (ncoll, got) in res["per_call"].items():
-        assert ncoll == 1, (q, ncoll)
+    assert res["board"]
+    for q, (ncoll, nboard, got) in res["per_call"].items():
+        # small partials: the shared-memory results board, no collective
+        assert (ncoll, nboard) == (0, 1), (q, ncoll, nboard)
         assert got == _canon(ex.execute("i", q).results), q
+    assert res["rccl_calls"] == 1 and res["rccl_sum"] == _canon(ex.execute("i", "Sum(field=v)").results)
     want_row = _canon(ex.execute("i", "Row(f=1)").results)
     ex.close()
     holder.close()

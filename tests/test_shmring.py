@@ -21,7 +21,7 @@ def _reader(name, r, n, q):
     try:
         for _ in range(n):
             got.append(ring.read(r, 50.0))
-        q.put(("done", r, [(op, len(b), b[:8]) for op, b in got]))
+        q.put(("done", r, [(op, len(b), b[:8]) for op, b, _ in got]))
         ring.read(r, 50.0)           # blocks until the producer closes the ring
     except RuntimeError as e:
         q.put(("closed", r, str(e)))
@@ -84,3 +84,40 @@ def test_reader_raises_when_producer_dies():
     assert time.time() - t0 < 5
     if os.path.exists("/dev/shm" + name):
         os.unlink("/dev/shm" + name)
+
+
+def _poster(name, r, q):
+    ring = _shmring.Ring(name, False)
+    ring.attach(r)
+    q.put("ready")
+    for _ in range(3):
+        op, data, seq = ring.read(r, 50.0)
+        payload = b"x" * (20000 if op == 2 else 10 * (r + 1))
+        ring.post(r + 1, seq, payload)
+
+
+def test_results_board_one_shot_gather():
+    """The results board: every rank posts its result of command `seq`; the
+    producer collects all of them with no collective; a result larger than
+    the board's entry posts its size only (the caller falls back)."""
+    name = f"/pilosa_test_{uuid.uuid4().hex[:12]}"
+    ring = _shmring.Ring(name, True, nslots=4, slot_bytes=256, nreaders=2, board_bytes=8192)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_poster, args=(name, r, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for _ in range(2):
+        q.get(timeout=60)
+    for op in (1, 1, 2):
+        seq = ring.publish(op, b"cmd")
+        ring.post(0, seq, b"front")
+        got = ring.collect(seq, 30.0, 50.0)
+        if op == 1:
+            assert got == [b"front", b"x" * 10, b"x" * 20]
+        else:
+            assert got == [b"front", -20000, -20000]
+    for p in ps:
+        p.join(30)
+    with pytest.raises(RuntimeError, match="timed out"):
+        ring.collect(ring.publish(1, b""), 0.2, 10.0)
