@@ -5,6 +5,8 @@ Attributes are string/int/bool/float key-values per id.  Setting a key to
 checksums for anti-entropy diffs (attrBlockSize=100).
 
 Backed by SQLite (stdlib; one file per store), one JSON document per id.
+A ``.data`` file written by a reference node (BoltDB, boltdb/attrstore.go)
+is converted on open (models/boltdb.py), so its attributes carry over.
 """
 from __future__ import annotations
 
@@ -99,13 +101,30 @@ class SQLiteAttrStore(MemAttrStore):
 
     def open(self):
         os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+        migrated = self._migrate_bolt()
         self._db = sqlite3.connect(self.path, check_same_thread=False, isolation_level=None)
         self._db.execute("PRAGMA journal_mode=WAL")
         self._db.execute("CREATE TABLE IF NOT EXISTS attrs (id INTEGER PRIMARY KEY, doc TEXT NOT NULL)")
+        if migrated:
+            self._db.execute("BEGIN")
+            self._db.executemany("INSERT OR REPLACE INTO attrs (id, doc) VALUES (?, ?)",
+                                 [(i, json.dumps(a)) for i, a in sorted(migrated.items())])
+            self._db.execute("COMMIT")
         with self.mu:
             for id, doc in self._db.execute("SELECT id, doc FROM attrs"):
                 self._d[int(id)] = json.loads(doc)
         return self
+
+    def _migrate_bolt(self) -> Optional[Dict[int, dict]]:
+        """A reference node's ``.data`` file is a BoltDB attribute store
+        (boltdb/attrstore.go): read it once (models/boltdb.py), keep it as
+        ``.data.bolt`` and let this store take its place with its contents."""
+        from pilosa_amd.models import boltdb
+        if not os.path.exists(self.path) or not boltdb.is_bolt(self.path):
+            return None
+        data = boltdb.read_bolt_attrs(self.path)
+        os.replace(self.path, self.path + ".bolt")
+        return data
 
     def close(self):
         if self._db is not None:

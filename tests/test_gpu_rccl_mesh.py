@@ -68,10 +68,11 @@ def _worker(rank, world, port, outdir):
         def both(qs):
             ex.mesh = mesh
             c0, s0, t0 = mesh.comm.data_calls, mesh.seq, mesh.topn_tensor_batches
-            p0 = mesh.topn_plain_batches
+            p0, g0 = mesh.topn_plain_batches, mesh.comm.board_gathers
             got = run(qs)
             stats = {"collectives": mesh.comm.data_calls - c0, "count_text": mesh.seq - s0,
-                     "topn_tensor": mesh.topn_tensor_batches - t0, "topn_plain": mesh.topn_plain_batches - p0}
+                     "topn_tensor": mesh.topn_tensor_batches - t0, "topn_plain": mesh.topn_plain_batches - p0,
+                     "board": mesh.comm.board_gathers - g0}
             ex.mesh = None
             want = run(qs)
             ex.mesh = mesh
@@ -81,6 +82,10 @@ def _worker(rank, world, port, outdir):
         r0 = mesh.row_blocks
         out["calls"] = both(QUERIES + ["Shift(Row(f=1), n=5)", "Union(Row(f=1), Row(g=2))"])
         out["row_blocks"] = mesh.row_blocks - r0
+        # the same partials through the RCCL all-gather (results board off)
+        mesh.comm.use_board = False
+        out["calls_rccl"] = both(QUERIES + ["Shift(Row(f=1), n=5)", "Union(Row(f=1), Row(g=2))"])
+        mesh.comm.use_board = True
         out["topn"] = both(TOPN)
         # steady-state TopN batch: its data collectives on RCCL
         run(["TopN(f, n=4) TopN(f, n=2)"])      # builds the node candidate space for n=4
@@ -118,12 +123,15 @@ def test_rccl_world1_mesh_matches_local(tmp_path):
     res = json.load(open(tmp_path / "rccl.json"))
     assert res["backend"] == "nccl" and res["dist_backend"] == "nccl", res
     assert res["ctrl"], "no gloo command group next to the RCCL group"
-    for part in ("counts", "calls", "topn", "after_write", "failover"):
+    for part in ("counts", "calls", "calls_rccl", "topn", "after_write", "failover"):
         for k, (g, w) in enumerate(zip(res[part]["got"], res[part]["want"])):
             assert g == w, (part, k)
     assert res["counts"]["count_text"] >= 1, "Count text did not take the mesh count_text path"
     assert res["counts"]["collectives"] >= 1
-    assert res["calls"]["collectives"] >= len(QUERIES), "general calls did not gather partials over RCCL"
+    # small partials through the shared-memory results board, all of them
+    # through RCCL with the board off
+    assert res["calls"]["board"] >= len(QUERIES) // 2, res["calls"]
+    assert res["calls_rccl"]["collectives"] >= len(QUERIES), "general calls did not gather partials over RCCL"
     # Row / Difference / Not / Shift / Union partials travelled as device container blocks
     assert res["row_blocks"] >= 5, res["row_blocks"]
     assert res["topn"]["topn_tensor"] >= 3 and res["after_write"]["topn_tensor"] >= 3, res
