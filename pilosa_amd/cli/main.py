@@ -124,6 +124,15 @@ def import_field_options(args) -> dict:
 
 
 # ------------------------------------------------------------------ server
+def _gossip_key(cfg):
+    """The ``gossip.key`` file's bytes (validated by validate_gossip), or None."""
+    path = cfg.get("gossip.key")
+    if not path:
+        return None
+    from pilosa_amd.parallel.gossip_udp import load_key
+    return load_key(str(path))
+
+
 def cmd_server(args, stdout, stderr) -> int:
     from pilosa_amd.server.config import parse_duration
     from pilosa_amd.server.server import Server
@@ -185,6 +194,8 @@ def cmd_server(args, stdout, stderr) -> int:
                  probe_timeout=cfg.duration("gossip.probe-timeout"),
                  suspicion_mult=float(cfg.get("gossip.suspicion-mult")),
                  gossip_nodes=int(cfg.get("gossip.nodes")),
+                 gossip_port=int(cfg.get("gossip.port") or 0),
+                 gossip_key=_gossip_key(cfg),
                  to_the_dead_time=cfg.duration("gossip.to-the-dead-time"),
                  stream_timeout=cfg.duration("gossip.stream-timeout"),
                  gossip_interval=cfg.duration("gossip.push-pull-interval"),

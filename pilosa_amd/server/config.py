@@ -205,10 +205,9 @@ def validate_gossip(cfg: "Config") -> None:
     """The ``[gossip]`` keys this build acts on (parallel/swim.py failure
     detection, NodeStatus push-pull) must hold usable values: positive
     probe interval / timeout, suspicion multiplier >= 1, indirect probers
-    >= 0, a port number, durations that parse.  Gossip travels over the
-    node's HTTP(S) port, so ``gossip.key`` (memberlist's symmetric
-    encryption key file) is refused: use ``[tls]`` to encrypt cluster
-    traffic instead of silently running unencrypted."""
+    >= 0, a port number, durations that parse, and a ``gossip.key`` file of
+    16, 24 or 32 bytes (memberlist's key sizes): the UDP probes on
+    ``gossip.port`` carry an HMAC of it (parallel/gossip_udp.py)."""
     try:
         pi = cfg.duration("gossip.probe-interval")
         pt = cfg.duration("gossip.probe-timeout")
@@ -229,8 +228,11 @@ def validate_gossip(cfg: "Config") -> None:
     if not port.isdigit() or not 0 <= int(port) <= 65535:
         raise ConfigError(f"gossip.port: invalid port {port!r}")
     if cfg.get("gossip.key"):
-        raise ConfigError("gossip.key: gossip runs over the node's HTTP port in this build; "
-                          "encrypt cluster traffic with [tls] instead")
+        from pilosa_amd.parallel.gossip_udp import load_key
+        try:
+            load_key(str(cfg.get("gossip.key")))
+        except (OSError, ValueError) as e:
+            raise ConfigError(f"gossip.key: {e}")
 
 
 # ------------------------------------------------------------ listen / advertise

@@ -89,7 +89,8 @@ class Server:
                  gossip_interval: float = 30.0, allowed_origins: Optional[List[str]] = None,
                  advertise: str = "", probe_timeout: float = 0.5, suspicion_mult: float = 4,
                  indirect_checks: int = 3, to_the_dead_time: float = 30.0, stream_timeout: float = 10.0,
-                 gossip_nodes: int = 3):
+                 gossip_nodes: int = 3, gossip_port: int = 0, gossip_key: Optional[bytes] = None,
+                 gossip_peer_ports: Optional[Dict[str, int]] = None):
         self.data_dir = data_dir
         # CORS origins ([handler] allowed-origins); none = no CORS headers at all
         self.allowed_origins = list(allowed_origins or [])
@@ -128,6 +129,13 @@ class Server:
         # (memberlist GossipNodes, gossip/gossip.go:273 -- the fan-out, not the
         # indirect-probe count, which stays memberlist's fixed 3)
         self.gossip_nodes = max(1, int(gossip_nodes))
+        # [gossip] port / key: SWIM probes over UDP on that port, HMAC-tagged
+        # with the key (parallel/gossip_udp.py); 0 = probes over the HTTP port.
+        # A peer's gossip port is the same port unless listed (one host, tests)
+        self.gossip_port = int(gossip_port or 0)
+        self.gossip_key = gossip_key
+        self.gossip_peer_ports: Dict[str, int] = dict(gossip_peer_ports or {})
+        self.udp_prober = None
         self.to_the_dead_time = to_the_dead_time
         self.stream_timeout = stream_timeout
         self.failure_detector = None
@@ -229,6 +237,15 @@ class Server:
             self.cluster.set_state(self.cluster.determine_state())
         else:
             self._join()
+        if not self.cluster_disabled and self.gossip_port > 0:
+            from pilosa_amd.parallel.gossip_udp import UdpProber
+            try:
+                self.udp_prober = UdpProber(self.node.id, host if host not in ("",) else "0.0.0.0", self.gossip_port,
+                                            lambda: list(self.cluster.nodes), self._gossip_addr, self.gossip_key,
+                                            self.logger)
+            except OSError as e:   # the port is taken: probes stay on the HTTP port
+                self.logger.printf("gossip: cannot listen on udp port %d (%s): probing over HTTP",
+                                   self.gossip_port, e)
         if not self.cluster_disabled and self.probe_interval > 0:
             self._start_loop(self._swim_loop, "swim")
         if not self.cluster_disabled and self.gossip_interval > 0:
@@ -388,6 +405,8 @@ class Server:
             self.gc_notifier.stop()
         if self.mesh is not None:
             self.mesh.stop()
+        if self.udp_prober is not None:
+            self.udp_prober.close()
         if self.httpd is not None:
             self.httpd.shutdown()
             self.httpd.server_close()
@@ -600,7 +619,9 @@ class Server:
         the coordinator (NodeState), as memberlist's leave event reaches the
         reference's coordinator.  A DOWN node that answers again is READY."""
         from pilosa_amd.parallel.swim import DOWN, FailureDetector
-        det = FailureDetector(self.node.id, self._swim_probe, self._swim_indirect,
+        up = self.udp_prober
+        det = FailureDetector(self.node.id, up.ping if up is not None else self._swim_probe,
+                              up.ping_req if up is not None else self._swim_indirect,
                               probe_interval=self.probe_interval, probe_timeout=self.probe_timeout,
                               suspicion_mult=self.suspicion_mult, indirect_checks=self.indirect_checks)
         self.failure_detector = det
@@ -630,6 +651,10 @@ class Server:
                         self._publish_status()
         finally:
             det.close()
+
+    def _gossip_addr(self, node):
+        """(host, UDP gossip port) of a node."""
+        return node.uri.host, self.gossip_peer_ports.get(node.id, self.gossip_port)
 
     def _swim_probe(self, node, timeout: float) -> bool:
         """Direct probe: the node's /version within ``timeout``."""

@@ -4,6 +4,7 @@ probe-interval, probe-timeout, suspicion-mult, nodes).  VERDICT r4 item 8:
 the keys must do something, and a paused node must be detected within the
 bound they imply."""
 import math
+import os
 import tempfile
 import threading
 import time
@@ -85,7 +86,7 @@ def test_gossip_config_validation():
     cfg = Config()
     validate_gossip(cfg)
     for key, bad in (("gossip.probe-interval", "0s"), ("gossip.probe-timeout", "0s"),
-                     ("gossip.suspicion-mult", 0), ("gossip.nodes", -1), ("gossip.key", "/etc/key"),
+                     ("gossip.suspicion-mult", 0), ("gossip.nodes", -1), ("gossip.key", "/nonexistent/key"),
                      ("gossip.port", "70000")):
         c = Config()
         c.set(key, bad)
@@ -181,3 +182,64 @@ def test_indirect_probe_route_only_probes_members():
         for s in (m1, m0):
             if s is not None:
                 s.close()
+
+
+
+def _udp_server(nid, gport, key, peers, coord=None):
+    s = Server(tempfile.mkdtemp(), bind="127.0.0.1:0", node_id=nid, gpu="off", coordinator=coord is None,
+               coordinator_uri=None if coord is None else coord.uri.normalize(), probe_interval=0.1,
+               probe_timeout=0.1, suspicion_mult=2, indirect_checks=1, logger=CaptureLogger(),
+               hasher="mod", native_http=False, gossip_interval=0, gossip_port=gport, gossip_key=key,
+               gossip_peer_ports=peers)
+    if coord is None:
+        from pilosa_amd.parallel.cluster import URI
+        s.hosts = [URI.parse("127.0.0.1:1")]
+    return s.open()
+
+
+@pytest.mark.timeout(120)
+def test_udp_gossip_port_probes_with_key():
+    """[gossip] port + key (VERDICT r5 missing 5): the SWIM probes travel as
+    UDP ping / ack / ping-req on each node's gossip port, tagged with an
+    HMAC of the key; a node whose UDP endpoint stops answering is DOWN
+    within the detector's bound, and packets with a wrong key are dropped."""
+    import socket
+
+    from pilosa_amd.parallel.gossip_udp import UdpProber, load_key
+
+    def free_udp():
+        x = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        x.bind(("127.0.0.1", 0))
+        p = x.getsockname()[1]
+        x.close()
+        return p
+    key = os.urandom(32)
+    kf = tempfile.NamedTemporaryFile(delete=False)
+    kf.write(key)
+    kf.close()
+    assert load_key(kf.name) == key
+    ports = {f"node{i}": free_udp() for i in range(3)}
+    m0 = _udp_server("node0", ports["node0"], key, ports)
+    m1 = m2 = None
+    try:
+        m1 = _udp_server("node1", ports["node1"], key, ports, m0)
+        m2 = _udp_server("node2", ports["node2"], key, ports, m0)
+        assert _wait(lambda: all(s.cluster.state == "NORMAL" and len(s.cluster.nodes) == 3 for s in (m0, m1, m2)),
+                     20)
+        assert all(s.udp_prober is not None for s in (m0, m1, m2))
+        assert _wait(lambda: m1.udp_prober.received > 5 and m0.udp_prober.received > 5, 10)
+        # a prober with another key: its pings are dropped, it hears nothing
+        bad = UdpProber("intruder", "127.0.0.1", 0, lambda: [], lambda n: ("127.0.0.1", ports[n.id]),
+                        key=os.urandom(32))
+        d0 = m1.udp_prober.dropped
+        assert not bad.ping(m1.node, 0.3)
+        assert m1.udp_prober.dropped > d0
+        bad.close()
+        # node2's UDP endpoint goes silent: DOWN on the coordinator
+        m2.udp_prober.close()
+        assert _wait(lambda: m0.cluster.node_by_id("node2").state == "DOWN", 20)
+    finally:
+        for s in (m2, m1, m0):
+            if s is not None:
+                s.close()
+        os.unlink(kf.name)
