@@ -1199,18 +1199,24 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
                      pairs);
   const int64_t units = int64_t(S) * 16;
   // serving-size batches (<= 128 queries: almost every pair is one-off):
-  // 8 queries per wave, one-off pairs probed in place / smaller array staged,
-  // batched array staging (variant 40) -- 68.7k vs 61.1k req/s with 2
-  // group-commit threads (profiles/r05_serve/).  Bigger batches keep v6.
-  if (variant == 6 && cq <= 0 && Q <= 128) variant = 40;
+  // batched array staging (variant 39: an array's chunk loads all in flight
+  // before the LDS scatter) at 4 queries per wave up to 32 queries, 16 up to
+  // 128.  Round 6 sweep (profiles/r06_serve/kbench_b*.log): 0.437 / 0.848 /
+  // 1.275 ms at 32 / 64 / 128 queries against 0.554 / 1.019 / 1.353 ms for
+  // round 5's variant 40 at 8 per wave (whose one-off in-place probes cost
+  // more than they save).  Bigger batches keep v6.
+  if (variant == 6 && cq <= 0 && Q <= 128) {
+    variant = 39;
+    cq = Q <= 32 ? 4 : 16;
+  }
 #ifdef PK_KBENCH
   if (variant == 50 && cq <= 0 && Q <= 128) variant = 51;   // the serving variant, lane-rotated
 #endif
   if (variant == 41 && cq <= 0 && Q <= 128) variant = 42;   // the same with dense shadows
   if (cq <= 0) cq = Q <= 128 ? 8 : (Q <= 2048 ? 32 : 64);
-// The shipped build instantiates v6 and its serving variant 40 only; every
+// The shipped build instantiates v6 and its serving variant 39 only; every
 // measured-and-rejected variant and cost-isolation skeleton (v10-v13,
-// 16-24, 31-42, 50/51) is built into the kbench module alone
+// 16-24, 31-38, 40-42, 50/51) is built into the kbench module alone
 // (pilosa_amd/native/build.py --kbench, scripts/kbench.py).
 #ifdef PK_KBENCH
 #define PK_LAUNCH(CQV)                                                                                       \
@@ -1276,8 +1282,8 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
 #define PK_LAUNCH(CQV)                                                                                       \
   {                                                                                                          \
     const int64_t wv = units * ((Q + CQV - 1) / CQV);                                                        \
-    if (variant == 40)                                                                                       \
-      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, true, true>), dim3(unsigned(wv)), dim3(64), 0, \
+    if (variant == 39)                                                                                       \
+      hipLaunchKernelGGL((and2_pairs_v6_kernel<CQV, false, 0, 0, 1, false, true>), dim3(unsigned(wv)), dim3(64), 0, \
                          st, progs, Q, views, S, pairs, partial);                                            \
     else                                                                                                     \
       hipLaunchKernelGGL(and2_pairs_v6_kernel<CQV>, dim3(unsigned(wv)), dim3(64), 0, st, progs, Q, views, S,  \
