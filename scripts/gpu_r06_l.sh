@@ -12,7 +12,8 @@ timeout -k 10 400 env PILOSA_HIPKERNELS=_hipkernels_kbench PILOSA_AND2_VARIANT=4
 grep "^{" $O/serve_v40.log | cut -c 1-600
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o serve -- python3 $R/scripts/bench_server.py --seconds 3 --batchers 2 > $O/serve_prof.log 2>&1 || { tail -c 3000 $O/serve_prof.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_head -o head -- python3 $R/bench.py --serve-seconds 0 --configs= --topn-batches 0 --topn-cache-batches 0 --topn-src-batches 0 --steps 10 --warmup 2 > $O/head_prof.log 2>&1 || { tail -c 3000 $O/head_prof.log; exit 1; }
 cd $R
-find $O/prof -name "*kernel_stats.csv" | head -3
-for f in $(find $O/prof -name "*kernel_stats.csv"); do head -12 $f | cut -c 1-220; done
+find $O/prof $O/prof_head -name "*kernel_stats.csv" | head -3
+for f in $(find $O/prof $O/prof_head -name "*kernel_stats.csv"); do echo $f; head -12 $f | cut -c 1-220; done
 echo done
