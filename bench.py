@@ -297,11 +297,26 @@ def bench_topn_exec(args, holder, ex, gpu, shards, fdir, world, rank, dev):
             prof = threading.Thread(target=lambda: prof_out.setdefault("p", pprof.cpu_profile(0.3, 500)), daemon=True)
             prof.start()
         t0 = time.perf_counter()
-        ts = [threading.Thread(target=client, args=(warm, len(texts))) for _ in range(nclients)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+        cprof = os.environ.get("PILOSA_BENCH_CPROFILE", "") if profile else ""
+        if cprof and nclients == 1:
+            # deterministic profile of the one request thread (host cost per call)
+            import cProfile
+            import io
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            client(warm, len(texts))
+            pr.disable()
+            sio = io.StringIO()
+            pstats.Stats(pr, stream=sio).sort_stats("tottime").print_stats(45)
+            with open(cprof, "w") as fh:
+                fh.write(sio.getvalue())
+        else:
+            ts = [threading.Thread(target=client, args=(warm, len(texts))) for _ in range(nclients)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
         if err:
             raise err[0]
         torch.cuda.synchronize(dev)

@@ -133,6 +133,23 @@ def pair_array(ids, counts) -> "PairArray":
     return PairArray(ids, counts)
 
 
+_new_pa = object.__new__
+
+
+def pair_arrays_split(ids: np.ndarray, counts: np.ndarray, offs) -> List["PairArray"]:
+    """PairArrays over consecutive slices ``offs[i]:offs[i+1]`` of contiguous
+    uint64 ids and int64 counts (a native batch's answers): views, no
+    conversion or per-result checks."""
+    out = []
+    for a, b in zip(offs, offs[1:]):
+        p = _new_pa(PairArray)
+        p.ids = ids[a:b]
+        p.counts = counts[a:b]
+        p._items = None
+        out.append(p)
+    return out
+
+
 _MAKE_PAIRS = []
 
 

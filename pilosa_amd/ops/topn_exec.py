@@ -35,7 +35,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from pilosa_amd.models.cache import Pair, pair_array, pairs_from_arrays
+from pilosa_amd.models.cache import Pair, pair_array, pair_arrays_split, pairs_from_arrays
 
 from .device import DeviceView, kernels
 
@@ -68,6 +68,9 @@ def clamp_topn_params(ns: Sequence[int], thresholds: Sequence[int]):
 
 
 SIDE_STREAM = os.environ.get("PILOSA_TOPN_SIDE_STREAM", "1") != "0"
+# cache-only batches through the native request object (binding.cpp CacheTopN);
+# 0 = the Python lane path (kept for A/B runs)
+NATIVE_FUSED = os.environ.get("PILOSA_TOPN_NATIVE", "1") != "0"
 
 
 class _Lane:
@@ -275,6 +278,33 @@ def mesh_cache_batch(rc: Optional["DeviceRankCaches"], ns: Sequence[int], thresh
     Q = len(ns)
     nn = [int(n) for n in ns]
     dev = rc.view.device if rc is not None else (device if device is not None else comm.device)
+    if space is None and cand is not None:
+        space = cand.space
+    if ids is None and cand is not None:
+        ids = cand.ids
+    k = kernels() if dev.type == "cuda" and NATIVE_FUSED else None
+    if k is not None and hasattr(k, "mesh_cache_issue"):
+        # parameters, partial and answers natively (binding.cpp mesh_cache_issue / _finish)
+        part = cand is not None and not stale and not declined and rc is not None and cand.nmax > 0 and rc.S > 0
+        z = _EMPTY_I32.get(dev)
+        if z is None:
+            z = _EMPTY_I32[dev] = torch.zeros(0, dtype=torch.int32, device=dev)
+        buf, prm_d, T, KK = k.mesh_cache_issue(rc.cache_cnt if part else z, cand.nmax if part else 0,
+                                               cand.inv if part else z, cand.cm if part else z, nn, thresholds,
+                                               int(U), rc.K if rc is not None else 0, int(bool(stale)),
+                                               int(bool(declined)), dev.index or 0)
+
+        def finish_native():
+            if ids is None or space is None:
+                return "stale"
+            got = k.mesh_cache_finish(buf, ids, prm_d, Q, T, KK, space)
+            if isinstance(got, str):
+                return got
+            if got is None:   # a query overflowed the select: the torch path below
+                return _finish_cache_batch(buf, prm_d, ids, space, Q, T, U, KK)
+            return pair_arrays_split(*got)
+        pend = Pending(comm, comm.all_reduce_async(buf), finish_native, keep=(buf, prm_d))
+        return pend if defer else pend.result()
     ths = [max(1, int(t)) for t in thresholds]
     uniq_t = sorted(set(ths))
     T = len(uniq_t)
@@ -306,42 +336,50 @@ def mesh_cache_batch(rc: Optional["DeviceRankCaches"], ns: Sequence[int], thresh
             buf.zero_()
             buf[-2] = int(bool(stale))
             buf[-1] = int(bool(declined))
-    if space is None and cand is not None:
-        space = cand.space
-    if ids is None and cand is not None:
-        ids = cand.ids
 
     def finish():
         if ids is None or space is None:
             return "stale"
-        if dev.type == "cuda":
-            out = torch.empty((Q, KK + 1), dtype=torch.int64, device=dev)
-            kernels().topn_cache_select32(buf, ids, prm_d, Q, T, out)
-        else:
-            out = cache_select_ref(buf, ids, prm_d, Q, T, KK)
-        h = _to_host_pinned(out)
-        if Q and h[0, 0] <= -3:
-            return "declined" if h[0, 0] == -4 else "stale"
-        lens = h[:, 0]
-        if (lens < 0).any():    # more members than one workgroup sorts: torch over the reduced buffer
-            parts = [_select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
-                     if lens[q] < 0 else h[q, 1:1 + int(lens[q])] for q in range(Q)]
-            ln = [len(r) for r in parts]
-        else:
-            ln = lens.tolist()
-            parts = [h[q, 1:1 + n] for q, n in enumerate(ln)]
-        # every query's kept keys end to end, decoded in one pass, then split
-        # (as the 1-GPU batch decodes: _topn_nosrc_fused_on)
-        keys = np.concatenate(parts) if Q else np.zeros(0, np.int64)
-        rid = space[0xFFFFFFFF - (keys & 0xFFFFFFFF)] if len(keys) else np.zeros(0, np.uint64)
-        cnt = keys >> 32
-        res, o = [], 0
-        for n in ln:
-            res.append(pair_array(rid[o:o + n], cnt[o:o + n]))
-            o += n
-        return res
+        return _finish_cache_batch(buf, prm_d, ids, space, Q, T, U, KK)
     pend = Pending(comm, comm.all_reduce_async(buf), finish, keep=(buf, prm_d))
     return pend if defer else pend.result()
+
+
+_EMPTY_I32: dict = {}
+
+
+def _finish_cache_batch(buf, prm_d, ids, space, Q: int, T: int, U: int, KK: int):
+    """The front end's end of a mesh cache-only batch in torch / numpy (the
+    CPU path, and the select-overflow case of the native one): per-query
+    top-n of the all-reduced buffer, decoded against the node space."""
+    import torch
+    if buf.device.type == "cuda":
+        out = torch.empty((Q, KK + 1), dtype=torch.int64, device=buf.device)
+        kernels().topn_cache_select32(buf, ids, prm_d, Q, T, out)
+    else:
+        out = cache_select_ref(buf, ids, prm_d, Q, T, KK)
+    h = _to_host_pinned(out)
+    if Q and h[0, 0] <= -3:
+        return "declined" if h[0, 0] == -4 else "stale"
+    prm = prm_d.cpu().numpy() if buf.device.type == "cuda" else prm_d.numpy()
+    lens = h[:, 0]
+    if (lens < 0).any():    # more members than one workgroup sorts: torch over the reduced buffer
+        parts = [_select_from_buffer(buf, Q, T, U, q, int(prm[2 * Q + q]), int(prm[3 * Q + q]))
+                 if lens[q] < 0 else h[q, 1:1 + int(lens[q])] for q in range(Q)]
+        ln = [len(r) for r in parts]
+    else:
+        ln = lens.tolist()
+        parts = [h[q, 1:1 + n] for q, n in enumerate(ln)]
+    # every query's kept keys end to end, decoded in one pass, then split
+    # (as the 1-GPU batch decodes: _topn_nosrc_fused_on)
+    keys = np.concatenate(parts) if Q else np.zeros(0, np.int64)
+    rid = space[0xFFFFFFFF - (keys & 0xFFFFFFFF)] if len(keys) else np.zeros(0, np.uint64)
+    cnt = keys >> 32
+    res, o = [], 0
+    for n in ln:
+        res.append(pair_array(rid[o:o + n], cnt[o:o + n]))
+        o += n
+    return res
 
 
 class DeviceRankCaches:
@@ -629,6 +667,27 @@ class DeviceRankCaches:
             memo[nmax] = got
         return got
 
+    def _native_fused(self, memo):
+        """The native request object (kernels/binding.cpp CacheTopN) over a
+        fused memo, made once per memo: it owns its streams and pinned
+        buffers and runs a batch without the interpreter between the H2D and
+        the decoded answers.  None off the GPU or without the extension."""
+        import torch
+        if self.view.device.type != "cuda":
+            return None
+        u32, inv32, cm = memo
+        stride = int(inv32.numel()) // max(self.S, 1)
+        nat = self.__dict__.setdefault("_nat", {})
+        got = nat.get(stride)
+        if got is None:
+            k = kernels()
+            if not hasattr(k, "CacheTopN"):
+                return None
+            self._ready.synchronize()   # the rank caches' build, once
+            rows = torch.from_numpy(np.ascontiguousarray(self.view.rows, dtype=np.uint64).view(np.int64))
+            got = nat[stride] = k.CacheTopN(self.cache_cnt, inv32, u32, cm, stride, rows)
+        return got
+
     # ------------------------------------------------------------ mesh (node-wide) cache-only batches
     def local_nmax(self, nreq: int) -> int:
         """This rank's cache prefix for a batch whose largest n is ``nreq``
@@ -698,8 +757,13 @@ class DeviceRankCaches:
         # the arena's own stream, where in-place arena writes (update_rows,
         # apply_deltas_multi, grow_segment) are ordered, and wait for it before
         # any side stream reads it.  Later batches find it built.
-        if self._fused_memo(nmax) is False:
+        memo = self._fused_memo(nmax)
+        if memo is False:
             return None
+        nat = self._native_fused(memo) if NATIVE_FUSED else None
+        if nat is not None:
+            got = nat.run(nn, thresholds, nmax)
+            return None if got is None else pair_arrays_split(*got)
         lane = _lane_take(dev)
         if not SIDE_STREAM:
             lane.run_stream = torch.cuda.current_stream(dev)

@@ -30,4 +30,6 @@ for k, d in agg.items():
     if g("SQ_WAVE_CYCLES"): print("  wait_any/wave_cycles", round(g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES"), 3), "busy/gui", round(g("SQ_BUSY_CYCLES") / max(g("GRBM_GUI_ACTIVE"), 1), 3))
     if g("TCC_HIT_sum") + g("TCC_MISS_sum"): print("  l2_hit", round(g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")), 3))
 PY
+timeout -k 10 400 env PILOSA_BENCH_TOPN_PROFILE=$O/plain_topn.folded PILOSA_BENCH_CPROFILE=$O/plain_topn_cprofile.txt python3 -u bench.py --serve-seconds 0 --configs= --steps 3 --warmup 1 --topn-src-batches 40 > $O/bench_prof.log 2> $O/bench_prof.err || { tail -c 3000 $O/bench_prof.err; exit 1; }
+head -40 $O/plain_topn_cprofile.txt
 echo done

@@ -207,12 +207,15 @@ def test_nosrc_fused_kernels_equal_torch_batch(lazy_env, monkeypatch):
     assert [_pairs(r) for r in rc.topn_nosrc(ns, ths)] == [_pairs(r) for r in ref]
 
 
-def test_nosrc_fused_concurrent_batches_on_lanes(lazy_env):
+@pytest.mark.parametrize("native", [False, True])
+def test_nosrc_fused_concurrent_batches_on_lanes(lazy_env, monkeypatch, native):
     """Concurrent cache-only batches each check out a (side stream, pinned
-    parameter buffer) lane: 8 threads x 12 batches of different n / threshold
-    mixes answer exactly as the same batches run one at a time, and the lanes
-    are reused (the pool never holds more than the concurrency)."""
+    parameter buffer) lane -- a Python lane, or a slot of the native request
+    object (binding.cpp CacheTopN) -- : 8 threads x 12 batches of different
+    n / threshold mixes answer exactly as the same batches run one at a time,
+    and the lanes are reused (the pool never holds more than the concurrency)."""
     from pilosa_amd.ops import topn_exec
+    monkeypatch.setattr(topn_exec, "NATIVE_FUSED", native)
     holder, ex, gpu, _, _ = lazy_env
     ex.execute("i", "TopN(h, n=10)")
     rc = next(iter(gpu._rank_cache_map.values()))[1]
@@ -243,7 +246,39 @@ def test_nosrc_fused_concurrent_batches_on_lanes(lazy_env):
     assert not err, err[0]
     assert got == want
     lanes = topn_exec._LANES.get(rc.view.device, [])
-    assert 1 <= len(lanes) <= n0 + 8
+    if native:
+        assert rc.__dict__.get("_nat"), "the native request object never ran"
+        assert len(lanes) == n0
+    else:
+        assert 1 <= len(lanes) <= n0 + 8
+
+
+def test_nosrc_native_request_equals_python_lane(lazy_env, monkeypatch):
+    """The native cache-only request (CacheTopN.run: parameters, kernels, D2H
+    and decode in C++) answers every batch exactly as the Python lane path
+    over the same memo, including n = 0, n beyond the candidates, int32-edge
+    n / thresholds and duplicate thresholds; results are columnar PairArrays."""
+    from pilosa_amd.models.cache import PairArray
+    from pilosa_amd.ops import topn_exec
+    holder, ex, gpu, _, _ = lazy_env
+    ex.execute("i", "TopN(h, n=10)")
+    rc = next(iter(gpu._rank_cache_map.values()))[1]
+    rc.__dict__.pop("_fused", None)
+    rng = np.random.default_rng(11)
+    batches = [([0, 10, (1 << 31) - 1], [1, 1, (1 << 31) - 1]), ([rc.K + 7], [2]), ([5] * 16, [3] * 16)]
+    for _ in range(40):
+        q = int(rng.integers(1, 33))
+        batches.append(([int(x) for x in rng.choice([0, 1, 3, 10, 64, 200, 999], q)],
+                        [int(x) for x in rng.choice([1, 2, 7, 40, 1000], q)]))
+    for ns, ths in batches:
+        monkeypatch.setattr(topn_exec, "NATIVE_FUSED", False)
+        want = rc._topn_nosrc_fused(ns, ths)
+        monkeypatch.setattr(topn_exec, "NATIVE_FUSED", True)
+        got = rc._topn_nosrc_fused(ns, ths)
+        assert want is not None and got is not None
+        assert all(isinstance(r, PairArray) for r in got)
+        assert [_pairs(r) for r in got] == [_pairs(r) for r in want], (ns, ths)
+    assert rc.__dict__.get("_nat")
 
 
 def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
