@@ -1587,6 +1587,7 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
             client()
             pr.disable()
             sio = io.StringIO()
+            pstats.Stats(pr, stream=sio).sort_stats("tottime").print_stats(45)
             pstats.Stats(pr, stream=sio).sort_stats("cumulative").print_stats(70)
             with open(cprof, "w") as fh:
                 fh.write(sio.getvalue())
