@@ -1487,8 +1487,13 @@ def mesh_breakdown(args, ex, mesh, all_shards, queries):
     topn = [" ".join(_wide_topn_calls(args.topn_batch, seed=900 + i)) for i in range(n)]
     for t in topn[:2]:      # their node candidate spaces (n buckets) built untimed
         ex.execute("i", t, shards=all_shards)
+    # src TopN requests as the src phase draws them (one untimed first)
+    hot = zipf_rows(np.random.default_rng(901), args.topn_batch * (n + 1), 1000)
+    src = [" ".join(f"TopN(f, Row(f={a}), n=100)" for a in hot[i * args.topn_batch:(i + 1) * args.topn_batch])
+           for i in range(n + 1)]
+    ex.execute("i", src[0], shards=all_shards)
     out = {}
-    for kind, reqs in (("count", texts), ("topn_cache", topn)):
+    for kind, reqs in (("count", texts), ("topn_cache", topn), ("topn_src", src[1:])):
         if not reqs:
             continue
         tr = tracing.HipEventTracer(limit=200000)
