@@ -344,15 +344,20 @@ class Server {
   }
 
   // kind-1 requests grouped by index: [(index, [ids], [ncalls], text)]
-  py::list take_counts(int max_n, int timeout_ms) { return take_grouped(1, max_n, timeout_ms); }
+  // min_n / hold_us: once a request is queued, wait up to hold_us more for
+  // min_n of them (adaptive group commit: the batcher asks for a fuller batch
+  // only while another batch keeps the device busy)
+  py::list take_counts(int max_n, int timeout_ms, int min_n, int hold_us) {
+    return take_grouped(1, max_n, timeout_ms, min_n, hold_us);
+  }
 
-  py::list take_grouped(int kind, int max_n, int timeout_ms) {
+  py::list take_grouped(int kind, int max_n, int timeout_ms, int min_n = 1, int hold_us = 0) {
     std::vector<std::shared_ptr<Req>> got;
     std::vector<std::pair<std::string, std::vector<size_t>>> groups;
     std::vector<std::string> texts;
     {
       py::gil_scoped_release nogil;
-      pop(kind, size_t(std::max(1, max_n)), timeout_ms, got);
+      pop(kind, size_t(std::max(1, max_n)), timeout_ms, got, size_t(std::max(1, min_n)), hold_us);
       for (size_t i = 0; i < got.size(); i++) {
         size_t g = 0;
         while (g < groups.size() && groups[g].first != got[i]->index) g++;
@@ -467,7 +472,8 @@ class Server {
  private:
   static constexpr uint64_t LISTEN_TAG = 1, WAKE_TAG = 2;
 
-  void pop(int kind, size_t max_n, int timeout_ms, std::vector<std::shared_ptr<Req>>& got) {
+  void pop(int kind, size_t max_n, int timeout_ms, std::vector<std::shared_ptr<Req>>& got, size_t min_n = 1,
+           int hold_us = 0) {
     std::unique_lock<std::mutex> g(qmu_);
     auto& q = q_[kind];
     // system_clock deadline: its wait maps to pthread_cond_timedwait, which
@@ -478,6 +484,9 @@ class Server {
     if (q.empty())
       qcv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms)),
                       [&] { return !q.empty() || stopping_; });
+    if (!q.empty() && q.size() < std::min(min_n, max_n) && hold_us > 0)
+      qcv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::microseconds(hold_us),
+                      [&] { return q.size() >= std::min(min_n, max_n) || stopping_; });
     while (!q.empty() && got.size() < max_n) {
       got.push_back(std::move(q.front()));
       q.pop_front();
@@ -1124,7 +1133,8 @@ PYBIND11_MODULE(_httpd, m) {
       .def("start", &httpd::Server::start)
       .def("stop", &httpd::Server::stop, py::call_guard<py::gil_scoped_release>())
       .def("take", &httpd::Server::take, py::arg("max_n") = 1, py::arg("timeout_ms") = 100)
-      .def("take_counts", &httpd::Server::take_counts, py::arg("max_n") = 1 << 16, py::arg("timeout_ms") = 100)
+      .def("take_counts", &httpd::Server::take_counts, py::arg("max_n") = 1 << 16, py::arg("timeout_ms") = 100,
+           py::arg("min_n") = 1, py::arg("hold_us") = 0)
       .def("take_topn", &httpd::Server::take_topn, py::arg("max_n") = 1 << 16, py::arg("timeout_ms") = 100)
       .def("set_topn_batching", &httpd::Server::set_topn_batching)
       .def("requeue", &httpd::Server::requeue)

@@ -107,6 +107,14 @@ class NativeHTTPServer:
         self.srv.set_cors(list(getattr(handler, "allowed_origins", None) or []))
         self.n_workers, self.n_batchers, self.max_batch = workers, batchers, max_batch
         self.n_topn_batchers = topn_batchers
+        # adaptive group commit (off with min 0): while another Count batch is
+        # on the device, a batcher waits up to hold_us for hold_min requests
+        # so the next batch is fuller; with the device idle it takes what is queued
+        self.hold_min = int(os.environ.get("PILOSA_HTTP_HOLD_MIN", "0"))
+        self.hold_us = int(os.environ.get("PILOSA_HTTP_HOLD_US", "300"))
+        self._in_flight = 0
+        self._if_mu = threading.Lock()
+        self.held_batches = 0
         self.topn_batches = 0
         self.topn_batched_requests = 0
         self.topn_requeued = 0
@@ -171,7 +179,8 @@ class NativeHTTPServer:
                  count_ms_per_batch=round(1000 * self.count_s / max(self.batches, 1), 3),
                  topn_batches=self.topn_batches, topn_batched_requests=self.topn_batched_requests,
                  topn_requeued=self.topn_requeued, count_batchers=self.n_batchers,
-                 topn_batchers=self.n_topn_batchers)
+                 topn_batchers=self.n_topn_batchers, hold_min=self.hold_min, hold_us=self.hold_us,
+                 held_batches=self.held_batches)
         server = self.handler.server
         gpu = getattr(getattr(server, "executor", None), "gpu", None)
         nb = getattr(gpu, "text_batches", 0)
@@ -203,17 +212,32 @@ class NativeHTTPServer:
     def _count_loop(self, gen: int = 0):
         srv = self.srv
         while not self._stop.is_set() and gen == self._gen:
-            for index, ids, ncalls, text in srv.take_counts(self.max_batch, 500):
-                t0 = time.perf_counter()
-                counts = self._count_group(index, text, sum(ncalls))
-                self.count_s += time.perf_counter() - t0
-                if counts is None:
-                    self.requeued += len(ids)
-                    srv.requeue(ids)
-                    continue
-                self.batches += 1
-                self.batched_requests += len(ids)
-                srv.respond_counts(ids, ncalls, counts)
+            hold = self.hold_min > 1 and self._in_flight > 0
+            if hold:
+                self.held_batches += 1
+            groups = srv.take_counts(self.max_batch, 500, self.hold_min if hold else 1, self.hold_us if hold else 0)
+            if not groups:
+                continue
+            with self._if_mu:
+                self._in_flight += 1
+            try:
+                self._count_groups(srv, groups)
+            finally:
+                with self._if_mu:
+                    self._in_flight -= 1
+
+    def _count_groups(self, srv, groups):
+        for index, ids, ncalls, text in groups:
+            t0 = time.perf_counter()
+            counts = self._count_group(index, text, sum(ncalls))
+            self.count_s += time.perf_counter() - t0
+            if counts is None:
+                self.requeued += len(ids)
+                srv.requeue(ids)
+                continue
+            self.batches += 1
+            self.batched_requests += len(ids)
+            srv.respond_counts(ids, ncalls, counts)
 
     def _topn_loop(self, gen: int = 0):
         """Concurrent flat-TopN requests of an index, answered as ONE device
