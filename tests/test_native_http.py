@@ -190,6 +190,35 @@ def test_count_group_commit_and_fallback():
         srv.close()
 
 
+def test_count_group_commit_with_adaptive_hold():
+    """Adaptive group commit (take_counts min_n / hold_us): while another
+    batch is in flight a batcher waits briefly for a fuller batch; every
+    answer is unchanged and the held takes are counted."""
+    from pilosa_amd import _httpd
+    srv = _server(True)
+    try:
+        port = srv.httpd.server_address[1]
+        for m, p, b in SCRIPT[:4]:
+            _raw(port, _req(m, p, b, close=True))
+        ex = srv.executor
+        calls = []
+        ex._count_text_fast = _host_fast(ex, calls)
+        srv.httpd.hold_min, srv.httpd.hold_us = 8, 2000
+        srv.httpd.set_batchers(2)
+        srv.httpd.srv.set_count_batching(True)
+        bodies = [b"Count(Row(f=2))", b"Count(Row(f=7)) Count(Row(f=2))"]
+        want = [[2], [1, 2]]
+        res = _httpd.load("127.0.0.1", port, "/index/i/query", bodies, 32, 4, 1.0, 200)
+        assert res["errors"] == 0 and res["requests"] >= 8
+        for k, body in res["samples"]:
+            assert json.loads(body)["results"] == want[k]
+        st = srv.httpd.stats()
+        assert st["hold_min"] == 8 and st["batched_requests"] > 0
+        assert st["held_batches"] > 0, "no batcher ever held for a fuller batch"
+    finally:
+        srv.close()
+
+
 def test_concurrent_generic_requests():
     srv = _server(True)
     try:
