@@ -433,8 +433,11 @@ class DeviceTopNIndex:
         P = int(pair_idx.numel())
         out = torch.zeros(P, dtype=torch.int64, device=dev)
         if P and self.S:
-            off = torch.zeros(Q + 1, dtype=torch.int64, device=dev)
-            off[1:] = torch.cumsum(torch.bincount(pair_q, minlength=Q), 0)
+            # pairs come sorted by query (nonzero / the union's sorted keys):
+            # per-query offsets by a search, no bincount (whose output size
+            # needs a host read of the max)
+            off = torch.searchsorted(pair_q.to(torch.int64),
+                                     torch.arange(Q + 1, device=dev, dtype=torch.int64))
             h, tb = hist if hist is not None else (None, None)
             self._launch(3 if h is not None else 2, Q, src, ns_t, th_t, pair_off=off,
                          pair_idx=pair_idx.to(torch.int32).contiguous(), out=out, hist=h, hot_cnt=hot,
@@ -583,21 +586,24 @@ def finish_batch_dev(space: np.ndarray, Q: int, pq, pa, cnt, ns: Sequence[int]) 
     bq, ba = max(1, int(Q - 1).bit_length()), max(1, int(len(space) - 1).bit_length())
     if bq + 31 + ba <= 63:
         # one sort of a composite key (query, ~count, acc index): acc indexes
-        # are in id order, so this is (query, count desc, id asc) with no
-        # masking sync; zero counts sort last in their query and are dropped
-        # with the trim
-        c = cnt.to(torch.int64).clamp_(0, (1 << 31) - 1)
-        key = (pq.to(torch.int64) << (31 + ba)) | (((1 << 31) - 1 - c) << ba) | pa.to(torch.int64)
-        key = torch.sort(key)[0]
+        # are in id order, so this is (query, count desc, id asc); zero counts
+        # sort last in their query and are dropped with the trim.  The
+        # (query, index, count) triples are a few thousand: ONE D2H and the
+        # sort / trim on the host (the device version was ~8 small launches
+        # and two syncs, 0.33 ms of a src batch -- a third of an 8-GPU
+        # rank's fixed per-batch cost, profiles/r06_topn/)
+        from .topn_exec import _to_host_pinned
+        h = _to_host_pinned(torch.stack([pq.to(torch.int64), pa.to(torch.int64), cnt.to(torch.int64)]))
+        c = np.clip(h[2], 0, (1 << 31) - 1)
+        key = np.sort((h[0] << (31 + ba)) | (((1 << 31) - 1 - c) << ba) | h[1])
         q_s = key >> (31 + ba)
         c_s = ((1 << 31) - 1) - ((key >> ba) & ((1 << 31) - 1))
-        bounds = torch.searchsorted(q_s, torch.arange(Q + 1, device=key.device, dtype=torch.int64))
-        lim = torch.tensor([int(n) if int(n) else (1 << 62) for n in ns], dtype=torch.int64).to(key.device)
-        rank = torch.arange(key.numel(), device=key.device) - bounds[q_s]
+        bounds = np.searchsorted(q_s, np.arange(Q + 1, dtype=np.int64))
+        lim = np.array([int(n) if int(n) else (1 << 62) for n in ns], dtype=np.int64)
+        rank = np.arange(len(key), dtype=np.int64) - bounds[q_s]
         sel = (rank < lim[q_s]) & (c_s > 0)
-        kept = key[sel].cpu().numpy()
-        return _split_by_query(Q, kept >> (31 + ba), space[kept & ((1 << ba) - 1)],
-                               ((1 << 31) - 1) - ((kept >> ba) & ((1 << 31) - 1)))
+        kept = key[sel]
+        return _split_by_query(Q, kept >> (31 + ba), space[kept & ((1 << ba) - 1)], c_s[sel])
     keep = cnt > 0
     pq, pa, cnt = pq[keep], pa[keep], cnt[keep]
     if pq.numel() == 0:
