@@ -380,9 +380,23 @@ class DeviceTopNIndex:
             offs = torch.zeros(Q * self.Sd * 16, dtype=torch.int64, device=dev)
             has_run = torch.zeros(1, dtype=torch.int32, device=dev)
             kernels().leaf_src(self._vd, rows, self.Sd, counts, offs, has_run)
-            if not int(has_run.item()):
+            # an arena without run containers cannot hand leaf_src one: no
+            # host read of the flag (a sync between the src kernel and the
+            # hot-rank launch, ~0.1 ms per batch)
+            if not self._arena_has_runs() or not int(has_run.item()):
                 return counts, offs, self.view.t_payload
         return engine.materialize_batch(srcs, self.Sd)
+
+    def _arena_has_runs(self) -> bool:
+        """Whether any container of the view's arena is a run container,
+        checked once per view generation (writes bump it)."""
+        v = self.view
+        gen = getattr(v, "generation", None)
+        got = self.__dict__.get("_runs_memo")
+        if got is None or got[0] != gen or gen is None:
+            got = (gen, bool((((v.t_meta >> 4) & 3) == 3).any().item()))
+            self._runs_memo = got
+        return got[1]
 
     def hot_counts(self, src, Q: int):
         """int32[S, Q, R]: src counts of the hot cache ranks (one row-major
