@@ -555,7 +555,14 @@ class Executor:
         f = idx.field(fname)
         if f is None or f.type == FIELD_TYPE_INT or f.options.keys or f.options.cache_type == "none":
             return None
-        shards = list(shards) if shards else (idx.available_shards() or [0])
+        skey = None
+        if shards:
+            shards = list(shards)
+        else:
+            # the index's memoised shard tuple, keyed by the shard epoch (no
+            # per-request copy or hash of ~1k shard ids)
+            ep, tup = idx.available_shards_memo()
+            shards, skey = (tup, ("avail", index, ep)) if tup else ([0], None)
         if self._has_remote(index, shards, ExecOptions()):
             return None
         ths = [t or DEFAULT_MIN_THRESHOLD for t in ths]
@@ -571,7 +578,7 @@ class Executor:
                 self.stats.count_with_tags("TopN", len(res), [f"index:{index}"])
             return res
         try:
-            res = gpu.topn_plain_batch(index, fname, ns, ths, shards)
+            res = gpu.topn_plain_batch(index, fname, ns, ths, shards, skey=skey)
         except PilosaError:
             return None
         except RuntimeError as err:   # HIP / torch device error: counted, the general path answers

@@ -153,18 +153,24 @@ class Index:
         # memoised on the shard epoch (bumped by every fragment / view /
         # field / remote-shard change): the walk over ~1k fragments per
         # request was a visible share of a serving request
+        return list(self.available_shards_memo()[1])
+
+    def available_shards_memo(self):
+        """(shard epoch, sorted shard tuple): the tuple is the same object
+        while the epoch holds, so a per-request fast path can key memos on the
+        epoch instead of hashing ~1k shard ids."""
         ep = shard_epoch()
         memo = self.__dict__.get("_avail_memo")
         if memo is not None and memo[0] == ep:
-            return list(memo[1])
+            return memo
         s = set()
         for f in list(self.fields.values()):
             s |= set(f.available_shards())
         out = sorted(s)
-        self._avail_memo = (ep, tuple(out))
+        memo = self._avail_memo = (ep, tuple(out))
         if self.stats is not None and out:
             self.stats.gauge("maxShard", out[-1])   # index.go:257
-        return out
+        return memo
 
     def options_json(self) -> dict:
         return {"keys": self.keys, "trackExistence": self.track_existence}

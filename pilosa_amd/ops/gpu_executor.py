@@ -1110,6 +1110,7 @@ class GpuExecutor:
         memo = self.__dict__.setdefault("_plain_memo", {})
         ent = memo.get(key)
         if ent is None or ent[0] != epoch:
+            shards = list(shards)
             frags = self._topn_frags(index, fname, shards)
             rv = self.view_arena(index, fname, VIEW_STANDARD, shards)
             rc = self._rank_caches(index, fname, shards, frags, rv) if rv is not None else None
@@ -1118,13 +1119,15 @@ class GpuExecutor:
             ent = memo[key] = (epoch, rv, rc)
         return ent[1], ent[2]
 
-    def topn_plain_batch(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: List[int]):
+    def topn_plain_batch(self, index: str, fname: str, ns: Sequence[int], ths: Sequence[int], shards: List[int],
+                         skey=None):
         """Cache-only TopN(fname, n=ns[i], threshold=ths[i]) calls over the
         local shards in one fused batch (Executor._topn_plain_fast): the
-        field's view and rank caches are resolved once per mutation epoch."""
+        field's view and rank caches are resolved once per mutation epoch.
+        ``skey`` names the shard list (else the list itself is the key)."""
         if self.comm is not None:
             return None
-        rv, rc = self._plain_rc(index, fname, shards)
+        rv, rc = self._plain_rc(index, fname, list(shards) if skey is None else shards, skey)
         if rc is None or not rc.K:
             return [[] for _ in ns]
         self.launches += 1
