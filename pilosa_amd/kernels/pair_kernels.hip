@@ -1200,14 +1200,14 @@ void launch_and2_pairs(const QueryProg* progs, int Q, const ViewDev* views, int 
   const int64_t units = int64_t(S) * 16;
   // serving-size batches (<= 128 queries: almost every pair is one-off):
   // batched array staging (variant 39: an array's chunk loads all in flight
-  // before the LDS scatter) at 4 queries per wave up to 32 queries, 16 up to
-  // 128.  Round 6 sweep (profiles/r06_serve/kbench_b*.log): 0.437 / 0.848 /
-  // 1.275 ms at 32 / 64 / 128 queries against 0.554 / 1.019 / 1.353 ms for
-  // round 5's variant 40 at 8 per wave (whose one-off in-place probes cost
-  // more than they save).  Bigger batches keep v6.
+  // before the LDS scatter) at 4 queries per wave up to 32 queries, 32 up to
+  // 64, 16 up to 128.  Round 6 sweeps (profiles/r06_serve/kbench_b*.log):
+  // 0.437 / 0.794 / 1.225 ms at 32 / 64 / 128 queries against 0.554 / 1.019 /
+  // 1.353 ms for round 5's variant 40 at 8 per wave (whose one-off in-place
+  // probes cost more than they save).  Bigger batches keep v6.
   if (variant == 6 && cq <= 0 && Q <= 128) {
     variant = 39;
-    cq = Q <= 32 ? 4 : 16;
+    cq = Q <= 32 ? 4 : (Q <= 64 ? 32 : 16);
   }
 #ifdef PK_KBENCH
   if (variant == 50 && cq <= 0 && Q <= 128) variant = 51;   // the serving variant, lane-rotated
