@@ -1635,13 +1635,29 @@ __global__ __launch_bounds__(TC_THREADS) void topn_cache_select_kernel(const uin
   __syncthreads();
   const uint8_t* mq = member + int64_t(q) * U;
   const TT* tq = tot + int64_t(prm[2 * Q + q]) * U;
-  for (int j = tid; j < U; j += TC_THREADS) {
-    if (!mq[j]) continue;
-    const int32_t d = u[j];
-    const long long sc = (long long)tq[j];
-    if (d < 0 || sc <= 0) continue;
-    const int p = atomicAdd(&nmem, 1);
-    if (p < TC_CAP) keys[p] = (sc << 32) | (0xFFFFFFFFll - d);
+  // compaction with one LDS atomic per wave (ballot + prefix popcount), not
+  // one per member: every member of a wave used to serialise on nmem
+  const int lane = tid & 63;
+  for (int j0 = 0; j0 < U; j0 += TC_THREADS) {   // block-uniform trip count
+    const int j = j0 + tid;
+    bool keep = false;
+    long long key = 0;
+    if (j < U && mq[j]) {
+      const int32_t d = u[j];
+      const long long sc = (long long)tq[j];
+      if (d >= 0 && sc > 0) {
+        keep = true;
+        key = (sc << 32) | (0xFFFFFFFFll - d);
+      }
+    }
+    const uint64_t m = __ballot(keep);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&nmem, __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const int p = base + __popcll(m & ((uint64_t(1) << lane) - 1));
+      if (p < TC_CAP) keys[p] = key;
+    }
   }
   __syncthreads();
   const int M = nmem;
