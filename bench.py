@@ -1636,7 +1636,8 @@ def bench_topn_mesh(args, ex, mesh, all_shards):
     src_q = [" ".join(src_calls[i * B:(i + 1) * B]) for i in range(nb + WS)]
     out["src"] = {}
     log("mesh topn: src requests")
-    res = timed(src_q, out["src"], warm=WS, nclients=args.topn_clients)
+    res = timed(src_q, out["src"], warm=WS, nclients=args.topn_clients,
+                profile=os.environ.get("PILOSA_BENCH_TOPN_SRC_PROFILE", ""))
     if args.verify > 0:
         last = (nb + WS - 1) * B
         calls = [parse_string(c).calls[0] for c in src_calls[last:last + 2]] + [parse_string(f"TopN(f, n={n})").calls[0]]

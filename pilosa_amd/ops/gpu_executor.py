@@ -1352,6 +1352,7 @@ class GpuExecutor:
             return False
         try:
             allp, finfo = self._batch_info(index, calls, shards)
+            tsh = tuple(shards)
             for c, (fname, n, ids, threshold, tanimoto, attr_name, attr_values) in zip(calls, allp):
                 if ids or tanimoto or (attr_name and attr_values) or len(c.children) > 1:
                     return False
@@ -1360,7 +1361,7 @@ class GpuExecutor:
                     return False
                 if c.children:
                     src = self.plan(index, c.children[0], shards)
-                    space = self._node_space((index, fname, tuple(shards)), rv)
+                    space = self._node_space((index, fname, tsh), rv)
                     if src is EMPTY or self._topn_index(index, fname, shards, rc, rv, space=space) is None:
                         return False
                     if not (type(src) is Leaf and src.view is rv):

@@ -147,7 +147,18 @@ class ShardMesh:
 
     def owned(self, shards: Sequence[int], rank: Optional[int] = None) -> List[int]:
         r = self.rank if rank is None else rank
-        return [int(s) for s in shards if self.owner(s) == r]
+        # memoised per shard list: a request over ~1k shards re-derived the
+        # owner of every shard (~0.17 ms of the front end's time under the
+        # mesh lock per TopN request)
+        key = (r, self.world, self.block, tuple(shards))
+        memo = self.__dict__.setdefault("_owned_memo", {})
+        got = memo.get(key)
+        if got is None:
+            got = [int(s) for s in shards if self.owner(s) == r]
+            if len(memo) >= 64:
+                memo.clear()
+            memo[key] = got
+        return list(got)
 
     @property
     def is_frontend(self) -> bool:
