@@ -306,7 +306,12 @@ class GpuExecutor:
                     else:
                         with f.mu:
                             f.take_dirty(token)  # register before the contents are read
-                            bms.append(_dev_storage(f))
+                            # a copy taken under the fragment lock: the native
+                            # builder reads the bitmaps with no lock held, and a
+                            # snapshot's to_bytes() optimises containers in place
+                            # (a concurrent rewrite crashed the builder)
+                            st = _dev_storage(f)
+                            bms.append(st if isinstance(f, SubFragment) or not hasattr(st, "clone") else st.clone())
                 dv = DeviceView.from_bitmaps(bms, self.device, shards=dshards, patchable=True)
             dv.token = token
             self.rebuilds += 1
