@@ -75,3 +75,51 @@ def test_patched_arena_matches_fragments():
             assert (dv.t_rowptr.view(dv.S, dv.D + 1)[si].numpy() == dv._rowptr_host[si]).all()
     finally:
         env.close()
+
+
+def test_arena_rebuild_races_snapshots():
+    """Stress of the scenario behind a CPU-suite crash: the native arena
+    builder reads the fragments' bitmaps with no lock held while writes and
+    the snapshot's to_bytes() (which optimises containers in place) change
+    them.  The rebuild now takes a copy under each fragment lock; rebuilds
+    racing writes + snapshots must not crash, and the quiescent arena
+    decodes to the fragments.  (The window is narrow: this does not
+    reproduce the crash reliably without the fix.)"""
+    import threading
+
+    from pilosa_amd.ops.gpu_executor import GpuExecutor
+    env = Env()
+    try:
+        env.create_index("i")
+        env.field("i", "g")
+        f = env.holder.index("i").field("g")
+        rng = np.random.default_rng(7)
+        for r in range(4):
+            f.import_bits(np.full(30000, r, np.uint64), rng.choice(4 * SW, 30000, replace=False).astype(np.uint64))
+        frags = [env.holder.fragment("i", "g", "standard", s) for s in SHARDS]
+        stop = threading.Event()
+
+        wr = np.random.default_rng(8)
+
+        def snapshots():
+            # writes leave containers un-optimised; the snapshot's to_bytes()
+            # then converts them in place
+            while not stop.is_set():
+                f.import_bits(np.full(64, int(wr.integers(0, 4)), np.uint64),
+                              wr.integers(0, 4 * SW, 64).astype(np.uint64))
+                for fr in frags:
+                    fr.snapshot()
+        t = threading.Thread(target=snapshots, daemon=True)
+        t.start()
+        try:
+            for _ in range(12):
+                GpuExecutor(env.holder, "cpu").view_arena("i", "g", "standard", SHARDS)
+        finally:
+            stop.set()
+            t.join(timeout=30)
+        # quiescent: a fresh arena decodes to exactly the fragments
+        dv = GpuExecutor(env.holder, "cpu").view_arena("i", "g", "standard", SHARDS)
+        for si, s in enumerate(SHARDS):
+            assert _decode(dv, si) == frags[si].storage.slice().astype(np.int64).tolist()
+    finally:
+        env.close()
