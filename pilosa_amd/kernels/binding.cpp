@@ -489,6 +489,16 @@ class CacheTopN {
     const int64_t Q = p.Q, T = p.T, KK = p.KK;
     const int64_t np = int64_t(p.prm.size()), nout = Q * (KK + 1);
     Slot* s = take(np, Q * U_, T * U_, nout);
+    // membership marks: the slot's buffer is cleared whole only when the
+    // epoch wraps (or the buffer was reallocated); a batch's members get its
+    // epoch byte and older bytes are all smaller, so no clear per batch
+    if (s->epoch < 2 || s->epoch >= 255) {
+      TORCH_CHECK(hipMemsetAsync(s->member.data_ptr(), 0, size_t(s->member.numel()), s->st) == hipSuccess,
+                  "CacheTopN member clear");
+      s->epoch = 2;
+    } else {
+      s->epoch++;
+    }
     std::copy(p.prm.begin(), p.prm.end(), s->pin_prm);
     TORCH_CHECK(hipMemcpyAsync(s->prm.data_ptr(), s->pin_prm, size_t(np) * 4, hipMemcpyHostToDevice, s->st) ==
                     hipSuccess, "CacheTopN params");
@@ -496,7 +506,8 @@ class CacheTopN {
                                 u_.data_ptr<int32_t>(), cm_.data_ptr<int32_t>(), s->prm.data_ptr<int32_t>(), int(Q),
                                 int(T), int(U_), int(KK), s->member.data_ptr<uint8_t>(),
                                 reinterpret_cast<long long*>(s->tot.data_ptr<int64_t>()),
-                                reinterpret_cast<long long*>(s->out.data_ptr<int64_t>()), s->st, int(nlim));
+                                reinterpret_cast<long long*>(s->out.data_ptr<int64_t>()), s->st, int(nlim),
+                                s->epoch);
     check_launch("CacheTopN kernels");
     TORCH_CHECK(hipMemcpyAsync(s->pin_out, s->out.data_ptr(), size_t(nout) * 8, hipMemcpyDeviceToHost, s->st) ==
                     hipSuccess, "CacheTopN answers");
@@ -520,6 +531,7 @@ class CacheTopN {
     int32_t* pin_prm = nullptr;
     int64_t* pin_out = nullptr;
     int64_t cap_prm = 0, cap_out = 0;
+    int epoch = 0;   // membership mark of the last batch (0: member buffer not cleared yet)
     torch::Tensor prm, member, tot, out;
   };
 
@@ -554,8 +566,10 @@ class CacheTopN {
                       hipSuccess, "CacheTopN pinned answers");
       s->out = torch::empty({s->cap_out}, dopt.dtype(torch::kInt64));
     }
-    if (!s->member.defined() || s->member.numel() < nmember)
+    if (!s->member.defined() || s->member.numel() < nmember) {
       s->member = torch::empty({grow(nmember)}, dopt.dtype(torch::kUInt8));
+      s->epoch = 0;   // uninitialised bytes: cleared before the next batch
+    }
     if (!s->tot.defined() || s->tot.numel() < ntot) s->tot = torch::empty({grow(ntot)}, dopt.dtype(torch::kInt64));
     return s;
   }

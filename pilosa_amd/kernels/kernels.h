@@ -154,7 +154,7 @@ void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, 
 // (prm = lim[Q] | mt[Q] | tsel[Q] | nq[Q] | th[T]; out[Q, KK+1], column 0 = rows kept or -2 on overflow).
 void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
                              const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
-                             long long* tot, long long* out, hipStream_t st, int nlim = 0);
+                             long long* tot, long long* out, hipStream_t st, int nlim = 0, int mark = 0);
 // Mesh cache-only TopN: one rank's buffer [member bytes | int32 totals[T, U] | flags[2]] (cleared here;
 // flags = this rank's [stale, declined] vote, which rides in the batch's one all-reduce) and the front
 // end's select over the reduced buffer (out[q, 0] = -3 / -4 when some rank was stale / declined).

@@ -1536,10 +1536,12 @@ __global__ __launch_bounds__(256) void topn_cache_member_kernel(const int32_t* _
 // The same membership with one thread per (shard, rank) for every query of
 // the batch (Q <= 256): the rank's count and candidate index are read once
 // instead of once per query (the per-query grid re-read them Q times).
-__global__ __launch_bounds__(256) void topn_cache_member_q_kernel(const int32_t* __restrict__ cnt, int K, int S,
-                                                                  int nmax, const int32_t* __restrict__ inv,
-                                                                  const int32_t* __restrict__ prm, int Q, int U,
-                                                                  uint8_t* __restrict__ member, int nlim) {
+// ``mark``: the byte a member gets (1 after a clear; a cycling epoch when the
+// buffer is reused uncleared, CacheTopN); block b of nb blocks.
+__device__ __forceinline__ void cache_member_q_body(const int32_t* __restrict__ cnt, int K, int S, int nmax,
+                                                    const int32_t* __restrict__ inv, const int32_t* __restrict__ prm,
+                                                    int Q, int U, uint8_t* __restrict__ member, int nlim, uint8_t mark,
+                                                    int b, int nb) {
   __shared__ int32_t lim[256], thr[256];
   for (int q = threadIdx.x; q < Q; q += blockDim.x) {
     lim[q] = min(prm[q], nlim);
@@ -1547,15 +1549,22 @@ __global__ __launch_bounds__(256) void topn_cache_member_q_kernel(const int32_t*
   }
   __syncthreads();
   const int64_t N = int64_t(S) * nlim;
-  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < N; e += int64_t(gridDim.x) * blockDim.x) {
+  for (int64_t e = int64_t(b) * blockDim.x + threadIdx.x; e < N; e += int64_t(nb) * blockDim.x) {
     const int64_t s = e / nlim;
     const int k = int(e - s * nlim);
     const int32_t c = cnt[s * K + k];
     if (c <= 0) continue;
     const int j = inv[s * nmax + k];
     for (int q = 0; q < Q; q++)
-      if (k < lim[q] && c >= thr[q]) member[int64_t(q) * U + j] = 1;
+      if (k < lim[q] && c >= thr[q]) member[int64_t(q) * U + j] = mark;
   }
+}
+
+__global__ __launch_bounds__(256) void topn_cache_member_q_kernel(const int32_t* __restrict__ cnt, int K, int S,
+                                                                  int nmax, const int32_t* __restrict__ inv,
+                                                                  const int32_t* __restrict__ prm, int Q, int U,
+                                                                  uint8_t* __restrict__ member, int nlim) {
+  cache_member_q_body(cnt, K, S, nmax, inv, prm, Q, U, member, nlim, 1, int(blockIdx.x), int(gridDim.x));
 }
 
 // tot[t*U + j] = sum over shards of cm[j*S + s] where it reaches th[t]; one
@@ -1587,10 +1596,22 @@ __global__ __launch_bounds__(256) void topn_cache_totals_kernel(const int32_t* _
 // registers (the per-threshold kernel re-read the [U x S] matrix T times:
 // ~1.2 GB for 16 distinct thresholds over a 20k-candidate prefix).
 template <class TT>
+__device__ __forceinline__ void cache_totals16_body(const int32_t* __restrict__ cm, int S, int U,
+                                                    const int32_t* __restrict__ th, int T, TT* __restrict__ tot,
+                                                    int b);
+
+template <class TT>
 __global__ __launch_bounds__(256) void topn_cache_totals16_kernel(const int32_t* __restrict__ cm, int S, int U,
                                                                   const int32_t* __restrict__ th, int T,
                                                                   TT* __restrict__ tot) {
-  const int j = int(blockIdx.x) * 4 + int(threadIdx.x >> 6);
+  cache_totals16_body<TT>(cm, S, U, th, T, tot, int(blockIdx.x));
+}
+
+template <class TT>
+__device__ __forceinline__ void cache_totals16_body(const int32_t* __restrict__ cm, int S, int U,
+                                                    const int32_t* __restrict__ th, int T, TT* __restrict__ tot,
+                                                    int b) {
+  const int j = b * 4 + int(threadIdx.x >> 6);
   const int lane = int(threadIdx.x & 63);
   if (j >= U) return;
   int32_t thr[16];
@@ -1614,13 +1635,27 @@ __global__ __launch_bounds__(256) void topn_cache_totals16_kernel(const int32_t*
   }
 }
 
+// Membership and the 16-threshold totals in ONE launch (Q <= 256, T <= 16):
+// blocks [0, nbm) run the membership, the rest the totals -- independent
+// work, one launch latency less per cache-only request.
+template <class TT>
+__global__ __launch_bounds__(256) void topn_cache_member_totals16_kernel(
+    const int32_t* __restrict__ cnt, int K, int S, int nmax, const int32_t* __restrict__ inv,
+    const int32_t* __restrict__ prm, int Q, int U, uint8_t* __restrict__ member, int nlim, uint8_t mark, int nbm,
+    const int32_t* __restrict__ cm, int T, TT* __restrict__ tot) {
+  if (int(blockIdx.x) < nbm)
+    cache_member_q_body(cnt, K, S, nmax, inv, prm, Q, U, member, nlim, mark, int(blockIdx.x), nbm);
+  else
+    cache_totals16_body<TT>(cm, S, U, prm + 4 * Q, T, tot, int(blockIdx.x) - nbm);
+}
+
 template <class TT>
 __global__ __launch_bounds__(TC_THREADS) void topn_cache_select_kernel(const uint8_t* __restrict__ member,
                                                                 const TT* __restrict__ tot,
                                                                 const int32_t* __restrict__ u,
                                                                 const int32_t* __restrict__ prm, int Q, int U, int KK,
                                                                 long long* __restrict__ out,
-                                                                const int32_t* __restrict__ flags) {
+                                                                const int32_t* __restrict__ flags, int mark) {
   __shared__ long long keys[TC_CAP];
   __shared__ int nmem;
   const int q = blockIdx.x;
@@ -1642,7 +1677,9 @@ __global__ __launch_bounds__(TC_THREADS) void topn_cache_select_kernel(const uin
     const int j = j0 + tid;
     bool keep = false;
     long long key = 0;
-    if (j < U && mq[j]) {
+    // a member: byte == mark (an epoch-marked reused buffer), or nonzero
+    // (mark 0: a cleared buffer, or the mesh's all-reduced byte sums)
+    if (j < U && (mark ? mq[j] == mark : mq[j] != 0)) {
       const int32_t d = u[j];
       const long long sc = (long long)tq[j];
       if (d >= 0 && sc > 0) {
@@ -1701,31 +1738,44 @@ void launch_topn_cache_counts(const ViewDev& v, int S, const int32_t* u, int U, 
 
 void launch_topn_cache_batch(const int32_t* cnt, int K, int S, int nmax, const int32_t* inv, const int32_t* u,
                              const int32_t* cm, const int32_t* prm, int Q, int T, int U, int KK, uint8_t* member,
-                             long long* tot, long long* out, hipStream_t st, int nlim) {
+                             long long* tot, long long* out, hipStream_t st, int nlim, int mark) {
   if (Q <= 0 || U <= 0) return;
   if (nlim <= 0 || nlim > nmax) nlim = nmax;
-  // the membership bytes start clear (was a separate torch fill launched from Python)
-  (void)hipMemsetAsync(member, 0, size_t(Q) * size_t(U), st);
+  // mark 0: the membership bytes are cleared here and members get 1; mark
+  // 1..255: the caller's buffer holds earlier batches' (smaller) marks and
+  // is cleared only when the epoch wraps to 1 -- no clear per batch
+  if (mark <= 1) (void)hipMemsetAsync(member, 0, size_t(Q) * size_t(U), st);
+  const uint8_t mk = uint8_t(mark <= 0 ? 1 : mark);
   const int64_t N = int64_t(S) * nlim;
-  if (N > 0) {
-    const int64_t want = (N + 255) / 256;
-    const int bx = int(want < 1024 ? want : 1024);
-    if (Q <= 256)
-      hipLaunchKernelGGL(topn_cache_member_q_kernel, dim3(unsigned(want < 8192 ? want : 8192)), dim3(256), 0, st, cnt,
-                         K, S, nmax, inv, prm, Q, U, member, nlim);
+  const int64_t want = N > 0 ? (N + 255) / 256 : 0;
+  if (Q <= 256 && T <= 16) {
+    // membership and totals in one launch
+    const int nbm = int(want < 8192 ? want : 8192);
+    const int nbt = (U + 3) / 4;
+    hipLaunchKernelGGL(topn_cache_member_totals16_kernel<long long>, dim3(unsigned(nbm + nbt)), dim3(256), 0, st, cnt,
+                       K, S, nmax, inv, prm, Q, U, member, nlim, mk, nbm, cm, T, tot);
+  } else {
+    if (N > 0) {
+      const int bx = int(want < 1024 ? want : 1024);
+      if (Q <= 256)
+        hipLaunchKernelGGL(topn_cache_member_q_kernel, dim3(unsigned(want < 8192 ? want : 8192)), dim3(256), 0, st,
+                           cnt, K, S, nmax, inv, prm, Q, U, member, nlim);
+      else
+        hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
+                           member, nlim);
+    }
+    const int64_t waves = int64_t(T) * U;
+    if (T <= 16)
+      hipLaunchKernelGGL(topn_cache_totals16_kernel<long long>, dim3(unsigned((U + 3) / 4)), dim3(256), 0, st, cm, S,
+                         U, prm + 4 * Q, T, tot);
     else
-      hipLaunchKernelGGL(topn_cache_member_kernel, dim3(bx, Q), dim3(256), 0, st, cnt, K, S, nmax, inv, prm, Q, U,
-                         member, nlim);
+      hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm,
+                         S, U, prm + 4 * Q, T, tot);
   }
-  const int64_t waves = int64_t(T) * U;
-  if (T <= 16)
-    hipLaunchKernelGGL(topn_cache_totals16_kernel<long long>, dim3(unsigned((U + 3) / 4)), dim3(256), 0, st, cm, S,
-                       U, prm + 4 * Q, T, tot);
-  else
-    hipLaunchKernelGGL(topn_cache_totals_kernel<long long>, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, cm,
-                       S, U, prm + 4 * Q, T, tot);
+  // the separate member kernels write 1 (a cleared buffer): test nonzero
+  const int smark = (Q <= 256 && T <= 16) ? int(mk) : 0;
   hipLaunchKernelGGL(topn_cache_select_kernel<long long>, dim3(Q), dim3(TC_THREADS), 0, st, member, tot, u, prm, Q, U,
-                     KK, out, (const int32_t*)nullptr);
+                     KK, out, (const int32_t*)nullptr, smark);
 }
 
 // A mesh rank's share of a cache-only batch over the NODE candidate space:
@@ -1767,7 +1817,7 @@ void launch_topn_cache_select32(const uint8_t* member, const int32_t* tot, const
                                 int Q, int U, int KK, long long* out, const int32_t* flags, hipStream_t st) {
   if (Q <= 0 || U <= 0) return;
   hipLaunchKernelGGL(topn_cache_select_kernel<int>, dim3(Q), dim3(TC_THREADS), 0, st, member, tot, ids, prm, Q, U, KK,
-                     out, flags);
+                     out, flags, 0);
 }
 
 }  // namespace pk

@@ -279,6 +279,14 @@ def test_nosrc_native_request_equals_python_lane(lazy_env, monkeypatch):
         assert all(isinstance(r, PairArray) for r in got)
         assert [_pairs(r) for r in got] == [_pairs(r) for r in want], (ns, ths)
     assert rc.__dict__.get("_nat")
+    # the member buffer is reused with a cycling epoch mark and cleared only
+    # when it wraps (every ~253 batches per slot): answers stay exact across
+    # several wraps, alternating batch shapes so stale marks would show
+    monkeypatch.setattr(topn_exec, "NATIVE_FUSED", True)
+    ref = {i: [_pairs(r) for r in rc._topn_nosrc_fused(*batches[i])] for i in (3, 4)}
+    for k in range(600):
+        i = 3 + (k & 1)
+        assert [_pairs(r) for r in rc._topn_nosrc_fused(*batches[i])] == ref[i], k
 
 
 def test_src_topn_after_write_burst_refreshes_index_in_place(lazy_env):
