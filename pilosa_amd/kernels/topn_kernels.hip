@@ -1795,6 +1795,13 @@ void launch_topn_cache_partial(const int32_t* cnt, int K, int S, int nmax, int n
   if (Q <= 0 || U <= 0 || stale || declined || cnt == nullptr) return;
   if (nlim <= 0 || nlim > nmax) nlim = nmax;
   const int64_t N = int64_t(S) * nlim;
+  if (Q <= 256 && T <= 16 && S > 0) {   // membership + totals in one launch
+    const int64_t want = N > 0 ? (N + 255) / 256 : 0;
+    const int nbm = int(want < 8192 ? want : 8192);
+    hipLaunchKernelGGL(topn_cache_member_totals16_kernel<int>, dim3(unsigned(nbm + (U + 3) / 4)), dim3(256), 0, st,
+                       cnt, K, S, nmax, inv, prm, Q, U, member, nlim, uint8_t(1), nbm, cm, T, tot);
+    return;
+  }
   if (N > 0) {
     const int64_t want = (N + 255) / 256;
     if (Q <= 256)
