@@ -370,6 +370,12 @@ def test_slot_index_on_fragment_caches_matches_host(lazy_env, hot):
     from pilosa_amd.ops.topn_index import DeviceTopNIndex
     from pilosa_amd.pql import parse_string
     holder, ex, gpu, _, _ = lazy_env
+    # earlier tests of the module write to h: settle every rank cache now.
+    # The host path re-ranks a dirty cache once its 10 s throttle expires
+    # (fragment._top_bitmap_pairs -> invalidate); without this, a re-rank
+    # landing between the device snapshot below and the host answers moved
+    # the cache boundary (n=0 walks the whole cache) -- a timing flake
+    holder.recalculate_caches()
     shards = holder.index("i").available_shards()
     rv = gpu.view_arena("i", "h", "standard", shards)
     frags = [holder.fragment("i", "h", "standard", s) for s in shards]
@@ -395,6 +401,7 @@ def test_src_topn_uses_the_slot_index_at_every_width(lazy_env):
     """Src TopN calls through the executor are answered by the device slot
     index (not the pair-count path) whatever the shard width."""
     holder, ex, gpu, _, _ = lazy_env
+    holder.recalculate_caches()   # no re-rank between the device and host answers
     gpu._topn_indexes.clear()
     b0 = gpu.topn_index_batches
     q = "TopN(h, Row(f=1), n=5) TopN(h, Row(f=0), n=9)"
@@ -413,6 +420,7 @@ def test_cache_only_batch_with_varied_n_matches_host(lazy_env):
     matrix / candidate memo is per power-of-two prefix) in one request, and
     again in another order: == the host answers."""
     holder, ex, gpu, _, _ = lazy_env
+    holder.recalculate_caches()   # no re-rank between the device and host answers
     calls = ["TopN(h, n=3)", "TopN(h, n=17, threshold=5)", "TopN(h, n=700)", "TopN(h, n=129, threshold=40)",
              "TopN(h, n=1)", "TopN(h, n=33)"]
     for order in (calls, calls[::-1], calls[2:] + calls[:2]):
