@@ -422,11 +422,12 @@ class DeviceRankCaches:
         shard_of = np.repeat(np.arange(S, dtype=np.int32), lens)
         ids = ids[keep] if len(ids) else ids
         t_shard = torch.from_numpy(shard_of).to(dev)
-        t_dense = dense_dev(view, torch.from_numpy(np.ascontiguousarray(ids).view(np.int64)).to(dev))
+        t_row = torch.from_numpy(np.ascontiguousarray(ids).view(np.int64)).to(dev)
+        t_dense = dense_dev(view, t_row)
         t_cnt = self._counts(t_shard, t_dense)
         if warm:
             # host rank caches of fragments loaded on the host (their live counts)
-            hs, hd, hc = [], [], []
+            hs, hd, hc, hr = [], [], [], []
             for si in warm:
                 with frags[si].mu:
                     pairs = list(frags[si].cache.top())
@@ -434,12 +435,14 @@ class DeviceRankCaches:
                     continue
                 a = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
                 hs.append(np.full(len(a), si, np.int32))
+                hr.append(a[:, 0])
                 hd.append(view.dense_many(a[:, 0].astype(np.uint64)).astype(np.int32))
                 hc.append(np.minimum(a[:, 1], 2 ** 31 - 1).astype(np.int32))
             if hs:
                 t_shard = torch.cat([t_shard, torch.from_numpy(np.concatenate(hs)).to(dev)])
                 t_dense = torch.cat([t_dense, torch.from_numpy(np.concatenate(hd)).to(dev)])
                 t_cnt = torch.cat([t_cnt, torch.from_numpy(np.concatenate(hc)).to(dev)])
+                t_row = torch.cat([t_row, torch.from_numpy(np.concatenate(hr)).to(dev)])
         N = t_dense.numel()
         if N == 0 or S == 0:
             self.K = 0
@@ -455,7 +458,15 @@ class DeviceRankCaches:
         pos = torch.arange(N, device=dev) - start[t_shard.to(torch.int64)]
         K = int(per.max().item())
         valid = (t_cnt > 0) & (t_dense >= 0)
-        key = torch.where(valid, (t_cnt.to(torch.int64) << 32) | (0xFFFFFFFF - t_dense.to(torch.int64)),
+        # ties order by row id as the host cache does (count desc, id asc),
+        # not by dense index: a dense index follows the arena's row order of
+        # first appearance, and at a cache_size cut of a tied count the two
+        # orders keep different rows.  The key's low word is the row's rank
+        # among the distinct row ids (order-preserving, < 2^32).
+        urow, rinv = torch.unique(t_row, sorted=True, return_inverse=True)
+        dense_of = torch.full((urow.numel(),), -1, dtype=torch.int64, device=dev)
+        dense_of[rinv] = t_dense.to(torch.int64)
+        key = torch.where(valid, (t_cnt.to(torch.int64) << 32) | (0xFFFFFFFF - rinv.to(torch.int64)),
                           torch.full_like(pos, -1))
         mat = torch.full((S, K), -1, dtype=torch.int64, device=dev)
         mat[t_shard.to(torch.int64), pos] = key
@@ -470,8 +481,8 @@ class DeviceRankCaches:
         mat, live = mat[:, :kmax], live[:, :kmax]
         self.K = kmax
         self.cache_cnt = torch.where(live, mat >> 32, torch.zeros_like(mat)).to(torch.int32).contiguous()
-        self.cache_dense = torch.where(live, 0xFFFFFFFF - (mat & 0xFFFFFFFF), torch.full_like(mat, -1)) \
-            .to(torch.int32).contiguous()
+        rix = torch.where(live, 0xFFFFFFFF - (mat & 0xFFFFFFFF), torch.zeros_like(mat))
+        self.cache_dense = torch.where(live, dense_of[rix], torch.full_like(mat, -1)).to(torch.int32).contiguous()
         if dev.type == "cuda":   # the side stream of cache-only batches starts after this point
             self._ready = torch.cuda.Event()
             self._ready.record()

@@ -28,6 +28,7 @@ types for the executor's result objects, packed into the same tensor.
 from __future__ import annotations
 
 import datetime as _dt
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -117,6 +118,10 @@ class Comm:
         self.board_gathers = 0
         self.use_board = True      # small OP_CALL partials through the results board (when the ring has one)
         self._ar_opts: dict = {}
+        # RCCL all-reduces of all_reduce_async on the caller's stream
+        # (asyncOp = False: no event hop to the process group's stream and
+        # back) instead of the process group's own stream
+        self.ar_current_stream = backend == "nccl" and os.environ.get("PILOSA_MESH_AR_STREAM", "pg") == "current"
 
     # ------------------------------------------------------------ guard
     def _guard(self, fn, *a, **kw):
@@ -291,6 +296,7 @@ class Comm:
             if opts is None:
                 opts = self.dist.AllreduceOptions()
                 opts.reduceOp = op
+                opts.asyncOp = not self.ar_current_stream
                 self._ar_opts[op] = opts
             if self.broken is not None:
                 raise CommError(f"communicator broken: {self.broken}")
