@@ -324,6 +324,12 @@ class RankCache:
         self._rankings = None
         self.version += 1
         self.update_time = time.monotonic()
+        # a re-rank with no write (the 10 s throttle expiring on a read, an
+        # explicit recalculate) changes top() too: device rank-cache memos
+        # skip their per-fragment version check only while the process-wide
+        # mutation epoch stands still
+        from pilosa_amd.models.fragment import _bump_epoch
+        _bump_epoch()
 
     @property
     def rankings(self) -> List[Tuple[int, int]]:
