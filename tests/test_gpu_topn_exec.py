@@ -3,11 +3,10 @@ opened holder answers cache-only and src-filtered TopN from the fragments'
 ``.cache`` files and the HBM arena, with every fragment still cold afterwards,
 and the answers equal the host executor's (fragment.top two-phase TopN,
 executor.go:863-1000) computed on the same data before the lazy reopen."""
+import os
 import threading
 
 import numpy as np
-import os
-
 import pytest
 
 from pilosa_amd.executor import Executor

@@ -142,3 +142,20 @@ def test_anti_entropy_zero_interval_returns():  # TestMonitorAntiEntropyZero
         assert not any(t.name == "anti-entropy" and t.is_alive() for t in threading.enumerate())
     finally:
         s.close()
+
+
+def test_rank_cache_rerank_moves_the_mutation_epoch():
+    """A re-rank with no write (explicit recalculate, or the 10 s throttle
+    expiring on a read) changes top(): device rank-cache memos keyed on the
+    mutation epoch must see it (GpuExecutor._rank_caches fast path)."""
+    from pilosa_amd.models.fragment import mutation_epoch
+    c = RankCache(2)
+    for rid, n in ((1, 5), (2, 4), (3, 4)):
+        c.bulk_add(rid, n)
+    e0 = mutation_epoch()
+    c.recalculate()
+    assert mutation_epoch() > e0
+    assert c.top() == [(1, 5), (2, 4)]   # tie at the cut: row id ascending
+    e1 = mutation_epoch()
+    c.invalidate()                       # inside the throttle window: no re-rank
+    assert mutation_epoch() == e1
